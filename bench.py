@@ -1,0 +1,244 @@
+"""Benchmark: env-steps/sec of the batched Sokoban rollout (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N ... bench.py --gpus N      (one rank per GPU)
+
+Workload (BASELINE.json configs[2], SURVEY §8(d) "SK"): Sokoban 6x6 / 1 box, 8192 envs per
+GPU (512 groups x 16, env i seeded 1000 + i // 16), 5 turns of up to K=5 synthetic actions
+per env (10 % unknown names), max 10 actions per trajectory.  One bench "step" = one whole
+rollout phase over the batch: restore the post-reset state (reset itself is excluded, as
+§8(d) specifies), 5 turn kernels, get_rollout_states metrics, trajectory scores and the
+StarPO reward normalisation.  Inputs are resident in HBM before timing.  The step is
+captured once in a HIP graph and replayed (launch-bound: one graph launch per rollout).
+
+Multi-GPU: weak scaling — every rank runs its own 8192 envs (global group ids preserved,
+rank r seeds groups r*512..), no collective on the data path; value = all ranks' env steps
+/ max-over-ranks time.
+
+Also reported: roofline of the dominant kernel (rmi_sokoban_step_turn) from HIP events,
+PMC HBM traffic from the committed rocprofv3 pass (profiles/), and the CPU baseline (the
+oracle's per-env Python port of the reference path, timed on this host).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from ragen_amd import ops, synthetic  # noqa: E402
+from ragen_amd.env import SokobanBatch  # noqa: E402
+from ragen_amd.env.configs import SokobanEnvConfig  # noqa: E402
+
+B_PER_GPU = 8192
+T_TURNS = 5
+K_ACTIONS = 5
+MAX_ACTIONS = 10
+GROUP = 16
+BYTES_PER_ENV_TURN = 141  # algorithmic bytes per Sokoban env-turn
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_sokoban_step_turn.json")
+
+
+class Rollout:
+    def __init__(self, device, rank, B=B_PER_GPU):
+        self.device = device
+        self.B = B
+        cfg = SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100)
+        self.env = SokobanBatch(cfg, B, T_TURNS, K_ACTIONS, device)
+        first_group = rank * (B // GROUP)
+        self.env.reset(synthetic.env_seeds(B, synthetic.ENV_SEED, GROUP, first_group))
+        e = self.env
+        self.snap = [x.clone() for x in (e.room_state, e.player, e.num_env_steps, e.boxes_on_target)]
+        ids, n = synthetic.rollout_actions(B, T_TURNS, K_ACTIONS, 1, 4, seed=synthetic.ACTION_SEED + rank)
+        self.ids = torch.from_numpy(ids).to(device)
+        self.n = torch.from_numpy(n).to(device)
+        self.seg = torch.arange(0, B + 1, GROUP, dtype=torch.int32, device=device)
+        self.norm = torch.empty(B, dtype=torch.float32, device=device)
+        self.metrics = torch.empty(B, 4, dtype=torch.float64, device=device)
+        self.turns = [ops.turn_struct(t, self.ids[t], self.n[t], None, MAX_ACTIONS, -0.1) for t in range(T_TURNS)]
+        self.st = e.struct()
+
+    def restore(self):
+        e = self.env
+        for dst, src in zip((e.room_state, e.player, e.num_env_steps, e.boxes_on_target), self.snap):
+            dst.copy_(src, non_blocking=True)
+        e.ep.reset_()
+
+    def step(self, events=None):
+        """One rollout phase.  events: optional list collecting (start, end) per turn kernel."""
+        self.restore()
+        for t in range(T_TURNS):
+            if events is not None:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+            ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
+            if events is not None:
+                b.record()
+                events.append((a, b))
+        m = ops.rollout_metrics(self.env.ep)
+        self.metrics.copy_(m)
+        score, pen = ops.trajectory_scores(self.env.ep)
+        ops.group_normalize(score, pen, self.seg, "identity", out=self.norm)
+
+
+def cpu_baseline(R, seconds_budget=20.0):
+    """Reference-shaped CPU path (oracle/port.py: per-env Python objects mirroring
+    EnvStateManager.step + SokobanEnv.step) on a bounded sample of the same workload:
+    the first n_envs envs of this rank's batch, same rooms, same synthetic actions."""
+    from oracle import port
+    n_envs = 2048
+    fixed = R.env.room_fixed[:n_envs].cpu().numpy()
+    state0 = R.snap[0][:n_envs].cpu().numpy()
+    player0 = R.snap[1][:n_envs].cpu().numpy()
+    ids = R.ids[:, :n_envs].cpu().numpy()
+    n = R.n[:, :n_envs].cpu().numpy()
+    steps = 0
+    reps = 0
+    dt = 0.0
+    while True:
+        envs = port.make_sokoban_envs(fixed, state0, player0)
+        t0 = time.perf_counter()
+        steps += port.sokoban_rollout(envs, ids, n, MAX_ACTIONS)
+        dt += time.perf_counter() - t0
+        reps += 1
+        if dt > seconds_budget / 2 or reps >= 8:
+            break
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{reps} x Sokoban 6x6 rollout of {n_envs} envs x {T_TURNS} turns (reset excluded), "
+                      f"{steps} env.step calls in {dt:.1f}s, 1 thread, oracle/port.py"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+
+    R = Rollout(device, rank)
+    # env steps per rollout (deterministic: every replay executes the same actions)
+    R.step()
+    torch.cuda.synchronize()
+    steps_per_rollout = int(R.env.ep.turn_exec.sum().item())
+    # active envs per launch = envs stepped in that turn (n_turns > t)
+    n_turns = R.env.ep.n_turns.cpu().numpy()
+    active_per_turn = [int((n_turns > t).sum()) for t in range(T_TURNS)]
+
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream(device)
+        s.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                R.step()
+        torch.cuda.current_stream(device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            R.step()
+        run = graph.replay
+    else:
+        run = R.step
+
+    for _ in range(args.warmup):
+        run()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.perf_counter() - t0
+    total_steps = steps_per_rollout * args.steps
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        c = torch.tensor([total_steps], dtype=torch.float64, device=device)
+        tdist.all_reduce(c)
+        total_steps = int(c.item())
+
+    # ---- dominant-kernel roofline: HIP events around every turn launch (eager, same stream)
+    events = []
+    n_prof = min(args.steps, 50)
+    for _ in range(n_prof):
+        R.step(events)
+    torch.cuda.synchronize()
+    durs = np.array([a.elapsed_time(b) for a, b in events]).reshape(n_prof, T_TURNS) * 1e-3  # s
+    bytes_per_launch = np.array(active_per_turn, np.float64) * BYTES_PER_ENV_TURN
+    achieved = float(bytes_per_launch.sum() * n_prof / durs.sum()) / 1e9  # GB/s
+    avg_launch_us = float(durs.mean() * 1e6)
+    traffic = None
+    if os.path.exists(PMC_FILE):
+        with open(PMC_FILE) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    # eager (no graph) rate, for reference
+    eager_steps = 20
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    for _ in range(eager_steps):
+        R.step()
+    torch.cuda.synchronize()
+    eager_ms = (time.perf_counter() - te) / eager_steps * 1e3
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            try:
+                cpu = cpu_baseline(R)
+            except Exception as ex:  # the baseline must never break the bench line
+                cpu = {"value": None, "unit": "env-steps/s", "cores": 1, "kind": "port", "sample": f"failed: {ex}"}
+        value = total_steps / elapsed
+        line = {
+            "metric": "env-steps/sec (whole node), Sokoban 6x6, 8192 envs x 5 turns",
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (fixed-seed actions; rooms generated with the reference's exact RNG streams)",
+            "config": {"workload": f"Sokoban 6x6 1-box, {B_PER_GPU} envs/GPU x {T_TURNS} turns, K={K_ACTIONS}, "
+                                   f"cap {MAX_ACTIONS}, groups of {GROUP}; rollout phase (reset excluded)",
+                       "envs_per_gpu": B_PER_GPU, "env_steps_per_rollout_rank0": steps_per_rollout,
+                       "graph": graph is not None, "parallelism": f"env-sharded x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "rmi_sokoban_step_turn", "avg_launch_us": avg_launch_us,
+                         "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn},
+            "cpu_baseline": cpu,
+            "eager_ms_per_step": eager_ms,
+            "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu and cpu.get("value") else None,
+        }
+        print(json.dumps(line), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,235 @@
+/*
+ * ragen_amd.h — C ABI of the MI355X (gfx950) rollout-and-advantage engine.
+ *
+ * Drop-in boundary for RAGEN's StarPO hot path (quanwei0/RAGEN @ 2025-07-04).
+ * The reference is pure Python; every entry point below replaces a Python loop of the
+ * reference, cited per function as  <file>:<line>  relative to the reference root.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) unless marked
+ *    [host].  The caller owns every buffer; no entry point allocates, frees or
+ *    synchronises.  Work is enqueued on `stream` (a hipStream_t; NULL = default stream).
+ *  - Env state is updated IN PLACE (the reference mutates env objects in place,
+ *    es_manager.py:161-167).
+ *  - Return value: RMI_OK (0) when the launch was enqueued; a negative code for an
+ *    invalid argument or a HIP launch failure.  Data-dependent errors that the reference
+ *    raises as Python exceptions (e.g. IndexError in bi-level GAE, core_algos.py:79)
+ *    are reported per row through the optional `err` buffer (u8[B], bit set = error),
+ *    readable after the stream has been synchronised.
+ *  - Per-turn episode outputs are stored turn-major ([T, B]) so each per-turn kernel
+ *    writes one contiguous row of B elements (coalesced).
+ */
+#ifndef RAGEN_AMD_H
+#define RAGEN_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rmi_stream_t; /* hipStream_t */
+
+enum {
+  RMI_OK = 0,
+  RMI_EINVAL = -1,  /* bad pointer / shape / parameter */
+  RMI_EDEVICE = -2, /* HIP runtime reported an error on launch */
+  RMI_EUNSUP = -3   /* configuration outside the kernels' supported envelope */
+};
+
+/* Episode-status flag bits (A1: EnvStatus, es_manager.py:17-24). */
+enum {
+  RMI_FLAG_TERMINATED = 1, /* EnvStatus.terminated */
+  RMI_FLAG_TRUNCATED = 2,  /* EnvStatus.truncated */
+  RMI_FLAG_DONE = 4        /* env no longer returned by step() (es_manager.py:168-169) */
+};
+
+/* Per-turn info bits (the turn_info dict of es_manager.py:116-128). */
+enum {
+  RMI_INFO_PRESENT = 1,   /* >=1 action executed this turn (turn_info non-empty) */
+  RMI_INFO_EFFECTIVE = 2, /* info['action_is_effective'] of the last executed action */
+  RMI_INFO_VALID = 4,     /* info['action_is_valid'] */
+  RMI_INFO_SUCCESS = 8    /* info['success'] */
+};
+
+/* Per-row error bits written to an optional err buffer. */
+enum {
+  RMI_ERR_ACTION = 1,  /* action id outside the env's action space */
+  RMI_ERR_INDEX = 2,   /* grid index out of range (numpy would raise IndexError) */
+  RMI_ERR_STATE = 4,   /* malformed state (e.g. grid byte > 7) */
+  RMI_ERR_UNSUP = 8    /* expression outside the Countdown evaluator's grammar */
+};
+
+/* ------------------------------------------------------------------ A1 episode status
+ * Replaces: EnvStatus + rollout_cache bookkeeping of EnvStateManager
+ *           (es_manager.py:17-24, :85, :130-144, :158-169).                          */
+typedef struct {
+  int32_t B;             /* number of envs in this batch (one env tag)                  */
+  int32_t T;             /* rows of the per-turn outputs (>= max_turn)                  */
+  int32_t* num_actions;  /* [B]  EnvStatus.num_actions                                  */
+  uint8_t* flags;        /* [B]  RMI_FLAG_* bits                                        */
+  int32_t* n_turns;      /* [B]  turns stepped = len(history) - 1                       */
+  double* penalty;       /* [B]  rollout_cache[env]['penalty'] (format penalty sum)     */
+  double* turn_reward;   /* [T,B] acc_reward of each turn (EnvStatus.rewards)           */
+  uint8_t* turn_info;    /* [T,B] RMI_INFO_* bits                                       */
+  uint8_t* turn_exec;    /* [T,B] number of actions executed in the turn                */
+} rmi_episode_t;
+
+/* Common per-turn inputs (what ContextManager.get_env_inputs hands to
+ * EnvStateManager.step, ctx_manager.py:332-352, after name->id mapping
+ * es_manager.py:230-240).                                                              */
+typedef struct {
+  int32_t turn;                /* row of the per-turn outputs to write                  */
+  int32_t K;                   /* max actions per turn (agent_proxy.max_actions_per_turn) */
+  const int8_t* actions;       /* [B,K] mapped action ids; 0 = name not in action_lookup  */
+  const uint8_t* n_actions;    /* [B]  number of parsed action strings (len(actions))     */
+  const uint8_t* has_input;    /* [B]  1 = env receives an input this turn; NULL = every
+                                  env whose RMI_FLAG_DONE bit is clear                     */
+  int32_t max_actions_per_traj;/* custom_envs.<tag>.max_actions_per_traj                  */
+  double format_penalty;       /* es_manager.format_penalty                               */
+} rmi_turn_t;
+
+/* ------------------------------------------------------------------------ Sokoban
+ * Replaces: EnvStateManager.step (es_manager.py:105-171) driving SokobanEnv.step
+ *           (sokoban/env.py:44-51) -> gym_sokoban SokobanEnv.step/_push/_move/_calc_reward
+ *           (third-party, restated in SURVEY.md App. A.1).
+ * One launch executes one whole turn (up to K actions) for every env of the batch.    */
+typedef struct {
+  int32_t H, W;               /* dim_room; H*W <= 64                                      */
+  int32_t num_boxes;          /* SokobanEnvConfig.num_boxes                               */
+  int32_t max_steps;          /* SokobanEnvConfig.max_steps                               */
+  const uint8_t* room_fixed;  /* [B,H*W]  room_fixed (0 wall, 1 floor, 2 target)           */
+  uint8_t* room_state;        /* [B,H*W]  room_state (0..5)                                */
+  int8_t* player;             /* [B,2]    player_position (row, col)                       */
+  int32_t* num_env_steps;     /* [B]                                                      */
+  int32_t* boxes_on_target;   /* [B]                                                      */
+} rmi_sokoban_t;
+
+int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                          uint8_t* err, rmi_stream_t stream);
+
+/* Replaces: SokobanEnv.reset (sokoban/env.py:28-42) -> generate_room (sokoban/utils.py:221-278)
+ * under all_seed (ragen/utils.py:7-18).  [host] CPU function: exact CPython-random /
+ * numpy-legacy MT19937 semantics.  Writes one room per seed.  Returns per seed
+ * 0 = ok, 1 = the reference would raise RuntimeError/RuntimeWarning (caller reseeds with
+ * abs(hash(str(seed))) % 2**32 exactly as sokoban/env.py:41).                           */
+int rmi_sokoban_generate_rooms(const int64_t* seeds /*[host][n]*/, int32_t n, int32_t H, int32_t W,
+                               int32_t num_boxes, int32_t search_depth,
+                               uint8_t* room_fixed /*[host][n,H*W]*/, uint8_t* room_state /*[host][n,H*W]*/,
+                               int8_t* player /*[host][n,2]*/, uint8_t* status /*[host][n]*/,
+                               int32_t n_threads);
+
+/* --------------------------------------------------------------------- FrozenLake
+ * Replaces: FrozenLakeEnv.step (frozen_lake/env.py:39-45) -> gymnasium FrozenLakeEnv.step
+ *           + categorical_sample (third-party, App. A.2), numpy PCG64 draws (App. A.5). */
+typedef struct {
+  int32_t nrow, ncol;         /* nrow*ncol <= 64                                          */
+  int32_t is_slippery;
+  double cs0, cs1, cs2;       /* cumsum of the slippery transition probabilities          */
+  const uint8_t* desc;        /* [B,nrow*ncol] ASCII 'S' 'F' 'H' 'G'                       */
+  int32_t* s;                 /* [B] current state                                        */
+  uint64_t* rng;              /* [4,B] PCG64 state_hi, state_lo, inc_hi, inc_lo            */
+} rmi_frozenlake_t;
+
+int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                             uint8_t* err, rmi_stream_t stream);
+
+/* ------------------------------------------------------------------------- Bandit
+ * Replaces: BanditEnv.step/compute_reward (bandit/env.py:62-76).                       */
+typedef struct {
+  int32_t action_space_start;
+  double lo_arm_score, hi_arm_loscore, hi_arm_hiscore, hi_arm_hiscore_prob;
+  const uint8_t* hi_is_first; /* [B] ACTION_LOOKUP[start] is the hi arm (bandit/env.py:25-39) */
+  uint64_t* rng;              /* [4,B] PCG64 state                                         */
+} rmi_bandit_t;
+
+int rmi_bandit_step_turn(const rmi_bandit_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                         uint8_t* err, rmi_stream_t stream);
+
+/* ---------------------------------------------------------------------- Countdown
+ * Replaces: CountdownEnv.step/compute_reward, check_format, check_correctness
+ *           (countdown/env.py:9-21, :58-78).  Actions are answer strings: in->actions is
+ * ignored; answer k of env b is answers[(b*K+k)*Lmax .. +answer_len[b*K+k]).             */
+typedef struct {
+  int32_t max_nums;           /* row stride of nums                                       */
+  double score, format_score; /* CountdownEnvConfig.score / .format_score                  */
+  const int32_t* nums;        /* [B,max_nums]                                              */
+  const int32_t* n_nums;      /* [B]                                                       */
+  const int32_t* target;      /* [B]                                                       */
+} rmi_countdown_t;
+
+int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                            const uint8_t* answers, const int32_t* answer_len, int32_t Lmax,
+                            uint8_t* err, rmi_stream_t stream);
+
+/* Single reward evaluation (no episode bookkeeping), for parity tests and the reward
+ * path of a batch of answers: reward[i] of answer i against nums/target row i.          */
+int rmi_countdown_reward(const rmi_countdown_t* env, const uint8_t* answers, const int32_t* answer_len,
+                         int32_t Lmax, int32_t n, double* reward, uint8_t* flags /*bit0 format bit1 correct*/,
+                         uint8_t* err, rmi_stream_t stream);
+
+/* --------------------------------------------------------- A16 rollout-state metrics
+ * Replaces: EnvStateManager.get_rollout_states (es_manager.py:173-207).
+ * out[B,4] f64: success, num_actions, action_is_effective, action_is_valid
+ * (the last two NaN when no turn carried info, i.e. the key is absent).                 */
+int rmi_rollout_metrics(const rmi_episode_t* ep, double* out, rmi_stream_t stream);
+
+/* Trajectory scores (ctx_manager.py:282 + get_masks_and_scores:64-65 + :217):
+ * score[b] = f32(sum over turns of turn_reward), pen[b] = f32(penalty[b]).              */
+int rmi_trajectory_scores(const rmi_episode_t* ep, float* score, float* pen, rmi_stream_t stream);
+
+/* ------------------------------------------------------- A10 reward normalisation
+ * Replaces: ContextManager._normalize_score_tensor (ctx_manager.py:175-226).
+ * Groups are contiguous segments [seg[g], seg[g+1]) (state: group_size runs, inductive:
+ * tag runs, batch: one segment).  out[b] = norm(score[b] + pen[b]).                     */
+enum { RMI_NORM_IDENTITY = 0, RMI_NORM_MEAN = 1, RMI_NORM_MEAN_STD = 2, RMI_NORM_ASYM_CLIP = 3 };
+int rmi_group_normalize(const float* score, const float* pen, const int32_t* seg, int32_t G, int32_t B,
+                        int32_t method, float* out, rmi_stream_t stream);
+
+/* --------------------------------------------------------------- A12 rollout filter
+ * Replaces: _filter_rollout (agent_trainer.py:461-500).  scores[G*gs] (row sums of
+ * original_rm_scores).  Writes per-group std/max/mean, keep[G] (1 = selected) and
+ * metrics[6] (f64: in_group_std/max/mean, chosen_in_group_std/max/mean means).
+ * Selection = top int(ratio*G) by std ('std', type 0) or by -std ('std_rev', type 1);
+ * ties broken by ascending group index (documented deviation: torch.topk's tie order is
+ * implementation-defined).  ratio == 1 keeps everything.  G <= 8192.                    */
+int rmi_filter_groups(const float* scores, int32_t G, int32_t gs, double ratio, int32_t type, float* g_std,
+                      float* g_max, float* g_mean, uint8_t* keep, double* metrics, rmi_stream_t stream);
+
+/* Row sum of a [B,L] f32 tensor (rm_scores.sum(-1), agent_trainer.py:467).              */
+int rmi_row_sum(const float* x, int64_t B, int64_t L, float* out, rmi_stream_t stream);
+
+/* ------------------------------------------------------------------- A13 advantages
+ * Replaces: verl compute_gae_advantage_return (called agent_trainer.py:77-83; App. A.4).
+ * variant 0 = legacy (RAGEN's snapshot), 1 = masked (newer verl).  Sequential f32
+ * recurrence in the reference's op order: bit-exact advantages/returns BEFORE whitening.
+ * row_stats [B,3] f64 (optional): per-row sum(adv*m), sum(adv^2*m), sum(m) for whitening.      */
+int rmi_gae(const float* r, const float* v, const uint8_t* mask, int64_t B, int64_t L, double gamma,
+            double lam, int32_t variant, float* adv, float* ret, double* row_stats, rmi_stream_t stream);
+
+/* Replaces: compute_bi_level_gae_advantage_return (core_algos.py:4-92) without the final
+ * whitening.  err[b] = RMI_ERR_INDEX where the reference raises IndexError (core_algos.py:79). */
+int rmi_bilevel_gae(const float* r, const float* v, const uint8_t* mask, int64_t B, int64_t L, double gamma,
+                    double lam, double high_level_gamma, float* adv, float* ret, double* row_stats,
+                    uint8_t* err, rmi_stream_t stream);
+
+/* Replaces: verl masked_whiten (core_algos.py:90; App. A.4), in place on x.
+ * If row_stats is NULL they are computed here.  scratch: rmi_whiten_scratch_bytes(B).    */
+size_t rmi_whiten_scratch_bytes(int64_t B);
+int rmi_masked_whiten(float* x, const uint8_t* mask, int64_t B, int64_t L, const double* row_stats,
+                      void* scratch, rmi_stream_t stream);
+
+/* Replaces: verl compute_grpo_outcome_advantage (agent_trainer.py:94-99; App. A.4) with
+ * contiguous groups seg[G+1] (RAGEN passes unique uids => every group has size 1).       */
+int rmi_grpo_outcome(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G,
+                     double eps, int32_t norm_by_std, float* adv, float* ret, rmi_stream_t stream);
+
+/* ------------------------------------------------------------------------- misc */
+const char* rmi_version(void);
+int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RAGEN_AMD_H */

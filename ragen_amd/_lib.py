@@ -1,0 +1,117 @@
+"""ctypes binding of the C ABI (include/ragen_amd.h) exported by ``_build/libragen_amd.so``.
+
+This is the Python side of the drop-in boundary: the product path always runs the HIP
+kernels in this library and fails loudly when the library is missing — there is no CPU
+fallback anywhere in ``ragen_amd``.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's libamdhip64 first so the library binds to the same HIP runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "libragen_amd.so")
+
+c_int32, c_int64, c_double, c_void_p, c_size_t = (ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
+                                                   ctypes.c_void_p, ctypes.c_size_t)
+
+RMI_OK, RMI_EINVAL, RMI_EDEVICE, RMI_EUNSUP = 0, -1, -2, -3
+FLAG_TERMINATED, FLAG_TRUNCATED, FLAG_DONE = 1, 2, 4
+INFO_PRESENT, INFO_EFFECTIVE, INFO_VALID, INFO_SUCCESS = 1, 2, 4, 8
+ERR_ACTION, ERR_INDEX, ERR_STATE, ERR_UNSUP = 1, 2, 4, 8
+NORM_METHODS = {"identity": 0, "mean": 1, "mean_std": 2, "asym_clip": 3}
+
+
+class Episode(ctypes.Structure):
+    _fields_ = [("B", c_int32), ("T", c_int32), ("num_actions", c_void_p), ("flags", c_void_p),
+                ("n_turns", c_void_p), ("penalty", c_void_p), ("turn_reward", c_void_p),
+                ("turn_info", c_void_p), ("turn_exec", c_void_p)]
+
+
+class Turn(ctypes.Structure):
+    _fields_ = [("turn", c_int32), ("K", c_int32), ("actions", c_void_p), ("n_actions", c_void_p),
+                ("has_input", c_void_p), ("max_actions_per_traj", c_int32), ("format_penalty", c_double)]
+
+
+class Sokoban(ctypes.Structure):
+    _fields_ = [("H", c_int32), ("W", c_int32), ("num_boxes", c_int32), ("max_steps", c_int32),
+                ("room_fixed", c_void_p), ("room_state", c_void_p), ("player", c_void_p),
+                ("num_env_steps", c_void_p), ("boxes_on_target", c_void_p)]
+
+
+class FrozenLake(ctypes.Structure):
+    _fields_ = [("nrow", c_int32), ("ncol", c_int32), ("is_slippery", c_int32), ("cs0", c_double),
+                ("cs1", c_double), ("cs2", c_double), ("desc", c_void_p), ("s", c_void_p), ("rng", c_void_p)]
+
+
+class Bandit(ctypes.Structure):
+    _fields_ = [("action_space_start", c_int32), ("lo_arm_score", c_double), ("hi_arm_loscore", c_double),
+                ("hi_arm_hiscore", c_double), ("hi_arm_hiscore_prob", c_double), ("hi_is_first", c_void_p),
+                ("rng", c_void_p)]
+
+
+class Countdown(ctypes.Structure):
+    _fields_ = [("max_nums", c_int32), ("score", c_double), ("format_score", c_double), ("nums", c_void_p),
+                ("n_nums", c_void_p), ("target", c_void_p)]
+
+
+_P = ctypes.POINTER
+_SIGS = {
+    "rmi_version": (ctypes.c_char_p, []),
+    "rmi_sokoban_step_turn": (c_int32, [_P(Sokoban), _P(Episode), _P(Turn), c_void_p, c_void_p]),
+    "rmi_sokoban_generate_rooms": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
+                                             c_void_p, c_void_p, c_void_p, c_int32]),
+    "rmi_frozenlake_step_turn": (c_int32, [_P(FrozenLake), _P(Episode), _P(Turn), c_void_p, c_void_p]),
+    "rmi_bandit_step_turn": (c_int32, [_P(Bandit), _P(Episode), _P(Turn), c_void_p, c_void_p]),
+    "rmi_countdown_step_turn": (c_int32, [_P(Countdown), _P(Episode), _P(Turn), c_void_p, c_void_p, c_int32,
+                                          c_void_p, c_void_p]),
+    "rmi_countdown_reward": (c_int32, [_P(Countdown), c_void_p, c_void_p, c_int32, c_int32, c_void_p, c_void_p,
+                                       c_void_p, c_void_p]),
+    "rmi_rollout_metrics": (c_int32, [_P(Episode), c_void_p, c_void_p]),
+    "rmi_trajectory_scores": (c_int32, [_P(Episode), c_void_p, c_void_p, c_void_p]),
+    "rmi_group_normalize": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
+    "rmi_filter_groups": (c_int32, [c_void_p, c_int32, c_int32, c_double, c_int32, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p]),
+    "rmi_row_sum": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "rmi_gae": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_double, c_double, c_int32, c_void_p,
+                          c_void_p, c_void_p, c_void_p]),
+    "rmi_bilevel_gae": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_double, c_double, c_double,
+                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_whiten_scratch_bytes": (c_size_t, [c_int64]),
+    "rmi_masked_whiten": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rmi_grpo_outcome": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_double, c_int32,
+                                   c_void_p, c_void_p, c_void_p]),
+    "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load the library (once).  Raises if it has not been built — no fallback."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"ragen_amd native library missing: {LIB_PATH}. Build it with `python -m ragen_amd.build` "
+                              "(hipcc, gfx950). The engine has no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc, what):
+    if rc == RMI_OK:
+        return
+    if rc == RMI_EINVAL:
+        raise ValueError(f"{what}: invalid argument (RMI_EINVAL)")
+    if rc == RMI_EUNSUP:
+        raise NotImplementedError(f"{what}: configuration outside the kernel envelope (RMI_EUNSUP)")
+    raise RuntimeError(f"{what}: HIP launch failed (code {rc})")

@@ -1,0 +1,126 @@
+// common.hpp — shared device helpers for the gfx950 rollout kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ragen_amd.h"
+
+#define RMI_API extern "C" __attribute__((visibility("default")))
+
+namespace rmi {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+constexpr int kMaxK = 8;     // max actions per turn handled by the step kernels
+
+inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? RMI_OK : RMI_EDEVICE;
+}
+
+inline hipStream_t as_stream(rmi_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// --------------------------------------------------------------- PCG64 (numpy)
+// numpy PCG64 = pcg_setseq_128_xsl_rr_64: step state = state*M + inc (mod 2^128),
+// then output XSL-RR of the NEW state; Generator.random() = (out >> 11) * 2^-53.
+// (verified bit-exact against numpy in tests/test_oracle.py.)
+struct Pcg64 {
+  uint64_t s_hi, s_lo, i_hi, i_lo;
+
+  __device__ __forceinline__ uint64_t next64() {
+    const uint64_t m_hi = 0x2360ED051FC65DA4ull, m_lo = 0x4385DF649FCCF645ull;
+    uint64_t lo = s_lo * m_lo;
+    uint64_t hi = __umul64hi(s_lo, m_lo) + s_lo * m_hi + s_hi * m_lo;
+    uint64_t nlo = lo + i_lo;
+    hi += i_hi + (nlo < lo ? 1ull : 0ull);
+    s_lo = nlo;
+    s_hi = hi;
+    uint64_t x = s_hi ^ s_lo;
+    unsigned rot = (unsigned)(s_hi >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+  }
+  __device__ __forceinline__ double next_double() {
+    return (double)(next64() >> 11) * (1.0 / 9007199254740992.0);
+  }
+};
+
+__device__ __forceinline__ Pcg64 load_pcg(const uint64_t* rng, int64_t B, int64_t b) {
+  Pcg64 p;
+  p.s_hi = rng[b];
+  p.s_lo = rng[B + b];
+  p.i_hi = rng[2 * B + b];
+  p.i_lo = rng[3 * B + b];
+  return p;
+}
+__device__ __forceinline__ void store_pcg(uint64_t* rng, int64_t B, int64_t b, const Pcg64& p) {
+  rng[b] = p.s_hi;
+  rng[B + b] = p.s_lo;
+}
+
+// ------------------------------------------------------------ the turn driver (A3)
+// EnvStateManager.step for one env (es_manager.py:149-169):
+//   valid = [ids of known names]           (_extract_map_valid_actions :230-240)
+//   execute valid[:max - num_actions] one by one, stop at the first done (:116-128)
+//   penalty if len(valid) != len(actions) or not valid                    (:158-159)
+//   num_actions += executed; rewards.append(acc); done => terminated, truncated = !success
+//   cap: num_actions >= max and not done => truncated = terminated = True    (:163-166)
+// Env::step(a, reward&, done&, effective&, success&) -> false on an invalid action id.
+struct TurnOut {
+  double acc;
+  uint8_t info;
+  uint8_t exec;
+  bool stepped_any_state;  // the env's state may have changed
+};
+
+template <class Env>
+__device__ __forceinline__ TurnOut run_turn(Env& e, const int8_t* acts, int n_act, int K, int32_t& num_actions,
+                                            uint8_t& flags, int32_t& n_turns, double& penalty, int max_actions,
+                                            double format_penalty, uint8_t& err) {
+  TurnOut o;
+  o.acc = 0.0;
+  o.info = 0;
+  o.exec = 0;
+  o.stepped_any_state = false;
+  flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (:168)
+  const int left = max_actions - num_actions;
+  int nv = 0;
+  bool stop = false, succ_last = false;
+  if (n_act > K) n_act = K;
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) {
+    if (k < n_act) {
+      const int a = acts[k];
+      if (a != 0) {
+        if (!stop && nv < left) {
+          double r;
+          bool done, eff, succ;
+          if (!e.step(a, r, done, eff, succ)) {
+            err |= RMI_ERR_ACTION;
+            stop = true;  // the reference raises here; leave the rest of the turn untouched
+          } else {
+            o.acc += r;
+            o.exec++;
+            o.stepped_any_state = true;
+            o.info = (uint8_t)(RMI_INFO_PRESENT | (eff ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID |
+                               (succ ? RMI_INFO_SUCCESS : 0));
+            succ_last = succ;
+            if (done) stop = true;
+          }
+        }
+        nv++;
+      }
+    }
+  }
+  const bool turn_done = (o.info & RMI_INFO_PRESENT) && stop && !(err & RMI_ERR_ACTION);
+  if (nv != n_act || nv == 0) penalty += format_penalty;
+  num_actions += o.exec;
+  n_turns += 1;
+  if (turn_done) {
+    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_DONE;
+    flags = succ_last ? (uint8_t)(flags & ~RMI_FLAG_TRUNCATED) : (uint8_t)(flags | RMI_FLAG_TRUNCATED);
+  } else if (num_actions >= max_actions) {
+    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
+  }
+  return o;
+}
+
+}  // namespace rmi

@@ -1,0 +1,688 @@
+// countdown.hip — Countdown rule reward on device (gfx950), one thread per answer.
+//
+// Replaces CountdownEnv.step/compute_reward (countdown/env.py:58-78) with
+//   check_format      (:9-14)  re.findall(r'\d+') multiset == nums   -> exact, incl. every
+//                               Unicode Nd digit (Python 3.10 / Unicode 13.0 table below)
+//   check_correctness (:16-21) eval(expr, {"__builtins__": None}, {}) within 1e-5 of target
+// The evaluator implements Python's expression semantics for the grammar an arithmetic
+// answer can use: int literals (underscores, no leading zeros), float literals, + - * / //
+// % ** << >> & | ^, unary + - ~, parentheses, whitespace, '#' comments, Python int/float
+// rules (true division, floor division/modulo signs, int**negative -> float, ZeroDivision
+// -> not correct).  Bytes whose eval result the evaluator does not model (letters and
+// keywords, '_' outside a literal, quotes, '[', '{', '.', comparisons, '\\') make the answer
+// "not correct" AND set RMI_ERR_UNSUP in err[] so a caller can see the envelope was left;
+// every other byte only yields errors in Python too (SyntaxError/TypeError -> False).
+// int results beyond 64 bits (Python big ints) are flagged RMI_ERR_UNSUP as well.
+#include <math.h>
+
+#include "common.hpp"
+
+namespace rmi {
+namespace {
+
+__constant__ uint32_t kNdStarts[65] = {
+    0x30,    0x660,   0x6f0,   0x7c0,   0x966,   0x9e6,   0xa66,   0xae6,   0xb66,   0xbe6,   0xc66,   0xce6,   0xd66,
+    0xde6,   0xe50,   0xed0,   0xf20,   0x1040,  0x1090,  0x17e0,  0x1810,  0x1946,  0x19d0,  0x1a80,  0x1a90,  0x1b50,
+    0x1bb0,  0x1c40,  0x1c50,  0xa620,  0xa8d0,  0xa900,  0xa9d0,  0xa9f0,  0xaa50,  0xabf0,  0xff10,  0x104a0, 0x10d30,
+    0x11066, 0x110f0, 0x11136, 0x111d0, 0x112f0, 0x11450, 0x114d0, 0x11650, 0x116c0, 0x11730, 0x118e0, 0x11950, 0x11c50,
+    0x11d50, 0x11da0, 0x16a60, 0x16b50, 0x1d7ce, 0x1d7d8, 0x1d7e2, 0x1d7ec, 0x1d7f6, 0x1e140, 0x1e2f0, 0x1e950, 0x1fbf0};
+
+__device__ __forceinline__ int nd_value(uint32_t cp) {  // -1 if not a decimal digit
+  if (cp < 0x30) return -1;
+  if (cp <= 0x39) return (int)(cp - 0x30);
+  if (cp < 0x660) return -1;
+#pragma unroll 1
+  for (int i = 1; i < 65; ++i)
+    if (cp >= kNdStarts[i] && cp < kNdStarts[i] + 10) return (int)(cp - kNdStarts[i]);
+  return -1;
+}
+
+// decode one UTF-8 code point at s[i]; returns its length (invalid bytes decode as themselves)
+__device__ __forceinline__ int utf8_next(const uint8_t* s, int n, int i, uint32_t& cp) {
+  const uint8_t c = s[i];
+  if (c < 0x80) {
+    cp = c;
+    return 1;
+  }
+  int len = (c >= 0xF0) ? 4 : (c >= 0xE0) ? 3 : (c >= 0xC0) ? 2 : 1;
+  if (i + len > n || len == 1) {
+    cp = c;
+    return 1;
+  }
+  cp = c & (0x7F >> len);
+  for (int k = 1; k < len; ++k) cp = (cp << 6) | (s[i + k] & 0x3F);
+  return len;
+}
+
+// check_format: sorted([int(x) for x in re.findall(r'\d+', eq)]) == sorted(nums)
+__device__ bool check_format(const uint8_t* s, int n, const int32_t* nums, int n_nums) {
+  constexpr int kMax = 8;
+  uint64_t found[kMax];
+  int nf = 0;
+  bool in_run = false, overflow = false, too_many = false;
+  uint64_t cur = 0;
+  for (int i = 0; i < n;) {
+    uint32_t cp;
+    const int len = utf8_next(s, n, i, cp);
+    const int d = nd_value(cp);
+    if (d >= 0) {
+      if (!in_run) {
+        in_run = true;
+        cur = 0;
+        overflow = false;
+      }
+      if (cur > (0xFFFFFFFFFFFFFFFFull - 9) / 10) overflow = true;
+      else cur = cur * 10 + (uint64_t)d;
+    } else if (in_run) {
+      in_run = false;
+      if (nf < kMax) found[nf++] = overflow ? 0xFFFFFFFFFFFFFFFFull : cur;
+      else too_many = true;
+    }
+    i += len;
+  }
+  if (in_run) {
+    if (nf < kMax) found[nf++] = overflow ? 0xFFFFFFFFFFFFFFFFull : cur;
+    else too_many = true;
+  }
+  if (too_many || nf != n_nums) return false;
+  // multiset equality: match every num (nums may be negative -> never equal a digit run)
+  bool used[kMax] = {false, false, false, false, false, false, false, false};
+  for (int j = 0; j < n_nums; ++j) {
+    bool hit = false;
+    for (int k = 0; k < nf; ++k) {
+      if (!used[k] && nums[j] >= 0 && found[k] == (uint64_t)nums[j]) {
+        used[k] = true;
+        hit = true;
+        break;
+      }
+    }
+    if (!hit) return false;
+  }
+  return true;
+}
+
+// ------------------------------------------------------------------ evaluator
+struct Val {
+  bool is_f;
+  long long i;
+  double f;
+  __device__ double as_f() const { return is_f ? f : (double)i; }
+};
+
+enum Op : int8_t {
+  OP_LPAREN = 0,
+  OP_OR, OP_XOR, OP_AND, OP_SHL, OP_SHR, OP_ADD, OP_SUB, OP_MUL, OP_DIV, OP_FDIV, OP_MOD,
+  OP_NEG, OP_POS, OP_INV, OP_POW
+};
+__device__ __forceinline__ int prec(int op) {
+  switch (op) {
+    case OP_OR: return 1;
+    case OP_XOR: return 2;
+    case OP_AND: return 3;
+    case OP_SHL: case OP_SHR: return 4;
+    case OP_ADD: case OP_SUB: return 5;
+    case OP_MUL: case OP_DIV: case OP_FDIV: case OP_MOD: return 6;
+    case OP_NEG: case OP_POS: case OP_INV: return 7;
+    case OP_POW: return 8;
+    default: return 0;
+  }
+}
+
+enum EvalStatus { EV_OK = 0, EV_ERR = 1, EV_UNSUP = 2 };
+
+__device__ double py_floor_div_f(double vx, double wx, double* modp) {  // CPython float_divmod
+  double mod = fmod(vx, wx);
+  double div = (vx - mod) / wx;
+  if (mod != 0.0) {
+    if ((wx < 0) != (mod < 0)) {
+      mod += wx;
+      div -= 1.0;
+    }
+  } else {
+    mod = copysign(0.0, wx);
+  }
+  double floordiv;
+  if (div != 0.0) {
+    floordiv = floor(div);
+    if (div - floordiv > 0.5) floordiv += 1.0;
+  } else {
+    floordiv = copysign(0.0, vx / wx);
+  }
+  *modp = mod;
+  return floordiv;
+}
+
+__device__ int apply_unary(int op, Val& a) {
+  if (op == OP_POS) return EV_OK;
+  if (op == OP_NEG) {
+    if (a.is_f) a.f = -a.f;
+    else {
+      if (a.i == (-9223372036854775807LL - 1)) return EV_UNSUP;
+      a.i = -a.i;
+    }
+    return EV_OK;
+  }
+  if (a.is_f) return EV_ERR;  // ~float -> TypeError
+  a.i = ~a.i;
+  return EV_OK;
+}
+
+__device__ int float_pow(double iv, double iw, double& out) {  // CPython float_pow (non-complex cases)
+  if (iw == 0.0) { out = 1.0; return EV_OK; }
+  if (iv != iv) { out = iv; return EV_OK; }
+  if (iw != iw) { out = iv == 1.0 ? 1.0 : iw; return EV_OK; }
+  if (iv == 1.0) { out = 1.0; return EV_OK; }
+  if (iv == 0.0) {
+    if (iw < 0.0) return EV_ERR;  // ZeroDivisionError
+    const bool odd = floor(iw) == iw && fmod(fabs(iw), 2.0) == 1.0;
+    out = odd ? iv : 0.0;
+    return EV_OK;
+  }
+  bool negate = false;
+  if (iv < 0.0) {
+    if (iw != floor(iw)) return EV_UNSUP;  // Python returns a complex number
+    iv = -iv;
+    negate = fmod(fabs(iw), 2.0) == 1.0;
+  }
+  double r = pow(iv, iw);
+  if (negate) r = -r;
+  if (isinf(r) && !isinf(iv) && !isinf(iw)) return EV_ERR;  // OverflowError
+  out = r;
+  return EV_OK;
+}
+
+__device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
+  const bool fl = a.is_f || b.is_f;
+  out.is_f = false;
+  out.i = 0;
+  out.f = 0;
+  switch (op) {
+    case OP_ADD:
+    case OP_SUB:
+    case OP_MUL:
+      if (fl) {
+        const double x = a.as_f(), y = b.as_f();
+        out.is_f = true;
+        out.f = op == OP_ADD ? x + y : (op == OP_SUB ? x - y : x * y);
+        return EV_OK;
+      } else {
+        long long r;
+        bool ov = op == OP_ADD ? __builtin_add_overflow(a.i, b.i, &r)
+                               : (op == OP_SUB ? __builtin_sub_overflow(a.i, b.i, &r) : __builtin_mul_overflow(a.i, b.i, &r));
+        if (ov) return EV_UNSUP;
+        out.i = r;
+        return EV_OK;
+      }
+    case OP_DIV: {
+      if (!fl) {
+        if (b.i == 0) return EV_ERR;
+        const long long lim = 9007199254740992LL;
+        if (a.i > lim || a.i < -lim || b.i > lim || b.i < -lim) return EV_UNSUP;
+      }
+      const double y = b.as_f();
+      if (y == 0.0) return EV_ERR;
+      out.is_f = true;
+      out.f = a.as_f() / y;
+      return EV_OK;
+    }
+    case OP_FDIV:
+    case OP_MOD:
+      if (fl) {
+        const double y = b.as_f();
+        if (y == 0.0) return EV_ERR;
+        double mod;
+        const double q = py_floor_div_f(a.as_f(), y, &mod);
+        out.is_f = true;
+        out.f = op == OP_FDIV ? q : mod;
+        return EV_OK;
+      } else {
+        if (b.i == 0) return EV_ERR;
+        if (a.i == (-9223372036854775807LL - 1) && b.i == -1) return EV_UNSUP;
+        long long q = a.i / b.i, r = a.i % b.i;
+        if (r != 0 && ((r < 0) != (b.i < 0))) {
+          q -= 1;
+          r += b.i;
+        }
+        out.i = op == OP_FDIV ? q : r;
+        return EV_OK;
+      }
+    case OP_POW:
+      if (!fl && b.i >= 0) {
+        long long base = a.i, e = b.i, acc = 1;
+        while (e) {
+          if (e & 1) {
+            if (__builtin_mul_overflow(acc, base, &acc)) return EV_UNSUP;
+          }
+          e >>= 1;
+          if (e && __builtin_mul_overflow(base, base, &base)) {
+            // base overflow only matters if another bit remains
+            return EV_UNSUP;
+          }
+        }
+        out.i = acc;
+        return EV_OK;
+      } else {
+        if (!fl && a.i == 0) return EV_ERR;  // 0 ** negative int -> ZeroDivisionError
+        out.is_f = true;
+        return float_pow(a.as_f(), b.as_f(), out.f);
+      }
+    case OP_SHL:
+    case OP_SHR:
+      if (fl) return EV_ERR;
+      if (b.i < 0) return EV_ERR;  // ValueError: negative shift count
+      if (op == OP_SHR) {
+        out.i = b.i >= 64 ? (a.i < 0 ? -1 : 0) : (a.i >> b.i);
+      } else {
+        if (a.i == 0) { out.i = 0; return EV_OK; }
+        if (b.i >= 63) return EV_UNSUP;
+        const long long r = a.i * (1LL << b.i);
+        if ((r >> b.i) != a.i) return EV_UNSUP;
+        out.i = r;
+      }
+      return EV_OK;
+    case OP_AND:
+    case OP_OR:
+    case OP_XOR:
+      if (fl) return EV_ERR;
+      out.i = op == OP_AND ? (a.i & b.i) : (op == OP_OR ? (a.i | b.i) : (a.i ^ b.i));
+      return EV_OK;
+  }
+  return EV_ERR;
+}
+
+constexpr int kStack = 48;
+
+struct Machine {
+  Val vals[kStack];
+  int8_t ops[kStack];
+  int nv = 0, no = 0;
+  int status = EV_OK;
+
+  __device__ bool reduce_one() {
+    const int op = ops[--no];
+    if (op == OP_NEG || op == OP_POS || op == OP_INV) {
+      if (nv < 1) { status = EV_ERR; return false; }
+      const int st = apply_unary(op, vals[nv - 1]);
+      if (st != EV_OK) { status = st; return false; }
+      return true;
+    }
+    if (nv < 2) { status = EV_ERR; return false; }
+    Val r;
+    const int st = apply_binary(op, vals[nv - 2], vals[nv - 1], r);
+    if (st != EV_OK) { status = st; return false; }
+    vals[nv - 2] = r;
+    nv -= 1;
+    return true;
+  }
+  __device__ bool push_op(int op) {
+    if (no >= kStack) { status = EV_UNSUP; return false; }
+    ops[no++] = (int8_t)op;
+    return true;
+  }
+  __device__ bool push_val(const Val& v) {
+    if (nv >= kStack) { status = EV_UNSUP; return false; }
+    vals[nv++] = v;
+    return true;
+  }
+  __device__ bool binary(int op) {  // pop higher/equal-precedence operators, then push
+    const int p = prec(op);
+    const bool right = op == OP_POW;
+    while (no > 0 && ops[no - 1] != OP_LPAREN) {
+      const int q = prec(ops[no - 1]);
+      if (q > p || (q == p && !right)) {
+        if (!reduce_one()) return false;
+      } else {
+        break;
+      }
+    }
+    return push_op(op);
+  }
+};
+
+__device__ __forceinline__ bool is_digit(uint8_t c) { return c >= '0' && c <= '9'; }
+__device__ __forceinline__ bool is_alpha(uint8_t c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+
+__device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                      1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+// Lex a number literal at s[i]; returns the index after it.  status EV_ERR = SyntaxError.
+__device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
+  uint64_t mant = 0;
+  int ndig = 0, frac = 0, exp10 = 0;
+  bool is_float = false, overflow = false, leading_zero = false, nonzero_digit = false;
+  bool first = true;
+  auto digits = [&](bool in_frac) {
+    bool prev_digit = false;
+    while (i < n && (is_digit(s[i]) || (s[i] == '_' && prev_digit && i + 1 < n && is_digit(s[i + 1])))) {
+      if (s[i] == '_') {
+        i++;
+        prev_digit = false;
+        continue;
+      }
+      const int d = s[i] - '0';
+      if (first && !in_frac) {
+        leading_zero = d == 0;
+        first = false;
+      }
+      if (d) nonzero_digit = true;
+      if (mant > (0xFFFFFFFFFFFFFFFFull - 9) / 10) overflow = true;
+      else {
+        mant = mant * 10 + (uint64_t)d;
+        if (mant || ndig) ndig++;
+      }
+      if (in_frac) frac++;
+      prev_digit = true;
+      i++;
+    }
+    return prev_digit;
+  };
+  const bool had_int = digits(false);
+  if (i < n && s[i] == '.') {
+    is_float = true;
+    i++;
+    digits(true);
+  }
+  (void)had_int;
+  if (i < n && (s[i] == 'e' || s[i] == 'E')) {
+    int j = i + 1;
+    int sign = 1;
+    if (j < n && (s[j] == '+' || s[j] == '-')) {
+      sign = s[j] == '-' ? -1 : 1;
+      j++;
+    }
+    if (j < n && is_digit(s[j])) {
+      int e = 0;
+      bool prev = false;
+      while (j < n && (is_digit(s[j]) || (s[j] == '_' && prev && j + 1 < n && is_digit(s[j + 1])))) {
+        if (s[j] != '_') {
+          if (e < 100000) e = e * 10 + (s[j] - '0');
+          prev = true;
+        } else {
+          prev = false;
+        }
+        j++;
+      }
+      exp10 = sign * e;
+      is_float = true;
+      i = j;
+    } else {
+      status = EV_UNSUP;  // "1e" / "1ex": name-like tail
+      return i;
+    }
+  }
+  if (i < n && (is_alpha(s[i]) || s[i] == '_' || s[i] == '.' || s[i] >= 0x80)) {
+    status = EV_UNSUP;  // 1j, 0x.., 1if.., attribute access: outside the modelled grammar
+    return i;
+  }
+  if (!is_float) {
+    if (leading_zero && nonzero_digit) {
+      status = EV_ERR;  // leading zeros in decimal integer literals are not permitted
+      return i;
+    }
+    if (overflow || mant > 9223372036854775807ull) {
+      status = EV_UNSUP;  // Python big int
+      return i;
+    }
+    v.is_f = false;
+    v.i = (long long)mant;
+    return i;
+  }
+  // float literal: exact when mantissa <= 2^53 and |power of ten| <= 22 (one rounding)
+  const int e10 = exp10 - frac;
+  if (overflow || mant > 9007199254740992ull || e10 > 22 || e10 < -22) {
+    if (mant == 0 && !overflow) {
+      v.is_f = true;
+      v.f = 0.0;
+      return i;
+    }
+    status = EV_UNSUP;
+    return i;
+  }
+  v.is_f = true;
+  v.f = e10 >= 0 ? (double)mant * kPow10[e10] : (double)mant / kPow10[-e10];
+  return i;
+}
+
+// returns EV_OK with value in out, EV_ERR (Python raises), EV_UNSUP (outside the model)
+__device__ int py_eval(const uint8_t* s, int n, Val& out) {
+  Machine m;
+  bool expect_operand = true;
+  int depth = 0;
+  // eval() strips leading spaces/tabs; ctx_manager already .strip()s the action
+  int i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    if (c == ' ' || c == '\t' || c == '\f') { i++; continue; }
+    if (c == '#') {  // comment to end of line
+      while (i < n && s[i] != '\n' && s[i] != '\r') i++;
+      continue;
+    }
+    if (c == '\n' || c == '\r') {
+      if (depth > 0) { i++; continue; }
+      // a newline at depth 0 ends the expression: only whitespace/comments may follow
+      int j = i;
+      while (j < n) {
+        const uint8_t d = s[j];
+        if (d == ' ' || d == '\t' || d == '\f' || d == '\n' || d == '\r') { j++; continue; }
+        if (d == '#') { while (j < n && s[j] != '\n' && s[j] != '\r') j++; continue; }
+        return EV_ERR;
+      }
+      i = n;
+      break;
+    }
+    if (is_digit(c) || (c == '.' && i + 1 < n && is_digit(s[i + 1]))) {
+      if (!expect_operand) return EV_ERR;
+      Val v;
+      int st = EV_OK;
+      i = lex_number(s, n, i, v, st);
+      if (st != EV_OK) return st;
+      if (!m.push_val(v)) return m.status;
+      expect_operand = false;
+      continue;
+    }
+    if (c == '(') {
+      if (!expect_operand) return EV_ERR;  // call of a number -> TypeError (not correct either way)
+      if (!m.push_op(OP_LPAREN)) return m.status;
+      depth++;
+      i++;
+      continue;
+    }
+    if (c == ')') {
+      if (expect_operand || depth == 0) return EV_ERR;  // "()" is an empty tuple -> TypeError
+      while (m.no > 0 && m.ops[m.no - 1] != OP_LPAREN)
+        if (!m.reduce_one()) return m.status;
+      m.no--;  // pop '('
+      depth--;
+      i++;
+      continue;
+    }
+    if (expect_operand) {
+      int op = -1;
+      if (c == '-') op = OP_NEG;
+      else if (c == '+') op = OP_POS;
+      else if (c == '~') op = OP_INV;
+      if (op >= 0) {
+        if (!m.push_op(op)) return m.status;
+        i++;
+        continue;
+      }
+    } else {
+      int op = -1, len = 1;
+      const uint8_t d = i + 1 < n ? s[i + 1] : 0;
+      switch (c) {
+        case '+': op = OP_ADD; break;
+        case '-': op = OP_SUB; break;
+        case '*': if (d == '*') { op = OP_POW; len = 2; } else op = OP_MUL; break;
+        case '/': if (d == '/') { op = OP_FDIV; len = 2; } else op = OP_DIV; break;
+        case '%': op = OP_MOD; break;
+        case '&': op = OP_AND; break;
+        case '|': op = OP_OR; break;
+        case '^': op = OP_XOR; break;
+        case '<': if (d == '<') { op = OP_SHL; len = 2; } break;
+        case '>': if (d == '>') { op = OP_SHR; len = 2; } break;
+        default: break;
+      }
+      if (op >= 0) {
+        // augmented assignment ("+=") and '==' etc. are not expressions
+        if (i + len < n && s[i + len] == '=') {
+          if (c == '<' || c == '>') return EV_UNSUP;  // "<<=" / ">>=" vs comparisons: leave the model
+          return EV_ERR;
+        }
+        if (!m.binary(op)) return m.status;
+        expect_operand = true;
+        i += len;
+        continue;
+      }
+    }
+    // anything else
+    if (is_alpha(c) || c == '_' || c == '"' || c == '\'' || c == '[' || c == '{' || c == '.' || c == '<' ||
+        c == '>' || c == '=' || c == '!' || c == '\\' || c >= 0x80)
+      return (c == '=' && !(i + 1 < n && s[i + 1] == '=')) ? EV_ERR : EV_UNSUP;
+    return EV_ERR;  // ',', ';', ':', '@', '$', '?', '`', ']', '}', control chars ...
+  }
+  if (expect_operand || depth != 0) return EV_ERR;
+  while (m.no > 0) {
+    if (m.ops[m.no - 1] == OP_LPAREN) return EV_ERR;
+    if (!m.reduce_one()) return m.status;
+  }
+  if (m.nv != 1) return EV_ERR;
+  out = m.vals[0];
+  return EV_OK;
+}
+
+// compute_reward (countdown/env.py:69-78): 0 | format_score | score ; flags bit0 format bit1 correct
+__device__ double countdown_reward(const uint8_t* s, int n, const int32_t* nums, int n_nums, int32_t target,
+                                   double score, double format_score, uint8_t& flags, uint8_t& err) {
+  flags = 0;
+  if (!check_format(s, n, nums, n_nums)) return 0.0;
+  flags |= 1;
+  Val v;
+  const int st = py_eval(s, n, v);
+  bool correct = false;
+  if (st == EV_UNSUP) err |= RMI_ERR_UNSUP;
+  if (st == EV_OK) {
+    if (v.is_f) correct = fabs(v.f - (double)target) < 1e-5;  // abs(result - target) < 1e-5
+    else correct = v.i == (long long)target;
+  }
+  if (!correct) return format_score;
+  flags |= 2;
+  return score;
+}
+
+struct CountdownDev {
+  const uint8_t* answers;  // this env's [K, Lmax]
+  const int32_t* lens;     // this env's [K]
+  int Lmax;
+  const int32_t* nums;
+  int n_nums;
+  int32_t target;
+  double score, format_score;
+  int k_next;  // index of the answer the next step() consumes
+  uint8_t err;
+  __device__ bool step(int a, double& reward, bool& done, bool& eff, bool& success) {
+    // `a` is the 1-based slot of the answer string (the host passes 1..K for every parsed action)
+    const int k = a - 1;
+    if (k < 0) return false;
+    int n = lens[k];
+    if (n > Lmax) n = Lmax;
+    uint8_t fl;
+    reward = countdown_reward(answers + (int64_t)k * Lmax, n, nums, n_nums, target, score, format_score, fl, err);
+    done = true;
+    eff = reward > 0;
+    success = reward == score;
+    return true;
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
+                                                                     rmi_turn_t in, const uint8_t* __restrict__ answers,
+                                                                     const int32_t* __restrict__ answer_len, int Lmax,
+                                                                     uint8_t* __restrict__ err_out) {
+  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int B = ep.B;
+  if (b >= B) return;
+  uint8_t flags = ep.flags[b];
+  const bool act = in.has_input ? (in.has_input[b] != 0) : !(flags & RMI_FLAG_DONE);
+  if (!act) return;
+  CountdownDev e;
+  e.answers = answers + b * (int64_t)in.K * Lmax;
+  e.lens = answer_len + b * (int64_t)in.K;
+  e.Lmax = Lmax;
+  e.nums = env.nums + b * (int64_t)env.max_nums;
+  e.n_nums = env.n_nums[b];
+  e.target = env.target[b];
+  e.score = env.score;
+  e.format_score = env.format_score;
+  e.err = 0;
+  // every parsed answer string is a valid action (no action_lookup: es_manager.py:234-235)
+  int8_t acts[kMaxK];
+  const int n_act = in.n_actions[b];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) acts[k] = (int8_t)(k + 1);
+  uint8_t err = 0;
+  int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
+  double penalty = ep.penalty[b];
+  TurnOut o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
+                       in.format_penalty, err);
+  ep.num_actions[b] = num_actions;
+  ep.flags[b] = flags;
+  ep.n_turns[b] = n_turns;
+  ep.penalty[b] = penalty;
+  const int64_t tb = (int64_t)in.turn * B + b;
+  ep.turn_reward[tb] = o.acc;
+  ep.turn_info[tb] = o.info;
+  ep.turn_exec[tb] = o.exec;
+  err |= e.err;
+  if (err_out && err) err_out[b] |= err;
+}
+
+__global__ __launch_bounds__(kBlock) void countdown_reward_kernel(rmi_countdown_t env,
+                                                                  const uint8_t* __restrict__ answers,
+                                                                  const int32_t* __restrict__ answer_len, int Lmax,
+                                                                  int n, double* __restrict__ reward,
+                                                                  uint8_t* __restrict__ flags_out,
+                                                                  uint8_t* __restrict__ err_out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint8_t fl = 0, err = 0;
+  int len = answer_len[i];
+  if (len > Lmax) len = Lmax;
+  if (len < 0) len = 0;
+  const double r = countdown_reward(answers + i * (int64_t)Lmax, len, env.nums + i * (int64_t)env.max_nums,
+                                    env.n_nums[i], env.target[i], env.score, env.format_score, fl, err);
+  reward[i] = r;
+  if (flags_out) flags_out[i] = fl;
+  if (err_out) err_out[i] = err;
+}
+
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                    const uint8_t* answers, const int32_t* answer_len, int32_t Lmax, uint8_t* err,
+                                    rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !ep || !in || !answers || !answer_len || Lmax <= 0 || !env->nums || !env->n_nums || !env->target ||
+      env->max_nums <= 0 || env->max_nums > 8)
+    return RMI_EINVAL;
+  if (in->K < 0 || in->K > kMaxK || in->turn < 0 || in->turn >= ep->T || !in->n_actions || !ep->num_actions ||
+      !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
+    return RMI_EINVAL;
+  if (ep->B == 0) return RMI_OK;
+  hipLaunchKernelGGL(countdown_step_turn_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     as_stream(stream), *env, *ep, *in, answers, answer_len, Lmax, err);
+  return launch_status();
+}
+
+RMI_API int rmi_countdown_reward(const rmi_countdown_t* env, const uint8_t* answers, const int32_t* answer_len,
+                                 int32_t Lmax, int32_t n, double* reward, uint8_t* flags, uint8_t* err,
+                                 rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !answers || !answer_len || !reward || Lmax <= 0 || n < 0 || !env->nums || !env->n_nums ||
+      !env->target || env->max_nums <= 0 || env->max_nums > 8)
+    return RMI_EINVAL;
+  if (n == 0) return RMI_OK;
+  hipLaunchKernelGGL(countdown_reward_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, as_stream(stream),
+                     *env, answers, answer_len, Lmax, n, reward, flags, err);
+  return launch_status();
+}

@@ -1,0 +1,256 @@
+// episode.hip — per-trajectory reductions after the turn loop (gfx950).
+//
+//  rmi_rollout_metrics   EnvStateManager.get_rollout_states   (es_manager.py:173-207)
+//  rmi_trajectory_scores ctx_manager scores/penalty tensors    (ctx_manager.py:64-65, :217, :282)
+//  rmi_group_normalize   ContextManager._normalize_score_tensor (ctx_manager.py:175-226)
+//  rmi_filter_groups     _filter_rollout                        (agent_trainer.py:461-500)
+//  rmi_row_sum           rm_scores.sum(-1)                      (agent_trainer.py:467)
+//
+// Segmented reductions: one 64-lane wave per segment / row, DPP-free __shfl_xor trees in
+// fp64 (fixed order => bit-reproducible run to run and independent of the launch grid).
+#include <math.h>
+
+#include "common.hpp"
+
+namespace rmi {
+namespace {
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  return x;
+}
+
+__global__ __launch_bounds__(kBlock) void rollout_metrics_kernel(rmi_episode_t ep, double* __restrict__ out) {
+  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (b >= ep.B) return;
+  const uint8_t f = ep.flags[b];
+  int eff = 0, val = 0, present = 0;
+  for (int t = 0; t < ep.T; ++t) {
+    const uint8_t inf = ep.turn_info[(int64_t)t * ep.B + b];
+    if (inf & RMI_INFO_PRESENT) {
+      present = 1;
+      eff += (inf & RMI_INFO_EFFECTIVE) ? 1 : 0;
+      val += (inf & RMI_INFO_VALID) ? 1 : 0;
+    }
+  }
+  const double nt = (double)ep.n_turns[b];
+  const bool success = (f & RMI_FLAG_TERMINATED) && !(f & RMI_FLAG_TRUNCATED);
+  out[4 * b + 0] = success ? 1.0 : 0.0;
+  out[4 * b + 1] = (double)ep.num_actions[b];
+  out[4 * b + 2] = present ? (double)eff / nt : __builtin_nan("");
+  out[4 * b + 3] = present ? (double)val / nt : __builtin_nan("");
+}
+
+__global__ __launch_bounds__(kBlock) void trajectory_scores_kernel(rmi_episode_t ep, float* __restrict__ score,
+                                                                   float* __restrict__ pen) {
+  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (b >= ep.B) return;
+  double s = 0.0;  // python sum() over the turn rewards, in turn order
+  for (int t = 0; t < ep.T; ++t) s += ep.turn_reward[(int64_t)t * ep.B + b];
+  score[b] = (float)s;
+  if (pen) pen[b] = (float)ep.penalty[b];
+}
+
+// one wave per segment; 4 segments per 256-thread workgroup
+__global__ __launch_bounds__(kBlock) void group_normalize_kernel(const float* __restrict__ score,
+                                                                 const float* __restrict__ pen,
+                                                                 const int32_t* __restrict__ seg, int G, int method,
+                                                                 float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (g >= G) return;
+  const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
+  if (n <= 0) return;
+  double s = 0.0;
+  for (int i = lo + lane; i < hi; i += 64) s += (double)(score[i] + (pen ? pen[i] : 0.0f));
+  s = wave_sum(s);
+  const float mean = (float)(s / (double)n);
+  float sd = 0.0f;
+  if (method == RMI_NORM_MEAN_STD || method == RMI_NORM_ASYM_CLIP) {
+    const double md = s / (double)n;
+    double q = 0.0;
+    for (int i = lo + lane; i < hi; i += 64) {
+      const double d = (double)(score[i] + (pen ? pen[i] : 0.0f)) - md;
+      q += d * d;
+    }
+    q = wave_sum(q);
+    sd = n > 1 ? (float)sqrt(q / (double)(n - 1)) : __builtin_nanf("");  // torch.std: unbiased
+  }
+  const bool use = sd > 1e-6f;  // std.abs().max() > 1e-6 (NaN compares false)
+  for (int i = lo + lane; i < hi; i += 64) {
+    const float x = score[i] + (pen ? pen[i] : 0.0f);
+    float y;
+    if (method == RMI_NORM_IDENTITY) y = x;
+    else if (method == RMI_NORM_MEAN) y = x - mean;
+    else {
+      y = use ? (x - mean) / (sd + 1e-6f) : 0.0f;
+      if (method == RMI_NORM_ASYM_CLIP) y = fminf(fmaxf(y, -1.0f), 3.0f);
+    }
+    out[i] = y;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void row_sum_kernel(const float* __restrict__ x, int64_t B, int64_t L,
+                                                         float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (r >= B) return;
+  double s = 0.0;
+  for (int64_t i = lane; i < L; i += 64) s += (double)x[r * L + i];
+  s = wave_sum(s);
+  if (lane == 0) out[r] = (float)s;
+}
+
+// ---- rollout filter: per-group stats, then a deterministic top-k by a bitonic sort in LDS
+constexpr int kFilterThreads = 1024;
+constexpr int kFilterMaxG = 8192;
+
+__device__ __forceinline__ uint32_t orderable(float f) {  // monotone float -> u32 (NaN = largest)
+  if (f != f) return 0xffffffffu;
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__global__ __launch_bounds__(kFilterThreads) void filter_kernel(const float* __restrict__ scores, int G, int gs,
+                                                                int k, int type, float* __restrict__ g_std,
+                                                                float* __restrict__ g_max, float* __restrict__ g_mean,
+                                                                uint8_t* __restrict__ keep,
+                                                                double* __restrict__ metrics) {
+  __shared__ uint64_t key[kFilterMaxG];
+  __shared__ double red[6][kFilterThreads / 64];
+  int P = 1;
+  while (P < G) P <<= 1;
+  double a_std = 0, a_max = 0, a_mean = 0;
+  for (int g = threadIdx.x; g < P; g += kFilterThreads) {
+    if (g < G) {
+      const float* x = scores + (int64_t)g * gs;
+      double s = 0.0;
+      float mx = -INFINITY;
+      for (int i = 0; i < gs; ++i) {
+        s += (double)x[i];
+        mx = fmaxf(mx, x[i]);
+      }
+      const double m = s / gs;
+      double q = 0.0;
+      for (int i = 0; i < gs; ++i) q += ((double)x[i] - m) * ((double)x[i] - m);
+      const float sd = gs > 1 ? (float)sqrt(q / (gs - 1)) : __builtin_nanf("");
+      g_std[g] = sd;
+      g_max[g] = mx;
+      g_mean[g] = (float)m;
+      a_std += sd;
+      a_max += mx;
+      a_mean += (float)m;
+      const float kf = type == 1 ? -sd : sd;
+      key[g] = ((uint64_t)orderable(kf) << 32) | (uint64_t)(0xffffffffu - (uint32_t)g);
+    } else {
+      key[g] = 0;  // padding sorts last
+    }
+  }
+  __syncthreads();
+  // bitonic sort, descending
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < P; i += kFilterThreads) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const uint64_t a = key[i], bb = key[j];
+          if ((a < bb) == desc) {
+            key[i] = bb;
+            key[j] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int g = threadIdx.x; g < G; g += kFilterThreads) keep[g] = 0;
+  __syncthreads();
+  double c_std = 0, c_max = 0, c_mean = 0;
+  for (int i = threadIdx.x; i < k; i += kFilterThreads) {
+    const int g = (int)(0xffffffffu - (uint32_t)(key[i] & 0xffffffffu));
+    keep[g] = 1;
+    c_std += g_std[g];
+    c_max += g_max[g];
+    c_mean += g_mean[g];
+  }
+  double v[6] = {a_std, a_max, a_mean, c_std, c_max, c_mean};
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double t = wave_sum(v[j]);
+    if (lane == 0) red[j][w] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double t = 0;
+    for (int i = 0; i < kFilterThreads / 64; ++i) t += red[threadIdx.x][i];
+    const double d = threadIdx.x < 3 ? (double)G : (double)k;
+    metrics[threadIdx.x] = (float)(t / d);  // torch f32 .mean()
+  }
+}
+
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_rollout_metrics(const rmi_episode_t* ep, double* out, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!ep || !out || ep->B < 0 || !ep->flags || !ep->turn_info || !ep->n_turns || !ep->num_actions)
+    return RMI_EINVAL;
+  if (ep->B == 0) return RMI_OK;
+  hipLaunchKernelGGL(rollout_metrics_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     as_stream(stream), *ep, out);
+  return launch_status();
+}
+
+RMI_API int rmi_trajectory_scores(const rmi_episode_t* ep, float* score, float* pen, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!ep || !score || ep->B < 0 || !ep->turn_reward || (pen && !ep->penalty)) return RMI_EINVAL;
+  if (ep->B == 0) return RMI_OK;
+  hipLaunchKernelGGL(trajectory_scores_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                     as_stream(stream), *ep, score, pen);
+  return launch_status();
+}
+
+RMI_API int rmi_group_normalize(const float* score, const float* pen, const int32_t* seg, int32_t G, int32_t B,
+                                int32_t method, float* out, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!score || !seg || !out || G < 0 || B < 0 || method < 0 || method > 3) return RMI_EINVAL;
+  if (B == 0 || G == 0) return RMI_OK;
+  // the reference normalises only when some group has more than one member (ctx_manager.py:220)
+  if (G >= B) method = RMI_NORM_IDENTITY;
+  const int per = kBlock / 64;
+  hipLaunchKernelGGL(group_normalize_kernel, dim3((G + per - 1) / per), dim3(kBlock), 0, as_stream(stream), score,
+                     pen, seg, G, method, out);
+  return launch_status();
+}
+
+RMI_API int rmi_row_sum(const float* x, int64_t B, int64_t L, float* out, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!x || !out || B < 0 || L < 0) return RMI_EINVAL;
+  if (B == 0) return RMI_OK;
+  const int per = kBlock / 64;
+  hipLaunchKernelGGL(row_sum_kernel, dim3((unsigned)((B + per - 1) / per)), dim3(kBlock), 0, as_stream(stream), x,
+                     B, L, out);
+  return launch_status();
+}
+
+RMI_API int rmi_filter_groups(const float* scores, int32_t G, int32_t gs, double ratio, int32_t type, float* g_std,
+                              float* g_max, float* g_mean, uint8_t* keep, double* metrics, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!scores || !g_std || !g_max || !g_mean || !keep || !metrics || G <= 0 || gs <= 0) return RMI_EINVAL;
+  if (G > kFilterMaxG) return RMI_EUNSUP;
+  if (type != 0 && type != 1) return RMI_EINVAL;
+  int k = (ratio == 1.0) ? G : (int)(ratio * (double)G);  // int(rollout_filter_ratio * num_groups)
+  if (k < 0) k = 0;
+  if (k > G) k = G;
+  hipLaunchKernelGGL(filter_kernel, dim3(1), dim3(kFilterThreads), 0, as_stream(stream), scores, G, gs, k, type,
+                     g_std, g_max, g_mean, keep, metrics);
+  return launch_status();
+}

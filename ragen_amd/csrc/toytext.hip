@@ -1,0 +1,180 @@
+// toytext.hip — FrozenLake and Bandit turns (gfx950), one thread per env.
+//
+// FrozenLake: replaces es_manager.py:105-171 driving frozen_lake/env.py:39-45 ->
+//   gymnasium FrozenLakeEnv.step + categorical_sample (App. A.2) with numpy PCG64
+//   draws (App. A.5).  Every step consumes exactly one Generator.random() draw, also on
+//   non-slippery maps and from terminal cells, as upstream does.
+// Bandit: replaces bandit/env.py:62-76 (one draw only when the hi arm is pulled).
+//
+// Per-env state is tiny (FrozenLake: desc row <= 64 B + s + 32 B of PCG64 state), so
+// the kernels are plain coalesced SoA loads: rng is [4,B] u64 planes, desc is [B,n] u8.
+#include "common.hpp"
+
+namespace rmi {
+namespace {
+
+struct FrozenLakeDev {
+  const uint8_t* desc;  // this env's row
+  int nrow, ncol, s;
+  bool slippery;
+  double cs0, cs1, cs2;
+  Pcg64 rng;
+
+  __device__ __forceinline__ int inc(int s0, int a) const {
+    int row = s0 / ncol, col = s0 - (s0 / ncol) * ncol;
+    if (a == 0) col = col - 1 < 0 ? 0 : col - 1;                       // LEFT
+    else if (a == 1) row = row + 1 > nrow - 1 ? nrow - 1 : row + 1;    // DOWN
+    else if (a == 2) col = col + 1 > ncol - 1 ? ncol - 1 : col + 1;    // RIGHT
+    else row = row - 1 < 0 ? 0 : row - 1;                              // UP
+    return row * ncol + col;
+  }
+  // action ids 1..4 -> gym 0..3 via FrozenLakeEnvConfig.action_map (frozen_lake/config.py:15)
+  __device__ __forceinline__ bool step(int a, double& reward, bool& done, bool& eff, bool& success) {
+    if (a < 1 || a > 4) return false;
+    const int ga = a - 1;
+    const int prev = s;
+    const double u = rng.next_double();  // categorical_sample draw
+    const uint8_t letter = desc[s];
+    if (letter == 'G' || letter == 'H') {  // P[s][a] = [(1.0, s, 0, True)]
+      reward = 0.0;
+      done = true;
+    } else {
+      int b = ga;
+      if (slippery) {  // argmax(cumsum(p) > u) over [(a-1)%4, a, (a+1)%4]
+        const int i = (cs0 > u) ? 0 : (cs1 > u) ? 1 : (cs2 > u) ? 2 : 0;
+        b = (ga + 3 + i) & 3;
+      }
+      s = inc(s, b);
+      const uint8_t nl = desc[s];
+      reward = (nl == 'G') ? 1.0 : 0.0;
+      done = (nl == 'G' || nl == 'H');
+    }
+    eff = prev != s;                   // frozen_lake/env.py:43
+    success = desc[s] == 'G';
+    return true;
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void frozenlake_step_turn_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
+                                                                      rmi_turn_t in, uint8_t* __restrict__ err_out) {
+  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int B = ep.B;
+  if (b >= B) return;
+  uint8_t flags = ep.flags[b];
+  const bool act = in.has_input ? (in.has_input[b] != 0) : !(flags & RMI_FLAG_DONE);
+  if (!act) return;
+  const int n = env.nrow * env.ncol;
+  FrozenLakeDev e;
+  e.desc = env.desc + b * n;
+  e.nrow = env.nrow;
+  e.ncol = env.ncol;
+  e.s = env.s[b];
+  e.slippery = env.is_slippery != 0;
+  e.cs0 = env.cs0;
+  e.cs1 = env.cs1;
+  e.cs2 = env.cs2;
+  e.rng = load_pcg(env.rng, B, b);
+  uint8_t err = 0;
+  if (e.s < 0 || e.s >= n) {
+    if (err_out) err_out[b] |= RMI_ERR_STATE;
+    return;
+  }
+  int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
+  double penalty = ep.penalty[b];
+  TurnOut o = run_turn(e, in.actions + b * (int64_t)in.K, in.n_actions[b], in.K, num_actions, flags, n_turns,
+                       penalty, in.max_actions_per_traj, in.format_penalty, err);
+  ep.num_actions[b] = num_actions;
+  ep.flags[b] = flags;
+  ep.n_turns[b] = n_turns;
+  ep.penalty[b] = penalty;
+  const int64_t tb = (int64_t)in.turn * B + b;
+  ep.turn_reward[tb] = o.acc;
+  ep.turn_info[tb] = o.info;
+  ep.turn_exec[tb] = o.exec;
+  if (o.stepped_any_state) {
+    env.s[b] = e.s;
+    store_pcg(env.rng, B, b, e.rng);
+  }
+  if (err_out && err) err_out[b] |= err;
+}
+
+struct BanditDev {
+  int start;
+  bool hi_first;
+  double lo_score, hi_lo, hi_hi, hi_prob;
+  Pcg64 rng;
+  __device__ __forceinline__ bool step(int a, double& reward, bool& done, bool& eff, bool& success) {
+    if (a != start && a != start + 1) return false;  // assert action in ACTION_LOOKUP
+    const bool is_hi = (a == start) == hi_first;
+    if (is_hi) reward = rng.next_double() < hi_prob ? hi_hi : hi_lo;  // _hi_arm_reward
+    else reward = lo_score;                                            // _lo_arm_reward
+    done = true;
+    eff = true;
+    success = is_hi;
+    return true;
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void bandit_step_turn_kernel(rmi_bandit_t env, rmi_episode_t ep, rmi_turn_t in,
+                                                                  uint8_t* __restrict__ err_out) {
+  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int B = ep.B;
+  if (b >= B) return;
+  uint8_t flags = ep.flags[b];
+  const bool act = in.has_input ? (in.has_input[b] != 0) : !(flags & RMI_FLAG_DONE);
+  if (!act) return;
+  BanditDev e;
+  e.start = env.action_space_start;
+  e.hi_first = env.hi_is_first[b] != 0;
+  e.lo_score = env.lo_arm_score;
+  e.hi_lo = env.hi_arm_loscore;
+  e.hi_hi = env.hi_arm_hiscore;
+  e.hi_prob = env.hi_arm_hiscore_prob;
+  e.rng = load_pcg(env.rng, B, b);
+  uint8_t err = 0;
+  int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
+  double penalty = ep.penalty[b];
+  TurnOut o = run_turn(e, in.actions + b * (int64_t)in.K, in.n_actions[b], in.K, num_actions, flags, n_turns,
+                       penalty, in.max_actions_per_traj, in.format_penalty, err);
+  ep.num_actions[b] = num_actions;
+  ep.flags[b] = flags;
+  ep.n_turns[b] = n_turns;
+  ep.penalty[b] = penalty;
+  const int64_t tb = (int64_t)in.turn * B + b;
+  ep.turn_reward[tb] = o.acc;
+  ep.turn_info[tb] = o.info;
+  ep.turn_exec[tb] = o.exec;
+  if (o.stepped_any_state) store_pcg(env.rng, B, b, e.rng);
+  if (err_out && err) err_out[b] |= err;
+}
+
+bool episode_ok(const rmi_episode_t* ep, const rmi_turn_t* in) {
+  return ep && in && ep->B >= 0 && in->K >= 0 && in->K <= kMaxK && in->turn >= 0 && in->turn < ep->T &&
+         ep->num_actions && ep->flags && ep->n_turns && ep->penalty && ep->turn_reward && ep->turn_info &&
+         ep->turn_exec && (in->K == 0 || in->actions) && in->n_actions;
+}
+
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                     uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !episode_ok(ep, in) || !env->desc || !env->s || !env->rng) return RMI_EINVAL;
+  if (env->nrow <= 0 || env->ncol <= 0 || env->nrow * env->ncol > 64) return RMI_EUNSUP;
+  if (ep->B == 0) return RMI_OK;
+  const unsigned grid = (unsigned)((ep->B + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(frozenlake_step_turn_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *env, *ep, *in,
+                     err);
+  return launch_status();
+}
+
+RMI_API int rmi_bandit_step_turn(const rmi_bandit_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                 uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !episode_ok(ep, in) || !env->hi_is_first || !env->rng) return RMI_EINVAL;
+  if (ep->B == 0) return RMI_OK;
+  const unsigned grid = (unsigned)((ep->B + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(bandit_step_turn_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *env, *ep, *in, err);
+  return launch_status();
+}

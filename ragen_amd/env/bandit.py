@@ -1,0 +1,90 @@
+"""Batched Bandit (replaces ragen/env/bandit/env.py:14-86)."""
+import numpy as np
+import torch
+
+from .. import _lib, ops
+from .base import BatchEnv
+from .configs import BanditEnvConfig
+from .frozen_lake import _pcg_state
+
+# bandit/env.py:6-12 (exact text, trailing spaces included: it is part of the observation)
+INIT_PROMPT = ("You are playing a bandit game. Goal: Maximize your total reward by choosing which arm to pull. \n"
+               "Game Rules: \n"
+               "1. There are 2 arms, named {name_a} and {name_b}\n"
+               "2. Each arm has its own reward distribution, related to their names. \n"
+               "3. Analyze the symbolic meaning of each arm's name to guess how their reward distribution might "
+               "behave.\n"
+               "4. Based on the symbolic meaning of their names, which arm do you think is more likely to give higher "
+               "rewards on average? Choose between {name_a} and {name_b}, and output like <answer> {name_a} "
+               "</answer> or <answer> {name_b} </answer>.\n")
+
+
+class BanditBatch(BatchEnv):
+    env_type = "bandit"
+
+    def __init__(self, config: BanditEnvConfig, n_envs, max_turns, max_actions_per_turn, device=None):
+        super().__init__(config or BanditEnvConfig(), n_envs, max_turns, max_actions_per_turn, device)
+        d = self.device
+        self.hi_is_first = torch.zeros(self.B, dtype=torch.uint8, device=d)
+        self.rng = torch.zeros(4, self.B, dtype=torch.int64, device=d)
+        self._hi_first_host = np.zeros(self.B, np.uint8)
+        self._last_obs = [None] * self.B
+
+    def struct(self):
+        c = self.config
+        return _lib.Bandit(int(c.action_space_start), float(c.lo_arm_score), float(c.hi_arm_loscore),
+                           float(c.hi_arm_hiscore), float(c.hi_arm_hiscore_prob), self.hi_is_first.data_ptr(),
+                           self.rng.data_ptr())
+
+    # BanditEnv.reset + _randomize_arms (bandit/env.py:25-39, :52-60): one draw < 0.5
+    @staticmethod
+    def reset_arrays(seeds):
+        seeds = np.asarray(seeds, np.int64)
+        uniq, inv = np.unique(seeds, return_inverse=True)
+        hi_first = np.zeros(len(uniq), np.uint8)
+        rng = np.zeros((4, len(uniq)), np.uint64)
+        for i, sd in enumerate(uniq):
+            st = _pcg_state(int(sd), 1)
+            hi_first[i] = 0 if st[4] < 0.5 else 1
+            rng[:, i] = st[:4]
+        return hi_first[inv], rng[:, inv]
+
+    def reset(self, seeds):
+        self.seeds = np.asarray(seeds, np.int64).copy()
+        hi_first, rng = self.reset_arrays(self.seeds)
+        self.load_state(hi_first, rng)
+
+    def load_state(self, hi_first, rng):
+        self._hi_first_host = np.asarray(hi_first, np.uint8).copy()
+        self.hi_is_first.copy_(torch.from_numpy(self._hi_first_host))
+        self.rng.copy_(torch.from_numpy(np.ascontiguousarray(rng).view(np.int64)))
+        self.ep.reset_()
+        self._last_obs = [None] * self.B
+        self._invalidate()
+
+    def action_lookup(self, i):
+        c, s = self.config, int(self.config.action_space_start)
+        if self._hi_first_host[i]:
+            return {s: c.hi_arm_name, s + 1: c.lo_arm_name}
+        return {s: c.lo_arm_name, s + 1: c.hi_arm_name}
+
+    def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
+        t = ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty)
+        ops.bandit_step_turn(self.struct(), self.ep, t, err)
+        self._invalidate()
+
+    def render(self, i: int) -> str:
+        # render_cache (bandit/env.py:49-50): the init prompt after reset,
+        # f"{arm_name}: {reward} points" after a step (bandit/env.py:66-67)
+        if self._last_obs[i] is None:
+            lk, s = self.action_lookup(i), int(self.config.action_space_start)
+            return INIT_PROMPT.format(name_a=lk[s], name_b=lk[s + 1])
+        if self._host is None:
+            self._host = self.ep.turn_reward.cpu().numpy()
+        turn, arm = self._last_obs[i]
+        return f"{arm}: {float(self._host[turn, i])} points"
+
+    def note_executed(self, turn, env_id, executed_ids):
+        """Called by the facade after a turn with the ids the kernel executed."""
+        if executed_ids:
+            self._last_obs[env_id] = (turn, self.action_lookup(env_id)[executed_ids[-1]])

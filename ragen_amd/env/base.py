@@ -1,0 +1,65 @@
+"""Batched env plugin API.
+
+The reference registers one Python object per env (ragen/env/base.py:5-73,
+ragen/env/__init__.py:15-31).  Here one *batch* object owns the device SoA state of every
+env of a tag; its ``step_turn`` runs one whole EnvStateManager turn for all of them in a
+single HIP launch.  Per-env views (``render``, ``action_lookup``) keep the reference's
+observable API for the Python facade (llm_agent/es_manager.py).
+"""
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+
+
+class BatchEnv:
+    env_type = "base"
+
+    def __init__(self, config, n_envs: int, max_turns: int, max_actions_per_turn: int, device=None):
+        self.config = config
+        self.B = int(n_envs)
+        self.T = int(max_turns)
+        self.K = int(max_actions_per_turn)
+        self.device = torch.device(device if device is not None else "cuda")
+        self.ep = ops.EpisodeState.empty(self.B, self.T, self.device)
+        self.seeds = np.zeros(self.B, np.int64)
+        self._host = None  # lazily synced host mirror for render()
+
+    # --- API ----------------------------------------------------------------------
+    def reset(self, seeds) -> None:
+        raise NotImplementedError
+
+    def step_turn(self, turn: int, actions: torch.Tensor, n_actions: torch.Tensor, has_input: Optional[torch.Tensor],
+                  max_actions_per_traj: int, format_penalty: float, err: Optional[torch.Tensor] = None,
+                  **kw) -> None:
+        raise NotImplementedError
+
+    def render(self, i: int) -> str:
+        raise NotImplementedError
+
+    def action_lookup(self, i: int) -> Optional[Dict[int, str]]:
+        return getattr(self.config, "action_lookup", None)
+
+    def map_actions(self, i: int, actions: List[str]) -> List[int]:
+        """Positional ids for es_manager._extract_map_valid_actions (es_manager.py:230-240):
+        case-insensitive exact match against action_lookup; 0 = unknown (dropped by the kernel)."""
+        lookup = self.action_lookup(i)
+        rev = {v.lower(): k for k, v in lookup.items()}
+        return [rev.get(a.lower(), 0) for a in actions]
+
+    def get_all_actions(self):
+        return list(self.action_lookup(0).keys())
+
+    def close(self):
+        self._host = None
+
+    # --- helpers ------------------------------------------------------------------
+    def _invalidate(self):
+        self._host = None
+
+    def expand_seeds(self, base_seed: int, group_size: int, first_group: int = 0) -> np.ndarray:
+        """es_manager.py:80-82: env i of the batch gets base + (global group index)."""
+        g = first_group + np.arange(self.B) // group_size
+        return (int(base_seed) + g).astype(np.int64)

@@ -1,0 +1,130 @@
+"""Batched FrozenLake (replaces ragen/env/frozen_lake/env.py + gymnasium FrozenLakeEnv, App. A.2)."""
+import numpy as np
+import torch
+
+from .. import _lib, ops
+from .base import BatchEnv
+from .configs import FrozenLakeEnvConfig
+
+_MASK64 = (1 << 64) - 1
+
+
+def _pcg_state(seed: int, draws: int) -> tuple:
+    """numpy Generator(PCG64(SeedSequence(seed))) advanced by `draws` random() calls
+    (gymnasium.utils.seeding.np_random) -> (state_hi, state_lo, inc_hi, inc_lo, last draw)."""
+    g = np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(seed))))
+    u = None
+    for _ in range(draws):
+        u = g.random()
+    st = g.bit_generator.state["state"]
+    return (st["state"] >> 64, st["state"] & _MASK64, st["inc"] >> 64, st["inc"] & _MASK64, u)
+
+
+def _is_valid(board, max_size):  # frozen_lake/utils.py:6-22
+    frontier, discovered = [], set()
+    sr, sc = np.where(np.array(board) == "S")
+    frontier.append((sr[0], sc[0]))
+    while frontier:
+        r, c = frontier.pop()
+        if (r, c) not in discovered:
+            discovered.add((r, c))
+            for dr, dc in [(1, 0), (0, 1), (-1, 0), (0, -1)]:
+                rn, cn = r + dr, c + dc
+                if 0 <= rn < max_size and 0 <= cn < max_size:
+                    if board[rn][cn] == "G":
+                        return True
+                    if board[rn][cn] != "H":
+                        frontier.append((rn, cn))
+    return False
+
+
+def generate_random_map(size=8, p=0.8, seed=None):
+    """frozen_lake/utils.py:25-47 (numpy Generator seeded like gymnasium seeding.np_random)."""
+    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+    while True:
+        board = rng.choice(["F", "H"], (size, size), p=[p, 1 - p])
+        start_r, start_c = rng.integers(size, size=2)
+        goal_r, goal_c = rng.integers(size, size=2)
+        if (start_r, start_c) != (goal_r, goal_c):
+            board[start_r][start_c], board[goal_r][goal_c] = "S", "G"
+            if _is_valid(board, size):
+                break
+    return ["".join(row) for row in board]
+
+
+def slippery_cumsum(success_rate: float):
+    """np.cumsum of the probabilities gymnasium lists for [(a-1)%4, a, (a+1)%4]."""
+    other = (1.0 - success_rate) / 2.0
+    return tuple(float(x) for x in np.cumsum([other, success_rate, other]))
+
+
+class FrozenLakeBatch(BatchEnv):
+    env_type = "frozen_lake"
+
+    def __init__(self, config: FrozenLakeEnvConfig, n_envs, max_turns, max_actions_per_turn, device=None):
+        super().__init__(config or FrozenLakeEnvConfig(), n_envs, max_turns, max_actions_per_turn, device)
+        n = int(self.config.size)
+        self.nrow = self.ncol = n
+        if n * n > 64:
+            raise NotImplementedError("FrozenLake kernel supports maps of at most 64 cells")
+        d = self.device
+        self.desc = torch.zeros(self.B, n * n, dtype=torch.uint8, device=d)
+        self.s = torch.zeros(self.B, dtype=torch.int32, device=d)
+        self.rng = torch.zeros(4, self.B, dtype=torch.int64, device=d)  # u64 bit patterns
+        self.cs = slippery_cumsum(self.config.success_rate)
+
+    def struct(self):
+        return _lib.FrozenLake(self.nrow, self.ncol, int(bool(self.config.is_slippery)), self.cs[0], self.cs[1],
+                               self.cs[2], self.desc.data_ptr(), self.s.data_ptr(), self.rng.data_ptr())
+
+    # FrozenLakeEnv.reset (frozen_lake/env.py:28-37): map from seed, env RNG reseeded with the
+    # same seed, one draw for the initial-state categorical_sample.
+    @staticmethod
+    def reset_arrays(seeds, size, p):
+        seeds = np.asarray(seeds, np.int64)
+        uniq, inv = np.unique(seeds, return_inverse=True)
+        desc = np.zeros((len(uniq), size * size), np.uint8)
+        s0 = np.zeros(len(uniq), np.int32)
+        rng = np.zeros((4, len(uniq)), np.uint64)
+        for i, sd in enumerate(uniq):
+            m = generate_random_map(size=size, p=p, seed=int(sd))
+            flat = "".join(m).encode()
+            desc[i] = np.frombuffer(flat, np.uint8)
+            s0[i] = flat.index(b"S")
+            st = _pcg_state(int(sd), 1)
+            rng[:, i] = st[:4]
+        return desc[inv], s0[inv], rng[:, inv]
+
+    def reset(self, seeds):
+        self.seeds = np.asarray(seeds, np.int64).copy()
+        desc, s0, rng = self.reset_arrays(self.seeds, self.nrow, float(self.config.p))
+        self.load_state(desc, s0, rng)
+
+    def load_state(self, desc, s0, rng):
+        self.desc.copy_(torch.from_numpy(np.ascontiguousarray(desc)))
+        self.s.copy_(torch.from_numpy(np.ascontiguousarray(s0, dtype=np.int32)))
+        self.rng.copy_(torch.from_numpy(np.ascontiguousarray(rng).view(np.int64)))
+        self.ep.reset_()
+        self._invalidate()
+
+    def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
+        t = ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty)
+        ops.frozenlake_step_turn(self.struct(), self.ep, t, err)
+        self._invalidate()
+
+    # FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61)
+    def render(self, i: int) -> str:
+        if self._host is None:
+            self._host = (self.desc.cpu().numpy(), self.s.cpu().numpy())
+        desc, s = self._host
+        n = self.ncol
+        d = desc[i].reshape(self.nrow, n)
+        pr, pc = int(s[i]) // n, int(s[i]) % n
+        ml = {ord("P"): 0, ord("F"): 1, ord("H"): 2, ord("G"): 3}
+        room = np.where(d == ord("S"), ord("F"), d)
+        room[pr, pc] = ord("P")
+        codes = np.vectorize(lambda x: ml[int(x)])(room)
+        letter = d[pr, pc]
+        codes[pr, pc] = 4 if letter == ord("H") else 5 if letter == ord("G") else 0
+        lk = self.config.grid_lookup
+        return "\n".join("".join(lk.get(int(c), "?") for c in row) for row in codes)

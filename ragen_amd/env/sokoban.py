@@ -1,0 +1,81 @@
+"""Batched Sokoban (replaces ragen/env/sokoban/env.py + gym_sokoban step, App. A.1)."""
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .. import _lib, ops
+from .base import BatchEnv
+from .configs import SokobanEnvConfig
+
+
+class SokobanBatch(BatchEnv):
+    env_type = "sokoban"
+
+    def __init__(self, config: SokobanEnvConfig, n_envs, max_turns, max_actions_per_turn, device=None):
+        super().__init__(config or SokobanEnvConfig(), n_envs, max_turns, max_actions_per_turn, device)
+        H, W = self.config.dim_room
+        self.H, self.W = int(H), int(W)
+        if self.H * self.W > 64:
+            raise NotImplementedError("Sokoban kernel supports rooms of at most 64 cells")
+        d = self.device
+        B, HW = self.B, self.H * self.W
+        self.room_fixed = torch.zeros(B, HW, dtype=torch.uint8, device=d)
+        self.room_state = torch.zeros(B, HW, dtype=torch.uint8, device=d)
+        self.player = torch.zeros(B, 2, dtype=torch.int8, device=d)
+        self.num_env_steps = torch.zeros(B, dtype=torch.int32, device=d)
+        self.boxes_on_target = torch.zeros(B, dtype=torch.int32, device=d)
+
+    def struct(self) -> _lib.Sokoban:
+        c = self.config
+        return _lib.Sokoban(self.H, self.W, int(c.num_boxes), int(c.max_steps), self.room_fixed.data_ptr(),
+                            self.room_state.data_ptr(), self.player.data_ptr(), self.num_env_steps.data_ptr(),
+                            self.boxes_on_target.data_ptr())
+
+    # SokobanEnv.reset (sokoban/env.py:28-42): generate_room under all_seed(seed); on
+    # RuntimeError/RuntimeWarning reseed with abs(hash(str(seed))) % 2**32 and retry.
+    @staticmethod
+    def generate(seeds, H, W, num_boxes, search_depth, n_threads=8):
+        seeds = np.asarray(seeds, np.int64)
+        uniq, inv = np.unique(seeds, return_inverse=True)
+        fixed, state, player, status = ops.generate_sokoban_rooms(uniq, H, W, num_boxes, search_depth, n_threads)
+        for i in np.nonzero(status)[0]:
+            s = int(uniq[i])
+            for _ in range(64):
+                s = abs(hash(str(s))) % (2 ** 32)
+                f, st, p, ok = ops.generate_sokoban_rooms([s], H, W, num_boxes, search_depth, 1)
+                if ok[0] == 0:
+                    fixed[i], state[i], player[i] = f[0], st[0], p[0]
+                    break
+            else:
+                raise RuntimeError(f"Sokoban generation failed repeatedly for seed {uniq[i]}")
+        return fixed[inv], state[inv], player[inv]
+
+    def reset(self, seeds):
+        self.seeds = np.asarray(seeds, np.int64).copy()
+        c = self.config
+        fixed, state, player = self.generate(self.seeds, self.H, self.W, int(c.num_boxes), int(c.search_depth))
+        self.load_state(fixed, state, player)
+
+    def load_state(self, fixed, state, player):
+        self.room_fixed.copy_(torch.from_numpy(np.ascontiguousarray(fixed)))
+        self.room_state.copy_(torch.from_numpy(np.ascontiguousarray(state)))
+        self.player.copy_(torch.from_numpy(np.ascontiguousarray(player)))
+        self.num_env_steps.zero_()
+        self.boxes_on_target.zero_()
+        self.ep.reset_()
+        self._invalidate()
+
+    def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
+        t = ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty)
+        ops.sokoban_step_turn(self.struct(), self.ep, t, err)
+        self._invalidate()
+
+    # SokobanEnv.render text mode (sokoban/env.py:53-57)
+    def render(self, i: int) -> str:
+        if self._host is None:
+            self._host = (self.room_state.cpu().numpy(), self.room_fixed.cpu().numpy())
+        st, fx = self._host
+        room = np.where((st[i] == 5) & (fx[i] == 2), 6, st[i]).reshape(self.H, self.W)
+        lk = self.config.grid_lookup
+        return "\n".join("".join(lk.get(int(c), "?") for c in row) for row in room.tolist())

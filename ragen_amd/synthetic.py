@@ -1,0 +1,74 @@
+"""Synthetic, fixed-seed workloads of SURVEY.md §8(d) (no LLM / dataset offline).
+
+Actions stand in for parsed LLM responses: per env per turn n ~ U{0..K} actions, each a
+known action id U{lo..hi} or, with probability p_unknown, an unknown name (id 0, dropped
+by the name->id map and charged the format penalty).  GAE inputs are token rows shaped
+like StarPO transcripts: a 150-token prompt (mask 0), then per executed turn a state block
+U[32,96] (mask 0) and a response block U[16,128] (mask 1); rows left-padded to the batch
+max length; V ~ N(0,1)*mask; reward = trajectory score at the last column.
+"""
+import numpy as np
+
+ACTION_SEED = 20250704
+ENV_SEED = 1000
+GROUP_SIZE = 16
+
+
+def turn_actions(rng: np.random.Generator, B: int, K: int, lo: int, hi: int, p_unknown: float = 0.1):
+    """-> (ids i8[B,K], n_actions u8[B])"""
+    n = rng.integers(0, K + 1, size=B).astype(np.uint8)
+    ids = rng.integers(lo, hi + 1, size=(B, K)).astype(np.int8)
+    unk = rng.random((B, K)) < p_unknown
+    ids[unk] = 0
+    ids[np.arange(K)[None, :] >= n[:, None]] = 0
+    return ids, n
+
+
+def rollout_actions(B: int, T: int, K: int, lo: int, hi: int, seed: int = ACTION_SEED, p_unknown: float = 0.1):
+    """Pre-generated actions for T turns: (ids i8[T,B,K], n_actions u8[T,B])."""
+    rng = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+    ids = np.zeros((T, B, K), np.int8)
+    n = np.zeros((T, B), np.uint8)
+    for t in range(T):
+        ids[t], n[t] = turn_actions(rng, B, K, lo, hi, p_unknown)
+    return ids, n
+
+
+def env_seeds(B: int, base: int = ENV_SEED, group_size: int = GROUP_SIZE, first_group: int = 0):
+    """env i -> base + i // group_size (es_manager.py:80-82)."""
+    return (base + first_group + np.arange(B) // group_size).astype(np.int64)
+
+
+def token_rows(n_turns, scores, seed: int = 7, prompt: int = 150, turn_scores=None, max_len=None):
+    """Token-level GAE inputs for trajectories with n_turns[b] executed turns.
+
+    -> r f32[B,L], v f32[B,L], mask u8[B,L] (left padded).  With ``turn_scores`` [B,T] the
+    reward of turn t sits on the last response token of that turn (bi-level / turn-score
+    variant); otherwise scores[b] sits at the last column (StarPO default)."""
+    rng = np.random.default_rng(seed)
+    B = len(n_turns)
+    lens, blocks = [], []
+    for b in range(B):
+        segs = [(prompt, 0)]
+        for _ in range(max(int(n_turns[b]), 1)):
+            segs.append((int(rng.integers(32, 97)), 0))
+            segs.append((int(rng.integers(16, 129)), 1))
+        blocks.append(segs)
+        lens.append(sum(s for s, _ in segs))
+    L = max(lens) if max_len is None else int(max_len)
+    r = np.zeros((B, L), np.float32)
+    mask = np.zeros((B, L), np.uint8)
+    for b in range(B):
+        pos = L - lens[b]
+        t = 0
+        for size, m in blocks[b]:
+            if m:
+                mask[b, pos:pos + size] = 1
+                if turn_scores is not None:
+                    r[b, pos + size - 1] = turn_scores[b, t]
+                t += 1
+            pos += size
+        if turn_scores is None:
+            r[b, L - 1] = scores[b]
+    v = (rng.standard_normal((B, L)).astype(np.float32) * mask).astype(np.float32)
+    return r, v, mask

@@ -1,0 +1,284 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the golden traces recorded from
+the reference and against the pinned CPU oracle at the BASELINE sizes.
+
+Bar: bit-exact for grid state, player, counters, flags, rewards (f64) and penalties;
+returns/advantages: returns bit-exact, whitened advantages within 1e-5 (f32 whitening
+uses a global reduction whose order torch does not define).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from ragen_amd import _lib, ops, synthetic
+from ragen_amd.env import BanditBatch, CountdownBatch, FrozenLakeBatch, SokobanBatch
+from ragen_amd.env.configs import BanditEnvConfig, CountdownEnvConfig, FrozenLakeEnvConfig, SokobanEnvConfig
+from trace_util import load, strings, trace_inputs
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev, dt=None):
+    x = torch.from_numpy(np.ascontiguousarray(a))
+    if dt is not None:
+        x = x.to(dt)
+    return x.to(dev)
+
+
+def _host_ep(ep):
+    return {k: getattr(ep, k).cpu().numpy() for k in ("num_actions", "flags", "n_turns", "penalty", "turn_reward",
+                                                      "turn_info", "turn_exec")}
+
+
+def _check_turn(ep, d, t):
+    h = _host_ep(ep)
+    np.testing.assert_array_equal(h["turn_reward"][t], d["turn_reward"][t])
+    np.testing.assert_array_equal(h["turn_exec"][t], d["n_exec"][t])
+    np.testing.assert_array_equal(h["turn_info"][t], d["info"][t])
+    np.testing.assert_array_equal(h["penalty"], d["penalty"][t])
+    np.testing.assert_array_equal(h["num_actions"], d["num_actions"][t])
+    np.testing.assert_array_equal((h["flags"] & 1) > 0, d["term"][t] > 0)
+    np.testing.assert_array_equal((h["flags"] & 2) > 0, d["trunc"][t] > 0)
+    active = (d["act_in"][t] > 0) & ((h["flags"] & 4) == 0)
+    np.testing.assert_array_equal(active, d["active_after"][t] > 0)
+
+
+def _check_final(ep, d):
+    m = ops.rollout_metrics(ep).cpu().numpy()
+    for j, k in enumerate(["success", "num_actions", "action_is_effective", "action_is_valid"]):
+        np.testing.assert_array_equal(m[:, j], d["metric_" + k])
+    s, p = ops.trajectory_scores(ep)
+    np.testing.assert_array_equal(s.cpu().numpy(), d["score_f32"])
+    np.testing.assert_array_equal(p.cpu().numpy(), d["penalty_f32"])
+
+
+@pytest.mark.parametrize("name", ["sokoban_es", "sokoban8_es"])
+def test_sokoban_golden_trace(device, name):
+    d, ids = trace_inputs(name)
+    B, T, K = int(d["B"]), int(d["T"]), int(d["K"])
+    H = int(np.sqrt(d["init_room_state"].shape[1]))
+    cfg = SokobanEnvConfig(dim_x=H, dim_y=H, num_boxes=1 if H == 6 else 2, max_steps=100)
+    env = SokobanBatch(cfg, B, T, K, device)
+    env.load_state(d["init_room_fixed"].astype(np.uint8), d["init_room_state"].astype(np.uint8),
+                   d["init_player"].astype(np.int8))
+    err = torch.zeros(B, dtype=torch.uint8, device=device)
+    for t in range(T):
+        env.step_turn(t, _t(ids[t], device), _t(d["n_act"][t].astype(np.uint8), device),
+                      _t(d["act_in"][t].astype(np.uint8), device), 10, -0.1, err)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(env.room_state.cpu().numpy(), d["turn_room_state"][t].astype(np.uint8))
+        np.testing.assert_array_equal(env.player.cpu().numpy(), d["turn_player"][t].astype(np.int8))
+        np.testing.assert_array_equal(env.num_env_steps.cpu().numpy(), d["turn_num_env_steps"][t])
+        np.testing.assert_array_equal(env.boxes_on_target.cpu().numpy(), d["turn_boxes_on_target"][t])
+        _check_turn(env.ep, d, t)
+    assert not err.any()
+    _check_final(env.ep, d)
+    final = strings()[name]["final_obs"]
+    assert [env.render(i) for i in range(B)] == final
+
+
+def test_frozenlake_golden_trace(device):
+    d, ids = trace_inputs("frozenlake_es")
+    B, T, K = int(d["B"]), int(d["T"]), int(d["K"])
+    env = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
+    env.reset(synthetic.env_seeds(B, int(d["seed"]), int(d["group_size"])))
+    np.testing.assert_array_equal(env.desc.cpu().numpy(), d["init_desc"])
+    np.testing.assert_array_equal(env.s.cpu().numpy(), d["init_s"])
+    np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64).T, d["init_rng_state"])
+    for t in range(T):
+        env.step_turn(t, _t(ids[t], device), _t(d["n_act"][t].astype(np.uint8), device),
+                      _t(d["act_in"][t].astype(np.uint8), device), 10, -0.1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(env.s.cpu().numpy(), d["turn_s"][t])
+        np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64).T, d["turn_rng_state"][t])
+        _check_turn(env.ep, d, t)
+    _check_final(env.ep, d)
+    assert [env.render(i) for i in range(B)] == strings()["frozenlake_es"]["final_obs"]
+
+
+def test_bandit_golden_trace(device):
+    d, ids = trace_inputs("bandit_es")
+    B, T, K = int(d["B"]), int(d["T"]), int(d["K"])
+    env = BanditBatch(BanditEnvConfig(lo_arm_name="Phoenix", hi_arm_name="Dragon"), B, T, K, device)
+    env.reset(synthetic.env_seeds(B, int(d["seed"]), int(d["group_size"])))
+    np.testing.assert_array_equal(env.hi_is_first.cpu().numpy(), d["init_hi_is_first"])
+    for t in range(T):
+        env.step_turn(t, _t(ids[t], device), _t(d["n_act"][t].astype(np.uint8), device),
+                      _t(d["act_in"][t].astype(np.uint8), device), 1, -0.1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64).T, d["turn_rng_state"][t])
+        _check_turn(env.ep, d, t)
+    _check_final(env.ep, d)
+
+
+def test_countdown_golden_trace(device):
+    d = load("countdown_es")
+    S = strings()
+    B, T, K = int(d["B"]), int(d["T"]), int(d["K"])
+    env = CountdownBatch(CountdownEnvConfig(data=S["countdown_data"]), B, T, K, device)
+    env.reset(synthetic.env_seeds(B, int(d["seed"]), int(d["group_size"])))
+    np.testing.assert_array_equal(env.target.cpu().numpy(), d["init_target"])
+    np.testing.assert_array_equal(env.nums.cpu().numpy(), d["init_nums"])
+    answers = S["countdown_es"]["answers"]
+    for t in range(T):
+        lists = [[a] if a is not None else [] for a in answers[t]]
+        buf, lens = env.encode_answers(lists)
+        n = np.array([len(x) for x in lists], np.uint8)
+        env.step_turn(t, torch.zeros(B, K, dtype=torch.int8, device=device), _t(n, device),
+                      _t(d["act_in"][t].astype(np.uint8), device), 1, -0.1, answers=_t(buf, device),
+                      answer_len=_t(lens, device))
+        torch.cuda.synchronize()
+        _check_turn(env.ep, d, t)
+    _check_final(env.ep, d)
+
+
+def test_countdown_reward_kat(device):
+    k = strings()["countdown_kat"]
+    exprs = [c["expr"] for c in k["cases"]]
+    n = len(exprs)
+    env = CountdownBatch(CountdownEnvConfig(data=[{"nums": k["nums"], "target": k["target"]}]), n, 1, 1, device)
+    env.reset(np.zeros(n, np.int64))
+    buf, lens = env.encode_answers([[e] if e else [""] for e in exprs])
+    r, fl, err = ops.countdown_reward(env.struct(), _t(buf[:, 0], device), _t(lens[:, 0].copy(), device))
+    r = r.cpu().numpy()
+    for i, c in enumerate(k["cases"]):
+        assert r[i] == c["reward"], (c, r[i], int(err[i]))
+
+
+# ------------------------------------------------------------- BASELINE-size parity vs oracle
+def test_sokoban_full_size_vs_oracle(device):
+    """SK config: 8192 envs x 5 turns, K=5, cap 10 — kernel == oracle bit for bit each turn."""
+    B, T, K = 8192, 5, 5
+    cfg = SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100)
+    env = SokobanBatch(cfg, B, T, K, device)
+    env.reset(synthetic.env_seeds(B))
+    fixed = env.room_fixed.cpu().numpy()
+    state = env.room_state.cpu().numpy()
+    player = env.player.cpu().numpy()
+    nes = np.zeros(B, np.int32)
+    bot = np.zeros(B, np.int32)
+    oep = oracle.Episode(B, T)
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4)
+    total_steps = 0
+    for t in range(T):
+        env.step_turn(t, _t(ids[t], device), _t(n[t], device), None, 10, -0.1)
+        oracle.sokoban_turn(6, 6, 1, 100, fixed, state, player, nes, bot, oep, t, ids[t], n[t], None, 10, -0.1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(env.room_state.cpu().numpy(), state)
+        np.testing.assert_array_equal(env.player.cpu().numpy(), player)
+        h = _host_ep(env.ep)
+        for k in ("num_actions", "flags", "n_turns", "penalty", "turn_reward", "turn_info", "turn_exec"):
+            np.testing.assert_array_equal(h[k], getattr(oep, k), err_msg=k)
+        total_steps += int(oep.turn_exec[t].sum())
+    assert total_steps > 50000
+    np.testing.assert_array_equal(ops.rollout_metrics(env.ep).cpu().numpy(), oracle.rollout_metrics(oep))
+
+
+def test_frozenlake_full_size_vs_oracle(device):
+    B, T, K = 4096, 8, 5
+    env = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
+    env.reset(synthetic.env_seeds(B))
+    desc = env.desc.cpu().numpy()
+    s = env.s.cpu().numpy()
+    rng = env.rng.cpu().numpy().view(np.uint64).copy()
+    oep = oracle.Episode(B, T)
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=5)
+    for t in range(T):
+        env.step_turn(t, _t(ids[t], device), _t(n[t], device), None, 10, -0.1)
+        oracle.frozenlake_turn(4, 4, True, env.cs, desc, s, rng, oep, t, ids[t], n[t], None, 10, -0.1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(env.s.cpu().numpy(), s)
+        np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64), rng)
+        h = _host_ep(env.ep)
+        for k in ("num_actions", "flags", "penalty", "turn_reward", "turn_info", "turn_exec"):
+            np.testing.assert_array_equal(h[k], getattr(oep, k), err_msg=k)
+
+
+def test_gae_full_size(device):
+    """B=8192 rows ~1k tokens: legacy/masked GAE returns bit-exact vs oracle, whitened adv <= 1e-5."""
+    B = 8192
+    rng = np.random.default_rng(0)
+    n_turns = rng.integers(1, 6, size=B)
+    scores = rng.choice([-0.5, 0.9, 10.4, -1.2], size=B).astype(np.float32)
+    r, v, m = synthetic.token_rows(n_turns, scores, seed=1)
+    tr, tv, tm = _t(r, device), _t(v, device), _t(m, device)
+    for variant, (g, lam) in (("legacy", (1.0, 1.0)), ("legacy", (1.0, 0.95)), ("masked", (0.99, 0.95))):
+        stats = torch.zeros(B, 3, dtype=torch.float64, device=device)
+        adv, ret = ops.gae(tr, tv, tm, g, lam, variant, row_stats=stats)
+        oadv, oret = oracle.gae(r, v, m, g, lam, variant)
+        np.testing.assert_array_equal(ret.cpu().numpy(), oret)
+        np.testing.assert_array_equal(adv.cpu().numpy(), oadv)
+        ops.masked_whiten_(adv, tm, stats)
+        np.testing.assert_allclose(adv.cpu().numpy(), oracle.masked_whiten(oadv, m), rtol=0, atol=1e-5)
+
+
+def test_gae_golden(device):
+    d = load("gae")
+    m = d["mask"]
+    tm = _t(m, device)
+    for gl in ("g1.0_l1.0", "g1.0_l0.95", "g0.99_l0.95"):
+        g, lam = (float(x[1:]) for x in gl.split("_"))
+        for rn in ("last", "turn"):
+            r = _t(d["rew"] if rn == "last" else d["rew_turn"], device)
+            v = _t(d["values"], device)
+            for var, key in (("legacy", "gae"), ("masked", "gaem")):
+                adv, ret = ops.gae(r, v, tm, g, lam, var)
+                np.testing.assert_array_equal(ret.cpu().numpy(), d[f"{key}_{rn}_{gl}_ret"])
+                ops.masked_whiten_(adv, tm)
+                np.testing.assert_allclose(adv.cpu().numpy(), d[f"{key}_{rn}_{gl}_adv"], rtol=0, atol=1e-5)
+            adv, ret = ops.bilevel_gae(r, v, tm, g, lam, 0.95)
+            np.testing.assert_array_equal(ret.cpu().numpy(), d[f"bilevel_{rn}_{gl}_ret"])
+            ops.masked_whiten_(adv, tm)
+            np.testing.assert_allclose(adv.cpu().numpy(), d[f"bilevel_{rn}_{gl}_adv"], rtol=0, atol=1e-5)
+    with pytest.raises(IndexError):
+        ops.bilevel_gae(_t(np.array([[0, 1, 0, 0]], np.float32), device), torch.zeros(1, 4, device=device),
+                        torch.ones(1, 4, dtype=torch.uint8, device=device), 1.0, 1.0, 0.95)
+
+
+def test_grpo_golden(device):
+    d = load("gae")
+    B = d["mask"].shape[0]
+    r, tm = _t(d["rew_turn"], device), _t(d["mask"], device)
+    adv, ret = ops.grpo_outcome(r, tm, _t(np.arange(B + 1, dtype=np.int32), device))
+    np.testing.assert_allclose(adv.cpu().numpy(), d["ca_grpo_0_adv"], rtol=1e-6, atol=1e-6)
+    adv, ret = ops.grpo_outcome(r, tm, _t(np.arange(0, B + 1, 4, dtype=np.int32), device))
+    np.testing.assert_allclose(adv.cpu().numpy(), d["grpo_g4_adv"], rtol=1e-5, atol=1e-5)
+
+
+def test_normalize_golden(device):
+    d = load("normalize")
+    B = len(d["scores"])
+    sc, pen = _t(d["scores"], device), _t(d["penalty"].astype(np.float32), device)
+    segs = {"state": np.arange(0, B + 1, 16), "inductive": np.array([0, 48, 96]), "batch": np.array([0, B])}
+    for grouping, seg in segs.items():
+        for method in ("mean_std", "mean", "asym_clip", "identity"):
+            out = ops.group_normalize(sc, pen, _t(seg.astype(np.int32), device), method)
+            np.testing.assert_allclose(out.cpu().numpy(), d[f"norm_{grouping}_{method}"], rtol=0, atol=1e-5)
+
+
+def test_filter_vs_oracle(device):
+    d = load("filter")
+    for key in ("r0.25_std", "r0.25_std_rev", "r1.0_std", "r0.5_std"):
+        ratio = float(key.split("_")[0][1:])
+        ftype = key.split("_", 1)[1]
+        rows = ops.row_sum(_t(d[key + "_scores"], device))
+        keep, met, (sd, mx, mn) = ops.filter_groups(rows, 64, 16, ratio, ftype)
+        okeep, omet, (osd, omx, omn) = oracle.filter_groups(rows.cpu().numpy(), 64, 16, ratio, ftype)
+        np.testing.assert_array_equal(keep.cpu().numpy(), okeep)
+        np.testing.assert_allclose(met.cpu().numpy(), omet, rtol=1e-6)
+        np.testing.assert_array_equal(sd.cpu().numpy(), osd)
+    # large G with many ties: deterministic selection identical to the oracle's documented order
+    G, gs = 4096, 16
+    rng = np.random.default_rng(2)
+    sc = np.repeat(rng.choice([0.0, 1.0, -0.5], size=G), gs).astype(np.float32)
+    sc[rng.random(G * gs) < 0.05] = 10.0
+    keep, met, _ = ops.filter_groups(_t(sc, device), G, gs, 0.25, "std")
+    okeep, omet, _ = oracle.filter_groups(sc, G, gs, 0.25, "std")
+    np.testing.assert_array_equal(keep.cpu().numpy(), okeep)
+
+
+def test_whiten_errors_and_empty(device):
+    x = torch.zeros(2, 3, device=device)
+    ops.masked_whiten_(x, torch.zeros(2, 3, dtype=torch.uint8, device=device))  # status recorded, no crash
+    e = ops.EpisodeState.empty(0, 1, device)
+    assert ops.rollout_metrics(e).shape == (0, 4)
