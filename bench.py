@@ -54,7 +54,6 @@ class Rollout:
         first_group = rank * (B // GROUP)
         self.env.reset(synthetic.env_seeds(B, synthetic.ENV_SEED, GROUP, first_group))
         e = self.env
-        self.snap = [x.clone() for x in (e.room_state, e.player, e.num_env_steps, e.boxes_on_target)]
         ids, n = synthetic.rollout_actions(B, T_TURNS, K_ACTIONS, 1, 4, seed=synthetic.ACTION_SEED + rank)
         self.ids = torch.from_numpy(ids).to(device)
         self.n = torch.from_numpy(n).to(device)
@@ -64,15 +63,9 @@ class Rollout:
         self.turns = [ops.turn_struct(t, self.ids[t], self.n[t], None, MAX_ACTIONS, -0.1) for t in range(T_TURNS)]
         self.st = e.struct()
 
-    def restore(self):
-        e = self.env
-        for dst, src in zip((e.room_state, e.player, e.num_env_steps, e.boxes_on_target), self.snap):
-            dst.copy_(src, non_blocking=True)
-        e.ep.reset_()
-
     def step(self, events=None):
         """One rollout phase.  events: optional list collecting (start, end) per turn kernel."""
-        self.restore()
+        self.env.restore()
         for t in range(T_TURNS):
             if events is not None:
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -81,10 +74,7 @@ class Rollout:
             if events is not None:
                 b.record()
                 events.append((a, b))
-        m = ops.rollout_metrics(self.env.ep)
-        self.metrics.copy_(m)
-        score, pen = ops.trajectory_scores(self.env.ep)
-        ops.group_normalize(score, pen, self.seg, "identity", out=self.norm)
+        ops.rollout_finalize(self.env.ep, self.seg, "identity", self.norm, metrics=self.metrics)
 
 
 def cpu_baseline(R, seconds_budget=20.0):
@@ -94,8 +84,8 @@ def cpu_baseline(R, seconds_budget=20.0):
     from oracle import port
     n_envs = 2048
     fixed = R.env.room_fixed[:n_envs].cpu().numpy()
-    state0 = R.snap[0][:n_envs].cpu().numpy()
-    player0 = R.snap[1][:n_envs].cpu().numpy()
+    state0 = R.env.init_state[:n_envs].cpu().numpy()
+    player0 = R.env.init_player[:n_envs].cpu().numpy()
     ids = R.ids[:, :n_envs].cpu().numpy()
     n = R.n[:, :n_envs].cpu().numpy()
     steps = 0

@@ -109,6 +109,12 @@ typedef struct {
 int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                           uint8_t* err, rmi_stream_t stream);
 
+/* Device part of SokobanEnv.reset (sokoban/env.py:37-38) + EnvStatus(seed) (es_manager.py:95):
+ * room_state/player := init_state/init_player (the generated rooms), num_env_steps =
+ * boxes_on_target = 0, and the whole episode record zeroed — one launch.  B*H*W % 4 == 0. */
+int rmi_sokoban_reset(const rmi_sokoban_t* env, const rmi_episode_t* ep, const uint8_t* init_state,
+                      const int8_t* init_player, rmi_stream_t stream);
+
 /* Replaces: SokobanEnv.reset (sokoban/env.py:28-42) -> generate_room (sokoban/utils.py:221-278)
  * under all_seed (ragen/utils.py:7-18).  [host] CPU function: exact CPython-random /
  * numpy-legacy MT19937 semantics.  Writes one room per seed.  Returns per seed
@@ -178,6 +184,11 @@ int rmi_rollout_metrics(const rmi_episode_t* ep, double* out, rmi_stream_t strea
 /* Trajectory scores (ctx_manager.py:282 + get_masks_and_scores:64-65 + :217):
  * score[b] = f32(sum over turns of turn_reward), pen[b] = f32(penalty[b]).              */
 int rmi_trajectory_scores(const rmi_episode_t* ep, float* score, float* pen, rmi_stream_t stream);
+
+/* Fused end of rollout: rmi_rollout_metrics + rmi_trajectory_scores + rmi_group_normalize in
+ * one launch (any output pointer may be NULL except norm when G > 0).                    */
+int rmi_rollout_finalize(const rmi_episode_t* ep, const int32_t* seg, int32_t G, int32_t method, double* metrics,
+                         float* score, float* pen, float* norm, rmi_stream_t stream);
 
 /* ------------------------------------------------------- A10 reward normalisation
  * Replaces: ContextManager._normalize_score_tensor (ctx_manager.py:175-226).

@@ -71,8 +71,17 @@ struct TurnOut {
   bool stepped_any_state;  // the env's state may have changed
 };
 
+// Actions of one env packed into a u64 (K <= 8 bytes), loaded once per turn.
+__device__ __forceinline__ uint64_t load_actions(const int8_t* acts, int K) {
+  uint64_t packed = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k)
+    if (k < K) packed |= (uint64_t)(uint8_t)acts[k] << (8 * k);
+  return packed;
+}
+
 template <class Env>
-__device__ __forceinline__ TurnOut run_turn(Env& e, const int8_t* acts, int n_act, int K, int32_t& num_actions,
+__device__ __forceinline__ TurnOut run_turn(Env& e, uint64_t packed_acts, int n_act, int K, int32_t& num_actions,
                                             uint8_t& flags, int32_t& n_turns, double& penalty, int max_actions,
                                             double format_penalty, uint8_t& err) {
   TurnOut o;
@@ -83,34 +92,33 @@ __device__ __forceinline__ TurnOut run_turn(Env& e, const int8_t* acts, int n_ac
   flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (:168)
   const int left = max_actions - num_actions;
   int nv = 0;
-  bool stop = false, succ_last = false;
+  bool stop = false, succ_last = false, turn_done = false;
   if (n_act > K) n_act = K;
-#pragma unroll
-  for (int k = 0; k < kMaxK; ++k) {
-    if (k < n_act) {
-      const int a = acts[k];
-      if (a != 0) {
-        if (!stop && nv < left) {
-          double r;
-          bool done, eff, succ;
-          if (!e.step(a, r, done, eff, succ)) {
-            err |= RMI_ERR_ACTION;
-            stop = true;  // the reference raises here; leave the rest of the turn untouched
-          } else {
-            o.acc += r;
-            o.exec++;
-            o.stepped_any_state = true;
-            o.info = (uint8_t)(RMI_INFO_PRESENT | (eff ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID |
-                               (succ ? RMI_INFO_SUCCESS : 0));
-            succ_last = succ;
-            if (done) stop = true;
-          }
+#pragma unroll 1
+  for (int k = 0; k < n_act; ++k) {
+    const int a = (int)(int8_t)(uint8_t)(packed_acts >> (8 * k));
+    if (a == 0) continue;  // name not in action_lookup: dropped (es_manager.py:239)
+    if (!stop && nv < left) {
+      double r;
+      bool done, eff, succ;
+      if (!e.step(a, r, done, eff, succ)) {
+        err |= RMI_ERR_ACTION;
+        stop = true;  // the reference raises here; the rest of the turn is not executed
+      } else {
+        o.acc += r;
+        o.exec++;
+        o.stepped_any_state = true;
+        o.info = (uint8_t)(RMI_INFO_PRESENT | (eff ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID |
+                           (succ ? RMI_INFO_SUCCESS : 0));
+        succ_last = succ;
+        if (done) {
+          stop = true;
+          turn_done = true;
         }
-        nv++;
       }
     }
+    nv++;
   }
-  const bool turn_done = (o.info & RMI_INFO_PRESENT) && stop && !(err & RMI_ERR_ACTION);
   if (nv != n_act || nv == 0) penalty += format_penalty;
   num_actions += o.exec;
   n_turns += 1;
@@ -121,6 +129,17 @@ __device__ __forceinline__ TurnOut run_turn(Env& e, const int8_t* acts, int n_ac
     flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
   }
   return o;
+}
+
+// Validation shared by every *_step_turn entry point (an empty batch is always fine).
+inline int check_turn_args(const rmi_episode_t* ep, const rmi_turn_t* in) {
+  if (!ep || !in || ep->B < 0 || ep->T <= 0) return RMI_EINVAL;
+  if (in->K < 0 || in->K > kMaxK || in->turn < 0 || in->turn >= ep->T) return RMI_EINVAL;
+  if (ep->B == 0) return 1;
+  if (!ep->num_actions || !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info ||
+      !ep->turn_exec || (in->K > 0 && !in->actions) || !in->n_actions)
+    return RMI_EINVAL;
+  return RMI_OK;
 }
 
 }  // namespace rmi

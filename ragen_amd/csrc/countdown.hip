@@ -615,10 +615,8 @@ __global__ __launch_bounds__(kBlock) void countdown_step_turn_kernel(rmi_countdo
   e.format_score = env.format_score;
   e.err = 0;
   // every parsed answer string is a valid action (no action_lookup: es_manager.py:234-235)
-  int8_t acts[kMaxK];
+  const uint64_t acts = 0x0807060504030201ull;  // slot k holds answer k+1
   const int n_act = in.n_actions[b];
-#pragma unroll
-  for (int k = 0; k < kMaxK; ++k) acts[k] = (int8_t)(k + 1);
   uint8_t err = 0;
   int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
   double penalty = ep.penalty[b];
@@ -662,13 +660,12 @@ RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episod
                                     const uint8_t* answers, const int32_t* answer_len, int32_t Lmax, uint8_t* err,
                                     rmi_stream_t stream) {
   using namespace rmi;
-  if (!env || !ep || !in || !answers || !answer_len || Lmax <= 0 || !env->nums || !env->n_nums || !env->target ||
-      env->max_nums <= 0 || env->max_nums > 8)
-    return RMI_EINVAL;
-  if (in->K < 0 || in->K > kMaxK || in->turn < 0 || in->turn >= ep->T || !in->n_actions || !ep->num_actions ||
+  if (!env || Lmax <= 0 || env->max_nums <= 0 || env->max_nums > 8) return RMI_EINVAL;
+  if (!ep || !in || in->K < 0 || in->K > kMaxK || ep->B < 0 || in->turn < 0 || in->turn >= ep->T) return RMI_EINVAL;
+  if (ep->B == 0) return RMI_OK;
+  if (!answers || !answer_len || !env->nums || !env->n_nums || !env->target || !in->n_actions || !ep->num_actions ||
       !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
     return RMI_EINVAL;
-  if (ep->B == 0) return RMI_OK;
   hipLaunchKernelGGL(countdown_step_turn_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      as_stream(stream), *env, *ep, *in, answers, answer_len, Lmax, err);
   return launch_status();
@@ -678,10 +675,9 @@ RMI_API int rmi_countdown_reward(const rmi_countdown_t* env, const uint8_t* answ
                                  int32_t Lmax, int32_t n, double* reward, uint8_t* flags, uint8_t* err,
                                  rmi_stream_t stream) {
   using namespace rmi;
-  if (!env || !answers || !answer_len || !reward || Lmax <= 0 || n < 0 || !env->nums || !env->n_nums ||
-      !env->target || env->max_nums <= 0 || env->max_nums > 8)
-    return RMI_EINVAL;
+  if (!env || Lmax <= 0 || n < 0 || env->max_nums <= 0 || env->max_nums > 8) return RMI_EINVAL;
   if (n == 0) return RMI_OK;
+  if (!answers || !answer_len || !reward || !env->nums || !env->n_nums || !env->target) return RMI_EINVAL;
   hipLaunchKernelGGL(countdown_reward_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, as_stream(stream),
                      *env, answers, answer_len, Lmax, n, reward, flags, err);
   return launch_status();

@@ -196,14 +196,82 @@ __global__ __launch_bounds__(kFilterThreads) void filter_kernel(const float* __r
   }
 }
 
+// Fused end-of-rollout pass: per env metrics + trajectory score + penalty, then the group
+// normalisation, one wave per segment (get_rollout_states + get_masks_and_scores score
+// placement + _normalize_score_tensor in one launch).
+__global__ __launch_bounds__(kBlock) void finalize_kernel(rmi_episode_t ep, const int32_t* __restrict__ seg, int G,
+                                                          int method, double* __restrict__ metrics,
+                                                          float* __restrict__ score_out, float* __restrict__ pen_out,
+                                                          float* __restrict__ norm_out) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (g >= G) return;
+  const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
+  const int64_t B = ep.B;
+  double s = 0.0;
+  for (int i = lo + lane; i < hi; i += 64) {
+    double sc = 0.0;
+    int eff = 0, val = 0, present = 0;
+    for (int t = 0; t < ep.T; ++t) {
+      sc += ep.turn_reward[(int64_t)t * B + i];
+      const uint8_t inf = ep.turn_info[(int64_t)t * B + i];
+      present |= inf & RMI_INFO_PRESENT;
+      eff += (inf >> 1) & 1;
+      val += (inf >> 2) & 1;
+    }
+    const float scf = (float)sc, pf = (float)ep.penalty[i];
+    if (score_out) score_out[i] = scf;
+    if (pen_out) pen_out[i] = pf;
+    if (metrics) {
+      const uint8_t f = ep.flags[i];
+      const double nt = (double)ep.n_turns[i];
+      metrics[4 * i + 0] = ((f & RMI_FLAG_TERMINATED) && !(f & RMI_FLAG_TRUNCATED)) ? 1.0 : 0.0;
+      metrics[4 * i + 1] = (double)ep.num_actions[i];
+      metrics[4 * i + 2] = present ? (double)eff / nt : __builtin_nan("");
+      metrics[4 * i + 3] = present ? (double)val / nt : __builtin_nan("");
+    }
+    s += (double)(scf + pf);
+  }
+  if (!norm_out || n <= 0) return;
+  s = wave_sum(s);
+  const double md = s / (double)n;
+  const float mean = (float)md;
+  float sd = 0.0f;
+  if (method == RMI_NORM_MEAN_STD || method == RMI_NORM_ASYM_CLIP) {
+    double q = 0.0;
+    for (int i = lo + lane; i < hi; i += 64) {
+      double sc = 0.0;
+      for (int t = 0; t < ep.T; ++t) sc += ep.turn_reward[(int64_t)t * B + i];
+      const double d = (double)((float)sc + (float)ep.penalty[i]) - md;
+      q += d * d;
+    }
+    q = wave_sum(q);
+    sd = n > 1 ? (float)sqrt(q / (double)(n - 1)) : __builtin_nanf("");
+  }
+  const bool use = sd > 1e-6f;
+  for (int i = lo + lane; i < hi; i += 64) {
+    double sc = 0.0;
+    for (int t = 0; t < ep.T; ++t) sc += ep.turn_reward[(int64_t)t * B + i];
+    const float x = (float)sc + (float)ep.penalty[i];
+    float y;
+    if (method == RMI_NORM_IDENTITY) y = x;
+    else if (method == RMI_NORM_MEAN) y = x - mean;
+    else {
+      y = use ? (x - mean) / (sd + 1e-6f) : 0.0f;
+      if (method == RMI_NORM_ASYM_CLIP) y = fminf(fmaxf(y, -1.0f), 3.0f);
+    }
+    norm_out[i] = y;
+  }
+}
+
 }  // namespace
 }  // namespace rmi
 
 RMI_API int rmi_rollout_metrics(const rmi_episode_t* ep, double* out, rmi_stream_t stream) {
   using namespace rmi;
-  if (!ep || !out || ep->B < 0 || !ep->flags || !ep->turn_info || !ep->n_turns || !ep->num_actions)
-    return RMI_EINVAL;
+  if (!ep || ep->B < 0) return RMI_EINVAL;
   if (ep->B == 0) return RMI_OK;
+  if (!out || !ep->flags || !ep->turn_info || !ep->n_turns || !ep->num_actions) return RMI_EINVAL;
   hipLaunchKernelGGL(rollout_metrics_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      as_stream(stream), *ep, out);
   return launch_status();
@@ -211,8 +279,9 @@ RMI_API int rmi_rollout_metrics(const rmi_episode_t* ep, double* out, rmi_stream
 
 RMI_API int rmi_trajectory_scores(const rmi_episode_t* ep, float* score, float* pen, rmi_stream_t stream) {
   using namespace rmi;
-  if (!ep || !score || ep->B < 0 || !ep->turn_reward || (pen && !ep->penalty)) return RMI_EINVAL;
+  if (!ep || ep->B < 0) return RMI_EINVAL;
   if (ep->B == 0) return RMI_OK;
+  if (!score || !ep->turn_reward || (pen && !ep->penalty)) return RMI_EINVAL;
   hipLaunchKernelGGL(trajectory_scores_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), 0,
                      as_stream(stream), *ep, score, pen);
   return launch_status();
@@ -221,8 +290,9 @@ RMI_API int rmi_trajectory_scores(const rmi_episode_t* ep, float* score, float* 
 RMI_API int rmi_group_normalize(const float* score, const float* pen, const int32_t* seg, int32_t G, int32_t B,
                                 int32_t method, float* out, rmi_stream_t stream) {
   using namespace rmi;
-  if (!score || !seg || !out || G < 0 || B < 0 || method < 0 || method > 3) return RMI_EINVAL;
+  if (G < 0 || B < 0 || method < 0 || method > 3) return RMI_EINVAL;
   if (B == 0 || G == 0) return RMI_OK;
+  if (!score || !seg || !out) return RMI_EINVAL;
   // the reference normalises only when some group has more than one member (ctx_manager.py:220)
   if (G >= B) method = RMI_NORM_IDENTITY;
   const int per = kBlock / 64;
@@ -233,8 +303,9 @@ RMI_API int rmi_group_normalize(const float* score, const float* pen, const int3
 
 RMI_API int rmi_row_sum(const float* x, int64_t B, int64_t L, float* out, rmi_stream_t stream) {
   using namespace rmi;
-  if (!x || !out || B < 0 || L < 0) return RMI_EINVAL;
+  if (B < 0 || L < 0) return RMI_EINVAL;
   if (B == 0) return RMI_OK;
+  if (!x || !out) return RMI_EINVAL;
   const int per = kBlock / 64;
   hipLaunchKernelGGL(row_sum_kernel, dim3((unsigned)((B + per - 1) / per)), dim3(kBlock), 0, as_stream(stream), x,
                      B, L, out);
@@ -252,5 +323,19 @@ RMI_API int rmi_filter_groups(const float* scores, int32_t G, int32_t gs, double
   if (k > G) k = G;
   hipLaunchKernelGGL(filter_kernel, dim3(1), dim3(kFilterThreads), 0, as_stream(stream), scores, G, gs, k, type,
                      g_std, g_max, g_mean, keep, metrics);
+  return launch_status();
+}
+
+RMI_API int rmi_rollout_finalize(const rmi_episode_t* ep, const int32_t* seg, int32_t G, int32_t method,
+                                 double* metrics, float* score, float* pen, float* norm, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!ep || ep->B < 0 || G < 0 || method < 0 || method > 3) return RMI_EINVAL;
+  if (ep->B == 0 || G == 0) return RMI_OK;
+  if (!seg || !ep->turn_reward || !ep->turn_info || !ep->penalty || !ep->flags || !ep->n_turns || !ep->num_actions)
+    return RMI_EINVAL;
+  if (G >= ep->B) method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: only if some group has > 1 member
+  const int per = kBlock / 64;
+  hipLaunchKernelGGL(finalize_kernel, dim3((G + per - 1) / per), dim3(kBlock), 0, as_stream(stream), *ep, seg, G,
+                     method, metrics, score, pen, norm);
   return launch_status();
 }

@@ -81,7 +81,7 @@ __global__ __launch_bounds__(kBlock) void frozenlake_step_turn_kernel(rmi_frozen
   }
   int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
   double penalty = ep.penalty[b];
-  TurnOut o = run_turn(e, in.actions + b * (int64_t)in.K, in.n_actions[b], in.K, num_actions, flags, n_turns,
+  TurnOut o = run_turn(e, load_actions(in.actions + b * (int64_t)in.K, in.K), in.n_actions[b], in.K, num_actions, flags, n_turns,
                        penalty, in.max_actions_per_traj, in.format_penalty, err);
   ep.num_actions[b] = num_actions;
   ep.flags[b] = flags;
@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void bandit_step_turn_kernel(rmi_bandit_t e
   uint8_t err = 0;
   int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
   double penalty = ep.penalty[b];
-  TurnOut o = run_turn(e, in.actions + b * (int64_t)in.K, in.n_actions[b], in.K, num_actions, flags, n_turns,
+  TurnOut o = run_turn(e, load_actions(in.actions + b * (int64_t)in.K, in.K), in.n_actions[b], in.K, num_actions, flags, n_turns,
                        penalty, in.max_actions_per_traj, in.format_penalty, err);
   ep.num_actions[b] = num_actions;
   ep.flags[b] = flags;
@@ -148,21 +148,17 @@ __global__ __launch_bounds__(kBlock) void bandit_step_turn_kernel(rmi_bandit_t e
   if (err_out && err) err_out[b] |= err;
 }
 
-bool episode_ok(const rmi_episode_t* ep, const rmi_turn_t* in) {
-  return ep && in && ep->B >= 0 && in->K >= 0 && in->K <= kMaxK && in->turn >= 0 && in->turn < ep->T &&
-         ep->num_actions && ep->flags && ep->n_turns && ep->penalty && ep->turn_reward && ep->turn_info &&
-         ep->turn_exec && (in->K == 0 || in->actions) && in->n_actions;
-}
-
 }  // namespace
 }  // namespace rmi
 
 RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                      uint8_t* err, rmi_stream_t stream) {
   using namespace rmi;
-  if (!env || !episode_ok(ep, in) || !env->desc || !env->s || !env->rng) return RMI_EINVAL;
+  if (!env) return RMI_EINVAL;
   if (env->nrow <= 0 || env->ncol <= 0 || env->nrow * env->ncol > 64) return RMI_EUNSUP;
-  if (ep->B == 0) return RMI_OK;
+  const int rc = check_turn_args(ep, in);
+  if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
+  if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
   const unsigned grid = (unsigned)((ep->B + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(frozenlake_step_turn_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *env, *ep, *in,
                      err);
@@ -172,8 +168,10 @@ RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_epis
 RMI_API int rmi_bandit_step_turn(const rmi_bandit_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                  uint8_t* err, rmi_stream_t stream) {
   using namespace rmi;
-  if (!env || !episode_ok(ep, in) || !env->hi_is_first || !env->rng) return RMI_EINVAL;
-  if (ep->B == 0) return RMI_OK;
+  if (!env) return RMI_EINVAL;
+  const int rc = check_turn_args(ep, in);
+  if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
+  if (!env->hi_is_first || !env->rng) return RMI_EINVAL;
   const unsigned grid = (unsigned)((ep->B + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(bandit_step_turn_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *env, *ep, *in, err);
   return launch_status();

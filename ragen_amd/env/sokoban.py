@@ -25,6 +25,9 @@ class SokobanBatch(BatchEnv):
         self.player = torch.zeros(B, 2, dtype=torch.int8, device=d)
         self.num_env_steps = torch.zeros(B, dtype=torch.int32, device=d)
         self.boxes_on_target = torch.zeros(B, dtype=torch.int32, device=d)
+        # the generated rooms: reset() uploads here once, restore() re-initialises from them
+        self.init_state = torch.zeros(B, HW, dtype=torch.uint8, device=d)
+        self.init_player = torch.zeros(B, 2, dtype=torch.int8, device=d)
 
     def struct(self) -> _lib.Sokoban:
         c = self.config
@@ -59,11 +62,13 @@ class SokobanBatch(BatchEnv):
 
     def load_state(self, fixed, state, player):
         self.room_fixed.copy_(torch.from_numpy(np.ascontiguousarray(fixed)))
-        self.room_state.copy_(torch.from_numpy(np.ascontiguousarray(state)))
-        self.player.copy_(torch.from_numpy(np.ascontiguousarray(player)))
-        self.num_env_steps.zero_()
-        self.boxes_on_target.zero_()
-        self.ep.reset_()
+        self.init_state.copy_(torch.from_numpy(np.ascontiguousarray(state)))
+        self.init_player.copy_(torch.from_numpy(np.ascontiguousarray(player)))
+        self.restore()
+
+    def restore(self):
+        """Back to the post-reset state of the last reset() (one fused launch)."""
+        ops.sokoban_reset(self.struct(), self.ep, self.init_state, self.init_player)
         self._invalidate()
 
     def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):

@@ -92,6 +92,13 @@ def sokoban_step_turn(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn, err:
     check(lib().rmi_sokoban_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_sokoban_step_turn")
 
 
+def sokoban_reset(env: _lib.Sokoban, ep: EpisodeState, init_state: torch.Tensor, init_player: torch.Tensor):
+    """Fused device reset from the generated rooms (state, player, counters, episode record)."""
+    _dev(init_state, init_player)
+    check(lib().rmi_sokoban_reset(env, ep.struct(), _ptr(init_state), _ptr(init_player), _stream()),
+          "rmi_sokoban_reset")
+
+
 def frozenlake_step_turn(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn,
                          err: Optional[torch.Tensor] = None):
     check(lib().rmi_frozenlake_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_frozenlake_step_turn")
@@ -152,6 +159,19 @@ def trajectory_scores(ep: EpisodeState):
     pen = torch.empty(ep.B, dtype=torch.float32, device=dev)
     check(lib().rmi_trajectory_scores(ep.struct(), _ptr(score), _ptr(pen), _stream()), "rmi_trajectory_scores")
     return score, pen
+
+
+def rollout_finalize(ep: EpisodeState, seg: torch.Tensor, method: str, norm: torch.Tensor,
+                     metrics: Optional[torch.Tensor] = None, score: Optional[torch.Tensor] = None,
+                     pen: Optional[torch.Tensor] = None):
+    """Fused get_rollout_states metrics + trajectory scores + reward normalisation (one launch)."""
+    if method not in _lib.NORM_METHODS:
+        raise ValueError(f"Invalid normalization method: {method}")
+    _dev(seg, norm, metrics, score, pen)
+    check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, _lib.NORM_METHODS[method],
+                                     _ptr(metrics), _ptr(score), _ptr(pen), _ptr(norm), _stream()),
+          "rmi_rollout_finalize")
+    return norm
 
 
 def group_normalize(score: torch.Tensor, pen: Optional[torch.Tensor], seg: torch.Tensor, method: str,

@@ -282,3 +282,31 @@ def test_whiten_errors_and_empty(device):
     ops.masked_whiten_(x, torch.zeros(2, 3, dtype=torch.uint8, device=device))  # status recorded, no crash
     e = ops.EpisodeState.empty(0, 1, device)
     assert ops.rollout_metrics(e).shape == (0, 4)
+
+
+def test_fused_reset_and_finalize(device):
+    """rmi_sokoban_reset == a fresh load; rmi_rollout_finalize == metrics + scores + normalize."""
+    B, T, K = 1024, 5, 5
+    env = SokobanBatch(SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100), B, T, K, device)
+    env.reset(synthetic.env_seeds(B))
+    s0 = env.room_state.clone()
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=11)
+    outs = []
+    for rep in range(2):
+        env.restore()
+        assert torch.equal(env.room_state, s0)
+        for t in range(T):
+            env.step_turn(t, _t(ids[t], device), _t(n[t], device), None, 10, -0.1)
+        outs.append(env.room_state.clone())
+    assert torch.equal(outs[0], outs[1])
+    seg = torch.arange(0, B + 1, 16, dtype=torch.int32, device=device)
+    for method in ("identity", "mean", "mean_std", "asym_clip"):
+        norm = torch.empty(B, dtype=torch.float32, device=device)
+        met = torch.empty(B, 4, dtype=torch.float64, device=device)
+        sc = torch.empty(B, dtype=torch.float32, device=device)
+        pe = torch.empty(B, dtype=torch.float32, device=device)
+        ops.rollout_finalize(env.ep, seg, method, norm, met, sc, pe)
+        s2, p2 = ops.trajectory_scores(env.ep)
+        assert torch.equal(sc, s2) and torch.equal(pe, p2)
+        assert torch.equal(torch.nan_to_num(met, 7.0), torch.nan_to_num(ops.rollout_metrics(env.ep), 7.0))
+        assert torch.equal(norm, ops.group_normalize(s2, p2, seg, method))
