@@ -1,0 +1,63 @@
+"""LLMAgentProxy — drop-in for ragen/llm_agent/agent_proxy.py:115-159 (the turn loop).
+
+The actor is any object with ``generate_sequences(DataProto) -> DataProto`` (a veRL
+RayWorkerGroup, a vLLM wrapper, or a scripted policy in tests/benchmarks).  LLM
+generation itself (vLLM, API clients) is outside this engine's scope.
+"""
+from typing import Dict, List
+
+from ..protocol import DataProto
+from .ctx_manager import ContextManager
+from .es_manager import EnvStateManager
+
+
+class ScriptedActor:
+    """Stand-in LLM: returns one response text per env from a user callable
+    ``policy(env_id, turn) -> str`` (no tokenizer round trip: non_tensor 'response_texts')."""
+
+    def __init__(self, policy):
+        self.policy = policy
+        self.turn = 0
+
+    def generate_sequences(self, lm_inputs: DataProto) -> DataProto:
+        env_ids = lm_inputs.non_tensor_batch["env_ids"]
+        out = DataProto(None, {"env_ids": env_ids,
+                               "response_texts": [self.policy(int(e), self.turn) for e in env_ids]},
+                        dict(lm_inputs.meta_info))
+        self.turn += 1
+        return out
+
+
+class LLMAgentProxy:
+    def __init__(self, config, actor_rollout_wg, tokenizer, device=None):
+        self.config = config
+        self.train_ctx_manager = ContextManager(config, tokenizer, mode="train", device=device)
+        self.train_es_manager = EnvStateManager(config, mode="train", device=device)
+        self.val_ctx_manager = ContextManager(config, tokenizer, mode="val", device=device)
+        self.val_es_manager = EnvStateManager(config, mode="val", device=device)
+        self.actor_wg = actor_rollout_wg
+        self.tokenizer = tokenizer
+
+    def generate_sequences(self, lm_inputs: DataProto) -> DataProto:
+        out = self.actor_wg.generate_sequences(lm_inputs)
+        if "env_ids" not in out.non_tensor_batch:
+            out.non_tensor_batch["env_ids"] = lm_inputs.non_tensor_batch["env_ids"]
+        return out
+
+    def rollout(self, dataproto: DataProto, val: bool = False) -> DataProto:
+        """agent_proxy.py:143-159."""
+        es = self.val_es_manager if val else self.train_es_manager
+        ctx = self.val_ctx_manager if val else self.train_ctx_manager
+        if hasattr(self.actor_wg, "turn"):
+            self.actor_wg.turn = 0
+        env_outputs: List[Dict] = es.reset()
+        for _ in range(self.config.agent_proxy.max_turn):
+            lm_inputs = ctx.get_lm_inputs(env_outputs, prepare_for_update=False)
+            lm_inputs.meta_info = dataproto.meta_info
+            lm_outputs = self.generate_sequences(lm_inputs)
+            env_inputs = ctx.get_env_inputs(lm_outputs)
+            env_outputs = es.step(env_inputs)
+            if len(env_outputs) == 0:
+                break
+        rollout_states = es.get_rollout_states()
+        return ctx.formulate_rollouts(rollout_states)

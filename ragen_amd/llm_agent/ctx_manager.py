@@ -1,0 +1,253 @@
+"""ContextManager — drop-in for ragen/llm_agent/ctx_manager.py:74-356.
+
+Text in/out stays on the host (prompt building, tokenizer, response regex: the LLM owns
+those bytes).  The numeric hot path runs on the GPU engine:
+  * ``get_masks_and_scores`` (ctx_manager.py:35-70) as torch device ops on the token ids
+    (cumsum / compare / scatter on the GPU tensor);
+  * ``_normalize_score_tensor`` (ctx_manager.py:175-226) through rmi_group_normalize;
+  * trajectory scores come straight from the device episode record when the rollout came
+    from this package's EnvStateManager.
+"""
+import re
+from itertools import zip_longest
+from typing import Dict, List
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..env import REGISTERED_ENV_CONFIGS
+from ..protocol import DataProto
+
+
+def get_special_tokens(tokenizer):
+    """ctx_manager.py:24-33."""
+    if "qwen" in tokenizer.name_or_path.lower():
+        return tokenizer.encode("<|im_start|>")[0], tokenizer.encode("<|im_end|>")[0]
+    if "llama-3" in tokenizer.name_or_path.lower():
+        return 128006, 128009
+    raise ValueError(f"Unsupported model: {tokenizer.name_or_path}")
+
+
+def get_masks_and_scores(input_ids: torch.Tensor, tokenizer, all_scores: List[List[float]] = None,
+                         use_turn_scores: bool = False, enable_response_mask: bool = False):
+    """ctx_manager.py:35-70, computed on the device holding ``input_ids`` (GPU in the engine)."""
+    special_token, reward_token = get_special_tokens(tokenizer)
+    turn_indicators = torch.cumsum((input_ids == special_token).to(torch.int64), dim=-1)
+    response_mask = (turn_indicators % 2 == 1) & (turn_indicators > 1)
+    loss_mask = response_mask.clone() if enable_response_mask else (turn_indicators > 1)
+    score_tensor = torch.zeros(input_ids.shape, dtype=torch.float32, device=input_ids.device)
+    if use_turn_scores:
+        for idx, scores in enumerate(zip_longest(*all_scores, fillvalue=0)):
+            scores = torch.tensor(scores, dtype=torch.float32, device=input_ids.device)
+            turn_indicator = idx * 2 + 3  # 0: pad. 1: system. 2+2n: user. 3+2n: assistant
+            reward_position = (input_ids == reward_token) & (turn_indicators == turn_indicator)
+            reward_position[~reward_position.any(dim=-1), -1] = True
+            score_tensor[reward_position] = scores
+        if "qwen" in tokenizer.name_or_path.lower():
+            score_tensor = score_tensor.roll(shifts=1, dims=-1)
+    else:
+        scores = [sum(i) for i in all_scores]
+        score_tensor[:, -1] = torch.tensor(scores, dtype=torch.float32, device=input_ids.device)
+    return score_tensor[:, 1:], loss_mask[:, :-1], response_mask[:, :-1]
+
+
+def segments_for(grouping: str, env_outputs: List[Dict]):
+    """Group ids of ctx_manager.py:184-191 as contiguous segments (first-seen order)."""
+    if grouping == "state":
+        tags = [o["group_id"] for o in env_outputs]
+    elif grouping == "inductive":
+        tags = [o["tag"] for o in env_outputs]
+    elif grouping == "batch":
+        tags = [1] * len(env_outputs)
+    else:
+        raise ValueError(f"Invalid grouping: {grouping}")
+    order, seen = {}, []
+    for i, t in enumerate(tags):
+        if t not in order:
+            order[t] = []
+            seen.append(t)
+        order[t].append(i)
+    perm = np.concatenate([np.asarray(order[t], np.int64) for t in seen]) if tags else np.zeros(0, np.int64)
+    seg = np.zeros(len(seen) + 1, np.int32)
+    seg[1:] = np.cumsum([len(order[t]) for t in seen])
+    return perm, seg
+
+
+class ContextManager:
+    def __init__(self, config, tokenizer, processor=None, mode: str = "train", device=None):
+        self.config = config
+        self.tokenizer = tokenizer
+        self.processor = processor
+        self.action_sep = self.config.agent_proxy.action_sep
+        self.special_token_list = ["<think>", "</think>", "<answer>", "</answer>", "<|im_start|>", "<|im_end|>"]
+        self.es_cfg = self.config.es_manager[mode]
+        self.env_nums = {tag: n * self.es_cfg.group_size
+                         for n, tag in zip(self.es_cfg.env_configs.n_groups, self.es_cfg.env_configs.tags)}
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._init_prefix_lookup()
+
+    def _init_prefix_lookup(self):
+        """ctx_manager.py:107-146."""
+        from dataclasses import asdict
+        prefixes, env_config_lookup = {}, {}
+        for env_tag, env_config in self.config.custom_envs.items():
+            if env_tag not in self.es_cfg.env_configs.tags:
+                continue
+            if env_config.env_type not in REGISTERED_ENV_CONFIGS:
+                raise ValueError(f"Environment {env_config.env_type} is not installed.")
+            new = asdict(REGISTERED_ENV_CONFIGS[env_config.env_type]())
+            for k, v in env_config.items():
+                new[k] = v
+            instr = new.get("env_instruction", "")
+            if new.get("grid_vocab", False):
+                instr += "\nThe meaning of each symbol in the state is:\n" + ", ".join(
+                    f"{k}: {v}" for k, v in new["grid_vocab"].items())
+            if new.get("action_lookup", False):
+                instr += "\nYour available actions are:\n" + ", ".join(f"{v}" for k, v in new["action_lookup"].items())
+                instr += (f"\nYou can make up to {new['max_actions_per_traj']} actions, separated by the action "
+                          f"separator \" " + self.action_sep + " \"\n")
+            prefixes[env_tag] = instr
+            env_config_lookup[env_tag] = {"max_tokens": env_config.get(
+                "max_tokens", self.config.actor_rollout_ref.rollout.response_length)}
+        self.prefix_lookup, self.env_config_lookup = {}, {}
+        cur = 0
+        gs = self.es_cfg.group_size
+        for tag, ng in zip(self.es_cfg.env_configs.tags, self.es_cfg.env_configs.n_groups):
+            for i in range(cur * gs, (cur + ng) * gs):
+                self.prefix_lookup[i] = prefixes[tag]
+                self.env_config_lookup[i] = env_config_lookup[tag]
+            cur += ng
+
+    def _parse_response(self, response: str):
+        """ctx_manager.py:148-173."""
+        ap = self.config.agent_proxy
+        pattern = r"<think>(.*?)</think>\s*<answer>(.*?)</answer>" if ap.enable_think else r"<answer>(.*?)</answer>"
+        match = re.search(pattern, response, re.DOTALL)
+        if not match:
+            return response, []
+        think_content, action_content = (match.group(1), match.group(2)) if ap.enable_think else ("", match.group(1))
+        for tok in self.special_token_list:
+            action_content = action_content.replace(tok, "").strip()
+            think_content = think_content.replace(tok, "").strip()
+        actions = [a.strip() for a in action_content.split(self.action_sep) if a.strip()]
+        if len(actions) > ap.max_actions_per_turn:
+            actions = actions[:ap.max_actions_per_turn]
+            action_content = (" " + self.action_sep + " ").join(actions)
+        llm_response = (f"<think>{think_content}</think><answer>{action_content}</answer>" if ap.enable_think
+                        else f"<answer>{action_content}</answer>")
+        return llm_response, actions
+
+    def _normalize_score_tensor(self, score_tensor: torch.Tensor, env_outputs: List[Dict]) -> torch.Tensor:
+        """ctx_manager.py:175-226 on the GPU (in place on score_tensor[:, -1], as the reference)."""
+        assert self.config.agent_proxy.use_turn_scores is False, \
+            "Reward normalization is not supported for use_turn_scores == True"
+        rn = self.config.agent_proxy.reward_normalization
+        if rn.method not in ("mean_std", "mean", "asym_clip", "identity"):
+            raise ValueError(f"Invalid normalization method: {rn.method}")
+        perm, seg = segments_for(rn.grouping, env_outputs)
+        dev = self.device
+        acc = score_tensor[:, -1].to(dev, torch.float32)
+        pen = torch.tensor([o.get("penalty", 0) for o in env_outputs], dtype=torch.float32).to(dev)
+        identity_perm = np.array_equal(perm, np.arange(len(perm)))
+        p = None if identity_perm else torch.from_numpy(perm).to(dev)
+        a = acc if p is None else acc[p].contiguous()
+        b = pen if p is None else pen[p].contiguous()
+        out = ops.group_normalize(a.contiguous(), b.contiguous(), torch.from_numpy(seg).to(dev), rn.method)
+        if p is not None:
+            res = torch.empty_like(out)
+            res[p] = out
+            out = res
+        score_tensor[:, -1] = out.to(score_tensor.device)
+        return score_tensor
+
+    def get_lm_inputs(self, env_outputs: List[Dict], prepare_for_update: bool) -> DataProto:
+        """ctx_manager.py:228-330."""
+        ap = self.config.agent_proxy
+        llm_input_texts, messages_list = [], []
+        for env_output in env_outputs:
+            if "state" in env_output["history"][-1] and prepare_for_update:
+                env_output["history"] = env_output["history"][:-1]
+            max_k = getattr(ap, "max_context_window", None)
+            if max_k is not None and isinstance(max_k, int) and max_k > 0:
+                env_output["history"] = env_output["history"][-max_k:]
+            messages = [{"role": "system", "content": "You're a helpful assistant. "},
+                        {"role": "user", "content": self.prefix_lookup[env_output["env_id"]]}]
+            for idx, content in enumerate(env_output["history"]):
+                messages[-1]["content"] += f"\nTurn {idx + 1}:\n"
+                if "state" in content:
+                    fmt = ("<think> [Your thoughts] </think> <answer> [your answer] </answer>" if ap.enable_think
+                           else "<answer> [your answer] </answer>")
+                    length = (f"Max response length: {self.env_config_lookup[env_output['env_id']]['max_tokens']} "
+                              "words (tokens).")
+                    messages[-1]["content"] += (f"State:\n{content['state']}\nYou have {content['actions_left']} "
+                                                f"actions left. Always output: {fmt} with no extra text. Strictly "
+                                                f"follow this format. {length}\n")
+                if "llm_response" in content:
+                    messages.append({"role": "assistant", "content": content["llm_response"]})
+                if "reward" in content and not (prepare_for_update and idx == len(env_output["history"]) - 1):
+                    messages.append({"role": "user", "content": f"Reward:\n{content['reward']}\n"})
+            assert all(msg["role"] == "assistant" for msg in messages[2::2])
+            text = self.tokenizer.apply_chat_template(messages, add_generation_prompt=(not prepare_for_update),
+                                                      tokenize=False)
+            if not prepare_for_update:
+                text += "<think>" if ap.enable_think else "<answer>"
+            llm_input_texts.append(text)
+            messages_list.append(messages)
+        inputs = self.tokenizer(llm_input_texts, return_tensors="pt", padding=True, padding_side="left",
+                                truncation=False)
+        input_ids, attention_mask = inputs.input_ids, inputs.attention_mask
+        position_ids = attention_mask.cumsum(dim=-1)
+        batch = {"input_ids": input_ids, "attention_mask": attention_mask, "position_ids": position_ids,
+                 "responses": input_ids[:, 1:]}
+        if prepare_for_update:
+            scores = [[i.get("reward", 0.0) for i in o["history"]] for o in env_outputs]
+            ids_dev = input_ids.to(self.device)
+            score_tensor, loss_mask, response_mask = get_masks_and_scores(
+                ids_dev, self.tokenizer, scores, use_turn_scores=ap.use_turn_scores,
+                enable_response_mask=self.config.enable_response_mask)
+            normalized = score_tensor
+            if not ap.use_turn_scores:
+                normalized = self._normalize_score_tensor(score_tensor, env_outputs)
+            response_length = response_mask.sum(dim=-1).float().mean().item()
+            batch["loss_mask"] = loss_mask
+            batch["rm_scores"] = normalized
+            batch["original_rm_scores"] = score_tensor  # aliases rm_scores, as in the reference
+        out = DataProto(batch)
+        out.non_tensor_batch = {
+            "env_ids": np.array([o["env_id"] for o in env_outputs], dtype=object),
+            "group_ids": np.array([o["group_id"] for o in env_outputs], dtype=object),
+            "messages_list": np.array(messages_list, dtype=object),
+        }
+        if prepare_for_update:
+            metrics = {}
+            for o in env_outputs:
+                for k, v in o["metrics"].items():
+                    metrics.setdefault(k, []).append(v)
+            mean_metrics = {k: np.sum(v) / self.env_nums[k.split("/")[0]] for k, v in metrics.items()}
+            for k, values in metrics.items():
+                prefix, suffix = k.split("/", 1)
+                nz = [v for v in values if v != 0]
+                if nz:
+                    mean_metrics[f"{prefix}/non-zero/{suffix}"] = np.mean(nz)
+            mean_metrics["response_length"] = response_length
+            out.meta_info = {"metrics": mean_metrics}
+        return out
+
+    def get_env_inputs(self, lm_outputs: DataProto) -> List[Dict]:
+        """ctx_manager.py:332-352."""
+        if lm_outputs.batch is not None and "responses" in lm_outputs.batch.keys():
+            responses = self.tokenizer.batch_decode(lm_outputs.batch["responses"], skip_special_tokens=True)
+        else:
+            responses = lm_outputs.non_tensor_batch["response_texts"]
+        prefix = "<think>" if self.config.agent_proxy.enable_think else "<answer>"
+        responses = [prefix + r for r in responses]
+        env_inputs = []
+        for env_id, response in zip(lm_outputs.non_tensor_batch["env_ids"], responses):
+            llm_response, actions = self._parse_response(response)
+            env_inputs.append({"env_id": env_id, "llm_raw_response": response, "llm_response": llm_response,
+                               "actions": actions})
+        return env_inputs
+
+    def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:
+        return self.get_lm_inputs(env_outputs, prepare_for_update=True)

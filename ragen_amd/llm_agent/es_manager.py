@@ -1,0 +1,241 @@
+"""EnvStateManager — drop-in for ragen/llm_agent/es_manager.py:28-258 on the GPU engine.
+
+Same constructor, ``reset(seed) -> rollout_cache``, ``step(all_env_inputs) -> env_outputs``,
+``get_rollout_states()``, ``render()`` and ``close()``, same dict shapes.  All env state
+lives in device SoA tensors owned by one batch object per tag; ``step`` maps the parsed
+action strings to ids on the host (es_manager.py:230-240), runs ONE kernel launch per tag
+for the whole turn, then reads back four small per-env vectors to build the dicts.
+
+``step_tensor`` is the dict-free fast path (used by the benchmark's kernel variant).
+"""
+import random
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import _lib
+from ..env import REGISTERED_ENV_CONFIGS, REGISTERED_ENVS
+
+
+@dataclass
+class EnvStatus:
+    """Status of an environment (es_manager.py:17-24), materialised from the device record."""
+    truncated: bool = False
+    terminated: bool = False
+    num_actions: int = 0
+    rewards: List[float] = field(default_factory=list)
+    seed: Optional[int] = None
+
+
+class _Tag:
+    """One env tag = one contiguous env range [lo, hi) = one batch object."""
+
+    def __init__(self, tag, lo, hi, batch, max_actions_per_traj, env_type):
+        self.tag, self.lo, self.hi, self.batch = tag, lo, hi, batch
+        self.max_actions_per_traj = int(max_actions_per_traj)
+        self.env_type = env_type
+
+
+def _make_env_config(env_type, env_config):
+    cls = REGISTERED_ENV_CONFIGS[env_type]
+    if env_config is None:
+        return cls()
+    return cls(**dict(env_config))
+
+
+class EnvStateManager:
+    def __init__(self, config, mode: str = "train", device=None):
+        self.sys_config = config
+        self.mode = mode
+        self.config = getattr(self.sys_config.es_manager, mode)
+        self.env_groups = int(self.config.env_groups)
+        self.group_size = int(self.config.group_size)
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        ap = self.sys_config.agent_proxy
+        self.max_turn = int(ap.max_turn)
+        self.K = int(ap.max_actions_per_turn)
+        self.format_penalty = float(self.sys_config.es_manager.format_penalty)
+        self._init_envs()
+        self.rollout_cache = None
+        self._turn = 0
+
+    def _init_envs(self):
+        n_groups = list(self.config.env_configs.n_groups)
+        tags = list(self.config.env_configs.tags)
+        assert sum(n_groups) == self.env_groups, \
+            f"Sum of n_groups must equal env_groups. Got sum({n_groups}) != {self.env_groups}"
+        assert len(tags) == len(n_groups), \
+            f"Number of tags must equal number of n_groups. Got {len(tags)} != {len(n_groups)}"
+        self.tags: List[_Tag] = []
+        done_groups = 0
+        for tag, ng in zip(tags, n_groups):
+            cfg_t = self.sys_config.custom_envs[tag]
+            env_type = cfg_t.env_type
+            env_config = _make_env_config(env_type, cfg_t.get("env_config"))
+            lo, hi = done_groups * self.group_size, (done_groups + ng) * self.group_size
+            batch = REGISTERED_ENVS[env_type](env_config, hi - lo, self.max_turn, self.K, self.device)
+            self.tags.append(_Tag(tag, lo, hi, batch, cfg_t.max_actions_per_traj, env_type))
+            done_groups += ng
+        self.n_envs = done_groups * self.group_size
+        self._tag_of = np.zeros(self.n_envs, np.int32)
+        for j, t in enumerate(self.tags):
+            self._tag_of[t.lo:t.hi] = j
+        # reference-shaped entries (es_manager.py:69-70); 'env' is the batch, 'local' its row
+        self.envs = [{"tag": t.tag, "group_id": i // self.group_size, "env_id": i, "env": t.batch,
+                      "local": i - t.lo, "config": t.batch.config, "status": EnvStatus(),
+                      "max_actions_per_traj": t.max_actions_per_traj}
+                     for t in self.tags for i in range(t.lo, t.hi)]
+
+    # ---------------------------------------------------------------------- reset
+    def reset(self, seed: Optional[int] = None):
+        """es_manager.py:75-103."""
+        if self.mode == "train":
+            seed = random.randint(0, 1000000) if seed is None else seed
+        else:
+            seed = 123
+        seeds = seed + np.arange(self.n_envs) // self.group_size  # _expand_seed
+        for t in self.tags:
+            t.batch.reset(seeds[t.lo:t.hi])
+        self._turn = 0
+        self._seeds = seeds
+        self.rollout_cache = [{"env_id": e["env_id"], "history": [], "group_id": e["group_id"], "tag": e["tag"],
+                               "penalty": 0} for e in self.envs]
+        for e, cache in zip(self.envs, self.rollout_cache):
+            e["status"] = EnvStatus(seed=int(seeds[e["env_id"]]))
+            cache["history"] = self._update_cache_history(cache["history"], e["env"].render(e["local"]),
+                                                          e["max_actions_per_traj"], None)
+        return self.rollout_cache
+
+    # ----------------------------------------------------------------------- step
+    def step(self, all_env_inputs: List[Dict]):
+        """es_manager.py:105-171: one kernel launch per tag for the whole turn."""
+        if self._turn >= self.max_turn:
+            raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
+        t = self._turn
+        per_tag = {j: [] for j in range(len(self.tags))}
+        for inp in all_env_inputs:
+            per_tag[int(self._tag_of[int(inp["env_id"])])].append(inp)
+        still_active = set()
+        for j, tg in enumerate(self.tags):
+            inputs = per_tag[j]
+            if not inputs:
+                continue
+            B = tg.hi - tg.lo
+            ids = np.zeros((B, self.K), np.int8)
+            n = np.zeros(B, np.uint8)
+            has = np.zeros(B, np.uint8)
+            mapped = {}
+            answers = [[] for _ in range(B)] if tg.env_type == "countdown" else None
+            for inp in inputs:
+                i = int(inp["env_id"]) - tg.lo
+                acts = list(inp["actions"])
+                if len(acts) > self.K:
+                    raise ValueError(f"env {inp['env_id']}: {len(acts)} actions > max_actions_per_turn={self.K}")
+                m = tg.batch.map_actions(i, acts)
+                mapped[i] = (acts, m)
+                ids[i, :len(m)] = m
+                n[i] = len(acts)
+                has[i] = 1
+                if answers is not None:
+                    answers[i] = acts
+            dev = self.device
+            ids_t = torch.from_numpy(ids).to(dev, non_blocking=True)
+            n_t = torch.from_numpy(n).to(dev, non_blocking=True)
+            has_t = torch.from_numpy(has).to(dev, non_blocking=True)
+            kw = {}
+            if answers is not None:
+                buf, lens = tg.batch.encode_answers(answers)
+                kw = {"answers": torch.from_numpy(buf).to(dev), "answer_len": torch.from_numpy(lens).to(dev)}
+            tg.batch.step_turn(t, ids_t, n_t, has_t, tg.max_actions_per_traj, self.format_penalty, **kw)
+            ep = tg.batch.ep
+            host = torch.stack([ep.flags.to(torch.int64), ep.num_actions.to(torch.int64),
+                                ep.turn_info[t].to(torch.int64), ep.turn_exec[t].to(torch.int64)]).cpu().numpy()
+            rw = ep.turn_reward[t].cpu().numpy()
+            pen = ep.penalty.cpu().numpy()
+            flags, num_actions, info, n_exec = host
+            for inp in inputs:
+                i = int(inp["env_id"]) - tg.lo
+                gid = tg.lo + i
+                entry, cache = self.envs[gid], self.rollout_cache[gid]
+                acts, m = mapped[i]
+                valid = [a for a in m if a != 0] if tg.env_type != "countdown" else list(acts)
+                executed = valid[:int(n_exec[i])]
+                if hasattr(tg.batch, "note_executed"):
+                    tg.batch.note_executed(t, i, executed)
+                acc = float(rw[i]) if n_exec[i] else 0
+                if tg.env_type == "countdown" and n_exec[i] and acc in (0.0, 1.0):
+                    acc = int(acc)  # compute_reward returns int 0 / int score (countdown/env.py:73-78)
+                inf = int(info[i])
+                turn_info = {}
+                if inf & _lib.INFO_PRESENT:
+                    turn_info = {"action_is_effective": bool(inf & _lib.INFO_EFFECTIVE),
+                                 "action_is_valid": bool(inf & _lib.INFO_VALID),
+                                 "success": bool(inf & _lib.INFO_SUCCESS)}
+                st = entry["status"]
+                st.num_actions = int(num_actions[i])
+                st.rewards.append(acc)
+                st.terminated = bool(flags[i] & _lib.FLAG_TERMINATED)
+                st.truncated = bool(flags[i] & _lib.FLAG_TRUNCATED)
+                cache["penalty"] = float(pen[i]) if pen[i] != 0 else cache["penalty"]
+                cache["history"] = self._update_cache_history(
+                    cache["history"], entry["env"].render(i), entry["max_actions_per_traj"] - st.num_actions,
+                    {"actions": executed, "reward": acc, "info": turn_info, "llm_response": inp["llm_response"],
+                     "llm_raw_response": inp["llm_raw_response"]})
+                if not (flags[i] & _lib.FLAG_DONE):
+                    still_active.add(gid)
+        self._turn += 1
+        # only not-done envs go back for generation, in input order (es_manager.py:168-169)
+        return [self.rollout_cache[int(inp["env_id"])] for inp in all_env_inputs
+                if int(inp["env_id"]) in still_active]
+
+    def step_tensor(self, actions: torch.Tensor, n_actions: torch.Tensor, has_input: Optional[torch.Tensor] = None,
+                    tag_index: int = 0, **kw):
+        """Dict-free turn on the device (kernel variant): ids i8[B,K] of one tag batch."""
+        tg = self.tags[tag_index]
+        tg.batch.step_turn(self._turn, actions, n_actions, has_input, tg.max_actions_per_traj, self.format_penalty,
+                           **kw)
+        self._turn += 1
+        return tg.batch.ep
+
+    # ------------------------------------------------------- get_rollout_states
+    def get_rollout_states(self):
+        """es_manager.py:173-207 (per-env metrics reduced on the device)."""
+        from .. import ops
+        for tg in self.tags:
+            ep = tg.batch.ep
+            m = ops.rollout_metrics(ep).cpu().numpy()
+            info = ep.turn_info.cpu().numpy()
+            for i in range(tg.hi - tg.lo):
+                gid = tg.lo + i
+                cache = self.rollout_cache[gid]
+                env_metric = {"success": float(m[i, 0]), "num_actions": int(m[i, 1])}
+                custom = {}
+                for tt in range(min(self._turn, info.shape[0])):
+                    if info[tt, i] & _lib.INFO_PRESENT:
+                        custom.setdefault("action_is_effective", []).append(
+                            float(bool(info[tt, i] & _lib.INFO_EFFECTIVE)))
+                        custom.setdefault("action_is_valid", []).append(float(bool(info[tt, i] & _lib.INFO_VALID)))
+                if custom:
+                    env_metric["action_is_effective"] = float(m[i, 2])
+                    env_metric["action_is_valid"] = float(m[i, 3])
+                cache["history"][-1]["metrics"] = custom
+                cache["metrics"] = {f"{tg.tag}/{k}": v for k, v in env_metric.items()}
+        return self.rollout_cache
+
+    @staticmethod
+    def _update_cache_history(history, next_state, actions_left, num_actions_info=None):
+        """es_manager.py:212-228."""
+        if num_actions_info is not None:
+            assert len(history), "History should not be empty"
+            history[-1].update(num_actions_info)
+        history.append({"state": next_state, "actions_left": actions_left})
+        return history
+
+    def render(self):
+        return [e["env"].render(e["local"]) for e in self.envs]
+
+    def close(self):
+        for t in self.tags:
+            t.batch.close()
