@@ -37,15 +37,18 @@ class SokobanBatch(BatchEnv):
 
     # SokobanEnv.reset (sokoban/env.py:28-42): generate_room under all_seed(seed); on
     # RuntimeError/RuntimeWarning reseed with abs(hash(str(seed))) % 2**32 and retry.
-    @staticmethod
-    def generate(seeds, H, W, num_boxes, search_depth, n_threads=8):
+    # (hash() of a str depends on PYTHONHASHSEED — exactly as in the reference process.)
+    reseed_fn = staticmethod(lambda s: abs(hash(str(s))) % (2 ** 32))
+
+    @classmethod
+    def generate(cls, seeds, H, W, num_boxes, search_depth, n_threads=8):
         seeds = np.asarray(seeds, np.int64)
         uniq, inv = np.unique(seeds, return_inverse=True)
         fixed, state, player, status = ops.generate_sokoban_rooms(uniq, H, W, num_boxes, search_depth, n_threads)
         for i in np.nonzero(status)[0]:
             s = int(uniq[i])
             for _ in range(64):
-                s = abs(hash(str(s))) % (2 ** 32)
+                s = cls.reseed_fn(s)
                 f, st, p, ok = ops.generate_sokoban_rooms([s], H, W, num_boxes, search_depth, 1)
                 if ok[0] == 0:
                     fixed[i], state[i], player[i] = f[0], st[0], p[0]
