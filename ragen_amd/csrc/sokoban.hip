@@ -95,6 +95,116 @@ struct SokobanLdsEnv {
   }
 };
 
+// One EnvStateManager turn for one Sokoban env (es_manager.py:149-169), specialised for the
+// latency of a lone wave: the executed-action list valid[:left] is built up front with
+// predicated byte ops, then each step is straight-line code — the index arithmetic of an
+// interior player (every generated room: the border is wall) and six independent LDS reads;
+// the rare player that can reach the border (hand-made rooms) takes the exact numpy-wrap path
+// of SokobanLdsEnv::step.  Same results as run_turn + step, bit for bit.
+__device__ __forceinline__ TurnOut sokoban_turn(SokobanLdsEnv& e, uint64_t acts, int n_act, int K, int32_t& num_actions,
+                                                uint8_t& flags, int32_t& n_turns, double& penalty, int max_actions,
+                                                double format_penalty, uint8_t& err) {
+  TurnOut o;
+  o.acc = 0.0;
+  o.info = 0;
+  o.exec = 0;
+  o.stepped_any_state = false;
+  flags &= (uint8_t)~RMI_FLAG_DONE;
+  if (n_act > K) n_act = K;
+  const int left = max_actions - num_actions;
+  // valid = [ids of known names]; exec list = valid[:left]  (es_manager.py:156-157)
+  uint64_t run = 0;
+  int nv = 0, cnt = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) {
+    const uint32_t a = (uint32_t)(acts >> (8 * k)) & 0xFFu;
+    const bool valid = k < n_act && a != 0;
+    const bool take = valid && cnt < left;
+    run |= take ? ((uint64_t)a << (8 * cnt)) : 0ull;
+    cnt += take;
+    nv += valid;
+  }
+  if (nv != n_act || nv == 0) penalty += format_penalty;  // :158-159
+  const int W = e.W, H = e.H;
+  int p = e.r * W + e.c;  // player cell (fast path: interior player)
+  bool stop = false, turn_done = false, succ_last = false;
+  for (int i = 0; i < kMaxK; ++i) {
+    const bool go = i < cnt && !stop;
+    if (!__any(go)) break;  // wave-uniform trip count
+    if (!go) continue;
+    const int a = (int)(int8_t)(uint8_t)(run >> (8 * i));
+    const int d = (a - 1) & 3;
+    const int dr = (d == 1) - (d == 0), dc = (d == 3) - (d == 2);
+    const int nr = e.r + dr, nc = e.c + dc, br = nr + dr, bc = nc + dc;
+    const bool in_n = (unsigned)nr < (unsigned)H && (unsigned)nc < (unsigned)W;
+    const bool in_b = (unsigned)br < (unsigned)H && (unsigned)bc < (unsigned)W;
+    const bool high = br >= H || bc >= W;
+    const bool fast = a >= 1 && a <= 8 && in_n && (in_b || high) && (unsigned)e.r < (unsigned)H &&
+                      (unsigned)e.c < (unsigned)W;
+    double r;
+    bool done, eff, succ;
+    if (fast) {
+      const int delta = dr * W + dc;
+      const int ni = p + delta, bi = in_b ? ni + delta : p;
+      const int vn = e.st[ni], vb = e.st[bi], vo = e.st[p];
+      const int fn = e.fx[ni], fb = e.fx[bi], fo = e.fx[p];
+      const bool push_act = a <= 4;
+      const bool is_push = push_act && !high && (vn == 3 || vn == 4) && (vb == 1 || vb == 2);
+      const bool try_move = !push_act || (!high && !is_push);  // _push falls back to _move
+      const bool moved = is_push || (try_move && (vn == 1 || vn == 2));
+      const int vbn = fb == 2 ? 3 : 4;  // box_type
+      e.num_env_steps += 1;
+      if (moved) {
+        e.n_open += SokobanLdsEnv::open_of(5, fn) - SokobanLdsEnv::open_of(vn, fn) + (fo == 2) -
+                    SokobanLdsEnv::open_of(vo, fo);
+        e.st[ni] = 5;
+        e.st[p] = (uint8_t)fo;
+        e.r = nr;
+        e.c = nc;
+        p = ni;
+      }
+      if (is_push) {
+        e.n_open += SokobanLdsEnv::open_of(vbn, fb) - SokobanLdsEnv::open_of(vb, fb);
+        e.st[bi] = (uint8_t)vbn;
+      }
+      const int cur = e.num_boxes - e.n_open;
+      double rw = -0.1;
+      rw += cur > e.boxes_on_target ? 1.0 : (cur < e.boxes_on_target ? -1.0 : 0.0);
+      const bool all_on = e.n_open == 0;
+      rw += all_on ? 10.0 : 0.0;
+      e.boxes_on_target = cur;
+      r = rw;
+      done = all_on || (e.max_steps == e.num_env_steps);
+      succ = cur == e.num_boxes;
+      eff = moved;
+    } else if (!e.step(a, r, done, eff, succ)) {  // exact numpy-wrap / error path
+      err |= (a < 1 || a > 8) ? RMI_ERR_ACTION : 0;
+      stop = true;
+      continue;
+    } else {
+      p = e.r * W + e.c;
+    }
+    o.acc += r;
+    o.exec++;
+    o.stepped_any_state = true;
+    o.info = (uint8_t)(RMI_INFO_PRESENT | (eff ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID | (succ ? RMI_INFO_SUCCESS : 0));
+    succ_last = succ;
+    if (done) {
+      stop = true;
+      turn_done = true;
+    }
+  }
+  num_actions += o.exec;
+  n_turns += 1;
+  if (turn_done) {
+    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_DONE;
+    flags = succ_last ? (uint8_t)(flags & ~RMI_FLAG_TRUNCATED) : (uint8_t)(flags | RMI_FLAG_TRUNCATED);
+  } else if (num_actions >= max_actions) {
+    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
+  }
+  return o;
+}
+
 // Stage `nwords` dwords global -> LDS (16 B per lane when both are 16-B aligned).
 __device__ __forceinline__ void stage_in(uint32_t* lds, const uint8_t* g, int nwords, int lane, bool vec) {
   const uint32_t* g1 = reinterpret_cast<const uint32_t*>(g);
@@ -193,8 +303,8 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     e.max_steps = env.max_steps;
 
     uint8_t err = 0, flags = flags0;
-    TurnOut o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
-                         in.format_penalty, err);
+    TurnOut o = sokoban_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
+                             in.format_penalty, err);
     err |= e.err;
     changed = o.stepped_any_state;
     ep.num_actions[b] = num_actions;

@@ -1,0 +1,65 @@
+"""Multi-GPU sharding of the rollout: one process per GPU, torch.distributed
+("nccl" = RCCL over xGMI on ROCm; "gloo" in CPU tests).
+
+Partitioning: contiguous, group-aligned — rank r of W owns env groups
+[r*G/W, (r+1)*G/W); global env ids, group ids and seeds (base + global group id) are kept,
+so a rank's envs are bit-identical to the same envs of a 1-GPU run.  The rollout itself
+needs no collective.  The real exchange steps after it are:
+  * the rollout filter (agent_trainer.py:461-500) ranks groups GLOBALLY: all-gather the
+    per-group trajectory scores, then every rank runs the identical deterministic top-k;
+  * masked whitening (verl masked_whiten) uses batch-global mean/var: all-gather the
+    per-row (sum, sum_sq, count) partials and reduce them in global row order, so the
+    statistics are identical for every world size;
+  * optional reassembly of per-env trajectory tensors before the PPO update
+    (``gather_rollout``), an all-gather of fixed-shape per-env rows.
+"""
+from typing import Dict, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def shard_groups(n_groups: int, world_size: int, rank: int) -> Tuple[int, int]:
+    """-> (first global group, number of local groups); contiguous and group-aligned."""
+    lo = (n_groups * rank) // world_size
+    hi = (n_groups * (rank + 1)) // world_size
+    return lo, hi - lo
+
+
+def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
+    """Concatenate every rank's [n_r, ...] rows in rank order (n_r may differ by rank)."""
+    W, _ = world()
+    if W == 1:
+        return x
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    sizes = [torch.zeros_like(n) for _ in range(W)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    m = max(sizes)
+    pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    pad[:x.shape[0]] = x
+    bufs = [torch.empty_like(pad) for _ in range(W)]
+    dist.all_gather(bufs, pad)
+    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
+
+
+def global_whiten_stats(row_stats: torch.Tensor) -> torch.Tensor:
+    """[n_local, 3] f64 (sum, sum_sq, count) -> [n_global, 3] in global row order."""
+    return all_gather_rows(row_stats)
+
+
+def gather_group_scores(scores: torch.Tensor, group_size: int) -> torch.Tensor:
+    """Per-env trajectory scores of the local groups -> all groups' scores (global order)."""
+    assert scores.shape[0] % group_size == 0
+    return all_gather_rows(scores.view(-1, group_size)).reshape(-1)
+
+
+def gather_rollout(tensors: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """Reassemble fixed-shape per-env trajectory tensors [n_local, ...] from every rank."""
+    return {k: all_gather_rows(v) for k, v in tensors.items()}
