@@ -113,8 +113,10 @@ static int sok_move(sok_t* e, int a, int* moved) {
   const int dr = CHG[(a - 1) % 4][0], dc = CHG[(a - 1) % 4][1];
   int ni, oi;
   *moved = 0;
-  if (!sok_idx(e, e->pr + dr, e->pc + dc, &ni) || !sok_idx(e, e->pr, e->pc, &oi)) return 0;
+  if (!sok_idx(e, e->pr + dr, e->pc + dc, &ni)) return 0;
   if (e->state[ni] == 1 || e->state[ni] == 2) {
+    /* current_position is indexed only once the move happens (after state[new] = 5) */
+    if (!sok_idx(e, e->pr, e->pc, &oi)) return 0;
     e->pr += dr;
     e->pc += dc;
     e->state[ni] = 5;
@@ -135,11 +137,17 @@ static int sok_step(void* ctx, int a, double* r, int* done, int* eff, int* succ)
     const int nr = e->pr + dr, nc = e->pc + dc, br = nr + dr, bc = nc + dc;
     if (!(br >= e->H || bc >= e->W)) {
       int ni, bi, oi;
-      if (!sok_idx(e, nr, nc, &ni) || !sok_idx(e, br, bc, &bi) || !sok_idx(e, e->pr, e->pc, &oi)) {
+      /* can_push_box = state[new] in [3, 4]; can_push_box &= state[new_box] in [1, 2]:
+       * both cells are indexed whatever the first test gave */
+      if (!sok_idx(e, nr, nc, &ni) || !sok_idx(e, br, bc, &bi)) {
         e->err |= 2;
         return 0;
       }
       if ((e->state[ni] == 3 || e->state[ni] == 4) && (e->state[bi] == 1 || e->state[bi] == 2)) {
+        if (!sok_idx(e, e->pr, e->pc, &oi)) {
+          e->err |= 2;
+          return 0;
+        }
         e->pr = nr;
         e->pc = nc;
         e->state[ni] = 5;

@@ -21,6 +21,23 @@
 namespace rmi {
 namespace {
 
+// Diagnostic build only (tools/microbench.hip defines RMI_STAMPS): per-wave s_memtime /
+// s_memrealtime stamps at phase boundaries.  Compiled out of the library.
+#ifdef RMI_STAMPS
+__device__ unsigned long long* g_stamps;
+#define RMI_STAMP(i)                                                                   \
+  do {                                                                                 \
+    if (threadIdx.x == 0) {                                                            \
+      g_stamps[blockIdx.x * 16 + 2 * (i)] = __builtin_amdgcn_s_memtime();              \
+      g_stamps[blockIdx.x * 16 + 2 * (i) + 1] = __builtin_amdgcn_s_memrealtime();      \
+    }                                                                                  \
+  } while (0)
+#else
+#define RMI_STAMP(i) \
+  do {               \
+  } while (0)
+#endif
+
 constexpr int kWave = 64;
 constexpr int kMaxCells = 64;
 
@@ -63,7 +80,9 @@ struct SokobanLdsEnv {
     const bool is_push = push_act && !high && (vn == 3 || vn == 4) && (vb == 1 || vb == 2);
     const bool try_move = !push_act || (!high && !is_push);  // _push falls back to _move
     const bool moved = is_push || (try_move && (vn == 1 || vn == 2));
-    if ((push_act && !high && (!ok_n || !ok_b)) || (try_move && !ok_n) || !ok_o) {
+    // _push indexes new and new_box whenever the box side is not high; the player's own cell
+    // is indexed only when the player actually moves (gym_sokoban _push / _move)
+    if ((push_act && !high && (!ok_n || !ok_b)) || (try_move && !ok_n) || (moved && !ok_o)) {
       err |= RMI_ERR_INDEX;  // the reference raises IndexError; flag it, leave the env untouched
       return false;
     }
@@ -95,44 +114,163 @@ struct SokobanLdsEnv {
   }
 };
 
-// One EnvStateManager turn for one Sokoban env (es_manager.py:149-169), specialised for the
-// latency of a lone wave: the executed-action list valid[:left] is built up front with
-// predicated byte ops, then each step is straight-line code — the index arithmetic of an
-// interior player (every generated room: the border is wall) and six independent LDS reads;
-// the rare player that can reach the border (hand-made rooms) takes the exact numpy-wrap path
-// of SokobanLdsEnv::step.  Same results as run_turn + step, bit for bit.
-__device__ __forceinline__ TurnOut sokoban_turn(SokobanLdsEnv& e, uint64_t acts, int n_act, int K, int32_t& num_actions,
-                                                uint8_t& flags, int32_t& n_turns, double& penalty, int max_actions,
-                                                double format_penalty, uint8_t& err) {
+// valid = [ids of known names], exec list = valid[:left] (es_manager.py:156-157), packed one
+// byte per action; format penalty if len(valid) != len(actions) or nothing valid (:158-159).
+struct ExecList {
+  uint64_t run;
+  int cnt;
+};
+__device__ __forceinline__ ExecList exec_list(uint64_t acts, int n_act, int K, int left, double& penalty,
+                                              double format_penalty) {
+  if (n_act > K) n_act = K;
+  ExecList x;
+  x.run = 0;
+  x.cnt = 0;
+  int nv = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) {
+    const uint32_t a = (uint32_t)(acts >> (8 * k)) & 0xFFu;
+    const bool valid = k < n_act && a != 0;
+    const bool take = valid && x.cnt < left;
+    x.run |= take ? ((uint64_t)a << (8 * x.cnt)) : 0ull;
+    x.cnt += take;
+    nv += valid;
+  }
+  if (nv != n_act || nv == 0) penalty += format_penalty;
+  return x;
+}
+
+// End of the turn: counters and done / truncated flags (es_manager.py:160-169).
+__device__ __forceinline__ void finish_turn(const TurnOut& o, bool turn_done, bool succ_last, int32_t& num_actions,
+                                            uint8_t& flags, int32_t& n_turns, int max_actions) {
+  num_actions += o.exec;
+  n_turns += 1;
+  if (turn_done) {
+    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_DONE;
+    flags = succ_last ? (uint8_t)(flags & ~RMI_FLAG_TRUNCATED) : (uint8_t)(flags | RMI_FLAG_TRUNCATED);
+  } else if (num_actions >= max_actions) {
+    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
+  }
+}
+
+// _calc_reward + _check_if_done after one executed step (gym_sokoban sokoban_env.py).
+__device__ __forceinline__ double step_reward(int n_open, int num_boxes, int& boxes_on_target, bool& all_on) {
+  const int cur = num_boxes - n_open;
+  double rw = -0.1;                                                           // penalty_for_step
+  rw += cur > boxes_on_target ? 1.0 : (cur < boxes_on_target ? -1.0 : 0.0);  // box on / off target
+  all_on = n_open == 0;
+  rw += all_on ? 10.0 : 0.0;  // reward_finished
+  boxes_on_target = cur;
+  return rw;
+}
+
+// ------------------------------------------------------------------ bitboard fast path
+// A room is "regular" when room_state is exactly what room_fixed + box set + player imply
+// (every state byte equals the fixed byte, except boxes = 3 on a target / 4 on floor and the
+// player's 5 on a non-wall cell), room_fixed holds only {0,1,2}, its whole border is wall and
+// the player is interior.  Every generated room is regular and gym_sokoban's writes keep it
+// so.  For a regular room H*W <= 64 cells fit a u64 per class (cell i = bit i, row-major),
+// a step is a handful of register bit operations with no memory access, and numpy's
+// negative-index wrap can never trigger (the player never reaches the border).  Anything
+// else takes the exact LDS path (SokobanLdsEnv::step).
+
+// high bit of each selected byte of a dword -> 4-bit nibble (byte j -> bit j)
+__device__ __forceinline__ uint32_t nib(uint32_t m) { return (((m >> 7) * 0x01020408u) >> 24) & 0xFu; }
+// 4-bit nibble -> byte mask (bit j -> byte j = 0xFF)
+__device__ __forceinline__ uint32_t unnib(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) * 0xFFu; }
+
+template <int NW>
+__device__ __forceinline__ bool decode_board(const uint32_t (&xs)[NW], const uint32_t (&xf)[NW], int row_words,
+                                             uint64_t& wall, uint64_t& target, uint64_t& box, uint64_t& player) {
+  uint32_t bad = 0;
+  wall = target = box = player = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < row_words) {
+      const uint32_t s = xs[w], f = xf[w];
+      const uint32_t f0 = zero_bytes(f), f1 = eq_bytes(f, 1u), f2 = eq_bytes(f, 2u);
+      const uint32_t s3 = eq_bytes(s, 3u), s4 = eq_bytes(s, 4u), s5 = eq_bytes(s, 5u);
+      bad |= ~(f0 | f1 | f2) & 0x80808080u;                                         // fixed in {0,1,2}
+      bad |= ~(zero_bytes(s ^ f) | (s3 & f2) | (s4 & f1) | s5) & 0x80808080u;  // state consistent
+      wall |= (uint64_t)nib(f0) << (4 * w);
+      target |= (uint64_t)nib(f2) << (4 * w);
+      box |= (uint64_t)nib(s3 | s4) << (4 * w);
+      player |= (uint64_t)nib(s5) << (4 * w);
+    }
+  }
+  return bad == 0;
+}
+
+// One EnvStateManager turn of one regular room on bitboards; bit-identical to the LDS path.
+__device__ __forceinline__ TurnOut board_turn(uint64_t wall, uint64_t target, uint64_t& box, int& r, int& c, int W,
+                                              int hw, int& num_env_steps, int& boxes_on_target, int num_boxes,
+                                              int max_steps, const ExecList& x, bool& turn_done, bool& succ_last,
+                                              bool& moved_any) {
   TurnOut o;
   o.acc = 0.0;
   o.info = 0;
   o.exec = 0;
   o.stepped_any_state = false;
-  flags &= (uint8_t)~RMI_FLAG_DONE;
-  if (n_act > K) n_act = K;
-  const int left = max_actions - num_actions;
-  // valid = [ids of known names]; exec list = valid[:left]  (es_manager.py:156-157)
-  uint64_t run = 0;
-  int nv = 0, cnt = 0;
-#pragma unroll
-  for (int k = 0; k < kMaxK; ++k) {
-    const uint32_t a = (uint32_t)(acts >> (8 * k)) & 0xFFu;
-    const bool valid = k < n_act && a != 0;
-    const bool take = valid && cnt < left;
-    run |= take ? ((uint64_t)a << (8 * cnt)) : 0ull;
-    cnt += take;
-    nv += valid;
-  }
-  if (nv != n_act || nv == 0) penalty += format_penalty;  // :158-159
-  const int W = e.W, H = e.H;
-  int p = e.r * W + e.c;  // player cell (fast path: interior player)
-  bool stop = false, turn_done = false, succ_last = false;
+  int p = r * W + c;
+  bool stop = false;
   for (int i = 0; i < kMaxK; ++i) {
-    const bool go = i < cnt && !stop;
+    const bool go = i < x.cnt && !stop;
     if (!__any(go)) break;  // wave-uniform trip count
     if (!go) continue;
-    const int a = (int)(int8_t)(uint8_t)(run >> (8 * i));
+    const int a = (int)(x.run >> (8 * i)) & 0xFF;  // 1..8, checked by the caller
+    const int d = (a - 1) & 3;                      // CHANGE_COORDINATES[(a-1) % 4]
+    const int dr = (d == 1) - (d == 0), dc = (d == 3) - (d == 2);
+    const int s = dr * W + dc;
+    const int n = p + s, bb = n + s;  // n is always inside: the player is interior
+    const uint64_t nbit = 1ull << n;
+    const bool n_wall = (wall & nbit) != 0, n_box = (box & nbit) != 0;
+    const bool bb_in = (unsigned)bb < (unsigned)hw;  // outside only when n is border wall
+    const uint64_t bbit = bb_in ? 1ull << bb : 0ull;
+    const bool b_free = bb_in && ((wall | box) & bbit) == 0;  // state[bb] in {1, 2}
+    const bool is_push = a <= 4 && n_box && b_free;           // _push
+    const bool moved = is_push || (!n_wall && !n_box);        // _push falls back to _move
+    box ^= is_push ? (nbit | bbit) : 0ull;
+    p = moved ? n : p;
+    r += moved ? dr : 0;
+    c += moved ? dc : 0;
+    moved_any |= moved;
+    num_env_steps += 1;
+    bool all_on;
+    const int n_open = __popcll(target & ~box);  // (state == 2) | ((fixed == 2) & (state == 5))
+    o.acc += step_reward(n_open, num_boxes, boxes_on_target, all_on);
+    const bool done = all_on || (max_steps == num_env_steps);
+    const bool succ = boxes_on_target == num_boxes;  // sokoban/env.py:49
+    o.exec++;
+    o.stepped_any_state = true;
+    o.info = (uint8_t)(RMI_INFO_PRESENT | (moved ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID |
+                       (succ ? RMI_INFO_SUCCESS : 0));
+    succ_last = succ;
+    if (done) {
+      stop = true;
+      turn_done = true;
+    }
+  }
+  return o;
+}
+
+// --------------------------------------------------------------------- exact LDS path
+// One EnvStateManager turn for one Sokoban env on its LDS row: interior players take
+// straight-line index arithmetic, the rest SokobanLdsEnv::step's exact numpy-wrap code.
+__device__ __forceinline__ TurnOut lds_turn(SokobanLdsEnv& e, const ExecList& x, uint8_t& err, bool& turn_done,
+                                            bool& succ_last) {
+  TurnOut o;
+  o.acc = 0.0;
+  o.info = 0;
+  o.exec = 0;
+  o.stepped_any_state = false;
+  const int W = e.W, H = e.H;
+  int p = e.r * W + e.c;
+  bool stop = false;
+  for (int i = 0; i < kMaxK; ++i) {
+    const bool go = i < x.cnt && !stop;
+    if (!__any(go)) break;
+    if (!go) continue;
+    const int a = (int)(int8_t)(uint8_t)(x.run >> (8 * i));
     const int d = (a - 1) & 3;
     const int dr = (d == 1) - (d == 0), dc = (d == 3) - (d == 2);
     const int nr = e.r + dr, nc = e.c + dc, br = nr + dr, bc = nc + dc;
@@ -167,15 +305,10 @@ __device__ __forceinline__ TurnOut sokoban_turn(SokobanLdsEnv& e, uint64_t acts,
         e.n_open += SokobanLdsEnv::open_of(vbn, fb) - SokobanLdsEnv::open_of(vb, fb);
         e.st[bi] = (uint8_t)vbn;
       }
-      const int cur = e.num_boxes - e.n_open;
-      double rw = -0.1;
-      rw += cur > e.boxes_on_target ? 1.0 : (cur < e.boxes_on_target ? -1.0 : 0.0);
-      const bool all_on = e.n_open == 0;
-      rw += all_on ? 10.0 : 0.0;
-      e.boxes_on_target = cur;
-      r = rw;
+      bool all_on;
+      r = step_reward(e.n_open, e.num_boxes, e.boxes_on_target, all_on);
       done = all_on || (e.max_steps == e.num_env_steps);
-      succ = cur == e.num_boxes;
+      succ = e.boxes_on_target == e.num_boxes;
       eff = moved;
     } else if (!e.step(a, r, done, eff, succ)) {  // exact numpy-wrap / error path
       err |= (a < 1 || a > 8) ? RMI_ERR_ACTION : 0;
@@ -194,70 +327,43 @@ __device__ __forceinline__ TurnOut sokoban_turn(SokobanLdsEnv& e, uint64_t acts,
       turn_done = true;
     }
   }
-  num_actions += o.exec;
-  n_turns += 1;
-  if (turn_done) {
-    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_DONE;
-    flags = succ_last ? (uint8_t)(flags & ~RMI_FLAG_TRUNCATED) : (uint8_t)(flags | RMI_FLAG_TRUNCATED);
-  } else if (num_actions >= max_actions) {
-    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
-  }
   return o;
 }
 
-// Stage `nwords` dwords global -> LDS (16 B per lane when both are 16-B aligned).
-__device__ __forceinline__ void stage_in(uint32_t* lds, const uint8_t* g, int nwords, int lane, bool vec) {
-  const uint32_t* g1 = reinterpret_cast<const uint32_t*>(g);
-  int done = 0;
-  if (vec) {
-    const uint4* g4 = reinterpret_cast<const uint4*>(g);
-    uint4* l4 = reinterpret_cast<uint4*>(lds);
-    const int n4 = nwords >> 2;
-#pragma unroll 4
-    for (int i = lane; i < n4; i += kWave) l4[i] = g4[i];
-    done = n4 << 2;
-  }
-  for (int i = done + lane; i < nwords; i += kWave) lds[i] = g1[i];
-}
+constexpr int kMaxWords = kMaxCells / 4;
 
-__device__ __forceinline__ void stage_out(uint8_t* g, const uint32_t* lds, int nwords, int lane, bool vec) {
-  uint32_t* g1 = reinterpret_cast<uint32_t*>(g);
-  int done = 0;
-  if (vec) {
-    uint4* g4 = reinterpret_cast<uint4*>(g);
-    const uint4* l4 = reinterpret_cast<const uint4*>(lds);
-    const int n4 = nwords >> 2;
-#pragma unroll 4
-    for (int i = lane; i < n4; i += kWave) g4[i] = l4[i];
-    done = n4 << 2;
-  }
-  for (int i = done + lane; i < nwords; i += kWave) g1[i] = lds[i];
-}
-
+// One launch = one turn of every env.  Lane = env; each lane loads and stores only its own
+// rows (no barriers): every load of the turn is issued up front (one memory round trip),
+// the rows live in VGPRs as dwords, and a wave of regular rooms steps on bitboards.
 template <int HW>  // H*W for the common sizes (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint8_t* __restrict__ err_out) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds_state[kWave * kMaxCells / 4];
-  __shared__ __attribute__((aligned(16))) uint32_t lds_fixed[kWave * kMaxCells / 4];
+  constexpr int NW = HW ? HW / 4 : kMaxWords;
+  __shared__ uint32_t lds_state[kWave * NW];  // exact path only: lane-private rows
+  __shared__ uint32_t lds_fixed[kWave * NW];
   const int hw = HW ? HW : hw_rt;
   const int row_words = hw >> 2;
   const int B = ep.B;
   const int lane = threadIdx.x;
-  const int64_t b0 = (int64_t)blockIdx.x * kWave;
-  const int64_t b = b0 + lane;
-  const int nb = (int)min<int64_t>(kWave, B - b0);
+  const int64_t b = (int64_t)blockIdx.x * kWave + lane;
   const bool live = b < B;
+  const int H = env.H, W = env.W;
+  RMI_STAMP(0);
 
   // ---- 1. every load of the turn, issued together
-  const uint8_t flags0 = live ? ep.flags[b] : (uint8_t)RMI_FLAG_DONE;
-  const bool act = live && (in.has_input ? (in.has_input[b] != 0) : !(flags0 & RMI_FLAG_DONE));
-  int8_t pr = 0, pc = 0;
-  int32_t nes = 0, bot = 0, num_actions = 0, n_turns = 0, n_act = 0;
+  uint8_t flags = RMI_FLAG_DONE, has_in = 0;
+  int r = 0, c = 0, nes = 0, bot = 0, n_act = 0;
+  int32_t num_actions = 0, n_turns = 0;
   double penalty = 0.0;
   uint64_t acts = 0;
+  uint32_t xs[NW], xf[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) xs[w] = xf[w] = 0;
   if (live) {
-    pr = env.player[2 * b];
-    pc = env.player[2 * b + 1];
+    flags = ep.flags[b];
+    if (in.has_input) has_in = in.has_input[b];
+    r = env.player[2 * b];
+    c = env.player[2 * b + 1];
     nes = env.num_env_steps[b];
     bot = env.boxes_on_target[b];
     num_actions = ep.num_actions[b];
@@ -265,48 +371,117 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     penalty = ep.penalty[b];
     n_act = in.n_actions[b];
     acts = load_actions(in.actions + b * (int64_t)in.K, in.K);
-  }
-  const int nwords = nb * row_words;
-  uint8_t* gstate = env.room_state + b0 * hw;
-  const uint8_t* gfixed = env.room_fixed + b0 * hw;
-  const bool vec = ((reinterpret_cast<uintptr_t>(gstate) | reinterpret_cast<uintptr_t>(gfixed)) & 15u) == 0;
-  stage_in(lds_state, gstate, nwords, lane, vec);
-  stage_in(lds_fixed, gfixed, nwords, lane, vec);
-  __syncthreads();
-
-  // ---- 2-3. the turn
-  bool changed = false;
-  if (act) {
-    SokobanLdsEnv e;
-    e.st = reinterpret_cast<uint8_t*>(lds_state) + lane * hw;
-    e.fx = reinterpret_cast<const uint8_t*>(lds_fixed) + lane * hw;
-    e.H = env.H;
-    e.W = env.W;
-    e.err = 0;
-    // open targets of _calc_reward, SWAR over the row's dwords
-    const uint32_t* ws = lds_state + lane * row_words;
-    const uint32_t* wf = lds_fixed + lane * row_words;
-    int n_open = 0;
+    const uint32_t* gs = reinterpret_cast<const uint32_t*>(env.room_state + b * hw);
+    const uint32_t* gf = reinterpret_cast<const uint32_t*>(env.room_fixed + b * hw);
 #pragma unroll
-    for (int w = 0; w < kMaxCells / 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       if (w < row_words) {
-        const uint32_t xs = ws[w], xf = wf[w];
-        n_open += __popc(eq_bytes(xs, 2u) | (eq_bytes(xs, 5u) & eq_bytes(xf, 2u)));
+        xs[w] = gs[w];
+        xf[w] = gf[w];
       }
     }
-    e.n_open = n_open;
-    e.r = pr;
-    e.c = pc;
-    e.num_env_steps = nes;
-    e.boxes_on_target = bot;
-    e.num_boxes = env.num_boxes;
-    e.max_steps = env.max_steps;
+  }
+  const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
 
-    uint8_t err = 0, flags = flags0;
-    TurnOut o = sokoban_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
-                             in.format_penalty, err);
-    err |= e.err;
-    changed = o.stepped_any_state;
+  // ---- 2. exec list and the regular-room test
+  ExecList x;
+  x.run = 0;
+  x.cnt = 0;
+  uint64_t wall = 0, target = 0, box = 0;
+  bool regular = true;
+  if (act) {
+    flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (:168)
+    x = exec_list(acts, n_act, in.K, in.max_actions_per_traj - num_actions, penalty, in.format_penalty);
+    uint64_t player;
+    const bool consistent = decode_board<NW>(xs, xf, row_words, wall, target, box, player);
+    uint64_t border = 0;  // wave-uniform
+    const uint64_t row_mask = W >= 64 ? ~0ull : (1ull << W) - 1;
+    for (int rr = 0; rr < H; ++rr)
+      border |= (rr == 0 || rr == H - 1) ? row_mask << (rr * W) : (1ull << (rr * W)) | (1ull << (rr * W + W - 1));
+    bool acts_ok = true;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) {
+      const uint32_t a = (uint32_t)(x.run >> (8 * k)) & 0xFFu;
+      acts_ok &= k >= x.cnt || a <= 8u;
+    }
+    const bool interior = r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2;
+    regular = consistent && acts_ok && interior && (border & ~wall) == 0 &&
+              player == (interior ? 1ull << (r * W + c) : 0ull);
+  }
+  RMI_STAMP(1);
+
+  // ---- 3. the turn
+  TurnOut o;
+  o.acc = 0.0;
+  o.info = 0;
+  o.exec = 0;
+  o.stepped_any_state = false;
+  bool turn_done = false, succ_last = false, row_changed = false;
+  uint8_t err = 0;
+  if (__all(regular)) {
+    if (act) {
+      o = board_turn(wall, target, box, r, c, W, hw, nes, bot, env.num_boxes, env.max_steps, x, turn_done,
+                     succ_last, row_changed);
+      if (row_changed) {  // rebuild the state row: fixed, boxes 3/4, player 5
+        const int p = r * W + c;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          if (w < row_words) {
+            const uint32_t f = xf[w], bm = unnib((uint32_t)(box >> (4 * w)) & 0xFu);
+            uint32_t v = (f & ~bm) | ((0x05050505u - f) & bm);  // 5 - fixed: 3 on target, 4 on floor
+            const int sh = 8 * (p - 4 * w);
+            v = (p >> 2) == w ? ((v & ~(0xFFu << sh)) | (5u << sh)) : v;
+            xs[w] = v;
+          }
+        }
+      }
+    }
+  } else {
+    // rare: some room of the wave is irregular -> the exact path on lane-private LDS rows
+    uint32_t* ls = lds_state + lane * row_words;
+    uint32_t* lf = lds_fixed + lane * row_words;
+    if (act) {
+      int n_open = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        if (w < row_words) {
+          ls[w] = xs[w];
+          lf[w] = xf[w];
+          n_open += __popc(eq_bytes(xs[w], 2u) | (eq_bytes(xs[w], 5u) & eq_bytes(xf[w], 2u)));
+        }
+      }
+      SokobanLdsEnv e;
+      e.st = reinterpret_cast<uint8_t*>(ls);
+      e.fx = reinterpret_cast<const uint8_t*>(lf);
+      e.H = H;
+      e.W = W;
+      e.r = r;
+      e.c = c;
+      e.num_env_steps = nes;
+      e.boxes_on_target = bot;
+      e.num_boxes = env.num_boxes;
+      e.max_steps = env.max_steps;
+      e.n_open = n_open;
+      e.err = 0;
+      o = lds_turn(e, x, err, turn_done, succ_last);
+      err |= e.err;
+      r = e.r;
+      c = e.c;
+      nes = e.num_env_steps;
+      bot = e.boxes_on_target;
+      row_changed = o.stepped_any_state;
+      if (row_changed) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+          if (w < row_words) xs[w] = ls[w];
+      }
+    }
+  }
+  RMI_STAMP(2);
+
+  // ---- 4. outputs
+  if (act) {
+    finish_turn(o, turn_done, succ_last, num_actions, flags, n_turns, in.max_actions_per_traj);
     ep.num_actions[b] = num_actions;
     ep.flags[b] = flags;
     ep.n_turns[b] = n_turns;
@@ -315,17 +490,21 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     ep.turn_reward[tb] = o.acc;
     ep.turn_info[tb] = o.info;
     ep.turn_exec[tb] = o.exec;
-    if (changed) {
-      env.player[2 * b] = (int8_t)e.r;
-      env.player[2 * b + 1] = (int8_t)e.c;
-      env.num_env_steps[b] = e.num_env_steps;
-      env.boxes_on_target[b] = e.boxes_on_target;
+    if (o.stepped_any_state) {
+      env.player[2 * b] = (int8_t)r;
+      env.player[2 * b + 1] = (int8_t)c;
+      env.num_env_steps[b] = nes;
+      env.boxes_on_target[b] = bot;
+    }
+    if (row_changed) {
+      uint32_t* gs = reinterpret_cast<uint32_t*>(env.room_state + b * hw);
+#pragma unroll
+      for (int w = 0; w < NW; ++w)
+        if (w < row_words) gs[w] = xs[w];
     }
     if (err_out && err) err_out[b] |= err;
   }
-  // ---- 4. rows back (only if some env of the wave changed)
-  if (!__syncthreads_or(changed)) return;
-  stage_out(gstate, lds_state, nwords, lane, vec);
+  RMI_STAMP(3);
 }
 
 // Fused reset: room_state/player from the generated rooms, counters and the whole episode

@@ -310,3 +310,75 @@ def test_fused_reset_and_finalize(device):
         assert torch.equal(sc, s2) and torch.equal(pe, p2)
         assert torch.equal(torch.nan_to_num(met, 7.0), torch.nan_to_num(ops.rollout_metrics(env.ep), 7.0))
         assert torch.equal(norm, ops.group_normalize(s2, p2, seg, method))
+
+
+def _irregular_rooms(rng, B, H, W, fixed, state, player):
+    """Overwrite some rooms with hand-made ones the generator never makes: open borders, a
+    player on / outside the border (numpy wrap and IndexError), inconsistent state bytes."""
+    hw = H * W
+    kind = rng.integers(0, 4, size=B)
+    for i in np.nonzero(kind == 0)[0]:          # random grids, anything goes
+        f = rng.choice([0, 1, 2], size=hw, p=[0.3, 0.5, 0.2]).astype(np.uint8)
+        s = f.copy()
+        m = rng.random(hw) < 0.2
+        s[m] = rng.choice([3, 4], size=int(m.sum()))
+        fixed[i], state[i] = f, s
+        player[i] = rng.integers(-H - 1, H + 1, size=2)
+    for i in np.nonzero(kind == 1)[0]:          # regular room, player moved onto the border
+        r, c = (0, int(rng.integers(0, W))) if rng.random() < 0.5 else (int(rng.integers(0, H)), W - 1)
+        fixed[i].reshape(H, W)[r, c] = 1
+        state[i].reshape(H, W)[r, c] = 5
+        state[i][state[i] == 5] = fixed[i][state[i] == 5]
+        state[i].reshape(H, W)[r, c] = 5
+        player[i] = (r, c)
+    for i in np.nonzero(kind == 2)[0]:          # one inconsistent byte
+        state[i][int(rng.integers(0, hw))] = int(rng.integers(0, 6))
+
+
+@pytest.mark.parametrize("frac_irregular", [0.0, 0.01, 0.5])
+def test_sokoban_irregular_rooms_vs_oracle(device, frac_irregular):
+    """Waves mixing regular (bitboard path) and irregular rooms (exact LDS path), invalid and
+    out-of-range action ids: kernel == oracle on every env the reference would not raise on,
+    and the same error flags where it would."""
+    rng = np.random.default_rng(int(frac_irregular * 1000) + 5)
+    B, T, K, H, W = 2048, 4, 6, 6, 6
+    env = SokobanBatch(SokobanEnvConfig(dim_x=H, dim_y=W, num_boxes=1, max_steps=12), B, T, K, device)
+    env.reset(synthetic.env_seeds(B))
+    fixed = env.room_fixed.cpu().numpy().copy()
+    state = env.room_state.cpu().numpy().copy()
+    player = env.player.cpu().numpy().copy()
+    sel = rng.random(B) < frac_irregular
+    idx = np.nonzero(sel)[0]
+    f2, s2, p2 = fixed[idx].copy(), state[idx].copy(), player[idx].copy()
+    _irregular_rooms(rng, len(idx), H, W, f2, s2, p2)
+    fixed[idx], state[idx], player[idx] = f2, s2, p2
+    env.load_state(fixed, state, player)
+    nes = np.zeros(B, np.int32)
+    bot = np.zeros(B, np.int32)
+    oep = oracle.Episode(B, T)
+    bad = np.zeros(B, bool)
+    for t in range(T):
+        ids = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, -1], size=(B, K),
+                         p=[0.05] + [0.11] * 8 + [0.03, 0.04]).astype(np.int8)
+        if frac_irregular == 0.0:
+            ids = np.clip(ids, 1, 8).astype(np.int8)
+        n = rng.integers(0, K + 1, size=B).astype(np.uint8)
+        err = torch.zeros(B, dtype=torch.uint8, device=device)
+        env.step_turn(t, _t(ids, device), _t(n, device), None, 9, -0.1, err)
+        oerr = oracle.sokoban_turn(H, W, 1, 12, fixed, state, player, nes, bot, oep, t, ids, n, None, 9, -0.1)
+        torch.cuda.synchronize()
+        kerr = err.cpu().numpy()
+        np.testing.assert_array_equal(kerr != 0, oerr != 0)
+        bad |= oerr != 0
+        ok = ~bad
+        np.testing.assert_array_equal(env.room_state.cpu().numpy()[ok], state[ok])
+        np.testing.assert_array_equal(env.player.cpu().numpy()[ok], player[ok])
+        np.testing.assert_array_equal(env.num_env_steps.cpu().numpy()[ok], nes[ok])
+        np.testing.assert_array_equal(env.boxes_on_target.cpu().numpy()[ok], bot[ok])
+        h = _host_ep(env.ep)
+        for k in ("num_actions", "flags", "n_turns", "penalty"):
+            np.testing.assert_array_equal(h[k][ok], getattr(oep, k)[ok], err_msg=k)
+        for k in ("turn_reward", "turn_info", "turn_exec"):
+            np.testing.assert_array_equal(h[k][:, ok], getattr(oep, k)[:, ok], err_msg=k)
+    if frac_irregular == 0.0:
+        assert not bad.any()
