@@ -15,11 +15,14 @@ Multi-GPU: weak scaling — every rank runs its own 8192 envs (global group ids 
 rank r seeds groups r*512..), no collective on the data path; value = all ranks' env steps
 / max-over-ranks time.
 
-Also reported: roofline of the dominant kernel (rmi_sokoban_step_turn) from HIP events,
-PMC HBM traffic from the committed rocprofv3 pass (profiles/), and the CPU baseline (the
-oracle's per-env Python port of the reference path, timed on this host).
+Also reported: roofline of the dominant kernel (rmi_sokoban_step_turn) — algorithmic bytes
+(141 B per active env-turn) over the average launch duration measured with HIP
+events around back-to-back launches — PMC HBM traffic per launch from the committed
+rocprofv3 pass (profiles/), and the CPU baseline (the oracle's per-env Python port of the
+reference path, timed on this host).
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -42,7 +45,7 @@ MAX_ACTIONS = 10
 GROUP = 16
 BYTES_PER_ENV_TURN = 141  # algorithmic bytes per Sokoban env-turn
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured copy)
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_sokoban_step_turn.json")
+PMC_GLOB = os.path.join(ROOT, "profiles", "r*_pmc_sokoban_step_turn.json")  # latest round's PMC pass
 
 
 class Rollout:
@@ -63,18 +66,26 @@ class Rollout:
         self.turns = [ops.turn_struct(t, self.ids[t], self.n[t], None, MAX_ACTIONS, -0.1) for t in range(T_TURNS)]
         self.st = e.struct()
 
-    def step(self, events=None):
-        """One rollout phase.  events: optional list collecting (start, end) per turn kernel."""
+    def step(self):
+        """One rollout phase: restore, T turn launches, fused finalize."""
         self.env.restore()
         for t in range(T_TURNS):
-            if events is not None:
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
             ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
-            if events is not None:
-                b.record()
-                events.append((a, b))
         ops.rollout_finalize(self.env.ep, self.seg, "identity", self.norm, metrics=self.metrics)
+
+    def timed_turns(self):
+        """One rollout phase with HIP events (on the launch stream) around its T back-to-back
+        turn launches.  A spin kernel queued first keeps the GPU busy while the host enqueues,
+        so no host gap falls inside the bracket.  -> (start, end) events."""
+        torch.cuda._sleep(2_000_000)
+        self.env.restore()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for t in range(T_TURNS):
+            ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
+        b.record()
+        ops.rollout_finalize(self.env.ep, self.seg, "identity", self.norm, metrics=self.metrics)
+        return a, b
 
 
 def cpu_baseline(R, seconds_budget=20.0):
@@ -168,19 +179,18 @@ def main():
         tdist.all_reduce(c)
         total_steps = int(c.item())
 
-    # ---- dominant-kernel roofline: HIP events around every turn launch (eager, same stream)
-    events = []
+    # ---- dominant-kernel roofline: HIP events around the turn launches (eager, same stream)
     n_prof = min(args.steps, 50)
-    for _ in range(n_prof):
-        R.step(events)
+    events = [R.timed_turns() for _ in range(n_prof)]
     torch.cuda.synchronize()
-    durs = np.array([a.elapsed_time(b) for a, b in events]).reshape(n_prof, T_TURNS) * 1e-3  # s
-    bytes_per_launch = np.array(active_per_turn, np.float64) * BYTES_PER_ENV_TURN
-    achieved = float(bytes_per_launch.sum() * n_prof / durs.sum()) / 1e9  # GB/s
-    avg_launch_us = float(durs.mean() * 1e6)
+    durs = np.array([a.elapsed_time(b) for a, b in events]) * 1e-3  # s per rollout's T launches
+    bytes_per_rollout = float(np.sum(active_per_turn)) * BYTES_PER_ENV_TURN
+    achieved = bytes_per_rollout * n_prof / float(durs.sum()) / 1e9  # GB/s
+    avg_launch_us = float(durs.mean() / T_TURNS * 1e6)
     traffic = None
-    if os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
+    pmc = sorted(glob.glob(PMC_GLOB))
+    if pmc:
+        with open(pmc[-1]) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     # eager (no graph) rate, for reference

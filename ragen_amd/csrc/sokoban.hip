@@ -32,10 +32,16 @@ __device__ unsigned long long* g_stamps;
       g_stamps[blockIdx.x * 16 + 2 * (i) + 1] = __builtin_amdgcn_s_memrealtime();      \
     }                                                                                  \
   } while (0)
+#define RMI_STAMP_WAIT(i)          \
+  do {                             \
+    __builtin_amdgcn_s_waitcnt(0); \
+    RMI_STAMP(i);                  \
+  } while (0)
 #else
 #define RMI_STAMP(i) \
   do {               \
   } while (0)
+#define RMI_STAMP_WAIT(i) RMI_STAMP(i)
 #endif
 
 constexpr int kWave = 64;
@@ -115,28 +121,22 @@ struct SokobanLdsEnv {
 };
 
 // valid = [ids of known names], exec list = valid[:left] (es_manager.py:156-157), packed one
-// byte per action; format penalty if len(valid) != len(actions) or nothing valid (:158-159).
+// byte per action (exact LDS path).
 struct ExecList {
   uint64_t run;
   int cnt;
 };
-__device__ __forceinline__ ExecList exec_list(uint64_t acts, int n_act, int K, int left, double& penalty,
-                                              double format_penalty) {
-  if (n_act > K) n_act = K;
+__device__ __forceinline__ ExecList exec_list(uint64_t acts, int n_act, int left) {  // n_act <= K
   ExecList x;
   x.run = 0;
   x.cnt = 0;
-  int nv = 0;
 #pragma unroll
   for (int k = 0; k < kMaxK; ++k) {
     const uint32_t a = (uint32_t)(acts >> (8 * k)) & 0xFFu;
-    const bool valid = k < n_act && a != 0;
-    const bool take = valid && x.cnt < left;
+    const bool take = k < n_act && a != 0 && x.cnt < left;
     x.run |= take ? ((uint64_t)a << (8 * x.cnt)) : 0ull;
     x.cnt += take;
-    nv += valid;
   }
-  if (nv != n_act || nv == 0) penalty += format_penalty;
   return x;
 }
 
@@ -169,87 +169,174 @@ __device__ __forceinline__ double step_reward(int n_open, int num_boxes, int& bo
 // (every state byte equals the fixed byte, except boxes = 3 on a target / 4 on floor and the
 // player's 5 on a non-wall cell), room_fixed holds only {0,1,2}, its whole border is wall and
 // the player is interior.  Every generated room is regular and gym_sokoban's writes keep it
-// so.  For a regular room H*W <= 64 cells fit a u64 per class (cell i = bit i, row-major),
-// a step is a handful of register bit operations with no memory access, and numpy's
-// negative-index wrap can never trigger (the player never reaches the border).  Anything
-// else takes the exact LDS path (SokobanLdsEnv::step).
+// so.  A regular room steps on bitboards held in registers — a handful of bit operations
+// per action, no memory access — and numpy's negative-index wrap can never trigger (the
+// player never reaches the border).  Anything else takes the exact LDS path.
+//
+// Board window: bit j = cell W + j (row 0, all wall, is left out), so a 6x6 room's rows
+// 1..5 fit a u32 (an 8x8 one a u64).  The only cells a step can address outside the window
+// are row-0 cells (j in [1-W, -1]); shift amounts are taken mod the word size, which aliases
+// them onto the top bits — the bottom border row and the padding above it, all wall.  So the
+// hot loop needs no range test at all.  Requires (H-1)*W <= bits of the word type.
 
-// high bit of each selected byte of a dword -> 4-bit nibble (byte j -> bit j)
-__device__ __forceinline__ uint32_t nib(uint32_t m) { return (((m >> 7) * 0x01020408u) >> 24) & 0xFu; }
+__device__ __forceinline__ uint32_t nonzero_bytes(uint32_t y) {  // high bit of each byte != 0
+  return (((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t gt8_bytes(uint32_t y) {  // high bit of each byte > 8
+  return (y | ((y & 0x7F7F7F7Fu) + 0x77777777u)) & 0x80808080u;
+}
+// bit 0 of each byte of a dword -> 4-bit nibble (byte j -> bit j); exact, no carries.
+// (One multiply beats the 5-instruction shift/or gather on a latency-bound lone wave.)
+__device__ __forceinline__ uint32_t nib(uint32_t x) { return (x * 0x01020408u) >> 24; }
+// 0/1 per byte -> 0x00/0xFF per byte
+__device__ __forceinline__ uint32_t byte_mask(uint32_t x) { return (x << 8) - x; }
 // 4-bit nibble -> byte mask (bit j -> byte j = 0xFF)
-__device__ __forceinline__ uint32_t unnib(uint32_t n) { return ((n * 0x00204081u) & 0x01010101u) * 0xFFu; }
+__device__ __forceinline__ uint32_t unnib(uint32_t n) { return byte_mask((n * 0x00204081u) & 0x01010101u); }
 
+// Bitboards (cell i = bit i, row-major) of one row pair, and whether the room is consistent:
+// fixed bytes in {0,1,2}, and the state row equals its rebuild from (fixed, boxes, player p).
 template <int NW>
-__device__ __forceinline__ bool decode_board(const uint32_t (&xs)[NW], const uint32_t (&xf)[NW], int row_words,
-                                             uint64_t& wall, uint64_t& target, uint64_t& box, uint64_t& player) {
-  uint32_t bad = 0;
-  wall = target = box = player = 0;
+__device__ __forceinline__ bool decode_rows(const uint32_t (&xs)[NW], const uint32_t (&xf)[NW], int row_words, int p,
+                                            uint64_t& wall, uint64_t& target, uint64_t& box) {
+  constexpr uint32_t L = 0x01010101u;
+  const int pw = p >> 2;
+  const uint32_t pmask = 0xFFu << (8 * (p & 3)), p5 = 5u << (8 * (p & 3));
+  uint32_t bad = 0, wl = 0, wh = 0, tl = 0, th = 0, bl = 0, bh = 0;
 #pragma unroll
   for (int w = 0; w < NW; ++w) {
     if (w < row_words) {
-      const uint32_t s = xs[w], f = xf[w];
-      const uint32_t f0 = zero_bytes(f), f1 = eq_bytes(f, 1u), f2 = eq_bytes(f, 2u);
-      const uint32_t s3 = eq_bytes(s, 3u), s4 = eq_bytes(s, 4u), s5 = eq_bytes(s, 5u);
-      bad |= ~(f0 | f1 | f2) & 0x80808080u;                                         // fixed in {0,1,2}
-      bad |= ~(zero_bytes(s ^ f) | (s3 & f2) | (s4 & f1) | s5) & 0x80808080u;  // state consistent
-      wall |= (uint64_t)nib(f0) << (4 * w);
-      target |= (uint64_t)nib(f2) << (4 * w);
-      box |= (uint64_t)nib(s3 | s4) << (4 * w);
-      player |= (uint64_t)nib(s5) << (4 * w);
+      const uint32_t f = xf[w], s = xs[w];
+      const uint32_t f1 = f >> 1, s1 = s >> 1, s2 = s >> 2;
+      bad |= (f & 0xFCFCFCFCu) | (f & f1 & L);           // fixed byte in {0, 1, 2}
+      const uint32_t fw = ~(f | f1) & L;                   // fixed == 0 (wall)
+      const uint32_t ft = f1 & L;                          // fixed == 2 (target)
+      const uint32_t bx = ((s & s1 & ~s2) | (s2 & ~s1 & ~s)) & L;  // low bits 011 / 100: 3 or 4
+      const uint32_t bm = byte_mask(bx);
+      uint32_t reb = (f & ~bm) | ((0x05050505u - f) & bm);  // boxes: 5 - fixed = 3 on target, 4 on floor
+      reb = w == pw ? ((reb & ~pmask) | p5) : reb;           // the player's 5
+      bad |= reb ^ s;
+      const uint32_t nw_ = nib(fw), nt = nib(ft), nb = nib(bx);
+      if (w < 8) {
+        wl |= nw_ << (4 * w);
+        tl |= nt << (4 * w);
+        bl |= nb << (4 * w);
+      } else {
+        wh |= nw_ << (4 * (w - 8));
+        th |= nt << (4 * (w - 8));
+        bh |= nb << (4 * (w - 8));
+      }
     }
   }
+  wall = ((uint64_t)wh << 32) | wl;
+  target = ((uint64_t)th << 32) | tl;
+  box = ((uint64_t)bh << 32) | bl;
   return bad == 0;
 }
 
-// One EnvStateManager turn of one regular room on bitboards; bit-identical to the LDS path.
-__device__ __forceinline__ TurnOut board_turn(uint64_t wall, uint64_t target, uint64_t& box, int& r, int& c, int W,
-                                              int hw, int& num_env_steps, int& boxes_on_target, int num_boxes,
-                                              int max_steps, const ExecList& x, bool& turn_done, bool& succ_last,
-                                              bool& moved_any) {
-  TurnOut o;
-  o.acc = 0.0;
-  o.info = 0;
-  o.exec = 0;
-  o.stepped_any_state = false;
-  int p = r * W + c;
-  bool stop = false;
-  for (int i = 0; i < kMaxK; ++i) {
-    const bool go = i < x.cnt && !stop;
-    if (!__any(go)) break;  // wave-uniform trip count
-    if (!go) continue;
-    const int a = (int)(x.run >> (8 * i)) & 0xFF;  // 1..8, checked by the caller
-    const int d = (a - 1) & 3;                      // CHANGE_COORDINATES[(a-1) % 4]
-    const int dr = (d == 1) - (d == 0), dc = (d == 3) - (d == 2);
-    const int s = dr * W + dc;
-    const int n = p + s, bb = n + s;  // n is always inside: the player is interior
-    const uint64_t nbit = 1ull << n;
-    const bool n_wall = (wall & nbit) != 0, n_box = (box & nbit) != 0;
-    const bool bb_in = (unsigned)bb < (unsigned)hw;  // outside only when n is border wall
-    const uint64_t bbit = bb_in ? 1ull << bb : 0ull;
-    const bool b_free = bb_in && ((wall | box) & bbit) == 0;  // state[bb] in {1, 2}
-    const bool is_push = a <= 4 && n_box && b_free;           // _push
-    const bool moved = is_push || (!n_wall && !n_box);        // _push falls back to _move
-    box ^= is_push ? (nbit | bbit) : 0ull;
-    p = moved ? n : p;
-    r += moved ? dr : 0;
-    c += moved ? dc : 0;
-    moved_any |= moved;
-    num_env_steps += 1;
-    bool all_on;
-    const int n_open = __popcll(target & ~box);  // (state == 2) | ((fixed == 2) & (state == 5))
-    o.acc += step_reward(n_open, num_boxes, boxes_on_target, all_on);
-    const bool done = all_on || (max_steps == num_env_steps);
-    const bool succ = boxes_on_target == num_boxes;  // sokoban/env.py:49
-    o.exec++;
-    o.stepped_any_state = true;
-    o.info = (uint8_t)(RMI_INFO_PRESENT | (moved ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID |
-                       (succ ? RMI_INFO_SUCCESS : 0));
-    succ_last = succ;
-    if (done) {
-      stop = true;
-      turn_done = true;
-    }
+template <class M>
+struct WordBits;
+template <>
+struct WordBits<uint32_t> {
+  static constexpr int kBits = 32;
+  __device__ __forceinline__ static int popc(uint32_t x) { return __popc(x); }
+};
+template <>
+struct WordBits<uint64_t> {
+  static constexpr int kBits = 64;
+  __device__ __forceinline__ static int popc(uint64_t x) { return __popcll(x); }
+};
+
+// One EnvStateManager turn (es_manager.py:149-169) of one regular room on window bitboards,
+// straight-line and predicated: action slot k runs iff it is a known name (id != 0), the
+// turn has not hit done and fewer than `left` actions ran (valid[:left]).  K (slots per
+// turn) is a template parameter so the K steps unroll into one branch-free block the
+// compiler can interleave (a lone wave is latency-bound: ILP is what shortens it).
+// Bit-identical to the LDS path.
+struct BoardTurn {
+  double acc;
+  uint32_t info, taken, stop, succ, moved;
+  int nes, bot;
+};
+template <class M, int K>
+__device__ __forceinline__ BoardTurn board_turn_k(M wall, M target, M& box, int& jp, int W, uint64_t acts, int n_act,
+                                                  int left, int nes, int bot, int num_boxes, int max_steps) {
+  constexpr int kMask = WordBits<M>::kBits - 1;
+  BoardTurn t;
+  t.acc = 0.0;
+  t.info = t.taken = t.stop = t.succ = t.moved = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int a = (int)(acts >> (8 * k)) & 0xFF;  // 1..8 when valid (checked by the caller)
+    const uint32_t go = (t.stop == 0) & (k < n_act) & ((int)t.taken < left) & (a != 0);
+    const int dir = (a - 1) & 3;  // CHANGE_COORDINATES[(a-1) % 4]: up down left right
+    const int mag = (dir & 2) ? 1 : W;
+    const int s = (dir & 1) ? mag : -mag;
+    const int jn = jp + s, jb = jn + s;
+    const M nb = (M)1 << (jn & kMask), bb = (M)1 << (jb & kMask);
+    const M occ = wall | box;
+    const uint32_t n_box = (box & nb) != 0;
+    const uint32_t n_free = (occ & nb) == 0;                             // state[new] in {1, 2}
+    const uint32_t is_push = go & (a <= 4) & n_box & ((occ & bb) == 0);  // _push; state[new_box] in {1, 2}
+    const uint32_t moved = go & (is_push | n_free);                      // _push falls back to _move
+    box ^= is_push ? (nb | bb) : (M)0;
+    jp = moved ? jn : jp;
+    // _calc_reward: open targets = (state == 2) | ((fixed == 2) & (state == 5)) = targets without a box
+    const int n_open = WordBits<M>::popc(target & ~box);
+    const int cur = num_boxes - n_open;
+    const double d_box = cur > bot ? 1.0 : (cur < bot ? -1.0 : 0.0);
+    const uint32_t all_on = n_open == 0;
+    const double rw = (-0.1 + d_box) + (all_on ? 10.0 : 0.0);  // penalty_for_step, box on/off, finished
+    const int nes1 = nes + 1;
+    const uint32_t done = all_on | (max_steps == nes1);
+    const uint32_t succ = cur == num_boxes;  // sokoban/env.py:49
+    nes = go ? nes1 : nes;
+    bot = go ? cur : bot;
+    t.acc += go ? rw : 0.0;  // acc is never -0.0, so + 0.0 is an exact identity
+    t.info = go ? (RMI_INFO_PRESENT | RMI_INFO_VALID | (moved << 1) | (succ << 3)) : t.info;
+    t.succ = go ? succ : t.succ;
+    t.moved |= moved;
+    t.taken += go;
+    t.stop |= go & done;
   }
+  t.nes = nes;
+  t.bot = bot;
+  return t;
+}
+
+template <class M>
+__device__ __forceinline__ TurnOut board_turn(M wall, M target, M& box, int& jp, int W, uint64_t acts, int K, int n_act,
+                                              int left, int& num_env_steps, int& boxes_on_target, int num_boxes,
+                                              int max_steps, bool& turn_done, bool& succ_last, bool& moved_any) {
+  BoardTurn t;
+#define RMI_BOARD_K(k_)                                                                                           \
+  case k_:                                                                                                      \
+    t = board_turn_k<M, k_>(wall, target, box, jp, W, acts, n_act, left, num_env_steps, boxes_on_target, num_boxes, \
+                            max_steps);                                                                         \
+    break;
+  switch (K) {  // wave-uniform
+    RMI_BOARD_K(1)
+    RMI_BOARD_K(2)
+    RMI_BOARD_K(3)
+    RMI_BOARD_K(4)
+    RMI_BOARD_K(5)
+    RMI_BOARD_K(6)
+    RMI_BOARD_K(7)
+    RMI_BOARD_K(8)
+    default:  // K == 0: no action slots
+      t = board_turn_k<M, 0>(wall, target, box, jp, W, acts, n_act, left, num_env_steps, boxes_on_target, num_boxes,
+                             max_steps);
+  }
+#undef RMI_BOARD_K
+  TurnOut o;
+  o.acc = t.acc;
+  o.info = (uint8_t)t.info;
+  o.exec = (uint8_t)t.taken;
+  o.stepped_any_state = t.taken > 0;
+  num_env_steps = t.nes;
+  boxes_on_target = t.bot;
+  turn_done = t.stop != 0;
+  succ_last = t.succ != 0;
+  moved_any = t.moved != 0;
   return o;
 }
 
@@ -334,10 +421,12 @@ constexpr int kMaxWords = kMaxCells / 4;
 
 // One launch = one turn of every env.  Lane = env; each lane loads and stores only its own
 // rows (no barriers): every load of the turn is issued up front (one memory round trip),
-// the rows live in VGPRs as dwords, and a wave of regular rooms steps on bitboards.
-template <int HW>  // H*W for the common sizes (0 = runtime); H*W % 4 == 0
+// the rows live in VGPRs as dwords, and a wave of regular rooms steps on bitboards of word
+// type M.  `border` = bitmask of the border cells (row-major), precomputed by the launcher.
+template <int HW, class M>  // HW = H*W for the common sizes (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
-                                                                  int hw_rt, uint8_t* __restrict__ err_out) {
+                                                                  int hw_rt, uint64_t border,
+                                                                  uint8_t* __restrict__ err_out) {
   constexpr int NW = HW ? HW / 4 : kMaxWords;
   __shared__ uint32_t lds_state[kWave * NW];  // exact path only: lane-private rows
   __shared__ uint32_t lds_fixed[kWave * NW];
@@ -382,33 +471,38 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     }
   }
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
+  RMI_STAMP_WAIT(1);
 
-  // ---- 2. exec list and the regular-room test
-  ExecList x;
-  x.run = 0;
-  x.cnt = 0;
-  uint64_t wall = 0, target = 0, box = 0;
+  // ---- 2. format penalty and the regular-room test
+  if (n_act > in.K) n_act = in.K;
+  const int left = in.max_actions_per_traj - num_actions;
   bool regular = true;
+  M wall = 0, target = 0, box = 0;
+  int jp = 0;
   if (act) {
     flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (:168)
-    x = exec_list(acts, n_act, in.K, in.max_actions_per_traj - num_actions, penalty, in.format_penalty);
-    uint64_t player;
-    const bool consistent = decode_board<NW>(xs, xf, row_words, wall, target, box, player);
-    uint64_t border = 0;  // wave-uniform
-    const uint64_t row_mask = W >= 64 ? ~0ull : (1ull << W) - 1;
-    for (int rr = 0; rr < H; ++rr)
-      border |= (rr == 0 || rr == H - 1) ? row_mask << (rr * W) : (1ull << (rr * W)) | (1ull << (rr * W + W - 1));
-    bool acts_ok = true;
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k) {
-      const uint32_t a = (uint32_t)(x.run >> (8 * k)) & 0xFFu;
-      acts_ok &= k >= x.cnt || a <= 8u;
-    }
+    // valid = action slots < n_act holding a known name (id != 0)  (es_manager.py:156, :239)
+    const uint64_t slots = n_act >= 8 ? ~0ull : (1ull << (8 * n_act)) - 1;
+    const uint32_t sl = (uint32_t)slots, sh = (uint32_t)(slots >> 32);
+    const uint32_t al = (uint32_t)acts, ah = (uint32_t)(acts >> 32);
+    const uint32_t vl = nonzero_bytes(al) & sl, vh = nonzero_bytes(ah) & sh;
+    const int nv = __popc(vl) + __popc(vh);
+    if (nv != n_act || nv == 0) penalty += in.format_penalty;  // :158-159
+    const bool acts_ok = ((gt8_bytes(al) & vl) | (gt8_bytes(ah) & vh)) == 0;
     const bool interior = r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2;
-    regular = consistent && acts_ok && interior && (border & ~wall) == 0 &&
-              player == (interior ? 1ull << (r * W + c) : 0ull);
+    const int p = interior ? r * W + c : 0;
+    uint64_t wall64, target64, box64;
+    const bool consistent = decode_rows<NW>(xs, xf, row_words, p, wall64, target64, box64);
+    regular = consistent && acts_ok && interior && (border & ~wall64) == 0 && ((wall64 >> p) & 1) == 0;
+    // window: bit j = cell W + j; the cells past row H-1 are padding walls
+    const int used = (H - 1) * W;
+    const M pad = used >= WordBits<M>::kBits ? (M)0 : ~(((M)1 << used) - 1);
+    wall = (M)(wall64 >> W) | pad;
+    target = (M)(target64 >> W);
+    box = (M)(box64 >> W);
+    jp = p - W;
   }
-  RMI_STAMP(1);
+  RMI_STAMP(2);
 
   // ---- 3. the turn
   TurnOut o;
@@ -420,15 +514,18 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   uint8_t err = 0;
   if (__all(regular)) {
     if (act) {
-      o = board_turn(wall, target, box, r, c, W, hw, nes, bot, env.num_boxes, env.max_steps, x, turn_done,
-                     succ_last, row_changed);
+      o = board_turn<M>(wall, target, box, jp, W, acts, in.K, n_act, left, nes, bot, env.num_boxes, env.max_steps,
+                        turn_done, succ_last, row_changed);
       if (row_changed) {  // rebuild the state row: fixed, boxes 3/4, player 5
-        const int p = r * W + c;
+        const int p = jp + W;
+        r = p / W;
+        c = p - r * W;
+        const uint64_t box64 = (uint64_t)box << W;
 #pragma unroll
         for (int w = 0; w < NW; ++w) {
           if (w < row_words) {
-            const uint32_t f = xf[w], bm = unnib((uint32_t)(box >> (4 * w)) & 0xFu);
-            uint32_t v = (f & ~bm) | ((0x05050505u - f) & bm);  // 5 - fixed: 3 on target, 4 on floor
+            const uint32_t f = xf[w], bm = unnib((uint32_t)(box64 >> (4 * w)) & 0xFu);
+            uint32_t v = (f & ~bm) | ((0x05050505u - f) & bm);
             const int sh = 8 * (p - 4 * w);
             v = (p >> 2) == w ? ((v & ~(0xFFu << sh)) | (5u << sh)) : v;
             xs[w] = v;
@@ -463,6 +560,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
       e.max_steps = env.max_steps;
       e.n_open = n_open;
       e.err = 0;
+      const ExecList x = exec_list(acts, n_act, left);
       o = lds_turn(e, x, err, turn_done, succ_last);
       err |= e.err;
       r = e.r;
@@ -477,7 +575,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
       }
     }
   }
-  RMI_STAMP(2);
+  RMI_STAMP(3);
 
   // ---- 4. outputs
   if (act) {
@@ -504,7 +602,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     }
     if (err_out && err) err_out[b] |= err;
   }
-  RMI_STAMP(3);
+  RMI_STAMP(4);
 }
 
 // Fused reset: room_state/player from the generated rooms, counters and the whole episode
@@ -552,12 +650,27 @@ RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t*
     return RMI_EUNSUP;
   const unsigned grid = (unsigned)((ep->B + kWave - 1) / kWave);
   hipStream_t s = as_stream(stream);
-  if (hw == 36)
-    hipLaunchKernelGGL(sokoban_step_turn_kernel<36>, dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw, err);
+  const int H = env->H, W = env->W;
+  uint64_t border = 0;  // border cells, row-major
+  for (int r = 0; r < H; ++r)
+    for (int c = 0; c < W; ++c)
+      if (r == 0 || c == 0 || r == H - 1 || c == W - 1) border |= 1ull << (r * W + c);
+  const bool w32 = (H - 1) * W <= 32;  // the board window fits a u32
+  if (hw == 36 && w32)
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint32_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
+                       border, err);
+  else if (hw == 36)
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint64_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
+                       border, err);
   else if (hw == 64)
-    hipLaunchKernelGGL(sokoban_step_turn_kernel<64>, dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw, err);
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<64, uint64_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
+                       border, err);
+  else if (w32)
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<0, uint32_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
+                       border, err);
   else
-    hipLaunchKernelGGL(sokoban_step_turn_kernel<0>, dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw, err);
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<0, uint64_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
+                       border, err);
   return launch_status();
 }
 

@@ -10,9 +10,9 @@ mkdir -p "$OUT"
 python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { echo build failed; exit 3; }
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters.txt" 2>&1
 i=0
-for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
-           "GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
-           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do
+for set in "FETCH_SIZE" "WRITE_SIZE" \
+           "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+           "TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $set --kernel-trace -d "$OUT/pass$i" -o pmc --output-format csv \
     -- python3 tools/prof_sokoban.py --reps 20 > "$OUT/pass$i.log" 2>&1
@@ -20,4 +20,5 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   echo "pass$i [$set] rc=$rc" | tee -a "$OUT/status.txt"
   if [ $rc -ne 0 ]; then tail -5 "$OUT/pass$i.log"; [ $rc -ge 124 ] && exit $rc; fi
 done
+python3 tools/pmc_summary.py "$OUT" "$OUT/pmc_sokoban_step_turn.json"
 echo done

@@ -1,7 +1,7 @@
 // stampbench.hip — where the time of one Sokoban turn launch goes (diagnostic, not product).
 // Compiles the kernel source itself with RMI_STAMPS so every wave records s_memtime (shader
 // clock) and s_memrealtime (100 MHz) at its phase boundaries:
-//   0 kernel entry | 1 loads + exec list + board decode done | 2 turn done | 3 outputs issued
+//   0 kernel entry | 1 loads landed | 2 exec list + board decode done | 3 turn done | 4 outputs issued
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -Iinclude -Iragen_amd/csrc tools/stampbench.hip -o tools/stampbench
 #define RMI_STAMPS 1
 #include "../ragen_amd/csrc/sokoban.hip"
@@ -89,22 +89,22 @@ int main(int argc, char** argv) {
     double cyc = 0, rts = 0;
     for (int g = 0; g < grid; ++g) {
       const unsigned long long* s = &h[(size_t)g * 16];
-      for (int p = 1; p < 4; ++p) {
+      for (int p = 1; p < 5; ++p) {
         phase[p] += (double)(s[2 * p] - s[2 * (p - 1)]) / grid;
         phase_rt[p] += (double)(s[2 * p + 1] - s[2 * (p - 1) + 1]) / grid;
       }
       rt_min = std::min(rt_min, s[1]);
-      rt_max = std::max(rt_max, s[7]);
-      cyc += (double)(s[6] - s[0]);
-      rts += (double)(s[7] - s[1]);
+      rt_max = std::max(rt_max, s[9]);
+      cyc += (double)(s[8] - s[0]);
+      rts += (double)(s[9] - s[1]);
     }
     span_rt += (double)(rt_max - rt_min);
     clk += cyc / rts * 100.0;  // MHz
   }
   printf("B=%d grid=%d  event %.2f us/launch | first-entry..last-store span %.2f us | shader clock %.0f MHz\n", B, grid,
          ev_us / reps, span_rt / reps / 100.0, clk / reps);
-  const char* names[4] = {"", "loads+decode", "turn", "outputs"};
-  for (int p = 1; p < 4; ++p)
+  const char* names[5] = {"", "loads", "decode", "turn", "outputs"};
+  for (int p = 1; p < 5; ++p)
     printf("  %-12s %8.0f cycles  %6.2f us\n", names[p], phase[p] / reps, phase_rt[p] / reps / 100.0);
   return 0;
 }
