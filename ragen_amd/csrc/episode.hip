@@ -26,34 +26,66 @@ __device__ __forceinline__ float wave_max(float x) {
   return x;
 }
 
+struct EnvTotals {
+  double score;
+  int eff, val, present;
+};
+// Trajectory score sum(turn rewards) (python sum, turn order) and the turn-info counts of env
+// i.  The loads of a chunk of 8 turns are issued together (clamped, always-valid addresses),
+// so an env costs one memory round trip per 8 turns instead of one per turn.
+template <bool kInfo>
+__device__ __forceinline__ EnvTotals env_totals(const rmi_episode_t& ep, int64_t i) {
+  const int64_t B = ep.B;
+  EnvTotals e;
+  e.score = 0.0;
+  e.eff = e.val = e.present = 0;
+  for (int t0 = 0; t0 < ep.T; t0 += 8) {
+    double r[8];
+    uint8_t inf[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t t = min(t0 + k, ep.T - 1);
+      r[k] = ep.turn_reward[t * B + i];
+      if (kInfo) inf[k] = ep.turn_info[t * B + i];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (t0 + k < ep.T) {
+        e.score += r[k];
+        if (kInfo) {
+          e.present |= inf[k] & RMI_INFO_PRESENT;
+          e.eff += (inf[k] >> 1) & 1;
+          e.val += (inf[k] >> 2) & 1;
+        }
+      }
+    }
+  }
+  return e;
+}
+
+// get_rollout_states (es_manager.py:173-207): success, num_actions, and the per-info-key means
+// over turns (turns without an executed action count in the denominator, NaN if none had one)
+__device__ __forceinline__ void env_metrics(const rmi_episode_t& ep, int64_t i, const EnvTotals& e,
+                                            double* __restrict__ out) {
+  const uint8_t f = ep.flags[i];
+  const double nt = (double)ep.n_turns[i];
+  out[4 * i + 0] = ((f & RMI_FLAG_TERMINATED) && !(f & RMI_FLAG_TRUNCATED)) ? 1.0 : 0.0;
+  out[4 * i + 1] = (double)ep.num_actions[i];
+  out[4 * i + 2] = e.present ? (double)e.eff / nt : __builtin_nan("");
+  out[4 * i + 3] = e.present ? (double)e.val / nt : __builtin_nan("");
+}
+
 __global__ __launch_bounds__(kBlock) void rollout_metrics_kernel(rmi_episode_t ep, double* __restrict__ out) {
   const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (b >= ep.B) return;
-  const uint8_t f = ep.flags[b];
-  int eff = 0, val = 0, present = 0;
-  for (int t = 0; t < ep.T; ++t) {
-    const uint8_t inf = ep.turn_info[(int64_t)t * ep.B + b];
-    if (inf & RMI_INFO_PRESENT) {
-      present = 1;
-      eff += (inf & RMI_INFO_EFFECTIVE) ? 1 : 0;
-      val += (inf & RMI_INFO_VALID) ? 1 : 0;
-    }
-  }
-  const double nt = (double)ep.n_turns[b];
-  const bool success = (f & RMI_FLAG_TERMINATED) && !(f & RMI_FLAG_TRUNCATED);
-  out[4 * b + 0] = success ? 1.0 : 0.0;
-  out[4 * b + 1] = (double)ep.num_actions[b];
-  out[4 * b + 2] = present ? (double)eff / nt : __builtin_nan("");
-  out[4 * b + 3] = present ? (double)val / nt : __builtin_nan("");
+  env_metrics(ep, b, env_totals<true>(ep, b), out);
 }
 
 __global__ __launch_bounds__(kBlock) void trajectory_scores_kernel(rmi_episode_t ep, float* __restrict__ score,
                                                                    float* __restrict__ pen) {
   const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (b >= ep.B) return;
-  double s = 0.0;  // python sum() over the turn rewards, in turn order
-  for (int t = 0; t < ep.T; ++t) s += ep.turn_reward[(int64_t)t * ep.B + b];
-  score[b] = (float)s;
+  score[b] = (float)env_totals<false>(ep, b).score;
   if (pen) pen[b] = (float)ep.penalty[b];
 }
 
@@ -196,9 +228,15 @@ __global__ __launch_bounds__(kFilterThreads) void filter_kernel(const float* __r
   }
 }
 
+// score_tensor[:, -1] + penalty in f32 (ctx_manager.py:194-217)
+__device__ __forceinline__ float env_x(const rmi_episode_t& ep, int64_t i) {
+  return (float)env_totals<false>(ep, i).score + (float)ep.penalty[i];
+}
+
 // Fused end-of-rollout pass: per env metrics + trajectory score + penalty, then the group
 // normalisation, one wave per segment (get_rollout_states + get_masks_and_scores score
-// placement + _normalize_score_tensor in one launch).
+// placement + _normalize_score_tensor in one launch).  A segment's first 64 envs keep their
+// x in a register across the mean / variance / output passes.
 __global__ __launch_bounds__(kBlock) void finalize_kernel(rmi_episode_t ep, const int32_t* __restrict__ seg, int G,
                                                           int method, double* __restrict__ metrics,
                                                           float* __restrict__ score_out, float* __restrict__ pen_out,
@@ -207,30 +245,18 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(rmi_episode_t ep, cons
   const int g = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (g >= G) return;
   const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
-  const int64_t B = ep.B;
   double s = 0.0;
+  float x0 = 0.0f;
   for (int i = lo + lane; i < hi; i += 64) {
-    double sc = 0.0;
-    int eff = 0, val = 0, present = 0;
-    for (int t = 0; t < ep.T; ++t) {
-      sc += ep.turn_reward[(int64_t)t * B + i];
-      const uint8_t inf = ep.turn_info[(int64_t)t * B + i];
-      present |= inf & RMI_INFO_PRESENT;
-      eff += (inf >> 1) & 1;
-      val += (inf >> 2) & 1;
-    }
-    const float scf = (float)sc, pf = (float)ep.penalty[i];
+    const float pf = (float)ep.penalty[i];
+    const EnvTotals e = env_totals<true>(ep, i);
+    const float scf = (float)e.score;
     if (score_out) score_out[i] = scf;
     if (pen_out) pen_out[i] = pf;
-    if (metrics) {
-      const uint8_t f = ep.flags[i];
-      const double nt = (double)ep.n_turns[i];
-      metrics[4 * i + 0] = ((f & RMI_FLAG_TERMINATED) && !(f & RMI_FLAG_TRUNCATED)) ? 1.0 : 0.0;
-      metrics[4 * i + 1] = (double)ep.num_actions[i];
-      metrics[4 * i + 2] = present ? (double)eff / nt : __builtin_nan("");
-      metrics[4 * i + 3] = present ? (double)val / nt : __builtin_nan("");
-    }
-    s += (double)(scf + pf);
+    if (metrics) env_metrics(ep, i, e, metrics);
+    const float x = scf + pf;
+    if (i < lo + 64) x0 = x;
+    s += (double)x;
   }
   if (!norm_out || n <= 0) return;
   s = wave_sum(s);
@@ -240,9 +266,7 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(rmi_episode_t ep, cons
   if (method == RMI_NORM_MEAN_STD || method == RMI_NORM_ASYM_CLIP) {
     double q = 0.0;
     for (int i = lo + lane; i < hi; i += 64) {
-      double sc = 0.0;
-      for (int t = 0; t < ep.T; ++t) sc += ep.turn_reward[(int64_t)t * B + i];
-      const double d = (double)((float)sc + (float)ep.penalty[i]) - md;
+      const double d = (double)(i < lo + 64 ? x0 : env_x(ep, i)) - md;
       q += d * d;
     }
     q = wave_sum(q);
@@ -250,9 +274,7 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(rmi_episode_t ep, cons
   }
   const bool use = sd > 1e-6f;
   for (int i = lo + lane; i < hi; i += 64) {
-    double sc = 0.0;
-    for (int t = 0; t < ep.T; ++t) sc += ep.turn_reward[(int64_t)t * B + i];
-    const float x = (float)sc + (float)ep.penalty[i];
+    const float x = i < lo + 64 ? x0 : env_x(ep, i);
     float y;
     if (method == RMI_NORM_IDENTITY) y = x;
     else if (method == RMI_NORM_MEAN) y = x - mean;

@@ -193,44 +193,54 @@ __device__ __forceinline__ uint32_t byte_mask(uint32_t x) { return (x << 8) - x;
 // 4-bit nibble -> byte mask (bit j -> byte j = 0xFF)
 __device__ __forceinline__ uint32_t unnib(uint32_t n) { return byte_mask((n * 0x00204081u) & 0x01010101u); }
 
-// Bitboards (cell i = bit i, row-major) of one row pair, and whether the room is consistent:
-// fixed bytes in {0,1,2}, and the state row equals its rebuild from (fixed, boxes, player p).
-template <int NW>
-__device__ __forceinline__ bool decode_rows(const uint32_t (&xs)[NW], const uint32_t (&xf)[NW], int row_words, int p,
-                                            uint64_t& wall, uint64_t& target, uint64_t& box) {
+// OR across the LPE lanes that share an env (consecutive lanes; DPP inside a row of 16).
+template <int LPE>
+__device__ __forceinline__ uint32_t env_or(uint32_t x) {
+  if (LPE >= 2) x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  if (LPE >= 4) x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  if (LPE >= 8) x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return x;
+}
+template <int LPE>
+__device__ __forceinline__ uint64_t env_or64(uint64_t x) {
+  return ((uint64_t)env_or<LPE>((uint32_t)(x >> 32)) << 32) | env_or<LPE>((uint32_t)x);
+}
+
+// Bitboards (cell i = bit i, row-major) of one room, and whether it is consistent: fixed
+// bytes in {0,1,2}, and the state row equals its rebuild from (fixed, boxes, player p).
+// Lane `sub` of the env's LPE lanes holds row dwords w = sub + LPE * i; the partial boards
+// are OR-combined across those lanes, so every lane ends with the whole room.
+template <int NWL, int LPE>
+__device__ __forceinline__ bool decode_rows(const uint32_t (&xs)[NWL], const uint32_t (&xf)[NWL], int sub,
+                                            int row_words, int p, uint64_t& wall, uint64_t& target, uint64_t& box) {
   constexpr uint32_t L = 0x01010101u;
   const int pw = p >> 2;
   const uint32_t pmask = 0xFFu << (8 * (p & 3)), p5 = 5u << (8 * (p & 3));
-  uint32_t bad = 0, wl = 0, wh = 0, tl = 0, th = 0, bl = 0, bh = 0;
+  uint32_t bad = 0;
+  uint64_t wl = 0, tl = 0, bl = 0;
 #pragma unroll
-  for (int w = 0; w < NW; ++w) {
+  for (int i = 0; i < NWL; ++i) {
+    const int w = sub + LPE * i;
     if (w < row_words) {
-      const uint32_t f = xf[w], s = xs[w];
+      const uint32_t f = xf[i], s = xs[i];
       const uint32_t f1 = f >> 1, s1 = s >> 1, s2 = s >> 2;
-      bad |= (f & 0xFCFCFCFCu) | (f & f1 & L);           // fixed byte in {0, 1, 2}
-      const uint32_t fw = ~(f | f1) & L;                   // fixed == 0 (wall)
-      const uint32_t ft = f1 & L;                          // fixed == 2 (target)
+      bad |= (f & 0xFCFCFCFCu) | (f & f1 & L);                     // fixed byte in {0, 1, 2}
+      const uint32_t fw = ~(f | f1) & L;                             // fixed == 0 (wall)
+      const uint32_t ft = f1 & L;                                    // fixed == 2 (target)
       const uint32_t bx = ((s & s1 & ~s2) | (s2 & ~s1 & ~s)) & L;  // low bits 011 / 100: 3 or 4
       const uint32_t bm = byte_mask(bx);
       uint32_t reb = (f & ~bm) | ((0x05050505u - f) & bm);  // boxes: 5 - fixed = 3 on target, 4 on floor
       reb = w == pw ? ((reb & ~pmask) | p5) : reb;           // the player's 5
       bad |= reb ^ s;
-      const uint32_t nw_ = nib(fw), nt = nib(ft), nb = nib(bx);
-      if (w < 8) {
-        wl |= nw_ << (4 * w);
-        tl |= nt << (4 * w);
-        bl |= nb << (4 * w);
-      } else {
-        wh |= nw_ << (4 * (w - 8));
-        th |= nt << (4 * (w - 8));
-        bh |= nb << (4 * (w - 8));
-      }
+      wl |= (uint64_t)nib(fw) << (4 * w);
+      tl |= (uint64_t)nib(ft) << (4 * w);
+      bl |= (uint64_t)nib(bx) << (4 * w);
     }
   }
-  wall = ((uint64_t)wh << 32) | wl;
-  target = ((uint64_t)th << 32) | tl;
-  box = ((uint64_t)bh << 32) | bl;
-  return bad == 0;
+  wall = env_or64<LPE>(wl);
+  target = env_or64<LPE>(tl);
+  box = env_or64<LPE>(bl);
+  return env_or<LPE>(bad) == 0;
 }
 
 template <class M>
@@ -417,24 +427,81 @@ __device__ __forceinline__ TurnOut lds_turn(SokobanLdsEnv& e, const ExecList& x,
   return o;
 }
 
-constexpr int kMaxWords = kMaxCells / 4;
+// A lane's row dwords w = sub + LPE*i.  With one lane per env and a compile-time row size the
+// row is moved as 16-B pieces (global_load/store_dwordx4 need only dword alignment): 3
+// instructions per 36-B row instead of 9, i.e. fewer address passes through the TA.
+struct __attribute__((packed, aligned(4))) Dw4 {
+  uint32_t x, y, z, w;
+};
+template <int NWL, int LPE, bool kWide>
+__device__ __forceinline__ void load_row(const uint8_t* row, uint32_t (&x)[NWL], int sub, int row_words) {
+  const uint32_t* r1 = reinterpret_cast<const uint32_t*>(row);
+  if (kWide && LPE == 1) {
+    const Dw4* r4 = reinterpret_cast<const Dw4*>(row);
+#pragma unroll
+    for (int i = 0; i < NWL / 4; ++i) {
+      const Dw4 v = r4[i];
+      x[4 * i] = v.x;
+      x[4 * i + 1] = v.y;
+      x[4 * i + 2] = v.z;
+      x[4 * i + 3] = v.w;
+    }
+#pragma unroll
+    for (int i = NWL / 4 * 4; i < NWL; ++i) x[i] = r1[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NWL; ++i) {
+      const int w = sub + LPE * i;
+      if (w < row_words) x[i] = r1[w];
+    }
+  }
+}
+template <int NWL, int LPE, bool kWide>
+__device__ __forceinline__ void store_row(uint8_t* row, const uint32_t (&x)[NWL], int sub, int row_words) {
+  uint32_t* r1 = reinterpret_cast<uint32_t*>(row);
+  if (kWide && LPE == 1) {
+    Dw4* r4 = reinterpret_cast<Dw4*>(row);
+#pragma unroll
+    for (int i = 0; i < NWL / 4; ++i) r4[i] = Dw4{x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]};
+#pragma unroll
+    for (int i = NWL / 4 * 4; i < NWL; ++i) r1[i] = x[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < NWL; ++i) {
+      const int w = sub + LPE * i;
+      if (w < row_words) r1[w] = x[i];
+    }
+  }
+}
 
-// One launch = one turn of every env.  Lane = env; each lane loads and stores only its own
-// rows (no barriers): every load of the turn is issued up front (one memory round trip),
-// the rows live in VGPRs as dwords, and a wave of regular rooms steps on bitboards of word
+constexpr int kMaxWords = kMaxCells / 4;
+#ifndef RMI_SPREAD_MAX_ENVS  // (tools/stampbench.hip overrides it to compare the layouts)
+#define RMI_SPREAD_MAX_ENVS 4096
+#endif
+constexpr int64_t kSpreadMaxEnvs = RMI_SPREAD_MAX_ENVS;  // 4 lanes per env up to this batch
+
+// One launch = one turn of every env.  LPE consecutive lanes own one env (LPE = 1 for big
+// batches; 4 when the batch is too small to fill the chip, so the per-wave instruction
+// chain — decode, row rebuild, loads, stores — is split LPE ways; the steps themselves run
+// redundantly on the env's lanes).  Each lane loads and stores only its own row dwords
+// w = sub + LPE*i (no barriers); every load of the turn is issued up front (one memory
+// round trip), rows live in VGPRs, and a wave of regular rooms steps on bitboards of word
 // type M.  `border` = bitmask of the border cells (row-major), precomputed by the launcher.
-template <int HW, class M>  // HW = H*W for the common sizes (0 = runtime); H*W % 4 == 0
+template <int HW, class M, int LPE>  // HW = H*W for the common sizes (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
                                                                   uint8_t* __restrict__ err_out) {
   constexpr int NW = HW ? HW / 4 : kMaxWords;
-  __shared__ uint32_t lds_state[kWave * NW];  // exact path only: lane-private rows
-  __shared__ uint32_t lds_fixed[kWave * NW];
+  constexpr int NWL = (NW + LPE - 1) / LPE;      // row dwords per lane
+  constexpr int kEnvs = kWave / LPE;             // envs per wave
+  __shared__ uint32_t lds_state[kEnvs * NW];     // exact path only: env-private rows
+  __shared__ uint32_t lds_fixed[kEnvs * NW];
   const int hw = HW ? HW : hw_rt;
   const int row_words = hw >> 2;
   const int B = ep.B;
   const int lane = threadIdx.x;
-  const int64_t b = (int64_t)blockIdx.x * kWave + lane;
+  const int sub = lane % LPE, slot = lane / LPE;
+  const int64_t b = (int64_t)blockIdx.x * kEnvs + slot;
   const bool live = b < B;
   const int H = env.H, W = env.W;
   RMI_STAMP(0);
@@ -445,9 +512,9 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   int32_t num_actions = 0, n_turns = 0;
   double penalty = 0.0;
   uint64_t acts = 0;
-  uint32_t xs[NW], xf[NW];
+  uint32_t xs[NWL], xf[NWL];
 #pragma unroll
-  for (int w = 0; w < NW; ++w) xs[w] = xf[w] = 0;
+  for (int i = 0; i < NWL; ++i) xs[i] = xf[i] = 0;
   if (live) {
     flags = ep.flags[b];
     if (in.has_input) has_in = in.has_input[b];
@@ -460,15 +527,8 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     penalty = ep.penalty[b];
     n_act = in.n_actions[b];
     acts = load_actions(in.actions + b * (int64_t)in.K, in.K);
-    const uint32_t* gs = reinterpret_cast<const uint32_t*>(env.room_state + b * hw);
-    const uint32_t* gf = reinterpret_cast<const uint32_t*>(env.room_fixed + b * hw);
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      if (w < row_words) {
-        xs[w] = gs[w];
-        xf[w] = gf[w];
-      }
-    }
+    load_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(env.room_fixed + b * hw, xf, sub, row_words);
   }
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
   RMI_STAMP_WAIT(1);
@@ -492,7 +552,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     const bool interior = r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2;
     const int p = interior ? r * W + c : 0;
     uint64_t wall64, target64, box64;
-    const bool consistent = decode_rows<NW>(xs, xf, row_words, p, wall64, target64, box64);
+    const bool consistent = decode_rows<NWL, LPE>(xs, xf, sub, row_words, p, wall64, target64, box64);
     regular = consistent && acts_ok && interior && (border & ~wall64) == 0 && ((wall64 >> p) & 1) == 0;
     // window: bit j = cell W + j; the cells past row H-1 are padding walls
     const int used = (H - 1) * W;
@@ -516,37 +576,44 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     if (act) {
       o = board_turn<M>(wall, target, box, jp, W, acts, in.K, n_act, left, nes, bot, env.num_boxes, env.max_steps,
                         turn_done, succ_last, row_changed);
-      if (row_changed) {  // rebuild the state row: fixed, boxes 3/4, player 5
+      if (row_changed) {  // rebuild this lane's row dwords: fixed, boxes 3/4, player 5
         const int p = jp + W;
         r = p / W;
         c = p - r * W;
         const uint64_t box64 = (uint64_t)box << W;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) {
+        for (int i = 0; i < NWL; ++i) {
+          const int w = sub + LPE * i;
           if (w < row_words) {
-            const uint32_t f = xf[w], bm = unnib((uint32_t)(box64 >> (4 * w)) & 0xFu);
+            const uint32_t f = xf[i], bm = unnib((uint32_t)(box64 >> (4 * w)) & 0xFu);
             uint32_t v = (f & ~bm) | ((0x05050505u - f) & bm);
             const int sh = 8 * (p - 4 * w);
             v = (p >> 2) == w ? ((v & ~(0xFFu << sh)) | (5u << sh)) : v;
-            xs[w] = v;
+            xs[i] = v;
           }
         }
       }
     }
   } else {
-    // rare: some room of the wave is irregular -> the exact path on lane-private LDS rows
-    uint32_t* ls = lds_state + lane * row_words;
-    uint32_t* lf = lds_fixed + lane * row_words;
+    // rare: some room of the wave is irregular -> the exact path on an env-private LDS row,
+    // assembled from the env's lanes and stepped by its first lane
+    uint32_t* ls = lds_state + slot * row_words;
+    uint32_t* lf = lds_fixed + slot * row_words;
     if (act) {
-      int n_open = 0;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
+      for (int i = 0; i < NWL; ++i) {
+        const int w = sub + LPE * i;
         if (w < row_words) {
-          ls[w] = xs[w];
-          lf[w] = xf[w];
-          n_open += __popc(eq_bytes(xs[w], 2u) | (eq_bytes(xs[w], 5u) & eq_bytes(xf[w], 2u)));
+          ls[w] = xs[i];
+          lf[w] = xf[i];
         }
       }
+    }
+    __syncthreads();
+    if (act && sub == 0) {
+      int n_open = 0;
+      for (int w = 0; w < row_words; ++w)
+        n_open += __popc(eq_bytes(ls[w], 2u) | (eq_bytes(ls[w], 5u) & eq_bytes(lf[w], 2u)));
       SokobanLdsEnv e;
       e.st = reinterpret_cast<uint8_t*>(ls);
       e.fx = reinterpret_cast<const uint8_t*>(lf);
@@ -568,39 +635,40 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
       nes = e.num_env_steps;
       bot = e.boxes_on_target;
       row_changed = o.stepped_any_state;
-      if (row_changed) {
+    }
+    __syncthreads();
+    row_changed = env_or<LPE>(row_changed) != 0;  // the env's other lanes store their dwords too
+    if (act && row_changed) {
 #pragma unroll
-        for (int w = 0; w < NW; ++w)
-          if (w < row_words) xs[w] = ls[w];
+      for (int i = 0; i < NWL; ++i) {
+        const int w = sub + LPE * i;
+        if (w < row_words) xs[i] = ls[w];
       }
     }
   }
   RMI_STAMP(3);
 
-  // ---- 4. outputs
+  // ---- 4. outputs: scalars from the env's first lane, row dwords from every lane
   if (act) {
-    finish_turn(o, turn_done, succ_last, num_actions, flags, n_turns, in.max_actions_per_traj);
-    ep.num_actions[b] = num_actions;
-    ep.flags[b] = flags;
-    ep.n_turns[b] = n_turns;
-    ep.penalty[b] = penalty;
-    const int64_t tb = (int64_t)in.turn * B + b;
-    ep.turn_reward[tb] = o.acc;
-    ep.turn_info[tb] = o.info;
-    ep.turn_exec[tb] = o.exec;
-    if (o.stepped_any_state) {
-      env.player[2 * b] = (int8_t)r;
-      env.player[2 * b + 1] = (int8_t)c;
-      env.num_env_steps[b] = nes;
-      env.boxes_on_target[b] = bot;
+    if (sub == 0) {
+      finish_turn(o, turn_done, succ_last, num_actions, flags, n_turns, in.max_actions_per_traj);
+      ep.num_actions[b] = num_actions;
+      ep.flags[b] = flags;
+      ep.n_turns[b] = n_turns;
+      ep.penalty[b] = penalty;
+      const int64_t tb = (int64_t)in.turn * B + b;
+      ep.turn_reward[tb] = o.acc;
+      ep.turn_info[tb] = o.info;
+      ep.turn_exec[tb] = o.exec;
+      if (o.stepped_any_state) {
+        env.player[2 * b] = (int8_t)r;
+        env.player[2 * b + 1] = (int8_t)c;
+        env.num_env_steps[b] = nes;
+        env.boxes_on_target[b] = bot;
+      }
+      if (err_out && err) err_out[b] |= err;
     }
-    if (row_changed) {
-      uint32_t* gs = reinterpret_cast<uint32_t*>(env.room_state + b * hw);
-#pragma unroll
-      for (int w = 0; w < NW; ++w)
-        if (w < row_words) gs[w] = xs[w];
-    }
-    if (err_out && err) err_out[b] |= err;
+    if (row_changed) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
   }
   RMI_STAMP(4);
 }
@@ -656,21 +724,28 @@ RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t*
     for (int c = 0; c < W; ++c)
       if (r == 0 || c == 0 || r == H - 1 || c == W - 1) border |= 1ull << (r * W + c);
   const bool w32 = (H - 1) * W <= 32;  // the board window fits a u32
+  // lanes per env: spread a batch too small to fill the chip over 4 lanes per env
+  const bool spread = ep->B <= kSpreadMaxEnvs;
+#define RMI_LAUNCH(HW_, M_)                                                                                   \
+  do {                                                                                                        \
+    if (spread)                                                                                               \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 4>), dim3((unsigned)((ep->B + 15) / 16)), dim3(kWave), \
+                         0, s, *env, *ep, *in, hw, border, err);                                              \
+    else                                                                                                      \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw, \
+                         border, err);                                                                        \
+  } while (0)
   if (hw == 36 && w32)
-    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint32_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
-                       border, err);
+    RMI_LAUNCH(36, uint32_t);
   else if (hw == 36)
-    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint64_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
-                       border, err);
+    RMI_LAUNCH(36, uint64_t);
   else if (hw == 64)
-    hipLaunchKernelGGL((sokoban_step_turn_kernel<64, uint64_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
-                       border, err);
+    RMI_LAUNCH(64, uint64_t);
   else if (w32)
-    hipLaunchKernelGGL((sokoban_step_turn_kernel<0, uint32_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
-                       border, err);
+    RMI_LAUNCH(0, uint32_t);
   else
-    hipLaunchKernelGGL((sokoban_step_turn_kernel<0, uint64_t>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw,
-                       border, err);
+    RMI_LAUNCH(0, uint64_t);
+#undef RMI_LAUNCH
   return launch_status();
 }
 

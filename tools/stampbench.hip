@@ -16,7 +16,7 @@
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 8192, T = 5, K = 5, HW = 36;
-  const int grid = (B + 63) / 64;
+  const int grid = B <= RMI_SPREAD_MAX_ENVS ? (B + 15) / 16 : (B + 63) / 64;  // the launcher's lanes-per-env choice
   uint8_t *fixed, *state, *flags, *info, *exec, *n_act, *init_state;
   int8_t *player, *acts, *init_player;
   int32_t *nes, *bot, *num_actions, *n_turns;
@@ -103,6 +103,21 @@ int main(int argc, char** argv) {
   }
   printf("B=%d grid=%d  event %.2f us/launch | first-entry..last-store span %.2f us | shader clock %.0f MHz\n", B, grid,
          ev_us / reps, span_rt / reps / 100.0, clk / reps);
+  // back-to-back: (reset + turn) pairs minus resets alone
+  auto run_pairs = [&](bool turn) {
+    for (int i = 0; i < 210; ++i) {
+      if (i == 10) CK(hipEventRecord(a, nullptr));
+      rmi_sokoban_reset(&env, &ep, init_state, init_player, nullptr);
+      if (turn) rmi_sokoban_step_turn(&env, &ep, &in, nullptr, nullptr);
+    }
+    CK(hipEventRecord(b, nullptr));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms * 1000.0 / 200;
+  };
+  const double t_reset = run_pairs(false), t_pair = run_pairs(true);
+  printf("  back-to-back: reset %.2f us, turn %.2f us (spread<=%d)\n", t_reset, t_pair - t_reset, RMI_SPREAD_MAX_ENVS);
   const char* names[5] = {"", "loads", "decode", "turn", "outputs"};
   for (int p = 1; p < 5; ++p)
     printf("  %-12s %8.0f cycles  %6.2f us\n", names[p], phase[p] / reps, phase_rt[p] / reps / 100.0);
