@@ -34,6 +34,7 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from ragen_amd import distributed as rd  # noqa: E402
 from ragen_amd import ops, synthetic  # noqa: E402
 from ragen_amd.env import SokobanBatch  # noqa: E402
 from ragen_amd.env.configs import SokobanEnvConfig  # noqa: E402
@@ -88,6 +89,56 @@ class Rollout:
         return a, b
 
 
+def hbm_copy_peak(device, nbytes=1 << 30, reps=10):
+    """Achievable HBM bandwidth on this box: a 1 GiB device-to-device copy (read + write)."""
+    x = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
+    y = torch.empty_like(x)
+    y.copy_(x)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        y.copy_(x)
+    b.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (a.elapsed_time(b) * 1e-3) / 1e9
+    del x, y
+    return gbs
+
+
+def advantage_leg(R, device, reps=20):
+    """The StarPO advantage step on this rollout's trajectories (compute_advantage hot path):
+    token rows [B, L] in SURVEY §8(d)'s synthetic layout (150-token prompt, per executed turn a
+    state block + a response block, score at the last column), verl GAE (legacy, gamma = lam = 1)
+    with fp64 per-row whitening partials, then masked whitening.  Timed with HIP events around
+    back-to-back launches; algorithmic bytes 17 per token (r, V, mask in; adv, ret out)."""
+    n_turns = R.env.ep.n_turns.cpu().numpy()
+    score = R.norm.cpu().numpy()
+    r, v, m = synthetic.token_rows(n_turns, score, seed=11)
+    r, v, m = (torch.from_numpy(x).to(device) for x in (r, v, m))
+    B, L = r.shape
+    stats = torch.empty(B, 3, dtype=torch.float64, device=device)
+    for _ in range(3):
+        adv, ret = ops.gae(r, v, m, 1.0, 1.0, row_stats=stats)
+        ops.masked_whiten_(adv, m, stats)
+    torch.cuda._sleep(2_000_000)
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    e[0].record()
+    for _ in range(reps):
+        adv, ret = ops.gae(r, v, m, 1.0, 1.0, row_stats=stats)
+    e[1].record()
+    for _ in range(reps):
+        ops.masked_whiten_(adv, m, stats)
+    e[2].record()
+    torch.cuda.synchronize()
+    gae_us = e[0].elapsed_time(e[1]) * 1e3 / reps
+    whiten_us = e[1].elapsed_time(e[2]) * 1e3 / reps
+    tokens = B * L
+    gbs = tokens * 17 / (gae_us * 1e-6) / 1e9
+    return {"kernel": "rmi_gae (legacy) + row stats", "rows": B, "cols": L, "tokens_per_launch": tokens,
+            "gae_us": gae_us, "whiten_us": whiten_us, "tokens_per_s": tokens / ((gae_us + whiten_us) * 1e-6),
+            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_token": 17}
+
+
 def cpu_baseline(R, seconds_budget=20.0):
     """Reference-shaped CPU path (oracle/port.py: per-env Python objects mirroring
     EnvStateManager.step + SokobanEnv.step) on a bounded sample of the same workload:
@@ -122,6 +173,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the advantage leg and the copy-peak probe")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -143,6 +195,10 @@ def main():
     n_turns = R.env.ep.n_turns.cpu().numpy()
     active_per_turn = [int((n_turns > t).sum()) for t in range(T_TURNS)]
 
+    # N > 1: the rollout's real exchange step (north_star): reassemble every
+    # rank's trajectory record before the PPO update — one RCCL all-gather of the episode arena
+    exchange = (lambda: rd.gather_episode(R.env.ep)) if dist else (lambda: None)
+
     graph = None
     if not args.no_graph:
         s = torch.cuda.Stream(device)
@@ -154,9 +210,14 @@ def main():
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             R.step()
-        run = graph.replay
+
+        def run():
+            graph.replay()
+            exchange()
     else:
-        run = R.step
+        def run():
+            R.step()
+            exchange()
 
     for _ in range(args.warmup):
         run()
@@ -202,6 +263,9 @@ def main():
     torch.cuda.synchronize()
     eager_ms = (time.perf_counter() - te) / eager_steps * 1e3
 
+    adv = advantage_leg(R, device) if not args.no_extras else None
+    copy_peak = hbm_copy_peak(device) if not args.no_extras else None
+
     if rank == 0:
         cpu = None
         if not args.no_cpu_baseline and world == 1:
@@ -229,9 +293,13 @@ def main():
                        "graph": graph is not None, "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "achievable_peak": copy_peak,
+                         "frac_of_achievable": (achieved / copy_peak) if copy_peak else None,
                          "kernel": "rmi_sokoban_step_turn", "avg_launch_us": avg_launch_us,
                          "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn},
             "cpu_baseline": cpu,
+            "advantage": adv,
+            "exchange": "all-gather of the episode arena per rollout" if dist else None,
             "eager_ms_per_step": eager_ms,
             "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu and cpu.get("value") else None,
         }

@@ -12,9 +12,11 @@
 // bit-identical to the torch CPU loop.  Whitening statistics are fp64 with a fixed
 // reduction tree (run-to-run reproducible; within ~1 ulp of torch's f32 sums).
 //
-// Memory: one 64-lane wave owns 32 rows.  Column chunks of 64 are streamed right-to-left
-// through LDS with coalesced 256-B row segments (r, v, mask in; adv, ret out), the LDS
-// tiles padded to 65 floats per row so the per-row (per-lane) column walk is conflict-free.
+// Memory (GAE): one 64-lane wave owns 32 rows and streams them right to left in 32 x 64
+// tiles: every lane moves 4-column groups (16-B loads/stores; 256-B coalesced row segments),
+// the tile is staged in LDS, the NEXT tile's loads are issued before the current one is
+// walked (lane = row, 16-B LDS reads, row stride 272 B: conflict-free), so HBM latency hides
+// behind the serial recurrence.  Algorithmic traffic 17 B/token (r, v, mask in; adv, ret out).
 #include <math.h>
 
 #include "common.hpp"
@@ -22,9 +24,6 @@
 namespace rmi {
 namespace {
 
-constexpr int kRows = 32;   // rows per wave (256 workgroups at B = 8192)
-constexpr int kCols = 64;   // columns per LDS chunk
-constexpr int kPad = kCols + 1;
 
 __device__ __forceinline__ double wave_sum(double x) {
 #pragma unroll
@@ -32,75 +31,330 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
+constexpr int kGRows = 32;            // rows per wave: lane < 32 walks its row (256 waves at B = 8192)
+constexpr int kGCols = 64;            // columns per tile
+constexpr int kGStr = kGCols + 4;     // LDS row stride in floats (272 B): conflict-free 16-B row walks
+constexpr int kGMStr = kGCols + 4;    // LDS mask row stride in bytes
+constexpr int kGLoads = kGRows * kGCols / 4 / 64;  // 4-column groups per lane per array per tile (8)
+
+struct __attribute__((packed, aligned(4))) F4 {
+  float x, y, z, w;
+};
+struct __attribute__((packed, aligned(1))) U8x4 {
+  uint32_t x;
+};
+
+// One tile = rows [row0, row0+32) x columns [c0, c0+64) of r, v, mask, as 4-column groups:
+// lane l, slot j -> row 4j + l/16, columns c0 + 4*(l%16) .. +3 (256-B coalesced row segments).
+// Columns >= L and rows >= B read as zeros (a zero tail is an exact no-op for the recurrence:
+// it starts the walk at column L-1 with last = nv = 0).
+struct GaeTile {
+  F4 r[kGLoads], v[kGLoads];
+  uint32_t m[kGLoads];
+};
+
+__device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restrict__ r, const float* __restrict__ v,
+                                              const uint8_t* __restrict__ mask, int64_t B, int64_t L, int64_t row0,
+                                              int64_t c0, int lane) {
+  const int g = lane & 15;
+  const int64_t col = c0 + 4 * g;
+  const bool dummy = c0 < 0;  // a pipeline slot past column 0: every lane reads one shared line
+  const bool full_col = col + 4 <= L && !dummy;
+  // 1. every full 4-column group, branch-free from clamped (always valid) addresses, so all
+  //    loads of the tile are in flight together; invalid groups are zeroed when staged
+#pragma unroll
+  for (int j = 0; j < kGLoads; ++j) {
+    const int64_t row = min<int64_t>(row0 + 4 * j + (lane >> 4), B - 1);
+    const int64_t o = dummy ? min<int64_t>(row0, B - 1) * L : (full_col ? row * L + col : row * L);
+    t.r[j] = *reinterpret_cast<const F4*>(r + o);
+    t.v[j] = *reinterpret_cast<const F4*>(v + o);
+    t.m[j] = mask ? reinterpret_cast<const U8x4*>(mask + o)->x : 0x01010101u;
+  }
+  // 2. the ragged group at a row end (L % 4 != 0: one group per row, in one tile) and rows
+  //    past B, element by element, never past the row
+  if (__any(!full_col || row0 + kGRows > B)) {
+#pragma unroll
+    for (int j = 0; j < kGLoads; ++j) {
+      const int64_t row = row0 + 4 * j + (lane >> 4);
+      if (row >= B || col >= L || dummy) {
+        t.r[j] = F4{0.f, 0.f, 0.f, 0.f};
+        t.v[j] = F4{0.f, 0.f, 0.f, 0.f};
+        t.m[j] = 0;
+      } else if (!full_col) {
+        const int64_t o = row * L + col;
+        float rr[4] = {0.f, 0.f, 0.f, 0.f}, vv[4] = {0.f, 0.f, 0.f, 0.f};
+        uint32_t mm = 0;
+        for (int e = 0; e < 4; ++e) {
+          if (col + e < L) {
+            rr[e] = r[o + e];
+            vv[e] = v[o + e];
+            mm |= (uint32_t)(mask ? mask[o + e] : 1) << (8 * e);
+          }
+        }
+        t.r[j] = F4{rr[0], rr[1], rr[2], rr[3]};
+        t.v[j] = F4{vv[0], vv[1], vv[2], vv[3]};
+        t.m[j] = mm;
+      }
+    }
+  }
+}
+
+// verl compute_gae_advantage_return, reverse recurrence in the reference's f32 op order:
+//   delta = (r_t + g * nv) - v_t ;  last = delta + gl * last ;  adv = last ; ret = adv + v_t
+// legacy (VARIANT 0): nv = v_{t+1}; masked (1): nv / last carried through mask-0 positions.
+template <int VARIANT>
+__device__ __forceinline__ void gae_col(float rt, float vt, float mt, float g, float gl, float& nv, float& last,
+                                        float& a_out, float& ret_out) {
+  const float delta = (rt + g * nv) - vt;
+  if (VARIANT == 0) {
+    last = delta + gl * last;
+    nv = vt;
+  } else {
+    const float l2 = delta + gl * last;
+    nv = vt * mt + (1.0f - mt) * nv;
+    last = l2 * mt + (1.0f - mt) * last;
+  }
+  a_out = last;
+  ret_out = last + vt;
+}
+
 template <int VARIANT>
 __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                  const uint8_t* __restrict__ mask, int64_t B, int64_t L, float g,
                                                  float gl, float* __restrict__ adv, float* __restrict__ ret,
                                                  double* __restrict__ row_stats) {
-  __shared__ float sr[kRows * kPad];
-  __shared__ float sv[kRows * kPad];
-  __shared__ float sm[kRows * kPad];
+  __shared__ __attribute__((aligned(16))) float sr[kGRows * kGStr];  // r in, adv out
+  __shared__ __attribute__((aligned(16))) float sv[kGRows * kGStr];  // v in, ret out
+  __shared__ __attribute__((aligned(16))) uint8_t sm[kGRows * kGMStr];
   const int lane = threadIdx.x;
-  const int64_t row0 = (int64_t)blockIdx.x * kRows;
-  const int nrows = (int)min<int64_t>(kRows, B - row0);
-  // per-row carried state (lane < nrows owns row row0 + lane)
+  const int64_t row0 = (int64_t)blockIdx.x * kGRows;
+  const int64_t ntiles = (L + kGCols - 1) / kGCols;
+  const bool walker = lane < kGRows && row0 + lane < B;
   float last = 0.0f, nv = 0.0f;
-  double s1 = 0.0, s2 = 0.0, cnt = 0.0;
-  const int64_t nchunks = (L + kCols - 1) / kCols;
-  for (int64_t ch = nchunks - 1; ch >= 0; --ch) {
-    const int64_t c0 = ch * kCols;
-    const int ncols = (int)min<int64_t>(kCols, L - c0);
-    // coalesced load: lane = column
-    for (int rr = 0; rr < nrows; ++rr) {
-      const int64_t base = (row0 + rr) * L + c0;
-      if (lane < ncols) {
-        sr[rr * kPad + lane] = r[base + lane];
-        sv[rr * kPad + lane] = v[base + lane];
-        sm[rr * kPad + lane] = mask ? (float)mask[base + lane] : 1.0f;
+  double s1a = 0.0, s1b = 0.0, s2a = 0.0, s2b = 0.0, cnt = 0.0;  // row stats, two chains each
+
+  GaeTile t;
+  gae_load_tile(t, r, v, mask, B, L, row0, (ntiles - 1) * kGCols, lane);
+  for (int64_t k = ntiles - 1; k >= 0; --k) {
+    const int64_t c0 = k * kGCols;
+    // registers -> LDS (the tile's 4-column groups), then prefetch the next tile to the left
+#pragma unroll
+    for (int j = 0; j < kGLoads; ++j) {
+      const int row = 4 * j + (lane >> 4), grp = lane & 15;
+      *reinterpret_cast<F4*>(sr + row * kGStr + 4 * grp) = t.r[j];
+      *reinterpret_cast<F4*>(sv + row * kGStr + 4 * grp) = t.v[j];
+      *reinterpret_cast<uint32_t*>(sm + row * kGMStr + 4 * grp) = t.m[j];
+    }
+    __syncthreads();
+    if (k > 0) gae_load_tile(t, r, v, mask, B, L, row0, c0 - kGCols, lane);
+    // the walk: lane = row, columns right to left, 4 at a time
+    if (walker) {
+      float* pr = sr + lane * kGStr;
+      float* pv = sv + lane * kGStr;
+      const uint8_t* pm = sm + lane * kGMStr;
+#pragma unroll 4
+      for (int q = kGCols / 4 - 1; q >= 0; --q) {
+        const F4 r4 = *reinterpret_cast<const F4*>(pr + 4 * q);
+        const F4 v4 = *reinterpret_cast<const F4*>(pv + 4 * q);
+        const uint32_t m4 = *reinterpret_cast<const uint32_t*>(pm + 4 * q);
+        F4 a4, t4;
+        gae_col<VARIANT>(r4.w, v4.w, (float)((m4 >> 24) & 0xFF), g, gl, nv, last, a4.w, t4.w);
+        gae_col<VARIANT>(r4.z, v4.z, (float)((m4 >> 16) & 0xFF), g, gl, nv, last, a4.z, t4.z);
+        gae_col<VARIANT>(r4.y, v4.y, (float)((m4 >> 8) & 0xFF), g, gl, nv, last, a4.y, t4.y);
+        gae_col<VARIANT>(r4.x, v4.x, (float)(m4 & 0xFF), g, gl, nv, last, a4.x, t4.x);
+        *reinterpret_cast<F4*>(pr + 4 * q) = a4;
+        *reinterpret_cast<F4*>(pv + 4 * q) = t4;
+        // whitening partials over in-mask positions (mask bytes are 0/1)
+        const double dw = (double)a4.w, dz = (double)a4.z, dy = (double)a4.y, dx = (double)a4.x;
+        const bool mw = (m4 >> 24) & 0xFF, mz = (m4 >> 16) & 0xFF, my = (m4 >> 8) & 0xFF, mx = m4 & 0xFF;
+        s1a += (mw ? dw : 0.0) + (mz ? dz : 0.0);
+        s1b += (my ? dy : 0.0) + (mx ? dx : 0.0);
+        s2a += (mw ? dw * dw : 0.0) + (mz ? dz * dz : 0.0);
+        s2b += (my ? dy * dy : 0.0) + (mx ? dx * dx : 0.0);
+        cnt += (double)((int)mw + (int)mz + (int)my + (int)mx);
       }
     }
     __syncthreads();
-    if (lane < nrows) {
-      float* pr = sr + lane * kPad;
-      float* pv = sv + lane * kPad;
-      const float* pm = sm + lane * kPad;
-      for (int c = ncols - 1; c >= 0; --c) {
-        const float rt = pr[c], vt = pv[c], mt = pm[c];
-        const float delta = (rt + g * nv) - vt;
-        float a;
-        if (VARIANT == 0) {  // legacy: nextvalues = values[:, t+1]
-          last = delta + gl * last;
-          a = last;
-          nv = vt;
-        } else {  // masked: carry next in-mask value / advantage
-          const float l2 = delta + gl * last;
-          nv = vt * mt + (1.0f - mt) * nv;
-          last = l2 * mt + (1.0f - mt) * last;
-          a = last;
+    // LDS -> global (same 4-column group mapping), never past a row's end
+    const int grp = lane & 15;
+    const int64_t col = c0 + 4 * grp;
+#pragma unroll
+    for (int j = 0; j < kGLoads; ++j) {
+      const int row = 4 * j + (lane >> 4);
+      const int64_t grow = row0 + row;
+      if (grow < B && col < L) {
+        const F4 a4 = *reinterpret_cast<const F4*>(sr + row * kGStr + 4 * grp);
+        const F4 t4 = *reinterpret_cast<const F4*>(sv + row * kGStr + 4 * grp);
+        const int64_t o = grow * L + col;
+        if (col + 4 <= L) {
+          *reinterpret_cast<F4*>(adv + o) = a4;
+          *reinterpret_cast<F4*>(ret + o) = t4;
+        } else {
+          const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
+          for (int e = 0; e < 4; ++e)
+            if (col + e < L) {
+              adv[o + e] = aa[e];
+              ret[o + e] = tt[e];
+            }
         }
-        pr[c] = a;           // adv (overwrite r tile)
-        pv[c] = a + vt;      // ret = adv + values (overwrite v tile)
-        if (mt != 0.0f) {
-          s1 += (double)a;
-          s2 += (double)a * (double)a;
-          cnt += 1.0;
-        }
-      }
-    }
-    __syncthreads();
-    for (int rr = 0; rr < nrows; ++rr) {
-      const int64_t base = (row0 + rr) * L + c0;
-      if (lane < ncols) {
-        adv[base + lane] = sr[rr * kPad + lane];
-        ret[base + lane] = sv[rr * kPad + lane];
       }
     }
     __syncthreads();
   }
-  if (row_stats && lane < nrows) {
-    row_stats[3 * (row0 + lane) + 0] = s1;
-    row_stats[3 * (row0 + lane) + 1] = s2;
-    row_stats[3 * (row0 + lane) + 2] = cnt;
+  if (row_stats && walker) {
+    const int64_t row = row0 + lane;
+    row_stats[3 * row + 0] = s1a + s1b;
+    row_stats[3 * row + 1] = s2a + s2b;
+    row_stats[3 * row + 2] = cnt;
+  }
+}
+
+// Legacy GAE (the StarPO default) with the column-parallel work lifted out of the serial walk.
+// In legacy verl nv_t = v_{t+1} whatever the mask, so delta_t = (r_t + g*v_{t+1}) - v_t is
+// independent across columns: every lane computes it for its 4-column groups (the next
+// column's value comes from the neighbouring lane by a DPP row rotate, or from the tile to
+// the right), the tile is staged in LDS, and the serial walk (lane = row) is reduced to the
+// recurrence last = delta + gl*last — two dependent f32 ops per column.  ret = adv + v and
+// the fp64 whitening partials are again column-parallel, on the staging lanes.  Same f32
+// op order as the reference (bit-exact adv / ret).
+__device__ __forceinline__ float ror15(float x) {  // lane l of each 16-lane row <- lane (l+1) % 16
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x12F, 0xF, 0xF, false));  // row_ror:15
+}
+__device__ __forceinline__ double xor_sum16(double x) {  // sum over the 16 lanes of a DPP row
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) x += __shfl_xor(x, o, 16);
+  return x;
+}
+
+// Per-lane walk state of the legacy kernel.
+struct GaeLegacyState {
+  float last;                 // walkers: the running advantage of their row
+  float nv_right[kGLoads];    // lane 15 of a row: v at the first column of the tile to the right
+  double s1[kGLoads], s2[kGLoads];
+  int cnt[kGLoads];
+};
+
+// One 32 x 64 tile (columns [c0, c0+64)); c0 < 0 is a pipeline dummy (zero data: the walk
+// continues past column 0 harmlessly, nothing is stored).
+__device__ __forceinline__ void gae_legacy_tile(const GaeTile& cur, int64_t c0, GaeLegacyState& st, float* sd,
+                                                int lane, bool walker, int64_t row0, int64_t B, int64_t L, float g,
+                                                float gl, float* __restrict__ adv, float* __restrict__ ret) {
+  const int grp = lane & 15;
+  // 1. delta for this lane's groups, staged in LDS
+#pragma unroll
+  for (int j = 0; j < kGLoads; ++j) {
+    const F4 r4 = cur.r[j], v4 = cur.v[j];
+    const float rot = ror15(v4.x);
+    const float nvx = grp == 15 ? st.nv_right[j] : rot;
+    st.nv_right[j] = rot;  // lane 15 now holds group 0's v.x: the next tile's right neighbour
+    F4 d4;
+    d4.x = (r4.x + g * v4.y) - v4.x;
+    d4.y = (r4.y + g * v4.z) - v4.y;
+    d4.z = (r4.z + g * v4.w) - v4.z;
+    d4.w = (r4.w + g * nvx) - v4.w;
+    const int row = 4 * j + (lane >> 4);
+    *reinterpret_cast<F4*>(sd + row * kGStr + 4 * grp) = d4;
+  }
+  __syncthreads();
+  // 2. the serial walk: lane = row, right to left, last = delta + gl * last
+  if (walker) {
+    float* p = sd + lane * kGStr;
+    float last = st.last;
+#pragma unroll 4
+    for (int q = kGCols / 4 - 1; q >= 0; --q) {
+      F4 d4 = *reinterpret_cast<const F4*>(p + 4 * q);
+      last = d4.w + gl * last;
+      d4.w = last;
+      last = d4.z + gl * last;
+      d4.z = last;
+      last = d4.y + gl * last;
+      d4.y = last;
+      last = d4.x + gl * last;
+      d4.x = last;
+      *reinterpret_cast<F4*>(p + 4 * q) = d4;
+    }
+    st.last = last;
+  }
+  __syncthreads();
+  // 3. ret = adv + v, whitening partials, stores (column-parallel again)
+  const int64_t col = c0 + 4 * grp;
+#pragma unroll
+  for (int j = 0; j < kGLoads; ++j) {
+    const int row = 4 * j + (lane >> 4);
+    const int64_t grow = row0 + row;
+    const F4 a4 = *reinterpret_cast<const F4*>(sd + row * kGStr + 4 * grp);
+    const F4 v4 = cur.v[j];
+    const F4 t4 = F4{a4.x + v4.x, a4.y + v4.y, a4.z + v4.z, a4.w + v4.w};
+    const uint32_t m4 = cur.m[j];
+    const double ax = (m4 & 0xFF) ? (double)a4.x : 0.0, ay = ((m4 >> 8) & 0xFF) ? (double)a4.y : 0.0;
+    const double az = ((m4 >> 16) & 0xFF) ? (double)a4.z : 0.0, aw = (m4 >> 24) ? (double)a4.w : 0.0;
+    st.s1[j] += (ax + ay) + (az + aw);
+    st.s2[j] += (ax * ax + ay * ay) + (az * az + aw * aw);
+    st.cnt[j] += __popc(m4 & 0x01010101u);
+    if (grow < B && col >= 0 && col < L) {
+      const int64_t o = grow * L + col;
+      if (col + 4 <= L) {
+        *reinterpret_cast<F4*>(adv + o) = a4;
+        *reinterpret_cast<F4*>(ret + o) = t4;
+      } else {
+        const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
+        for (int e = 0; e < 4; ++e)
+          if (col + e < L) {
+            adv[o + e] = aa[e];
+            ret[o + e] = tt[e];
+          }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void gae_legacy_kernel(const float* __restrict__ r, const float* __restrict__ v,
+                                                        const uint8_t* __restrict__ mask, int64_t B, int64_t L,
+                                                        float g, float gl, float* __restrict__ adv,
+                                                        float* __restrict__ ret, double* __restrict__ row_stats) {
+  __shared__ __attribute__((aligned(16))) float sd[kGRows * kGStr];  // delta in, adv out
+  const int lane = threadIdx.x;
+  const int grp = lane & 15;
+  const int64_t row0 = (int64_t)blockIdx.x * kGRows;
+  const int64_t ntiles = (L + kGCols - 1) / kGCols;
+  const bool walker = lane < kGRows && row0 + lane < B;
+  GaeLegacyState st;
+  st.last = 0.0f;
+#pragma unroll
+  for (int j = 0; j < kGLoads; ++j) {
+    st.nv_right[j] = 0.0f;
+    st.s1[j] = st.s2[j] = 0.0;
+    st.cnt[j] = 0;
+  }
+  // three register tiles, two loads in flight behind the tile being walked; the loop body
+  // is straight-line (dummy tiles past column 0 keep it so) so the compiler's vmcnt
+  // accounting lets the prefetches overlap the walk
+  GaeTile ta, tb, tc;
+  const int64_t k0 = ntiles - 1;
+  gae_load_tile(ta, r, v, mask, B, L, row0, k0 * kGCols, lane);
+  gae_load_tile(tb, r, v, mask, B, L, row0, (k0 - 1) * kGCols, lane);
+  for (int64_t k = k0; k >= 0; k -= 3) {
+    gae_load_tile(tc, r, v, mask, B, L, row0, (k - 2) * kGCols, lane);
+    gae_legacy_tile(ta, k * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
+    gae_load_tile(ta, r, v, mask, B, L, row0, (k - 3) * kGCols, lane);
+    gae_legacy_tile(tb, (k - 1) * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
+    gae_load_tile(tb, r, v, mask, B, L, row0, (k - 4) * kGCols, lane);
+    gae_legacy_tile(tc, (k - 2) * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
+  }
+  // per-row partials: the 16 lanes of a DPP row hold one row's groups
+  if (row_stats) {
+#pragma unroll
+    for (int j = 0; j < kGLoads; ++j) {
+      const double a = xor_sum16(st.s1[j]), b = xor_sum16(st.s2[j]);
+      const double n = xor_sum16((double)st.cnt[j]);
+      const int64_t grow = row0 + 4 * j + (lane >> 4);
+      if (grp == 0 && grow < B) {
+        row_stats[3 * grow + 0] = a;
+        row_stats[3 * grow + 1] = b;
+        row_stats[3 * grow + 2] = n;
+      }
+    }
   }
 }
 
@@ -306,10 +560,10 @@ RMI_API int rmi_gae(const float* r, const float* v, const uint8_t* mask, int64_t
   if (B == 0 || L == 0) return RMI_OK;
   const float g = (float)gamma;
   const float gl = (float)(gamma * lam);  // python: gamma * lam * lastgaelam
-  const unsigned grid = (unsigned)((B + kRows - 1) / kRows);
+  const unsigned grid = (unsigned)((B + kGRows - 1) / kGRows);
   if (variant == 0)
-    hipLaunchKernelGGL(gae_kernel<0>, dim3(grid), dim3(64), 0, as_stream(stream), r, v, mask, B, L, g, gl, adv, ret,
-                       row_stats);
+    hipLaunchKernelGGL(gae_legacy_kernel, dim3(grid), dim3(64), 0, as_stream(stream), r, v, mask, B, L, g, gl, adv,
+                       ret, row_stats);
   else
     hipLaunchKernelGGL(gae_kernel<1>, dim3(grid), dim3(64), 0, as_stream(stream), r, v, mask, B, L, g, gl, adv, ret,
                        row_stats);

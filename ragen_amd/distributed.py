@@ -10,8 +10,10 @@ needs no collective.  The real exchange steps after it are:
   * masked whitening (verl masked_whiten) uses batch-global mean/var: all-gather the
     per-row (sum, sum_sq, count) partials and reduce them in global row order, so the
     statistics are identical for every world size;
-  * optional reassembly of per-env trajectory tensors before the PPO update
-    (``gather_rollout``), an all-gather of fixed-shape per-env rows.
+  * reassembly of the trajectory record before the PPO update: every rank's episode arena
+    (``EpisodeState``: counters, flags, penalties, per-turn rewards / info / exec counts — one
+    contiguous buffer by construction) in ONE all-gather (``gather_episode``), plus optional
+    fixed-shape per-env rows (``gather_rollout``).
 """
 from typing import Dict, Tuple
 
@@ -58,6 +60,27 @@ def gather_group_scores(scores: torch.Tensor, group_size: int) -> torch.Tensor:
     """Per-env trajectory scores of the local groups -> all groups' scores (global order)."""
     assert scores.shape[0] % group_size == 0
     return all_gather_rows(scores.view(-1, group_size)).reshape(-1)
+
+
+def gather_episode(ep) -> torch.Tensor:
+    """Every rank's episode arena -> u8[W, nbytes] in rank order, one collective.  All ranks
+    must hold the same (B, T) shard shape; ``episode_views`` re-types a rank's row."""
+    W, _ = world()
+    if W == 1:
+        return ep.arena.view(1, -1)
+    n = ep.arena.numel()
+    out = torch.empty(W * n, dtype=torch.uint8, device=ep.arena.device)  # flat: gloo and RCCL both take it
+    dist.all_gather_into_tensor(out, ep.arena)
+    return out.view(W, n)
+
+
+def episode_views(gathered: torch.Tensor, B: int, T: int):
+    """u8[W, nbytes] from gather_episode -> one EpisodeState (views) per rank."""
+    from .ops import EpisodeState
+    fields, total = EpisodeState.layout(B, T)
+    assert gathered.shape[1] == max(total, 1)
+    return [EpisodeState(arena=row, **{n: EpisodeState.view(row, dt, sh, off) for n, dt, sh, off in fields})
+            for row in gathered]
 
 
 def gather_rollout(tensors: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:

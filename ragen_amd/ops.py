@@ -8,6 +8,7 @@ GAE case the reference raises on, core_algos.py:79, when ``check=True``).
 from dataclasses import dataclass
 from typing import Optional
 
+import numpy as np
 import torch
 
 from . import _lib
@@ -47,15 +48,42 @@ class EpisodeState:
     turn_reward: torch.Tensor   # f64[T,B]
     turn_info: torch.Tensor     # u8[T,B]
     turn_exec: torch.Tensor     # u8[T,B]
+    arena: Optional[torch.Tensor] = None  # u8[nbytes]: every field above is a view into it
+
+    # field order inside the arena (each field 256-B aligned)
+    FIELDS = (("num_actions", torch.int32, False), ("flags", torch.uint8, False), ("n_turns", torch.int32, False),
+              ("penalty", torch.float64, False), ("turn_reward", torch.float64, True),
+              ("turn_info", torch.uint8, True), ("turn_exec", torch.uint8, True))
+
+    @staticmethod
+    def layout(B: int, T: int):
+        """-> ([(name, dtype, shape, byte offset)], total bytes) of the arena."""
+        out, off = [], 0
+        for name, dt, per_turn in EpisodeState.FIELDS:
+            shape = (T, B) if per_turn else (B,)
+            n = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            out.append((name, dt, shape, off))
+            off += (n + 255) // 256 * 256
+        return out, off
 
     @staticmethod
     def empty(B: int, T: int, device) -> "EpisodeState":
-        z = lambda *s, dt: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
-        return EpisodeState(z(B, dt=torch.int32), z(B, dt=torch.uint8), z(B, dt=torch.int32),
-                            z(B, dt=torch.float64), z(T, B, dt=torch.float64), z(T, B, dt=torch.uint8),
-                            z(T, B, dt=torch.uint8))
+        """All fields live in one contiguous zeroed arena, so a rank's whole episode record is a
+        single buffer: one collective moves it (ragen_amd.distributed.gather_episode)."""
+        fields, total = EpisodeState.layout(B, T)
+        arena = torch.zeros(max(total, 1), dtype=torch.uint8, device=device)
+        views = {name: EpisodeState.view(arena, dt, shape, off) for name, dt, shape, off in fields}
+        return EpisodeState(arena=arena, **views)
+
+    @staticmethod
+    def view(buf: torch.Tensor, dt, shape, off: int) -> torch.Tensor:
+        n = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+        return buf[off:off + n].view(dt).view(*shape)
 
     def reset_(self):
+        if self.arena is not None:
+            self.arena.zero_()
+            return self
         for t in (self.num_actions, self.flags, self.n_turns, self.penalty, self.turn_reward, self.turn_info,
                   self.turn_exec):
             t.zero_()

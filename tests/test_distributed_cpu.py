@@ -57,7 +57,14 @@ def _worker(rank, world, port, q):
     traj = rd.gather_rollout({"turn_reward": torch.from_numpy(out["turn_reward"]),
                               "state": torch.from_numpy(out["state"])})
     keep, met, _ = oracle.filter_groups(scores, G_TOTAL, GS, 0.25, "std")
-    q.put((rank, scores, stats, traj["turn_reward"].numpy(), traj["state"].numpy(), keep, met))
+    # the whole episode record in one collective (same shard shape on every rank)
+    ep = ops.EpisodeState.empty(ng * GS, T, "cpu")
+    ep.turn_reward.copy_(torch.from_numpy(out["turn_reward"].T.copy()))
+    ep.flags.fill_(rank + 1)
+    views = rd.episode_views(rd.gather_episode(ep), ng * GS, T)
+    ep_tr = torch.cat([v.turn_reward for v in views], dim=1).numpy()
+    ep_fl = [int(v.flags[0]) for v in views]
+    q.put((rank, scores, stats, traj["turn_reward"].numpy(), traj["state"].numpy(), keep, met, ep_tr, ep_fl))
     dist.destroy_process_group()
 
 
@@ -88,7 +95,9 @@ def test_two_rank_gloo_matches_single_process():
         assert p.exitcode == 0
     full = _rollout(0, G_TOTAL)
     fkeep, fmet, _ = oracle.filter_groups(full["score"], G_TOTAL, GS, 0.25, "std")
-    for rank, scores, stats, tr, state, keep, met in res:
+    for rank, scores, stats, tr, state, keep, met, ep_tr, ep_fl in res:
+        np.testing.assert_array_equal(ep_tr, full["turn_reward"].T)   # gather_episode == full record
+        assert ep_fl == [1, 2]
         np.testing.assert_array_equal(scores, full["score"])        # bit-identical global scores
         np.testing.assert_array_equal(tr, full["turn_reward"])
         np.testing.assert_array_equal(state, full["state"])
