@@ -12,11 +12,14 @@
 // bit-identical to the torch CPU loop.  Whitening statistics are fp64 with a fixed
 // reduction tree (run-to-run reproducible; within ~1 ulp of torch's f32 sums).
 //
-// Memory (GAE): one 64-lane wave owns 32 rows and streams them right to left in 32 x 64
-// tiles: every lane moves 4-column groups (16-B loads/stores; 256-B coalesced row segments),
-// the tile is staged in LDS, the NEXT tile's loads are issued before the current one is
-// walked (lane = row, 16-B LDS reads, row stride 272 B: conflict-free), so HBM latency hides
-// behind the serial recurrence.  Algorithmic traffic 17 B/token (r, v, mask in; adv, ret out).
+// Memory (GAE): one 64-lane wave owns kGRows = 4 rows and streams them right to left in
+// 4 x 64 tiles: every lane moves 4-column groups (16-B loads/stores, 256-B coalesced row
+// segments) into a 3-deep register pipeline (two tiles in flight behind the one being
+// worked on).  The column-parallel work (delta, ret = adv + v, fp64 whitening partials)
+// runs on all 64 lanes; the tile is staged in LDS for the serial recurrence, walked by one
+// lane per row (16-B LDS reads, row stride 272 B: conflict-free).  Few rows per wave keeps
+// the serial walk the only long per-wave chain and puts 2 waves on every SIMD; at 8192 x
+// 1093 tokens the kernel streams ~4.8 TB/s (HBM-bound).  Algorithmic traffic 17 B/token.
 #include <math.h>
 
 #include "common.hpp"
@@ -31,7 +34,7 @@ __device__ __forceinline__ double wave_sum(double x) {
   return x;
 }
 
-constexpr int kGRows = 32;            // rows per wave: lane < 32 walks its row (256 waves at B = 8192)
+constexpr int kGRows = 4;             // rows per wave: lane < 4 walks its row (2048 waves at B = 8192, 2 per SIMD)
 constexpr int kGCols = 64;            // columns per tile
 constexpr int kGStr = kGCols + 4;     // LDS row stride in floats (272 B): conflict-free 16-B row walks
 constexpr int kGMStr = kGCols + 4;    // LDS mask row stride in bytes
