@@ -139,6 +139,121 @@ def advantage_leg(R, device, reps=20):
             "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_token": 17}
 
 
+def _graph_rollout(step, reps=50, warmup=5):
+    """Capture one rollout (step()) in a HIP graph, replay it, -> ms per rollout."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    for _ in range(warmup):
+        g.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        g.replay()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+def toytext_legs(device):
+    """BASELINE configs[1] and [4] on this GPU (parity cases of the bench, reported as extras):
+    FrozenLake 4x4 slippery, 4096 envs x 8 turns (K=5, cap 10), and Countdown 16384 envs x 4
+    turns (K=1, cap 1; half the turns carry no answer -> mixed episode lengths).  A rollout =
+    restore the post-reset state (device copies), T turn launches, fused finalize."""
+    from ragen_amd.env import CountdownBatch, FrozenLakeBatch
+    from ragen_amd.env.configs import CountdownEnvConfig, FrozenLakeEnvConfig
+    from ragen_amd.env.countdown import synthetic_instances
+    out = {}
+    # FrozenLake
+    B, T, K = 4096, 8, 5
+    fl = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
+    fl.reset(synthetic.env_seeds(B))
+    snap = [x.clone() for x in (fl.desc, fl.s, fl.rng)]
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=synthetic.ACTION_SEED + 1)
+    ids, n = torch.from_numpy(ids).to(device), torch.from_numpy(n).to(device)
+    seg = torch.arange(0, B + 1, GROUP, dtype=torch.int32, device=device)
+    norm = torch.empty(B, dtype=torch.float32, device=device)
+    turns = [ops.turn_struct(t, ids[t], n[t], None, 10, -0.1) for t in range(T)]
+    st = fl.struct()
+
+    def fl_step():
+        for dst, src in zip((fl.desc, fl.s, fl.rng), snap):
+            dst.copy_(src)
+        fl.ep.arena.zero_()
+        for t in range(T):
+            ops.frozenlake_step_turn(st, fl.ep, turns[t])
+        ops.rollout_finalize(fl.ep, seg, "mean_std", norm)
+    fl_step()
+    torch.cuda.synchronize()
+    steps = int(fl.ep.turn_exec.sum().item())
+    ms = _graph_rollout(fl_step)
+    out["frozenlake"] = {"config": f"FrozenLake 4x4 slippery, {B} envs x {T} turns, K={K}, cap 10",
+                         "env_steps_per_rollout": steps, "ms_per_rollout": ms, "env_steps_per_s": steps / ms * 1e3}
+    # Countdown
+    B, T, K = 16384, 4, 1
+    inst = synthetic_instances(1024, 7)
+    cd = CountdownBatch(CountdownEnvConfig(data=inst), B, T, K, device)
+    cd.reset(synthetic.env_seeds(B))
+    answers = synthetic.countdown_answers([inst[int(i)] for i in cd.index], T)
+    bufs = []
+    for t in range(T):
+        lists = [[a] if a is not None else [] for a in answers[t]]
+        buf, lens = cd.encode_answers(lists)
+        bufs.append((torch.from_numpy(buf).to(device), torch.from_numpy(lens).to(device),
+                     torch.from_numpy(np.array([len(x) for x in lists], np.uint8)).to(device)))
+    zeros = torch.zeros(B, K, dtype=torch.int8, device=device)
+    seg = torch.arange(0, B + 1, GROUP, dtype=torch.int32, device=device)
+    norm = torch.empty(B, dtype=torch.float32, device=device)
+    turns = [ops.turn_struct(t, zeros, bufs[t][2], None, 1, -0.1) for t in range(T)]
+    st = cd.struct()
+
+    def cd_step():
+        cd.ep.arena.zero_()
+        for t in range(T):
+            ops.countdown_step_turn(st, cd.ep, turns[t], bufs[t][0], bufs[t][1])
+        ops.rollout_finalize(cd.ep, seg, "mean_std", norm)
+    cd_step()
+    torch.cuda.synchronize()
+    steps = int(cd.ep.turn_exec.sum().item())
+    ms = _graph_rollout(cd_step)
+    out["countdown"] = {"config": f"Countdown, {B} envs x {T} turns, K={K}, cap 1, 50% empty answers",
+                        "env_steps_per_rollout": steps, "ms_per_rollout": ms, "env_steps_per_s": steps / ms * 1e3}
+    return out
+
+
+def api_leg(device):
+    """SURVEY §8(d)'s "API" variant of the headline: the same SK workload driven through the
+    drop-in EnvStateManager (list-of-dict inputs with action NAMES, per-turn device round trip,
+    history dicts and text observations materialised on the host), reset excluded."""
+    from ragen_amd.config import env_task
+    from ragen_amd.llm_agent import EnvStateManager
+    cfg = env_task("SimpleSokoban", B_PER_GPU // GROUP, GROUP, max_turn=T_TURNS, max_actions_per_turn=K_ACTIONS)
+    es = EnvStateManager(cfg, mode="train", device=device)
+    es.reset(seed=synthetic.ENV_SEED)
+    ids, n = synthetic.rollout_actions(B_PER_GPU, T_TURNS, K_ACTIONS, 1, 4)
+    names = {1: "Up", 2: "Down", 3: "Left", 4: "Right", 0: "Jump"}  # 0 = a name outside the action lookup
+    active = list(range(B_PER_GPU))
+    steps = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(T_TURNS):
+        inputs = [{"env_id": i, "llm_response": "", "llm_raw_response": "",
+                   "actions": [names[int(a)] for a in ids[t, i, :int(n[t, i])]]} for i in active]
+        outs = es.step(inputs)
+        active = [o["env_id"] for o in outs]
+        steps += int(es.tags[0].batch.ep.turn_exec[t].sum().item())
+        if not active:
+            break
+    dt = time.perf_counter() - t0
+    return {"env_steps": steps, "seconds": dt, "env_steps_per_s": steps / dt,
+            "note": "EnvStateManager.step facade, 8192 envs x 5 turns, host dicts + text obs each turn"}
+
+
 def cpu_baseline(R, seconds_budget=20.0):
     """Reference-shaped CPU path (oracle/port.py: per-env Python objects mirroring
     EnvStateManager.step + SokobanEnv.step) on a bounded sample of the same workload:
@@ -265,6 +380,8 @@ def main():
 
     adv = advantage_leg(R, device) if not args.no_extras else None
     copy_peak = hbm_copy_peak(device) if not args.no_extras else None
+    toytext = toytext_legs(device) if not args.no_extras else None
+    api = api_leg(device) if not args.no_extras and rank == 0 else None
 
     if rank == 0:
         cpu = None
@@ -299,6 +416,8 @@ def main():
                          "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn},
             "cpu_baseline": cpu,
             "advantage": adv,
+            "toytext": toytext,
+            "api_variant": api,
             "exchange": "all-gather of the episode arena per rollout" if dist else None,
             "eager_ms_per_step": eager_ms,
             "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu and cpu.get("value") else None,

@@ -72,3 +72,33 @@ def token_rows(n_turns, scores, seed: int = 7, prompt: int = 150, turn_scores=No
             r[b, L - 1] = scores[b]
     v = (rng.standard_normal((B, L)).astype(np.float32) * mask).astype(np.float32)
     return r, v, mask
+
+
+def countdown_answers(instances, T: int, seed: int = ACTION_SEED, p_empty: float = 0.5):
+    """Per env per turn a Countdown answer: with p_empty no parsed answer (the
+    turn only costs the format penalty), else a '+'/'-' expression over the instance's numbers
+    that is correct (1/3), uses every number but evaluates wrong (1/3: format score), or uses a
+    wrong number (1/3: reward 0).  -> [T][B] str or None."""
+    rng = np.random.default_rng(seed)
+    out = [[None] * len(instances) for _ in range(T)]
+    for t in range(T):
+        for i, inst in enumerate(instances):
+            if rng.random() < p_empty:
+                continue
+            nums, target = list(inst["nums"]), int(inst["target"])
+            kind = int(rng.integers(0, 3))
+            signs = None
+            for m in range(1 << len(nums)):  # a sign pattern reaching the target (it exists)
+                sg = [1 if (m >> j) & 1 else -1 for j in range(len(nums))]
+                if sum(s * v for s, v in zip(sg, nums)) == target:
+                    signs = sg
+                    break
+            if signs is None or kind == 1:
+                signs = [1] * len(nums)  # all '+': uses every number, misses the target
+            if kind == 2:
+                nums[int(rng.integers(0, len(nums)))] += 1
+            expr = ("-" if signs[0] < 0 else "") + str(nums[0])
+            for s, v in zip(signs[1:], nums[1:]):
+                expr += (" + " if s > 0 else " - ") + str(v)
+            out[t][i] = expr
+    return out
