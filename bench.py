@@ -134,9 +134,28 @@ def advantage_leg(R, device, reps=20):
     whiten_us = e[1].elapsed_time(e[2]) * 1e3 / reps
     tokens = B * L
     gbs = tokens * 17 / (gae_us * 1e-6) / 1e9
+    # get_masks_and_scores (rmi_masks_and_scores) on token ids of the same [B, L+1] shape:
+    # 8 B/token in (ids), 6 B/token out (score f32 + two masks)
+    g = torch.Generator(device=device).manual_seed(3)
+    ids = torch.randint(100, 1000, (B, L + 1), generator=g, device=device, dtype=torch.int64)
+    ids[torch.rand(B, L + 1, generator=g, device=device) < 0.02] = 151644
+    ids[torch.rand(B, L + 1, generator=g, device=device) < 0.01] = 151645
+    n_sc = R.env.ep.n_turns.to(torch.int32)
+    for _ in range(3):
+        ops.masks_and_scores(ids, 151644, 151645, R.env.ep.turn_reward, n_sc, T_TURNS, False, True, True)
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(reps):
+        ops.masks_and_scores(ids, 151644, 151645, R.env.ep.turn_reward, n_sc, T_TURNS, False, True, True)
+    e[1].record()
+    torch.cuda.synchronize()
+    masks_us = e[0].elapsed_time(e[1]) * 1e3 / reps
+    mgbs = B * (L + 1) * 14 / (masks_us * 1e-6) / 1e9
     return {"kernel": "rmi_gae (legacy) + row stats", "rows": B, "cols": L, "tokens_per_launch": tokens,
             "gae_us": gae_us, "whiten_us": whiten_us, "tokens_per_s": tokens / ((gae_us + whiten_us) * 1e-6),
-            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_token": 17}
+            "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_token": 17,
+            "masks_and_scores": {"kernel": "rmi_masks_and_scores", "us": masks_us, "achieved_GBs": mgbs,
+                                 "frac": mgbs / HBM_PEAK_GBS, "bytes_per_token": 14}}
 
 
 def _graph_rollout(step, reps=50, warmup=5):

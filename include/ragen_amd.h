@@ -211,6 +211,24 @@ int rmi_filter_groups(const float* scores, int32_t G, int32_t gs, double ratio, 
 /* Row sum of a [B,L] f32 tensor (rm_scores.sum(-1), agent_trainer.py:467).              */
 int rmi_row_sum(const float* x, int64_t B, int64_t L, float* out, rmi_stream_t stream);
 
+/* ------------------------------------------------------ A11 token masks and scores
+ * Replaces: get_masks_and_scores (ctx_manager.py:35-70).  ids i64[B,S] row-major.
+ * turn = cumsum(ids == special_token); response_mask = turn odd and > 1; loss_mask =
+ * response_mask (RMI_MS_RESPONSE_MASK) or turn > 1.  Scores: scores f64[T,B] turn-major
+ * (EnvStatus.rewards, i.e. rmi_episode_t.turn_reward), n_scores i32[B] = len(all_scores[b]).
+ *   - without RMI_MS_TURN_SCORES: f32(python sum of row b's scores) at the last column;
+ *   - with it: for idx < n_slots (= zip_longest length = max len), the score (0 past the
+ *     row's own scores) goes to the position with ids == reward_token and turn == 2*idx+3,
+ *     or to the last column when there is none; RMI_MS_ROLL (Qwen) then rolls by +1.
+ * Outputs (the reference's [:, 1:] / [:, :-1] slices): score_out f32[B,S-1], loss_mask
+ * u8[B,S-1], response_mask u8[B,S-1].  err[b] = RMI_ERR_STATE where the reference raises
+ * (a turn with more than one reward token position).  n_slots <= 64.                    */
+enum { RMI_MS_TURN_SCORES = 1, RMI_MS_RESPONSE_MASK = 2, RMI_MS_ROLL = 4 };
+int rmi_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64_t special_token, int64_t reward_token,
+                         const double* scores, const int32_t* n_scores, int32_t T, int32_t n_slots, int32_t flags,
+                         float* score_out, uint8_t* loss_mask, uint8_t* response_mask, uint8_t* err,
+                         rmi_stream_t stream);
+
 /* ------------------------------------------------------------------- A13 advantages
  * Replaces: verl compute_gae_advantage_return (called agent_trainer.py:77-83; App. A.4).
  * variant 0 = legacy (RAGEN's snapshot), 1 = masked (newer verl).  Sequential f32

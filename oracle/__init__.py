@@ -206,6 +206,24 @@ def filter_groups(scores, G, gs, ratio, ftype):
 
 
 # --------------------------------------------------------- Countdown rule (exact reference)
+def masks_and_scores(ids, sp, rt, scores_tb, n_scores, n_slots, use_turn_scores, enable_response_mask, roll):
+    """get_masks_and_scores (ctx_manager.py:35-70) -> (score f32[B,S-1], loss u8, resp u8, err u8[B])."""
+    ids = np.ascontiguousarray(ids, np.int64)
+    B, S = ids.shape
+    sc = np.ascontiguousarray(scores_tb, np.float64).reshape(-1, B) if B else np.zeros((0, 0))
+    n = np.ascontiguousarray(n_scores, np.int32)
+    So = max(S - 1, 0)
+    score = np.zeros((B, So), np.float32)
+    lm = np.zeros((B, So), np.uint8)
+    rm = np.zeros((B, So), np.uint8)
+    err = np.zeros(B, np.uint8)
+    flags = (1 if use_turn_scores else 0) | (2 if enable_response_mask else 0) | (4 if roll else 0)
+    lib().orc_masks_and_scores(_p(ids), ctypes.c_int64(B), ctypes.c_int64(S), ctypes.c_int64(int(sp)),
+                               ctypes.c_int64(int(rt)), _p(sc), _p(n), sc.shape[0], int(n_slots), flags, _p(score),
+                               _p(lm), _p(rm), _p(err))
+    return score, lm, rm, err
+
+
 def check_format(equation, nums):  # countdown/env.py:9-14
     try:
         nums_in_eq = [int(n) for n in re.findall(r"\d+", equation)]

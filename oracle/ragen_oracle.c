@@ -561,3 +561,63 @@ void orc_filter(const float* scores, int32_t G, int32_t gs, double ratio, int32_
   }
   free(kv);
 }
+
+/* ------------------------------------------------------------------ A11 masks / scores
+ * get_masks_and_scores (ctx_manager.py:35-70), literally: turn_indicators = cumsum(ids ==
+ * special) (:43-44); masks (:45-49); with turn scores, for idx over zip_longest(*all_scores,
+ * fillvalue=0) (:52) the boolean-mask assignment score_tensor[reward_position] = scores with
+ * the "no position -> last column" rule (:54-57), then the Qwen roll(+1) (:58-60); without,
+ * python sum at the last column (:62-63); then [:, 1:] and [:, :-1] (:64-66).  A row whose
+ * turn has several reward positions makes the reference raise: err[b] = 1.              */
+int orc_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64_t sp, int64_t rt, const double* scores,
+                         const int32_t* n_scores, int32_t T, int32_t n_slots, int32_t flags, float* score_out,
+                         uint8_t* loss_mask, uint8_t* response_mask, uint8_t* err) {
+  if (S <= 1) return 0;
+  int64_t* turn = (int64_t*)malloc(sizeof(int64_t) * S);
+  float* full = (float*)malloc(sizeof(float) * S);
+  int bad = 0;
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t* row = ids + b * S;
+    int64_t c = 0;
+    for (int64_t p = 0; p < S; ++p) {
+      c += row[p] == sp;
+      turn[p] = c;
+    }
+    err[b] = 0;
+    for (int64_t p = 0; p < S; ++p) full[p] = 0.0f;
+    if (flags & 1) {
+      for (int idx = 0; idx < n_slots; ++idx) {
+        const float s = (idx < n_scores[b] && idx < T) ? (float)scores[(int64_t)idx * B + b] : 0.0f;
+        const int64_t want = 2 * (int64_t)idx + 3;
+        int64_t count = 0;
+        for (int64_t p = 0; p < S; ++p)
+          if (row[p] == rt && turn[p] == want) {
+            full[p] = s;
+            count++;
+          }
+        if (count == 0) full[S - 1] = s;
+        if (count > 1) err[b] = 1;
+      }
+      if (flags & 4) { /* roll(shifts=1): new[p] = old[p-1], new[0] = old[S-1] */
+        const float lastv = full[S - 1];
+        for (int64_t p = S - 1; p >= 1; --p) full[p] = full[p - 1];
+        full[0] = lastv;
+      }
+    } else {
+      double sum = 0.0;
+      for (int i = 0; i < n_scores[b]; ++i) sum += scores[(int64_t)i * B + b];
+      full[S - 1] = (float)sum;
+    }
+    for (int64_t p = 0; p + 1 < S; ++p) {
+      const int64_t t = turn[p];
+      const uint8_t r = (t % 2 == 1) && t > 1;
+      response_mask[b * (S - 1) + p] = r;
+      loss_mask[b * (S - 1) + p] = (flags & 2) ? r : (uint8_t)(t > 1);
+      score_out[b * (S - 1) + p] = full[p + 1];
+    }
+    bad |= err[b];
+  }
+  free(turn);
+  free(full);
+  return bad;
+}

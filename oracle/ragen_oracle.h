@@ -55,6 +55,11 @@ int orc_bandit_turn(int32_t start, double lo, double hi_lo, double hi_hi, double
 
 double orc_pcg64_random(uint64_t st[4]); /* st = {state_hi, state_lo, inc_hi, inc_lo} */
 
+/* get_masks_and_scores (ctx_manager.py:35-70).  flags: 1 turn scores, 2 response mask, 4 roll (Qwen). */
+int orc_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64_t sp, int64_t rt, const double* scores,
+                         const int32_t* n_scores, int32_t T, int32_t n_slots, int32_t flags, float* score_out,
+                         uint8_t* loss_mask, uint8_t* response_mask, uint8_t* err);
+
 void orc_rollout_metrics(const orc_episode_t* ep, double* out /*[B,4]*/);
 void orc_trajectory_scores(const orc_episode_t* ep, float* score, float* pen);
 void orc_group_normalize(const float* score, const float* pen, const int32_t* seg, int32_t G, int32_t B, int32_t method,

@@ -19,6 +19,7 @@ RMI_OK, RMI_EINVAL, RMI_EDEVICE, RMI_EUNSUP = 0, -1, -2, -3
 FLAG_TERMINATED, FLAG_TRUNCATED, FLAG_DONE = 1, 2, 4
 INFO_PRESENT, INFO_EFFECTIVE, INFO_VALID, INFO_SUCCESS = 1, 2, 4, 8
 ERR_ACTION, ERR_INDEX, ERR_STATE, ERR_UNSUP = 1, 2, 4, 8
+MS_TURN_SCORES, MS_RESPONSE_MASK, MS_ROLL = 1, 2, 4
 NORM_METHODS = {"identity": 0, "mean": 1, "mean_std": 2, "asym_clip": 3}
 
 
@@ -76,6 +77,8 @@ _SIGS = {
     "rmi_filter_groups": (c_int32, [c_void_p, c_int32, c_int32, c_double, c_int32, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p]),
     "rmi_row_sum": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "rmi_masks_and_scores": (c_int32, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
+                                       c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_gae": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_double, c_double, c_int32, c_void_p,
                           c_void_p, c_void_p, c_void_p]),
     "rmi_bilevel_gae": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_double, c_double, c_double,

@@ -1,0 +1,172 @@
+// masks.hip — token-level loss / response masks and score placement (gfx950).
+//
+//  rmi_masks_and_scores   get_masks_and_scores (ctx_manager.py:35-70)
+//
+// One wave per row streams the row's token ids in chunks of 256 (4 consecutive ids per lane,
+// 32-B loads): turn = cumsum(ids == <|im_start|>) is a wave prefix scan per chunk plus a
+// running carry, the masks are written as they are produced ([:, :-1] slice), the score row
+// is zero-filled in the same pass ([:, 1:] slice), and the reward-token positions of each
+// assistant turn are recorded in LDS.  After the pass (stores fenced) the <= 64 turn scores
+// are scattered to their positions (Qwen: rolled by +1) — exactly the boolean-mask
+// assignment order of the reference, including its fallback to the last column.
+// Algorithmic traffic: 8 B/token in, 6 B/token out.
+#include "common.hpp"
+
+namespace rmi {
+namespace {
+
+constexpr int kMaxSlots = 64;  // turn slots (zip_longest length) handled per row
+constexpr int kTok = 4;        // token ids per lane per chunk
+constexpr int kChunk = 64 * kTok;
+
+struct __attribute__((packed, aligned(8))) I64x4 {
+  int64_t a, b, c, d;
+};
+struct __attribute__((packed, aligned(1))) U32u {
+  uint32_t x;
+};
+struct __attribute__((packed, aligned(4))) F4u {
+  float x, y, z, w;
+};
+
+__device__ __forceinline__ int wave_inclusive_scan(int x, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    x += lane >= o ? y : 0;
+  }
+  return x;
+}
+
+__global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ ids, int64_t B, int64_t S, int64_t sp,
+                                                   int64_t rt, const double* __restrict__ scores,
+                                                   const int32_t* __restrict__ n_scores, int T, int n_slots,
+                                                   int flags, float* __restrict__ score_out,
+                                                   uint8_t* __restrict__ lmask, uint8_t* __restrict__ rmask,
+                                                   uint8_t* __restrict__ err) {
+  __shared__ int pos[kMaxSlots], cnt[kMaxSlots];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  pos[lane] = -1;
+  cnt[lane] = 0;
+  __syncthreads();
+  const int64_t So = S - 1;  // output columns
+  const int64_t* row = ids + b * S;
+  float* srow = score_out + b * So;
+  uint8_t* lrow = lmask + b * So;
+  uint8_t* rrow = rmask + b * So;
+  const bool turn_scores = flags & RMI_MS_TURN_SCORES, resp_only = flags & RMI_MS_RESPONSE_MASK;
+  // an id matching neither special token, for positions past the row end
+  const int64_t none = (sp != -1 && rt != -1) ? -1 : ((sp != -2 && rt != -2) ? -2 : -3);
+  int carry = 0;
+  for (int64_t c0 = 0; c0 < S; c0 += kChunk) {
+    const int64_t p0 = c0 + kTok * lane;
+    int64_t t[kTok];
+    if (p0 + kTok <= S) {
+      const I64x4 v = *reinterpret_cast<const I64x4*>(row + p0);
+      t[0] = v.a;
+      t[1] = v.b;
+      t[2] = v.c;
+      t[3] = v.d;
+    } else {
+#pragma unroll
+      for (int e = 0; e < kTok; ++e) t[e] = p0 + e < S ? row[p0 + e] : none;
+    }
+    int st[kTok], c = 0;
+#pragma unroll
+    for (int e = 0; e < kTok; ++e) {
+      st[e] = t[e] == sp;
+      c += st[e];
+    }
+    const int incl = wave_inclusive_scan(c, lane);
+    int turn = carry + incl - c;
+    carry += __shfl(incl, 63, 64);
+    uint32_t lm = 0, rm = 0;
+#pragma unroll
+    for (int e = 0; e < kTok; ++e) {
+      turn += st[e];  // turn_indicators at p0 + e
+      const uint32_t r = (turn & 1) && turn > 1;
+      const uint32_t l = resp_only ? r : (uint32_t)(turn > 1);
+      rm |= r << (8 * e);
+      lm |= l << (8 * e);
+      if (turn_scores && t[e] == rt && (turn & 1) && turn >= 3) {
+        const int idx = (turn - 3) >> 1;  // turn_indicator = idx * 2 + 3
+        if (idx < n_slots) {
+          atomicAdd(&cnt[idx], 1);
+          pos[idx] = (int)(p0 + e);
+        }
+      }
+    }
+    // masks[:, :-1]: columns p < S - 1
+    if (p0 + kTok <= So) {
+      reinterpret_cast<U32u*>(lrow + p0)->x = lm;
+      reinterpret_cast<U32u*>(rrow + p0)->x = rm;
+    } else {
+#pragma unroll
+      for (int e = 0; e < kTok; ++e)
+        if (p0 + e < So) {
+          lrow[p0 + e] = (uint8_t)(lm >> (8 * e));
+          rrow[p0 + e] = (uint8_t)(rm >> (8 * e));
+        }
+    }
+    // score[:, 1:] zero fill: output column p - 1 for p in [1, S)
+    if (p0 >= 1 && p0 + kTok <= S) {
+      *reinterpret_cast<F4u*>(srow + p0 - 1) = F4u{0.f, 0.f, 0.f, 0.f};
+    } else {
+#pragma unroll
+      for (int e = 0; e < kTok; ++e)
+        if (p0 + e >= 1 && p0 + e < S) srow[p0 + e - 1] = 0.f;
+    }
+  }
+  __threadfence();  // the zero fill is complete before the scattered scores land on it
+  __syncthreads();  // LDS position records visible to every lane
+  if (!turn_scores) {
+    if (lane == 0) {  // score_tensor[:, -1] = python sum(all_scores[b]), kept by [:, 1:]
+      double sum = 0.0;
+      for (int i = 0; i < n_scores[b]; ++i) sum += scores[(int64_t)i * B + b];
+      srow[So - 1] = (float)sum;
+    }
+    return;
+  }
+  const bool roll = flags & RMI_MS_ROLL;
+  const int nb = n_scores[b];
+  const bool slot = lane < n_slots;
+  const float s = slot && lane < nb && lane < T ? (float)scores[(int64_t)lane * B + b] : 0.0f;
+  const int n = slot ? cnt[lane] : 0, p = slot ? pos[lane] : -1;
+  if (__any(n > 1) && lane == 0) err[b] |= RMI_ERR_STATE;  // the reference's mask assignment raises
+  // positions -> output column: roll (+1, Qwen) then drop column 0
+  auto out_col = [&](int64_t q) -> int64_t { return (roll ? (q + 1) % S : q) - 1; };
+  if (slot && n == 1 && p != S - 1) {
+    const int64_t o = out_col(p);
+    if (o >= 0) srow[o] = s;
+  }
+  // the last column: written by every slot without a position (fallback) or positioned there,
+  // the largest such slot last
+  const uint64_t last = __ballot(slot && (n == 0 || p == S - 1));
+  if (last) {
+    const int hi = 63 - __clzll(last);
+    if (lane == hi) {
+      const int64_t o = out_col(S - 1);
+      if (o >= 0) srow[o] = s;
+    }
+  }
+}
+
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64_t special_token,
+                                 int64_t reward_token, const double* scores, const int32_t* n_scores, int32_t T,
+                                 int32_t n_slots, int32_t flags, float* score_out, uint8_t* loss_mask,
+                                 uint8_t* response_mask, uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || S < 0 || T < 0 || n_slots < 0) return RMI_EINVAL;
+  if (n_slots > kMaxSlots || B > 0x7FFFFFFF) return RMI_EUNSUP;
+  if (B == 0 || S <= 1) return RMI_OK;
+  if (!ids || !n_scores || !score_out || !loss_mask || !response_mask || !err || (T > 0 && !scores))
+    return RMI_EINVAL;
+  hipLaunchKernelGGL(masks_kernel, dim3((unsigned)B), dim3(64), 0, as_stream(stream), ids, B, S, special_token,
+                     reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out, loss_mask,
+                     response_mask, err);
+  return launch_status();
+}

@@ -9,7 +9,6 @@ those bytes).  The numeric hot path runs on the GPU engine:
     from this package's EnvStateManager.
 """
 import re
-from itertools import zip_longest
 from typing import Dict, List
 
 import numpy as np
@@ -31,25 +30,27 @@ def get_special_tokens(tokenizer):
 
 def get_masks_and_scores(input_ids: torch.Tensor, tokenizer, all_scores: List[List[float]] = None,
                          use_turn_scores: bool = False, enable_response_mask: bool = False):
-    """ctx_manager.py:35-70, computed on the device holding ``input_ids`` (GPU in the engine)."""
+    """ctx_manager.py:35-70 on the device holding ``input_ids``: one HIP kernel
+    (rmi_masks_and_scores) — turn prefix scan, both masks, score placement incl. the Qwen roll
+    and the last-column fallback.  Raises RuntimeError where the reference's boolean-mask
+    assignment would (a turn with more than one reward-token position)."""
     special_token, reward_token = get_special_tokens(tokenizer)
-    turn_indicators = torch.cumsum((input_ids == special_token).to(torch.int64), dim=-1)
-    response_mask = (turn_indicators % 2 == 1) & (turn_indicators > 1)
-    loss_mask = response_mask.clone() if enable_response_mask else (turn_indicators > 1)
-    score_tensor = torch.zeros(input_ids.shape, dtype=torch.float32, device=input_ids.device)
-    if use_turn_scores:
-        for idx, scores in enumerate(zip_longest(*all_scores, fillvalue=0)):
-            scores = torch.tensor(scores, dtype=torch.float32, device=input_ids.device)
-            turn_indicator = idx * 2 + 3  # 0: pad. 1: system. 2+2n: user. 3+2n: assistant
-            reward_position = (input_ids == reward_token) & (turn_indicators == turn_indicator)
-            reward_position[~reward_position.any(dim=-1), -1] = True
-            score_tensor[reward_position] = scores
-        if "qwen" in tokenizer.name_or_path.lower():
-            score_tensor = score_tensor.roll(shifts=1, dims=-1)
-    else:
-        scores = [sum(i) for i in all_scores]
-        score_tensor[:, -1] = torch.tensor(scores, dtype=torch.float32, device=input_ids.device)
-    return score_tensor[:, 1:], loss_mask[:, :-1], response_mask[:, :-1]
+    B = input_ids.shape[0]
+    all_scores = all_scores if all_scores is not None else [[] for _ in range(B)]
+    n = [len(x) for x in all_scores]
+    T = max(n) if n else 0
+    tab = np.zeros((max(T, 1), B), np.float64)
+    for b, row in enumerate(all_scores):
+        tab[:len(row), b] = row
+    dev = input_ids.device
+    score, lm, rm, err = ops.masks_and_scores(
+        input_ids.to(torch.int64), special_token, reward_token, torch.from_numpy(tab).to(dev),
+        torch.tensor(n, dtype=torch.int32, device=dev), T, use_turn_scores, enable_response_mask,
+        "qwen" in tokenizer.name_or_path.lower())
+    if use_turn_scores and bool(err.any()):
+        raise RuntimeError("shape mismatch: a turn has more than one reward-token position "
+                           "(reference score_tensor[reward_position] = scores)")
+    return score, lm, rm
 
 
 def segments_for(grouping: str, env_outputs: List[Dict]):

@@ -241,6 +241,36 @@ def row_sum(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# ------------------------------------------------------------------- token masks (A11)
+def masks_and_scores(ids: torch.Tensor, special_token: int, reward_token: int, scores: torch.Tensor,
+                     n_scores: torch.Tensor, n_slots: int, use_turn_scores: bool, enable_response_mask: bool,
+                     roll: bool):
+    """get_masks_and_scores (ctx_manager.py:35-70) on the device.  ids i64[B,S]; scores f64[T,B]
+    turn-major (e.g. EpisodeState.turn_reward); n_scores i32[B]; n_slots = zip_longest length.
+    -> (score f32[B,S-1], loss_mask bool[B,S-1], response_mask bool[B,S-1], err u8[B])."""
+    _dev(ids, scores, n_scores)
+    _dt(ids, torch.int64, "input_ids")
+    _dt(scores, torch.float64, "scores")
+    _dt(n_scores, torch.int32, "n_scores")
+    ids = ids.contiguous()
+    B, S = ids.shape
+    T = scores.shape[0] if scores.dim() == 2 else 0
+    if T and scores.shape[1] != B:
+        raise ValueError(f"scores must be [T, B={B}], got {tuple(scores.shape)}")
+    dev = ids.device
+    So = max(S - 1, 0)
+    score = torch.empty(B, So, dtype=torch.float32, device=dev)
+    lm = torch.empty(B, So, dtype=torch.bool, device=dev)
+    rm = torch.empty(B, So, dtype=torch.bool, device=dev)
+    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    flags = ((_lib.MS_TURN_SCORES if use_turn_scores else 0) | (_lib.MS_RESPONSE_MASK if enable_response_mask else 0)
+             | (_lib.MS_ROLL if roll else 0))
+    check(lib().rmi_masks_and_scores(_ptr(ids), B, S, int(special_token), int(reward_token), _ptr(scores.contiguous()),
+                                     _ptr(n_scores), T, int(n_slots), flags, _ptr(score), _ptr(lm), _ptr(rm), _ptr(err),
+                                     _stream()), "rmi_masks_and_scores")
+    return score, lm, rm, err
+
+
 # ------------------------------------------------------------------------ advantages
 def _mask_u8(mask: torch.Tensor) -> torch.Tensor:
     if mask.dtype == torch.bool:

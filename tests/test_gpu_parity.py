@@ -385,3 +385,60 @@ def test_sokoban_irregular_rooms_vs_oracle(device, frac_irregular, B):
             np.testing.assert_array_equal(h[k][:, ok], getattr(oep, k)[:, ok], err_msg=k)
     if frac_irregular == 0.0:
         assert not bad.any()
+
+
+def _chat_ids(rng, B, S, sp, rt, dup_rate=0.0):
+    """Left-padded chat-shaped token rows: system, then user/assistant turns, each turn
+    <sp> body <rt> [\\n]; some rows get a second reward token inside an assistant turn."""
+    ids = np.full((B, S), 151643, np.int64)
+    for b in range(B):
+        row = [sp] + list(rng.integers(100, 1000, size=int(rng.integers(2, 6)))) + [rt, 198]
+        for _ in range(int(rng.integers(0, 6))):
+            row += [sp] + list(rng.integers(100, 1000, size=int(rng.integers(1, 7)))) + [rt, 198]
+            body = list(rng.integers(100, 1000, size=int(rng.integers(1, 7))))
+            if rng.random() < dup_rate:
+                body.insert(int(rng.integers(0, len(body) + 1)), rt)
+            row += [sp] + body + [rt]
+            if rng.random() < 0.5:
+                row += [198]
+        row = row[-S:]
+        ids[b, S - len(row):] = row
+    return ids
+
+
+@pytest.mark.parametrize("B,S,roll", [(257, 97, True), (300, 130, False), (64, 1, True), (33, 2, True)])
+def test_masks_and_scores_vs_oracle(device, B, S, roll):
+    rng = np.random.default_rng(B * 1000 + S)
+    sp, rt = 151644, 151645
+    ids = _chat_ids(rng, B, S, sp, rt, dup_rate=0.05)
+    n = rng.integers(0, 6, size=B).astype(np.int32)
+    T = 6
+    tab = rng.standard_normal((T, B))
+    for uts in (False, True):
+        for erm in (False, True):
+            for n_slots in (int(n.max()), T + 2):
+                want = oracle.masks_and_scores(ids, sp, rt, tab, n, n_slots, uts, erm, roll)
+                got = ops.masks_and_scores(_t(ids, device), sp, rt, _t(tab, device), _t(n, device), n_slots, uts,
+                                           erm, roll)
+                sc, lm, rm, err = (x.cpu().numpy() for x in got)
+                np.testing.assert_array_equal(lm.astype(np.uint8), want[1])
+                np.testing.assert_array_equal(rm.astype(np.uint8), want[2])
+                if uts:
+                    np.testing.assert_array_equal(err != 0, want[3] != 0)
+                ok = want[3] == 0 if uts else np.ones(B, bool)
+                np.testing.assert_array_equal(sc[ok], want[0][ok])
+
+
+def test_masks_and_scores_full_size(device):
+    """SK-sized token batch (8192 rows x 1024) against the oracle, turn scores + Qwen roll."""
+    rng = np.random.default_rng(5)
+    B, S, T = 8192, 1024, 5
+    sp, rt = 151644, 151645
+    ids = _chat_ids(rng, B, S, sp, rt)
+    n = rng.integers(1, T + 1, size=B).astype(np.int32)
+    tab = rng.standard_normal((T, B))
+    want = oracle.masks_and_scores(ids, sp, rt, tab, n, T, True, True, True)
+    got = ops.masks_and_scores(_t(ids, device), sp, rt, _t(tab, device), _t(n, device), T, True, True, True)
+    for g, w in zip(got[:3], want[:3]):
+        np.testing.assert_array_equal(g.cpu().numpy().astype(w.dtype), w)
+    assert not got[3].any()

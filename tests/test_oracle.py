@@ -235,3 +235,25 @@ def test_host_sokoban_generator_golden():
         np.testing.assert_array_equal(player, d[tag + "_player"].astype(np.int8))
     assert set(d["SimpleSokoban_seeds"][np.nonzero(ops.generate_sokoban_rooms(
         d["SimpleSokoban_seeds"], 6, 6, 1, 300)[3])[0]]) == {3248, 3701}
+
+
+def test_masks_and_scores_golden():
+    """oracle.masks_and_scores == get_masks_and_scores run by the reference (Qwen ids, roll)."""
+    d = load("masks_scores")
+    lens = d["scores_len"]
+    flat = d["scores_flat"]
+    B = len(lens)
+    T = int(lens.max())
+    tab = np.zeros((T, B), np.float64)
+    o = 0
+    for b, n in enumerate(lens):
+        tab[:n, b] = flat[o:o + n]
+        o += n
+    for uts in (False, True):
+        for erm in (False, True):
+            sc, lm, rm, err = oracle.masks_and_scores(d["input_ids"], 151644, 151645, tab, lens, T, uts, erm, True)
+            key = f"uts{int(uts)}_erm{int(erm)}"
+            np.testing.assert_array_equal(sc, d[key + "_score"])
+            np.testing.assert_array_equal(lm, d[key + "_loss_mask"])
+            np.testing.assert_array_equal(rm, d[key + "_response_mask"])
+            assert not err.any()
