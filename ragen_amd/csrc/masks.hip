@@ -3,8 +3,8 @@
 //  rmi_masks_and_scores   get_masks_and_scores (ctx_manager.py:35-70)
 //
 // One wave per row streams the row's token ids in chunks of 256 (4 consecutive ids per lane,
-// 32-B loads): turn = cumsum(ids == <|im_start|>) is a wave prefix scan per chunk plus a
-// running carry, the masks are written as they are produced ([:, :-1] slice), the score row
+// 32-B loads; the loads of 8 chunks are issued together): turn = cumsum(ids == <|im_start|>)
+// is a DPP wave prefix scan per chunk plus a running carry, the masks are written as they are produced ([:, :-1] slice), the score row
 // is zero-filled in the same pass ([:, 1:] slice), and the reward-token positions of each
 // assistant turn are recorded in LDS.  After the pass (stores fenced) the <= 64 turn scores
 // are scattered to their positions (Qwen: rolled by +1) — exactly the boolean-mask
@@ -29,14 +29,19 @@ struct __attribute__((packed, aligned(4))) F4u {
   float x, y, z, w;
 };
 
-__device__ __forceinline__ int wave_inclusive_scan(int x, int lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    x += lane >= o ? y : 0;
-  }
+// 64-lane inclusive prefix sum on DPP (no LDS): row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast:15 / row_bcast:31 carry the row totals across rows (gfx9 DPP).
+__device__ __forceinline__ int wave_inclusive_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
   return x;
 }
+
+constexpr int kSuper = 8;  // chunks whose loads are issued together (2048 ids per row)
 
 __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ ids, int64_t B, int64_t S, int64_t sp,
                                                    int64_t rt, const double* __restrict__ scores,
@@ -59,67 +64,84 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   // an id matching neither special token, for positions past the row end
   const int64_t none = (sp != -1 && rt != -1) ? -1 : ((sp != -2 && rt != -2) ? -2 : -3);
   int carry = 0;
-  for (int64_t c0 = 0; c0 < S; c0 += kChunk) {
-    const int64_t p0 = c0 + kTok * lane;
-    int64_t t[kTok];
-    if (p0 + kTok <= S) {
-      const I64x4 v = *reinterpret_cast<const I64x4*>(row + p0);
-      t[0] = v.a;
-      t[1] = v.b;
-      t[2] = v.c;
-      t[3] = v.d;
-    } else {
+  for (int64_t s0 = 0; s0 < S; s0 += kSuper * kChunk) {
+    // 1. every load of the super-chunk in flight together (clamped addresses, branch-free);
+    //    the group at the row end and groups past it are fixed up element-wise afterwards
+    I64x4 v[kSuper];
 #pragma unroll
-      for (int e = 0; e < kTok; ++e) t[e] = p0 + e < S ? row[p0 + e] : none;
+    for (int k = 0; k < kSuper; ++k) {
+      const int64_t p0 = s0 + k * kChunk + kTok * lane;
+      v[k] = *reinterpret_cast<const I64x4*>(row + (p0 + kTok <= S ? p0 : 0));
     }
-    int st[kTok], c = 0;
+    if (s0 + kSuper * kChunk > S) {
 #pragma unroll
-    for (int e = 0; e < kTok; ++e) {
-      st[e] = t[e] == sp;
-      c += st[e];
-    }
-    const int incl = wave_inclusive_scan(c, lane);
-    int turn = carry + incl - c;
-    carry += __shfl(incl, 63, 64);
-    uint32_t lm = 0, rm = 0;
-#pragma unroll
-    for (int e = 0; e < kTok; ++e) {
-      turn += st[e];  // turn_indicators at p0 + e
-      const uint32_t r = (turn & 1) && turn > 1;
-      const uint32_t l = resp_only ? r : (uint32_t)(turn > 1);
-      rm |= r << (8 * e);
-      lm |= l << (8 * e);
-      if (turn_scores && t[e] == rt && (turn & 1) && turn >= 3) {
-        const int idx = (turn - 3) >> 1;  // turn_indicator = idx * 2 + 3
-        if (idx < n_slots) {
-          atomicAdd(&cnt[idx], 1);
-          pos[idx] = (int)(p0 + e);
+      for (int k = 0; k < kSuper; ++k) {
+        const int64_t p0 = s0 + k * kChunk + kTok * lane;
+        if (p0 + kTok > S) {
+          int64_t e4[kTok];
+          for (int e = 0; e < kTok; ++e) e4[e] = p0 + e < S ? row[p0 + e] : none;
+          v[k] = I64x4{e4[0], e4[1], e4[2], e4[3]};
         }
       }
     }
-    // masks[:, :-1]: columns p < S - 1
-    if (p0 + kTok <= So) {
-      reinterpret_cast<U32u*>(lrow + p0)->x = lm;
-      reinterpret_cast<U32u*>(rrow + p0)->x = rm;
-    } else {
+    // 2. per chunk: turn prefix scan, masks, zero fill, reward positions
 #pragma unroll
-      for (int e = 0; e < kTok; ++e)
-        if (p0 + e < So) {
-          lrow[p0 + e] = (uint8_t)(lm >> (8 * e));
-          rrow[p0 + e] = (uint8_t)(rm >> (8 * e));
+    for (int k = 0; k < kSuper; ++k) {
+      const int64_t p0 = s0 + k * kChunk + kTok * lane;
+      if (s0 + k * kChunk >= S) break;  // wave-uniform
+      const int64_t t[kTok] = {v[k].a, v[k].b, v[k].c, v[k].d};
+      int st[kTok], c = 0;
+#pragma unroll
+      for (int e = 0; e < kTok; ++e) {
+        st[e] = t[e] == sp;
+        c += st[e];
+      }
+      const int incl = wave_inclusive_scan(c);
+      int turn = carry + incl - c;
+      carry += __builtin_amdgcn_readlane(incl, 63);
+      uint32_t lm = 0, rm = 0;
+#pragma unroll
+      for (int e = 0; e < kTok; ++e) {
+        turn += st[e];  // turn_indicators at p0 + e
+        const uint32_t r = (turn & 1) && turn > 1;
+        const uint32_t l = resp_only ? r : (uint32_t)(turn > 1);
+        rm |= r << (8 * e);
+        lm |= l << (8 * e);
+        if (turn_scores && t[e] == rt && (turn & 1) && turn >= 3) {
+          const int idx = (turn - 3) >> 1;  // turn_indicator = idx * 2 + 3
+          if (idx < n_slots) {
+            atomicAdd(&cnt[idx], 1);
+            pos[idx] = (int)(p0 + e);
+          }
         }
-    }
-    // score[:, 1:] zero fill: output column p - 1 for p in [1, S)
-    if (p0 >= 1 && p0 + kTok <= S) {
-      *reinterpret_cast<F4u*>(srow + p0 - 1) = F4u{0.f, 0.f, 0.f, 0.f};
-    } else {
+      }
+      // masks[:, :-1]: columns p < S - 1
+      if (p0 + kTok <= So) {
+        reinterpret_cast<U32u*>(lrow + p0)->x = lm;
+        reinterpret_cast<U32u*>(rrow + p0)->x = rm;
+      } else {
 #pragma unroll
-      for (int e = 0; e < kTok; ++e)
-        if (p0 + e >= 1 && p0 + e < S) srow[p0 + e - 1] = 0.f;
+        for (int e = 0; e < kTok; ++e)
+          if (p0 + e < So) {
+            lrow[p0 + e] = (uint8_t)(lm >> (8 * e));
+            rrow[p0 + e] = (uint8_t)(rm >> (8 * e));
+          }
+      }
+      // score[:, 1:] zero fill: output column p - 1 for p in [1, S)
+      if (p0 >= 1 && p0 + kTok <= S) {
+        *reinterpret_cast<F4u*>(srow + p0 - 1) = F4u{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int e = 0; e < kTok; ++e)
+          if (p0 + e >= 1 && p0 + e < S) srow[p0 + e - 1] = 0.f;
+      }
     }
   }
-  __threadfence();  // the zero fill is complete before the scattered scores land on it
-  __syncthreads();  // LDS position records visible to every lane
+  // the zero fill has completed (this wave's stores retired) before the scattered scores land
+  // on it, and the LDS position records are visible to every lane: a plain counter wait —
+  // a __threadfence() here would add an L2 write-back per row
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
   if (!turn_scores) {
     if (lane == 0) {  // score_tensor[:, -1] = python sum(all_scores[b]), kept by [:, 1:]
       double sum = 0.0;
