@@ -151,11 +151,36 @@ def advantage_leg(R, device, reps=20):
     torch.cuda.synchronize()
     masks_us = e[0].elapsed_time(e[1]) * 1e3 / reps
     mgbs = B * (L + 1) * 14 / (masks_us * 1e-6) / 1e9
+    # bi-level GAE (turn-level rewards at each turn's last response token) and GRPO outcome
+    tr = R.env.ep.turn_reward.t().contiguous().cpu().numpy().astype(np.float32)
+    tr[tr == 0] = 0.5  # a zero turn reward would end the row's high-level segment early
+    rb, vb, mb = synthetic.token_rows(n_turns, score, seed=12, turn_scores=tr)
+    rb, vb, mb = (torch.from_numpy(x).to(device) for x in (rb, vb, mb))
+    seg = torch.arange(0, rb.shape[0] + 1, dtype=torch.int32, device=device)
+    for _ in range(2):
+        ops.bilevel_gae(rb, vb, mb, 1.0, 0.95, 0.95, check_errors=False)
+        ops.grpo_outcome(rb, mb, seg)
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(reps):
+        ops.bilevel_gae(rb, vb, mb, 1.0, 0.95, 0.95, check_errors=False)
+    e[1].record()
+    for _ in range(reps):
+        ops.grpo_outcome(rb, mb, seg)
+    e[2].record()
+    torch.cuda.synchronize()
+    bl_us = e[0].elapsed_time(e[1]) * 1e3 / reps
+    grpo_us = e[1].elapsed_time(e[2]) * 1e3 / reps
+    tok_b = rb.shape[0] * rb.shape[1]
     return {"kernel": "rmi_gae (legacy) + row stats", "rows": B, "cols": L, "tokens_per_launch": tokens,
             "gae_us": gae_us, "whiten_us": whiten_us, "tokens_per_s": tokens / ((gae_us + whiten_us) * 1e-6),
             "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_token": 17,
             "masks_and_scores": {"kernel": "rmi_masks_and_scores", "us": masks_us, "achieved_GBs": mgbs,
-                                 "frac": mgbs / HBM_PEAK_GBS, "bytes_per_token": 14}}
+                                 "frac": mgbs / HBM_PEAK_GBS, "bytes_per_token": 14},
+            "bilevel_gae": {"kernel": "rmi_bilevel_gae", "tokens": tok_b, "us": bl_us,
+                            "achieved_GBs": tok_b * 17 / (bl_us * 1e-6) / 1e9},
+            "grpo": {"kernel": "rmi_grpo_outcome", "tokens": tok_b, "us": grpo_us,
+                     "achieved_GBs": tok_b * 13 / (grpo_us * 1e-6) / 1e9}}
 
 
 def _graph_rollout(step, reps=50, warmup=5):

@@ -361,64 +361,146 @@ __global__ __launch_bounds__(64) void gae_legacy_kernel(const float* __restrict_
   }
 }
 
-// One thread per row, one reverse sweep doing both levels of core_algos.py:44-88.
-__global__ __launch_bounds__(kBlock) void bilevel_kernel(const float* __restrict__ r, const float* __restrict__ v,
-                                                         const uint8_t* __restrict__ mask, int64_t B, int64_t L,
-                                                         float g, float gl, float hg, float hgl,
-                                                         float* __restrict__ adv, float* __restrict__ ret,
-                                                         double* __restrict__ row_stats, uint8_t* __restrict__ err) {
-  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (b >= B) return;
-  const float* rr = r + b * L;
-  const float* vv = v + b * L;
-  const uint8_t* mm = mask + b * L;
-  float* aa = adv + b * L;
-  float* qq = ret + b * L;
-  float hl = 0.0f, ll = 0.0f, v_next_eos = 0.0f, v_next_valid = 0.0f;
-  bool has_eos = false, has_valid = false, bad = false;
-  double s1 = 0.0, s2 = 0.0, cnt = 0.0;
-  for (int64_t t = L - 1; t >= 0; --t) {
-    const float rt = rr[t], vt = vv[t];
-    const bool m = mm[t] != 0;
-    const bool eos = rt != 0.0f || rt != rt;  // token_level_rewards.bool()
-    float a = 0.0f, q = 0.0f, upd = rt;
+// Bi-level GAE on the same tiled stream as the legacy kernel: tiles of 4 rows x 64 columns in
+// a 3-deep register pipeline, staged in LDS (r, v, mask), walked right to left by one lane
+// per row with the exact per-token logic of core_algos.py:44-88 (one reverse sweep doing both levels), the
+// results staged back and stored as 16-B groups.
+struct BilevelState {
+  float hl, ll, v_next_eos, v_next_valid;
+  bool has_eos, has_valid, bad;
+  double s1, s2, cnt;
+};
+
+__device__ __forceinline__ void bilevel_col(float rt, float vt, bool m, float g, float gl, float hg, float hgl,
+                                            BilevelState& w, float& a_out, float& q_out) {
+  const bool eos = rt != 0.0f || rt != rt;  // token_level_rewards.bool()
+  float a = 0.0f, q = 0.0f, upd = rt;
+  if (eos) {
+    const float delta = (rt + (w.has_eos ? hg * w.v_next_eos : 0.0f)) - vt;
+    w.hl = delta + hgl * w.hl;
+    a = w.hl;
+    upd = w.hl + vt;  // updated_reward = advantages + values
+    q = upd;          // returns = advantages + values
+    w.v_next_eos = vt;
+    w.has_eos = true;
+  }
+  if (m) {
+    float nvv;
     if (eos) {
-      const float delta = (rt + (has_eos ? hg * v_next_eos : 0.0f)) - vt;
-      hl = delta + hgl * hl;
-      a = hl;
-      upd = hl + vt;  // updated_reward = advantages + values
-      q = upd;        // returns = advantages + values
-      v_next_eos = vt;
-      has_eos = true;
+      nvv = 0.0f;
+      w.ll = 0.0f;
+    } else {
+      if (!w.has_valid) w.bad = true;  // valid_positions[i + 1] -> IndexError
+      nvv = w.v_next_valid;
     }
-    if (m) {
-      float nvv;
-      if (eos) {
-        nvv = 0.0f;
-        ll = 0.0f;
+    const float delta = (upd + g * nvv) - vt;
+    w.ll = delta + gl * w.ll;
+    a = w.ll;
+    q = w.ll + vt;
+    w.v_next_valid = vt;
+    w.has_valid = true;
+    w.s1 += (double)a;
+    w.s2 += (double)a * (double)a;
+    w.cnt += 1.0;
+  }
+  a_out = a;
+  q_out = q;
+}
+
+__device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, BilevelState& w, float* sr, float* sv,
+                                             uint8_t* sm, int lane, bool walker, int64_t row0, int64_t B, int64_t L,
+                                             float g, float gl, float hg, float hgl, float* __restrict__ adv,
+                                             float* __restrict__ ret) {
+  const int grp = lane & 15;
+#pragma unroll
+  for (int j = 0; j < kGLoads; ++j) {
+    const int row = 4 * j + (lane >> 4);
+    *reinterpret_cast<F4*>(sr + row * kGStr + 4 * grp) = cur.r[j];
+    *reinterpret_cast<F4*>(sv + row * kGStr + 4 * grp) = cur.v[j];
+    *reinterpret_cast<uint32_t*>(sm + row * kGMStr + 4 * grp) = cur.m[j];
+  }
+  __syncthreads();
+  if (walker) {
+    float* pr = sr + lane * kGStr;
+    float* pv = sv + lane * kGStr;
+    const uint8_t* pm = sm + lane * kGMStr;
+    for (int q = kGCols / 4 - 1; q >= 0; --q) {
+      const F4 r4 = *reinterpret_cast<const F4*>(pr + 4 * q);
+      const F4 v4 = *reinterpret_cast<const F4*>(pv + 4 * q);
+      const uint32_t m4 = *reinterpret_cast<const uint32_t*>(pm + 4 * q);
+      F4 a4, t4;
+      bilevel_col(r4.w, v4.w, (m4 >> 24) & 0xFF, g, gl, hg, hgl, w, a4.w, t4.w);
+      bilevel_col(r4.z, v4.z, (m4 >> 16) & 0xFF, g, gl, hg, hgl, w, a4.z, t4.z);
+      bilevel_col(r4.y, v4.y, (m4 >> 8) & 0xFF, g, gl, hg, hgl, w, a4.y, t4.y);
+      bilevel_col(r4.x, v4.x, m4 & 0xFF, g, gl, hg, hgl, w, a4.x, t4.x);
+      *reinterpret_cast<F4*>(pr + 4 * q) = a4;
+      *reinterpret_cast<F4*>(pv + 4 * q) = t4;
+    }
+  }
+  __syncthreads();
+  const int64_t col = c0 + 4 * grp;
+#pragma unroll
+  for (int j = 0; j < kGLoads; ++j) {
+    const int row = 4 * j + (lane >> 4);
+    const int64_t grow = row0 + row;
+    if (grow < B && col >= 0 && col < L) {
+      const F4 a4 = *reinterpret_cast<const F4*>(sr + row * kGStr + 4 * grp);
+      const F4 t4 = *reinterpret_cast<const F4*>(sv + row * kGStr + 4 * grp);
+      const int64_t o = grow * L + col;
+      if (col + 4 <= L) {
+        *reinterpret_cast<F4*>(adv + o) = a4;
+        *reinterpret_cast<F4*>(ret + o) = t4;
       } else {
-        if (!has_valid) bad = true;  // valid_positions[i + 1] -> IndexError
-        nvv = v_next_valid;
+        const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
+        for (int e = 0; e < 4; ++e)
+          if (col + e < L) {
+            adv[o + e] = aa[e];
+            ret[o + e] = tt[e];
+          }
       }
-      const float delta = (upd + g * nvv) - vt;
-      ll = delta + gl * ll;
-      a = ll;
-      q = ll + vt;
-      v_next_valid = vt;
-      has_valid = true;
-      s1 += (double)a;
-      s2 += (double)a * (double)a;
-      cnt += 1.0;
     }
-    aa[t] = a;
-    qq[t] = q;
   }
-  if (row_stats) {
-    row_stats[3 * b + 0] = s1;
-    row_stats[3 * b + 1] = s2;
-    row_stats[3 * b + 2] = cnt;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restrict__ r, const float* __restrict__ v,
+                                                           const uint8_t* __restrict__ mask, int64_t B, int64_t L,
+                                                           float g, float gl, float hg, float hgl,
+                                                           float* __restrict__ adv, float* __restrict__ ret,
+                                                           double* __restrict__ row_stats,
+                                                           uint8_t* __restrict__ err) {
+  __shared__ __attribute__((aligned(16))) float sr[kGRows * kGStr];
+  __shared__ __attribute__((aligned(16))) float sv[kGRows * kGStr];
+  __shared__ __attribute__((aligned(16))) uint8_t sm[kGRows * kGMStr];
+  const int lane = threadIdx.x;
+  const int64_t row0 = (int64_t)blockIdx.x * kGRows;
+  const int64_t ntiles = (L + kGCols - 1) / kGCols;
+  const bool walker = lane < kGRows && row0 + lane < B;
+  BilevelState w;
+  w.hl = w.ll = w.v_next_eos = w.v_next_valid = 0.0f;
+  w.has_eos = w.has_valid = w.bad = false;
+  w.s1 = w.s2 = w.cnt = 0.0;
+  GaeTile ta, tb, tc;
+  const int64_t k0 = ntiles - 1;
+  gae_load_tile(ta, r, v, mask, B, L, row0, k0 * kGCols, lane);
+  gae_load_tile(tb, r, v, mask, B, L, row0, (k0 - 1) * kGCols, lane);
+  for (int64_t k = k0; k >= 0; k -= 3) {
+    gae_load_tile(tc, r, v, mask, B, L, row0, (k - 2) * kGCols, lane);
+    bilevel_tile(ta, k * kGCols, w, sr, sv, sm, lane, walker, row0, B, L, g, gl, hg, hgl, adv, ret);
+    gae_load_tile(ta, r, v, mask, B, L, row0, (k - 3) * kGCols, lane);
+    bilevel_tile(tb, (k - 1) * kGCols, w, sr, sv, sm, lane, walker, row0, B, L, g, gl, hg, hgl, adv, ret);
+    gae_load_tile(tb, r, v, mask, B, L, row0, (k - 4) * kGCols, lane);
+    bilevel_tile(tc, (k - 2) * kGCols, w, sr, sv, sm, lane, walker, row0, B, L, g, gl, hg, hgl, adv, ret);
   }
-  if (err) err[b] = bad ? RMI_ERR_INDEX : 0;
+  if (walker) {
+    const int64_t row = row0 + lane;
+    if (row_stats) {
+      row_stats[3 * row + 0] = w.s1;
+      row_stats[3 * row + 1] = w.s2;
+      row_stats[3 * row + 2] = w.cnt;
+    }
+    if (err) err[row] = w.bad ? RMI_ERR_INDEX : 0;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void row_stats_kernel(const float* __restrict__ x,
@@ -579,8 +661,8 @@ RMI_API int rmi_bilevel_gae(const float* r, const float* v, const uint8_t* mask,
   using namespace rmi;
   if (!r || !v || !mask || !adv || !ret || B < 0 || L < 0) return RMI_EINVAL;
   if (B == 0 || L == 0) return RMI_OK;
-  hipLaunchKernelGGL(bilevel_kernel, dim3((unsigned)((B + kBlock - 1) / kBlock)), dim3(kBlock), 0, as_stream(stream),
-                     r, v, mask, B, L, (float)gamma, (float)(gamma * lam), (float)high_level_gamma,
+  hipLaunchKernelGGL(bilevel_tiled_kernel, dim3((unsigned)((B + kGRows - 1) / kGRows)), dim3(64), 0,
+                     as_stream(stream), r, v, mask, B, L, (float)gamma, (float)(gamma * lam), (float)high_level_gamma,
                      (float)(high_level_gamma * lam), adv, ret, row_stats, err);
   return launch_status();
 }
