@@ -569,9 +569,26 @@ __device__ double countdown_reward(const uint8_t* s, int n, const int32_t* nums,
   return score;
 }
 
+// An answer string is parsed byte by byte twice (check_format, then the evaluator): staged
+// once into this thread's LDS row with independent 4-B loads, the parse reads LDS instead of
+// paying a global-memory round trip per byte.
+constexpr int kStageMax = 256;  // answers up to this many bytes are staged (Lmax above: parsed in place)
+__device__ __forceinline__ const uint8_t* stage_answer(const uint8_t* g, int n, bool words_in_slot, uint8_t* lds_row) {
+  if (words_in_slot && (reinterpret_cast<uintptr_t>(g) & 3u) == 0) {
+    const uint32_t* g4 = reinterpret_cast<const uint32_t*>(g);
+    uint32_t* l4 = reinterpret_cast<uint32_t*>(lds_row);
+    const int nw = (n + 3) >> 2;
+    for (int i = 0; i < nw; ++i) l4[i] = g4[i];  // up to 3 bytes past n, still inside the [Lmax] slot
+  } else {
+    for (int i = 0; i < n; ++i) lds_row[i] = g[i];
+  }
+  return lds_row;
+}
+
 struct CountdownDev {
   const uint8_t* answers;  // this env's [K, Lmax]
   const int32_t* lens;     // this env's [K]
+  uint8_t* stage;          // this thread's LDS row (nullptr: parse global memory in place)
   int Lmax;
   const int32_t* nums;
   int n_nums;
@@ -586,7 +603,9 @@ struct CountdownDev {
     int n = lens[k];
     if (n > Lmax) n = Lmax;
     uint8_t fl;
-    reward = countdown_reward(answers + (int64_t)k * Lmax, n, nums, n_nums, target, score, format_score, fl, err);
+    const uint8_t* src = answers + (int64_t)k * Lmax;
+    if (stage && n > 0) src = stage_answer(src, n, ((n + 3) & ~3) <= Lmax, stage);
+    reward = countdown_reward(src, n, nums, n_nums, target, score, format_score, fl, err);
     done = true;
     eff = reward > 0;
     success = reward == score;
@@ -598,6 +617,7 @@ __global__ __launch_bounds__(kBlock) void countdown_step_turn_kernel(rmi_countdo
                                                                      rmi_turn_t in, const uint8_t* __restrict__ answers,
                                                                      const int32_t* __restrict__ answer_len, int Lmax,
                                                                      uint8_t* __restrict__ err_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t stage_lds[];  // [kBlock][round4(Lmax) + 4]
   const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int B = ep.B;
   if (b >= B) return;
@@ -607,6 +627,7 @@ __global__ __launch_bounds__(kBlock) void countdown_step_turn_kernel(rmi_countdo
   CountdownDev e;
   e.answers = answers + b * (int64_t)in.K * Lmax;
   e.lens = answer_len + b * (int64_t)in.K;
+  e.stage = Lmax <= kStageMax ? stage_lds + threadIdx.x * (((Lmax + 3) & ~3) + 4) : nullptr;
   e.Lmax = Lmax;
   e.nums = env.nums + b * (int64_t)env.max_nums;
   e.n_nums = env.n_nums[b];
@@ -666,7 +687,8 @@ RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episod
   if (!answers || !answer_len || !env->nums || !env->n_nums || !env->target || !in->n_actions || !ep->num_actions ||
       !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
     return RMI_EINVAL;
-  hipLaunchKernelGGL(countdown_step_turn_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), 0,
+  const size_t lds = Lmax <= kStageMax ? (size_t)kBlock * (((Lmax + 3) & ~3) + 4) : 0;
+  hipLaunchKernelGGL(countdown_step_turn_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), lds,
                      as_stream(stream), *env, *ep, *in, answers, answer_len, Lmax, err);
   return launch_status();
 }

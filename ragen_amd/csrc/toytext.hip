@@ -15,6 +15,8 @@ namespace {
 
 struct FrozenLakeDev {
   const uint8_t* desc;  // this env's row
+  uint64_t d_lo, d_hi;  // the row itself when it has <= 16 cells (loaded once; no per-step load)
+  bool in_regs;
   int nrow, ncol, s;
   bool slippery;
   double cs0, cs1, cs2;
@@ -28,13 +30,17 @@ struct FrozenLakeDev {
     else row = row - 1 < 0 ? 0 : row - 1;                              // UP
     return row * ncol + col;
   }
+  __device__ __forceinline__ uint8_t cell(int i) const {
+    if (in_regs) return (uint8_t)((i < 8 ? d_lo >> (8 * i) : d_hi >> (8 * (i - 8))) & 0xFF);
+    return desc[i];
+  }
   // action ids 1..4 -> gym 0..3 via FrozenLakeEnvConfig.action_map (frozen_lake/config.py:15)
   __device__ __forceinline__ bool step(int a, double& reward, bool& done, bool& eff, bool& success) {
     if (a < 1 || a > 4) return false;
     const int ga = a - 1;
     const int prev = s;
     const double u = rng.next_double();  // categorical_sample draw
-    const uint8_t letter = desc[s];
+    const uint8_t letter = cell(s);
     if (letter == 'G' || letter == 'H') {  // P[s][a] = [(1.0, s, 0, True)]
       reward = 0.0;
       done = true;
@@ -45,12 +51,12 @@ struct FrozenLakeDev {
         b = (ga + 3 + i) & 3;
       }
       s = inc(s, b);
-      const uint8_t nl = desc[s];
+      const uint8_t nl = cell(s);
       reward = (nl == 'G') ? 1.0 : 0.0;
       done = (nl == 'G' || nl == 'H');
     }
     eff = prev != s;                   // frozen_lake/env.py:43
-    success = desc[s] == 'G';
+    success = cell(s) == 'G';
     return true;
   }
 };
@@ -60,12 +66,29 @@ __global__ __launch_bounds__(kBlock) void frozenlake_step_turn_kernel(rmi_frozen
   const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int B = ep.B;
   if (b >= B) return;
+  // every load of the turn is issued before the first use (one memory round trip)
   uint8_t flags = ep.flags[b];
-  const bool act = in.has_input ? (in.has_input[b] != 0) : !(flags & RMI_FLAG_DONE);
-  if (!act) return;
+  const uint8_t has_in = in.has_input ? in.has_input[b] : 0;
+  int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
+  double penalty = ep.penalty[b];
+  const int n_act = in.n_actions[b];
+  const uint64_t acts = load_actions(in.actions + b * (int64_t)in.K, in.K);
   const int n = env.nrow * env.ncol;
   FrozenLakeDev e;
   e.desc = env.desc + b * n;
+  e.in_regs = n <= 16;
+  e.d_lo = e.d_hi = 0;
+  if (n == 16 && (reinterpret_cast<uintptr_t>(env.desc) & 15u) == 0) {  // the 4x4 default: one 16-B load
+    const uint4 q = *reinterpret_cast<const uint4*>(e.desc);
+    e.d_lo = ((uint64_t)q.y << 32) | q.x;
+    e.d_hi = ((uint64_t)q.w << 32) | q.z;
+  } else if (e.in_regs) {
+    for (int i = 0; i < n; ++i) {
+      const uint64_t c = e.desc[i];
+      if (i < 8) e.d_lo |= c << (8 * i);
+      else e.d_hi |= c << (8 * (i - 8));
+    }
+  }
   e.nrow = env.nrow;
   e.ncol = env.ncol;
   e.s = env.s[b];
@@ -74,15 +97,15 @@ __global__ __launch_bounds__(kBlock) void frozenlake_step_turn_kernel(rmi_frozen
   e.cs1 = env.cs1;
   e.cs2 = env.cs2;
   e.rng = load_pcg(env.rng, B, b);
+  const bool act = in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE);
+  if (!act) return;
   uint8_t err = 0;
   if (e.s < 0 || e.s >= n) {
     if (err_out) err_out[b] |= RMI_ERR_STATE;
     return;
   }
-  int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
-  double penalty = ep.penalty[b];
-  TurnOut o = run_turn(e, load_actions(in.actions + b * (int64_t)in.K, in.K), in.n_actions[b], in.K, num_actions, flags, n_turns,
-                       penalty, in.max_actions_per_traj, in.format_penalty, err);
+  TurnOut o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
+                       in.format_penalty, err);
   ep.num_actions[b] = num_actions;
   ep.flags[b] = flags;
   ep.n_turns[b] = n_turns;
