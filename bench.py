@@ -298,6 +298,33 @@ def api_leg(device):
             "note": "EnvStateManager.step facade, 8192 envs x 5 turns, host dicts + text obs each turn"}
 
 
+def cpu_baseline_parallel(R, workers=16, reps=6):
+    """SURVEY §8(d) CPU baseline (b): one process per host core (the box's 16-core share),
+    env groups partitioned across processes, no shared state.  Worker w runs ``reps`` rollouts
+    of the 2048-env slice (w % 4) of this rank's batch; value = all workers' env steps / wall
+    time of the parallel phase (process start-up excluded)."""
+    import multiprocessing as mp
+    from oracle import port
+    n_envs = 2048
+    jobs = []
+    for w in range(workers):
+        lo = (w % (B_PER_GPU // n_envs)) * n_envs
+        sl = slice(lo, lo + n_envs)
+        jobs.append((R.env.room_fixed[sl].cpu().numpy(), R.env.init_state[sl].cpu().numpy(),
+                     R.env.init_player[sl].cpu().numpy(), R.ids[:, sl].cpu().numpy(), R.n[:, sl].cpu().numpy(),
+                     MAX_ACTIONS, reps))
+    ctx = mp.get_context("spawn")  # a child process per worker (no fork of this GPU process)
+    with ctx.Pool(workers) as pool:
+        pool.map(abs, range(workers))  # workers started and warm
+        t0 = time.perf_counter()
+        res = pool.starmap(port.timed_rollouts, jobs)
+        wall = time.perf_counter() - t0
+    steps = sum(r[0] for r in res)
+    return {"value": steps / wall, "unit": "env-steps/s", "cores": workers, "kind": "port",
+            "sample": f"{workers} processes x {reps} rollouts of {n_envs} envs x {T_TURNS} turns, {steps} env.step "
+                      f"calls in {wall:.1f}s wall, oracle/port.py"}
+
+
 def cpu_baseline(R, seconds_budget=20.0):
     """Reference-shaped CPU path (oracle/port.py: per-env Python objects mirroring
     EnvStateManager.step + SokobanEnv.step) on a bounded sample of the same workload:
@@ -339,11 +366,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    torch.cuda.set_device(local)  # before the process group: RCCL binds its communicator to this device
+    device = torch.device("cuda", local)
     if dist:
         import torch.distributed as tdist
-        tdist.init_process_group("nccl")
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+        tdist.init_process_group("nccl", device_id=device)
 
     R = Rollout(device, rank)
     # env steps per rollout (deterministic: every replay executes the same actions)
@@ -428,12 +455,16 @@ def main():
     api = api_leg(device) if not args.no_extras and rank == 0 else None
 
     if rank == 0:
-        cpu = None
+        cpu = cpu_par = None
         if not args.no_cpu_baseline and world == 1:
             try:
                 cpu = cpu_baseline(R)
             except Exception as ex:  # the baseline must never break the bench line
                 cpu = {"value": None, "unit": "env-steps/s", "cores": 1, "kind": "port", "sample": f"failed: {ex}"}
+            try:
+                cpu_par = cpu_baseline_parallel(R)
+            except Exception as ex:
+                cpu_par = {"value": None, "sample": f"failed: {ex}"}
         value = total_steps / elapsed
         line = {
             "metric": "env-steps/sec (whole node), Sokoban 6x6, 8192 envs x 5 turns",
@@ -459,6 +490,7 @@ def main():
                          "kernel": "rmi_sokoban_step_turn", "avg_launch_us": avg_launch_us,
                          "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn},
             "cpu_baseline": cpu,
+            "cpu_baseline_parallel": cpu_par,
             "advantage": adv,
             "toytext": toytext,
             "api_variant": api,

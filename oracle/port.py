@@ -164,3 +164,16 @@ def sokoban_rollout(envs, ids, n, max_actions=10):
         if not active:
             break
     return sum(e["env"].num_env_steps for e in envs) - steps0
+
+
+def timed_rollouts(fixed, state0, player0, ids, n, max_actions, reps):
+    """``reps`` fresh rollouts of these envs (reset excluded from timing) -> (env steps, seconds).
+    The unit of work of bench.py's multi-process CPU baseline (one call per worker process)."""
+    import time
+    steps, dt = 0, 0.0
+    for _ in range(reps):
+        envs = make_sokoban_envs(fixed, state0, player0)
+        t0 = time.perf_counter()
+        steps += sokoban_rollout(envs, ids, n, max_actions)
+        dt += time.perf_counter() - t0
+    return steps, dt
