@@ -126,6 +126,14 @@ int rmi_sokoban_generate_rooms(const int64_t* seeds /*[host][n]*/, int32_t n, in
                                int8_t* player /*[host][n,2]*/, uint8_t* status /*[host][n]*/,
                                int32_t n_threads);
 
+/* Replaces: SokobanEnv.render text mode (sokoban/env.py:53-61): room_state, the player on a
+ * target shown as code 6, each code through the config's grid_lookup, rows joined by '\n'.
+ * glyph_bytes[16] / glyph_len[16] (HOST memory): UTF-8 bytes of each code packed little-endian,
+ * length 0..4 (0 = absent: rendered '?').  out u8[B, stride] (device, 4-B aligned, stride a
+ * multiple of 4 and >= H*W*4 + H - 1), len i32[B] bytes written.                         */
+int rmi_sokoban_render(const rmi_sokoban_t* env, int32_t B, const uint32_t* glyph_bytes, const uint8_t* glyph_len,
+                       uint8_t* out, int32_t stride, int32_t* len, rmi_stream_t stream);
+
 /* --------------------------------------------------------------------- FrozenLake
  * Replaces: FrozenLakeEnv.step (frozen_lake/env.py:39-45) -> gymnasium FrozenLakeEnv.step
  *           + categorical_sample (third-party, App. A.2), numpy PCG64 draws (App. A.5). */
@@ -140,6 +148,13 @@ typedef struct {
 
 int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                              uint8_t* err, rmi_stream_t stream);
+
+/* Replaces: FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61): codes P=0 (player), floor
+ * (S, F) 1, hole 2, goal 3, player in a hole 4, player on the goal 5, through grid_lookup;
+ * glyph table and output as rmi_sokoban_render (stride >= nrow*ncol*4 + nrow - 1).        */
+int rmi_frozenlake_render(const rmi_frozenlake_t* env, int32_t B, const uint32_t* glyph_bytes,
+                          const uint8_t* glyph_len, uint8_t* out, int32_t stride, int32_t* len,
+                          rmi_stream_t stream);
 
 /* ------------------------------------------------------------------------- Bandit
  * Replaces: BanditEnv.step/compute_reward (bandit/env.py:62-76).                       */

@@ -224,6 +224,23 @@ def masks_and_scores(ids, sp, rt, scores_tb, n_scores, n_slots, use_turn_scores,
     return score, lm, rm, err
 
 
+def sokoban_render(state, fixed, H, W, lookup):
+    """SokobanEnv.render text (sokoban/env.py:53-61) of one env: player on target -> 6."""
+    room = np.where((state == 5) & (fixed == 2), 6, state).reshape(H, W)
+    return "\n".join("".join(lookup.get(int(c), "?") for c in row) for row in room.tolist())
+
+
+def frozenlake_render(desc, s, n, lookup):
+    """FrozenLakeEnv.render text (frozen_lake/env.py:47-61) of one env (desc: bytes of the map)."""
+    d = np.asarray(desc).reshape(n, n)
+    ml = {ord("P"): 0, ord("F"): 1, ord("H"): 2, ord("G"): 3, ord("S"): 1}
+    codes = np.vectorize(lambda x: ml.get(int(x), 1))(d)
+    if 0 <= s < n * n:
+        letter = d[s // n, s % n]
+        codes[s // n, s % n] = 4 if letter == ord("H") else 5 if letter == ord("G") else 0
+    return "\n".join("".join(lookup.get(int(c), "?") for c in row) for row in codes)
+
+
 def check_format(equation, nums):  # countdown/env.py:9-14
     try:
         nums_in_eq = [int(n) for n in re.findall(r"\d+", equation)]

@@ -25,7 +25,8 @@ class BatchEnv:
         self.device = torch.device(device if device is not None else "cuda")
         self.ep = ops.EpisodeState.empty(self.B, self.T, self.device)
         self.seeds = np.zeros(self.B, np.int64)
-        self._host = None  # lazily synced host mirror for render()
+        self._host = None  # lazily synced host mirror (env-specific use)
+        self._text = None  # this turn's observations, rendered on the device for every env at once
 
     # --- API ----------------------------------------------------------------------
     def reset(self, seeds) -> None:
@@ -37,6 +38,10 @@ class BatchEnv:
         raise NotImplementedError
 
     def render(self, i: int) -> str:
+        return self.render_all()[i]
+
+    def render_all(self) -> List[str]:
+        """Observation text of every env, cached until the state changes."""
         raise NotImplementedError
 
     def action_lookup(self, i: int) -> Optional[Dict[int, str]]:
@@ -54,10 +59,12 @@ class BatchEnv:
 
     def close(self):
         self._host = None
+        self._text = None
 
     # --- helpers ------------------------------------------------------------------
     def _invalidate(self):
         self._host = None
+        self._text = None
 
     def expand_seeds(self, base_seed: int, group_size: int, first_group: int = 0) -> np.ndarray:
         """es_manager.py:80-82: env i of the batch gets base + (global group index)."""

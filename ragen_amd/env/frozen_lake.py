@@ -112,19 +112,9 @@ class FrozenLakeBatch(BatchEnv):
         ops.frozenlake_step_turn(self.struct(), self.ep, t, err)
         self._invalidate()
 
-    # FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61)
-    def render(self, i: int) -> str:
-        if self._host is None:
-            self._host = (self.desc.cpu().numpy(), self.s.cpu().numpy())
-        desc, s = self._host
-        n = self.ncol
-        d = desc[i].reshape(self.nrow, n)
-        pr, pc = int(s[i]) // n, int(s[i]) % n
-        ml = {ord("P"): 0, ord("F"): 1, ord("H"): 2, ord("G"): 3}
-        room = np.where(d == ord("S"), ord("F"), d)
-        room[pr, pc] = ord("P")
-        codes = np.vectorize(lambda x: ml[int(x)])(room)
-        letter = d[pr, pc]
-        codes[pr, pc] = 4 if letter == ord("H") else 5 if letter == ord("G") else 0
-        lk = self.config.grid_lookup
-        return "\n".join("".join(lk.get(int(c), "?") for c in row) for row in codes)
+    # FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61): one device kernel for every env
+    def render_all(self):
+        if self._text is None:
+            out, n = ops.frozenlake_render(self.struct(), self.B, self.config.grid_lookup, self.device)
+            self._text = ops.decode_rows(out, n)
+        return self._text

@@ -79,11 +79,9 @@ class SokobanBatch(BatchEnv):
         ops.sokoban_step_turn(self.struct(), self.ep, t, err)
         self._invalidate()
 
-    # SokobanEnv.render text mode (sokoban/env.py:53-57)
-    def render(self, i: int) -> str:
-        if self._host is None:
-            self._host = (self.room_state.cpu().numpy(), self.room_fixed.cpu().numpy())
-        st, fx = self._host
-        room = np.where((st[i] == 5) & (fx[i] == 2), 6, st[i]).reshape(self.H, self.W)
-        lk = self.config.grid_lookup
-        return "\n".join("".join(lk.get(int(c), "?") for c in row) for row in room.tolist())
+    # SokobanEnv.render text mode (sokoban/env.py:53-61): one device kernel for every env
+    def render_all(self):
+        if self._text is None:
+            out, n = ops.sokoban_render(self.struct(), self.B, self.config.grid_lookup, self.device)
+            self._text = ops.decode_rows(out, n)
+        return self._text

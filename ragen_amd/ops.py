@@ -241,6 +241,47 @@ def row_sum(x: torch.Tensor) -> torch.Tensor:
     return out
 
 
+# ------------------------------------------------------------- text observations (A6)
+def glyph_table(lookup):
+    """grid_lookup {code: str} -> (u32[16] packed UTF-8, u8[16] lengths) host arrays."""
+    gb = np.zeros(16, np.uint32)
+    gl = np.zeros(16, np.uint8)
+    for code, ch in (lookup or {}).items():
+        if 0 <= int(code) < 16:
+            b = str(ch).encode("utf-8")
+            if len(b) > 4:
+                raise ValueError(f"glyph for {code} longer than 4 UTF-8 bytes")
+            gb[int(code)] = int.from_bytes(b.ljust(4, b"\0"), "little")
+            gl[int(code)] = len(b)
+    return gb, gl
+
+
+def _render(fn, env_struct, B: int, cells: int, rows: int, lookup, device):
+    gb, gl = glyph_table(lookup)
+    stride = (cells * 4 + rows - 1 + 3) // 4 * 4
+    out = torch.empty(B, stride, dtype=torch.uint8, device=device)
+    n = torch.empty(B, dtype=torch.int32, device=device)
+    check(fn(env_struct, B, gb.ctypes.data, gl.ctypes.data, _ptr(out), stride, _ptr(n), _stream()), fn.__name__)
+    return out, n
+
+
+def decode_rows(out: torch.Tensor, n: torch.Tensor):
+    """u8[B, stride] + i32[B] lengths -> list of str (one host copy, one decode per row)."""
+    buf = out.cpu().numpy()
+    lens = n.cpu().numpy()
+    return [buf[i, :lens[i]].tobytes().decode("utf-8") for i in range(len(lens))]
+
+
+def sokoban_render(env: _lib.Sokoban, B: int, lookup, device):
+    """SokobanEnv.render text of every env (sokoban/env.py:53-61) -> (u8[B,stride], i32[B])."""
+    return _render(lib().rmi_sokoban_render, env, B, env.H * env.W, env.H, lookup, device)
+
+
+def frozenlake_render(env: _lib.FrozenLake, B: int, lookup, device):
+    """FrozenLakeEnv.render text of every env (frozen_lake/env.py:47-61) -> (u8[B,stride], i32[B])."""
+    return _render(lib().rmi_frozenlake_render, env, B, env.nrow * env.ncol, env.nrow, lookup, device)
+
+
 # ------------------------------------------------------------------- token masks (A11)
 def masks_and_scores(ids: torch.Tensor, special_token: int, reward_token: int, scores: torch.Tensor,
                      n_scores: torch.Tensor, n_slots: int, use_turn_scores: bool, enable_response_mask: bool,

@@ -442,3 +442,30 @@ def test_masks_and_scores_full_size(device):
     for g, w in zip(got[:3], want[:3]):
         np.testing.assert_array_equal(g.cpu().numpy().astype(w.dtype), w)
     assert not got[3].any()
+
+
+def test_render_vs_oracle(device):
+    """Device text observations == the reference's render, incl. unknown
+    codes ('?'), multi-byte glyphs and players on targets / holes / goals."""
+    rng = np.random.default_rng(9)
+    B = 777
+    env = SokobanBatch(SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100), B, 2, 5, device)
+    env.reset(synthetic.env_seeds(B))
+    st = env.room_state.cpu().numpy()
+    fx = env.room_fixed.cpu().numpy()
+    st[:100] = rng.integers(0, 20, size=(100, 36))
+    fx[:100] = rng.integers(0, 3, size=(100, 36))
+    env.room_state.copy_(torch.from_numpy(st))
+    env.room_fixed.copy_(torch.from_numpy(fx))
+    env._invalidate()
+    lk = env.config.grid_lookup
+    got = env.render_all()
+    assert got == [oracle.sokoban_render(st[i], fx[i], 6, 6, lk) for i in range(B)]
+    fl = FrozenLakeBatch(FrozenLakeEnvConfig(), B, 2, 5, device)
+    fl.reset(synthetic.env_seeds(B))
+    s = rng.integers(0, 16, size=B).astype(np.int32)
+    fl.s.copy_(torch.from_numpy(s))
+    fl._invalidate()
+    desc = fl.desc.cpu().numpy()
+    assert fl.render_all() == [oracle.frozenlake_render(desc[i], int(s[i]), 4, fl.config.grid_lookup)
+                               for i in range(B)]
