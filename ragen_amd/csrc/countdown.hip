@@ -54,13 +54,28 @@ __device__ __forceinline__ int utf8_next(const uint8_t* s, int n, int i, uint32_
   return len;
 }
 
-// check_format: sorted([int(x) for x in re.findall(r'\d+', eq)]) == sorted(nums)
-__device__ bool check_format(const uint8_t* s, int n, const int32_t* nums, int n_nums) {
-  constexpr int kMax = 8;
-  uint64_t found[kMax];
+// check_format: sorted([int(x) for x in re.findall(r'\d+', eq)]) == sorted(nums).
+// The digit runs and the numbers live in registers (every array index is a compile-time
+// constant after unrolling), so nothing of this goes through scratch memory.
+constexpr int kMaxNums = 8;
+__device__ bool check_format(const uint8_t* s, int n, const int32_t (&nums)[kMaxNums], int n_nums) {
+  uint64_t found[kMaxNums];
+#pragma unroll
+  for (int k = 0; k < kMaxNums; ++k) found[k] = 0;
   int nf = 0;
   bool in_run = false, overflow = false, too_many = false;
   uint64_t cur = 0;
+  auto close_run = [&]() {
+    if (nf < kMaxNums) {
+      const uint64_t val = overflow ? 0xFFFFFFFFFFFFFFFFull : cur;
+#pragma unroll
+      for (int k = 0; k < kMaxNums; ++k)
+        if (k == nf) found[k] = val;
+      nf++;
+    } else {
+      too_many = true;
+    }
+  };
   for (int i = 0; i < n;) {
     uint32_t cp;
     const int len = utf8_next(s, n, i, cp);
@@ -75,28 +90,27 @@ __device__ bool check_format(const uint8_t* s, int n, const int32_t* nums, int n
       else cur = cur * 10 + (uint64_t)d;
     } else if (in_run) {
       in_run = false;
-      if (nf < kMax) found[nf++] = overflow ? 0xFFFFFFFFFFFFFFFFull : cur;
-      else too_many = true;
+      close_run();
     }
     i += len;
   }
-  if (in_run) {
-    if (nf < kMax) found[nf++] = overflow ? 0xFFFFFFFFFFFFFFFFull : cur;
-    else too_many = true;
-  }
+  if (in_run) close_run();
   if (too_many || nf != n_nums) return false;
   // multiset equality: match every num (nums may be negative -> never equal a digit run)
-  bool used[kMax] = {false, false, false, false, false, false, false, false};
-  for (int j = 0; j < n_nums; ++j) {
-    bool hit = false;
-    for (int k = 0; k < nf; ++k) {
-      if (!used[k] && nums[j] >= 0 && found[k] == (uint64_t)nums[j]) {
-        used[k] = true;
-        hit = true;
-        break;
+  uint32_t used = 0;
+#pragma unroll
+  for (int j = 0; j < kMaxNums; ++j) {
+    if (j < n_nums) {
+      bool hit = false;
+#pragma unroll
+      for (int k = 0; k < kMaxNums; ++k) {
+        if (!hit && k < nf && !((used >> k) & 1) && nums[j] >= 0 && found[k] == (uint64_t)nums[j]) {
+          used |= 1u << k;
+          hit = true;
+        }
       }
+      if (!hit) return false;
     }
-    if (!hit) return false;
   }
   return true;
 }
@@ -290,11 +304,33 @@ __device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
   return EV_ERR;
 }
 
-constexpr int kStack = 48;
+constexpr int kStack = 32;  // deeper expressions are flagged RMI_ERR_UNSUP (host re-evaluates)
+
+// A stack slot: 16 B (value bits + kind) — the stacks live in the thread's LDS slice, not in
+// scratch: a private array indexed at run time would spill every push/pop to memory.
+struct SVal {
+  long long bits;
+  int is_f, pad;
+};
+__device__ __forceinline__ SVal pack(const Val& v) {
+  SVal s;
+  s.bits = v.is_f ? __double_as_longlong(v.f) : v.i;
+  s.is_f = v.is_f;
+  s.pad = 0;
+  return s;
+}
+__device__ __forceinline__ Val unpack(const SVal& s) {
+  Val v;
+  v.is_f = s.is_f != 0;
+  v.i = s.is_f ? 0 : s.bits;
+  v.f = s.is_f ? __longlong_as_double(s.bits) : 0.0;
+  return v;
+}
+constexpr int kMachineBytes = kStack * (int)sizeof(SVal) + kStack;  // per thread, in LDS
 
 struct Machine {
-  Val vals[kStack];
-  int8_t ops[kStack];
+  SVal* vals;    // [kStack] in LDS
+  int8_t* ops;   // [kStack] in LDS
   int nv = 0, no = 0;
   int status = EV_OK;
 
@@ -302,15 +338,17 @@ struct Machine {
     const int op = ops[--no];
     if (op == OP_NEG || op == OP_POS || op == OP_INV) {
       if (nv < 1) { status = EV_ERR; return false; }
-      const int st = apply_unary(op, vals[nv - 1]);
+      Val a = unpack(vals[nv - 1]);
+      const int st = apply_unary(op, a);
       if (st != EV_OK) { status = st; return false; }
+      vals[nv - 1] = pack(a);
       return true;
     }
     if (nv < 2) { status = EV_ERR; return false; }
     Val r;
-    const int st = apply_binary(op, vals[nv - 2], vals[nv - 1], r);
+    const int st = apply_binary(op, unpack(vals[nv - 2]), unpack(vals[nv - 1]), r);
     if (st != EV_OK) { status = st; return false; }
-    vals[nv - 2] = r;
+    vals[nv - 2] = pack(r);
     nv -= 1;
     return true;
   }
@@ -321,7 +359,7 @@ struct Machine {
   }
   __device__ bool push_val(const Val& v) {
     if (nv >= kStack) { status = EV_UNSUP; return false; }
-    vals[nv++] = v;
+    vals[nv++] = pack(v);
     return true;
   }
   __device__ bool binary(int op) {  // pop higher/equal-precedence operators, then push
@@ -444,8 +482,10 @@ __device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
 }
 
 // returns EV_OK with value in out, EV_ERR (Python raises), EV_UNSUP (outside the model)
-__device__ int py_eval(const uint8_t* s, int n, Val& out) {
+__device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work) {
   Machine m;
+  m.vals = reinterpret_cast<SVal*>(work);
+  m.ops = reinterpret_cast<int8_t*>(work + kStack * sizeof(SVal));
   bool expect_operand = true;
   int depth = 0;
   // eval() strips leading spaces/tabs; ctx_manager already .strip()s the action
@@ -546,18 +586,19 @@ __device__ int py_eval(const uint8_t* s, int n, Val& out) {
     if (!m.reduce_one()) return m.status;
   }
   if (m.nv != 1) return EV_ERR;
-  out = m.vals[0];
+  out = unpack(m.vals[0]);
   return EV_OK;
 }
 
 // compute_reward (countdown/env.py:69-78): 0 | format_score | score ; flags bit0 format bit1 correct
-__device__ double countdown_reward(const uint8_t* s, int n, const int32_t* nums, int n_nums, int32_t target,
-                                   double score, double format_score, uint8_t& flags, uint8_t& err) {
+__device__ double countdown_reward(const uint8_t* s, int n, const int32_t (&nums)[kMaxNums], int n_nums,
+                                   int32_t target, double score, double format_score, uint8_t& flags, uint8_t& err,
+                                   uint8_t* work) {
   flags = 0;
   if (!check_format(s, n, nums, n_nums)) return 0.0;
   flags |= 1;
   Val v;
-  const int st = py_eval(s, n, v);
+  const int st = py_eval(s, n, v, work);
   bool correct = false;
   if (st == EV_UNSUP) err |= RMI_ERR_UNSUP;
   if (st == EV_OK) {
@@ -590,8 +631,9 @@ struct CountdownDev {
   const int32_t* lens;     // this env's [K]
   uint8_t* stage;          // this thread's LDS row (nullptr: parse global memory in place)
   int Lmax;
-  const int32_t* nums;
+  int32_t nums[kMaxNums];
   int n_nums;
+  uint8_t* work;  // this thread's evaluator stacks (LDS)
   int32_t target;
   double score, format_score;
   int k_next;  // index of the answer the next step() consumes
@@ -605,7 +647,7 @@ struct CountdownDev {
     uint8_t fl;
     const uint8_t* src = answers + (int64_t)k * Lmax;
     if (stage && n > 0) src = stage_answer(src, n, ((n + 3) & ~3) <= Lmax, stage);
-    reward = countdown_reward(src, n, nums, n_nums, target, score, format_score, fl, err);
+    reward = countdown_reward(src, n, nums, n_nums, target, score, format_score, fl, err, work);
     done = true;
     eff = reward > 0;
     success = reward == score;
@@ -613,23 +655,37 @@ struct CountdownDev {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
-                                                                     rmi_turn_t in, const uint8_t* __restrict__ answers,
-                                                                     const int32_t* __restrict__ answer_len, int Lmax,
-                                                                     uint8_t* __restrict__ err_out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t stage_lds[];  // [kBlock][round4(Lmax) + 4]
-  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// Per-thread LDS: the staged answer row, then the evaluator stacks.  64-thread blocks keep the
+// slices small enough for several blocks per CU.
+constexpr int kCdBlock = 64;
+__host__ __device__ constexpr int stage_stride(int Lmax) { return Lmax <= kStageMax ? ((Lmax + 3) & ~3) + 4 : 0; }
+__host__ __device__ constexpr int cd_slice(int Lmax) { return stage_stride(Lmax) + kMachineBytes; }
+
+__device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b, int32_t (&nums)[kMaxNums]) {
+#pragma unroll
+  for (int k = 0; k < kMaxNums; ++k) nums[k] = k < env.max_nums ? env.nums[b * env.max_nums + k] : -1;
+}
+
+__global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
+                                                                       rmi_turn_t in,
+                                                                       const uint8_t* __restrict__ answers,
+                                                                       const int32_t* __restrict__ answer_len,
+                                                                       int Lmax, uint8_t* __restrict__ err_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];  // [kCdBlock][cd_slice(Lmax)]
+  const int64_t b = (int64_t)blockIdx.x * kCdBlock + threadIdx.x;
   const int B = ep.B;
   if (b >= B) return;
   uint8_t flags = ep.flags[b];
   const bool act = in.has_input ? (in.has_input[b] != 0) : !(flags & RMI_FLAG_DONE);
   if (!act) return;
+  uint8_t* slice = cd_lds + threadIdx.x * cd_slice(Lmax);
   CountdownDev e;
   e.answers = answers + b * (int64_t)in.K * Lmax;
   e.lens = answer_len + b * (int64_t)in.K;
-  e.stage = Lmax <= kStageMax ? stage_lds + threadIdx.x * (((Lmax + 3) & ~3) + 4) : nullptr;
+  e.stage = Lmax <= kStageMax ? slice : nullptr;
+  e.work = slice + stage_stride(Lmax);
   e.Lmax = Lmax;
-  e.nums = env.nums + b * (int64_t)env.max_nums;
+  load_nums(env, b, e.nums);
   e.n_nums = env.n_nums[b];
   e.target = env.target[b];
   e.score = env.score;
@@ -655,20 +711,26 @@ __global__ __launch_bounds__(kBlock) void countdown_step_turn_kernel(rmi_countdo
   if (err_out && err) err_out[b] |= err;
 }
 
-__global__ __launch_bounds__(kBlock) void countdown_reward_kernel(rmi_countdown_t env,
-                                                                  const uint8_t* __restrict__ answers,
-                                                                  const int32_t* __restrict__ answer_len, int Lmax,
-                                                                  int n, double* __restrict__ reward,
-                                                                  uint8_t* __restrict__ flags_out,
-                                                                  uint8_t* __restrict__ err_out) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+__global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdown_t env,
+                                                                    const uint8_t* __restrict__ answers,
+                                                                    const int32_t* __restrict__ answer_len, int Lmax,
+                                                                    int n, double* __restrict__ reward,
+                                                                    uint8_t* __restrict__ flags_out,
+                                                                    uint8_t* __restrict__ err_out) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];
+  const int64_t i = (int64_t)blockIdx.x * kCdBlock + threadIdx.x;
   if (i >= n) return;
+  uint8_t* slice = cd_lds + threadIdx.x * cd_slice(Lmax);
   uint8_t fl = 0, err = 0;
   int len = answer_len[i];
   if (len > Lmax) len = Lmax;
   if (len < 0) len = 0;
-  const double r = countdown_reward(answers + i * (int64_t)Lmax, len, env.nums + i * (int64_t)env.max_nums,
-                                    env.n_nums[i], env.target[i], env.score, env.format_score, fl, err);
+  int32_t nums[kMaxNums];
+  load_nums(env, i, nums);
+  const uint8_t* src = answers + i * (int64_t)Lmax;
+  if (Lmax <= kStageMax && len > 0) src = stage_answer(src, len, ((len + 3) & ~3) <= Lmax, slice);
+  const double r = countdown_reward(src, len, nums, env.n_nums[i], env.target[i], env.score, env.format_score, fl,
+                                    err, slice + stage_stride(Lmax));
   reward[i] = r;
   if (flags_out) flags_out[i] = fl;
   if (err_out) err_out[i] = err;
@@ -687,9 +749,9 @@ RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episod
   if (!answers || !answer_len || !env->nums || !env->n_nums || !env->target || !in->n_actions || !ep->num_actions ||
       !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
     return RMI_EINVAL;
-  const size_t lds = Lmax <= kStageMax ? (size_t)kBlock * (((Lmax + 3) & ~3) + 4) : 0;
-  hipLaunchKernelGGL(countdown_step_turn_kernel, dim3((ep->B + kBlock - 1) / kBlock), dim3(kBlock), lds,
-                     as_stream(stream), *env, *ep, *in, answers, answer_len, Lmax, err);
+  hipLaunchKernelGGL(countdown_step_turn_kernel, dim3((ep->B + kCdBlock - 1) / kCdBlock), dim3(kCdBlock),
+                     (size_t)kCdBlock * cd_slice(Lmax), as_stream(stream), *env, *ep, *in, answers, answer_len, Lmax,
+                     err);
   return launch_status();
 }
 
@@ -700,7 +762,8 @@ RMI_API int rmi_countdown_reward(const rmi_countdown_t* env, const uint8_t* answ
   if (!env || Lmax <= 0 || n < 0 || env->max_nums <= 0 || env->max_nums > 8) return RMI_EINVAL;
   if (n == 0) return RMI_OK;
   if (!answers || !answer_len || !reward || !env->nums || !env->n_nums || !env->target) return RMI_EINVAL;
-  hipLaunchKernelGGL(countdown_reward_kernel, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, as_stream(stream),
-                     *env, answers, answer_len, Lmax, n, reward, flags, err);
+  hipLaunchKernelGGL(countdown_reward_kernel, dim3((n + kCdBlock - 1) / kCdBlock), dim3(kCdBlock),
+                     (size_t)kCdBlock * cd_slice(Lmax), as_stream(stream), *env, answers, answer_len, Lmax, n, reward,
+                     flags, err);
   return launch_status();
 }
