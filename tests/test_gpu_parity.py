@@ -196,6 +196,37 @@ def test_frozenlake_full_size_vs_oracle(device):
             np.testing.assert_array_equal(h[k], getattr(oep, k), err_msg=k)
 
 
+def test_bandit_full_size_vs_oracle(device):
+    """BD at scale: 16384 envs x 3 turns (cap 2), ids 0..3 (unknown names and invalid ids
+    included): kernel == oracle incl. PCG64 states and error flags."""
+    B, T, K = 16384, 3, 2
+    env = BanditBatch(BanditEnvConfig(lo_arm_name="Phoenix", hi_arm_name="Dragon"), B, T, K, device)
+    env.reset(synthetic.env_seeds(B))
+    hi = env.hi_is_first.cpu().numpy()
+    rng = env.rng.cpu().numpy().view(np.uint64).copy()
+    c = env.config
+    oep = oracle.Episode(B, T)
+    g = np.random.default_rng(8)
+    bad = np.zeros(B, bool)
+    for t in range(T):
+        ids = g.integers(0, 4, size=(B, K)).astype(np.int8)
+        n = g.integers(0, K + 1, size=B).astype(np.uint8)
+        err = torch.zeros(B, dtype=torch.uint8, device=device)
+        env.step_turn(t, _t(ids, device), _t(n, device), None, 2, -0.1, err)
+        oerr = oracle.bandit_turn(int(c.action_space_start), c.lo_arm_score, c.hi_arm_loscore, c.hi_arm_hiscore,
+                                  c.hi_arm_hiscore_prob, hi, rng, oep, t, ids, n, None, 2, -0.1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal((err.cpu().numpy() != 0)[~bad], (oerr != 0)[~bad])
+        bad |= oerr != 0
+        ok = ~bad
+        np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64)[:, ok], rng[:, ok])
+        h = _host_ep(env.ep)
+        for k in ("num_actions", "flags", "penalty"):
+            np.testing.assert_array_equal(h[k][ok], getattr(oep, k)[ok], err_msg=k)
+        for k in ("turn_reward", "turn_info", "turn_exec"):
+            np.testing.assert_array_equal(h[k][:, ok], getattr(oep, k)[:, ok], err_msg=k)
+
+
 def test_gae_full_size(device):
     """B=8192 rows ~1k tokens: legacy/masked GAE returns bit-exact vs oracle, whitened adv <= 1e-5."""
     B = 8192
