@@ -506,30 +506,34 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   const int H = env.H, W = env.W;
   RMI_STAMP(0);
 
-  // ---- 1. every load of the turn, issued together
-  uint8_t flags = RMI_FLAG_DONE, has_in = 0;
-  int r = 0, c = 0, nes = 0, bot = 0, n_act = 0;
-  int32_t num_actions = 0, n_turns = 0;
-  double penalty = 0.0;
-  uint64_t acts = 0;
+  // ---- 1. every load of the turn, issued together: branch-free from clamped (always valid)
+  //         addresses, rows first, nothing consumed before the last load is issued — so the
+  //         compiler's vmcnt waits all fall after one memory round trip
+  const int64_t bc = live ? b : (int64_t)B - 1;
   uint32_t xs[NWL], xf[NWL];
 #pragma unroll
   for (int i = 0; i < NWL; ++i) xs[i] = xf[i] = 0;
-  if (live) {
-    flags = ep.flags[b];
-    if (in.has_input) has_in = in.has_input[b];
-    r = env.player[2 * b];
-    c = env.player[2 * b + 1];
-    nes = env.num_env_steps[b];
-    bot = env.boxes_on_target[b];
-    num_actions = ep.num_actions[b];
-    n_turns = ep.n_turns[b];
-    penalty = ep.penalty[b];
-    n_act = in.n_actions[b];
-    acts = load_actions(in.actions + b * (int64_t)in.K, in.K);
-    load_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
-    load_row<NWL, LPE, HW != 0>(env.room_fixed + b * hw, xf, sub, row_words);
+  load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
+  load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+  uint8_t flags = ep.flags[bc];
+  const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
+  int r = env.player[2 * bc], c = env.player[2 * bc + 1];
+  int nes = env.num_env_steps[bc], bot = env.boxes_on_target[bc];
+  int32_t num_actions = ep.num_actions[bc], n_turns = ep.n_turns[bc];
+  double penalty = ep.penalty[bc];
+  int n_act = in.n_actions[bc];
+  uint8_t av[kMaxK];
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) av[k] = 0;
+  if (in.K > 0) {  // wave-uniform
+    const int8_t* ap = in.actions + bc * (int64_t)in.K;
+#pragma unroll
+    for (int k = 0; k < kMaxK; ++k) av[k] = (uint8_t)ap[k < in.K ? k : in.K - 1];
   }
+  uint64_t acts = 0;
+#pragma unroll
+  for (int k = 0; k < kMaxK; ++k) acts |= k < in.K ? (uint64_t)av[k] << (8 * k) : 0ull;
+  if (!live) flags = RMI_FLAG_DONE;
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
   RMI_STAMP_WAIT(1);
 
