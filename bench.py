@@ -30,6 +30,7 @@ import time
 
 import numpy as np
 import torch
+import torch.distributed as tdist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -360,16 +361,23 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the advantage leg and the copy-peak probe")
+    ap.add_argument("--group", type=int, default=8, help="rollouts per graph replay (reduced to divide --steps)")
+    ap.add_argument("--exchange", choices=("auto", "overlap", "serial"), default="auto",
+                    help="N>1: gather overlapped with the next rollouts on a comm stream, or serial after them")
+    ap.add_argument("--double-buffer", action="store_true",
+                    help="run the N>1 exchange path at N=1 (a 1-rank RCCL group, real collectives)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
+    dist = world > 1 or args.double_buffer
     torch.cuda.set_device(local)  # before the process group: RCCL binds its communicator to this device
     device = torch.device("cuda", local)
     if dist:
-        import torch.distributed as tdist
+        if world == 1:  # --double-buffer at N=1: a 1-rank RCCL group exercises the N>1 path
+            for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29517"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+                os.environ.setdefault(k, v)
         tdist.init_process_group("nccl", device_id=device)
 
     R = Rollout(device, rank)
@@ -381,11 +389,28 @@ def main():
     n_turns = R.env.ep.n_turns.cpu().numpy()
     active_per_turn = [int((n_turns > t).sum()) for t in range(T_TURNS)]
 
-    # N > 1: the rollout's real exchange step (north_star): reassemble every
-    # rank's trajectory record before the PPO update — one RCCL all-gather of the episode arena
-    exchange = (lambda: rd.gather_episode(R.env.ep)) if dist else (lambda: None)
+    # Graph replay, G rollouts per replay (G = --group, reduced until it divides --steps; every
+    # rollout is a full restore + T turns + finalize into its own episode arena).
+    # N > 1: the rollout's real exchange step (north_star) — reassemble every
+    # rank's trajectory record before the PPO update — is ONE RCCL all-gather of the G arenas of
+    # a replay (they are contiguous: EpisodeState.pool), captured in its own graph and replayed
+    # on a comm stream, so it overlaps the next G rollouts.  Two arena sets alternate; a set is
+    # rewritten only after its previous gather finished (events).  Multi-stream capture and one
+    # event pair per rollout were both measured slower (tools/overlap_probe.py).
+    G = 1
+    for g in (args.group, 8, 4, 2, 1):
+        if 1 <= g <= args.group and args.steps % g == 0:
+            G = g
+            break
+
+    def capture(fn, stream=None):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            fn()
+        return g
 
     graph = None
+    exchange_mode = None
     if not args.no_graph:
         s = torch.cuda.Stream(device)
         s.wait_stream(torch.cuda.current_stream(device))
@@ -393,27 +418,89 @@ def main():
             for _ in range(3):
                 R.step()
         torch.cuda.current_stream(device).wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            R.step()
+        pool, eps = ops.EpisodeState.pool(2 * G, R.env.B, R.env.T, device)
+        sets = pool.view(2, -1)  # set h = arenas [h*G, (h+1)*G), contiguous
 
-        def run():
-            graph.replay()
-            exchange()
+        def rollouts(h):
+            for j in range(G):
+                R.env.ep = eps[h * G + j]
+                R.step()
+
+        roll_g = [capture(lambda h=h: rollouts(h)) for h in (0, 1)]
+        R.env.ep = eps[0]
+        graph = roll_g[0]
+        main_s = torch.cuda.current_stream(device)
+        count = [0]
+        if not dist:
+            def run():
+                roll_g[(count[0] // G) & 1].replay()
+                count[0] += G
+        else:
+            W = tdist.get_world_size()
+            outs = [torch.empty(W * sets.shape[1], dtype=torch.uint8, device=device) for _ in (0, 1)]
+            comm, cap_s = torch.cuda.Stream(device), torch.cuda.Stream(device)
+            comm.wait_stream(main_s)
+            with torch.cuda.stream(comm):  # communicator setup must not happen under capture
+                for h in (0, 1):
+                    rd.gather_bytes(sets[h], outs[h])
+            torch.cuda.synchronize()
+            gather_g = [capture(lambda h=h: rd.gather_bytes(sets[h], outs[h]), stream=cap_s) for h in (0, 1)]
+            serial_g = [capture(lambda h=h: (rollouts(h), rd.gather_bytes(sets[h], outs[h]))) for h in (0, 1)]
+            R.env.ep = eps[0]
+            rolled = [torch.cuda.Event(), torch.cuda.Event()]
+            gathered = [torch.cuda.Event(), torch.cuda.Event()]
+
+            def run_overlap():
+                h = (count[0] // G) & 1
+                if count[0] >= 2 * G:
+                    main_s.wait_event(gathered[h])  # set h's previous gather has read it
+                roll_g[h].replay()
+                rolled[h].record(main_s)
+                torch.cuda.set_stream(comm)
+                comm.wait_event(rolled[h])
+                gather_g[h].replay()
+                gathered[h].record(comm)
+                torch.cuda.set_stream(main_s)
+                count[0] += G
+
+            def run_serial():  # G rollouts, then their gather, one single-stream graph
+                serial_g[(count[0] // G) & 1].replay()
+                count[0] += G
+
+            def trial(fn, n=4):
+                tdist.barrier()
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                for _ in range(n):
+                    fn()
+                torch.cuda.synchronize()
+                dt = torch.tensor([time.perf_counter() - t], dtype=torch.float64, device=device)
+                tdist.all_reduce(dt, op=tdist.ReduceOp.MAX)  # every rank picks the same mode
+                return float(dt.item())
+
+            exchange_mode = args.exchange
+            if exchange_mode == "auto":  # which wins depends on the gather's cost at this W
+                t_ov = min(trial(run_overlap) for _ in range(3))
+                t_se = min(trial(run_serial) for _ in range(3))
+                exchange_mode = "overlap" if t_ov <= t_se else "serial"
+            run = run_overlap if exchange_mode == "overlap" else run_serial
     else:
+        G = 1
+
         def run():
             R.step()
-            exchange()
+            if dist:
+                rd.gather_episode(R.env.ep)
 
-    for _ in range(args.warmup):
+    for _ in range(-(-args.warmup // G)):
         run()
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps // G):
         run()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # every stream: the last set's gather is inside the timed region
     if dist:
         tdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -425,6 +512,16 @@ def main():
         c = torch.tensor([total_steps], dtype=torch.float64, device=device)
         tdist.all_reduce(c)
         total_steps = int(c.item())
+    # every replayed rollout wrote a full record (deterministic: all arenas identical), and at
+    # N > 1 this rank's row of each gathered set is its own arenas
+    exchange_ok = None
+    if graph is not None:
+        exchange_ok = all(torch.equal(e.arena, eps[0].arena) for e in eps)
+        if dist:
+            r = tdist.get_rank()
+            exchange_ok = exchange_ok and all(torch.equal(outs[h].view(W, -1)[r], sets[h]) for h in (0, 1))
+        if not exchange_ok:
+            raise RuntimeError("replayed rollouts / gathered arenas do not match")
 
     # ---- dominant-kernel roofline: HIP events around the turn launches (eager, same stream)
     n_prof = min(args.steps, 50)
@@ -482,7 +579,7 @@ def main():
             "config": {"workload": f"Sokoban 6x6 1-box, {B_PER_GPU} envs/GPU x {T_TURNS} turns, K={K_ACTIONS}, "
                                    f"cap {MAX_ACTIONS}, groups of {GROUP}; rollout phase (reset excluded)",
                        "envs_per_gpu": B_PER_GPU, "env_steps_per_rollout_rank0": steps_per_rollout,
-                       "graph": graph is not None, "parallelism": f"env-sharded x{world}"},
+                       "graph": graph is not None, "rollouts_per_replay": G, "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "achievable_peak": copy_peak,
@@ -494,7 +591,12 @@ def main():
             "advantage": adv,
             "toytext": toytext,
             "api_variant": api,
-            "exchange": "all-gather of the episode arena per rollout" if dist else None,
+            "exchange": ("all-gather of the episode arena per rollout"
+                         + (f", one captured all-gather per {G} rollouts, "
+                            + (f"overlapped with the next {G} on a comm stream" if exchange_mode == "overlap"
+                               else "after them on the same stream") + " (chosen by --exchange " + args.exchange + ")"
+                            if graph is not None else "")) if dist else None,
+            "records_checked": exchange_ok,
             "eager_ms_per_step": eager_ms,
             "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu and cpu.get("value") else None,
         }

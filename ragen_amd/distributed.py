@@ -62,16 +62,28 @@ def gather_group_scores(scores: torch.Tensor, group_size: int) -> torch.Tensor:
     return all_gather_rows(scores.view(-1, group_size)).reshape(-1)
 
 
-def gather_episode(ep) -> torch.Tensor:
-    """Every rank's episode arena -> u8[W, nbytes] in rank order, one collective.  All ranks
-    must hold the same (B, T) shard shape; ``episode_views`` re-types a rank's row."""
-    W, _ = world()
-    if W == 1:
-        return ep.arena.view(1, -1)
-    n = ep.arena.numel()
-    out = torch.empty(W * n, dtype=torch.uint8, device=ep.arena.device)  # flat: gloo and RCCL both take it
-    dist.all_gather_into_tensor(out, ep.arena)
+def gather_bytes(buf: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """Every rank's contiguous u8 buffer (same size on all ranks) -> u8[W, numel] in rank order,
+    one all-gather.  ``out`` (u8, W*numel, preallocated) makes the call graph-capturable.
+    Without a process group the local buffer is returned as a view."""
+    flat = buf.reshape(-1)
+    if not (dist.is_available() and dist.is_initialized()):
+        return flat.view(1, -1)
+    W = dist.get_world_size()
+    n = flat.numel()
+    if out is None:
+        out = torch.empty(W * n, dtype=torch.uint8, device=buf.device)  # flat: gloo and RCCL both take it
+    assert buf.dtype == torch.uint8 and buf.is_contiguous()
+    assert out.dtype == torch.uint8 and out.numel() == W * n and out.is_contiguous()
+    dist.all_gather_into_tensor(out.view(-1), flat)
     return out.view(W, n)
+
+
+def gather_episode(ep, out: torch.Tensor = None) -> torch.Tensor:
+    """Every rank's episode arena -> u8[W, nbytes] in rank order, one collective.  All ranks
+    must hold the same (B, T) shard shape; ``episode_views`` re-types a rank's row.  Several
+    rollouts' arenas from ``EpisodeState.pool`` move together with ``gather_bytes``."""
+    return gather_bytes(ep.arena, out)
 
 
 def episode_views(gathered: torch.Tensor, B: int, T: int):

@@ -76,6 +76,16 @@ class EpisodeState:
         return EpisodeState(arena=arena, **views)
 
     @staticmethod
+    def pool(n: int, B: int, T: int, device):
+        """n arenas back to back in one zeroed buffer -> (u8[n, nbytes], [EpisodeState] * n), so
+        several rollouts' records move in one collective."""
+        fields, total = EpisodeState.layout(B, T)
+        buf = torch.zeros(n, max(total, 1), dtype=torch.uint8, device=device)
+        eps = [EpisodeState(arena=row, **{name: EpisodeState.view(row, dt, shape, off)
+                                          for name, dt, shape, off in fields}) for row in buf]
+        return buf, eps
+
+    @staticmethod
     def view(buf: torch.Tensor, dt, shape, off: int) -> torch.Tensor:
         n = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
         return buf[off:off + n].view(dt).view(*shape)
