@@ -299,7 +299,7 @@ def api_leg(device):
             "note": "EnvStateManager.step facade, 8192 envs x 5 turns, host dicts + text obs each turn"}
 
 
-def cpu_baseline_parallel(R, workers=16, reps=6):
+def cpu_baseline_parallel(R, workers=16, reps=20):
     """SURVEY §8(d) CPU baseline (b): one process per host core (the box's 16-core share),
     env groups partitioned across processes, no shared state.  Worker w runs ``reps`` rollouts
     of the 2048-env slice (w % 4) of this rank's batch; value = all workers' env steps / wall
@@ -326,6 +326,34 @@ def cpu_baseline_parallel(R, workers=16, reps=6):
                       f"calls in {wall:.1f}s wall, oracle/port.py"}
 
 
+def cpu_gae_baseline(R, reps=2):
+    """the advantage step as the reference runs it — verl GAE (legacy, a Python
+    loop over token columns, torch on the host) + masked whitening (oracle/port.py) — on the
+    same token rows as the `advantage` leg, with 1 thread and with 16.  -> tokens/s each."""
+    from oracle import port
+    n_turns = R.env.ep.n_turns.cpu().numpy()
+    score = R.norm.cpu().numpy()
+    r, v, m = (torch.from_numpy(x) for x in synthetic.token_rows(n_turns, score, seed=11))
+    out = {"kind": "port", "rows": int(r.shape[0]), "cols": int(r.shape[1]),
+           "sample": "verl compute_gae_advantage_return (legacy) + masked_whiten on the advantage leg's rows, "
+                     f"best of {reps}"}
+    old = torch.get_num_threads()
+    try:
+        for threads in (1, 16):
+            torch.set_num_threads(threads)
+            best = None
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                port.verl_gae_whiten(r, v, m, 1.0, 1.0)
+                dt = time.perf_counter() - t0
+                best = dt if best is None else min(best, dt)
+            out[f"tokens_per_s_{threads}t"] = r.numel() / best
+            out[f"ms_{threads}t"] = best * 1e3
+    finally:
+        torch.set_num_threads(old)
+    return out
+
+
 def cpu_baseline(R, seconds_budget=20.0):
     """Reference-shaped CPU path (oracle/port.py: per-env Python objects mirroring
     EnvStateManager.step + SokobanEnv.step) on a bounded sample of the same workload:
@@ -346,7 +374,7 @@ def cpu_baseline(R, seconds_budget=20.0):
         steps += port.sokoban_rollout(envs, ids, n, MAX_ACTIONS)
         dt += time.perf_counter() - t0
         reps += 1
-        if dt > seconds_budget / 2 or reps >= 8:
+        if dt > seconds_budget / 2 or reps >= 40:
             break
     return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
             "sample": f"{reps} x Sokoban 6x6 rollout of {n_envs} envs x {T_TURNS} turns (reset excluded), "
@@ -356,8 +384,8 @@ def cpu_baseline(R, seconds_budget=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=40)
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the advantage leg and the copy-peak probe")
@@ -562,6 +590,12 @@ def main():
                 cpu_par = cpu_baseline_parallel(R)
             except Exception as ex:
                 cpu_par = {"value": None, "sample": f"failed: {ex}"}
+            if adv is not None:
+                try:
+                    adv["cpu_baseline"] = cpu_gae_baseline(R)
+                    adv["speedup_vs_cpu_1t"] = adv["tokens_per_s"] / adv["cpu_baseline"]["tokens_per_s_1t"]
+                except Exception as ex:
+                    adv["cpu_baseline"] = {"value": None, "sample": f"failed: {ex}"}
         value = total_steps / elapsed
         line = {
             "metric": "env-steps/sec (whole node), Sokoban 6x6, 8192 envs x 5 turns",

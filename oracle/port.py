@@ -177,3 +177,28 @@ def timed_rollouts(fixed, state0, player0, ids, n, max_actions, reps):
         steps += sokoban_rollout(envs, ids, n, max_actions)
         dt += time.perf_counter() - t0
     return steps, dt
+
+
+def verl_gae_whiten(r, v, mask, gamma=1.0, lam=1.0):
+    """verl compute_gae_advantage_return (legacy; SURVEY App. A.4, called from
+    agent_trainer.py:77-83) + masked_whiten (core_algos.py:90) as the reference runs them:
+    torch on the host, one Python iteration per token column.  CPU baseline of the advantage
+    step; checked against the C oracle in tests/test_oracle_port.py.  torch tensors in/out."""
+    import torch
+    with torch.no_grad():
+        L = r.shape[1]
+        last = torch.zeros_like(r[:, 0])
+        rev = []
+        for t in reversed(range(L)):
+            nxt = v[:, t + 1] if t < L - 1 else 0.0
+            delta = r[:, t] + gamma * nxt - v[:, t]
+            last = delta + gamma * lam * last
+            rev.append(last)
+        adv = torch.stack(rev[::-1], dim=1)
+        ret = adv + v
+        m = mask.to(adv.dtype)
+        n = m.sum()
+        mean = (adv * m).sum() / n
+        var = (((adv - mean) ** 2) * m).sum() / n * (n / (n - 1))  # unbiased, as verl masked_var
+        adv = (adv - mean) * torch.rsqrt(var + 1e-8)
+        return adv, ret

@@ -30,3 +30,16 @@ def test_port_matches_c_oracle():
         assert np.float64(e["cache"]["penalty"]) == ep.penalty[i]
         rw = e["status"]["rewards"]
         np.testing.assert_array_equal(np.array(rw + [0.0] * (T - len(rw))), ep.turn_reward[:, i])
+
+
+def test_port_gae_matches_c_oracle():
+    """The timed GAE baseline (torch column loop) == the C oracle's legacy GAE + whitening."""
+    import torch
+    rng = np.random.default_rng(5)
+    n_turns = rng.integers(1, 6, 48).astype(np.int32)
+    r, v, m = synthetic.token_rows(n_turns, rng.standard_normal(48).astype(np.float32), seed=3)
+    for gamma, lam in ((1.0, 1.0), (1.0, 0.95)):
+        adv, ret = port.verl_gae_whiten(torch.from_numpy(r), torch.from_numpy(v), torch.from_numpy(m), gamma, lam)
+        oa, oret = oracle.gae(r, v, m, gamma, lam)
+        np.testing.assert_allclose(ret.numpy(), oret, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(adv.numpy(), oracle.masked_whiten(oa, m), rtol=1e-4, atol=1e-4)
