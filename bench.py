@@ -67,13 +67,15 @@ class Rollout:
         self.metrics = torch.empty(B, 4, dtype=torch.float64, device=device)
         self.turns = [ops.turn_struct(t, self.ids[t], self.n[t], None, MAX_ACTIONS, -0.1) for t in range(T_TURNS)]
         self.st = e.struct()
+        self.fin = ops.finalize_struct(GROUP, "identity", self.norm, self.metrics)
 
     def step(self):
-        """One rollout phase: restore, T turn launches, fused finalize."""
+        """One rollout phase: restore, T turn launches, the last one fused with the rollout's
+        finalize (metrics + scores + normalisation; == rmi_rollout_finalize, tested bit-exact)."""
         self.env.restore()
-        for t in range(T_TURNS):
+        for t in range(T_TURNS - 1):
             ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
-        ops.rollout_finalize(self.env.ep, self.seg, "identity", self.norm, metrics=self.metrics)
+        ops.sokoban_step_turn_finalize(self.st, self.env.ep, self.turns[-1], self.fin)
 
     def timed_turns(self):
         """One rollout phase with HIP events (on the launch stream) around its T back-to-back

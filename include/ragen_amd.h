@@ -109,6 +109,24 @@ typedef struct {
 int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                           uint8_t* err, rmi_stream_t stream);
 
+/* The rollout's last turn fused with its end: rmi_sokoban_step_turn, then exactly what
+ * rmi_rollout_finalize computes (get_rollout_states es_manager.py:173-207, trajectory scores,
+ * _normalize_score_tensor ctx_manager.py:175-226), in one launch.  Groups must be uniform and
+ * contiguous: env b is in group b / group_size (the StarPO "state" grouping of es_manager.py:80-82).
+ * Outputs as rmi_rollout_finalize (metrics f64[B,4], score / pen / norm f32[B]; any may be NULL).
+ * RMI_EUNSUP when a group would straddle a wave (group_size must divide 64, or 16 for
+ * B <= 4096) or B % group_size != 0: then launch the two separately.                          */
+typedef struct {
+  int32_t group_size;
+  int32_t method; /* RMI_NORM_* */
+  double* metrics;
+  float* score;
+  float* pen;
+  float* norm;
+} rmi_finalize_t;
+int rmi_sokoban_step_turn_finalize(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                   uint8_t* err, const rmi_finalize_t* fin, rmi_stream_t stream);
+
 /* Device part of SokobanEnv.reset (sokoban/env.py:37-38) + EnvStatus(seed) (es_manager.py:95):
  * room_state/player := init_state/init_player (the generated rooms), num_env_steps =
  * boxes_on_target = 0, and the whole episode record zeroed — one launch.  B*H*W % 4 == 0. */

@@ -40,6 +40,11 @@ class Sokoban(ctypes.Structure):
                 ("num_env_steps", c_void_p), ("boxes_on_target", c_void_p)]
 
 
+class Finalize(ctypes.Structure):
+    _fields_ = [("group_size", c_int32), ("method", c_int32), ("metrics", c_void_p), ("score", c_void_p),
+                ("pen", c_void_p), ("norm", c_void_p)]
+
+
 class FrozenLake(ctypes.Structure):
     _fields_ = [("nrow", c_int32), ("ncol", c_int32), ("is_slippery", c_int32), ("cs0", c_double),
                 ("cs1", c_double), ("cs2", c_double), ("desc", c_void_p), ("s", c_void_p), ("rng", c_void_p)]
@@ -60,6 +65,8 @@ _P = ctypes.POINTER
 _SIGS = {
     "rmi_version": (ctypes.c_char_p, []),
     "rmi_sokoban_step_turn": (c_int32, [_P(Sokoban), _P(Episode), _P(Turn), c_void_p, c_void_p]),
+    "rmi_sokoban_step_turn_finalize": (c_int32, [_P(Sokoban), _P(Episode), _P(Turn), c_void_p, _P(Finalize),
+                                                 c_void_p]),
     "rmi_sokoban_generate_rooms": (c_int32, [c_void_p, c_int32, c_int32, c_int32, c_int32, c_int32, c_void_p,
                                              c_void_p, c_void_p, c_void_p, c_int32]),
     "rmi_sokoban_reset": (c_int32, [_P(Sokoban), _P(Episode), c_void_p, c_void_p, c_void_p]),

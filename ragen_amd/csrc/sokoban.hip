@@ -23,14 +23,23 @@ namespace {
 
 // Diagnostic build only (tools/microbench.hip defines RMI_STAMPS): per-wave s_memtime /
 // s_memrealtime stamps at phase boundaries.  Compiled out of the library.
+// The stamps stay in SGPRs until the wave's last one, so the instrumentation adds no memory
+// round trip inside the phases it measures (one s_memtime each; s_memrealtime at 0 and 4).
 #ifdef RMI_STAMPS
 __device__ unsigned long long* g_stamps;
-#define RMI_STAMP(i)                                                                   \
-  do {                                                                                 \
-    if (threadIdx.x == 0) {                                                            \
-      g_stamps[blockIdx.x * 16 + 2 * (i)] = __builtin_amdgcn_s_memtime();              \
-      g_stamps[blockIdx.x * 16 + 2 * (i) + 1] = __builtin_amdgcn_s_memrealtime();      \
-    }                                                                                  \
+#define RMI_STAMP_DECL unsigned long long rmi_st_[5], rmi_rt0_ = __builtin_amdgcn_s_memrealtime()
+#define RMI_STAMP(i)                                 \
+  do {                                               \
+    rmi_st_[i] = __builtin_amdgcn_s_memtime();       \
+    if ((i) == 4) {                                  \
+      const unsigned long long rt4 = __builtin_amdgcn_s_memrealtime(); \
+      if (threadIdx.x == 0) {                        \
+        unsigned long long* g = g_stamps + blockIdx.x * 16; \
+        for (int s_ = 0; s_ < 5; ++s_) g[2 * s_] = rmi_st_[s_]; \
+        g[1] = rmi_rt0_;                             \
+        g[9] = rt4;                                  \
+      }                                              \
+    }                                                \
   } while (0)
 #define RMI_STAMP_WAIT(i)          \
   do {                             \
@@ -38,6 +47,9 @@ __device__ unsigned long long* g_stamps;
     RMI_STAMP(i);                  \
   } while (0)
 #else
+#define RMI_STAMP_DECL \
+  do {                 \
+  } while (0)
 #define RMI_STAMP(i) \
   do {               \
   } while (0)
@@ -188,10 +200,18 @@ __device__ __forceinline__ uint32_t gt8_bytes(uint32_t y) {  // high bit of each
 // bit 0 of each byte of a dword -> 4-bit nibble (byte j -> bit j); exact, no carries.
 // (One multiply beats the 5-instruction shift/or gather on a latency-bound lone wave.)
 __device__ __forceinline__ uint32_t nib(uint32_t x) { return (x * 0x01020408u) >> 24; }
-// 0/1 per byte -> 0x00/0xFF per byte
-__device__ __forceinline__ uint32_t byte_mask(uint32_t x) { return (x << 8) - x; }
-// 4-bit nibble -> byte mask (bit j -> byte j = 0xFF)
-__device__ __forceinline__ uint32_t unnib(uint32_t n) { return byte_mask((n * 0x00204081u) & 0x01010101u); }
+// Two such dwords at once: y = x0 | x1 << 4 (bits 8j and 8j+4) -> byte nib(x0) | nib(x1) << 4.
+// The multiplier's shifts {21, 14, 7, 0} send bit 8j and bit 8j+4 to 21+j and 25+j; every
+// other partial product lands on a distinct bit outside 21..28, so nothing carries.  One
+// quarter-rate v_mul_lo_u32 per two dwords instead of two (host-checked exhaustively).
+__device__ __forceinline__ uint32_t nib2(uint32_t x0, uint32_t x1) {
+  return ((x0 | (x1 << 4)) * 0x00204081u) >> 21 & 0xFFu;
+}
+// 0/1 per byte -> 0x00/0xFF per byte.  Written as a subtract/xor on purpose: (x << 8) - x is
+// folded by the compiler into x * 255, a quarter-rate v_mul_lo_u32.  0x80 - {0,1} never borrows.
+__device__ __forceinline__ uint32_t byte_mask(uint32_t x) { return (0x80808080u - x) ^ 0x80808080u; }
+// 4-bit nibble -> byte mask (bit j -> byte j = 0xFF); n < 16, so the full-rate 24-bit multiply
+__device__ __forceinline__ uint32_t unnib(uint32_t n) { return byte_mask(__umul24(n, 0x00204081u) & 0x01010101u); }
 
 // OR across the LPE lanes that share an env (consecutive lanes; DPP inside a row of 16).
 template <int LPE>
@@ -218,23 +238,45 @@ __device__ __forceinline__ bool decode_rows(const uint32_t (&xs)[NWL], const uin
   const uint32_t pmask = 0xFFu << (8 * (p & 3)), p5 = 5u << (8 * (p & 3));
   uint32_t bad = 0;
   uint64_t wl = 0, tl = 0, bl = 0;
+  uint32_t fw[NWL], ft[NWL], bx[NWL];
 #pragma unroll
   for (int i = 0; i < NWL; ++i) {
     const int w = sub + LPE * i;
+    fw[i] = ft[i] = bx[i] = 0;
     if (w < row_words) {
       const uint32_t f = xf[i], s = xs[i];
       const uint32_t f1 = f >> 1, s1 = s >> 1, s2 = s >> 2;
-      bad |= (f & 0xFCFCFCFCu) | (f & f1 & L);                     // fixed byte in {0, 1, 2}
-      const uint32_t fw = ~(f | f1) & L;                             // fixed == 0 (wall)
-      const uint32_t ft = f1 & L;                                    // fixed == 2 (target)
-      const uint32_t bx = ((s & s1 & ~s2) | (s2 & ~s1 & ~s)) & L;  // low bits 011 / 100: 3 or 4
-      const uint32_t bm = byte_mask(bx);
+      bad |= (f & 0xFCFCFCFCu) | (f & f1 & L);                   // fixed byte in {0, 1, 2}
+      fw[i] = ~(f | f1) & L;                                       // fixed == 0 (wall)
+      ft[i] = f1 & L;                                              // fixed == 2 (target)
+      bx[i] = ((s & s1 & ~s2) | (s2 & ~s1 & ~s)) & L;            // low bits 011 / 100: 3 or 4
+      const uint32_t bm = byte_mask(bx[i]);
       uint32_t reb = (f & ~bm) | ((0x05050505u - f) & bm);  // boxes: 5 - fixed = 3 on target, 4 on floor
       reb = w == pw ? ((reb & ~pmask) | p5) : reb;           // the player's 5
       bad |= reb ^ s;
-      wl |= (uint64_t)nib(fw) << (4 * w);
-      tl |= (uint64_t)nib(ft) << (4 * w);
-      bl |= (uint64_t)nib(bx) << (4 * w);
+    }
+  }
+  // gather bit 0 of every byte into the boards, two dwords per multiply (dwords w, w + LPE);
+  // dwords past the row are all-zero, so they add nothing
+#pragma unroll
+  for (int i = 0; i < NWL; i += 2) {
+    const int w = sub + LPE * i;
+    if (i + 1 < NWL) {
+      const uint64_t n_w = nib2(fw[i], fw[i + 1]), n_t = nib2(ft[i], ft[i + 1]), n_b = nib2(bx[i], bx[i + 1]);
+      if (LPE == 1) {  // adjacent nibbles: one byte at 4w
+        wl |= n_w << (4 * w);
+        tl |= n_t << (4 * w);
+        bl |= n_b << (4 * w);
+      } else {
+        const int w1 = w + LPE;
+        wl |= ((n_w & 0xF) << (4 * w)) | ((n_w >> 4) << (4 * w1));
+        tl |= ((n_t & 0xF) << (4 * w)) | ((n_t >> 4) << (4 * w1));
+        bl |= ((n_b & 0xF) << (4 * w)) | ((n_b >> 4) << (4 * w1));
+      }
+    } else {
+      wl |= (uint64_t)nib(fw[i]) << (4 * w);
+      tl |= (uint64_t)nib(ft[i]) << (4 * w);
+      bl |= (uint64_t)nib(bx[i]) << (4 * w);
     }
   }
   wall = env_or64<LPE>(wl);
@@ -479,6 +521,104 @@ constexpr int kMaxWords = kMaxCells / 4;
 #define RMI_SPREAD_MAX_ENVS 4096
 #endif
 constexpr int64_t kSpreadMaxEnvs = RMI_SPREAD_MAX_ENVS;  // 4 lanes per env up to this batch
+__host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMaxEnvs; }
+
+// ------------------------------------------------------- fused end of rollout (kFin)
+// The rollout's last turn launch also does rmi_rollout_finalize's work (episode.hip): per env
+// get_rollout_states metrics (es_manager.py:173-207), the trajectory score sum(turn rewards)
+// + penalty, and _normalize_score_tensor (ctx_manager.py:175-226) over uniform contiguous
+// groups of fin.group_size envs, which the launcher only accepts when every group lies in one
+// wave.  The episode record of the first 8 turns is loaded with the turn's other loads (no
+// extra round trip); the group sums are the same xor butterflies as finalize_kernel's
+// wave_sum restricted to the group's lanes (the lanes outside a group only ever add exact
+// zeros there), so every output is bit-identical to the separate launch.
+constexpr int kFinT = 8;  // turns of the record loaded up front
+struct FinRecord {
+  double r[kFinT];
+  uint8_t info[kFinT];
+  __device__ __forceinline__ void load(const rmi_episode_t& ep, int64_t bc) {
+    const int64_t B = ep.B;
+#pragma unroll
+    for (int k = 0; k < kFinT; ++k) {
+      const int64_t t = k < ep.T ? k : ep.T - 1;  // clamped, always valid
+      r[k] = ep.turn_reward[t * B + bc];
+      info[k] = ep.turn_info[t * B + bc];
+    }
+  }
+  __device__ __forceinline__ void set(int turn, double acc, uint8_t inf) {
+#pragma unroll
+    for (int k = 0; k < kFinT; ++k)
+      if (k == turn) {
+        r[k] = acc;
+        info[k] = inf;
+      }
+  }
+};
+
+template <int LPE>
+__device__ __forceinline__ double group_sum(double x, int gs) {  // xor butterfly over gs envs
+  for (int o = gs >> 1; o >= 1; o >>= 1) x += __shfl_xor(x, o * LPE, 64);
+  return x;
+}
+
+template <int LPE>
+__device__ __forceinline__ void finalize_envs(const rmi_episode_t& ep, const rmi_finalize_t& fin, const FinRecord& rec,
+                                              int64_t b, bool writer, uint8_t flags, int32_t n_turns,
+                                              int32_t num_actions, double penalty, int acted_turn, double acc,
+                                              uint8_t acc_info) {
+  const int64_t B = ep.B;
+  double score = 0.0;  // python sum over the turns, in turn order
+  int eff = 0, val = 0, present = 0;
+#pragma unroll
+  for (int k = 0; k < kFinT; ++k)
+    if (k < ep.T) {
+      score += rec.r[k];
+      present |= rec.info[k] & RMI_INFO_PRESENT;
+      eff += (rec.info[k] >> 1) & 1;
+      val += (rec.info[k] >> 2) & 1;
+    }
+  for (int t = kFinT; t < ep.T; ++t) {  // long episodes only
+    const int64_t bc = b < B ? b : B - 1;
+    const bool mine = t == acted_turn;  // written by this launch: use the registers
+    const uint8_t inf = mine ? acc_info : ep.turn_info[t * B + bc];
+    score += mine ? acc : ep.turn_reward[t * B + bc];
+    present |= inf & RMI_INFO_PRESENT;
+    eff += (inf >> 1) & 1;
+    val += (inf >> 2) & 1;
+  }
+  const float scf = (float)score, pf = (float)penalty, x = scf + pf;
+  if (writer) {
+    if (fin.score) fin.score[b] = scf;
+    if (fin.pen) fin.pen[b] = pf;
+    if (fin.metrics) {
+      const double nt = (double)n_turns;
+      double* m = fin.metrics + 4 * b;
+      m[0] = ((flags & RMI_FLAG_TERMINATED) && !(flags & RMI_FLAG_TRUNCATED)) ? 1.0 : 0.0;
+      m[1] = (double)num_actions;
+      m[2] = present ? (double)eff / nt : __builtin_nan("");
+      m[3] = present ? (double)val / nt : __builtin_nan("");
+    }
+  }
+  if (!fin.norm) return;
+  const int gs = fin.group_size, method = fin.method;  // uniform; all lanes reach the shuffles
+  const double md = group_sum<LPE>(0.0 + (double)x, gs) / (double)gs;
+  const float mean = (float)md;
+  float sd = 0.0f;
+  if (method == RMI_NORM_MEAN_STD || method == RMI_NORM_ASYM_CLIP) {
+    const double d = (double)x - md;
+    const double q = group_sum<LPE>(0.0 + d * d, gs);
+    sd = gs > 1 ? (float)sqrt(q / (double)(gs - 1)) : __builtin_nanf("");
+  }
+  const bool use = sd > 1e-6f;
+  float y;
+  if (method == RMI_NORM_IDENTITY) y = x;
+  else if (method == RMI_NORM_MEAN) y = x - mean;
+  else {
+    y = use ? (x - mean) / (sd + 1e-6f) : 0.0f;
+    if (method == RMI_NORM_ASYM_CLIP) y = fminf(fmaxf(y, -1.0f), 3.0f);
+  }
+  if (writer) fin.norm[b] = y;
+}
 
 // One launch = one turn of every env.  LPE consecutive lanes own one env (LPE = 1 for big
 // batches; 4 when the batch is too small to fill the chip, so the per-wave instruction
@@ -487,10 +627,12 @@ constexpr int64_t kSpreadMaxEnvs = RMI_SPREAD_MAX_ENVS;  // 4 lanes per env up t
 // w = sub + LPE*i (no barriers); every load of the turn is issued up front (one memory
 // round trip), rows live in VGPRs, and a wave of regular rooms steps on bitboards of word
 // type M.  `border` = bitmask of the border cells (row-major), precomputed by the launcher.
-template <int HW, class M, int LPE>  // HW = H*W for the common sizes (0 = runtime); H*W % 4 == 0
+// kFin: the launch is the rollout's last turn and also runs rmi_rollout_finalize for uniform
+// contiguous groups of fin.group_size envs (each group inside one wave): see finalize_envs.
+template <int HW, class M, int LPE, bool kFin>  // HW = H*W for the common sizes (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
-                                                                  uint8_t* __restrict__ err_out) {
+                                                                  uint8_t* __restrict__ err_out, rmi_finalize_t fin) {
   constexpr int NW = HW ? HW / 4 : kMaxWords;
   constexpr int NWL = (NW + LPE - 1) / LPE;      // row dwords per lane
   constexpr int kEnvs = kWave / LPE;             // envs per wave
@@ -504,6 +646,8 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   const int64_t b = (int64_t)blockIdx.x * kEnvs + slot;
   const bool live = b < B;
   const int H = env.H, W = env.W;
+  const uint32_t w_magic = (65536u + (uint32_t)W - 1u) / (uint32_t)W;  // off the critical path
+  RMI_STAMP_DECL;
   RMI_STAMP(0);
 
   // ---- 1. every load of the turn, issued together: branch-free from clamped (always valid)
@@ -533,6 +677,8 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   uint64_t acts = 0;
 #pragma unroll
   for (int k = 0; k < kMaxK; ++k) acts |= k < in.K ? (uint64_t)av[k] << (8 * k) : 0ull;
+  FinRecord rec;
+  if (kFin) rec.load(ep, bc);
   if (!live) flags = RMI_FLAG_DONE;
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
   RMI_STAMP_WAIT(1);
@@ -582,7 +728,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
                         turn_done, succ_last, row_changed);
       if (row_changed) {  // rebuild this lane's row dwords: fixed, boxes 3/4, player 5
         const int p = jp + W;
-        r = p / W;
+        r = (int)(((uint32_t)p * w_magic) >> 16);  // p / W (exact for p < 2^10, W < 2^10)
         c = p - r * W;
         const uint64_t box64 = (uint64_t)box << W;
 #pragma unroll
@@ -675,6 +821,11 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     if (row_changed) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
   }
   RMI_STAMP(4);
+  if (kFin) {
+    if (act) rec.set(in.turn, o.acc, o.info);  // this turn's record is still in registers
+    finalize_envs<LPE>(ep, fin, rec, b, live && sub == 0, flags, n_turns, num_actions, penalty, act ? in.turn : -1,
+                       o.acc, o.info);
+  }
 }
 
 // Fused reset: room_state/player from the generated rooms, counters and the whole episode
@@ -706,22 +857,13 @@ __global__ __launch_bounds__(kBlock) void sokoban_reset_kernel(rmi_sokoban_t env
 }  // namespace
 }  // namespace rmi
 
-RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
-                                  uint8_t* err, rmi_stream_t stream) {
-  using namespace rmi;
-  if (!env) return RMI_EINVAL;
+namespace rmi {
+namespace {
+template <bool kFin>
+int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in, uint8_t* err,
+                             const rmi_finalize_t& fin, hipStream_t s) {
   const int hw = env->H * env->W;
-  if (env->H <= 0 || env->W <= 0 || hw > kMaxCells) return RMI_EUNSUP;
-  const int rc = check_turn_args(ep, in);
-  if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
-  if (!env->room_fixed || !env->room_state || !env->player || !env->num_env_steps || !env->boxes_on_target)
-    return RMI_EINVAL;
-  // rows are staged as dwords: H*W must be a multiple of 4 and the grids 4-byte aligned
-  if (hw % 4 != 0 ||
-      ((reinterpret_cast<uintptr_t>(env->room_state) | reinterpret_cast<uintptr_t>(env->room_fixed)) & 3u))
-    return RMI_EUNSUP;
   const unsigned grid = (unsigned)((ep->B + kWave - 1) / kWave);
-  hipStream_t s = as_stream(stream);
   const int H = env->H, W = env->W;
   uint64_t border = 0;  // border cells, row-major
   for (int r = 0; r < H; ++r)
@@ -729,15 +871,15 @@ RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t*
       if (r == 0 || c == 0 || r == H - 1 || c == W - 1) border |= 1ull << (r * W + c);
   const bool w32 = (H - 1) * W <= 32;  // the board window fits a u32
   // lanes per env: spread a batch too small to fill the chip over 4 lanes per env
-  const bool spread = ep->B <= kSpreadMaxEnvs;
+  const bool spread = spread_lanes(ep->B);
 #define RMI_LAUNCH(HW_, M_)                                                                                   \
   do {                                                                                                        \
     if (spread)                                                                                               \
-      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 4>), dim3((unsigned)((ep->B + 15) / 16)), dim3(kWave), \
-                         0, s, *env, *ep, *in, hw, border, err);                                              \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 4, kFin>), dim3((unsigned)((ep->B + 15) / 16)),   \
+                         dim3(kWave), 0, s, *env, *ep, *in, hw, border, err, fin);                            \
     else                                                                                                      \
-      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1>), dim3(grid), dim3(kWave), 0, s, *env, *ep, *in, hw, \
-                         border, err);                                                                        \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin>), dim3(grid), dim3(kWave), 0, s, *env, *ep, \
+                         *in, hw, border, err, fin);                                                          \
   } while (0)
   if (hw == 36 && w32)
     RMI_LAUNCH(36, uint32_t);
@@ -751,6 +893,54 @@ RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t*
     RMI_LAUNCH(0, uint64_t);
 #undef RMI_LAUNCH
   return launch_status();
+}
+
+int sokoban_check(const rmi_sokoban_t* env) {
+  if (!env) return RMI_EINVAL;
+  const int hw = env->H * env->W;
+  if (env->H <= 0 || env->W <= 0 || hw > kMaxCells) return RMI_EUNSUP;
+  if (!env->room_fixed || !env->room_state || !env->player || !env->num_env_steps || !env->boxes_on_target)
+    return RMI_EINVAL;
+  // rows are staged as dwords: H*W must be a multiple of 4 and the grids 4-byte aligned
+  if (hw % 4 != 0 ||
+      ((reinterpret_cast<uintptr_t>(env->room_state) | reinterpret_cast<uintptr_t>(env->room_fixed)) & 3u))
+    return RMI_EUNSUP;
+  return RMI_OK;
+}
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                  uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env) return RMI_EINVAL;
+  if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
+  const int rc = check_turn_args(ep, in);
+  if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
+  const int ec = sokoban_check(env);
+  if (ec != RMI_OK) return ec;
+  return sokoban_step_turn_launch<false>(env, ep, in, err, rmi_finalize_t{}, as_stream(stream));
+}
+
+RMI_API int rmi_sokoban_step_turn_finalize(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                           uint8_t* err, const rmi_finalize_t* fin, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !fin) return RMI_EINVAL;
+  if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
+  const int rc = check_turn_args(ep, in);
+  if (rc < 0) return rc;
+  if (ep->B == 0) return RMI_OK;
+  const int ec = sokoban_check(env);
+  if (ec != RMI_OK) return ec;
+  if (fin->method < 0 || fin->method > 3 || fin->group_size < 1) return RMI_EINVAL;
+  if (!ep->turn_reward || !ep->turn_info || !ep->penalty || !ep->flags || !ep->n_turns || !ep->num_actions)
+    return RMI_EINVAL;
+  // every group inside one wave (64 envs, or 16 when 4 lanes share an env), and no partial group
+  const int per_wave = spread_lanes(ep->B) ? kWave / 4 : kWave;
+  if (per_wave % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;
+  rmi_finalize_t f = *fin;
+  if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member
+  return sokoban_step_turn_launch<true>(env, ep, in, err, f, as_stream(stream));
 }
 
 RMI_API int rmi_sokoban_reset(const rmi_sokoban_t* env, const rmi_episode_t* ep, const uint8_t* init_state,

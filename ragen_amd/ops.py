@@ -130,6 +130,36 @@ def sokoban_step_turn(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn, err:
     check(lib().rmi_sokoban_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_sokoban_step_turn")
 
 
+def finalize_struct(group_size: int, method: str, norm: Optional[torch.Tensor],
+                    metrics: Optional[torch.Tensor] = None, score: Optional[torch.Tensor] = None,
+                    pen: Optional[torch.Tensor] = None) -> _lib.Finalize:
+    """Outputs of the fused last turn (see sokoban_step_turn_finalize); the tensors must outlive
+    every launch (or graph replay) that uses the struct."""
+    if method not in _lib.NORM_METHODS:
+        raise ValueError(f"Invalid normalization method: {method}")
+    _dev(norm, metrics, score, pen)
+    _dt(norm, torch.float32, "norm")
+    _dt(score, torch.float32, "score")
+    _dt(pen, torch.float32, "pen")
+    _dt(metrics, torch.float64, "metrics")
+    return _lib.Finalize(int(group_size), _lib.NORM_METHODS[method], _ptr(metrics), _ptr(score), _ptr(pen),
+                         _ptr(norm))
+
+
+def sokoban_step_turn_finalize(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn, fin: _lib.Finalize,
+                               err: Optional[torch.Tensor] = None):
+    """The rollout's last turn + rollout_finalize (uniform groups of fin.group_size) in one launch.
+    Groups that would straddle a wave take the two launches instead (same results)."""
+    rc = lib().rmi_sokoban_step_turn_finalize(env, ep.struct(), turn, _ptr(err), fin, _stream())
+    if rc == _lib.RMI_EUNSUP and fin.group_size >= 1 and ep.B % fin.group_size == 0:
+        sokoban_step_turn(env, ep, turn, err)
+        seg = torch.arange(0, ep.B + 1, fin.group_size, dtype=torch.int32, device=ep.flags.device)
+        check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, fin.method, fin.metrics,
+                                         fin.score, fin.pen, fin.norm, _stream()), "rmi_rollout_finalize")
+        return
+    check(rc, "rmi_sokoban_step_turn_finalize")
+
+
 def sokoban_reset(env: _lib.Sokoban, ep: EpisodeState, init_state: torch.Tensor, init_player: torch.Tensor):
     """Fused device reset from the generated rooms (state, player, counters, episode record)."""
     _dev(init_state, init_player)

@@ -500,3 +500,39 @@ def test_render_vs_oracle(device):
     desc = fl.desc.cpu().numpy()
     assert fl.render_all() == [oracle.frozenlake_render(desc[i], int(s[i]), 4, fl.config.grid_lookup)
                                for i in range(B)]
+
+
+@pytest.mark.parametrize("B,T", [(1024, 5), (8192, 5), (2048, 10)])
+def test_fused_last_turn_finalize(device, B, T):
+    """rmi_sokoban_step_turn_finalize == rmi_sokoban_step_turn + rmi_rollout_finalize, bit for bit
+    (both lane layouts; groups that fit a wave, and the two-launch path for ones that do not)."""
+    K = 5
+    cfg = SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100)
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=23)
+    ids, n = _t(ids, device), _t(n, device)
+    for gs in (16, 4, 64):
+        for method in ("identity", "mean", "mean_std", "asym_clip"):
+            outs = []
+            for fused in (False, True):
+                env = SokobanBatch(cfg, B, T, K, device)
+                env.reset(synthetic.env_seeds(B))
+                st = env.struct()
+                norm = torch.full((B,), 7.0, dtype=torch.float32, device=device)
+                met = torch.full((B, 4), 7.0, dtype=torch.float64, device=device)
+                sc = torch.full((B,), 7.0, dtype=torch.float32, device=device)
+                pe = torch.full((B,), 7.0, dtype=torch.float32, device=device)
+                last = T - 2  # the rollout may end before the record is full
+                for t in range(last + 1):
+                    turn = ops.turn_struct(t, ids[t], n[t], None, 10, -0.1)
+                    if fused and t == last:
+                        fin = ops.finalize_struct(gs, method, norm, met, sc, pe)
+                        ops.sokoban_step_turn_finalize(st, env.ep, turn, fin)
+                    else:
+                        ops.sokoban_step_turn(st, env.ep, turn)
+                if not fused:
+                    seg = torch.arange(0, B + 1, gs, dtype=torch.int32, device=device)
+                    ops.rollout_finalize(env.ep, seg, method, norm, met, sc, pe)
+                torch.cuda.synchronize()
+                outs.append((env.room_state.clone(), env.ep.arena.clone(), norm, torch.nan_to_num(met, 9.0), sc, pe))
+            for a, b in zip(*outs):
+                assert torch.equal(a, b), (gs, method)

@@ -1,6 +1,7 @@
 // stampbench.hip — where the time of one Sokoban turn launch goes (diagnostic, not product).
 // Compiles the kernel source itself with RMI_STAMPS so every wave records s_memtime (shader
 // clock) and s_memrealtime (100 MHz) at its phase boundaries:
+// (kept in SGPRs, written at the end: no memory traffic inside the phases)
 //   0 kernel entry | 1 loads landed | 2 exec list + board decode done | 3 turn done | 4 outputs issued
 // Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -Iinclude -Iragen_amd/csrc tools/stampbench.hip -o tools/stampbench
 #define RMI_STAMPS 1
@@ -70,7 +71,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
   const int reps = 20;
-  std::vector<double> phase(5, 0.0), phase_rt(5, 0.0);
+  std::vector<double> phase(5, 0.0);
   double span_rt = 0.0, ev_us = 0.0, clk = 0.0;
   std::vector<unsigned long long> h((size_t)grid * 16);
   for (int it = 0; it < reps + 3; ++it) {
@@ -91,7 +92,6 @@ int main(int argc, char** argv) {
       const unsigned long long* s = &h[(size_t)g * 16];
       for (int p = 1; p < 5; ++p) {
         phase[p] += (double)(s[2 * p] - s[2 * (p - 1)]) / grid;
-        phase_rt[p] += (double)(s[2 * p + 1] - s[2 * (p - 1) + 1]) / grid;
       }
       rt_min = std::min(rt_min, s[1]);
       rt_max = std::max(rt_max, s[9]);
@@ -120,6 +120,6 @@ int main(int argc, char** argv) {
   printf("  back-to-back: reset %.2f us, turn %.2f us (spread<=%d)\n", t_reset, t_pair - t_reset, RMI_SPREAD_MAX_ENVS);
   const char* names[5] = {"", "loads", "decode", "turn", "outputs"};
   for (int p = 1; p < 5; ++p)
-    printf("  %-12s %8.0f cycles  %6.2f us\n", names[p], phase[p] / reps, phase_rt[p] / reps / 100.0);
+    printf("  %-12s %8.0f cycles  %6.2f us\n", names[p], phase[p] / reps, phase[p] / reps / (clk / reps));
   return 0;
 }
