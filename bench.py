@@ -220,7 +220,6 @@ def toytext_legs(device):
     B, T, K = 4096, 8, 5
     fl = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
     fl.reset(synthetic.env_seeds(B))
-    snap = [x.clone() for x in (fl.desc, fl.s, fl.rng)]
     ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=synthetic.ACTION_SEED + 1)
     ids, n = torch.from_numpy(ids).to(device), torch.from_numpy(n).to(device)
     seg = torch.arange(0, B + 1, GROUP, dtype=torch.int32, device=device)
@@ -229,9 +228,7 @@ def toytext_legs(device):
     st = fl.struct()
 
     def fl_step():
-        for dst, src in zip((fl.desc, fl.s, fl.rng), snap):
-            dst.copy_(src)
-        fl.ep.arena.zero_()
+        fl.restore()
         for t in range(T):
             ops.frozenlake_step_turn(st, fl.ep, turns[t])
         ops.rollout_finalize(fl.ep, seg, "mean_std", norm)

@@ -167,6 +167,12 @@ typedef struct {
 int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                              uint8_t* err, rmi_stream_t stream);
 
+/* Device part of FrozenLakeEnv.reset (frozen_lake/env.py:28-37) + EnvStatus(seed)
+ * (es_manager.py:95): desc / s / rng := the generated map, its start state and the seeded PCG64
+ * (generate_random_map and the seeding stay on the host), episode record zeroed — one launch.  */
+int rmi_frozenlake_reset(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const uint8_t* init_desc,
+                         const int32_t* init_s, const uint64_t* init_rng, rmi_stream_t stream);
+
 /* Replaces: FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61): codes P=0 (player), floor
  * (S, F) 1, hole 2, goal 3, player in a hole 4, player on the goal 5, through grid_lookup;
  * glyph table and output as rmi_sokoban_render (stride >= nrow*ncol*4 + nrow - 1).        */

@@ -171,8 +171,54 @@ __global__ __launch_bounds__(kBlock) void bandit_step_turn_kernel(rmi_bandit_t e
   if (err_out && err) err_out[b] |= err;
 }
 
+// Device part of FrozenLakeEnv.reset (frozen_lake/env.py:28-37) + EnvStatus(): desc / s / PCG64
+// state := the generated map, start state and seeded generator, and the episode record zeroed,
+// in one launch (thread i: env i's scalars and record, plus desc word i of the flat [B, n] map).
+__global__ __launch_bounds__(kBlock) void frozenlake_reset_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
+                                                                  const uint8_t* __restrict__ init_desc,
+                                                                  const int32_t* __restrict__ init_s,
+                                                                  const uint64_t* __restrict__ init_rng) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t B = ep.B, n = (int64_t)env.nrow * env.ncol;
+  const int64_t nbytes = B * n;
+  uint8_t* desc = const_cast<uint8_t*>(env.desc);
+  if (i < (nbytes >> 2)) reinterpret_cast<uint32_t*>(desc)[i] = reinterpret_cast<const uint32_t*>(init_desc)[i];
+  if (i < (nbytes & 3)) desc[(nbytes & ~3ll) + i] = init_desc[(nbytes & ~3ll) + i];
+  if (i < B) {
+    env.s[i] = init_s[i];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) env.rng[k * B + i] = init_rng[k * B + i];
+    ep.num_actions[i] = 0;
+    ep.flags[i] = 0;
+    ep.n_turns[i] = 0;
+    ep.penalty[i] = 0.0;
+    for (int t = 0; t < ep.T; ++t) {
+      ep.turn_reward[t * B + i] = 0.0;
+      ep.turn_info[t * B + i] = 0;
+      ep.turn_exec[t * B + i] = 0;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace rmi
+
+RMI_API int rmi_frozenlake_reset(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const uint8_t* init_desc,
+                                 const int32_t* init_s, const uint64_t* init_rng, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !ep || ep->B < 0 || ep->T <= 0) return RMI_EINVAL;
+  if (env->nrow <= 0 || env->ncol <= 0 || env->nrow * env->ncol > 64) return RMI_EUNSUP;
+  if (ep->B == 0) return RMI_OK;
+  if (!env->desc || !env->s || !env->rng || !init_desc || !init_s || !init_rng || !ep->num_actions || !ep->flags ||
+      !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
+    return RMI_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(env->desc) | reinterpret_cast<uintptr_t>(init_desc)) & 3u) return RMI_EUNSUP;
+  const int64_t nw = (int64_t)ep->B * env->nrow * env->ncol / 4;
+  const int64_t n = nw > ep->B ? nw : ep->B;
+  hipLaunchKernelGGL(frozenlake_reset_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                     as_stream(stream), *env, *ep, init_desc, init_s, init_rng);
+  return launch_status();
+}
 
 RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                      uint8_t* err, rmi_stream_t stream) {

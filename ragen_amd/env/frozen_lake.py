@@ -71,6 +71,7 @@ class FrozenLakeBatch(BatchEnv):
         self.desc = torch.zeros(self.B, n * n, dtype=torch.uint8, device=d)
         self.s = torch.zeros(self.B, dtype=torch.int32, device=d)
         self.rng = torch.zeros(4, self.B, dtype=torch.int64, device=d)  # u64 bit patterns
+        self.init_desc, self.init_s, self.init_rng = (torch.zeros_like(x) for x in (self.desc, self.s, self.rng))
         self.cs = slippery_cumsum(self.config.success_rate)
 
     def struct(self):
@@ -101,10 +102,14 @@ class FrozenLakeBatch(BatchEnv):
         self.load_state(desc, s0, rng)
 
     def load_state(self, desc, s0, rng):
-        self.desc.copy_(torch.from_numpy(np.ascontiguousarray(desc)))
-        self.s.copy_(torch.from_numpy(np.ascontiguousarray(s0, dtype=np.int32)))
-        self.rng.copy_(torch.from_numpy(np.ascontiguousarray(rng).view(np.int64)))
-        self.ep.reset_()
+        self.init_desc.copy_(torch.from_numpy(np.ascontiguousarray(desc)))
+        self.init_s.copy_(torch.from_numpy(np.ascontiguousarray(s0, dtype=np.int32)))
+        self.init_rng.copy_(torch.from_numpy(np.ascontiguousarray(rng).view(np.int64)))
+        self.restore()
+
+    def restore(self):
+        """Back to the post-reset state of the last reset() (one fused launch)."""
+        ops.frozenlake_reset(self.struct(), self.ep, self.init_desc, self.init_s, self.init_rng)
         self._invalidate()
 
     def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):

@@ -167,6 +167,14 @@ def sokoban_reset(env: _lib.Sokoban, ep: EpisodeState, init_state: torch.Tensor,
           "rmi_sokoban_reset")
 
 
+def frozenlake_reset(env: _lib.FrozenLake, ep: EpisodeState, init_desc: torch.Tensor, init_s: torch.Tensor,
+                     init_rng: torch.Tensor):
+    """Fused device reset from the generated maps (desc, start state, seeded PCG64, record)."""
+    _dev(init_desc, init_s, init_rng)
+    check(lib().rmi_frozenlake_reset(env, ep.struct(), _ptr(init_desc), _ptr(init_s), _ptr(init_rng), _stream()),
+          "rmi_frozenlake_reset")
+
+
 def frozenlake_step_turn(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn,
                          err: Optional[torch.Tensor] = None):
     check(lib().rmi_frozenlake_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_frozenlake_step_turn")

@@ -536,3 +536,22 @@ def test_fused_last_turn_finalize(device, B, T):
                 outs.append((env.room_state.clone(), env.ep.arena.clone(), norm, torch.nan_to_num(met, 9.0), sc, pe))
             for a, b in zip(*outs):
                 assert torch.equal(a, b), (gs, method)
+
+
+def test_frozenlake_restore(device):
+    """rmi_frozenlake_reset == the post-reset state: desc, start state, PCG64 state, zeroed record;
+    a rollout replayed after it is identical."""
+    B, T, K = 1000, 4, 5
+    fl = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
+    fl.reset(synthetic.env_seeds(B))
+    snap = [x.clone() for x in (fl.desc, fl.s, fl.rng)]
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=5)
+    outs = []
+    for rep in range(2):
+        fl.restore()
+        assert all(torch.equal(a, b) for a, b in zip((fl.desc, fl.s, fl.rng), snap))
+        assert int(fl.ep.arena.count_nonzero()) == 0
+        for t in range(T):
+            fl.step_turn(t, _t(ids[t], device), _t(n[t], device), None, 10, -0.1)
+        outs.append((fl.s.clone(), fl.rng.clone(), fl.ep.arena.clone()))
+    assert all(torch.equal(a, b) for a, b in zip(*outs))
