@@ -77,6 +77,14 @@ class Rollout:
             ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
         ops.sokoban_step_turn_finalize(self.st, self.env.ep, self.turns[-1], self.fin)
 
+    def step_unfused(self):
+        """The same rollout with T plain turn launches and the separate finalize launch (the
+        dominant kernel alone, for the roofline and PMC passes)."""
+        self.env.restore()
+        for t in range(T_TURNS):
+            ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
+        ops.rollout_finalize(self.env.ep, self.seg, "identity", self.norm, metrics=self.metrics)
+
     def timed_turns(self):
         """One rollout phase with HIP events (on the launch stream) around its T back-to-back
         turn launches.  A spin kernel queued first keeps the GPU busy while the host enqueues,

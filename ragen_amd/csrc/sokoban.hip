@@ -210,8 +210,6 @@ __device__ __forceinline__ uint32_t nib2(uint32_t x0, uint32_t x1) {
 // 0/1 per byte -> 0x00/0xFF per byte.  Written as a subtract/xor on purpose: (x << 8) - x is
 // folded by the compiler into x * 255, a quarter-rate v_mul_lo_u32.  0x80 - {0,1} never borrows.
 __device__ __forceinline__ uint32_t byte_mask(uint32_t x) { return (0x80808080u - x) ^ 0x80808080u; }
-// 4-bit nibble -> byte mask (bit j -> byte j = 0xFF); n < 16, so the full-rate 24-bit multiply
-__device__ __forceinline__ uint32_t unnib(uint32_t n) { return byte_mask(__umul24(n, 0x00204081u) & 0x01010101u); }
 
 // OR across the LPE lanes that share an env (consecutive lanes; DPP inside a row of 16).
 template <int LPE>
@@ -291,11 +289,13 @@ template <>
 struct WordBits<uint32_t> {
   static constexpr int kBits = 32;
   __device__ __forceinline__ static int popc(uint32_t x) { return __popc(x); }
+  __device__ __forceinline__ static int ctz(uint32_t x) { return __builtin_ctz(x); }
 };
 template <>
 struct WordBits<uint64_t> {
   static constexpr int kBits = 64;
   __device__ __forceinline__ static int popc(uint64_t x) { return __popcll(x); }
+  __device__ __forceinline__ static int ctz(uint64_t x) { return __builtin_ctzll(x); }
 };
 
 // One EnvStateManager turn (es_manager.py:149-169) of one regular room on window bitboards,
@@ -520,7 +520,11 @@ constexpr int kMaxWords = kMaxCells / 4;
 #ifndef RMI_SPREAD_MAX_ENVS  // (tools/stampbench.hip overrides it to compare the layouts)
 #define RMI_SPREAD_MAX_ENVS 4096
 #endif
-constexpr int64_t kSpreadMaxEnvs = RMI_SPREAD_MAX_ENVS;  // 4 lanes per env up to this batch
+#ifndef RMI_SPREAD_LPE
+#define RMI_SPREAD_LPE 4
+#endif
+constexpr int64_t kSpreadMaxEnvs = RMI_SPREAD_MAX_ENVS;  // RMI_SPREAD_LPE lanes per env up to this batch
+constexpr int kSpreadLpe = RMI_SPREAD_LPE;
 __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMaxEnvs; }
 
 // ------------------------------------------------------- fused end of rollout (kFin)
@@ -724,24 +728,30 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   uint8_t err = 0;
   if (__all(regular)) {
     if (act) {
+      const M box0 = box;
+      const int jp0 = jp;
       o = board_turn<M>(wall, target, box, jp, W, acts, in.K, n_act, left, nes, bot, env.num_boxes, env.max_steps,
                         turn_done, succ_last, row_changed);
-      if (row_changed) {  // rebuild this lane's row dwords: fixed, boxes 3/4, player 5
+      if (row_changed) {
         const int p = jp + W;
         r = (int)(((uint32_t)p * w_magic) >> 16);  // p / W (exact for p < 2^10, W < 2^10)
         c = p - r * W;
-        const uint64_t box64 = (uint64_t)box << W;
-#pragma unroll
-        for (int i = 0; i < NWL; ++i) {
-          const int w = sub + LPE * i;
-          if (w < row_words) {
-            const uint32_t f = xf[i], bm = unnib((uint32_t)(box64 >> (4 * w)) & 0xFu);
-            uint32_t v = (f & ~bm) | ((0x05050505u - f) & bm);
-            const int sh = 8 * (p - 4 * w);
-            v = (p >> 2) == w ? ((v & ~(0xFFu << sh)) | (5u << sh)) : v;
-            xs[i] = v;
+        // The room was regular before the turn (state == rebuild(fixed, box0, player p0)) and
+        // is after it, so the new row differs from the old one only at the old and new player
+        // cells and at the cells whose box bit flipped.  Those bytes are stored directly
+        // (rebuild values: player 5, box 3 on a target / 4, else the fixed byte 2 / 1) instead
+        // of rebuilding and storing the whole row.
+        if (sub == 0) {
+          uint8_t* win = env.room_state + b * hw + W;  // window bit j = cell W + j
+          M m = (box0 ^ box) | ((M)1 << jp0) | ((M)1 << jp);
+          while (m) {
+            const int j = WordBits<M>::ctz(m);
+            m &= m - 1;
+            const uint32_t t = (uint32_t)(target >> j) & 1u, bx = (uint32_t)(box >> j) & 1u;
+            win[j] = (uint8_t)(j == jp ? 5u : (bx ? 4u - t : 1u + t));
           }
         }
+        row_changed = false;  // stored
       }
     }
   } else {
@@ -875,7 +885,8 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
 #define RMI_LAUNCH(HW_, M_)                                                                                   \
   do {                                                                                                        \
     if (spread)                                                                                               \
-      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 4, kFin>), dim3((unsigned)((ep->B + 15) / 16)),   \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, kSpreadLpe, kFin>),                               \
+                         dim3((unsigned)((ep->B + kWave / kSpreadLpe - 1) / (kWave / kSpreadLpe))),           \
                          dim3(kWave), 0, s, *env, *ep, *in, hw, border, err, fin);                            \
     else                                                                                                      \
       hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin>), dim3(grid), dim3(kWave), 0, s, *env, *ep, \
@@ -936,7 +947,7 @@ RMI_API int rmi_sokoban_step_turn_finalize(const rmi_sokoban_t* env, const rmi_e
   if (!ep->turn_reward || !ep->turn_info || !ep->penalty || !ep->flags || !ep->n_turns || !ep->num_actions)
     return RMI_EINVAL;
   // every group inside one wave (64 envs, or 16 when 4 lanes share an env), and no partial group
-  const int per_wave = spread_lanes(ep->B) ? kWave / 4 : kWave;
+  const int per_wave = spread_lanes(ep->B) ? kWave / kSpreadLpe : kWave;
   if (per_wave % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;
   rmi_finalize_t f = *fin;
   if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member

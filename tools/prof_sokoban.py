@@ -21,7 +21,7 @@ def main():
     dev = torch.device("cuda", 0)
     R = Rollout(dev, 0, B=a.envs)
     for _ in range(a.reps):
-        R.step()
+        R.step_unfused()  # T plain turn launches: the per-launch counters of the turn kernel alone
     torch.cuda.synchronize()
     print("steps per rollout", int(R.env.ep.turn_exec.sum().item()))
 

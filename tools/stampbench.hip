@@ -17,7 +17,8 @@
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 8192, T = 5, K = 5, HW = 36;
-  const int grid = B <= RMI_SPREAD_MAX_ENVS ? (B + 15) / 16 : (B + 63) / 64;  // the launcher's lanes-per-env choice
+  const int per = 64 / RMI_SPREAD_LPE;
+  const int grid = B <= RMI_SPREAD_MAX_ENVS ? (B + per - 1) / per : (B + 63) / 64;  // the launcher's lanes-per-env choice
   uint8_t *fixed, *state, *flags, *info, *exec, *n_act, *init_state;
   int8_t *player, *acts, *init_player;
   int32_t *nes, *bot, *num_actions, *n_turns;

@@ -11,7 +11,8 @@
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
 
-__global__ void turn_loop(const uint32_t* in, int n, unsigned long long* cyc, uint32_t* out) {
+__global__ void turn_loop(const uint32_t* in, int n, unsigned long long* cyc, uint32_t* out, int W, int n_act,
+                          int left, int num_boxes, int max_steps) {
   const int i = threadIdx.x;
   const uint32_t wall = in[i], target = in[64 + i];
   uint32_t box = in[128 + i];
@@ -23,7 +24,8 @@ __global__ void turn_loop(const uint32_t* in, int n, unsigned long long* cyc, ui
   __builtin_amdgcn_s_waitcnt(0);
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < n; ++it) {
-    rmi::BoardTurn t = rmi::board_turn_k<uint32_t, 5>(wall, target, box, jp, 6, acts, 5, 1000, nes & 63, bot, 1, 1 << 30);
+    rmi::BoardTurn t =
+        rmi::board_turn_k<uint32_t, 5>(wall, target, box, jp, W, acts, n_act, left, nes & 63, bot, num_boxes, max_steps);
     acc += t.acc;
     sink += t.info + t.taken + t.stop + t.succ + t.moved;
     nes = t.nes;
@@ -60,7 +62,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dcyc, blocks * 8));
   CK(hipMemcpy(din, h.data(), h.size() * 4, hipMemcpyHostToDevice));
   for (int rep = 0; rep < 3; ++rep) {
-    hipLaunchKernelGGL(turn_loop, dim3(blocks), dim3(64), 0, 0, din, n, dcyc, dout);
+    hipLaunchKernelGGL(turn_loop, dim3(blocks), dim3(64), 0, 0, din, n, dcyc, dout, 6, 5, 1000, 1, 1 << 30);
     CK(hipDeviceSynchronize());
     std::vector<unsigned long long> c(blocks);
     CK(hipMemcpy(c.data(), dcyc, blocks * 8, hipMemcpyDeviceToHost));
