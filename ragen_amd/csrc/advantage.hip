@@ -361,103 +361,189 @@ __global__ __launch_bounds__(64) void gae_legacy_kernel(const float* __restrict_
   }
 }
 
-// Bi-level GAE on the same tiled stream as the legacy kernel: tiles of 4 rows x 64 columns in
-// a 3-deep register pipeline, staged in LDS (r, v, mask), walked right to left by one lane
-// per row with the exact per-token logic of core_algos.py:44-88 (one reverse sweep doing both levels), the
-// results staged back and stored as 16-B groups.
-struct BilevelState {
-  float hl, ll, v_next_eos, v_next_valid;
-  bool has_eos, has_valid, bad;
-  double s1, s2, cnt;
+// Bi-level GAE (core_algos.py:44-88) on the same tiled stream as the legacy kernel (tiles of
+// 4 rows x 64 columns, 3-deep register pipeline).  The reference's two sweeps are one reverse
+// sweep (the low level at a position needs the high level only at that same position), and
+// per tile it is split so that only true recurrences stay serial:
+//   P1 column-parallel (every lane, its 4 columns): eos = reward != 0 (bool()), valid = mask;
+//      the value at the next valid / next eos position to the right — a 16-lane DPP suffix
+//      selection across the row's column groups plus the carry from the tile to the right
+//      (selection only: no arithmetic, so nothing is reassociated); then each column's delta:
+//      eos -> high-level delta (r + hg * v_next_eos) - v, valid non-eos -> (r + g * v_next_valid) - v.
+//   P2 serial over the row's eos columns only (typically 0-2 per tile): hl = delta + hgl * hl,
+//      updated reward = hl + v, and the eos column's low-level delta (upd + g * 0) - v.
+//   P3 serial over the valid columns (groups with none are skipped): ll = d + gl * (eos ? 0 : ll).
+//   P4 column-parallel: outputs (valid: ll, ll + v; eos only: hl, upd; else 0) and fp64 row stats.
+// Every f32 operation is the reference's, in its order (-ffp-contract=off).
+constexpr int kBStr = kGCols + 4;  // LDS row stride (floats / bytes)
+
+struct BilevelCarry {  // per row, replicated on the row's 16 lanes
+  float v_valid, v_eos;  // value at the leftmost valid / eos position right of this tile
+  uint32_t h_valid, h_eos;
 };
 
-__device__ __forceinline__ void bilevel_col(float rt, float vt, bool m, float g, float gl, float hg, float hgl,
-                                            BilevelState& w, float& a_out, float& q_out) {
-  const bool eos = rt != 0.0f || rt != rt;  // token_level_rewards.bool()
-  float a = 0.0f, q = 0.0f, upd = rt;
-  if (eos) {
-    const float delta = (rt + (w.has_eos ? hg * w.v_next_eos : 0.0f)) - vt;
-    w.hl = delta + hgl * w.hl;
-    a = w.hl;
-    upd = w.hl + vt;  // updated_reward = advantages + values
-    q = upd;          // returns = advantages + values
-    w.v_next_eos = vt;
-    w.has_eos = true;
+// inclusive suffix selection over the 16 column groups of a DPP row: (h, v) <- first (h, v) with
+// h set at or right of this group; lanes past the row end read h = 0 (bound_ctrl)
+__device__ __forceinline__ void row_suffix_first(uint32_t& h, float& v) {
+#define RMI_SHL(K)                                                                                        \
+  {                                                                                                       \
+    const uint32_t h2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)h, 0x100 + (K), 0xF, 0xF, true);    \
+    const float v2 = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x100 + (K), 0xF, 0xF, true)); \
+    v = h ? v : v2;                                                                                       \
+    h |= h2;                                                                                              \
   }
-  if (m) {
-    float nvv;
-    if (eos) {
-      nvv = 0.0f;
-      w.ll = 0.0f;
-    } else {
-      if (!w.has_valid) w.bad = true;  // valid_positions[i + 1] -> IndexError
-      nvv = w.v_next_valid;
-    }
-    const float delta = (upd + g * nvv) - vt;
-    w.ll = delta + gl * w.ll;
-    a = w.ll;
-    q = w.ll + vt;
-    w.v_next_valid = vt;
-    w.has_valid = true;
-    w.s1 += (double)a;
-    w.s2 += (double)a * (double)a;
-    w.cnt += 1.0;
-  }
-  a_out = a;
-  q_out = q;
+  RMI_SHL(1) RMI_SHL(2) RMI_SHL(4) RMI_SHL(8)
+#undef RMI_SHL
+}
+__device__ __forceinline__ void row_shift_left1(uint32_t& h, float& v) {  // group g <- group g + 1
+  h = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)h, 0x101, 0xF, 0xF, true);
+  v = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x101, 0xF, 0xF, true));
 }
 
-__device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, BilevelState& w, float* sr, float* sv,
-                                             uint8_t* sm, int lane, bool walker, int64_t row0, int64_t B, int64_t L,
-                                             float g, float gl, float hg, float hgl, float* __restrict__ adv,
-                                             float* __restrict__ ret) {
-  const int grp = lane & 15;
+struct BilevelWalk {  // the row walker's (group-0 lane's) chain state
+  float hl, ll;
+};
+
+__device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, BilevelCarry& cy, BilevelWalk& wk,
+                                             double& s1, double& s2, double& cnt, uint32_t& bad, float* sv, float* sd,
+                                             float* sh, float* su, uint32_t* sf, int lane, int64_t row0, int64_t B,
+                                             int64_t L, float g, float gl, float hg, float hgl,
+                                             float* __restrict__ adv, float* __restrict__ ret) {
+  const int grp = lane & 15, rho = lane >> 4;
+  const F4 r4 = cur.r[0], v4 = cur.v[0];
+  const uint32_t m4 = cur.m[0];
+  const float rr[4] = {r4.x, r4.y, r4.z, r4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+  uint32_t valid[4], eos[4];
 #pragma unroll
-  for (int j = 0; j < kGLoads; ++j) {
-    const int row = 4 * j + (lane >> 4);
-    *reinterpret_cast<F4*>(sr + row * kGStr + 4 * grp) = cur.r[j];
-    *reinterpret_cast<F4*>(sv + row * kGStr + 4 * grp) = cur.v[j];
-    *reinterpret_cast<uint32_t*>(sm + row * kGMStr + 4 * grp) = cur.m[j];
+  for (int e = 0; e < 4; ++e) {
+    valid[e] = ((m4 >> (8 * e)) & 0xFFu) != 0;
+    eos[e] = rr[e] != 0.0f || rr[e] != rr[e];  // token_level_rewards.bool()
   }
+  // ---- P1: next valid / next eos values, columns' deltas
+  uint32_t hv = 0, he = 0;
+  float fv = 0.0f, fe = 0.0f;  // leftmost valid / eos value of this group
+#pragma unroll
+  for (int e = 3; e >= 0; --e) {
+    fv = valid[e] ? vv[e] : fv;
+    hv |= valid[e];
+    fe = eos[e] ? vv[e] : fe;
+    he |= eos[e];
+  }
+  uint32_t hsv = hv, hse = he;
+  float vsv = fv, vse = fe;
+  row_suffix_first(hsv, vsv);
+  row_suffix_first(hse, vse);
+  uint32_t nhv = hsv, nhe = hse;  // groups strictly right of this one
+  float nvv = vsv, nve = vse;
+  row_shift_left1(nhv, nvv);
+  row_shift_left1(nhe, nve);
+  nvv = nhv ? nvv : cy.v_valid;
+  nhv |= cy.h_valid;
+  nve = nhe ? nve : cy.v_eos;
+  nhe |= cy.h_eos;
+  float d[4];
+  uint32_t fl = 0;
+#pragma unroll
+  for (int e = 3; e >= 0; --e) {
+    if (eos[e]) d[e] = (rr[e] + (nhe ? hg * nve : 0.0f)) - vv[e];          // high-level delta
+    else d[e] = (rr[e] + g * (nhv ? nvv : 0.0f)) - vv[e];                   // low level (upd = reward)
+    bad |= valid[e] & (eos[e] ^ 1u) & (nhv ^ 1u);                            // valid_positions[i + 1]
+    fl |= (valid[e] | (eos[e] << 1)) << (8 * e);
+    nvv = valid[e] ? vv[e] : nvv;
+    nhv |= valid[e];
+    nve = eos[e] ? vv[e] : nve;
+    nhe |= eos[e];
+  }
+  // the next tile to the left continues from this tile's leftmost valid / eos position
+  const int lead = lane & ~15;
+  const uint32_t row_hv = (uint32_t)__shfl((int)hsv, lead), row_he = (uint32_t)__shfl((int)hse, lead);
+  const float row_vv = __shfl(vsv, lead), row_ve = __shfl(vse, lead);
+  cy.v_valid = row_hv ? row_vv : cy.v_valid;
+  cy.h_valid |= row_hv;
+  cy.v_eos = row_he ? row_ve : cy.v_eos;
+  cy.h_eos |= row_he;
+  const int o = rho * kBStr + 4 * grp;
+  *reinterpret_cast<F4*>(sv + o) = v4;
+  *reinterpret_cast<F4*>(sd + o) = F4{d[0], d[1], d[2], d[3]};
+  sf[rho * (kBStr / 4) + grp] = fl;
+  const uint64_t any_eos = __ballot(he), any_valid = __ballot(hv);
   __syncthreads();
-  if (walker) {
-    float* pr = sr + lane * kGStr;
-    float* pv = sv + lane * kGStr;
-    const uint8_t* pm = sm + lane * kGMStr;
-    for (int q = kGCols / 4 - 1; q >= 0; --q) {
-      const F4 r4 = *reinterpret_cast<const F4*>(pr + 4 * q);
-      const F4 v4 = *reinterpret_cast<const F4*>(pv + 4 * q);
-      const uint32_t m4 = *reinterpret_cast<const uint32_t*>(pm + 4 * q);
-      F4 a4, t4;
-      bilevel_col(r4.w, v4.w, (m4 >> 24) & 0xFF, g, gl, hg, hgl, w, a4.w, t4.w);
-      bilevel_col(r4.z, v4.z, (m4 >> 16) & 0xFF, g, gl, hg, hgl, w, a4.z, t4.z);
-      bilevel_col(r4.y, v4.y, (m4 >> 8) & 0xFF, g, gl, hg, hgl, w, a4.y, t4.y);
-      bilevel_col(r4.x, v4.x, m4 & 0xFF, g, gl, hg, hgl, w, a4.x, t4.x);
-      *reinterpret_cast<F4*>(pr + 4 * q) = a4;
-      *reinterpret_cast<F4*>(pv + 4 * q) = t4;
+  // ---- P2 / P3: the row walkers (group-0 lanes)
+  if (grp == 0) {
+    const float* pv = sv + rho * kBStr;
+    float* pd = sd + rho * kBStr;
+    float* ph = sh + rho * kBStr;
+    float* pu = su + rho * kBStr;
+    const uint32_t* pf = sf + rho * (kBStr / 4);
+    uint32_t ge = (uint32_t)(any_eos >> (16 * rho)) & 0xFFFFu;
+    while (ge) {  // eos groups, right to left
+      const int q = 31 - __clz(ge);
+      ge &= ~(1u << q);
+      const uint32_t f4 = pf[q];
+#pragma unroll
+      for (int e = 3; e >= 0; --e) {
+        if ((f4 >> (8 * e + 1)) & 1u) {
+          const int c = 4 * q + e;
+          wk.hl = pd[c] + hgl * wk.hl;
+          const float vt = pv[c], upd = wk.hl + vt;  // updated_reward = returns = advantages + values
+          ph[c] = wk.hl;
+          pu[c] = upd;
+          if (f4 >> (8 * e) & 1u) pd[c] = (upd + g * 0.0f) - vt;  // its low-level delta (nextvalue = 0)
+        }
+      }
+    }
+    uint32_t gv = (uint32_t)(any_valid >> (16 * rho)) & 0xFFFFu;
+    while (gv) {  // valid groups, right to left
+      const int q = 31 - __clz(gv);
+      gv &= ~(1u << q);
+      const uint32_t f4 = pf[q];
+      F4 d4 = *reinterpret_cast<const F4*>(pd + 4 * q);
+      float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int e = 3; e >= 0; --e) {
+        if ((f4 >> (8 * e)) & 1u) {
+          wk.ll = dd[e] + gl * (((f4 >> (8 * e + 1)) & 1u) ? 0.0f : wk.ll);  // reset at an eos
+          dd[e] = wk.ll;
+        }
+      }
+      *reinterpret_cast<F4*>(pd + 4 * q) = F4{dd[0], dd[1], dd[2], dd[3]};
     }
   }
   __syncthreads();
-  const int64_t col = c0 + 4 * grp;
+  // ---- P4: outputs and row stats
+  const F4 a4 = *reinterpret_cast<const F4*>(sd + o);
+  const F4 h4 = *reinterpret_cast<const F4*>(sh + o);
+  const F4 u4 = *reinterpret_cast<const F4*>(su + o);
+  const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, hh[4] = {h4.x, h4.y, h4.z, h4.w}, uu[4] = {u4.x, u4.y, u4.z, u4.w};
+  float oa[4], oq[4];
 #pragma unroll
-  for (int j = 0; j < kGLoads; ++j) {
-    const int row = 4 * j + (lane >> 4);
-    const int64_t grow = row0 + row;
-    if (grow < B && col >= 0 && col < L) {
-      const F4 a4 = *reinterpret_cast<const F4*>(sr + row * kGStr + 4 * grp);
-      const F4 t4 = *reinterpret_cast<const F4*>(sv + row * kGStr + 4 * grp);
-      const int64_t o = grow * L + col;
-      if (col + 4 <= L) {
-        *reinterpret_cast<F4*>(adv + o) = a4;
-        *reinterpret_cast<F4*>(ret + o) = t4;
-      } else {
-        const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
-        for (int e = 0; e < 4; ++e)
-          if (col + e < L) {
-            adv[o + e] = aa[e];
-            ret[o + e] = tt[e];
-          }
-      }
+  for (int e = 0; e < 4; ++e) {
+    if (valid[e]) {
+      oa[e] = aa[e];
+      oq[e] = aa[e] + vv[e];
+      s1 += (double)aa[e];
+      s2 += (double)aa[e] * (double)aa[e];
+      cnt += 1.0;
+    } else if (eos[e]) {
+      oa[e] = hh[e];
+      oq[e] = uu[e];
+    } else {
+      oa[e] = 0.0f;
+      oq[e] = 0.0f;
+    }
+  }
+  const int64_t grow = row0 + rho, col = c0 + 4 * grp;
+  if (grow < B && col >= 0 && col < L) {
+    const int64_t go = grow * L + col;
+    if (col + 4 <= L) {
+      *reinterpret_cast<F4*>(adv + go) = F4{oa[0], oa[1], oa[2], oa[3]};
+      *reinterpret_cast<F4*>(ret + go) = F4{oq[0], oq[1], oq[2], oq[3]};
+    } else {
+      for (int e = 0; e < 4; ++e)
+        if (col + e < L) {
+          adv[go + e] = oa[e];
+          ret[go + e] = oq[e];
+        }
     }
   }
   __syncthreads();
@@ -469,37 +555,46 @@ __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restri
                                                            float* __restrict__ adv, float* __restrict__ ret,
                                                            double* __restrict__ row_stats,
                                                            uint8_t* __restrict__ err) {
-  __shared__ __attribute__((aligned(16))) float sr[kGRows * kGStr];
-  __shared__ __attribute__((aligned(16))) float sv[kGRows * kGStr];
-  __shared__ __attribute__((aligned(16))) uint8_t sm[kGRows * kGMStr];
+  static_assert(kGLoads == 1 && kGRows * 16 == 64, "one 4-column group per lane");
+  __shared__ __attribute__((aligned(16))) float sv[kGRows * kBStr];
+  __shared__ __attribute__((aligned(16))) float sd[kGRows * kBStr];
+  __shared__ __attribute__((aligned(16))) float sh[kGRows * kBStr];
+  __shared__ __attribute__((aligned(16))) float su[kGRows * kBStr];
+  __shared__ uint32_t sf[kGRows * kBStr / 4];
   const int lane = threadIdx.x;
   const int64_t row0 = (int64_t)blockIdx.x * kGRows;
   const int64_t ntiles = (L + kGCols - 1) / kGCols;
-  const bool walker = lane < kGRows && row0 + lane < B;
-  BilevelState w;
-  w.hl = w.ll = w.v_next_eos = w.v_next_valid = 0.0f;
-  w.has_eos = w.has_valid = w.bad = false;
-  w.s1 = w.s2 = w.cnt = 0.0;
+  BilevelCarry cy{0.0f, 0.0f, 0u, 0u};
+  BilevelWalk wk{0.0f, 0.0f};
+  double s1 = 0.0, s2 = 0.0, cnt = 0.0;
+  uint32_t bad = 0;
   GaeTile ta, tb, tc;
   const int64_t k0 = ntiles - 1;
   gae_load_tile(ta, r, v, mask, B, L, row0, k0 * kGCols, lane);
   gae_load_tile(tb, r, v, mask, B, L, row0, (k0 - 1) * kGCols, lane);
   for (int64_t k = k0; k >= 0; k -= 3) {
     gae_load_tile(tc, r, v, mask, B, L, row0, (k - 2) * kGCols, lane);
-    bilevel_tile(ta, k * kGCols, w, sr, sv, sm, lane, walker, row0, B, L, g, gl, hg, hgl, adv, ret);
+    bilevel_tile(ta, k * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg, hgl,
+                 adv, ret);
+    if (k - 1 < 0) break;
     gae_load_tile(ta, r, v, mask, B, L, row0, (k - 3) * kGCols, lane);
-    bilevel_tile(tb, (k - 1) * kGCols, w, sr, sv, sm, lane, walker, row0, B, L, g, gl, hg, hgl, adv, ret);
+    bilevel_tile(tb, (k - 1) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
+                 hgl, adv, ret);
+    if (k - 2 < 0) break;
     gae_load_tile(tb, r, v, mask, B, L, row0, (k - 4) * kGCols, lane);
-    bilevel_tile(tc, (k - 2) * kGCols, w, sr, sv, sm, lane, walker, row0, B, L, g, gl, hg, hgl, adv, ret);
+    bilevel_tile(tc, (k - 2) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
+                 hgl, adv, ret);
   }
-  if (walker) {
-    const int64_t row = row0 + lane;
+  const double a = xor_sum16(s1), b2 = xor_sum16(s2), n = xor_sum16(cnt);
+  const uint64_t bads = __ballot(bad);
+  const int64_t row = row0 + (lane >> 4);
+  if ((lane & 15) == 0 && row < B) {
     if (row_stats) {
-      row_stats[3 * row + 0] = w.s1;
-      row_stats[3 * row + 1] = w.s2;
-      row_stats[3 * row + 2] = w.cnt;
+      row_stats[3 * row + 0] = a;
+      row_stats[3 * row + 1] = b2;
+      row_stats[3 * row + 2] = n;
     }
-    if (err) err[row] = w.bad ? RMI_ERR_INDEX : 0;
+    if (err) err[row] = ((bads >> (lane & ~15)) & 0xFFFFull) ? RMI_ERR_INDEX : 0;
   }
 }
 

@@ -555,3 +555,34 @@ def test_frozenlake_restore(device):
             fl.step_turn(t, _t(ids[t], device), _t(n[t], device), None, 10, -0.1)
         outs.append((fl.s.clone(), fl.rng.clone(), fl.ep.arena.clone()))
     assert all(torch.equal(a, b) for a, b in zip(*outs))
+
+
+@pytest.mark.parametrize("B", [1000, 8192])
+def test_bilevel_vs_oracle_large(device, B):
+    """Bi-level GAE at SK-like shapes vs the C oracle: returns and pre-whitening advantages
+    bit-exact, the IndexError rows identical; turn rewards with zeros, negative and NaN-free
+    values, rows ending in mask-0 and in mask-1 without reward, ragged L % 4."""
+    rng = np.random.default_rng(B)
+    n_turns = rng.integers(1, 6, B).astype(np.int32)
+    tr = rng.choice([0.0, 0.5, -1.1, 10.9], size=(B, 5), p=[0.2, 0.4, 0.2, 0.2]).astype(np.float32)
+    r, v, m = synthetic.token_rows(n_turns, rng.standard_normal(B).astype(np.float32), seed=B, turn_scores=tr)
+    pad = 1 if (r.shape[1] + 1) % 4 else 2  # trailing mask-0 columns, L % 4 != 0
+    r, v, m = (np.pad(x, ((0, 0), (0, pad))) for x in (r, v, m))
+    rd, vd, md = _t(r, device), _t(v, device), _t(m, device)
+    for g, lam, hg in ((1.0, 1.0, 0.95), (0.99, 0.95, 0.9)):
+        oa, oret, oerr = oracle.bilevel_gae(r, v, m, g, lam, hg)
+        assert 0 < int((oerr != 0).sum()) < B  # rows whose last turn scored 0 raise IndexError
+        adv, ret = ops.bilevel_gae(rd, vd, md, g, lam, hg, check_errors=False)
+        ok = oerr == 0  # rows the reference completes
+        np.testing.assert_array_equal(ret.cpu().numpy()[ok], oret[ok])
+        np.testing.assert_array_equal(adv.cpu().numpy()[ok], oa[ok])
+        stats = torch.empty(B, 3, dtype=torch.float64, device=device)
+        errs = torch.empty(B, dtype=torch.uint8, device=device)
+        check = ops.lib().rmi_bilevel_gae(ops._ptr(rd), ops._ptr(vd), ops._ptr(md), B, r.shape[1], g, lam, hg,
+                                          ops._ptr(adv), ops._ptr(ret), ops._ptr(stats), ops._ptr(errs),
+                                          ops._stream())
+        assert check == 0
+        np.testing.assert_array_equal(errs.cpu().numpy() != 0, oerr != 0)
+        s1 = (oa.astype(np.float64) * m).sum(1)
+        np.testing.assert_allclose(stats[:, 0].cpu().numpy()[ok], s1[ok], rtol=1e-12, atol=1e-9)
+        np.testing.assert_array_equal(stats[:, 2].cpu().numpy(), m.sum(1).astype(np.float64))
