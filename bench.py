@@ -278,6 +278,91 @@ def toytext_legs(device):
     return out
 
 
+def text_leg(R, device, reps=20):
+    """SURVEY §8(f) rank 2 on the bench's workload: the response -> action boundary on the device.
+    * parse: rmi_parse_actions (_parse_response + name -> id map) over 8192 LLM-shaped
+      responses of this rollout's turn-0 actions; algorithmic bytes = the text bytes read +
+      the outputs (K action ids, n_actions, 4 spans) per row;
+    * detokenize: rmi_detokenize over [8192, 128] token ids of a Qwen-sized (151 646) synthetic
+      byte-level vocabulary; bytes = 8 per id in + the decoded bytes out;
+    * text rollout: the SK rollout driven from text (restore + 5 x (parse + turn) + finalize in
+      a HIP graph) -> env-steps/s of the device-resident text API."""
+    B = R.B
+    lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
+    ids_h, n_h = R.ids.cpu().numpy(), R.n.cpu().numpy()
+    bufs = []
+    for t in range(T_TURNS):
+        texts = synthetic.responses_for_actions(ids_h[t], n_h[t], lk, seed=100 + t)
+        buf, lens = synthetic.encode_rows(texts)
+        bufs.append((torch.from_numpy(buf).to(device), torch.from_numpy(lens).to(device)))
+    cfg = ops.parse_config(True, K_ACTIONS, "||", lk)
+    text, tlen = bufs[0]
+    for _ in range(3):
+        out = ops.parse_actions(cfg, text, tlen)
+    torch.cuda.synchronize()
+    assert torch.equal(out["actions"], R.ids[0]) and torch.equal(out["n_actions"], R.n[0])
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(reps):
+        ops.parse_actions(cfg, text, tlen)
+    e[1].record()
+    torch.cuda.synchronize()
+    parse_us = e[0].elapsed_time(e[1]) * 1e3 / reps
+    text_bytes = int(((tlen.to(torch.int64) + 3) // 4 * 4).sum().item())
+    pbytes = text_bytes + B * (4 + K_ACTIONS + 1 + 16)
+    # detokenize
+    V, Rt = 151646, 128
+    rng = np.random.default_rng(5)
+    lens_v = rng.integers(1, 9, size=V)
+    data = rng.integers(97, 123, size=int(lens_v.sum())).astype(np.uint8)
+    off = np.zeros(V + 1, np.int64)
+    np.cumsum(lens_v, out=off[1:])
+    skip = np.zeros(V, np.uint8)
+    skip[151643:] = 1
+    vt = ops.VocabTable(torch.from_numpy(off).to(device), torch.from_numpy(data).to(device),
+                        torch.from_numpy(skip).to(device))
+    tok = torch.from_numpy(rng.integers(0, 151643, size=(B, Rt)).astype(np.int64)).to(device)
+    for _ in range(3):
+        dt_out, dt_len, _ = ops.detokenize(tok, vt, 2048)
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(reps):
+        ops.detokenize(tok, vt, 2048)
+    e[1].record()
+    torch.cuda.synchronize()
+    detok_us = e[0].elapsed_time(e[1]) * 1e3 / reps
+    dbytes = B * Rt * 8 + int(dt_len.sum().item())
+    # the rollout driven from text
+    text_turns = []
+    for t in range(T_TURNS):
+        o = ops.parse_actions(cfg, bufs[t][0], bufs[t][1], with_spans=False)
+        text_turns.append((o, ops.turn_struct(t, o["actions"], o["n_actions"], None, MAX_ACTIONS, -0.1)))
+
+    def text_step():
+        R.env.restore()
+        for t in range(T_TURNS):
+            o, ts = text_turns[t]
+            ops.parse_actions(cfg, bufs[t][0], bufs[t][1], with_spans=False, out=o)
+            if t < T_TURNS - 1:
+                ops.sokoban_step_turn(R.st, R.env.ep, ts)
+            else:
+                ops.sokoban_step_turn_finalize(R.st, R.env.ep, ts, R.fin)
+    text_step()
+    torch.cuda.synchronize()
+    steps = int(R.env.ep.turn_exec.sum().item())
+    ms = _graph_rollout(text_step)
+    return {"parse": {"kernel": "rmi_parse_actions", "rows": B, "text_bytes": text_bytes, "us": parse_us,
+                      "achieved_GBs": pbytes / (parse_us * 1e-6) / 1e9,
+                      "frac": pbytes / (parse_us * 1e-6) / 1e9 / HBM_PEAK_GBS},
+            "detokenize": {"kernel": "rmi_detokenize", "rows": B, "ids_per_row": Rt, "vocab": V, "us": detok_us,
+                           "achieved_GBs": dbytes / (detok_us * 1e-6) / 1e9,
+                           "frac": dbytes / (detok_us * 1e-6) / 1e9 / HBM_PEAK_GBS},
+            "text_rollout": {"config": "SK rollout from response text: restore + 5 x (parse + turn) + finalize",
+                             "env_steps_per_rollout": steps, "ms_per_rollout": ms,
+                             "env_steps_per_s": steps / ms * 1e3}}
+
+
 def api_leg(device):
     """SURVEY §8(d)'s "API" variant of the headline: the same SK workload driven through the
     drop-in EnvStateManager (list-of-dict inputs with action NAMES, per-turn device round trip,
@@ -585,6 +670,7 @@ def main():
     copy_peak = hbm_copy_peak(device) if not args.no_extras else None
     toytext = toytext_legs(device) if not args.no_extras else None
     api = api_leg(device) if not args.no_extras and rank == 0 else None
+    text = text_leg(R, device) if not args.no_extras and rank == 0 else None
 
     if rank == 0:
         cpu = cpu_par = None
@@ -632,6 +718,7 @@ def main():
             "advantage": adv,
             "toytext": toytext,
             "api_variant": api,
+            "text_api": text,
             "exchange": ("all-gather of the episode arena per rollout"
                          + (f", one captured all-gather per {G} rollouts, "
                             + (f"overlapped with the next {G} on a comm stream" if exchange_mode == "overlap"

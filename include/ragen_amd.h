@@ -293,6 +293,53 @@ int rmi_masked_whiten(float* x, const uint8_t* mask, int64_t B, int64_t L, const
 int rmi_grpo_outcome(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G,
                      double eps, int32_t norm_by_std, float* adv, float* ret, rmi_stream_t stream);
 
+/* ------------------------------------------------ response -> action ids (§8(f) rank 2)
+ * Replaces: ContextManager.get_env_inputs (ctx_manager.py:332-352): the tokenizer's
+ *           batch_decode(responses, skip_special_tokens=True) (:334-337), the "<think>" /
+ *           "<answer>" prefix (:338-339), _parse_response (:148-173); and
+ *           EnvStateManager._extract_map_valid_actions (es_manager.py:230-240).
+ *
+ * rmi_detokenize: byte-level BPE decoding (the tokenizers ByteLevel decoder).  Token id t
+ * contributes vocab_bytes[vocab_off[t] .. vocab_off[t+1]) unless skip[t] (special tokens);
+ * the concatenation is UTF-8 decoded with U+FFFD replacing each maximal invalid subpart
+ * (String::from_utf8_lossy) and written back as UTF-8: out[b, 0 .. out_len[b]) is exactly
+ * decoded_str.encode("utf-8").  ids [B,R] (n_ids[b] <= R ids used per row, NULL = R).
+ * err[b]: RMI_ERR_INDEX for an id outside [0, V), RMI_ERR_UNSUP when the text exceeds
+ * `stride` bytes (truncated).  stride % 4 == 0, stride <= 16384.                         */
+int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const int64_t* vocab_off,
+                   const uint8_t* vocab_bytes, int64_t V, const uint8_t* skip, uint8_t* out, int32_t stride,
+                   int32_t* out_len, uint8_t* err, rmi_stream_t stream);
+
+/* Parse configuration (agent_proxy.* and the env's action_lookup).  Strings are packed
+ * little-endian into two u64 words (byte k of the string = byte k of lo|hi).             */
+#define RMI_PARSE_MAX_NAMES 8
+typedef struct {
+  int32_t enable_think;     /* agent_proxy.enable_think: <think>(.*?)</think>\s*<answer>(.*?)</answer>
+                               else <answer>(.*?)</answer>  (re.DOTALL, re.search)          */
+  int32_t prepend;          /* 1: the text lacks the "<think>"/"<answer>" tag that
+                               get_env_inputs prepends (ctx_manager.py:338-339)            */
+  int32_t K;                /* agent_proxy.max_actions_per_turn (<= 8)                     */
+  int32_t sep_len;          /* agent_proxy.action_sep, 1..16 bytes ("||")                  */
+  uint64_t sep_lo, sep_hi;
+  int32_t n_names;          /* 0: env has no action_lookup (actions pass through as text)  */
+  uint8_t name_len[RMI_PARSE_MAX_NAMES];   /* lowercased ASCII names, <= 16 bytes         */
+  uint64_t name_lo[RMI_PARSE_MAX_NAMES], name_hi[RMI_PARSE_MAX_NAMES];
+  int8_t name_id[2][RMI_PARSE_MAX_NAMES];  /* action id of each name; column sel[b]       */
+} rmi_parse_cfg_t;
+
+/* One response per row: text[b, 0 .. text_len[b]) (UTF-8, row stride `stride`).
+ * Outputs: actions[b,k] = action_lookup id of action k (0 = name not in the lookup, dropped
+ * by the step kernels) and n_actions[b] = len(actions) after the max_actions_per_turn cap —
+ * exactly the rmi_turn_t inputs.  Optional: sel[b] picks the id column (Bandit's per-env
+ * lookup, bandit/env.py:25-39); spans[b,4] = think [start, end), answer [start, end) in the
+ * prefixed text (all -1: no match); action_text [B,K,Lact] / action_len [B,K] = the stripped
+ * action strings (Countdown's answers).  err[b] |= RMI_ERR_UNSUP when an action is longer
+ * than Lact, RMI_ERR_STATE when text_len[b] is outside [0, stride].
+ * stride % 4 == 0, stride <= 16384.                                                        */
+int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, const int32_t* text_len, int64_t B,
+                      int32_t stride, const uint8_t* sel, int8_t* actions, uint8_t* n_actions, int32_t* spans,
+                      uint8_t* action_text, int32_t* action_len, int32_t Lact, uint8_t* err, rmi_stream_t stream);
+
 /* ------------------------------------------------------------------------- misc */
 const char* rmi_version(void);
 int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t stream);

@@ -61,6 +61,16 @@ class Countdown(ctypes.Structure):
                 ("n_nums", c_void_p), ("target", c_void_p)]
 
 
+PARSE_MAX_NAMES = 8
+
+
+class ParseCfg(ctypes.Structure):
+    _fields_ = [("enable_think", c_int32), ("prepend", c_int32), ("K", c_int32), ("sep_len", c_int32),
+                ("sep_lo", ctypes.c_uint64), ("sep_hi", ctypes.c_uint64), ("n_names", c_int32),
+                ("name_len", ctypes.c_uint8 * PARSE_MAX_NAMES), ("name_lo", ctypes.c_uint64 * PARSE_MAX_NAMES),
+                ("name_hi", ctypes.c_uint64 * PARSE_MAX_NAMES), ("name_id", (ctypes.c_int8 * PARSE_MAX_NAMES) * 2)]
+
+
 _P = ctypes.POINTER
 _SIGS = {
     "rmi_version": (ctypes.c_char_p, []),
@@ -99,6 +109,10 @@ _SIGS = {
     "rmi_masked_whiten": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "rmi_grpo_outcome": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_double, c_int32,
                                    c_void_p, c_void_p, c_void_p]),
+    "rmi_detokenize": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                 c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "rmi_parse_actions": (c_int32, [_P(ParseCfg), c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 

@@ -19,6 +19,18 @@ inline int launch_status() {
 
 inline hipStream_t as_stream(rmi_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// 64-lane inclusive prefix sum on DPP (no LDS): row_shr 1/2/4/8 inside each 16-lane row,
+// then row_bcast:15 / row_bcast:31 carry the row totals across rows (gfx9 DPP).
+__device__ __forceinline__ int wave_inclusive_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // --------------------------------------------------------------- PCG64 (numpy)
 // numpy PCG64 = pcg_setseq_128_xsl_rr_64: step state = state*M + inc (mod 2^128),
 // then output XSL-RR of the NEW state; Generator.random() = (out >> 11) * 2^-53.

@@ -29,18 +29,6 @@ struct __attribute__((packed, aligned(4))) F4u {
   float x, y, z, w;
 };
 
-// 64-lane inclusive prefix sum on DPP (no LDS): row_shr 1/2/4/8 inside each 16-lane row,
-// then row_bcast:15 / row_bcast:31 carry the row totals across rows (gfx9 DPP).
-__device__ __forceinline__ int wave_inclusive_scan(int x) {
-  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
-  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
-  return x;
-}
-
 constexpr int kSuper = 8;  // chunks whose loads are issued together (2048 ids per row)
 
 __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ ids, int64_t B, int64_t S, int64_t sp,

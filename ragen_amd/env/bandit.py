@@ -62,6 +62,14 @@ class BanditBatch(BatchEnv):
         self._last_obs = [None] * self.B
         self._invalidate()
 
+    def parse_setup(self, enable_think: bool, action_sep: str, prepend: bool = True):
+        """Per-env lookup (bandit/env.py:25-39): column 1 = hi arm first, selected by hi_is_first."""
+        c, s = self.config, int(self.config.action_space_start)
+        lo_first = {s: c.lo_arm_name, s + 1: c.hi_arm_name}
+        hi_first = {s: c.hi_arm_name, s + 1: c.lo_arm_name}
+        return ops.parse_config(enable_think, self.K, action_sep, lo_first, hi_first, prepend=prepend), \
+            self.hi_is_first, 0
+
     def action_lookup(self, i):
         c, s = self.config, int(self.config.action_space_start)
         if self._hi_first_host[i]:

@@ -57,6 +57,12 @@ class BatchEnv:
     def get_all_actions(self):
         return list(self.action_lookup(0).keys())
 
+    def parse_setup(self, enable_think: bool, action_sep: str, prepend: bool = True):
+        """Device parse configuration of this env type (ops.parse_config) for the
+        response -> action-id kernel: -> (rmi_parse_cfg_t, sel u8[B] | None, action-text bytes)."""
+        from .. import ops
+        return ops.parse_config(enable_think, self.K, action_sep, self.action_lookup(0), prepend=prepend), None, 0
+
     def close(self):
         self._host = None
         self._text = None

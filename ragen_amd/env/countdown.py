@@ -88,6 +88,10 @@ class CountdownBatch(BatchEnv):
         self._last_obs = [None] * self.B
         self._invalidate()
 
+    def parse_setup(self, enable_think: bool, action_sep: str, prepend: bool = True):
+        """No action_lookup: the answers pass through as text (es_manager.py:235-236)."""
+        return ops.parse_config(enable_think, self.K, action_sep, None, prepend=prepend), None, self.Lmax
+
     def encode_answers(self, answers: List[List[str]]):
         """[B][<=K] answer strings -> (u8[B,K,Lmax], i32[B,K]) host arrays (UTF-8)."""
         buf = np.zeros((self.B, self.K, self.Lmax), np.uint8)

@@ -200,6 +200,34 @@ class EnvStateManager:
         return tg.batch.ep
 
     # ------------------------------------------------------- get_rollout_states
+    def step_text(self, text: torch.Tensor, text_len: torch.Tensor, has_input: Optional[torch.Tensor] = None,
+                  enable_think: bool = True, action_sep: str = "||", prepend: bool = True):
+        """Device-resident turn from response text (§8(f) rank 2): rows are the envs in env-id
+        order, text u8[n_envs, stride] / text_len i32[n_envs] the decoded generations (e.g.
+        ops.detokenize of the response ids).  Per tag one parse launch
+        (_parse_response + _extract_map_valid_actions, ctx_manager.py:148-173,
+        es_manager.py:230-240) feeds one turn launch; nothing returns to the host.
+        -> list of per-tag parse outputs (ops.parse_actions dicts)."""
+        if self._turn >= self.max_turn:
+            raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
+        from .. import ops
+        if text.shape[0] != self.n_envs or text_len.shape[0] != self.n_envs:
+            raise ValueError(f"text rows must cover all {self.n_envs} envs")
+        outs = []
+        for tg in self.tags:
+            cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, prepend)
+            p = ops.parse_actions(cfg, text[tg.lo:tg.hi], text_len[tg.lo:tg.hi], sel, with_spans=False,
+                                  action_text_len=lact)
+            has = None if has_input is None else has_input[tg.lo:tg.hi]
+            kw = {}
+            if lact:
+                kw = {"answers": p["action_text"], "answer_len": p["action_len"]}
+            tg.batch.step_turn(self._turn, p["actions"], p["n_actions"], has, tg.max_actions_per_traj,
+                               self.format_penalty, **kw)
+            outs.append(p)
+        self._turn += 1
+        return outs
+
     def get_rollout_states(self):
         """es_manager.py:173-207 (per-env metrics reduced on the device)."""
         from .. import ops

@@ -5,6 +5,7 @@ on torch's current stream and returns without synchronising.  Validation mirrors
 reference's error behaviour (ValueError for bad arguments; IndexError for the bi-level
 GAE case the reference raises on, core_algos.py:79, when ``check=True``).
 """
+import ctypes
 from dataclasses import dataclass
 from typing import Optional
 
@@ -328,6 +329,170 @@ def sokoban_render(env: _lib.Sokoban, B: int, lookup, device):
 def frozenlake_render(env: _lib.FrozenLake, B: int, lookup, device):
     """FrozenLakeEnv.render text of every env (frozen_lake/env.py:47-61) -> (u8[B,stride], i32[B])."""
     return _render(lib().rmi_frozenlake_render, env, B, env.nrow * env.ncol, env.nrow, lookup, device)
+
+
+# ------------------------------------------------- response -> action ids (§8(f) rank 2)
+def _pack16(b: bytes):
+    if not 1 <= len(b) <= 16:
+        raise ValueError(f"string of {len(b)} bytes: 1..16 supported")
+    v = b.ljust(16, b"\0")
+    return int.from_bytes(v[:8], "little"), int.from_bytes(v[8:], "little")
+
+
+def parse_config(enable_think: bool, max_actions_per_turn: int, action_sep: str = "||", action_lookup=None,
+                 swapped_lookup=None, prepend: bool = True) -> _lib.ParseCfg:
+    """rmi_parse_cfg_t for agent_proxy.{enable_think, max_actions_per_turn, action_sep} and an env's
+    action_lookup ({id: name}; None = actions pass through as text).  ``swapped_lookup`` is the
+    second id column selected per env by ``sel`` (Bandit's per-env lookup, bandit/env.py:25-39);
+    it must name the same strings.  Names are matched as ``name.lower()`` (es_manager.py:237-239);
+    duplicate lowered names keep the last id, as the dict comprehension does."""
+    c = _lib.ParseCfg()
+    c.enable_think, c.prepend, c.K = int(bool(enable_think)), int(bool(prepend)), int(max_actions_per_turn)
+    c.sep_len = len(action_sep.encode("utf-8"))
+    c.sep_lo, c.sep_hi = _pack16(action_sep.encode("utf-8"))
+    if action_lookup is None:
+        c.n_names = 0
+        return c
+    cols = []
+    for lk in (action_lookup, swapped_lookup if swapped_lookup is not None else action_lookup):
+        rev = {}
+        for k, v in lk.items():
+            rev[str(v).lower()] = int(k)
+        cols.append(rev)
+    if set(cols[0]) != set(cols[1]):
+        raise ValueError("swapped_lookup must name the same actions")
+    names = list(cols[0])
+    if len(names) > _lib.PARSE_MAX_NAMES:
+        raise NotImplementedError(f"{len(names)} action names > {_lib.PARSE_MAX_NAMES}")
+    c.n_names = len(names)
+    for j, nm in enumerate(names):
+        b = nm.encode("utf-8")
+        if not nm.isascii():
+            raise NotImplementedError(f"non-ASCII action name {nm!r}")
+        c.name_len[j] = len(b)
+        c.name_lo[j], c.name_hi[j] = _pack16(b)
+        for col in range(2):
+            i = cols[col][nm]
+            if not 1 <= i <= 127:
+                raise NotImplementedError(f"action id {i}: 1..127 supported (0 marks an unknown name)")
+            c.name_id[col][j] = i
+    return c
+
+
+def parse_actions(cfg: _lib.ParseCfg, text: torch.Tensor, text_len: torch.Tensor, sel: Optional[torch.Tensor] = None,
+                  with_spans: bool = True, action_text_len: int = 0, out: Optional[dict] = None):
+    """_parse_response + _extract_map_valid_actions for every row (ctx_manager.py:148-173,
+    es_manager.py:230-240).  text u8[B,stride] UTF-8 rows, text_len i32[B].
+    -> dict(actions i8[B,K], n_actions u8[B], spans i32[B,4] | None, action_text u8[B,K,Lact] | None,
+            action_len i32[B,K] | None, err u8[B]).  ``out``: a previous result to write into
+    (no allocation: graph-capturable)."""
+    _dev(text, text_len, sel)
+    _dt(text, torch.uint8, "text")
+    _dt(text_len, torch.int32, "text_len")
+    _dt(sel, torch.uint8, "sel")
+    B, stride = text.shape
+    dev = text.device
+    K = int(cfg.K)
+    if out is not None:
+        actions, n_actions, spans, at, al, err = (out[k] for k in ("actions", "n_actions", "spans", "action_text",
+                                                                   "action_len", "err"))
+        if actions.shape != (B, K) or (at is not None and at.shape != (B, K, int(action_text_len))):
+            raise ValueError("out= buffers do not match this batch")
+        err.zero_()
+    else:
+        actions = torch.empty(B, K, dtype=torch.int8, device=dev)
+        n_actions = torch.empty(B, dtype=torch.uint8, device=dev)
+        spans = torch.empty(B, 4, dtype=torch.int32, device=dev) if with_spans else None
+        at = al = None
+        if action_text_len:
+            at = torch.empty(B, K, int(action_text_len), dtype=torch.uint8, device=dev)
+            al = torch.empty(B, K, dtype=torch.int32, device=dev)
+        err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    check(lib().rmi_parse_actions(ctypes.byref(cfg), _ptr(text), _ptr(text_len), B, stride, _ptr(sel), _ptr(actions),
+                                  _ptr(n_actions), _ptr(spans), _ptr(at), _ptr(al), int(action_text_len), _ptr(err),
+                                  _stream()), "rmi_parse_actions")
+    return {"actions": actions, "n_actions": n_actions, "spans": spans, "action_text": at, "action_len": al,
+            "err": err}
+
+
+@dataclass
+class VocabTable:
+    """Device byte table of a byte-level BPE vocabulary: token t decodes to
+    bytes[off[t]:off[t+1]]; skip[t] = special token (dropped by skip_special_tokens=True)."""
+    off: torch.Tensor    # i64[V+1]
+    data: torch.Tensor   # u8[total]
+    skip: torch.Tensor   # u8[V]
+
+    @staticmethod
+    def from_bytes(table, skip, device) -> "VocabTable":
+        lens = np.array([len(b) for b in table], np.int64)
+        off = np.zeros(len(table) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        data = np.frombuffer(b"".join(table) or b"\0", np.uint8).copy()
+        return VocabTable(torch.from_numpy(off).to(device), torch.from_numpy(data).to(device),
+                          torch.from_numpy(np.asarray(skip, np.uint8)).to(device))
+
+    @staticmethod
+    def from_tokenizer(tokenizer, device, skip_special_tokens: bool = True) -> "VocabTable":
+        """Per-id byte strings of a HF fast tokenizer whose decoder is ByteLevel (Qwen2,
+        Llama-3): regular tokens through the byte<->char map; tokens with a char outside the
+        map (added tokens) as their own UTF-8 bytes — the tokenizers ByteLevel decoder."""
+        import json
+        dec = json.loads(tokenizer.backend_tokenizer.to_str()).get("decoder") or {}
+        kinds = {dec.get("type")} | {d.get("type") for d in dec.get("decoders", [])}
+        if "ByteLevel" not in kinds:
+            raise NotImplementedError("device detokenize supports byte-level BPE tokenizers only")
+        if getattr(tokenizer, "clean_up_tokenization_spaces", False):
+            raise NotImplementedError("clean_up_tokenization_spaces=True is not supported on the device")
+        char_to_byte = {c: b for b, c in _bytes_to_unicode().items()}
+        V = len(tokenizer)
+        toks = tokenizer.convert_ids_to_tokens(list(range(V)))
+        special = set(tokenizer.all_special_ids) if skip_special_tokens else set()
+        if skip_special_tokens:
+            for i, at in tokenizer.added_tokens_decoder.items():
+                if at.special:
+                    special.add(int(i))
+        table, skip = [], []
+        for i, t in enumerate(toks):
+            if t is None:
+                table.append(b"")
+            else:
+                try:
+                    table.append(bytes(char_to_byte[ch] for ch in t))
+                except KeyError:
+                    table.append(t.encode("utf-8"))
+            skip.append(1 if i in special else 0)
+        return VocabTable.from_bytes(table, skip, device)
+
+
+def _bytes_to_unicode():
+    bs = list(range(33, 127)) + list(range(161, 173)) + list(range(174, 256))
+    cs = bs[:]
+    n = 0
+    for b in range(256):
+        if b not in bs:
+            bs.append(b)
+            cs.append(256 + n)
+            n += 1
+    return dict(zip(bs, map(chr, cs)))
+
+
+def detokenize(ids: torch.Tensor, vocab: VocabTable, stride: int, n_ids: Optional[torch.Tensor] = None):
+    """tokenizer.batch_decode(ids, skip_special_tokens=True) (ctx_manager.py:334-337) on the
+    device: ids i64[B,R] -> (text u8[B,stride] UTF-8 rows, text_len i32[B], err u8[B])."""
+    _dev(ids, n_ids)
+    _dt(ids, torch.int64, "ids")
+    _dt(n_ids, torch.int32, "n_ids")
+    B, R = ids.shape
+    stride = (int(stride) + 3) // 4 * 4
+    dev = ids.device
+    out = torch.empty(B, stride, dtype=torch.uint8, device=dev)
+    n = torch.empty(B, dtype=torch.int32, device=dev)
+    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    V = vocab.skip.numel()
+    check(lib().rmi_detokenize(_ptr(ids), B, R, _ptr(n_ids), _ptr(vocab.off), _ptr(vocab.data), V, _ptr(vocab.skip),
+                               _ptr(out), stride, _ptr(n), _ptr(err), _stream()), "rmi_detokenize")
+    return out, n, err
 
 
 # ------------------------------------------------------------------- token masks (A11)

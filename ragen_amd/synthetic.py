@@ -102,3 +102,49 @@ def countdown_answers(instances, T: int, seed: int = ACTION_SEED, p_empty: float
                 expr += (" + " if s > 0 else " - ") + str(v)
             out[t][i] = expr
     return out
+
+
+UNKNOWN_NAMES = ("Jump", "Wait", "north", "Stay", "upp")
+THINK_WORDS = ("the", "box", "is", "left", "of", "target", "so", "I", "should", "push", "it", "right", "then",
+               "move", "up", "avoid", "wall", "corner", "player", "at", "row", "column", "2", "3", "—", "→")
+
+
+def responses_for_actions(ids: np.ndarray, n_actions: np.ndarray, lookup, seed: int = 11, think_words=(8, 60),
+                          enable_think: bool = True):
+    """LLM-shaped responses (the generation after the '<think>' tag, ctx_manager.py:338) whose
+    answer lists the given actions: ids i8[B,K] (0 = an unknown name), n_actions u8[B].
+    Names in random case and spacing, " || "-separated.  -> list[str]."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in range(ids.shape[0]):
+        acts = []
+        for k in range(int(n_actions[b])):
+            i = int(ids[b, k])
+            nm = lookup[i] if i else UNKNOWN_NAMES[int(rng.integers(len(UNKNOWN_NAMES)))]
+            c = int(rng.integers(4))
+            nm = nm.lower() if c == 1 else (nm.upper() if c == 2 else nm)
+            acts.append(nm)
+        seps = [" || ", "||", " ||", "|| "]
+        body = ""
+        for k, a in enumerate(acts):
+            body += (seps[int(rng.integers(4))] if k else "") + a
+        nw = int(rng.integers(think_words[0], think_words[1] + 1))
+        think = " ".join(THINK_WORDS[int(j)] for j in rng.integers(len(THINK_WORDS), size=nw))
+        gap = ["", " ", "\n"][int(rng.integers(3))]
+        pad = [" ", ""][int(rng.integers(2))]
+        if enable_think:
+            out.append(f"{think}</think>{gap}<answer>{pad}{body}{pad}</answer>")
+        else:
+            out.append(f"{pad}{body}{pad}</answer>")
+    return out
+
+
+def encode_rows(texts, stride: int = 0):
+    """list[str] -> (u8[B, stride] UTF-8 rows, i32[B] byte lengths); stride rounded up to 4."""
+    bs = [t.encode("utf-8") for t in texts]
+    L = max([len(b) for b in bs] + [1, stride])
+    L = (L + 3) // 4 * 4
+    buf = np.zeros((len(bs), L), np.uint8)
+    for i, b in enumerate(bs):
+        buf[i, :len(b)] = np.frombuffer(b, np.uint8)
+    return buf, np.array([len(b) for b in bs], np.int32)

@@ -1,0 +1,263 @@
+"""GPU parity of the response -> action boundary (rmi_detokenize, rmi_parse_actions) against
+the oracle (oracle/parse.py, itself pinned to vectors recorded from the reference)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import parse as P
+from ragen_amd import ops, synthetic
+from ragen_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "parse_response.json")
+SOKOBAN = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
+
+
+def _golden():
+    d = json.load(open(GOLD))
+    lk = {k: (None if v is None else {int(a): b for a, b in v.items()}) for k, v in d["lookups"].items()}
+    return lk, d["cases"]
+
+
+def _run(texts, device, think, K, sep, lookup, swapped=None, sel=None, Lact=0, prepend=True):
+    buf, lens = synthetic.encode_rows(texts)
+    cfg = ops.parse_config(think, K, sep, lookup, swapped, prepend=prepend)
+    out = ops.parse_actions(cfg, torch.from_numpy(buf).to(device), torch.from_numpy(lens).to(device),
+                            None if sel is None else torch.from_numpy(sel).to(device), True, Lact)
+    torch.cuda.synchronize()
+    return {k: (None if v is None else v.cpu().numpy()) for k, v in out.items()}
+
+
+def _check_rows(texts, out, think, K, sep, lookup, prepend=True):
+    for b, t in enumerate(texts):
+        resp = P.prefixed(t, think) if prepend else t
+        _, acts = P.parse_response(resp, think, K, sep)
+        n = int(out["n_actions"][b])
+        assert n == len(acts), (b, t, acts)
+        ids = P.action_ids(acts, lookup)
+        assert list(out["actions"][b, :n]) == ids, (b, t, acts)
+        assert not out["actions"][b, n:].any()
+        assert tuple(out["spans"][b]) == P.match_spans(resp, think), (b, t)
+        if out["action_text"] is not None:
+            for k in range(n):
+                got = out["action_text"][b, k, :out["action_len"][b, k]].tobytes().decode("utf-8")
+                assert got == acts[k], (b, t, k)
+        assert out["err"][b] == 0
+
+
+@pytest.mark.parametrize("lookup_name", ["sokoban", "frozen_lake", "bandit", "kelvin", "none"])
+def test_parse_matches_reference_vectors(device, lookup_name):
+    lookups, cases = _golden()
+    lk = lookups[lookup_name]
+    groups = {}
+    for c in cases:
+        groups.setdefault((c["enable_think"], c["K"], c["sep"]), []).append(c)
+    for (think, K, sep), cs in groups.items():
+        texts = [c["text"] for c in cs]
+        out = _run(texts, device, think, K, sep, lk, Lact=256 if lk is None else 0)
+        for b, c in enumerate(cs):
+            n = int(out["n_actions"][b])
+            assert n == len(c["actions"]), c["text"]
+            ids = [int(i) for i in out["actions"][b, :n]]
+            if lk is None:
+                got = [out["action_text"][b, k, :out["action_len"][b, k]].tobytes().decode("utf-8") for k in range(n)]
+                assert got == c["mapped"]["none"], c["text"]
+            else:
+                assert [i for i in ids if i] == c["mapped"][lookup_name], c["text"]
+        _check_rows(texts, out, think, K, sep, lk)
+
+
+def test_parse_bandit_per_env_lookup(device):
+    """Bandit's action_lookup is per env (bandit/env.py:25-39): sel picks the id column."""
+    lo, hi = {1: "Phoenix", 2: "Dragon"}, {1: "Dragon", 2: "Phoenix"}
+    texts = ["x</think><answer>Dragon</answer>", "x</think><answer> phoenix </answer>",
+             "x</think><answer>DRAGON</answer>", "x</think><answer>tiger</answer>"] * 4
+    sel = np.array([0, 0, 0, 0, 1, 1, 1, 1] * 2, np.uint8)
+    out = _run(texts, device, True, 1, "||", lo, hi, sel=sel)
+    for b, t in enumerate(texts):
+        _, acts = P.parse_response(P.prefixed(t, True), True, 1)
+        assert list(out["actions"][b, :out["n_actions"][b]]) == P.action_ids(acts, hi if sel[b] else lo)
+
+
+def test_parse_full_batch_vs_oracle(device):
+    """8192 SK-shaped responses (synthetic actions of the bench), with no-think prefix too."""
+    ids, n = synthetic.rollout_actions(8192, 1, 5, 1, 4)
+    for think in (True, False):
+        texts = synthetic.responses_for_actions(ids[0], n[0], SOKOBAN, enable_think=think)
+        out = _run(texts, device, think, 5, "||", SOKOBAN)
+        _check_rows(texts, out, think, 5, "||", SOKOBAN)
+        assert np.array_equal(out["n_actions"], n[0])
+        assert np.array_equal(out["actions"], ids[0])
+
+
+def test_parse_fuzz_and_edges(device):
+    rng = random.Random(3)
+    frags = ["<think>", "</think>", "<answer>", "</answer>", "<|im_end|>", "<|im_start|>", "|", "||", " ", "\n",
+             "　", " ", "\xa0", "K", "Up", "down", "LEFT", "x", "é", "\U0001f600", "<", ">"]
+    texts = ["".join(rng.choice(frags) for _ in range(rng.randint(0, 40))) for _ in range(3000)]
+    texts += ["", "</think><answer>" + "Up || " * 2000 + "</answer>", "a" * 9000]
+    for think in (True, False):
+        for prepend in (True, False):
+            out = _run(texts, device, think, 5, "||", SOKOBAN, prepend=prepend)
+            _check_rows(texts, out, think, 5, "||", SOKOBAN, prepend=prepend)
+
+
+def test_parse_bad_lengths_and_overlong_actions(device):
+    buf, lens = synthetic.encode_rows(["x</think><answer>Up</answer>", "x</think><answer>abcdefghij</answer>"])
+    lens_t = torch.from_numpy(np.array([-1, lens[1]], np.int32)).to(device)
+    cfg = ops.parse_config(True, 5, "||", None)
+    out = ops.parse_actions(cfg, torch.from_numpy(buf).to(device), lens_t, None, True, 4)
+    torch.cuda.synchronize()
+    err = out["err"].cpu().numpy()
+    assert err[0] & _lib.ERR_STATE and out["n_actions"][0].item() == 0
+    assert err[1] & _lib.ERR_UNSUP and out["action_len"][1, 0].item() == 4
+    with pytest.raises(ValueError):
+        ops.parse_actions(ops.parse_config(True, 0, "||", None), torch.from_numpy(buf).to(device), lens_t)
+
+
+# ------------------------------------------------------------------ detokenize
+def _random_table(V, seed):
+    rng = np.random.default_rng(seed)
+    table = []
+    for i in range(V):
+        k = int(rng.integers(0, 9))
+        if i % 7 == 0:  # ASCII-only tokens
+            table.append(bytes(rng.integers(32, 127, size=k).astype(np.uint8)))
+        else:
+            table.append(bytes(rng.integers(0, 256, size=k).astype(np.uint8)))
+    skip = (rng.random(V) < 0.05).astype(np.uint8)
+    return table, skip
+
+
+def test_detokenize_vs_oracle(device):
+    V = 5000
+    table, skip = _random_table(V, 1)
+    vt = ops.VocabTable.from_bytes(table, skip, device)
+    rng = np.random.default_rng(2)
+    B, R = 2048, 96
+    ids = rng.integers(0, V, size=(B, R)).astype(np.int64)
+    n_ids = rng.integers(0, R + 1, size=B).astype(np.int32)
+    ids[5, 3] = V + 3   # out of range
+    ids[6, 0] = -2
+    n_ids[5] = max(n_ids[5], 4)
+    n_ids[6] = max(n_ids[6], 1)
+    out, n, err = ops.detokenize(torch.from_numpy(ids).to(device), vt, 4096, torch.from_numpy(n_ids).to(device))
+    torch.cuda.synchronize()
+    out, n, err = out.cpu().numpy(), n.cpu().numpy(), err.cpu().numpy()
+    for b in range(B):
+        row = [int(i) for i in ids[b, :n_ids[b]]]
+        if b in (5, 6):
+            assert err[b] & _lib.ERR_INDEX
+            row = [i for i in row if 0 <= i < V]
+        else:
+            assert err[b] == 0
+        want = P.detokenize(row, table, skip.astype(bool)).encode("utf-8")
+        assert out[b, :n[b]].tobytes() == want, b
+
+
+def test_detokenize_ascii_and_overflow(device):
+    table = [b"ab", b"<think>", b" Up", b" ||", b"\xe2\x80", b"\xa8"] + [b"x" * 8]
+    skip = np.zeros(len(table), np.uint8)
+    vt = ops.VocabTable.from_bytes(table, skip, device)
+    ids = np.array([[1, 2, 3, 2, 0, 4, 5, 6], [6] * 8], np.int64)
+    out, n, err = ops.detokenize(torch.from_numpy(ids).to(device), vt, 32)
+    torch.cuda.synchronize()
+    assert out[0, :n[0]].cpu().numpy().tobytes() == b"<think> Up || Upab\xe2\x80\xa8" + b"x" * 8
+    assert n[1].item() == 32 and err[1].item() & _lib.ERR_UNSUP and err[0].item() == 0
+
+
+def test_detokenize_parse_step_pipeline(device):
+    """token ids -> text -> action ids -> Sokoban turn, equal to the host-side path."""
+    from ragen_amd.env import SokobanBatch
+    from ragen_amd.env.configs import SokobanEnvConfig
+    import oracle
+    B, K = 1024, 5
+    ids, n = synthetic.rollout_actions(B, 1, K, 1, 4)
+    texts = synthetic.responses_for_actions(ids[0], n[0], SOKOBAN)
+    # a byte vocabulary: one token per byte + a few words, greedy tokenisation
+    words = [b"</think>", b"<answer>", b"</answer>", b" || ", b"Up", b"Down", b"Left", b"Right"]
+    table = [bytes([i]) for i in range(256)] + words + [b"<|endoftext|>"]
+    skip = np.zeros(len(table), np.uint8)
+    skip[-1] = 1
+    R = 0
+    rows = []
+    for t in texts:
+        bts, row, i = t.encode("utf-8"), [], 0
+        while i < len(bts):
+            for w, wb in enumerate(words):
+                if bts.startswith(wb, i):
+                    row.append(256 + w)
+                    i += len(wb)
+                    break
+            else:
+                row.append(bts[i])
+                i += 1
+        rows.append(row)
+        R = max(R, len(row))
+    tok = np.full((B, R + 3), len(table) - 1, np.int64)  # right padded with the (special) pad id
+    for b, r in enumerate(rows):
+        tok[b, :len(r)] = r
+    vt = ops.VocabTable.from_bytes(table, skip, device)
+    text, tlen, err = ops.detokenize(torch.from_numpy(tok).to(device), vt, 2048)
+    parsed = ops.parse_actions(ops.parse_config(True, K, "||", SOKOBAN), text, tlen)
+    env = SokobanBatch(SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100), B, 1, K, device)
+    env.reset(synthetic.env_seeds(B))
+    fixed, state, player = env.room_fixed.cpu().numpy(), env.room_state.cpu().numpy(), env.player.cpu().numpy()
+    env.step_turn(0, parsed["actions"], parsed["n_actions"], None, 10, -0.1)
+    nes, bot = np.zeros(B, np.int32), np.zeros(B, np.int32)
+    oep = oracle.Episode(B, 1)
+    oracle.sokoban_turn(6, 6, 1, 100, fixed, state, player, nes, bot, oep, 0, ids[0], n[0])
+    torch.cuda.synchronize()
+    assert not err.any()
+    assert np.array_equal(env.room_state.cpu().numpy(), state)
+    assert np.array_equal(env.ep.turn_reward.cpu().numpy(), oep.turn_reward)
+    assert np.array_equal(env.ep.penalty.cpu().numpy(), oep.penalty)
+
+
+@pytest.mark.parametrize("name", ["sokoban_es", "frozenlake_es", "bandit_es", "countdown_es"])
+def test_step_text_equals_dict_step(device, name, monkeypatch):
+    """EnvStateManager.step_text (device parse + turn, nothing on the host) == step() fed with
+    the host-parsed dicts, on the reference's recorded action traces."""
+    from test_gpu_facade import _config, _hashseed0_reseed
+    from trace_util import load, strings
+    from ragen_amd.env import SokobanBatch
+    from ragen_amd.llm_agent import EnvStateManager
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    d, S = load(name), strings()[name]
+    es_host = EnvStateManager(_config(name), mode="train", device=device)
+    es_dev = EnvStateManager(_config(name), mode="train", device=device)
+    es_host.reset(seed=int(d["seed"]))
+    es_dev.reset(seed=int(d["seed"]))
+    B, T = int(d["B"]), int(d["T"])
+    K = es_host.K
+    active = list(range(B))
+    for t in range(T):
+        texts = []
+        for i in range(B):
+            if name == "countdown_es":
+                a = S["answers"][t][i]
+                acts = [] if a is None else [a]
+            else:
+                acts = [S["vocab"][c] for c in d["codes"][t, i] if c >= 0]
+            texts.append("plan</think> <answer>" + " || ".join(acts) + "</answer>")
+        inputs = []
+        for i in active:
+            llm_response, acts = P.parse_response(P.prefixed(texts[i], True), True, K)
+            inputs.append({"env_id": i, "llm_response": llm_response, "llm_raw_response": texts[i], "actions": acts})
+        has = np.zeros(B, np.uint8)
+        has[active] = 1
+        buf, lens = synthetic.encode_rows(texts)
+        es_dev.step_text(torch.from_numpy(buf).to(device), torch.from_numpy(lens).to(device),
+                         torch.from_numpy(has).to(device))
+        active = [o["env_id"] for o in es_host.step(inputs)]
+        torch.cuda.synchronize()
+        for th, td in zip(es_host.tags, es_dev.tags):
+            for f in ("num_actions", "flags", "n_turns", "penalty", "turn_reward", "turn_info", "turn_exec"):
+                assert torch.equal(getattr(th.batch.ep, f), getattr(td.batch.ep, f)), (t, f)
+        if not active:
+            break
