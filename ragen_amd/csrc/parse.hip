@@ -6,13 +6,15 @@
 //                      "<think>"/"<answer>"-prefixed response (:338-339), then
 //                      EnvStateManager._extract_map_valid_actions (es_manager.py:230-240)
 //
-// One wave per response.  The row is staged in LDS with coalesced dword loads; every scan
-// over it (tag search, special-token test, separator search) is wave-parallel: 64 candidate
-// positions per step, the first hit found by ballot.  What the reference does with Python
-// string methods between the scans (regex backtracking over </think> candidates, \s* and
-// str.strip over Unicode whitespace, the special-token replace cascade) runs wave-uniformly
-// on the few bytes involved.  Only the rare row whose answer contains a special token takes
-// the serial replace cascade (lane 0).
+// One wave per response, the row staged in LDS.  The parse is driven by EVENTS instead of
+// byte scans: one SWAR pass (a dword per lane) compacts the positions of every '<' into an
+// LDS list; all six tags begin with '<', so the lanes then classify 64 events per step with
+// one 16-byte compare each, and the regex (its backtracking over </think> candidates
+// included) runs as ballots over the classified list.  The separator is handled the same
+// way (positions of its first byte -> full compare -> greedy left-to-right selection), and
+// the pieces between separators are stripped and name-matched one piece per lane.  Only the
+// rare answer that contains a special token takes the replace cascade (wave-parallel
+// stream compaction, one pass per token present).
 //
 // Exactness argument for working on UTF-8 bytes instead of Python str: every tag, the
 // separator and the action names are ASCII; UTF-8 is self-synchronising, so an ASCII byte is
@@ -26,9 +28,33 @@
 namespace rmi {
 namespace {
 
-constexpr int kPre = 8;             // room for the implicit prefix tag in front of the text
-constexpr int kPad = 16;            // zero bytes after the text
-constexpr int kMaxStride = 16384;
+// Diagnostic build only (tools/prof_parse_stamps.py compiles this file with RMI_PARSE_STAMPS):
+// per-wave s_memtime at phase boundaries, kept in SGPRs and written once at the end.
+#ifdef RMI_PARSE_STAMPS
+__device__ unsigned long long* g_parse_stamps;
+#define PSTAMP_DECL unsigned long long pst_[10] = {0}
+#define PSTAMP(i) (pst_[i] = __builtin_amdgcn_s_memtime())
+#define PSTAMP_FLUSH()                                                                 \
+  do {                                                                                 \
+    if (threadIdx.x == 0)                                                              \
+      for (int s_ = 0; s_ < 10; ++s_) g_parse_stamps[blockIdx.x * 10 + s_] = pst_[s_]; \
+  } while (0)
+#else
+#define PSTAMP_DECL \
+  do {              \
+  } while (0)
+#define PSTAMP(i) \
+  do {            \
+  } while (0)
+#define PSTAMP_FLUSH() \
+  do {                 \
+  } while (0)
+#endif
+
+constexpr int kPre = 8;                 // room for the implicit prefix tag in front of the text
+constexpr int kTail = 24;               // zero bytes after a row (16-byte compares read 20 past)
+constexpr int kMaxStride = 16384;       // detokenize rows (2 LDS rows per wave)
+constexpr int kMaxParseStride = 8192;   // parse rows (rows + event lists: < 64 KB of LDS)
 
 // A string of <= 16 bytes packed little-endian into two words (compile-time tags, the
 // runtime separator and names alike), so that no byte table needs dynamic indexing.
@@ -48,14 +74,11 @@ constexpr Tag make_tag(const char* s) {
   }
   return t;
 }
+__host__ __device__ constexpr uint64_t low_mask(int nbytes) {
+  return nbytes <= 0 ? 0ull : (nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1ull));
+}
 __device__ __forceinline__ uint8_t tag_byte(const Tag& t, int k) {
   return (uint8_t)(k < 8 ? t.lo >> (8 * k) : t.hi >> (8 * (k - 8)));
-}
-__device__ __forceinline__ bool match_at(const uint8_t* V, int p, int lim, const Tag& t) {
-  if (p < 0 || p + t.n > lim) return false;
-  bool ok = true;
-  for (int k = 0; k < t.n; ++k) ok = ok && V[p + k] == tag_byte(t, k);
-  return ok;
 }
 
 constexpr Tag kThinkOpen = make_tag("<think>");
@@ -64,28 +87,41 @@ constexpr Tag kAnsOpen = make_tag("<answer>");
 constexpr Tag kAnsClose = make_tag("</answer>");
 constexpr Tag kImStart = make_tag("<|im_start|>");
 constexpr Tag kImEnd = make_tag("<|im_end|>");
+// event ids (the special-token order of ctx_manager.py:94, 1-based; 0 = no tag)
+enum : int { E_NONE = 0, E_THINK_O = 1, E_THINK_C = 2, E_ANS_O = 3, E_ANS_C = 4, E_IM_S = 5, E_IM_E = 6 };
 
-// smallest p >= from with V[p, p + n) == tag inside [.., lim), else -1 (wave-uniform)
-__device__ int find_tag(const uint8_t* V, int from, int lim, const Tag& t, int lane) {
-  for (int base = from; base + t.n <= lim; base += 64) {
-    const int p = base + lane;
-    bool hit = p + t.n <= lim && V[p] == (uint8_t)t.lo;
-    if (hit)
-      for (int k = 1; k < t.n; ++k) hit = hit && V[p + k] == tag_byte(t, k);
-    const uint64_t m = __ballot(hit);
-    if (m) return base + __builtin_ctzll(m);
-  }
-  return -1;
+// bytes [s, s + 16) of an LDS row (dword-aligned base, >= 20 readable bytes past s)
+__device__ __forceinline__ void load16(const uint8_t* B, int s, uint64_t& lo, uint64_t& hi) {
+  const uint32_t* B4 = reinterpret_cast<const uint32_t*>(B);
+  const int q = s >> 2, r = s & 3;
+  uint32_t w[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) w[k] = B4[q + k];
+  const uint64_t a = (uint64_t)w[0] | ((uint64_t)w[1] << 32), c = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+  const uint64_t e = w[4];
+  lo = r == 0 ? a : (a >> (8 * r)) | (c << (64 - 8 * r));
+  hi = r == 0 ? c : (c >> (8 * r)) | (e << (64 - 8 * r));
+}
+__device__ __forceinline__ bool tag_eq(uint64_t lo, uint64_t hi, const Tag& t) {
+  return ((lo & low_mask(t.n)) == t.lo) & ((hi & low_mask(t.n - 8)) == t.hi);
+}
+// which of the six tags starts at B[x] (a '<'); tags never run into a row's zero tail
+__device__ __forceinline__ int classify_tag(const uint8_t* B, int x) {
+  uint64_t lo, hi;
+  load16(B, x, lo, hi);
+  return tag_eq(lo, hi, kThinkOpen)    ? E_THINK_O
+         : tag_eq(lo, hi, kThinkClose) ? E_THINK_C
+         : tag_eq(lo, hi, kAnsOpen)    ? E_ANS_O
+         : tag_eq(lo, hi, kAnsClose)   ? E_ANS_C
+         : tag_eq(lo, hi, kImStart)    ? E_IM_S
+         : tag_eq(lo, hi, kImEnd)      ? E_IM_E
+                                       : E_NONE;
 }
 
-// Length of the Unicode whitespace character (str.isspace / re \s) starting at p, or 0.
-__device__ __forceinline__ int ws_fwd(const uint8_t* V, int p, int lim) {
-  if (p >= lim) return 0;
-  const uint32_t c = V[p];
+// Length of the Unicode whitespace character (str.isspace / re \s) whose bytes are c, c1, c2.
+__device__ __forceinline__ int ws_len3(uint32_t c, uint32_t c1, uint32_t c2) {
   if (c < 0x80) return ((c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x20)) ? 1 : 0;
-  if (c == 0xC2) return (p + 1 < lim && (V[p + 1] == 0x85 || V[p + 1] == 0xA0)) ? 2 : 0;
-  if (p + 2 >= lim) return 0;
-  const uint32_t c1 = V[p + 1], c2 = V[p + 2];
+  if (c == 0xC2) return (c1 == 0x85 || c1 == 0xA0) ? 2 : 0;
   if (c == 0xE1) return (c1 == 0x9A && c2 == 0x80) ? 3 : 0;
   if (c == 0xE2) {
     if (c1 == 0x80) return ((c2 >= 0x80 && c2 <= 0x8A) || c2 == 0xA8 || c2 == 0xA9 || c2 == 0xAF) ? 3 : 0;
@@ -94,45 +130,179 @@ __device__ __forceinline__ int ws_fwd(const uint8_t* V, int p, int lim) {
   if (c == 0xE3) return (c1 == 0x80 && c2 == 0x80) ? 3 : 0;
   return 0;
 }
-// Length of the whitespace character ending at e (within [s, e)), or 0.
+// ... starting at p inside [.., lim), or 0
+__device__ __forceinline__ int ws_fwd(const uint8_t* V, int p, int lim) {
+  if (p >= lim) return 0;
+  const uint32_t c = V[p];
+  if (c < 0x80) return ws_len3(c, 0, 0);
+  const uint32_t c1 = p + 1 < lim ? V[p + 1] : 0u, c2 = p + 2 < lim ? V[p + 2] : 0u;
+  return ws_len3(c, c1, c2);
+}
+// ... ending at e (within [s, e)), or 0
 __device__ __forceinline__ int ws_back(const uint8_t* V, int s, int e) {
   if (e <= s) return 0;
   const uint32_t c = V[e - 1];
-  if (c < 0x80) return ((c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x20)) ? 1 : 0;
+  if (c < 0x80) return ws_len3(c, 0, 0);
   if (e - 2 >= s && V[e - 2] == 0xC2 && (c == 0x85 || c == 0xA0)) return 2;
   if (e - 3 < s) return 0;
-  return ws_fwd(V, e - 3, e) == 3 ? 3 : 0;
+  return ws_len3(V[e - 3], V[e - 2], c) == 3 ? 3 : 0;
 }
 __device__ __forceinline__ void strip(const uint8_t* V, int& a, int& z) {
   for (int l; (l = ws_fwd(V, a, z)) != 0;) a += l;
   for (int l; (l = ws_back(V, a, z)) != 0;) z -= l;
 }
 
-// any of the six special tokens (ctx_manager.py:94) inside [a, z)  (wave-uniform)
-__device__ bool has_special(const uint8_t* V, int a, int z, int lane) {
-  for (int base = a; base < z; base += 64) {
-    const int p = base + lane;
-    bool hit = false;
-    if (p < z && V[p] == '<')
-      hit = match_at(V, p, z, kThinkOpen) || match_at(V, p, z, kThinkClose) || match_at(V, p, z, kAnsOpen) ||
-            match_at(V, p, z, kAnsClose) || match_at(V, p, z, kImStart) || match_at(V, p, z, kImEnd);
-    if (__ballot(hit)) return true;
+// Positions x in [from, to) with B[x] == ch, ascending, into list; -> count (wave-uniform).
+// One dword per lane per 256 bytes, SWAR byte test, wave prefix sum for the slots.
+__device__ int collect(const uint8_t* B, int from, int to, uint32_t ch, uint16_t* list, int lane) {
+  int cnt = 0;
+  const uint32_t rep = ch * 0x01010101u;
+  for (int c = from & ~3; c < to; c += 256) {
+    const int i0 = c + 4 * lane;
+    uint32_t m4 = 0;
+    if (i0 < to) {
+      const uint32_t x = *reinterpret_cast<const uint32_t*>(B + i0) ^ rep;  // zero byte where B == ch
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = i0 + j;
+        const bool hit = ((x >> (8 * j)) & 0xFFu) == 0;
+        if (hit && p >= from && p < to) m4 |= 1u << j;
+      }
+    }
+    const int k = __builtin_popcount(m4);
+    const int incl = wave_inclusive_scan(k);
+    int o = cnt + incl - k;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (m4 & (1u << j)) list[o++] = (uint16_t)(i0 + j);
+    cnt += __builtin_amdgcn_readlane(incl, 63);
   }
-  return false;
+  return cnt;
 }
 
-// s = s.replace(tok, "").strip() in place on w[a, z)  (one lane)
-__device__ void replace_strip(uint8_t* w, int& a, int& z, const Tag& t) {
-  int o = a;
-  for (int i = a; i < z;) {
-    if (match_at(w, i, z, t)) {
-      i += t.n;
-    } else {
-      w[o++] = w[i++];
+// The classified '<' events: positions EL[i], tag ids EI[i] (i < n, position order); the
+// first 64 also in registers (lane i holds event i), so typical rows never re-read LDS.
+struct EvList {
+  const uint16_t* EL;
+  const uint8_t* EI;
+  int n, p0, id0;
+};
+// First event with id == want (want < 0: any tag) at position in [from, lim) -> its
+// position, else -1 (wave-uniform).
+__device__ int next_event(const EvList& E, int want, int from, int lim, int lane) {
+  for (int c = 0; c < E.n; c += 64) {
+    const int i = c + lane;
+    bool hit = false;
+    int p = 0;
+    if (i < E.n) {
+      p = c == 0 ? E.p0 : (int)E.EL[i];
+      const int id = c == 0 ? E.id0 : (int)E.EI[i];
+      hit = p >= from && p < lim && (want < 0 ? id != E_NONE : id == want);
+    }
+    const uint64_t m = __ballot(hit);
+    if (m) return __builtin_amdgcn_readlane(p, __builtin_ctzll(m));
+  }
+  return -1;
+}
+
+// Name ids of one piece against every name (lowercased ASCII, <= 16 bytes): 0 = no name.
+struct Names {
+  int n;
+  uint64_t lo[RMI_PARSE_MAX_NAMES], hi[RMI_PARSE_MAX_NAMES];
+  int len[RMI_PARSE_MAX_NAMES], id[RMI_PARSE_MAX_NAMES];
+};
+__device__ __forceinline__ uint64_t swar_lower(uint64_t x) {  // ASCII bytes: 'A'..'Z' += 0x20
+  constexpr uint64_t k80 = 0x8080808080808080ull;
+  const uint64_t ge_a = (x + 0x3F3F3F3F3F3F3F3Full) & k80;  // byte >= 'A'
+  const uint64_t gt_z = (x + 0x2525252525252525ull) & k80;  // byte > 'Z'
+  return x + ((ge_a & ~gt_z) >> 2);
+}
+__device__ int piece_id(const uint8_t* B, int s, int e, const Names& nm) {
+  const int L = e - s;
+  if (L <= 16) {
+    uint64_t lo, hi;
+    load16(B, s, lo, hi);
+    lo &= low_mask(L);
+    hi &= low_mask(L - 8);
+    if (((lo | hi) & 0x8080808080808080ull) == 0) {
+      lo = swar_lower(lo);  // zero bytes past L stay zero
+      hi = swar_lower(hi);
+      int id = 0;
+#pragma unroll
+      for (int j = 0; j < RMI_PARSE_MAX_NAMES; ++j)  // unrolled: the name table stays in registers
+        if (j < nm.n && L == nm.len[j] && lo == nm.lo[j] && hi == nm.hi[j]) id = nm.id[j];
+      return id;
     }
   }
-  z = o;
-  strip(w, a, z);
+  // non-ASCII (only U+212A KELVIN SIGN lowercases to ASCII) or long: per character
+  int id = 0;
+#pragma unroll
+  for (int j = 0; j < RMI_PARSE_MAX_NAMES; ++j) {
+    bool ok = j < nm.n && id == 0;
+    int q = 0;
+    for (int i = s; ok && i < e;) {
+      uint32_t c = B[i];
+      if (c < 0x80) {
+        c += (c >= 'A' && c <= 'Z') ? 32u : 0u;
+        ++i;
+      } else if (c == 0xE2 && i + 2 < e && B[i + 1] == 0x84 && B[i + 2] == 0xAA) {
+        c = 'k';
+        i += 3;
+      } else {
+        ok = false;
+        break;
+      }
+      const uint64_t w = q < 8 ? nm.lo[j] >> (8 * q) : nm.hi[j] >> (8 * (q - 8));
+      ok = q < nm.len[j] && (uint32_t)(w & 0xFFu) == c;
+      ++q;
+    }
+    if (ok && q == nm.len[j]) id = nm.id[j];
+  }
+  return id;
+}
+
+// s = s.replace(tok, "").strip() on src[a, z) -> the returned buffer's [a, z'): wave-parallel.
+// The six tokens cannot overlap themselves ('<' only first, '>' only last), so Python's
+// left-to-right non-overlapping replace removes exactly every occurrence present in src.
+// A pass whose token is absent copies nothing.
+__device__ uint8_t* replace_strip_wave(uint8_t* src, uint8_t* dst, uint16_t* lst, uint8_t* cov, int a, int& z,
+                                       const Tag& t, int lane) {
+  const int n = collect(src, a, z, '<', lst, lane);
+  __syncthreads();
+  for (int x = a + lane; x < z; x += 64) cov[x] = 0;
+  __syncthreads();
+  bool any = false;
+  for (int c = 0; c < n; c += 64) {
+    const int i = c + lane;
+    bool occ = false;
+    int x = 0;
+    if (i < n) {
+      x = lst[i];
+      uint64_t lo, hi;
+      load16(src, x, lo, hi);
+      occ = x + t.n <= z && tag_eq(lo, hi, t);
+    }
+    if (occ)
+      for (int d = 0; d < t.n; ++d) cov[x + d] = 1;
+    any |= __ballot(occ) != 0;
+  }
+  uint8_t* out = src;
+  if (any) {
+    __syncthreads();
+    int o = a;
+    for (int c = a; c < z; c += 64) {
+      const int x = c + lane;
+      const bool keep = x < z && !cov[x];
+      const int incl = wave_inclusive_scan(keep ? 1 : 0);
+      if (keep) dst[o + incl - 1] = src[x];
+      o += __builtin_amdgcn_readlane(incl, 63);
+    }
+    z = o;
+    out = dst;
+    if (lane < kTail) dst[z + lane] = 0;
+    __syncthreads();
+  }
+  return out;
 }
 
 struct ParseArgs {
@@ -151,59 +321,99 @@ struct ParseArgs {
   uint8_t* err;
 };
 
-// dword-staged row copy global -> LDS (row start 4-B aligned, stride % 4 == 0)
-__device__ __forceinline__ void stage_row(uint8_t* dst, const uint8_t* src, int len, int lane) {
-  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-  uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
-  const int nw = (len + 3) >> 2;
-  for (int i = lane; i < nw; i += 64) d4[i] = s4[i];
+__host__ __device__ constexpr int row_bytes(int stride) { return (4 + kPre + stride + kTail + 7) & ~7; }
+__host__ __device__ constexpr int list_cap(int stride) { return (kPre + stride + 8) & ~7; }
+// T row | W row | EL u16[cap] | ES u16[cap] | EI u8[cap]
+__host__ __device__ constexpr size_t parse_lds(int stride) {
+  return 2 * (size_t)row_bytes(stride) + 5 * (size_t)list_cap(stride);
 }
 
 __global__ __launch_bounds__(64) void parse_kernel(ParseArgs a) {
-  extern __shared__ uint32_t lds_words[];
-  uint8_t* t = reinterpret_cast<uint8_t*>(lds_words);  // [kPre + stride + kPad]
-  uint8_t* w = t + kPre + a.stride + kPad;              // replace-cascade work row [stride + kPre + kPad]
-  __shared__ int sh_a, sh_z;
+  extern __shared__ uint64_t lds_q[];
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_q);
+  const int cap = list_cap(a.stride);
+  uint8_t* T = lds + 4;                                                   // the prefixed row
+  uint8_t* Wb = lds + row_bytes(a.stride) + 4;                            // replace-cascade row
+  uint16_t* EL = reinterpret_cast<uint16_t*>(lds + 2 * row_bytes(a.stride));  // '<' positions
+  uint16_t* ES = EL + cap;                                                // separator candidates
+  uint8_t* EI = reinterpret_cast<uint8_t*>(ES + cap);                     // event ids
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
   const rmi_parse_cfg_t& cfg = a.cfg;
   const int K = cfg.K;
+  PSTAMP_DECL;
+  PSTAMP(0);
+  // ---- 0. stage.  The first 256 bytes are loaded together with the length (one round trip
+  //         for typical responses); the rest, if any, after it.
+  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(a.text + b * a.stride);
+  uint32_t* d4 = reinterpret_cast<uint32_t*>(T + kPre);
+  const int rw = a.stride >> 2;
+  const uint32_t first = lane < rw ? s4[lane] : 0u;
   int len = a.text_len[b];
   uint8_t err = 0;
   if (len < 0 || len > a.stride) {
     err |= RMI_ERR_STATE;
     len = 0;
   }
-  stage_row(t + kPre, a.text + b * a.stride, len, lane);
-  __syncthreads();
-  if (lane < kPad) t[kPre + len + lane] = 0;  // over-read bytes of the last dword -> 0
+  // the name table (kernel arguments) and the lookup column: loaded up front, their latency
+  // hides under the row's
+  Names nm;
+  nm.n = cfg.n_names;
+  const int col = (a.sel && a.sel[b]) ? 1 : 0;
+#pragma unroll
+  for (int j = 0; j < RMI_PARSE_MAX_NAMES; ++j) {
+    nm.lo[j] = cfg.name_lo[j];
+    nm.hi[j] = cfg.name_hi[j];
+    nm.len[j] = cfg.name_len[j];
+    nm.id[j] = cfg.name_id[col][j];
+  }
+  const int nw = (len + 3) >> 2;
+  if (lane < nw) d4[lane] = first;
+  for (int i = 64 + lane; i < nw; i += 64) d4[i] = s4[i];
   const Tag pre = cfg.enable_think ? kThinkOpen : kAnsOpen;
   const int plen = cfg.prepend ? pre.n : 0;
-  if (lane < plen) t[kPre - plen + lane] = tag_byte(pre, lane);
+  const int base = kPre - plen, n_end = kPre + len;  // the prefixed response is T[base, n_end)
   __syncthreads();
-  const uint8_t* V = t + kPre - plen;  // the prefixed response (get_env_inputs :338-339)
-  const int n = plen + len;
+  if (lane < kTail) T[n_end + lane] = 0;
+  if (lane < 4 + kPre) T[lane - 4] = (lane - 4 >= base) ? tag_byte(pre, lane - 4 - base) : 0;
+  __syncthreads();
+  PSTAMP(1);
 
-  // ---- 1. re.search(pattern, response, re.DOTALL)  (ctx_manager.py:149-150)
+  // ---- 1. '<' events, classified (64 per step)
+  EvList E{EL, EI, collect(T, base, n_end, '<', EL, lane), 0, E_NONE};
+  __syncthreads();
+  for (int i = lane; i < E.n; i += 64) {
+    const int p = EL[i], id = classify_tag(T, p);
+    if (i < 64) {
+      E.p0 = p;
+      E.id0 = id;
+    } else {
+      EI[i] = (uint8_t)id;
+    }
+  }
+  __syncthreads();
+  PSTAMP(2);
+
+  // ---- 2. re.search(pattern, response, re.DOTALL)  (ctx_manager.py:149-150)
   int ts = -1, te = -1, as = -1, ae = -1;
   if (cfg.enable_think) {
     // <think>(.*?)</think>\s*<answer>(.*?)</answer>: the leftmost <think> decides (a later
     // start only sees a subset of the </think> candidates); group 1 grows over the
     // </think> candidates in order until \s*<answer> follows; group 2 ends at the first
     // </answer> after it (if there is none, no later candidate can have one either)
-    const int i = find_tag(V, 0, n, kThinkOpen, lane);
+    const int i = next_event(E, E_THINK_O, base, n_end, lane);
     if (i >= 0) {
       int j = i + kThinkOpen.n, k = -1;
       for (;;) {
-        j = find_tag(V, j, n, kThinkClose, lane);
+        j = next_event(E, E_THINK_C, j, n_end, lane);
         if (j < 0) break;
         k = j + kThinkClose.n;
-        for (int l; (l = ws_fwd(V, k, n)) != 0;) k += l;  // \s* is greedy and '<' is no space
-        if (match_at(V, k, n, kAnsOpen)) break;
+        for (int l; (l = ws_fwd(T, k, n_end)) != 0;) k += l;  // \s* is greedy and '<' is no space
+        if (T[k] == '<' && next_event(E, E_ANS_O, k, k + 1, lane) == k) break;
         ++j;
       }
       if (j >= 0) {
-        const int e = find_tag(V, k + kAnsOpen.n, n, kAnsClose, lane);
+        const int e = next_event(E, E_ANS_C, k + kAnsOpen.n, n_end, lane);
         if (e >= 0) {
           ts = i + kThinkOpen.n;
           te = j;
@@ -213,114 +423,122 @@ __global__ __launch_bounds__(64) void parse_kernel(ParseArgs a) {
       }
     }
   } else {
-    const int i = find_tag(V, 0, n, kAnsOpen, lane);
+    const int i = next_event(E, E_ANS_O, base, n_end, lane);
     if (i >= 0) {
-      const int e = find_tag(V, i + kAnsOpen.n, n, kAnsClose, lane);
+      const int e = next_event(E, E_ANS_C, i + kAnsOpen.n, n_end, lane);
       if (e >= 0) {
         as = i + kAnsOpen.n;
         ae = e;
       }
     }
   }
+  PSTAMP(3);
 
-  // ---- 2. special-token replace cascade + strip of the action content (:161-163)
-  const uint8_t* C = V;
+  // ---- 3. special-token replace cascade + strip of the action content (:161-163).  A token
+  //         starting inside [as, ae) ends inside it (every token ends in '>', and the only '>'
+  //         of </answer> is its last byte), so the event test over [as, ae) is exact.
+  uint8_t* C = T;
   int ca = 0, cz = 0;
   if (as >= 0) {
     ca = as;
     cz = ae;
-    if (!has_special(V, ca, cz, lane)) {
-      strip(V, ca, cz);  // every replace is a no-op, and strip() six times is strip() once
+    if (next_event(E, -1, ca, cz, lane) < 0) {
+      strip(T, ca, cz);  // every replace is a no-op, and strip() six times is strip() once
     } else {
-      for (int i = ca + lane; i < cz; i += 64) w[i] = V[i];
-      __syncthreads();
-      if (lane == 0) {
-        int x = ca, y = cz;
-        replace_strip(w, x, y, kThinkOpen);
-        replace_strip(w, x, y, kThinkClose);
-        replace_strip(w, x, y, kAnsOpen);
-        replace_strip(w, x, y, kAnsClose);
-        replace_strip(w, x, y, kImStart);
-        replace_strip(w, x, y, kImEnd);
-        sh_a = x;
-        sh_z = y;
+      for (int q = 0; q < 6; ++q) {  // ctx_manager.py:94 order
+        const Tag tok = q == 0 ? kThinkOpen
+                        : q == 1 ? kThinkClose
+                        : q == 2 ? kAnsOpen
+                        : q == 3 ? kAnsClose
+                        : q == 4 ? kImStart
+                                 : kImEnd;
+        uint8_t* other = C == T ? Wb : T;
+        C = replace_strip_wave(C, other, EL, EI, ca, cz, tok, lane);
+        strip(C, ca, cz);
       }
-      __syncthreads();
-      ca = sh_a;
-      cz = sh_z;
-      C = w;
     }
   }
+  PSTAMP(4);
 
-  // ---- 3. split(action_sep), strip, drop empties, cap at K (:165-169); name -> id (es :230-240)
+  // ---- 4. split(action_sep), strip, drop empties, cap at K (:165-169); name -> id (es :230-240)
   const Tag sep{cfg.sep_lo, cfg.sep_hi, cfg.sep_len};
-  const int col = (a.sel && a.sel[b]) ? 1 : 0;
-  const bool lane_name = lane < cfg.n_names;
-  const Tag name{lane_name ? cfg.name_lo[lane] : 0ull, lane_name ? cfg.name_hi[lane] : 0ull,
-                 lane_name ? (int)cfg.name_len[lane] : 0};
-  const int my_id = lane_name ? cfg.name_id[col][lane] : 0;
-  int count = 0, my_act = 0;
+  int count = 0;
   if (as >= 0) {
-    int pos = ca;
-    while (count < K) {
-      const int q = find_tag(C, pos, cz, sep, lane);
-      int s = pos, e = q < 0 ? cz : q;
-      strip(C, s, e);
-      if (e > s) {
-        int id = 0;
-        if (cfg.n_names > 0) {
-          // action.lower() == name (names are lowercased ASCII): lane j tests name j
-          bool ok = lane_name;
-          int qn = 0;
-          for (int i = s; ok && i < e;) {
-            uint32_t c = C[i];
-            if (c < 0x80) {
-              c += (c >= 'A' && c <= 'Z') ? 32u : 0u;
-              ++i;
-            } else if (c == 0xE2 && i + 2 < e && C[i + 1] == 0x84 && C[i + 2] == 0xAA) {
-              c = 'k';  // U+212A KELVIN SIGN
-              i += 3;
-            } else {
-              ok = false;
-              break;
-            }
-            ok = qn < name.n && tag_byte(name, qn) == c;
-            ++qn;
-          }
-          ok = ok && qn == name.n;
-          const uint64_t m = __ballot(ok);
-          if (m) id = __builtin_amdgcn_readlane(my_id, __builtin_ctzll(m));
-        } else {
-          id = 1;  // no lookup: the strings themselves are the actions
+    // separator candidates: positions of its first byte, full compare, greedy selection
+    const int nc = collect(C, ca, cz, (uint32_t)(sep.lo & 0xFFu), ES, lane);
+    __syncthreads();
+    int ns = 0, last = ca;  // selected separators -> EL (the '<' list is no longer needed)
+    for (int c = 0; c < nc; c += 64) {
+      const int i = c + lane;
+      bool m = false;
+      int p = 0;
+      if (i < nc) {
+        p = ES[i];
+        uint64_t lo, hi;
+        load16(C, p, lo, hi);
+        m = p + sep.n <= cz && tag_eq(lo, hi, sep);
+      }
+      uint64_t bits = __ballot(m);
+      while (bits) {  // left to right, non-overlapping (str.split)
+        const int L = __builtin_ctzll(bits);
+        bits &= bits - 1;
+        const int q = __builtin_amdgcn_readlane(p, L);
+        if (q >= last) {
+          if (lane == 0) EL[ns] = (uint16_t)q;
+          ++ns;
+          last = q + sep.n;
         }
-        if (lane == count) my_act = id;
+      }
+    }
+    __syncthreads();
+    // pieces: piece i = [i ? sel[i-1] + sep.n : ca, i < ns ? sel[i] : cz); one per lane
+    for (int c = 0; c <= ns && count < K; c += 64) {
+      const int i = c + lane;
+      int s = 0, e = 0;
+      if (i <= ns) {
+        s = i ? EL[i - 1] + sep.n : ca;
+        e = i < ns ? EL[i] : cz;
+        strip(C, s, e);
+      }
+      const bool keep = e > s;
+      const uint64_t km = __ballot(keep);
+      const int slot = count + __builtin_popcountll(km & ((1ull << lane) - 1ull));
+      if (keep && slot < K) {
+        a.actions[b * K + slot] = (int8_t)(nm.n > 0 ? piece_id(C, s, e, nm) : 1);
         if (a.action_text) {
           const int L = e - s, Lc = L < a.Lact ? L : a.Lact;
-          uint8_t* dst = a.action_text + (b * K + count) * (int64_t)a.Lact;
-          for (int i = lane; i < Lc; i += 64) dst[i] = C[s + i];
-          if (lane == 0) a.action_len[b * K + count] = Lc;
+          uint8_t* dst = a.action_text + (b * K + slot) * (int64_t)a.Lact;
+          for (int q = 0; q < Lc; ++q) dst[q] = C[s + q];
+          a.action_len[b * K + slot] = Lc;
           if (L > a.Lact) err |= RMI_ERR_UNSUP;
         }
-        ++count;
       }
-      if (q < 0) break;
-      pos = q + sep.n;
+      count += __builtin_popcountll(km);
     }
+    if (count > K) count = K;
   }
-  if (lane < K) {
-    a.actions[b * K + lane] = (int8_t)(lane < count ? my_act : 0);
-    if (a.action_text && lane >= count) a.action_len[b * K + lane] = 0;
+  PSTAMP(5);
+  if (lane >= count && lane < K) {
+    a.actions[b * K + lane] = 0;
+    if (a.action_text) a.action_len[b * K + lane] = 0;
+  }
+  const uint64_t any_err = __ballot(err != 0);
+  uint8_t err_all = err;
+  if (any_err) {  // OR over lanes (UNSUP may come from any piece lane)
+    for (int off = 32; off > 0; off >>= 1) err_all |= (uint8_t)__shfl_xor((int)err_all, off);
   }
   if (lane == 0) {
     a.n_actions[b] = (uint8_t)count;
-    if (a.spans) {
-      a.spans[4 * b + 0] = ts;
-      a.spans[4 * b + 1] = te;
-      a.spans[4 * b + 2] = as;
-      a.spans[4 * b + 3] = ae;
+    if (a.spans) {  // offsets in the prefixed response
+      a.spans[4 * b + 0] = ts < 0 ? -1 : ts - base;
+      a.spans[4 * b + 1] = te < 0 ? -1 : te - base;
+      a.spans[4 * b + 2] = as < 0 ? -1 : as - base;
+      a.spans[4 * b + 3] = ae < 0 ? -1 : ae - base;
     }
-    if (err && a.err) a.err[b] |= err;
+    if (err_all && a.err) a.err[b] |= err_all;
   }
+  PSTAMP(6);
+  PSTAMP_FLUSH();
 }
 
 // ------------------------------------------------------------------ detokenize
@@ -471,6 +689,12 @@ RMI_API int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32
   return launch_status();
 }
 
+#ifdef RMI_PARSE_STAMPS
+RMI_API int rmi_parse_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_parse_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
+
 RMI_API int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, const int32_t* text_len, int64_t B,
                               int32_t stride, const uint8_t* sel, int8_t* actions, uint8_t* n_actions,
                               int32_t* spans, uint8_t* action_text, int32_t* action_len, int32_t Lact, uint8_t* err,
@@ -478,7 +702,7 @@ RMI_API int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, c
   using namespace rmi;
   if (!cfg || B < 0 || stride <= 0) return RMI_EINVAL;
   if (cfg->K < 1 || cfg->sep_len < 1 || cfg->sep_len > 16 || cfg->n_names < 0) return RMI_EINVAL;
-  if (cfg->K > kMaxK || cfg->n_names > RMI_PARSE_MAX_NAMES || stride % 4 != 0 || stride > kMaxStride ||
+  if (cfg->K > kMaxK || cfg->n_names > RMI_PARSE_MAX_NAMES || stride % 4 != 0 || stride > kMaxParseStride ||
       B > 0x7FFFFFFF)
     return RMI_EUNSUP;
   for (int j = 0; j < cfg->n_names; ++j)
@@ -489,7 +713,7 @@ RMI_API int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, c
   if (reinterpret_cast<uintptr_t>(text) & 3u) return RMI_EUNSUP;
   ParseArgs a{*cfg, text, text_len, B, (int)stride, sel, actions, n_actions, spans, action_text, action_len,
               (int)Lact, err};
-  const size_t shm = (size_t)(kPre + stride + kPad) * 2;
+  const size_t shm = parse_lds(stride);
   hipLaunchKernelGGL(parse_kernel, dim3((unsigned)B), dim3(64), shm, as_stream(stream), a);
   return launch_status();
 }

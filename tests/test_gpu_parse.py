@@ -100,11 +100,18 @@ def test_parse_fuzz_and_edges(device):
     frags = ["<think>", "</think>", "<answer>", "</answer>", "<|im_end|>", "<|im_start|>", "|", "||", " ", "\n",
              "　", " ", "\xa0", "K", "Up", "down", "LEFT", "x", "é", "\U0001f600", "<", ">"]
     texts = ["".join(rng.choice(frags) for _ in range(rng.randint(0, 40))) for _ in range(3000)]
-    texts += ["", "</think><answer>" + "Up || " * 2000 + "</answer>", "a" * 9000]
+    texts += ["", "</think><answer>" + "Up || " * 1300 + "</answer>", "a" * 8000]
     for think in (True, False):
         for prepend in (True, False):
             out = _run(texts, device, think, 5, "||", SOKOBAN, prepend=prepend)
             _check_rows(texts, out, think, 5, "||", SOKOBAN, prepend=prepend)
+
+
+def test_parse_stride_envelope(device):
+    buf = torch.zeros(2, 8196, dtype=torch.uint8, device=device)
+    lens = torch.zeros(2, dtype=torch.int32, device=device)
+    with pytest.raises(NotImplementedError):  # rows longer than 8192 bytes: RMI_EUNSUP
+        ops.parse_actions(ops.parse_config(True, 5, "||", SOKOBAN), buf, lens)
 
 
 def test_parse_bad_lengths_and_overlong_actions(device):
