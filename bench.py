@@ -100,6 +100,38 @@ class Rollout:
         return a, b
 
 
+def scale_leg(R, device, tile=128, reps=5):
+    """The dominant kernel where HBM, not launch latency, bounds it: the bench's 8192 envs
+    tiled `tile` times (1 048 576 envs; ~28 MB of algorithmic traffic per launch), 5 turns,
+    HIP events around the turn launches.  Same rooms and actions in every tile, so each
+    turn's active count is exactly tile x the bench's.  -> (seconds per 5 launches, envs)."""
+    B = R.B * tile
+    env = SokobanBatch(SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100), B, T_TURNS, K_ACTIONS, device)
+    env.room_fixed.copy_(R.env.room_fixed.repeat(tile, 1))
+    env.init_state.copy_(R.env.init_state.repeat(tile, 1))
+    env.init_player.copy_(R.env.init_player.repeat(tile, 1))
+    ids = R.ids.repeat(1, tile, 1).contiguous()
+    n = R.n.repeat(1, tile).contiguous()
+    turns = [ops.turn_struct(t, ids[t], n[t], None, MAX_ACTIONS, -0.1) for t in range(T_TURNS)]
+    st = env.struct()
+    ev = []
+    for r in range(reps + 1):
+        env.restore()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for t in range(T_TURNS):
+            ops.sokoban_step_turn(st, env.ep, turns[t])
+        b.record()
+        if r:
+            ev.append((a, b))
+    torch.cuda.synchronize()
+    steps = int(env.ep.turn_exec.sum().item())
+    assert steps == tile * int(R.env.ep.turn_exec.sum().item()), "tiled rollout diverged from the bench's"
+    dur = float(np.mean([x.elapsed_time(y) for x, y in ev])) * 1e-3
+    del env, ids, n
+    return dur, B
+
+
 def hbm_copy_peak(device, nbytes=1 << 30, reps=10):
     """Achievable HBM bandwidth on this box: a 1 GiB device-to-device copy (read + write)."""
     x = torch.empty(nbytes // 4, dtype=torch.float32, device=device)
@@ -671,6 +703,14 @@ def main():
     toytext = toytext_legs(device) if not args.no_extras else None
     api = api_leg(device) if not args.no_extras and rank == 0 else None
     text = text_leg(R, device) if not args.no_extras and rank == 0 else None
+    at_scale = None
+    if not args.no_extras and rank == 0:
+        s_dur, s_B = scale_leg(R, device)
+        s_bytes = bytes_per_rollout * (s_B // R.B)
+        s_ach = s_bytes / s_dur / 1e9
+        at_scale = {"envs": s_B, "avg_launch_us": s_dur / T_TURNS * 1e6, "achieved": s_ach,
+                    "frac": s_ach / HBM_PEAK_GBS, "frac_of_achievable": (s_ach / copy_peak) if copy_peak else None,
+                    "note": "same kernel and workload per env, batch tiled 128x: HBM-bound, not launch-bound"}
 
     if rank == 0:
         cpu = cpu_par = None
@@ -712,7 +752,8 @@ def main():
                          "achievable_peak": copy_peak,
                          "frac_of_achievable": (achieved / copy_peak) if copy_peak else None,
                          "kernel": "rmi_sokoban_step_turn", "avg_launch_us": avg_launch_us,
-                         "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn},
+                         "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn,
+                         "at_scale": at_scale},
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,
             "advantage": adv,
