@@ -5,17 +5,16 @@
 //
 // HBM layout (caller-owned SoA, include/ragen_amd.h): room grids are [B, H*W] u8 rows.
 // The kernel is latency-bound (8192 envs = 128 waves < 256 CUs), so it minimises each
-// lane's serial chain:
-//   1. every global load of the turn is issued up front: the wave's 64 rows of room_state
-//      and room_fixed as coalesced 16-B loads staged into LDS, and the per-env scalars and
-//      actions — one memory round trip;
-//   2. the grids stay in LDS; a lane's row starts at lane*H*W bytes (stride 9 dwords for
-//      6x6: coprime with the 32 banks).  An action reads its <= 6 cells as independent
-//      ds_read_u8 (one LDS round trip), decides push / move / blocked branch-free and
-//      writes <= 3 cells — byte-exact with upstream's numpy writes;
-//   3. _calc_reward's open-target count is computed once per turn with SWAR byte compares
-//      on the row's dwords and then maintained incrementally from the written cells;
-//   4. updated rows go back with coalesced 16-B stores, only if some env of the wave moved.
+// lane's serial chain (DESIGN.md §3.1 has the measurements behind each point):
+//   1. every global load of the turn is issued up front, branch-free from clamped addresses:
+//      the lane's own rows of room_state and room_fixed (16-B pieces), the per-env scalars and
+//      the actions — one memory round trip;
+//   2. the rows stay in VGPRs.  A regular room (every generated one) becomes wall / target /
+//      box bitboards; the K steps are one unrolled, predicated block of shifts and masks, and
+//      _calc_reward's open-target count is popc(target & ~box);
+//   3. only the changed cells (old / new player, moved boxes) are stored back;
+//   4. any irregular room sends its whole wave to the exact path (env-private LDS rows,
+//      numpy's negative-index wrap, gym_sokoban's IndexError points).
 #include "common.hpp"
 
 namespace rmi {
