@@ -6,10 +6,11 @@
 Workload (BASELINE.json configs[2], SURVEY §8(d) "SK"): Sokoban 6x6 / 1 box, 8192 envs per
 GPU (512 groups x 16, env i seeded 1000 + i // 16), 5 turns of up to K=5 synthetic actions
 per env (10 % unknown names), max 10 actions per trajectory.  One bench "step" = one whole
-rollout phase over the batch: restore the post-reset state (reset itself is excluded, as
-§8(d) specifies), 5 turn kernels, get_rollout_states metrics, trajectory scores and the
-StarPO reward normalisation.  Inputs are resident in HBM before timing.  The step is
-captured once in a HIP graph and replayed (launch-bound: one graph launch per rollout).
+rollout phase over the batch from the post-reset state (room generation is excluded, as
+§8(d) specifies; the device restore of the reset state is fused into the first turn), 5 turn
+kernels, get_rollout_states metrics, trajectory scores and the StarPO reward normalisation
+(fused into the last turn).  Inputs are resident in HBM before timing.  The step is captured
+in a HIP graph and replayed, several rollouts per replay.
 
 Multi-GPU: weak scaling — every rank runs its own 8192 envs (global group ids preserved,
 rank r seeds groups r*512..), no collective on the data path; value = all ranks' env steps
@@ -70,12 +71,15 @@ class Rollout:
         self.fin = ops.finalize_struct(GROUP, "identity", self.norm, self.metrics)
 
     def step(self):
-        """One rollout phase: restore, T turn launches, the last one fused with the rollout's
-        finalize (metrics + scores + normalisation; == rmi_rollout_finalize, tested bit-exact)."""
-        self.env.restore()
-        for t in range(T_TURNS - 1):
-            ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
-        ops.sokoban_step_turn_finalize(self.st, self.env.ep, self.turns[-1], self.fin)
+        """One rollout phase from the post-reset state: T turn launches.  The first is fused with
+        the reset's restore (rmi_sokoban_step_turn_first == rmi_sokoban_reset + turn, tested bit
+        for bit), the last with the rollout's finalize (metrics + scores + normalisation ==
+        rmi_rollout_finalize, tested bit for bit)."""
+        e = self.env
+        ops.sokoban_step_turn_first(self.st, e.ep, self.turns[0], e.init_state, e.init_player)
+        for t in range(1, T_TURNS - 1):
+            ops.sokoban_step_turn(self.st, e.ep, self.turns[t])
+        ops.sokoban_step_turn_finalize(self.st, e.ep, self.turns[-1], self.fin)
 
     def step_unfused(self):
         """The same rollout with T plain turn launches and the separate finalize launch (the
@@ -542,7 +546,7 @@ def main():
     active_per_turn = [int((n_turns > t).sum()) for t in range(T_TURNS)]
 
     # Graph replay, G rollouts per replay (G = --group, reduced until it divides --steps; every
-    # rollout is a full restore + T turns + finalize into its own episode arena).
+    # rollout is a full restore (fused into turn 0) + T turns + finalize into its own episode arena).
     # N > 1: the rollout's real exchange step (north_star) — reassemble every
     # rank's trajectory record before the PPO update — is ONE RCCL all-gather of the G arenas of
     # a replay (they are contiguous: EpisodeState.pool), captured in its own graph and replayed

@@ -127,6 +127,15 @@ typedef struct {
 int rmi_sokoban_step_turn_finalize(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                    uint8_t* err, const rmi_finalize_t* fin, rmi_stream_t stream);
 
+/* A fresh episode's first turn fused with its reset: exactly rmi_sokoban_reset(init_state,
+ * init_player) followed by rmi_sokoban_step_turn, in one launch (SokobanEnv.reset
+ * sokoban/env.py:37-38 + EnvStatus() es_manager.py:95, then EnvStateManager.step
+ * es_manager.py:105-171).  The counters and the episode record are not read (they start at
+ * zero); every env's row, player, counters and whole record (all T rows) are written.   */
+int rmi_sokoban_step_turn_first(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                const uint8_t* init_state, const int8_t* init_player, uint8_t* err,
+                                rmi_stream_t stream);
+
 /* Device part of SokobanEnv.reset (sokoban/env.py:37-38) + EnvStatus(seed) (es_manager.py:95):
  * room_state/player := init_state/init_player (the generated rooms), num_env_steps =
  * boxes_on_target = 0, and the whole episode record zeroed — one launch.  B*H*W % 4 == 0. */

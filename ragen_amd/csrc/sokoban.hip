@@ -632,10 +632,15 @@ __device__ __forceinline__ void finalize_envs(const rmi_episode_t& ep, const rmi
 // type M.  `border` = bitmask of the border cells (row-major), precomputed by the launcher.
 // kFin: the launch is the rollout's last turn and also runs rmi_rollout_finalize for uniform
 // contiguous groups of fin.group_size envs (each group inside one wave): see finalize_envs.
-template <int HW, class M, int LPE, bool kFin>  // HW = H*W for the common sizes (0 = runtime); H*W % 4 == 0
+// kFirst: the launch is a fresh episode's first turn fused with the reset (rmi_sokoban_reset):
+// the rows and players come from init_state / init_player, the counters and the episode record
+// start at zero without being read, and every env's state and whole record are written.
+template <int HW, class M, int LPE, bool kFin, bool kFirst = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
-                                                                  uint8_t* __restrict__ err_out, rmi_finalize_t fin) {
+                                                                  uint8_t* __restrict__ err_out, rmi_finalize_t fin,
+                                                                  const uint8_t* __restrict__ init_state = nullptr,
+                                                                  const int8_t* __restrict__ init_player = nullptr) {
   constexpr int NW = HW ? HW / 4 : kMaxWords;
   constexpr int NWL = (NW + LPE - 1) / LPE;      // row dwords per lane
   constexpr int kEnvs = kWave / LPE;             // envs per wave
@@ -660,14 +665,23 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   uint32_t xs[NWL], xf[NWL];
 #pragma unroll
   for (int i = 0; i < NWL; ++i) xs[i] = xf[i] = 0;
-  load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
+  load_row<NWL, LPE, HW != 0>((kFirst ? init_state : env.room_state) + bc * hw, xs, sub, row_words);
   load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
-  uint8_t flags = ep.flags[bc];
-  const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
-  int r = env.player[2 * bc], c = env.player[2 * bc + 1];
-  int nes = env.num_env_steps[bc], bot = env.boxes_on_target[bc];
-  int32_t num_actions = ep.num_actions[bc], n_turns = ep.n_turns[bc];
-  double penalty = ep.penalty[bc];
+  const int8_t* pl = kFirst ? init_player : env.player;
+  int r = pl[2 * bc], c = pl[2 * bc + 1];
+  const uint8_t has_in = in.has_input ? in.has_input[bc] : (uint8_t)0;
+  uint8_t flags = 0;
+  int nes = 0, bot = 0;
+  int32_t num_actions = 0, n_turns = 0;
+  double penalty = 0.0;
+  if (!kFirst) {  // a fresh episode's record is all zero (EnvStatus(), es_manager.py:95)
+    flags = ep.flags[bc];
+    nes = env.num_env_steps[bc];
+    bot = env.boxes_on_target[bc];
+    num_actions = ep.num_actions[bc];
+    n_turns = ep.n_turns[bc];
+    penalty = ep.penalty[bc];
+  }
   int n_act = in.n_actions[bc];
   uint8_t av[kMaxK];
 #pragma unroll
@@ -685,6 +699,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   if (!live) flags = RMI_FLAG_DONE;
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
   RMI_STAMP_WAIT(1);
+  if (kFirst && live) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);  // the reset
 
   // ---- 2. format penalty and the regular-room test
   if (n_act > in.K) n_act = in.K;
@@ -725,6 +740,9 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   o.stepped_any_state = false;
   bool turn_done = false, succ_last = false, row_changed = false;
   uint8_t err = 0;
+  // kFirst: the reset row's store (above) has completed before any lane of the env writes
+  // cells of it (with several lanes per env they are other lanes' dwords)
+  if (kFirst) __builtin_amdgcn_s_waitcnt(0);
   if (__all(regular)) {
     if (act) {
       const M box0 = box;
@@ -808,6 +826,23 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   RMI_STAMP(3);
 
   // ---- 4. outputs: scalars from the env's first lane, row dwords from every lane
+  if (kFirst && live && !act && sub == 0) {  // no input this turn: the env keeps its reset state
+    env.player[2 * b] = (int8_t)r;
+    env.player[2 * b + 1] = (int8_t)c;
+    env.num_env_steps[b] = 0;
+    env.boxes_on_target[b] = 0;
+    ep.num_actions[b] = 0;
+    ep.flags[b] = 0;
+    ep.n_turns[b] = 0;
+    ep.penalty[b] = 0.0;
+  }
+  if (kFirst && live && sub == 0)
+    for (int t = 0; t < ep.T; ++t)
+      if (t != in.turn || !act) {
+        ep.turn_reward[(int64_t)t * B + b] = 0.0;
+        ep.turn_info[(int64_t)t * B + b] = 0;
+        ep.turn_exec[(int64_t)t * B + b] = 0;
+      }
   if (act) {
     if (sub == 0) {
       finish_turn(o, turn_done, succ_last, num_actions, flags, n_turns, in.max_actions_per_traj);
@@ -819,7 +854,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
       ep.turn_reward[tb] = o.acc;
       ep.turn_info[tb] = o.info;
       ep.turn_exec[tb] = o.exec;
-      if (o.stepped_any_state) {
+      if (kFirst || o.stepped_any_state) {
         env.player[2 * b] = (int8_t)r;
         env.player[2 * b + 1] = (int8_t)c;
         env.num_env_steps[b] = nes;
@@ -868,9 +903,10 @@ __global__ __launch_bounds__(kBlock) void sokoban_reset_kernel(rmi_sokoban_t env
 
 namespace rmi {
 namespace {
-template <bool kFin>
+template <bool kFin, bool kFirst = false>
 int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in, uint8_t* err,
-                             const rmi_finalize_t& fin, hipStream_t s) {
+                             const rmi_finalize_t& fin, hipStream_t s, const uint8_t* init_state = nullptr,
+                             const int8_t* init_player = nullptr) {
   const int hw = env->H * env->W;
   const unsigned grid = (unsigned)((ep->B + kWave - 1) / kWave);
   const int H = env->H, W = env->W;
@@ -884,12 +920,12 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
 #define RMI_LAUNCH(HW_, M_)                                                                                   \
   do {                                                                                                        \
     if (spread)                                                                                               \
-      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, kSpreadLpe, kFin>),                               \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, kSpreadLpe, kFin, kFirst>),                       \
                          dim3((unsigned)((ep->B + kWave / kSpreadLpe - 1) / (kWave / kSpreadLpe))),           \
-                         dim3(kWave), 0, s, *env, *ep, *in, hw, border, err, fin);                            \
+                         dim3(kWave), 0, s, *env, *ep, *in, hw, border, err, fin, init_state, init_player);   \
     else                                                                                                      \
-      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin>), dim3(grid), dim3(kWave), 0, s, *env, *ep, \
-                         *in, hw, border, err, fin);                                                          \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, kFirst>), dim3(grid), dim3(kWave), 0, s,   \
+                         *env, *ep, *in, hw, border, err, fin, init_state, init_player);                      \
   } while (0)
   if (hw == 36 && w32)
     RMI_LAUNCH(36, uint32_t);
@@ -951,6 +987,26 @@ RMI_API int rmi_sokoban_step_turn_finalize(const rmi_sokoban_t* env, const rmi_e
   rmi_finalize_t f = *fin;
   if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member
   return sokoban_step_turn_launch<true>(env, ep, in, err, f, as_stream(stream));
+}
+
+RMI_API int rmi_sokoban_step_turn_first(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                        const uint8_t* init_state, const int8_t* init_player, uint8_t* err,
+                                        rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !ep) return RMI_EINVAL;
+  if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
+  const int rc = check_turn_args(ep, in);
+  if (rc < 0) return rc;
+  if (ep->B == 0) return RMI_OK;
+  const int ec = sokoban_check(env);
+  if (ec != RMI_OK) return ec;
+  if (!init_state || !init_player || !ep->num_actions || !ep->flags || !ep->n_turns || !ep->penalty ||
+      !ep->turn_reward || !ep->turn_info || !ep->turn_exec || ep->T <= 0)
+    return RMI_EINVAL;
+  if (in->turn < 0 || in->turn >= ep->T) return RMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(init_state) & 3u) return RMI_EUNSUP;
+  return sokoban_step_turn_launch<false, true>(env, ep, in, err, rmi_finalize_t{}, as_stream(stream), init_state,
+                                               init_player);
 }
 
 RMI_API int rmi_sokoban_reset(const rmi_sokoban_t* env, const rmi_episode_t* ep, const uint8_t* init_state,

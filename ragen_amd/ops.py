@@ -161,6 +161,17 @@ def sokoban_step_turn_finalize(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.T
     check(rc, "rmi_sokoban_step_turn_finalize")
 
 
+def sokoban_step_turn_first(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn, init_state: torch.Tensor,
+                            init_player: torch.Tensor, err: Optional[torch.Tensor] = None):
+    """sokoban_reset(init_state, init_player) + sokoban_step_turn(turn) in one launch: a fresh
+    episode's first turn (the record is written, never read)."""
+    _dev(init_state, init_player, err)
+    _dt(init_state, torch.uint8, "init_state")
+    _dt(init_player, torch.int8, "init_player")
+    check(lib().rmi_sokoban_step_turn_first(env, ep.struct(), turn, _ptr(init_state), _ptr(init_player), _ptr(err),
+                                            _stream()), "rmi_sokoban_step_turn_first")
+
+
 def sokoban_reset(env: _lib.Sokoban, ep: EpisodeState, init_state: torch.Tensor, init_player: torch.Tensor):
     """Fused device reset from the generated rooms (state, player, counters, episode record)."""
     _dev(init_state, init_player)

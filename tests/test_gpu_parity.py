@@ -586,3 +586,47 @@ def test_bilevel_vs_oracle_large(device, B):
         s1 = (oa.astype(np.float64) * m).sum(1)
         np.testing.assert_allclose(stats[:, 0].cpu().numpy()[ok], s1[ok], rtol=1e-12, atol=1e-9)
         np.testing.assert_array_equal(stats[:, 2].cpu().numpy(), m.sum(1).astype(np.float64))
+
+
+@pytest.mark.parametrize("B,frac_irregular,partial", [(8192, 0.0, False), (1000, 0.0, True), (2050, 0.3, False),
+                                                       (16500, 0.3, True)])
+def test_fused_first_turn(device, B, frac_irregular, partial):
+    """rmi_sokoban_step_turn_first == rmi_sokoban_reset + rmi_sokoban_step_turn, bit for bit:
+    rows, players, counters, the whole episode record and the error bits, starting from a
+    dirty (mid-rollout) state; both lane layouts, irregular rooms, envs without input."""
+    rng = np.random.default_rng(B + int(partial))
+    T, K, H, W = 4, 6, 6, 6
+    cfg = SokobanEnvConfig(dim_x=H, dim_y=W, num_boxes=1, max_steps=12)
+    env0 = SokobanBatch(cfg, B, T, K, device)
+    env0.reset(synthetic.env_seeds(B))
+    fixed = env0.room_fixed.cpu().numpy().copy()
+    state = env0.init_state.cpu().numpy().copy()
+    player = env0.init_player.cpu().numpy().copy()
+    idx = np.nonzero(rng.random(B) < frac_irregular)[0]
+    f2, s2, p2 = fixed[idx].copy(), state[idx].copy(), player[idx].copy()
+    _irregular_rooms(rng, len(idx), H, W, f2, s2, p2)
+    fixed[idx], state[idx], player[idx] = f2, s2, p2
+    turns = []
+    for t in range(3):
+        ids = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9], size=(B, K), p=[0.05] + [0.11] * 8 + [0.07]).astype(np.int8)
+        n = rng.integers(0, K + 1, size=B).astype(np.uint8)
+        turns.append((_t(ids, device), _t(n, device)))
+    has = _t((rng.random(B) < 0.7).astype(np.uint8), device) if partial else None
+    outs = []
+    for fused in (False, True):
+        env = SokobanBatch(cfg, B, T, K, device)
+        env.load_state(fixed, state, player)
+        for t in (0, 1):  # dirty the state and the record
+            env.step_turn(t, turns[t][0], turns[t][1], None, 9, -0.1)
+        err = torch.zeros(B, dtype=torch.uint8, device=device)
+        turn = ops.turn_struct(0, turns[2][0], turns[2][1], has, 9, -0.1)
+        if fused:
+            ops.sokoban_step_turn_first(env.struct(), env.ep, turn, env.init_state, env.init_player, err)
+        else:
+            env.restore()
+            ops.sokoban_step_turn(env.struct(), env.ep, turn, err)
+        torch.cuda.synchronize()
+        outs.append((env.room_state.clone(), env.player.clone(), env.num_env_steps.clone(),
+                     env.boxes_on_target.clone(), env.ep.arena.clone(), err))
+    for name, a, b in zip(("room_state", "player", "nes", "bot", "episode", "err"), *outs):
+        assert torch.equal(a, b), name
