@@ -255,7 +255,8 @@ def toytext_legs(device):
     """BASELINE configs[1] and [4] on this GPU (parity cases of the bench, reported as extras):
     FrozenLake 4x4 slippery, 4096 envs x 8 turns (K=5, cap 10), and Countdown 16384 envs x 4
     turns (K=1, cap 1; half the turns carry no answer -> mixed episode lengths).  A rollout =
-    restore the post-reset state (device copies), T turn launches, fused finalize."""
+    T turn launches from the post-reset state (FrozenLake's first one fused with the device
+    restore; Countdown's record zeroed), then the fused finalize."""
     from ragen_amd.env import CountdownBatch, FrozenLakeBatch
     from ragen_amd.env.configs import CountdownEnvConfig, FrozenLakeEnvConfig
     from ragen_amd.env.countdown import synthetic_instances
@@ -271,9 +272,9 @@ def toytext_legs(device):
     turns = [ops.turn_struct(t, ids[t], n[t], None, 10, -0.1) for t in range(T)]
     st = fl.struct()
 
-    def fl_step():
-        fl.restore()
-        for t in range(T):
+    def fl_step():  # the first turn fused with the restore of the reset state
+        ops.frozenlake_step_turn_first(st, fl.ep, turns[0], fl.init_desc, fl.init_s, fl.init_rng)
+        for t in range(1, T):
             ops.frozenlake_step_turn(st, fl.ep, turns[t])
         ops.rollout_finalize(fl.ep, seg, "mean_std", norm)
     fl_step()

@@ -179,6 +179,12 @@ int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* e
 /* Device part of FrozenLakeEnv.reset (frozen_lake/env.py:28-37) + EnvStatus(seed)
  * (es_manager.py:95): desc / s / rng := the generated map, its start state and the seeded PCG64
  * (generate_random_map and the seeding stay on the host), episode record zeroed — one launch.  */
+/* A fresh episode's first turn fused with its reset: exactly rmi_frozenlake_reset(init_desc,
+ * init_s, init_rng) followed by rmi_frozenlake_step_turn, in one launch (FrozenLakeEnv.reset
+ * frozen_lake/env.py:28-37 + EnvStatus() es_manager.py:95, then EnvStateManager.step).    */
+int rmi_frozenlake_step_turn_first(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                   const uint8_t* init_desc, const int32_t* init_s, const uint64_t* init_rng,
+                                   uint8_t* err, rmi_stream_t stream);
 int rmi_frozenlake_reset(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const uint8_t* init_desc,
                          const int32_t* init_s, const uint64_t* init_rng, rmi_stream_t stream);
 

@@ -13,6 +13,10 @@
 namespace rmi {
 namespace {
 
+// One wave per workgroup for the turn kernels: a turn is a latency-bound chain per env, and
+// 4096 envs in 256-thread blocks would occupy only 16 CUs (64 one-wave blocks spread over 64).
+constexpr int kToyBlock = 64;
+
 struct FrozenLakeDev {
   const uint8_t* desc;  // this env's row
   uint64_t d_lo, d_hi;  // the row itself when it has <= 16 cells (loaded once; no per-step load)
@@ -61,24 +65,37 @@ struct FrozenLakeDev {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void frozenlake_step_turn_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
-                                                                      rmi_turn_t in, uint8_t* __restrict__ err_out) {
-  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+// kFirst: a fresh episode's first turn fused with its reset (rmi_frozenlake_reset): desc, s and
+// the PCG64 state come from the init arrays, the counters and the record start at zero without
+// being read, and the env's reset state and whole record are written before the turn runs.
+template <bool kFirst>
+__global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
+                                                                         rmi_turn_t in, uint8_t* __restrict__ err_out,
+                                                                         const uint8_t* __restrict__ init_desc,
+                                                                         const int32_t* __restrict__ init_s,
+                                                                         const uint64_t* __restrict__ init_rng) {
+  const int64_t b = (int64_t)blockIdx.x * kToyBlock + threadIdx.x;
   const int B = ep.B;
   if (b >= B) return;
   // every load of the turn is issued before the first use (one memory round trip)
-  uint8_t flags = ep.flags[b];
+  uint8_t flags = 0;
+  int32_t num_actions = 0, n_turns = 0;
+  double penalty = 0.0;
+  if (!kFirst) {  // a fresh episode's record is all zero (EnvStatus(), es_manager.py:95)
+    flags = ep.flags[b];
+    num_actions = ep.num_actions[b];
+    n_turns = ep.n_turns[b];
+    penalty = ep.penalty[b];
+  }
   const uint8_t has_in = in.has_input ? in.has_input[b] : 0;
-  int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
-  double penalty = ep.penalty[b];
   const int n_act = in.n_actions[b];
   const uint64_t acts = load_actions(in.actions + b * (int64_t)in.K, in.K);
   const int n = env.nrow * env.ncol;
   FrozenLakeDev e;
-  e.desc = env.desc + b * n;
+  e.desc = (kFirst ? init_desc : env.desc) + b * n;
   e.in_regs = n <= 16;
   e.d_lo = e.d_hi = 0;
-  if (n == 16 && (reinterpret_cast<uintptr_t>(env.desc) & 15u) == 0) {  // the 4x4 default: one 16-B load
+  if (n == 16 && (reinterpret_cast<uintptr_t>(kFirst ? init_desc : env.desc) & 15u) == 0) {  // 4x4: one 16-B load
     const uint4 q = *reinterpret_cast<const uint4*>(e.desc);
     e.d_lo = ((uint64_t)q.y << 32) | q.x;
     e.d_hi = ((uint64_t)q.w << 32) | q.z;
@@ -91,12 +108,33 @@ __global__ __launch_bounds__(kBlock) void frozenlake_step_turn_kernel(rmi_frozen
   }
   e.nrow = env.nrow;
   e.ncol = env.ncol;
-  e.s = env.s[b];
+  e.s = kFirst ? init_s[b] : env.s[b];
   e.slippery = env.is_slippery != 0;
   e.cs0 = env.cs0;
   e.cs1 = env.cs1;
   e.cs2 = env.cs2;
-  e.rng = load_pcg(env.rng, B, b);
+  e.rng = load_pcg(kFirst ? init_rng : env.rng, B, b);
+  if (kFirst) {  // the reset, then the turn (same thread, later stores win)
+    uint8_t* desc = const_cast<uint8_t*>(env.desc) + b * n;
+    if (n == 16 && ((reinterpret_cast<uintptr_t>(env.desc) & 15u) == 0)) {
+      *reinterpret_cast<uint4*>(desc) = make_uint4((uint32_t)e.d_lo, (uint32_t)(e.d_lo >> 32), (uint32_t)e.d_hi,
+                                                   (uint32_t)(e.d_hi >> 32));
+    } else {
+      for (int i = 0; i < n; ++i) desc[i] = e.desc[i];
+    }
+    env.s[b] = e.s;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) env.rng[k * (int64_t)B + b] = init_rng[k * (int64_t)B + b];
+    ep.num_actions[b] = 0;
+    ep.flags[b] = 0;
+    ep.n_turns[b] = 0;
+    ep.penalty[b] = 0.0;
+    for (int t = 0; t < ep.T; ++t) {
+      ep.turn_reward[(int64_t)t * B + b] = 0.0;
+      ep.turn_info[(int64_t)t * B + b] = 0;
+      ep.turn_exec[(int64_t)t * B + b] = 0;
+    }
+  }
   const bool act = in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE);
   if (!act) return;
   uint8_t err = 0;
@@ -138,9 +176,9 @@ struct BanditDev {
   }
 };
 
-__global__ __launch_bounds__(kBlock) void bandit_step_turn_kernel(rmi_bandit_t env, rmi_episode_t ep, rmi_turn_t in,
+__global__ __launch_bounds__(kToyBlock) void bandit_step_turn_kernel(rmi_bandit_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   uint8_t* __restrict__ err_out) {
-  const int64_t b = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t b = (int64_t)blockIdx.x * kToyBlock + threadIdx.x;
   const int B = ep.B;
   if (b >= B) return;
   uint8_t flags = ep.flags[b];
@@ -228,9 +266,24 @@ RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_epis
   const int rc = check_turn_args(ep, in);
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
-  const unsigned grid = (unsigned)((ep->B + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(frozenlake_step_turn_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *env, *ep, *in,
-                     err);
+  const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
+  hipLaunchKernelGGL(frozenlake_step_turn_kernel<false>, dim3(grid), dim3(kToyBlock), 0, as_stream(stream), *env,
+                     *ep, *in, err, nullptr, nullptr, nullptr);
+  return launch_status();
+}
+
+RMI_API int rmi_frozenlake_step_turn_first(const rmi_frozenlake_t* env, const rmi_episode_t* ep,
+                                           const rmi_turn_t* in, const uint8_t* init_desc, const int32_t* init_s,
+                                           const uint64_t* init_rng, uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env) return RMI_EINVAL;
+  if (env->nrow <= 0 || env->ncol <= 0 || env->nrow * env->ncol > 64) return RMI_EUNSUP;
+  const int rc = check_turn_args(ep, in);
+  if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
+  if (!env->desc || !env->s || !env->rng || !init_desc || !init_s || !init_rng) return RMI_EINVAL;
+  const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
+  hipLaunchKernelGGL(frozenlake_step_turn_kernel<true>, dim3(grid), dim3(kToyBlock), 0, as_stream(stream), *env, *ep,
+                     *in, err, init_desc, init_s, init_rng);
   return launch_status();
 }
 
@@ -241,7 +294,7 @@ RMI_API int rmi_bandit_step_turn(const rmi_bandit_t* env, const rmi_episode_t* e
   const int rc = check_turn_args(ep, in);
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->hi_is_first || !env->rng) return RMI_EINVAL;
-  const unsigned grid = (unsigned)((ep->B + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(bandit_step_turn_kernel, dim3(grid), dim3(kBlock), 0, as_stream(stream), *env, *ep, *in, err);
+  const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
+  hipLaunchKernelGGL(bandit_step_turn_kernel, dim3(grid), dim3(kToyBlock), 0, as_stream(stream), *env, *ep, *in, err);
   return launch_status();
 }

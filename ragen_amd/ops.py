@@ -187,6 +187,14 @@ def frozenlake_reset(env: _lib.FrozenLake, ep: EpisodeState, init_desc: torch.Te
           "rmi_frozenlake_reset")
 
 
+def frozenlake_step_turn_first(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn, init_desc: torch.Tensor,
+                               init_s: torch.Tensor, init_rng: torch.Tensor, err: Optional[torch.Tensor] = None):
+    """frozenlake_reset(init_*) + frozenlake_step_turn(turn) in one launch (a fresh episode's first turn)."""
+    _dev(init_desc, init_s, init_rng, err)
+    check(lib().rmi_frozenlake_step_turn_first(env, ep.struct(), turn, _ptr(init_desc), _ptr(init_s), _ptr(init_rng),
+                                               _ptr(err), _stream()), "rmi_frozenlake_step_turn_first")
+
+
 def frozenlake_step_turn(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn,
                          err: Optional[torch.Tensor] = None):
     check(lib().rmi_frozenlake_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_frozenlake_step_turn")

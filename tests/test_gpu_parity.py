@@ -630,3 +630,30 @@ def test_fused_first_turn(device, B, frac_irregular, partial):
                      env.boxes_on_target.clone(), env.ep.arena.clone(), err))
     for name, a, b in zip(("room_state", "player", "nes", "bot", "episode", "err"), *outs):
         assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("B,partial", [(4096, False), (1000, True)])
+def test_frozenlake_fused_first_turn(device, B, partial):
+    """rmi_frozenlake_step_turn_first == rmi_frozenlake_reset + rmi_frozenlake_step_turn, bit for
+    bit (desc, s, the PCG64 state, the whole record, error bits), from a dirty state."""
+    rng = np.random.default_rng(B)
+    T, K = 4, 5
+    ids, n = synthetic.rollout_actions(B, 3, K, 1, 4, seed=B)
+    has = _t((rng.random(B) < 0.6).astype(np.uint8), device) if partial else None
+    outs = []
+    for fused in (False, True):
+        fl = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
+        fl.reset(synthetic.env_seeds(B))
+        for t in (0, 1):
+            fl.step_turn(t, _t(ids[t], device), _t(n[t], device), None, 10, -0.1)
+        err = torch.zeros(B, dtype=torch.uint8, device=device)
+        turn = ops.turn_struct(0, _t(ids[2], device), _t(n[2], device), has, 10, -0.1)
+        if fused:
+            ops.frozenlake_step_turn_first(fl.struct(), fl.ep, turn, fl.init_desc, fl.init_s, fl.init_rng, err)
+        else:
+            fl.restore()
+            ops.frozenlake_step_turn(fl.struct(), fl.ep, turn, err)
+        torch.cuda.synchronize()
+        outs.append((fl.desc.clone(), fl.s.clone(), fl.rng.clone(), fl.ep.arena.clone(), err))
+    for name, a, b in zip(("desc", "s", "rng", "episode", "err"), *outs):
+        assert torch.equal(a, b), name
