@@ -376,15 +376,17 @@ def text_leg(R, device, reps=20):
         o = ops.parse_actions(cfg, bufs[t][0], bufs[t][1], with_spans=False)
         text_turns.append((o, ops.turn_struct(t, o["actions"], o["n_actions"], None, MAX_ACTIONS, -0.1)))
 
-    def text_step():
-        R.env.restore()
+    def text_step():  # R.step()'s launches, each turn preceded by its parse
+        e = R.env
         for t in range(T_TURNS):
             o, ts = text_turns[t]
             ops.parse_actions(cfg, bufs[t][0], bufs[t][1], with_spans=False, out=o)
-            if t < T_TURNS - 1:
-                ops.sokoban_step_turn(R.st, R.env.ep, ts)
+            if t == 0:
+                ops.sokoban_step_turn_first(R.st, e.ep, ts, e.init_state, e.init_player)
+            elif t < T_TURNS - 1:
+                ops.sokoban_step_turn(R.st, e.ep, ts)
             else:
-                ops.sokoban_step_turn_finalize(R.st, R.env.ep, ts, R.fin)
+                ops.sokoban_step_turn_finalize(R.st, e.ep, ts, R.fin)
     text_step()
     torch.cuda.synchronize()
     steps = int(R.env.ep.turn_exec.sum().item())
@@ -395,7 +397,7 @@ def text_leg(R, device, reps=20):
             "detokenize": {"kernel": "rmi_detokenize", "rows": B, "ids_per_row": Rt, "vocab": V, "us": detok_us,
                            "achieved_GBs": dbytes / (detok_us * 1e-6) / 1e9,
                            "frac": dbytes / (detok_us * 1e-6) / 1e9 / HBM_PEAK_GBS},
-            "text_rollout": {"config": "SK rollout from response text: restore + 5 x (parse + turn) + finalize",
+            "text_rollout": {"config": "SK rollout from response text: 5 x (parse + turn), restore and finalize fused",
                              "env_steps_per_rollout": steps, "ms_per_rollout": ms,
                              "env_steps_per_s": steps / ms * 1e3}}
 

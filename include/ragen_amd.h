@@ -320,10 +320,11 @@ int rmi_grpo_outcome(const float* r, const uint8_t* mask, int64_t B, int64_t L, 
  * (String::from_utf8_lossy) and written back as UTF-8: out[b, 0 .. out_len[b]) is exactly
  * decoded_str.encode("utf-8").  ids [B,R] (n_ids[b] <= R ids used per row, NULL = R).
  * err[b]: RMI_ERR_INDEX for an id outside [0, V), RMI_ERR_UNSUP when the text exceeds
- * `stride` bytes (truncated).  stride % 4 == 0, stride <= 16384.                         */
+ * `stride` bytes (truncated).  vocab_bytes holds n_bytes bytes (4-byte aligned); stride % 4
+ * == 0, stride <= 16384.                                                                    */
 int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const int64_t* vocab_off,
-                   const uint8_t* vocab_bytes, int64_t V, const uint8_t* skip, uint8_t* out, int32_t stride,
-                   int32_t* out_len, uint8_t* err, rmi_stream_t stream);
+                   const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, const uint8_t* skip, uint8_t* out,
+                   int32_t stride, int32_t* out_len, uint8_t* err, rmi_stream_t stream);
 
 /* Parse configuration (agent_proxy.* and the env's action_lookup).  Strings are packed
  * little-endian into two u64 words (byte k of the string = byte k of lo|hi).             */

@@ -113,8 +113,8 @@ _SIGS = {
     "rmi_masked_whiten": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
     "rmi_grpo_outcome": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_double, c_int32,
                                    c_void_p, c_void_p, c_void_p]),
-    "rmi_detokenize": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
-                                 c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "rmi_detokenize": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                 c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "rmi_parse_actions": (c_int32, [_P(ParseCfg), c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -599,10 +599,16 @@ __device__ int utf8_lossy(const uint8_t* src, int n, uint8_t* dst, int cap, bool
   return o;
 }
 
+// Ids are processed 256 per step (4 per lane): their loads, then the (offset, end, skip)
+// gathers of all of them, then the byte gathers, each stage issued together so a step costs
+// three memory round trips however long its tokens are.  Token bytes come as the aligned
+// dwords covering them (tokens <= 9 bytes: 3 dwords; longer ones loop), clamped inside the
+// vocabulary blob.
+constexpr int kDetokG = 4;  // 64-id chunks per step
 __global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ ids, int64_t R,
                                                    const int32_t* __restrict__ n_ids,
                                                    const int64_t* __restrict__ voff,
-                                                   const uint8_t* __restrict__ vbytes, int64_t V,
+                                                   const uint8_t* __restrict__ vbytes, int64_t n_bytes, int64_t V,
                                                    const uint8_t* __restrict__ skip, uint8_t* __restrict__ out,
                                                    int stride, int32_t* __restrict__ out_len,
                                                    uint8_t* __restrict__ err_out) {
@@ -615,32 +621,60 @@ __global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ i
   int64_t rn = n_ids ? (int64_t)n_ids[b] : R;
   rn = rn < 0 ? 0 : (rn > R ? R : rn);
   const int64_t* row = ids + b * R;
+  const uint32_t* v4 = reinterpret_cast<const uint32_t*>(vbytes);
+  const int64_t last4 = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;  // last dword of the blob
   int pos = 0;
   bool bad = false, over = false;
   uint32_t high = 0;
-  for (int64_t c0 = 0; c0 < rn; c0 += 64) {
-    const int64_t i = c0 + lane;
-    const int64_t id = i < rn ? row[i] : -1;
-    const bool in = i < rn;
-    const bool valid = id >= 0 && id < V;
-    bad |= in && !valid;
-    int64_t off = 0;
-    int len = 0;
-    if (valid && !skip[id]) {
-      off = voff[id];
-      len = (int)(voff[id + 1] - off);
+  for (int64_t c0 = 0; c0 < rn; c0 += 64 * kDetokG) {
+    int64_t id[kDetokG], off[kDetokG], end[kDetokG];
+    uint8_t sk[kDetokG];
+#pragma unroll
+    for (int g = 0; g < kDetokG; ++g) {
+      const int64_t i = c0 + 64 * g + lane;
+      id[g] = i < rn ? row[i] : -1;
     }
-    const int incl = wave_inclusive_scan(len);
-    const int start = pos + incl - len;
-    pos += __builtin_amdgcn_readlane(incl, 63);
-    for (int k = 0; k < len; ++k) {
-      const int p = start + k;
-      if (p < stride) {
-        const uint8_t c = vbytes[off + k];
-        buf[p] = c;
-        high |= c;
-      } else {
-        over = true;
+#pragma unroll
+    for (int g = 0; g < kDetokG; ++g) {
+      const bool in = c0 + 64 * g + lane < rn;
+      const bool valid = id[g] >= 0 && id[g] < V;
+      bad |= in && !valid;
+      const int64_t k = valid ? id[g] : 0;  // clamped, branch-free gathers
+      off[g] = voff[k];
+      end[g] = voff[k + 1];
+      sk[g] = valid ? skip[k] : (uint8_t)1;
+    }
+    int len[kDetokG], start[kDetokG];
+#pragma unroll
+    for (int g = 0; g < kDetokG; ++g) {
+      len[g] = sk[g] ? 0 : (int)(end[g] - off[g]);
+      const int incl = wave_inclusive_scan(len[g]);
+      start[g] = pos + incl - len[g];
+      pos += __builtin_amdgcn_readlane(incl, 63);
+    }
+    uint32_t w[kDetokG][3];
+#pragma unroll
+    for (int g = 0; g < kDetokG; ++g) {
+      const int64_t q = off[g] >> 2;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) w[g][k] = v4[q + k <= last4 ? q + k : last4];
+    }
+#pragma unroll
+    for (int g = 0; g < kDetokG; ++g) {
+      const int r = (int)(off[g] & 3);
+      const uint64_t lo = (uint64_t)w[g][0] | ((uint64_t)w[g][1] << 32);
+      for (int k = 0; k < len[g]; ++k) {
+        const int p = start[g] + k;
+        const int o = k + r;
+        const uint32_t c = o < 8 ? (uint32_t)(lo >> (8 * o)) & 0xFFu
+                         : o < 12 ? (w[g][2] >> (8 * (o - 8))) & 0xFFu
+                                  : vbytes[off[g] + k];  // tokens longer than 9 bytes
+        if (p < stride) {
+          buf[p] = (uint8_t)c;
+          high |= c;
+        } else {
+          over = true;
+        }
       }
     }
   }
@@ -675,17 +709,17 @@ __global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ i
 }  // namespace rmi
 
 RMI_API int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const int64_t* vocab_off,
-                           const uint8_t* vocab_bytes, int64_t V, const uint8_t* skip, uint8_t* out, int32_t stride,
-                           int32_t* out_len, uint8_t* err, rmi_stream_t stream) {
+                           const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, const uint8_t* skip, uint8_t* out,
+                           int32_t stride, int32_t* out_len, uint8_t* err, rmi_stream_t stream) {
   using namespace rmi;
   if (B < 0 || R < 0 || V < 0 || stride <= 0) return RMI_EINVAL;
   if (stride % 4 != 0 || stride > kMaxStride || B > 0x7FFFFFFF) return RMI_EUNSUP;
   if (B == 0) return RMI_OK;
-  if (!out || !out_len || !vocab_off || !skip || (R > 0 && !ids) || (V > 0 && !vocab_bytes)) return RMI_EINVAL;
-  if (reinterpret_cast<uintptr_t>(out) & 3u) return RMI_EUNSUP;
+  if (!out || !out_len || !vocab_off || !skip || (R > 0 && !ids) || !vocab_bytes || n_bytes < 0) return RMI_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(vocab_bytes)) & 3u) return RMI_EUNSUP;
   const size_t shm = 2 * ((size_t)stride + 4);
   hipLaunchKernelGGL(detok_kernel, dim3((unsigned)B), dim3(64), shm, as_stream(stream), ids, R, n_ids, vocab_off,
-                     vocab_bytes, V, skip, out, (int)stride, out_len, err);
+                     vocab_bytes, n_bytes, V, skip, out, (int)stride, out_len, err);
   return launch_status();
 }
 

@@ -447,7 +447,8 @@ class VocabTable:
         lens = np.array([len(b) for b in table], np.int64)
         off = np.zeros(len(table) + 1, np.int64)
         np.cumsum(lens, out=off[1:])
-        data = np.frombuffer(b"".join(table) or b"\0", np.uint8).copy()
+        blob = b"".join(table)
+        data = np.frombuffer(blob + b"\0" * (4 + (-len(blob)) % 4), np.uint8).copy()  # whole dwords
         return VocabTable(torch.from_numpy(off).to(device), torch.from_numpy(data).to(device),
                           torch.from_numpy(np.asarray(skip, np.uint8)).to(device))
 
@@ -509,8 +510,9 @@ def detokenize(ids: torch.Tensor, vocab: VocabTable, stride: int, n_ids: Optiona
     n = torch.empty(B, dtype=torch.int32, device=dev)
     err = torch.zeros(B, dtype=torch.uint8, device=dev)
     V = vocab.skip.numel()
-    check(lib().rmi_detokenize(_ptr(ids), B, R, _ptr(n_ids), _ptr(vocab.off), _ptr(vocab.data), V, _ptr(vocab.skip),
-                               _ptr(out), stride, _ptr(n), _ptr(err), _stream()), "rmi_detokenize")
+    check(lib().rmi_detokenize(_ptr(ids), B, R, _ptr(n_ids), _ptr(vocab.off), _ptr(vocab.data), vocab.data.numel(),
+                               V, _ptr(vocab.skip), _ptr(out), stride, _ptr(n), _ptr(err), _stream()),
+          "rmi_detokenize")
     return out, n, err
 
 
