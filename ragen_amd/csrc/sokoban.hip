@@ -669,7 +669,8 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
   const int8_t* pl = kFirst ? init_player : env.player;
   int r = pl[2 * bc], c = pl[2 * bc + 1];
-  const uint8_t has_in = in.has_input ? in.has_input[bc] : (uint8_t)0;
+  // branch-free: a conditional load here would make the compiler wait for the rows first
+  const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
   uint8_t flags = 0;
   int nes = 0, bot = 0;
   int32_t num_actions = 0, n_turns = 0;

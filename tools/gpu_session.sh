@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: gpu tests -> smoke -> bench -> rocprofv3 kernel-trace stats.
 # Every GPU step has its own time limit; a fault / abort / timeout ends the session.
-# usage: bash tools/gpu_session.sh <tag> [steps...]   (steps: tests smoke bench prof pmc)
+# usage: bash tools/gpu_session.sh <tag> [steps...]   (steps: tests smoke bench prof prof_all pmc)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -33,10 +33,14 @@ for s in $STEPS; do
     bench)
       timeout -k 10 600 python bench.py > "$OUT/bench.log" 2>&1
       ok_or_stop $? bench; tail -2 "$OUT/bench.log";;
-    prof)
+    prof)  # the headline path only: its kernel averages are the bench line's
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench --output-format csv \
-        -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > "$OUT/prof.log" 2>&1
+        -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-extras > "$OUT/prof.log" 2>&1
       ok_or_stop $? prof; tail -2 "$OUT/prof.log";;
+    prof_all)  # every leg (advantage, toy-text, text API, at-scale) for the extras' kernels
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_all" -o bench --output-format csv \
+        -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > "$OUT/prof_all.log" 2>&1
+      ok_or_stop $? prof_all; tail -2 "$OUT/prof_all.log";;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc_$c" -o pmc --output-format csv \
