@@ -272,11 +272,13 @@ def toytext_legs(device):
     turns = [ops.turn_struct(t, ids[t], n[t], None, 10, -0.1) for t in range(T)]
     st = fl.struct()
 
-    def fl_step():  # the first turn fused with the restore of the reset state
+    fl_fin = ops.finalize_struct(GROUP, "mean_std", norm)
+
+    def fl_step():  # the first turn fused with the restore of the reset state, the last with the finalize
         ops.frozenlake_step_turn_first(st, fl.ep, turns[0], fl.init_desc, fl.init_s, fl.init_rng)
-        for t in range(1, T):
+        for t in range(1, T - 1):
             ops.frozenlake_step_turn(st, fl.ep, turns[t])
-        ops.rollout_finalize(fl.ep, seg, "mean_std", norm)
+        ops.frozenlake_step_turn_finalize(st, fl.ep, turns[T - 1], fl_fin)
     fl_step()
     torch.cuda.synchronize()
     steps = int(fl.ep.turn_exec.sum().item())

@@ -526,103 +526,6 @@ constexpr int64_t kSpreadMaxEnvs = RMI_SPREAD_MAX_ENVS;  // RMI_SPREAD_LPE lanes
 constexpr int kSpreadLpe = RMI_SPREAD_LPE;
 __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMaxEnvs; }
 
-// ------------------------------------------------------- fused end of rollout (kFin)
-// The rollout's last turn launch also does rmi_rollout_finalize's work (episode.hip): per env
-// get_rollout_states metrics (es_manager.py:173-207), the trajectory score sum(turn rewards)
-// + penalty, and _normalize_score_tensor (ctx_manager.py:175-226) over uniform contiguous
-// groups of fin.group_size envs, which the launcher only accepts when every group lies in one
-// wave.  The episode record of the first 8 turns is loaded with the turn's other loads (no
-// extra round trip); the group sums are the same xor butterflies as finalize_kernel's
-// wave_sum restricted to the group's lanes (the lanes outside a group only ever add exact
-// zeros there), so every output is bit-identical to the separate launch.
-constexpr int kFinT = 8;  // turns of the record loaded up front
-struct FinRecord {
-  double r[kFinT];
-  uint8_t info[kFinT];
-  __device__ __forceinline__ void load(const rmi_episode_t& ep, int64_t bc) {
-    const int64_t B = ep.B;
-#pragma unroll
-    for (int k = 0; k < kFinT; ++k) {
-      const int64_t t = k < ep.T ? k : ep.T - 1;  // clamped, always valid
-      r[k] = ep.turn_reward[t * B + bc];
-      info[k] = ep.turn_info[t * B + bc];
-    }
-  }
-  __device__ __forceinline__ void set(int turn, double acc, uint8_t inf) {
-#pragma unroll
-    for (int k = 0; k < kFinT; ++k)
-      if (k == turn) {
-        r[k] = acc;
-        info[k] = inf;
-      }
-  }
-};
-
-template <int LPE>
-__device__ __forceinline__ double group_sum(double x, int gs) {  // xor butterfly over gs envs
-  for (int o = gs >> 1; o >= 1; o >>= 1) x += __shfl_xor(x, o * LPE, 64);
-  return x;
-}
-
-template <int LPE>
-__device__ __forceinline__ void finalize_envs(const rmi_episode_t& ep, const rmi_finalize_t& fin, const FinRecord& rec,
-                                              int64_t b, bool writer, uint8_t flags, int32_t n_turns,
-                                              int32_t num_actions, double penalty, int acted_turn, double acc,
-                                              uint8_t acc_info) {
-  const int64_t B = ep.B;
-  double score = 0.0;  // python sum over the turns, in turn order
-  int eff = 0, val = 0, present = 0;
-#pragma unroll
-  for (int k = 0; k < kFinT; ++k)
-    if (k < ep.T) {
-      score += rec.r[k];
-      present |= rec.info[k] & RMI_INFO_PRESENT;
-      eff += (rec.info[k] >> 1) & 1;
-      val += (rec.info[k] >> 2) & 1;
-    }
-  for (int t = kFinT; t < ep.T; ++t) {  // long episodes only
-    const int64_t bc = b < B ? b : B - 1;
-    const bool mine = t == acted_turn;  // written by this launch: use the registers
-    const uint8_t inf = mine ? acc_info : ep.turn_info[t * B + bc];
-    score += mine ? acc : ep.turn_reward[t * B + bc];
-    present |= inf & RMI_INFO_PRESENT;
-    eff += (inf >> 1) & 1;
-    val += (inf >> 2) & 1;
-  }
-  const float scf = (float)score, pf = (float)penalty, x = scf + pf;
-  if (writer) {
-    if (fin.score) fin.score[b] = scf;
-    if (fin.pen) fin.pen[b] = pf;
-    if (fin.metrics) {
-      const double nt = (double)n_turns;
-      double* m = fin.metrics + 4 * b;
-      m[0] = ((flags & RMI_FLAG_TERMINATED) && !(flags & RMI_FLAG_TRUNCATED)) ? 1.0 : 0.0;
-      m[1] = (double)num_actions;
-      m[2] = present ? (double)eff / nt : __builtin_nan("");
-      m[3] = present ? (double)val / nt : __builtin_nan("");
-    }
-  }
-  if (!fin.norm) return;
-  const int gs = fin.group_size, method = fin.method;  // uniform; all lanes reach the shuffles
-  const double md = group_sum<LPE>(0.0 + (double)x, gs) / (double)gs;
-  const float mean = (float)md;
-  float sd = 0.0f;
-  if (method == RMI_NORM_MEAN_STD || method == RMI_NORM_ASYM_CLIP) {
-    const double d = (double)x - md;
-    const double q = group_sum<LPE>(0.0 + d * d, gs);
-    sd = gs > 1 ? (float)sqrt(q / (double)(gs - 1)) : __builtin_nanf("");
-  }
-  const bool use = sd > 1e-6f;
-  float y;
-  if (method == RMI_NORM_IDENTITY) y = x;
-  else if (method == RMI_NORM_MEAN) y = x - mean;
-  else {
-    y = use ? (x - mean) / (sd + 1e-6f) : 0.0f;
-    if (method == RMI_NORM_ASYM_CLIP) y = fminf(fmaxf(y, -1.0f), 3.0f);
-  }
-  if (writer) fin.norm[b] = y;
-}
-
 // One launch = one turn of every env.  LPE consecutive lanes own one env (LPE = 1 for big
 // batches; 4 when the batch is too small to fill the chip, so the per-wave instruction
 // chain — decode, row rebuild, loads, stores — is split LPE ways; the steps themselves run

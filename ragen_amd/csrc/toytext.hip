@@ -68,31 +68,38 @@ struct FrozenLakeDev {
 // kFirst: a fresh episode's first turn fused with its reset (rmi_frozenlake_reset): desc, s and
 // the PCG64 state come from the init arrays, the counters and the record start at zero without
 // being read, and the env's reset state and whole record are written before the turn runs.
-template <bool kFirst>
+// kFin: the launch is the rollout's last turn and also runs rmi_rollout_finalize for uniform
+// contiguous groups of fin.group_size envs (each group inside the launch's one wave): every
+// lane, live or not, reaches the group shuffles of finalize_envs.
+template <bool kFirst, bool kFin>
 __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
                                                                          rmi_turn_t in, uint8_t* __restrict__ err_out,
                                                                          const uint8_t* __restrict__ init_desc,
                                                                          const int32_t* __restrict__ init_s,
-                                                                         const uint64_t* __restrict__ init_rng) {
+                                                                         const uint64_t* __restrict__ init_rng,
+                                                                         rmi_finalize_t fin) {
   const int64_t b = (int64_t)blockIdx.x * kToyBlock + threadIdx.x;
   const int B = ep.B;
-  if (b >= B) return;
+  if (!kFin && b >= B) return;
+  const bool live = b < B;
+  const int64_t bc = live ? b : (int64_t)B - 1;  // clamped: every load below is valid
   // every load of the turn is issued before the first use (one memory round trip)
   uint8_t flags = 0;
   int32_t num_actions = 0, n_turns = 0;
   double penalty = 0.0;
   if (!kFirst) {  // a fresh episode's record is all zero (EnvStatus(), es_manager.py:95)
-    flags = ep.flags[b];
-    num_actions = ep.num_actions[b];
-    n_turns = ep.n_turns[b];
-    penalty = ep.penalty[b];
+    flags = ep.flags[bc];
+    num_actions = ep.num_actions[bc];
+    n_turns = ep.n_turns[bc];
+    penalty = ep.penalty[bc];
   }
-  const uint8_t has_in = in.has_input ? in.has_input[b] : 0;
-  const int n_act = in.n_actions[b];
-  const uint64_t acts = load_actions(in.actions + b * (int64_t)in.K, in.K);
+  // branch-free: a conditional load would make the compiler wait for the earlier loads
+  const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
+  const int n_act = in.n_actions[bc];
+  const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K);
   const int n = env.nrow * env.ncol;
   FrozenLakeDev e;
-  e.desc = (kFirst ? init_desc : env.desc) + b * n;
+  e.desc = (kFirst ? init_desc : env.desc) + bc * n;
   e.in_regs = n <= 16;
   e.d_lo = e.d_hi = 0;
   if (n == 16 && (reinterpret_cast<uintptr_t>(kFirst ? init_desc : env.desc) & 15u) == 0) {  // 4x4: one 16-B load
@@ -108,13 +115,15 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
   }
   e.nrow = env.nrow;
   e.ncol = env.ncol;
-  e.s = kFirst ? init_s[b] : env.s[b];
+  e.s = kFirst ? init_s[bc] : env.s[bc];
   e.slippery = env.is_slippery != 0;
   e.cs0 = env.cs0;
   e.cs1 = env.cs1;
   e.cs2 = env.cs2;
-  e.rng = load_pcg(kFirst ? init_rng : env.rng, B, b);
-  if (kFirst) {  // the reset, then the turn (same thread, later stores win)
+  e.rng = load_pcg(kFirst ? init_rng : env.rng, B, bc);
+  FinRecord rec;
+  if (kFin) rec.load(ep, bc);
+  if (kFirst && live) {  // the reset, then the turn (same thread, later stores win)
     uint8_t* desc = const_cast<uint8_t*>(env.desc) + b * n;
     if (n == 16 && ((reinterpret_cast<uintptr_t>(env.desc) & 15u) == 0)) {
       *reinterpret_cast<uint4*>(desc) = make_uint4((uint32_t)e.d_lo, (uint32_t)(e.d_lo >> 32), (uint32_t)e.d_hi,
@@ -135,28 +144,41 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
       ep.turn_exec[(int64_t)t * B + b] = 0;
     }
   }
-  const bool act = in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE);
-  if (!act) return;
-  uint8_t err = 0;
-  if (e.s < 0 || e.s >= n) {
-    if (err_out) err_out[b] |= RMI_ERR_STATE;
-    return;
+  const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
+  TurnOut o;
+  o.acc = 0.0;
+  o.info = 0;
+  o.exec = 0;
+  o.stepped_any_state = false;
+  bool stepped = false;
+  if (act) {
+    if (e.s < 0 || e.s >= n) {
+      if (err_out) err_out[b] |= RMI_ERR_STATE;
+    } else {
+      uint8_t err = 0;
+      o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
+                   in.format_penalty, err);
+      stepped = true;
+      ep.num_actions[b] = num_actions;
+      ep.flags[b] = flags;
+      ep.n_turns[b] = n_turns;
+      ep.penalty[b] = penalty;
+      const int64_t tb = (int64_t)in.turn * B + b;
+      ep.turn_reward[tb] = o.acc;
+      ep.turn_info[tb] = o.info;
+      ep.turn_exec[tb] = o.exec;
+      if (o.stepped_any_state) {
+        env.s[b] = e.s;
+        store_pcg(env.rng, B, b, e.rng);
+      }
+      if (err_out && err) err_out[b] |= err;
+    }
   }
-  TurnOut o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
-                       in.format_penalty, err);
-  ep.num_actions[b] = num_actions;
-  ep.flags[b] = flags;
-  ep.n_turns[b] = n_turns;
-  ep.penalty[b] = penalty;
-  const int64_t tb = (int64_t)in.turn * B + b;
-  ep.turn_reward[tb] = o.acc;
-  ep.turn_info[tb] = o.info;
-  ep.turn_exec[tb] = o.exec;
-  if (o.stepped_any_state) {
-    env.s[b] = e.s;
-    store_pcg(env.rng, B, b, e.rng);
+  if (kFin) {
+    if (stepped) rec.set(in.turn, o.acc, o.info);  // this turn's record is still in registers
+    finalize_envs<1>(ep, fin, rec, b, live, flags, n_turns, num_actions, penalty, stepped ? in.turn : -1, o.acc,
+                     o.info);
   }
-  if (err_out && err) err_out[b] |= err;
 }
 
 struct BanditDev {
@@ -267,8 +289,8 @@ RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_epis
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
   const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
-  hipLaunchKernelGGL(frozenlake_step_turn_kernel<false>, dim3(grid), dim3(kToyBlock), 0, as_stream(stream), *env,
-                     *ep, *in, err, nullptr, nullptr, nullptr);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, false>), dim3(grid), dim3(kToyBlock), 0, as_stream(stream),
+                     *env, *ep, *in, err, nullptr, nullptr, nullptr, rmi_finalize_t{});
   return launch_status();
 }
 
@@ -282,8 +304,29 @@ RMI_API int rmi_frozenlake_step_turn_first(const rmi_frozenlake_t* env, const rm
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->desc || !env->s || !env->rng || !init_desc || !init_s || !init_rng) return RMI_EINVAL;
   const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
-  hipLaunchKernelGGL(frozenlake_step_turn_kernel<true>, dim3(grid), dim3(kToyBlock), 0, as_stream(stream), *env, *ep,
-                     *in, err, init_desc, init_s, init_rng);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<true, false>), dim3(grid), dim3(kToyBlock), 0, as_stream(stream),
+                     *env, *ep, *in, err, init_desc, init_s, init_rng, rmi_finalize_t{});
+  return launch_status();
+}
+
+RMI_API int rmi_frozenlake_step_turn_finalize(const rmi_frozenlake_t* env, const rmi_episode_t* ep,
+                                              const rmi_turn_t* in, uint8_t* err, const rmi_finalize_t* fin,
+                                              rmi_stream_t stream) {
+  using namespace rmi;
+  if (!env || !fin) return RMI_EINVAL;
+  if (env->nrow <= 0 || env->ncol <= 0 || env->nrow * env->ncol > 64) return RMI_EUNSUP;
+  const int rc = check_turn_args(ep, in);
+  if (rc < 0) return rc;
+  if (ep->B == 0) return RMI_OK;
+  if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
+  if (fin->method < 0 || fin->method > 3 || fin->group_size < 1) return RMI_EINVAL;
+  // every group inside the one-wave workgroup, and no partial group
+  if (kToyBlock % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;
+  rmi_finalize_t f = *fin;
+  if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member
+  const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, true>), dim3(grid), dim3(kToyBlock), 0, as_stream(stream),
+                     *env, *ep, *in, err, nullptr, nullptr, nullptr, f);
   return launch_status();
 }
 

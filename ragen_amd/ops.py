@@ -187,6 +187,21 @@ def frozenlake_reset(env: _lib.FrozenLake, ep: EpisodeState, init_desc: torch.Te
           "rmi_frozenlake_reset")
 
 
+def frozenlake_step_turn_finalize(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn, fin: _lib.Finalize,
+                                  err: Optional[torch.Tensor] = None):
+    """frozenlake_step_turn + rollout_finalize (uniform contiguous groups) in one launch.  Groups
+    that would straddle the one-wave workgroup take the two launches instead (same results)."""
+    _dev(err)
+    rc = lib().rmi_frozenlake_step_turn_finalize(env, ep.struct(), turn, _ptr(err), fin, _stream())
+    if rc == _lib.RMI_EUNSUP and fin.group_size >= 1 and ep.B % fin.group_size == 0:
+        frozenlake_step_turn(env, ep, turn, err)
+        seg = torch.arange(0, ep.B + 1, fin.group_size, dtype=torch.int32, device=ep.flags.device)
+        check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, fin.method, fin.metrics,
+                                         fin.score, fin.pen, fin.norm, _stream()), "rmi_rollout_finalize")
+        return
+    check(rc, "rmi_frozenlake_step_turn_finalize")
+
+
 def frozenlake_step_turn_first(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn, init_desc: torch.Tensor,
                                init_s: torch.Tensor, init_rng: torch.Tensor, err: Optional[torch.Tensor] = None):
     """frozenlake_reset(init_*) + frozenlake_step_turn(turn) in one launch (a fresh episode's first turn)."""

@@ -657,3 +657,39 @@ def test_frozenlake_fused_first_turn(device, B, partial):
         outs.append((fl.desc.clone(), fl.s.clone(), fl.rng.clone(), fl.ep.arena.clone(), err))
     for name, a, b in zip(("desc", "s", "rng", "episode", "err"), *outs):
         assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("B,T", [(4096, 8), (1024, 5)])
+def test_frozenlake_fused_last_turn_finalize(device, B, T):
+    """rmi_frozenlake_step_turn_finalize == rmi_frozenlake_step_turn + rmi_rollout_finalize, bit for
+    bit (groups inside the wave, and the two-launch fallback for groups of 128)."""
+    K = 5
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=31)
+    ids, n = _t(ids, device), _t(n, device)
+    for gs in (16, 4, 64, 128):
+        for method in ("identity", "mean", "mean_std", "asym_clip"):
+            outs = []
+            for fused in (False, True):
+                fl = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
+                fl.reset(synthetic.env_seeds(B))
+                st = fl.struct()
+                norm = torch.full((B,), 7.0, dtype=torch.float32, device=device)
+                met = torch.full((B, 4), 7.0, dtype=torch.float64, device=device)
+                sc = torch.full((B,), 7.0, dtype=torch.float32, device=device)
+                pe = torch.full((B,), 7.0, dtype=torch.float32, device=device)
+                last = T - 2
+                for t in range(last + 1):
+                    turn = ops.turn_struct(t, ids[t], n[t], None, 10, -0.1)
+                    if fused and t == last:
+                        ops.frozenlake_step_turn_finalize(st, fl.ep, turn,
+                                                          ops.finalize_struct(gs, method, norm, met, sc, pe))
+                    else:
+                        ops.frozenlake_step_turn(st, fl.ep, turn)
+                if not fused:
+                    seg = torch.arange(0, B + 1, gs, dtype=torch.int32, device=device)
+                    ops.rollout_finalize(fl.ep, seg, method, norm, met, sc, pe)
+                torch.cuda.synchronize()
+                outs.append((fl.s.clone(), fl.rng.clone(), fl.ep.arena.clone(), norm, torch.nan_to_num(met, 9.0),
+                             sc, pe))
+            for a, b in zip(*outs):
+                assert torch.equal(a, b), (gs, method)
