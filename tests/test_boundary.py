@@ -48,3 +48,34 @@ def test_ops_refuse_cpu_tensors():
     from ragen_amd import ops
     with pytest.raises(ValueError):
         ops.row_sum(torch.zeros(2, 3))
+
+
+STRUCTS = {  # ctypes mirror in ragen_amd/_lib.py -> C type in include/ragen_amd.h
+    "Episode": "rmi_episode_t", "Turn": "rmi_turn_t", "Sokoban": "rmi_sokoban_t", "Finalize": "rmi_finalize_t",
+    "FrozenLake": "rmi_frozenlake_t", "Bandit": "rmi_bandit_t", "Countdown": "rmi_countdown_t",
+    "ParseCfg": "rmi_parse_cfg_t",
+}
+
+
+def test_ctypes_structs_match_the_c_layout(tmp_path):
+    """Every ctypes Structure the binding passes by pointer has the C struct's size and field
+    offsets (compiled from the header with gcc: the ABI the kernels read)."""
+    import ctypes
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "ragen_amd.h"', "int main(void) {"]
+    for py, c in STRUCTS.items():
+        cls = getattr(_lib, py)
+        lines.append(f'  printf("{py} size %zu\\n", sizeof({c}));')
+        for name, _ in cls._fields_:
+            lines.append(f'  printf("{py} {name} %zu\\n", offsetof({c}, {name}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    c_vals = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for py in STRUCTS:
+        cls = getattr(_lib, py)
+        assert c_vals[(py, "size")] == ctypes.sizeof(cls), py
+        for name, _ in cls._fields_:
+            assert c_vals[(py, name)] == getattr(cls, name).offset, (py, name)
