@@ -377,6 +377,21 @@ __global__ __launch_bounds__(64) void gae_legacy_kernel(const float* __restrict_
 // Every f32 operation is the reference's, in its order (-ffp-contract=off).
 constexpr int kBStr = kGCols + 4;  // LDS row stride (floats / bytes)
 
+// Diagnostic build only (tools/prof_bilevel_stamps.py compiles with RMI_BL_STAMPS): per-wave
+// s_memtime sums of the tile phases (P1 incl. the tile's load wait | P2+P3 walk | P4).
+#ifdef RMI_BL_STAMPS
+__device__ unsigned long long* g_bl_stamps;
+#define BL_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
+#define BL_ACC(i, d) (bl_acc[i] += (d))
+#else
+#define BL_T(x) \
+  do {          \
+  } while (0)
+#define BL_ACC(i, d) \
+  do {               \
+  } while (0)
+#endif
+
 struct BilevelCarry {  // per row, replicated on the row's 16 lanes
   float v_valid, v_eos;  // value at the leftmost valid / eos position right of this tile
   uint32_t h_valid, h_eos;
@@ -408,7 +423,12 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
                                              double& s1, double& s2, double& cnt, uint32_t& bad, float* sv, float* sd,
                                              float* sh, float* su, uint32_t* sf, int lane, int64_t row0, int64_t B,
                                              int64_t L, float g, float gl, float hg, float hgl,
-                                             float* __restrict__ adv, float* __restrict__ ret) {
+                                             float* __restrict__ adv, float* __restrict__ ret
+#ifdef RMI_BL_STAMPS
+                                             , unsigned long long* bl_acc
+#endif
+) {
+  BL_T(t0);
   const int grp = lane & 15, rho = lane >> 4;
   const F4 r4 = cur.r[0], v4 = cur.v[0];
   const uint32_t m4 = cur.m[0];
@@ -468,6 +488,8 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
   sf[rho * (kBStr / 4) + grp] = fl;
   const uint64_t any_eos = __ballot(he), any_valid = __ballot(hv);
   __syncthreads();
+  BL_T(t1);
+  BL_ACC(0, t1 - t0);
   // ---- P2 / P3: the row walkers (group-0 lanes)
   if (grp == 0) {
     const float* pv = sv + rho * kBStr;
@@ -510,6 +532,8 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
     }
   }
   __syncthreads();
+  BL_T(t2);
+  BL_ACC(1, t2 - t1);
   // ---- P4: outputs and row stats
   const F4 a4 = *reinterpret_cast<const F4*>(sd + o);
   const F4 h4 = *reinterpret_cast<const F4*>(sh + o);
@@ -547,8 +571,15 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
     }
   }
   __syncthreads();
+  BL_T(t3);
+  BL_ACC(2, t3 - t2);
 }
 
+#ifdef RMI_BL_STAMPS
+#define BL_ARG , bl_acc
+#else
+#define BL_ARG
+#endif
 __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                            const uint8_t* __restrict__ mask, int64_t B, int64_t L,
                                                            float g, float gl, float hg, float hgl,
@@ -569,22 +600,35 @@ __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restri
   double s1 = 0.0, s2 = 0.0, cnt = 0.0;
   uint32_t bad = 0;
   GaeTile ta, tb, tc;
+#ifdef RMI_BL_STAMPS
+  unsigned long long bl_acc[3] = {0, 0, 0};
+  BL_T(tbeg);
+#endif
   const int64_t k0 = ntiles - 1;
   gae_load_tile(ta, r, v, mask, B, L, row0, k0 * kGCols, lane);
   gae_load_tile(tb, r, v, mask, B, L, row0, (k0 - 1) * kGCols, lane);
   for (int64_t k = k0; k >= 0; k -= 3) {
     gae_load_tile(tc, r, v, mask, B, L, row0, (k - 2) * kGCols, lane);
     bilevel_tile(ta, k * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg, hgl,
-                 adv, ret);
+                 adv, ret BL_ARG);
     if (k - 1 < 0) break;
     gae_load_tile(ta, r, v, mask, B, L, row0, (k - 3) * kGCols, lane);
     bilevel_tile(tb, (k - 1) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
-                 hgl, adv, ret);
+                 hgl, adv, ret BL_ARG);
     if (k - 2 < 0) break;
     gae_load_tile(tb, r, v, mask, B, L, row0, (k - 4) * kGCols, lane);
     bilevel_tile(tc, (k - 2) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
-                 hgl, adv, ret);
+                 hgl, adv, ret BL_ARG);
   }
+#ifdef RMI_BL_STAMPS
+  BL_T(tend);
+  if (lane == 0) {
+    g_bl_stamps[blockIdx.x * 4 + 0] = bl_acc[0];
+    g_bl_stamps[blockIdx.x * 4 + 1] = bl_acc[1];
+    g_bl_stamps[blockIdx.x * 4 + 2] = bl_acc[2];
+    g_bl_stamps[blockIdx.x * 4 + 3] = tend - tbeg;
+  }
+#endif
   const double a = xor_sum16(s1), b2 = xor_sum16(s2), n = xor_sum16(cnt);
   const uint64_t bads = __ballot(bad);
   const int64_t row = row0 + (lane >> 4);
@@ -749,6 +793,12 @@ RMI_API int rmi_gae(const float* r, const float* v, const uint8_t* mask, int64_t
                        row_stats);
   return launch_status();
 }
+
+#ifdef RMI_BL_STAMPS
+RMI_API int rmi_bilevel_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_bl_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 RMI_API int rmi_bilevel_gae(const float* r, const float* v, const uint8_t* mask, int64_t B, int64_t L, double gamma,
                             double lam, double high_level_gamma, float* adv, float* ret, double* row_stats,
