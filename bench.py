@@ -254,7 +254,8 @@ def _graph_rollout(step, reps=50, warmup=5):
 def toytext_legs(device):
     """BASELINE configs[1] and [4] on this GPU (parity cases of the bench, reported as extras):
     FrozenLake 4x4 slippery, 4096 envs x 8 turns (K=5, cap 10), and Countdown 16384 envs x 4
-    turns (K=1, cap 1; half the turns carry no answer -> mixed episode lengths).  A rollout =
+    turns (K=1, cap 1; half the turns carry no answer -> mixed episode lengths).  Each also
+    reports its algorithmic bytes (SURVEY §8(d) per env-turn) over the whole rollout's time.  A rollout =
     T turn launches from the post-reset state (FrozenLake's first one fused with the device
     restore; Countdown's record zeroed), then the fused finalize."""
     from ragen_amd.env import CountdownBatch, FrozenLakeBatch
@@ -282,9 +283,12 @@ def toytext_legs(device):
     fl_step()
     torch.cuda.synchronize()
     steps = int(fl.ep.turn_exec.sum().item())
+    env_turns = int(fl.ep.n_turns.sum().item())
     ms = _graph_rollout(fl_step)
+    gbs = env_turns * 107 / (ms * 1e-3) / 1e9  # 107 B per FrozenLake env-turn
     out["frozenlake"] = {"config": f"FrozenLake 4x4 slippery, {B} envs x {T} turns, K={K}, cap 10",
-                         "env_steps_per_rollout": steps, "ms_per_rollout": ms, "env_steps_per_s": steps / ms * 1e3}
+                         "env_steps_per_rollout": steps, "ms_per_rollout": ms, "env_steps_per_s": steps / ms * 1e3,
+                         "env_turns_per_rollout": env_turns, "rollout_GBs": gbs, "rollout_frac": gbs / HBM_PEAK_GBS}
     # Countdown
     B, T, K = 16384, 4, 1
     inst = synthetic_instances(1024, 7)
@@ -311,9 +315,12 @@ def toytext_legs(device):
     cd_step()
     torch.cuda.synchronize()
     steps = int(cd.ep.turn_exec.sum().item())
+    env_turns = int(cd.ep.n_turns.sum().item())
     ms = _graph_rollout(cd_step)
+    gbs = env_turns * 159 / (ms * 1e-3) / 1e9  # 159 B per Countdown env-turn
     out["countdown"] = {"config": f"Countdown, {B} envs x {T} turns, K={K}, cap 1, 50% empty answers",
-                        "env_steps_per_rollout": steps, "ms_per_rollout": ms, "env_steps_per_s": steps / ms * 1e3}
+                        "env_steps_per_rollout": steps, "ms_per_rollout": ms, "env_steps_per_s": steps / ms * 1e3,
+                        "env_turns_per_rollout": env_turns, "rollout_GBs": gbs, "rollout_frac": gbs / HBM_PEAK_GBS}
     return out
 
 
