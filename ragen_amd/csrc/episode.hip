@@ -20,12 +20,6 @@ __device__ __forceinline__ double wave_sum(double x) {
   for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
   return x;
 }
-__device__ __forceinline__ float wave_max(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
-  return x;
-}
-
 struct EnvTotals {
   double score;
   int eff, val, present;

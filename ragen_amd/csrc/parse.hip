@@ -103,7 +103,7 @@ __device__ __forceinline__ void load16(const uint8_t* B, int s, uint64_t& lo, ui
   hi = r == 0 ? c : (c >> (8 * r)) | (e << (64 - 8 * r));
 }
 __device__ __forceinline__ bool tag_eq(uint64_t lo, uint64_t hi, const Tag& t) {
-  return ((lo & low_mask(t.n)) == t.lo) & ((hi & low_mask(t.n - 8)) == t.hi);
+  return ((lo & low_mask(t.n)) == t.lo) && ((hi & low_mask(t.n - 8)) == t.hi);
 }
 // which of the six tags starts at B[x] (a '<'); tags never run into a row's zero tail
 __device__ __forceinline__ int classify_tag(const uint8_t* B, int x) {
