@@ -331,14 +331,18 @@ def text_leg(R, device, reps=20):
       the outputs (K action ids, n_actions, 4 spans) per row;
     * detokenize: rmi_detokenize over [8192, 128] token ids of a Qwen-sized (151 646) synthetic
       byte-level vocabulary; bytes = 8 per id in + the decoded bytes out;
-    * text rollout: the SK rollout driven from text (restore + 5 x (parse + turn) + finalize in
-      a HIP graph) -> env-steps/s of the device-resident text API."""
+    * text rollout: the SK rollout driven from text (5 x (parse + turn), restore and finalize
+      fused, in a HIP graph) -> env-steps/s of the device-resident text API;
+    * token rollout: the whole per-turn loop between two LLM generations on the device: the
+      response token ids -> rmi_detokenize -> rmi_parse_actions -> the turn -> rmi_sokoban_render
+      (the next observation's text), 5 turns per rollout, in a HIP graph."""
     B = R.B
     lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
     ids_h, n_h = R.ids.cpu().numpy(), R.n.cpu().numpy()
-    bufs = []
+    bufs, all_texts = [], []
     for t in range(T_TURNS):
         texts = synthetic.responses_for_actions(ids_h[t], n_h[t], lk, seed=100 + t)
+        all_texts.append(texts)
         buf, lens = synthetic.encode_rows(texts)
         bufs.append((torch.from_numpy(buf).to(device), torch.from_numpy(lens).to(device)))
     cfg = ops.parse_config(True, K_ACTIONS, "||", lk)
@@ -400,6 +404,42 @@ def text_leg(R, device, reps=20):
     torch.cuda.synchronize()
     steps = int(R.env.ep.turn_exec.sum().item())
     ms = _graph_rollout(text_step)
+    # token rollout: ids -> text -> actions -> state -> observation, every turn on the device
+    table, skip = synthetic.byte_vocab()
+    tvocab = ops.VocabTable.from_bytes(table, skip, device)
+    tok = [torch.from_numpy(synthetic.tokenize_greedy(all_texts[t], table)).to(device) for t in range(T_TURNS)]
+    stride = max(b[0].shape[1] for b in bufs)
+    dec = [ops.detokenize(tok[t], tvocab, stride) for t in range(T_TURNS)]
+    torch.cuda.synchronize()
+    for t in range(T_TURNS):  # the decode reproduces the response texts byte for byte
+        assert torch.equal(dec[t][1], bufs[t][1])
+    obs = ops.sokoban_render(R.st, B, R.env.config.grid_lookup, device)
+
+    def token_step():
+        e = R.env
+        for t in range(T_TURNS):
+            o, ts = text_turns[t]
+            txt, tl, _ = ops.detokenize(tok[t], tvocab, stride, out=dec[t])
+            ops.parse_actions(cfg, txt, tl, with_spans=False, out=o)
+            if t == 0:
+                ops.sokoban_step_turn_first(R.st, e.ep, ts, e.init_state, e.init_player)
+            elif t < T_TURNS - 1:
+                ops.sokoban_step_turn(R.st, e.ep, ts)
+            else:
+                ops.sokoban_step_turn_finalize(R.st, e.ep, ts, R.fin)
+            ops.sokoban_render(R.st, B, e.config.grid_lookup, device, out=obs)
+    token_step()
+    torch.cuda.synchronize()
+    assert int(R.env.ep.turn_exec.sum().item()) == steps
+    ms_tok = _graph_rollout(token_step)
+    # render alone
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(reps):
+        ops.sokoban_render(R.st, B, R.env.config.grid_lookup, device, out=obs)
+    e[1].record()
+    torch.cuda.synchronize()
+    render_us = e[0].elapsed_time(e[1]) * 1e3 / reps
     return {"parse": {"kernel": "rmi_parse_actions", "rows": B, "text_bytes": text_bytes, "us": parse_us,
                       "achieved_GBs": pbytes / (parse_us * 1e-6) / 1e9,
                       "frac": pbytes / (parse_us * 1e-6) / 1e9 / HBM_PEAK_GBS},
@@ -408,7 +448,11 @@ def text_leg(R, device, reps=20):
                            "frac": dbytes / (detok_us * 1e-6) / 1e9 / HBM_PEAK_GBS},
             "text_rollout": {"config": "SK rollout from response text: 5 x (parse + turn), restore and finalize fused",
                              "env_steps_per_rollout": steps, "ms_per_rollout": ms,
-                             "env_steps_per_s": steps / ms * 1e3}}
+                             "env_steps_per_s": steps / ms * 1e3},
+            "token_rollout": {"config": "SK rollout from response token ids: 5 x (detokenize + parse + turn + render)",
+                              "env_steps_per_rollout": steps, "ms_per_rollout": ms_tok,
+                              "env_steps_per_s": steps / ms_tok * 1e3},
+            "render": {"kernel": "rmi_sokoban_render", "envs": B, "us": render_us}}
 
 
 def api_leg(device):

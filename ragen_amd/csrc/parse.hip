@@ -613,8 +613,8 @@ __global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ i
                                                    int stride, int32_t* __restrict__ out_len,
                                                    uint8_t* __restrict__ err_out) {
   extern __shared__ uint32_t lds_words[];
-  uint8_t* buf = reinterpret_cast<uint8_t*>(lds_words);  // raw concatenation [stride + 4]
-  uint8_t* fix = buf + stride + 4;                          // lossy-decoded row  [stride + 4]
+  uint8_t* buf = reinterpret_cast<uint8_t*>(lds_words) + 4;  // raw concatenation [stride + 8], 4 B in front
+  uint8_t* fix = buf + stride + 8;                             // lossy-decoded row  [stride + 4]
   __shared__ int sh_len, sh_over;
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
@@ -679,9 +679,63 @@ __global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ i
     }
   }
   int n = pos < stride ? pos : stride;
+  if (lane < 8) buf[n + lane] = 0;  // the validity windows read up to 8 bytes past the end
+  if (lane < 4) buf[lane - 4] = 0;  // ... and 4 before the start
   __syncthreads();
   const uint8_t* res = buf;
-  if (__ballot((high & 0x80u) != 0)) {  // some non-ASCII byte: validate (one lane)
+  // Non-ASCII bytes: a wave-parallel validity test first (UTF-8 validity is local: every lead
+  // byte needs its continuation bytes with the Table 3-7 ranges, every continuation byte a lead
+  // at most 3 bytes back whose sequence covers it).  Only an invalid row takes the serial
+  // replacement pass.
+  bool invalid = false;
+  if (__ballot((high & 0x80u) != 0)) {
+    for (int c0 = 0; c0 < n; c0 += 256) {
+      const int i0 = c0 + 4 * lane;
+      if (i0 >= n) continue;
+      const uint32_t* b4 = reinterpret_cast<const uint32_t*>(buf + i0 - 4);
+      const uint64_t lo = (uint64_t)b4[0] | ((uint64_t)b4[1] << 32);  // bytes [i0 - 4, i0 + 4)
+      const uint32_t hi = b4[2];                                       // bytes [i0 + 4, i0 + 8)
+      auto at = [&](int k) -> uint32_t {  // byte i0 + k, k in [-4, 8)
+        return k < 4 ? (uint32_t)(lo >> (8 * (k + 4))) & 0xFFu : (hi >> (8 * (k - 4))) & 0xFFu;
+      };
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = i0 + j;
+        if (p >= n) break;
+        const uint32_t c = at(j);
+        if (c < 0x80) continue;
+        if (c >= 0xC2 && c <= 0xF4) {  // lead: its continuation bytes, inside the row
+          const int need = c >= 0xF0 ? 3 : (c >= 0xE0 ? 2 : 1);
+          const uint32_t lo1 = c == 0xE0 ? 0xA0u : (c == 0xF0 ? 0x90u : 0x80u);
+          const uint32_t hi1 = c == 0xED ? 0x9Fu : (c == 0xF4 ? 0x8Fu : 0xBFu);
+          bool ok = p + need < n;
+#pragma unroll
+          for (int k = 1; k <= 3; ++k)
+            if (k <= need) {
+              const uint32_t d = at(j + k);
+              ok = ok && d >= (k == 1 ? lo1 : 0x80u) && d <= (k == 1 ? hi1 : 0xBFu);
+            }
+          invalid |= !ok;
+        } else if (c >= 0x80 && c <= 0xBF) {  // continuation: the nearest non-continuation byte back
+          int back = 0;
+          uint32_t lead = 0;
+#pragma unroll
+          for (int k = 1; k <= 3; ++k) {
+            const uint32_t d = p - k >= 0 ? at(j - k) : 0u;
+            if (back == 0 && (d < 0x80 || d > 0xBF)) {
+              back = k;
+              lead = d;
+            }
+          }
+          const int need = lead >= 0xF0 ? 3 : (lead >= 0xE0 ? 2 : (lead >= 0xC2 ? 1 : 0));
+          invalid |= back == 0 || lead < 0xC2 || lead > 0xF4 || back > need;
+        } else {
+          invalid = true;  // C0, C1, F5..FF never appear in UTF-8
+        }
+      }
+    }
+  }
+  if (__ballot(invalid)) {  // some invalid sequence: the lossy rewrite (one lane)
     if (lane == 0) {
       bool ov = false;
       sh_len = utf8_lossy(buf, n, fix, stride, ov);
@@ -717,7 +771,7 @@ RMI_API int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32
   if (B == 0) return RMI_OK;
   if (!out || !out_len || !vocab_off || !skip || (R > 0 && !ids) || !vocab_bytes || n_bytes < 0) return RMI_EINVAL;
   if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(vocab_bytes)) & 3u) return RMI_EUNSUP;
-  const size_t shm = 2 * ((size_t)stride + 4);
+  const size_t shm = 2 * ((size_t)stride + 4) + 16;
   hipLaunchKernelGGL(detok_kernel, dim3((unsigned)B), dim3(64), shm, as_stream(stream), ids, R, n_ids, vocab_off,
                      vocab_bytes, n_bytes, V, skip, out, (int)stride, out_len, err);
   return launch_status();

@@ -339,11 +339,14 @@ def glyph_table(lookup):
     return gb, gl
 
 
-def _render(fn, env_struct, B: int, cells: int, rows: int, lookup, device):
+def _render(fn, env_struct, B: int, cells: int, rows: int, lookup, device, out=None):
     gb, gl = glyph_table(lookup)
     stride = (cells * 4 + rows - 1 + 3) // 4 * 4
-    out = torch.empty(B, stride, dtype=torch.uint8, device=device)
-    n = torch.empty(B, dtype=torch.int32, device=device)
+    if out is not None:  # (rows, lengths) of a previous call: no allocation (graph-capturable)
+        out, n = out
+    else:
+        out = torch.empty(B, stride, dtype=torch.uint8, device=device)
+        n = torch.empty(B, dtype=torch.int32, device=device)
     check(fn(env_struct, B, gb.ctypes.data, gl.ctypes.data, _ptr(out), stride, _ptr(n), _stream()), fn.__name__)
     return out, n
 
@@ -355,14 +358,14 @@ def decode_rows(out: torch.Tensor, n: torch.Tensor):
     return [buf[i, :lens[i]].tobytes().decode("utf-8") for i in range(len(lens))]
 
 
-def sokoban_render(env: _lib.Sokoban, B: int, lookup, device):
+def sokoban_render(env: _lib.Sokoban, B: int, lookup, device, out=None):
     """SokobanEnv.render text of every env (sokoban/env.py:53-61) -> (u8[B,stride], i32[B])."""
-    return _render(lib().rmi_sokoban_render, env, B, env.H * env.W, env.H, lookup, device)
+    return _render(lib().rmi_sokoban_render, env, B, env.H * env.W, env.H, lookup, device, out)
 
 
-def frozenlake_render(env: _lib.FrozenLake, B: int, lookup, device):
+def frozenlake_render(env: _lib.FrozenLake, B: int, lookup, device, out=None):
     """FrozenLakeEnv.render text of every env (frozen_lake/env.py:47-61) -> (u8[B,stride], i32[B])."""
-    return _render(lib().rmi_frozenlake_render, env, B, env.nrow * env.ncol, env.nrow, lookup, device)
+    return _render(lib().rmi_frozenlake_render, env, B, env.nrow * env.ncol, env.nrow, lookup, device, out)
 
 
 # ------------------------------------------------- response -> action ids (§8(f) rank 2)
@@ -512,18 +515,26 @@ def _bytes_to_unicode():
     return dict(zip(bs, map(chr, cs)))
 
 
-def detokenize(ids: torch.Tensor, vocab: VocabTable, stride: int, n_ids: Optional[torch.Tensor] = None):
+def detokenize(ids: torch.Tensor, vocab: VocabTable, stride: int, n_ids: Optional[torch.Tensor] = None,
+               out=None):
     """tokenizer.batch_decode(ids, skip_special_tokens=True) (ctx_manager.py:334-337) on the
-    device: ids i64[B,R] -> (text u8[B,stride] UTF-8 rows, text_len i32[B], err u8[B])."""
+    device: ids i64[B,R] -> (text u8[B,stride] UTF-8 rows, text_len i32[B], err u8[B]).
+    ``out``: a previous result to write into (no allocation: graph-capturable)."""
     _dev(ids, n_ids)
     _dt(ids, torch.int64, "ids")
     _dt(n_ids, torch.int32, "n_ids")
     B, R = ids.shape
     stride = (int(stride) + 3) // 4 * 4
     dev = ids.device
-    out = torch.empty(B, stride, dtype=torch.uint8, device=dev)
-    n = torch.empty(B, dtype=torch.int32, device=dev)
-    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    if out is not None:
+        out, n, err = out
+        if out.shape != (B, stride):
+            raise ValueError("out= buffers do not match this batch")
+        err.zero_()
+    else:
+        out = torch.empty(B, stride, dtype=torch.uint8, device=dev)
+        n = torch.empty(B, dtype=torch.int32, device=dev)
+        err = torch.zeros(B, dtype=torch.uint8, device=dev)
     V = vocab.skip.numel()
     check(lib().rmi_detokenize(_ptr(ids), B, R, _ptr(n_ids), _ptr(vocab.off), _ptr(vocab.data), vocab.data.numel(),
                                V, _ptr(vocab.skip), _ptr(out), stride, _ptr(n), _ptr(err), _stream()),

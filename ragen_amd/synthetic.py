@@ -148,3 +148,45 @@ def encode_rows(texts, stride: int = 0):
     for i, b in enumerate(bs):
         buf[i, :len(b)] = np.frombuffer(b, np.uint8)
     return buf, np.array([len(b) for b in bs], np.int32)
+
+
+def byte_vocab(extra_words=()):
+    """A byte-level vocabulary for synthetic token ids: one token per byte, whole words of the
+    synthetic responses, and a special pad token (last id).  -> (table list[bytes], skip u8[V])."""
+    words = ["</think>", "<answer>", "</answer>", " || ", "||", " ||", "|| "]
+    for nm in ("Up", "Down", "Left", "Right") + UNKNOWN_NAMES:
+        words += [nm, nm.lower(), nm.upper()]
+    words += [" " + w for w in THINK_WORDS] + list(extra_words)
+    table = [bytes([i]) for i in range(256)] + [w.encode("utf-8") for w in dict.fromkeys(words)] + [b"<|endoftext|>"]
+    skip = np.zeros(len(table), np.uint8)
+    skip[-1] = 1
+    return table, skip
+
+
+def tokenize_greedy(texts, table, R=None):
+    """Longest-match tokenisation of UTF-8 texts over `table` (the byte tokens guarantee
+    coverage), right-padded with the last (special) id.  -> i64[B, R]."""
+    by_first = {}
+    for i, t in enumerate(table[:-1]):
+        if len(t) > 1:
+            by_first.setdefault(t[0], []).append((t, i))
+    for k in by_first:
+        by_first[k].sort(key=lambda x: -len(x[0]))
+    rows = []
+    for txt in texts:
+        b, i, row = txt.encode("utf-8"), 0, []
+        while i < len(b):
+            for t, tid in by_first.get(b[i], ()):
+                if b.startswith(t, i):
+                    row.append(tid)
+                    i += len(t)
+                    break
+            else:
+                row.append(b[i])
+                i += 1
+        rows.append(row)
+    R = R or max(len(r) for r in rows)
+    out = np.full((len(rows), R), len(table) - 1, np.int64)
+    for j, r in enumerate(rows):
+        out[j, :len(r)] = r[:R]
+    return out

@@ -268,3 +268,38 @@ def test_step_text_equals_dict_step(device, name, monkeypatch):
                 assert torch.equal(getattr(th.batch.ep, f), getattr(td.batch.ep, f)), (t, f)
         if not active:
             break
+
+
+def test_detokenize_utf8_validity_edges(device):
+    """Token byte strings that split multi-byte characters (valid once concatenated) and the
+    invalid forms (overlong, surrogate, > U+10FFFF, lone / extra continuation bytes, truncated
+    sequences at the row end, C0/C1/F5..FF): the device decode == bytes.decode("utf-8", "replace")."""
+    rng = np.random.default_rng(17)
+    valid_text = "Up — → 12 + 3 ✓ 😀 é ü 中文   x".encode("utf-8")
+    invalid = [b"\xc0\xaf", b"\xe0\x80\xaf", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\x80", b"\xbf\xbf",
+               b"\xc2", b"\xe2\x82", b"\xf0\x9f\x98", b"\xc2\x80\x80", b"\xf5", b"\xff", b"a\xe2\x28\xa1b"]
+    rows = []
+    for i in range(600):
+        if i % 3 == 0:  # valid text cut at random byte boundaries into tokens
+            src = valid_text * int(rng.integers(1, 4))
+        else:
+            src = valid_text[: int(rng.integers(0, len(valid_text)))] + invalid[i % len(invalid)] + \
+                valid_text[: int(rng.integers(0, 8))]
+        cuts = sorted(set(int(x) for x in rng.integers(0, len(src) + 1, size=int(rng.integers(0, 12)))))
+        pieces = [src[a:b] for a, b in zip([0] + cuts, cuts + [len(src)]) if b > a]
+        rows.append(pieces)
+    table = sorted({p for r in rows for p in r})
+    index = {p: i for i, p in enumerate(table)}
+    R = max(len(r) for r in rows)
+    ids = np.zeros((len(rows), R), np.int64)
+    n_ids = np.array([len(r) for r in rows], np.int32)
+    for i, r in enumerate(rows):
+        ids[i, :len(r)] = [index[p] for p in r]
+    vt = ops.VocabTable.from_bytes(table, np.zeros(len(table), np.uint8), device)
+    out, n, err = ops.detokenize(torch.from_numpy(ids).to(device), vt, 512, torch.from_numpy(n_ids).to(device))
+    torch.cuda.synchronize()
+    out, n = out.cpu().numpy(), n.cpu().numpy()
+    for i, r in enumerate(rows):
+        want = b"".join(r).decode("utf-8", "replace").encode("utf-8")
+        assert out[i, :n[i]].tobytes() == want, (i, b"".join(r))
+    assert not err.any()
