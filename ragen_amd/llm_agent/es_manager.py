@@ -154,36 +154,45 @@ class EnvStateManager:
                                 ep.turn_info[t].to(torch.int64), ep.turn_exec[t].to(torch.int64)]).cpu().numpy()
             rw = ep.turn_reward[t].cpu().numpy()
             pen = ep.penalty.cpu().numpy()
-            flags, num_actions, info, n_exec = host
+            # one host copy per turn, as Python lists (numpy scalar indexing per env is slower)
+            flags, num_actions, info, n_exec = (x.tolist() for x in host)
+            rw, pen = rw.tolist(), pen.tolist()
+            is_cd = tg.env_type == "countdown"
+            note = getattr(tg.batch, "note_executed", None)
+            render = tg.batch.render
+            F_TERM, F_TRUNC, F_DONE = _lib.FLAG_TERMINATED, _lib.FLAG_TRUNCATED, _lib.FLAG_DONE
+            I_PRES, I_EFF, I_VAL, I_SUCC = _lib.INFO_PRESENT, _lib.INFO_EFFECTIVE, _lib.INFO_VALID, _lib.INFO_SUCCESS
+            envs, rcache, lo = self.envs, self.rollout_cache, tg.lo
             for inp in inputs:
-                i = int(inp["env_id"]) - tg.lo
-                gid = tg.lo + i
-                entry, cache = self.envs[gid], self.rollout_cache[gid]
+                gid = int(inp["env_id"])
+                i = gid - lo
+                entry, cache = envs[gid], rcache[gid]
                 acts, m = mapped[i]
-                valid = [a for a in m if a != 0] if tg.env_type != "countdown" else list(acts)
-                executed = valid[:int(n_exec[i])]
-                if hasattr(tg.batch, "note_executed"):
-                    tg.batch.note_executed(t, i, executed)
-                acc = float(rw[i]) if n_exec[i] else 0
-                if tg.env_type == "countdown" and n_exec[i] and acc in (0.0, 1.0):
+                ne = n_exec[i]
+                executed = (list(acts) if is_cd else [a for a in m if a != 0])[:ne]
+                if note is not None:
+                    note(t, i, executed)
+                acc = rw[i] if ne else 0
+                if is_cd and ne and acc in (0.0, 1.0):
                     acc = int(acc)  # compute_reward returns int 0 / int score (countdown/env.py:73-78)
-                inf = int(info[i])
+                inf = info[i]
                 turn_info = {}
-                if inf & _lib.INFO_PRESENT:
-                    turn_info = {"action_is_effective": bool(inf & _lib.INFO_EFFECTIVE),
-                                 "action_is_valid": bool(inf & _lib.INFO_VALID),
-                                 "success": bool(inf & _lib.INFO_SUCCESS)}
+                if inf & I_PRES:
+                    turn_info = {"action_is_effective": bool(inf & I_EFF), "action_is_valid": bool(inf & I_VAL),
+                                 "success": bool(inf & I_SUCC)}
                 st = entry["status"]
-                st.num_actions = int(num_actions[i])
+                st.num_actions = num_actions[i]
                 st.rewards.append(acc)
-                st.terminated = bool(flags[i] & _lib.FLAG_TERMINATED)
-                st.truncated = bool(flags[i] & _lib.FLAG_TRUNCATED)
-                cache["penalty"] = float(pen[i]) if pen[i] != 0 else cache["penalty"]
-                cache["history"] = self._update_cache_history(
-                    cache["history"], entry["env"].render(i), entry["max_actions_per_traj"] - st.num_actions,
-                    {"actions": executed, "reward": acc, "info": turn_info, "llm_response": inp["llm_response"],
-                     "llm_raw_response": inp["llm_raw_response"]})
-                if not (flags[i] & _lib.FLAG_DONE):
+                fl = flags[i]
+                st.terminated = bool(fl & F_TERM)
+                st.truncated = bool(fl & F_TRUNC)
+                if pen[i] != 0:
+                    cache["penalty"] = pen[i]
+                hist = cache["history"]
+                hist[-1].update({"actions": executed, "reward": acc, "info": turn_info,
+                                 "llm_response": inp["llm_response"], "llm_raw_response": inp["llm_raw_response"]})
+                hist.append({"state": render(i), "actions_left": entry["max_actions_per_traj"] - st.num_actions})
+                if not (fl & F_DONE):
                     still_active.add(gid)
         self._turn += 1
         # only not-done envs go back for generation, in input order (es_manager.py:168-169)
