@@ -31,6 +31,16 @@ __device__ __forceinline__ int wave_inclusive_scan(int x) {
   return x;
 }
 
+// LDS hand-off between the lanes of ONE wave.  The wave-per-row kernels put several waves in a
+// workgroup (a one-wave workgroup per row caps how many rows a CU holds at once); the waves
+// work on separate rows and never share LDS, so a wavefront-scope release / acquire around a
+// wave barrier replaces __syncthreads().
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // --------------------------------------------------------------- PCG64 (numpy)
 // numpy PCG64 = pcg_setseq_128_xsl_rr_64: step state = state*M + inc (mod 2^128),
 // then output XSL-RR of the NEW state; Generator.random() = (out >> 11) * 2^-53.

@@ -36,8 +36,8 @@ __device__ unsigned long long* g_parse_stamps;
 #define PSTAMP(i) (pst_[i] = __builtin_amdgcn_s_memtime())
 #define PSTAMP_FLUSH()                                                                 \
   do {                                                                                 \
-    if (threadIdx.x == 0)                                                              \
-      for (int s_ = 0; s_ < 10; ++s_) g_parse_stamps[blockIdx.x * 10 + s_] = pst_[s_]; \
+    if ((threadIdx.x & 63) == 0)                                                       \
+      for (int s_ = 0; s_ < 10; ++s_) g_parse_stamps[b * 10 + s_] = pst_[s_];          \
   } while (0)
 #else
 #define PSTAMP_DECL \
@@ -54,7 +54,13 @@ __device__ unsigned long long* g_parse_stamps;
 constexpr int kPre = 8;                 // room for the implicit prefix tag in front of the text
 constexpr int kTail = 24;               // zero bytes after a row (16-byte compares read 20 past)
 constexpr int kMaxStride = 16384;       // detokenize rows (2 LDS rows per wave)
-constexpr int kMaxParseStride = 8192;   // parse rows (rows + event lists: < 64 KB of LDS)
+constexpr int kMaxParseStride = 8192;   // parse rows (rows + event lists: < 64 KB of LDS per wave)
+constexpr int kRowWaves = 4;            // at most this many rows (one wave each) per workgroup
+constexpr size_t kWgLds = 65536;        // LDS one workgroup may take; fewer rows per group on long rows
+inline int row_waves(size_t lds_per_wave) {
+  const size_t n = kWgLds / lds_per_wave;
+  return n >= (size_t)kRowWaves ? kRowWaves : (n < 1 ? 1 : (int)n);
+}
 
 // A string of <= 16 bytes packed little-endian into two words (compile-time tags, the
 // runtime separator and names alike), so that no byte table needs dynamic indexing.
@@ -268,9 +274,9 @@ __device__ int piece_id(const uint8_t* B, int s, int e, const Names& nm) {
 __device__ uint8_t* replace_strip_wave(uint8_t* src, uint8_t* dst, uint16_t* lst, uint8_t* cov, int a, int& z,
                                        const Tag& t, int lane) {
   const int n = collect(src, a, z, '<', lst, lane);
-  __syncthreads();
+  wave_sync();
   for (int x = a + lane; x < z; x += 64) cov[x] = 0;
-  __syncthreads();
+  wave_sync();
   bool any = false;
   for (int c = 0; c < n; c += 64) {
     const int i = c + lane;
@@ -288,7 +294,7 @@ __device__ uint8_t* replace_strip_wave(uint8_t* src, uint8_t* dst, uint16_t* lst
   }
   uint8_t* out = src;
   if (any) {
-    __syncthreads();
+    wave_sync();
     int o = a;
     for (int c = a; c < z; c += 64) {
       const int x = c + lane;
@@ -300,7 +306,7 @@ __device__ uint8_t* replace_strip_wave(uint8_t* src, uint8_t* dst, uint16_t* lst
     z = o;
     out = dst;
     if (lane < kTail) dst[z + lane] = 0;
-    __syncthreads();
+    wave_sync();
   }
   return out;
 }
@@ -324,21 +330,23 @@ struct ParseArgs {
 __host__ __device__ constexpr int row_bytes(int stride) { return (4 + kPre + stride + kTail + 7) & ~7; }
 __host__ __device__ constexpr int list_cap(int stride) { return (kPre + stride + 8) & ~7; }
 // T row | W row | EL u16[cap] | ES u16[cap] | EI u8[cap]
-__host__ __device__ constexpr size_t parse_lds(int stride) {
-  return 2 * (size_t)row_bytes(stride) + 5 * (size_t)list_cap(stride);
+__host__ __device__ constexpr size_t parse_lds(int stride) {  // per wave, a multiple of 8
+  return (2 * (size_t)row_bytes(stride) + 5 * (size_t)list_cap(stride) + 7) & ~(size_t)7;
 }
 
-__global__ __launch_bounds__(64) void parse_kernel(ParseArgs a) {
+__global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(8))) void parse_kernel(ParseArgs a) {
   extern __shared__ uint64_t lds_q[];
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_q);
+  const int wv = threadIdx.x >> 6;
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_q) + wv * parse_lds(a.stride);
   const int cap = list_cap(a.stride);
   uint8_t* T = lds + 4;                                                   // the prefixed row
   uint8_t* Wb = lds + row_bytes(a.stride) + 4;                            // replace-cascade row
   uint16_t* EL = reinterpret_cast<uint16_t*>(lds + 2 * row_bytes(a.stride));  // '<' positions
   uint16_t* ES = EL + cap;                                                // separator candidates
   uint8_t* EI = reinterpret_cast<uint8_t*>(ES + cap);                     // event ids
-  const int lane = threadIdx.x;
-  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (b >= a.B) return;  // the whole wave: no cross-wave barrier follows
   const rmi_parse_cfg_t& cfg = a.cfg;
   const int K = cfg.K;
   PSTAMP_DECL;
@@ -373,15 +381,15 @@ __global__ __launch_bounds__(64) void parse_kernel(ParseArgs a) {
   const Tag pre = cfg.enable_think ? kThinkOpen : kAnsOpen;
   const int plen = cfg.prepend ? pre.n : 0;
   const int base = kPre - plen, n_end = kPre + len;  // the prefixed response is T[base, n_end)
-  __syncthreads();
+  wave_sync();
   if (lane < kTail) T[n_end + lane] = 0;
   if (lane < 4 + kPre) T[lane - 4] = (lane - 4 >= base) ? tag_byte(pre, lane - 4 - base) : 0;
-  __syncthreads();
+  wave_sync();
   PSTAMP(1);
 
   // ---- 1. '<' events, classified (64 per step)
   EvList E{EL, EI, collect(T, base, n_end, '<', EL, lane), 0, E_NONE};
-  __syncthreads();
+  wave_sync();
   for (int i = lane; i < E.n; i += 64) {
     const int p = EL[i], id = classify_tag(T, p);
     if (i < 64) {
@@ -391,7 +399,7 @@ __global__ __launch_bounds__(64) void parse_kernel(ParseArgs a) {
       EI[i] = (uint8_t)id;
     }
   }
-  __syncthreads();
+  wave_sync();
   PSTAMP(2);
 
   // ---- 2. re.search(pattern, response, re.DOTALL)  (ctx_manager.py:149-150)
@@ -466,7 +474,7 @@ __global__ __launch_bounds__(64) void parse_kernel(ParseArgs a) {
   if (as >= 0) {
     // separator candidates: positions of its first byte, full compare, greedy selection
     const int nc = collect(C, ca, cz, (uint32_t)(sep.lo & 0xFFu), ES, lane);
-    __syncthreads();
+    wave_sync();
     int ns = 0, last = ca;  // selected separators -> EL (the '<' list is no longer needed)
     for (int c = 0; c < nc; c += 64) {
       const int i = c + lane;
@@ -490,7 +498,7 @@ __global__ __launch_bounds__(64) void parse_kernel(ParseArgs a) {
         }
       }
     }
-    __syncthreads();
+    wave_sync();
     // pieces: piece i = [i ? sel[i-1] + sep.n : ca, i < ns ? sel[i] : cz); one per lane
     for (int c = 0; c <= ns && count < K; c += 64) {
       const int i = c + lane;
@@ -605,19 +613,24 @@ __device__ int utf8_lossy(const uint8_t* src, int n, uint8_t* dst, int cap, bool
 // dwords covering them (tokens <= 9 bytes: 3 dwords; longer ones loop), clamped inside the
 // vocabulary blob.
 constexpr int kDetokG = 4;  // 64-id chunks per step
-__global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ ids, int64_t R,
+__host__ __device__ constexpr size_t detok_lds(int stride) { return 2 * ((size_t)stride + 4) + 16; }  // per wave
+__global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __restrict__ ids, int64_t R,
                                                    const int32_t* __restrict__ n_ids,
                                                    const int64_t* __restrict__ voff,
                                                    const uint8_t* __restrict__ vbytes, int64_t n_bytes, int64_t V,
                                                    const uint8_t* __restrict__ skip, uint8_t* __restrict__ out,
                                                    int stride, int32_t* __restrict__ out_len,
-                                                   uint8_t* __restrict__ err_out) {
+                                                   uint8_t* __restrict__ err_out, int64_t B) {
   extern __shared__ uint32_t lds_words[];
-  uint8_t* buf = reinterpret_cast<uint8_t*>(lds_words) + 4;  // raw concatenation [stride + 8], 4 B in front
-  uint8_t* fix = buf + stride + 8;                             // lossy-decoded row  [stride + 4]
-  __shared__ int sh_len, sh_over;
-  const int lane = threadIdx.x;
-  const int64_t b = blockIdx.x;
+  const int wv = threadIdx.x >> 6;
+  uint8_t* buf = reinterpret_cast<uint8_t*>(lds_words) + wv * detok_lds(stride) + 4;  // raw row [stride + 8]
+  uint8_t* fix = buf + stride + 8;                                                      // lossy row [stride + 4]
+  __shared__ int sh_len_a[kRowWaves], sh_over_a[kRowWaves];
+  int& sh_len = sh_len_a[wv];
+  int& sh_over = sh_over_a[wv];
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (b >= B) return;  // the whole wave
   int64_t rn = n_ids ? (int64_t)n_ids[b] : R;
   rn = rn < 0 ? 0 : (rn > R ? R : rn);
   const int64_t* row = ids + b * R;
@@ -681,7 +694,7 @@ __global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ i
   int n = pos < stride ? pos : stride;
   if (lane < 8) buf[n + lane] = 0;  // the validity windows read up to 8 bytes past the end
   if (lane < 4) buf[lane - 4] = 0;  // ... and 4 before the start
-  __syncthreads();
+  wave_sync();
   const uint8_t* res = buf;
   // Non-ASCII bytes: a wave-parallel validity test first (UTF-8 validity is local: every lead
   // byte needs its continuation bytes with the Table 3-7 ranges, every continuation byte a lead
@@ -741,14 +754,14 @@ __global__ __launch_bounds__(64) void detok_kernel(const int64_t* __restrict__ i
       sh_len = utf8_lossy(buf, n, fix, stride, ov);
       sh_over = ov;
     }
-    __syncthreads();
+    wave_sync();
     n = sh_len;
     over |= sh_over != 0;
     res = fix;
   }
   const int nw = (n + 3) >> 2;
   if (lane < 4 && (n & 3)) const_cast<uint8_t*>(res)[n + lane] = 0;  // deterministic tail bytes
-  __syncthreads();
+  wave_sync();
   uint32_t* o4 = reinterpret_cast<uint32_t*>(out + b * (int64_t)stride);
   const uint32_t* r4 = reinterpret_cast<const uint32_t*>(res);
   for (int i = lane; i < nw; i += 64) o4[i] = r4[i];
@@ -771,9 +784,11 @@ RMI_API int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32
   if (B == 0) return RMI_OK;
   if (!out || !out_len || !vocab_off || !skip || (R > 0 && !ids) || !vocab_bytes || n_bytes < 0) return RMI_EINVAL;
   if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(vocab_bytes)) & 3u) return RMI_EUNSUP;
-  const size_t shm = 2 * ((size_t)stride + 4) + 16;
-  hipLaunchKernelGGL(detok_kernel, dim3((unsigned)B), dim3(64), shm, as_stream(stream), ids, R, n_ids, vocab_off,
-                     vocab_bytes, n_bytes, V, skip, out, (int)stride, out_len, err);
+  const int nw = row_waves(detok_lds(stride));
+  const size_t shm = detok_lds(stride) * nw;
+  hipLaunchKernelGGL(detok_kernel, dim3((unsigned)((B + nw - 1) / nw)), dim3(64 * nw), shm,
+                     as_stream(stream), ids, R, n_ids, vocab_off, vocab_bytes, n_bytes, V, skip, out, (int)stride,
+                     out_len, err, B);
   return launch_status();
 }
 
@@ -801,7 +816,9 @@ RMI_API int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, c
   if (reinterpret_cast<uintptr_t>(text) & 3u) return RMI_EUNSUP;
   ParseArgs a{*cfg, text, text_len, B, (int)stride, sel, actions, n_actions, spans, action_text, action_len,
               (int)Lact, err};
-  const size_t shm = parse_lds(stride);
-  hipLaunchKernelGGL(parse_kernel, dim3((unsigned)B), dim3(64), shm, as_stream(stream), a);
+  const int nw = row_waves(parse_lds(stride));
+  const size_t shm = parse_lds(stride) * nw;
+  hipLaunchKernelGGL(parse_kernel, dim3((unsigned)((B + nw - 1) / nw)), dim3(64 * nw), shm,
+                     as_stream(stream), a);
   return launch_status();
 }
