@@ -58,6 +58,8 @@ __device__ __forceinline__ int utf8_next(const uint8_t* s, int n, int i, uint32_
 // The digit runs and the numbers live in registers (every array index is a compile-time
 // constant after unrolling), so nothing of this goes through scratch memory.
 constexpr int kMaxNums = 8;
+__device__ __forceinline__ bool same_multiset(const uint64_t (&found)[kMaxNums], int nf, bool too_many,
+                                              const int32_t (&nums)[kMaxNums], int n_nums);
 __device__ bool check_format(const uint8_t* s, int n, const int32_t (&nums)[kMaxNums], int n_nums) {
   uint64_t found[kMaxNums];
 #pragma unroll
@@ -95,8 +97,13 @@ __device__ bool check_format(const uint8_t* s, int n, const int32_t (&nums)[kMax
     i += len;
   }
   if (in_run) close_run();
+  return same_multiset(found, nf, too_many, nums, n_nums);
+}
+
+// sorted(found[:nf]) == sorted(nums[:n_nums])  (nums may be negative -> never equal a digit run)
+__device__ __forceinline__ bool same_multiset(const uint64_t (&found)[kMaxNums], int nf, bool too_many,
+                                              const int32_t (&nums)[kMaxNums], int n_nums) {
   if (too_many || nf != n_nums) return false;
-  // multiset equality: match every num (nums may be negative -> never equal a digit run)
   uint32_t used = 0;
 #pragma unroll
   for (int j = 0; j < kMaxNums; ++j) {
@@ -116,10 +123,10 @@ __device__ bool check_format(const uint8_t* s, int n, const int32_t (&nums)[kMax
 }
 
 // ------------------------------------------------------------------ evaluator
-struct Val {
-  bool is_f;
+struct Val {  // no padding: copies stay in registers
   long long i;
   double f;
+  int is_f;
   __device__ double as_f() const { return is_f ? f : (double)i; }
 };
 
@@ -302,6 +309,29 @@ __device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
       return EV_OK;
   }
   return EV_ERR;
+}
+
+// The four operators of the fast path (fast_reward below), each exactly as apply_binary, but
+// branch-free: every candidate result is computed and the right one selected, so a wave whose
+// lanes apply different operators runs one short straight-line sequence.
+__device__ __forceinline__ int fast_binary(int op, const Val& a, const Val& b, Val& out) {
+  const bool fl = a.is_f || b.is_f;
+  const double x = a.as_f(), y = b.as_f();
+  long long rs, rd, rm;
+  const bool os = __builtin_add_overflow(a.i, b.i, &rs);
+  const bool od = __builtin_sub_overflow(a.i, b.i, &rd);
+  const bool om = __builtin_mul_overflow(a.i, b.i, &rm);
+  const double q = x / y;
+  const bool div = op == OP_DIV;
+  const long long lim = 9007199254740992LL;
+  const bool big = a.i > lim || a.i < -lim || b.i > lim || b.i < -lim;
+  int st = EV_OK;
+  if (div) st = (!fl && b.i == 0) ? EV_ERR : (!fl && big) ? EV_UNSUP : (y == 0.0) ? EV_ERR : EV_OK;
+  else if (!fl && (op == OP_ADD ? os : op == OP_SUB ? od : om)) st = EV_UNSUP;
+  out.is_f = fl || div;
+  out.f = div ? q : op == OP_ADD ? x + y : op == OP_SUB ? x - y : x * y;
+  out.i = out.is_f ? 0 : op == OP_ADD ? rs : op == OP_SUB ? rd : rm;
+  return st;
 }
 
 constexpr int kStack = 32;  // deeper expressions are flagged RMI_ERR_UNSUP (host re-evaluates)
@@ -590,15 +620,179 @@ __device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work) {
   return EV_OK;
 }
 
+// Fast path for answers over the bytes "0-9 +-*/()" and ' ' (the usual arithmetic answer):
+// check_format and the evaluation in ONE pass, byte per loop iteration, with the evaluator's
+// state in registers, so the lanes of a wave (one answer each) run the same short loop body
+// whatever their answers look like (the general path branches per token kind, and a wave pays
+// the union of its lanes' paths).  The evaluator is the two-level form of the grammar
+//   expr := term (('+'|'-') term)* ; term := factor (('*'|'/') factor)* ;
+//   factor := ('+'|'-')* (literal | '(' expr ')')
+// computed eagerly left to right: acc (aop) term (mop) operand — the same operations in the
+// same order as Python's AST evaluation (and py_eval's postfix), so every value is identical.
+// Syntax is checked exactly as py_eval does (expect_operand, depth); parentheses save the
+// outer (acc, aop, term, mop, signs) in the thread's LDS work area.  A unary '-' on the int
+// -2**63 is EV_UNSUP as in apply_unary.  Returns false if the answer leaves the subset ('**',
+// '//', a multi-digit literal with a leading '0', > 18 digits, nesting > kFastDepth, any other
+// byte): the caller then runs check_format + py_eval.  fmt = check_format; st / out = the
+// evaluation (st differs from py_eval's only between EV_ERR and EV_UNSUP on answers that are
+// not correct either way).
+constexpr int kFastDepth = kStack / 2;  // two stack slots (acc, term) per open parenthesis
+enum : int { F_NONE = 0, F_ADD, F_SUB, F_MUL, F_DIV };
+__device__ __forceinline__ int fast_op(int f) {
+  return f == F_ADD ? OP_ADD : f == F_SUB ? OP_SUB : f == F_MUL ? OP_MUL : OP_DIV;
+}
+typedef const __attribute__((address_space(3))) uint8_t lds_cu8;
+// Per-lane state is kept in integer words, not bools: a bool that merges at a join of
+// divergent control flow is a 64-bit lane mask, and keeping a dozen of them costs more
+// scalar instructions than the evaluation itself.
+enum : int { S_EXPECT = 1, S_SLOW = 2, S_GROUP = 4, S_NEG = 8, S_NEGANY = 16, S_TOOMANY = 32 };
+// One token per loop iteration (spaces and a literal's digits in short inner loops), and at
+// most ONE arithmetic operation per iteration at ONE code site: ')' hands its group's value
+// to the next iteration as an operand token.  s: the answer staged in LDS.
+__device__ __forceinline__ bool fast_reward(const uint8_t* s_lds, int n, const int32_t (&nums)[kMaxNums], int n_nums,
+                                            bool& fmt, int& st, Val& out, uint8_t* work) {
+  lds_cu8* s = (lds_cu8*)s_lds;
+  SVal* stk = reinterpret_cast<SVal*>(work);
+  uint8_t* stf = work + kStack * sizeof(SVal);
+  uint64_t found[kMaxNums];
+#pragma unroll
+  for (int k = 0; k < kMaxNums; ++k) found[k] = 0;
+  int nf = 0, depth = 0, sf = S_EXPECT, aop = F_NONE, mop = F_NONE, i = 0;
+  Val acc, term, gv;
+  acc.is_f = term.is_f = gv.is_f = 0;
+  acc.i = term.i = gv.i = 0;
+  acc.f = term.f = gv.f = 0.0;
+  st = EV_OK;
+  for (;;) {
+    // ---- the next token: 0 = the end, 1 = an operand (a literal or a group's value), else the byte
+    int tok = 1;
+    Val v = gv;
+    if (sf & S_GROUP) {
+      sf &= ~S_GROUP;
+    } else {
+      while (i < n && s[i] == ' ') ++i;
+      tok = i < n ? s[i] : 0;
+      i += i < n;
+      if ((unsigned)(tok - '0') < 10u) {  // a literal = a check_format digit run
+        long long cur = tok - '0';
+        int ndig = 1;
+        for (int c; i < n && (unsigned)((c = s[i]) - '0') < 10u; ++i, ++ndig) cur = cur * 10 + (c - '0');
+        if ((tok == '0' && ndig > 1) || ndig > 18) sf |= S_SLOW;
+#pragma unroll
+        for (int k = 0; k < kMaxNums; ++k)
+          if (k == nf) found[k] = (uint64_t)cur;
+        sf |= nf == kMaxNums ? S_TOOMANY : 0;
+        nf += nf < kMaxNums;
+        if (st == EV_OK && !(sf & S_EXPECT)) st = EV_ERR;
+        v.is_f = 0;
+        v.i = cur;
+        v.f = 0.0;
+        tok = 1;
+      } else if (tok != 0) {
+        const int d = i < n ? s[i] : 0;
+        const bool arith = tok == '+' || tok == '-' || tok == '*' || tok == '/';
+        if ((!arith && tok != '(' && tok != ')') || ((tok == '*' || tok == '/') && d == tok)) sf |= S_SLOW;
+      }
+    }
+    if (sf & S_SLOW) break;
+    if (st == EV_OK) {  // else py_eval has returned: only check_format goes on
+      // ---- the token's effect: at most one operation (opc on x, y) and where its result goes
+      int opc = F_NONE, dst = 0;  // dst: 1 term, 2 acc, 3 group value, 4 out
+      Val x = acc, y = term;
+      if (tok == 1) {
+        if ((sf & S_NEGANY) && !v.is_f && v.i == (-9223372036854775807LL - 1)) st = EV_UNSUP;
+        if (sf & S_NEG) {
+          v.i = -v.i;
+          v.f = -v.f;
+        }
+        sf &= ~(S_EXPECT | S_NEG | S_NEGANY);
+        if (mop == F_NONE) term = v;
+        opc = mop;
+        x = term;
+        y = v;
+        dst = 1;
+        mop = F_NONE;
+      } else if (tok == 0) {
+        if ((sf & S_EXPECT) || depth != 0) st = EV_ERR;
+        if (aop == F_NONE) out = term;
+        opc = aop;
+        dst = 4;
+      } else if (tok == '(') {
+        if (!(sf & S_EXPECT)) {
+          st = EV_ERR;
+        } else if (depth == kFastDepth) {
+          sf |= S_SLOW;
+          break;
+        } else {
+          stk[2 * depth] = pack(acc);
+          stk[2 * depth + 1] = pack(term);
+          stf[depth] = (uint8_t)(aop | (mop << 3) | ((sf & (S_NEG | S_NEGANY)) << 3));
+          depth++;
+          aop = mop = F_NONE;
+          sf &= ~(S_NEG | S_NEGANY);
+        }
+      } else if (tok == ')') {
+        if ((sf & S_EXPECT) || depth == 0) {
+          st = EV_ERR;
+        } else {
+          if (aop == F_NONE) gv = term;
+          opc = aop;
+          dst = 3;
+          sf |= S_GROUP;  // the value is the next iteration's operand
+          depth--;
+        }
+      } else if (sf & S_EXPECT) {
+        if (tok == '-') sf = (sf ^ S_NEG) | S_NEGANY;
+        else if (tok != '+') st = EV_ERR;  // '*' or '/' where an operand is expected
+      } else if (tok == '*' || tok == '/') {
+        mop = tok == '*' ? F_MUL : F_DIV;
+        sf |= S_EXPECT;
+      } else {  // binary '+' / '-': the term joins acc
+        if (aop == F_NONE) acc = term;
+        opc = aop;
+        dst = 2;
+        aop = tok == '+' ? F_ADD : F_SUB;
+        sf |= S_EXPECT;
+      }
+      if (opc != F_NONE && st == EV_OK) {
+        Val r;
+        st = fast_binary(fast_op(opc), x, y, r);
+        if (dst == 1) term = r;
+        if (dst == 2) acc = r;
+        if (dst == 3) gv = r;
+        if (dst == 4) out = r;
+      }
+      if ((sf & S_GROUP) && st == EV_OK) {  // restore the enclosing level (its operation has read it)
+        acc = unpack(stk[2 * depth]);
+        term = unpack(stk[2 * depth + 1]);
+        const int f = stf[depth];
+        aop = f & 7;
+        mop = (f >> 3) & 7;
+        sf |= (f >> 3) & (S_NEG | S_NEGANY);
+      }
+    }
+    if (tok == 0) break;
+  }
+  if (sf & S_SLOW) return false;
+  fmt = same_multiset(found, nf, (sf & S_TOOMANY) != 0, nums, n_nums);
+  return true;
+}
+
 // compute_reward (countdown/env.py:69-78): 0 | format_score | score ; flags bit0 format bit1 correct
-__device__ double countdown_reward(const uint8_t* s, int n, const int32_t (&nums)[kMaxNums], int n_nums,
-                                   int32_t target, double score, double format_score, uint8_t& flags, uint8_t& err,
-                                   uint8_t* work) {
+// staged: s is the answer in this thread's LDS row (the fast path reads it there)
+__device__ double countdown_reward(const uint8_t* s, int n, bool staged, const int32_t (&nums)[kMaxNums],
+                                   int n_nums, int32_t target, double score, double format_score, uint8_t& flags,
+                                   uint8_t& err, uint8_t* work) {
   flags = 0;
-  if (!check_format(s, n, nums, n_nums)) return 0.0;
-  flags |= 1;
   Val v;
-  const int st = py_eval(s, n, v, work);
+  bool fmt = false;
+  int st = EV_ERR;
+  if (!staged || !fast_reward(s, n, nums, n_nums, fmt, st, v, work)) {
+    fmt = check_format(s, n, nums, n_nums);
+    if (fmt) st = py_eval(s, n, v, work);
+  }
+  if (!fmt) return 0.0;
+  flags |= 1;
   bool correct = false;
   if (st == EV_UNSUP) err |= RMI_ERR_UNSUP;
   if (st == EV_OK) {
@@ -610,20 +804,38 @@ __device__ double countdown_reward(const uint8_t* s, int n, const int32_t (&nums
   return score;
 }
 
-// An answer string is parsed byte by byte twice (check_format, then the evaluator): staged
-// once into this thread's LDS row with independent 4-B loads, the parse reads LDS instead of
-// paying a global-memory round trip per byte.
+// An answer string is parsed from this thread's LDS row: staged there with 16-B loads issued
+// four at a time (one memory round trip per 64 B), not a dependent load per word.  The first
+// 64 B of answer 0 are loaded with the kernel's other loads (prestage); only longer answers
+// pay a round trip of their own.
 constexpr int kStageMax = 256;  // answers up to this many bytes are staged (Lmax above: parsed in place)
-__device__ __forceinline__ const uint8_t* stage_answer(const uint8_t* g, int n, bool words_in_slot, uint8_t* lds_row) {
-  if (words_in_slot && (reinterpret_cast<uintptr_t>(g) & 3u) == 0) {
-    const uint32_t* g4 = reinterpret_cast<const uint32_t*>(g);
-    uint32_t* l4 = reinterpret_cast<uint32_t*>(lds_row);
-    const int nw = (n + 3) >> 2;
-    for (int i = 0; i < nw; ++i) l4[i] = g4[i];  // up to 3 bytes past n, still inside the [Lmax] slot
+constexpr int kPre = 64;        // bytes of answer 0 prestaged
+__device__ __forceinline__ bool stage16(const uint8_t* g, int Lmax) {  // 16-B loads stay inside the slot
+  return (Lmax & 15) == 0 && (reinterpret_cast<uintptr_t>(g) & 15u) == 0;
+}
+__device__ __forceinline__ void put16(uint8_t* lds_row, int off, const uint4& q) {
+  uint32_t* l4 = reinterpret_cast<uint32_t*>(lds_row + off);  // rows are 4-B aligned, not 16
+  l4[0] = q.x;
+  l4[1] = q.y;
+  l4[2] = q.z;
+  l4[3] = q.w;
+}
+// bytes [from, n) of the answer at g into lds_row (from a multiple of 16 when stage16)
+__device__ __forceinline__ void stage_answer(const uint8_t* g, int from, int n, int Lmax, uint8_t* lds_row) {
+  if (stage16(g, Lmax)) {
+    const uint4* g16 = reinterpret_cast<const uint4*>(g);
+    for (int c = from >> 4; 16 * c < n; c += 4) {
+      uint4 q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (16 * (c + j) < n) q[j] = g16[c + j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (16 * (c + j) < n) put16(lds_row, 16 * (c + j), q[j]);
+    }
   } else {
-    for (int i = 0; i < n; ++i) lds_row[i] = g[i];
+    for (int i = from; i < n; ++i) lds_row[i] = g[i];
   }
-  return lds_row;
 }
 
 struct CountdownDev {
@@ -631,6 +843,8 @@ struct CountdownDev {
   const int32_t* lens;     // this env's [K]
   uint8_t* stage;          // this thread's LDS row (nullptr: parse global memory in place)
   int Lmax;
+  int pre_n;     // bytes of answer 0 already in stage (0: none)
+  int32_t len0;  // lens[0], loaded with them
   int32_t nums[kMaxNums];
   int n_nums;
   uint8_t* work;  // this thread's evaluator stacks (LDS)
@@ -642,12 +856,16 @@ struct CountdownDev {
     // `a` is the 1-based slot of the answer string (the host passes 1..K for every parsed action)
     const int k = a - 1;
     if (k < 0) return false;
-    int n = lens[k];
+    const bool pre = k == 0 && pre_n > 0;
+    int n = pre ? len0 : lens[k];
     if (n > Lmax) n = Lmax;
     uint8_t fl;
     const uint8_t* src = answers + (int64_t)k * Lmax;
-    if (stage && n > 0) src = stage_answer(src, n, ((n + 3) & ~3) <= Lmax, stage);
-    reward = countdown_reward(src, n, nums, n_nums, target, score, format_score, fl, err, work);
+    if (stage && n > 0) {
+      stage_answer(src, pre ? pre_n : 0, n, Lmax, stage);
+      src = stage;
+    }
+    reward = countdown_reward(src, n, stage != nullptr, nums, n_nums, target, score, format_score, fl, err, work);
     done = true;
     eff = reward > 0;
     success = reward == score;
@@ -685,6 +903,21 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   e.stage = Lmax <= kStageMax ? slice : nullptr;
   e.work = slice + stage_stride(Lmax);
   e.Lmax = Lmax;
+  e.pre_n = 0;
+  e.len0 = 0;
+  if (in.K > 0 && e.stage && stage16(e.answers, Lmax)) {  // answer 0's head, with the other loads
+    const uint4* g16 = reinterpret_cast<const uint4*>(e.answers);
+    const int nc = (Lmax < kPre ? Lmax : kPre) >> 4;
+    uint4 q[kPre / 16];
+#pragma unroll
+    for (int j = 0; j < kPre / 16; ++j)
+      if (j < nc) q[j] = g16[j];
+    e.len0 = e.lens[0];
+#pragma unroll
+    for (int j = 0; j < kPre / 16; ++j)
+      if (j < nc) put16(e.stage, 16 * j, q[j]);
+    e.pre_n = 16 * nc;
+  }
   load_nums(env, b, e.nums);
   e.n_nums = env.n_nums[b];
   e.target = env.target[b];
@@ -728,8 +961,11 @@ __global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdow
   int32_t nums[kMaxNums];
   load_nums(env, i, nums);
   const uint8_t* src = answers + i * (int64_t)Lmax;
-  if (Lmax <= kStageMax && len > 0) src = stage_answer(src, len, ((len + 3) & ~3) <= Lmax, slice);
-  const double r = countdown_reward(src, len, nums, env.n_nums[i], env.target[i], env.score, env.format_score, fl,
+  if (Lmax <= kStageMax && len > 0) {
+    stage_answer(src, 0, len, Lmax, slice);
+    src = slice;
+  }
+  const double r = countdown_reward(src, len, Lmax <= kStageMax, nums, env.n_nums[i], env.target[i], env.score, env.format_score, fl,
                                     err, slice + stage_stride(Lmax));
   reward[i] = r;
   if (flags_out) flags_out[i] = fl;

@@ -76,11 +76,29 @@ def token_rows(n_turns, scores, seed: int = 7, prompt: int = 150, turn_scores=No
 
 def countdown_answers(instances, T: int, seed: int = ACTION_SEED, p_empty: float = 0.5):
     """Per env per turn a Countdown answer: with p_empty no parsed answer (the
-    turn only costs the format penalty), else a '+'/'-' expression over the instance's numbers
-    that is correct (1/3), uses every number but evaluates wrong (1/3: format score), or uses a
-    wrong number (1/3: reward 0).  -> [T][B] str or None."""
+    turn only costs the format penalty), else an expression over {digits + - * / ( )} and the
+    instance's numbers that is
+    * correct (1/3): the signed sum reaching the target, a left prefix of it parenthesised
+      half of the time ("(-12 + 40) - 7");
+    * format-only (1/3): every number once, in a random order, joined by random + - * / with
+      random parentheses (evaluates to the target only by chance);
+    * wrong numbers (1/3): the same grammar with one number off by one (reward 0).
+    -> [T][B] str or None."""
     rng = np.random.default_rng(seed)
     out = [[None] * len(instances) for _ in range(T)]
+
+    def grammar(vals):  # a random binary tree over vals in order, fully parenthesised inside
+        if len(vals) == 1:
+            return str(vals[0])
+        cut = int(rng.integers(1, len(vals)))
+        op = "+-*/"[int(rng.integers(0, 4))]
+        left, right = grammar(vals[:cut]), grammar(vals[cut:])
+        if cut > 1:
+            left = "(" + left + ")"
+        if len(vals) - cut > 1:
+            right = "(" + right + ")"
+        return left + " " + op + " " + right
+
     for t in range(T):
         for i, inst in enumerate(instances):
             if rng.random() < p_empty:
@@ -93,14 +111,17 @@ def countdown_answers(instances, T: int, seed: int = ACTION_SEED, p_empty: float
                 if sum(s * v for s, v in zip(sg, nums)) == target:
                     signs = sg
                     break
-            if signs is None or kind == 1:
-                signs = [1] * len(nums)  # all '+': uses every number, misses the target
+            if kind == 0 and signs is not None:
+                terms = [("-" if signs[0] < 0 else "") + str(nums[0])]
+                terms += [("+ " if s > 0 else "- ") + str(v) for s, v in zip(signs[1:], nums[1:])]
+                cut = int(rng.integers(2, len(terms) + 1)) if rng.random() < 0.5 and len(terms) > 2 else 0
+                if cut:
+                    terms = ["(" + " ".join(terms[:cut]) + ")"] + terms[cut:]
+                out[t][i] = " ".join(terms)
+                continue
             if kind == 2:
                 nums[int(rng.integers(0, len(nums)))] += 1
-            expr = ("-" if signs[0] < 0 else "") + str(nums[0])
-            for s, v in zip(signs[1:], nums[1:]):
-                expr += (" + " if s > 0 else " - ") + str(v)
-            out[t][i] = expr
+            out[t][i] = grammar([nums[j] for j in rng.permutation(len(nums))])
     return out
 
 

@@ -145,6 +145,91 @@ def test_countdown_reward_kat(device):
         assert r[i] == c["reward"], (c, r[i], int(err[i]))
 
 
+def test_countdown_reward_grammar_full_size(device):
+    """CD config size (16 384 answers) of the SURVEY §8(d) answer grammar ({digits + - * / ( )},
+    correct / format-only / wrong numbers): rmi_countdown_reward == oracle.countdown_reward
+    (countdown/env.py:69-78, Python eval) for every answer, no answer outside the model."""
+    from ragen_amd.env.countdown import synthetic_instances
+    n = 16384
+    inst = synthetic_instances(1024, 7)
+    env = CountdownBatch(CountdownEnvConfig(data=inst), n, 1, 1, device)
+    env.reset(synthetic.env_seeds(n))
+    mine = [inst[int(i)] for i in env.index]
+    exprs = synthetic.countdown_answers(mine, 1, p_empty=0.0)[0]
+    buf, lens = env.encode_answers([[e] for e in exprs])
+    r, fl, err = ops.countdown_reward(env.struct(), _t(buf[:, 0], device), _t(lens[:, 0].copy(), device))
+    r, err = r.cpu().numpy(), err.cpu().numpy()
+    want = np.array([oracle.countdown_reward(e, list(m["nums"]), int(m["target"])) for e, m in zip(exprs, mine)])
+    assert not err.any()
+    bad = np.nonzero(r != want)[0]
+    assert bad.size == 0, [(exprs[i], r[i], want[i]) for i in bad[:5]]
+    assert (want == 1).sum() > n // 4 and (want == 0.1).sum() > n // 8 and (want == 0).sum() > n // 4
+
+
+def _fuzz_answers(n, seed):
+    """Random strings over the fast path's bytes "0-9 +-*/()" and ' ' (plus, rarely, bytes that
+    leave it: '.', '%', '\\t', '**', '//', 'x'), each with nums = its digit runs and target =
+    its Python value where that is an int32, so format and value hit both outcomes."""
+    import re
+    import warnings
+    warnings.simplefilter("ignore", SyntaxWarning)  # "'int' object is not callable" from eval
+    rng = np.random.default_rng(seed)
+    alpha = list("0123456789+-*/() ") + ["12", "7", " + ", " - ", " * ", " / ", "(", ")"]
+    rare = [".", "%", "\t", "//", "x", "05", "0"]
+    def tree(depth):  # a valid expression: unary signs, nesting, all four operators
+        if depth == 0 or rng.random() < 0.3:
+            e = str(int(rng.choice([0, 1, 2, 7, 12, 99, 12345, 99999999999])))
+        else:
+            e = tree(depth - 1) + " " + "+-*/"[int(rng.integers(0, 4))] + " " + tree(depth - 1)
+            if rng.random() < 0.5:
+                e = "(" + e + ")"
+        return "".join(rng.choice(["-", "+", "- "], int(rng.integers(0, 3)))) + e
+
+    out, data = [], []
+    for _ in range(n):
+        if rng.random() < 0.5:
+            e = tree(int(rng.integers(1, 5)))
+            if len(e) > 60 or e.count("(") > 12:
+                e = "((((((((((((((((((1))))))))))))))))))"  # nesting beyond the fast path
+        else:
+            toks = [alpha[int(j)] for j in rng.integers(0, len(alpha), int(rng.integers(0, 14)))]
+            if rng.random() < 0.1:
+                toks.insert(int(rng.integers(0, len(toks) + 1)), rare[int(rng.integers(0, len(rare)))])
+            e = "".join(toks)[:58]
+        if rng.random() < 0.02:
+            e += "**2"  # at the end only: a random exponent could take Python forever
+        runs = [int(x) for x in re.findall(r"\d+", e)][:4]
+        try:
+            v = eval(e, {"__builtins__": None}, {})
+            tgt = int(v) if isinstance(v, (int, float)) and abs(v) < 2**31 and v == int(v) else 1
+        except Exception:
+            tgt = 1
+        if rng.random() < 0.2:
+            tgt += 1
+        out.append(e)
+        data.append({"nums": [x if x < 2**31 else 1 for x in runs] or [1], "target": tgt})
+    return out, data
+
+
+def test_countdown_reward_fuzz(device):
+    """Random answers over the fast path's alphabet (syntax errors, unary chains, deep parens,
+    division by zero, int overflow, bytes that leave the fast path) == oracle.countdown_reward;
+    an answer flagged RMI_ERR_UNSUP (outside the evaluator's model) is only allowed where
+    Python's value is beyond int64 / not modelled."""
+    n = 20000
+    exprs, data = _fuzz_answers(n, 7)
+    env = CountdownBatch(CountdownEnvConfig(data=data), n, 1, 1, device, max_answer_bytes=64)
+    env.reset(np.arange(n, dtype=np.int64))
+    buf, lens = env.encode_answers([[e] for e in exprs])
+    r, fl, err = ops.countdown_reward(env.struct(), _t(buf[:, 0], device), _t(lens[:, 0].copy(), device))
+    r, err = r.cpu().numpy(), err.cpu().numpy()
+    want = np.array([oracle.countdown_reward(e, d["nums"], d["target"]) for e, d in zip(exprs, data)])
+    bad = [i for i in np.nonzero(r != want)[0] if not err[i]]
+    assert not bad, [(exprs[i], r[i], want[i]) for i in bad[:5]]
+    assert (err != 0).sum() < n // 50
+    assert (want == 1).sum() > n // 20 and (want == 0.1).sum() > n // 20
+
+
 # ------------------------------------------------------------- BASELINE-size parity vs oracle
 @pytest.mark.parametrize("B", [8192, 20000])
 def test_sokoban_full_size_vs_oracle(device, B):

@@ -16,6 +16,8 @@ def run(answers, label):
     n = torch.from_numpy(np.array([len(x) for x in lists], np.uint8)).to(dev)
     z = torch.zeros(B, K, dtype=torch.int8, device=dev)
     t = ops.turn_struct(0, z, n, None, 1, -0.1)
+    ones = torch.ones(B, dtype=torch.uint8, device=dev)
+    tb = ops.turn_struct(0, z, n, ones, 1 << 30, -0.1)  # every env steps again: back-to-back launches
     st = cd.struct()
     for _ in range(3):
         cd.ep.arena.zero_(); ops.countdown_step_turn(st, cd.ep, t, bt, lt)
@@ -26,7 +28,13 @@ def run(answers, label):
         cd.ep.arena.zero_()
         e0.record(); ops.countdown_step_turn(st, cd.ep, t, bt, lt); e1.record(); torch.cuda.synchronize()
         tot += e0.elapsed_time(e1)
-    print(label, round(tot / 20 * 1000, 1), "us")
+    torch.cuda._sleep(1_000_000)
+    e0.record()
+    for _ in range(50):
+        ops.countdown_step_turn(st, cd.ep, tb, bt, lt)
+    e1.record()
+    torch.cuda.synchronize()
+    print(label, round(tot / 20 * 1000, 1), "us single,", round(e0.elapsed_time(e1) * 1000 / 50, 1), "us back-to-back")
 insts = [inst[int(i)] for i in cd.index]
 run([None] * B, "empty")
 run(["1"] * B, "one digit")
