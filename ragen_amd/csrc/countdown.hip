@@ -893,9 +893,10 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   const int64_t b = (int64_t)blockIdx.x * kCdBlock + threadIdx.x;
   const int B = ep.B;
   if (b >= B) return;
+  // every load of this env is issued before the activity test (one memory round trip): the
+  // has_input byte through a pointer that is always valid, selected afterwards
   uint8_t flags = ep.flags[b];
-  const bool act = in.has_input ? (in.has_input[b] != 0) : !(flags & RMI_FLAG_DONE);
-  if (!act) return;
+  const uint8_t has_in = *(in.has_input ? in.has_input + b : ep.flags + b);
   uint8_t* slice = cd_lds + threadIdx.x * cd_slice(Lmax);
   CountdownDev e;
   e.answers = answers + b * (int64_t)in.K * Lmax;
@@ -930,6 +931,8 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   uint8_t err = 0;
   int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
   double penalty = ep.penalty[b];
+  const bool act = in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE);
+  if (!act) return;
   TurnOut o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
                        in.format_penalty, err);
   ep.num_actions[b] = num_actions;

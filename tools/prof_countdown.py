@@ -9,7 +9,12 @@ B, K = 16384, 1
 inst = synthetic_instances(1024, 7)
 cd = CountdownBatch(CountdownEnvConfig(data=inst), B, 1, K, dev)
 cd.reset(synthetic.env_seeds(B))
+ONLY = sys.argv[1] if len(sys.argv) > 1 else None
+
+
 def run(answers, label):
+    if ONLY and label != ONLY:
+        return
     lists = [[a] if a is not None else [] for a in answers]
     buf, lens = cd.encode_answers(lists)
     bt, lt = torch.from_numpy(buf).to(dev), torch.from_numpy(lens).to(dev)
@@ -41,3 +46,4 @@ run(["1"] * B, "one digit")
 run([" + ".join(str(x) for x in i["nums"]) for i in insts], "sum of nums")
 run(synthetic.countdown_answers(insts, 1, p_empty=0.0)[0], "synthetic mix")
 run(["(" * 10 + "1" + ")" * 10] * B, "nested")
+run([None] * B, "empty")
