@@ -70,6 +70,13 @@ class BanditBatch(BatchEnv):
         return ops.parse_config(enable_think, self.K, action_sep, lo_first, hi_first, prepend=prepend), \
             self.hi_is_first, 0
 
+    def map_actions_many(self, rows, actions):
+        c, s0 = self.config, int(self.config.action_space_start)
+        hi, lo = c.hi_arm_name.lower(), c.lo_arm_name.lower()
+        revs = ({lo: s0, hi: s0 + 1}, {hi: s0, lo: s0 + 1})  # by hi_is_first (action_lookup below)
+        hf = self._hi_first_host
+        return [[revs[1 if hf[i] else 0].get(a.lower(), 0) for a in acts] for i, acts in zip(rows, actions)]
+
     def action_lookup(self, i):
         c, s = self.config, int(self.config.action_space_start)
         if self._hi_first_host[i]:

@@ -54,6 +54,18 @@ class BatchEnv:
         rev = {v.lower(): k for k, v in lookup.items()}
         return [rev.get(a.lower(), 0) for a in actions]
 
+    def map_actions_many(self, rows: List[int], actions: List[List[str]]) -> List[List[int]]:
+        """map_actions for many envs of one turn; the reverse table is built once per lookup."""
+        revs = {}
+        out = []
+        for i, acts in zip(rows, actions):
+            lookup = self.action_lookup(i)
+            rev = revs.get(id(lookup))
+            if rev is None:
+                rev = revs[id(lookup)] = {v.lower(): k for k, v in lookup.items()}
+            out.append([rev.get(a.lower(), 0) for a in acts])
+        return out
+
     def get_all_actions(self):
         return list(self.action_lookup(0).keys())
 

@@ -68,6 +68,9 @@ class CountdownBatch(BatchEnv):
     def map_actions(self, i, actions: List[str]) -> List[int]:
         return [k + 1 for k in range(len(actions))]
 
+    def map_actions_many(self, rows, actions):
+        return [list(range(1, len(a) + 1)) for a in actions]
+
     def reset(self, seeds):
         self.seeds = np.asarray(seeds, np.int64).copy()
         self.index = self.seeds % len(self.data)  # countdown/env.py:53

@@ -17,6 +17,7 @@ import torch
 
 from .. import _lib
 from ..env import REGISTERED_ENV_CONFIGS, REGISTERED_ENVS
+from ..env.base import BatchEnv
 
 
 @dataclass
@@ -114,40 +115,55 @@ class EnvStateManager:
         if self._turn >= self.max_turn:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
-        per_tag = {j: [] for j in range(len(self.tags))}
-        for inp in all_env_inputs:
-            per_tag[int(self._tag_of[int(inp["env_id"])])].append(inp)
+        gids_all = [int(inp["env_id"]) for inp in all_env_inputs]
+        if len(self.tags) == 1:
+            per_tag = {0: (all_env_inputs, gids_all)}
+        else:
+            per_tag = {j: ([], []) for j in range(len(self.tags))}
+            tag_of = self._tag_of
+            for inp, g in zip(all_env_inputs, gids_all):
+                ins, gs = per_tag[int(tag_of[g])]
+                ins.append(inp)
+                gs.append(g)
         still_active = set()
+        F_TERM, F_TRUNC, F_DONE = _lib.FLAG_TERMINATED, _lib.FLAG_TRUNCATED, _lib.FLAG_DONE
+        I_PRES, I_EFF, I_VAL, I_SUCC = _lib.INFO_PRESENT, _lib.INFO_EFFECTIVE, _lib.INFO_VALID, _lib.INFO_SUCCESS
         for j, tg in enumerate(self.tags):
-            inputs = per_tag[j]
+            inputs, gids = per_tag[j]
             if not inputs:
                 continue
-            B = tg.hi - tg.lo
-            ids = np.zeros((B, self.K), np.int8)
+            B, lo, K = tg.hi - tg.lo, tg.lo, self.K
+            rows = [g - lo for g in gids]
+            acts_l = [list(inp["actions"]) for inp in inputs]
+            lens = [len(a) for a in acts_l]
+            if max(lens) > K:
+                k = lens.index(max(lens))
+                raise ValueError(f"env {gids[k]}: {lens[k]} actions > max_actions_per_turn={K}")
+            m_l = tg.batch.map_actions_many(rows, acts_l)
+            # the turn's inputs as arrays: one scatter for every env's ids
+            ids = np.zeros((B, K), np.int8)
             n = np.zeros(B, np.uint8)
             has = np.zeros(B, np.uint8)
-            mapped = {}
-            answers = [[] for _ in range(B)] if tg.env_type == "countdown" else None
-            for inp in inputs:
-                i = int(inp["env_id"]) - tg.lo
-                acts = list(inp["actions"])
-                if len(acts) > self.K:
-                    raise ValueError(f"env {inp['env_id']}: {len(acts)} actions > max_actions_per_turn={self.K}")
-                m = tg.batch.map_actions(i, acts)
-                mapped[i] = (acts, m)
-                ids[i, :len(m)] = m
-                n[i] = len(acts)
-                has[i] = 1
-                if answers is not None:
-                    answers[i] = acts
+            r = np.asarray(rows, np.int64)
+            ln = np.asarray(lens, np.int64)
+            n[r] = ln
+            has[r] = 1
+            if ln.sum():
+                starts = np.repeat(np.cumsum(ln) - ln, ln)
+                cols = np.arange(int(ln.sum())) - starts
+                ids[np.repeat(r, ln), cols] = [x for m in m_l for x in m]
+            is_cd = tg.env_type == "countdown"
             dev = self.device
             ids_t = torch.from_numpy(ids).to(dev, non_blocking=True)
             n_t = torch.from_numpy(n).to(dev, non_blocking=True)
             has_t = torch.from_numpy(has).to(dev, non_blocking=True)
             kw = {}
-            if answers is not None:
-                buf, lens = tg.batch.encode_answers(answers)
-                kw = {"answers": torch.from_numpy(buf).to(dev), "answer_len": torch.from_numpy(lens).to(dev)}
+            if is_cd:
+                answers = [[] for _ in range(B)]
+                for i, a in zip(rows, acts_l):
+                    answers[i] = a
+                buf, alens = tg.batch.encode_answers(answers)
+                kw = {"answers": torch.from_numpy(buf).to(dev), "answer_len": torch.from_numpy(alens).to(dev)}
             tg.batch.step_turn(t, ids_t, n_t, has_t, tg.max_actions_per_traj, self.format_penalty, **kw)
             ep = tg.batch.ep
             host = torch.stack([ep.flags.to(torch.int64), ep.num_actions.to(torch.int64),
@@ -157,19 +173,15 @@ class EnvStateManager:
             # one host copy per turn, as Python lists (numpy scalar indexing per env is slower)
             flags, num_actions, info, n_exec = (x.tolist() for x in host)
             rw, pen = rw.tolist(), pen.tolist()
-            is_cd = tg.env_type == "countdown"
             note = getattr(tg.batch, "note_executed", None)
+            # the text observation of every env at once unless the env type renders per env
+            obs = tg.batch.render_all() if type(tg.batch).render is BatchEnv.render else None
             render = tg.batch.render
-            F_TERM, F_TRUNC, F_DONE = _lib.FLAG_TERMINATED, _lib.FLAG_TRUNCATED, _lib.FLAG_DONE
-            I_PRES, I_EFF, I_VAL, I_SUCC = _lib.INFO_PRESENT, _lib.INFO_EFFECTIVE, _lib.INFO_VALID, _lib.INFO_SUCCESS
-            envs, rcache, lo = self.envs, self.rollout_cache, tg.lo
-            for inp in inputs:
-                gid = int(inp["env_id"])
-                i = gid - lo
+            envs, rcache = self.envs, self.rollout_cache
+            for inp, gid, i, acts, m in zip(inputs, gids, rows, acts_l, m_l):
                 entry, cache = envs[gid], rcache[gid]
-                acts, m = mapped[i]
                 ne = n_exec[i]
-                executed = (list(acts) if is_cd else [a for a in m if a != 0])[:ne]
+                executed = (acts if is_cd else [a for a in m if a != 0])[:ne]
                 if note is not None:
                     note(t, i, executed)
                 acc = rw[i] if ne else 0
@@ -181,7 +193,8 @@ class EnvStateManager:
                     turn_info = {"action_is_effective": bool(inf & I_EFF), "action_is_valid": bool(inf & I_VAL),
                                  "success": bool(inf & I_SUCC)}
                 st = entry["status"]
-                st.num_actions = num_actions[i]
+                na = num_actions[i]
+                st.num_actions = na
                 st.rewards.append(acc)
                 fl = flags[i]
                 st.terminated = bool(fl & F_TERM)
@@ -189,15 +202,20 @@ class EnvStateManager:
                 if pen[i] != 0:
                     cache["penalty"] = pen[i]
                 hist = cache["history"]
-                hist[-1].update({"actions": executed, "reward": acc, "info": turn_info,
-                                 "llm_response": inp["llm_response"], "llm_raw_response": inp["llm_raw_response"]})
-                hist.append({"state": render(i), "actions_left": entry["max_actions_per_traj"] - st.num_actions})
+                h = hist[-1]
+                h["actions"] = executed
+                h["reward"] = acc
+                h["info"] = turn_info
+                h["llm_response"] = inp["llm_response"]
+                h["llm_raw_response"] = inp["llm_raw_response"]
+                hist.append({"state": obs[i] if obs is not None else render(i),
+                             "actions_left": entry["max_actions_per_traj"] - na})
                 if not (fl & F_DONE):
                     still_active.add(gid)
         self._turn += 1
         # only not-done envs go back for generation, in input order (es_manager.py:168-169)
-        return [self.rollout_cache[int(inp["env_id"])] for inp in all_env_inputs
-                if int(inp["env_id"]) in still_active]
+        rc = self.rollout_cache
+        return [rc[g] for g in gids_all if g in still_active]
 
     def step_tensor(self, actions: torch.Tensor, n_actions: torch.Tensor, has_input: Optional[torch.Tensor] = None,
                     tag_index: int = 0, **kw):

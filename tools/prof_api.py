@@ -1,19 +1,14 @@
-"""Host profile of the EnvStateManager facade on the SK workload (cProfile, top functions)."""
-import cProfile
-import os
-import pstats
-import sys
-
-import torch
-
+"""cProfile of bench.api_leg (the EnvStateManager.step facade on the SK workload)."""
+import cProfile, os, pstats, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import bench  # noqa: E402
+import torch
+import bench
 
-if __name__ == "__main__":
-    dev = torch.device("cuda", 0)
-    bench.api_leg(dev)  # warm
-    pr = cProfile.Profile()
-    pr.enable()
-    print(bench.api_leg(dev))
-    pr.disable()
-    pstats.Stats(pr).sort_stats("cumulative").print_stats(25)
+dev = torch.device("cuda", 0)
+print(bench.api_leg(dev))
+pr = cProfile.Profile()
+pr.enable()
+r = bench.api_leg(dev)
+pr.disable()
+print(r)
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
