@@ -362,6 +362,17 @@ int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, const int
                       int32_t stride, const uint8_t* sel, int8_t* actions, uint8_t* n_actions, int32_t* spans,
                       uint8_t* action_text, int32_t* action_len, int32_t Lact, uint8_t* err, rmi_stream_t stream);
 
+/* --------------------------------------------------------------- reset seeding */
+/* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and
+ * FrozenLakeEnv.reset's env RNG (frozen_lake/env.py:28-37), both via gymnasium
+ * seeding.np_random = Generator(PCG64(SeedSequence(seed))): per seed the PCG64 state after
+ * seeding and `draws` Generator.random() calls, written as rng[4][ld] (state hi, state lo,
+ * inc hi, inc lo — the layout every rmi_*_t rng pointer uses); last_draw[n] (optional) = the
+ * last draw (0.0 if draws == 0).  err[n] (optional): RMI_ERR_STATE for a negative seed
+ * (SeedSequence raises ValueError), else 0.                                               */
+int rmi_pcg64_seed(const int64_t* seeds, int64_t n, int32_t draws, uint64_t* rng, int64_t ld,
+                   double* last_draw, uint8_t* err, rmi_stream_t stream);
+
 /* ------------------------------------------------------------------------- misc */
 const char* rmi_version(void);
 int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t stream);

@@ -86,6 +86,7 @@ _SIGS = {
                                        c_void_p, c_void_p]),
     "rmi_frozenlake_step_turn": (c_int32, [_P(FrozenLake), _P(Episode), _P(Turn), c_void_p, c_void_p]),
     "rmi_frozenlake_reset": (c_int32, [_P(FrozenLake), _P(Episode), c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_pcg64_seed": (c_int32, [c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rmi_frozenlake_step_turn_finalize": (c_int32, [_P(FrozenLake), _P(Episode), _P(Turn), c_void_p, _P(Finalize),
                                                     c_void_p]),
     "rmi_frozenlake_step_turn_first": (c_int32, [_P(FrozenLake), _P(Episode), _P(Turn), c_void_p, c_void_p,

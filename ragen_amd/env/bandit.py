@@ -5,7 +5,6 @@ import torch
 from .. import _lib, ops
 from .base import BatchEnv
 from .configs import BanditEnvConfig
-from .frozen_lake import _pcg_state
 
 # bandit/env.py:6-12 (exact text, trailing spaces included: it is part of the observation)
 INIT_PROMPT = ("You are playing a bandit game. Goal: Maximize your total reward by choosing which arm to pull. \n"
@@ -36,23 +35,17 @@ class BanditBatch(BatchEnv):
                            float(c.hi_arm_hiscore), float(c.hi_arm_hiscore_prob), self.hi_is_first.data_ptr(),
                            self.rng.data_ptr())
 
-    # BanditEnv.reset + _randomize_arms (bandit/env.py:25-39, :52-60): one draw < 0.5
-    @staticmethod
-    def reset_arrays(seeds):
-        seeds = np.asarray(seeds, np.int64)
-        uniq, inv = np.unique(seeds, return_inverse=True)
-        hi_first = np.zeros(len(uniq), np.uint8)
-        rng = np.zeros((4, len(uniq)), np.uint64)
-        for i, sd in enumerate(uniq):
-            st = _pcg_state(int(sd), 1)
-            hi_first[i] = 0 if st[4] < 0.5 else 1
-            rng[:, i] = st[:4]
-        return hi_first[inv], rng[:, inv]
-
+    # BanditEnv.reset + _randomize_arms (bandit/env.py:25-39, :52-60): the env's Generator
+    # reseeded (gymnasium seeding.np_random) and one draw < 0.5 -> lo arm first; seeded on the
+    # device for every env at once (rmi_pcg64_seed)
     def reset(self, seeds):
         self.seeds = np.asarray(seeds, np.int64).copy()
-        hi_first, rng = self.reset_arrays(self.seeds)
-        self.load_state(hi_first, rng)
+        _, last = ops.pcg64_seed(torch.from_numpy(self.seeds).to(self.device), 1, self.rng)
+        self.hi_is_first.copy_((last >= 0.5).to(torch.uint8))
+        self._hi_first_host = self.hi_is_first.cpu().numpy()
+        self.ep.reset_()
+        self._last_obs = [None] * self.B
+        self._invalidate()
 
     def load_state(self, hi_first, rng):
         self._hi_first_host = np.asarray(hi_first, np.uint8).copy()

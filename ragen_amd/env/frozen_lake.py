@@ -6,18 +6,6 @@ from .. import _lib, ops
 from .base import BatchEnv
 from .configs import FrozenLakeEnvConfig
 
-_MASK64 = (1 << 64) - 1
-
-
-def _pcg_state(seed: int, draws: int) -> tuple:
-    """numpy Generator(PCG64(SeedSequence(seed))) advanced by `draws` random() calls
-    (gymnasium.utils.seeding.np_random) -> (state_hi, state_lo, inc_hi, inc_lo, last draw)."""
-    g = np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(seed))))
-    u = None
-    for _ in range(draws):
-        u = g.random()
-    st = g.bit_generator.state["state"]
-    return (st["state"] >> 64, st["state"] & _MASK64, st["inc"] >> 64, st["inc"] & _MASK64, u)
 
 
 def _is_valid(board, max_size):  # frozen_lake/utils.py:6-22
@@ -78,28 +66,29 @@ class FrozenLakeBatch(BatchEnv):
         return _lib.FrozenLake(self.nrow, self.ncol, int(bool(self.config.is_slippery)), self.cs[0], self.cs[1],
                                self.cs[2], self.desc.data_ptr(), self.s.data_ptr(), self.rng.data_ptr())
 
-    # FrozenLakeEnv.reset (frozen_lake/env.py:28-37): map from seed, env RNG reseeded with the
-    # same seed, one draw for the initial-state categorical_sample.
+    # FrozenLakeEnv.reset (frozen_lake/env.py:28-37): map from seed (host, once per distinct
+    # seed), env RNG reseeded with the same seed and one draw for the initial-state
+    # categorical_sample (device, rmi_pcg64_seed).
     @staticmethod
-    def reset_arrays(seeds, size, p):
+    def reset_maps(seeds, size, p):
         seeds = np.asarray(seeds, np.int64)
         uniq, inv = np.unique(seeds, return_inverse=True)
         desc = np.zeros((len(uniq), size * size), np.uint8)
         s0 = np.zeros(len(uniq), np.int32)
-        rng = np.zeros((4, len(uniq)), np.uint64)
         for i, sd in enumerate(uniq):
             m = generate_random_map(size=size, p=p, seed=int(sd))
             flat = "".join(m).encode()
             desc[i] = np.frombuffer(flat, np.uint8)
             s0[i] = flat.index(b"S")
-            st = _pcg_state(int(sd), 1)
-            rng[:, i] = st[:4]
-        return desc[inv], s0[inv], rng[:, inv]
+        return desc[inv], s0[inv]
 
     def reset(self, seeds):
         self.seeds = np.asarray(seeds, np.int64).copy()
-        desc, s0, rng = self.reset_arrays(self.seeds, self.nrow, float(self.config.p))
-        self.load_state(desc, s0, rng)
+        desc, s0 = self.reset_maps(self.seeds, self.nrow, float(self.config.p))
+        self.init_desc.copy_(torch.from_numpy(np.ascontiguousarray(desc)))
+        self.init_s.copy_(torch.from_numpy(np.ascontiguousarray(s0, dtype=np.int32)))
+        ops.pcg64_seed(torch.from_numpy(self.seeds).to(self.device), 1, self.init_rng)
+        self.restore()
 
     def load_state(self, desc, s0, rng):
         self.init_desc.copy_(torch.from_numpy(np.ascontiguousarray(desc)))

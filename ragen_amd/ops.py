@@ -187,6 +187,27 @@ def frozenlake_reset(env: _lib.FrozenLake, ep: EpisodeState, init_desc: torch.Te
           "rmi_frozenlake_reset")
 
 
+def pcg64_seed(seeds: torch.Tensor, draws: int = 0, rng: Optional[torch.Tensor] = None):
+    """Generator(PCG64(SeedSequence(seed))) seeded per element of seeds i64[n] on the device and
+    advanced by `draws` random() calls (gymnasium seeding.np_random; bandit/env.py:25-39,
+    frozen_lake/env.py:28-37).  -> (rng i64[4, n] (state hi, lo, inc hi, lo), last draw f64[n]).
+    Raises ValueError for a negative seed, as SeedSequence does."""
+    _dev(seeds, rng)
+    _dt(seeds, torch.int64, "seeds")
+    n = seeds.shape[0]
+    if rng is None:
+        rng = torch.empty(4, n, dtype=torch.int64, device=seeds.device)
+    if rng.dim() != 2 or rng.shape[0] != 4 or rng.shape[1] != n or not rng.is_contiguous():
+        raise ValueError("rng must be a contiguous i64[4, n]")
+    last = torch.empty(n, dtype=torch.float64, device=seeds.device)
+    err = torch.empty(n, dtype=torch.uint8, device=seeds.device)
+    check(lib().rmi_pcg64_seed(_ptr(seeds), n, int(draws), _ptr(rng), n, _ptr(last), _ptr(err),
+                               _stream()), "rmi_pcg64_seed")
+    if n and bool(err.any()):
+        raise ValueError("expected non-negative integer seeds")
+    return rng, last
+
+
 def frozenlake_step_turn_finalize(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn, fin: _lib.Finalize,
                                   err: Optional[torch.Tensor] = None):
     """frozenlake_step_turn + rollout_finalize (uniform contiguous groups) in one launch.  Groups

@@ -778,3 +778,27 @@ def test_frozenlake_fused_last_turn_finalize(device, B, T):
                              sc, pe))
             for a, b in zip(*outs):
                 assert torch.equal(a, b), (gs, method)
+
+
+def test_pcg64_seed_matches_numpy(device):
+    """rmi_pcg64_seed == numpy Generator(PCG64(SeedSequence(seed))) after `draws` random()
+    calls (gymnasium seeding.np_random as BanditEnv / FrozenLakeEnv reset it), for seeds across
+    the one-word / two-word entropy boundary and the 63-bit maximum."""
+    rs = np.random.default_rng(5)
+    seeds = np.concatenate([np.arange(0, 70), [2**32 - 1, 2**32, 2**32 + 1, 2**40 + 7, 2**63 - 1, 123, 1000000],
+                            rs.integers(0, 2**63 - 1, 200, dtype=np.int64)]).astype(np.int64)
+    for draws in (0, 1, 3):
+        rng, last = ops.pcg64_seed(_t(seeds, device), draws)
+        rng = rng.cpu().numpy().view(np.uint64)
+        last = last.cpu().numpy()
+        for i, sd in enumerate(seeds):
+            g = np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(sd))))
+            u = 0.0
+            for _ in range(draws):
+                u = g.random()
+            st = g.bit_generator.state["state"]
+            got = (int(rng[0, i]) << 64 | int(rng[1, i]), int(rng[2, i]) << 64 | int(rng[3, i]))
+            assert got == (st["state"], st["inc"]), (sd, draws)
+            assert last[i] == u, (sd, draws)
+    with pytest.raises(ValueError):
+        ops.pcg64_seed(_t(np.array([3, -1], np.int64), device), 1)
