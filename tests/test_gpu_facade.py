@@ -235,3 +235,46 @@ def test_agent_proxy_rollout_end_to_end(device):
     # each row's score sits in the last column, normalised per group of 16 (mean_std)
     last = out.batch["rm_scores"][:, -1].view(4, 16)
     assert torch.all(last.mean(-1).abs() < 1e-4)
+
+
+def test_es_manager_mixed_tags_equal_single_tag_runs(device):
+    """Two tags in one EnvStateManager (es_manager.py:44-73: env ids laid out tag after tag,
+    seeds seed + i // group_size across the whole list) == each tag run alone with the seed its
+    first group gets, turn by turn: the per-tag grouping of the inputs, the batched name
+    mapping and the one-launch-per-tag step."""
+    gs, T, K = 4, 3, 5
+    ov = {"es_manager": {"train": {"env_groups": 4, "group_size": gs,
+                                   "env_configs": {"tags": ["SimpleSokoban", "FrozenLake"], "n_groups": [2, 2]}}},
+          "agent_proxy": {"max_turn": T, "max_actions_per_turn": K}}
+    mixed = EnvStateManager(default_config(**ov), mode="train", device=device)
+    alone = [EnvStateManager(env_task(tag, 2, gs, max_turn=T, max_actions_per_turn=K), mode="train", device=device)
+             for tag in ("SimpleSokoban", "FrozenLake")]
+    seed = 77
+    mixed.reset(seed=seed)
+    alone[0].reset(seed=seed)
+    alone[1].reset(seed=seed + 2)  # FrozenLake's first group is group 2 of the mixed list
+    names = ["Up", "down", "LEFT", "Right", "jump"]
+    rng = np.random.default_rng(3)
+    active = list(range(16))
+    for t in range(T):
+        acts = {i: [names[int(a)] for a in rng.integers(0, 5, int(rng.integers(0, K + 1)))] for i in active}
+        # inputs in a shuffled env order: the grouping must not depend on it
+        order = [int(i) for i in rng.permutation(active)]
+        outs = mixed.step([{"env_id": i, "llm_response": "x", "llm_raw_response": "y", "actions": acts[i]}
+                           for i in order])
+        ref = []
+        for j, es in enumerate(alone):
+            mine = [i for i in order if (i >= 8) == (j == 1)]
+            if mine:
+                ref += es.step([{"env_id": i - 8 * j, "llm_response": "x", "llm_raw_response": "y",
+                                 "actions": acts[i]} for i in mine])
+        got = {o["env_id"]: o for o in outs}
+        want = {r["env_id"] + (8 if r["tag"] == "FrozenLake" else 0): r for r in ref}
+        assert sorted(got) == sorted(want)
+        assert [o["env_id"] for o in outs] == [i for i in order if i in want]  # input order kept
+        for i in got:
+            assert got[i]["history"] == want[i]["history"], (t, i)
+            assert got[i]["penalty"] == want[i]["penalty"]
+        active = [o["env_id"] for o in outs]
+        if not active:
+            break
