@@ -261,6 +261,38 @@ def test_sokoban_full_size_vs_oracle(device, B):
     np.testing.assert_array_equal(ops.rollout_metrics(env.ep).cpu().numpy(), oracle.rollout_metrics(oep))
 
 
+def test_sokoban_big_batch_vs_oracle(device):
+    """131 072 envs (the bench's 8192 rooms tiled 16x, 2048 one-wave workgroups: every CU holds
+    several) — kernel == oracle bit for bit each turn, with has_input both given and derived
+    from the done flags."""
+    T, K, tile = 5, 5, 16
+    cfg = SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100)
+    small = SokobanBatch(cfg, 8192, T, K, device)
+    small.reset(synthetic.env_seeds(8192))
+    B = 8192 * tile
+    env = SokobanBatch(cfg, B, T, K, device)
+    fixed = np.tile(small.room_fixed.cpu().numpy(), (tile, 1))
+    state = np.tile(small.room_state.cpu().numpy(), (tile, 1))
+    player = np.tile(small.player.cpu().numpy(), (tile, 1))
+    env.load_state(fixed, state, player)
+    nes = np.zeros(B, np.int32)
+    bot = np.zeros(B, np.int32)
+    oep = oracle.Episode(B, T)
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=9)
+    has = (np.random.default_rng(4).random((T, B)) < 0.9).astype(np.uint8)
+    for t in range(T):
+        h_in = has[t] if t % 2 else None
+        env.step_turn(t, _t(ids[t], device), _t(n[t], device), None if h_in is None else _t(h_in, device), 10, -0.1)
+        oracle.sokoban_turn(6, 6, 1, 100, fixed, state, player, nes, bot, oep, t, ids[t], n[t], h_in, 10, -0.1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(env.room_state.cpu().numpy(), state)
+        np.testing.assert_array_equal(env.player.cpu().numpy(), player)
+        h = _host_ep(env.ep)
+        for k in ("num_actions", "flags", "n_turns", "penalty", "turn_reward", "turn_info", "turn_exec"):
+            np.testing.assert_array_equal(h[k], getattr(oep, k), err_msg=k)
+    assert (oep.flags & 4).any() and not (oep.flags & 4).all()
+
+
 def test_frozenlake_full_size_vs_oracle(device):
     B, T, K = 4096, 8, 5
     env = FrozenLakeBatch(FrozenLakeEnvConfig(), B, T, K, device)
