@@ -264,8 +264,10 @@ int rmi_group_normalize(const float* score, const float* pen, const int32_t* seg
  * metrics[6] (f64: in_group_std/max/mean, chosen_in_group_std/max/mean means).
  * Selection = top int(ratio*G) by std ('std', type 0) or by -std ('std_rev', type 1);
  * ties broken by ascending group index (documented deviation: torch.topk's tie order is
- * implementation-defined).  ratio == 1 keeps everything.  G <= 8192.                    */
-int rmi_filter_groups(const float* scores, int32_t G, int32_t gs, double ratio, int32_t type, float* g_std,
+ * implementation-defined).  ratio == 1 keeps everything.  n = number of scores: RMI_EINVAL
+ * unless n == G*gs (the reference's rm_scores.view(num_groups, group_size) raises).
+ * G <= 8192 sorts in LDS; larger G takes a radix-select path with the same result.       */
+int rmi_filter_groups(const float* scores, int64_t n, int32_t G, int32_t gs, double ratio, int32_t type, float* g_std,
                       float* g_max, float* g_mean, uint8_t* keep, double* metrics, rmi_stream_t stream);
 
 /* Row sum of a [B,L] f32 tensor (rm_scores.sum(-1), agent_trainer.py:467).              */
@@ -308,6 +310,20 @@ int rmi_bilevel_gae(const float* r, const float* v, const uint8_t* mask, int64_t
 size_t rmi_whiten_scratch_bytes(int64_t B);
 int rmi_masked_whiten(float* x, const uint8_t* mask, int64_t B, int64_t L, const double* row_stats,
                       void* scratch, rmi_stream_t stream);
+
+/* The per-row whitening partials alone: row_stats[B,3] f64 = (sum, sum_sq, count) of x over
+ * the nonzero mask bytes of each row (what rmi_gae / rmi_bilevel_gae write as row_stats), for
+ * masked_whiten of a tensor no estimator produced (verl masked_whiten, core_algos.py:90).  */
+int rmi_whiten_row_stats(const float* x, const uint8_t* mask, int64_t B, int64_t L, double* row_stats,
+                         rmi_stream_t stream);
+
+/* masked_whiten with batch statistics gathered from several shards (the multi-GPU form of
+ * verl masked_whiten): stats[n_stats,3] = every rank's per-row (sum, sum_sq,
+ * count) in global row order (rmi_gae / rmi_bilevel_gae row_stats, all-gathered); x[B,L] =
+ * this rank's rows, whitened in place.  scratch >= 64 bytes; on return (stream order) its
+ * int32 at byte 8 = 0 ok, 1 mask sum 0, 2 mask sum 1 (verl raises ValueError for both). */
+int rmi_masked_whiten_stats(float* x, int64_t B, int64_t L, const double* stats, int64_t n_stats, void* scratch,
+                            rmi_stream_t stream);
 
 /* Replaces: verl compute_grpo_outcome_advantage (agent_trainer.py:94-99; App. A.4) with
  * contiguous groups seg[G+1] (RAGEN passes unique uids => every group has size 1).       */

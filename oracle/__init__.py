@@ -263,3 +263,50 @@ def countdown_reward(answer, nums, target, score=1, format_score=0.1):  # countd
     if not check_correctness(answer, target):
         return format_score
     return score
+
+
+def countdown_turn(answers, nums, targets, ep, turn, has_input=None, max_actions=1, fpen=-0.1, score=1,
+                   format_score=0.1):
+    """One EnvStateManager.step (es_manager.py:149-169) over CountdownEnv.step
+    (countdown/env.py:58-62) for every env, written into the Episode record ``ep``.
+
+    answers[b]: the parsed answer strings of env b (list, maybe empty).  Countdown has no
+    action_lookup, so every string is a valid action (es_manager.py:235-236) and the format
+    penalty is charged only for an empty list (:158-159).  A step is always done, so at most
+    one answer executes per turn (_execute_actions :116-128); a turn without an answer
+    costs the penalty and leaves the env active unless the cap of :163-166 is reached.
+    ``left <= 0`` executes nothing (DESIGN deviation 5: Python's ``valid[:left]`` would slice
+    from the end, a state the reference never reaches by itself).
+    has_input[b] (optional): env b receives an input this turn; default = not done."""
+    for b in range(ep.B):
+        active = bool(has_input[b]) if has_input is not None else not (int(ep.flags[b]) & FLAG_DONE)
+        if not active:
+            continue
+        valid = list(answers[b])
+        left = max_actions - int(ep.num_actions[b])
+        acc, info, turn_done, executed = 0, None, False, 0
+        for a in (valid[:left] if left > 0 else []):
+            reward = countdown_reward(a, list(nums[b]), int(targets[b]), score, format_score)
+            acc += reward
+            info = (reward > 0, reward == score)
+            executed += 1
+            turn_done = True  # countdown/env.py:60: done is always True
+            break
+        if not valid:
+            ep.penalty[b] += fpen
+        ep.num_actions[b] += executed
+        ep.n_turns[b] += 1
+        ep.turn_reward[turn, b] = acc
+        ep.turn_exec[turn, b] = executed
+        ep.turn_info[turn, b] = 0 if info is None else (INFO_PRESENT | (INFO_EFF if info[0] else 0) | INFO_VALID
+                                                        | (INFO_SUCC if info[1] else 0))
+        f = int(ep.flags[b]) & ~FLAG_DONE
+        if turn_done:
+            f |= FLAG_TERM
+            f = (f & ~FLAG_TRUNC) if info[1] else (f | FLAG_TRUNC)
+        if ep.num_actions[b] >= max_actions and not turn_done:
+            f |= FLAG_TERM | FLAG_TRUNC
+            turn_done = True
+        if turn_done:
+            f |= FLAG_DONE
+        ep.flags[b] = f

@@ -103,8 +103,8 @@ _SIGS = {
     "rmi_rollout_metrics": (c_int32, [_P(Episode), c_void_p, c_void_p]),
     "rmi_trajectory_scores": (c_int32, [_P(Episode), c_void_p, c_void_p, c_void_p]),
     "rmi_group_normalize": (c_int32, [c_void_p, c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p]),
-    "rmi_filter_groups": (c_int32, [c_void_p, c_int32, c_int32, c_double, c_int32, c_void_p, c_void_p, c_void_p,
-                                    c_void_p, c_void_p, c_void_p]),
+    "rmi_filter_groups": (c_int32, [c_void_p, c_int64, c_int32, c_int32, c_double, c_int32, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_row_sum": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "rmi_masks_and_scores": (c_int32, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
                                        c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
@@ -114,6 +114,8 @@ _SIGS = {
                                   c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_whiten_scratch_bytes": (c_size_t, [c_int64]),
     "rmi_masked_whiten": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rmi_whiten_row_stats": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "rmi_masked_whiten_stats": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_grpo_outcome": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_double, c_int32,
                                    c_void_p, c_void_p, c_void_p]),
     "rmi_detokenize": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int64,

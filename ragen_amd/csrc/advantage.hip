@@ -56,6 +56,16 @@ struct GaeTile {
   uint32_t m[kGLoads];
 };
 
+// Mask bytes -> 0x01 per nonzero byte: a mask is a boolean (RAGEN passes a bool loss_mask,
+// ctx_manager.py:46-49), so any nonzero byte counts as 1 in the recurrence, the whitening
+// count and the sums alike.
+__device__ __forceinline__ uint32_t nz8(uint32_t x) {
+  x |= x >> 4;
+  x |= x >> 2;
+  x |= x >> 1;
+  return x & 0x01010101u;
+}
+
 __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restrict__ r, const float* __restrict__ v,
                                               const uint8_t* __restrict__ mask, int64_t B, int64_t L, int64_t row0,
                                               int64_t c0, int lane) {
@@ -71,7 +81,7 @@ __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restric
     const int64_t o = dummy ? min<int64_t>(row0, B - 1) * L : (full_col ? row * L + col : row * L);
     t.r[j] = *reinterpret_cast<const F4*>(r + o);
     t.v[j] = *reinterpret_cast<const F4*>(v + o);
-    t.m[j] = mask ? reinterpret_cast<const U8x4*>(mask + o)->x : 0x01010101u;
+    t.m[j] = mask ? nz8(reinterpret_cast<const U8x4*>(mask + o)->x) : 0x01010101u;
   }
   // 2. the ragged group at a row end (L % 4 != 0: one group per row, in one tile) and rows
   //    past B, element by element, never past the row
@@ -91,7 +101,7 @@ __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restric
           if (col + e < L) {
             rr[e] = r[o + e];
             vv[e] = v[o + e];
-            mm |= (uint32_t)(mask ? mask[o + e] : 1) << (8 * e);
+            mm |= (uint32_t)(mask ? mask[o + e] != 0 : 1) << (8 * e);
           }
         }
         t.r[j] = F4{rr[0], rr[1], rr[2], rr[3]};
@@ -734,13 +744,14 @@ __global__ __launch_bounds__(kBlock) void whiten_apply_kernel(float* __restrict_
 // GRPO: one wave per group segment; rows of the group are summed (fp64 -> f32) per row,
 // group mean/std in fp64, then the per-row score is broadcast over the row's mask.
 __global__ __launch_bounds__(kBlock) void grpo_kernel(const float* __restrict__ r, const uint8_t* __restrict__ mask,
-                                                      int64_t L, const int32_t* __restrict__ seg, int G, float eps,
-                                                      int norm_by_std, float* __restrict__ adv,
+                                                      int64_t B, int64_t L, const int32_t* __restrict__ seg, int G,
+                                                      float eps, int norm_by_std, float* __restrict__ adv,
                                                       float* __restrict__ ret) {
   const int lane = threadIdx.x & 63;
   const int g = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (g >= G) return;
   const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
+  if (n <= 0 || lo < 0 || hi > B) return;  // malformed segments are never read past [0, B)
   // pass 1: group sums of row scores
   double gs = 0.0, gq = 0.0;
   for (int row = lo; row < hi; ++row) {
@@ -839,13 +850,41 @@ RMI_API int rmi_masked_whiten(float* x, const uint8_t* mask, int64_t B, int64_t 
   return launch_status();
 }
 
+RMI_API int rmi_whiten_row_stats(const float* x, const uint8_t* mask, int64_t B, int64_t L, double* row_stats,
+                                 rmi_stream_t stream) {
+  using namespace rmi;
+  if (!x || !mask || !row_stats || B < 0 || L < 0) return RMI_EINVAL;
+  if (B == 0) return RMI_OK;
+  const int per = kBlock / 64;
+  hipLaunchKernelGGL(row_stats_kernel, dim3((unsigned)((B + per - 1) / per)), dim3(kBlock), 0, as_stream(stream), x,
+                     mask, B, L, row_stats);
+  return launch_status();
+}
+
+RMI_API int rmi_masked_whiten_stats(float* x, int64_t B, int64_t L, const double* stats, int64_t n_stats,
+                                    void* scratch, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!x || !stats || !scratch || B < 0 || L < 0 || n_stats < 0) return RMI_EINVAL;
+  hipStream_t s = as_stream(stream);
+  WhitenParams* params = reinterpret_cast<WhitenParams*>(scratch);
+  hipLaunchKernelGGL(whiten_finalize_kernel, dim3(1), dim3(1024), 0, s, stats, n_stats, params);
+  const int64_t n = B * L;
+  if (n > 0) {
+    int64_t blocks = (n / 4 + kBlock - 1) / kBlock;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(whiten_apply_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, x, n, params);
+  }
+  return launch_status();
+}
+
 RMI_API int rmi_grpo_outcome(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G,
                              double eps, int32_t norm_by_std, float* adv, float* ret, rmi_stream_t stream) {
   using namespace rmi;
   if (!r || !mask || !seg || !adv || !ret || B < 0 || L < 0 || G < 0) return RMI_EINVAL;
   if (B == 0 || G == 0) return RMI_OK;
   const int per = kBlock / 64;
-  hipLaunchKernelGGL(grpo_kernel, dim3((G + per - 1) / per), dim3(kBlock), 0, as_stream(stream), r, mask, L, seg, G,
+  hipLaunchKernelGGL(grpo_kernel, dim3((G + per - 1) / per), dim3(kBlock), 0, as_stream(stream), r, mask, B, L, seg, G,
                      (float)eps, norm_by_std, adv, ret);
   return launch_status();
 }

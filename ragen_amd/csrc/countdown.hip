@@ -9,8 +9,9 @@
 // % ** << >> & | ^, unary + - ~, parentheses, whitespace, '#' comments, Python int/float
 // rules (true division, floor division/modulo signs, int**negative -> float, ZeroDivision
 // -> not correct).  Bytes whose eval result the evaluator does not model (letters and
-// keywords, '_' outside a literal, quotes, '[', '{', '.', comparisons, '\\') make the answer
-// "not correct" AND set RMI_ERR_UNSUP in err[] so a caller can see the envelope was left;
+// keywords, quotes, '[', '{', '.', comparisons, '\\') make the answer "not correct" AND set
+// RMI_ERR_UNSUP in err[] so a caller can see the envelope was left; bare names are modelled
+// (every lookup raises under {"__builtins__": None}: not correct, see name_outcome);
 // every other byte only yields errors in Python too (SyntaxError/TypeError -> False).
 // int results beyond 64 bits (Python big ints) are flagged RMI_ERR_UNSUP as well.
 #include <math.h>
@@ -511,6 +512,83 @@ __device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
   return i;
 }
 
+// Python 3.10 keyword.kwlist, each packed little-endian into a u64
+__constant__ uint64_t kPyKeywords[35] = {
+    0x00000065736c6146ull /* False */,
+    0x00000000656e6f4eull /* None */,
+    0x0000000065757254ull /* True */,
+    0x0000000000646e61ull /* and */,
+    0x0000000000007361ull /* as */,
+    0x0000747265737361ull /* assert */,
+    0x000000636e797361ull /* async */,
+    0x0000007469617761ull /* await */,
+    0x0000006b61657262ull /* break */,
+    0x0000007373616c63ull /* class */,
+    0x65756e69746e6f63ull /* continue */,
+    0x0000000000666564ull /* def */,
+    0x00000000006c6564ull /* del */,
+    0x0000000066696c65ull /* elif */,
+    0x0000000065736c65ull /* else */,
+    0x0000747065637865ull /* except */,
+    0x00796c6c616e6966ull /* finally */,
+    0x0000000000726f66ull /* for */,
+    0x000000006d6f7266ull /* from */,
+    0x00006c61626f6c67ull /* global */,
+    0x0000000000006669ull /* if */,
+    0x000074726f706d69ull /* import */,
+    0x0000000000006e69ull /* in */,
+    0x0000000000007369ull /* is */,
+    0x00006164626d616cull /* lambda */,
+    0x6c61636f6c6e6f6eull /* nonlocal */,
+    0x0000000000746f6eull /* not */,
+    0x000000000000726full /* or */,
+    0x0000000073736170ull /* pass */,
+    0x0000006573696172ull /* raise */,
+    0x00006e7275746572ull /* return */,
+    0x0000000000797274ull /* try */,
+    0x000000656c696877ull /* while */,
+    0x0000000068746977ull /* with */,
+    0x000000646c656979ull /* yield */};
+
+// A bare name in the answer (countdown/env.py:16-21 evaluates with {"__builtins__": None}):
+// every name lookup raises there (TypeError: None is not subscriptable), so an answer whose
+// names are all plain identifiers and whose other bytes only form strict operators cannot be
+// correct — every operand is evaluated, the name included, or the parse fails.  The answer
+// stays outside the model (EV_UNSUP) when something could bind or skip a name: a keyword
+// (lambda, if/else, and/or, not, in, is, True/False/None ...), ':' (walrus, slices, dicts),
+// '.' (attribute names, floats), comparisons ('<' '>' '=' '!': chains short-circuit), quotes,
+// '\\', non-ASCII bytes (Unicode identifiers), or a digit run fused with letters (1if, 0x10).
+__device__ int name_outcome(const uint8_t* s, int n) {
+  int i = 0;
+  while (i < n) {
+    const uint8_t c = s[i];
+    if (c >= 0x80 || c == ':' || c == '\'' || c == '"' || c == '\\' || c == '.' || c == '<' || c == '>' ||
+        c == '=' || c == '!')
+      return EV_UNSUP;
+    if (is_alpha(c) || c == '_' || is_digit(c)) {
+      const bool digit_start = is_digit(c);
+      bool letters = false;
+      uint64_t packed = 0;
+      int j = i;
+      while (j < n && (is_alpha(s[j]) || s[j] == '_' || is_digit(s[j]))) {
+        letters |= !is_digit(s[j]);
+        if (j - i < 8) packed |= (uint64_t)s[j] << (8 * (j - i));
+        j++;
+      }
+      if (digit_start && letters) return EV_UNSUP;
+      if (!digit_start && j - i <= 8) {
+#pragma unroll 1
+        for (int k = 0; k < 35; ++k)
+          if (packed == kPyKeywords[k]) return EV_UNSUP;
+      }
+      i = j;
+      continue;
+    }
+    i++;
+  }
+  return EV_ERR;
+}
+
 // returns EV_OK with value in out, EV_ERR (Python raises), EV_UNSUP (outside the model)
 __device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work) {
   Machine m;
@@ -605,7 +683,8 @@ __device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work) {
       }
     }
     // anything else
-    if (is_alpha(c) || c == '_' || c == '"' || c == '\'' || c == '[' || c == '{' || c == '.' || c == '<' ||
+    if (is_alpha(c) || c == '_') return name_outcome(s, n);
+    if (c == '"' || c == '\'' || c == '[' || c == '{' || c == '.' || c == '<' ||
         c == '>' || c == '=' || c == '!' || c == '\\' || c >= 0x80)
       return (c == '=' && !(i + 1 < n && s[i + 1] == '=')) ? EV_ERR : EV_UNSUP;
     return EV_ERR;  // ',', ';', ':', '@', '$', '?', '`', ']', '}', control chars ...

@@ -86,13 +86,13 @@ __global__ __launch_bounds__(kBlock) void trajectory_scores_kernel(rmi_episode_t
 // one wave per segment; 4 segments per 256-thread workgroup
 __global__ __launch_bounds__(kBlock) void group_normalize_kernel(const float* __restrict__ score,
                                                                  const float* __restrict__ pen,
-                                                                 const int32_t* __restrict__ seg, int G, int method,
-                                                                 float* __restrict__ out) {
+                                                                 const int32_t* __restrict__ seg, int G, int B,
+                                                                 int method, float* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const int g = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (g >= G) return;
   const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
-  if (n <= 0) return;
+  if (n <= 0 || lo < 0 || hi > B) return;  // malformed segments are never read past [0, B)
   double s = 0.0;
   for (int i = lo + lane; i < hi; i += 64) s += (double)(score[i] + (pen ? pen[i] : 0.0f));
   s = wave_sum(s);
@@ -143,6 +143,22 @@ __device__ __forceinline__ uint32_t orderable(float f) {  // monotone float -> u
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// per-group statistics of _filter_rollout (agent_trainer.py:466-469): unbiased std (NaN for a
+// group of one, as torch), max and mean of the group's row scores; fp64 accumulation.
+__device__ __forceinline__ void group_stats(const float* __restrict__ x, int gs, float& sd, float& mx, float& mean) {
+  double s = 0.0;
+  mx = -INFINITY;
+  for (int i = 0; i < gs; ++i) {
+    s += (double)x[i];
+    mx = fmaxf(mx, x[i]);
+  }
+  const double m = s / gs;
+  double q = 0.0;
+  for (int i = 0; i < gs; ++i) q += ((double)x[i] - m) * ((double)x[i] - m);
+  sd = gs > 1 ? (float)sqrt(q / (gs - 1)) : __builtin_nanf("");
+  mean = (float)m;
+}
+
 __global__ __launch_bounds__(kFilterThreads) void filter_kernel(const float* __restrict__ scores, int G, int gs,
                                                                 int k, int type, float* __restrict__ g_std,
                                                                 float* __restrict__ g_max, float* __restrict__ g_mean,
@@ -155,23 +171,14 @@ __global__ __launch_bounds__(kFilterThreads) void filter_kernel(const float* __r
   double a_std = 0, a_max = 0, a_mean = 0;
   for (int g = threadIdx.x; g < P; g += kFilterThreads) {
     if (g < G) {
-      const float* x = scores + (int64_t)g * gs;
-      double s = 0.0;
-      float mx = -INFINITY;
-      for (int i = 0; i < gs; ++i) {
-        s += (double)x[i];
-        mx = fmaxf(mx, x[i]);
-      }
-      const double m = s / gs;
-      double q = 0.0;
-      for (int i = 0; i < gs; ++i) q += ((double)x[i] - m) * ((double)x[i] - m);
-      const float sd = gs > 1 ? (float)sqrt(q / (gs - 1)) : __builtin_nanf("");
+      float sd, mx, m;
+      group_stats(scores + (int64_t)g * gs, gs, sd, mx, m);
       g_std[g] = sd;
       g_max[g] = mx;
-      g_mean[g] = (float)m;
+      g_mean[g] = m;
       a_std += sd;
       a_max += mx;
-      a_mean += (float)m;
+      a_mean += m;
       const float kf = type == 1 ? -sd : sd;
       key[g] = ((uint64_t)orderable(kf) << 32) | (uint64_t)(0xffffffffu - (uint32_t)g);
     } else {
@@ -222,6 +229,114 @@ __global__ __launch_bounds__(kFilterThreads) void filter_kernel(const float* __r
   }
 }
 
+// G > kFilterMaxG (no LDS sort): the group statistics in parallel, then one workgroup selects
+// the same set the sort would — the k largest (key, -index) pairs — by a 4-pass radix select
+// of the threshold key over LDS histograms, and takes the tied groups at the threshold in
+// ascending index order with a block-wide prefix count.  The reductions are fp64 as above.
+__global__ __launch_bounds__(kBlock) void filter_stats_kernel(const float* __restrict__ scores, int G, int gs,
+                                                              float* __restrict__ g_std, float* __restrict__ g_max,
+                                                              float* __restrict__ g_mean) {
+  const int g = blockIdx.x * kBlock + threadIdx.x;
+  if (g >= G) return;
+  float sd, mx, m;
+  group_stats(scores + (int64_t)g * gs, gs, sd, mx, m);
+  g_std[g] = sd;
+  g_max[g] = mx;
+  g_mean[g] = m;
+}
+
+__device__ __forceinline__ uint32_t filter_key(const float* g_std, int g, int type) {
+  const float sd = g_std[g];
+  return orderable(type == 1 ? -sd : sd);
+}
+
+__global__ __launch_bounds__(kFilterThreads) void filter_select_kernel(int G, int k, int type,
+                                                                       const float* __restrict__ g_std,
+                                                                       const float* __restrict__ g_max,
+                                                                       const float* __restrict__ g_mean,
+                                                                       uint8_t* __restrict__ keep,
+                                                                       double* __restrict__ metrics) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t sel[2];  // chosen bin, keys still to take below it
+  __shared__ uint32_t wcount[kFilterThreads / 64];
+  __shared__ double red[6][kFilterThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // radix select of the threshold T: #(key > T) < k <= #(key >= T)
+  uint32_t prefix = 0, pmask = 0, need = (uint32_t)k;
+  for (int shift = 24; shift >= 0 && k > 0; shift -= 8) {
+    for (int i = tid; i < 256; i += kFilterThreads) hist[i] = 0;
+    __syncthreads();
+    for (int g = tid; g < G; g += kFilterThreads) {
+      const uint32_t key = filter_key(g_std, g, type);
+      if ((key & pmask) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t cum = 0;
+      int b = 255;
+      for (; b > 0; --b) {
+        if (cum + hist[b] >= need) break;
+        cum += hist[b];
+      }
+      sel[0] = (uint32_t)b;
+      sel[1] = need - cum;
+    }
+    __syncthreads();
+    prefix |= sel[0] << shift;
+    pmask |= 255u << shift;
+    need = sel[1];
+    __syncthreads();
+  }
+  // keep = key > T, or key == T among the first `need` such groups in index order
+  double c_std = 0, c_max = 0, c_mean = 0, a_std = 0, a_max = 0, a_mean = 0;
+  uint32_t base = 0;
+  for (int g0 = 0; g0 < G; g0 += kFilterThreads) {
+    const int g = g0 + tid;
+    uint32_t key = 0;
+    bool eq = false;
+    if (g < G) {
+      key = filter_key(g_std, g, type);
+      eq = k > 0 && key == prefix;
+      a_std += g_std[g];
+      a_max += g_max[g];
+      a_mean += g_mean[g];
+    }
+    const uint64_t bal = __ballot(eq);
+    const uint32_t below = (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wcount[w] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t before = base, total = 0;
+    for (int i = 0; i < kFilterThreads / 64; ++i) {
+      if (i < w) before += wcount[i];
+      total += wcount[i];
+    }
+    if (g < G) {
+      const bool kp = k > 0 && (key > prefix || (eq && before + below < need));
+      keep[g] = kp ? 1 : 0;
+      if (kp) {
+        c_std += g_std[g];
+        c_max += g_max[g];
+        c_mean += g_mean[g];
+      }
+    }
+    base += total;
+    __syncthreads();
+  }
+  double v[6] = {a_std, a_max, a_mean, c_std, c_max, c_mean};
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const double t = wave_sum(v[j]);
+    if (lane == 0) red[j][w] = t;
+  }
+  __syncthreads();
+  if (tid < 6) {
+    double t = 0;
+    for (int i = 0; i < kFilterThreads / 64; ++i) t += red[tid][i];
+    const double d = tid < 3 ? (double)G : (double)k;
+    metrics[tid] = (float)(t / d);  // torch f32 .mean()
+  }
+}
+
 // score_tensor[:, -1] + penalty in f32 (ctx_manager.py:194-217)
 __device__ __forceinline__ float env_x(const rmi_episode_t& ep, int64_t i) {
   return (float)env_totals<false>(ep, i).score + (float)ep.penalty[i];
@@ -239,6 +354,7 @@ __global__ __launch_bounds__(kBlock) void finalize_kernel(rmi_episode_t ep, cons
   const int g = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
   if (g >= G) return;
   const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
+  if (n <= 0 || lo < 0 || hi > ep.B) return;  // malformed segments are never read past [0, B)
   double s = 0.0;
   float x0 = 0.0f;
   for (int i = lo + lane; i < hi; i += 64) {
@@ -313,7 +429,7 @@ RMI_API int rmi_group_normalize(const float* score, const float* pen, const int3
   if (G >= B) method = RMI_NORM_IDENTITY;
   const int per = kBlock / 64;
   hipLaunchKernelGGL(group_normalize_kernel, dim3((G + per - 1) / per), dim3(kBlock), 0, as_stream(stream), score,
-                     pen, seg, G, method, out);
+                     pen, seg, G, B, method, out);
   return launch_status();
 }
 
@@ -328,17 +444,26 @@ RMI_API int rmi_row_sum(const float* x, int64_t B, int64_t L, float* out, rmi_st
   return launch_status();
 }
 
-RMI_API int rmi_filter_groups(const float* scores, int32_t G, int32_t gs, double ratio, int32_t type, float* g_std,
-                              float* g_max, float* g_mean, uint8_t* keep, double* metrics, rmi_stream_t stream) {
+RMI_API int rmi_filter_groups(const float* scores, int64_t n, int32_t G, int32_t gs, double ratio, int32_t type,
+                              float* g_std, float* g_max, float* g_mean, uint8_t* keep, double* metrics,
+                              rmi_stream_t stream) {
   using namespace rmi;
   if (!scores || !g_std || !g_max || !g_mean || !keep || !metrics || G <= 0 || gs <= 0) return RMI_EINVAL;
-  if (G > kFilterMaxG) return RMI_EUNSUP;
+  if (n != (int64_t)G * gs) return RMI_EINVAL;  // rm_scores.view(num_groups, group_size) raises
   if (type != 0 && type != 1) return RMI_EINVAL;
   int k = (ratio == 1.0) ? G : (int)(ratio * (double)G);  // int(rollout_filter_ratio * num_groups)
   if (k < 0) k = 0;
   if (k > G) k = G;
-  hipLaunchKernelGGL(filter_kernel, dim3(1), dim3(kFilterThreads), 0, as_stream(stream), scores, G, gs, k, type,
-                     g_std, g_max, g_mean, keep, metrics);
+  hipStream_t s = as_stream(stream);
+  if (G <= kFilterMaxG) {
+    hipLaunchKernelGGL(filter_kernel, dim3(1), dim3(kFilterThreads), 0, s, scores, G, gs, k, type, g_std, g_max,
+                       g_mean, keep, metrics);
+  } else {
+    hipLaunchKernelGGL(filter_stats_kernel, dim3((unsigned)((G + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, scores,
+                       G, gs, g_std, g_max, g_mean);
+    hipLaunchKernelGGL(filter_select_kernel, dim3(1), dim3(kFilterThreads), 0, s, G, k, type, g_std, g_max, g_mean,
+                       keep, metrics);
+  }
   return launch_status();
 }
 

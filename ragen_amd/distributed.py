@@ -15,14 +15,18 @@ needs no collective.  The real exchange steps after it are:
     contiguous buffer by construction) in ONE all-gather (``gather_episode``), plus optional
     fixed-shape per-env rows (``gather_rollout``).
 """
-from typing import Dict, Tuple
+from typing import Callable, Dict, Tuple
 
 import torch
 import torch.distributed as dist
 
 
+def initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def world() -> Tuple[int, int]:
-    if dist.is_available() and dist.is_initialized():
+    if initialized():
         return dist.get_world_size(), dist.get_rank()
     return 1, 0
 
@@ -34,21 +38,33 @@ def shard_groups(n_groups: int, world_size: int, rank: int) -> Tuple[int, int]:
     return lo, hi - lo
 
 
-def all_gather_rows(x: torch.Tensor) -> torch.Tensor:
-    """Concatenate every rank's [n_r, ...] rows in rank order (n_r may differ by rank)."""
-    W, _ = world()
-    if W == 1:
-        return x
-    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+def _staged(x: torch.Tensor) -> torch.Tensor:
+    """gloo moves host memory: a GPU tensor goes through a host copy (RCCL takes it directly)."""
+    if x.is_cuda and dist.get_backend() == "gloo":
+        return x.cpu()
+    return x
+
+
+def all_gather_rows(x: torch.Tensor, with_offset: bool = False):
+    """Concatenate every rank's [n_r, ...] rows in rank order (n_r may differ by rank).
+    Whenever a process group exists the collective runs (also at world size 1, so the one-GPU
+    tests exercise the RCCL path); without one the local rows are returned.
+    with_offset: -> (rows, this rank's first row in the result)."""
+    if not initialized():
+        return (x, 0) if with_offset else x
+    W, rank = world()
+    xs = _staged(x.contiguous())
+    n = torch.tensor([xs.shape[0]], dtype=torch.int64, device=xs.device)
     sizes = [torch.zeros_like(n) for _ in range(W)]
     dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
+    sizes = [int(s) for s in torch.cat(sizes).cpu().tolist()]
     m = max(sizes)
-    pad = torch.zeros((m,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-    pad[:x.shape[0]] = x
+    pad = torch.zeros((m,) + tuple(xs.shape[1:]), dtype=xs.dtype, device=xs.device)
+    pad[:xs.shape[0]] = xs
     bufs = [torch.empty_like(pad) for _ in range(W)]
     dist.all_gather(bufs, pad)
-    return torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0)
+    out = torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0).to(x.device)
+    return (out, sum(sizes[:rank])) if with_offset else out
 
 
 def global_whiten_stats(row_stats: torch.Tensor) -> torch.Tensor:
@@ -56,10 +72,24 @@ def global_whiten_stats(row_stats: torch.Tensor) -> torch.Tensor:
     return all_gather_rows(row_stats)
 
 
-def gather_group_scores(scores: torch.Tensor, group_size: int) -> torch.Tensor:
-    """Per-env trajectory scores of the local groups -> all groups' scores (global order)."""
+def gather_group_scores(scores: torch.Tensor, group_size: int, with_offset: bool = False):
+    """Per-env trajectory scores of the local groups -> all groups' scores (global order);
+    with_offset also returns the first global GROUP index of this rank."""
     assert scores.shape[0] % group_size == 0
-    return all_gather_rows(scores.view(-1, group_size)).reshape(-1)
+    rows, off = all_gather_rows(scores.view(-1, group_size), with_offset=True)
+    return (rows.reshape(-1), off) if with_offset else rows.reshape(-1)
+
+
+def global_filter(local_scores: torch.Tensor, group_size: int, select: Callable):
+    """The rollout filter over the GLOBAL batch (agent_trainer.py:461-500 ranks groups across all
+    of them): every rank gathers every group's scores, runs the same deterministic
+    ``select(all_scores, num_groups) -> (keep u8[G], metrics)`` and keeps its own slice.
+    -> (keep of the local groups, metrics)."""
+    all_scores, g0 = gather_group_scores(local_scores, group_size, with_offset=True)
+    G = all_scores.numel() // group_size
+    keep, metrics = select(all_scores, G)
+    n_local = local_scores.shape[0] // group_size
+    return keep[g0:g0 + n_local], metrics
 
 
 def gather_bytes(buf: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
@@ -67,7 +97,7 @@ def gather_bytes(buf: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     one all-gather.  ``out`` (u8, W*numel, preallocated) makes the call graph-capturable.
     Without a process group the local buffer is returned as a view."""
     flat = buf.reshape(-1)
-    if not (dist.is_available() and dist.is_initialized()):
+    if not initialized():
         return flat.view(1, -1)
     W = dist.get_world_size()
     n = flat.numel()

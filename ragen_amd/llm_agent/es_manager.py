@@ -9,6 +9,7 @@ for the whole turn, then reads back four small per-env vectors to build the dict
 ``step_tensor`` is the dict-free fast path (used by the benchmark's kernel variant).
 """
 import random
+import warnings
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -164,14 +165,17 @@ class EnvStateManager:
                     answers[i] = a
                 buf, alens = tg.batch.encode_answers(answers)
                 kw = {"answers": torch.from_numpy(buf).to(dev), "answer_len": torch.from_numpy(alens).to(dev)}
-            tg.batch.step_turn(t, ids_t, n_t, has_t, tg.max_actions_per_traj, self.format_penalty, **kw)
+            err = torch.zeros(B, dtype=torch.uint8, device=dev)
+            tg.batch.step_turn(t, ids_t, n_t, has_t, tg.max_actions_per_traj, self.format_penalty, err, **kw)
             ep = tg.batch.ep
             host = torch.stack([ep.flags.to(torch.int64), ep.num_actions.to(torch.int64),
-                                ep.turn_info[t].to(torch.int64), ep.turn_exec[t].to(torch.int64)]).cpu().numpy()
+                                ep.turn_info[t].to(torch.int64), ep.turn_exec[t].to(torch.int64),
+                                err.to(torch.int64)]).cpu().numpy()
+            self._raise_errors(tg, host[4], rows, gids)
             rw = ep.turn_reward[t].cpu().numpy()
             pen = ep.penalty.cpu().numpy()
             # one host copy per turn, as Python lists (numpy scalar indexing per env is slower)
-            flags, num_actions, info, n_exec = (x.tolist() for x in host)
+            flags, num_actions, info, n_exec = (x.tolist() for x in host[:4])
             rw, pen = rw.tolist(), pen.tolist()
             note = getattr(tg.batch, "note_executed", None)
             # the text observation of every env at once unless the env type renders per env
@@ -216,6 +220,26 @@ class EnvStateManager:
         # only not-done envs go back for generation, in input order (es_manager.py:168-169)
         rc = self.rollout_cache
         return [rc[g] for g in gids_all if g in still_active]
+
+    def _raise_errors(self, tg, err, rows, gids):
+        """Per-env error bits of the turn launch, as the reference would surface them: an action
+        id outside the env's space is the AssertionError of bandit/env.py:63, a grid index numpy
+        rejects is gym_sokoban's IndexError.  (The kernel leaves such an env untouched; the
+        reference raises inside its per-env loop.)  A Countdown answer outside the evaluator's
+        grammar was scored 'not correct' (DESIGN §5 deviation 4): counted and warned about."""
+        if not err.any():
+            return
+        bad = [(g, int(err[i])) for i, g in zip(rows, gids) if err[i]]
+        if any(e & _lib.ERR_ACTION for _, e in bad):
+            raise AssertionError(f"env {next(g for g, e in bad if e & _lib.ERR_ACTION)}: invalid action")
+        if any(e & (_lib.ERR_INDEX | _lib.ERR_STATE) for _, e in bad):
+            raise IndexError(f"env {next(g for g, e in bad if e & (_lib.ERR_INDEX | _lib.ERR_STATE))}: "
+                             "index out of range in the env step")
+        n_unsup = sum(1 for _, e in bad if e & _lib.ERR_UNSUP)
+        if n_unsup:
+            tg.batch.unsupported_answers = getattr(tg.batch, "unsupported_answers", 0) + n_unsup
+            warnings.warn(f"{n_unsup} Countdown answers outside the device evaluator's grammar were scored as not "
+                          "correct (ragen_amd DESIGN §5, deviation 4)", RuntimeWarning)
 
     def step_tensor(self, actions: torch.Tensor, n_actions: torch.Tensor, has_input: Optional[torch.Tensor] = None,
                     tag_index: int = 0, **kw):

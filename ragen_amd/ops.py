@@ -20,17 +20,25 @@ def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
-def _stream(device=None):
+def _stream(device):
+    """torch's current stream ON THE TENSORS' DEVICE (not on the process's current device)."""
     return torch.cuda.current_stream(device).cuda_stream
 
 
 def _dev(*ts):
+    """Validate GPU tensors (contiguous, one device) -> that device (None if all are None)."""
+    dev = None
     for t in ts:
         if t is not None:
             if not t.is_cuda:
                 raise ValueError("ragen_amd ops take GPU tensors (the engine has no CPU path)")
             if not t.is_contiguous():
                 raise ValueError("ragen_amd ops take contiguous tensors")
+            if dev is None:
+                dev = t.device
+            elif t.device != dev:
+                raise ValueError(f"ragen_amd ops take tensors on one device, got {dev} and {t.device}")
+    return dev
 
 
 def _dt(t, dtype, name):
@@ -108,6 +116,10 @@ class EpisodeState:
     def T(self):
         return self.turn_reward.shape[0]
 
+    @property
+    def device(self):
+        return self.flags.device
+
     def struct(self) -> _lib.Episode:
         _dev(self.num_actions, self.flags, self.n_turns, self.penalty, self.turn_reward, self.turn_info,
              self.turn_exec)
@@ -128,7 +140,7 @@ def turn_struct(turn: int, actions: torch.Tensor, n_actions: torch.Tensor, has_i
 
 # ------------------------------------------------------------------------ env steps
 def sokoban_step_turn(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn, err: Optional[torch.Tensor] = None):
-    check(lib().rmi_sokoban_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_sokoban_step_turn")
+    check(lib().rmi_sokoban_step_turn(env, ep.struct(), turn, _ptr(err), _stream(ep.device)), "rmi_sokoban_step_turn")
 
 
 def finalize_struct(group_size: int, method: str, norm: Optional[torch.Tensor],
@@ -151,12 +163,12 @@ def sokoban_step_turn_finalize(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.T
                                err: Optional[torch.Tensor] = None):
     """The rollout's last turn + rollout_finalize (uniform groups of fin.group_size) in one launch.
     Groups that would straddle a wave take the two launches instead (same results)."""
-    rc = lib().rmi_sokoban_step_turn_finalize(env, ep.struct(), turn, _ptr(err), fin, _stream())
+    rc = lib().rmi_sokoban_step_turn_finalize(env, ep.struct(), turn, _ptr(err), fin, _stream(ep.device))
     if rc == _lib.RMI_EUNSUP and fin.group_size >= 1 and ep.B % fin.group_size == 0:
         sokoban_step_turn(env, ep, turn, err)
         seg = torch.arange(0, ep.B + 1, fin.group_size, dtype=torch.int32, device=ep.flags.device)
         check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, fin.method, fin.metrics,
-                                         fin.score, fin.pen, fin.norm, _stream()), "rmi_rollout_finalize")
+                                         fin.score, fin.pen, fin.norm, _stream(ep.device)), "rmi_rollout_finalize")
         return
     check(rc, "rmi_sokoban_step_turn_finalize")
 
@@ -169,13 +181,13 @@ def sokoban_step_turn_first(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn
     _dt(init_state, torch.uint8, "init_state")
     _dt(init_player, torch.int8, "init_player")
     check(lib().rmi_sokoban_step_turn_first(env, ep.struct(), turn, _ptr(init_state), _ptr(init_player), _ptr(err),
-                                            _stream()), "rmi_sokoban_step_turn_first")
+                                            _stream(ep.device)), "rmi_sokoban_step_turn_first")
 
 
 def sokoban_reset(env: _lib.Sokoban, ep: EpisodeState, init_state: torch.Tensor, init_player: torch.Tensor):
     """Fused device reset from the generated rooms (state, player, counters, episode record)."""
     _dev(init_state, init_player)
-    check(lib().rmi_sokoban_reset(env, ep.struct(), _ptr(init_state), _ptr(init_player), _stream()),
+    check(lib().rmi_sokoban_reset(env, ep.struct(), _ptr(init_state), _ptr(init_player), _stream(ep.device)),
           "rmi_sokoban_reset")
 
 
@@ -183,7 +195,7 @@ def frozenlake_reset(env: _lib.FrozenLake, ep: EpisodeState, init_desc: torch.Te
                      init_rng: torch.Tensor):
     """Fused device reset from the generated maps (desc, start state, seeded PCG64, record)."""
     _dev(init_desc, init_s, init_rng)
-    check(lib().rmi_frozenlake_reset(env, ep.struct(), _ptr(init_desc), _ptr(init_s), _ptr(init_rng), _stream()),
+    check(lib().rmi_frozenlake_reset(env, ep.struct(), _ptr(init_desc), _ptr(init_s), _ptr(init_rng), _stream(ep.device)),
           "rmi_frozenlake_reset")
 
 
@@ -202,7 +214,7 @@ def pcg64_seed(seeds: torch.Tensor, draws: int = 0, rng: Optional[torch.Tensor] 
     last = torch.empty(n, dtype=torch.float64, device=seeds.device)
     err = torch.empty(n, dtype=torch.uint8, device=seeds.device)
     check(lib().rmi_pcg64_seed(_ptr(seeds), n, int(draws), _ptr(rng), n, _ptr(last), _ptr(err),
-                               _stream()), "rmi_pcg64_seed")
+                               _stream(seeds.device)), "rmi_pcg64_seed")
     if n and bool(err.any()):
         raise ValueError("expected non-negative integer seeds")
     return rng, last
@@ -213,12 +225,12 @@ def frozenlake_step_turn_finalize(env: _lib.FrozenLake, ep: EpisodeState, turn: 
     """frozenlake_step_turn + rollout_finalize (uniform contiguous groups) in one launch.  Groups
     that would straddle the one-wave workgroup take the two launches instead (same results)."""
     _dev(err)
-    rc = lib().rmi_frozenlake_step_turn_finalize(env, ep.struct(), turn, _ptr(err), fin, _stream())
+    rc = lib().rmi_frozenlake_step_turn_finalize(env, ep.struct(), turn, _ptr(err), fin, _stream(ep.device))
     if rc == _lib.RMI_EUNSUP and fin.group_size >= 1 and ep.B % fin.group_size == 0:
         frozenlake_step_turn(env, ep, turn, err)
         seg = torch.arange(0, ep.B + 1, fin.group_size, dtype=torch.int32, device=ep.flags.device)
         check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, fin.method, fin.metrics,
-                                         fin.score, fin.pen, fin.norm, _stream()), "rmi_rollout_finalize")
+                                         fin.score, fin.pen, fin.norm, _stream(ep.device)), "rmi_rollout_finalize")
         return
     check(rc, "rmi_frozenlake_step_turn_finalize")
 
@@ -228,16 +240,16 @@ def frozenlake_step_turn_first(env: _lib.FrozenLake, ep: EpisodeState, turn: _li
     """frozenlake_reset(init_*) + frozenlake_step_turn(turn) in one launch (a fresh episode's first turn)."""
     _dev(init_desc, init_s, init_rng, err)
     check(lib().rmi_frozenlake_step_turn_first(env, ep.struct(), turn, _ptr(init_desc), _ptr(init_s), _ptr(init_rng),
-                                               _ptr(err), _stream()), "rmi_frozenlake_step_turn_first")
+                                               _ptr(err), _stream(ep.device)), "rmi_frozenlake_step_turn_first")
 
 
 def frozenlake_step_turn(env: _lib.FrozenLake, ep: EpisodeState, turn: _lib.Turn,
                          err: Optional[torch.Tensor] = None):
-    check(lib().rmi_frozenlake_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_frozenlake_step_turn")
+    check(lib().rmi_frozenlake_step_turn(env, ep.struct(), turn, _ptr(err), _stream(ep.device)), "rmi_frozenlake_step_turn")
 
 
 def bandit_step_turn(env: _lib.Bandit, ep: EpisodeState, turn: _lib.Turn, err: Optional[torch.Tensor] = None):
-    check(lib().rmi_bandit_step_turn(env, ep.struct(), turn, _ptr(err), _stream()), "rmi_bandit_step_turn")
+    check(lib().rmi_bandit_step_turn(env, ep.struct(), turn, _ptr(err), _stream(ep.device)), "rmi_bandit_step_turn")
 
 
 def countdown_step_turn(env: _lib.Countdown, ep: EpisodeState, turn: _lib.Turn, answers: torch.Tensor,
@@ -246,7 +258,7 @@ def countdown_step_turn(env: _lib.Countdown, ep: EpisodeState, turn: _lib.Turn, 
     _dt(answers, torch.uint8, "answers")
     _dt(answer_len, torch.int32, "answer_len")
     check(lib().rmi_countdown_step_turn(env, ep.struct(), turn, _ptr(answers), _ptr(answer_len), answers.shape[-1],
-                                        _ptr(err), _stream()), "rmi_countdown_step_turn")
+                                        _ptr(err), _stream(ep.device)), "rmi_countdown_step_turn")
 
 
 def countdown_reward(env: _lib.Countdown, answers: torch.Tensor, answer_len: torch.Tensor):
@@ -258,7 +270,7 @@ def countdown_reward(env: _lib.Countdown, answers: torch.Tensor, answer_len: tor
     flags = torch.empty(n, dtype=torch.uint8, device=dev)
     err = torch.empty(n, dtype=torch.uint8, device=dev)
     check(lib().rmi_countdown_reward(env, _ptr(answers), _ptr(answer_len), answers.shape[-1], n, _ptr(reward),
-                                     _ptr(flags), _ptr(err), _stream()), "rmi_countdown_reward")
+                                     _ptr(flags), _ptr(err), _stream(answers.device)), "rmi_countdown_reward")
     return reward, flags, err
 
 
@@ -281,7 +293,7 @@ def generate_sokoban_rooms(seeds, H: int, W: int, num_boxes: int, search_depth: 
 # ------------------------------------------------------------------- episode reductions
 def rollout_metrics(ep: EpisodeState) -> torch.Tensor:
     out = torch.empty(ep.B, 4, dtype=torch.float64, device=ep.flags.device)
-    check(lib().rmi_rollout_metrics(ep.struct(), _ptr(out), _stream()), "rmi_rollout_metrics")
+    check(lib().rmi_rollout_metrics(ep.struct(), _ptr(out), _stream(ep.device)), "rmi_rollout_metrics")
     return out
 
 
@@ -289,7 +301,7 @@ def trajectory_scores(ep: EpisodeState):
     dev = ep.flags.device
     score = torch.empty(ep.B, dtype=torch.float32, device=dev)
     pen = torch.empty(ep.B, dtype=torch.float32, device=dev)
-    check(lib().rmi_trajectory_scores(ep.struct(), _ptr(score), _ptr(pen), _stream()), "rmi_trajectory_scores")
+    check(lib().rmi_trajectory_scores(ep.struct(), _ptr(score), _ptr(pen), _stream(ep.device)), "rmi_trajectory_scores")
     return score, pen
 
 
@@ -301,7 +313,7 @@ def rollout_finalize(ep: EpisodeState, seg: torch.Tensor, method: str, norm: tor
         raise ValueError(f"Invalid normalization method: {method}")
     _dev(seg, norm, metrics, score, pen)
     check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, _lib.NORM_METHODS[method],
-                                     _ptr(metrics), _ptr(score), _ptr(pen), _ptr(norm), _stream()),
+                                     _ptr(metrics), _ptr(score), _ptr(pen), _ptr(norm), _stream(ep.device)),
           "rmi_rollout_finalize")
     return norm
 
@@ -310,13 +322,13 @@ def group_normalize(score: torch.Tensor, pen: Optional[torch.Tensor], seg: torch
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if method not in _lib.NORM_METHODS:
         raise ValueError(f"Invalid normalization method: {method}")
-    _dev(score, pen, seg)
+    _dev(score, pen)
     _dt(score, torch.float32, "score")
     _dt(pen, torch.float32, "pen")
-    _dt(seg, torch.int32, "seg")
+    seg = segments(seg, score.numel(), score.device)
     out = torch.empty_like(score) if out is None else out
     check(lib().rmi_group_normalize(_ptr(score), _ptr(pen), _ptr(seg), seg.numel() - 1, score.numel(),
-                                    _lib.NORM_METHODS[method], _ptr(out), _stream()), "rmi_group_normalize")
+                                    _lib.NORM_METHODS[method], _ptr(out), _stream(score.device)), "rmi_group_normalize")
     return out
 
 
@@ -325,14 +337,17 @@ def filter_groups(scores: torch.Tensor, num_groups: int, group_size: int, ratio:
         raise ValueError(f"Invalid rollout filter type: {ftype}")
     _dev(scores)
     _dt(scores, torch.float32, "scores")
+    if scores.numel() != num_groups * group_size:
+        raise RuntimeError(f"shape '[{num_groups}, {group_size}]' is invalid for input of size {scores.numel()}")
     dev = scores.device
     g_std = torch.empty(num_groups, dtype=torch.float32, device=dev)
     g_max = torch.empty_like(g_std)
     g_mean = torch.empty_like(g_std)
     keep = torch.empty(num_groups, dtype=torch.uint8, device=dev)
     metrics = torch.empty(6, dtype=torch.float64, device=dev)
-    check(lib().rmi_filter_groups(_ptr(scores), num_groups, group_size, float(ratio), 0 if ftype == "std" else 1,
-                                  _ptr(g_std), _ptr(g_max), _ptr(g_mean), _ptr(keep), _ptr(metrics), _stream()),
+    check(lib().rmi_filter_groups(_ptr(scores), scores.numel(), num_groups, group_size, float(ratio),
+                                  0 if ftype == "std" else 1,
+                                  _ptr(g_std), _ptr(g_max), _ptr(g_mean), _ptr(keep), _ptr(metrics), _stream(scores.device)),
           "rmi_filter_groups")
     return keep, metrics, (g_std, g_max, g_mean)
 
@@ -341,7 +356,7 @@ def row_sum(x: torch.Tensor) -> torch.Tensor:
     _dev(x)
     _dt(x, torch.float32, "x")
     out = torch.empty(x.shape[0], dtype=torch.float32, device=x.device)
-    check(lib().rmi_row_sum(_ptr(x), x.shape[0], x.shape[1], _ptr(out), _stream()), "rmi_row_sum")
+    check(lib().rmi_row_sum(_ptr(x), x.shape[0], x.shape[1], _ptr(out), _stream(x.device)), "rmi_row_sum")
     return out
 
 
@@ -368,7 +383,7 @@ def _render(fn, env_struct, B: int, cells: int, rows: int, lookup, device, out=N
     else:
         out = torch.empty(B, stride, dtype=torch.uint8, device=device)
         n = torch.empty(B, dtype=torch.int32, device=device)
-    check(fn(env_struct, B, gb.ctypes.data, gl.ctypes.data, _ptr(out), stride, _ptr(n), _stream()), fn.__name__)
+    check(fn(env_struct, B, gb.ctypes.data, gl.ctypes.data, _ptr(out), stride, _ptr(n), _stream(out.device)), fn.__name__)
     return out, n
 
 
@@ -468,7 +483,7 @@ def parse_actions(cfg: _lib.ParseCfg, text: torch.Tensor, text_len: torch.Tensor
         err = torch.zeros(B, dtype=torch.uint8, device=dev)
     check(lib().rmi_parse_actions(ctypes.byref(cfg), _ptr(text), _ptr(text_len), B, stride, _ptr(sel), _ptr(actions),
                                   _ptr(n_actions), _ptr(spans), _ptr(at), _ptr(al), int(action_text_len), _ptr(err),
-                                  _stream()), "rmi_parse_actions")
+                                  _stream(text.device)), "rmi_parse_actions")
     return {"actions": actions, "n_actions": n_actions, "spans": spans, "action_text": at, "action_len": al,
             "err": err}
 
@@ -558,7 +573,7 @@ def detokenize(ids: torch.Tensor, vocab: VocabTable, stride: int, n_ids: Optiona
         err = torch.zeros(B, dtype=torch.uint8, device=dev)
     V = vocab.skip.numel()
     check(lib().rmi_detokenize(_ptr(ids), B, R, _ptr(n_ids), _ptr(vocab.off), _ptr(vocab.data), vocab.data.numel(),
-                               V, _ptr(vocab.skip), _ptr(out), stride, _ptr(n), _ptr(err), _stream()),
+                               V, _ptr(vocab.skip), _ptr(out), stride, _ptr(n), _ptr(err), _stream(ids.device)),
           "rmi_detokenize")
     return out, n, err
 
@@ -589,12 +604,14 @@ def masks_and_scores(ids: torch.Tensor, special_token: int, reward_token: int, s
              | (_lib.MS_ROLL if roll else 0))
     check(lib().rmi_masks_and_scores(_ptr(ids), B, S, int(special_token), int(reward_token), _ptr(scores.contiguous()),
                                      _ptr(n_scores), T, int(n_slots), flags, _ptr(score), _ptr(lm), _ptr(rm), _ptr(err),
-                                     _stream()), "rmi_masks_and_scores")
+                                     _stream(ids.device)), "rmi_masks_and_scores")
     return score, lm, rm, err
 
 
 # ------------------------------------------------------------------------ advantages
 def _mask_u8(mask: torch.Tensor) -> torch.Tensor:
+    """A boolean mask as u8 bytes.  The kernels read any nonzero byte as 1 (RAGEN passes a bool
+    loss_mask, ctx_manager.py:46-49); a float mask is binarised the same way (nonzero = in)."""
     if mask.dtype == torch.bool:
         return mask.view(torch.uint8)
     if mask.dtype == torch.uint8:
@@ -602,53 +619,150 @@ def _mask_u8(mask: torch.Tensor) -> torch.Tensor:
     return (mask != 0).to(torch.uint8)
 
 
+def _rows(r, *others, names=()):
+    if r.dim() != 2:
+        raise ValueError(f"expected a [B, L] tensor, got shape {tuple(r.shape)}")
+    for t, nm in zip(others, names):
+        if t is not None and tuple(t.shape) != tuple(r.shape):
+            raise ValueError(f"{nm} must have shape {tuple(r.shape)}, got {tuple(t.shape)}")
+    return r.shape
+
+
+def _row_stats(row_stats, B):
+    if row_stats is not None:
+        _dt(row_stats, torch.float64, "row_stats")
+        if tuple(row_stats.shape) != (B, 3):
+            raise ValueError(f"row_stats must be f64[{B}, 3], got {tuple(row_stats.shape)}")
+
+
 def gae(r, v, mask, gamma, lam, variant="legacy", row_stats=None):
-    _dev(r, v, mask)
+    """verl compute_gae_advantage_return before whitening (App. A.4): -> (adv, ret) f32[B, L];
+    row_stats f64[B, 3] (optional) receives the per-row whitening partials."""
+    if variant not in ("legacy", "masked"):
+        raise ValueError(f"GAE variant must be 'legacy' or 'masked', got {variant!r}")
+    _dev(r, v, mask, row_stats)
     _dt(r, torch.float32, "token_level_rewards")
     _dt(v, torch.float32, "values")
+    B, L = _rows(r, v, mask, names=("values", "response_mask"))
+    _row_stats(row_stats, B)
     m = _mask_u8(mask).contiguous()
-    B, L = r.shape
     adv = torch.empty_like(r)
     ret = torch.empty_like(r)
     check(lib().rmi_gae(_ptr(r), _ptr(v), _ptr(m), B, L, float(gamma), float(lam), 0 if variant == "legacy" else 1,
-                        _ptr(adv), _ptr(ret), _ptr(row_stats), _stream()), "rmi_gae")
+                        _ptr(adv), _ptr(ret), _ptr(row_stats), _stream(r.device)), "rmi_gae")
     return adv, ret
 
 
-def bilevel_gae(r, v, mask, gamma, lam, high_level_gamma, row_stats=None, check_errors=True):
-    _dev(r, v, mask)
+def bilevel_gae(r, v, mask, gamma, lam, high_level_gamma, row_stats=None, check_errors=True, err=None):
+    """compute_bi_level_gae_advantage_return before whitening (core_algos.py:4-88).  Rows where
+    the reference raises IndexError (core_algos.py:79) are flagged in err u8[B]; with
+    check_errors the flag is read back (one sync) and raised as IndexError."""
+    _dev(r, v, mask, row_stats, err)
     _dt(r, torch.float32, "token_level_rewards")
     _dt(v, torch.float32, "values")
+    B, L = _rows(r, v, mask, names=("values", "loss_mask"))
+    _row_stats(row_stats, B)
     m = _mask_u8(mask).contiguous()
-    B, L = r.shape
     adv = torch.empty_like(r)
     ret = torch.empty_like(r)
-    err = torch.empty(B, dtype=torch.uint8, device=r.device)
+    if err is None:
+        err = torch.empty(B, dtype=torch.uint8, device=r.device)
+    elif err.dtype != torch.uint8 or err.shape != (B,):
+        raise ValueError(f"err must be u8[{B}]")
     check(lib().rmi_bilevel_gae(_ptr(r), _ptr(v), _ptr(m), B, L, float(gamma), float(lam), float(high_level_gamma),
-                                _ptr(adv), _ptr(ret), _ptr(row_stats), _ptr(err), _stream()), "rmi_bilevel_gae")
+                                _ptr(adv), _ptr(ret), _ptr(row_stats), _ptr(err), _stream(r.device)), "rmi_bilevel_gae")
     if check_errors and bool(err.any()):
         raise IndexError("index out of range: last loss-mask position of a row carries no reward "
                          "(reference core_algos.py:79)")
     return adv, ret
 
 
+WHITEN_OK, WHITEN_EMPTY, WHITEN_ONE = 0, 1, 2
+
+
+def whiten_status(scratch: torch.Tensor) -> torch.Tensor:
+    """The i32 status a whitening launch left in its scratch (device scalar; no sync):
+    0 ok, 1 mask sum 0, 2 mask sum 1 (verl's masked_var raises ValueError for 1 and 2)."""
+    return scratch[8:12].view(torch.int32)
+
+
+def raise_whiten_status(code: int):
+    if code == WHITEN_EMPTY:
+        raise ValueError("At least one element in the mask has to be 1.")
+    if code == WHITEN_ONE:
+        raise ValueError("The sum of the mask is one, which can cause a division by zero.")
+
+
 def masked_whiten_(x, mask, row_stats=None):
+    """verl masked_whiten in place on x f32[B, L] (mean / unbiased var over the masked elements,
+    applied to every element).  row_stats f64[B, 3] from rmi_gae saves the stats pass.
+    -> (x, scratch); whiten_status(scratch) holds verl's error cases (no sync here)."""
     _dev(x, mask, row_stats)
+    _dt(x, torch.float32, "values")
+    B, L = _rows(x, mask, names=("mask",))
+    _row_stats(row_stats, B)
     m = _mask_u8(mask).contiguous()
-    B, L = x.shape
     nbytes = int(lib().rmi_whiten_scratch_bytes(B))
     scratch = torch.empty(nbytes, dtype=torch.uint8, device=x.device)
-    check(lib().rmi_masked_whiten(_ptr(x), _ptr(m), B, L, _ptr(row_stats), _ptr(scratch), _stream()),
+    check(lib().rmi_masked_whiten(_ptr(x), _ptr(m), B, L, _ptr(row_stats), _ptr(scratch), _stream(x.device)),
           "rmi_masked_whiten")
     return x, scratch
 
 
-def grpo_outcome(r, mask, seg, eps=1e-6, norm_by_std=True):
-    _dev(r, mask, seg)
+def whiten_row_stats(x, mask, out=None):
+    """Per-row fp64 whitening partials (sum, sum_sq, count) of x f32[B, L] over the mask."""
+    _dev(x, mask, out)
+    _dt(x, torch.float32, "values")
+    B, L = _rows(x, mask, names=("mask",))
+    out = torch.empty(B, 3, dtype=torch.float64, device=x.device) if out is None else out
+    _row_stats(out, B)
     m = _mask_u8(mask).contiguous()
-    B, L = r.shape
+    check(lib().rmi_whiten_row_stats(_ptr(x), _ptr(m), B, L, _ptr(out), _stream(x.device)), "rmi_whiten_row_stats")
+    return out
+
+
+def masked_whiten_stats_(x, stats):
+    """masked_whiten of this shard's rows x f32[B, L] with batch statistics from all shards:
+    stats f64[n, 3] = every rank's per-row partials in global row order (the multi-GPU form,
+    ragen_amd.distributed.global_whiten_stats).  -> (x, scratch) as masked_whiten_."""
+    _dev(x, stats)
+    _dt(x, torch.float32, "values")
+    _dt(stats, torch.float64, "stats")
+    if x.dim() != 2 or stats.dim() != 2 or stats.shape[1] != 3:
+        raise ValueError("x must be [B, L] and stats [n, 3]")
+    B, L = x.shape
+    scratch = torch.empty(64, dtype=torch.uint8, device=x.device)
+    check(lib().rmi_masked_whiten_stats(_ptr(x), B, L, _ptr(stats), stats.shape[0], _ptr(scratch),
+                                        _stream(x.device)), "rmi_masked_whiten_stats")
+    return x, scratch
+
+
+def segments(seg, B: int, device) -> torch.Tensor:
+    """Contiguous group segments as i32[G+1] on `device`.  Host segments (list / numpy / CPU
+    tensor) are validated (seg[0] == 0, non-decreasing, seg[-1] == B) before the upload; a
+    device tensor is taken as is (the kernels never read outside [0, B) either way)."""
+    if isinstance(seg, torch.Tensor) and seg.is_cuda:
+        _dt(seg, torch.int32, "seg")
+        if seg.dim() != 1 or seg.numel() < 1:
+            raise ValueError("seg must be a 1-D i32 tensor of G+1 offsets")
+        return seg.contiguous()
+    h = np.asarray(seg.cpu().numpy() if isinstance(seg, torch.Tensor) else seg, np.int64).reshape(-1)
+    if h.size < 1 or h[0] != 0 or h[-1] != B or (np.diff(h) < 0).any():
+        raise ValueError(f"seg must be non-decreasing offsets from 0 to B={B}")
+    return torch.from_numpy(h.astype(np.int32)).to(device)
+
+
+def grpo_outcome(r, mask, seg, eps=1e-6, norm_by_std=True):
+    """verl compute_grpo_outcome_advantage over contiguous row groups seg (App. A.4)."""
+    _dev(r, mask)
+    _dt(r, torch.float32, "token_level_rewards")
+    B, L = _rows(r, mask, names=("response_mask",))
+    seg = segments(seg, B, r.device)
+    if seg.device != r.device:
+        raise ValueError("seg must be on the rows' device")
+    m = _mask_u8(mask).contiguous()
     adv = torch.empty_like(r)
     ret = torch.empty_like(r)
     check(lib().rmi_grpo_outcome(_ptr(r), _ptr(m), B, L, _ptr(seg), seg.numel() - 1, float(eps), int(norm_by_std),
-                                 _ptr(adv), _ptr(ret), _stream()), "rmi_grpo_outcome")
+                                 _ptr(adv), _ptr(ret), _stream(r.device)), "rmi_grpo_outcome")
     return adv, ret

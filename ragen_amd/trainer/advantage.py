@@ -2,6 +2,7 @@
 agent_trainer.py:461-500, running on the GPU engine."""
 import torch
 
+from .. import distributed as rd
 from .. import ops
 from ..protocol import DataProto
 from . import core_algos
@@ -16,12 +17,19 @@ class AdvantageEstimator:
     RLOO = "rloo"
 
 
+def compute_response_mask(data: DataProto) -> torch.Tensor:
+    """verl compute_response_mask (the fallback of agent_trainer.py:61-62): the attention mask
+    over the response columns."""
+    response_length = data.batch["responses"].size(1)
+    return data.batch["attention_mask"][:, -response_length:]
+
+
 def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_repeat=1, multi_turn=False,
                       norm_adv_by_std_in_grpo=True, bi_level_gae=False, high_level_gamma=1.0):
     """agent_trainer.py:60-137 for the estimators of RAGEN's StarPO loop (GAE, bi-level GAE,
     GRPO).  REINFORCE++/REMAX/RLOO are verl estimators outside this engine's scope."""
     if "response_mask" not in data.batch:
-        data.batch["response_mask"] = data.batch["loss_mask"]
+        data.batch["response_mask"] = compute_response_mask(data)
     est = getattr(adv_estimator, "value", adv_estimator)
     if est == AdvantageEstimator.GAE:
         if bi_level_gae:
@@ -45,18 +53,33 @@ def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_re
     return data
 
 
+FILTER_METRICS = ("rollout/in_group_std", "rollout/in_group_max", "rollout/in_group_mean",
+                  "rollout/chosen_in_group_std", "rollout/chosen_in_group_max", "rollout/chosen_in_group_mean")
+
+
 def filter_rollout(batch: DataProto, num_groups: int, group_size: int, ratio: float, ftype: str):
     """_filter_rollout (agent_trainer.py:461-500): returns (filtered batch, metrics).
 
     Tie order among equal in-group std values: ascending group index (documented deviation:
-    torch.topk's choice among ties is implementation-defined)."""
-    dev = torch.device("cuda", torch.cuda.current_device())
-    rm = batch.batch["original_rm_scores"].to(dev, torch.float32).contiguous()
-    rows = ops.row_sum(rm)
-    keep, met, _ = ops.filter_groups(rows, num_groups, group_size, ratio, ftype)
-    metrics = dict(zip(["rollout/in_group_std", "rollout/in_group_max", "rollout/in_group_mean",
-                        "rollout/chosen_in_group_std", "rollout/chosen_in_group_max",
-                        "rollout/chosen_in_group_mean"], met.cpu().tolist()))
+    torch.topk's choice among ties is implementation-defined).  With a process group the
+    batch is this rank's shard: the groups are ranked over every rank's scores
+    (ragen_amd.distributed.global_filter), so the kept set equals the 1-GPU run's and
+    ``num_groups`` is the GLOBAL count (es_manager.train.env_groups), as in the reference."""
+    rm = batch.batch["original_rm_scores"]
+    dev = rm.device if rm.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    rows = ops.row_sum(rm.to(dev, torch.float32).contiguous())
+
+    def select(scores, G):
+        if G != num_groups:
+            raise RuntimeError(f"shape '[{num_groups}, {group_size}]' is invalid for input of size {scores.numel()}")
+        keep, met, _ = ops.filter_groups(scores, G, group_size, ratio, ftype)
+        return keep, met
+
+    if rd.initialized():
+        keep, met = rd.global_filter(rows, group_size, select)
+    else:
+        keep, met = select(rows, rows.numel() // group_size if rows.numel() % group_size == 0 else -1)
+    metrics = dict(zip(FILTER_METRICS, met.cpu().tolist()))
     if ratio == 1:
         return batch, metrics
     mask = keep.bool().unsqueeze(1).expand(-1, group_size).flatten().cpu()

@@ -1,89 +1,114 @@
 """Advantage estimators on the GPU engine — drop-ins for ragen/trainer/core_algos.py:4-92 and
 the verl functions RAGEN imports from it (App. A.4): same names, signatures and return
-values; tensors may arrive on the CPU (as in the reference) and are moved to the device.
+values.  Tensors may arrive on the CPU (as in the reference trainer, whose batch lives on the
+driver) and go back there; GPU tensors stay on their own device.
+
+No host synchronisation inside an estimator: the only wait is the copy of the results back to
+a CPU caller, and verl's error cases (mask sum 0 or 1 -> ValueError; bi-level IndexError,
+core_algos.py:79) are read from the device after that copy.  Results that stay on the device
+are not checked (reading the flag would be the sync the engine avoids).
+
+With a process group initialised (one rank per GPU, ragen_amd.distributed) the whitening
+statistics are batch-global: every rank all-gathers the per-row fp64 partials and reduces
+them in global row order, so a sharded batch whitens exactly like the whole batch.
 """
 from collections import OrderedDict
 
 import numpy as np
 import torch
 
+from .. import distributed as rd
 from .. import ops
 
 
-def _dev(x, device):
-    return x.to(device).contiguous()
-
-
-def _device():
+def _device(*xs):
+    for x in xs:
+        if isinstance(x, torch.Tensor) and x.is_cuda:
+            return x.device
     return torch.device("cuda", torch.cuda.current_device())
 
 
+def _dev(x, device):
+    return x.to(device, non_blocking=True).contiguous()
+
+
+def _whiten(adv, mask, row_stats):
+    """In place; -> device status scalar (ops.whiten_status)."""
+    if rd.initialized():
+        _, scratch = ops.masked_whiten_stats_(adv, rd.global_whiten_stats(row_stats))
+    else:
+        _, scratch = ops.masked_whiten_(adv, mask, row_stats)
+    return ops.whiten_status(scratch)
+
+
+def _back(out_device, tensors, status=None, err=None):
+    """Results to the caller's device.  For a CPU caller the copy is the one sync; the error
+    flags written by the kernels are read after it."""
+    if out_device.type == "cuda":
+        return [t.to(out_device) for t in tensors]
+    res = [t.to(out_device) for t in tensors]
+    if status is not None:
+        ops.raise_whiten_status(int(status.cpu()))
+    if err is not None and bool(err.any().cpu()):
+        raise IndexError("index out of range: last loss-mask position of a row carries no reward "
+                         "(reference core_algos.py:79)")
+    return res
+
+
 def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True) -> torch.Tensor:
-    """verl masked_whiten; raises ValueError for a mask sum of 0 or 1 like verl's masked_var."""
+    """verl masked_whiten; ValueError for a mask sum of 0 or 1 like verl's masked_var."""
     if not shift_mean:
         raise NotImplementedError("shift_mean=False is not used by RAGEN")
-    dev = _device()
+    dev = _device(values, mask)
     x = _dev(values.float(), dev).clone()
     m = _dev(mask, dev)
-    n = int((m != 0).sum().item())
-    if n == 0:
-        raise ValueError("At least one element in the mask has to be 1.")
-    if n == 1:
-        raise ValueError("The sum of the mask is one, which can cause a division by zero.")
-    ops.masked_whiten_(x, m)
-    return x.to(values.device)
+    stats = ops.whiten_row_stats(x, m)
+    status = _whiten(x, m, stats)
+    return _back(values.device, [x], status)[0]
 
 
 def compute_gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam, variant="legacy"):
     """verl compute_gae_advantage_return (legacy form by default)."""
-    dev = _device()
+    dev = _device(token_level_rewards, values, response_mask)
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(response_mask, dev)
-    B = r.shape[0]
-    stats = torch.zeros(B, 3, dtype=torch.float64, device=dev)
+    stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
     adv, ret = ops.gae(r, v, m, gamma, lam, variant, row_stats=stats)
-    _check_mask_sum(stats)
-    ops.masked_whiten_(adv, m, stats)
-    return adv.to(token_level_rewards.device), ret.to(token_level_rewards.device)
+    status = _whiten(adv, m, stats)
+    return tuple(_back(token_level_rewards.device, [adv, ret], status))
 
 
 def compute_bi_level_gae_advantage_return(token_level_rewards, values, loss_mask, gamma, lam, high_level_gamma):
     """core_algos.py:4-92 (IndexError where the reference raises it, core_algos.py:79)."""
-    dev = _device()
+    dev = _device(token_level_rewards, values, loss_mask)
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(loss_mask, dev)
-    stats = torch.zeros(r.shape[0], 3, dtype=torch.float64, device=dev)
-    adv, ret = ops.bilevel_gae(r, v, m, gamma, lam, high_level_gamma, row_stats=stats)
-    _check_mask_sum(stats)
-    ops.masked_whiten_(adv, m, stats)
-    return adv.to(token_level_rewards.device), ret.to(token_level_rewards.device)
-
-
-def _check_mask_sum(stats):
-    n = float(stats[:, 2].sum().item())
-    if n == 0:
-        raise ValueError("At least one element in the mask has to be 1.")
-    if n == 1:
-        raise ValueError("The sum of the mask is one, which can cause a division by zero.")
+    stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
+    err = torch.empty(r.shape[0], dtype=torch.uint8, device=dev)
+    adv, ret = ops.bilevel_gae(r, v, m, gamma, lam, high_level_gamma, row_stats=stats, check_errors=False, err=err)
+    status = _whiten(adv, m, stats)
+    return tuple(_back(token_level_rewards.device, [adv, ret], status, err))
 
 
 def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6,
                                    norm_adv_by_std_in_grpo: bool = True):
-    """verl compute_grpo_outcome_advantage: rows grouped by ``index`` (any hashable ids)."""
-    dev = _device()
+    """verl compute_grpo_outcome_advantage: rows grouped by ``index`` (any hashable ids).
+    Groups are rank-local under sharding (RAGEN's uids are unique per row, so every group has
+    one member, agent_trainer.py:551-552)."""
+    dev = _device(token_level_rewards, response_mask)
     r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
     groups = OrderedDict()
     for i, k in enumerate(index):
         groups.setdefault(k, []).append(i)
-    perm = np.concatenate([np.asarray(v, np.int64) for v in groups.values()])
+    perm = np.concatenate([np.asarray(v, np.int64) for v in groups.values()]) if groups else np.zeros(0, np.int64)
     seg = np.zeros(len(groups) + 1, np.int32)
     seg[1:] = np.cumsum([len(v) for v in groups.values()])
     ident = np.array_equal(perm, np.arange(len(perm)))
-    p = torch.from_numpy(perm).to(dev)
+    p = None if ident else torch.from_numpy(perm).to(dev)
     rr = r if ident else r[p].contiguous()
     mm = m if ident else m[p].contiguous()
-    adv, _ = ops.grpo_outcome(rr, mm, torch.from_numpy(seg).to(dev), epsilon, norm_adv_by_std_in_grpo)
+    adv, _ = ops.grpo_outcome(rr, mm, seg, epsilon, norm_adv_by_std_in_grpo)
     if not ident:
         out = torch.empty_like(adv)
         out[p] = adv
         adv = out
-    adv = adv.to(token_level_rewards.device)
+    adv = _back(token_level_rewards.device, [adv])[0]
     return adv, adv

@@ -427,6 +427,26 @@ def test_filter_vs_oracle(device):
     np.testing.assert_array_equal(keep.cpu().numpy(), okeep)
 
 
+@pytest.mark.parametrize("G", [8193, 40000])
+def test_filter_large_g_vs_oracle(device, G):
+    """G above the LDS sort's 8192 groups: the radix-select path keeps the same groups (ties by
+    ascending index) and reports the same metrics; a score count != G*gs raises as view() does."""
+    gs = 16
+    rng = np.random.default_rng(G)
+    sc = np.repeat(rng.choice([0.0, 1.0, -0.5, 2.5], size=G), gs).astype(np.float32)
+    sc[rng.random(G * gs) < 0.03] = 10.0
+    sc[rng.random(G * gs) < 0.01] = rng.standard_normal(1)[0]
+    for ratio, ftype in ((0.25, "std"), (0.25, "std_rev"), (0.5, "std"), (1.0, "std"), (0.0, "std")):
+        keep, met, (sd, mx, mn) = ops.filter_groups(_t(sc, device), G, gs, ratio, ftype)
+        okeep, omet, (osd, omx, omn) = oracle.filter_groups(sc, G, gs, ratio, ftype)
+        np.testing.assert_array_equal(keep.cpu().numpy(), okeep, err_msg=f"{ratio} {ftype}")
+        np.testing.assert_allclose(met.cpu().numpy(), omet, rtol=1e-6)
+        np.testing.assert_array_equal(sd.cpu().numpy(), osd)
+        np.testing.assert_array_equal(mx.cpu().numpy(), omx)
+    with pytest.raises(RuntimeError):
+        ops.filter_groups(_t(sc[:-gs], device), G, gs, 0.25, "std")
+
+
 def test_whiten_errors_and_empty(device):
     x = torch.zeros(2, 3, device=device)
     ops.masked_whiten_(x, torch.zeros(2, 3, dtype=torch.uint8, device=device))  # status recorded, no crash
@@ -834,3 +854,32 @@ def test_pcg64_seed_matches_numpy(device):
             assert last[i] == u, (sd, draws)
     with pytest.raises(ValueError):
         ops.pcg64_seed(_t(np.array([3, -1], np.int64), device), 1)
+
+
+NAME_CASES = [  # (answer, modelled): bare names -> not correct without RMI_ERR_UNSUP
+    ("x", True), ("abs(3) + 4", True), ("a + 3 - 4", True), ("12 + x * 3", True), ("_", True),
+    ("print(12, 3)", True), ("12 3 foo", True), ("(x) - 12 + 3", True), ("12+3 # x", True), ("match + 15", True),
+    ("1if 1 else 2", False), ("(x := 15) - 0", False), ("True + 14", False), ("None", False), ("1 < 0 < x", False),
+    ("x.real", False), ("(12).real + 3", False), ("lambda: 15", False), ("15 if x else 0", False), ("'a'", False),
+    ("not x", False), ("x or 15", False), ("0x0f", False), ("ℌ + 15", False),
+]
+
+
+def test_countdown_bare_names(device):
+    """countdown/env.py:16-21 evaluates under {"__builtins__": None}, where every name lookup
+    raises: answers whose only non-arithmetic tokens are plain names are 'not correct' and
+    are modelled (format_score or 0, no error flag); answers where a keyword, ':', '.', a
+    comparison, a quote or a fused literal could bind or skip a name stay flagged."""
+    n = len(NAME_CASES)
+    data = [{"nums": [12, 3], "target": 15}] * n
+    env = CountdownBatch(CountdownEnvConfig(data=data), n, 1, 1, device)
+    env.reset(np.zeros(n, dtype=np.int64))
+    buf, lens = env.encode_answers([[e] for e, _ in NAME_CASES])
+    r, fl, err = ops.countdown_reward(env.struct(), _t(buf[:, 0], device), _t(lens[:, 0].copy(), device))
+    r, err = r.cpu().numpy(), err.cpu().numpy()
+    for i, (e, modelled) in enumerate(NAME_CASES):
+        want = oracle.countdown_reward(e, [12, 3], 15)
+        if modelled:
+            assert err[i] == 0 and r[i] == want, (e, r[i], want, err[i])
+        else:
+            assert err[i] & _lib.ERR_UNSUP, (e, err[i])

@@ -132,6 +132,22 @@ def test_countdown_kat():
         assert oracle.countdown_reward(c["expr"], k["nums"], k["target"]) == c["reward"], c
 
 
+def test_countdown_trace():
+    """oracle.countdown_turn (es_manager.py:149-169 over countdown/env.py:58-62) replays the
+    reference-run 64 x 4 trace: rewards, penalties, caps, flags, metrics and scores."""
+    d = load("countdown_es")
+    S = strings()
+    B, T = int(d["B"]), int(d["T"])
+    answers = S["countdown_es"]["answers"]
+    nums = [list(d["init_nums"][b, :d["init_n_nums"][b]]) for b in range(B)]
+    ep = oracle.Episode(B, T)
+    for t in range(T):
+        lists = [[a] if a is not None else [] for a in answers[t]]
+        oracle.countdown_turn(lists, nums, d["init_target"], ep, t, d["act_in"][t], 1, -0.1)
+        check_episode_turn(ep, d, t)
+    check_final(ep, d)
+
+
 def test_normalize_golden():
     d = load("normalize")
     B = len(d["scores"])

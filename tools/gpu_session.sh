@@ -25,7 +25,7 @@ python -c "import __graft_entry__ as g; g.build()" > "$OUT/build.log" 2>&1 || { 
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > "$OUT/pytest_gpu.log" 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
       ok_or_stop $? tests; tail -5 "$OUT/pytest_gpu.log";;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
