@@ -66,10 +66,10 @@ enum {
  *           (es_manager.py:17-24, :85, :130-144, :158-169).                          */
 typedef struct {
   int32_t B;             /* number of envs in this batch (one env tag)                  */
-  int32_t T;             /* rows of the per-turn outputs (>= max_turn)                  */
-  int32_t* num_actions;  /* [B]  EnvStatus.num_actions                                  */
+  int32_t T;             /* rows of the per-turn outputs (>= max_turn), <= 255          */
+  uint8_t* num_actions;  /* [B]  EnvStatus.num_actions (<= max_actions_per_traj <= 255)  */
   uint8_t* flags;        /* [B]  RMI_FLAG_* bits                                        */
-  int32_t* n_turns;      /* [B]  turns stepped = len(history) - 1                       */
+  uint8_t* n_turns;      /* [B]  turns stepped = len(history) - 1 (<= T <= 255)         */
   double* penalty;       /* [B]  rollout_cache[env]['penalty'] (format penalty sum)     */
   double* turn_reward;   /* [T,B] acc_reward of each turn (EnvStatus.rewards)           */
   uint8_t* turn_info;    /* [T,B] RMI_INFO_* bits                                       */
@@ -86,7 +86,8 @@ typedef struct {
   const uint8_t* n_actions;    /* [B]  number of parsed action strings (len(actions))     */
   const uint8_t* has_input;    /* [B]  1 = env receives an input this turn; NULL = every
                                   env whose RMI_FLAG_DONE bit is clear                     */
-  int32_t max_actions_per_traj;/* custom_envs.<tag>.max_actions_per_traj                  */
+  int32_t max_actions_per_traj;/* custom_envs.<tag>.max_actions_per_traj, 1..255 (u8
+                                  counters; a larger cap is RMI_EUNSUP)                    */
   double format_penalty;       /* es_manager.format_penalty                               */
 } rmi_turn_t;
 
@@ -102,8 +103,8 @@ typedef struct {
   const uint8_t* room_fixed;  /* [B,H*W]  room_fixed (0 wall, 1 floor, 2 target)           */
   uint8_t* room_state;        /* [B,H*W]  room_state (0..5)                                */
   int8_t* player;             /* [B,2]    player_position (row, col)                       */
-  int32_t* num_env_steps;     /* [B]                                                      */
-  int32_t* boxes_on_target;   /* [B]                                                      */
+  uint8_t* num_env_steps;     /* [B]  (<= num_actions <= 255: one env step per action)     */
+  uint8_t* boxes_on_target;   /* [B]  (<= num_boxes <= 255)                               */
 } rmi_sokoban_t;
 
 int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,

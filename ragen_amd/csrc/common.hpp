@@ -259,6 +259,8 @@ __device__ __forceinline__ void finalize_envs(const rmi_episode_t& ep, const rmi
 inline int check_turn_args(const rmi_episode_t* ep, const rmi_turn_t* in) {
   if (!ep || !in || ep->B < 0 || ep->T <= 0) return RMI_EINVAL;
   if (in->K < 0 || in->K > kMaxK || in->turn < 0 || in->turn >= ep->T) return RMI_EINVAL;
+  // the record's counters are u8: num_actions <= cap, n_turns <= T
+  if (ep->T > 255 || in->max_actions_per_traj > 255) return RMI_EUNSUP;
   if (ep->B == 0) return 1;
   if (!ep->num_actions || !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info ||
       !ep->turn_exec || (in->K > 0 && !in->actions) || !in->n_actions)

@@ -1063,6 +1063,7 @@ RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episod
   using namespace rmi;
   if (!env || Lmax <= 0 || env->max_nums <= 0 || env->max_nums > 8) return RMI_EINVAL;
   if (!ep || !in || in->K < 0 || in->K > kMaxK || ep->B < 0 || in->turn < 0 || in->turn >= ep->T) return RMI_EINVAL;
+  if (ep->T > 255 || in->max_actions_per_traj > 255) return RMI_EUNSUP;  // u8 counters
   if (ep->B == 0) return RMI_OK;
   if (!answers || !answer_len || !env->nums || !env->n_nums || !env->target || !in->n_actions || !ep->num_actions ||
       !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)

@@ -662,9 +662,29 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
         // cells and at the cells whose box bit flipped.  Those bytes are stored directly
         // (rebuild values: player 5, box 3 on a target / 4, else the fixed byte 2 / 1) instead
         // of rebuilding and storing the whole row.
-        if (sub == 0) {
+        M m = (box0 ^ box) | ((M)1 << jp0) | ((M)1 << jp);
+        if (LPE == 1) {
+          // patch the changed bytes into the row dwords held in registers and store each
+          // dirty dword once (a read-modify-write inside the lane's own row: whole dwords, no
+          // byte stores)
+          uint32_t dirty = 0;
+          while (m) {
+            const int j = WordBits<M>::ctz(m);
+            m &= m - 1;
+            const uint32_t t = (uint32_t)(target >> j) & 1u, bx = (uint32_t)(box >> j) & 1u;
+            const uint32_t v = j == jp ? 5u : (bx ? 4u - t : 1u + t);
+            const int q = j + W, dw = q >> 2, sh = (q & 3) * 8;
+#pragma unroll
+            for (int i = 0; i < NWL; ++i)
+              if (i == dw) xs[i] = (xs[i] & ~(0xFFu << sh)) | (v << sh);
+            dirty |= 1u << dw;
+          }
+          uint32_t* r1 = reinterpret_cast<uint32_t*>(env.room_state + b * hw);
+#pragma unroll
+          for (int i = 0; i < NWL; ++i)
+            if ((dirty >> i) & 1u) r1[i] = xs[i];
+        } else if (sub == 0) {
           uint8_t* win = env.room_state + b * hw + W;  // window bit j = cell W + j
-          M m = (box0 ^ box) | ((M)1 << jp0) | ((M)1 << jp);
           while (m) {
             const int j = WordBits<M>::ctz(m);
             m &= m - 1;

@@ -50,9 +50,9 @@ def _dt(t, dtype, name):
 @dataclass
 class EpisodeState:
     """Device SoA of EnvStatus + rollout-cache bookkeeping (es_manager.py:17-24, :85)."""
-    num_actions: torch.Tensor   # i32[B]
+    num_actions: torch.Tensor   # u8[B]
     flags: torch.Tensor         # u8[B]   FLAG_* bits
-    n_turns: torch.Tensor       # i32[B]
+    n_turns: torch.Tensor       # u8[B]
     penalty: torch.Tensor       # f64[B]
     turn_reward: torch.Tensor   # f64[T,B]
     turn_info: torch.Tensor     # u8[T,B]
@@ -60,7 +60,7 @@ class EpisodeState:
     arena: Optional[torch.Tensor] = None  # u8[nbytes]: every field above is a view into it
 
     # field order inside the arena (each field 256-B aligned)
-    FIELDS = (("num_actions", torch.int32, False), ("flags", torch.uint8, False), ("n_turns", torch.int32, False),
+    FIELDS = (("num_actions", torch.uint8, False), ("flags", torch.uint8, False), ("n_turns", torch.uint8, False),
               ("penalty", torch.float64, False), ("turn_reward", torch.float64, True),
               ("turn_info", torch.uint8, True), ("turn_exec", torch.uint8, True))
 

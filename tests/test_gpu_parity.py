@@ -717,7 +717,7 @@ def test_bilevel_vs_oracle_large(device, B):
         errs = torch.empty(B, dtype=torch.uint8, device=device)
         check = ops.lib().rmi_bilevel_gae(ops._ptr(rd), ops._ptr(vd), ops._ptr(md), B, r.shape[1], g, lam, hg,
                                           ops._ptr(adv), ops._ptr(ret), ops._ptr(stats), ops._ptr(errs),
-                                          ops._stream())
+                                          ops._stream(device))
         assert check == 0
         np.testing.assert_array_equal(errs.cpu().numpy() != 0, oerr != 0)
         s1 = (oa.astype(np.float64) * m).sum(1)
@@ -856,12 +856,14 @@ def test_pcg64_seed_matches_numpy(device):
         ops.pcg64_seed(_t(np.array([3, -1], np.int64), device), 1)
 
 
-NAME_CASES = [  # (answer, modelled): bare names -> not correct without RMI_ERR_UNSUP
-    ("x", True), ("abs(3) + 4", True), ("a + 3 - 4", True), ("12 + x * 3", True), ("_", True),
-    ("print(12, 3)", True), ("12 3 foo", True), ("(x) - 12 + 3", True), ("12+3 # x", True), ("match + 15", True),
-    ("1if 1 else 2", False), ("(x := 15) - 0", False), ("True + 14", False), ("None", False), ("1 < 0 < x", False),
-    ("x.real", False), ("(12).real + 3", False), ("lambda: 15", False), ("15 if x else 0", False), ("'a'", False),
-    ("not x", False), ("x or 15", False), ("0x0f", False), ("ℌ + 15", False),
+NAME_CASES = [  # (answer, modelled); every answer's digit runs are exactly {12, 3}, so the
+    # format check passes and the evaluation decides (0.1 = not correct, 1 = correct)
+    ("x + 12 + 3", True), ("abs(12) + 3", True), ("a + 12 - 3", True), ("12 + x * 3", True), ("_ + 12 + 3", True),
+    ("print(12, 3)", True), ("12 3 foo", True), ("(x) - 12 + 3", True), ("12+3 # x", True),
+    ("match + 12 + 3", True),
+    ("12if x else 3", False), ("(x := 12) + 3", False), ("True + 12 + 3", False), ("3 < 12 < x", False),
+    ("x.real + 12 + 3", False), ("(12).real + 3", False), ("lambda: 12 + 3", False), ("12 if x else 3", False),
+    ("not x + 12 + 3", False), ("x or 12 + 3", False), ("12 + 3j", False), ("\u210c + 12 + 3", False),
 ]
 
 
