@@ -104,7 +104,7 @@ typedef struct {
   uint8_t* room_state;        /* [B,H*W]  room_state (0..5)                                */
   int8_t* player;             /* [B,2]    player_position (row, col)                       */
   uint8_t* num_env_steps;     /* [B]  (<= num_actions <= 255: one env step per action)     */
-  uint8_t* boxes_on_target;   /* [B]  (<= num_boxes <= 255)                               */
+  int8_t* boxes_on_target;    /* [B]  num_boxes - open targets: -64..64 for H*W <= 64      */
 } rmi_sokoban_t;
 
 int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,

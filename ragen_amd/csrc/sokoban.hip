@@ -663,27 +663,38 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
         // (rebuild values: player 5, box 3 on a target / 4, else the fixed byte 2 / 1) instead
         // of rebuilding and storing the whole row.
         M m = (box0 ^ box) | ((M)1 << jp0) | ((M)1 << jp);
+#ifndef RMI_SOKOBAN_BYTE_STORES
         if (LPE == 1) {
-          // patch the changed bytes into the row dwords held in registers and store each
-          // dirty dword once (a read-modify-write inside the lane's own row: whole dwords, no
-          // byte stores)
+          // every dword holding a changed cell is rebuilt from the bitboards (a regular room's
+          // state byte is wall 0 / player 5 / box 4 or 3 on a target / floor 1 or target 2) and
+          // stored whole: a read-modify-write of the lane's own row without byte stores
           uint32_t dirty = 0;
           while (m) {
             const int j = WordBits<M>::ctz(m);
             m &= m - 1;
-            const uint32_t t = (uint32_t)(target >> j) & 1u, bx = (uint32_t)(box >> j) & 1u;
-            const uint32_t v = j == jp ? 5u : (bx ? 4u - t : 1u + t);
-            const int q = j + W, dw = q >> 2, sh = (q & 3) * 8;
-#pragma unroll
-            for (int i = 0; i < NWL; ++i)
-              if (i == dw) xs[i] = (xs[i] & ~(0xFFu << sh)) | (v << sh);
-            dirty |= 1u << dw;
+            dirty |= 1u << ((j + W) >> 2);
           }
           uint32_t* r1 = reinterpret_cast<uint32_t*>(env.room_state + b * hw);
+          while (dirty) {
+            const int dw = __builtin_ctz(dirty);
+            dirty &= dirty - 1;
+            uint32_t word = 0;
 #pragma unroll
-          for (int i = 0; i < NWL; ++i)
-            if ((dirty >> i) & 1u) r1[i] = xs[i];
-        } else if (sub == 0) {
+            for (int k = 0; k < 4; ++k) {
+              const int j = 4 * dw + k - W;  // window bit of the cell (row 0 is all wall)
+              uint32_t v = 0;
+              if (j >= 0) {
+                const uint32_t wl = (uint32_t)(wall >> j) & 1u, tg = (uint32_t)(target >> j) & 1u;
+                const uint32_t bx = (uint32_t)(box >> j) & 1u;
+                v = wl ? 0u : (j == jp ? 5u : (bx ? 4u - tg : 1u + tg));
+              }
+              word |= v << (8 * k);
+            }
+            r1[dw] = word;
+          }
+        } else
+#endif
+        if (sub == 0) {
           uint8_t* win = env.room_state + b * hw + W;  // window bit j = cell W + j
           while (m) {
             const int j = WordBits<M>::ctz(m);

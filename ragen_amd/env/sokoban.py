@@ -24,7 +24,7 @@ class SokobanBatch(BatchEnv):
         self.room_state = torch.zeros(B, HW, dtype=torch.uint8, device=d)
         self.player = torch.zeros(B, 2, dtype=torch.int8, device=d)
         self.num_env_steps = torch.zeros(B, dtype=torch.uint8, device=d)  # u8 (include/ragen_amd.h)
-        self.boxes_on_target = torch.zeros(B, dtype=torch.uint8, device=d)
+        self.boxes_on_target = torch.zeros(B, dtype=torch.int8, device=d)  # may go negative (App. A.1)
         # the generated rooms: reset() uploads here once, restore() re-initialises from them
         self.init_state = torch.zeros(B, HW, dtype=torch.uint8, device=d)
         self.init_player = torch.zeros(B, 2, dtype=torch.int8, device=d)

@@ -1,0 +1,553 @@
+"""The hot path as PyTorch custom operators: ``torch.ops.ragen_amd.*``.
+
+Every entry point of the C ABI (include/ragen_amd.h) is registered with the dispatcher through
+``torch.library.custom_op`` — a schema (argument types, which tensors an op mutates in place),
+a CUDA (= HIP on ROCm) implementation that enqueues the HIP kernel on the current stream of
+the tensors' device, and a fake (meta) implementation so shape propagation, FakeTensor
+tracing and ``torch.compile`` see the ops as opaque nodes.  The trainer-facing facades
+(``ragen_amd.llm_agent``, ``ragen_amd.trainer``, ``ragen_amd.env``) call these operators, so
+the reference's callers (agent_trainer.py:514-515, 623-633; agent_proxy.py:146-157) drive the
+kernels through ordinary torch ops, as north_star asks.
+
+The ops are registered for the CUDA dispatch key only: a CPU tensor raises
+``NotImplementedError`` from the dispatcher (the engine has no CPU path).
+
+Episode record arguments are the seven tensors of ``ops.EpisodeState`` in its field order
+(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec), each listed among
+the mutated arguments of the ops that write the record.
+"""
+from typing import List, Optional, Tuple
+
+import torch
+from torch import Tensor
+from torch.library import custom_op
+
+from . import _lib, ops
+
+NS = "ragen_amd"
+EP = ("num_actions", "flags", "n_turns", "penalty", "turn_reward", "turn_info", "turn_exec")
+NORM = {"identity": 0, "mean": 1, "mean_std": 2, "asym_clip": 3}
+FILTER = {"std": 0, "std_rev": 1}
+VARIANT = {"legacy": 0, "masked": 1}
+
+
+def _op(name, mutates=()):
+    return custom_op(f"{NS}::{name}", mutates_args=tuple(mutates), device_types="cuda")
+
+
+def _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec) -> ops.EpisodeState:
+    return ops.EpisodeState(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec)
+
+
+def ep_args(ep: ops.EpisodeState):
+    """The seven record tensors of an EpisodeState, in the ops' argument order."""
+    return tuple(getattr(ep, k) for k in EP)
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+# ====================================================================== Sokoban (A4)
+def _sokoban(room_fixed, room_state, player, num_env_steps, boxes_on_target, H, W, num_boxes, max_steps):
+    ops._dev(room_fixed, room_state, player, num_env_steps, boxes_on_target)
+    for t, dt, nm in ((room_fixed, torch.uint8, "room_fixed"), (room_state, torch.uint8, "room_state"),
+                      (player, torch.int8, "player"), (num_env_steps, torch.uint8, "num_env_steps"),
+                      (boxes_on_target, torch.int8, "boxes_on_target")):
+        ops._dt(t, dt, nm)
+    return _lib.Sokoban(int(H), int(W), int(num_boxes), int(max_steps), _ptr(room_fixed), _ptr(room_state),
+                        _ptr(player), _ptr(num_env_steps), _ptr(boxes_on_target))
+
+
+_SOK_MUT = ("room_state", "player", "num_env_steps", "boxes_on_target") + EP
+
+
+@_op("sokoban_step_turn", _SOK_MUT + ("err",))
+def sokoban_step_turn(room_fixed: Tensor, room_state: Tensor, player: Tensor, num_env_steps: Tensor,
+                      boxes_on_target: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor, penalty: Tensor,
+                      turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor, actions: Tensor, n_actions: Tensor,
+                      has_input: Optional[Tensor], err: Optional[Tensor], turn: int, max_actions_per_traj: int,
+                      format_penalty: float, H: int, W: int, num_boxes: int, max_steps: int) -> None:
+    """EnvStateManager.step (es_manager.py:105-171) over SokobanEnv.step (sokoban/env.py:44-51)."""
+    env = _sokoban(room_fixed, room_state, player, num_env_steps, boxes_on_target, H, W, num_boxes, max_steps)
+    ep = _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec)
+    ops._dev(room_state, flags, actions, n_actions, has_input, err)
+    ops.sokoban_step_turn(env, ep, ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                                   format_penalty), err)
+
+
+@_op("sokoban_step_turn_first", _SOK_MUT + ("err",))
+def sokoban_step_turn_first(room_fixed: Tensor, room_state: Tensor, player: Tensor, num_env_steps: Tensor,
+                            boxes_on_target: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor,
+                            penalty: Tensor, turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor,
+                            actions: Tensor, n_actions: Tensor, has_input: Optional[Tensor], err: Optional[Tensor],
+                            init_state: Tensor, init_player: Tensor, turn: int, max_actions_per_traj: int,
+                            format_penalty: float, H: int, W: int, num_boxes: int, max_steps: int) -> None:
+    """SokobanEnv.reset's device part (sokoban/env.py:37-38, es_manager.py:95) + the first turn."""
+    env = _sokoban(room_fixed, room_state, player, num_env_steps, boxes_on_target, H, W, num_boxes, max_steps)
+    ep = _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec)
+    ops._dev(room_state, flags, actions, n_actions, has_input, err, init_state, init_player)
+    ops.sokoban_step_turn_first(env, ep, ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                                         format_penalty), init_state, init_player, err)
+
+
+@_op("sokoban_step_turn_finalize", _SOK_MUT + ("err", "metrics", "score", "pen", "norm"))
+def sokoban_step_turn_finalize(room_fixed: Tensor, room_state: Tensor, player: Tensor, num_env_steps: Tensor,
+                               boxes_on_target: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor,
+                               penalty: Tensor, turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor,
+                               actions: Tensor, n_actions: Tensor, has_input: Optional[Tensor], err: Optional[Tensor],
+                               metrics: Optional[Tensor], score: Optional[Tensor], pen: Optional[Tensor],
+                               norm: Optional[Tensor], turn: int, max_actions_per_traj: int, format_penalty: float,
+                               H: int, W: int, num_boxes: int, max_steps: int, group_size: int, method: int) -> None:
+    """The rollout's last turn + get_rollout_states / scores / _normalize_score_tensor
+    (es_manager.py:173-207, ctx_manager.py:175-226) over groups of group_size envs."""
+    env = _sokoban(room_fixed, room_state, player, num_env_steps, boxes_on_target, H, W, num_boxes, max_steps)
+    ep = _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec)
+    ops._dev(room_state, flags, actions, n_actions, has_input, err, metrics, score, pen, norm)
+    fin = ops.finalize_struct(group_size, _method_name(method), norm, metrics, score, pen)
+    ops.sokoban_step_turn_finalize(env, ep, ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                                            format_penalty), fin, err)
+
+
+@_op("sokoban_reset", _SOK_MUT)
+def sokoban_reset(room_fixed: Tensor, room_state: Tensor, player: Tensor, num_env_steps: Tensor,
+                  boxes_on_target: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor, penalty: Tensor,
+                  turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor, init_state: Tensor, init_player: Tensor,
+                  H: int, W: int, num_boxes: int, max_steps: int) -> None:
+    """SokobanEnv.reset's device part (sokoban/env.py:37-38) + EnvStatus() (es_manager.py:95)."""
+    env = _sokoban(room_fixed, room_state, player, num_env_steps, boxes_on_target, H, W, num_boxes, max_steps)
+    ops._dev(room_state, flags, init_state, init_player)
+    ops.sokoban_reset(env, _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec), init_state,
+                      init_player)
+
+
+def _method_name(method: int) -> str:
+    for k, v in NORM.items():
+        if v == method:
+            return k
+    raise ValueError(f"Invalid normalization method: {method}")
+
+
+# =================================================================== FrozenLake (A7)
+def _frozenlake(desc, s, rng, nrow, ncol, is_slippery, cs0, cs1, cs2):
+    ops._dev(desc, s, rng)
+    ops._dt(desc, torch.uint8, "desc")
+    ops._dt(s, torch.int32, "s")
+    ops._dt(rng, torch.int64, "rng")
+    return _lib.FrozenLake(int(nrow), int(ncol), int(is_slippery), float(cs0), float(cs1), float(cs2), _ptr(desc),
+                           _ptr(s), _ptr(rng))
+
+
+_FL_MUT = ("s", "rng") + EP
+
+
+@_op("frozenlake_step_turn", _FL_MUT + ("err",))
+def frozenlake_step_turn(desc: Tensor, s: Tensor, rng: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor,
+                         penalty: Tensor, turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor, actions: Tensor,
+                         n_actions: Tensor, has_input: Optional[Tensor], err: Optional[Tensor], turn: int,
+                         max_actions_per_traj: int, format_penalty: float, nrow: int, ncol: int, is_slippery: bool,
+                         cs0: float, cs1: float, cs2: float) -> None:
+    """EnvStateManager.step over FrozenLakeEnv.step (frozen_lake/env.py:39-45, gymnasium App. A.2)."""
+    env = _frozenlake(desc, s, rng, nrow, ncol, is_slippery, cs0, cs1, cs2)
+    ops._dev(s, flags, actions, n_actions, has_input, err)
+    ops.frozenlake_step_turn(env, _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec),
+                             ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                             format_penalty), err)
+
+
+@_op("frozenlake_step_turn_first", ("desc",) + _FL_MUT + ("err",))
+def frozenlake_step_turn_first(desc: Tensor, s: Tensor, rng: Tensor, num_actions: Tensor, flags: Tensor,
+                               n_turns: Tensor, penalty: Tensor, turn_reward: Tensor, turn_info: Tensor,
+                               turn_exec: Tensor, actions: Tensor, n_actions: Tensor, has_input: Optional[Tensor],
+                               err: Optional[Tensor], init_desc: Tensor, init_s: Tensor, init_rng: Tensor, turn: int,
+                               max_actions_per_traj: int, format_penalty: float, nrow: int, ncol: int,
+                               is_slippery: bool, cs0: float, cs1: float, cs2: float) -> None:
+    """FrozenLakeEnv.reset's device part (frozen_lake/env.py:28-37) + the first turn."""
+    env = _frozenlake(desc, s, rng, nrow, ncol, is_slippery, cs0, cs1, cs2)
+    ops._dev(s, flags, actions, n_actions, has_input, err, init_desc, init_s, init_rng)
+    ops.frozenlake_step_turn_first(env, _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec),
+                                   ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                                   format_penalty), init_desc, init_s, init_rng, err)
+
+
+@_op("frozenlake_step_turn_finalize", _FL_MUT + ("err", "metrics", "score", "pen", "norm"))
+def frozenlake_step_turn_finalize(desc: Tensor, s: Tensor, rng: Tensor, num_actions: Tensor, flags: Tensor,
+                                  n_turns: Tensor, penalty: Tensor, turn_reward: Tensor, turn_info: Tensor,
+                                  turn_exec: Tensor, actions: Tensor, n_actions: Tensor, has_input: Optional[Tensor],
+                                  err: Optional[Tensor], metrics: Optional[Tensor], score: Optional[Tensor],
+                                  pen: Optional[Tensor], norm: Optional[Tensor], turn: int, max_actions_per_traj: int,
+                                  format_penalty: float, nrow: int, ncol: int, is_slippery: bool, cs0: float,
+                                  cs1: float, cs2: float, group_size: int, method: int) -> None:
+    """The rollout's last FrozenLake turn + the fused finalize (as sokoban_step_turn_finalize)."""
+    env = _frozenlake(desc, s, rng, nrow, ncol, is_slippery, cs0, cs1, cs2)
+    ops._dev(s, flags, actions, n_actions, has_input, err, metrics, score, pen, norm)
+    fin = ops.finalize_struct(group_size, _method_name(method), norm, metrics, score, pen)
+    ops.frozenlake_step_turn_finalize(env, _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info,
+                                               turn_exec),
+                                      ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                                      format_penalty), fin, err)
+
+
+@_op("frozenlake_reset", ("desc",) + _FL_MUT)
+def frozenlake_reset(desc: Tensor, s: Tensor, rng: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor,
+                     penalty: Tensor, turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor, init_desc: Tensor,
+                     init_s: Tensor, init_rng: Tensor, nrow: int, ncol: int, is_slippery: bool, cs0: float, cs1: float,
+                     cs2: float) -> None:
+    """FrozenLakeEnv.reset's device part (frozen_lake/env.py:28-37) + EnvStatus()."""
+    env = _frozenlake(desc, s, rng, nrow, ncol, is_slippery, cs0, cs1, cs2)
+    ops._dev(s, flags, init_desc, init_s, init_rng)
+    ops.frozenlake_reset(env, _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec), init_desc,
+                         init_s, init_rng)
+
+
+# ======================================================================= Bandit (A8)
+@_op("bandit_step_turn", ("rng",) + EP + ("err",))
+def bandit_step_turn(hi_is_first: Tensor, rng: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor,
+                     penalty: Tensor, turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor, actions: Tensor,
+                     n_actions: Tensor, has_input: Optional[Tensor], err: Optional[Tensor], turn: int,
+                     max_actions_per_traj: int, format_penalty: float, action_space_start: int, lo_arm_score: float,
+                     hi_arm_loscore: float, hi_arm_hiscore: float, hi_arm_hiscore_prob: float) -> None:
+    """EnvStateManager.step over BanditEnv.step (bandit/env.py:62-76)."""
+    ops._dev(hi_is_first, rng, flags, actions, n_actions, has_input, err)
+    env = _lib.Bandit(int(action_space_start), float(lo_arm_score), float(hi_arm_loscore), float(hi_arm_hiscore),
+                      float(hi_arm_hiscore_prob), _ptr(hi_is_first), _ptr(rng))
+    ops.bandit_step_turn(env, _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec),
+                         ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty),
+                         err)
+
+
+# ==================================================================== Countdown (A9)
+def _countdown(nums, n_nums, target, score, format_score):
+    ops._dev(nums, n_nums, target)
+    for t, nm in ((nums, "nums"), (n_nums, "n_nums"), (target, "target")):
+        ops._dt(t, torch.int32, nm)
+    return _lib.Countdown(int(nums.shape[1]), float(score), float(format_score), _ptr(nums), _ptr(n_nums),
+                          _ptr(target))
+
+
+@_op("countdown_step_turn", EP + ("err",))
+def countdown_step_turn(nums: Tensor, n_nums: Tensor, target: Tensor, num_actions: Tensor, flags: Tensor,
+                        n_turns: Tensor, penalty: Tensor, turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor,
+                        actions: Tensor, n_actions: Tensor, has_input: Optional[Tensor], err: Optional[Tensor],
+                        answers: Tensor, answer_len: Tensor, turn: int, max_actions_per_traj: int,
+                        format_penalty: float, score: float, format_score: float) -> None:
+    """EnvStateManager.step over CountdownEnv.step (countdown/env.py:58-78)."""
+    env = _countdown(nums, n_nums, target, score, format_score)
+    ops._dev(nums, flags, actions, n_actions, has_input, err, answers, answer_len)
+    ops.countdown_step_turn(env, _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec),
+                            ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                            format_penalty), answers, answer_len, err)
+
+
+@_op("countdown_reward")
+def countdown_reward(nums: Tensor, n_nums: Tensor, target: Tensor, answers: Tensor, answer_len: Tensor, score: float,
+                     format_score: float) -> Tuple[Tensor, Tensor, Tensor]:
+    """compute_reward (countdown/env.py:69-78) per answer -> (reward f64, flags u8, err u8)."""
+    env = _countdown(nums, n_nums, target, score, format_score)
+    ops._dev(nums, answers, answer_len)
+    return ops.countdown_reward(env, answers, answer_len)
+
+
+@countdown_reward.register_fake
+def _(nums, n_nums, target, answers, answer_len, score, format_score):
+    n = answers.shape[0]
+    return (answers.new_empty(n, dtype=torch.float64), answers.new_empty(n, dtype=torch.uint8),
+            answers.new_empty(n, dtype=torch.uint8))
+
+
+# ============================================================ seeding (A7 / A8 reset)
+@_op("pcg64_seed")
+def pcg64_seed(seeds: Tensor, draws: int) -> Tuple[Tensor, Tensor]:
+    """Generator(PCG64(SeedSequence(seed))) per seed + `draws` random() calls -> (rng i64[4,n], last f64[n])."""
+    rng, last = ops.pcg64_seed(seeds, draws)
+    return rng, last
+
+
+@pcg64_seed.register_fake
+def _(seeds, draws):
+    n = seeds.shape[0]
+    return seeds.new_empty(4, n, dtype=torch.int64), seeds.new_empty(n, dtype=torch.float64)
+
+
+# ============================================================== episode (A10, A16)
+@_op("rollout_metrics")
+def rollout_metrics(num_actions: Tensor, flags: Tensor, n_turns: Tensor, penalty: Tensor, turn_reward: Tensor,
+                    turn_info: Tensor, turn_exec: Tensor) -> Tensor:
+    """get_rollout_states (es_manager.py:173-207) -> f64[B, 4]."""
+    return ops.rollout_metrics(_ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec))
+
+
+@rollout_metrics.register_fake
+def _(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec):
+    return flags.new_empty(flags.shape[0], 4, dtype=torch.float64)
+
+
+@_op("trajectory_scores")
+def trajectory_scores(num_actions: Tensor, flags: Tensor, n_turns: Tensor, penalty: Tensor, turn_reward: Tensor,
+                      turn_info: Tensor, turn_exec: Tensor) -> Tuple[Tensor, Tensor]:
+    """Trajectory score sum(turn rewards) and penalty as f32 (ctx_manager.py:282, :217)."""
+    return ops.trajectory_scores(_ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec))
+
+
+@trajectory_scores.register_fake
+def _(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec):
+    B = flags.shape[0]
+    return flags.new_empty(B, dtype=torch.float32), flags.new_empty(B, dtype=torch.float32)
+
+
+@_op("rollout_finalize", ("metrics", "score", "pen", "norm"))
+def rollout_finalize(num_actions: Tensor, flags: Tensor, n_turns: Tensor, penalty: Tensor, turn_reward: Tensor,
+                     turn_info: Tensor, turn_exec: Tensor, seg: Tensor, method: int, metrics: Optional[Tensor],
+                     score: Optional[Tensor], pen: Optional[Tensor], norm: Tensor) -> None:
+    """Metrics + trajectory scores + _normalize_score_tensor in one launch (contiguous segments)."""
+    ops.rollout_finalize(_ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec), seg,
+                         _method_name(method), norm, metrics, score, pen)
+
+
+@_op("group_normalize")
+def group_normalize(score: Tensor, pen: Optional[Tensor], seg: Tensor, method: int) -> Tensor:
+    """_normalize_score_tensor (ctx_manager.py:175-226) over contiguous segments seg i32[G+1]."""
+    return ops.group_normalize(score, pen, seg, _method_name(method))
+
+
+@group_normalize.register_fake
+def _(score, pen, seg, method):
+    return torch.empty_like(score)
+
+
+# ======================================================================= filter (A12)
+@_op("row_sum")
+def row_sum(x: Tensor) -> Tensor:
+    """rm_scores.sum(-1) in fp64 then f32 (agent_trainer.py:467)."""
+    return ops.row_sum(x)
+
+
+@row_sum.register_fake
+def _(x):
+    return x.new_empty(x.shape[0], dtype=torch.float32)
+
+
+@_op("filter_groups")
+def filter_groups(scores: Tensor, num_groups: int, group_size: int, ratio: float,
+                  ftype: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """_filter_rollout (agent_trainer.py:461-500) -> (keep u8[G], metrics f64[6], std, max, mean f32[G])."""
+    keep, met, (sd, mx, mn) = ops.filter_groups(scores, num_groups, group_size, ratio,
+                                                "std" if ftype == 0 else "std_rev")
+    return keep, met, sd, mx, mn
+
+
+@filter_groups.register_fake
+def _(scores, num_groups, group_size, ratio, ftype):
+    G = num_groups
+    return (scores.new_empty(G, dtype=torch.uint8), scores.new_empty(6, dtype=torch.float64),
+            scores.new_empty(G, dtype=torch.float32), scores.new_empty(G, dtype=torch.float32),
+            scores.new_empty(G, dtype=torch.float32))
+
+
+# ================================================================ token masks (A11)
+@_op("masks_and_scores")
+def masks_and_scores(ids: Tensor, special_token: int, reward_token: int, scores: Tensor, n_scores: Tensor,
+                     n_slots: int, use_turn_scores: bool, enable_response_mask: bool,
+                     roll: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """get_masks_and_scores (ctx_manager.py:35-70) -> (score f32, loss_mask, response_mask bool [B,S-1], err u8[B])."""
+    return ops.masks_and_scores(ids, special_token, reward_token, scores, n_scores, n_slots, use_turn_scores,
+                                enable_response_mask, roll)
+
+
+@masks_and_scores.register_fake
+def _(ids, special_token, reward_token, scores, n_scores, n_slots, use_turn_scores, enable_response_mask, roll):
+    B, S = ids.shape
+    So = max(S - 1, 0)
+    return (ids.new_empty(B, So, dtype=torch.float32), ids.new_empty(B, So, dtype=torch.bool),
+            ids.new_empty(B, So, dtype=torch.bool), ids.new_empty(B, dtype=torch.uint8))
+
+
+# ================================================================== advantages (A13)
+@_op("gae", ("row_stats",))
+def gae(r: Tensor, v: Tensor, mask: Tensor, gamma: float, lam: float, variant: int,
+        row_stats: Optional[Tensor]) -> Tuple[Tensor, Tensor]:
+    """verl compute_gae_advantage_return before whitening (App. A.4); variant 0 legacy, 1 masked."""
+    return ops.gae(r, v, mask, gamma, lam, "legacy" if variant == 0 else "masked", row_stats)
+
+
+@gae.register_fake
+def _(r, v, mask, gamma, lam, variant, row_stats):
+    return torch.empty_like(r), torch.empty_like(r)
+
+
+@_op("bilevel_gae", ("row_stats", "err"))
+def bilevel_gae(r: Tensor, v: Tensor, mask: Tensor, gamma: float, lam: float, high_level_gamma: float,
+                row_stats: Optional[Tensor], err: Optional[Tensor]) -> Tuple[Tensor, Tensor]:
+    """compute_bi_level_gae_advantage_return before whitening (core_algos.py:4-88); err u8[B]
+    flags the rows where the reference raises IndexError (core_algos.py:79)."""
+    return ops.bilevel_gae(r, v, mask, gamma, lam, high_level_gamma, row_stats, check_errors=False, err=err)
+
+
+@bilevel_gae.register_fake
+def _(r, v, mask, gamma, lam, high_level_gamma, row_stats, err):
+    return torch.empty_like(r), torch.empty_like(r)
+
+
+@_op("masked_whiten_", ("x",))
+def masked_whiten_(x: Tensor, mask: Tensor, row_stats: Optional[Tensor]) -> Tensor:
+    """verl masked_whiten in place (core_algos.py:90) -> i32[1] status (0 ok, 1/2: verl's ValueError)."""
+    _, scratch = ops.masked_whiten_(x, mask, row_stats)
+    return ops.whiten_status(scratch).clone()
+
+
+@masked_whiten_.register_fake
+def _(x, mask, row_stats):
+    return x.new_empty(1, dtype=torch.int32)
+
+
+@_op("masked_whiten_stats_", ("x",))
+def masked_whiten_stats_(x: Tensor, stats: Tensor) -> Tensor:
+    """masked_whiten of this shard's rows with all shards' per-row partials -> i32[1] status."""
+    _, scratch = ops.masked_whiten_stats_(x, stats)
+    return ops.whiten_status(scratch).clone()
+
+
+@masked_whiten_stats_.register_fake
+def _(x, stats):
+    return x.new_empty(1, dtype=torch.int32)
+
+
+@_op("whiten_row_stats")
+def whiten_row_stats(x: Tensor, mask: Tensor) -> Tensor:
+    """Per-row fp64 (sum, sum_sq, count) over the mask -> f64[B, 3]."""
+    return ops.whiten_row_stats(x, mask)
+
+
+@whiten_row_stats.register_fake
+def _(x, mask):
+    return x.new_empty(x.shape[0], 3, dtype=torch.float64)
+
+
+@_op("grpo_outcome")
+def grpo_outcome(r: Tensor, mask: Tensor, seg: Tensor, eps: float, norm_by_std: bool) -> Tuple[Tensor, Tensor]:
+    """verl compute_grpo_outcome_advantage over contiguous row groups seg i32[G+1] (device)."""
+    return ops.grpo_outcome(r, mask, seg, eps, norm_by_std)
+
+
+@grpo_outcome.register_fake
+def _(r, mask, seg, eps, norm_by_std):
+    return torch.empty_like(r), torch.empty_like(r)
+
+
+# ============================================================= text boundary (§8(f) 2)
+def _glyphs(glyph_bytes: List[int], glyph_len: List[int]):
+    import numpy as np
+    if len(glyph_bytes) != 16 or len(glyph_len) != 16:
+        raise ValueError("glyph tables hold 16 entries")
+    return np.asarray(glyph_bytes, np.uint32), np.asarray(glyph_len, np.uint8)
+
+
+def render_stride(cells: int, rows: int) -> int:
+    return (cells * 4 + rows - 1 + 3) // 4 * 4
+
+
+@_op("sokoban_render")
+def sokoban_render(room_fixed: Tensor, room_state: Tensor, H: int, W: int, glyph_bytes: List[int],
+                   glyph_len: List[int]) -> Tuple[Tensor, Tensor]:
+    """SokobanEnv.render text of every env (sokoban/env.py:53-61) -> (UTF-8 rows u8[B, stride], len i32[B])."""
+    ops._dev(room_fixed, room_state)
+    B = room_state.shape[0]
+    env = _lib.Sokoban(int(H), int(W), 0, 0, _ptr(room_fixed), _ptr(room_state), None, None, None)
+    gb, gl = _glyphs(glyph_bytes, glyph_len)
+    stride = render_stride(H * W, H)
+    out = torch.empty(B, stride, dtype=torch.uint8, device=room_state.device)
+    n = torch.empty(B, dtype=torch.int32, device=room_state.device)
+    ops.check(ops.lib().rmi_sokoban_render(env, B, gb.ctypes.data, gl.ctypes.data, out.data_ptr(), stride,
+                                           n.data_ptr(), ops._stream(room_state.device)), "rmi_sokoban_render")
+    return out, n
+
+
+@sokoban_render.register_fake
+def _(room_fixed, room_state, H, W, glyph_bytes, glyph_len):
+    B = room_state.shape[0]
+    return room_state.new_empty(B, render_stride(H * W, H)), room_state.new_empty(B, dtype=torch.int32)
+
+
+@_op("frozenlake_render")
+def frozenlake_render(desc: Tensor, s: Tensor, nrow: int, ncol: int, glyph_bytes: List[int],
+                      glyph_len: List[int]) -> Tuple[Tensor, Tensor]:
+    """FrozenLakeEnv.render text of every env (frozen_lake/env.py:47-61) -> (u8[B, stride], i32[B])."""
+    ops._dev(desc, s)
+    B = s.shape[0]
+    env = _lib.FrozenLake(int(nrow), int(ncol), 0, 0.0, 0.0, 0.0, _ptr(desc), _ptr(s), None)
+    gb, gl = _glyphs(glyph_bytes, glyph_len)
+    stride = render_stride(nrow * ncol, nrow)
+    out = torch.empty(B, stride, dtype=torch.uint8, device=s.device)
+    n = torch.empty(B, dtype=torch.int32, device=s.device)
+    ops.check(ops.lib().rmi_frozenlake_render(env, B, gb.ctypes.data, gl.ctypes.data, out.data_ptr(), stride,
+                                              n.data_ptr(), ops._stream(s.device)), "rmi_frozenlake_render")
+    return out, n
+
+
+@frozenlake_render.register_fake
+def _(desc, s, nrow, ncol, glyph_bytes, glyph_len):
+    B = s.shape[0]
+    return s.new_empty(B, render_stride(nrow * ncol, nrow), dtype=torch.uint8), s.new_empty(B, dtype=torch.int32)
+
+
+@_op("detokenize")
+def detokenize(ids: Tensor, n_ids: Optional[Tensor], vocab_off: Tensor, vocab_bytes: Tensor, skip: Tensor,
+               stride: int) -> Tuple[Tensor, Tensor, Tensor]:
+    """tokenizer.batch_decode(responses, skip_special_tokens=True) (ctx_manager.py:334-337)
+    -> (UTF-8 rows u8[B, stride], len i32[B], err u8[B])."""
+    return ops.detokenize(ids, ops.VocabTable(vocab_off, vocab_bytes, skip), stride, n_ids)
+
+
+@detokenize.register_fake
+def _(ids, n_ids, vocab_off, vocab_bytes, skip, stride):
+    B = ids.shape[0]
+    st = (int(stride) + 3) // 4 * 4
+    return (ids.new_empty(B, st, dtype=torch.uint8), ids.new_empty(B, dtype=torch.int32),
+            ids.new_empty(B, dtype=torch.uint8))
+
+
+def parse_cfg_bytes(cfg: _lib.ParseCfg) -> List[int]:
+    """An rmi_parse_cfg_t as the list of its bytes (the form the parse op takes)."""
+    import ctypes
+    return list(ctypes.string_at(ctypes.addressof(cfg), ctypes.sizeof(cfg)))
+
+
+def _parse_cfg(cfg_bytes: List[int]) -> _lib.ParseCfg:
+    import ctypes
+    if len(cfg_bytes) != ctypes.sizeof(_lib.ParseCfg):
+        raise ValueError("cfg must be the bytes of an rmi_parse_cfg_t (torch_ops.parse_cfg_bytes)")
+    return _lib.ParseCfg.from_buffer_copy(bytes(cfg_bytes))
+
+
+@_op("parse_actions")
+def parse_actions(cfg: List[int], text: Tensor, text_len: Tensor, sel: Optional[Tensor], with_spans: bool,
+                  action_text_len: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """_parse_response + _extract_map_valid_actions (ctx_manager.py:148-173, es_manager.py:230-240)
+    -> (actions i8[B,K], n_actions u8[B], spans i32[B,4] (0 rows without spans),
+        action_text u8[B,K,Lact], action_len i32[B,K], err u8[B])."""
+    c = _parse_cfg(cfg)
+    o = ops.parse_actions(c, text, text_len, sel, with_spans, action_text_len)
+    B, K = text.shape[0], int(c.K)
+    dev = text.device
+    spans = o["spans"] if o["spans"] is not None else torch.empty(0, 4, dtype=torch.int32, device=dev)
+    at = o["action_text"] if o["action_text"] is not None else torch.empty(B, K, 0, dtype=torch.uint8, device=dev)
+    al = o["action_len"] if o["action_len"] is not None else torch.zeros(B, K, dtype=torch.int32, device=dev)
+    return o["actions"], o["n_actions"], spans, at, al, o["err"]
+
+
+@parse_actions.register_fake
+def _(cfg, text, text_len, sel, with_spans, action_text_len):
+    B, K = text.shape[0], int(_parse_cfg(cfg).K)
+    return (text.new_empty(B, K, dtype=torch.int8), text.new_empty(B, dtype=torch.uint8),
+            text.new_empty(B if with_spans else 0, 4, dtype=torch.int32),
+            text.new_empty(B, K, action_text_len, dtype=torch.uint8), text.new_empty(B, K, dtype=torch.int32),
+            text.new_empty(B, dtype=torch.uint8))
+
+
+# the mutating ops return nothing: their fake kernels only have to exist
+for _name in ("sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_reset",
+              "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
+              "frozenlake_reset", "bandit_step_turn", "countdown_step_turn", "rollout_finalize"):
+    torch.library.register_fake(f"{NS}::{_name}")(lambda *a, **k: None)
+
+OPS = tuple(sorted(n for n in dir(torch.ops.ragen_amd) if not n.startswith("_")))

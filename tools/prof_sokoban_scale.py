@@ -1,12 +1,13 @@
 """Sokoban turn kernel at scale under different lanes-per-env layouts (diagnostic).
-Builds variants of libragen_amd.so into tools/_build/ (RMI_SPREAD_MAX_ENVS / RMI_SPREAD_LPE
-overrides), then times 5 turn launches at B = 8192 and B = 8192 * 128 in a child process each.
+Builds variants of libragen_amd.so into tools/_build/ (compile-time switches of sokoban.hip,
+e.g. RMI_SOKOBAN_BYTE_STORES), then times 5 turn launches at B = 8192 * tile in a child
+process each.
 usage: python tools/prof_sokoban_scale.py [build]"""
 import os, subprocess, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tools", "_build")
-VARIANTS = {"default": [], "lpe4_always": ["-DRMI_SPREAD_MAX_ENVS=1000000000", "-DRMI_SPREAD_LPE=4"],
-            "coop": ["-DRMI_COOP_ROWS=1"]}
+VARIANTS = {"default": [], "bytestore": ["-DRMI_SOKOBAN_BYTE_STORES"]}
+TILES = (1, 16, 128, 512)  # 8192 .. 4 194 304 envs (the last one past the 256 MiB Infinity Cache)
 
 
 def build():
@@ -35,7 +36,7 @@ def child(name):
     R.step()
     torch.cuda.synchronize()
     res = {}
-    for tile in (1, 16, 128):
+    for tile in TILES:
         dur, B = bench.scale_leg(R, dev, tile=tile)
         n_turns = R.env.ep.n_turns.cpu().numpy()
         act = sum(int((n_turns > t).sum()) for t in range(bench.T_TURNS)) * tile
