@@ -10,7 +10,8 @@ import os
 import torch  # noqa: F401  (load torch's libamdhip64 first so the library binds to the same HIP runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "libragen_amd.so")
+# RAGEN_AMD_LIB: a variant build of the same ABI, for the A/B tools under tools/ only
+LIB_PATH = os.environ.get("RAGEN_AMD_LIB") or os.path.join(_HERE, "_build", "libragen_amd.so")
 
 c_int32, c_int64, c_double, c_void_p, c_size_t = (ctypes.c_int32, ctypes.c_int64, ctypes.c_double,
                                                    ctypes.c_void_p, ctypes.c_size_t)

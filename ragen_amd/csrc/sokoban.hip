@@ -663,11 +663,12 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
         // (rebuild values: player 5, box 3 on a target / 4, else the fixed byte 2 / 1) instead
         // of rebuilding and storing the whole row.
         M m = (box0 ^ box) | ((M)1 << jp0) | ((M)1 << jp);
-#ifndef RMI_SOKOBAN_BYTE_STORES
+#ifdef RMI_SOKOBAN_DWORD_STORES
         if (LPE == 1) {
+          // measured variant (tools/prof_sokoban_scale.py), not built by default:
           // every dword holding a changed cell is rebuilt from the bitboards (a regular room's
           // state byte is wall 0 / player 5 / box 4 or 3 on a target / floor 1 or target 2) and
-          // stored whole: a read-modify-write of the lane's own row without byte stores
+          // stored whole.  +1.1 us per launch at 8192 envs against the byte stores below.
           uint32_t dirty = 0;
           while (m) {
             const int j = WordBits<M>::ctz(m);

@@ -3,6 +3,7 @@ import numpy as np
 import torch
 
 from .. import _lib, ops
+from ..torch_ops import ep_args
 from .base import BatchEnv
 from .configs import BanditEnvConfig
 
@@ -40,7 +41,8 @@ class BanditBatch(BatchEnv):
     # device for every env at once (rmi_pcg64_seed)
     def reset(self, seeds):
         self.seeds = np.asarray(seeds, np.int64).copy()
-        _, last = ops.pcg64_seed(torch.from_numpy(self.seeds).to(self.device), 1, self.rng)
+        rng, last = torch.ops.ragen_amd.pcg64_seed(torch.from_numpy(self.seeds).to(self.device), 1)
+        self.rng.copy_(rng)
         self.hi_is_first.copy_((last >= 0.5).to(torch.uint8))
         self._hi_first_host = self.hi_is_first.cpu().numpy()
         self.ep.reset_()
@@ -77,8 +79,12 @@ class BanditBatch(BatchEnv):
         return {s: c.lo_arm_name, s + 1: c.hi_arm_name}
 
     def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
-        t = ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty)
-        ops.bandit_step_turn(self.struct(), self.ep, t, err)
+        c = self.config
+        torch.ops.ragen_amd.bandit_step_turn(self.hi_is_first, self.rng, *ep_args(self.ep), actions, n_actions,
+                                             has_input, err, int(turn), int(max_actions_per_traj),
+                                             float(format_penalty), int(c.action_space_start), float(c.lo_arm_score),
+                                             float(c.hi_arm_loscore), float(c.hi_arm_hiscore),
+                                             float(c.hi_arm_hiscore_prob))
         self._invalidate()
 
     def render(self, i: int) -> str:

@@ -6,6 +6,7 @@ import numpy as np
 import torch
 
 from .. import _lib, ops
+from ..torch_ops import ep_args
 from .base import BatchEnv
 from .configs import CountdownEnvConfig
 
@@ -110,8 +111,11 @@ class CountdownBatch(BatchEnv):
 
     def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None,
                   answers: Optional[torch.Tensor] = None, answer_len: Optional[torch.Tensor] = None, **kw):
-        t = ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty)
-        ops.countdown_step_turn(self.struct(), self.ep, t, answers, answer_len, err)
+        c = self.config
+        torch.ops.ragen_amd.countdown_step_turn(self.nums, self.n_nums, self.target, *ep_args(self.ep), actions,
+                                                n_actions, has_input, err, answers, answer_len, int(turn),
+                                                int(max_actions_per_traj), float(format_penalty), float(c.score),
+                                                float(c.format_score))
         self._invalidate()
 
     def note_executed(self, turn, env_id, executed_ids):

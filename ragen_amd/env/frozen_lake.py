@@ -3,6 +3,7 @@ import numpy as np
 import torch
 
 from .. import _lib, ops
+from ..torch_ops import ep_args
 from .base import BatchEnv
 from .configs import FrozenLakeEnvConfig
 
@@ -87,7 +88,8 @@ class FrozenLakeBatch(BatchEnv):
         desc, s0 = self.reset_maps(self.seeds, self.nrow, float(self.config.p))
         self.init_desc.copy_(torch.from_numpy(np.ascontiguousarray(desc)))
         self.init_s.copy_(torch.from_numpy(np.ascontiguousarray(s0, dtype=np.int32)))
-        ops.pcg64_seed(torch.from_numpy(self.seeds).to(self.device), 1, self.init_rng)
+        rng, _ = torch.ops.ragen_amd.pcg64_seed(torch.from_numpy(self.seeds).to(self.device), 1)
+        self.init_rng.copy_(rng)
         self.restore()
 
     def load_state(self, desc, s0, rng):
@@ -96,19 +98,31 @@ class FrozenLakeBatch(BatchEnv):
         self.init_rng.copy_(torch.from_numpy(np.ascontiguousarray(rng).view(np.int64)))
         self.restore()
 
+    # ---- the custom ops (torch.ops.ragen_amd.*) over this batch's tensors
+    def state_args(self):
+        return (self.desc, self.s, self.rng) + ep_args(self.ep)
+
+    def dims(self):
+        return self.nrow, self.ncol, bool(self.config.is_slippery), self.cs[0], self.cs[1], self.cs[2]
+
     def restore(self):
         """Back to the post-reset state of the last reset() (one fused launch)."""
-        ops.frozenlake_reset(self.struct(), self.ep, self.init_desc, self.init_s, self.init_rng)
+        torch.ops.ragen_amd.frozenlake_reset(*self.state_args(), self.init_desc, self.init_s, self.init_rng,
+                                             *self.dims())
         self._invalidate()
 
     def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
-        t = ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty)
-        ops.frozenlake_step_turn(self.struct(), self.ep, t, err)
+        torch.ops.ragen_amd.frozenlake_step_turn(*self.state_args(), actions, n_actions, has_input, err, int(turn),
+                                                 int(max_actions_per_traj), float(format_penalty), *self.dims())
         self._invalidate()
 
-    # FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61): one device kernel for every env
+    def render_rows(self):
+        """FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61) of every env on the device."""
+        gb, gl = ops.glyph_table(self.config.grid_lookup)
+        return torch.ops.ragen_amd.frozenlake_render(self.desc, self.s, self.nrow, self.ncol, gb.tolist(),
+                                                     gl.tolist())
+
     def render_all(self):
         if self._text is None:
-            out, n = ops.frozenlake_render(self.struct(), self.B, self.config.grid_lookup, self.device)
-            self._text = ops.decode_rows(out, n)
+            self._text = ops.decode_rows(*self.render_rows())
         return self._text

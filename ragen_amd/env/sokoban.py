@@ -5,6 +5,7 @@ import numpy as np
 import torch
 
 from .. import _lib, ops
+from ..torch_ops import ep_args
 from .base import BatchEnv
 from .configs import SokobanEnvConfig
 
@@ -69,19 +70,34 @@ class SokobanBatch(BatchEnv):
         self.init_player.copy_(torch.from_numpy(np.ascontiguousarray(player)))
         self.restore()
 
+    # ---- the custom ops (torch.ops.ragen_amd.*) over this batch's tensors
+    def state_args(self):
+        """Tensor arguments of the Sokoban ops: the env SoA then the episode record."""
+        return (self.room_fixed, self.room_state, self.player, self.num_env_steps, self.boxes_on_target) + \
+            ep_args(self.ep)
+
+    def dims(self):
+        c = self.config
+        return self.H, self.W, int(c.num_boxes), int(c.max_steps)
+
     def restore(self):
         """Back to the post-reset state of the last reset() (one fused launch)."""
-        ops.sokoban_reset(self.struct(), self.ep, self.init_state, self.init_player)
+        torch.ops.ragen_amd.sokoban_reset(*self.state_args(), self.init_state, self.init_player, *self.dims())
         self._invalidate()
 
     def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
-        t = ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty)
-        ops.sokoban_step_turn(self.struct(), self.ep, t, err)
+        torch.ops.ragen_amd.sokoban_step_turn(*self.state_args(), actions, n_actions, has_input, err, int(turn),
+                                              int(max_actions_per_traj), float(format_penalty), *self.dims())
         self._invalidate()
 
-    # SokobanEnv.render text mode (sokoban/env.py:53-61): one device kernel for every env
+    def render_rows(self):
+        """SokobanEnv.render text mode (sokoban/env.py:53-61) of every env on the device:
+        -> (UTF-8 rows u8[B, stride], lengths i32[B])."""
+        gb, gl = ops.glyph_table(self.config.grid_lookup)
+        return torch.ops.ragen_amd.sokoban_render(self.room_fixed, self.room_state, self.H, self.W, gb.tolist(),
+                                                  gl.tolist())
+
     def render_all(self):
         if self._text is None:
-            out, n = ops.sokoban_render(self.struct(), self.B, self.config.grid_lookup, self.device)
-            self._text = ops.decode_rows(out, n)
+            self._text = ops.decode_rows(*self.render_rows())
         return self._text

@@ -16,6 +16,7 @@ import torch
 
 from .. import ops
 from ..env import REGISTERED_ENV_CONFIGS
+from ..torch_ops import NORM
 from ..protocol import DataProto
 
 
@@ -43,9 +44,9 @@ def get_masks_and_scores(input_ids: torch.Tensor, tokenizer, all_scores: List[Li
     for b, row in enumerate(all_scores):
         tab[:len(row), b] = row
     dev = input_ids.device
-    score, lm, rm, err = ops.masks_and_scores(
-        input_ids.to(torch.int64), special_token, reward_token, torch.from_numpy(tab).to(dev),
-        torch.tensor(n, dtype=torch.int32, device=dev), T, use_turn_scores, enable_response_mask,
+    score, lm, rm, err = torch.ops.ragen_amd.masks_and_scores(
+        input_ids.to(torch.int64).contiguous(), int(special_token), int(reward_token), torch.from_numpy(tab).to(dev),
+        torch.tensor(n, dtype=torch.int32, device=dev), T, bool(use_turn_scores), bool(enable_response_mask),
         "qwen" in tokenizer.name_or_path.lower())
     if use_turn_scores and bool(err.any()):
         raise RuntimeError("shape mismatch: a turn has more than one reward-token position "
@@ -154,7 +155,8 @@ class ContextManager:
         p = None if identity_perm else torch.from_numpy(perm).to(dev)
         a = acc if p is None else acc[p].contiguous()
         b = pen if p is None else pen[p].contiguous()
-        out = ops.group_normalize(a.contiguous(), b.contiguous(), torch.from_numpy(seg).to(dev), rn.method)
+        out = torch.ops.ragen_amd.group_normalize(a.contiguous(), b.contiguous(), ops.segments(seg, len(perm), dev),
+                                                  NORM[rn.method])
         if p is not None:
             res = torch.empty_like(out)
             res[p] = out
@@ -211,9 +213,12 @@ class ContextManager:
             if not ap.use_turn_scores:
                 normalized = self._normalize_score_tensor(score_tensor, env_outputs)
             response_length = response_mask.sum(dim=-1).float().mean().item()
-            batch["loss_mask"] = loss_mask
-            batch["rm_scores"] = normalized
-            batch["original_rm_scores"] = score_tensor  # aliases rm_scores, as in the reference
+            # one host copy: the formulated batch lives on the CPU like the reference's
+            # (ctx_manager.py:290-301), so Ray / the worker groups get a single-device batch
+            scores_host = normalized.cpu()
+            batch["loss_mask"] = loss_mask.cpu()
+            batch["rm_scores"] = scores_host
+            batch["original_rm_scores"] = scores_host  # aliases rm_scores, as in the reference
         out = DataProto(batch)
         out.non_tensor_batch = {
             "env_ids": np.array([o["env_id"] for o in env_outputs], dtype=object),

@@ -18,6 +18,7 @@ import torch
 
 from .. import _lib
 from ..env import REGISTERED_ENV_CONFIGS, REGISTERED_ENVS
+from ..torch_ops import ep_args, parse_cfg_bytes
 from ..env.base import BatchEnv
 
 
@@ -261,14 +262,15 @@ class EnvStateManager:
         -> list of per-tag parse outputs (ops.parse_actions dicts)."""
         if self._turn >= self.max_turn:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
-        from .. import ops
         if text.shape[0] != self.n_envs or text_len.shape[0] != self.n_envs:
             raise ValueError(f"text rows must cover all {self.n_envs} envs")
         outs = []
         for tg in self.tags:
             cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, prepend)
-            p = ops.parse_actions(cfg, text[tg.lo:tg.hi], text_len[tg.lo:tg.hi], sel, with_spans=False,
-                                  action_text_len=lact)
+            acts, n_act, _, at, al, perr = torch.ops.ragen_amd.parse_actions(
+                parse_cfg_bytes(cfg), text[tg.lo:tg.hi], text_len[tg.lo:tg.hi], sel, False, int(lact))
+            p = {"actions": acts, "n_actions": n_act, "action_text": at if lact else None,
+                 "action_len": al if lact else None, "err": perr}
             has = None if has_input is None else has_input[tg.lo:tg.hi]
             kw = {}
             if lact:
@@ -281,10 +283,9 @@ class EnvStateManager:
 
     def get_rollout_states(self):
         """es_manager.py:173-207 (per-env metrics reduced on the device)."""
-        from .. import ops
         for tg in self.tags:
             ep = tg.batch.ep
-            m = ops.rollout_metrics(ep).cpu().numpy()
+            m = torch.ops.ragen_amd.rollout_metrics(*ep_args(ep)).cpu().numpy()
             info = ep.turn_info.cpu().numpy()
             for i in range(tg.hi - tg.lo):
                 gid = tg.lo + i

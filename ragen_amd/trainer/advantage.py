@@ -3,8 +3,8 @@ agent_trainer.py:461-500, running on the GPU engine."""
 import torch
 
 from .. import distributed as rd
-from .. import ops
 from ..protocol import DataProto
+from ..torch_ops import FILTER
 from . import core_algos
 
 
@@ -67,12 +67,14 @@ def filter_rollout(batch: DataProto, num_groups: int, group_size: int, ratio: fl
     ``num_groups`` is the GLOBAL count (es_manager.train.env_groups), as in the reference."""
     rm = batch.batch["original_rm_scores"]
     dev = rm.device if rm.is_cuda else torch.device("cuda", torch.cuda.current_device())
-    rows = ops.row_sum(rm.to(dev, torch.float32).contiguous())
+    rows = torch.ops.ragen_amd.row_sum(rm.to(dev, torch.float32).contiguous())
 
     def select(scores, G):
         if G != num_groups:
             raise RuntimeError(f"shape '[{num_groups}, {group_size}]' is invalid for input of size {scores.numel()}")
-        keep, met, _ = ops.filter_groups(scores, G, group_size, ratio, ftype)
+        if ftype not in FILTER:
+            raise ValueError(f"Invalid rollout filter type: {ftype}")
+        keep, met, _, _, _ = torch.ops.ragen_amd.filter_groups(scores, G, group_size, float(ratio), FILTER[ftype])
         return keep, met
 
     if rd.initialized():

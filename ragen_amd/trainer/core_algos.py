@@ -19,6 +19,7 @@ import torch
 
 from .. import distributed as rd
 from .. import ops
+from ..torch_ops import VARIANT
 
 
 def _device(*xs):
@@ -33,12 +34,10 @@ def _dev(x, device):
 
 
 def _whiten(adv, mask, row_stats):
-    """In place; -> device status scalar (ops.whiten_status)."""
+    """In place; -> device status i32[1] (0 ok; 1 / 2 = verl's ValueError cases)."""
     if rd.initialized():
-        _, scratch = ops.masked_whiten_stats_(adv, rd.global_whiten_stats(row_stats))
-    else:
-        _, scratch = ops.masked_whiten_(adv, mask, row_stats)
-    return ops.whiten_status(scratch)
+        return torch.ops.ragen_amd.masked_whiten_stats_(adv, rd.global_whiten_stats(row_stats))
+    return torch.ops.ragen_amd.masked_whiten_(adv, mask, row_stats)
 
 
 def _back(out_device, tensors, status=None, err=None):
@@ -62,7 +61,7 @@ def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = T
     dev = _device(values, mask)
     x = _dev(values.float(), dev).clone()
     m = _dev(mask, dev)
-    stats = ops.whiten_row_stats(x, m)
+    stats = torch.ops.ragen_amd.whiten_row_stats(x, m)
     status = _whiten(x, m, stats)
     return _back(values.device, [x], status)[0]
 
@@ -72,7 +71,9 @@ def compute_gae_advantage_return(token_level_rewards, values, response_mask, gam
     dev = _device(token_level_rewards, values, response_mask)
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(response_mask, dev)
     stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
-    adv, ret = ops.gae(r, v, m, gamma, lam, variant, row_stats=stats)
+    if variant not in VARIANT:
+        raise ValueError(f"GAE variant must be 'legacy' or 'masked', got {variant!r}")
+    adv, ret = torch.ops.ragen_amd.gae(r, v, m, float(gamma), float(lam), VARIANT[variant], stats)
     status = _whiten(adv, m, stats)
     return tuple(_back(token_level_rewards.device, [adv, ret], status))
 
@@ -83,7 +84,7 @@ def compute_bi_level_gae_advantage_return(token_level_rewards, values, loss_mask
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(loss_mask, dev)
     stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
     err = torch.empty(r.shape[0], dtype=torch.uint8, device=dev)
-    adv, ret = ops.bilevel_gae(r, v, m, gamma, lam, high_level_gamma, row_stats=stats, check_errors=False, err=err)
+    adv, ret = torch.ops.ragen_amd.bilevel_gae(r, v, m, float(gamma), float(lam), float(high_level_gamma), stats, err)
     status = _whiten(adv, m, stats)
     return tuple(_back(token_level_rewards.device, [adv, ret], status, err))
 
@@ -105,7 +106,8 @@ def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, ep
     p = None if ident else torch.from_numpy(perm).to(dev)
     rr = r if ident else r[p].contiguous()
     mm = m if ident else m[p].contiguous()
-    adv, _ = ops.grpo_outcome(rr, mm, seg, epsilon, norm_adv_by_std_in_grpo)
+    adv, _ = torch.ops.ragen_amd.grpo_outcome(rr, mm, ops.segments(seg, rr.shape[0], dev), float(epsilon),
+                                              bool(norm_adv_by_std_in_grpo))
     if not ident:
         out = torch.empty_like(adv)
         out[p] = adv

@@ -9,6 +9,7 @@ from ragen_amd.config import default_config, env_task
 from ragen_amd.llm_agent import ContextManager, EnvStateManager, LLMAgentProxy, ScriptedActor, get_masks_and_scores
 from ragen_amd.protocol import DataProto
 from ragen_amd.trainer import compute_advantage, filter_rollout
+from fake_tok import FakeQwenTok
 from trace_util import load, strings
 
 pytestmark = pytest.mark.gpu
@@ -101,47 +102,6 @@ def test_normalize_score_tensor_golden(device):
                     for g, t, p in zip(d["group_id"], tags, d["penalty"])]
             res = cm._normalize_score_tensor(st, outs)
             np.testing.assert_allclose(res[:, -1].numpy(), d[f"norm_{grouping}_{method}"], atol=1e-5, rtol=0)
-
-
-class FakeQwenTok:
-    name_or_path = "Qwen/Qwen2.5-0.5B-Instruct"
-    IM_START, IM_END, PAD = 151644, 151645, 151643
-
-    def encode(self, text):
-        return {"<|im_start|>": [self.IM_START], "<|im_end|>": [self.IM_END]}[text]
-
-    def apply_chat_template(self, messages, add_generation_prompt, tokenize):
-        s = "".join(f"<|im_start|>{m['role']}\n{m['content']}<|im_end|>\n" for m in messages)
-        return s + ("<|im_start|>assistant\n" if add_generation_prompt else "")
-
-    def _ids(self, text):
-        out, i = [], 0
-        while i < len(text):
-            if text.startswith("<|im_start|>", i):
-                out.append(self.IM_START)
-                i += 12
-            elif text.startswith("<|im_end|>", i):
-                out.append(self.IM_END)
-                i += 10
-            else:
-                out.append(ord(text[i]) % 150000)
-                i += 1
-        return out
-
-    def __call__(self, texts, return_tensors, padding, padding_side, truncation):
-        rows = [self._ids(t) for t in texts]
-        L = max(len(r) for r in rows)
-        ids = torch.full((len(rows), L), self.PAD, dtype=torch.long)
-        am = torch.zeros((len(rows), L), dtype=torch.long)
-        for b, r in enumerate(rows):
-            ids[b, L - len(r):] = torch.tensor(r)
-            am[b, L - len(r):] = 1
-
-        class O:
-            pass
-        o = O()
-        o.input_ids, o.attention_mask = ids, am
-        return o
 
 
 def test_get_masks_and_scores_golden(device):
