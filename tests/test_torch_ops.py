@@ -1,0 +1,78 @@
+"""The custom-operator boundary (ragen_amd.torch_ops, torch.ops.ragen_amd.*) on the CPU: every
+op is registered with a schema, CPU tensors are refused by the dispatcher (no CPU path), and
+each fake kernel propagates the documented shapes and dtypes (FakeTensorMode: what torch.compile
+and FakeTensor tracing see) — no kernel is launched."""
+import pytest
+import torch
+from torch._subclasses.fake_tensor import FakeTensorMode
+
+from ragen_amd import ops, torch_ops
+
+R = torch.ops.ragen_amd
+
+MUTATING = {"sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_reset",
+            "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
+            "frozenlake_reset", "bandit_step_turn", "countdown_step_turn", "rollout_finalize", "masked_whiten_",
+            "masked_whiten_stats_", "gae", "bilevel_gae"}
+
+
+def test_every_device_entry_point_is_an_op():
+    names = set(torch_ops.OPS)
+    # the C-ABI entry points that launch kernels, by their op names
+    want = {"sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_reset",
+            "sokoban_render", "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
+            "frozenlake_reset", "frozenlake_render", "bandit_step_turn", "countdown_step_turn", "countdown_reward",
+            "rollout_metrics", "trajectory_scores", "rollout_finalize", "group_normalize", "filter_groups", "row_sum",
+            "masks_and_scores", "gae", "bilevel_gae", "masked_whiten_", "masked_whiten_stats_", "whiten_row_stats",
+            "grpo_outcome", "detokenize", "parse_actions", "pcg64_seed"}
+    assert want <= names, want - names
+    for n in MUTATING:  # the schema names what an op writes in place
+        assert "!" in str(getattr(R, n).default._schema), n
+
+
+def test_cpu_tensors_are_refused():
+    with pytest.raises(NotImplementedError):
+        R.gae(torch.zeros(2, 3), torch.zeros(2, 3), torch.zeros(2, 3, dtype=torch.uint8), 1.0, 1.0, 0, None)
+    with pytest.raises(NotImplementedError):
+        R.row_sum(torch.zeros(2, 3))
+
+
+def test_fake_kernels_shapes():
+    with FakeTensorMode():
+        d = "cuda"
+        B, L = 6, 11
+        r = torch.empty(B, L, device=d)
+        m = torch.empty(B, L, dtype=torch.uint8, device=d)
+        adv, ret = R.gae(r, r, m, 1.0, 0.95, 0, None)
+        assert adv.shape == (B, L) and adv.dtype == torch.float32
+        adv, ret = R.bilevel_gae(r, r, m, 1.0, 0.95, 0.95, None, None)
+        assert ret.shape == (B, L)
+        assert R.masked_whiten_(r, m, None).shape == (1,)
+        assert R.whiten_row_stats(r, m).shape == (B, 3)
+        seg = torch.empty(B + 1, dtype=torch.int32, device=d)
+        assert R.grpo_outcome(r, m, seg, 1e-6, True)[0].shape == (B, L)
+        assert R.row_sum(r).shape == (B,)
+        keep, met, sd, mx, mn = R.filter_groups(torch.empty(64, device=d), 4, 16, 0.25, 0)
+        assert keep.shape == (4,) and keep.dtype == torch.uint8 and met.shape == (6,)
+        ids = torch.empty(B, L, dtype=torch.int64, device=d)
+        sc, lm, rm, err = R.masks_and_scores(ids, 1, 2, torch.empty(3, B, dtype=torch.float64, device=d),
+                                             torch.empty(B, dtype=torch.int32, device=d), 3, False, True, True)
+        assert sc.shape == (B, L - 1) and lm.dtype == torch.bool and err.shape == (B,)
+        ep = ops.EpisodeState.empty(B, 5, d)
+        assert R.rollout_metrics(*torch_ops.ep_args(ep)).shape == (B, 4)
+        s, p = R.trajectory_scores(*torch_ops.ep_args(ep))
+        assert s.dtype == torch.float32 and p.shape == (B,)
+        rng, last = R.pcg64_seed(torch.empty(B, dtype=torch.int64, device=d), 1)
+        assert rng.shape == (4, B) and last.dtype == torch.float64
+        out, n = R.sokoban_render(torch.empty(B, 36, dtype=torch.uint8, device=d),
+                                  torch.empty(B, 36, dtype=torch.uint8, device=d), 6, 6, [0] * 16, [0] * 16)
+        assert out.shape == (B, torch_ops.render_stride(36, 6)) and n.dtype == torch.int32
+        cfg = ops.parse_config(True, 5, "||", {1: "Up", 2: "Down"})
+        a, na, sp, at, al, e = R.parse_actions(torch_ops.parse_cfg_bytes(cfg), torch.empty(B, 64, dtype=torch.uint8,
+                                               device=d), torch.empty(B, dtype=torch.int32, device=d), None, True, 0)
+        assert a.shape == (B, 5) and a.dtype == torch.int8 and sp.shape == (B, 4)
+        txt, tl, te = R.detokenize(torch.empty(B, 9, dtype=torch.int64, device=d), None,
+                                   torch.empty(11, dtype=torch.int64, device=d), torch.empty(40, dtype=torch.uint8,
+                                                                                          device=d),
+                                   torch.empty(10, dtype=torch.uint8, device=d), 30)
+        assert txt.shape == (B, 32)
