@@ -392,6 +392,8 @@ int rmi_pcg64_seed(const int64_t* seeds, int64_t n, int32_t draws, uint64_t* rng
 
 /* ------------------------------------------------------------------------- misc */
 const char* rmi_version(void);
+/* Stream-ordered device-to-device copy: a 16-B-per-lane grid-stride streaming kernel (the
+ * achievable-HBM-bandwidth probe bench.py reports as roofline.achievable_peak).            */
 int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t stream);
 
 #ifdef __cplusplus

@@ -36,7 +36,7 @@ def test_sokoban_op_equals_ctypes(device):
     torch.cuda.synchronize()
     _same(a, b, ("room_state", "player", "num_env_steps", "boxes_on_target"))
     ra, rb = a.render_rows(), ops.sokoban_render(b.struct(), B, b.config.grid_lookup, device)
-    assert torch.equal(ra[1], rb[1]) and torch.equal(ra[0], rb[0])
+    assert ops.decode_rows(*ra) == ops.decode_rows(*rb)  # bytes past a row's length are not written
 
 
 def test_frozenlake_bandit_countdown_op_equals_ctypes(device):

@@ -16,11 +16,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rows", type=int, default=8192)
+    ap.add_argument("--cols", type=int, default=0, help="left-pad the rows to this many tokens (0: the batch max)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
     n_turns = rng.integers(1, 6, size=a.rows)
-    r, v, m = synthetic.token_rows(n_turns, rng.standard_normal(a.rows).astype(np.float32), seed=11)
+    r, v, m = synthetic.token_rows(n_turns, rng.standard_normal(a.rows).astype(np.float32), seed=11, max_len=a.cols or None)
     r, v, m = (torch.from_numpy(x).to(dev) for x in (r, v, m))
     stats = torch.empty(a.rows, 3, dtype=torch.float64, device=dev)
     for _ in range(a.reps):
