@@ -502,31 +502,65 @@ def text_leg(R, device, reps=20):
 
 
 def api_leg(device):
-    """SURVEY §8(d)'s "API" variant of the headline: the same SK workload driven through the
-    drop-in EnvStateManager (list-of-dict inputs with action NAMES, per-turn device round trip,
-    history dicts and text observations materialised on the host), reset excluded."""
+    """SURVEY §8(d)'s "API" variant of the headline: the same SK workload (8192 envs, 5 turns, the
+    bench's synthetic actions written as LLM responses) driven through the drop-in
+    LLMAgentProxy.rollout (agent_proxy.py:143-159), reset excluded:
+    * ``device`` path — the actor hands back response token ids on the GPU (TokenActor); the
+      ContextManager decodes them on the device, EnvStateManager parses, steps and renders on
+      the device and keeps the history dicts lazy; env-steps/s over the turn loop, with the
+      end-of-rollout costs (get_rollout_states materialising the dicts, formulate_rollouts
+      tokenising the transcripts) reported beside it;
+    * ``dict`` path — EnvStateManager.step fed the reference's list of dicts with action names
+      (per-turn device round trip, host history dicts and text observations each turn)."""
+    import random
     from ragen_amd.config import env_task
-    from ragen_amd.llm_agent import EnvStateManager
-    cfg = env_task("SimpleSokoban", B_PER_GPU // GROUP, GROUP, max_turn=T_TURNS, max_actions_per_turn=K_ACTIONS)
+    from ragen_amd.llm_agent import EnvStateManager, LLMAgentProxy, TokenActor
+    from ragen_amd.protocol import DataProto
+    B, T, K = B_PER_GPU, T_TURNS, K_ACTIONS
+    cfg = env_task("SimpleSokoban", B // GROUP, GROUP, max_turn=T, max_actions_per_turn=K)
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4)
+    lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
+    table, skip = synthetic.byte_vocab()
+    tokens = [torch.from_numpy(synthetic.tokenize_greedy(synthetic.responses_for_actions(ids[t], n[t], lk,
+                                                                                        seed=100 + t), table)).to(device)
+              for t in range(T)]
+    tok = synthetic.ByteChatTokenizer()
+    actor = TokenActor(tokens)
+    proxy = LLMAgentProxy(cfg, actor, tok, device=device)
+    proxy.train_ctx_manager.set_device_vocab(ops.VocabTable.from_bytes(table, skip, device))
+    runs = []
+    for rep in range(3):
+        random.seed(rep)
+        actor.turn = 0
+        torch.cuda.synchronize()
+        out = proxy.rollout(DataProto(meta_info={}), val=False)
+        steps = int(proxy.train_es_manager.tags[0].batch.ep.turn_exec.sum().item())
+        runs.append((steps, dict(proxy.last_timing), len(out)))
+    steps, tm, rows = runs[-1]
+    device_path = {"env_steps": steps, "turn_loop_s": tm["turns_s"], "env_steps_per_s": steps / tm["turns_s"],
+                   "get_rollout_states_s": tm["rollout_states_s"], "formulate_rollouts_s": tm["formulate_s"],
+                   "rows_formulated": rows,
+                   "note": "LLMAgentProxy.rollout, generations as device token ids, lazy history; last of 3 rollouts"}
+    # the dict facade: EnvStateManager.step with the reference's list-of-dict inputs
     es = EnvStateManager(cfg, mode="train", device=device)
     es.reset(seed=synthetic.ENV_SEED)
-    ids, n = synthetic.rollout_actions(B_PER_GPU, T_TURNS, K_ACTIONS, 1, 4)
     names = {1: "Up", 2: "Down", 3: "Left", 4: "Right", 0: "Jump"}  # 0 = a name outside the action lookup
-    active = list(range(B_PER_GPU))
-    steps = 0
+    active = list(range(B))
+    dsteps = 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for t in range(T_TURNS):
+    for t in range(T):
         inputs = [{"env_id": i, "llm_response": "", "llm_raw_response": "",
                    "actions": [names[int(a)] for a in ids[t, i, :int(n[t, i])]]} for i in active]
         outs = es.step(inputs)
         active = [o["env_id"] for o in outs]
-        steps += int(es.tags[0].batch.ep.turn_exec[t].sum().item())
+        dsteps += int(es.tags[0].batch.ep.turn_exec[t].sum().item())
         if not active:
             break
     dt = time.perf_counter() - t0
-    return {"env_steps": steps, "seconds": dt, "env_steps_per_s": steps / dt,
-            "note": "EnvStateManager.step facade, 8192 envs x 5 turns, host dicts + text obs each turn"}
+    return {"env_steps_per_s": device_path["env_steps_per_s"], "device_path": device_path,
+            "dict_path": {"env_steps": dsteps, "seconds": dt, "env_steps_per_s": dsteps / dt,
+                          "note": "EnvStateManager.step facade, host dicts + text obs each turn"}}
 
 
 def cpu_baseline_parallel(R, workers=16, reps=20):

@@ -4,7 +4,11 @@ The actor is any object with ``generate_sequences(DataProto) -> DataProto`` (a v
 RayWorkerGroup, a vLLM wrapper, or a scripted policy in tests/benchmarks).  LLM
 generation itself (vLLM, API clients) is outside this engine's scope.
 """
+import time
 from typing import Dict, List
+
+import numpy as np
+import torch
 
 from ..protocol import DataProto
 from .ctx_manager import ContextManager
@@ -26,6 +30,23 @@ class ScriptedActor:
                         dict(lm_inputs.meta_info))
         self.turn += 1
         return out
+
+
+class TokenActor:
+    """Stand-in LLM whose generations are token ids on the GPU (what a device-resident policy or
+    a vLLM worker on the same GPU hands back): ``turn_tokens[t]`` i64[n_envs, R] holds every
+    env's response ids for turn t; each call returns the rows of the envs asked for."""
+
+    def __init__(self, turn_tokens):
+        self.turn_tokens = turn_tokens
+        self.turn = 0
+
+    def generate_sequences(self, lm_inputs: DataProto) -> DataProto:
+        env_ids = np.asarray(lm_inputs.non_tensor_batch["env_ids"], dtype=np.int64)
+        tok = self.turn_tokens[self.turn]
+        resp = tok[torch.from_numpy(env_ids).to(tok.device)]
+        self.turn += 1
+        return DataProto({"responses": resp}, {"env_ids": env_ids}, {})
 
 
 class LLMAgentProxy:
@@ -50,7 +71,9 @@ class LLMAgentProxy:
         ctx = self.val_ctx_manager if val else self.train_ctx_manager
         if hasattr(self.actor_wg, "turn"):
             self.actor_wg.turn = 0
+        t0 = time.perf_counter()
         env_outputs: List[Dict] = es.reset()
+        t1 = time.perf_counter()
         for _ in range(self.config.agent_proxy.max_turn):
             lm_inputs = ctx.get_lm_inputs(env_outputs, prepare_for_update=False)
             lm_inputs.meta_info = dataproto.meta_info
@@ -59,5 +82,11 @@ class LLMAgentProxy:
             env_outputs = es.step(env_inputs)
             if len(env_outputs) == 0:
                 break
+        t2 = time.perf_counter()
         rollout_states = es.get_rollout_states()
-        return ctx.formulate_rollouts(rollout_states)
+        t3 = time.perf_counter()
+        out = ctx.formulate_rollouts(rollout_states)
+        # phase wall times of the last call (the turn loop is what env-steps/s is measured on)
+        self.last_timing = {"reset_s": t1 - t0, "turns_s": t2 - t1, "rollout_states_s": t3 - t2,
+                            "formulate_s": time.perf_counter() - t3}
+        return out

@@ -54,6 +54,31 @@ def get_masks_and_scores(input_ids: torch.Tensor, tokenizer, all_scores: List[Li
     return score, lm, rm
 
 
+SPECIAL_TOKENS = ["<think>", "</think>", "<answer>", "</answer>", "<|im_start|>", "<|im_end|>"]
+
+
+def parse_response(response: str, enable_think: bool, action_sep: str, max_actions_per_turn: int):
+    """ContextManager._parse_response (ctx_manager.py:148-173) as a function of the agent_proxy
+    settings: -> (llm_response, actions).  The device path (rmi_parse_actions) computes the
+    same actions; this host form rebuilds the history strings when a device-path rollout is
+    materialised (EnvStateManager._materialize)."""
+    pattern = r"<think>(.*?)</think>\s*<answer>(.*?)</answer>" if enable_think else r"<answer>(.*?)</answer>"
+    match = re.search(pattern, response, re.DOTALL)
+    if not match:
+        return response, []
+    think_content, action_content = (match.group(1), match.group(2)) if enable_think else ("", match.group(1))
+    for tok in SPECIAL_TOKENS:
+        action_content = action_content.replace(tok, "").strip()
+        think_content = think_content.replace(tok, "").strip()
+    actions = [a.strip() for a in action_content.split(action_sep) if a.strip()]
+    if len(actions) > max_actions_per_turn:
+        actions = actions[:max_actions_per_turn]
+        action_content = (" " + action_sep + " ").join(actions)
+    llm_response = (f"<think>{think_content}</think><answer>{action_content}</answer>" if enable_think
+                    else f"<answer>{action_content}</answer>")
+    return llm_response, actions
+
+
 def segments_for(grouping: str, env_outputs: List[Dict]):
     """Group ids of ctx_manager.py:184-191 as contiguous segments (first-seen order)."""
     if grouping == "state":
@@ -76,18 +101,119 @@ def segments_for(grouping: str, env_outputs: List[Dict]):
     return perm, seg
 
 
+class DeviceEnvInputs:
+    """What ``get_env_inputs`` returns on the device path: the generations of the active envs
+    decoded on the device (rmi_detokenize, = batch_decode(skip_special_tokens=True),
+    ctx_manager.py:334-337) into UTF-8 rows of the FULL env batch (rows of envs without a
+    generation are empty and carry no input), ready for EnvStateManager.step's device turn.
+    Iterating it yields the reference's env-input dicts (host decode + parse), built lazily."""
+
+    def __init__(self, ctx, env_ids, env_ids_t, text, text_len, err):
+        self.ctx, self.env_ids, self.env_ids_t = ctx, env_ids, env_ids_t
+        self.text, self.text_len, self.err = text, text_len, err
+        self._decoded = None
+
+    def __len__(self):
+        return len(self.env_ids)
+
+    def decoded(self):
+        """-> list[str] of every env's decoded generation (host copy; index = env id)."""
+        if self._decoded is None:
+            if bool(self.err.any()):
+                raise ValueError("a decoded generation exceeded the device row buffer (rmi_detokenize RMI_ERR_UNSUP)")
+            self._decoded = ops.decode_rows(self.text, self.text_len)
+        return self._decoded
+
+    def __iter__(self):
+        ap = self.ctx.config.agent_proxy
+        prefix = "<think>" if ap.enable_think else "<answer>"
+        texts = self.decoded()
+        for e in self.env_ids:
+            raw = prefix + texts[int(e)]
+            llm_response, actions = parse_response(raw, ap.enable_think, ap.action_sep, ap.max_actions_per_turn)
+            yield {"env_id": int(e), "llm_raw_response": raw, "llm_response": llm_response, "actions": actions}
+
+
+class _LazyNonTensor(dict):
+    """non_tensor_batch of a LazyDataProto: 'env_ids' eager, any other access builds the batch."""
+
+    def __init__(self, owner, env_ids):
+        super().__init__(env_ids=env_ids)
+        self._owner = owner
+
+    def __missing__(self, k):
+        self._owner._build()
+        return dict.__getitem__(self, k)
+
+    def _full(self):
+        self._owner._build()
+        return self
+
+    def keys(self):
+        return dict.keys(self._full())
+
+    def items(self):
+        return dict.items(self._full())
+
+    def values(self):
+        return dict.values(self._full())
+
+    def __iter__(self):
+        return dict.__iter__(self._full())
+
+
+class LazyDataProto(DataProto):
+    """The per-turn LM inputs on the device path (get_lm_inputs, ctx_manager.py:228-330): the env
+    ids right away, the chat-templated prompts and their token ids built on first access.  An
+    actor that reads only the env ids (a device-resident policy) never pays for them."""
+
+    def __init__(self, env_ids, build):
+        self._build_fn, self._built, self._batch = build, False, None
+        self.non_tensor_batch = _LazyNonTensor(self, np.asarray(env_ids, dtype=object))
+        self.meta_info = {}
+
+    @property
+    def batch(self):
+        self._build()
+        return self._batch
+
+    @batch.setter
+    def batch(self, v):
+        self._batch = v
+
+    def __len__(self):
+        return len(dict.__getitem__(self.non_tensor_batch, "env_ids"))
+
+    def _build(self):
+        if self._built:
+            return
+        self._built = True
+        real = self._build_fn()
+        self._batch = real.batch
+        dict.update(self.non_tensor_batch, real.non_tensor_batch)
+
+
 class ContextManager:
     def __init__(self, config, tokenizer, processor=None, mode: str = "train", device=None):
         self.config = config
         self.tokenizer = tokenizer
         self.processor = processor
         self.action_sep = self.config.agent_proxy.action_sep
-        self.special_token_list = ["<think>", "</think>", "<answer>", "</answer>", "<|im_start|>", "<|im_end|>"]
+        self.special_token_list = list(SPECIAL_TOKENS)
         self.es_cfg = self.config.es_manager[mode]
         self.env_nums = {tag: n * self.es_cfg.group_size
                          for n, tag in zip(self.es_cfg.env_configs.n_groups, self.es_cfg.env_configs.tags)}
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.n_envs = sum(self.env_nums.values())
+        self.device_vocab = None
         self._init_prefix_lookup()
+
+    def set_device_vocab(self, vocab: "ops.VocabTable"):
+        """Turn on the device path: generations that arrive as token ids on the GPU are decoded by
+        rmi_detokenize against this byte table (ops.VocabTable.from_tokenizer for a byte-level
+        BPE tokenizer), the turn runs on the device, prompts are built only when read."""
+        self.device_vocab = vocab
+        return self
 
     def _init_prefix_lookup(self):
         """ctx_manager.py:107-146."""
@@ -124,21 +250,7 @@ class ContextManager:
     def _parse_response(self, response: str):
         """ctx_manager.py:148-173."""
         ap = self.config.agent_proxy
-        pattern = r"<think>(.*?)</think>\s*<answer>(.*?)</answer>" if ap.enable_think else r"<answer>(.*?)</answer>"
-        match = re.search(pattern, response, re.DOTALL)
-        if not match:
-            return response, []
-        think_content, action_content = (match.group(1), match.group(2)) if ap.enable_think else ("", match.group(1))
-        for tok in self.special_token_list:
-            action_content = action_content.replace(tok, "").strip()
-            think_content = think_content.replace(tok, "").strip()
-        actions = [a.strip() for a in action_content.split(self.action_sep) if a.strip()]
-        if len(actions) > ap.max_actions_per_turn:
-            actions = actions[:ap.max_actions_per_turn]
-            action_content = (" " + self.action_sep + " ").join(actions)
-        llm_response = (f"<think>{think_content}</think><answer>{action_content}</answer>" if ap.enable_think
-                        else f"<answer>{action_content}</answer>")
-        return llm_response, actions
+        return parse_response(response, ap.enable_think, self.action_sep, ap.max_actions_per_turn)
 
     def _normalize_score_tensor(self, score_tensor: torch.Tensor, env_outputs: List[Dict]) -> torch.Tensor:
         """ctx_manager.py:175-226 on the GPU (in place on score_tensor[:, -1], as the reference)."""
@@ -165,7 +277,15 @@ class ContextManager:
         return score_tensor
 
     def get_lm_inputs(self, env_outputs: List[Dict], prepare_for_update: bool) -> DataProto:
-        """ctx_manager.py:228-330."""
+        """ctx_manager.py:228-330.  On the device path the generation inputs are lazy
+        (LazyDataProto): env ids now, prompts when the actor reads them."""
+        if self.device_vocab is not None and not prepare_for_update:
+            env_ids = env_outputs.env_ids if hasattr(env_outputs, "env_ids") else \
+                np.array([o["env_id"] for o in env_outputs], np.int64)
+            return LazyDataProto(env_ids, lambda: self.get_lm_inputs_eager(list(env_outputs)))
+        return self.get_lm_inputs_eager(env_outputs, prepare_for_update)
+
+    def get_lm_inputs_eager(self, env_outputs: List[Dict], prepare_for_update: bool = False) -> DataProto:
         ap = self.config.agent_proxy
         llm_input_texts, messages_list = [], []
         for env_output in env_outputs:
@@ -241,7 +361,11 @@ class ContextManager:
         return out
 
     def get_env_inputs(self, lm_outputs: DataProto) -> List[Dict]:
-        """ctx_manager.py:332-352."""
+        """ctx_manager.py:332-352.  Generations that arrive as token ids on the GPU with the device
+        path on are decoded there (-> DeviceEnvInputs, no host round trip)."""
+        if self.device_vocab is not None and lm_outputs.batch is not None and "responses" in lm_outputs.batch \
+                and lm_outputs.batch["responses"].is_cuda:
+            return self._device_env_inputs(lm_outputs)
         if lm_outputs.batch is not None and "responses" in lm_outputs.batch.keys():
             responses = self.tokenizer.batch_decode(lm_outputs.batch["responses"], skip_special_tokens=True)
         else:
@@ -255,5 +379,21 @@ class ContextManager:
                                "actions": actions})
         return env_inputs
 
+    def _device_env_inputs(self, lm_outputs: DataProto) -> DeviceEnvInputs:
+        vocab = self.device_vocab
+        dev = self.device
+        resp = lm_outputs.batch["responses"].to(dev)
+        env_ids = np.asarray(lm_outputs.non_tensor_batch["env_ids"], dtype=np.int64)
+        idx = torch.from_numpy(env_ids).to(dev)
+        R = resp.shape[1]
+        ids = torch.zeros(self.n_envs, R, dtype=torch.int64, device=dev)
+        n_ids = torch.zeros(self.n_envs, dtype=torch.int32, device=dev)
+        ids[idx] = resp.to(torch.int64)
+        n_ids[idx] = R
+        per_tok = vocab.max_token_bytes or 16
+        stride = min(12288, (R * per_tok + 3) // 4 * 4)
+        text, tlen, err = torch.ops.ragen_amd.detokenize(ids, n_ids, vocab.off, vocab.data, vocab.skip, stride)
+        return DeviceEnvInputs(self, env_ids, idx, text, tlen, err)
+
     def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:
-        return self.get_lm_inputs(env_outputs, prepare_for_update=True)
+        return self.get_lm_inputs_eager(env_outputs, prepare_for_update=True)

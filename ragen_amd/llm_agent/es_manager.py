@@ -32,6 +32,32 @@ class EnvStatus:
     seed: Optional[int] = None
 
 
+class LazyEnvOutputs:
+    """What ``step`` returns on the device path: the rollout-cache entries of the envs still
+    active after the turn, in input order (es_manager.py:168-169).  ``len()`` and ``env_ids``
+    are known right away (one small device -> host copy per turn); the history dicts are
+    materialised from the device record on first access."""
+
+    def __init__(self, es, env_ids):
+        self._es = es
+        self.env_ids = np.asarray(env_ids, np.int64)
+
+    def __len__(self):
+        return len(self.env_ids)
+
+    def __getitem__(self, k):
+        self._es._materialize()
+        rc = self._es.rollout_cache
+        if isinstance(k, slice):
+            return [rc[int(g)] for g in self.env_ids[k]]
+        return rc[int(self.env_ids[k])]
+
+    def __iter__(self):
+        self._es._materialize()
+        rc = self._es.rollout_cache
+        return iter([rc[int(g)] for g in self.env_ids])
+
+
 class _Tag:
     """One env tag = one contiguous env range [lo, hi) = one batch object."""
 
@@ -63,6 +89,7 @@ class EnvStateManager:
         self._init_envs()
         self.rollout_cache = None
         self._turn = 0
+        self._device_turns = []  # device-path turns whose host bookkeeping is still pending
 
     def _init_envs(self):
         n_groups = list(self.config.env_configs.n_groups)
@@ -102,6 +129,7 @@ class EnvStateManager:
         for t in self.tags:
             t.batch.reset(seeds[t.lo:t.hi])
         self._turn = 0
+        self._device_turns = []
         self._seeds = seeds
         self.rollout_cache = [{"env_id": e["env_id"], "history": [], "group_id": e["group_id"], "tag": e["tag"],
                                "penalty": 0} for e in self.envs]
@@ -113,7 +141,13 @@ class EnvStateManager:
 
     # ----------------------------------------------------------------------- step
     def step(self, all_env_inputs: List[Dict]):
-        """es_manager.py:105-171: one kernel launch per tag for the whole turn."""
+        """es_manager.py:105-171: one kernel launch per tag for the whole turn.  Given the device
+        form of the inputs (ContextManager.get_env_inputs on the device path) the turn runs
+        without host round trips (``_step_device``)."""
+        from .ctx_manager import DeviceEnvInputs
+        if isinstance(all_env_inputs, DeviceEnvInputs):
+            return self._step_device(all_env_inputs)
+        self._materialize()
         if self._turn >= self.max_turn:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
@@ -128,8 +162,6 @@ class EnvStateManager:
                 ins.append(inp)
                 gs.append(g)
         still_active = set()
-        F_TERM, F_TRUNC, F_DONE = _lib.FLAG_TERMINATED, _lib.FLAG_TRUNCATED, _lib.FLAG_DONE
-        I_PRES, I_EFF, I_VAL, I_SUCC = _lib.INFO_PRESENT, _lib.INFO_EFFECTIVE, _lib.INFO_VALID, _lib.INFO_SUCCESS
         for j, tg in enumerate(self.tags):
             inputs, gids = per_tag[j]
             if not inputs:
@@ -177,50 +209,61 @@ class EnvStateManager:
             pen = ep.penalty.cpu().numpy()
             # one host copy per turn, as Python lists (numpy scalar indexing per env is slower)
             flags, num_actions, info, n_exec = (x.tolist() for x in host[:4])
-            rw, pen = rw.tolist(), pen.tolist()
-            note = getattr(tg.batch, "note_executed", None)
             # the text observation of every env at once unless the env type renders per env
             obs = tg.batch.render_all() if type(tg.batch).render is BatchEnv.render else None
-            render = tg.batch.render
-            envs, rcache = self.envs, self.rollout_cache
-            for inp, gid, i, acts, m in zip(inputs, gids, rows, acts_l, m_l):
-                entry, cache = envs[gid], rcache[gid]
-                ne = n_exec[i]
-                executed = (acts if is_cd else [a for a in m if a != 0])[:ne]
-                if note is not None:
-                    note(t, i, executed)
-                acc = rw[i] if ne else 0
-                if is_cd and ne and acc in (0.0, 1.0):
-                    acc = int(acc)  # compute_reward returns int 0 / int score (countdown/env.py:73-78)
-                inf = info[i]
-                turn_info = {}
-                if inf & I_PRES:
-                    turn_info = {"action_is_effective": bool(inf & I_EFF), "action_is_valid": bool(inf & I_VAL),
-                                 "success": bool(inf & I_SUCC)}
-                st = entry["status"]
-                na = num_actions[i]
-                st.num_actions = na
-                st.rewards.append(acc)
-                fl = flags[i]
-                st.terminated = bool(fl & F_TERM)
-                st.truncated = bool(fl & F_TRUNC)
-                if pen[i] != 0:
-                    cache["penalty"] = pen[i]
-                hist = cache["history"]
-                h = hist[-1]
-                h["actions"] = executed
-                h["reward"] = acc
-                h["info"] = turn_info
-                h["llm_response"] = inp["llm_response"]
-                h["llm_raw_response"] = inp["llm_raw_response"]
-                hist.append({"state": obs[i] if obs is not None else render(i),
-                             "actions_left": entry["max_actions_per_traj"] - na})
-                if not (fl & F_DONE):
-                    still_active.add(gid)
+            still_active |= self._book(tg, t, inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec,
+                                       rw.tolist(), pen.tolist(), obs)
         self._turn += 1
         # only not-done envs go back for generation, in input order (es_manager.py:168-169)
         rc = self.rollout_cache
         return [rc[g] for g in gids_all if g in still_active]
+
+    def _book(self, tg, t, inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec, rw, pen, obs):
+        """The host side of one turn for one tag (es_manager.py:130-169): EnvStatus, penalty and the
+        history entries of the stepped envs, from the turn's device results (lists indexed by the
+        tag-local row).  -> the global ids of the envs still active."""
+        F_TERM, F_TRUNC, F_DONE = _lib.FLAG_TERMINATED, _lib.FLAG_TRUNCATED, _lib.FLAG_DONE
+        I_PRES, I_EFF, I_VAL, I_SUCC = _lib.INFO_PRESENT, _lib.INFO_EFFECTIVE, _lib.INFO_VALID, _lib.INFO_SUCCESS
+        is_cd = tg.env_type == "countdown"
+        note = getattr(tg.batch, "note_executed", None)
+        render = tg.batch.render
+        envs, rcache = self.envs, self.rollout_cache
+        still_active = set()
+        for inp, gid, i, acts, m in zip(inputs, gids, rows, acts_l, m_l):
+            entry, cache = envs[gid], rcache[gid]
+            ne = n_exec[i]
+            executed = (acts if is_cd else [a for a in m if a != 0])[:ne]
+            if note is not None:
+                note(t, i, executed)
+            acc = rw[i] if ne else 0
+            if is_cd and ne and acc in (0.0, 1.0):
+                acc = int(acc)  # compute_reward returns int 0 / int score (countdown/env.py:73-78)
+            inf = info[i]
+            turn_info = {}
+            if inf & I_PRES:
+                turn_info = {"action_is_effective": bool(inf & I_EFF), "action_is_valid": bool(inf & I_VAL),
+                             "success": bool(inf & I_SUCC)}
+            st = entry["status"]
+            na = num_actions[i]
+            st.num_actions = na
+            st.rewards.append(acc)
+            fl = flags[i]
+            st.terminated = bool(fl & F_TERM)
+            st.truncated = bool(fl & F_TRUNC)
+            if pen[i] != 0:
+                cache["penalty"] = pen[i]
+            hist = cache["history"]
+            h = hist[-1]
+            h["actions"] = executed
+            h["reward"] = acc
+            h["info"] = turn_info
+            h["llm_response"] = inp["llm_response"]
+            h["llm_raw_response"] = inp["llm_raw_response"]
+            hist.append({"state": obs[i] if obs is not None else render(i),
+                         "actions_left": entry["max_actions_per_traj"] - na})
+            if not (fl & F_DONE):
+                still_active.add(gid)
+        return still_active
 
     def _raise_errors(self, tg, err, rows, gids):
         """Per-env error bits of the turn launch, as the reference would surface them: an action
@@ -253,7 +296,8 @@ class EnvStateManager:
 
     # ------------------------------------------------------- get_rollout_states
     def step_text(self, text: torch.Tensor, text_len: torch.Tensor, has_input: Optional[torch.Tensor] = None,
-                  enable_think: bool = True, action_sep: str = "||", prepend: bool = True):
+                  enable_think: bool = True, action_sep: str = "||", prepend: bool = True,
+                  err: Optional[torch.Tensor] = None):
         """Device-resident turn from response text (§8(f) rank 2): rows are the envs in env-id
         order, text u8[n_envs, stride] / text_len i32[n_envs] the decoded generations (e.g.
         ops.detokenize of the response ids).  Per tag one parse launch
@@ -276,13 +320,73 @@ class EnvStateManager:
             if lact:
                 kw = {"answers": p["action_text"], "answer_len": p["action_len"]}
             tg.batch.step_turn(self._turn, p["actions"], p["n_actions"], has, tg.max_actions_per_traj,
-                               self.format_penalty, **kw)
+                               self.format_penalty, None if err is None else err[tg.lo:tg.hi], **kw)
             outs.append(p)
         self._turn += 1
         return outs
 
+    def _step_device(self, inp):
+        """One turn from the decoded generations on the device: parse + turn per tag (step_text),
+        the next observation rendered on the device, the active set read back.  The host
+        bookkeeping (EnvStatus, history dicts, penalties) is deferred to ``_materialize``."""
+        if self._turn >= self.max_turn:
+            raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
+        t = self._turn
+        dev = self.device
+        has = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
+        has[inp.env_ids_t] = 1
+        err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
+        ap = self.sys_config.agent_proxy
+        self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
+        obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
+        self._device_turns.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs})
+        flags = self.tags[0].batch.ep.flags if len(self.tags) == 1 else \
+            torch.cat([tg.batch.ep.flags for tg in self.tags])
+        still = ((flags[inp.env_ids_t] & _lib.FLAG_DONE) == 0).cpu().numpy()
+        return LazyEnvOutputs(self, inp.env_ids[still])
+
+    def _materialize(self):
+        """The host side of the pending device-path turns, in turn order: exactly what ``step``
+        records per turn (``_book``), from the device record — the per-turn rewards / info /
+        executed counts, the final flags and penalties, num_actions as the running sum of the
+        executed counts — plus the host parse of each decoded generation for the history
+        strings (llm_response, llm_raw_response, the executed action names)."""
+        if not self._device_turns:
+            return
+        from .. import ops
+        from .ctx_manager import parse_response
+        turns, self._device_turns = self._device_turns, []
+        ap = self.sys_config.agent_proxy
+        prefix = "<think>" if ap.enable_think else "<answer>"
+        rec = []
+        for tg in self.tags:
+            ep = tg.batch.ep
+            rec.append((ep.turn_reward.cpu().numpy(), ep.turn_info.cpu().numpy(), ep.turn_exec.cpu().numpy(),
+                        ep.flags.cpu().numpy(), ep.penalty.cpu().numpy()))
+        for d in turns:
+            t, inp = d["turn"], d["inp"]
+            texts = inp.decoded()
+            err = d["err"].cpu().numpy()
+            for j, tg in enumerate(self.tags):
+                gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]
+                if not gids:
+                    continue
+                rows = [g - tg.lo for g in gids]
+                raws = [prefix + texts[g] for g in gids]
+                parsed = [parse_response(r, bool(ap.enable_think), ap.action_sep, self.K) for r in raws]
+                inputs = [{"llm_response": lr, "llm_raw_response": raw} for (lr, _), raw in zip(parsed, raws)]
+                acts_l = [a for _, a in parsed]
+                m_l = tg.batch.map_actions_many(rows, acts_l)
+                self._raise_errors(tg, err[tg.lo:tg.hi], rows, gids)
+                tr, ti, te, fl, pen = rec[j]
+                num_actions = te[:t + 1].astype(np.int64).sum(0)
+                obs = ops.decode_rows(*d["obs"][j]) if j in d["obs"] else None
+                self._book(tg, t, inputs, gids, rows, acts_l, m_l, fl.tolist(), num_actions.tolist(), ti[t].tolist(),
+                           te[t].tolist(), tr[t].tolist(), pen.tolist(), obs)
+
     def get_rollout_states(self):
         """es_manager.py:173-207 (per-env metrics reduced on the device)."""
+        self._materialize()
         for tg in self.tags:
             ep = tg.batch.ep
             m = torch.ops.ragen_amd.rollout_metrics(*ep_args(ep)).cpu().numpy()

@@ -495,6 +495,7 @@ class VocabTable:
     off: torch.Tensor    # i64[V+1]
     data: torch.Tensor   # u8[total]
     skip: torch.Tensor   # u8[V]
+    max_token_bytes: int = 0  # longest token's bytes (0 = unknown): sizes the decoded rows
 
     @staticmethod
     def from_bytes(table, skip, device) -> "VocabTable":
@@ -504,7 +505,7 @@ class VocabTable:
         blob = b"".join(table)
         data = np.frombuffer(blob + b"\0" * (4 + (-len(blob)) % 4), np.uint8).copy()  # whole dwords
         return VocabTable(torch.from_numpy(off).to(device), torch.from_numpy(data).to(device),
-                          torch.from_numpy(np.asarray(skip, np.uint8)).to(device))
+                          torch.from_numpy(np.asarray(skip, np.uint8)).to(device), int(lens.max()) if len(lens) else 0)
 
     @staticmethod
     def from_tokenizer(tokenizer, device, skip_special_tokens: bool = True) -> "VocabTable":

@@ -211,3 +211,51 @@ def tokenize_greedy(texts, table, R=None):
     for j, r in enumerate(rows):
         out[j, :len(r)] = r[:R]
     return out
+
+
+class ByteChatTokenizer:
+    """Offline stand-in for the Qwen2.5 tokenizer (a hub download, unavailable here) for the
+    benchmark's end-to-end rollout: Qwen's chat template and <|im_start|> / <|im_end|> /
+    <|endoftext|> ids, every other byte its own id (0..255).  Vectorised (numpy per text), so
+    formulating an 8192-env batch takes well under a second."""
+    name_or_path = "Qwen/Qwen2.5-0.5B-Instruct (byte-level stand-in)"
+    IM_START, IM_END, PAD = 151644, 151645, 151643
+    _SPECIAL = {"<|im_start|>": 151644, "<|im_end|>": 151645, "<|endoftext|>": 151643}
+
+    def encode(self, text):
+        return [self._SPECIAL[text]] if text in self._SPECIAL else list(text.encode("utf-8"))
+
+    def apply_chat_template(self, messages, add_generation_prompt, tokenize):
+        s = "".join(f"<|im_start|>{m['role']}\n{m['content']}<|im_end|>\n" for m in messages)
+        return s + ("<|im_start|>assistant\n" if add_generation_prompt else "")
+
+    def _ids(self, text):
+        import re
+        parts = re.split(r"(<\|im_start\|>|<\|im_end\|>|<\|endoftext\|>)", text)
+        out = [np.array([self._SPECIAL[p]], np.int64) if p in self._SPECIAL else
+               np.frombuffer(p.encode("utf-8"), np.uint8).astype(np.int64) for p in parts if p]
+        return np.concatenate(out) if out else np.zeros(0, np.int64)
+
+    def __call__(self, texts, return_tensors="pt", padding=True, padding_side="left", truncation=False):
+        import torch
+        rows = [self._ids(t) for t in texts]
+        L = max(len(r) for r in rows)
+        ids = np.full((len(rows), L), self.PAD, np.int64)
+        am = np.zeros((len(rows), L), np.int64)
+        for b, r in enumerate(rows):
+            ids[b, L - len(r):] = r
+            am[b, L - len(r):] = 1
+
+        class Enc:
+            pass
+        e = Enc()
+        e.input_ids, e.attention_mask = torch.from_numpy(ids), torch.from_numpy(am)
+        return e
+
+    def batch_decode(self, rows, skip_special_tokens=True):
+        out = []
+        for r in rows:
+            r = np.asarray(r.tolist() if hasattr(r, "tolist") else r, np.int64)
+            keep = r[r < 256] if skip_special_tokens else r
+            out.append(bytes(keep.astype(np.uint8).tolist()).decode("utf-8", errors="replace"))
+        return out

@@ -46,3 +46,17 @@ class FakeQwenTok:
     def decode(self, ids, skip_special_tokens=True):
         drop = {self.IM_START, self.IM_END, self.PAD} if skip_special_tokens else set()
         return "".join(chr(int(i)) for i in ids if int(i) not in drop)
+
+    def batch_decode(self, rows, skip_special_tokens=True):
+        return [self.decode(r.tolist() if hasattr(r, "tolist") else r, skip_special_tokens) for r in rows]
+
+    def byte_table(self, V=151646):
+        """(table, skip) for ops.VocabTable.from_bytes: id -> UTF-8 of chr(id), as decode() does."""
+        table = []
+        for i in range(V):
+            try:
+                table.append(chr(i).encode("utf-8"))
+            except UnicodeEncodeError:  # surrogates
+                table.append(b"")
+        skip = [1 if i in (self.IM_START, self.IM_END, self.PAD) else 0 for i in range(V)]
+        return table, skip

@@ -1,0 +1,69 @@
+"""LLMAgentProxy.rollout on the device path (generations as token ids on the GPU -> device
+detokenize -> device parse + turn -> device render, history materialised lazily) against the
+dict path (host batch_decode -> regex -> EnvStateManager.step dicts) on the configs and
+actions of all five golden traces: the formulated batch, the metrics and every history dict
+must be identical."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from fake_tok import FakeQwenTok
+from ragen_amd import ops
+from ragen_amd.llm_agent import LLMAgentProxy, TokenActor
+from ragen_amd.protocol import DataProto
+from test_gpu_facade import TRACES, _config, _hashseed0_reseed
+from trace_util import load, strings
+
+pytestmark = pytest.mark.gpu
+
+
+def _turn_tokens(name, tok, device):
+    d = load(name)
+    S = strings()[name]
+    B, T = int(d["B"]), int(d["T"])
+    rows = []
+    for t in range(T):
+        texts = []
+        for i in range(B):
+            if name == "countdown_es":
+                a = S["answers"][t][i]
+                acts = [] if a is None else [a]
+            else:
+                acts = [S["vocab"][c] for c in d["codes"][t, i] if c >= 0]
+            texts.append(f"thinking about turn {t}</think> <answer>{' || '.join(acts)}</answer>")
+        ids = [tok._ids(x) for x in texts]
+        R = max(len(x) for x in ids)
+        a = np.full((B, R), tok.PAD, np.int64)
+        for i, x in enumerate(ids):
+            a[i, :len(x)] = x
+        rows.append(torch.from_numpy(a).to(device))
+    return rows
+
+
+def _rollout(name, device, vocab):
+    tok = FakeQwenTok()
+    proxy = LLMAgentProxy(_config(name), TokenActor(_turn_tokens(name, tok, device)), tok, device=device)
+    if vocab is not None:
+        proxy.train_ctx_manager.set_device_vocab(vocab)
+    random.seed(7)
+    out = proxy.rollout(DataProto(meta_info={}), val=False)
+    return out, proxy.train_es_manager.rollout_cache
+
+
+@pytest.mark.parametrize("name", list(TRACES))
+def test_device_rollout_equals_dict_rollout(device, name, monkeypatch):
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok()
+    vocab = ops.VocabTable.from_bytes(*tok.byte_table(), device)
+    ref, ref_cache = _rollout(name, device, None)
+    dev, dev_cache = _rollout(name, device, vocab)
+    assert set(ref.batch.keys()) == set(dev.batch.keys())
+    for k in ref.batch.keys():
+        assert torch.equal(ref.batch[k], dev.batch[k]), k
+    assert ref.meta_info == dev.meta_info
+    assert list(ref.non_tensor_batch["env_ids"]) == list(dev.non_tensor_batch["env_ids"])
+    assert list(ref.non_tensor_batch["messages_list"]) == list(dev.non_tensor_batch["messages_list"])
+    assert ref_cache == dev_cache
