@@ -65,5 +65,6 @@ def test_device_rollout_equals_dict_rollout(device, name, monkeypatch):
         assert torch.equal(ref.batch[k], dev.batch[k]), k
     assert ref.meta_info == dev.meta_info
     assert list(ref.non_tensor_batch["env_ids"]) == list(dev.non_tensor_batch["env_ids"])
-    assert list(ref.non_tensor_batch["messages_list"]) == list(dev.non_tensor_batch["messages_list"])
+    assert np.asarray(ref.non_tensor_batch["messages_list"]).tolist() == \
+        np.asarray(dev.non_tensor_batch["messages_list"]).tolist()
     assert ref_cache == dev_cache
