@@ -242,6 +242,31 @@ def advantage_leg(R, device, reps=20):
     torch.cuda.synchronize()
     masks_us = e[0].elapsed_time(e[1]) * 1e3 / reps
     mgbs = B * (L + 1) * 14 / (masks_us * 1e-6) / 1e9
+    # the whole formulate batch in one pass (rmi_assemble_batch): ragged rows (the same ids, each
+    # row cut to its own length) -> padded ids, attention_mask, position_ids, masks, scores;
+    # 8 B/token in, 30 B/token out (3 x i64, f32 score, 2 masks)
+    lens = torch.randint(L // 2, L + 2, (B,), generator=g, device=device)
+    keep = torch.arange(L + 1, device=device)[None, :] < lens[:, None]
+    toks = ids[keep].contiguous()
+    off = torch.zeros(B + 1, dtype=torch.int64, device=device)
+    off[1:] = torch.cumsum(lens, 0)
+    S_asm = int(lens.max())
+    for _ in range(3):
+        ops.assemble_batch(toks, off, S_asm, 151643, 151644, 151645, R.env.ep.turn_reward, n_sc, T_TURNS, False,
+                           True, True)
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(reps):
+        ops.assemble_batch(toks, off, S_asm, 151643, 151644, 151645, R.env.ep.turn_reward, n_sc, T_TURNS, False,
+                           True, True)
+    e[1].record()
+    torch.cuda.synchronize()
+    asm_us = e[0].elapsed_time(e[1]) * 1e3 / reps
+    asm_bytes = toks.numel() * 8 + B * S_asm * 24 + B * (S_asm - 1) * 6
+    assemble = {"kernel": "rmi_assemble_batch", "rows": B, "S": S_asm, "tokens": int(toks.numel()), "us": asm_us,
+                "achieved_GBs": asm_bytes / (asm_us * 1e-6) / 1e9, "frac": asm_bytes / (asm_us * 1e-6) / 1e9 /
+                HBM_PEAK_GBS, "bytes": int(asm_bytes)}
+    del toks, keep
     # bi-level GAE (turn-level rewards at each turn's last response token) and GRPO outcome
     tr = R.env.ep.turn_reward.t().contiguous().cpu().numpy().astype(np.float32)
     tr[tr == 0] = 0.5  # a zero turn reward would end the row's high-level segment early
@@ -270,6 +295,7 @@ def advantage_leg(R, device, reps=20):
             "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS, "bytes_per_token": 17,
             "masks_and_scores": {"kernel": "rmi_masks_and_scores", "us": masks_us, "achieved_GBs": mgbs,
                                  "frac": mgbs / HBM_PEAK_GBS, "bytes_per_token": 14},
+            "assemble_batch": assemble,
             "bilevel_gae": {"kernel": "rmi_bilevel_gae", "tokens": tok_b, "us": bl_us,
                             "achieved_GBs": tok_b * 17 / (bl_us * 1e-6) / 1e9},
             "grpo": {"kernel": "rmi_grpo_outcome", "tokens": tok_b, "us": grpo_us,

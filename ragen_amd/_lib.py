@@ -109,6 +109,9 @@ _SIGS = {
     "rmi_row_sum": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "rmi_masks_and_scores": (c_int32, [c_void_p, c_int64, c_int64, c_int64, c_int64, c_void_p, c_void_p, c_int32,
                                        c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_assemble_batch": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64, c_void_p,
+                                     c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_gae": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_double, c_double, c_int32, c_void_p,
                           c_void_p, c_void_p, c_void_p]),
     "rmi_bilevel_gae": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_double, c_double, c_double,

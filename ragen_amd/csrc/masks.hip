@@ -31,12 +31,26 @@ struct __attribute__((packed, aligned(4))) F4u {
 
 constexpr int kSuper = 8;  // chunks whose loads are issued together (2048 ids per row)
 
+// The batch assembly of formulate_rollouts (ctx_manager.py:278-306) fused into the same pass
+// (kAsm): row b of the left-padded batch is pad_id * (S - n_b) followed by the row's n_b
+// tokens tokens[off[b] .. off[b+1]); the pass writes input_ids, attention_mask (1 on the
+// tokens) and position_ids = cumsum(attention_mask) next to the masks and scores.
+struct AsmArgs {
+  const int64_t* tokens;
+  const int64_t* off;
+  int64_t pad_id;
+  int64_t* input_ids;
+  int64_t* attention_mask;
+  int64_t* position_ids;
+};
+
+template <bool kAsm>
 __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ ids, int64_t B, int64_t S, int64_t sp,
                                                    int64_t rt, const double* __restrict__ scores,
                                                    const int32_t* __restrict__ n_scores, int T, int n_slots,
                                                    int flags, float* __restrict__ score_out,
                                                    uint8_t* __restrict__ lmask, uint8_t* __restrict__ rmask,
-                                                   uint8_t* __restrict__ err) {
+                                                   uint8_t* __restrict__ err, AsmArgs as) {
   __shared__ int pos[kMaxSlots], cnt[kMaxSlots];
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
@@ -44,7 +58,19 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   cnt[lane] = 0;
   __syncthreads();
   const int64_t So = S - 1;  // output columns
-  const int64_t* row = ids + b * S;
+  const int64_t* row = kAsm ? nullptr : ids + b * S;
+  int64_t a_src = 0, pad = 0;
+  if (kAsm) {
+    const int64_t o0 = as.off[b], o1 = as.off[b + 1];
+    pad = S - (o1 - o0);
+    if (pad < 0) {  // a row longer than S: flagged, assembled from its last S tokens
+      if (lane == 0) err[b] |= RMI_ERR_STATE;
+      a_src = o1 - S;
+      pad = 0;
+    } else {
+      a_src = o0 - pad;  // column p holds tokens[a_src + p] for p >= pad
+    }
+  }
   float* srow = score_out + b * So;
   uint8_t* lrow = lmask + b * So;
   uint8_t* rrow = rmask + b * So;
@@ -56,12 +82,26 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
     // 1. every load of the super-chunk in flight together (clamped addresses, branch-free);
     //    the group at the row end and groups past it are fixed up element-wise afterwards
     I64x4 v[kSuper];
+    if (kAsm) {  // padded ids from the ragged rows, element-wise (the pad shifts the alignment)
 #pragma unroll
-    for (int k = 0; k < kSuper; ++k) {
-      const int64_t p0 = s0 + k * kChunk + kTok * lane;
-      v[k] = *reinterpret_cast<const I64x4*>(row + (p0 + kTok <= S ? p0 : 0));
+      for (int k = 0; k < kSuper; ++k) {
+        const int64_t p0 = s0 + k * kChunk + kTok * lane;
+        int64_t e4[kTok];
+#pragma unroll
+        for (int e = 0; e < kTok; ++e) {
+          const int64_t p = p0 + e;
+          e4[e] = p >= S ? none : (p < pad ? as.pad_id : as.tokens[a_src + p]);
+        }
+        v[k] = I64x4{e4[0], e4[1], e4[2], e4[3]};
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kSuper; ++k) {
+        const int64_t p0 = s0 + k * kChunk + kTok * lane;
+        v[k] = *reinterpret_cast<const I64x4*>(row + (p0 + kTok <= S ? p0 : 0));
+      }
     }
-    if (s0 + kSuper * kChunk > S) {
+    if (!kAsm && s0 + kSuper * kChunk > S) {
 #pragma unroll
       for (int k = 0; k < kSuper; ++k) {
         const int64_t p0 = s0 + k * kChunk + kTok * lane;
@@ -78,6 +118,20 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
       const int64_t p0 = s0 + k * kChunk + kTok * lane;
       if (s0 + k * kChunk >= S) break;  // wave-uniform
       const int64_t t[kTok] = {v[k].a, v[k].b, v[k].c, v[k].d};
+      if (kAsm) {  // input_ids, attention_mask, position_ids of the padded row
+        int64_t* io = as.input_ids + b * S;
+        int64_t* ao = as.attention_mask + b * S;
+        int64_t* po = as.position_ids + b * S;
+#pragma unroll
+        for (int e = 0; e < kTok; ++e) {
+          const int64_t p = p0 + e;
+          if (p < S) {
+            io[p] = t[e];
+            ao[p] = p >= pad ? 1 : 0;
+            po[p] = p >= pad ? p - pad + 1 : 0;
+          }
+        }
+      }
       int st[kTok], c = 0;
 #pragma unroll
       for (int e = 0; e < kTok; ++e) {
@@ -130,6 +184,7 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   // a __threadfence() here would add an L2 write-back per row
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (So <= 0) return;  // a one-column batch has no score / mask columns
   if (!turn_scores) {
     if (lane == 0) {  // score_tensor[:, -1] = python sum(all_scores[b]), kept by [:, 1:]
       double sum = 0.0;
@@ -175,8 +230,27 @@ RMI_API int rmi_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64
   if (B == 0 || S <= 1) return RMI_OK;
   if (!ids || !n_scores || !score_out || !loss_mask || !response_mask || !err || (T > 0 && !scores))
     return RMI_EINVAL;
-  hipLaunchKernelGGL(masks_kernel, dim3((unsigned)B), dim3(64), 0, as_stream(stream), ids, B, S, special_token,
+  hipLaunchKernelGGL(masks_kernel<false>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), ids, B, S, special_token,
                      reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out, loss_mask,
-                     response_mask, err);
+                     response_mask, err, AsmArgs{});
+  return launch_status();
+}
+
+RMI_API int rmi_assemble_batch(const int64_t* tokens, const int64_t* row_off, int64_t B, int64_t S, int64_t pad_id,
+                               int64_t special_token, int64_t reward_token, const double* scores,
+                               const int32_t* n_scores, int32_t T, int32_t n_slots, int32_t flags, int64_t* input_ids,
+                               int64_t* attention_mask, int64_t* position_ids, float* score_out, uint8_t* loss_mask,
+                               uint8_t* response_mask, uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || S < 1 || T < 0 || n_slots < 0) return RMI_EINVAL;
+  if (n_slots > kMaxSlots || B > 0x7FFFFFFF) return RMI_EUNSUP;
+  if (B == 0) return RMI_OK;
+  if (!tokens || !row_off || !input_ids || !attention_mask || !position_ids || !n_scores || !err ||
+      (T > 0 && !scores) || (S > 1 && (!score_out || !loss_mask || !response_mask)))
+    return RMI_EINVAL;
+  hipLaunchKernelGGL(masks_kernel<true>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), nullptr, B, S,
+                     special_token, reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out,
+                     loss_mask, response_mask, err, AsmArgs{tokens, row_off, pad_id, input_ids, attention_mask,
+                                                            position_ids});
   return launch_status();
 }

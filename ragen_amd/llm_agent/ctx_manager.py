@@ -29,6 +29,17 @@ def get_special_tokens(tokenizer):
     raise ValueError(f"Unsupported model: {tokenizer.name_or_path}")
 
 
+def _score_table(all_scores, B, dev):
+    """all_scores (per row a list of turn rewards) -> (f64[T, B] turn-major, i32[B] lengths, T)."""
+    all_scores = all_scores if all_scores is not None else [[] for _ in range(B)]
+    n = [len(x) for x in all_scores]
+    T = max(n) if n else 0
+    tab = np.zeros((max(T, 1), B), np.float64)
+    for b, row in enumerate(all_scores):
+        tab[:len(row), b] = row
+    return torch.from_numpy(tab).to(dev), torch.tensor(n, dtype=torch.int32, device=dev), T
+
+
 def get_masks_and_scores(input_ids: torch.Tensor, tokenizer, all_scores: List[List[float]] = None,
                          use_turn_scores: bool = False, enable_response_mask: bool = False):
     """ctx_manager.py:35-70 on the device holding ``input_ids``: one HIP kernel
@@ -37,21 +48,40 @@ def get_masks_and_scores(input_ids: torch.Tensor, tokenizer, all_scores: List[Li
     assignment would (a turn with more than one reward-token position)."""
     special_token, reward_token = get_special_tokens(tokenizer)
     B = input_ids.shape[0]
-    all_scores = all_scores if all_scores is not None else [[] for _ in range(B)]
-    n = [len(x) for x in all_scores]
-    T = max(n) if n else 0
-    tab = np.zeros((max(T, 1), B), np.float64)
-    for b, row in enumerate(all_scores):
-        tab[:len(row), b] = row
     dev = input_ids.device
+    tab, n, T = _score_table(all_scores, B, dev)
     score, lm, rm, err = torch.ops.ragen_amd.masks_and_scores(
-        input_ids.to(torch.int64).contiguous(), int(special_token), int(reward_token), torch.from_numpy(tab).to(dev),
-        torch.tensor(n, dtype=torch.int32, device=dev), T, bool(use_turn_scores), bool(enable_response_mask),
-        "qwen" in tokenizer.name_or_path.lower())
+        input_ids.to(torch.int64).contiguous(), int(special_token), int(reward_token), tab, n, T,
+        bool(use_turn_scores), bool(enable_response_mask), "qwen" in tokenizer.name_or_path.lower())
     if use_turn_scores and bool(err.any()):
         raise RuntimeError("shape mismatch: a turn has more than one reward-token position "
                            "(reference score_tensor[reward_position] = scores)")
     return score, lm, rm
+
+
+def assemble_batch(rows, tokenizer, all_scores, use_turn_scores: bool, enable_response_mask: bool, device):
+    """The tokenizer's left-padded batch + attention_mask + position_ids (ctx_manager.py:278-306)
+    and get_masks_and_scores on it, from ragged token rows (lists / arrays of ids), in one device
+    pass (rmi_assemble_batch).  -> device tensors (input_ids, attention_mask, position_ids,
+    score, loss_mask, response_mask)."""
+    special_token, reward_token = get_special_tokens(tokenizer)
+    lens = np.array([len(r) for r in rows], np.int64)
+    B = len(rows)
+    off = np.zeros(B + 1, np.int64)
+    np.cumsum(lens, out=off[1:])
+    flat = np.concatenate([np.asarray(r, np.int64) for r in rows]) if B else np.zeros(0, np.int64)
+    S = int(lens.max()) if B else 0
+    pad = tokenizer.pad_token_id if getattr(tokenizer, "pad_token_id", None) is not None else 0
+    tab, n, T = _score_table(all_scores, B, device)
+    out = torch.ops.ragen_amd.assemble_batch(
+        torch.from_numpy(flat if flat.size else np.zeros(1, np.int64)).to(device), torch.from_numpy(off).to(device),
+        S, int(pad), int(special_token), int(reward_token), tab, n, T, bool(use_turn_scores),
+        bool(enable_response_mask), "qwen" in tokenizer.name_or_path.lower())
+    ids, am, pos, score, lm, rm, err = out
+    if use_turn_scores and bool(err.any()):
+        raise RuntimeError("shape mismatch: a turn has more than one reward-token position "
+                           "(reference score_tensor[reward_position] = scores)")
+    return ids, am, pos, score, lm, rm
 
 
 SPECIAL_TOKENS = ["<think>", "</think>", "<answer>", "</answer>", "<|im_start|>", "<|im_end|>"]
@@ -317,28 +347,33 @@ class ContextManager:
                 text += "<think>" if ap.enable_think else "<answer>"
             llm_input_texts.append(text)
             messages_list.append(messages)
-        inputs = self.tokenizer(llm_input_texts, return_tensors="pt", padding=True, padding_side="left",
-                                truncation=False)
-        input_ids, attention_mask = inputs.input_ids, inputs.attention_mask
-        position_ids = attention_mask.cumsum(dim=-1)
-        batch = {"input_ids": input_ids, "attention_mask": attention_mask, "position_ids": position_ids,
-                 "responses": input_ids[:, 1:]}
         if prepare_for_update:
+            # ragged token rows -> the padded batch, masks and scores in one device pass
+            # (rmi_assemble_batch); the batch is copied to the CPU, single-device like the
+            # reference's (ctx_manager.py:290-301)
             scores = [[i.get("reward", 0.0) for i in o["history"]] for o in env_outputs]
-            ids_dev = input_ids.to(self.device)
-            score_tensor, loss_mask, response_mask = get_masks_and_scores(
-                ids_dev, self.tokenizer, scores, use_turn_scores=ap.use_turn_scores,
-                enable_response_mask=self.config.enable_response_mask)
+            enc = self.tokenizer(llm_input_texts, padding=False, truncation=False)
+            ids, am, pos, score_tensor, loss_mask, response_mask = assemble_batch(
+                enc.input_ids, self.tokenizer, scores, ap.use_turn_scores, self.config.enable_response_mask,
+                self.device)
             normalized = score_tensor
             if not ap.use_turn_scores:
                 normalized = self._normalize_score_tensor(score_tensor, env_outputs)
             response_length = response_mask.sum(dim=-1).float().mean().item()
-            # one host copy: the formulated batch lives on the CPU like the reference's
-            # (ctx_manager.py:290-301), so Ray / the worker groups get a single-device batch
+            input_ids = ids.cpu()
+            batch = {"input_ids": input_ids, "attention_mask": am.cpu(), "position_ids": pos.cpu(),
+                     "responses": input_ids[:, 1:]}
             scores_host = normalized.cpu()
             batch["loss_mask"] = loss_mask.cpu()
             batch["rm_scores"] = scores_host
             batch["original_rm_scores"] = scores_host  # aliases rm_scores, as in the reference
+        else:
+            inputs = self.tokenizer(llm_input_texts, return_tensors="pt", padding=True, padding_side="left",
+                                    truncation=False)
+            input_ids, attention_mask = inputs.input_ids, inputs.attention_mask
+            position_ids = attention_mask.cumsum(dim=-1)
+            batch = {"input_ids": input_ids, "attention_mask": attention_mask, "position_ids": position_ids,
+                     "responses": input_ids[:, 1:]}
         out = DataProto(batch)
         out.non_tensor_batch = {
             "env_ids": np.array([o["env_id"] for o in env_outputs], dtype=object),

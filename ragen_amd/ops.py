@@ -609,6 +609,40 @@ def masks_and_scores(ids: torch.Tensor, special_token: int, reward_token: int, s
     return score, lm, rm, err
 
 
+def assemble_batch(tokens: torch.Tensor, row_off: torch.Tensor, S: int, pad_id: int, special_token: int,
+                   reward_token: int, scores: torch.Tensor, n_scores: torch.Tensor, n_slots: int, use_turn_scores: bool,
+                   enable_response_mask: bool, roll: bool):
+    """The formulate_rollouts batch (ctx_manager.py:278-306) from ragged token rows in one pass:
+    tokens i64[N] (rows back to back), row_off i64[B+1], S >= the longest row.
+    -> (input_ids, attention_mask, position_ids i64[B,S], score f32[B,S-1], loss_mask,
+        response_mask bool[B,S-1], err u8[B])."""
+    _dev(tokens, row_off, scores, n_scores)
+    _dt(tokens, torch.int64, "tokens")
+    _dt(row_off, torch.int64, "row_off")
+    _dt(scores, torch.float64, "scores")
+    _dt(n_scores, torch.int32, "n_scores")
+    B = row_off.numel() - 1
+    T = scores.shape[0] if scores.dim() == 2 else 0
+    if T and scores.shape[1] != B:
+        raise ValueError(f"scores must be [T, B={B}], got {tuple(scores.shape)}")
+    dev = tokens.device
+    So = max(int(S) - 1, 0)
+    ids = torch.empty(B, S, dtype=torch.int64, device=dev)
+    am = torch.empty_like(ids)
+    pos = torch.empty_like(ids)
+    score = torch.empty(B, So, dtype=torch.float32, device=dev)
+    lm = torch.empty(B, So, dtype=torch.bool, device=dev)
+    rm = torch.empty(B, So, dtype=torch.bool, device=dev)
+    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    flags = ((_lib.MS_TURN_SCORES if use_turn_scores else 0) | (_lib.MS_RESPONSE_MASK if enable_response_mask else 0)
+             | (_lib.MS_ROLL if roll else 0))
+    check(lib().rmi_assemble_batch(_ptr(tokens), _ptr(row_off), B, int(S), int(pad_id), int(special_token),
+                                   int(reward_token), _ptr(scores), _ptr(n_scores), T, int(n_slots), flags, _ptr(ids),
+                                   _ptr(am), _ptr(pos), _ptr(score), _ptr(lm), _ptr(rm), _ptr(err), _stream(dev)),
+          "rmi_assemble_batch")
+    return ids, am, pos, score, lm, rm, err
+
+
 # ------------------------------------------------------------------------ advantages
 def _mask_u8(mask: torch.Tensor) -> torch.Tensor:
     """A boolean mask as u8 bytes.  The kernels read any nonzero byte as 1 (RAGEN passes a bool

@@ -220,6 +220,7 @@ class ByteChatTokenizer:
     formulating an 8192-env batch takes well under a second."""
     name_or_path = "Qwen/Qwen2.5-0.5B-Instruct (byte-level stand-in)"
     IM_START, IM_END, PAD = 151644, 151645, 151643
+    pad_token_id = 151643
     _SPECIAL = {"<|im_start|>": 151644, "<|im_end|>": 151645, "<|endoftext|>": 151643}
 
     def encode(self, text):
@@ -239,6 +240,10 @@ class ByteChatTokenizer:
     def __call__(self, texts, return_tensors="pt", padding=True, padding_side="left", truncation=False):
         import torch
         rows = [self._ids(t) for t in texts]
+        if not padding:  # ragged rows, as a HF tokenizer's padding=False
+            o = type("Enc", (), {})()
+            o.input_ids = rows
+            return o
         L = max(len(r) for r in rows)
         ids = np.full((len(rows), L), self.PAD, np.int64)
         am = np.zeros((len(rows), L), np.int64)

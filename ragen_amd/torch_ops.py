@@ -362,6 +362,27 @@ def _(ids, special_token, reward_token, scores, n_scores, n_slots, use_turn_scor
             ids.new_empty(B, So, dtype=torch.bool), ids.new_empty(B, dtype=torch.uint8))
 
 
+@_op("assemble_batch")
+def assemble_batch(tokens: Tensor, row_off: Tensor, S: int, pad_id: int, special_token: int, reward_token: int,
+                   scores: Tensor, n_scores: Tensor, n_slots: int, use_turn_scores: bool, enable_response_mask: bool,
+                   roll: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """formulate_rollouts' batch (ctx_manager.py:278-306) from ragged token rows, one pass ->
+    (input_ids, attention_mask, position_ids, score, loss_mask, response_mask, err)."""
+    return ops.assemble_batch(tokens, row_off, S, pad_id, special_token, reward_token, scores, n_scores, n_slots,
+                              use_turn_scores, enable_response_mask, roll)
+
+
+@assemble_batch.register_fake
+def _(tokens, row_off, S, pad_id, special_token, reward_token, scores, n_scores, n_slots, use_turn_scores,
+      enable_response_mask, roll):
+    B = row_off.shape[0] - 1
+    So = max(S - 1, 0)
+    i = tokens.new_empty(B, S, dtype=torch.int64)
+    return (i, torch.empty_like(i), torch.empty_like(i), tokens.new_empty(B, So, dtype=torch.float32),
+            tokens.new_empty(B, So, dtype=torch.bool), tokens.new_empty(B, So, dtype=torch.bool),
+            tokens.new_empty(B, dtype=torch.uint8))
+
+
 # ================================================================== advantages (A13)
 @_op("gae", ("row_stats",))
 def gae(r: Tensor, v: Tensor, mask: Tensor, gamma: float, lam: float, variant: int,

@@ -6,6 +6,7 @@ import torch
 class FakeQwenTok:
     name_or_path = "Qwen/Qwen2.5-0.5B-Instruct"
     IM_START, IM_END, PAD = 151644, 151645, 151643
+    pad_token_id = 151643
 
     def encode(self, text):
         return {"<|im_start|>": [self.IM_START], "<|im_end|>": [self.IM_END]}[text]
@@ -28,8 +29,12 @@ class FakeQwenTok:
                 i += 1
         return out
 
-    def __call__(self, texts, return_tensors, padding, padding_side, truncation):
+    def __call__(self, texts, return_tensors="pt", padding=True, padding_side="left", truncation=False):
         rows = [self._ids(t) for t in texts]
+        if not padding:  # ragged rows, as a HF tokenizer's padding=False
+            o = type("Enc", (), {})()
+            o.input_ids = rows
+            return o
         L = max(len(r) for r in rows)
         ids = torch.full((len(rows), L), self.PAD, dtype=torch.long)
         am = torch.zeros((len(rows), L), dtype=torch.long)
