@@ -59,7 +59,7 @@ def get_masks_and_scores(input_ids: torch.Tensor, tokenizer, all_scores: List[Li
     return score, lm, rm
 
 
-def assemble_batch(rows, tokenizer, all_scores, use_turn_scores: bool, enable_response_mask: bool, device):
+def assemble_batch(rows, tokenizer, all_scores, use_turn_scores: bool, enable_response_mask: bool, device, S=None):
     """The tokenizer's left-padded batch + attention_mask + position_ids (ctx_manager.py:278-306)
     and get_masks_and_scores on it, from ragged token rows (lists / arrays of ids), in one device
     pass (rmi_assemble_batch).  -> device tensors (input_ids, attention_mask, position_ids,
@@ -70,7 +70,7 @@ def assemble_batch(rows, tokenizer, all_scores, use_turn_scores: bool, enable_re
     off = np.zeros(B + 1, np.int64)
     np.cumsum(lens, out=off[1:])
     flat = np.concatenate([np.asarray(r, np.int64) for r in rows]) if B else np.zeros(0, np.int64)
-    S = int(lens.max()) if B else 0
+    S = (int(lens.max()) if B else 0) if S is None else int(S)  # the tokenizer pads to the longest row
     pad = tokenizer.pad_token_id if getattr(tokenizer, "pad_token_id", None) is not None else 0
     tab, n, T = _score_table(all_scores, B, device)
     out = torch.ops.ragen_amd.assemble_batch(

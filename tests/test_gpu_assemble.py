@@ -39,7 +39,7 @@ def test_assemble_golden(device):
     tok = FakeQwenTok()
     for uts in (False, True):
         for erm in (False, True):
-            i, am, pos, sc, lm, rm = assemble_batch(rows, tok, scores, uts, erm, device)
+            i, am, pos, sc, lm, rm = assemble_batch(rows, tok, scores, uts, erm, device, S=ids.shape[1])
             key = f"uts{int(uts)}_erm{int(erm)}"
             np.testing.assert_array_equal(i.cpu().numpy(), ids)
             ref_am = (np.arange(ids.shape[1])[None, :] >= (ids.shape[1] - np.array([len(r) for r in rows]))[:, None])
