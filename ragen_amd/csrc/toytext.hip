@@ -65,6 +65,130 @@ struct FrozenLakeDev {
   }
 };
 
+// ---- the 4x4 turn, straight-line (the bench's and RAGEN's FrozenLake: size 4)
+// The generic turn (run_turn over FrozenLakeDev::step) is a data-dependent loop: a wave pays
+// every branch side of every lane, ~300 instructions per step.  For 4x4 maps the whole turn is
+// written as K predicated steps on bitboards (hole / goal bits of the 16 cells, s in 0..15):
+//  * the exec list (known-name actions in order, es_manager.py:156) is compacted first, so
+//    step k always consumes draw k of the turn;
+//  * the turn's <= K PCG64 draws are the LCG chain's next K outputs, computed up front in one
+//    block (their only dependence is the chain itself, not the steps) — the state after the
+//    turn is chain state number `exec`;
+//  * categorical_sample's argmax(cumsum(p) > u) with u = (x >> 11) * 2^-53 compares the 53-bit
+//    integer against ceil(cs_i * 2^53) (exact: cs_i * 2^53 is an exact double);
+//  * rows and columns are s >> 2 and s & 3.
+// Same results bit for bit as the generic turn (FrozenLakeDev::step); taken when every lane
+// of the wave has a 4x4 map, a state in range and action ids in 0..4.
+struct Fl4Out {
+  TurnOut o;
+  bool turn_done, succ_last;
+  int s;
+  Pcg64 rng;
+};
+
+__device__ __forceinline__ uint64_t pcg_out(uint64_t hi, uint64_t lo) {
+  const uint64_t x = hi ^ lo;
+  const unsigned rot = (unsigned)(hi >> 58);
+  return (x >> rot) | (x << ((64u - rot) & 63u));
+}
+
+template <int K>
+__device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, Pcg64 rng, uint64_t acts, int n_act,
+                                           int left, bool slippery, uint64_t t0, uint64_t t1, uint64_t t2) {
+  Fl4Out r;
+  r.o.acc = 0.0;
+  r.o.info = 0;
+  r.o.exec = 0;
+  r.o.stepped_any_state = false;
+  r.turn_done = false;
+  r.succ_last = false;
+  // exec list: the first min(nv, left) known-name ids, in order
+  uint64_t cl = 0;
+  int nv = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint64_t a = (acts >> (8 * k)) & 0xFF;
+    const bool use = k < n_act && a != 0;
+    cl |= use ? a << (8 * nv) : 0ull;
+    nv += use ? 1 : 0;
+  }
+  const int n_try = nv < left ? nv : (left > 0 ? left : 0);
+  // the chain's next K states and outputs (draw k of the turn = output of state k + 1)
+  uint64_t shi[K + 1], slo[K + 1], draw[K];
+  shi[0] = rng.s_hi;
+  slo[0] = rng.s_lo;
+  {
+    Pcg64 c = rng;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      c.next64();
+      shi[k + 1] = c.s_hi;
+      slo[k + 1] = c.s_lo;
+      draw[k] = pcg_out(c.s_hi, c.s_lo) >> 11;
+    }
+  }
+  bool stop = false;
+  int ex = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const bool go = k < n_try && !stop;
+    const int ga = (int)((cl >> (8 * k)) & 0xFF) - 1;  // gym action 0..3 (LEFT, DOWN, RIGHT, UP)
+    const uint64_t u = draw[k];
+    const bool term = ((hole | goal) >> s) & 1u;
+    const int i = (u < t0) ? 0 : (u < t1) ? 1 : (u < t2) ? 2 : 0;
+    const int b = slippery ? ((ga + 3 + i) & 3) : ga;
+    const int row = s >> 2, col = s & 3;
+    int ns = b == 0 ? (col > 0 ? s - 1 : s) : b == 1 ? (row < 3 ? s + 4 : s) : b == 2 ? (col < 3 ? s + 1 : s)
+                                                                                      : (row > 0 ? s - 4 : s);
+    ns = term ? s : ns;
+    const bool g = (goal >> ns) & 1u, h = (hole >> ns) & 1u;
+    const double rw = (!term && g) ? 1.0 : 0.0;
+    const bool done = term || g || h;
+    const bool eff = ns != s;
+    r.o.acc = go ? r.o.acc + rw : r.o.acc;
+    r.o.info = go ? (uint8_t)(RMI_INFO_PRESENT | (eff ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID |
+                              (g ? RMI_INFO_SUCCESS : 0))
+                  : r.o.info;
+    r.succ_last = go ? g : r.succ_last;
+    r.turn_done = go ? done : r.turn_done;
+    s = go ? ns : s;
+    ex += go ? 1 : 0;
+    stop = stop || (go && done);
+  }
+  r.o.exec = (uint8_t)ex;
+  r.o.stepped_any_state = ex > 0;
+  r.s = s;
+  r.rng = rng;
+#pragma unroll
+  for (int k = 1; k <= K; ++k)
+    if (k == ex) {
+      r.rng.s_hi = shi[k];
+      r.rng.s_lo = slo[k];
+    }
+  r.o.info = ex ? r.o.info : 0;
+  return r;
+}
+
+// ceil(cs * 2^53): u = (x >> 11) * 2^-53 satisfies cs > u  <=>  (x >> 11) < ceil(cs * 2^53)
+__device__ __forceinline__ uint64_t draw_threshold(double cs) {
+  return (uint64_t)ceil(cs * 9007199254740992.0);
+}
+
+__device__ __forceinline__ Fl4Out fl4_dispatch(int K, uint32_t hole, uint32_t goal, int s, const Pcg64& rng,
+                                              uint64_t acts, int n_act, int left, bool slip, uint64_t t0,
+                                              uint64_t t1, uint64_t t2) {
+  switch (K) {  // wave-uniform
+    case 1: return fl4_turn<1>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    case 2: return fl4_turn<2>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    case 3: return fl4_turn<3>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    case 4: return fl4_turn<4>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    case 5: return fl4_turn<5>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    case 6: return fl4_turn<6>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    case 7: return fl4_turn<7>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    default: return fl4_turn<8>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+  }
+}
+
 // kFirst: a fresh episode's first turn fused with its reset (rmi_frozenlake_reset): desc, s and
 // the PCG64 state come from the init arrays, the counters and the record start at zero without
 // being read, and the env's reset state and whole record are written before the turn runs.
@@ -151,7 +275,53 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
   o.exec = 0;
   o.stepped_any_state = false;
   bool stepped = false;
-  if (act) {
+  // the 4x4 straight-line turn when every lane of the wave can take it (see fl4_turn)
+  const bool ids_ok = ((((acts & 0x7F7F7F7F7F7F7F7Full) + 0x7B7B7B7B7B7B7B7Bull) | acts) &  // every id byte <= 4
+                       0x8080808080808080ull) == 0;
+  const bool fast = n == 16 && env.ncol == 4 && e.in_regs && in.K >= 1 && ids_ok && e.s >= 0 && e.s < 16;
+  if (__all(fast || !act)) {
+    if (act) {
+      uint32_t hole = 0, goal = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint8_t c = e.cell(i);
+        hole |= (uint32_t)(c == 'H') << i;
+        goal |= (uint32_t)(c == 'G') << i;
+      }
+      int n_a = n_act > in.K ? in.K : n_act;
+      flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (es_manager.py:168)
+      const Fl4Out f = fl4_dispatch(in.K, hole, goal, e.s, e.rng, acts, n_a, in.max_actions_per_traj - num_actions,
+                                    e.slippery, draw_threshold(e.cs0), draw_threshold(e.cs1), draw_threshold(e.cs2));
+      // the format penalty (es_manager.py:158-159): not every parsed name known, or none
+      int nv = 0;
+      for (int k = 0; k < n_a; ++k) nv += ((acts >> (8 * k)) & 0xFF) != 0;
+      if (nv != n_a || nv == 0) penalty += in.format_penalty;
+      o = f.o;
+      e.s = f.s;
+      e.rng = f.rng;
+      num_actions += o.exec;
+      n_turns += 1;
+      if (f.turn_done) {
+        flags |= RMI_FLAG_TERMINATED | RMI_FLAG_DONE;
+        flags = f.succ_last ? (uint8_t)(flags & ~RMI_FLAG_TRUNCATED) : (uint8_t)(flags | RMI_FLAG_TRUNCATED);
+      } else if (num_actions >= in.max_actions_per_traj) {
+        flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
+      }
+      stepped = true;
+      ep.num_actions[b] = num_actions;
+      ep.flags[b] = flags;
+      ep.n_turns[b] = n_turns;
+      ep.penalty[b] = penalty;
+      const int64_t tb = (int64_t)in.turn * B + b;
+      ep.turn_reward[tb] = o.acc;
+      ep.turn_info[tb] = o.info;
+      ep.turn_exec[tb] = o.exec;
+      if (o.stepped_any_state) {
+        env.s[b] = e.s;
+        store_pcg(env.rng, B, b, e.rng);
+      }
+    }
+  } else if (act) {
     if (e.s < 0 || e.s >= n) {
       if (err_out) err_out[b] |= RMI_ERR_STATE;
     } else {

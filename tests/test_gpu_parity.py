@@ -885,3 +885,39 @@ def test_countdown_bare_names(device):
             assert err[i] == 0 and r[i] == want, (e, r[i], want, err[i])
         else:
             assert err[i] & _lib.ERR_UNSUP, (e, err[i])
+
+
+@pytest.mark.parametrize("slippery,bad_waves", [(True, 0.0), (False, 0.0), (True, 0.3)])
+def test_frozenlake_fast_and_generic_paths_vs_oracle(device, slippery, bad_waves):
+    """The 4x4 straight-line turn (waves whose ids are all 0..4) and the generic turn (waves with
+    an out-of-range id somewhere) against the oracle, slippery and not, K = 8 / 3 / 5."""
+    B, T = 8192, 6
+    rng = np.random.default_rng(int(slippery) * 10 + int(bad_waves * 10))
+    for K in (8, 3, 5):
+        env = FrozenLakeBatch(FrozenLakeEnvConfig(is_slippery=slippery), B, T, K, device)
+        env.reset(synthetic.env_seeds(B, 2000 + K))
+        desc = env.desc.cpu().numpy()
+        s = env.s.cpu().numpy()
+        st = env.rng.cpu().numpy().view(np.uint64).copy()
+        oep = oracle.Episode(B, T)
+        bad = np.zeros(B, bool)
+        for t in range(T):
+            ids = rng.integers(0, 5, size=(B, K)).astype(np.int8)
+            n = rng.integers(0, K + 1, size=B).astype(np.uint8)
+            waves = rng.random(B // 64) < bad_waves
+            for w in np.nonzero(waves)[0]:
+                ids[w * 64 + int(rng.integers(0, 64)), int(rng.integers(0, K))] = int(rng.choice([5, 9, -1]))
+            err = torch.zeros(B, dtype=torch.uint8, device=device)
+            env.step_turn(t, _t(ids, device), _t(n, device), None, 9, -0.1, err)
+            oerr = oracle.frozenlake_turn(4, 4, slippery, env.cs, desc, s, st, oep, t, ids, n, None, 9, -0.1)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(err.cpu().numpy() != 0, oerr != 0)
+            bad |= oerr != 0
+            ok = ~bad
+            np.testing.assert_array_equal(env.s.cpu().numpy()[ok], s[ok])
+            np.testing.assert_array_equal(env.rng.cpu().numpy().view(np.uint64)[:, ok], st[:, ok])
+            h = _host_ep(env.ep)
+            for k in ("num_actions", "flags", "n_turns", "penalty"):
+                np.testing.assert_array_equal(h[k][ok], getattr(oep, k)[ok], err_msg=f"K={K} t={t} {k}")
+            for k in ("turn_reward", "turn_info", "turn_exec"):
+                np.testing.assert_array_equal(h[k][:, ok], getattr(oep, k)[:, ok], err_msg=f"K={K} t={t} {k}")
