@@ -963,20 +963,32 @@ __device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b,
   for (int k = 0; k < kMaxNums; ++k) nums[k] = k < env.max_nums ? env.nums[b * env.max_nums + k] : -1;
 }
 
+// Lanes per answer.  An answer's evaluation is one lane's data-dependent token loop, and a wave
+// pays the union of its lanes' control paths: with one answer per lane, 16 384 answers are 256
+// waves — one per CU, 3 of 4 SIMDs idle, every wave walking 64 answers' paths.  Spreading the
+// answers LPA lanes apart (only every LPA-th lane works) gives LPA x the waves, each walking
+// 64 / LPA answers' paths, and fills all SIMDs of every CU.  The other lanes of an answer's
+// group exit at once.
+__host__ __device__ constexpr int cd_lpa_for(int64_t n) {
+  return n >= (int64_t)1 << 18 ? 1 : n >= (int64_t)1 << 16 ? 4 : 16;
+}
+
+template <int LPA>
 __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
                                                                        rmi_turn_t in,
                                                                        const uint8_t* __restrict__ answers,
                                                                        const int32_t* __restrict__ answer_len,
                                                                        int Lmax, uint8_t* __restrict__ err_out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];  // [kCdBlock][cd_slice(Lmax)]
-  const int64_t b = (int64_t)blockIdx.x * kCdBlock + threadIdx.x;
+  extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];  // [kCdBlock / LPA][cd_slice(Lmax)]
+  if (threadIdx.x % LPA) return;
+  const int64_t b = ((int64_t)blockIdx.x * kCdBlock + threadIdx.x) / LPA;
   const int B = ep.B;
   if (b >= B) return;
   // every load of this env is issued before the activity test (one memory round trip): the
   // has_input byte through a pointer that is always valid, selected afterwards
   uint8_t flags = ep.flags[b];
   const uint8_t has_in = *(in.has_input ? in.has_input + b : ep.flags + b);
-  uint8_t* slice = cd_lds + threadIdx.x * cd_slice(Lmax);
+  uint8_t* slice = cd_lds + (threadIdx.x / LPA) * cd_slice(Lmax);
   CountdownDev e;
   e.answers = answers + b * (int64_t)in.K * Lmax;
   e.lens = answer_len + b * (int64_t)in.K;
@@ -1026,6 +1038,7 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   if (err_out && err) err_out[b] |= err;
 }
 
+template <int LPA>
 __global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdown_t env,
                                                                     const uint8_t* __restrict__ answers,
                                                                     const int32_t* __restrict__ answer_len, int Lmax,
@@ -1033,9 +1046,10 @@ __global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdow
                                                                     uint8_t* __restrict__ flags_out,
                                                                     uint8_t* __restrict__ err_out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];
-  const int64_t i = (int64_t)blockIdx.x * kCdBlock + threadIdx.x;
+  if (threadIdx.x % LPA) return;
+  const int64_t i = ((int64_t)blockIdx.x * kCdBlock + threadIdx.x) / LPA;
   if (i >= n) return;
-  uint8_t* slice = cd_lds + threadIdx.x * cd_slice(Lmax);
+  uint8_t* slice = cd_lds + (threadIdx.x / LPA) * cd_slice(Lmax);
   uint8_t fl = 0, err = 0;
   int len = answer_len[i];
   if (len > Lmax) len = Lmax;
@@ -1068,9 +1082,24 @@ RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episod
   if (!answers || !answer_len || !env->nums || !env->n_nums || !env->target || !in->n_actions || !ep->num_actions ||
       !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
     return RMI_EINVAL;
-  hipLaunchKernelGGL(countdown_step_turn_kernel, dim3((ep->B + kCdBlock - 1) / kCdBlock), dim3(kCdBlock),
-                     (size_t)kCdBlock * cd_slice(Lmax), as_stream(stream), *env, *ep, *in, answers, answer_len, Lmax,
-                     err);
+#ifdef RMI_CD_LPA
+  constexpr int kL = RMI_CD_LPA;  // measurement builds (tools/prof_countdown_lpa.py)
+  const int lpa = kL;
+#else
+  const int lpa = cd_lpa_for(ep->B);
+#endif
+  const int64_t lanes = (int64_t)ep->B * lpa;
+  const dim3 grid((unsigned)((lanes + kCdBlock - 1) / kCdBlock));
+  const size_t lds = (size_t)(kCdBlock / lpa) * cd_slice(Lmax);
+  hipStream_t s = as_stream(stream);
+#define RMI_CD_LAUNCH(L) \
+  hipLaunchKernelGGL(countdown_step_turn_kernel<L>, grid, dim3(kCdBlock), lds, s, *env, *ep, *in, answers, \
+                     answer_len, Lmax, err)
+  if (lpa == 1) RMI_CD_LAUNCH(1);
+  else if (lpa == 4) RMI_CD_LAUNCH(4);
+  else if (lpa == 16) RMI_CD_LAUNCH(16);
+  else RMI_CD_LAUNCH(64);
+#undef RMI_CD_LAUNCH
   return launch_status();
 }
 
@@ -1081,8 +1110,18 @@ RMI_API int rmi_countdown_reward(const rmi_countdown_t* env, const uint8_t* answ
   if (!env || Lmax <= 0 || n < 0 || env->max_nums <= 0 || env->max_nums > 8) return RMI_EINVAL;
   if (n == 0) return RMI_OK;
   if (!answers || !answer_len || !reward || !env->nums || !env->n_nums || !env->target) return RMI_EINVAL;
-  hipLaunchKernelGGL(countdown_reward_kernel, dim3((n + kCdBlock - 1) / kCdBlock), dim3(kCdBlock),
-                     (size_t)kCdBlock * cd_slice(Lmax), as_stream(stream), *env, answers, answer_len, Lmax, n, reward,
-                     flags, err);
+  const int lpa = cd_lpa_for(n);
+  const dim3 grid((unsigned)(((int64_t)n * lpa + kCdBlock - 1) / kCdBlock));
+  const size_t lds = (size_t)(kCdBlock / lpa) * cd_slice(Lmax);
+  hipStream_t s = as_stream(stream);
+  if (lpa == 1)
+    hipLaunchKernelGGL(countdown_reward_kernel<1>, grid, dim3(kCdBlock), lds, s, *env, answers, answer_len, Lmax, n,
+                       reward, flags, err);
+  else if (lpa == 4)
+    hipLaunchKernelGGL(countdown_reward_kernel<4>, grid, dim3(kCdBlock), lds, s, *env, answers, answer_len, Lmax, n,
+                       reward, flags, err);
+  else
+    hipLaunchKernelGGL(countdown_reward_kernel<16>, grid, dim3(kCdBlock), lds, s, *env, answers, answer_len, Lmax, n,
+                       reward, flags, err);
   return launch_status();
 }
