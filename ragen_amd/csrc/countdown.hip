@@ -312,29 +312,6 @@ __device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
   return EV_ERR;
 }
 
-// The four operators of the fast path (fast_reward below), each exactly as apply_binary, but
-// branch-free: every candidate result is computed and the right one selected, so a wave whose
-// lanes apply different operators runs one short straight-line sequence.
-__device__ __forceinline__ int fast_binary(int op, const Val& a, const Val& b, Val& out) {
-  const bool fl = a.is_f || b.is_f;
-  const double x = a.as_f(), y = b.as_f();
-  long long rs, rd, rm;
-  const bool os = __builtin_add_overflow(a.i, b.i, &rs);
-  const bool od = __builtin_sub_overflow(a.i, b.i, &rd);
-  const bool om = __builtin_mul_overflow(a.i, b.i, &rm);
-  const double q = x / y;
-  const bool div = op == OP_DIV;
-  const long long lim = 9007199254740992LL;
-  const bool big = a.i > lim || a.i < -lim || b.i > lim || b.i < -lim;
-  int st = EV_OK;
-  if (div) st = (!fl && b.i == 0) ? EV_ERR : (!fl && big) ? EV_UNSUP : (y == 0.0) ? EV_ERR : EV_OK;
-  else if (!fl && (op == OP_ADD ? os : op == OP_SUB ? od : om)) st = EV_UNSUP;
-  out.is_f = fl || div;
-  out.f = div ? q : op == OP_ADD ? x + y : op == OP_SUB ? x - y : x * y;
-  out.i = out.is_f ? 0 : op == OP_ADD ? rs : op == OP_SUB ? rd : rm;
-  return st;
-}
-
 constexpr int kStack = 32;  // deeper expressions are flagged RMI_ERR_UNSUP (host re-evaluates)
 
 // A stack slot: 16 B (value bits + kind) — the stacks live in the thread's LDS slice, not in
@@ -699,160 +676,206 @@ __device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work) {
   return EV_OK;
 }
 
-// Fast path for answers over the bytes "0-9 +-*/()" and ' ' (the usual arithmetic answer):
-// check_format and the evaluation in ONE pass, byte per loop iteration, with the evaluator's
-// state in registers, so the lanes of a wave (one answer each) run the same short loop body
-// whatever their answers look like (the general path branches per token kind, and a wave pays
-// the union of its lanes' paths).  The evaluator is the two-level form of the grammar
-//   expr := term (('+'|'-') term)* ; term := factor (('*'|'/') factor)* ;
-//   factor := ('+'|'-')* (literal | '(' expr ')')
-// computed eagerly left to right: acc (aop) term (mop) operand — the same operations in the
-// same order as Python's AST evaluation (and py_eval's postfix), so every value is identical.
-// Syntax is checked exactly as py_eval does (expect_operand, depth); parentheses save the
-// outer (acc, aop, term, mop, signs) in the thread's LDS work area.  A unary '-' on the int
-// -2**63 is EV_UNSUP as in apply_unary.  Returns false if the answer leaves the subset ('**',
-// '//', a multi-digit literal with a leading '0', > 18 digits, nesting > kFastDepth, any other
-// byte): the caller then runs check_format + py_eval.  fmt = check_format; st / out = the
-// evaluation (st differs from py_eval's only between EV_ERR and EV_UNSUP on answers that are
-// not correct either way).
-constexpr int kFastDepth = kStack / 2;  // two stack slots (acc, term) per open parenthesis
+// Fast path for answers of at most 64 bytes over "0-9 +-*/()" and ' ' (the usual arithmetic
+// answer): check_format and the evaluation in ONE pass over the answer's TOKENS, with no
+// per-byte loop and (almost) no branches, so the lanes of a wave (one answer each) run one
+// straight-line body per token whatever their answers look like.
+//  * Structure from bit masks: SWAR over the staged row gives a 64-bit digit mask D and a
+//    space mask SP; token starts are the non-space bytes that do not continue a digit run.
+//    A token is found with one ctz, its bytes with two aligned 8-B LDS reads, a literal's
+//    value (<= 8 digits) with three SWAR multiply steps.
+//  * One value representation: every value is an f64 plus an is-float bit.  Python int
+//    arithmetic on ints below 2**53 in magnitude is exact in f64, and true division of two
+//    such ints is CPython's single correctly rounded double division (long_true_divide's
+//    small-int case), so every result is bit-identical to Python's as long as every int
+//    result stays below 2**53; one that reaches it leaves the fast path.
+//  * The evaluator is the two-level form of the grammar
+//      expr := term (('+'|'-') term)* ; term := factor (('*'|'/') factor)* ;
+//      factor := ('+'|'-')* (literal | '(' expr ')')
+//    computed eagerly left to right: acc (aop) term (mop) operand — the same operations in
+//    the same order as Python's AST evaluation (and py_eval's postfix).  At most ONE
+//    arithmetic operation per token at ONE code site; ')' hands its group's value to the
+//    next iteration as an operand token.  Parentheses save the outer level in the thread's
+//    LDS stack (the push slot is always written, the pop slot always read, so neither
+//    needs a branch).  Syntax is checked exactly as py_eval does (expect-operand, depth).
+// Returns false when the answer leaves the subset (longer than 64 bytes, another byte,
+// '**', '//', a literal of more than 8 digits or with a leading 0, nesting deeper than
+// kFastDepth, an int result >= 2**53): the caller then runs check_format + py_eval.
+// fmt = check_format; st / out = the evaluation.
+constexpr int kFastDepth = 16;
+constexpr int kFastMax = 64;       // answer bytes covered by the masks
+constexpr int kSlotBytes = 24;     // stack slot: acc f64, term f64, state word
+static_assert((kFastDepth + 1) * kSlotBytes + (kMaxNums + 1) * 8 <= kStack * (int)sizeof(SVal) + kStack,
+              "the fast path's stack and digit runs fit the LDS work area");
 enum : int { F_NONE = 0, F_ADD, F_SUB, F_MUL, F_DIV };
-__device__ __forceinline__ int fast_op(int f) {
-  return f == F_ADD ? OP_ADD : f == F_SUB ? OP_SUB : f == F_MUL ? OP_MUL : OP_DIV;
-}
-typedef const __attribute__((address_space(3))) uint8_t lds_cu8;
 // Per-lane state is kept in integer words, not bools: a bool that merges at a join of
 // divergent control flow is a 64-bit lane mask, and keeping a dozen of them costs more
 // scalar instructions than the evaluation itself.
 enum : int { S_EXPECT = 1, S_SLOW = 2, S_GROUP = 4, S_NEG = 8, S_NEGANY = 16, S_TOOMANY = 32 };
-// One token per loop iteration (spaces and a literal's digits in short inner loops), and at
-// most ONE arithmetic operation per iteration at ONE code site: ')' hands its group's value
-// to the next iteration as an operand token.  s: the answer staged in LDS.
-__device__ __forceinline__ bool fast_reward(const uint8_t* s_lds, int n, const int32_t (&nums)[kMaxNums], int n_nums,
-                                            bool& fmt, int& st, Val& out, uint8_t* work) {
-  lds_cu8* s = (lds_cu8*)s_lds;
-  SVal* stk = reinterpret_cast<SVal*>(work);
-  uint8_t* stf = work + kStack * sizeof(SVal);
-  uint64_t found[kMaxNums];
+__device__ __forceinline__ uint32_t nib4(uint32_t hi) {  // bit 7 of each byte -> a 4-bit mask
+  return ((hi >> 7) * 0x01020408u) >> 24;
+}
+__device__ __forceinline__ uint32_t digit4(uint32_t x) {  // bytes '0'..'9' (ASCII only)
+  const uint32_t h = x & 0x7F7F7F7Fu;
+  return nib4((h + 0x50505050u) & ~(h + 0x46464646u) & ~x & 0x80808080u);
+}
+__device__ __forceinline__ uint32_t space4(uint32_t x) {  // bytes == ' '
+  const uint32_t y = x ^ 0x20202020u;
+  return nib4(~(((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u);
+}
+__device__ __forceinline__ int ctz64(uint64_t x) { return x ? __builtin_ctzll(x) : 64; }
+
+__device__ __forceinline__ uint64_t load8(const uint8_t* row, int p) {  // bytes [p, p+8) of a staged row
+  const uint64_t* r8 = reinterpret_cast<const uint64_t*>(row);
+  const int pw = p >> 3, ps = (p & 7) * 8;
+  const uint64_t lo = r8[pw], hi = r8[pw + 1];
+  return (lo >> ps) | ((hi << 1) << (63 - ps));  // branch-free funnel shift (ps = 0 included)
+}
+
+// row: the answer staged in LDS, 16-B aligned, readable 80 bytes past its start.
+// work: the thread's LDS work area (the parenthesis stack, then the digit runs found).
+// The loop body has no data-dependent branch: the token tests are 0/1 ints combined with
+// bitwise operators (C's && and || would become divergent control flow), every state word
+// is updated by selects, the stack slot is always written and read, and the next token's
+// bytes are read one iteration ahead.
+__device__ __forceinline__ bool fast_reward(const uint8_t* row, int n, const int32_t (&nums)[kMaxNums], int n_nums,
+                                            bool& fmt, int& st_out, Val& out, uint8_t* work) {
+  if (n > kFastMax) return false;
+  const uint4* r16 = reinterpret_cast<const uint4*>(row);
+  uint64_t D = 0, SP = 0;
 #pragma unroll
-  for (int k = 0; k < kMaxNums; ++k) found[k] = 0;
-  int nf = 0, depth = 0, sf = S_EXPECT, aop = F_NONE, mop = F_NONE, i = 0;
-  Val acc, term, gv;
-  acc.is_f = term.is_f = gv.is_f = 0;
-  acc.i = term.i = gv.i = 0;
-  acc.f = term.f = gv.f = 0.0;
-  st = EV_OK;
-  for (;;) {
-    // ---- the next token: 0 = the end, 1 = an operand (a literal or a group's value), else the byte
-    int tok = 1;
-    Val v = gv;
-    if (sf & S_GROUP) {
-      sf &= ~S_GROUP;
-    } else {
-      while (i < n && s[i] == ' ') ++i;
-      tok = i < n ? s[i] : 0;
-      i += i < n;
-      if ((unsigned)(tok - '0') < 10u) {  // a literal = a check_format digit run
-        long long cur = tok - '0';
-        int ndig = 1;
-        for (int c; i < n && (unsigned)((c = s[i]) - '0') < 10u; ++i, ++ndig) cur = cur * 10 + (c - '0');
-        if ((tok == '0' && ndig > 1) || ndig > 18) sf |= S_SLOW;
-#pragma unroll
-        for (int k = 0; k < kMaxNums; ++k)
-          if (k == nf) found[k] = (uint64_t)cur;
-        sf |= nf == kMaxNums ? S_TOOMANY : 0;
-        nf += nf < kMaxNums;
-        if (st == EV_OK && !(sf & S_EXPECT)) st = EV_ERR;
-        v.is_f = 0;
-        v.i = cur;
-        v.f = 0.0;
-        tok = 1;
-      } else if (tok != 0) {
-        const int d = i < n ? s[i] : 0;
-        const bool arith = tok == '+' || tok == '-' || tok == '*' || tok == '/';
-        if ((!arith && tok != '(' && tok != ')') || ((tok == '*' || tok == '/') && d == tok)) sf |= S_SLOW;
-      }
+  for (int c = 0; c < kFastMax / 16; ++c) {
+    const uint4 q = r16[c];
+    D |= (uint64_t)(digit4(q.x) | digit4(q.y) << 4 | digit4(q.z) << 8 | digit4(q.w) << 12) << (16 * c);
+    SP |= (uint64_t)(space4(q.x) | space4(q.y) << 4 | space4(q.z) << 8 | space4(q.w) << 12) << (16 * c);
+  }
+  const uint64_t lm = n >= 64 ? ~0ull : ((1ull << n) - 1);
+  D &= lm;
+  uint64_t TS = lm & ~SP & ~(D & (D << 1));  // token starts
+  uint8_t* lits = work + (kFastDepth + 1) * kSlotBytes;  // the digit runs (kMaxNums + 1 slots of 8 B)
+  int p = ctz64(TS);
+  TS &= TS - 1;
+  uint64_t w = load8(row, p);
+  int nf = 0, depth = 0, sf = S_EXPECT, aop = F_NONE, mop = F_NONE, st = EV_OK;
+  double acc = 0.0, term = 0.0, gv = 0.0, res = 0.0;
+  int accf = 0, termf = 0, gvf = 0, resf = 0;
+  // at most 64 tokens + 32 group operands + the end: the cap is only a guard every wave reaches
+  for (int it = 0;; ++it) {
+    if (it > 2 * kFastMax + 2) {
+      sf |= S_SLOW;
+      break;
     }
-    if (sf & S_SLOW) break;
-    if (st == EV_OK) {  // else py_eval has returned: only check_format goes on
-      // ---- the token's effect: at most one operation (opc on x, y) and where its result goes
-      int opc = F_NONE, dst = 0;  // dst: 1 term, 2 acc, 3 group value, 4 out
-      Val x = acc, y = term;
-      if (tok == 1) {
-        if ((sf & S_NEGANY) && !v.is_f && v.i == (-9223372036854775807LL - 1)) st = EV_UNSUP;
-        if (sf & S_NEG) {
-          v.i = -v.i;
-          v.f = -v.f;
-        }
-        sf &= ~(S_EXPECT | S_NEG | S_NEGANY);
-        if (mop == F_NONE) term = v;
-        opc = mop;
-        x = term;
-        y = v;
-        dst = 1;
-        mop = F_NONE;
-      } else if (tok == 0) {
-        if ((sf & S_EXPECT) || depth != 0) st = EV_ERR;
-        if (aop == F_NONE) out = term;
-        opc = aop;
-        dst = 4;
-      } else if (tok == '(') {
-        if (!(sf & S_EXPECT)) {
-          st = EV_ERR;
-        } else if (depth == kFastDepth) {
-          sf |= S_SLOW;
-          break;
-        } else {
-          stk[2 * depth] = pack(acc);
-          stk[2 * depth + 1] = pack(term);
-          stf[depth] = (uint8_t)(aop | (mop << 3) | ((sf & (S_NEG | S_NEGANY)) << 3));
-          depth++;
-          aop = mop = F_NONE;
-          sf &= ~(S_NEG | S_NEGANY);
-        }
-      } else if (tok == ')') {
-        if ((sf & S_EXPECT) || depth == 0) {
-          st = EV_ERR;
-        } else {
-          if (aop == F_NONE) gv = term;
-          opc = aop;
-          dst = 3;
-          sf |= S_GROUP;  // the value is the next iteration's operand
-          depth--;
-        }
-      } else if (sf & S_EXPECT) {
-        if (tok == '-') sf = (sf ^ S_NEG) | S_NEGANY;
-        else if (tok != '+') st = EV_ERR;  // '*' or '/' where an operand is expected
-      } else if (tok == '*' || tok == '/') {
-        mop = tok == '*' ? F_MUL : F_DIV;
-        sf |= S_EXPECT;
-      } else {  // binary '+' / '-': the term joins acc
-        if (aop == F_NONE) acc = term;
-        opc = aop;
-        dst = 2;
-        aop = tok == '+' ? F_ADD : F_SUB;
-        sf |= S_EXPECT;
-      }
-      if (opc != F_NONE && st == EV_OK) {
-        Val r;
-        st = fast_binary(fast_op(opc), x, y, r);
-        if (dst == 1) term = r;
-        if (dst == 2) acc = r;
-        if (dst == 3) gv = r;
-        if (dst == 4) out = r;
-      }
-      if ((sf & S_GROUP) && st == EV_OK) {  // restore the enclosing level (its operation has read it)
-        acc = unpack(stk[2 * depth]);
-        term = unpack(stk[2 * depth + 1]);
-        const int f = stf[depth];
-        aop = f & 7;
-        mop = (f >> 3) & 7;
-        sf |= (f >> 3) & (S_NEG | S_NEGANY);
-      }
+    const int grp = (sf >> 2) & 1;  // S_GROUP
+    sf &= ~S_GROUP;
+    // the slot a ')' pops, and the next token's bytes (both reads issued up front)
+    const uint8_t* pslot = work + (depth > 0 ? depth - 1 : 0) * kSlotBytes;
+    const double pacc = *reinterpret_cast<const double*>(pslot);
+    const double pterm = *reinterpret_cast<const double*>(pslot + 8);
+    const uint32_t pword = *reinterpret_cast<const uint32_t*>(pslot + 16);
+    const int cp = p;
+    const uint64_t cw = w;
+    p = grp ? p : ctz64(TS);
+    TS = grp ? TS : TS & (TS - 1);
+    w = load8(row, p);
+    // ---- this iteration's token: an operand (a digit run, or the group value after ')'),
+    //      the end, or one of ( ) * + - /
+    const int b0 = (int)(cw & 0xFF), b1 = cp + 1 < n ? (int)((cw >> 8) & 0xFF) : 0;
+    const int nogrp = grp ^ 1;
+    const int end = nogrp & (cp >= n);
+    const int lit = nogrp & (end ^ 1) & ((unsigned)(b0 - '0') < 10u);
+    const int tok = nogrp & (end ^ 1) & (lit ^ 1);
+    const unsigned kc = (unsigned)(b0 - '(');
+    const int kind = (kc < 8u ? (int)((0x60504321u >> (4 * kc)) & 15u) : 0) * tok;  // ( ) * + , - . /
+    const int lp = kind == 1, rp = kind == 2, star = kind == 3, plus = kind == 4, minus = kind == 5,
+              slash = kind == 6, md = star | slash, pm = plus | minus;
+    const int L = lit ? ctz64(~(D >> (cp & 63))) : 0;
+    const int Lc = L < 1 ? 1 : L > 8 ? 8 : L;
+    uint64_t x8 = (cw & (~0ull >> (64 - 8 * Lc))) << (8 * (8 - Lc));
+    x8 &= 0x0F0F0F0F0F0F0F0Full;
+    x8 = (x8 * 10 + (x8 >> 8)) & 0x00FF00FF00FF00FFull;
+    x8 = (x8 * 100 + (x8 >> 16)) & 0x0000FFFF0000FFFFull;
+    x8 = (x8 * 10000 + (x8 >> 32)) & 0xFFFFFFFFull;
+    const int slow_tok = (lit & (((b0 == '0') & (L > 1)) | (L > 8))) | (tok & (kind == 0)) | (md & (b1 == b0));
+    // a check_format digit run (the slot past the last run is free: written unconditionally)
+    *reinterpret_cast<uint64_t*>(lits + 8 * nf) = x8;
+    sf |= (lit & (nf == kMaxNums)) ? S_TOOMANY : 0;
+    nf += lit & (nf < kMaxNums);
+    // ---- syntax (py_eval's checks) and this token's effect
+    const int expect = sf & S_EXPECT, noexp = expect ^ 1;
+    const int err = (lit & noexp) | (end & (expect | (depth != 0))) | (lp & noexp) | (rp & (expect | (depth == 0))) |
+                    (md & expect);
+    const int stok = st == EV_OK;
+    const int go = stok & (err ^ 1);
+    st = (stok & err) ? EV_ERR : st;
+    const int g_opnd = go & (lit | grp), g_end = go & end, g_rp = go & rp;
+    const int g_lp = go & lp & (depth < kFastDepth);
+    const int g_neg = go & expect & minus;
+    const int g_md = go & noexp & md, g_pm = go & noexp & pm;
+    const int slow = slow_tok | (go & lp & (depth == kFastDepth));
+    double v = grp ? gv : (double)(uint32_t)x8;
+    const int vf = grp ? gvf : 0;
+    v = (sf & S_NEG) ? (vf ? -v : 0.0 - v) : v;  // an int -0 is 0
+    // the push slot is free whether or not this token opens a group
+    {
+      uint8_t* s = work + depth * kSlotBytes;
+      *reinterpret_cast<double*>(s) = acc;
+      *reinterpret_cast<double*>(s + 8) = term;
+      *reinterpret_cast<uint32_t*>(s + 16) =
+          (uint32_t)(aop | (mop << 3) | ((sf & (S_NEG | S_NEGANY)) << 3) | (accf << 8) | (termf << 9));
     }
-    if (tok == 0) break;
+    // at most one operation: operand -> term (mop) v; end / ')' / binary +- -> acc (aop) term
+    const int opc = g_opnd ? mop : (g_end | g_rp | g_pm) ? aop : F_NONE;
+    const double x = g_opnd ? term : acc, y = g_opnd ? v : term;
+    const int xf = g_opnd ? termf : accf, yf = g_opnd ? vf : termf;
+    const int did = opc != F_NONE, dv = opc == F_DIV;
+    const double sm = x + (opc == F_SUB ? -y : y), pr = x * y, qt = x / y;
+    double r = opc == F_MUL ? pr : dv ? qt : sm;
+    const int rf = xf | yf | (int)dv;
+    r = rf ? r : r + 0.0;  // an int -0 is 0
+    st = (did & dv & (y == 0.0)) ? EV_ERR : st;  // ZeroDivisionError
+    const int big = did & (rf ^ 1) & (fabs(r) >= 9007199254740992.0);  // an int past 2**53: leave the f64 model
+    const double val = did ? r : g_opnd ? v : term;                 // the token's result
+    const int valf = did ? rf : g_opnd ? vf : termf;
+    term = g_opnd ? val : term;
+    termf = g_opnd ? valf : termf;
+    acc = g_pm ? val : acc;
+    accf = g_pm ? valf : accf;
+    gv = g_rp ? val : gv;
+    gvf = g_rp ? valf : gvf;
+    res = g_end ? val : res;
+    resf = g_end ? valf : resf;
+    // state words
+    int nsf = sf;
+    nsf = g_opnd ? nsf & ~(S_EXPECT | S_NEG | S_NEGANY) : nsf;
+    nsf = g_lp ? nsf & ~(S_NEG | S_NEGANY) : nsf;
+    nsf = g_neg ? (nsf ^ S_NEG) | S_NEGANY : nsf;
+    nsf = g_md | g_pm ? nsf | S_EXPECT : nsf;
+    nsf = g_rp ? nsf | S_GROUP : nsf;
+    nsf |= slow | big ? S_SLOW : 0;
+    mop = g_opnd | g_lp ? F_NONE : g_md ? (star ? F_MUL : F_DIV) : mop;
+    aop = g_lp ? F_NONE : g_pm ? (plus ? F_ADD : F_SUB) : aop;
+    depth += g_lp ? 1 : 0;
+    // ')': the enclosing level comes back (its operation has read it)
+    const int rs = g_rp & (st == EV_OK);
+    depth -= rs ? 1 : 0;
+    acc = rs ? pacc : acc;
+    term = rs ? pterm : term;
+    accf = rs ? (int)((pword >> 8) & 1) : accf;
+    termf = rs ? (int)((pword >> 9) & 1) : termf;
+    aop = rs ? (int)(pword & 7) : aop;
+    mop = rs ? (int)((pword >> 3) & 7) : mop;
+    nsf |= rs ? (int)((pword >> 3) & (S_NEG | S_NEGANY)) : 0;
+    sf = nsf;
+    if ((sf & S_SLOW) | end) break;
   }
   if (sf & S_SLOW) return false;
+  uint64_t found[kMaxNums];
+#pragma unroll
+  for (int k = 0; k < kMaxNums; ++k) found[k] = *reinterpret_cast<const uint64_t*>(lits + 8 * k);
+  st_out = st;
+  out.is_f = resf;
+  out.f = resf ? res : 0.0;
+  out.i = resf ? 0 : (long long)res;
   fmt = same_multiset(found, nf, (sf & S_TOOMANY) != 0, nums, n_nums);
   return true;
 }
@@ -955,7 +978,8 @@ struct CountdownDev {
 // Per-thread LDS: the staged answer row, then the evaluator stacks.  64-thread blocks keep the
 // slices small enough for several blocks per CU.
 constexpr int kCdBlock = 64;
-__host__ __device__ constexpr int stage_stride(int Lmax) { return Lmax <= kStageMax ? ((Lmax + 3) & ~3) + 4 : 0; }
+// a staged row is 16-B aligned and readable 80 bytes past its start (fast_reward's token reads)
+__host__ __device__ constexpr int stage_stride(int Lmax) { return Lmax <= kStageMax ? ((Lmax + 15) & ~15) + 16 : 0; }
 __host__ __device__ constexpr int cd_slice(int Lmax) { return stage_stride(Lmax) + kMachineBytes; }
 
 __device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b, int32_t (&nums)[kMaxNums]) {
@@ -963,15 +987,13 @@ __device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b,
   for (int k = 0; k < kMaxNums; ++k) nums[k] = k < env.max_nums ? env.nums[b * env.max_nums + k] : -1;
 }
 
-// Lanes per answer.  An answer's evaluation is one lane's data-dependent token loop, and a wave
-// pays the union of its lanes' control paths: with one answer per lane, 16 384 answers are 256
-// waves — one per CU, 3 of 4 SIMDs idle, every wave walking 64 answers' paths.  Spreading the
-// answers LPA lanes apart (only every LPA-th lane works) gives LPA x the waves, each walking
-// 64 / LPA answers' paths, and fills all SIMDs of every CU.  The other lanes of an answer's
-// group exit at once.
-__host__ __device__ constexpr int cd_lpa_for(int64_t n) {
-  return n >= (int64_t)1 << 18 ? 1 : n >= (int64_t)1 << 16 ? 4 : 16;
-}
+// Lanes per answer.  An answer's evaluation is one lane's token loop; every lane of a wave runs
+// it to the wave's longest answer, so a turn costs one wave's latency, and that latency does not
+// shrink with fewer answers per wave: with the branch-free token loop, one answer per lane (LPA 1)
+// measured best at every size (tools/prof_countdown_lpa.py: 16 384 envs 17.0 us per turn vs
+// 20.1 / 47.1 us at LPA 4 / 16; equal at 1024 and 4096 envs).  Spreading answers LPA lanes
+// apart stays available for measurement builds (-DRMI_CD_LPA).
+__host__ __device__ constexpr int cd_lpa_for(int64_t) { return 1; }
 
 template <int LPA>
 __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,

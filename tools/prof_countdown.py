@@ -22,7 +22,7 @@ def run(answers, label):
     z = torch.zeros(B, K, dtype=torch.int8, device=dev)
     t = ops.turn_struct(0, z, n, None, 1, -0.1)
     ones = torch.ones(B, dtype=torch.uint8, device=dev)
-    tb = ops.turn_struct(0, z, n, ones, 1 << 30, -0.1)  # every env steps again: back-to-back launches
+    tb = ops.turn_struct(0, z, n, ones, 200, -0.1)  # every env steps again: back-to-back launches
     st = cd.struct()
     for _ in range(3):
         cd.ep.arena.zero_(); ops.countdown_step_turn(st, cd.ep, t, bt, lt)
@@ -47,3 +47,7 @@ run([" + ".join(str(x) for x in i["nums"]) for i in insts], "sum of nums")
 run(synthetic.countdown_answers(insts, 1, p_empty=0.0)[0], "synthetic mix")
 run(["(" * 10 + "1" + ")" * 10] * B, "nested")
 run([None] * B, "empty")
+mix = synthetic.countdown_answers(insts, 1, p_empty=0.0)[0]
+run([a if i % 2 == 0 else None for i, a in enumerate(mix)], "mix half")
+run([a if i % 16 == 0 else None for i, a in enumerate(mix)], "mix 1/16")
+run([a if i % 1024 == 0 else None for i, a in enumerate(mix)], "mix 1/1024")

@@ -33,10 +33,40 @@ def build():
 
 def child():
     sys.path.insert(0, ROOT)
+    import numpy as np
     import torch
     import bench
-    r = bench.toytext_legs(torch.device("cuda", 0))["countdown"]
-    print(json.dumps({"lib": os.environ.get("RAGEN_AMD_LIB"), "ms_per_rollout": r["ms_per_rollout"]}))
+    from ragen_amd import ops, synthetic
+    from ragen_amd.env import CountdownBatch
+    from ragen_amd.env.configs import CountdownEnvConfig
+    from ragen_amd.env.countdown import synthetic_instances
+    dev = torch.device("cuda", 0)
+    r = bench.toytext_legs(dev)["countdown"]
+    out = {"lib": os.path.basename(os.environ.get("RAGEN_AMD_LIB", "")), "ms_per_rollout": r["ms_per_rollout"]}
+    inst = synthetic_instances(1024, 7)
+    for B in (1024, 4096, 16384, 65536):  # one turn, half the envs answering, back-to-back launches
+        cd = CountdownBatch(CountdownEnvConfig(data=inst), B, 1, 1, dev)
+        cd.reset(synthetic.env_seeds(B))
+        ans = synthetic.countdown_answers([inst[int(i)] for i in cd.index], 1, p_empty=0.5)[0]
+        lists = [[a] if a is not None else [] for a in ans]
+        buf, lens = cd.encode_answers(lists)
+        bt, lt = torch.from_numpy(buf).to(dev), torch.from_numpy(lens).to(dev)
+        n = torch.from_numpy(np.array([len(x) for x in lists], np.uint8)).to(dev)
+        z = torch.zeros(B, 1, dtype=torch.int8, device=dev)
+        ones = torch.ones(B, dtype=torch.uint8, device=dev)
+        t = ops.turn_struct(0, z, n, ones, 200, -0.1)
+        st = cd.struct()
+        for _ in range(3):
+            ops.countdown_step_turn(st, cd.ep, t, bt, lt)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            ops.countdown_step_turn(st, cd.ep, t, bt, lt)
+        e1.record()
+        torch.cuda.synchronize()
+        out[f"turn_us_B{B}"] = round(e0.elapsed_time(e1) * 1000 / 50, 2)
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
