@@ -213,6 +213,37 @@ __device__ int float_pow(double iv, double iw, double& out) {  // CPython float_
   return EV_OK;
 }
 
+// int / int past 2**53 (CPython long_true_divide): the correctly rounded (half-even) quotient.
+// q = floor(|a| 2^s / |b|) with s chosen so that q has 55 or 56 bits (128-bit restoring
+// division), then 53 bits kept, rounded with the dropped bits and the remainder as sticky.
+// |a / b| lies in [2^-63, 2^63]: no overflow, no subnormal.  b != 0.
+__device__ double int_true_div(long long a, long long b) {
+  const bool neg = (a < 0) != (b < 0);
+  const unsigned long long x = a < 0 ? 0ull - (unsigned long long)a : (unsigned long long)a;
+  const unsigned long long y = b < 0 ? 0ull - (unsigned long long)b : (unsigned long long)b;
+  if (x == 0) return neg ? -0.0 : 0.0;
+  const int lx = 64 - __builtin_clzll(x), ly = 64 - __builtin_clzll(y);
+  const int s = 55 - (lx - ly);
+  const unsigned __int128 N = s >= 0 ? (unsigned __int128)x << s : (unsigned __int128)x;
+  const unsigned __int128 D = s < 0 ? (unsigned __int128)y << -s : (unsigned __int128)y;
+  unsigned __int128 rem = N;
+  unsigned long long q = 0;
+  for (int i = 55; i >= 0; --i) {
+    const unsigned __int128 t = D << i;
+    if (rem >= t) {
+      rem -= t;
+      q |= 1ull << i;
+    }
+  }
+  const int extra = (64 - __builtin_clzll(q)) - 53;  // 2 or 3
+  unsigned long long mant = q >> extra;
+  const unsigned long long dropped = q & ((1ull << extra) - 1), half = 1ull << (extra - 1);
+  const bool up = dropped > half || (dropped == half && (rem != 0 || (mant & 1)));
+  mant += up;
+  const double v = ldexp((double)mant, extra - s);
+  return neg ? -v : v;
+}
+
 __device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
   const bool fl = a.is_f || b.is_f;
   out.is_f = false;
@@ -239,7 +270,11 @@ __device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
       if (!fl) {
         if (b.i == 0) return EV_ERR;
         const long long lim = 9007199254740992LL;
-        if (a.i > lim || a.i < -lim || b.i > lim || b.i < -lim) return EV_UNSUP;
+        if (a.i > lim || a.i < -lim || b.i > lim || b.i < -lim) {
+          out.is_f = true;
+          out.f = int_true_div(a.i, b.i);
+          return EV_OK;
+        }
       }
       const double y = b.as_f();
       if (y == 0.0) return EV_ERR;
@@ -341,9 +376,16 @@ struct Machine {
   int8_t* ops;   // [kStack] in LDS
   int nv = 0, no = 0;
   int status = EV_OK;
+  bool ev = true;  // false: the syntax pass (stack shapes only, no arithmetic)
 
   __device__ bool reduce_one() {
     const int op = ops[--no];
+    if (!ev) {
+      const int need = (op == OP_NEG || op == OP_POS || op == OP_INV) ? 1 : 2;
+      if (nv < need) { status = EV_ERR; return false; }
+      nv -= need - 1;
+      return true;
+    }
     if (op == OP_NEG || op == OP_POS || op == OP_INV) {
       if (nv < 1) { status = EV_ERR; return false; }
       Val a = unpack(vals[nv - 1]);
@@ -391,7 +433,9 @@ __device__ __forceinline__ bool is_alpha(uint8_t c) { return (c >= 'a' && c <= '
 __device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                       1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
-// Lex a number literal at s[i]; returns the index after it.  status EV_ERR = SyntaxError.
+// Lex a number literal at s[i]; returns the index after it.  status EV_ERR = SyntaxError;
+// EV_UNSUP with v.is_f == kValidLit: a valid literal whose value is outside the model.
+constexpr int kValidLit = 2;
 __device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
   uint64_t mant = 0;
   int ndig = 0, frac = 0, exp10 = 0;
@@ -467,6 +511,7 @@ __device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
     }
     if (overflow || mant > 9223372036854775807ull) {
       status = EV_UNSUP;  // Python big int
+      v.is_f = kValidLit;
       return i;
     }
     v.is_f = false;
@@ -481,7 +526,8 @@ __device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
       v.f = 0.0;
       return i;
     }
-    status = EV_UNSUP;
+    status = EV_UNSUP;  // a float literal this parser does not round exactly
+    v.is_f = kValidLit;
     return i;
   }
   v.is_f = true;
@@ -566,9 +612,13 @@ __device__ int name_outcome(const uint8_t* s, int n) {
   return EV_ERR;
 }
 
-// returns EV_OK with value in out, EV_ERR (Python raises), EV_UNSUP (outside the model)
-__device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work) {
+// returns EV_OK with value in out, EV_ERR (Python raises), EV_UNSUP (outside the model).
+// evaluate = false: the syntax pass.  Python compiles before it evaluates, so a syntax error
+// anywhere wins over whatever the evaluation would meet first (an int past int64: EV_UNSUP);
+// countdown_reward runs this pass first and evaluates only a well-formed answer.
+__device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work, bool evaluate = true) {
   Machine m;
+  m.ev = evaluate;
   m.vals = reinterpret_cast<SVal*>(work);
   m.ops = reinterpret_cast<int8_t*>(work + kStack * sizeof(SVal));
   bool expect_operand = true;
@@ -600,6 +650,7 @@ __device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work) {
       Val v;
       int st = EV_OK;
       i = lex_number(s, n, i, v, st);
+      if (st == EV_UNSUP && !evaluate && v.is_f == kValidLit) st = EV_OK;  // a valid literal, value outside the model
       if (st != EV_OK) return st;
       if (!m.push_val(v)) return m.status;
       expect_operand = false;
@@ -891,7 +942,8 @@ __device__ double countdown_reward(const uint8_t* s, int n, bool staged, const i
   int st = EV_ERR;
   if (!staged || !fast_reward(s, n, nums, n_nums, fmt, st, v, work)) {
     fmt = check_format(s, n, nums, n_nums);
-    if (fmt) st = py_eval(s, n, v, work);
+    if (fmt) st = py_eval(s, n, v, work, false);
+    if (fmt && st == EV_OK) st = py_eval(s, n, v, work, true);
   }
   if (!fmt) return 0.0;
   flags |= 1;
@@ -906,54 +958,354 @@ __device__ double countdown_reward(const uint8_t* s, int n, bool staged, const i
   return score;
 }
 
-// An answer string is parsed from this thread's LDS row: staged there with 16-B loads issued
-// four at a time (one memory round trip per 64 B), not a dependent load per word.  The first
-// 64 B of answer 0 are loaded with the kernel's other loads (prestage); only longer answers
-// pay a round trip of their own.
+// ================================================================ 16 lanes per answer
+// A turn's answers are few next to the machine (16 384 envs: 256 full waves), so a turn costs
+// one wave's latency, and a lane-per-answer token loop makes that latency the length of the
+// longest answer's token chain (~17 iterations of ~250 instructions).  Here the 16 lanes of one
+// DPP row own one answer, one TOKEN per lane, and everything but the arithmetic runs across
+// the tokens at once:
+//  * classify: lane j builds the digit / space nibbles of answer bytes 4j..4j+3; the row
+//    assembles the 64-bit masks through LDS; lane k finds the k-th token start (popcount
+//    search), reads its bytes (two 8-B LDS reads) and parses its digit run (SWAR);
+//  * syntax: py_eval's checks are local to neighbouring tokens (an operand where an operator
+//    is expected, ')' '*' '/' where an operand is expected, the end) plus the parenthesis
+//    depth (a DPP row scan), so each lane checks its own token against the previous one;
+//    unary + / - signs fold into the digit run they precede;
+//  * tree: a binary operator's key is 2 * depth + (1 for * /).  Python's parse tree
+//    (left-associative) is the Cartesian tree of the keys with the rightmost of equal keys
+//    on top: the parent of operator i is the tighter (larger key; the left one on a tie) of
+//    L = the nearest operator left of i with a smaller key and R = the nearest one right of
+//    i with a key <= key_i (ballot masks per key), and i is R's left / L's right operand;
+//  * evaluate: each operator computes once both operands are ready (tree height rounds, LDS
+//    value slots), with exactly the node's f64 operation of the per-lane path, so every value
+//    is bit-identical (an operator's value depends only on its two operands);
+//  * check_format: for each of the instance's numbers, the count of equal digit runs (ballot)
+//    against its count among the numbers.
+// Whatever leaves this envelope (more than 16 tokens or 64 bytes, nesting deeper than 3, a
+// sign before '(' or a run of more than 3 signs, and everything the per-lane path itself
+// leaves: other bytes, '**', '//', long or 0-led literals, ints past 2**53) is evaluated by
+// the row's lane 0 with the per-lane path (countdown_reward) and broadcast.
+// Diagnostic build only (tools/prof_countdown_stamps.py compiles with RMI_CD_STAMPS): per-wave
+// s_memtime at the turn's phase boundaries (row 0 of each wave), written by lane 0 at the end.
+#ifdef RMI_CD_STAMPS
+__device__ unsigned long long* g_cd_stamps;
+constexpr int kCdStamps = 6;
+__device__ unsigned long long* g_cd_pstamps;  // [waves][8] inside par_reward (row 0, lane 0)
+#define CD_STAMP(arr, i) ((arr)[i] = __builtin_amdgcn_s_memtime())
+#define CD_PSTAMP(i, dep)                                                                          \
+  do {                                                                                              \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime() + (unsigned long long)((dep) == -7); \
+    if ((threadIdx.x & 63) == 0) g_cd_pstamps[(int64_t)blockIdx.x * 8 + (i)] = t_;                 \
+  } while (0)
+#else
+#define CD_STAMP(arr, i) ((void)0)
+#define CD_PSTAMP(i, dep) ((void)0)
+#endif
+constexpr int kRow = 16;
+constexpr int kParDepth = 3;
+constexpr int kParBytes = 16 * kRow + 2 * kRow + kRow + kRow;  // value slots, children, keys, mask bytes
+enum : int { C_NONE = 0, C_NUM, C_LP, C_RP, C_ADD, C_SUB, C_MUL, C_DIV };
+
+template <int CTRL>
+__device__ __forceinline__ int dpp(int old, int x) {  // row_shr:n = 0x110 + n, row_shl:n = 0x100 + n
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t row_bits(uint64_t ballot, int rowbase) {
+  return (uint32_t)(ballot >> rowbase) & 0xFFFFu;
+}
+__device__ __forceinline__ int hi_bit(uint32_t x) { return x ? 31 - __builtin_clz(x) : -1; }
+__device__ __forceinline__ int lo_bit(uint32_t x) { return x ? __builtin_ctz(x) : -1; }
+__device__ __forceinline__ int nth_bit(uint64_t t, int k) {  // position of set bit k (k < popcount)
+  int pos = 0;
+  int c = __popc((uint32_t)t);
+  if (k >= c) { k -= c; pos = 32; t >>= 32; }
+  c = __popc((uint32_t)t & 0xFFFFu);
+  if (k >= c) { k -= c; pos += 16; t >>= 16; }
+  c = __popc((uint32_t)t & 0xFFu);
+  if (k >= c) { k -= c; pos += 8; t >>= 8; }
+  c = __popc((uint32_t)t & 0xFu);
+  if (k >= c) { k -= c; pos += 4; t >>= 4; }
+  c = __popc((uint32_t)t & 0x3u);
+  if (k >= c) { k -= c; pos += 2; t >>= 2; }
+  c = (int)(t & 1u);
+  if (k >= c) pos += 1;
+  return pos;
+}
+
+__device__ __forceinline__ int ok_dep(int x) { return x; }
+struct ParOut {
+  int fb;  // leave to the per-lane path
+  int fmt, correct;
+};
+
+// Called by the 16 lanes of a row together (j = lane in the row), the answer staged at row
+// (16-B aligned, 80 bytes readable), n <= 64.  par: the row's kParBytes of LDS scratch.
+__device__ ParOut par_reward(const uint8_t* row, int n, int j, int rowbase, uint8_t* par,
+                             const int32_t (&nums)[kMaxNums], int n_nums, int32_t target) {
+  ParOut o;
+  o.fb = 0;
+  o.fmt = 0;
+  o.correct = 0;
+  volatile double* slot_v = reinterpret_cast<volatile double*>(par);             // [16] value (stride 16 B)
+  volatile uint32_t* slot_f = reinterpret_cast<volatile uint32_t*>(par + 8);     // [16] 1 ready | 2 float
+  volatile uint8_t* child = par + 16 * kRow;                                      // [16][2]
+  volatile uint8_t* mbytes = par + 16 * kRow + 3 * kRow;                          // [16]
+  // ---- masks: lane j classifies bytes 4j..4j+3
+  {
+    const uint32_t x = reinterpret_cast<const uint32_t*>(row)[j];
+    mbytes[j] = (uint8_t)(digit4(x) | space4(x) << 4);
+  }
+  asm volatile("" ::: "memory");  // the row's mask bytes (same wave: LDS keeps program order)
+  const uint4 mb = *reinterpret_cast<const uint4*>(const_cast<uint8_t*>(mbytes));
+  CD_PSTAMP(0, (int)mb.x);
+  uint64_t D = 0, SP = 0;
+  {
+    const uint32_t w4[4] = {mb.x, mb.y, mb.z, mb.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // 4 mask bytes -> 16 bits of each mask
+      uint32_t d = w4[q] & 0x0F0F0F0Fu, s = (w4[q] >> 4) & 0x0F0F0F0Fu;
+      d = (d | d >> 4) & 0x00FF00FFu;
+      d = (d | d >> 8) & 0xFFFFu;
+      s = (s | s >> 4) & 0x00FF00FFu;
+      s = (s | s >> 8) & 0xFFFFu;
+      D |= (uint64_t)d << (16 * q);
+      SP |= (uint64_t)s << (16 * q);
+    }
+  }
+  const uint64_t lm = n >= 64 ? ~0ull : ((1ull << n) - 1);
+  D &= lm;
+  const uint64_t TS = lm & ~SP & ~(D & (D << 1));
+  const int ntok = __popcll(TS);
+  if (ntok > kRow) {
+    o.fb = 1;
+    return o;
+  }
+  // ---- lane k = token k
+  const int k = j;
+  const int valid = k < ntok;
+  const int p = valid ? nth_bit(TS, k) : 0;
+  const uint64_t cw = load8(row, p);
+  const int b0 = (int)(cw & 0xFF), b1 = p + 1 < n ? (int)((cw >> 8) & 0xFF) : 0;
+  const int isdig = (unsigned)(b0 - '0') < 10u;
+  const unsigned kc = (unsigned)(b0 - '(');
+  const int kind = kc < 8u ? (int)((0x70504632u >> (4 * kc)) & 15u) : 0;  // ( ) * + , - . /  -> C_*
+  const int cls = valid ? (isdig ? C_NUM : kind) : C_NONE;
+  const int L = cls == C_NUM ? ctz64(~(D >> p)) : 0;
+  const int Lc = L < 1 ? 1 : L > 8 ? 8 : L;
+  uint64_t x8 = (cw & (~0ull >> (64 - 8 * Lc))) << (8 * (8 - Lc));
+  x8 &= 0x0F0F0F0F0F0F0F0Full;
+  x8 = (x8 * 10 + (x8 >> 8)) & 0x00FF00FF00FF00FFull;
+  x8 = (x8 * 100 + (x8 >> 16)) & 0x0000FFFF0000FFFFull;
+  x8 = (x8 * 10000 + (x8 >> 32)) & 0xFFFFFFFFull;
+  const uint32_t u = (uint32_t)x8;
+  CD_PSTAMP(1, (int)u);
+  int fb = valid & (cls == C_NONE);                                           // a byte outside the subset
+  fb |= (cls == C_NUM) & (((b0 == '0') & (L > 1)) | (L > 8));                 // 0-led or > 8 digits
+  fb |= ((cls == C_MUL) | (cls == C_DIV)) & (b1 == b0);                      // ** or //
+  // ---- syntax against the previous token, parenthesis depth
+  const int prev = dpp<0x111>(C_NONE, cls), next = dpp<0x101>(C_NONE, cls);
+  const int ends_prev = (prev == C_NUM) | (prev == C_RP);
+  const int expect = ends_prev ^ 1;
+  int err = valid & ((((cls == C_NUM) | (cls == C_LP)) & (expect ^ 1)) |
+                     (((cls == C_RP) | (cls == C_MUL) | (cls == C_DIV)) & expect));
+  err |= (k == ntok - 1) & (cls != C_NUM) & (cls != C_RP);  // the end where an operand is expected
+  const int delta = (cls == C_LP) - (cls == C_RP);
+  int incl = delta;
+  incl += dpp<0x111>(0, incl);
+  incl += dpp<0x112>(0, incl);
+  incl += dpp<0x114>(0, incl);
+  incl += dpp<0x118>(0, incl);
+  err |= valid & (incl < 0);
+  err |= (k == ntok - 1) & (incl != 0);
+  fb |= incl > kParDepth;
+  const int depth = incl - delta;
+  const int un = valid & ((cls == C_ADD) | (cls == C_SUB)) & expect;
+  fb |= un & (next == C_LP);  // a sign before a group
+  const int uw = un | ((un & (cls == C_SUB)) << 1);
+  const int p1 = dpp<0x111>(0, uw), p2 = dpp<0x112>(0, uw), p3 = dpp<0x113>(0, uw), p4 = dpp<0x114>(0, uw);
+  int c = p1 & 1, neg = c & (p1 >> 1);
+  c &= p2 & 1;
+  neg ^= c & (p2 >> 1);
+  c &= p3 & 1;
+  neg ^= c & (p3 >> 1);
+  fb |= (cls == C_NUM) & c & (p4 & 1);  // a run of more than 3 signs
+  const int bin = valid & (cls >= C_ADD) & (expect ^ 1);
+  const int key = 2 * depth + ((cls == C_MUL) | (cls == C_DIV));
+  const uint32_t rerr = row_bits(__ballot(err), rowbase), rfb = row_bits(__ballot(fb), rowbase);
+  CD_PSTAMP(2, (int)(rerr + rfb + key));
+  if (rfb) {  // first: check_format needs every digit run exactly (> 8 digits, other Unicode digits)
+    o.fb = 1;
+    return o;
+  }
+  // check_format: every digit run is a C_NUM token (<= 8 digits here).  For each of the numbers
+  // q, the count of equal runs must equal its count among the numbers: every run lane and every
+  // number lane j < n_nums add 1 << 4q per matching q (<= 8 per nibble when nf == n_nums), two
+  // DPP row sums, compared in lane 15
+  const uint32_t nummask = row_bits(__ballot(cls == C_NUM), rowbase);
+  {
+    int32_t mine = -1;
+#pragma unroll
+    for (int q = 0; q < kMaxNums; ++q) mine = q == j ? nums[q] : mine;
+    uint32_t cl = 0, cn = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxNums; ++q) {
+      const int live = q < n_nums;
+      cl += (uint32_t)(live & (cls == C_NUM) & ((int64_t)u == (int64_t)nums[q])) << (4 * q);
+      cn += (uint32_t)(live & (j < n_nums) & (mine == nums[q])) << (4 * q);
+    }
+    cl += (uint32_t)dpp<0x111>(0, (int)cl);
+    cn += (uint32_t)dpp<0x111>(0, (int)cn);
+    cl += (uint32_t)dpp<0x112>(0, (int)cl);
+    cn += (uint32_t)dpp<0x112>(0, (int)cn);
+    cl += (uint32_t)dpp<0x114>(0, (int)cl);
+    cn += (uint32_t)dpp<0x114>(0, (int)cn);
+    cl += (uint32_t)dpp<0x118>(0, (int)cl);
+    cn += (uint32_t)dpp<0x118>(0, (int)cn);
+    o.fmt = (__popc(nummask) == n_nums) & (row_bits(__ballot((j == kRow - 1) & (cl == cn)), rowbase) != 0);
+  }
+  CD_PSTAMP(3, ok_dep(o.fmt));
+  if (ntok == 0 || rerr) return o;  // a syntax error: not correct
+  // ---- the parse tree: per key value (up to the OR of the wave's keys, an upper bound of the
+  // largest) a ballot of the row's operators; L / R and their keys from the same masks
+  const uint32_t below = (1u << k) - 1, above = 0xFFFFu & ~((2u << k) - 1);
+  int kmax = 0;
+#pragma unroll
+  for (int bit = 0; bit < 3; ++bit) kmax |= __ballot(bin & ((key >> bit) & 1)) ? 1 << bit : 0;
+  int Lp = -1, Rp = -1, kL = -1, kR = -1;
+  for (int kk = 0; kk <= kmax; ++kk) {
+    const uint32_t m = row_bits(__ballot(bin & (key == kk)), rowbase);
+    const int cl = hi_bit(m & below), cr = lo_bit(m & above);
+    const int takeL = (kk < key) & (cl > Lp);
+    Lp = takeL ? cl : Lp;
+    kL = takeL ? kk : kL;
+    const int takeR = (kk <= key) & (cr >= 0) & ((Rp < 0) | (cr < Rp));
+    Rp = takeR ? cr : Rp;
+    kR = takeR ? kk : kR;
+  }
+  child[2 * k] = 0xFF;
+  child[2 * k + 1] = 0xFF;
+  const int toR = Rp >= 0 && (Lp < 0 || kR > kL);
+  const int parent = toR ? Rp : Lp;
+  if (bin && parent >= 0) child[2 * parent + (toR ? 0 : 1)] = (uint8_t)k;
+  const int cl = child[2 * k], cr = child[2 * k + 1];
+  const int lo = cl != 0xFF ? cl : hi_bit(nummask & below), ro = cr != 0xFF ? cr : lo_bit(nummask & above);
+  if (row_bits(__ballot(bin & ((lo < 0) | (ro < 0))), rowbase)) {  // not reached for valid syntax
+    o.fb = 1;
+    return o;
+  }
+  const uint32_t rootm = row_bits(__ballot(bin & (parent < 0)), rowbase);
+  const int root = rootm ? lo_bit(rootm) : lo_bit(nummask);
+  CD_PSTAMP(4, root + lo + ro);
+  // ---- evaluate: literals are ready, each operator fires once both operands are
+  {
+    const double uv = (double)u;
+    slot_v[2 * k] = neg ? 0.0 - uv : uv;  // an int -0 is 0
+    slot_f[4 * k] = cls == C_NUM ? 1u : 0u;
+  }
+  int ready = cls == C_NUM, zdiv = 0, big = 0;
+  for (int round = 0; round < kRow; ++round) {
+    if (!__ballot(bin & (ready ^ 1))) break;  // every operator of the wave has fired
+    if (bin && !ready) {
+      asm volatile("" ::: "memory");  // value + flags of both operands: two 16-B reads, one round trip
+      const uint4 sx = *reinterpret_cast<const uint4*>(par + 16 * lo);
+      const uint4 sy = *reinterpret_cast<const uint4*>(par + 16 * ro);
+      const uint32_t fx = sx.z, fy = sy.z;
+      if (fx & fy & 1u) {
+        const double x = __hiloint2double((int)sx.y, (int)sx.x), y = __hiloint2double((int)sy.y, (int)sy.x);
+        const int dv = cls == C_DIV;
+        const double sm = x + (cls == C_SUB ? -y : y), pr = x * y, qt = x / y;
+        double r = cls == C_MUL ? pr : dv ? qt : sm;
+        const int rf = (int)((fx | fy) >> 1 & 1u) | dv;
+        r = rf ? r : r + 0.0;  // an int -0 is 0
+        zdiv |= dv & (y == 0.0);
+        big |= (rf ^ 1) & (fabs(r) >= 9007199254740992.0);
+        slot_v[2 * k] = r;
+        slot_f[4 * k] = 1u | (uint32_t)rf << 1;
+        ready = 1;
+      }
+    }
+  }
+  CD_PSTAMP(5, ready);
+  if (row_bits(__ballot(big), rowbase)) {
+    o.fb = 1;
+    return o;
+  }
+  const int zd = row_bits(__ballot(zdiv), rowbase) != 0;
+  const double rv = slot_v[2 * root];
+  const uint32_t rfl = slot_f[4 * root];
+  o.correct = !zd && ((rfl & 2u) ? fabs(rv - (double)target) < 1e-5 : rv == (double)target);
+  CD_PSTAMP(6, o.correct);
+  return o;
+}
+
+// The row's reward: the 16 lanes call this together; every lane gets the same result.
+// fallback: lane 0 runs the per-lane path and broadcasts through par.
+__device__ double row_reward(const uint8_t* stage, const uint8_t* src_global, int n, int j, int rowbase,
+                             uint8_t* par, uint8_t* work, const int32_t (&nums)[kMaxNums], int n_nums,
+                             int32_t target, double score, double format_score, uint8_t& flags, uint8_t& err) {
+  int fb = !stage || n > kFastMax;
+  int fmt = 0, correct = 0;
+  if (!fb) {
+    const ParOut o = par_reward(stage, n, j, rowbase, par, nums, n_nums, target);
+    fb = o.fb;
+    correct = o.correct;
+    fmt = o.fmt;
+  }
+  if (fb) {
+    volatile double* bv = reinterpret_cast<volatile double*>(par);
+    volatile uint32_t* bf = reinterpret_cast<volatile uint32_t*>(par + 8);
+    if (j == 0) {
+      uint8_t fl = 0, e = 0;
+      const double r = countdown_reward(stage ? stage : src_global, n, stage != nullptr, nums, n_nums, target,
+                                        score, format_score, fl, e, work);
+      *bv = r;
+      *bf = (uint32_t)fl | (uint32_t)e << 8;
+    }
+    const double r = *bv;
+    const uint32_t w = *bf;
+    flags = (uint8_t)(w & 0xFF);
+    err |= (uint8_t)(w >> 8);
+    return r;
+  }
+  flags = (uint8_t)(fmt ? (correct ? 3 : 1) : 0);
+  return fmt ? (correct ? score : format_score) : 0.0;
+}
+
+// An answer string is staged into its row's LDS with 16-B loads, one per lane of the row
+// (a 256-B answer in one round trip); answer 0's first 64 B are loaded with the kernel's other
+// loads (prestage), so only longer answers pay a round trip of their own.
 constexpr int kStageMax = 256;  // answers up to this many bytes are staged (Lmax above: parsed in place)
 constexpr int kPre = 64;        // bytes of answer 0 prestaged
 __device__ __forceinline__ bool stage16(const uint8_t* g, int Lmax) {  // 16-B loads stay inside the slot
   return (Lmax & 15) == 0 && (reinterpret_cast<uintptr_t>(g) & 15u) == 0;
 }
-__device__ __forceinline__ void put16(uint8_t* lds_row, int off, const uint4& q) {
-  uint32_t* l4 = reinterpret_cast<uint32_t*>(lds_row + off);  // rows are 4-B aligned, not 16
-  l4[0] = q.x;
-  l4[1] = q.y;
-  l4[2] = q.z;
-  l4[3] = q.w;
-}
-// bytes [from, n) of the answer at g into lds_row (from a multiple of 16 when stage16)
-__device__ __forceinline__ void stage_answer(const uint8_t* g, int from, int n, int Lmax, uint8_t* lds_row) {
+// bytes [from, n) of the answer at g into lds_row (from a multiple of 16 when stage16); lane j of the row
+__device__ __forceinline__ void stage_answer(const uint8_t* g, int from, int n, int Lmax, uint8_t* lds_row, int j) {
   if (stage16(g, Lmax)) {
-    const uint4* g16 = reinterpret_cast<const uint4*>(g);
-    for (int c = from >> 4; 16 * c < n; c += 4) {
-      uint4 q[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (16 * (c + j) < n) q[j] = g16[c + j];
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (16 * (c + j) < n) put16(lds_row, 16 * (c + j), q[j]);
-    }
+    const int c = j;
+    if (16 * c >= from && 16 * c < n) *reinterpret_cast<uint4*>(lds_row + 16 * c) = reinterpret_cast<const uint4*>(g)[c];
   } else {
-    for (int i = from; i < n; ++i) lds_row[i] = g[i];
+    for (int i = from + j; i < n; i += kRow) lds_row[i] = g[i];
   }
 }
 
 struct CountdownDev {
   const uint8_t* answers;  // this env's [K, Lmax]
   const int32_t* lens;     // this env's [K]
-  uint8_t* stage;          // this thread's LDS row (nullptr: parse global memory in place)
-  int Lmax;
+  uint8_t* stage;          // the row's LDS answer (nullptr: parse global memory in place)
+  uint8_t* par;            // the row's cooperative scratch
+  uint8_t* work;           // the row's per-lane evaluator stacks (lane 0's fallback)
+  int Lmax, j, rowbase;
   int pre_n;     // bytes of answer 0 already in stage (0: none)
   int32_t len0;  // lens[0], loaded with them
   int32_t nums[kMaxNums];
   int n_nums;
-  uint8_t* work;  // this thread's evaluator stacks (LDS)
   int32_t target;
   double score, format_score;
-  int k_next;  // index of the answer the next step() consumes
   uint8_t err;
+#ifdef RMI_CD_STAMPS
+  unsigned long long st[kCdStamps];
+#endif
   __device__ bool step(int a, double& reward, bool& done, bool& eff, bool& success) {
     // `a` is the 1-based slot of the answer string (the host passes 1..K for every parsed action)
     const int k = a - 1;
@@ -961,13 +1313,15 @@ struct CountdownDev {
     const bool pre = k == 0 && pre_n > 0;
     int n = pre ? len0 : lens[k];
     if (n > Lmax) n = Lmax;
-    uint8_t fl;
+    if (n < 0) n = 0;
     const uint8_t* src = answers + (int64_t)k * Lmax;
-    if (stage && n > 0) {
-      stage_answer(src, pre ? pre_n : 0, n, Lmax, stage);
-      src = stage;
-    }
-    reward = countdown_reward(src, n, stage != nullptr, nums, n_nums, target, score, format_score, fl, err, work);
+    if (stage && n > 0) stage_answer(src, pre ? pre_n : 0, n, Lmax, stage, j);
+    uint8_t fl;
+    CD_STAMP(st, 2);  // the staging stores wait for their loads
+    reward = row_reward(stage, src, n, j, rowbase, par, work, nums, n_nums, target, score, format_score, fl, err);
+#ifdef RMI_CD_STAMPS
+    st[3] = (unsigned long long)(reward != -12345.0) * __builtin_amdgcn_s_memtime();
+#endif
     done = true;
     eff = reward > 0;
     success = reward == score;
@@ -975,61 +1329,54 @@ struct CountdownDev {
   }
 };
 
-// Per-thread LDS: the staged answer row, then the evaluator stacks.  64-thread blocks keep the
-// slices small enough for several blocks per CU.
+// Per row (16 lanes, one env or answer) of LDS: the staged answer, lane 0's per-lane evaluator
+// stacks, the cooperative scratch.  64-thread blocks = 4 rows.
 constexpr int kCdBlock = 64;
-// a staged row is 16-B aligned and readable 80 bytes past its start (fast_reward's token reads)
+// a staged row is 16-B aligned and readable 80 bytes past its start (the token reads)
 __host__ __device__ constexpr int stage_stride(int Lmax) { return Lmax <= kStageMax ? ((Lmax + 15) & ~15) + 16 : 0; }
-__host__ __device__ constexpr int cd_slice(int Lmax) { return stage_stride(Lmax) + kMachineBytes; }
+__host__ __device__ constexpr int cd_slice(int Lmax) { return stage_stride(Lmax) + kMachineBytes + kParBytes; }
 
 __device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b, int32_t (&nums)[kMaxNums]) {
 #pragma unroll
   for (int k = 0; k < kMaxNums; ++k) nums[k] = k < env.max_nums ? env.nums[b * env.max_nums + k] : -1;
 }
 
-// Lanes per answer.  An answer's evaluation is one lane's token loop; every lane of a wave runs
-// it to the wave's longest answer, so a turn costs one wave's latency, and that latency does not
-// shrink with fewer answers per wave: with the branch-free token loop, one answer per lane (LPA 1)
-// measured best at every size (tools/prof_countdown_lpa.py: 16 384 envs 17.0 us per turn vs
-// 20.1 / 47.1 us at LPA 4 / 16; equal at 1024 and 4096 envs).  Spreading answers LPA lanes
-// apart stays available for measurement builds (-DRMI_CD_LPA).
-__host__ __device__ constexpr int cd_lpa_for(int64_t) { return 1; }
-
-template <int LPA>
+// One env per DPP row: all 16 lanes load the env's words (one broadcast per word) and run the
+// turn's bookkeeping redundantly, so the answer evaluation inside step() is convergent across
+// the row; lane 0 stores.
 __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
                                                                        rmi_turn_t in,
                                                                        const uint8_t* __restrict__ answers,
                                                                        const int32_t* __restrict__ answer_len,
                                                                        int Lmax, uint8_t* __restrict__ err_out) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];  // [kCdBlock / LPA][cd_slice(Lmax)]
-  if (threadIdx.x % LPA) return;
-  const int64_t b = ((int64_t)blockIdx.x * kCdBlock + threadIdx.x) / LPA;
+  extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];  // [kCdBlock / kRow][cd_slice(Lmax)]
+  const int j = threadIdx.x & (kRow - 1), rowbase = threadIdx.x & 63 & ~(kRow - 1);
+  const int64_t b = ((int64_t)blockIdx.x * kCdBlock + threadIdx.x) / kRow;
   const int B = ep.B;
   if (b >= B) return;
+#ifdef RMI_CD_STAMPS
+  unsigned long long st0 = __builtin_amdgcn_s_memtime();
+#endif
   // every load of this env is issued before the activity test (one memory round trip): the
   // has_input byte through a pointer that is always valid, selected afterwards
   uint8_t flags = ep.flags[b];
   const uint8_t has_in = *(in.has_input ? in.has_input + b : ep.flags + b);
-  uint8_t* slice = cd_lds + (threadIdx.x / LPA) * cd_slice(Lmax);
+  uint8_t* slice = cd_lds + (threadIdx.x / kRow) * cd_slice(Lmax);
   CountdownDev e;
   e.answers = answers + b * (int64_t)in.K * Lmax;
   e.lens = answer_len + b * (int64_t)in.K;
   e.stage = Lmax <= kStageMax ? slice : nullptr;
   e.work = slice + stage_stride(Lmax);
+  e.par = e.work + kMachineBytes;
   e.Lmax = Lmax;
+  e.j = j;
+  e.rowbase = rowbase;
   e.pre_n = 0;
   e.len0 = 0;
   if (in.K > 0 && e.stage && stage16(e.answers, Lmax)) {  // answer 0's head, with the other loads
-    const uint4* g16 = reinterpret_cast<const uint4*>(e.answers);
     const int nc = (Lmax < kPre ? Lmax : kPre) >> 4;
-    uint4 q[kPre / 16];
-#pragma unroll
-    for (int j = 0; j < kPre / 16; ++j)
-      if (j < nc) q[j] = g16[j];
     e.len0 = e.lens[0];
-#pragma unroll
-    for (int j = 0; j < kPre / 16; ++j)
-      if (j < nc) put16(e.stage, 16 * j, q[j]);
+    if (j < nc) *reinterpret_cast<uint4*>(e.stage + 16 * j) = reinterpret_cast<const uint4*>(e.answers)[j];
     e.pre_n = 16 * nc;
   }
   load_nums(env, b, e.nums);
@@ -1046,8 +1393,17 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   double penalty = ep.penalty[b];
   const bool act = in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE);
   if (!act) return;
+#ifdef RMI_CD_STAMPS
+  e.st[0] = st0;
+  e.st[1] = __builtin_amdgcn_s_memtime() + (unsigned long long)(penalty == -12345.0);  // loads landed
+  e.st[2] = e.st[3] = e.st[1];
+#endif
   TurnOut o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
                        in.format_penalty, err);
+#ifdef RMI_CD_STAMPS
+  e.st[4] = __builtin_amdgcn_s_memtime();
+#endif
+  if (j) return;
   ep.num_actions[b] = num_actions;
   ep.flags[b] = flags;
   ep.n_turns[b] = n_turns;
@@ -1058,9 +1414,14 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   ep.turn_exec[tb] = o.exec;
   err |= e.err;
   if (err_out && err) err_out[b] |= err;
+#ifdef RMI_CD_STAMPS
+  if ((threadIdx.x & 63) == 0) {
+    e.st[5] = __builtin_amdgcn_s_memtime();
+    for (int q = 0; q < kCdStamps; ++q) g_cd_stamps[(int64_t)blockIdx.x * kCdStamps + q] = e.st[q];
+  }
+#endif
 }
 
-template <int LPA>
 __global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdown_t env,
                                                                     const uint8_t* __restrict__ answers,
                                                                     const int32_t* __restrict__ answer_len, int Lmax,
@@ -1068,10 +1429,12 @@ __global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdow
                                                                     uint8_t* __restrict__ flags_out,
                                                                     uint8_t* __restrict__ err_out) {
   extern __shared__ __attribute__((aligned(16))) uint8_t cd_lds[];
-  if (threadIdx.x % LPA) return;
-  const int64_t i = ((int64_t)blockIdx.x * kCdBlock + threadIdx.x) / LPA;
+  const int j = threadIdx.x & (kRow - 1), rowbase = threadIdx.x & 63 & ~(kRow - 1);
+  const int64_t i = ((int64_t)blockIdx.x * kCdBlock + threadIdx.x) / kRow;
   if (i >= n) return;
-  uint8_t* slice = cd_lds + (threadIdx.x / LPA) * cd_slice(Lmax);
+  uint8_t* slice = cd_lds + (threadIdx.x / kRow) * cd_slice(Lmax);
+  uint8_t* stage = Lmax <= kStageMax ? slice : nullptr;
+  uint8_t* work = slice + stage_stride(Lmax);
   uint8_t fl = 0, err = 0;
   int len = answer_len[i];
   if (len > Lmax) len = Lmax;
@@ -1079,12 +1442,10 @@ __global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdow
   int32_t nums[kMaxNums];
   load_nums(env, i, nums);
   const uint8_t* src = answers + i * (int64_t)Lmax;
-  if (Lmax <= kStageMax && len > 0) {
-    stage_answer(src, 0, len, Lmax, slice);
-    src = slice;
-  }
-  const double r = countdown_reward(src, len, Lmax <= kStageMax, nums, env.n_nums[i], env.target[i], env.score, env.format_score, fl,
-                                    err, slice + stage_stride(Lmax));
+  if (stage && len > 0) stage_answer(src, 0, len, Lmax, stage, j);
+  const double r = row_reward(stage, src, len, j, rowbase, work + kMachineBytes, work, nums, env.n_nums[i],
+                              env.target[i], env.score, env.format_score, fl, err);
+  if (j) return;
   reward[i] = r;
   if (flags_out) flags_out[i] = fl;
   if (err_out) err_out[i] = err;
@@ -1092,6 +1453,13 @@ __global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdow
 
 }  // namespace
 }  // namespace rmi
+
+#ifdef RMI_CD_STAMPS
+RMI_API int rmi_countdown_set_stamps(unsigned long long* buf, unsigned long long* pbuf) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_cd_stamps), &buf, sizeof(buf)) != hipSuccess) return -2;
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_cd_pstamps), &pbuf, sizeof(pbuf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                     const uint8_t* answers, const int32_t* answer_len, int32_t Lmax, uint8_t* err,
@@ -1104,24 +1472,11 @@ RMI_API int rmi_countdown_step_turn(const rmi_countdown_t* env, const rmi_episod
   if (!answers || !answer_len || !env->nums || !env->n_nums || !env->target || !in->n_actions || !ep->num_actions ||
       !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
     return RMI_EINVAL;
-#ifdef RMI_CD_LPA
-  constexpr int kL = RMI_CD_LPA;  // measurement builds (tools/prof_countdown_lpa.py)
-  const int lpa = kL;
-#else
-  const int lpa = cd_lpa_for(ep->B);
-#endif
-  const int64_t lanes = (int64_t)ep->B * lpa;
+  const int64_t lanes = (int64_t)ep->B * kRow;
   const dim3 grid((unsigned)((lanes + kCdBlock - 1) / kCdBlock));
-  const size_t lds = (size_t)(kCdBlock / lpa) * cd_slice(Lmax);
-  hipStream_t s = as_stream(stream);
-#define RMI_CD_LAUNCH(L) \
-  hipLaunchKernelGGL(countdown_step_turn_kernel<L>, grid, dim3(kCdBlock), lds, s, *env, *ep, *in, answers, \
-                     answer_len, Lmax, err)
-  if (lpa == 1) RMI_CD_LAUNCH(1);
-  else if (lpa == 4) RMI_CD_LAUNCH(4);
-  else if (lpa == 16) RMI_CD_LAUNCH(16);
-  else RMI_CD_LAUNCH(64);
-#undef RMI_CD_LAUNCH
+  const size_t lds = (size_t)(kCdBlock / kRow) * cd_slice(Lmax);
+  hipLaunchKernelGGL(countdown_step_turn_kernel, grid, dim3(kCdBlock), lds, as_stream(stream), *env, *ep, *in,
+                     answers, answer_len, Lmax, err);
   return launch_status();
 }
 
@@ -1132,18 +1487,9 @@ RMI_API int rmi_countdown_reward(const rmi_countdown_t* env, const uint8_t* answ
   if (!env || Lmax <= 0 || n < 0 || env->max_nums <= 0 || env->max_nums > 8) return RMI_EINVAL;
   if (n == 0) return RMI_OK;
   if (!answers || !answer_len || !reward || !env->nums || !env->n_nums || !env->target) return RMI_EINVAL;
-  const int lpa = cd_lpa_for(n);
-  const dim3 grid((unsigned)(((int64_t)n * lpa + kCdBlock - 1) / kCdBlock));
-  const size_t lds = (size_t)(kCdBlock / lpa) * cd_slice(Lmax);
-  hipStream_t s = as_stream(stream);
-  if (lpa == 1)
-    hipLaunchKernelGGL(countdown_reward_kernel<1>, grid, dim3(kCdBlock), lds, s, *env, answers, answer_len, Lmax, n,
-                       reward, flags, err);
-  else if (lpa == 4)
-    hipLaunchKernelGGL(countdown_reward_kernel<4>, grid, dim3(kCdBlock), lds, s, *env, answers, answer_len, Lmax, n,
-                       reward, flags, err);
-  else
-    hipLaunchKernelGGL(countdown_reward_kernel<16>, grid, dim3(kCdBlock), lds, s, *env, answers, answer_len, Lmax, n,
-                       reward, flags, err);
+  const dim3 grid((unsigned)(((int64_t)n * kRow + kCdBlock - 1) / kCdBlock));
+  const size_t lds = (size_t)(kCdBlock / kRow) * cd_slice(Lmax);
+  hipLaunchKernelGGL(countdown_reward_kernel, grid, dim3(kCdBlock), lds, as_stream(stream), *env, answers, answer_len,
+                     Lmax, n, reward, flags, err);
   return launch_status();
 }

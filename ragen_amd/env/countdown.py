@@ -44,11 +44,14 @@ def load_instances(config: CountdownEnvConfig):
 
 class CountdownBatch(BatchEnv):
     env_type = "countdown"
-    MAX_NUMS = 4
+    MAX_NUMS = 4  # the reference's instances (has_solution pads to 4, countdown/env.py:25-27)
 
     def __init__(self, config: CountdownEnvConfig, n_envs, max_turns, max_actions_per_turn, device=None,
-                 max_answer_bytes: int = 128):
+                 max_answer_bytes: int = 128, max_nums: int = MAX_NUMS):
         super().__init__(config or CountdownEnvConfig(), n_envs, max_turns, max_actions_per_turn, device)
+        if not 1 <= max_nums <= 8:
+            raise ValueError("max_nums: the kernel holds 1..8 numbers per instance")
+        self.MAX_NUMS = int(max_nums)
         self.data = load_instances(self.config)
         self.Lmax = int(max_answer_bytes)
         d = self.device
@@ -81,7 +84,7 @@ class CountdownBatch(BatchEnv):
         for i, ix in enumerate(self.index):
             inst = self.data[int(ix)]
             if len(inst["nums"]) > self.MAX_NUMS:
-                raise NotImplementedError("Countdown kernel supports at most 4 numbers per instance")
+                raise NotImplementedError(f"{len(inst['nums'])} numbers > max_nums={self.MAX_NUMS} for this batch")
             nums[i, :len(inst["nums"])] = inst["nums"]
             nn[i] = len(inst["nums"])
             tg[i] = inst["target"]

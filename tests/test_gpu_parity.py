@@ -230,6 +230,104 @@ def test_countdown_reward_fuzz(device):
     assert (want == 1).sum() > n // 20 and (want == 0.1).sum() > n // 20
 
 
+def _tree_answers(n, seed):
+    """Valid expressions shaped for the 16-lane evaluator's envelope edges: random binary trees
+    over + - * / (left chains, ties of equal keys, groups on either side), redundant parens,
+    signs on literals and on groups, 1..8 literals, depth up to 5, 14..18 tokens, ints around
+    2**53, float results, zero divisors, 0 and -0 operands."""
+    rng = np.random.default_rng(seed)
+    lits = [0, 1, 2, 3, 7, 12, 99, 100, 12345, 94906265, 94906266, 99999999]
+
+    def expr(nl, depth):
+        if nl == 1:
+            e = str(int(rng.choice(lits)))
+        else:
+            cut = int(rng.integers(1, nl))
+            e = expr(cut, depth + 1) + rng.choice([" ", ""]) + "+-*/"[int(rng.integers(0, 4))] + \
+                rng.choice([" ", ""]) + expr(nl - cut, depth + 1)
+            if rng.random() < 0.45:
+                e = "(" + e + ")"
+        if rng.random() < 0.08:
+            e = "(" + e + ")"  # redundant group
+        if rng.random() < 0.15:
+            e = "".join(rng.choice(["-", "+", "- "], int(rng.integers(1, 5)))) + e  # signs, some before '('
+        return e
+
+    out, data = [], []
+    for _ in range(n):
+        e = expr(int(rng.integers(1, 9)), 0)
+        if len(e) > 64:
+            e = e[:64]  # a cut expression: a syntax error (or > 64 bytes handled by the fallback)
+        runs = [int(x) for x in __import__("re").findall(r"\d+", e)]
+        try:
+            v = eval(e, {"__builtins__": None}, {})
+            tgt = int(v) if isinstance(v, (int, float)) and abs(v) < 2**31 and v == int(v) else 5
+        except Exception:
+            tgt = 5
+        if rng.random() < 0.15:
+            tgt += 1
+        nums = [x if x < 2**31 else 1 for x in runs][:8] or [1]
+        if rng.random() < 0.1:
+            nums = nums[::-1] + [3]  # format mismatch
+        out.append(e)
+        data.append({"nums": nums[:8], "target": tgt})
+    return out, data
+
+
+def _past_int64(expr):
+    """True if evaluating expr (+ - * / and unary signs) makes an int of 2**63 or more in
+    magnitude (a Python big int: outside the device evaluator's int64 model)."""
+    import ast
+    try:
+        tree = ast.parse(expr, mode="eval")
+    except SyntaxError:
+        return False
+    seen = [False]
+
+    def ev(n):
+        if isinstance(n, ast.Expression):
+            return ev(n.body)
+        if isinstance(n, ast.Constant):
+            return n.value
+        if isinstance(n, ast.UnaryOp):
+            v = ev(n.operand)
+            v = -v if isinstance(n.op, ast.USub) else v
+        else:
+            a, b = ev(n.left), ev(n.right)
+            op = type(n.op)
+            v = a + b if op is ast.Add else a - b if op is ast.Sub else a * b if op is ast.Mult else a / b
+        if isinstance(v, int) and abs(v) >= 2**63:
+            seen[0] = True
+        return v
+    try:
+        ev(tree)
+    except ZeroDivisionError:
+        pass
+    return seen[0]
+
+
+def test_countdown_reward_tree_shapes(device):
+    """The 16-lane evaluator (one token per lane: syntax from neighbours, the Cartesian tree of
+    operator keys, node-by-node f64 evaluation) and its fallbacks == oracle.countdown_reward
+    (Python eval) on 20 000 tree-shaped answers, with no RMI_ERR_UNSUP."""
+    n = 20000
+    exprs, data = _tree_answers(n, 11)
+    env = CountdownBatch(CountdownEnvConfig(data=data), n, 1, 1, device, max_answer_bytes=64, max_nums=8)
+    env.reset(np.arange(n, dtype=np.int64))
+    buf, lens = env.encode_answers([[e] for e in exprs])
+    r, fl, err = ops.countdown_reward(env.struct(), _t(buf[:, 0], device), _t(lens[:, 0].copy(), device))
+    r, fl, err = r.cpu().numpy(), fl.cpu().numpy(), err.cpu().numpy()
+    want = np.array([oracle.countdown_reward(e, d["nums"], d["target"]) for e, d in zip(exprs, data)])
+    big = np.array([_past_int64(e) for e in exprs])
+    bad = np.nonzero((r != want) & ~big)[0]
+    assert bad.size == 0, [(exprs[i], data[i], r[i], want[i]) for i in bad[:5]]
+    assert not (err.astype(bool) & ~big).any()  # only Python big ints leave the model
+    ok = ~big
+    assert np.array_equal((fl & 1)[ok], (want[ok] > 0).astype(np.uint8))
+    assert np.array_equal((fl >> 1 & 1)[ok], (want[ok] == 1).astype(np.uint8))
+    assert (want == 1).sum() > n // 10 and (want == 0.1).sum() > n // 10
+
+
 # ------------------------------------------------------------- BASELINE-size parity vs oracle
 @pytest.mark.parametrize("B", [8192, 20000])
 def test_sokoban_full_size_vs_oracle(device, B):

@@ -4,6 +4,6 @@ OUT=gpurun_out/cdpmc; mkdir -p $OUT
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU" "SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_SALU"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $set --kernel-trace -d $OUT/p$i -o pmc --output-format csv -- python3 tools/prof_countdown.py "sum of nums" > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $OUT/p$i.log; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $set --kernel-trace -d $OUT/p$i -o pmc --output-format csv -- python3 tools/prof_countdown.py "${CASE:-sum of nums}" > $OUT/p$i.log 2>&1 || { echo "pass $i failed"; tail -3 $OUT/p$i.log; exit 1; }
 done
 echo ok
