@@ -345,6 +345,29 @@ int rmi_masked_whiten_stats(float* x, int64_t B, int64_t L, const double* stats,
 int rmi_grpo_outcome(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G,
                      double eps, int32_t norm_by_std, float* adv, float* ret, rmi_stream_t stream);
 
+/* Replaces: verl compute_reinforce_plus_plus_outcome_advantage (agent_trainer.py:110-117)
+ * before its masked_whiten: ret[b,t] = running = r[b,t] + gamma * running, then
+ * running *= mask[b,t], right to left in f32 (adv = ret).  row_stats (optional) gets the
+ * per-row whitening partials of adv; the caller then whitens adv and applies rmi_mask_mul. */
+int rmi_reinforce_pp_returns(const float* r, const uint8_t* mask, int64_t B, int64_t L, double gamma, float* adv,
+                             float* ret, double* row_stats, rmi_stream_t stream);
+
+/* Replaces: verl compute_remax_outcome_advantage (agent_trainer.py:118-126): ret = reverse
+ * cumsum of r * mask (torch's CPU accumulator: double, each output rounded to f32);
+ * adv = ret - baseline[b] * mask. */
+int rmi_remax(const float* r, const uint8_t* mask, const float* baseline, int64_t B, int64_t L, float* adv,
+              float* ret, rmi_stream_t stream);
+
+/* Replaces: verl compute_rloo_outcome_advantage (agent_trainer.py:127-134) with contiguous
+ * groups seg[G+1]: score s = sum_t r; for a group of n > 1, s * n / (n-1) - mean * n / (n-1),
+ * else s; broadcast over the row's mask (adv = ret). */
+int rmi_rloo_outcome(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G,
+                     float* adv, float* ret, rmi_stream_t stream);
+
+/* x[i] *= (mask[i] != 0), in f32: the trailing `* response_mask` of verl's REINFORCE++ and
+ * REINFORCE++-baseline estimators (agent_trainer.py:102-117) after their masked_whiten. */
+int rmi_mask_mul(float* x, const uint8_t* mask, int64_t n, rmi_stream_t stream);
+
 /* ------------------------------------------------ response -> action ids (§8(f) rank 2)
  * Replaces: ContextManager.get_env_inputs (ctx_manager.py:332-352): the tokenizer's
  *           batch_decode(responses, skip_special_tokens=True) (:334-337), the "<think>" /

@@ -193,6 +193,47 @@ def grpo(r, mask, seg, eps=1e-6, norm_by_std=True):
     return adv, ret
 
 
+def reinforce_pp(r, mask, gamma, whiten=True):
+    """verl REINFORCE++ (ragen_oracle.c: orc_reinforce_pp): -> (adv, ret); adv = the whitened
+    returns times the mask (whitening in double, as orc_masked_whiten)."""
+    r = np.ascontiguousarray(r, np.float32)
+    m = np.ascontiguousarray(mask, np.uint8)
+    ret = np.zeros_like(r)
+    lib().orc_reinforce_pp(_p(r), _p(m), ctypes.c_int64(r.shape[0]), ctypes.c_int64(r.shape[1]),
+                           ctypes.c_double(gamma), _p(ret))
+    adv = masked_whiten(ret, m) * (m != 0) if whiten else ret.copy()
+    return adv.astype(np.float32), ret
+
+
+def remax(r, mask, base):
+    r = np.ascontiguousarray(r, np.float32)
+    m = np.ascontiguousarray(mask, np.uint8)
+    base = np.ascontiguousarray(base, np.float32)
+    adv = np.zeros_like(r)
+    ret = np.zeros_like(r)
+    lib().orc_remax(_p(r), _p(m), _p(base), ctypes.c_int64(r.shape[0]), ctypes.c_int64(r.shape[1]), _p(adv), _p(ret))
+    return adv, ret
+
+
+def rloo(r, mask, seg):
+    r = np.ascontiguousarray(r, np.float32)
+    m = np.ascontiguousarray(mask, np.uint8)
+    seg = np.ascontiguousarray(seg, np.int32)
+    adv = np.zeros_like(r)
+    lib().orc_rloo(_p(r), _p(m), ctypes.c_int64(r.shape[0]), ctypes.c_int64(r.shape[1]), _p(seg), len(seg) - 1,
+                   _p(adv))
+    return adv, adv
+
+
+def reinforce_pp_baseline(r, mask, seg):
+    """verl REINFORCE++-baseline: the group-centred score tiled over the mask (GRPO without
+    std), whitened, times the mask."""
+    adv, _ = grpo(r, mask, seg, norm_by_std=False)
+    m = np.ascontiguousarray(mask, np.uint8)
+    adv = masked_whiten(adv, m) * (m != 0)
+    return adv.astype(np.float32), adv.astype(np.float32)
+
+
 def filter_groups(scores, G, gs, ratio, ftype):
     scores = np.ascontiguousarray(scores, np.float32)
     sd = np.zeros(G, np.float32)

@@ -521,6 +521,56 @@ static int kv_cmp(const void* a, const void* b) {
   if (!xn && x->key != y->key) return x->key > y->key ? -1 : 1;
   return x->g - y->g;
 }
+/* verl compute_reinforce_plus_plus_outcome_advantage, before its whitening (agent_trainer.py:110-117):
+ * for t from L-1 down: running = r_t + gamma * running; ret_t = running; running *= mask_t (f32). */
+void orc_reinforce_pp(const float* r, const uint8_t* mask, int64_t B, int64_t L, double gamma, float* ret) {
+  const float g = (float)gamma;
+  for (int64_t b = 0; b < B; ++b) {
+    float run = 0.0f;
+    for (int64_t t = L - 1; t >= 0; --t) {
+      run = r[b * L + t] + g * run;
+      ret[b * L + t] = run;
+      run = run * (mask[b * L + t] ? 1.0f : 0.0f);
+    }
+  }
+}
+
+/* verl compute_remax_outcome_advantage (agent_trainer.py:118-126): ret = flip(cumsum(flip(r * m)))
+ * with torch's CPU cumsum accumulator (double, each output cast to f32); adv = ret - base * m. */
+void orc_remax(const float* r, const uint8_t* mask, const float* base, int64_t B, int64_t L, float* adv, float* ret) {
+  for (int64_t b = 0; b < B; ++b) {
+    double acc = 0.0;
+    for (int64_t t = L - 1; t >= 0; --t) {
+      const float m = mask[b * L + t] ? 1.0f : 0.0f;
+      acc += (double)(r[b * L + t] * m);
+      ret[b * L + t] = (float)acc;
+      adv[b * L + t] = ret[b * L + t] - base[b] * m;
+    }
+  }
+}
+
+/* verl compute_rloo_outcome_advantage (agent_trainer.py:127-134), contiguous groups seg[G+1]:
+ * s = sum_t r (f32 result); n > 1: s * n / (n-1) - mean * n / (n-1), else s; times the mask. */
+void orc_rloo(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G, float* adv) {
+  float* sc = (float*)malloc(sizeof(float) * (B ? B : 1));
+  for (int64_t b = 0; b < B; ++b) {
+    double s = 0;
+    for (int64_t t = 0; t < L; ++t) s += r[b * L + t];
+    sc[b] = (float)s;
+  }
+  for (int g = 0; g < G; ++g) {
+    const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
+    double s = 0;
+    for (int i = lo; i < hi; ++i) s += sc[i];
+    const float mean = n > 0 ? (float)(s / n) : 0.0f, fn = (float)n, fd = (float)(n - 1);
+    for (int i = lo; i < hi; ++i) {
+      const float y = n > 1 ? (sc[i] * fn) / fd - (mean * fn) / fd : sc[i];
+      for (int64_t t = 0; t < L; ++t) adv[(int64_t)i * L + t] = y * (mask[(int64_t)i * L + t] ? 1.0f : 0.0f);
+    }
+  }
+  free(sc);
+}
+
 void orc_filter(const float* scores, int32_t G, int32_t gs, double ratio, int32_t type, float* g_std, float* g_max,
                 float* g_mean, uint8_t* keep, double* metrics) {
   kv_t* kv = (kv_t*)malloc(sizeof(kv_t) * G);

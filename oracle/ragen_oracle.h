@@ -72,6 +72,9 @@ int orc_bilevel_gae(const float* r, const float* v, const uint8_t* mask, int64_t
 int orc_masked_whiten(float* x, const uint8_t* mask, int64_t B, int64_t L);
 void orc_grpo(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G, double eps,
               int32_t norm_by_std, float* adv, float* ret);
+void orc_reinforce_pp(const float* r, const uint8_t* mask, int64_t B, int64_t L, double gamma, float* ret);
+void orc_remax(const float* r, const uint8_t* mask, const float* base, int64_t B, int64_t L, float* adv, float* ret);
+void orc_rloo(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G, float* adv);
 void orc_filter(const float* scores, int32_t G, int32_t gs, double ratio, int32_t type, float* g_std, float* g_max,
                 float* g_mean, uint8_t* keep, double* metrics);
 

@@ -122,6 +122,12 @@ _SIGS = {
     "rmi_masked_whiten_stats": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_grpo_outcome": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_double, c_int32,
                                    c_void_p, c_void_p, c_void_p]),
+    "rmi_reinforce_pp_returns": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_double, c_void_p, c_void_p,
+                                           c_void_p, c_void_p]),
+    "rmi_remax": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rmi_rloo_outcome": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int32, c_void_p, c_void_p,
+                                   c_void_p]),
+    "rmi_mask_mul": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "rmi_detokenize": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                  c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     "rmi_parse_actions": (c_int32, [_P(ParseCfg), c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p,

@@ -5,6 +5,11 @@
 //  rmi_bilevel_gae   compute_bi_level_gae_advantage_return (core_algos.py:4-92)
 //  rmi_masked_whiten verl masked_whiten (core_algos.py:90)
 //  rmi_grpo_outcome  verl compute_grpo_outcome_advantage (agent_trainer.py:94-99)
+//  rmi_reinforce_pp_returns  verl compute_reinforce_plus_plus_outcome_advantage before its
+//                    whitening (agent_trainer.py:110-117)
+//  rmi_remax         verl compute_remax_outcome_advantage (agent_trainer.py:118-126)
+//  rmi_rloo_outcome  verl compute_rloo_outcome_advantage (agent_trainer.py:127-134)
+//  rmi_mask_mul      the trailing `* response_mask` of verl's REINFORCE++ estimators
 //
 // Exactness: the GAE recurrence runs sequentially per row in the reference's f32 op order
 // ((r + g*nv) - v, then delta + (g*lam)*last, g*lam formed in double as Python does) and
@@ -115,9 +120,26 @@ __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restric
 // verl compute_gae_advantage_return, reverse recurrence in the reference's f32 op order:
 //   delta = (r_t + g * nv) - v_t ;  last = delta + gl * last ;  adv = last ; ret = adv + v_t
 // legacy (VARIANT 0): nv = v_{t+1}; masked (1): nv / last carried through mask-0 positions.
+// VARIANT 2, REINFORCE++ returns (verl, torch CPU loop): running = r_t + g * running;
+//   ret_t = running; running = running * m_t  (adv_t = ret_t: whitened afterwards).
+// VARIANT 3, REMAX: ret = flip(cumsum(flip(r * m))) with torch's CPU cumsum accumulator
+//   (double, each output rounded to f32); adv_t = ret_t - base * m_t  (base: the row's baseline).
 template <int VARIANT>
 __device__ __forceinline__ void gae_col(float rt, float vt, float mt, float g, float gl, float& nv, float& last,
-                                        float& a_out, float& ret_out) {
+                                        float& a_out, float& ret_out, double& dacc, float base) {
+  if (VARIANT == 2) {
+    const float run = rt + g * last;
+    a_out = run;
+    ret_out = run;
+    last = run * mt;
+    return;
+  }
+  if (VARIANT == 3) {
+    dacc += (double)(rt * mt);
+    ret_out = (float)dacc;
+    a_out = ret_out - base * mt;
+    return;
+  }
   const float delta = (rt + g * nv) - vt;
   if (VARIANT == 0) {
     last = delta + gl * last;
@@ -135,7 +157,8 @@ template <int VARIANT>
 __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                  const uint8_t* __restrict__ mask, int64_t B, int64_t L, float g,
                                                  float gl, float* __restrict__ adv, float* __restrict__ ret,
-                                                 double* __restrict__ row_stats) {
+                                                 double* __restrict__ row_stats,
+                                                 const float* __restrict__ row_base = nullptr) {
   __shared__ __attribute__((aligned(16))) float sr[kGRows * kGStr];  // r in, adv out
   __shared__ __attribute__((aligned(16))) float sv[kGRows * kGStr];  // v in, ret out
   __shared__ __attribute__((aligned(16))) uint8_t sm[kGRows * kGMStr];
@@ -144,6 +167,8 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, co
   const int64_t ntiles = (L + kGCols - 1) / kGCols;
   const bool walker = lane < kGRows && row0 + lane < B;
   float last = 0.0f, nv = 0.0f;
+  double dacc = 0.0;  // REMAX: torch CPU cumsum's double accumulator
+  const float base = (VARIANT == 3 && walker) ? row_base[row0 + lane] : 0.0f;
   double s1a = 0.0, s1b = 0.0, s2a = 0.0, s2b = 0.0, cnt = 0.0;  // row stats, two chains each
 
   GaeTile t;
@@ -171,10 +196,10 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, co
         const F4 v4 = *reinterpret_cast<const F4*>(pv + 4 * q);
         const uint32_t m4 = *reinterpret_cast<const uint32_t*>(pm + 4 * q);
         F4 a4, t4;
-        gae_col<VARIANT>(r4.w, v4.w, (float)((m4 >> 24) & 0xFF), g, gl, nv, last, a4.w, t4.w);
-        gae_col<VARIANT>(r4.z, v4.z, (float)((m4 >> 16) & 0xFF), g, gl, nv, last, a4.z, t4.z);
-        gae_col<VARIANT>(r4.y, v4.y, (float)((m4 >> 8) & 0xFF), g, gl, nv, last, a4.y, t4.y);
-        gae_col<VARIANT>(r4.x, v4.x, (float)(m4 & 0xFF), g, gl, nv, last, a4.x, t4.x);
+        gae_col<VARIANT>(r4.w, v4.w, (float)((m4 >> 24) & 0xFF), g, gl, nv, last, a4.w, t4.w, dacc, base);
+        gae_col<VARIANT>(r4.z, v4.z, (float)((m4 >> 16) & 0xFF), g, gl, nv, last, a4.z, t4.z, dacc, base);
+        gae_col<VARIANT>(r4.y, v4.y, (float)((m4 >> 8) & 0xFF), g, gl, nv, last, a4.y, t4.y, dacc, base);
+        gae_col<VARIANT>(r4.x, v4.x, (float)(m4 & 0xFF), g, gl, nv, last, a4.x, t4.x, dacc, base);
         *reinterpret_cast<F4*>(pr + 4 * q) = a4;
         *reinterpret_cast<F4*>(pv + 4 * q) = t4;
         // whitening partials over in-mask positions (mask bytes are 0/1)
@@ -741,8 +766,17 @@ __global__ __launch_bounds__(kBlock) void whiten_apply_kernel(float* __restrict_
     x[i] = (x[i] - mean) * scale;
 }
 
+// x *= (mask != 0) elementwise (f32 multiply, so a negative value becomes -0.0 as in torch)
+__global__ __launch_bounds__(kBlock) void mask_mul_kernel(float* __restrict__ x, const uint8_t* __restrict__ mask,
+                                                          int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock)
+    x[i] = x[i] * (mask[i] ? 1.0f : 0.0f);
+}
+
 // GRPO: one wave per group segment; rows of the group are summed (fp64 -> f32) per row,
 // group mean/std in fp64, then the per-row score is broadcast over the row's mask.
+// mode 0: GRPO without std (also REINFORCE++-baseline's centred score), 1: GRPO, 2: RLOO
+// (n > 1: s * n / (n - 1) - mean * n / (n - 1) in the reference's f32 op order; n == 1: s).
 __global__ __launch_bounds__(kBlock) void grpo_kernel(const float* __restrict__ r, const uint8_t* __restrict__ mask,
                                                       int64_t B, int64_t L, const int32_t* __restrict__ seg, int G,
                                                       float eps, int norm_by_std, float* __restrict__ adv,
@@ -774,8 +808,14 @@ __global__ __launch_bounds__(kBlock) void grpo_kernel(const float* __restrict__ 
     double s = 0.0;
     for (int64_t i = lane; i < L; i += 64) s += (double)r[row * L + i];
     s = wave_sum(s);
-    float sc = (float)s - mean;
-    if (norm_by_std) sc = sc / (sd + eps);
+    float sc;
+    if (norm_by_std == 2) {
+      const float fn = (float)n, fd = (float)(n - 1);
+      sc = n > 1 ? ((float)s * fn) / fd - (mean * fn) / fd : (float)s;
+    } else {
+      sc = (float)s - mean;
+      if (norm_by_std) sc = sc / (sd + eps);
+    }
     for (int64_t i = lane; i < L; i += 64) {
       const float y = sc * (float)(mask[row * L + i] != 0);
       adv[row * L + i] = y;
@@ -886,5 +926,49 @@ RMI_API int rmi_grpo_outcome(const float* r, const uint8_t* mask, int64_t B, int
   const int per = kBlock / 64;
   hipLaunchKernelGGL(grpo_kernel, dim3((G + per - 1) / per), dim3(kBlock), 0, as_stream(stream), r, mask, B, L, seg, G,
                      (float)eps, norm_by_std, adv, ret);
+  return launch_status();
+}
+
+RMI_API int rmi_reinforce_pp_returns(const float* r, const uint8_t* mask, int64_t B, int64_t L, double gamma,
+                                     float* adv, float* ret, double* row_stats, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!r || !mask || !adv || !ret || B < 0 || L < 0) return RMI_EINVAL;
+  if (B == 0 || L == 0) return RMI_OK;
+  const unsigned grid = (unsigned)((B + kGRows - 1) / kGRows);
+  // v is not part of this recurrence: r stands in for it (read, never used)
+  hipLaunchKernelGGL(gae_kernel<2>, dim3(grid), dim3(64), 0, as_stream(stream), r, r, mask, B, L, (float)gamma, 0.0f,
+                     adv, ret, row_stats, nullptr);
+  return launch_status();
+}
+
+RMI_API int rmi_remax(const float* r, const uint8_t* mask, const float* baseline, int64_t B, int64_t L, float* adv,
+                      float* ret, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!r || !mask || !baseline || !adv || !ret || B < 0 || L < 0) return RMI_EINVAL;
+  if (B == 0 || L == 0) return RMI_OK;
+  const unsigned grid = (unsigned)((B + kGRows - 1) / kGRows);
+  hipLaunchKernelGGL(gae_kernel<3>, dim3(grid), dim3(64), 0, as_stream(stream), r, r, mask, B, L, 0.0f, 0.0f, adv,
+                     ret, nullptr, baseline);
+  return launch_status();
+}
+
+RMI_API int rmi_rloo_outcome(const float* r, const uint8_t* mask, int64_t B, int64_t L, const int32_t* seg, int32_t G,
+                             float* adv, float* ret, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!r || !mask || !seg || !adv || !ret || B < 0 || L < 0 || G < 0) return RMI_EINVAL;
+  if (B == 0 || G == 0) return RMI_OK;
+  const int per = kBlock / 64;
+  hipLaunchKernelGGL(grpo_kernel, dim3((G + per - 1) / per), dim3(kBlock), 0, as_stream(stream), r, mask, B, L, seg, G,
+                     0.0f, 2, adv, ret);
+  return launch_status();
+}
+
+RMI_API int rmi_mask_mul(float* x, const uint8_t* mask, int64_t n, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!x || !mask || n < 0) return RMI_EINVAL;
+  if (n == 0) return RMI_OK;
+  int64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(mask_mul_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, as_stream(stream), x, mask, n);
   return launch_status();
 }

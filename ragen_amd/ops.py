@@ -772,6 +772,65 @@ def masked_whiten_stats_(x, stats):
     return x, scratch
 
 
+def reinforce_pp_returns(r, mask, gamma, row_stats=None):
+    """verl compute_reinforce_plus_plus_outcome_advantage before its whitening: the masked
+    discounted returns (adv = ret) -> (adv, ret) f32[B, L]; row_stats f64[B, 3] (optional)
+    receives adv's per-row whitening partials."""
+    _dev(r, mask, row_stats)
+    _dt(r, torch.float32, "token_level_rewards")
+    B, L = _rows(r, mask, names=("response_mask",))
+    _row_stats(row_stats, B)
+    m = _mask_u8(mask).contiguous()
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    check(lib().rmi_reinforce_pp_returns(_ptr(r), _ptr(m), B, L, float(gamma), _ptr(adv), _ptr(ret),
+                                         _ptr(row_stats), _stream(r.device)), "rmi_reinforce_pp_returns")
+    return adv, ret
+
+
+def remax(r, mask, baseline):
+    """verl compute_remax_outcome_advantage -> (adv, ret) f32[B, L]; baseline f32[B]."""
+    _dev(r, mask, baseline)
+    _dt(r, torch.float32, "token_level_rewards")
+    _dt(baseline, torch.float32, "reward_baselines")
+    B, L = _rows(r, mask, names=("response_mask",))
+    if baseline.dim() != 1 or baseline.shape[0] != B:
+        raise ValueError(f"reward_baselines must be [B={B}], got {tuple(baseline.shape)}")
+    m = _mask_u8(mask).contiguous()
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    check(lib().rmi_remax(_ptr(r), _ptr(m), _ptr(baseline), B, L, _ptr(adv), _ptr(ret), _stream(r.device)),
+          "rmi_remax")
+    return adv, ret
+
+
+def rloo_outcome(r, mask, seg):
+    """verl compute_rloo_outcome_advantage over contiguous row groups seg -> (adv, ret)."""
+    _dev(r, mask)
+    _dt(r, torch.float32, "token_level_rewards")
+    B, L = _rows(r, mask, names=("response_mask",))
+    seg = segments(seg, B, r.device)
+    if seg.device != r.device:
+        raise ValueError("seg must be on the rows' device")
+    m = _mask_u8(mask).contiguous()
+    adv = torch.empty_like(r)
+    ret = torch.empty_like(r)
+    check(lib().rmi_rloo_outcome(_ptr(r), _ptr(m), B, L, _ptr(seg), seg.numel() - 1, _ptr(adv), _ptr(ret),
+                                 _stream(r.device)), "rmi_rloo_outcome")
+    return adv, ret
+
+
+def mask_mul_(x, mask):
+    """x *= (mask != 0) in place (f32), the `* response_mask` after verl's masked_whiten."""
+    _dev(x, mask)
+    _dt(x, torch.float32, "values")
+    if x.shape != mask.shape:
+        raise ValueError(f"mask must match x {tuple(x.shape)}, got {tuple(mask.shape)}")
+    m = _mask_u8(mask).contiguous()
+    check(lib().rmi_mask_mul(_ptr(x), _ptr(m), x.numel(), _stream(x.device)), "rmi_mask_mul")
+    return x
+
+
 def segments(seg, B: int, device) -> torch.Tensor:
     """Contiguous group segments as i32[G+1] on `device`.  Host segments (list / numpy / CPU
     tensor) are validated (seg[0] == 0, non-decreasing, seg[-1] == B) before the upload; a

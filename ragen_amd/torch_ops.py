@@ -455,6 +455,50 @@ def _(r, mask, seg, eps, norm_by_std):
     return torch.empty_like(r), torch.empty_like(r)
 
 
+@_op("reinforce_pp_returns", ("row_stats",))
+def reinforce_pp_returns(r: Tensor, mask: Tensor, gamma: float, row_stats: Optional[Tensor]) -> Tuple[Tensor, Tensor]:
+    """verl compute_reinforce_plus_plus_outcome_advantage before its whitening (adv = ret)."""
+    return ops.reinforce_pp_returns(r, mask, gamma, row_stats)
+
+
+@reinforce_pp_returns.register_fake
+def _(r, mask, gamma, row_stats):
+    return torch.empty_like(r), torch.empty_like(r)
+
+
+@_op("remax")
+def remax(r: Tensor, mask: Tensor, baseline: Tensor) -> Tuple[Tensor, Tensor]:
+    """verl compute_remax_outcome_advantage."""
+    return ops.remax(r, mask, baseline)
+
+
+@remax.register_fake
+def _(r, mask, baseline):
+    return torch.empty_like(r), torch.empty_like(r)
+
+
+@_op("rloo_outcome")
+def rloo_outcome(r: Tensor, mask: Tensor, seg: Tensor) -> Tuple[Tensor, Tensor]:
+    """verl compute_rloo_outcome_advantage over contiguous row groups seg i32[G+1] (device)."""
+    return ops.rloo_outcome(r, mask, seg)
+
+
+@rloo_outcome.register_fake
+def _(r, mask, seg):
+    return torch.empty_like(r), torch.empty_like(r)
+
+
+@_op("mask_mul_", ("x",))
+def mask_mul_(x: Tensor, mask: Tensor) -> None:
+    """x *= (mask != 0) in place."""
+    ops.mask_mul_(x, mask)
+
+
+@mask_mul_.register_fake
+def _(x, mask):
+    return None
+
+
 # ============================================================= text boundary (§8(f) 2)
 def _glyphs(glyph_bytes: List[int], glyph_len: List[int]):
     import numpy as np

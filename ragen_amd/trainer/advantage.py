@@ -26,8 +26,9 @@ def compute_response_mask(data: DataProto) -> torch.Tensor:
 
 def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_repeat=1, multi_turn=False,
                       norm_adv_by_std_in_grpo=True, bi_level_gae=False, high_level_gamma=1.0):
-    """agent_trainer.py:60-137 for the estimators of RAGEN's StarPO loop (GAE, bi-level GAE,
-    GRPO).  REINFORCE++/REMAX/RLOO are verl estimators outside this engine's scope."""
+    """agent_trainer.py:60-137: GAE (verl, or RAGEN's bi-level), GRPO, REINFORCE++ (and its
+    baseline form), REMAX and RLOO, each on the engine's kernels; an unknown estimator raises
+    NotImplementedError as the reference does."""
     if "response_mask" not in data.batch:
         data.batch["response_mask"] = compute_response_mask(data)
     est = getattr(adv_estimator, "value", adv_estimator)
@@ -46,8 +47,20 @@ def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_re
         adv, ret = core_algos.compute_grpo_outcome_advantage(data.batch["token_level_rewards"], mask,
                                                              data.non_tensor_batch["uid"],
                                                              norm_adv_by_std_in_grpo=norm_adv_by_std_in_grpo)
+    elif est == AdvantageEstimator.REINFORCE_PLUS_PLUS_BASELINE:
+        adv, ret = core_algos.compute_reinforce_plus_plus_baseline_outcome_advantage(
+            data.batch["token_level_rewards"], data.batch["response_mask"], data.non_tensor_batch["uid"])
+    elif est == AdvantageEstimator.REINFORCE_PLUS_PLUS:
+        adv, ret = core_algos.compute_reinforce_plus_plus_outcome_advantage(
+            data.batch["token_level_rewards"], data.batch["response_mask"], gamma)
+    elif est == AdvantageEstimator.REMAX:
+        adv, ret = core_algos.compute_remax_outcome_advantage(
+            data.batch["token_level_rewards"], data.batch["reward_baselines"], data.batch["response_mask"])
+    elif est == AdvantageEstimator.RLOO:
+        adv, ret = core_algos.compute_rloo_outcome_advantage(
+            data.batch["token_level_rewards"], data.batch["response_mask"], data.non_tensor_batch["uid"])
     else:
-        raise NotImplementedError(f"advantage estimator {est!r} is not part of the StarPO hot path")
+        raise NotImplementedError
     data.batch["advantages"] = adv
     data.batch["returns"] = ret
     return data

@@ -89,13 +89,9 @@ def compute_bi_level_gae_advantage_return(token_level_rewards, values, loss_mask
     return tuple(_back(token_level_rewards.device, [adv, ret], status, err))
 
 
-def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6,
-                                   norm_adv_by_std_in_grpo: bool = True):
-    """verl compute_grpo_outcome_advantage: rows grouped by ``index`` (any hashable ids).
-    Groups are rank-local under sharding (RAGEN's uids are unique per row, so every group has
-    one member, agent_trainer.py:551-552)."""
-    dev = _device(token_level_rewards, response_mask)
-    r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
+def _grouped(r, m, index, dev, run):
+    """Rows grouped by ``index`` (any hashable ids, first-seen order, as verl's id2score dict):
+    permute to contiguous groups if needed, run(rows, mask, seg) -> adv, scatter back."""
     groups = OrderedDict()
     for i, k in enumerate(index):
         groups.setdefault(k, []).append(i)
@@ -106,11 +102,73 @@ def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, ep
     p = None if ident else torch.from_numpy(perm).to(dev)
     rr = r if ident else r[p].contiguous()
     mm = m if ident else m[p].contiguous()
-    adv, _ = torch.ops.ragen_amd.grpo_outcome(rr, mm, ops.segments(seg, rr.shape[0], dev), float(epsilon),
-                                              bool(norm_adv_by_std_in_grpo))
+    adv = run(rr, mm, ops.segments(seg, rr.shape[0], dev))
     if not ident:
         out = torch.empty_like(adv)
         out[p] = adv
         adv = out
+    return adv
+
+
+def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6,
+                                   norm_adv_by_std_in_grpo: bool = True):
+    """verl compute_grpo_outcome_advantage: rows grouped by ``index`` (any hashable ids).
+    Groups are rank-local under sharding (RAGEN's uids are unique per row, so every group has
+    one member, agent_trainer.py:551-552)."""
+    dev = _device(token_level_rewards, response_mask)
+    r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
+    adv = _grouped(r, m, index, dev, lambda rr, mm, seg: torch.ops.ragen_amd.grpo_outcome(
+        rr, mm, seg, float(epsilon), bool(norm_adv_by_std_in_grpo))[0])
     adv = _back(token_level_rewards.device, [adv])[0]
     return adv, adv
+
+
+# The verl estimators agent_trainer.compute_advantage dispatches to besides GAE / GRPO
+# (agent_trainer.py:102-134).  verl is an empty submodule in the reference: restated from
+# verl's published core_algos (the v0.3 line RAGEN pins through vllm 0.8.2); parity unpinned
+# beyond that restatement (tests/verl_restated.py runs it on CPU torch as the checker).
+
+def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, gamma):
+    """verl: returns = right-to-left running = r + gamma * running, reset by the mask;
+    advantages = masked_whiten(returns, mask) * mask."""
+    dev = _device(token_level_rewards, response_mask)
+    r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
+    stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
+    adv, ret = torch.ops.ragen_amd.reinforce_pp_returns(r, m, float(gamma), stats)
+    status = _whiten(adv, m, stats)
+    torch.ops.ragen_amd.mask_mul_(adv, m)
+    return tuple(_back(token_level_rewards.device, [adv, ret], status))
+
+
+def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, response_mask, index,
+                                                           epsilon: float = 1e-6):
+    """verl: score = sum_t r minus its group's mean (0 for a single-row group), tiled over the
+    mask, then masked_whiten(., mask) * mask.  -> (adv, adv)."""
+    dev = _device(token_level_rewards, response_mask)
+    r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
+    adv = _grouped(r, m, index, dev, lambda rr, mm, seg: torch.ops.ragen_amd.grpo_outcome(
+        rr, mm, seg, float(epsilon), False)[0])
+    stats = torch.ops.ragen_amd.whiten_row_stats(adv, m)
+    status = _whiten(adv, m, stats)
+    torch.ops.ragen_amd.mask_mul_(adv, m)
+    adv = _back(token_level_rewards.device, [adv], status)[0]
+    return adv, adv
+
+
+def compute_rloo_outcome_advantage(token_level_rewards, response_mask, index, epsilon: float = 1e-6):
+    """verl: leave-one-out baseline, s * n/(n-1) - mean * n/(n-1) for groups of n > 1, tiled
+    over the mask.  -> (adv, adv)."""
+    dev = _device(token_level_rewards, response_mask)
+    r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
+    adv = _grouped(r, m, index, dev, lambda rr, mm, seg: torch.ops.ragen_amd.rloo_outcome(rr, mm, seg)[0])
+    adv = _back(token_level_rewards.device, [adv])[0]
+    return adv, adv
+
+
+def compute_remax_outcome_advantage(token_level_rewards, reward_baselines, response_mask):
+    """verl: returns = reverse cumsum of r * mask; advantages = returns - baseline * mask."""
+    dev = _device(token_level_rewards, reward_baselines, response_mask)
+    r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
+    b = _dev(reward_baselines.float(), dev)
+    adv, ret = torch.ops.ragen_amd.remax(r, m, b)
+    return tuple(_back(token_level_rewards.device, [adv, ret]))

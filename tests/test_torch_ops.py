@@ -13,7 +13,7 @@ R = torch.ops.ragen_amd
 MUTATING = {"sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_reset",
             "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
             "frozenlake_reset", "bandit_step_turn", "countdown_step_turn", "rollout_finalize", "masked_whiten_",
-            "masked_whiten_stats_", "gae", "bilevel_gae"}
+            "masked_whiten_stats_", "gae", "bilevel_gae", "reinforce_pp_returns", "mask_mul_"}
 
 
 def test_every_device_entry_point_is_an_op():
@@ -24,7 +24,8 @@ def test_every_device_entry_point_is_an_op():
             "frozenlake_reset", "frozenlake_render", "bandit_step_turn", "countdown_step_turn", "countdown_reward",
             "rollout_metrics", "trajectory_scores", "rollout_finalize", "group_normalize", "filter_groups", "row_sum",
             "masks_and_scores", "gae", "bilevel_gae", "masked_whiten_", "masked_whiten_stats_", "whiten_row_stats",
-            "grpo_outcome", "detokenize", "parse_actions", "pcg64_seed"}
+            "grpo_outcome", "detokenize", "parse_actions", "pcg64_seed", "reinforce_pp_returns", "remax",
+            "rloo_outcome", "mask_mul_"}
     assert want <= names, want - names
     for n in MUTATING:  # the schema names what an op writes in place
         assert "!" in str(getattr(R, n).default._schema), n
@@ -51,6 +52,9 @@ def test_fake_kernels_shapes():
         assert R.whiten_row_stats(r, m).shape == (B, 3)
         seg = torch.empty(B + 1, dtype=torch.int32, device=d)
         assert R.grpo_outcome(r, m, seg, 1e-6, True)[0].shape == (B, L)
+        assert R.rloo_outcome(r, m, seg)[1].shape == (B, L)
+        assert R.reinforce_pp_returns(r, m, 0.99, None)[0].shape == (B, L)
+        assert R.remax(r, m, torch.empty(B, device=d))[1].dtype == torch.float32
         assert R.row_sum(r).shape == (B,)
         keep, met, sd, mx, mn = R.filter_groups(torch.empty(64, device=d), 4, 16, 0.25, 0)
         assert keep.shape == (4,) and keep.dtype == torch.uint8 and met.shape == (6,)
