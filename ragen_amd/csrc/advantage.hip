@@ -26,6 +26,7 @@
 // the serial walk the only long per-wave chain and puts 2 waves on every SIMD; at 8192 x
 // 1093 tokens the kernel streams ~4.8 TB/s (HBM-bound).  Algorithmic traffic 17 B/token.
 #include <math.h>
+#include <stdlib.h>
 
 #include "common.hpp"
 
@@ -52,15 +53,6 @@ struct __attribute__((packed, aligned(1))) U8x4 {
   uint32_t x;
 };
 
-// One tile = rows [row0, row0+32) x columns [c0, c0+64) of r, v, mask, as 4-column groups:
-// lane l, slot j -> row 4j + l/16, columns c0 + 4*(l%16) .. +3 (256-B coalesced row segments).
-// Columns >= L and rows >= B read as zeros (a zero tail is an exact no-op for the recurrence:
-// it starts the walk at column L-1 with last = nv = 0).
-struct GaeTile {
-  F4 r[kGLoads], v[kGLoads];
-  uint32_t m[kGLoads];
-};
-
 // Mask bytes -> 0x01 per nonzero byte: a mask is a boolean (RAGEN passes a bool loss_mask,
 // ctx_manager.py:46-49), so any nonzero byte counts as 1 in the recurrence, the whitening
 // count and the sums alike.
@@ -71,6 +63,21 @@ __device__ __forceinline__ uint32_t nz8(uint32_t x) {
   return x & 0x01010101u;
 }
 
+// One tile = rows [row0, row0+32) x columns [c0, c0+64) of r, v, mask, as 4-column groups:
+// lane l, slot j -> row 4j + l/16, columns c0 + 4*(l%16) .. +3 (256-B coalesced row segments).
+// Columns >= L and rows >= B read as zeros (a zero tail is an exact no-op for the recurrence:
+// it starts the walk at column L-1 with last = nv = 0).
+// m holds the raw mask words: they are normalised (nz8(m | mor)) where they are used, not
+// where they are loaded — consuming a load right after issuing it would make the compiler wait
+// for every load in flight (s_waitcnt vmcnt(0)) and drain the tile pipeline.  mor = 0x01010101
+// without a mask (every column counts), else 0.
+struct GaeTile {
+  F4 r[kGLoads], v[kGLoads];
+  uint32_t m[kGLoads];
+  uint32_t mor;
+  __device__ __forceinline__ uint32_t mask(int j) const { return nz8(m[j] | mor); }
+};
+
 __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restrict__ r, const float* __restrict__ v,
                                               const uint8_t* __restrict__ mask, int64_t B, int64_t L, int64_t row0,
                                               int64_t c0, int lane) {
@@ -78,6 +85,7 @@ __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restric
   const int64_t col = c0 + 4 * g;
   const bool dummy = c0 < 0;  // a pipeline slot past column 0: every lane reads one shared line
   const bool full_col = col + 4 <= L && !dummy;
+  t.mor = mask ? 0u : 0x01010101u;
   // 1. every full 4-column group, branch-free from clamped (always valid) addresses, so all
   //    loads of the tile are in flight together; invalid groups are zeroed when staged
 #pragma unroll
@@ -86,7 +94,7 @@ __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restric
     const int64_t o = dummy ? min<int64_t>(row0, B - 1) * L : (full_col ? row * L + col : row * L);
     t.r[j] = *reinterpret_cast<const F4*>(r + o);
     t.v[j] = *reinterpret_cast<const F4*>(v + o);
-    t.m[j] = mask ? nz8(reinterpret_cast<const U8x4*>(mask + o)->x) : 0x01010101u;
+    t.m[j] = reinterpret_cast<const U8x4*>((mask ? mask : reinterpret_cast<const uint8_t*>(r)) + o)->x;
   }
   // 2. the ragged group at a row end (L % 4 != 0: one group per row, in one tile) and rows
   //    past B, element by element, never past the row
@@ -181,7 +189,7 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, co
       const int row = 4 * j + (lane >> 4), grp = lane & 15;
       *reinterpret_cast<F4*>(sr + row * kGStr + 4 * grp) = t.r[j];
       *reinterpret_cast<F4*>(sv + row * kGStr + 4 * grp) = t.v[j];
-      *reinterpret_cast<uint32_t*>(sm + row * kGMStr + 4 * grp) = t.m[j];
+      *reinterpret_cast<uint32_t*>(sm + row * kGMStr + 4 * grp) = t.mask(j);
     }
     __syncthreads();
     if (k > 0) gae_load_tile(t, r, v, mask, B, L, row0, c0 - kGCols, lane);
@@ -323,7 +331,7 @@ __device__ __forceinline__ void gae_legacy_tile(const GaeTile& cur, int64_t c0, 
     const F4 a4 = *reinterpret_cast<const F4*>(sd + row * kGStr + 4 * grp);
     const F4 v4 = cur.v[j];
     const F4 t4 = F4{a4.x + v4.x, a4.y + v4.y, a4.z + v4.z, a4.w + v4.w};
-    const uint32_t m4 = cur.m[j];
+    const uint32_t m4 = cur.mask(j);
     const double ax = (m4 & 0xFF) ? (double)a4.x : 0.0, ay = ((m4 >> 8) & 0xFF) ? (double)a4.y : 0.0;
     const double az = ((m4 >> 16) & 0xFF) ? (double)a4.z : 0.0, aw = (m4 >> 24) ? (double)a4.w : 0.0;
     st.s1[j] += (ax + ay) + (az + aw);
@@ -466,7 +474,7 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
   BL_T(t0);
   const int grp = lane & 15, rho = lane >> 4;
   const F4 r4 = cur.r[0], v4 = cur.v[0];
-  const uint32_t m4 = cur.m[0];
+  const uint32_t m4 = cur.mask(0);
   const float rr[4] = {r4.x, r4.y, r4.z, r4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
   uint32_t valid[4], eos[4];
 #pragma unroll
@@ -677,6 +685,333 @@ __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restri
   }
 }
 
+// ---- Bi-level GAE, segment-parallel (rows of up to kBsMaxCols columns; longer rows take
+// bilevel_tiled_kernel above).  The low-level walk restarts at every valid eos column
+// (core_algos.py:81-84: lastgaelam = 0.0 there), so after the high-level pass a row's
+// low-level recurrence is independent per *segment* — the valid columns from one segment
+// start (a valid eos column, or the rightmost valid column when it is not one) leftwards up to
+// the next start.  The tiled kernel walks a row's segments one after another on one lane per
+// row; here the whole row's deltas stay in LDS and every segment gets its own lane (16 per
+// row), each walking its columns in the reference's order, so each element's f32 operations
+// and operands are unchanged (bit-identical) while a wave's walk takes its longest segment
+// instead of its longest row.
+//   tile loop (right to left, the 3-deep register pipeline):  P1 column-parallel deltas and
+//     flags into the row buffer, segment starts appended to a per-row list (DPP suffix count),
+//     P2 the serial high-level walk over the tile's eos columns (as in the tiled kernel);
+//   P3 the segment walks (a wave with more than kBsSeg starts in a row walks each row serially,
+//     one lane per row, over the same buffer);
+//   P4 column-parallel outputs and fp64 row stats (v re-read: an L2 hit, the row was read
+//     microseconds before).
+// LDS per wave: D f32[4][Lr], F u8[4][Lr/4] (valid nibble | eos nibble << 4 per 4-column
+// group), S u16[4][kBsSeg], the tile's v staging, VG u16[4][tiles] (groups holding a valid
+// column); at L = 1107 this is 20 KB (8 waves per CU).
+constexpr int kBsSeg = 48;
+#ifndef RMI_BS_PIPE
+#define RMI_BS_PIPE 6
+#endif
+constexpr int kBsPipe = RMI_BS_PIPE;
+constexpr int64_t kBsMaxLds = 65536;
+
+__host__ __device__ inline int64_t bs_lr(int64_t L) { return (L + 3) & ~(int64_t)3; }
+__host__ __device__ inline int64_t bs_foff(int64_t Lr) { return (int64_t)kGRows * Lr * 4; }
+__host__ __device__ inline int64_t bs_soff(int64_t Lr) { return bs_foff(Lr) + (((int64_t)kGRows * (Lr / 4) + 15) & ~15); }
+__host__ __device__ inline int64_t bs_voff(int64_t Lr) { return bs_soff(Lr) + (int64_t)kGRows * kBsSeg * 2; }
+__host__ __device__ inline int64_t bs_nt(int64_t Lr) { return ((Lr + 63) / 64 + 1) & ~(int64_t)1; }  // VG words per row
+__host__ __device__ inline int64_t bs_goff(int64_t Lr) { return bs_voff(Lr) + (int64_t)kGRows * kBStr * 4; }
+__host__ __device__ inline int64_t bs_lds_bytes(int64_t L) {
+  return bs_goff(bs_lr(L)) + (int64_t)kGRows * bs_nt(bs_lr(L)) * 2;
+}
+
+// inclusive suffix sum over the 16 groups of a DPP row (group g <- sum of groups >= g)
+__device__ __forceinline__ int row_suffix_sum(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x101, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x102, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x104, 0xF, 0xF, true);
+  x += __builtin_amdgcn_update_dpp(0, x, 0x108, 0xF, 0xF, true);
+  return x;
+}
+
+__device__ __forceinline__ void bs_tile(const GaeTile& cur, int64_t c0, BilevelCarry& cy, float& hl, int& nseg,
+                                        uint32_t& bad, float* __restrict__ D, uint8_t* __restrict__ F,
+                                        uint16_t* __restrict__ S, float* __restrict__ sv, uint16_t* __restrict__ VG,
+                                        int64_t Lr, int lane, float g, float hg, float hgl) {
+  const int grp = lane & 15, rho = lane >> 4;
+  const F4 r4 = cur.r[0], v4 = cur.v[0];
+  const uint32_t m4 = cur.mask(0);
+  const float rr[4] = {r4.x, r4.y, r4.z, r4.w}, vv[4] = {v4.x, v4.y, v4.z, v4.w};
+  uint32_t valid[4], eos[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    valid[e] = ((m4 >> (8 * e)) & 0xFFu) != 0;
+    eos[e] = rr[e] != 0.0f || rr[e] != rr[e];  // token_level_rewards.bool()
+  }
+  // ---- P1: as bilevel_tile (next valid / next eos values by DPP suffix selection + carry)
+  uint32_t hv = 0, he = 0;
+  float fv = 0.0f, fe = 0.0f;
+#pragma unroll
+  for (int e = 3; e >= 0; --e) {
+    fv = valid[e] ? vv[e] : fv;
+    hv |= valid[e];
+    fe = eos[e] ? vv[e] : fe;
+    he |= eos[e];
+  }
+  uint32_t hsv = hv, hse = he;
+  float vsv = fv, vse = fe;
+  row_suffix_first(hsv, vsv);
+  row_suffix_first(hse, vse);
+  uint32_t nhv = hsv, nhe = hse;
+  float nvv = vsv, nve = vse;
+  row_shift_left1(nhv, nvv);
+  row_shift_left1(nhe, nve);
+  nvv = nhv ? nvv : cy.v_valid;
+  nhv |= cy.h_valid;
+  nve = nhe ? nve : cy.v_eos;
+  nhe |= cy.h_eos;
+  float d[4];
+  uint32_t fl = 0, st = 0;
+#pragma unroll
+  for (int e = 3; e >= 0; --e) {
+    if (eos[e]) d[e] = (rr[e] + (nhe ? hg * nve : 0.0f)) - vv[e];  // high-level delta
+    else d[e] = (rr[e] + g * (nhv ? nvv : 0.0f)) - vv[e];           // low level (upd = reward)
+    bad |= valid[e] & (eos[e] ^ 1u) & (nhv ^ 1u);                    // valid_positions[i + 1]
+    st |= (valid[e] & (eos[e] | (nhv ^ 1u))) << e;                   // segment start
+    fl |= (valid[e] << e) | (eos[e] << (4 + e));
+    nvv = valid[e] ? vv[e] : nvv;
+    nhv |= valid[e];
+    nve = eos[e] ? vv[e] : nve;
+    nhe |= eos[e];
+  }
+  const int lead = lane & ~15;
+  const uint32_t row_hv = (uint32_t)__shfl((int)hsv, lead), row_he = (uint32_t)__shfl((int)hse, lead);
+  const float row_vv = __shfl(vsv, lead), row_ve = __shfl(vse, lead);
+  cy.v_valid = row_hv ? row_vv : cy.v_valid;
+  cy.h_valid |= row_hv;
+  cy.v_eos = row_he ? row_ve : cy.v_eos;
+  cy.h_eos |= row_he;
+  const int64_t col = c0 + 4 * grp;
+  float* Dr = D + rho * Lr;
+  if (col < Lr) {
+    *reinterpret_cast<F4*>(Dr + col) = F4{d[0], d[1], d[2], d[3]};
+    F[rho * (Lr / 4) + (col >> 2)] = (uint8_t)fl;
+  }
+  *reinterpret_cast<F4*>(sv + rho * kBStr + 4 * grp) = v4;
+  // segment starts, right to left: this group's rank = starts in the row's groups to its right
+  const int ns = __popc(st);
+  const int incl = row_suffix_sum(ns);
+  const int tot = __shfl(incl, lead);
+  int idx = nseg + incl - ns;
+#pragma unroll
+  for (int e = 3; e >= 0; --e) {
+    if ((st >> e) & 1u) {
+      if (idx < kBsSeg) S[rho * kBsSeg + idx] = (uint16_t)(col + e);
+      ++idx;
+    }
+  }
+  nseg += tot;
+  const uint64_t any_eos = __ballot(he), any_valid = __ballot(hv);
+  if (grp == 0) VG[rho * bs_nt(Lr) + (c0 >> 6)] = (uint16_t)((any_valid >> (16 * rho)) & 0xFFFFu);
+  __syncthreads();
+  // ---- P2: the row's high-level walk over this tile's eos columns (group-0 lanes)
+  if (grp == 0) {
+    const uint8_t* Fr = F + rho * (Lr / 4) + (c0 >> 2);
+    const float* pv = sv + rho * kBStr;
+    float* pd = Dr + c0;
+    uint32_t ge = (uint32_t)(any_eos >> (16 * rho)) & 0xFFFFu;
+    while (ge) {
+      const int q = 31 - __clz(ge);
+      ge &= ~(1u << q);
+      const uint32_t f = Fr[q];
+#pragma unroll
+      for (int e = 3; e >= 0; --e) {
+        if ((f >> (4 + e)) & 1u) {
+          const int c = 4 * q + e;
+          hl = pd[c] + hgl * hl;
+          const float vt = pv[c], upd = hl + vt;  // updated_reward = returns = advantages + values
+          pd[c] = ((f >> e) & 1u) ? (upd + g * 0.0f) - vt : hl;  // valid: its low-level delta
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// One segment's low-level walk: valid columns from s leftwards while > end, in the
+// reference's order (ll = d + gl * (eos ? 0 : ll), the reset at a valid eos, core_algos.py:81-88).
+// Branch-free over the segment's 4-column groups: the next group's flag byte and deltas are
+// read before this one is worked on, every column is computed and a column outside the segment
+// (mask 0, or owned by the neighbouring segment in a shared group) keeps its value and the
+// chain, and its store goes to the lane's dummy slot — so the loop body has no divergent
+// branch and no read-modify-write of a neighbour's column.
+__device__ __forceinline__ void bs_walk(float* __restrict__ Dr, const uint8_t* __restrict__ Fr,
+                                        float* __restrict__ dummy, int s, int end, float gl) {
+  float ll = 0.0f;
+  const int qs = s >> 2, qe = (end + 1) >> 2;
+  const uint32_t ms = (2u << (s & 3)) - 1u, me = ~((1u << ((end + 1) & 3)) - 1u) & 0xFu;
+  uint32_t f = Fr[qs];
+  float4 d4 = *reinterpret_cast<const float4*>(Dr + 4 * qs);
+  for (int q = qs; q >= qe; --q) {
+    const int qn = q > qe ? q - 1 : q;
+    const uint32_t fn = Fr[qn];
+    const float4 dn = *reinterpret_cast<const float4*>(Dr + 4 * qn);
+    uint32_t vm = f & (q == qs ? ms : 0xFu);
+    vm &= q == qe ? me : 0xFu;
+    const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+    for (int e = 3; e >= 0; --e) {
+      const float nl = dd[e] + gl * (((f >> (4 + e)) & 1u) ? 0.0f : ll);
+      const bool in = (vm >> e) & 1u;
+      ll = in ? nl : ll;
+      *(in ? Dr + 4 * q + e : dummy) = nl;
+    }
+    f = fn;
+    d4 = dn;
+  }
+}
+
+// v groups c0, c0 + 64, ..., c0 + 7 * 64 of one row (zeros past L; the ragged group at L % 4)
+__device__ __forceinline__ void bs_load_v(F4 (&vq)[8], const float* __restrict__ vrow, int64_t c0, int64_t L) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int64_t c = c0 + (int64_t)u * kGCols;
+    vq[u] = F4{0.f, 0.f, 0.f, 0.f};
+    if (c + 4 <= L) {
+      vq[u] = *reinterpret_cast<const F4*>(vrow + c);
+    } else if (c < L) {
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int e = 0; e < 4; ++e)
+        if (c + e < L) t[e] = vrow[c + e];
+      vq[u] = F4{t[0], t[1], t[2], t[3]};
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict__ r, const float* __restrict__ v,
+                                                         const uint8_t* __restrict__ mask, int64_t B, int64_t L,
+                                                         float g, float gl, float hg, float hgl,
+                                                         float* __restrict__ adv, float* __restrict__ ret,
+                                                         double* __restrict__ row_stats, uint8_t* __restrict__ err) {
+  static_assert(kGLoads == 1 && kGRows * 16 == 64, "one 4-column group per lane");
+  extern __shared__ __attribute__((aligned(16))) uint8_t bs_smem[];
+  const int64_t Lr = bs_lr(L);
+  float* D = reinterpret_cast<float*>(bs_smem);
+  uint8_t* F = bs_smem + bs_foff(Lr);
+  uint16_t* S = reinterpret_cast<uint16_t*>(bs_smem + bs_soff(Lr));
+  float* sv = reinterpret_cast<float*>(bs_smem + bs_voff(Lr));
+  uint16_t* VG = reinterpret_cast<uint16_t*>(bs_smem + bs_goff(Lr));
+  const int lane = threadIdx.x, grp = lane & 15, rho = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * kGRows;
+  const int64_t ntiles = (L + kGCols - 1) / kGCols;
+  BilevelCarry cy{0.0f, 0.0f, 0u, 0u};
+  float hl = 0.0f;
+  int nseg = 0;
+  uint32_t bad = 0;
+  BL_T(tb0);
+  // kBsPipe register tiles, kBsPipe - 1 loads in flight behind the tile being worked on: the
+  // tile work here is short (the walks come later), so the loads need the deeper pipeline
+  GaeTile tq[kBsPipe];
+  const int64_t k0 = ntiles - 1;
+#pragma unroll
+  for (int u = 0; u < kBsPipe - 1; ++u) gae_load_tile(tq[u], r, v, mask, B, L, row0, (k0 - u) * kGCols, lane);
+  for (int64_t k = k0; k >= 0; k -= kBsPipe) {
+#pragma unroll
+    for (int u = 0; u < kBsPipe; ++u) {
+      if (k - u < 0) break;
+      gae_load_tile(tq[(u + kBsPipe - 1) % kBsPipe], r, v, mask, B, L, row0, (k - u - (kBsPipe - 1)) * kGCols, lane);
+      bs_tile(tq[u], (k - u) * kGCols, cy, hl, nseg, bad, D, F, S, sv, VG, Lr, lane, g, hg, hgl);
+    }
+  }
+  BL_T(tb1);
+  const int64_t grow = row0 + rho;
+  const bool live = grow < B;
+  const float* vrow = v + (live ? grow : B - 1) * L;
+  // ---- P3: segment walks
+  float* Dr = D + rho * Lr;
+  const uint8_t* Fr = F + rho * (Lr / 4);
+  const uint16_t* Sr = S + rho * kBsSeg;
+  const uint16_t* VGr = VG + rho * bs_nt(Lr);
+  float* dummy = sv + lane;  // the tile staging is free now: one scratch slot per lane
+  // the row's leftmost valid column bounds its last segment (the prompt and the left padding
+  // to its left hold no valid column)
+  int clo = 0;
+  if (nseg > 0) {
+    int tl = 0;
+    while (VGr[tl] == 0) ++tl;
+    const int ql = 16 * tl + __builtin_ctz((uint32_t)VGr[tl]);
+    clo = 4 * ql + __builtin_ctz((uint32_t)Fr[ql] & 0xFu);
+  }
+  if (!__any(nseg > kBsSeg)) {
+    for (int j = grp; j < nseg; j += 16)
+      bs_walk(Dr, Fr, dummy, Sr[j], j + 1 < nseg ? (int)Sr[j + 1] : clo - 1, gl);
+  } else if (grp == 0 && nseg > 0) {
+    bs_walk(Dr, Fr, dummy, Sr[0], clo - 1, gl);  // the row's whole walk on one lane (the same element order)
+  }
+  __syncthreads();
+  BL_T(tb2);
+  // ---- P4: outputs and row stats; v re-read (an L2 hit) 8 tiles' groups at a time
+  double s1 = 0.0, s2 = 0.0, cnt = 0.0;
+  for (int64_t cb = 4 * grp; cb < L; cb += 8 * kGCols) {
+    F4 cur[8];
+    bs_load_v(cur, vrow, cb, L);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t c = cb + (int64_t)u * kGCols;
+      if (c >= L) break;
+      const F4 a4 = *reinterpret_cast<const F4*>(Dr + c);
+      const uint32_t f = Fr[c >> 2];
+      const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, vv[4] = {cur[u].x, cur[u].y, cur[u].z, cur[u].w};
+      float oa[4], oq[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if ((f >> e) & 1u) {  // valid: the low-level walk
+          oa[e] = aa[e];
+          oq[e] = aa[e] + vv[e];
+          s1 += (double)aa[e];
+          s2 += (double)aa[e] * (double)aa[e];
+          cnt += 1.0;
+        } else if ((f >> (4 + e)) & 1u) {  // eos outside the mask: the high level (ret = adv + v)
+          oa[e] = aa[e];
+          oq[e] = aa[e] + vv[e];
+        } else {
+          oa[e] = 0.0f;
+          oq[e] = 0.0f;
+        }
+      }
+      if (live) {
+        const int64_t go = grow * L + c;
+        if (c + 4 <= L) {
+          *reinterpret_cast<F4*>(adv + go) = F4{oa[0], oa[1], oa[2], oa[3]};
+          *reinterpret_cast<F4*>(ret + go) = F4{oq[0], oq[1], oq[2], oq[3]};
+        } else {
+          for (int e = 0; e < 4; ++e)
+            if (c + e < L) {
+              adv[go + e] = oa[e];
+              ret[go + e] = oq[e];
+            }
+        }
+      }
+    }
+  }
+  const double a = xor_sum16(s1), b2 = xor_sum16(s2), n = xor_sum16(cnt);
+  const uint64_t bads = __ballot(bad);
+#ifdef RMI_BL_STAMPS
+  BL_T(tb3);
+  if (lane == 0) {
+    g_bl_stamps[blockIdx.x * 4 + 0] = tb1 - tb0;
+    g_bl_stamps[blockIdx.x * 4 + 1] = tb2 - tb1;
+    g_bl_stamps[blockIdx.x * 4 + 2] = tb3 - tb2;
+    g_bl_stamps[blockIdx.x * 4 + 3] = tb3 - tb0;
+  }
+#endif
+  if (grp == 0 && live) {
+    if (row_stats) {
+      row_stats[3 * grow + 0] = a;
+      row_stats[3 * grow + 1] = b2;
+      row_stats[3 * grow + 2] = n;
+    }
+    if (err) err[grow] = ((bads >> (lane & ~15)) & 0xFFFFull) ? RMI_ERR_INDEX : 0;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void row_stats_kernel(const float* __restrict__ x,
                                                            const uint8_t* __restrict__ mask, int64_t B, int64_t L,
                                                            double* __restrict__ stats) {
@@ -824,6 +1159,13 @@ __global__ __launch_bounds__(kBlock) void grpo_kernel(const float* __restrict__ 
   }
 }
 
+// RAGEN_AMD_BILEVEL_TILED=1 routes every row length to bilevel_tiled_kernel (parity tests run
+// both kernels on the same rows; read per call so a test can flip it).
+bool bilevel_force_tiled() {
+  const char* s = getenv("RAGEN_AMD_BILEVEL_TILED");
+  return s && s[0] == '1';
+}
+
 }  // namespace
 }  // namespace rmi
 
@@ -857,9 +1199,16 @@ RMI_API int rmi_bilevel_gae(const float* r, const float* v, const uint8_t* mask,
   using namespace rmi;
   if (!r || !v || !mask || !adv || !ret || B < 0 || L < 0) return RMI_EINVAL;
   if (B == 0 || L == 0) return RMI_OK;
-  hipLaunchKernelGGL(bilevel_tiled_kernel, dim3((unsigned)((B + kGRows - 1) / kGRows)), dim3(64), 0,
-                     as_stream(stream), r, v, mask, B, L, (float)gamma, (float)(gamma * lam), (float)high_level_gamma,
-                     (float)(high_level_gamma * lam), adv, ret, row_stats, err);
+  const dim3 grid((unsigned)((B + kGRows - 1) / kGRows));
+  const float g = (float)gamma, gl = (float)(gamma * lam), hg = (float)high_level_gamma,
+              hgl = (float)(high_level_gamma * lam);
+  const int64_t lds = bs_lds_bytes(L);
+  if (lds <= kBsMaxLds && !bilevel_force_tiled())
+    hipLaunchKernelGGL(bilevel_seg_kernel, grid, dim3(64), (unsigned)lds, as_stream(stream), r, v, mask, B, L, g, gl,
+                       hg, hgl, adv, ret, row_stats, err);
+  else
+    hipLaunchKernelGGL(bilevel_tiled_kernel, grid, dim3(64), 0, as_stream(stream), r, v, mask, B, L, g, gl, hg, hgl,
+                       adv, ret, row_stats, err);
   return launch_status();
 }
 

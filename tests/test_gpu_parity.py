@@ -823,6 +823,43 @@ def test_bilevel_vs_oracle_large(device, B):
         np.testing.assert_array_equal(stats[:, 2].cpu().numpy(), m.sum(1).astype(np.float64))
 
 
+@pytest.mark.parametrize("B,L,p_eos,p_valid", [
+    (512, 700, 0.05, 0.6),   # ~20 segments per row: the segment-parallel walk
+    (512, 700, 0.4, 0.7),    # > 64 segment starts in most rows: the serial fallback walk
+    (300, 257, 0.02, 0.3),   # few segments, many rows without any (a tail segment: IndexError rows)
+    (64, 9001, 0.01, 0.5),   # a row too long for the LDS row buffer: bilevel_tiled_kernel
+])
+def test_bilevel_segment_walks_vs_oracle(device, monkeypatch, B, L, p_eos, p_valid):
+    """rmi_bilevel_gae's segment-parallel kernel and its tiled kernel (RAGEN_AMD_BILEVEL_TILED=1)
+    both equal the oracle bit for bit on rows the reference completes: rewards (eos) at random
+    columns inside and outside the mask, NaN-free, negative and -0.0 rewards among them."""
+    rng = np.random.default_rng(L)
+    r = np.where(rng.random((B, L)) < p_eos, rng.choice([0.5, -1.25, 3.0, -0.0], size=(B, L)), 0.0).astype(np.float32)
+    m = (rng.random((B, L)) < p_valid).astype(np.uint8)
+    v = rng.standard_normal((B, L)).astype(np.float32)
+    last = L - 1 - np.argmax(m[:, ::-1], axis=1)  # each row's last valid column: a turn end in 80 % of rows
+    pick = (rng.random(B) < 0.8) & (m.sum(1) > 0)
+    r[np.nonzero(pick)[0], last[pick]] = 1.5
+    rd, vd, md = _t(r, device), _t(v, device), _t(m, device)
+    for g, lam, hg in ((1.0, 1.0, 0.95), (0.99, 0.95, 0.9)):
+        oa, oret, oerr = oracle.bilevel_gae(r, v, m, g, lam, hg)
+        ok = oerr == 0
+        assert 0 < ok.sum() < B
+        for tiled in ("0", "1"):
+            monkeypatch.setenv("RAGEN_AMD_BILEVEL_TILED", tiled)
+            adv, ret = ops.bilevel_gae(rd, vd, md, g, lam, hg, check_errors=False)
+            np.testing.assert_array_equal(ret.cpu().numpy()[ok], oret[ok])
+            np.testing.assert_array_equal(adv.cpu().numpy()[ok], oa[ok])
+            stats = torch.empty(B, 3, dtype=torch.float64, device=device)
+            errs = torch.empty(B, dtype=torch.uint8, device=device)
+            assert ops.lib().rmi_bilevel_gae(ops._ptr(rd), ops._ptr(vd), ops._ptr(md), B, L, g, lam, hg, ops._ptr(adv),
+                                             ops._ptr(ret), ops._ptr(stats), ops._ptr(errs), ops._stream(device)) == 0
+            np.testing.assert_array_equal(errs.cpu().numpy() != 0, oerr != 0)
+            np.testing.assert_array_equal(stats[:, 2].cpu().numpy(), m.sum(1).astype(np.float64))
+            s1 = (oa.astype(np.float64) * m).sum(1)
+            np.testing.assert_allclose(stats[:, 0].cpu().numpy()[ok], s1[ok], rtol=1e-12, atol=1e-9)
+
+
 @pytest.mark.parametrize("B,frac_irregular,partial", [(8192, 0.0, False), (1000, 0.0, True), (2050, 0.3, False),
                                                        (16500, 0.3, True)])
 def test_fused_first_turn(device, B, frac_irregular, partial):

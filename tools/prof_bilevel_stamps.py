@@ -1,7 +1,10 @@
 """Where the time of one rmi_bilevel_gae launch goes (diagnostic, not product).  Builds
 advantage.hip with RMI_BL_STAMPS into tools/_build/libbilevel_stamps.so and prints each
 wave's mean cycles in P1 (incl. the tile load wait), the P2+P3 walk and P4, summed over its
-tiles, for the bench's bi-level rows (8192 rows, turn rewards at each turn's end)."""
+tiles, for the bench's bi-level rows (8192 rows, turn rewards at each turn's end).
+The segment-parallel kernel (the default at these row lengths) stamps its tile loop (P1+P2),
+the segment walks (P3) and the outputs (P4) instead; RAGEN_AMD_BILEVEL_TILED=1 selects the
+tiled kernel's stamps."""
 import ctypes, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
