@@ -1048,6 +1048,7 @@ __global__ __launch_bounds__(1024) void whiten_finalize_kernel(const double* __r
                                                                WhitenParams* __restrict__ out) {
   __shared__ double red[3][16];
   double s1 = 0, s2 = 0, c = 0;
+#pragma unroll 8  // the loads of 8 strides in flight together (the sums keep their order)
   for (int64_t i = threadIdx.x; i < B; i += 1024) {
     s1 += stats[3 * i];
     s2 += stats[3 * i + 1];
@@ -1112,6 +1113,31 @@ __global__ __launch_bounds__(kBlock) void mask_mul_kernel(float* __restrict__ x,
 // group mean/std in fp64, then the per-row score is broadcast over the row's mask.
 // mode 0: GRPO without std (also REINFORCE++-baseline's centred score), 1: GRPO, 2: RLOO
 // (n > 1: s * n / (n - 1) - mean * n / (n - 1) in the reference's f32 op order; n == 1: s).
+// Rows are read once: the first 64 row scores of a group stay in registers (lane i: row lo + i)
+// for the broadcast pass, which reads only the mask.  Each row is split at 4-element
+// boundaries of the flat index (a head and a tail of < 4 elements, one per lane, and a body
+// where a lane moves 4 columns with 16-B accesses), whatever L is; `vec` = the base pointers
+// allow it.
+struct GrpoSpan {
+  int64_t o, b0, b1, e;  // row start, body [b0, b1) (multiples of 4), row end
+};
+__device__ __forceinline__ GrpoSpan grpo_span(int64_t row, int64_t L, bool vec) {
+  const int64_t o = row * L, e = o + L;
+  int64_t b0 = vec ? (o + 3) & ~(int64_t)3 : e, b1 = vec ? e & ~(int64_t)3 : e;
+  if (b0 > b1) b0 = b1 = e;
+  return GrpoSpan{o, b0, b1, e};
+}
+__device__ __forceinline__ double grpo_row_sum(const float* __restrict__ r, const GrpoSpan& sp, int lane) {
+  double s = 0.0;
+  for (int64_t i = sp.o + lane; i < sp.b0; i += 64) s += (double)r[i];   // head (all of it without vec)
+  for (int64_t i = sp.b0 + 4 * lane; i < sp.b1; i += 256) {
+    const float4 x = *reinterpret_cast<const float4*>(r + i);
+    s += ((double)x.x + (double)x.y) + ((double)x.z + (double)x.w);
+  }
+  for (int64_t i = sp.b1 + lane; i < sp.e; i += 64) s += (double)r[i];   // tail
+  return wave_sum(s);
+}
+
 __global__ __launch_bounds__(kBlock) void grpo_kernel(const float* __restrict__ r, const uint8_t* __restrict__ mask,
                                                       int64_t B, int64_t L, const int32_t* __restrict__ seg, int G,
                                                       float eps, int norm_by_std, float* __restrict__ adv,
@@ -1121,15 +1147,16 @@ __global__ __launch_bounds__(kBlock) void grpo_kernel(const float* __restrict__ 
   if (g >= G) return;
   const int lo = seg[g], hi = seg[g + 1], n = hi - lo;
   if (n <= 0 || lo < 0 || hi > B) return;  // malformed segments are never read past [0, B)
+  const bool vec = ((reinterpret_cast<uintptr_t>(r) | reinterpret_cast<uintptr_t>(adv) |
+                     reinterpret_cast<uintptr_t>(ret)) & 15) == 0 && (reinterpret_cast<uintptr_t>(mask) & 3) == 0;
   // pass 1: group sums of row scores
   double gs = 0.0, gq = 0.0;
+  float kept = 0.0f;
   for (int row = lo; row < hi; ++row) {
-    double s = 0.0;
-    for (int64_t i = lane; i < L; i += 64) s += (double)r[row * L + i];
-    s = wave_sum(s);
-    const float sf = (float)s;
+    const float sf = (float)grpo_row_sum(r, grpo_span(row, L, vec), lane);
     gs += sf;
     gq += (double)sf * (double)sf;
+    kept = row - lo == lane ? sf : kept;
   }
   float mean = 0.0f, sd = 1.0f;
   if (n > 1) {
@@ -1140,21 +1167,32 @@ __global__ __launch_bounds__(kBlock) void grpo_kernel(const float* __restrict__ 
     sd = (float)sqrt(var);
   }
   for (int row = lo; row < hi; ++row) {
-    double s = 0.0;
-    for (int64_t i = lane; i < L; i += 64) s += (double)r[row * L + i];
-    s = wave_sum(s);
+    const GrpoSpan sp = grpo_span(row, L, vec);
+    const float sf = row - lo < 64 ? __shfl(kept, row - lo) : (float)grpo_row_sum(r, sp, lane);
     float sc;
     if (norm_by_std == 2) {
       const float fn = (float)n, fd = (float)(n - 1);
-      sc = n > 1 ? ((float)s * fn) / fd - (mean * fn) / fd : (float)s;
+      sc = n > 1 ? (sf * fn) / fd - (mean * fn) / fd : sf;
     } else {
-      sc = (float)s - mean;
+      sc = sf - mean;
       if (norm_by_std) sc = sc / (sd + eps);
     }
-    for (int64_t i = lane; i < L; i += 64) {
-      const float y = sc * (float)(mask[row * L + i] != 0);
-      adv[row * L + i] = y;
-      ret[row * L + i] = y;
+    for (int64_t i = sp.o + lane; i < sp.b0; i += 64) {
+      const float y = sc * (float)(mask[i] != 0);
+      adv[i] = y;
+      ret[i] = y;
+    }
+    for (int64_t i = sp.b0 + 4 * lane; i < sp.b1; i += 256) {
+      const uint32_t m4 = *reinterpret_cast<const uint32_t*>(mask + i);
+      const float4 y = make_float4(sc * (float)((m4 & 0xFFu) != 0), sc * (float)((m4 & 0xFF00u) != 0),
+                                   sc * (float)((m4 & 0xFF0000u) != 0), sc * (float)((m4 >> 24) != 0));
+      *reinterpret_cast<float4*>(adv + i) = y;
+      *reinterpret_cast<float4*>(ret + i) = y;
+    }
+    for (int64_t i = sp.b1 + lane; i < sp.e; i += 64) {
+      const float y = sc * (float)(mask[i] != 0);
+      adv[i] = y;
+      ret[i] = y;
     }
   }
 }

@@ -96,11 +96,17 @@ struct TurnOut {
 // Actions of one env packed into a u64 (K <= 8 bytes), loaded once per turn.  The K byte
 // loads are issued back to back with clamped (always in-row) addresses and masked
 // afterwards, so they share one memory round trip instead of one wait per byte.
-__device__ __forceinline__ uint64_t load_actions(const int8_t* acts, int K) {
-  if (K <= 0) return 0;
+// One env's action ids packed 8 bits each (slot k in byte k), branch-free: with K == 0 (no
+// action slots; `acts` may then be null) the loads read `alt`, any valid byte, and the result
+// is 0.  No branch around the loads: a branch here makes the compiler fetch the actions
+// pointer from the kernel arguments only inside it, after the turn's other loads (a second
+// scalar round trip ahead of the action loads).
+__device__ __forceinline__ uint64_t load_actions(const int8_t* acts, int K, const uint8_t* alt) {
+  const int8_t* p = K > 0 ? acts : reinterpret_cast<const int8_t*>(alt);
+  const int Kc = K > 0 ? K : 1;
   uint8_t v[kMaxK];
 #pragma unroll
-  for (int k = 0; k < kMaxK; ++k) v[k] = (uint8_t)acts[k < K ? k : K - 1];
+  for (int k = 0; k < kMaxK; ++k) v[k] = (uint8_t)p[k < Kc ? k : Kc - 1];
   uint64_t packed = 0;
 #pragma unroll
   for (int k = 0; k < kMaxK; ++k) packed |= k < K ? (uint64_t)v[k] << (8 * k) : 0ull;

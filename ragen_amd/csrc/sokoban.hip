@@ -587,17 +587,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
     penalty = ep.penalty[bc];
   }
   int n_act = in.n_actions[bc];
-  uint8_t av[kMaxK];
-#pragma unroll
-  for (int k = 0; k < kMaxK; ++k) av[k] = 0;
-  if (in.K > 0) {  // wave-uniform
-    const int8_t* ap = in.actions + bc * (int64_t)in.K;
-#pragma unroll
-    for (int k = 0; k < kMaxK; ++k) av[k] = (uint8_t)ap[k < in.K ? k : in.K - 1];
-  }
-  uint64_t acts = 0;
-#pragma unroll
-  for (int k = 0; k < kMaxK; ++k) acts |= k < in.K ? (uint64_t)av[k] << (8 * k) : 0ull;
+  const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K, ep.flags + bc);
   FinRecord rec;
   if (kFin) rec.load(ep, bc);
   if (!live) flags = RMI_FLAG_DONE;

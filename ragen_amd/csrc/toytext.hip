@@ -220,7 +220,7 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
   // branch-free: a conditional load would make the compiler wait for the earlier loads
   const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
   const int n_act = in.n_actions[bc];
-  const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K);
+  const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K, ep.flags + bc);
   const int n = env.nrow * env.ncol;
   FrozenLakeDev e;
   e.desc = (kFirst ? init_desc : env.desc) + bc * n;
@@ -387,7 +387,7 @@ __global__ __launch_bounds__(kToyBlock) void bandit_step_turn_kernel(rmi_bandit_
   uint8_t err = 0;
   int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
   double penalty = ep.penalty[b];
-  TurnOut o = run_turn(e, load_actions(in.actions + b * (int64_t)in.K, in.K), in.n_actions[b], in.K, num_actions, flags, n_turns,
+  TurnOut o = run_turn(e, load_actions(in.actions + b * (int64_t)in.K, in.K, ep.flags + b), in.n_actions[b], in.K, num_actions, flags, n_turns,
                        penalty, in.max_actions_per_traj, in.format_penalty, err);
   ep.num_actions[b] = num_actions;
   ep.flags[b] = flags;
