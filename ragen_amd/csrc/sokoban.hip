@@ -20,41 +20,6 @@
 namespace rmi {
 namespace {
 
-// Diagnostic build only (tools/microbench.hip defines RMI_STAMPS): per-wave s_memtime /
-// s_memrealtime stamps at phase boundaries.  Compiled out of the library.
-// The stamps stay in SGPRs until the wave's last one, so the instrumentation adds no memory
-// round trip inside the phases it measures (one s_memtime each; s_memrealtime at 0 and 4).
-#ifdef RMI_STAMPS
-__device__ unsigned long long* g_stamps;
-#define RMI_STAMP_DECL unsigned long long rmi_st_[5], rmi_rt0_ = __builtin_amdgcn_s_memrealtime()
-#define RMI_STAMP(i)                                 \
-  do {                                               \
-    rmi_st_[i] = __builtin_amdgcn_s_memtime();       \
-    if ((i) == 4) {                                  \
-      const unsigned long long rt4 = __builtin_amdgcn_s_memrealtime(); \
-      if (threadIdx.x == 0) {                        \
-        unsigned long long* g = g_stamps + blockIdx.x * 16; \
-        for (int s_ = 0; s_ < 5; ++s_) g[2 * s_] = rmi_st_[s_]; \
-        g[1] = rmi_rt0_;                             \
-        g[9] = rt4;                                  \
-      }                                              \
-    }                                                \
-  } while (0)
-#define RMI_STAMP_WAIT(i)          \
-  do {                             \
-    __builtin_amdgcn_s_waitcnt(0); \
-    RMI_STAMP(i);                  \
-  } while (0)
-#else
-#define RMI_STAMP_DECL \
-  do {                 \
-  } while (0)
-#define RMI_STAMP(i) \
-  do {               \
-  } while (0)
-#define RMI_STAMP_WAIT(i) RMI_STAMP(i)
-#endif
-
 constexpr int kWave = 64;
 constexpr int kMaxCells = 64;
 

@@ -169,6 +169,21 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
   return r;
 }
 
+// bit i = (cell i == letter) for a 16-cell map held as two u64 (cell i in byte i): SWAR byte
+// compare, then each dword's 4 byte flags gathered by one multiply (bit 8j -> bit 24 + j).
+__device__ __forceinline__ uint32_t cell_bits(uint64_t lo, uint64_t hi, uint32_t letter) {
+  const uint32_t pat = letter * 0x01010101u;
+  const uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+  uint32_t bits = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t x = w[j] ^ pat;                                              // zero byte = match
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // high bit of a zero byte
+    bits |= (((z >> 7) * 0x01020408u) >> 24) << (4 * j);
+  }
+  return bits;
+}
+
 // ceil(cs * 2^53): u = (x >> 11) * 2^-53 satisfies cs > u  <=>  (x >> 11) < ceil(cs * 2^53)
 __device__ __forceinline__ uint64_t draw_threshold(double cs) {
   return (uint64_t)ceil(cs * 9007199254740992.0);
@@ -207,7 +222,22 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
   if (!kFin && b >= B) return;
   const bool live = b < B;
   const int64_t bc = live ? b : (int64_t)B - 1;  // clamped: every load below is valid
-  // every load of the turn is issued before the first use (one memory round trip)
+  RMI_STAMP_DECL;
+  RMI_STAMP(0);
+  // every load of the turn is issued before the first use (one memory round trip); the env
+  // state first (its pointers and the record's come from different kernel-argument fetches)
+  const int n = env.nrow * env.ncol;
+  FrozenLakeDev e;
+  e.desc = (kFirst ? init_desc : env.desc) + bc * n;
+  e.in_regs = n <= 16;
+  e.d_lo = e.d_hi = 0;
+  e.s = kFirst ? init_s[bc] : env.s[bc];
+  e.rng = load_pcg(kFirst ? init_rng : env.rng, B, bc);
+  if (n == 16 && (reinterpret_cast<uintptr_t>(kFirst ? init_desc : env.desc) & 15u) == 0) {  // 4x4: one 16-B load
+    const uint4 q = *reinterpret_cast<const uint4*>(e.desc);
+    e.d_lo = ((uint64_t)q.y << 32) | q.x;
+    e.d_hi = ((uint64_t)q.w << 32) | q.z;
+  }
   uint8_t flags = 0;
   int32_t num_actions = 0, n_turns = 0;
   double penalty = 0.0;
@@ -221,17 +251,8 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
   const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
   const int n_act = in.n_actions[bc];
   const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K, ep.flags + bc);
-  const int n = env.nrow * env.ncol;
-  FrozenLakeDev e;
-  e.desc = (kFirst ? init_desc : env.desc) + bc * n;
-  e.in_regs = n <= 16;
-  e.d_lo = e.d_hi = 0;
-  if (n == 16 && (reinterpret_cast<uintptr_t>(kFirst ? init_desc : env.desc) & 15u) == 0) {  // 4x4: one 16-B load
-    const uint4 q = *reinterpret_cast<const uint4*>(e.desc);
-    e.d_lo = ((uint64_t)q.y << 32) | q.x;
-    e.d_hi = ((uint64_t)q.w << 32) | q.z;
-  } else if (e.in_regs) {
-    for (int i = 0; i < n; ++i) {
+  if (!(n == 16 && (reinterpret_cast<uintptr_t>(kFirst ? init_desc : env.desc) & 15u) == 0) && e.in_regs) {
+    for (int i = 0; i < n; ++i) {  // small maps other than an aligned 4x4: byte by byte
       const uint64_t c = e.desc[i];
       if (i < 8) e.d_lo |= c << (8 * i);
       else e.d_hi |= c << (8 * (i - 8));
@@ -239,12 +260,10 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
   }
   e.nrow = env.nrow;
   e.ncol = env.ncol;
-  e.s = kFirst ? init_s[bc] : env.s[bc];
   e.slippery = env.is_slippery != 0;
   e.cs0 = env.cs0;
   e.cs1 = env.cs1;
   e.cs2 = env.cs2;
-  e.rng = load_pcg(kFirst ? init_rng : env.rng, B, bc);
   FinRecord rec;
   if (kFin) rec.load(ep, bc);
   if (kFirst && live) {  // the reset, then the turn (same thread, later stores win)
@@ -268,6 +287,7 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
       ep.turn_exec[(int64_t)t * B + b] = 0;
     }
   }
+  RMI_STAMP_WAIT(1);
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
   TurnOut o;
   o.acc = 0.0;
@@ -281,17 +301,13 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
   const bool fast = n == 16 && env.ncol == 4 && e.in_regs && in.K >= 1 && ids_ok && e.s >= 0 && e.s < 16;
   if (__all(fast || !act)) {
     if (act) {
-      uint32_t hole = 0, goal = 0;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint8_t c = e.cell(i);
-        hole |= (uint32_t)(c == 'H') << i;
-        goal |= (uint32_t)(c == 'G') << i;
-      }
+      const uint32_t hole = cell_bits(e.d_lo, e.d_hi, 'H'), goal = cell_bits(e.d_lo, e.d_hi, 'G');
       int n_a = n_act > in.K ? in.K : n_act;
       flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (es_manager.py:168)
+      RMI_STAMP(2);
       const Fl4Out f = fl4_dispatch(in.K, hole, goal, e.s, e.rng, acts, n_a, in.max_actions_per_traj - num_actions,
                                     e.slippery, draw_threshold(e.cs0), draw_threshold(e.cs1), draw_threshold(e.cs2));
+      RMI_STAMP(3);
       // the format penalty (es_manager.py:158-159): not every parsed name known, or none
       int nv = 0;
       for (int k = 0; k < n_a; ++k) nv += ((acts >> (8 * k)) & 0xFF) != 0;
@@ -349,6 +365,7 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
     finalize_envs<1>(ep, fin, rec, b, live, flags, n_turns, num_actions, penalty, stepped ? in.turn : -1, o.acc,
                      o.info);
   }
+  RMI_STAMP(4);
 }
 
 struct BanditDev {
@@ -432,6 +449,12 @@ __global__ __launch_bounds__(kBlock) void frozenlake_reset_kernel(rmi_frozenlake
 
 }  // namespace
 }  // namespace rmi
+
+#ifdef RMI_STAMPS
+RMI_API int rmi_toytext_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 RMI_API int rmi_frozenlake_reset(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const uint8_t* init_desc,
                                  const int32_t* init_s, const uint64_t* init_rng, rmi_stream_t stream) {
