@@ -84,6 +84,9 @@ struct Fl4Out {
   bool turn_done, succ_last;
   int s;
   Pcg64 rng;
+#ifdef RMI_STAMPS
+  unsigned long long t_draws;  // diagnostic: s_memtime once the turn's draws are computed
+#endif
 };
 
 __device__ __forceinline__ uint64_t pcg_out(uint64_t hi, uint64_t lo) {
@@ -91,6 +94,8 @@ __device__ __forceinline__ uint64_t pcg_out(uint64_t hi, uint64_t lo) {
   const unsigned rot = (unsigned)(hi >> 58);
   return (x >> rot) | (x << ((64u - rot) & 63u));
 }
+
+constexpr uint64_t kFl4Allow = 0x9ddcbffebffe3776ull;
 
 template <int K>
 __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, Pcg64 rng, uint64_t acts, int n_act,
@@ -127,33 +132,37 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
       draw[k] = pcg_out(c.s_hi, c.s_lo) >> 11;
     }
   }
-  bool stop = false;
+#ifdef RMI_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  r.t_draws = __builtin_amdgcn_s_memtime();
+#endif
+  uint32_t stop = 0;
   int ex = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const bool go = k < n_try && !stop;
+    // 0/1 words and bitwise operators throughout: a short-circuit && / || here compiles to a
+    // divergent branch per step
+    const uint32_t go = (uint32_t)(k < n_try) & (stop ^ 1u);
     const int ga = (int)((cl >> (8 * k)) & 0xFF) - 1;  // gym action 0..3 (LEFT, DOWN, RIGHT, UP)
     const uint64_t u = draw[k];
-    const bool term = ((hole | goal) >> s) & 1u;
+    const uint32_t term = ((hole | goal) >> s) & 1u;
     const int i = (u < t0) ? 0 : (u < t1) ? 1 : (u < t2) ? 2 : 0;
-    const int b = slippery ? ((ga + 3 + i) & 3) : ga;
-    const int row = s >> 2, col = s & 3;
-    int ns = b == 0 ? (col > 0 ? s - 1 : s) : b == 1 ? (row < 3 ? s + 4 : s) : b == 2 ? (col < 3 ? s + 1 : s)
-                                                                                      : (row > 0 ? s - 4 : s);
-    ns = term ? s : ns;
-    const bool g = (goal >> ns) & 1u, h = (hole >> ns) & 1u;
-    const double rw = (!term && g) ? 1.0 : 0.0;
-    const bool done = term || g || h;
-    const bool eff = ns != s;
+    const int b = (slippery ? ga + 3 + i : ga) & 3;  // & 3: a step past the exec list (ga = -1) is discarded
+    // branch-free move: bit 4s + b of kFl4Allow = the move stays on the board (LEFT col > 0,
+    // DOWN row < 3, RIGHT col < 3, UP row > 0); the deltas -1 / +4 / +1 / -4 as packed bytes
+    const uint32_t moves = (term ^ 1u) & (uint32_t)((kFl4Allow >> (4 * s + b)) & 1ull);
+    const int ns = s + (moves ? (int)(int8_t)(uint8_t)(0xFC0104FFu >> (8 * b)) : 0);
+    const uint32_t g = (goal >> ns) & 1u, h = (hole >> ns) & 1u;
+    const double rw = ((term ^ 1u) & g) ? 1.0 : 0.0;
+    const uint32_t done = term | g | h;
+    const uint32_t eff = (uint32_t)(ns != s);
     r.o.acc = go ? r.o.acc + rw : r.o.acc;
-    r.o.info = go ? (uint8_t)(RMI_INFO_PRESENT | (eff ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID |
-                              (g ? RMI_INFO_SUCCESS : 0))
-                  : r.o.info;
-    r.succ_last = go ? g : r.succ_last;
-    r.turn_done = go ? done : r.turn_done;
+    r.o.info = go ? (uint8_t)(RMI_INFO_PRESENT | RMI_INFO_VALID | (eff << 1) | (g << 3)) : r.o.info;
+    r.succ_last = go ? (bool)g : r.succ_last;
+    r.turn_done = go ? (bool)done : r.turn_done;
     s = go ? ns : s;
-    ex += go ? 1 : 0;
-    stop = stop || (go && done);
+    ex += (int)go;
+    stop |= go & done;
   }
   r.o.exec = (uint8_t)ex;
   r.o.stepped_any_state = ex > 0;
@@ -308,6 +317,9 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
       const Fl4Out f = fl4_dispatch(in.K, hole, goal, e.s, e.rng, acts, n_a, in.max_actions_per_traj - num_actions,
                                     e.slippery, draw_threshold(e.cs0), draw_threshold(e.cs1), draw_threshold(e.cs2));
       RMI_STAMP(3);
+#ifdef RMI_STAMPS
+      if (threadIdx.x == 0) g_stamps[blockIdx.x * 16 + 11] = f.t_draws;
+#endif
       // the format penalty (es_manager.py:158-159): not every parsed name known, or none
       int nv = 0;
       for (int k = 0; k < n_a; ++k) nv += ((acts >> (8 * k)) & 0xFF) != 0;

@@ -50,4 +50,5 @@ print(f"B={B}, plain turn 3, {int(ok.sum())} of {waves} waves: mean cycles " +
       "  ".join(f"{nm} {p.mean():.0f}" for nm, p in zip(names, ph)) +
       f"  | span {(a[:, 8] - a[:, 0]).mean():.0f} cycles, {(a[:, 9] - a[:, 1]).mean() / 100:.2f} us realtime; "
       f"first-to-last wave start {(a[:, 1].max() - a[:, 1].min()) / 100:.2f} us, "
-      f"kernel window {(a[:, 9].max() - a[:, 1].min()) / 100:.2f} us")
+      f"kernel window {(a[:, 9].max() - a[:, 1].min()) / 100:.2f} us; of the turn: the {K} draws "
+      f"{(a[:, 11] - a[:, 4]).mean():.0f} cycles (incl. the exec list)")
