@@ -21,8 +21,8 @@ __device__ unsigned long long* g_stamps;
     rmi_st_[i] = __builtin_amdgcn_s_memtime();       \
     if ((i) == 4) {                                  \
       const unsigned long long rt4 = __builtin_amdgcn_s_memrealtime(); \
-      if (threadIdx.x == 0) {                        \
-        unsigned long long* g = g_stamps + blockIdx.x * 16; \
+      if ((threadIdx.x & 63) == 0) {                 \
+        unsigned long long* g = g_stamps + (blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64) * 16; \
         for (int s_ = 0; s_ < 5; ++s_) g[2 * s_] = rmi_st_[s_]; \
         g[1] = rmi_rt0_;                             \
         g[9] = rt4;                                  \

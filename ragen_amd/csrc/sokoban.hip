@@ -489,6 +489,10 @@ constexpr int kMaxWords = kMaxCells / 4;
 #endif
 constexpr int64_t kSpreadMaxEnvs = RMI_SPREAD_MAX_ENVS;  // RMI_SPREAD_LPE lanes per env up to this batch
 constexpr int kSpreadLpe = RMI_SPREAD_LPE;
+#ifndef RMI_SOK_WPB  // waves per workgroup of the turn kernel (every wave owns its own envs)
+#define RMI_SOK_WPB 2
+#endif
+constexpr int kSokWpb = RMI_SOK_WPB;
 __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMaxEnvs; }
 
 // One launch = one turn of every env.  LPE consecutive lanes own one env (LPE = 1 for big
@@ -504,7 +508,7 @@ __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMax
 // the rows and players come from init_state / init_player, the counters and the episode record
 // start at zero without being read, and every env's state and whole record are written.
 template <int HW, class M, int LPE, bool kFin, bool kFirst = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
-__global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
+__global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
                                                                   uint8_t* __restrict__ err_out, rmi_finalize_t fin,
                                                                   const uint8_t* __restrict__ init_state = nullptr,
@@ -512,14 +516,14 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   constexpr int NW = HW ? HW / 4 : kMaxWords;
   constexpr int NWL = (NW + LPE - 1) / LPE;      // row dwords per lane
   constexpr int kEnvs = kWave / LPE;             // envs per wave
-  __shared__ uint32_t lds_state[kEnvs * NW];     // exact path only: env-private rows
-  __shared__ uint32_t lds_fixed[kEnvs * NW];
+  __shared__ uint32_t lds_state[kSokWpb * kEnvs * NW];  // exact path only: env-private rows
+  __shared__ uint32_t lds_fixed[kSokWpb * kEnvs * NW];
   const int hw = HW ? HW : hw_rt;
   const int row_words = hw >> 2;
   const int B = ep.B;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int sub = lane % LPE, slot = lane / LPE;
-  const int64_t b = (int64_t)blockIdx.x * kEnvs + slot;
+  const int64_t b = ((int64_t)blockIdx.x * kSokWpb + wave) * kEnvs + slot;
   const bool live = b < B;
   const int H = env.H, W = env.W;
   const uint32_t w_magic = (65536u + (uint32_t)W - 1u) / (uint32_t)W;  // off the critical path
@@ -665,8 +669,8 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
   } else {
     // rare: some room of the wave is irregular -> the exact path on an env-private LDS row,
     // assembled from the env's lanes and stepped by its first lane
-    uint32_t* ls = lds_state + slot * row_words;
-    uint32_t* lf = lds_fixed + slot * row_words;
+    uint32_t* ls = lds_state + (wave * kEnvs + slot) * row_words;
+    uint32_t* lf = lds_fixed + (wave * kEnvs + slot) * row_words;
     if (act) {
 #pragma unroll
       for (int i = 0; i < NWL; ++i) {
@@ -677,7 +681,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
         }
       }
     }
-    __syncthreads();
+    wave_sync();  // the rows are wave-private; the workgroup's other waves may be on the fast path
     if (act && sub == 0) {
       int n_open = 0;
       for (int w = 0; w < row_words; ++w)
@@ -704,7 +708,7 @@ __global__ __launch_bounds__(kWave) void sokoban_step_turn_kernel(rmi_sokoban_t 
       bot = e.boxes_on_target;
       row_changed = o.stepped_any_state;
     }
-    __syncthreads();
+    wave_sync();  // the rows are wave-private; the workgroup's other waves may be on the fast path
     row_changed = env_or<LPE>(row_changed) != 0;  // the env's other lanes store their dwords too
     if (act && row_changed) {
 #pragma unroll
@@ -799,7 +803,7 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
                              const rmi_finalize_t& fin, hipStream_t s, const uint8_t* init_state = nullptr,
                              const int8_t* init_player = nullptr) {
   const int hw = env->H * env->W;
-  const unsigned grid = (unsigned)((ep->B + kWave - 1) / kWave);
+  const unsigned grid = (unsigned)((ep->B + kWave * kSokWpb - 1) / (kWave * kSokWpb));
   const int H = env->H, W = env->W;
   uint64_t border = 0;  // border cells, row-major
   for (int r = 0; r < H; ++r)
@@ -812,10 +816,13 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
   do {                                                                                                        \
     if (spread)                                                                                               \
       hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, kSpreadLpe, kFin, kFirst>),                       \
-                         dim3((unsigned)((ep->B + kWave / kSpreadLpe - 1) / (kWave / kSpreadLpe))),           \
-                         dim3(kWave), 0, s, *env, *ep, *in, hw, border, err, fin, init_state, init_player);   \
+                         dim3((unsigned)((ep->B + kWave * kSokWpb / kSpreadLpe - 1) /                          \
+                                         (kWave * kSokWpb / kSpreadLpe))),                                   \
+                         dim3(kWave * kSokWpb), 0, s, *env, *ep, *in, hw, border, err, fin, init_state,      \
+                         init_player);                                                                        \
     else                                                                                                      \
-      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, kFirst>), dim3(grid), dim3(kWave), 0, s,   \
+      hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, kFirst>), dim3(grid), dim3(kWave * kSokWpb), \
+                         0, s,                                                                                \
                          *env, *ep, *in, hw, border, err, fin, init_state, init_player);                      \
   } while (0)
   if (hw == 36 && w32)
@@ -846,6 +853,12 @@ int sokoban_check(const rmi_sokoban_t* env) {
 }
 }  // namespace
 }  // namespace rmi
+
+#ifdef RMI_STAMPS
+RMI_API int rmi_sokoban_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                   uint8_t* err, rmi_stream_t stream) {
