@@ -940,6 +940,13 @@ def main():
                          "frac_of_achievable": (achieved / copy_peak) if copy_peak else None,
                          "kernel": "rmi_sokoban_step_turn", "avg_launch_us": avg_launch_us,
                          "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn,
+                         "timed_region": {
+                             "avg_launch_us": elapsed / args.steps / T_TURNS * 1e6,
+                             "achieved": bytes_per_rollout * args.steps / elapsed / 1e9,
+                             "frac": bytes_per_rollout * args.steps / elapsed / 1e9 / HBM_PEAK_GBS,
+                             "note": "the same bytes over the timed region itself (graph replays of the fused "
+                                     "first / plain / last-turn launches, boundaries included); `achieved` "
+                                     "above brackets 5 plain launches with events, as rocprof times them"},
                          "at_scale": at_scale},
             "cpu_baseline": cpu,
             "cpu_baseline_parallel": cpu_par,
