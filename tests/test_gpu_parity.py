@@ -737,6 +737,23 @@ def test_render_vs_oracle(device):
                                for i in range(B)]
 
 
+@pytest.mark.parametrize("H,W", [(8, 8), (3, 5), (1, 64), (16, 4), (2, 3)])
+def test_render_shapes_vs_oracle(device, H, W):
+    """The 16-lanes-per-env render at other grid shapes (token runs of 1..8 per lane, rows of
+    1..64 cells, one row without any newline), random codes incl. unknown ones, multi-byte
+    glyphs, players on targets."""
+    rng = np.random.default_rng(H * 100 + W)
+    B = 300
+    st = rng.integers(0, 9, size=(B, H * W)).astype(np.uint8)
+    fx = rng.integers(0, 3, size=(B, H * W)).astype(np.uint8)
+    lk = {0: "#", 1: "_", 2: "O", 3: "\u221a", 4: "X", 5: "P", 6: "S", 7: "\U0001F600"}
+    gb, gl = ops.glyph_table(lk)
+    out, n = torch.ops.ragen_amd.sokoban_render(_t(fx, device), _t(st, device), H, W, [int(x) for x in gb],
+                                                [int(x) for x in gl])
+    got = [bytes(out[i, :int(n[i])].cpu().numpy()).decode() for i in range(B)]
+    assert got == [oracle.sokoban_render(st[i], fx[i], H, W, lk) for i in range(B)]
+
+
 @pytest.mark.parametrize("B,T", [(1024, 5), (8192, 5), (2048, 10)])
 def test_fused_last_turn_finalize(device, B, T):
     """rmi_sokoban_step_turn_finalize == rmi_sokoban_step_turn + rmi_rollout_finalize, bit for bit
