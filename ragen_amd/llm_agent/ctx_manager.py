@@ -109,6 +109,34 @@ def parse_response(response: str, enable_think: bool, action_sep: str, max_actio
     return llm_response, actions
 
 
+def parse_response_spans(raw: str, span, enable_think: bool, action_sep: str, max_actions_per_turn: int):
+    """parse_response with the regex match taken from the device parse (rmi_parse_actions'
+    spans: think [start, end), answer [start, end) in the UTF-8 bytes of ``raw``, -1 = no
+    match; tested against the reference's match on every parse vector).  The rest is
+    parse_response's own string code; a content holding a '<' runs the special-token cascade,
+    any other content only needs its strip (the cascade is a no-op on it)."""
+    ts, te, a0, a1 = (int(x) for x in span)
+    if a0 < 0:
+        return raw, []
+    rb = raw.encode("utf-8")
+    think_content = rb[ts:te].decode("utf-8") if enable_think else ""
+    action_content = rb[a0:a1].decode("utf-8")
+    if "<" in action_content or "<" in think_content:
+        for tok in SPECIAL_TOKENS:
+            action_content = action_content.replace(tok, "").strip()
+            think_content = think_content.replace(tok, "").strip()
+    else:
+        action_content = action_content.strip()
+        think_content = think_content.strip()
+    actions = [a.strip() for a in action_content.split(action_sep) if a.strip()]
+    if len(actions) > max_actions_per_turn:
+        actions = actions[:max_actions_per_turn]
+        action_content = (" " + action_sep + " ").join(actions)
+    llm_response = (f"<think>{think_content}</think><answer>{action_content}</answer>" if enable_think
+                    else f"<answer>{action_content}</answer>")
+    return llm_response, actions
+
+
 def segments_for(grouping: str, env_outputs: List[Dict]):
     """Group ids of ctx_manager.py:184-191 as contiguous segments (first-seen order)."""
     if grouping == "state":

@@ -311,9 +311,9 @@ class EnvStateManager:
         outs = []
         for tg in self.tags:
             cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, prepend)
-            acts, n_act, _, at, al, perr = torch.ops.ragen_amd.parse_actions(
-                parse_cfg_bytes(cfg), text[tg.lo:tg.hi], text_len[tg.lo:tg.hi], sel, False, int(lact))
-            p = {"actions": acts, "n_actions": n_act, "action_text": at if lact else None,
+            acts, n_act, spans, at, al, perr = torch.ops.ragen_amd.parse_actions(
+                parse_cfg_bytes(cfg), text[tg.lo:tg.hi], text_len[tg.lo:tg.hi], sel, True, int(lact))
+            p = {"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
                  "action_len": al if lact else None, "err": perr}
             has = None if has_input is None else has_input[tg.lo:tg.hi]
             kw = {}
@@ -337,9 +337,10 @@ class EnvStateManager:
         has[inp.env_ids_t] = 1
         err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
         ap = self.sys_config.agent_proxy
-        self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
+        parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
         obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
-        self._device_turns.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs})
+        self._device_turns.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs,
+                                   "spans": [p["spans"] for p in parsed]})
         flags = self.tags[0].batch.ep.flags if len(self.tags) == 1 else \
             torch.cat([tg.batch.ep.flags for tg in self.tags])
         still = ((flags[inp.env_ids_t] & _lib.FLAG_DONE) == 0).cpu().numpy()
@@ -354,7 +355,7 @@ class EnvStateManager:
         if not self._device_turns:
             return
         from .. import ops
-        from .ctx_manager import parse_response
+        from .ctx_manager import parse_response_spans
         turns, self._device_turns = self._device_turns, []
         ap = self.sys_config.agent_proxy
         prefix = "<think>" if ap.enable_think else "<answer>"
@@ -373,7 +374,9 @@ class EnvStateManager:
                     continue
                 rows = [g - tg.lo for g in gids]
                 raws = [prefix + texts[g] for g in gids]
-                parsed = [parse_response(r, bool(ap.enable_think), ap.action_sep, self.K) for r in raws]
+                spans = d["spans"][j].cpu().numpy()  # the device parse's regex match, per tag row
+                parsed = [parse_response_spans(r, spans[i], bool(ap.enable_think), ap.action_sep, self.K)
+                          for r, i in zip(raws, rows)]
                 inputs = [{"llm_response": lr, "llm_raw_response": raw} for (lr, _), raw in zip(parsed, raws)]
                 acts_l = [a for _, a in parsed]
                 m_l = tg.batch.map_actions_many(rows, acts_l)

@@ -99,3 +99,17 @@ def test_synthetic_responses_parse_to_their_actions():
         assert len(acts) == n[0][b]
         got = P.action_ids(acts, lk)
         assert got == [int(x) for x in ids[0][b, :n[0][b]]]
+
+
+def test_parse_response_from_spans_matches_regex():
+    """EnvStateManager._materialize builds the history strings from the device parse's match
+    spans (ctx_manager.parse_response_spans) instead of re-running the regex: equal to
+    parse_response and to the reference's outputs on every vector, with the spans of the
+    reference's match."""
+    from ragen_amd.llm_agent.ctx_manager import parse_response, parse_response_spans
+    for c in golden()[1]:
+        resp = P.prefixed(c["text"], c["enable_think"])
+        sp = P.match_spans(resp, c["enable_think"])
+        got = parse_response_spans(resp, sp, c["enable_think"], c["sep"], c["K"])
+        assert got == parse_response(resp, c["enable_think"], c["sep"], c["K"])
+        assert got == (c["llm_response"], c["actions"])
