@@ -613,6 +613,10 @@ __device__ int utf8_lossy(const uint8_t* src, int n, uint8_t* dst, int cap, bool
 // dwords covering them (tokens <= 9 bytes: 3 dwords; longer ones loop), clamped inside the
 // vocabulary blob.
 constexpr int kDetokG = 4;  // 64-id chunks per step
+// the low n bytes of a dword set (n clamped to [0, 4])
+__device__ __forceinline__ uint32_t byte_mask_n(int n) {
+  return n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << (8 * n)) - 1u);
+}
 __host__ __device__ constexpr size_t detok_lds(int stride) { return 2 * ((size_t)stride + 4) + 16; }  // per wave
 __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __restrict__ ids, int64_t R,
                                                    const int32_t* __restrict__ n_ids,
@@ -639,16 +643,22 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
   int pos = 0;
   bool bad = false, over = false;
   uint32_t high = 0;
+  // the row buffer starts zeroed: token bytes are OR-ed into its dwords
+  for (int i = lane; i < (stride + 8) / 4; i += 64) reinterpret_cast<uint32_t*>(buf)[i] = 0u;
+  wave_sync();
   for (int64_t c0 = 0; c0 < rn; c0 += 64 * kDetokG) {
     int64_t id[kDetokG], off[kDetokG], end[kDetokG];
     uint8_t sk[kDetokG];
 #pragma unroll
-    for (int g = 0; g < kDetokG; ++g) {
+    for (int g = 0; g < kDetokG; ++g) {  // (c0 + 64 * g < rn: wave-uniform; empty chunks issue nothing)
       const int64_t i = c0 + 64 * g + lane;
-      id[g] = i < rn ? row[i] : -1;
+      id[g] = c0 + 64 * g < rn && i < rn ? row[i] : -1;
     }
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {
+      off[g] = end[g] = 0;
+      sk[g] = 1;
+      if (c0 + 64 * g >= rn) continue;
       const bool in = c0 + 64 * g + lane < rn;
       const bool valid = id[g] >= 0 && id[g] < V;
       bad |= in && !valid;
@@ -661,6 +671,8 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {
       len[g] = sk[g] ? 0 : (int)(end[g] - off[g]);
+      start[g] = pos;
+      if (c0 + 64 * g >= rn) continue;
       const int incl = wave_inclusive_scan(len[g]);
       start[g] = pos + incl - len[g];
       pos += __builtin_amdgcn_readlane(incl, 63);
@@ -668,25 +680,49 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
     uint32_t w[kDetokG][3];
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {
+      w[g][0] = w[g][1] = w[g][2] = 0u;
+      if (c0 + 64 * g >= rn) continue;
       const int64_t q = off[g] >> 2;
 #pragma unroll
       for (int k = 0; k < 3; ++k) w[g][k] = v4[q + k <= last4 ? q + k : last4];
     }
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {
+      if (c0 + 64 * g >= rn) continue;
       const int r = (int)(off[g] & 3);
-      const uint64_t lo = (uint64_t)w[g][0] | ((uint64_t)w[g][1] << 32);
-      for (int k = 0; k < len[g]; ++k) {
-        const int p = start[g] + k;
-        const int o = k + r;
-        const uint32_t c = o < 8 ? (uint32_t)(lo >> (8 * o)) & 0xFFu
-                         : o < 12 ? (w[g][2] >> (8 * (o - 8))) & 0xFFu
-                                  : vbytes[off[g] + k];  // tokens longer than 9 bytes
-        if (p < stride) {
-          buf[p] = (uint8_t)c;
-          high |= c;
-        } else {
-          over = true;
+      const int sl = start[g], ln = len[g];
+      if (ln <= 12 - r && sl + ln <= stride) {
+        // the token's bytes: the 12-byte window at byte r of its dwords, masked to ln bytes,
+        // shifted to the destination's byte offset and OR-ed into <= 4 zeroed dwords (no loop
+        // over the bytes, no divergence)
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(w[g][1], w[g][0], r) & byte_mask_n(ln);
+        const uint32_t x1 = __builtin_amdgcn_alignbyte(w[g][2], w[g][1], r) & byte_mask_n(ln - 4);
+        const uint32_t x2 = (w[g][2] >> (8 * r)) & byte_mask_n(ln - 8);
+        high |= x0 | x1 | x2;
+        const int sh = sl & 3;
+        const uint32_t y0 = x0 << (8 * sh);
+        const uint32_t y1 = sh ? __builtin_amdgcn_alignbyte(x1, x0, 4 - sh) : x1;
+        const uint32_t y2 = sh ? __builtin_amdgcn_alignbyte(x2, x1, 4 - sh) : x2;
+        const uint32_t y3 = sh ? x2 >> (8 * (4 - sh)) : 0u;
+        uint32_t* q = reinterpret_cast<uint32_t*>(buf) + (sl >> 2);
+        if (y0) atomicOr(q, y0);
+        if (y1) atomicOr(q + 1, y1);
+        if (y2) atomicOr(q + 2, y2);
+        if (y3) atomicOr(q + 3, y3);
+      } else {
+        const uint64_t lo = (uint64_t)w[g][0] | ((uint64_t)w[g][1] << 32);
+        for (int k = 0; k < ln; ++k) {  // tokens longer than the window, or running past the row
+          const int p = sl + k;
+          const int o = k + r;
+          const uint32_t c = o < 8 ? (uint32_t)(lo >> (8 * o)) & 0xFFu
+                           : o < 12 ? (w[g][2] >> (8 * (o - 8))) & 0xFFu
+                                    : vbytes[off[g] + k];
+          if (p < stride) {
+            atomicOr(reinterpret_cast<uint32_t*>(buf) + (p >> 2), c << (8 * (p & 3)));
+            high |= c;
+          } else {
+            over = true;
+          }
         }
       }
     }
@@ -701,7 +737,7 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
   // at most 3 bytes back whose sequence covers it).  Only an invalid row takes the serial
   // replacement pass.
   bool invalid = false;
-  if (__ballot((high & 0x80u) != 0)) {
+  if (__ballot((high & 0x80808080u) != 0)) {  // high: the OR of the row's bytes, 4 per dword
     for (int c0 = 0; c0 < n; c0 += 256) {
       const int i0 = c0 + 4 * lane;
       if (i0 >= n) continue;
