@@ -835,37 +835,57 @@ __device__ __forceinline__ void bs_tile(const GaeTile& cur, int64_t c0, BilevelC
   __syncthreads();
 }
 
+// one group of the walk: columns in vm advance the chain, the others keep their value
+__device__ __forceinline__ float4 bs_group(uint32_t f, uint32_t vm, float4 d4, float gl, float& ll) {
+  float dd[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+  for (int e = 3; e >= 0; --e) {
+    const float nl = dd[e] + gl * (((f >> (4 + e)) & 1u) ? 0.0f : ll);
+    const bool in = (vm >> e) & 1u;
+    ll = in ? nl : ll;
+    dd[e] = in ? nl : dd[e];
+  }
+  return make_float4(dd[0], dd[1], dd[2], dd[3]);
+}
+// a group shared with a neighbouring segment: only vm's columns are stored (the others go to
+// the lane's dummy slot), so neither segment overwrites the other's results
+__device__ __forceinline__ void bs_store_part(float* Dq, float4 r, uint32_t vm, float* dummy) {
+  *((vm & 1u) ? Dq + 0 : dummy) = r.x;
+  *((vm & 2u) ? Dq + 1 : dummy) = r.y;
+  *((vm & 4u) ? Dq + 2 : dummy) = r.z;
+  *((vm & 8u) ? Dq + 3 : dummy) = r.w;
+}
 // One segment's low-level walk: valid columns from s leftwards while > end, in the
 // reference's order (ll = d + gl * (eos ? 0 : ll), the reset at a valid eos, core_algos.py:81-88).
-// Branch-free over the segment's 4-column groups: the next group's flag byte and deltas are
-// read before this one is worked on, every column is computed and a column outside the segment
-// (mask 0, or owned by the neighbouring segment in a shared group) keeps its value and the
-// chain, and its store goes to the lane's dummy slot — so the loop body has no divergent
-// branch and no read-modify-write of a neighbour's column.
+// Branch-free over the segment's 4-column groups: every column is computed, and one outside
+// the segment's valid columns keeps its value and the chain; the next group's flag byte and
+// deltas are read before this one is worked on.
 __device__ __forceinline__ void bs_walk(float* __restrict__ Dr, const uint8_t* __restrict__ Fr,
                                         float* __restrict__ dummy, int s, int end, float gl) {
   float ll = 0.0f;
   const int qs = s >> 2, qe = (end + 1) >> 2;
   const uint32_t ms = (2u << (s & 3)) - 1u, me = ~((1u << ((end + 1) & 3)) - 1u) & 0xFu;
+  // the start group (shared with the segment to the right), then the interior groups — wholly
+  // this segment's, stored as 16 B — then the end group (shared with the next segment)
   uint32_t f = Fr[qs];
   float4 d4 = *reinterpret_cast<const float4*>(Dr + 4 * qs);
-  for (int q = qs; q >= qe; --q) {
-    const int qn = q > qe ? q - 1 : q;
-    const uint32_t fn = Fr[qn];
-    const float4 dn = *reinterpret_cast<const float4*>(Dr + 4 * qn);
-    uint32_t vm = f & (q == qs ? ms : 0xFu);
-    vm &= q == qe ? me : 0xFu;
-    const float dd[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-    for (int e = 3; e >= 0; --e) {
-      const float nl = dd[e] + gl * (((f >> (4 + e)) & 1u) ? 0.0f : ll);
-      const bool in = (vm >> e) & 1u;
-      ll = in ? nl : ll;
-      *(in ? Dr + 4 * q + e : dummy) = nl;
-    }
+  const int q1 = qs > qe ? qs - 1 : qs;
+  uint32_t fn = Fr[q1];
+  float4 dn = *reinterpret_cast<const float4*>(Dr + 4 * q1);
+  uint32_t vm = f & ms & (qs == qe ? me : 0xFu);
+  bs_store_part(Dr + 4 * qs, bs_group(f, vm, d4, gl, ll), vm, dummy);
+  if (qs == qe) return;
+  f = fn;
+  d4 = dn;
+  for (int q = qs - 1; q > qe; --q) {
+    fn = Fr[q - 1];  // the next group's flags and deltas, read before this one is worked on
+    dn = *reinterpret_cast<const float4*>(Dr + 4 * (q - 1));
+    *reinterpret_cast<float4*>(Dr + 4 * q) = bs_group(f, f & 0xFu, d4, gl, ll);
     f = fn;
     d4 = dn;
   }
+  vm = f & me;
+  bs_store_part(Dr + 4 * qe, bs_group(f, vm, d4, gl, ll), vm, dummy);
 }
 
 // v groups c0, c0 + 64, ..., c0 + 7 * 64 of one row (zeros past L; the ragged group at L % 4)
