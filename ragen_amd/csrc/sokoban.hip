@@ -655,7 +655,25 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
         } else
 #endif
         if (sub == 0) {
+          // the changed cells: the old and new player cells and the cells whose box bit
+          // flipped — 2 to 4 for one box pushed any number of times.  The first 4 are stored
+          // straight-line (a missing one repeats the first: the same byte, the same value); only
+          // a turn that moved several boxes loops over the rest.
           uint8_t* win = env.room_state + b * hw + W;  // window bit j = cell W + j
+          int jj[4];
+          jj[0] = WordBits<M>::ctz(m);
+          m &= m - 1;
+#pragma unroll
+          for (int k = 1; k < 4; ++k) {
+            jj[k] = m ? WordBits<M>::ctz(m) : jj[0];
+            m &= m - 1;
+          }
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int j = jj[k];
+            const uint32_t t = (uint32_t)(target >> j) & 1u, bx = (uint32_t)(box >> j) & 1u;
+            win[j] = (uint8_t)(j == jp ? 5u : (bx ? 4u - t : 1u + t));
+          }
           while (m) {
             const int j = WordBits<M>::ctz(m);
             m &= m - 1;
