@@ -29,6 +29,9 @@ struct __attribute__((packed, aligned(4))) F4u {
   float x, y, z, w;
 };
 
+// 32 readable bytes for the clamped loads of groups outside a row's tokens
+__device__ const int64_t kZero4[kTok] = {0, 0, 0, 0};
+
 constexpr int kSuper = 8;  // chunks whose loads are issued together (2048 ids per row)
 
 // The batch assembly of formulate_rollouts (ctx_manager.py:278-306) fused into the same pass
@@ -82,17 +85,26 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
     // 1. every load of the super-chunk in flight together (clamped addresses, branch-free);
     //    the group at the row end and groups past it are fixed up element-wise afterwards
     I64x4 v[kSuper];
-    if (kAsm) {  // padded ids from the ragged rows, element-wise (the pad shifts the alignment)
+    if (kAsm) {  // padded ids from the ragged rows: 32-B loads where the group lies inside the
+                 // row's tokens (clamped to a zero block elsewhere), element-wise fix-up after
 #pragma unroll
       for (int k = 0; k < kSuper; ++k) {
         const int64_t p0 = s0 + k * kChunk + kTok * lane;
-        int64_t e4[kTok];
+        const bool full = p0 >= pad && p0 + kTok <= S;
+        v[k] = *reinterpret_cast<const I64x4*>(full ? as.tokens + a_src + p0 : kZero4);
+      }
 #pragma unroll
-        for (int e = 0; e < kTok; ++e) {
-          const int64_t p = p0 + e;
-          e4[e] = p >= S ? none : (p < pad ? as.pad_id : as.tokens[a_src + p]);
+      for (int k = 0; k < kSuper; ++k) {
+        const int64_t p0 = s0 + k * kChunk + kTok * lane;
+        if (!(p0 >= pad && p0 + kTok <= S)) {  // the pad, the pad / token edge and the row end
+          int64_t e4[kTok];
+#pragma unroll
+          for (int e = 0; e < kTok; ++e) {
+            const int64_t p = p0 + e;
+            e4[e] = p >= S ? none : (p < pad ? as.pad_id : as.tokens[a_src + p]);
+          }
+          v[k] = I64x4{e4[0], e4[1], e4[2], e4[3]};
         }
-        v[k] = I64x4{e4[0], e4[1], e4[2], e4[3]};
       }
     } else {
 #pragma unroll
@@ -122,14 +134,25 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
         int64_t* io = as.input_ids + b * S;
         int64_t* ao = as.attention_mask + b * S;
         int64_t* po = as.position_ids + b * S;
+        int64_t am[kTok], ps[kTok];
 #pragma unroll
         for (int e = 0; e < kTok; ++e) {
           const int64_t p = p0 + e;
-          if (p < S) {
-            io[p] = t[e];
-            ao[p] = p >= pad ? 1 : 0;
-            po[p] = p >= pad ? p - pad + 1 : 0;
-          }
+          am[e] = p >= pad ? 1 : 0;
+          ps[e] = p >= pad ? p - pad + 1 : 0;
+        }
+        if (p0 + kTok <= S) {  // 32-B stores
+          *reinterpret_cast<I64x4*>(io + p0) = v[k];
+          *reinterpret_cast<I64x4*>(ao + p0) = I64x4{am[0], am[1], am[2], am[3]};
+          *reinterpret_cast<I64x4*>(po + p0) = I64x4{ps[0], ps[1], ps[2], ps[3]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < kTok; ++e)
+            if (p0 + e < S) {
+              io[p0 + e] = t[e];
+              ao[p0 + e] = am[e];
+              po[p0 + e] = ps[e];
+            }
         }
       }
       int st[kTok], c = 0;
