@@ -1252,8 +1252,8 @@ __device__ double row_reward(const uint8_t* stage, const uint8_t* src_global, in
     fmt = o.fmt;
   }
   if (fb) {
-    volatile double* bv = reinterpret_cast<volatile double*>(par);
-    volatile uint32_t* bf = reinterpret_cast<volatile uint32_t*>(par + 8);
+    double* bv = reinterpret_cast<double*>(par);  // LDS: the row's lanes read lane 0's result
+    uint32_t* bf = reinterpret_cast<uint32_t*>(par + 8);
     if (j == 0) {
       uint8_t fl = 0, e = 0;
       const double r = countdown_reward(stage ? stage : src_global, n, stage != nullptr, nums, n_nums, target,
@@ -1261,6 +1261,7 @@ __device__ double row_reward(const uint8_t* stage, const uint8_t* src_global, in
       *bv = r;
       *bf = (uint32_t)fl | (uint32_t)e << 8;
     }
+    wave_sync();
     const double r = *bv;
     const uint32_t w = *bf;
     flags = (uint8_t)(w & 0xFF);
@@ -1289,49 +1290,11 @@ __device__ __forceinline__ void stage_answer(const uint8_t* g, int from, int n, 
   }
 }
 
-struct CountdownDev {
-  const uint8_t* answers;  // this env's [K, Lmax]
-  const int32_t* lens;     // this env's [K]
-  uint8_t* stage;          // the row's LDS answer (nullptr: parse global memory in place)
-  uint8_t* par;            // the row's cooperative scratch
-  uint8_t* work;           // the row's per-lane evaluator stacks (lane 0's fallback)
-  int Lmax, j, rowbase;
-  int pre_n;     // bytes of answer 0 already in stage (0: none)
-  int32_t len0;  // lens[0], loaded with them
-  int32_t nums[kMaxNums];
-  int n_nums;
-  int32_t target;
-  double score, format_score;
-  uint8_t err;
-#ifdef RMI_CD_STAMPS
-  unsigned long long st[kCdStamps];
-#endif
-  __device__ bool step(int a, double& reward, bool& done, bool& eff, bool& success) {
-    // `a` is the 1-based slot of the answer string (the host passes 1..K for every parsed action)
-    const int k = a - 1;
-    if (k < 0) return false;
-    const bool pre = k == 0 && pre_n > 0;
-    int n = pre ? len0 : lens[k];
-    if (n > Lmax) n = Lmax;
-    if (n < 0) n = 0;
-    const uint8_t* src = answers + (int64_t)k * Lmax;
-    if (stage && n > 0) stage_answer(src, pre ? pre_n : 0, n, Lmax, stage, j);
-    uint8_t fl;
-    CD_STAMP(st, 2);  // the staging stores wait for their loads
-    reward = row_reward(stage, src, n, j, rowbase, par, work, nums, n_nums, target, score, format_score, fl, err);
-#ifdef RMI_CD_STAMPS
-    st[3] = (unsigned long long)(reward != -12345.0) * __builtin_amdgcn_s_memtime();
-#endif
-    done = true;
-    eff = reward > 0;
-    success = reward == score;
-    return true;
-  }
-};
-
 // Per row (16 lanes, one env or answer) of LDS: the staged answer, lane 0's per-lane evaluator
 // stacks, the cooperative scratch.  64-thread blocks = 4 rows.
 constexpr int kCdBlock = 64;
+// 16 readable bytes for the clamped answer-head loads of rows without one
+__device__ __attribute__((aligned(16))) const uint32_t kZero16[4] = {0, 0, 0, 0};
 // a staged row is 16-B aligned and readable 80 bytes past its start (the token reads)
 __host__ __device__ constexpr int stage_stride(int Lmax) { return Lmax <= kStageMax ? ((Lmax + 15) & ~15) + 16 : 0; }
 __host__ __device__ constexpr int cd_slice(int Lmax) { return stage_stride(Lmax) + kMachineBytes + kParBytes; }
@@ -1342,8 +1305,13 @@ __device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b,
 }
 
 // One env per DPP row: all 16 lanes load the env's words (one broadcast per word) and run the
-// turn's bookkeeping redundantly, so the answer evaluation inside step() is convergent across
-// the row; lane 0 stores.
+// turn's bookkeeping redundantly, so the answer evaluation is convergent across the row; lane
+// 0 stores.  The turn is EnvStateManager.step's loop (run_turn, common.hpp) specialised to
+// Countdown: every parsed answer is a valid action (no action_lookup, es_manager.py:234-235)
+// and step() always ends the episode (env.py:58-62), so a turn steps at most once, on answer
+// slot 0, when it has a parsed answer and the cap leaves room; the format penalty applies iff
+// it has none.  Straight-line, so the wave carries no loop state (the generic loop's hoisted
+// per-slot predicates spilled SGPRs and put ≈2 k cycles between the loads and the evaluator).
 __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
                                                                        rmi_turn_t in,
                                                                        const uint8_t* __restrict__ answers,
@@ -1355,53 +1323,76 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   const int B = ep.B;
   if (b >= B) return;
 #ifdef RMI_CD_STAMPS
-  unsigned long long st0 = __builtin_amdgcn_s_memtime();
+  unsigned long long st[kCdStamps];
+  st[0] = __builtin_amdgcn_s_memtime();
 #endif
-  // every load of this env is issued before the activity test (one memory round trip): the
-  // has_input byte through a pointer that is always valid, selected afterwards
+  // every load of this env is issued before the first use (one memory round trip): no load
+  // sits behind a branch or a store that needs an earlier load's data (either makes the
+  // compiler wait there and split the loads into serial round trips); the has_input byte,
+  // lens[0], the answer head and the numbers come through pointers that are always valid
+  // (clamped), selected afterwards
   uint8_t flags = ep.flags[b];
   const uint8_t has_in = *(in.has_input ? in.has_input + b : ep.flags + b);
   uint8_t* slice = cd_lds + (threadIdx.x / kRow) * cd_slice(Lmax);
-  CountdownDev e;
-  e.answers = answers + b * (int64_t)in.K * Lmax;
-  e.lens = answer_len + b * (int64_t)in.K;
-  e.stage = Lmax <= kStageMax ? slice : nullptr;
-  e.work = slice + stage_stride(Lmax);
-  e.par = e.work + kMachineBytes;
-  e.Lmax = Lmax;
-  e.j = j;
-  e.rowbase = rowbase;
-  e.pre_n = 0;
-  e.len0 = 0;
-  if (in.K > 0 && e.stage && stage16(e.answers, Lmax)) {  // answer 0's head, with the other loads
-    const int nc = (Lmax < kPre ? Lmax : kPre) >> 4;
-    e.len0 = e.lens[0];
-    if (j < nc) *reinterpret_cast<uint4*>(e.stage + 16 * j) = reinterpret_cast<const uint4*>(e.answers)[j];
-    e.pre_n = 16 * nc;
-  }
-  load_nums(env, b, e.nums);
-  e.n_nums = env.n_nums[b];
-  e.target = env.target[b];
-  e.score = env.score;
-  e.format_score = env.format_score;
-  e.err = 0;
-  // every parsed answer string is a valid action (no action_lookup: es_manager.py:234-235)
-  const uint64_t acts = 0x0807060504030201ull;  // slot k holds answer k+1
+  const uint8_t* ans = answers + b * (int64_t)in.K * Lmax;  // answer slot 0 of this env
+  uint8_t* stage = Lmax <= kStageMax ? slice : nullptr;
+  uint8_t* work = slice + stage_stride(Lmax);
+  uint8_t* par = work + kMachineBytes;
+  const bool pre_ok = in.K > 0 && stage && stage16(ans, Lmax);  // answer 0's head, with the other loads
+  const int nc = (Lmax < kPre ? Lmax : kPre) >> 4;
+  const uint4 head = *(pre_ok && j < nc ? reinterpret_cast<const uint4*>(ans) + j
+                                        : reinterpret_cast<const uint4*>(kZero16));
+  const int32_t len0 = *(in.K > 0 ? answer_len + b * (int64_t)in.K : env.n_nums + b);
+  const int mn = env.max_nums;
+  int32_t raw[kMaxNums];
+#pragma unroll
+  for (int k = 0; k < kMaxNums; ++k) raw[k] = env.nums[b * mn + (k < mn ? k : mn - 1)];
+  const int n_nums = env.n_nums[b];
+  const int32_t target = env.target[b];
   const int n_act = in.n_actions[b];
-  uint8_t err = 0;
   int32_t num_actions = ep.num_actions[b], n_turns = ep.n_turns[b];
   double penalty = ep.penalty[b];
+  // uses
+  int32_t nums[kMaxNums];
+#pragma unroll
+  for (int k = 0; k < kMaxNums; ++k) nums[k] = k < mn ? raw[k] : -1;
+  const int pre_n = pre_ok ? 16 * nc : 0;
+  if (pre_ok && j < nc) *reinterpret_cast<uint4*>(stage + 16 * j) = head;
   const bool act = in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE);
   if (!act) return;
 #ifdef RMI_CD_STAMPS
-  e.st[0] = st0;
-  e.st[1] = __builtin_amdgcn_s_memtime() + (unsigned long long)(penalty == -12345.0);  // loads landed
-  e.st[2] = e.st[3] = e.st[1];
+  st[1] = __builtin_amdgcn_s_memtime() + (unsigned long long)(penalty == -12345.0);  // loads landed
+  st[2] = st[3] = st[1];
 #endif
-  TurnOut o = run_turn(e, acts, n_act, in.K, num_actions, flags, n_turns, penalty, in.max_actions_per_traj,
-                       in.format_penalty, err);
+  uint8_t err = 0;
+  flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (es_manager.py:168)
+  const int nact = n_act < in.K ? n_act : in.K;
+  const bool stp = nact >= 1 && in.max_actions_per_traj - num_actions > 0;  // row-uniform
+  double acc = 0.0;
+  uint8_t info = 0, exec = 0;
+  if (stp) {
+    const int n = len0 > Lmax ? Lmax : (len0 < 0 ? 0 : len0);
+    if (stage && n > 0) stage_answer(ans, pre_n, n, Lmax, stage, j);
+    CD_STAMP(st, 2);  // the staging stores wait for their loads
+    uint8_t fl;
+    const double r = row_reward(stage, ans, n, j, rowbase, par, work, nums, n_nums, target, env.score,
+                                env.format_score, fl, err);
 #ifdef RMI_CD_STAMPS
-  e.st[4] = __builtin_amdgcn_s_memtime();
+    st[3] = (unsigned long long)(r != -12345.0) * __builtin_amdgcn_s_memtime();
+#endif
+    const bool eff = r > 0, succ = r == env.score;
+    acc += r;
+    exec = 1;
+    info = (uint8_t)(RMI_INFO_PRESENT | (eff ? RMI_INFO_EFFECTIVE : 0) | RMI_INFO_VALID | (succ ? RMI_INFO_SUCCESS : 0));
+    flags |= RMI_FLAG_TERMINATED | RMI_FLAG_DONE;  // done: terminated, truncated = not success
+    flags = succ ? (uint8_t)(flags & ~RMI_FLAG_TRUNCATED) : (uint8_t)(flags | RMI_FLAG_TRUNCATED);
+  }
+  if (nact == 0) penalty += in.format_penalty;  // every parsed answer is valid: penalty iff none
+  num_actions += exec;
+  n_turns += 1;
+  if (!stp && num_actions >= in.max_actions_per_traj) flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
+#ifdef RMI_CD_STAMPS
+  st[4] = __builtin_amdgcn_s_memtime();
 #endif
   if (j) return;
   ep.num_actions[b] = num_actions;
@@ -1409,15 +1400,14 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
   ep.n_turns[b] = n_turns;
   ep.penalty[b] = penalty;
   const int64_t tb = (int64_t)in.turn * B + b;
-  ep.turn_reward[tb] = o.acc;
-  ep.turn_info[tb] = o.info;
-  ep.turn_exec[tb] = o.exec;
-  err |= e.err;
+  ep.turn_reward[tb] = acc;
+  ep.turn_info[tb] = info;
+  ep.turn_exec[tb] = exec;
   if (err_out && err) err_out[b] |= err;
 #ifdef RMI_CD_STAMPS
   if ((threadIdx.x & 63) == 0) {
-    e.st[5] = __builtin_amdgcn_s_memtime();
-    for (int q = 0; q < kCdStamps; ++q) g_cd_stamps[(int64_t)blockIdx.x * kCdStamps + q] = e.st[q];
+    st[5] = __builtin_amdgcn_s_memtime();
+    for (int q = 0; q < kCdStamps; ++q) g_cd_stamps[(int64_t)blockIdx.x * kCdStamps + q] = st[q];
   }
 #endif
 }
