@@ -475,6 +475,7 @@ __global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(
     // separator candidates: positions of its first byte, full compare, greedy selection
     const int nc = collect(C, ca, cz, (uint32_t)(sep.lo & 0xFFu), ES, lane);
     wave_sync();
+    PSTAMP(7);
     int ns = 0, last = ca;  // selected separators -> EL (the '<' list is no longer needed)
     for (int c = 0; c < nc; c += 64) {
       const int i = c + lane;
@@ -499,6 +500,7 @@ __global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(
       }
     }
     wave_sync();
+    PSTAMP(8);
     // pieces: piece i = [i ? sel[i-1] + sep.n : ca, i < ns ? sel[i] : cz); one per lane
     for (int c = 0; c <= ns && count < K; c += 64) {
       const int i = c + lane;

@@ -2,7 +2,8 @@
 Builds parse.hip with RMI_PARSE_STAMPS into tools/_build/libparse_stamps.so (s_memtime per
 phase per wave) and prints the mean cycles of each phase at a few batch shapes.
   0 entry | 1 text staged | 2 '<' events classified | 3 regex match | 4 cascade/strip |
-  5 split + names | 6 stores"""
+  5 split + names | 6 stores; inside the split: 7 separator candidates collected, 8 separators
+  selected"""
 import ctypes, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -49,3 +50,7 @@ for B, tw, think in ((1024, (8, 60), True), (8192, (8, 60), True), (8192, (0, 2)
     print(f"B={B} words={tw} think={think}: wave span mean {np.mean(s[:, 6] - s[:, 0]):.0f} cyc, "
           f"grid span {span:.0f} cyc ({span / 2.4e3:.1f} us @2.4GHz)")
     print("   " + "  ".join(f"{nm}={d[:, i].mean():.0f}" for i, nm in enumerate(names)))
+    sp = s[:, 7] > 0  # rows with a match: the split's separator collect / greedy selection / pieces
+    if sp.any():
+        print(f"   split: collect={np.mean(s[sp, 7] - s[sp, 4]):.0f}  select={np.mean(s[sp, 8] - s[sp, 7]):.0f}  "
+              f"pieces={np.mean(s[sp, 5] - s[sp, 8]):.0f}")
