@@ -83,6 +83,7 @@ struct Fl4Out {
   TurnOut o;
   bool turn_done, succ_last;
   int s;
+  int nv;  // known-name actions among the first n_act slots
   Pcg64 rng;
 #ifdef RMI_STAMPS
   unsigned long long t_draws;  // diagnostic: s_memtime once the turn's draws are computed
@@ -117,6 +118,7 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
     cl |= use ? a << (8 * nv) : 0ull;
     nv += use ? 1 : 0;
   }
+  r.nv = nv;
   const int n_try = nv < left ? nv : (left > 0 ? left : 0);
   // the chain's next K states and outputs (draw k of the turn = output of state k + 1)
   uint64_t shi[K + 1], slo[K + 1], draw[K];
@@ -321,20 +323,16 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
       if (threadIdx.x == 0) g_stamps[blockIdx.x * 16 + 11] = f.t_draws;
 #endif
       // the format penalty (es_manager.py:158-159): not every parsed name known, or none
-      int nv = 0;
-      for (int k = 0; k < n_a; ++k) nv += ((acts >> (8 * k)) & 0xFF) != 0;
-      if (nv != n_a || nv == 0) penalty += in.format_penalty;
+      // (fl4_turn counted the known names; selects, no branches, down to the stores)
+      penalty = (f.nv != n_a) | (f.nv == 0) ? penalty + in.format_penalty : penalty;
       o = f.o;
-      e.s = f.s;
-      e.rng = f.rng;
       num_actions += o.exec;
       n_turns += 1;
-      if (f.turn_done) {
-        flags |= RMI_FLAG_TERMINATED | RMI_FLAG_DONE;
-        flags = f.succ_last ? (uint8_t)(flags & ~RMI_FLAG_TRUNCATED) : (uint8_t)(flags | RMI_FLAG_TRUNCATED);
-      } else if (num_actions >= in.max_actions_per_traj) {
-        flags |= RMI_FLAG_TERMINATED | RMI_FLAG_TRUNCATED | RMI_FLAG_DONE;
-      }
+      const uint8_t fd = (uint8_t)(RMI_FLAG_TERMINATED | RMI_FLAG_DONE);
+      const uint8_t f_done = f.succ_last ? (uint8_t)((flags | fd) & ~RMI_FLAG_TRUNCATED)
+                                         : (uint8_t)(flags | fd | RMI_FLAG_TRUNCATED);
+      const uint8_t f_cap = (uint8_t)(flags | fd | RMI_FLAG_TRUNCATED);
+      flags = f.turn_done ? f_done : (num_actions >= in.max_actions_per_traj ? f_cap : flags);
       stepped = true;
       ep.num_actions[b] = num_actions;
       ep.flags[b] = flags;
@@ -344,10 +342,11 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
       ep.turn_reward[tb] = o.acc;
       ep.turn_info[tb] = o.info;
       ep.turn_exec[tb] = o.exec;
-      if (o.stepped_any_state) {
-        env.s[b] = e.s;
-        store_pcg(env.rng, B, b, e.rng);
-      }
+      // s and the PCG64 state: written back whether or not a step ran (unchanged then)
+      e.s = f.s;
+      e.rng = f.rng;
+      env.s[b] = e.s;
+      store_pcg(env.rng, B, b, e.rng);
     }
   } else if (act) {
     if (e.s < 0 || e.s >= n) {
