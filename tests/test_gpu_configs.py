@@ -59,6 +59,42 @@ def _countdown_rollout(device, B=16384, T=4):
     return env, oep
 
 
+@pytest.mark.parametrize("use_has_input", [False, True])
+def test_countdown_multi_slot_cap_vs_oracle(device, use_has_input):
+    """The turn kernel's single-step form (countdown.hip: at most one step per turn, on slot 0)
+    against the oracle's general loop with K = 3 answer slots, 0..3 answers per turn, cap 2, and
+    (has_input) envs stepped again after they are done, so turns with no room left under the
+    cap (left <= 0) and turns after a done episode both occur."""
+    B, T, K, cap = 2048, 5, 3, 2
+    inst = synthetic_instances(256, 11)
+    env = CountdownBatch(CountdownEnvConfig(data=inst), B, T, K, device)
+    env.reset(synthetic.env_seeds(B))
+    mine = [inst[int(i)] for i in env.index]
+    nums = [list(m["nums"]) for m in mine]
+    targets = [int(m["target"]) for m in mine]
+    oep = oracle.Episode(B, T)
+    rng = np.random.default_rng(5)
+    zeros = torch.zeros(B, K, dtype=torch.int8, device=device)
+    has = np.ones(B, np.uint8)
+    has[rng.random(B) < 0.2] = 0
+    for t in range(T):
+        per_turn = [synthetic.countdown_answers(mine, 1, seed=100 * t + k, p_empty=0.0)[0] for k in range(K)]
+        lists = [[per_turn[k][b] for k in range(int(rng.integers(0, K + 1)))] for b in range(B)]
+        buf, lens = env.encode_answers(lists)
+        n = np.array([len(x) for x in lists], np.uint8)
+        err = torch.zeros(B, dtype=torch.uint8, device=device)
+        hi = _t(has, device) if use_has_input else None
+        env.step_turn(t, zeros, _t(n, device), hi, cap, -0.1, err, answers=_t(buf, device), answer_len=_t(lens, device))
+        oracle.countdown_turn(lists, nums, targets, oep, t, has if use_has_input else None, cap, -0.1)
+        torch.cuda.synchronize()
+        assert not err.any()
+        for k in EP_FIELDS:
+            np.testing.assert_array_equal(getattr(env.ep, k).cpu().numpy(), getattr(oep, k), err_msg=f"turn {t} {k}")
+    assert (oep.turn_exec <= 1).all() and (oep.turn_exec == 1).any()
+    if use_has_input:  # stepped again after done: the cap is reached, then turns with left <= 0
+        assert (oep.num_actions == cap).any()
+
+
 def test_countdown_config4_vs_oracle(device):
     env, oep = _countdown_rollout(device)
     B = env.B
