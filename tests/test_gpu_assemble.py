@@ -95,3 +95,50 @@ def test_assemble_edge_rows(device):
     assert pos.cpu().tolist() == [[0, 0, 0], [0, 0, 1], [1, 2, 3]]
     i, am, pos, sc, lm, rm = assemble_batch([[7], [SP]], tok, [[], []], False, False, device)
     assert i.cpu().tolist() == [[7], [SP]] and sc.shape == (2, 0)
+
+
+@pytest.mark.parametrize("S", [1, 2, 3, 5, 7, 64, 257, 1029])
+def test_assemble_ragged_shapes_vs_host(device, S):
+    """ops.assemble_batch over ragged rows of 0..S+5 tokens at widths S that are not multiples
+    of the kernel's 4-id groups: the 32-B group loads and stores, the element-wise pad edge and
+    row end, and rows longer than S (flagged RMI_ERR_STATE, their last S tokens kept) against
+    host left padding + cumsum and the oracle's masks / scores on the assembled ids."""
+    rng = np.random.default_rng(S)
+    B, T = 300, 4
+    rows = []
+    for b in range(B):
+        n = int(rng.integers(0, S + 6))
+        r = rng.integers(100, 1000, size=n).astype(np.int64)
+        r[rng.random(n) < 0.1] = SP
+        r[rng.random(n) < 0.05] = RT
+        rows.append(r)
+    lens = np.array([len(r) for r in rows], np.int64)
+    off = np.zeros(B + 1, np.int64)
+    off[1:] = np.cumsum(lens)
+    toks = np.concatenate(rows) if lens.sum() else np.zeros(1, np.int64)
+    sc = rng.choice([0.0, -0.1, 1.0, 10.9], size=(T, B))
+    n_sc = rng.integers(0, T + 1, size=B).astype(np.int32)
+    padded = np.full((B, S), PAD, np.int64)
+    am_ref = np.zeros((B, S), np.int64)
+    for b, r in enumerate(rows):
+        k = min(len(r), S)
+        if k:
+            padded[b, S - k:] = r[len(r) - k:]
+            am_ref[b, S - k:] = 1
+    for uts in (False, True):
+        ids, am, pos, score, lm, rm, err = ops.assemble_batch(
+            torch.from_numpy(toks).to(device), torch.from_numpy(off).to(device), S, PAD, SP, RT,
+            torch.from_numpy(sc).to(device), torch.from_numpy(n_sc).to(device), T, uts, True, True)
+        np.testing.assert_array_equal(ids.cpu().numpy(), padded)
+        np.testing.assert_array_equal(am.cpu().numpy(), am_ref)
+        np.testing.assert_array_equal(pos.cpu().numpy(), np.cumsum(am_ref, axis=1))
+        exp_err = lens > S  # RMI_ERR_STATE: an overlong row, or a row where the reference raises
+        if S > 1:
+            osc, olm, orm, oerr = oracle.masks_and_scores(padded, SP, RT, sc, n_sc, T, uts, True, True)
+            ok = np.asarray(oerr) == 0  # rows where the reference raises (a turn with two reward tokens) are flagged only
+            assert ok.sum() > B // 4
+            np.testing.assert_array_equal(score.cpu().numpy()[ok], osc[ok])
+            np.testing.assert_array_equal(lm.cpu().numpy().astype(np.uint8), olm)
+            np.testing.assert_array_equal(rm.cpu().numpy().astype(np.uint8), orm)
+            exp_err |= np.asarray(oerr) != 0
+        np.testing.assert_array_equal(err.cpu().numpy(), np.where(exp_err, 4, 0).astype(np.uint8))
