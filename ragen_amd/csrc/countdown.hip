@@ -1293,6 +1293,9 @@ __device__ __forceinline__ void stage_answer(const uint8_t* g, int from, int n, 
 // Per row (16 lanes, one env or answer) of LDS: the staged answer, lane 0's per-lane evaluator
 // stacks, the cooperative scratch.  64-thread blocks = 4 rows.
 constexpr int kCdBlock = 64;
+#ifndef RMI_CD_WPE
+#define RMI_CD_WPE 4
+#endif
 // 16 readable bytes for the clamped answer-head loads of rows without one
 __device__ __attribute__((aligned(16))) const uint32_t kZero16[4] = {0, 0, 0, 0};
 // a staged row is 16-B aligned and readable 80 bytes past its start (the token reads)
@@ -1312,7 +1315,7 @@ __device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b,
 // slot 0, when it has a parsed answer and the cap leaves room; the format penalty applies iff
 // it has none.  Straight-line, so the wave carries no loop state (the generic loop's hoisted
 // per-slot predicates spilled SGPRs and put ≈2 k cycles between the loads and the evaluator).
-__global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
+__global__ __launch_bounds__(kCdBlock) __attribute__((amdgpu_waves_per_eu(RMI_CD_WPE))) void countdown_step_turn_kernel(rmi_countdown_t env, rmi_episode_t ep,
                                                                        rmi_turn_t in,
                                                                        const uint8_t* __restrict__ answers,
                                                                        const int32_t* __restrict__ answer_len,
@@ -1412,7 +1415,7 @@ __global__ __launch_bounds__(kCdBlock) void countdown_step_turn_kernel(rmi_count
 #endif
 }
 
-__global__ __launch_bounds__(kCdBlock) void countdown_reward_kernel(rmi_countdown_t env,
+__global__ __launch_bounds__(kCdBlock) __attribute__((amdgpu_waves_per_eu(RMI_CD_WPE))) void countdown_reward_kernel(rmi_countdown_t env,
                                                                     const uint8_t* __restrict__ answers,
                                                                     const int32_t* __restrict__ answer_len, int Lmax,
                                                                     int n, double* __restrict__ reward,
