@@ -440,6 +440,12 @@ struct BilevelCarry {  // per row, replicated on the row's 16 lanes
   uint32_t h_valid, h_eos;
 };
 
+// lane 0 of each 16-lane DPP row, broadcast to the whole row (DPP row_newbcast:0): a VALU move,
+// where __shfl from the row's lead lane is a ds_bpermute and an LDS round trip per tile
+__device__ __forceinline__ int row_lead(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x150, 0xF, 0xF, false); }
+__device__ __forceinline__ uint32_t row_lead(uint32_t x) { return (uint32_t)row_lead((int)x); }
+__device__ __forceinline__ float row_lead(float x) { return __int_as_float(row_lead(__float_as_int(x))); }
+
 // inclusive suffix selection over the 16 column groups of a DPP row: (h, v) <- first (h, v) with
 // h set at or right of this group; lanes past the row end read h = 0 (bound_ctrl)
 __device__ __forceinline__ void row_suffix_first(uint32_t& h, float& v) {
@@ -518,9 +524,8 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
     nhe |= eos[e];
   }
   // the next tile to the left continues from this tile's leftmost valid / eos position
-  const int lead = lane & ~15;
-  const uint32_t row_hv = (uint32_t)__shfl((int)hsv, lead), row_he = (uint32_t)__shfl((int)hse, lead);
-  const float row_vv = __shfl(vsv, lead), row_ve = __shfl(vse, lead);
+  const uint32_t row_hv = row_lead(hsv), row_he = row_lead(hse);
+  const float row_vv = row_lead(vsv), row_ve = row_lead(vse);
   cy.v_valid = row_hv ? row_vv : cy.v_valid;
   cy.h_valid |= row_hv;
   cy.v_eos = row_he ? row_ve : cy.v_eos;
@@ -781,9 +786,8 @@ __device__ __forceinline__ void bs_tile(const GaeTile& cur, int64_t c0, BilevelC
     nve = eos[e] ? vv[e] : nve;
     nhe |= eos[e];
   }
-  const int lead = lane & ~15;
-  const uint32_t row_hv = (uint32_t)__shfl((int)hsv, lead), row_he = (uint32_t)__shfl((int)hse, lead);
-  const float row_vv = __shfl(vsv, lead), row_ve = __shfl(vse, lead);
+  const uint32_t row_hv = row_lead(hsv), row_he = row_lead(hse);
+  const float row_vv = row_lead(vsv), row_ve = row_lead(vse);
   cy.v_valid = row_hv ? row_vv : cy.v_valid;
   cy.h_valid |= row_hv;
   cy.v_eos = row_he ? row_ve : cy.v_eos;
@@ -798,7 +802,7 @@ __device__ __forceinline__ void bs_tile(const GaeTile& cur, int64_t c0, BilevelC
   // segment starts, right to left: this group's rank = starts in the row's groups to its right
   const int ns = __popc(st);
   const int incl = row_suffix_sum(ns);
-  const int tot = __shfl(incl, lead);
+  const int tot = row_lead(incl);
   int idx = nseg + incl - ns;
 #pragma unroll
   for (int e = 3; e >= 0; --e) {
