@@ -507,7 +507,11 @@ __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMax
 // kFirst: the launch is a fresh episode's first turn fused with the reset (rmi_sokoban_reset):
 // the rows and players come from init_state / init_player, the counters and the episode record
 // start at zero without being read, and every env's state and whole record are written.
-template <int HW, class M, int LPE, bool kFin, bool kFirst = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
+// kLate (large batches, plain turns): the rows are loaded after the activity test and only by
+// the lanes whose env acts this turn, a second memory round trip that a batch this size hides,
+// so the rows of done envs are not fetched (HBM-bound there: done envs were ≈18 % of the bench
+// rollout's env-turns, their rows ≈9 % of its traffic).
+template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
                                                                   uint8_t* __restrict__ err_out, rmi_finalize_t fin,
@@ -537,8 +541,10 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   uint32_t xs[NWL], xf[NWL];
 #pragma unroll
   for (int i = 0; i < NWL; ++i) xs[i] = xf[i] = 0;
-  load_row<NWL, LPE, HW != 0>((kFirst ? init_state : env.room_state) + bc * hw, xs, sub, row_words);
-  load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+  if (!kLate) {
+    load_row<NWL, LPE, HW != 0>((kFirst ? init_state : env.room_state) + bc * hw, xs, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+  }
   const int8_t* pl = kFirst ? init_player : env.player;
   int r = pl[2 * bc], c = pl[2 * bc + 1];
   // branch-free: a conditional load here would make the compiler wait for the rows first
@@ -561,6 +567,10 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   if (kFin) rec.load(ep, bc);
   if (!live) flags = RMI_FLAG_DONE;
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
+  if (kLate && act) {
+    load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+  }
   RMI_STAMP_WAIT(1);
   if (kFirst && live) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);  // the reset
 
@@ -814,6 +824,9 @@ __global__ __launch_bounds__(kBlock) void sokoban_reset_kernel(rmi_sokoban_t env
 }  // namespace
 }  // namespace rmi
 
+#ifndef RMI_SOK_LATE_MIN
+#define RMI_SOK_LATE_MIN (1 << 17)  // envs from which plain turns take the late row loads (kLate)
+#endif
 namespace rmi {
 namespace {
 template <bool kFin, bool kFirst = false>
@@ -830,6 +843,7 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
   const bool w32 = (H - 1) * W <= 32;  // the board window fits a u32
   // lanes per env: spread a batch too small to fill the chip over 4 lanes per env
   const bool spread = spread_lanes(ep->B);
+  const bool late = !kFin && !kFirst && !spread && ep->B >= RMI_SOK_LATE_MIN;
 #define RMI_LAUNCH(HW_, M_)                                                                                   \
   do {                                                                                                        \
     if (spread)                                                                                               \
@@ -838,7 +852,12 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
                                          (kWave * kSokWpb / kSpreadLpe))),                                   \
                          dim3(kWave * kSokWpb), 0, s, *env, *ep, *in, hw, border, err, fin, init_state,      \
                          init_player);                                                                        \
-    else                                                                                                      \
+    else if (late) {                                                                                          \
+      if constexpr (!kFin && !kFirst)                                                                         \
+        hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, false, false, true>), dim3(grid),           \
+                           dim3(kWave * kSokWpb), 0, s, *env, *ep, *in, hw, border, err, fin, init_state,    \
+                           init_player);                                                                      \
+    } else                                                                                                    \
       hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, kFirst>), dim3(grid), dim3(kWave * kSokWpb), \
                          0, s,                                                                                \
                          *env, *ep, *in, hw, border, err, fin, init_state, init_player);                      \

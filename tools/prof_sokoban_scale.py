@@ -1,12 +1,12 @@
 """Sokoban turn kernel at scale under different lanes-per-env layouts (diagnostic).
 Builds variants of libragen_amd.so into tools/_build/ (compile-time switches of sokoban.hip,
-e.g. RMI_SOKOBAN_DWORD_STORES), then times 5 turn launches at B = 8192 * tile in a child
-process each.
+e.g. RMI_SOK_LATE_MIN, RMI_SOKOBAN_DWORD_STORES), then times 5 turn launches at B = 8192 * tile
+in a child process each.
 usage: python tools/prof_sokoban_scale.py [build]"""
 import os, subprocess, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "tools", "_build")
-VARIANTS = {"default": [], "dwordstore": ["-DRMI_SOKOBAN_DWORD_STORES"]}
+VARIANTS = {"default": [], "nolate": ["-DRMI_SOK_LATE_MIN=0x7fffffff"]}  # also: ["-DRMI_SOKOBAN_DWORD_STORES"]
 TILES = (1, 16, 128, 512)  # 8192 .. 4 194 304 envs (the last one past the 256 MiB Infinity Cache)
 
 
