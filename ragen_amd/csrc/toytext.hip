@@ -16,6 +16,10 @@ namespace {
 // One wave per workgroup for the turn kernels: a turn is a latency-bound chain per env, and
 // 4096 envs in 256-thread blocks would occupy only 16 CUs (64 one-wave blocks spread over 64).
 constexpr int kToyBlock = 64;
+#ifndef RMI_FL_BLOCK
+#define RMI_FL_BLOCK 64
+#endif
+constexpr int kFlBlock = RMI_FL_BLOCK;  // FrozenLake turn: threads per workgroup (envs, one per lane)
 
 struct FrozenLakeDev {
   const uint8_t* desc;  // this env's row
@@ -222,13 +226,13 @@ __device__ __forceinline__ Fl4Out fl4_dispatch(int K, uint32_t hole, uint32_t go
 // contiguous groups of fin.group_size envs (each group inside the launch's one wave): every
 // lane, live or not, reaches the group shuffles of finalize_envs.
 template <bool kFirst, bool kFin>
-__global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
+__global__ __launch_bounds__(kFlBlock) void frozenlake_step_turn_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
                                                                          rmi_turn_t in, uint8_t* __restrict__ err_out,
                                                                          const uint8_t* __restrict__ init_desc,
                                                                          const int32_t* __restrict__ init_s,
                                                                          const uint64_t* __restrict__ init_rng,
                                                                          rmi_finalize_t fin) {
-  const int64_t b = (int64_t)blockIdx.x * kToyBlock + threadIdx.x;
+  const int64_t b = (int64_t)blockIdx.x * kFlBlock + threadIdx.x;
   const int B = ep.B;
   if (!kFin && b >= B) return;
   const bool live = b < B;
@@ -320,11 +324,11 @@ __global__ __launch_bounds__(kToyBlock) void frozenlake_step_turn_kernel(rmi_fro
                                     e.slippery, draw_threshold(e.cs0), draw_threshold(e.cs1), draw_threshold(e.cs2));
       RMI_STAMP(3);
 #ifdef RMI_STAMPS
-      if (threadIdx.x == 0) g_stamps[blockIdx.x * 16 + 11] = f.t_draws;
+      if ((threadIdx.x & 63) == 0) g_stamps[(blockIdx.x * blockDim.x + threadIdx.x) / 64 * 16 + 11] = f.t_draws;
 #endif
       // the format penalty (es_manager.py:158-159): not every parsed name known, or none
       // (fl4_turn counted the known names; selects, no branches, down to the stores)
-      penalty = (f.nv != n_a) | (f.nv == 0) ? penalty + in.format_penalty : penalty;
+      penalty = ((f.nv != n_a) | (f.nv == 0)) ? penalty + in.format_penalty : penalty;
       o = f.o;
       num_actions += o.exec;
       n_turns += 1;
@@ -492,8 +496,8 @@ RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_epis
   const int rc = check_turn_args(ep, in);
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
-  const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
-  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, false>), dim3(grid), dim3(kToyBlock), 0, as_stream(stream),
+  const unsigned grid = (unsigned)((ep->B + kFlBlock - 1) / kFlBlock);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, false>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
                      *env, *ep, *in, err, nullptr, nullptr, nullptr, rmi_finalize_t{});
   return launch_status();
 }
@@ -507,8 +511,8 @@ RMI_API int rmi_frozenlake_step_turn_first(const rmi_frozenlake_t* env, const rm
   const int rc = check_turn_args(ep, in);
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->desc || !env->s || !env->rng || !init_desc || !init_s || !init_rng) return RMI_EINVAL;
-  const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
-  hipLaunchKernelGGL((frozenlake_step_turn_kernel<true, false>), dim3(grid), dim3(kToyBlock), 0, as_stream(stream),
+  const unsigned grid = (unsigned)((ep->B + kFlBlock - 1) / kFlBlock);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<true, false>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
                      *env, *ep, *in, err, init_desc, init_s, init_rng, rmi_finalize_t{});
   return launch_status();
 }
@@ -525,11 +529,11 @@ RMI_API int rmi_frozenlake_step_turn_finalize(const rmi_frozenlake_t* env, const
   if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
   if (fin->method < 0 || fin->method > 3 || fin->group_size < 1) return RMI_EINVAL;
   // every group inside the one-wave workgroup, and no partial group
-  if (kToyBlock % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;
+  if (64 % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;  // groups inside one wave
   rmi_finalize_t f = *fin;
   if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member
-  const unsigned grid = (unsigned)((ep->B + kToyBlock - 1) / kToyBlock);
-  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, true>), dim3(grid), dim3(kToyBlock), 0, as_stream(stream),
+  const unsigned grid = (unsigned)((ep->B + kFlBlock - 1) / kFlBlock);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, true>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
                      *env, *ep, *in, err, nullptr, nullptr, nullptr, f);
   return launch_status();
 }
