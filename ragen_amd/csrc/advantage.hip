@@ -986,19 +986,16 @@ __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict
       float oa[4], oq[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        if ((f >> e) & 1u) {  // valid: the low-level walk
-          oa[e] = aa[e];
-          oq[e] = aa[e] + vv[e];
-          s1 += (double)aa[e];
-          s2 += (double)aa[e] * (double)aa[e];
-          cnt += 1.0;
-        } else if ((f >> (4 + e)) & 1u) {  // eos outside the mask: the high level (ret = adv + v)
-          oa[e] = aa[e];
-          oq[e] = aa[e] + vv[e];
-        } else {
-          oa[e] = 0.0f;
-          oq[e] = 0.0f;
-        }
+        // valid: the low-level walk; eos outside the mask: the high level (ret = adv + v); else 0.
+        // Selects, not branches: an invalid column adds +0.0 to the row sums, which leaves them
+        // unchanged (they start at +0.0, so they are never -0.0)
+        const bool va = (f >> e) & 1u, out = ((f >> e) | (f >> (4 + e))) & 1u;
+        oa[e] = out ? aa[e] : 0.0f;
+        oq[e] = out ? aa[e] + vv[e] : 0.0f;
+        const double ad = va ? (double)aa[e] : 0.0;
+        s1 += ad;
+        s2 += ad * ad;
+        cnt += va ? 1.0 : 0.0;
       }
       if (live) {
         const int64_t go = grow * L + c;
