@@ -776,8 +776,11 @@ __device__ __forceinline__ void bs_tile(const GaeTile& cur, int64_t c0, BilevelC
   uint32_t fl = 0, st = 0;
 #pragma unroll
   for (int e = 3; e >= 0; --e) {
-    if (eos[e]) d[e] = (rr[e] + (nhe ? hg * nve : 0.0f)) - vv[e];  // high-level delta
-    else d[e] = (rr[e] + g * (nhv ? nvv : 0.0f)) - vv[e];           // low level (upd = reward)
+    // high-level delta (r + (next eos ? hg * v_next_eos : 0)) - v, or the low level's
+    // (r + g * (next valid ? v_next_valid : 0)) - v (upd = reward): each element's own f32
+    // operations, with the add and the subtract shared
+    const float t = eos[e] ? (nhe ? hg * nve : 0.0f) : g * (nhv ? nvv : 0.0f);
+    d[e] = (rr[e] + t) - vv[e];
     bad |= valid[e] & (eos[e] ^ 1u) & (nhv ^ 1u);                    // valid_positions[i + 1]
     st |= (valid[e] & (eos[e] | (nhv ^ 1u))) << e;                   // segment start
     fl |= (valid[e] << e) | (eos[e] << (4 + e));
