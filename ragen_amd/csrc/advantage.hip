@@ -975,7 +975,8 @@ __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict
   __syncthreads();
   BL_T(tb2);
   // ---- P4: outputs and row stats; v re-read (an L2 hit) 8 tiles' groups at a time
-  double s1 = 0.0, s2 = 0.0, cnt = 0.0;
+  double s1 = 0.0, s2 = 0.0;
+  int icnt = 0;  // the valid-column count (a sum of 1.0s is exact: counted as an integer)
   for (int64_t cb = 4 * grp; cb < L; cb += 8 * kGCols) {
     F4 cur[8];
     bs_load_v(cur, vrow, cb, L);
@@ -998,7 +999,7 @@ __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict
         const double ad = va ? (double)aa[e] : 0.0;
         s1 += ad;
         s2 += ad * ad;
-        cnt += va ? 1.0 : 0.0;
+        icnt += (int)va;
       }
       if (live) {
         const int64_t go = grow * L + c;
@@ -1015,7 +1016,7 @@ __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict
       }
     }
   }
-  const double a = xor_sum16(s1), b2 = xor_sum16(s2), n = xor_sum16(cnt);
+  const double a = xor_sum16(s1), b2 = xor_sum16(s2), n = xor_sum16((double)icnt);
   const uint64_t bads = __ballot(bad);
 #ifdef RMI_BL_STAMPS
   BL_T(tb3);
