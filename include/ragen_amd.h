@@ -297,8 +297,8 @@ int rmi_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64_t speci
  * (ctx_manager.py:278-306): the tokenizer's left padding (padding_side="left"), attention_mask,
  * position_ids = attention_mask.cumsum(-1), and get_masks_and_scores on the padded ids — in ONE
  * pass.  Row b is pad_id * (S - n_b) then tokens[row_off[b] .. row_off[b+1]) (n_b tokens,
- * ragged rows back to back; S >= max n_b, else the row is flagged RMI_ERR_STATE and keeps its
- * last S tokens).  Outputs input_ids / attention_mask / position_ids i64[B,S] (responses =
+ * ragged rows back to back; S >= max n_b, else the row is flagged RMI_ERR_UNSUP and keeps its
+ * last S tokens; RMI_ERR_STATE as in rmi_masks_and_scores).  Outputs input_ids / attention_mask / position_ids i64[B,S] (responses =
  * input_ids[:, 1:] is a view) and the rmi_masks_and_scores outputs with the same arguments.  */
 int rmi_assemble_batch(const int64_t* tokens, const int64_t* row_off, int64_t B, int64_t S, int64_t pad_id,
                        int64_t special_token, int64_t reward_token, const double* scores, const int32_t* n_scores,

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
     const int64_t o0 = as.off[b], o1 = as.off[b + 1];
     pad = S - (o1 - o0);
     if (pad < 0) {  // a row longer than S: flagged, assembled from its last S tokens
-      if (lane == 0) err[b] |= RMI_ERR_STATE;
+      if (lane == 0) err[b] |= RMI_ERR_UNSUP;
       a_src = o1 - S;
       pad = 0;
     } else {

@@ -38,54 +38,64 @@ def shard_groups(n_groups: int, world_size: int, rank: int) -> Tuple[int, int]:
     return lo, hi - lo
 
 
-def _staged(x: torch.Tensor) -> torch.Tensor:
+def _staged(x: torch.Tensor, group=None) -> torch.Tensor:
     """gloo moves host memory: a GPU tensor goes through a host copy (RCCL takes it directly)."""
-    if x.is_cuda and dist.get_backend() == "gloo":
+    if x.is_cuda and dist.get_backend(group) == "gloo":
         return x.cpu()
     return x
 
 
-def all_gather_rows(x: torch.Tensor, with_offset: bool = False):
+def all_reduce_max(x: torch.Tensor, group=None) -> torch.Tensor:
+    """Element-wise max over the ranks of ``group`` (the default group if None); the local
+    tensor without a process group."""
+    if not initialized():
+        return x
+    xs = _staged(x.contiguous().clone(), group)
+    dist.all_reduce(xs, op=dist.ReduceOp.MAX, group=group)
+    return xs.to(x.device)
+
+
+def all_gather_rows(x: torch.Tensor, with_offset: bool = False, group=None):
     """Concatenate every rank's [n_r, ...] rows in rank order (n_r may differ by rank).
     Whenever a process group exists the collective runs (also at world size 1, so the one-GPU
     tests exercise the RCCL path); without one the local rows are returned.
     with_offset: -> (rows, this rank's first row in the result)."""
     if not initialized():
         return (x, 0) if with_offset else x
-    W, rank = world()
-    xs = _staged(x.contiguous())
+    W, rank = dist.get_world_size(group), dist.get_rank(group)
+    xs = _staged(x.contiguous(), group)
     n = torch.tensor([xs.shape[0]], dtype=torch.int64, device=xs.device)
     sizes = [torch.zeros_like(n) for _ in range(W)]
-    dist.all_gather(sizes, n)
+    dist.all_gather(sizes, n, group=group)
     sizes = [int(s) for s in torch.cat(sizes).cpu().tolist()]
     m = max(sizes)
     pad = torch.zeros((m,) + tuple(xs.shape[1:]), dtype=xs.dtype, device=xs.device)
     pad[:xs.shape[0]] = xs
     bufs = [torch.empty_like(pad) for _ in range(W)]
-    dist.all_gather(bufs, pad)
+    dist.all_gather(bufs, pad, group=group)
     out = torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0).to(x.device)
     return (out, sum(sizes[:rank])) if with_offset else out
 
 
-def global_whiten_stats(row_stats: torch.Tensor) -> torch.Tensor:
+def global_whiten_stats(row_stats: torch.Tensor, group=None) -> torch.Tensor:
     """[n_local, 3] f64 (sum, sum_sq, count) -> [n_global, 3] in global row order."""
-    return all_gather_rows(row_stats)
+    return all_gather_rows(row_stats, group=group)
 
 
-def gather_group_scores(scores: torch.Tensor, group_size: int, with_offset: bool = False):
+def gather_group_scores(scores: torch.Tensor, group_size: int, with_offset: bool = False, group=None):
     """Per-env trajectory scores of the local groups -> all groups' scores (global order);
     with_offset also returns the first global GROUP index of this rank."""
     assert scores.shape[0] % group_size == 0
-    rows, off = all_gather_rows(scores.view(-1, group_size), with_offset=True)
+    rows, off = all_gather_rows(scores.view(-1, group_size), with_offset=True, group=group)
     return (rows.reshape(-1), off) if with_offset else rows.reshape(-1)
 
 
-def global_filter(local_scores: torch.Tensor, group_size: int, select: Callable):
+def global_filter(local_scores: torch.Tensor, group_size: int, select: Callable, group=None):
     """The rollout filter over the GLOBAL batch (agent_trainer.py:461-500 ranks groups across all
     of them): every rank gathers every group's scores, runs the same deterministic
     ``select(all_scores, num_groups) -> (keep u8[G], metrics)`` and keeps its own slice.
     -> (keep of the local groups, metrics)."""
-    all_scores, g0 = gather_group_scores(local_scores, group_size, with_offset=True)
+    all_scores, g0 = gather_group_scores(local_scores, group_size, with_offset=True, group=group)
     G = all_scores.numel() // group_size
     keep, metrics = select(all_scores, G)
     n_local = local_scores.shape[0] // group_size

@@ -14,7 +14,7 @@ from typing import Dict, List
 import numpy as np
 import torch
 
-from .. import ops
+from .. import _lib, ops
 from ..env import REGISTERED_ENV_CONFIGS
 from ..torch_ops import NORM
 from ..protocol import DataProto
@@ -78,10 +78,20 @@ def assemble_batch(rows, tokenizer, all_scores, use_turn_scores: bool, enable_re
         S, int(pad), int(special_token), int(reward_token), tab, n, T, bool(use_turn_scores),
         bool(enable_response_mask), "qwen" in tokenizer.name_or_path.lower())
     ids, am, pos, score, lm, rm, err = out
-    if use_turn_scores and bool(err.any()):
+    _raise_assemble_errors(err, S)
+    return ids, am, pos, score, lm, rm
+
+
+def _raise_assemble_errors(err, S):
+    """rmi_assemble_batch's per-row bits: RMI_ERR_UNSUP = a row longer than the batch width S
+    (it would have been truncated), RMI_ERR_STATE = a turn with more than one reward-token
+    position (the reference's boolean-mask score assignment raises there)."""
+    overlong, multi = torch.stack([(err & _lib.ERR_UNSUP).any(), (err & _lib.ERR_STATE).any()]).cpu().tolist()
+    if overlong:
+        raise ValueError(f"a token row is longer than the batch width S={S}")
+    if multi:
         raise RuntimeError("shape mismatch: a turn has more than one reward-token position "
                            "(reference score_tensor[reward_position] = scores)")
-    return ids, am, pos, score, lm, rm
 
 
 SPECIAL_TOKENS = ["<think>", "</think>", "<answer>", "</answer>", "<|im_start|>", "<|im_end|>"]

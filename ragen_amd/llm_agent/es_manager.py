@@ -333,6 +333,12 @@ class EnvStateManager:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
         dev = self.device
+        # a generation the device decode truncated (row stride cap) or could not decode (an id
+        # outside the vocabulary) must not be stepped on: checked before the turn runs
+        if bool(inp.err.any()):
+            bad = int(torch.nonzero(inp.err)[0, 0])
+            raise ValueError(f"env {bad}: the decoded generation exceeded the device row buffer or held an id "
+                             "outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP)")
         has = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
         has[inp.env_ids_t] = 1
         err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
@@ -340,10 +346,19 @@ class EnvStateManager:
         parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
         obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
         self._device_turns.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs,
-                                   "spans": [p["spans"] for p in parsed]})
+                                   "spans": [p["spans"] for p in parsed], "parsed": parsed})
         flags = self.tags[0].batch.ep.flags if len(self.tags) == 1 else \
             torch.cat([tg.batch.ep.flags for tg in self.tags])
-        still = ((flags[inp.env_ids_t] & _lib.FLAG_DONE) == 0).cpu().numpy()
+        # one device -> host copy: the active set and the turn's per-env error bits, raised in
+        # the step where they happen, as the reference raises inside its per-env loop
+        n_in = len(inp.env_ids)
+        host = torch.cat([((flags[inp.env_ids_t] & _lib.FLAG_DONE) == 0).to(torch.uint8), err]).cpu().numpy()
+        still, err_h = host[:n_in].astype(bool), host[n_in:]
+        if err_h.any():
+            for tg in self.tags:
+                gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]
+                self._raise_errors(tg, err_h[tg.lo:tg.hi], [g - tg.lo for g in gids], gids)
+            self._device_turns[-1]["err_seen"] = True
         return LazyEnvOutputs(self, inp.env_ids[still])
 
     def _materialize(self):
@@ -380,7 +395,8 @@ class EnvStateManager:
                 inputs = [{"llm_response": lr, "llm_raw_response": raw} for (lr, _), raw in zip(parsed, raws)]
                 acts_l = [a for _, a in parsed]
                 m_l = tg.batch.map_actions_many(rows, acts_l)
-                self._raise_errors(tg, err[tg.lo:tg.hi], rows, gids)
+                if not d.get("err_seen"):
+                    self._raise_errors(tg, err[tg.lo:tg.hi], rows, gids)
                 tr, ti, te, fl, pen = rec[j]
                 num_actions = te[:t + 1].astype(np.int64).sum(0)
                 obs = ops.decode_rows(*d["obs"][j]) if j in d["obs"] else None

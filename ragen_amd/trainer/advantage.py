@@ -25,10 +25,12 @@ def compute_response_mask(data: DataProto) -> torch.Tensor:
 
 
 def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_repeat=1, multi_turn=False,
-                      norm_adv_by_std_in_grpo=True, bi_level_gae=False, high_level_gamma=1.0):
+                      norm_adv_by_std_in_grpo=True, bi_level_gae=False, high_level_gamma=1.0, process_group=None):
     """agent_trainer.py:60-137: GAE (verl, or RAGEN's bi-level), GRPO, REINFORCE++ (and its
     baseline form), REMAX and RLOO, each on the engine's kernels; an unknown estimator raises
-    NotImplementedError as the reference does."""
+    NotImplementedError as the reference does.  ``process_group``: the batch is this rank's
+    shard and whitening uses the statistics of the whole sharded batch (core_algos)."""
+    pg = {"process_group": process_group}
     if "response_mask" not in data.batch:
         data.batch["response_mask"] = compute_response_mask(data)
     est = getattr(adv_estimator, "value", adv_estimator)
@@ -36,10 +38,10 @@ def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_re
         if bi_level_gae:
             adv, ret = core_algos.compute_bi_level_gae_advantage_return(
                 data.batch["token_level_rewards"], data.batch["values"], data.batch["response_mask"], gamma, lam,
-                high_level_gamma)
+                high_level_gamma, **pg)
         else:
             adv, ret = core_algos.compute_gae_advantage_return(
-                data.batch["token_level_rewards"], data.batch["values"], data.batch["response_mask"], gamma, lam)
+                data.batch["token_level_rewards"], data.batch["values"], data.batch["response_mask"], gamma, lam, **pg)
     elif est == AdvantageEstimator.GRPO:
         mask = data.batch["response_mask"]
         if multi_turn:
@@ -49,10 +51,10 @@ def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_re
                                                              norm_adv_by_std_in_grpo=norm_adv_by_std_in_grpo)
     elif est == AdvantageEstimator.REINFORCE_PLUS_PLUS_BASELINE:
         adv, ret = core_algos.compute_reinforce_plus_plus_baseline_outcome_advantage(
-            data.batch["token_level_rewards"], data.batch["response_mask"], data.non_tensor_batch["uid"])
+            data.batch["token_level_rewards"], data.batch["response_mask"], data.non_tensor_batch["uid"], **pg)
     elif est == AdvantageEstimator.REINFORCE_PLUS_PLUS:
         adv, ret = core_algos.compute_reinforce_plus_plus_outcome_advantage(
-            data.batch["token_level_rewards"], data.batch["response_mask"], gamma)
+            data.batch["token_level_rewards"], data.batch["response_mask"], gamma, **pg)
     elif est == AdvantageEstimator.REMAX:
         adv, ret = core_algos.compute_remax_outcome_advantage(
             data.batch["token_level_rewards"], data.batch["reward_baselines"], data.batch["response_mask"])
@@ -70,11 +72,12 @@ FILTER_METRICS = ("rollout/in_group_std", "rollout/in_group_max", "rollout/in_gr
                   "rollout/chosen_in_group_std", "rollout/chosen_in_group_max", "rollout/chosen_in_group_mean")
 
 
-def filter_rollout(batch: DataProto, num_groups: int, group_size: int, ratio: float, ftype: str):
+def filter_rollout(batch: DataProto, num_groups: int, group_size: int, ratio: float, ftype: str,
+                   process_group=None):
     """_filter_rollout (agent_trainer.py:461-500): returns (filtered batch, metrics).
 
     Tie order among equal in-group std values: ascending group index (documented deviation:
-    torch.topk's choice among ties is implementation-defined).  With a process group the
+    torch.topk's choice among ties is implementation-defined).  With ``process_group`` the
     batch is this rank's shard: the groups are ranked over every rank's scores
     (ragen_amd.distributed.global_filter), so the kept set equals the 1-GPU run's and
     ``num_groups`` is the GLOBAL count (es_manager.train.env_groups), as in the reference."""
@@ -90,8 +93,8 @@ def filter_rollout(batch: DataProto, num_groups: int, group_size: int, ratio: fl
         keep, met, _, _, _ = torch.ops.ragen_amd.filter_groups(scores, G, group_size, float(ratio), FILTER[ftype])
         return keep, met
 
-    if rd.initialized():
-        keep, met = rd.global_filter(rows, group_size, select)
+    if process_group is not None:
+        keep, met = rd.global_filter(rows, group_size, select, group=process_group)
     else:
         keep, met = select(rows, rows.numel() // group_size if rows.numel() % group_size == 0 else -1)
     metrics = dict(zip(FILTER_METRICS, met.cpu().tolist()))

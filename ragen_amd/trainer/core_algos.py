@@ -3,14 +3,17 @@ the verl functions RAGEN imports from it (App. A.4): same names, signatures and 
 values.  Tensors may arrive on the CPU (as in the reference trainer, whose batch lives on the
 driver) and go back there; GPU tensors stay on their own device.
 
-No host synchronisation inside an estimator: the only wait is the copy of the results back to
-a CPU caller, and verl's error cases (mask sum 0 or 1 -> ValueError; bi-level IndexError,
-core_algos.py:79) are read from the device after that copy.  Results that stay on the device
-are not checked (reading the flag would be the sync the engine avoids).
+Errors are raised where verl / RAGEN raise them (mask sum 0 or 1 -> ValueError; bi-level
+IndexError, core_algos.py:79): the kernels write a status word and per-row error bits, and
+the estimator reads them once (``check=True``, the default) — for a CPU caller after the copy
+of the results back, for a GPU caller with one small device -> host read.  ``check=False``
+leaves GPU results unchecked and the estimator free of host synchronisation.
 
-With a process group initialised (one rank per GPU, ragen_amd.distributed) the whitening
-statistics are batch-global: every rank all-gathers the per-row fp64 partials and reduces
-them in global row order, so a sharded batch whitens exactly like the whole batch.
+Batch-global whitening over a sharded batch is opt-in: ``process_group=<group>`` makes every
+rank all-gather the per-row fp64 partials and reduce them in global row order, so the shards
+whiten exactly like the whole batch; the error flags are then reduced over the group before
+anything is raised, so every rank raises together.  Without it the statistics are this
+process's rows only, whatever torch.distributed state exists.
 """
 from collections import OrderedDict
 
@@ -33,28 +36,42 @@ def _dev(x, device):
     return x.to(device, non_blocking=True).contiguous()
 
 
-def _whiten(adv, mask, row_stats):
-    """In place; -> device status i32[1] (0 ok; 1 / 2 = verl's ValueError cases)."""
-    if rd.initialized():
-        return torch.ops.ragen_amd.masked_whiten_stats_(adv, rd.global_whiten_stats(row_stats))
+def _whiten(adv, mask, row_stats, group=None):
+    """In place; -> device status i32[1] (0 ok; 1 / 2 = verl's ValueError cases).  With a
+    process group the statistics are the whole sharded batch's (opt-in, module docstring)."""
+    if group is not None:
+        return torch.ops.ragen_amd.masked_whiten_stats_(adv, rd.global_whiten_stats(row_stats, group))
     return torch.ops.ragen_amd.masked_whiten_(adv, mask, row_stats)
 
 
-def _back(out_device, tensors, status=None, err=None):
-    """Results to the caller's device.  For a CPU caller the copy is the one sync; the error
-    flags written by the kernels are read after it."""
-    if out_device.type == "cuda":
-        return [t.to(out_device) for t in tensors]
+def _back(out_device, tensors, status=None, err=None, check=True, group=None):
+    """Results to the caller's device, then the error flags the kernels wrote (one small read;
+    for a CPU caller it follows the copy).  Under a process group the flags are reduced over it
+    first, so a bad row on one rank raises on every rank instead of stranding the others."""
     res = [t.to(out_device) for t in tensors]
+    if not check and out_device.type == "cuda":
+        return res
+    flags = []
     if status is not None:
-        ops.raise_whiten_status(int(status.cpu()))
-    if err is not None and bool(err.any().cpu()):
+        flags.append(status.reshape(-1)[:1].to(torch.int64))
+    if err is not None:
+        flags.append(err.any().reshape(1).to(torch.int64))
+    if not flags:
+        return res
+    f = torch.cat(flags)
+    if group is not None:
+        f = rd.all_reduce_max(f, group)
+    f = f.cpu().tolist()
+    if status is not None:
+        ops.raise_whiten_status(int(f[0]))
+    if err is not None and f[-1]:
         raise IndexError("index out of range: last loss-mask position of a row carries no reward "
                          "(reference core_algos.py:79)")
     return res
 
 
-def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True) -> torch.Tensor:
+def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True, check: bool = True,
+                  process_group=None) -> torch.Tensor:
     """verl masked_whiten; ValueError for a mask sum of 0 or 1 like verl's masked_var."""
     if not shift_mean:
         raise NotImplementedError("shift_mean=False is not used by RAGEN")
@@ -62,11 +79,12 @@ def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = T
     x = _dev(values.float(), dev).clone()
     m = _dev(mask, dev)
     stats = torch.ops.ragen_amd.whiten_row_stats(x, m)
-    status = _whiten(x, m, stats)
-    return _back(values.device, [x], status)[0]
+    status = _whiten(x, m, stats, process_group)
+    return _back(values.device, [x], status, check=check, group=process_group)[0]
 
 
-def compute_gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam, variant="legacy"):
+def compute_gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam, variant="legacy",
+                                 check=True, process_group=None):
     """verl compute_gae_advantage_return (legacy form by default)."""
     dev = _device(token_level_rewards, values, response_mask)
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(response_mask, dev)
@@ -74,19 +92,20 @@ def compute_gae_advantage_return(token_level_rewards, values, response_mask, gam
     if variant not in VARIANT:
         raise ValueError(f"GAE variant must be 'legacy' or 'masked', got {variant!r}")
     adv, ret = torch.ops.ragen_amd.gae(r, v, m, float(gamma), float(lam), VARIANT[variant], stats)
-    status = _whiten(adv, m, stats)
-    return tuple(_back(token_level_rewards.device, [adv, ret], status))
+    status = _whiten(adv, m, stats, process_group)
+    return tuple(_back(token_level_rewards.device, [adv, ret], status, check=check, group=process_group))
 
 
-def compute_bi_level_gae_advantage_return(token_level_rewards, values, loss_mask, gamma, lam, high_level_gamma):
+def compute_bi_level_gae_advantage_return(token_level_rewards, values, loss_mask, gamma, lam, high_level_gamma,
+                                          check=True, process_group=None):
     """core_algos.py:4-92 (IndexError where the reference raises it, core_algos.py:79)."""
     dev = _device(token_level_rewards, values, loss_mask)
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(loss_mask, dev)
     stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
     err = torch.empty(r.shape[0], dtype=torch.uint8, device=dev)
     adv, ret = torch.ops.ragen_amd.bilevel_gae(r, v, m, float(gamma), float(lam), float(high_level_gamma), stats, err)
-    status = _whiten(adv, m, stats)
-    return tuple(_back(token_level_rewards.device, [adv, ret], status, err))
+    status = _whiten(adv, m, stats, process_group)
+    return tuple(_back(token_level_rewards.device, [adv, ret], status, err, check=check, group=process_group))
 
 
 def _grouped(r, m, index, dev, run):
@@ -128,20 +147,21 @@ def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, ep
 # verl's published core_algos (the v0.3 line RAGEN pins through vllm 0.8.2); parity unpinned
 # beyond that restatement (tests/verl_restated.py runs it on CPU torch as the checker).
 
-def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, gamma):
+def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, gamma, check=True,
+                                                  process_group=None):
     """verl: returns = right-to-left running = r + gamma * running, reset by the mask;
     advantages = masked_whiten(returns, mask) * mask."""
     dev = _device(token_level_rewards, response_mask)
     r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
     stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
     adv, ret = torch.ops.ragen_amd.reinforce_pp_returns(r, m, float(gamma), stats)
-    status = _whiten(adv, m, stats)
+    status = _whiten(adv, m, stats, process_group)
     torch.ops.ragen_amd.mask_mul_(adv, m)
-    return tuple(_back(token_level_rewards.device, [adv, ret], status))
+    return tuple(_back(token_level_rewards.device, [adv, ret], status, check=check, group=process_group))
 
 
 def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, response_mask, index,
-                                                           epsilon: float = 1e-6):
+                                                           epsilon: float = 1e-6, check=True, process_group=None):
     """verl: score = sum_t r minus its group's mean (0 for a single-row group), tiled over the
     mask, then masked_whiten(., mask) * mask.  -> (adv, adv)."""
     dev = _device(token_level_rewards, response_mask)
@@ -149,9 +169,9 @@ def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, 
     adv = _grouped(r, m, index, dev, lambda rr, mm, seg: torch.ops.ragen_amd.grpo_outcome(
         rr, mm, seg, float(epsilon), False)[0])
     stats = torch.ops.ragen_amd.whiten_row_stats(adv, m)
-    status = _whiten(adv, m, stats)
+    status = _whiten(adv, m, stats, process_group)
     torch.ops.ragen_amd.mask_mul_(adv, m)
-    adv = _back(token_level_rewards.device, [adv], status)[0]
+    adv = _back(token_level_rewards.device, [adv], status, check=check, group=process_group)[0]
     return adv, adv
 
 

@@ -101,7 +101,7 @@ def test_assemble_edge_rows(device):
 def test_assemble_ragged_shapes_vs_host(device, S):
     """ops.assemble_batch over ragged rows of 0..S+5 tokens at widths S that are not multiples
     of the kernel's 4-id groups: the 32-B group loads and stores, the element-wise pad edge and
-    row end, and rows longer than S (flagged RMI_ERR_STATE, their last S tokens kept) against
+    row end, and rows longer than S (flagged RMI_ERR_UNSUP, their last S tokens kept) against
     host left padding + cumsum and the oracle's masks / scores on the assembled ids."""
     rng = np.random.default_rng(S)
     B, T = 300, 4
@@ -132,7 +132,7 @@ def test_assemble_ragged_shapes_vs_host(device, S):
         np.testing.assert_array_equal(ids.cpu().numpy(), padded)
         np.testing.assert_array_equal(am.cpu().numpy(), am_ref)
         np.testing.assert_array_equal(pos.cpu().numpy(), np.cumsum(am_ref, axis=1))
-        exp_err = lens > S  # RMI_ERR_STATE: an overlong row, or a row where the reference raises
+        exp_err = np.where(lens > S, 8, 0)  # RMI_ERR_UNSUP: an overlong row
         if S > 1:
             osc, olm, orm, oerr = oracle.masks_and_scores(padded, SP, RT, sc, n_sc, T, uts, True, True)
             ok = np.asarray(oerr) == 0  # rows where the reference raises (a turn with two reward tokens) are flagged only
@@ -140,5 +140,5 @@ def test_assemble_ragged_shapes_vs_host(device, S):
             np.testing.assert_array_equal(score.cpu().numpy()[ok], osc[ok])
             np.testing.assert_array_equal(lm.cpu().numpy().astype(np.uint8), olm)
             np.testing.assert_array_equal(rm.cpu().numpy().astype(np.uint8), orm)
-            exp_err |= np.asarray(oerr) != 0
-        np.testing.assert_array_equal(err.cpu().numpy(), np.where(exp_err, 4, 0).astype(np.uint8))
+            exp_err |= np.where(np.asarray(oerr) != 0, 4, 0)  # RMI_ERR_STATE: the reference raises
+        np.testing.assert_array_equal(err.cpu().numpy(), exp_err.astype(np.uint8))

@@ -211,9 +211,9 @@ def test_rccl_global_whitening(device, rccl_group):
     ops.masked_whiten_(a2, tm, stats)
     torch.cuda.synchronize()
     assert torch.equal(a1, a2)
-    # the facade takes the global path whenever a group exists (CPU inputs, as the trainer's)
+    # the facade's opt-in global path (CPU inputs, as the trainer's)
     fa, fr = core_algos.compute_gae_advantage_return(torch.from_numpy(r), torch.from_numpy(v), torch.from_numpy(m),
-                                                     1.0, 0.95)
+                                                     1.0, 0.95, process_group=rccl_group.group.WORLD)
     assert torch.equal(fa, a1.cpu()) and torch.equal(fr, ret.cpu())
     oadv, _ = oracle.gae(r, v, m, 1.0, 0.95)
     np.testing.assert_allclose(fa.numpy(), oracle.masked_whiten(oadv, m), rtol=0, atol=1e-5)

@@ -141,3 +141,30 @@ def test_fit_sequence_on_rollout(device, estimator, bi_level):
         batch.meta_info["multi_turn"] = True
         wg.update_actor(batch)
         assert [n for _, n in critic.seen] == [len(batch) // 4] * 4
+
+
+def test_estimator_errors_with_gpu_inputs(device):
+    """verl's / RAGEN's error cases raise for GPU callers too (check=True, the default): a mask
+    sum of 0 or 1 (verl masked_var -> ValueError) and a bi-level row whose last loss-mask
+    position carries no reward (core_algos.py:79 -> IndexError); check=False leaves them
+    unread (no host synchronisation)."""
+    from ragen_amd.trainer import core_algos
+    B, L = 4, 16
+    r = torch.zeros(B, L, device=device)
+    v = torch.randn(B, L, device=device)
+    for n_on in (0, 1):
+        m = torch.zeros(B, L, dtype=torch.uint8, device=device)
+        m.view(-1)[:n_on] = 1
+        with pytest.raises(ValueError):
+            core_algos.compute_gae_advantage_return(r, v, m, 1.0, 1.0)
+        with pytest.raises(ValueError):
+            core_algos.masked_whiten(v, m)
+        core_algos.compute_gae_advantage_return(r, v, m, 1.0, 1.0, check=False)
+    m = torch.ones(B, L, dtype=torch.uint8, device=device)
+    rb = torch.zeros(B, L, device=device)
+    rb[:, 5] = 1.0  # the reward is not on the last valid column of any row
+    with pytest.raises(IndexError):
+        core_algos.compute_bi_level_gae_advantage_return(rb, v, m, 1.0, 1.0, 0.95)
+    rb[:, -1] = 2.0
+    adv, ret = core_algos.compute_bi_level_gae_advantage_return(rb, v, m, 1.0, 1.0, 0.95)
+    assert adv.is_cuda and torch.isfinite(adv).all()
