@@ -416,6 +416,54 @@ int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, const int
                       int32_t stride, const uint8_t* sel, int8_t* actions, uint8_t* n_actions, int32_t* spans,
                       uint8_t* action_text, int32_t* action_len, int32_t Lact, uint8_t* err, rmi_stream_t stream);
 
+/* ---------------------------------------------- prompt token ids (§8(f) ranks 1-2)
+ * Replaces: the tokenizer call of ContextManager.get_lm_inputs (ctx_manager.py:265-278,
+ *           tokenizer(llm_input_texts, ...)) for a byte-level BPE tokenizer (HF `tokenizers`
+ *           model "BPE", the Qwen2 pre-tokenizer Split(regex) + ByteLevel(use_regex=False),
+ *           normalizer NFC or none, added tokens matched leftmost-longest).
+ *
+ * Tables (built on the host from the tokenizer's JSON, ragen_amd/tokenizer.py):
+ *   cp_block[cp >> 8] -> block, cp_class[block * 256 + (cp & 255)] = RMI_CP_* bits of code
+ *   point cp; byte_id[256] = id of each byte's byte-level symbol; merges = open-addressed
+ *   (key, value) u64 pairs, key = left << 32 | right (~0 = empty slot), value = rank << 32 |
+ *   merged id, slot (key * 0x9E3779B97F4A7C15) >> merge_shift, linear probing (merge_mask =
+ *   slots - 1); added tokens = bytes [added_off[i], added_off[i+1]) of added_bytes -> id.   */
+#define RMI_CP_L 1u       /* \p{L}                                                          */
+#define RMI_CP_N 2u       /* \p{N}                                                          */
+#define RMI_CP_W 4u       /* \s (White_Space, as the pre-tokenizer's regex engine sees it)  */
+#define RMI_CP_NL 8u      /* \r or \n                                                       */
+#define RMI_CP_UNSAFE 16u /* NFC may change text containing it (the row is left to the host) */
+#define RMI_PRETOK_QWEN2 0 /* (?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}|
+                              ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+            */
+#define RMI_PRETOK_CHARS 1 /* every character is its own pre-token                           */
+typedef struct {
+  const uint16_t* cp_block; /* [0x1100]                                                      */
+  const uint8_t* cp_class;  /* [n_blocks * 256]                                              */
+  const int32_t* byte_id;   /* [256]                                                         */
+  const uint64_t* merges;   /* [2 * (merge_mask + 1)]                                        */
+  uint32_t merge_mask, merge_shift;
+  int32_t pretok;           /* RMI_PRETOK_*                                                  */
+  int32_t nfc;              /* 1: the tokenizer normalises NFC (rows holding RMI_CP_UNSAFE
+                               code points are flagged RMI_ERR_UNSUP, not encoded)           */
+  int32_t n_added;
+  const uint8_t* added_bytes;
+  const int32_t* added_off; /* [n_added + 1]                                                 */
+  const int32_t* added_id;  /* [n_added]                                                     */
+  uint32_t added_first[8];  /* bitmap of the added tokens' first bytes                       */
+} rmi_bpe_t;
+
+/* Row b: text[b, 0 .. text_len[b]) (UTF-8, row stride `stride`, stride % 4 == 0, <= 3072).
+ * Its token ids are appended to out row b (i64, row stride out_stride) at position
+ * out_len[b] (NULL: 0), and out_len[b] (if given) advances by their count; n_tok[b]
+ * (optional) = the count.  mark_byte[b] (optional, a pre-token boundary, e.g. the start of a
+ * chat-template block) -> mark_tok[b] = the row position of the first token at or after it.
+ * err[b]: RMI_ERR_STATE for invalid UTF-8 or text_len outside [0, stride]; RMI_ERR_UNSUP for
+ * a code point NFC may change (nfc = 1) or a row that would pass out_stride.  A flagged row
+ * writes no token and leaves out_len[b] as it was.                                         */
+int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int32_t stride, const int32_t* text_len, int64_t B,
+                   int64_t* out, int64_t out_stride, int32_t* out_len, int32_t* n_tok, const int32_t* mark_byte,
+                   int32_t* mark_tok, uint8_t* err, rmi_stream_t stream);
+
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and
  * FrozenLakeEnv.reset's env RNG (frozen_lake/env.py:28-37), both via gymnasium

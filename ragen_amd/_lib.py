@@ -133,6 +133,8 @@ _SIGS = {
     "rmi_parse_actions": (c_int32, [_P(ParseCfg), c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rmi_bpe_encode": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -1,0 +1,460 @@
+// bpe.hip — byte-level BPE encoding of prompt text on the device (gfx950).
+//
+//  rmi_bpe_encode   the tokenizer call of ContextManager.get_lm_inputs (ctx_manager.py:265-278)
+//                   for a HF `tokenizers` byte-level BPE (the Qwen2 model family's tokenizer)
+//
+// One wave per row, the row staged in LDS.  The phases follow the tokenizer's pipeline:
+//  1. UTF-8 decode + code-point classes (one lane per byte position, table lookups), written
+//     over every byte of a character so that runs can be counted in bytes;
+//  2. added tokens (<|im_start|> ...): candidate positions by a first-byte bitmap, the longest
+//     match per position, then the leftmost-longest non-overlapping selection (a short serial
+//     walk over the matches — the text holds a handful);
+//  3. the pre-tokenizer regex: the match length at EVERY position, computed lane-parallel from
+//     128-byte category bitmasks (wave ballots): the seven alternatives of the Qwen2 pattern are
+//     runs and last-bit queries on those masks; a run that outgrows the window takes a serial
+//     scan of the same rules;
+//  4. the leftmost match chain (pre-token starts) by one wave-uniform walk: the window's match
+//     lengths sit in a VGPR and each step is a v_readlane at the walk position;
+//  5. BPE per pre-token, one lane per pre-token: symbols start as byte ids, the rank of every
+//     adjacent pair is looked up once (all pairs of the row in parallel), then the lowest
+//     (rank, position) pair is merged until none is left — the tokenizers crate's merge order
+//     (word.rs merge_all: lowest rank first, leftmost on ties) — re-looking up only the two
+//     pairs a merge changes;
+//  6. token counts per pre-token, a wave scan for the row offsets, the ids written.
+// Merges are an open-addressed hash of (left, right) -> (rank, merged id) in HBM (L2 / MALL
+// resident for the hot pairs).
+#include "common.hpp"
+
+namespace rmi {
+namespace {
+
+// per-byte category bits in LDS (the code point's class spread over all its bytes)
+enum : uint32_t {
+  B_L = 1, B_N = 2, B_W = 4, B_NL = 8,  // = RMI_CP_L / N / W / NL
+  B_START = 16,                         // first byte of a character
+  B_SP = 32,                            // U+0020
+  B_ADD = 64,                           // first byte of a selected added token
+  B_IN = 128                            // any byte of a selected added token
+};
+constexpr uint32_t kNoRank = 0xFFFFFFFFu;
+constexpr uint16_t kEnd = 0xFFFF;
+constexpr int kMaxStride = 3072;
+
+struct Lds {  // carved from dynamic LDS, n = stride
+  uint8_t* T;    // text, n + 16 (zero tail)
+  uint8_t* C;    // category bits, n + 128
+  uint16_t* M;   // match length at a position; then the symbol chain (next symbol start)
+  int32_t* Y;    // symbol id at a symbol start
+  uint64_t* R;   // (rank << 32 | merged id) of the pair starting at a symbol start
+  uint16_t* P;   // pre-token starts
+  uint16_t* K;   // tokens per pre-token, then the row offsets
+  int32_t* BID;  // byte ids [256]
+  uint32_t* AF;  // added tokens' first-byte bitmap [8]
+};
+
+__device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a, uint32_t b) {
+  const uint64_t key = ((uint64_t)a << 32) | b;
+  uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> t.merge_shift;
+  for (;;) {
+    const uint64_t k = t.merges[2 * h];
+    if (k == key) return t.merges[2 * h + 1];
+    if (k == ~0ull) return ~0ull;
+    h = (h + 1) & t.merge_mask;
+  }
+}
+
+__device__ __forceinline__ int utf8_len(uint32_t b) {
+  return b < 0x80 ? 1 : (b >= 0xC2 && b <= 0xDF) ? 2 : (b >= 0xE0 && b <= 0xEF) ? 3 : (b >= 0xF0 && b <= 0xF4) ? 4 : 0;
+}
+
+// the 64 bits of a 128-bit window (lo = [base, base+64), hi = [base+64, base+128)) from bit i
+__device__ __forceinline__ uint64_t view(uint64_t lo, uint64_t hi, int i) {
+  return i == 0 ? lo : (lo >> i) | (hi << (64 - i));
+}
+// end of the run of set bits of v starting at bit k (k <= 64): the first clear bit >= k
+__device__ __forceinline__ int run_end(uint64_t v, int k) {
+  if (k >= 64) return 64;
+  const uint64_t r = ~(v >> k);
+  return r == 0 ? 64 : k + __builtin_ctzll(r);
+}
+__device__ __forceinline__ uint64_t low_bits(int e) { return e >= 64 ? ~0ull : ((1ull << e) - 1); }
+
+// case-insensitive match of the contraction letters after an apostrophe at p (the regex's
+// (?i:'s|'t|'re|'ve|'m|'ll|'d)); -> match length in bytes or 0.  s also folds U+017F.
+__device__ __forceinline__ int contraction(const uint8_t* T, int p, int lim) {
+  if (p + 1 >= lim) return 0;
+  const uint32_t a = T[p + 1] | 0x20, a_is = ((T[p + 1] & 0xDF) >= 'A' && (T[p + 1] & 0xDF) <= 'Z');
+  if (a_is && (a == 's' || a == 't' || a == 'm' || a == 'd')) return 2;
+  if (T[p + 1] == 0xC5 && p + 2 < lim && T[p + 2] == 0xBF) return 3;  // U+017F, folds to 's'
+  if (p + 2 >= lim) return 0;
+  const uint32_t b = T[p + 2] | 0x20, b_is = ((T[p + 2] & 0xDF) >= 'A' && (T[p + 2] & 0xDF) <= 'Z');
+  if (!a_is || !b_is) return 0;
+  if ((a == 'r' && b == 'e') || (a == 'v' && b == 'e') || (a == 'l' && b == 'l')) return 3;
+  return 0;
+}
+
+// The Qwen2 pre-tokenizer match at char start p by a serial scan of the category bytes (the
+// path for runs longer than the bitmask window, and the definition the fast path follows):
+//   1 (?i:'s|'t|'re|'ve|'m|'ll|'d)   2 [^\r\n\p{L}\p{N}]?\p{L}+   3 \p{N}
+//   4  ?[^\s\p{L}\p{N}]+[\r\n]*      5 \s*[\r\n]+   6 \s+(?!\S)   7 \s+
+// s1 = segment end (the next selected added token, or the text end): the regex engine sees
+// the segment as the whole input.
+__device__ int match_serial(const uint8_t* T, const uint8_t* C, int p, int s1) {
+  auto cat = [&](int q) -> uint32_t { return q < s1 ? C[q] : 0u; };
+  auto is_o = [&](int q) { return q < s1 && !(C[q] & (B_L | B_N | B_W)); };
+  auto run = [&](int q, uint32_t bit) {
+    while (q < s1 && (C[q] & bit)) ++q;
+    return q;
+  };
+  auto run_o = [&](int q) {
+    while (is_o(q)) ++q;
+    return q;
+  };
+  auto next_start = [&](int q) {
+    ++q;
+    while (q < s1 && !(C[q] & B_START)) ++q;
+    return q;
+  };
+  const uint32_t c = cat(p);
+  if (T[p] == '\'') {
+    const int l = contraction(T, p, s1);
+    if (l) return l;
+  }
+  const int n0 = next_start(p);
+  if (c & B_L) return run(p, B_L) - p;
+  if (!(c & (B_NL | B_N)) && (cat(n0) & B_L)) return run(n0, B_L) - p;
+  if (c & B_N) return n0 - p;
+  if ((c & B_SP) && is_o(n0)) return run(run_o(n0), B_NL) - p;
+  if (!(c & B_W)) return run(run_o(p), B_NL) - p;  // c is [^\s\p{L}\p{N}]
+  const int e = run(p, B_W);
+  int last_nl = -1, last_start = p;
+  for (int q = p; q < e; ++q) {
+    if (C[q] & B_NL) last_nl = q;
+    if (C[q] & B_START) last_start = q;
+  }
+  if (last_nl >= 0) return last_nl + 1 - p;
+  if (e == s1) return e - p;
+  if (last_start > p) return last_start - p;
+  return e - p;
+}
+
+__global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uint8_t* __restrict__ text, int stride,
+                                                        const int32_t* __restrict__ text_len, int64_t* __restrict__ out,
+                                                        int64_t out_stride, int32_t* __restrict__ out_len,
+                                                        int32_t* __restrict__ n_tok,
+                                                        const int32_t* __restrict__ mark_byte,
+                                                        int32_t* __restrict__ mark_tok, uint8_t* __restrict__ err) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int S = stride;
+  Lds L;
+  {
+    uint8_t* p = smem;
+    L.R = reinterpret_cast<uint64_t*>(p);
+    p += 8 * (size_t)S;
+    L.Y = reinterpret_cast<int32_t*>(p);
+    p += 4 * (size_t)S;
+    L.BID = reinterpret_cast<int32_t*>(p);
+    p += 4 * 256;
+    L.AF = reinterpret_cast<uint32_t*>(p);
+    p += 32;
+    L.M = reinterpret_cast<uint16_t*>(p);
+    p += 2 * (size_t)S;
+    L.P = reinterpret_cast<uint16_t*>(p);
+    p += 2 * (size_t)S;
+    L.K = reinterpret_cast<uint16_t*>(p);
+    p += 2 * (size_t)S + 128;
+    L.T = p;
+    p += S + 16;
+    L.C = p;
+  }
+  const int n = text_len[b];
+  const int base_len = out_len ? out_len[b] : 0;
+  if (n < 0 || n > S) {
+    if (lane == 0) {
+      err[b] = RMI_ERR_STATE;
+      if (n_tok) n_tok[b] = 0;
+      if (mark_tok) mark_tok[b] = base_len;
+    }
+    return;
+  }
+  // ---- stage the row (dwords, the bytes past n zeroed), the byte ids, the first-byte bitmap
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(text + b * (int64_t)S);
+  for (int w = lane; w < (n + 3) / 4 + 4; w += 64) {
+    uint32_t v = 4 * w < n ? src[w] : 0u;
+    if (4 * w + 4 > n && 4 * w < n) v &= 0xFFFFFFFFu >> (8 * (4 * w + 4 - n));
+    reinterpret_cast<uint32_t*>(L.T)[w] = v;
+  }
+  for (int i = lane; i < 256; i += 64) L.BID[i] = tok.byte_id[i];
+  if (lane < 8) L.AF[lane] = tok.added_first[lane];
+  for (int i = lane; i < n + 128; i += 64) L.C[i] = 0;
+  wave_sync();
+  // ---- 1. UTF-8 decode and classes
+  bool bad = false, unsafe = false;
+  for (int p = lane; p < n; p += 64) {
+    const uint32_t b0 = L.T[p];
+    if ((b0 & 0xC0) == 0x80) continue;  // continuation: written by its lead byte's lane
+    const int l = utf8_len(b0);
+    uint32_t cp = 0;
+    if (l == 0 || p + l > n) {
+      bad = true;
+      continue;
+    }
+    if (l == 1) {
+      cp = b0;
+    } else {
+      cp = b0 & (0x7F >> l);
+      for (int k = 1; k < l; ++k) {
+        const uint32_t bk = L.T[p + k];
+        if ((bk & 0xC0) != 0x80) bad = true;
+        cp = (cp << 6) | (bk & 0x3F);
+      }
+    }
+    if (cp > 0x10FFFF) {
+      bad = true;
+      continue;
+    }
+    const uint32_t cls = tok.cp_class[(uint32_t)tok.cp_block[cp >> 8] * 256u + (cp & 255u)];
+    if (tok.nfc && (cls & RMI_CP_UNSAFE)) unsafe = true;
+    const uint32_t cat = cls & (B_L | B_N | B_W | B_NL);
+    L.C[p] = (uint8_t)(cat | B_START | (b0 == 0x20 ? B_SP : 0u));
+    for (int k = 1; k < l; ++k) L.C[p + k] = (uint8_t)cat;
+  }
+  const bool row_bad = __any(bad), row_unsafe = __any(unsafe);
+  auto fail = [&](uint8_t code) {
+    if (lane == 0) {
+      err[b] = code;
+      if (n_tok) n_tok[b] = 0;
+      if (mark_tok) mark_tok[b] = base_len;
+    }
+  };
+  if (row_bad) return fail(RMI_ERR_STATE);
+  if (row_unsafe) return fail(RMI_ERR_UNSUP);
+  wave_sync();
+  // ---- 2. added tokens: longest match per candidate position, then leftmost-longest selection
+  int n_cand = 0;
+  if (tok.n_added > 0) {
+    for (int w0 = 0; w0 < n; w0 += 64) {
+      const int p = w0 + lane;
+      int best_len = 0, best_id = 0;
+      if (p < n && (L.C[p] & B_START) && ((L.AF[L.T[p] >> 5] >> (L.T[p] & 31)) & 1u)) {
+        for (int a = 0; a < tok.n_added; ++a) {
+          const int o0 = tok.added_off[a], len = tok.added_off[a + 1] - o0;
+          if (len <= best_len || p + len > n) continue;
+          int k = 0;
+          while (k < len && tok.added_bytes[o0 + k] == L.T[p + k]) ++k;
+          if (k == len) {
+            best_len = len;
+            best_id = tok.added_id[a];
+          }
+        }
+      }
+      const uint64_t m = __ballot(best_len > 0);
+      if (best_len > 0) {  // candidate list in the P / K arrays (ascending), lengths in M
+        const int slot = n_cand + __builtin_popcountll(m & ((1ull << lane) - 1));
+        L.P[slot] = (uint16_t)p;
+        L.K[slot] = (uint16_t)best_len;
+        L.Y[p] = best_id;
+      }
+      n_cand += __builtin_popcountll(m);
+    }
+    wave_sync();
+    if (lane == 0) {
+      int cur = 0;
+      for (int i = 0; i < n_cand; ++i) {
+        const int p = L.P[i], len = L.K[i];
+        if (p < cur) continue;
+        L.C[p] |= B_ADD;
+        for (int q = p; q < p + len; ++q) L.C[q] |= B_IN;
+        L.M[p] = (uint16_t)len;
+        cur = p + len;
+      }
+    }
+    wave_sync();
+  }
+  // ---- 3. match length at every character start (outside added tokens)
+  for (int w0 = 0; w0 < n; w0 += 64) {
+    const int p = w0 + lane;
+    const bool v0 = p < n, v1 = p + 64 < n;
+    const uint32_t c0 = v0 ? L.C[p] : 0u, c1 = v1 ? L.C[p + 64] : 0u;
+    // segment ends: the start of a selected added token, and every position from n on
+    const uint64_t E0 = __ballot(!v0 || (c0 & B_ADD)), E1 = __ballot(!v1 || (c1 & B_ADD));
+    const uint64_t Lm0 = __ballot(c0 & B_L), Lm1 = __ballot(c1 & B_L);
+    const uint64_t N0 = __ballot(c0 & B_N), N1 = __ballot(c1 & B_N);
+    const uint64_t W0 = __ballot(c0 & B_W), W1 = __ballot(c1 & B_W);
+    const uint64_t NL0 = __ballot(c0 & B_NL), NL1 = __ballot(c1 & B_NL);
+    const uint64_t S0 = __ballot(c0 & B_START), S1 = __ballot(c1 & B_START);
+    if (!v0 || !(c0 & B_START) || (c0 & B_IN)) continue;
+    const int l0 = utf8_len(L.T[p]);
+    int len = 0;
+    if (tok.pretok == RMI_PRETOK_CHARS) {
+      len = l0;
+    } else {
+      const int i = lane;
+      const uint64_t vE = view(E0, E1, i);
+      const int es = vE ? __builtin_ctzll(vE) : 64;  // segment end (64: beyond the view)
+      const uint64_t keep = low_bits(es);
+      const uint64_t vL = view(Lm0, Lm1, i) & keep, vN = view(N0, N1, i) & keep, vW = view(W0, W1, i) & keep;
+      const uint64_t vNL = view(NL0, NL1, i) & keep, vS = view(S0, S1, i);
+      const uint64_t vO = keep & ~(vL | vN | vW);
+      bool slow = false;
+      if (L.T[p] == '\'') len = contraction(L.T, p, p + es);
+      if (!len) {
+        if (c0 & B_L) {
+          len = run_end(vL, 0);
+          slow = len == 64;
+        } else if (!(c0 & (B_NL | B_N)) && ((vL >> l0) & 1)) {
+          len = run_end(vL, l0);
+          slow = len == 64;
+        } else if (c0 & B_N) {
+          len = l0;
+        } else if ((c0 & B_SP) && ((vO >> 1) & 1)) {
+          const int k = run_end(vO, 1);
+          len = run_end(vNL, k);
+          slow = k == 64 || len == 64;
+        } else if (!(c0 & B_W)) {
+          const int k = run_end(vO, 0);
+          len = run_end(vNL, k);
+          slow = k == 64 || len == 64;
+        } else {
+          const int e = run_end(vW, 0);
+          if (e == 64) {
+            slow = true;
+          } else {
+            const uint64_t nl = vNL & low_bits(e);
+            if (nl) {
+              len = 64 - __builtin_clzll(nl);
+            } else if (e == es) {
+              len = e;
+            } else {
+              const int ls = 63 - __builtin_clzll(vS & low_bits(e));
+              len = ls > 0 ? ls : e;
+            }
+          }
+        }
+      }
+#ifdef RMI_BPE_SERIAL_MATCH
+      slow = true;  // diagnostic build: every match by the serial scan
+#endif
+      if (slow) {
+        int s1 = p;
+        while (s1 < n && !(L.C[s1] & B_ADD)) ++s1;
+        len = match_serial(L.T, L.C, p, s1);
+      }
+    }
+    L.M[p] = (uint16_t)(len > 0 ? len : l0);
+  }
+  wave_sync();
+  // ---- 4. the leftmost match chain: pre-token starts (added tokens are pre-tokens too)
+  int np = 0;
+  for (int p = 0; p < n;) {
+    const int base = p;
+    const uint32_t mw = base + lane < n ? L.M[base + lane] : 1u;
+    uint64_t starts = 0;
+    while (p < n && p - base < 64) {
+      starts |= 1ull << (p - base);
+      p += (int)__builtin_amdgcn_readlane((int)mw, p - base);
+    }
+    const int j = np + __builtin_popcountll(starts & ((1ull << lane) - 1));
+    if ((starts >> lane) & 1) L.P[j] = (uint16_t)(base + lane);
+    np += __builtin_popcountll(starts);
+  }
+  wave_sync();
+  // ---- 5. BPE: symbols, pair ranks, merges (one lane per pre-token)
+  // piece bounds: P[j] .. P[j+1] (or n); the symbol chain in M: next symbol start or kEnd
+  for (int j = lane; j < np; j += 64) {
+    const int a = L.P[j], e = j + 1 < np ? L.P[j + 1] : n;
+    if (L.C[a] & B_ADD) {  // an added token: one symbol, id set in phase 2
+      L.M[a] = kEnd;
+      continue;
+    }
+    for (int q = a; q < e; ++q) {
+      L.Y[q] = L.BID[L.T[q]];
+      L.M[q] = q + 1 < e ? (uint16_t)(q + 1) : kEnd;
+    }
+  }
+  wave_sync();
+  // every adjacent pair of the row in parallel (independent lookups in flight together)
+  for (int q = lane; q < n; q += 64) {
+    const uint16_t nx = (L.C[q] & B_IN) ? kEnd : L.M[q];
+    L.R[q] = nx != kEnd ? merge_lookup(tok, (uint32_t)L.Y[q], (uint32_t)L.Y[nx]) : ~0ull;
+  }
+  wave_sync();
+  for (int j = lane; j < np; j += 64) {
+    const int a = L.P[j];
+    int cnt = 1;
+    if (!(L.C[a] & B_ADD)) {
+      for (;;) {
+        uint32_t best = kNoRank;
+        int bq = -1, bprev = -1, prev = -1;
+        for (int q = a; q != kEnd; prev = q, q = L.M[q]) {
+          const uint32_t r = (uint32_t)(L.R[q] >> 32);
+          if (r < best) {
+            best = r;
+            bq = q;
+            bprev = prev;
+          }
+        }
+        if (bq < 0) break;
+        const int rq = L.M[bq];
+        L.Y[bq] = (int32_t)(uint32_t)L.R[bq];
+        const uint16_t nn = L.M[rq];
+        L.M[bq] = nn;
+        L.R[bq] = nn != kEnd ? merge_lookup(tok, (uint32_t)L.Y[bq], (uint32_t)L.Y[nn]) : ~0ull;
+        if (bprev >= 0) L.R[bprev] = merge_lookup(tok, (uint32_t)L.Y[bprev], (uint32_t)L.Y[bq]);
+      }
+      cnt = 0;
+      for (int q = a; q != kEnd; q = L.M[q]) ++cnt;
+    }
+    L.K[j] = (uint16_t)cnt;
+  }
+  wave_sync();
+  // ---- 6. row offsets (wave scan over pre-tokens), mark, capacity, the ids
+  const int mk = mark_byte ? mark_byte[b] : -1;
+  int total = 0, before_mark = 0;
+  for (int j0 = 0; j0 < np; j0 += 64) {
+    const int j = j0 + lane;
+    const int c = j < np ? L.K[j] : 0;
+    const int incl = wave_inclusive_scan(c);
+    const bool pre = j < np && (int)L.P[j] < mk;
+    const int pre_sum = wave_inclusive_scan(pre ? c : 0);
+    before_mark += __builtin_amdgcn_readlane(pre_sum, 63);
+    if (j < np) L.K[j] = (uint16_t)(total + incl - c);  // exclusive offset (< 65536: n <= 3072)
+    total += __builtin_amdgcn_readlane(incl, 63);
+  }
+  if (base_len + total > out_stride) return fail(RMI_ERR_UNSUP);
+  wave_sync();
+  int64_t* orow = out + b * out_stride + base_len;
+  for (int j = lane; j < np; j += 64) {
+    int o = L.K[j];
+    for (int q = L.P[j]; q != kEnd; q = L.M[q]) orow[o++] = (int64_t)L.Y[q];
+  }
+  if (lane == 0) {
+    err[b] = 0;
+    if (out_len) out_len[b] = base_len + total;
+    if (n_tok) n_tok[b] = total;
+    if (mark_tok) mark_tok[b] = base_len + before_mark;
+  }
+}
+
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int32_t stride, const int32_t* text_len,
+                           int64_t B, int64_t* out, int64_t out_stride, int32_t* out_len, int32_t* n_tok,
+                           const int32_t* mark_byte, int32_t* mark_tok, uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!tok || B < 0 || stride <= 0 || stride % 4 || out_stride <= 0) return RMI_EINVAL;
+  if (stride > kMaxStride || B > 0x7FFFFFFF || tok->n_added < 0 || tok->n_added > 4096) return RMI_EUNSUP;
+  if (tok->pretok != RMI_PRETOK_QWEN2 && tok->pretok != RMI_PRETOK_CHARS) return RMI_EUNSUP;
+  if (B == 0) return RMI_OK;
+  if (!text || !text_len || !out || !err || !tok->cp_block || !tok->cp_class || !tok->byte_id || !tok->merges ||
+      (tok->n_added > 0 && (!tok->added_bytes || !tok->added_off || !tok->added_id)))
+    return RMI_EINVAL;
+  // R 8 + Y 4 + M, P, K 2 each + T 1 + C 1 bytes per text byte, the byte ids, bitmap and pads
+  const size_t lds = 20 * (size_t)stride + 4 * 256 + 32 + 128 + 16 + 128;
+  hipLaunchKernelGGL(bpe_encode_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text, (int)stride,
+                     text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);
+  return launch_status();
+}

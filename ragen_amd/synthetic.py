@@ -264,3 +264,85 @@ class ByteChatTokenizer:
             keep = r[r < 256] if skip_special_tokens else r
             out.append(bytes(keep.astype(np.uint8).tolist()).decode("utf-8", errors="replace"))
         return out
+
+
+# --------------------------------------------------------- a Qwen2-style BPE tokenizer
+QWEN_CHAT_TEMPLATE = (
+    "{%- if messages[0]['role'] == 'system' %}"
+    "{{- '<|im_start|>system\\n' + messages[0]['content'] + '<|im_end|>\\n' }}"
+    "{%- else %}"
+    "{{- '<|im_start|>system\\nYou are Qwen, created by Alibaba Cloud. You are a helpful assistant.<|im_end|>\\n' }}"
+    "{%- endif %}"
+    "{%- for message in messages %}"
+    "{%- if (message.role == 'user') or (message.role == 'system' and not loop.first) or "
+    "(message.role == 'assistant') %}"
+    "{{- '<|im_start|>' + message.role + '\\n' + message.content + '<|im_end|>' + '\\n' }}"
+    "{%- endif %}"
+    "{%- endfor %}"
+    "{%- if add_generation_prompt %}{{- '<|im_start|>assistant\\n' }}{%- endif %}")
+
+
+def _tokenizer_corpus(n_docs: int, seed: int):
+    """Text of the kind RAGEN's prompts and responses hold: the env instructions, grids,
+    'Turn k' blocks, rewards, think / answer tags, words, numbers and some non-ASCII."""
+    from .env import REGISTERED_ENV_CONFIGS
+    rng = np.random.default_rng(seed)
+    words = list(THINK_WORDS) + ["Up", "Down", "Left", "Right", "box", "target", "wall", "player", "State", "Turn",
+                                 "Reward", "actions", "left", "answer", "think", "You", "have", "Always", "output",
+                                 "format", "Strictly", "follow", "response", "length", "words", "tokens", "Target",
+                                 "nums", "hole", "goal", "Phoenix", "Dragon", "café", "naïve", "über", "中文", "日本",
+                                 "Привет", "мир", "ελληνικά", "√", "→", "…", "don't", "it's", "we're", "I'll"]
+    # pseudo-words with a Zipf-like frequency: a vocabulary with many merges, as a real one
+    syl = ["ka", "re", "to", "mi", "sa", "lo", "ne", "pu", "ti", "ga", "ber", "con", "ing", "tion", "er", "st", "an",
+           "th", "ou", "pre", "ex", "al", "ly", "ment", "ous", "ive", "de", "un", "ch", "qu", "sh", "ph", "or", "es"]
+    lex = ["".join(rng.choice(syl) for _ in range(int(rng.integers(1, 4)))) for _ in range(3000)]
+    zipf = 1.0 / np.arange(1, len(lex) + 1)
+    zipf /= zipf.sum()
+    docs = [" ".join(lex[int(i)] if rng.random() > 0.1 else lex[int(i)].capitalize()
+                     for i in rng.choice(len(lex), size=200, p=zipf)) for _ in range(n_docs // 3)]
+    for cls in REGISTERED_ENV_CONFIGS.values():
+        c = cls()
+        docs.append(str(getattr(c, "env_instruction", "")))
+        for k in ("grid_vocab", "action_lookup"):
+            v = getattr(c, k, None)
+            if v:
+                docs.append(", ".join(f"{a}: {b}" for a, b in v.items()))
+    for _ in range(n_docs):
+        k = int(rng.integers(8, 60))
+        toks = [words[int(i)] for i in rng.integers(0, len(words), size=k)]
+        for i in range(k):
+            r = rng.random()
+            if r < 0.08:
+                toks[i] = str(int(rng.integers(0, 1000)))
+            elif r < 0.12:
+                toks[i] = f"{rng.normal():.4g}"
+            elif r < 0.16:
+                toks[i] = rng.choice(["||", " || ", "\n", "\n\n", ":", ".", ",", "!", "?", "  ", "\t", "(", ")"])
+        grid = "\n".join("".join(rng.choice(list("#_OXP√")) for _ in range(6)) for _ in range(6))
+        docs.append(f"<think>{' '.join(toks)}</think><answer>{rng.choice(words)} || {rng.choice(words)}</answer>\n"
+                    f"Turn {int(rng.integers(1, 9))}:\nState:\n{grid}\nYou have {int(rng.integers(0, 11))} actions "
+                    f"left.\nReward:\n{rng.choice([0, -0.1, 1.0, -0.30000000000000004, 10.9])}\n")
+    return docs
+
+
+def qwen_like_tokenizer(vocab_size: int = 6000, n_docs: int = 1500, seed: int = 7):
+    """A byte-level BPE with the Qwen2 / Qwen2.5 tokenizer's pipeline (NFC normalizer, the Qwen2
+    pre-tokenizer regex + ByteLevel, <|endoftext|> / <|im_start|> / <|im_end|> added tokens, the
+    Qwen chat template), trained deterministically on RAGEN-like text.  The Qwen2.5 tokenizer is
+    a hub download (unavailable offline); this is its pipeline with a smaller vocabulary."""
+    from tokenizers import Regex, Tokenizer, decoders, models, normalizers, pre_tokenizers, trainers
+    from transformers import PreTrainedTokenizerFast
+    from .tokenizer import QWEN2_PATTERN
+    tok = Tokenizer(models.BPE())
+    tok.normalizer = normalizers.NFC()
+    tok.pre_tokenizer = pre_tokenizers.Sequence([
+        pre_tokenizers.Split(Regex(QWEN2_PATTERN), behavior="isolated", invert=False),
+        pre_tokenizers.ByteLevel(add_prefix_space=False, use_regex=False)])
+    tok.decoder = decoders.ByteLevel()
+    tr = trainers.BpeTrainer(vocab_size=vocab_size, initial_alphabet=pre_tokenizers.ByteLevel.alphabet(),
+                             show_progress=False)
+    tok.train_from_iterator(_tokenizer_corpus(n_docs, seed), tr)
+    tok.add_special_tokens(["<|endoftext|>", "<|im_start|>", "<|im_end|>"])
+    return PreTrainedTokenizerFast(tokenizer_object=tok, name_or_path="Qwen/Qwen2.5-0.5B-Instruct (synthetic BPE)",
+                                   eos_token="<|im_end|>", pad_token="<|endoftext|>", chat_template=QWEN_CHAT_TEMPLATE,
+                                   clean_up_tokenization_spaces=False)

@@ -609,6 +609,55 @@ def _(cfg, text, text_len, sel, with_spans, action_text_len):
             text.new_empty(B, dtype=torch.uint8))
 
 
+def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params):
+    from .tokenizer import Bpe
+    ops._dev(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id)
+    if len(params) != 13:
+        raise ValueError("params: merge_mask, merge_shift, pretok, nfc, n_added, added_first[8]")
+    s = Bpe(cp_block.data_ptr(), cp_class.data_ptr(), byte_id.data_ptr(), merges.data_ptr(), params[0], params[1],
+            params[2], params[3], params[4], added_bytes.data_ptr(), added_off.data_ptr(), added_id.data_ptr())
+    for i in range(8):
+        s.added_first[i] = params[5 + i] & 0xFFFFFFFF
+    return s
+
+
+@_op("bpe_encode", ("out", "out_len"))
+def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tensor, added_bytes: Tensor,
+               added_off: Tensor, added_id: Tensor, params: List[int], text: Tensor, text_len: Tensor, out: Tensor,
+               out_len: Optional[Tensor], mark_byte: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
+    """The tokenizer call of get_lm_inputs (ctx_manager.py:265-278) for a byte-level BPE:
+    every text row's ids appended to ``out`` (rmi_bpe_encode; tables: ragen_amd.tokenizer)
+    -> (n_tok i32[B], mark_tok i32[B], err u8[B])."""
+    import ctypes
+    tok = _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params)
+    ops._dev(text, text_len, out, out_len, mark_byte)
+    ops._dt(text, torch.uint8, "text")
+    ops._dt(text_len, torch.int32, "text_len")
+    ops._dt(out, torch.int64, "out")
+    ops._dt(out_len, torch.int32, "out_len")
+    ops._dt(mark_byte, torch.int32, "mark_byte")
+    B = text.shape[0]
+    if text_len.shape[0] != B or out.shape[0] != B or out.dim() != 2:
+        raise ValueError("text, text_len and out must have one row per text")
+    dev = text.device
+    n_tok = torch.empty(B, dtype=torch.int32, device=dev)
+    mark_tok = torch.zeros(B, dtype=torch.int32, device=dev)
+    err = torch.empty(B, dtype=torch.uint8, device=dev)
+    ops.check(ops.lib().rmi_bpe_encode(ctypes.addressof(tok), text.data_ptr(), int(text.shape[1]), text_len.data_ptr(),
+                                       B, out.data_ptr(), int(out.shape[1]), _ptr(out_len), n_tok.data_ptr(),
+                                       _ptr(mark_byte), mark_tok.data_ptr() if mark_byte is not None else None,
+                                       err.data_ptr(), ops._stream(dev)), "rmi_bpe_encode")
+    return n_tok, mark_tok, err
+
+
+@bpe_encode.register_fake
+def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, text, text_len, out, out_len,
+      mark_byte):
+    B = text.shape[0]
+    return (text.new_empty(B, dtype=torch.int32), text.new_empty(B, dtype=torch.int32),
+            text.new_empty(B, dtype=torch.uint8))
+
+
 # the mutating ops return nothing: their fake kernels only have to exist
 for _name in ("sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_reset",
               "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",

@@ -65,3 +65,63 @@ class FakeQwenTok:
                 table.append(b"")
         skip = [1 if i in (self.IM_START, self.IM_END, self.PAD) else 0 for i in range(V)]
         return table, skip
+
+    _backend = None
+
+    @property
+    def backend_tokenizer(self):
+        """The same encoding as a `tokenizers` byte-level BPE (what the device prompt path reads,
+        ragen_amd.tokenizer.DeviceTokenizer.from_hf): one pre-token per character, merges that
+        rebuild every Basic-Multilingual-Plane character from its UTF-8 bytes into the id
+        ord(c) % 150000, and <|im_start|> / <|im_end|> as added tokens.  Checked against _ids by
+        tests/test_tokenizer.py."""
+        if FakeQwenTok._backend is None:
+            FakeQwenTok._backend = _char_bpe(self.IM_START, self.IM_END)
+        return FakeQwenTok._backend
+
+
+def _char_bpe(im_start, im_end):
+    import json
+
+    from tokenizers import Tokenizer
+    from ragen_amd.tokenizer import bytes_to_unicode
+    b2u = bytes_to_unicode()
+    vocab, merges = {}, []
+    for b in range(256):
+        vocab[b2u[b]] = b if b < 0x80 else 150000 + b
+    nxt = 150256
+    for c in range(0x80, 0x10000):
+        if 0xD800 <= c <= 0xDFFF:
+            continue
+        bs = chr(c).encode("utf-8")
+        syms = [b2u[x] for x in bs]
+        cur = syms[0]
+        for k, s in enumerate(syms[1:], 1):
+            tok = cur + s
+            if tok not in vocab:
+                vocab[tok] = (c % 150000) if k == len(syms) - 1 else nxt
+                if k < len(syms) - 1:
+                    nxt += 1
+                merges.append([cur, s])
+            cur = tok
+    # the added tokens hold their Qwen ids in the model vocabulary too (else tokenizers renumbers
+    # them past the vocabulary); unused ids get placeholder tokens (no holes in the id space)
+    vocab["<|im_start|>"], vocab["<|im_end|>"] = im_start, im_end
+    used = set(vocab.values())
+    for i in range(max(used) + 1):
+        if i not in used:
+            vocab[f"<unused_{i}>"] = i
+    j = {"version": "1.0", "truncation": None, "padding": None,
+         "added_tokens": [{"id": i, "content": t, "single_word": False, "lstrip": False, "rstrip": False,
+                           "normalized": False, "special": True}
+                          for i, t in ((im_start, "<|im_start|>"), (im_end, "<|im_end|>"))],
+         "normalizer": None,
+         "pre_tokenizer": {"type": "Sequence", "pretokenizers": [
+             {"type": "Split", "pattern": {"Regex": "."}, "behavior": "Isolated", "invert": False},
+             {"type": "ByteLevel", "add_prefix_space": False, "trim_offsets": False, "use_regex": False}]},
+         "post_processor": None, "decoder": {"type": "ByteLevel", "add_prefix_space": False, "trim_offsets": False,
+                                             "use_regex": False},
+         "model": {"type": "BPE", "dropout": None, "unk_token": None, "continuing_subword_prefix": None,
+                   "end_of_word_suffix": None, "fuse_unk": False, "byte_fallback": False, "ignore_merges": False,
+                   "vocab": vocab, "merges": merges}}
+    return Tokenizer.from_str(json.dumps(j))
