@@ -306,6 +306,15 @@ int rmi_assemble_batch(const int64_t* tokens, const int64_t* row_off, int64_t B,
                        int64_t* position_ids, float* score_out, uint8_t* loss_mask, uint8_t* response_mask,
                        uint8_t* err, rmi_stream_t stream);
 
+/* rmi_assemble_batch with rows given by (start, length): row b = tokens[row_start[b] ..
+ * row_start[b] + row_len[b]) — e.g. the per-env prompt arena of the device prompt path, one
+ * row per env at a fixed stride (formulate_rollouts, ctx_manager.py:278-306).             */
+int rmi_assemble_rows(const int64_t* tokens, const int64_t* row_start, const int32_t* row_len, int64_t B, int64_t S,
+                      int64_t pad_id, int64_t special_token, int64_t reward_token, const double* scores,
+                      const int32_t* n_scores, int32_t T, int32_t n_slots, int32_t flags, int64_t* input_ids,
+                      int64_t* attention_mask, int64_t* position_ids, float* score_out, uint8_t* loss_mask,
+                      uint8_t* response_mask, uint8_t* err, rmi_stream_t stream);
+
 /* ------------------------------------------------------------------- A13 advantages
  * Replaces: verl compute_gae_advantage_return (called agent_trainer.py:77-83; App. A.4).
  * variant 0 = legacy (RAGEN's snapshot), 1 = masked (newer verl).  Sequential f32
@@ -463,6 +472,67 @@ typedef struct {
 int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int32_t stride, const int32_t* text_len, int64_t B,
                    int64_t* out, int64_t out_stride, int32_t* out_len, int32_t* n_tok, const int32_t* mark_byte,
                    int32_t* mark_tok, uint8_t* err, rmi_stream_t stream);
+
+/* Replaces: the prompt text of ContextManager.get_lm_inputs (ctx_manager.py:248-263) — the
+ *           chat messages of each env's history under the tokenizer's chat template — for
+ *           the part of it one turn adds, built on the device from the turn's own results.
+ * Row b = the concatenation of a small program of pieces (the same program for every row):
+ *   RMI_PT_CONST      pool[a .. a+b)
+ *   RMI_PT_TAG_CONST  pool bytes of the row's tag: (offset, length) = tag_const[2*(a*n_tags + tag[b])]
+ *   RMI_PT_OBS        obs[b, 0 .. obs_len[b])                    the env's rendered state
+ *   RMI_PT_INT        str(ints[a*B + b])                         e.g. actions_left
+ *   RMI_PT_REWARD     str(reward[b]): an int when reward_int[b], else repr(float) (CPython's
+ *                     shortest round-trip form; rows with |reward| outside [1e-5, 2^53) are
+ *                     flagged RMI_ERR_UNSUP)
+ *   RMI_PT_RESPONSE   the llm_response _parse_response builds (ctx_manager.py:148-173) from
+ *                     the decoded generation resp[b, 0 .. resp_len[b]) prefixed with
+ *                     "<think>" / "<answer>" (ctx_manager.py:338-339) and the parse's spans
+ *                     (rmi_parse_actions): no match -> the raw text; else the contents with the
+ *                     special-token replace / strip cascade, and the answer re-joined with
+ *                     " " + sep + " " when it holds more than K actions
+ *   RMI_PT_MARK       mark[b] = the row length so far
+ *   RMI_PT_IF         the row ends here unless cond[b]
+ * Rows with active[b] == 0 (active may be NULL) get length 0.  err[b] = RMI_ERR_UNSUP for a
+ * row past `stride` bytes (length 0) or an unsupported reward.  stride % 4 == 0, <= 3072.   */
+enum { RMI_PT_CONST = 0, RMI_PT_TAG_CONST, RMI_PT_OBS, RMI_PT_INT, RMI_PT_REWARD, RMI_PT_RESPONSE, RMI_PT_MARK,
+       RMI_PT_IF };
+#define RMI_PROMPT_MAX_PIECES 32
+typedef struct {
+  int32_t kind, a, b;
+} rmi_piece_t;
+typedef struct {
+  int32_t n_pieces;
+  rmi_piece_t pieces[RMI_PROMPT_MAX_PIECES];
+  const uint8_t* pool;
+  const int32_t* tag_const;
+  int32_t n_tags;
+  const uint8_t* tag;        /* [B] (NULL: tag 0)                                               */
+  const uint8_t* obs;        /* [B, obs_stride]                                                 */
+  int32_t obs_stride;
+  const int32_t* obs_len;
+  const int32_t* ints;       /* [n][B]                                                          */
+  const double* reward;      /* [B]                                                             */
+  const uint8_t* reward_int; /* [B]                                                             */
+  const uint8_t* resp;       /* [B, resp_stride] decoded generations (no prefix)                */
+  int32_t resp_stride;
+  const int32_t* resp_len;
+  const int32_t* spans;      /* [B, 4] think [s, e), answer [s, e) in the prefixed text, -1 none */
+  int32_t enable_think, K, sep_len;
+  uint8_t sep[16];
+  const uint8_t* cond;       /* [B]                                                             */
+  const uint8_t* active;     /* [B] (NULL: every row)                                           */
+} rmi_prompt_t;
+int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, int32_t stride, int32_t* out_len,
+                    int32_t* mark, uint8_t* err, rmi_stream_t stream);
+
+/* The generation batch of get_lm_inputs (ctx_manager.py:265-278: the tokenizer's left padding,
+ * attention_mask, position_ids = attention_mask.cumsum(-1)) from the prompt arena: row i =
+ * pad_id * (S - n) then arena[rows[i], 0 .. arena_len[rows[i]]) then tail[0 .. n_tail) (the
+ * generation prompt), n = arena_len + n_tail.  i64[n_rows, S] outputs; err[i] = RMI_ERR_UNSUP
+ * when n > S (the row keeps its last S tokens).                                             */
+int rmi_pad_rows(const int64_t* arena, int64_t arena_stride, const int32_t* arena_len, const int64_t* rows,
+                 int64_t n_rows, const int64_t* tail, int32_t n_tail, int64_t S, int64_t pad_id, int64_t* input_ids,
+                 int64_t* attention_mask, int64_t* position_ids, uint8_t* err, rmi_stream_t stream);
 
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and

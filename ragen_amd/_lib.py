@@ -72,6 +72,24 @@ class ParseCfg(ctypes.Structure):
                 ("name_hi", ctypes.c_uint64 * PARSE_MAX_NAMES), ("name_id", (ctypes.c_int8 * PARSE_MAX_NAMES) * 2)]
 
 
+PROMPT_MAX_PIECES = 32
+PT_CONST, PT_TAG_CONST, PT_OBS, PT_INT, PT_REWARD, PT_RESPONSE, PT_MARK, PT_IF = range(8)
+
+
+class Piece(ctypes.Structure):
+    _fields_ = [("kind", c_int32), ("a", c_int32), ("b", c_int32)]
+
+
+class Prompt(ctypes.Structure):
+    """rmi_prompt_t."""
+    _fields_ = [("n_pieces", c_int32), ("pieces", Piece * PROMPT_MAX_PIECES), ("pool", c_void_p),
+                ("tag_const", c_void_p), ("n_tags", c_int32), ("tag", c_void_p), ("obs", c_void_p),
+                ("obs_stride", c_int32), ("obs_len", c_void_p), ("ints", c_void_p), ("reward", c_void_p),
+                ("reward_int", c_void_p), ("resp", c_void_p), ("resp_stride", c_int32), ("resp_len", c_void_p),
+                ("spans", c_void_p), ("enable_think", c_int32), ("K", c_int32), ("sep_len", c_int32),
+                ("sep", ctypes.c_uint8 * 16), ("cond", c_void_p), ("active", c_void_p)]
+
+
 _P = ctypes.POINTER
 _SIGS = {
     "rmi_version": (ctypes.c_char_p, []),
@@ -133,6 +151,12 @@ _SIGS = {
     "rmi_parse_actions": (c_int32, [_P(ParseCfg), c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rmi_prompt_text": (c_int32, [_P(Prompt), c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_pad_rows": (c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_int64, c_int64,
+                               c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_assemble_rows": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                                    c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_bpe_encode": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }

@@ -40,7 +40,8 @@ constexpr int kSuper = 8;  // chunks whose loads are issued together (2048 ids p
 // tokens) and position_ids = cumsum(attention_mask) next to the masks and scores.
 struct AsmArgs {
   const int64_t* tokens;
-  const int64_t* off;
+  const int64_t* off;     // row b = tokens[off[b] .. off[b+1]), or with len: tokens[off[b] .. off[b] + len[b])
+  const int32_t* len;
   int64_t pad_id;
   int64_t* input_ids;
   int64_t* attention_mask;
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   const int64_t* row = kAsm ? nullptr : ids + b * S;
   int64_t a_src = 0, pad = 0;
   if (kAsm) {
-    const int64_t o0 = as.off[b], o1 = as.off[b + 1];
+    const int64_t o0 = as.off[b], o1 = as.len ? o0 + as.len[b] : as.off[b + 1];
     pad = S - (o1 - o0);
     if (pad < 0) {  // a row longer than S: flagged, assembled from its last S tokens
       if (lane == 0) err[b] |= RMI_ERR_UNSUP;
@@ -273,7 +274,26 @@ RMI_API int rmi_assemble_batch(const int64_t* tokens, const int64_t* row_off, in
     return RMI_EINVAL;
   hipLaunchKernelGGL(masks_kernel<true>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), nullptr, B, S,
                      special_token, reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out,
-                     loss_mask, response_mask, err, AsmArgs{tokens, row_off, pad_id, input_ids, attention_mask,
-                                                            position_ids});
+                     loss_mask, response_mask, err, AsmArgs{tokens, row_off, nullptr, pad_id, input_ids,
+                                                            attention_mask, position_ids});
+  return launch_status();
+}
+
+RMI_API int rmi_assemble_rows(const int64_t* tokens, const int64_t* row_start, const int32_t* row_len, int64_t B,
+                              int64_t S, int64_t pad_id, int64_t special_token, int64_t reward_token,
+                              const double* scores, const int32_t* n_scores, int32_t T, int32_t n_slots, int32_t flags,
+                              int64_t* input_ids, int64_t* attention_mask, int64_t* position_ids, float* score_out,
+                              uint8_t* loss_mask, uint8_t* response_mask, uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || S < 1 || T < 0 || n_slots < 0) return RMI_EINVAL;
+  if (n_slots > kMaxSlots || B > 0x7FFFFFFF) return RMI_EUNSUP;
+  if (B == 0) return RMI_OK;
+  if (!tokens || !row_start || !row_len || !input_ids || !attention_mask || !position_ids || !n_scores || !err ||
+      (T > 0 && !scores) || (S > 1 && (!score_out || !loss_mask || !response_mask)))
+    return RMI_EINVAL;
+  hipLaunchKernelGGL(masks_kernel<true>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), nullptr, B, S,
+                     special_token, reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out,
+                     loss_mask, response_mask, err, AsmArgs{tokens, row_start, row_len, pad_id, input_ids,
+                                                            attention_mask, position_ids});
   return launch_status();
 }

@@ -1,0 +1,359 @@
+// prompt.hip — the prompt text one turn adds, built on the device (gfx950), SURVEY §8(f) rank 2.
+//
+//  rmi_prompt_text   ContextManager.get_lm_inputs' messages (ctx_manager.py:248-263) under the
+//                    tokenizer's chat template, for the block a turn appends: the assistant
+//                    message (_parse_response's llm_response, ctx_manager.py:148-173) and the
+//                    next user message (Reward, Turn, State, actions left, the format line)
+//
+// One wave per row.  The row is a fixed program of pieces (constant bytes per launch or per
+// env tag, the env's rendered state, integers, the reward, the response); the wave assembles
+// it in LDS — constant and state bytes copied lane-parallel, numbers formatted by one lane
+// (pyrepr.hpp: CPython's str of an int / float) — and stores it as dwords.  The response
+// piece rebuilds _parse_response's normalised string from the parse kernel's regex spans:
+// each content is stripped (Python str.strip whitespace); a content holding '<' takes the
+// special-token replace / strip cascade on one lane; the separators of the answer are found
+// lane-parallel and, when the answer holds more than K non-empty actions, it is re-joined
+// from its first K stripped actions.
+#include "common.hpp"
+#include "pyrepr.hpp"
+#include "text.hpp"
+
+namespace rmi {
+namespace {
+
+constexpr int kMaxStride = 3072;
+
+struct Tok6 {
+  const char* s;
+  int n;
+};
+__device__ const char kThinkO[] = "<think>", kThinkC[] = "</think>", kAnsO[] = "<answer>", kAnsC[] = "</answer>",
+                      kImS[] = "<|im_start|>", kImE[] = "<|im_end|>";
+
+// lane-parallel copy of n bytes (global or LDS source) into the LDS row at pos
+__device__ __forceinline__ void put(uint8_t* row, int pos, const uint8_t* src, int n, int lane) {
+  for (int i = lane; i < n; i += 64) row[pos + i] = src[i];
+}
+
+// one lane: content <- content.replace(tok, "") for tok in SPECIAL_TOKENS, .strip() after each
+// (ctx_manager.py:163-165); in place on buf[a, z)
+__device__ void cascade(uint8_t* buf, int& a, int& z) {
+  const Tok6 toks[6] = {{kThinkO, 7}, {kThinkC, 8}, {kAnsO, 8}, {kAnsC, 9}, {kImS, 12}, {kImE, 10}};
+  for (int t = 0; t < 6; ++t) {
+    const char* s = toks[t].s;
+    const int n = toks[t].n;
+    int j = a;
+    for (int i = a; i < z;) {
+      bool m = i + n <= z;
+      for (int k = 0; m && k < n; ++k) m = buf[i + k] == (uint8_t)s[k];
+      if (m) {
+        i += n;
+      } else {
+        buf[j++] = buf[i++];
+      }
+    }
+    z = j;
+    strip(buf, a, z);
+  }
+}
+
+__global__ __launch_bounds__(64) void prompt_text_kernel(rmi_prompt_t P, int64_t B, uint8_t* __restrict__ out,
+                                                         int stride, int32_t* __restrict__ out_len,
+                                                         int32_t* __restrict__ mark, uint8_t* __restrict__ err) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  uint8_t* row = smem;                         // the assembled row, stride + 64
+  uint8_t* th = row + stride + 64;             // think content, stride
+  uint8_t* an = th + stride;                   // answer content + its re-joined form, 2 * stride + 64
+  uint8_t* num = an + 2 * stride + 64;         // formatted number, 64
+  int* sh = reinterpret_cast<int*>(num + 64);  // lane 0 -> wave hand-off, 16 ints
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  if (P.active && !P.active[b]) {
+    if (lane == 0) {
+      out_len[b] = 0;
+      if (mark) mark[b] = 0;
+      err[b] = 0;
+    }
+    return;
+  }
+  const int tg = P.tag ? P.tag[b] : 0;
+  int pos = 0, mk = 0;
+  bool over = false, unsup = false;
+  for (int pi = 0; pi < P.n_pieces && !over && !unsup; ++pi) {
+    const rmi_piece_t pc = P.pieces[pi];
+    switch (pc.kind) {
+      case RMI_PT_CONST:
+        if (pos + pc.b > stride) {
+          over = true;
+          break;
+        }
+        put(row, pos, P.pool + pc.a, pc.b, lane);
+        pos += pc.b;
+        break;
+      case RMI_PT_TAG_CONST: {
+        const int o = P.tag_const[2 * (pc.a * P.n_tags + tg)], l = P.tag_const[2 * (pc.a * P.n_tags + tg) + 1];
+        if (pos + l > stride) {
+          over = true;
+          break;
+        }
+        put(row, pos, P.pool + o, l, lane);
+        pos += l;
+        break;
+      }
+      case RMI_PT_OBS: {
+        const int l = P.obs_len[b];
+        if (pos + l > stride) {
+          over = true;
+          break;
+        }
+        put(row, pos, P.obs + b * (int64_t)P.obs_stride, l, lane);
+        pos += l;
+        break;
+      }
+      case RMI_PT_INT:
+      case RMI_PT_REWARD: {
+        if (lane == 0) {
+          char tmp[48];
+          int l;
+          if (pc.kind == RMI_PT_INT) {
+            l = py_int_repr(P.ints[(int64_t)pc.a * B + b], tmp);
+          } else {
+            const double r = P.reward[b];
+            l = (P.reward_int && P.reward_int[b]) ? py_int_repr((int64_t)r, tmp) : py_float_repr(r, tmp);
+          }
+          for (int i = 0; i < l; ++i) num[i] = (uint8_t)tmp[i];
+          sh[0] = l;
+        }
+        wave_sync();
+        const int l = sh[0];
+        if (l < 0) {
+          unsup = true;
+          break;
+        }
+        if (pos + l > stride) {
+          over = true;
+          break;
+        }
+        put(row, pos, num, l, lane);
+        pos += l;
+        break;
+      }
+      case RMI_PT_RESPONSE: {
+        const uint8_t* txt = P.resp + b * (int64_t)P.resp_stride;
+        const int tl = P.resp_len[b];
+        const int plen = P.enable_think ? 7 : 8;
+        const uint8_t* pre = reinterpret_cast<const uint8_t*>(P.enable_think ? kThinkO : kAnsO);
+        auto raw = [&](int i) -> uint8_t { return i < plen ? pre[i] : txt[i - plen]; };
+        const int32_t* sp = P.spans + 4 * b;
+        const int ts = sp[0], te = sp[1], as = sp[2], ae = sp[3];
+        if (as < 0) {  // no match: llm_response is the raw (prefixed) response
+          if (pos + plen + tl > stride) {
+            over = true;
+            break;
+          }
+          for (int i = lane; i < plen + tl; i += 64) row[pos + i] = raw(i);
+          pos += plen + tl;
+          break;
+        }
+        const int nt = P.enable_think ? te - ts : 0, na = ae - as;
+        if (nt > stride || na > stride) {
+          over = true;
+          break;
+        }
+        for (int i = lane; i < nt; i += 64) th[i] = raw(ts + i);
+        for (int i = lane; i < na; i += 64) an[i] = raw(as + i);
+        wave_sync();
+        bool lt = false;
+        for (int i = lane; i < nt; i += 64) lt |= th[i] == '<';
+        for (int i = lane; i < na; i += 64) lt |= an[i] == '<';
+        const bool any_lt = __any(lt);
+        // separator candidates of the answer (its first byte, then the full compare)
+        int ncand = 0;
+        for (int i0 = 0; i0 < na; i0 += 64) {
+          const int i = i0 + lane;
+          bool m = i + P.sep_len <= na;
+          for (int k = 0; m && k < P.sep_len; ++k) m = an[i + k] == P.sep[k];
+          ncand += __builtin_popcountll(__ballot(m));
+        }
+        wave_sync();
+        if (lane == 0) {
+          int t0 = 0, t1 = nt, a0 = 0, a1 = na;
+          if (any_lt) {
+            cascade(th, t0, t1);
+            cascade(an, a0, a1);
+          } else {
+            strip(th, t0, t1);
+            strip(an, a0, a1);
+          }
+          // actions = [a.strip() for a in action_content.split(sep) if a.strip()]; > K: re-join
+          // (a cascade can make new separators: then always counted)
+          bool rejoin = false;
+          if (any_lt || ncand + 1 > P.K) {
+            int n_act = 0, ps[RMI_PARSE_MAX_NAMES + 1], pe[RMI_PARSE_MAX_NAMES + 1];
+            int seg = a0, i = a0;
+            while (n_act <= P.K) {
+              bool m = i + P.sep_len <= a1;
+              for (int k = 0; m && k < P.sep_len; ++k) m = an[i + k] == P.sep[k];
+              if (m || i >= a1) {
+                int x = seg, y = m ? i : a1;
+                strip(an, x, y);
+                if (y > x) {
+                  ps[n_act] = x, pe[n_act] = y;
+                  ++n_act;
+                }
+                if (!m) break;
+                i += P.sep_len;
+                seg = i;
+              } else {
+                ++i;
+              }
+            }
+            if (n_act > P.K) {  // the first K actions joined by " sep ", after the contents
+              rejoin = true;
+              int w = a1;
+              for (int k = 0; k < P.K; ++k) {
+                if (k) {
+                  an[w++] = ' ';
+                  for (int q = 0; q < P.sep_len; ++q) an[w++] = P.sep[q];
+                  an[w++] = ' ';
+                }
+                for (int q = ps[k]; q < pe[k]; ++q) an[w++] = an[q];
+              }
+              a0 = a1;
+              a1 = w;
+            }
+          }
+          sh[0] = t0, sh[1] = t1, sh[2] = a0, sh[3] = a1, sh[4] = rejoin;
+        }
+        wave_sync();
+        const int t0 = sh[0], t1 = sh[1], a0 = sh[2], a1 = sh[3];
+        const int len = P.enable_think ? 7 + (t1 - t0) + 8 + 8 + (a1 - a0) + 9 : 8 + (a1 - a0) + 9;
+        if (pos + len > stride) {
+          over = true;
+          break;
+        }
+        if (P.enable_think) {
+          put(row, pos, reinterpret_cast<const uint8_t*>(kThinkO), 7, lane);
+          pos += 7;
+          put(row, pos, th + t0, t1 - t0, lane);
+          pos += t1 - t0;
+          put(row, pos, reinterpret_cast<const uint8_t*>(kThinkC), 8, lane);
+          pos += 8;
+        }
+        put(row, pos, reinterpret_cast<const uint8_t*>(kAnsO), 8, lane);
+        pos += 8;
+        put(row, pos, an + a0, a1 - a0, lane);
+        pos += a1 - a0;
+        put(row, pos, reinterpret_cast<const uint8_t*>(kAnsC), 9, lane);
+        pos += 9;
+        break;
+      }
+      case RMI_PT_MARK:
+        mk = pos;
+        break;
+      case RMI_PT_IF:
+        if (!P.cond[b]) pi = P.n_pieces;
+        break;
+      default:
+        unsup = true;
+    }
+    wave_sync();
+  }
+  if (over || unsup) {
+    if (lane == 0) {
+      out_len[b] = 0;
+      if (mark) mark[b] = 0;
+      err[b] = RMI_ERR_UNSUP;
+    }
+    return;
+  }
+  uint32_t* o4 = reinterpret_cast<uint32_t*>(out + b * (int64_t)stride);
+  const uint32_t* r4 = reinterpret_cast<const uint32_t*>(row);
+  for (int w = lane; w < (pos + 3) / 4; w += 64) {
+    uint32_t v = r4[w];
+    if (4 * w + 4 > pos) v &= 0xFFFFFFFFu >> (8 * (4 * w + 4 - pos));
+    o4[w] = v;
+  }
+  if (lane == 0) {
+    out_len[b] = pos;
+    if (mark) mark[b] = mk;
+    err[b] = 0;
+  }
+}
+
+// one wave per output row: the row's arena slice and the tail, left-padded (element-wise
+// 8-B loads and stores; consecutive lanes take consecutive columns)
+__global__ __launch_bounds__(64) void pad_rows_kernel(const int64_t* __restrict__ arena, int64_t arena_stride,
+                                                      const int32_t* __restrict__ arena_len,
+                                                      const int64_t* __restrict__ rows, const int64_t* __restrict__ tail,
+                                                      int n_tail, int64_t S, int64_t pad_id, int64_t* __restrict__ ids,
+                                                      int64_t* __restrict__ am, int64_t* __restrict__ pos,
+                                                      uint8_t* __restrict__ err) {
+  const int lane = threadIdx.x;
+  const int64_t i = blockIdx.x;
+  const int64_t r = rows[i];
+  const int64_t na = arena_len[r], n = na + n_tail;
+  const int64_t cut = n > S ? n - S : 0;  // an overlong row keeps its last S tokens
+  const int64_t pad = n > S ? 0 : S - n;
+  const int64_t* src = arena + r * arena_stride;
+  int64_t* io = ids + i * S;
+  int64_t* ao = am + i * S;
+  int64_t* po = pos + i * S;
+  for (int64_t c = lane; c < S; c += 64) {
+    const int64_t k = c - pad + cut;  // index into the row's n tokens
+    const bool on = c >= pad;
+    io[c] = !on ? pad_id : (k < na ? src[k] : tail[k - na]);
+    ao[c] = on ? 1 : 0;
+    po[c] = on ? c - pad + 1 : 0;
+  }
+  if (lane == 0) err[i] = n > S ? RMI_ERR_UNSUP : 0;
+}
+
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_pad_rows(const int64_t* arena, int64_t arena_stride, const int32_t* arena_len, const int64_t* rows,
+                         int64_t n_rows, const int64_t* tail, int32_t n_tail, int64_t S, int64_t pad_id,
+                         int64_t* input_ids, int64_t* attention_mask, int64_t* position_ids, uint8_t* err,
+                         rmi_stream_t stream) {
+  using namespace rmi;
+  if (n_rows < 0 || S < 1 || n_tail < 0 || arena_stride < 1) return RMI_EINVAL;
+  if (n_rows > 0x7FFFFFFF) return RMI_EUNSUP;
+  if (n_rows == 0) return RMI_OK;
+  if (!arena || !arena_len || !rows || (n_tail && !tail) || !input_ids || !attention_mask || !position_ids || !err)
+    return RMI_EINVAL;
+  hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)n_rows), dim3(64), 0, as_stream(stream), arena, arena_stride,
+                     arena_len, rows, tail, (int)n_tail, S, pad_id, input_ids, attention_mask, position_ids, err);
+  return launch_status();
+}
+
+RMI_API int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, int32_t stride, int32_t* out_len,
+                            int32_t* mark, uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!prog || B < 0 || stride <= 0 || stride % 4 || prog->n_pieces < 0) return RMI_EINVAL;
+  if (stride > kMaxStride || prog->n_pieces > RMI_PROMPT_MAX_PIECES || B > 0x7FFFFFFF || prog->sep_len > 16 ||
+      prog->K > RMI_PARSE_MAX_NAMES)
+    return RMI_EUNSUP;
+  if (B == 0) return RMI_OK;
+  if (!out || !out_len || !err) return RMI_EINVAL;
+  bool need_resp = false, need_obs = false, need_int = false, need_rew = false, need_if = false, need_tag = false;
+  for (int i = 0; i < prog->n_pieces; ++i) {
+    const int k = prog->pieces[i].kind;
+    need_resp |= k == RMI_PT_RESPONSE;
+    need_obs |= k == RMI_PT_OBS;
+    need_int |= k == RMI_PT_INT;
+    need_rew |= k == RMI_PT_REWARD;
+    need_if |= k == RMI_PT_IF;
+    need_tag |= k == RMI_PT_TAG_CONST;
+    if (k == RMI_PT_CONST && (prog->pieces[i].b < 0 || (prog->pieces[i].b > 0 && !prog->pool))) return RMI_EINVAL;
+  }
+  if ((need_resp && (!prog->resp || !prog->resp_len || !prog->spans || prog->sep_len < 1 || prog->K < 0)) ||
+      (need_obs && (!prog->obs || !prog->obs_len)) || (need_int && !prog->ints) || (need_rew && !prog->reward) ||
+      (need_if && !prog->cond) || (need_tag && (!prog->tag_const || !prog->pool || prog->n_tags < 1)))
+    return RMI_EINVAL;
+  // row (stride + 64) + think (stride) + answer and its re-joined form (2 * stride + 64) + number + hand-off
+  const size_t lds = (size_t)stride + 64 + (size_t)stride + 2 * (size_t)stride + 64 + 64 + 64;
+  hipLaunchKernelGGL(prompt_text_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *prog, B, out,
+                     (int)stride, out_len, mark, err);
+  return launch_status();
+}

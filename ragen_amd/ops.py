@@ -643,6 +643,59 @@ def assemble_batch(tokens: torch.Tensor, row_off: torch.Tensor, S: int, pad_id: 
     return ids, am, pos, score, lm, rm, err
 
 
+def assemble_rows(tokens: torch.Tensor, row_start: torch.Tensor, row_len: torch.Tensor, S: int, pad_id: int,
+                  special_token: int, reward_token: int, scores: torch.Tensor, n_scores: torch.Tensor, n_slots: int,
+                  use_turn_scores: bool, enable_response_mask: bool, roll: bool):
+    """assemble_batch with rows tokens[row_start[b] .. + row_len[b]) (the prompt arena)."""
+    _dev(tokens, row_start, row_len, scores, n_scores)
+    _dt(tokens, torch.int64, "tokens")
+    _dt(row_start, torch.int64, "row_start")
+    _dt(row_len, torch.int32, "row_len")
+    _dt(scores, torch.float64, "scores")
+    _dt(n_scores, torch.int32, "n_scores")
+    B = row_start.numel()
+    T = scores.shape[0] if scores.dim() == 2 else 0
+    if T and scores.shape[1] != B:
+        raise ValueError(f"scores must be [T, B={B}], got {tuple(scores.shape)}")
+    dev = tokens.device
+    So = max(int(S) - 1, 0)
+    ids = torch.empty(B, S, dtype=torch.int64, device=dev)
+    am = torch.empty_like(ids)
+    pos = torch.empty_like(ids)
+    score = torch.empty(B, So, dtype=torch.float32, device=dev)
+    lm = torch.empty(B, So, dtype=torch.bool, device=dev)
+    rm = torch.empty(B, So, dtype=torch.bool, device=dev)
+    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    flags = ((_lib.MS_TURN_SCORES if use_turn_scores else 0) | (_lib.MS_RESPONSE_MASK if enable_response_mask else 0)
+             | (_lib.MS_ROLL if roll else 0))
+    check(lib().rmi_assemble_rows(_ptr(tokens), _ptr(row_start), _ptr(row_len), B, int(S), int(pad_id),
+                                  int(special_token), int(reward_token), _ptr(scores), _ptr(n_scores), T, int(n_slots),
+                                  flags, _ptr(ids), _ptr(am), _ptr(pos), _ptr(score), _ptr(lm), _ptr(rm), _ptr(err),
+                                  _stream(dev)), "rmi_assemble_rows")
+    return ids, am, pos, score, lm, rm, err
+
+
+def pad_rows(arena: torch.Tensor, arena_len: torch.Tensor, rows: torch.Tensor, tail: torch.Tensor, S: int,
+             pad_id: int):
+    """The left-padded generation batch from arena rows + a common tail (rmi_pad_rows)
+    -> (input_ids, attention_mask, position_ids i64[n, S], err u8[n])."""
+    _dev(arena, arena_len, rows, tail)
+    _dt(arena, torch.int64, "arena")
+    _dt(arena_len, torch.int32, "arena_len")
+    _dt(rows, torch.int64, "rows")
+    _dt(tail, torch.int64, "tail")
+    n = rows.numel()
+    dev = arena.device
+    ids = torch.empty(n, S, dtype=torch.int64, device=dev)
+    am = torch.empty_like(ids)
+    pos = torch.empty_like(ids)
+    err = torch.zeros(n, dtype=torch.uint8, device=dev)
+    check(lib().rmi_pad_rows(_ptr(arena), arena.shape[1], _ptr(arena_len), _ptr(rows), n, _ptr(tail), tail.numel(),
+                             int(S), int(pad_id), _ptr(ids), _ptr(am), _ptr(pos), _ptr(err), _stream(dev)),
+          "rmi_pad_rows")
+    return ids, am, pos, err
+
+
 # ------------------------------------------------------------------------ advantages
 def _mask_u8(mask: torch.Tensor) -> torch.Tensor:
     """A boolean mask as u8 bytes.  The kernels read any nonzero byte as 1 (RAGEN passes a bool

@@ -383,6 +383,40 @@ def _(tokens, row_off, S, pad_id, special_token, reward_token, scores, n_scores,
             tokens.new_empty(B, dtype=torch.uint8))
 
 
+@_op("assemble_rows")
+def assemble_rows(tokens: Tensor, row_start: Tensor, row_len: Tensor, S: int, pad_id: int, special_token: int,
+                  reward_token: int, scores: Tensor, n_scores: Tensor, n_slots: int, use_turn_scores: bool,
+                  enable_response_mask: bool, roll: bool) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """assemble_batch over rows given by (start, length), e.g. the device prompt arena."""
+    return ops.assemble_rows(tokens, row_start, row_len, S, pad_id, special_token, reward_token, scores, n_scores,
+                             n_slots, use_turn_scores, enable_response_mask, roll)
+
+
+@assemble_rows.register_fake
+def _(tokens, row_start, row_len, S, pad_id, special_token, reward_token, scores, n_scores, n_slots, use_turn_scores,
+      enable_response_mask, roll):
+    B = row_start.shape[0]
+    So = max(S - 1, 0)
+    i = tokens.new_empty(B, S, dtype=torch.int64)
+    return (i, torch.empty_like(i), torch.empty_like(i), tokens.new_empty(B, So, dtype=torch.float32),
+            tokens.new_empty(B, So, dtype=torch.bool), tokens.new_empty(B, So, dtype=torch.bool),
+            tokens.new_empty(B, dtype=torch.uint8))
+
+
+@_op("pad_rows")
+def pad_rows(arena: Tensor, arena_len: Tensor, rows: Tensor, tail: Tensor, S: int,
+             pad_id: int) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """The generation batch of get_lm_inputs (ctx_manager.py:265-278) from the prompt arena."""
+    return ops.pad_rows(arena, arena_len, rows, tail, S, pad_id)
+
+
+@pad_rows.register_fake
+def _(arena, arena_len, rows, tail, S, pad_id):
+    n = rows.shape[0]
+    i = arena.new_empty(n, S)
+    return i, torch.empty_like(i), torch.empty_like(i), arena.new_empty(n, dtype=torch.uint8)
+
+
 # ================================================================== advantages (A13)
 @_op("gae", ("row_stats",))
 def gae(r: Tensor, v: Tensor, mask: Tensor, gamma: float, lam: float, variant: int,
@@ -656,6 +690,64 @@ def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, par
     B = text.shape[0]
     return (text.new_empty(B, dtype=torch.int32), text.new_empty(B, dtype=torch.int32),
             text.new_empty(B, dtype=torch.uint8))
+
+
+def prompt_struct(program: List[int], sep: List[int], tensors) -> _lib.Prompt:
+    """program = [n_pieces, (kind, a, b) * n_pieces, n_tags, obs_stride, resp_stride, enable_think, K];
+    tensors = (pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active)."""
+    pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active = tensors
+    n = program[0]
+    if n > _lib.PROMPT_MAX_PIECES or len(program) != 1 + 3 * n + 5 or len(sep) > 16:
+        raise ValueError("bad prompt program")
+    P = _lib.Prompt()
+    P.n_pieces = n
+    for i in range(n):
+        P.pieces[i] = _lib.Piece(*program[1 + 3 * i:4 + 3 * i])
+    n_tags, obs_stride, resp_stride, enable_think, K = program[1 + 3 * n:]
+    P.pool, P.tag_const, P.n_tags, P.tag = _ptr(pool), _ptr(tag_const), n_tags, _ptr(tag)
+    P.obs, P.obs_stride, P.obs_len, P.ints = _ptr(obs), obs_stride, _ptr(obs_len), _ptr(ints)
+    P.reward, P.reward_int, P.resp, P.resp_stride = _ptr(reward), _ptr(reward_int), _ptr(resp), resp_stride
+    P.resp_len, P.spans, P.enable_think, P.K = _ptr(resp_len), _ptr(spans), enable_think, K
+    P.sep_len = len(sep)
+    for i, x in enumerate(sep):
+        P.sep[i] = x
+    P.cond, P.active = _ptr(cond), _ptr(active)
+    return P
+
+
+@_op("prompt_text")
+def prompt_text(program: List[int], sep: List[int], B: int, stride: int, pool: Optional[Tensor],
+                tag_const: Optional[Tensor], tag: Optional[Tensor], obs: Optional[Tensor], obs_len: Optional[Tensor],
+                ints: Optional[Tensor], reward: Optional[Tensor], reward_int: Optional[Tensor], resp: Optional[Tensor],
+                resp_len: Optional[Tensor], spans: Optional[Tensor], cond: Optional[Tensor],
+                active: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+    """The prompt text one turn appends (ctx_manager.py:248-263, rmi_prompt_text)
+    -> (text u8[B, stride], text_len i32[B], mark i32[B], err u8[B])."""
+    ts = (pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active)
+    dev = ops._dev(*ts)
+    for t, dt, nm in ((pool, torch.uint8, "pool"), (tag_const, torch.int32, "tag_const"), (tag, torch.uint8, "tag"),
+                      (obs, torch.uint8, "obs"), (obs_len, torch.int32, "obs_len"), (ints, torch.int32, "ints"),
+                      (reward, torch.float64, "reward"), (reward_int, torch.uint8, "reward_int"),
+                      (resp, torch.uint8, "resp"), (resp_len, torch.int32, "resp_len"), (spans, torch.int32, "spans"),
+                      (cond, torch.uint8, "cond"), (active, torch.uint8, "active")):
+        ops._dt(t, dt, nm)
+    import ctypes
+    P = prompt_struct(program, sep, ts)
+    out = torch.empty(B, stride, dtype=torch.uint8, device=dev)
+    n = torch.empty(B, dtype=torch.int32, device=dev)
+    mark = torch.empty(B, dtype=torch.int32, device=dev)
+    err = torch.empty(B, dtype=torch.uint8, device=dev)
+    ops.check(ops.lib().rmi_prompt_text(ctypes.byref(P), B, out.data_ptr(), stride, n.data_ptr(), mark.data_ptr(),
+                                        err.data_ptr(), ops._stream(dev)), "rmi_prompt_text")
+    return out, n, mark, err
+
+
+@prompt_text.register_fake
+def _(program, sep, B, stride, pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans,
+      cond, active):
+    t = next(x for x in (pool, obs, resp, reward) if x is not None)
+    return (t.new_empty(B, stride, dtype=torch.uint8), t.new_empty(B, dtype=torch.int32),
+            t.new_empty(B, dtype=torch.int32), t.new_empty(B, dtype=torch.uint8))
 
 
 # the mutating ops return nothing: their fake kernels only have to exist
