@@ -461,7 +461,8 @@ typedef struct {
   uint32_t added_first[8];  /* bitmap of the added tokens' first bytes                       */
 } rmi_bpe_t;
 
-/* Row b: text[b, 0 .. text_len[b]) (UTF-8, row stride `stride`, stride % 4 == 0, <= 3072).
+/* Row b: text[b * pitch .. + text_len[b]) (UTF-8; pitch % 4 == 0); `stride` (% 4 == 0,
+ * <= 3072) bounds the row length and sizes the kernel's LDS (rows longer: RMI_ERR_STATE).
  * Its token ids are appended to out row b (i64, row stride out_stride) at position
  * out_len[b] (NULL: 0), and out_len[b] (if given) advances by their count; n_tok[b]
  * (optional) = the count.  mark_byte[b] (optional, a pre-token boundary, e.g. the start of a
@@ -469,9 +470,9 @@ typedef struct {
  * err[b]: RMI_ERR_STATE for invalid UTF-8 or text_len outside [0, stride]; RMI_ERR_UNSUP for
  * a code point NFC may change (nfc = 1) or a row that would pass out_stride.  A flagged row
  * writes no token and leaves out_len[b] as it was.                                         */
-int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int32_t stride, const int32_t* text_len, int64_t B,
-                   int64_t* out, int64_t out_stride, int32_t* out_len, int32_t* n_tok, const int32_t* mark_byte,
-                   int32_t* mark_tok, uint8_t* err, rmi_stream_t stream);
+int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pitch, int32_t stride, const int32_t* text_len,
+                   int64_t B, int64_t* out, int64_t out_stride, int32_t* out_len, int32_t* n_tok,
+                   const int32_t* mark_byte, int32_t* mark_tok, uint8_t* err, rmi_stream_t stream);
 
 /* Replaces: the prompt text of ContextManager.get_lm_inputs (ctx_manager.py:248-263) — the
  *           chat messages of each env's history under the tokenizer's chat template — for

@@ -157,8 +157,8 @@ _SIGS = {
     "rmi_assemble_rows": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
                                     c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "rmi_bpe_encode": (c_int32, [c_void_p, c_void_p, c_int32, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
-                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_bpe_encode": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_int64,
+                                 c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 
 _lib = None

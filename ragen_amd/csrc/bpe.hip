@@ -138,7 +138,8 @@ __device__ int match_serial(const uint8_t* T, const uint8_t* C, int p, int s1) {
   return e - p;
 }
 
-__global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uint8_t* __restrict__ text, int stride,
+__global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uint8_t* __restrict__ text, int64_t pitch,
+                                                        int stride,
                                                         const int32_t* __restrict__ text_len, int64_t* __restrict__ out,
                                                         int64_t out_stride, int32_t* __restrict__ out_len,
                                                         int32_t* __restrict__ n_tok,
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     return;
   }
   // ---- stage the row (dwords, the bytes past n zeroed), the byte ids, the first-byte bitmap
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(text + b * (int64_t)S);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(text + b * pitch);
   for (int w = lane; w < (n + 3) / 4 + 4; w += 64) {
     uint32_t v = 4 * w < n ? src[w] : 0u;
     if (4 * w + 4 > n && 4 * w < n) v &= 0xFFFFFFFFu >> (8 * (4 * w + 4 - n));
@@ -441,11 +442,12 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
 }  // namespace
 }  // namespace rmi
 
-RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int32_t stride, const int32_t* text_len,
-                           int64_t B, int64_t* out, int64_t out_stride, int32_t* out_len, int32_t* n_tok,
-                           const int32_t* mark_byte, int32_t* mark_tok, uint8_t* err, rmi_stream_t stream) {
+RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pitch, int32_t stride,
+                           const int32_t* text_len, int64_t B, int64_t* out, int64_t out_stride, int32_t* out_len,
+                           int32_t* n_tok, const int32_t* mark_byte, int32_t* mark_tok, uint8_t* err,
+                           rmi_stream_t stream) {
   using namespace rmi;
-  if (!tok || B < 0 || stride <= 0 || stride % 4 || out_stride <= 0) return RMI_EINVAL;
+  if (!tok || B < 0 || stride <= 0 || stride % 4 || pitch % 4 || out_stride <= 0) return RMI_EINVAL;
   if (stride > kMaxStride || B > 0x7FFFFFFF || tok->n_added < 0 || tok->n_added > 4096) return RMI_EUNSUP;
   if (tok->pretok != RMI_PRETOK_QWEN2 && tok->pretok != RMI_PRETOK_CHARS) return RMI_EUNSUP;
   if (B == 0) return RMI_OK;
@@ -454,7 +456,8 @@ RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int32_t st
     return RMI_EINVAL;
   // R 8 + Y 4 + M, P, K 2 each + T 1 + C 1 bytes per text byte, the byte ids, bitmap and pads
   const size_t lds = 20 * (size_t)stride + 4 * 256 + 32 + 128 + 16 + 128;
-  hipLaunchKernelGGL(bpe_encode_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text, (int)stride,
+  hipLaunchKernelGGL(bpe_encode_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text, pitch,
+                     (int)stride,
                      text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);
   return launch_status();
 }

@@ -17,6 +17,7 @@ needs no collective.  The real exchange steps after it are:
 """
 from typing import Callable, Dict, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -138,3 +139,50 @@ def episode_views(gathered: torch.Tensor, B: int, T: int):
 def gather_rollout(tensors: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
     """Reassemble fixed-shape per-env trajectory tensors [n_local, ...] from every rank."""
     return {k: all_gather_rows(v) for k, v in tensors.items()}
+
+
+def all_reduce_max_int(v: int, group=None, device=None) -> int:
+    """max of a Python int over the ranks (the local value without a process group)."""
+    if not initialized():
+        return int(v)
+    t = torch.tensor([int(v)], dtype=torch.int64, device=device if device is not None else "cpu")
+    return int(all_reduce_max(t, group).cpu()[0])
+
+
+def left_pad(x: torch.Tensor, width: int, value) -> torch.Tensor:
+    """[B, w] -> [B, width] with `value` columns added on the left (w <= width)."""
+    w = x.shape[1]
+    if w == width:
+        return x
+    out = torch.full((x.shape[0], width), value, dtype=x.dtype, device=x.device)
+    out[:, width - w:] = x
+    return out
+
+
+def gather_formulated(dp, pad_id: int, group=None):
+    """Token-level reassembly of formulate_rollouts' batch over the ranks: the
+    reference builds ONE left-padded batch (ctx_manager.py:278-306), so every rank pads its
+    shard to the global width S (an all-reduce of max S), then the rows are all-gathered in
+    rank order — the global env order, since shards are contiguous.  Token tensors [B, S],
+    masks / scores [B, S-1]; responses = input_ids[:, 1:]; original_rm_scores keeps aliasing
+    rm_scores.  env_ids / group_ids are gathered too (messages_list stays with its rank).
+    -> a DataProto of the whole batch, identical on every rank."""
+    from .protocol import DataProto
+    b = dp.batch
+    ids = b["input_ids"]
+    S = all_reduce_max_int(ids.shape[1], group, ids.device)
+    spec = {"input_ids": (S, int(pad_id)), "attention_mask": (S, 0), "position_ids": (S, 0),
+            "loss_mask": (S - 1, False), "rm_scores": (S - 1, 0.0)}
+    out = {}
+    for k, (w, v) in spec.items():
+        if k in b.keys():
+            out[k] = all_gather_rows(left_pad(b[k], w, v).contiguous(), group=group)
+    out["responses"] = out["input_ids"][:, 1:]
+    if "original_rm_scores" in b.keys():
+        out["original_rm_scores"] = out["rm_scores"]
+    nt = {}
+    for k in ("env_ids", "group_ids"):
+        if k in dp.non_tensor_batch:
+            loc = torch.tensor(np.asarray(dict.__getitem__(dp.non_tensor_batch, k), np.int64), device=ids.device)
+            nt[k] = np.array(all_gather_rows(loc, group=group).cpu().tolist(), dtype=object)
+    return DataProto(out, nt, dict(dp.meta_info))

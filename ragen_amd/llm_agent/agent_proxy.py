@@ -35,29 +35,51 @@ class ScriptedActor:
 class TokenActor:
     """Stand-in LLM whose generations are token ids on the GPU (what a device-resident policy or
     a vLLM worker on the same GPU hands back): ``turn_tokens[t]`` i64[n_envs, R] holds every
-    env's response ids for turn t; each call returns the rows of the envs asked for."""
+    env's response ids for turn t (rows by global env id - ``env_lo``); each call returns the
+    rows of the envs asked for.  With ``read_prompts`` it reads the prompt batch the way a real
+    actor does (agent_proxy.py:128-141: input_ids, attention_mask, position_ids), and keeps
+    each turn's shapes in ``prompt_shapes``."""
 
-    def __init__(self, turn_tokens):
+    def __init__(self, turn_tokens, read_prompts: bool = False, env_lo: int = 0):
         self.turn_tokens = turn_tokens
         self.turn = 0
+        self.read_prompts = read_prompts
+        self.env_lo = env_lo
+        self.prompt_shapes = []
+        self.prompts = []
 
     def generate_sequences(self, lm_inputs: DataProto) -> DataProto:
         env_ids = np.asarray(lm_inputs.non_tensor_batch["env_ids"], dtype=np.int64)
+        if self.read_prompts:
+            b = lm_inputs.batch
+            self.prompt_shapes.append(tuple(b["input_ids"].shape))
+            self.prompts.append((b["input_ids"], b["attention_mask"], b["position_ids"]))
         tok = self.turn_tokens[self.turn]
-        resp = tok[torch.from_numpy(env_ids).to(tok.device)]
+        resp = tok[torch.from_numpy(env_ids - self.env_lo).to(tok.device)]
         self.turn += 1
         return DataProto({"responses": resp}, {"env_ids": env_ids}, {})
 
 
 class LLMAgentProxy:
-    def __init__(self, config, actor_rollout_wg, tokenizer, device=None):
+    """agent_proxy.py:115-159.  Sharded (rank / world_size, or a process_group): each rank rolls
+    out its group-aligned shard of the envs (EnvStateManager); with ``gather=True`` (and a
+    process group) ``rollout`` reassembles the whole left-padded batch on every rank
+    (ragen_amd.distributed.gather_formulated), as the single-controller reference builds it."""
+
+    def __init__(self, config, actor_rollout_wg, tokenizer, device=None, rank=None, world_size=None,
+                 process_group=None, gather: bool = False):
         self.config = config
-        self.train_ctx_manager = ContextManager(config, tokenizer, mode="train", device=device)
-        self.train_es_manager = EnvStateManager(config, mode="train", device=device)
-        self.val_ctx_manager = ContextManager(config, tokenizer, mode="val", device=device)
-        self.val_es_manager = EnvStateManager(config, mode="val", device=device)
+        kw = dict(device=device, rank=rank, world_size=world_size, process_group=process_group)
+        self.train_ctx_manager = ContextManager(config, tokenizer, mode="train", **kw)
+        self.train_es_manager = EnvStateManager(config, mode="train", **kw)
+        self.val_ctx_manager = ContextManager(config, tokenizer, mode="val", **kw)
+        self.val_es_manager = EnvStateManager(config, mode="val", **kw)
+        self.train_ctx_manager.attach_env_manager(self.train_es_manager)
+        self.val_ctx_manager.attach_env_manager(self.val_es_manager)
         self.actor_wg = actor_rollout_wg
         self.tokenizer = tokenizer
+        self.process_group = process_group
+        self.gather = gather
 
     def generate_sequences(self, lm_inputs: DataProto) -> DataProto:
         out = self.actor_wg.generate_sequences(lm_inputs)
@@ -86,6 +108,10 @@ class LLMAgentProxy:
         rollout_states = es.get_rollout_states()
         t3 = time.perf_counter()
         out = ctx.formulate_rollouts(rollout_states)
+        if self.gather and self.process_group is not None:
+            from .. import distributed as rd
+            pad = self.tokenizer.pad_token_id if getattr(self.tokenizer, "pad_token_id", None) is not None else 0
+            out = rd.gather_formulated(out, pad, self.process_group)
         # phase wall times of the last call (the turn loop is what env-steps/s is measured on)
         self.last_timing = {"reset_s": t1 - t0, "turns_s": t2 - t1, "rollout_states_s": t3 - t2,
                             "formulate_s": time.perf_counter() - t3}

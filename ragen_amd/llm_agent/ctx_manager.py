@@ -9,7 +9,8 @@ those bytes).  The numeric hot path runs on the GPU engine:
     from this package's EnvStateManager.
 """
 import re
-from typing import Dict, List
+import warnings
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch
@@ -240,48 +241,110 @@ class LazyDataProto(DataProto):
         self.non_tensor_batch = _LazyNonTensor(self, np.asarray(env_ids, dtype=object))
         self.meta_info = {}
 
+    def __len__(self):
+        return len(dict.__getitem__(self.non_tensor_batch, "env_ids"))
+
+    def set_device_batch(self, batch: dict, env_ids, group_size: int):
+        """The device prompt path: the tensors are built already (on the GPU), and so are
+        env_ids / group_ids; only messages_list (host strings) is left to the lazy build."""
+        from ..protocol import TensorBatch
+        self._batch = TensorBatch(batch)
+        self._device_batch = True
+        ids = np.asarray(env_ids, np.int64)
+        dict.__setitem__(self.non_tensor_batch, "group_ids", np.array((ids // group_size).tolist(), dtype=object))
+        dict.__setitem__(self.non_tensor_batch, "env_ids", np.array(ids.tolist(), dtype=object))
+
     @property
     def batch(self):
-        self._build()
+        if not getattr(self, "_device_batch", False):
+            self._build()
         return self._batch
 
     @batch.setter
     def batch(self, v):
         self._batch = v
 
-    def __len__(self):
-        return len(dict.__getitem__(self.non_tensor_batch, "env_ids"))
-
     def _build(self):
         if self._built:
             return
         self._built = True
         real = self._build_fn()
+        if getattr(self, "_device_batch", False):  # only the host strings are missing
+            dict.__setitem__(self.non_tensor_batch, "messages_list", real.non_tensor_batch["messages_list"])
+            return
         self._batch = real.batch
         dict.update(self.non_tensor_batch, real.non_tensor_batch)
 
 
 class ContextManager:
-    def __init__(self, config, tokenizer, processor=None, mode: str = "train", device=None):
+    def __init__(self, config, tokenizer, processor=None, mode: str = "train", device=None,
+                 rank: Optional[int] = None, world_size: Optional[int] = None, process_group=None):
         self.config = config
         self.tokenizer = tokenizer
         self.processor = processor
         self.action_sep = self.config.agent_proxy.action_sep
         self.special_token_list = list(SPECIAL_TOKENS)
         self.es_cfg = self.config.es_manager[mode]
-        self.env_nums = {tag: n * self.es_cfg.group_size
+        self.env_nums = {tag: n * self.es_cfg.group_size  # GLOBAL counts (the metric denominators)
                          for n, tag in zip(self.es_cfg.env_configs.n_groups, self.es_cfg.env_configs.tags)}
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
-        self.n_envs = sum(self.env_nums.values())
+        self.process_group = process_group
+        if process_group is not None:
+            import torch.distributed as dist
+            rank, world_size = dist.get_rank(process_group), dist.get_world_size(process_group)
+        self.rank, self.world_size = int(rank or 0), int(world_size or 1)
+        from .. import distributed as rd
+        g0, ng = rd.shard_groups(int(self.es_cfg.env_groups), self.world_size, self.rank)
+        self.env_lo = g0 * int(self.es_cfg.group_size)
+        self.n_envs = ng * int(self.es_cfg.group_size)  # this shard's envs (all of them unsharded)
         self.device_vocab = None
+        self.device_prompts = True  # build prompt ids on the device when the device path is on
+        self._es = None
+        self._prompts = None
         self._init_prefix_lookup()
 
     def set_device_vocab(self, vocab: "ops.VocabTable"):
         """Turn on the device path: generations that arrive as token ids on the GPU are decoded by
         rmi_detokenize against this byte table (ops.VocabTable.from_tokenizer for a byte-level
-        BPE tokenizer), the turn runs on the device, prompts are built only when read."""
+        BPE tokenizer), the turn runs on the device, and — once an EnvStateManager is attached
+        (attach_env_manager; LLMAgentProxy does it) — the prompt ids are built on the device
+        turn by turn (prompts.DevicePrompts)."""
         self.device_vocab = vocab
         return self
+
+    def attach_env_manager(self, es):
+        """The EnvStateManager whose device record this manager reads on the device path."""
+        self._es = es
+        self._prompts = None
+        return self
+
+    def prompts(self):
+        """The device prompt builder, or None where it does not apply (no device vocab or env
+        manager, max_context_window set, or a tokenizer / chat template outside
+        prompts.DevicePrompts' envelope: the reason is warned once)."""
+        if self._prompts is not None:
+            return self._prompts or None
+        if self.device_vocab is None or self._es is None or not self.device_prompts:
+            return None
+        if getattr(self.config.agent_proxy, "max_context_window", None) not in (None, 0, -1):
+            self._prompts = False
+            return None
+        from .prompts import DevicePrompts
+        try:
+            self._prompts = DevicePrompts(self, self._es, self.tokenizer, self.device)
+        except NotImplementedError as e:
+            warnings.warn(f"device prompt ids off, host tokenizer used: {e}", RuntimeWarning)
+            self._prompts = False
+            return None
+        return self._prompts
+
+    def _sync_prompts(self, pr):
+        """Bring the prompt arena up to the env manager's turns."""
+        es = self._es
+        if pr.rollout != es.rollout_id:
+            pr.start()
+        for d in es._turn_records[pr.turns_done:]:
+            pr.advance(d)
 
     def _init_prefix_lookup(self):
         """ctx_manager.py:107-146."""
@@ -345,15 +408,26 @@ class ContextManager:
         return score_tensor
 
     def get_lm_inputs(self, env_outputs: List[Dict], prepare_for_update: bool) -> DataProto:
-        """ctx_manager.py:228-330.  On the device path the generation inputs are lazy
-        (LazyDataProto): env ids now, prompts when the actor reads them."""
+        """ctx_manager.py:228-330.  On the device path with device prompts the generation batch
+        is built from the device prompt arena (input_ids / attention_mask / position_ids on the
+        GPU; messages_list built on the host only when read); without them the inputs are lazy
+        (LazyDataProto): env ids now, the host-tokenized batch when the actor reads it."""
         if self.device_vocab is not None and not prepare_for_update:
             env_ids = env_outputs.env_ids if hasattr(env_outputs, "env_ids") else \
                 np.array([o["env_id"] for o in env_outputs], np.int64)
+            pr = self.prompts()
+            if pr is not None:
+                self._sync_prompts(pr)
+                batch = pr.gen_batch(env_ids)
+                out = LazyDataProto(env_ids, lambda: self._messages_only(list(env_outputs), False))
+                out.set_device_batch(batch, env_ids, self.es_cfg.group_size)
+                return out
             return LazyDataProto(env_ids, lambda: self.get_lm_inputs_eager(list(env_outputs)))
         return self.get_lm_inputs_eager(env_outputs, prepare_for_update)
 
-    def get_lm_inputs_eager(self, env_outputs: List[Dict], prepare_for_update: bool = False) -> DataProto:
+    def _build_messages(self, env_outputs: List[Dict], prepare_for_update: bool):
+        """ctx_manager.py:236-276: the chat messages of every env's history and their templated
+        text (the histories are trimmed in place as the reference does).  -> (texts, messages)."""
         ap = self.config.agent_proxy
         llm_input_texts, messages_list = [], []
         for env_output in env_outputs:
@@ -385,6 +459,18 @@ class ContextManager:
                 text += "<think>" if ap.enable_think else "<answer>"
             llm_input_texts.append(text)
             messages_list.append(messages)
+        return llm_input_texts, messages_list
+
+    def _messages_only(self, env_outputs, prepare_for_update):
+        """messages_list for a device-built batch (on shallow copies: the caller's histories are
+        trimmed by the device path's own bookkeeping)."""
+        copies = [dict(o) for o in env_outputs]
+        _, msgs = self._build_messages(copies, prepare_for_update)
+        return DataProto(None, {"messages_list": np.array(msgs, dtype=object)})
+
+    def get_lm_inputs_eager(self, env_outputs: List[Dict], prepare_for_update: bool = False) -> DataProto:
+        ap = self.config.agent_proxy
+        llm_input_texts, messages_list = self._build_messages(env_outputs, prepare_for_update)
         if prepare_for_update:
             # ragged token rows -> the padded batch, masks and scores in one device pass
             # (rmi_assemble_batch); the batch is copied to the CPU, single-device like the
@@ -461,12 +547,127 @@ class ContextManager:
         R = resp.shape[1]
         ids = torch.zeros(self.n_envs, R, dtype=torch.int64, device=dev)
         n_ids = torch.zeros(self.n_envs, dtype=torch.int32, device=dev)
-        ids[idx] = resp.to(torch.int64)
-        n_ids[idx] = R
+        ids[idx - self.env_lo] = resp.to(torch.int64)
+        n_ids[idx - self.env_lo] = R
         per_tok = vocab.max_token_bytes or 16
         stride = min(12288, (R * per_tok + 3) // 4 * 4)
         text, tlen, err = torch.ops.ragen_amd.detokenize(ids, n_ids, vocab.off, vocab.data, vocab.skip, stride)
         return DeviceEnvInputs(self, env_ids, idx, text, tlen, err)
 
     def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:
+        """ctx_manager.py:354-356.  The rollout states of the attached env manager's device path
+        (LazyRolloutStates) with device prompts are formulated on the device (formulate_device);
+        anything else through the reference's host code."""
+        from .es_manager import LazyRolloutStates
+        pr = self.prompts()
+        if (pr is not None and isinstance(env_outputs, LazyRolloutStates) and env_outputs.es is self._es
+                and env_outputs.rollout_id == self._es.rollout_id):
+            return self.formulate_device(pr)
         return self.get_lm_inputs_eager(env_outputs, prepare_for_update=True)
+
+    def formulate_device(self, pr) -> DataProto:
+        """formulate_rollouts (get_lm_inputs(prepare_for_update=True), ctx_manager.py:228-330) from
+        the device record: the update rows of the prompt arena (each env's conversation up to its
+        last assistant block) assembled with masks and scores in one pass (rmi_assemble_rows),
+        scores = the turn rewards (n_turns per env), the reward normalisation on the device, and
+        the metrics (ctx_manager.py:308-329) from one copy of the per-env metric rows.  The
+        batch stays on the GPU; messages_list is built on the host only when read."""
+        es = self._es
+        self._sync_prompts(pr)
+        ap = self.config.agent_proxy
+        dev = self.device
+        tokens, start, row_len = pr.update_rows()
+        S = int(row_len.max()) if row_len.numel() else 1
+        eps = [tg.batch.ep for tg in es.tags]
+        tab = (eps[0].turn_reward if len(eps) == 1 else torch.cat([ep.turn_reward for ep in eps], 1)).contiguous()
+        n_sc = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
+        special_token, reward_token = get_special_tokens(self.tokenizer)
+        ids, am, pos, score_tensor, loss_mask, response_mask, err = torch.ops.ragen_amd.assemble_rows(
+            tokens, start, row_len, max(S, 1), int(pr.pad_id), int(special_token), int(reward_token), tab, n_sc,
+            tab.shape[0], bool(ap.use_turn_scores), bool(self.config.enable_response_mask),
+            "qwen" in self.tokenizer.name_or_path.lower())
+        _raise_assemble_errors(err, S)
+        normalized = score_tensor
+        if not ap.use_turn_scores:
+            normalized = self._normalize_device(score_tensor, es)
+        response_length = response_mask.sum(dim=-1).float().mean().item()
+        batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
+                 "loss_mask": loss_mask, "rm_scores": normalized, "original_rm_scores": normalized}
+        env_ids = es.env_lo + np.arange(es.n_envs, dtype=np.int64)
+        out = LazyDataProto(env_ids, lambda: self._messages_only(es._rollout_states_full(), True))
+        out.set_device_batch(batch, env_ids, es.group_size)
+        metrics = self.device_metrics(es)
+        metrics["response_length"] = response_length
+        out.meta_info = {"metrics": metrics}
+        es._formulated = True
+        return out
+
+    def _normalize_device(self, score_tensor, es):
+        """_normalize_score_tensor (ctx_manager.py:175-226) from the device record: penalties from
+        the episode arena, groups by grouping (state: group ids, contiguous; inductive: tags;
+        batch: all).  Under sharding the "state" groups are rank-local; the other groupings
+        need every rank's scores (ragen_amd.distributed: gathered, normalised identically on
+        every rank, the own rows kept)."""
+        rn = self.config.agent_proxy.reward_normalization
+        if rn.method not in ("mean_std", "mean", "asym_clip", "identity"):
+            raise ValueError(f"Invalid normalization method: {rn.method}")
+        if rn.grouping not in ("state", "inductive", "batch"):
+            raise ValueError(f"Invalid grouping: {rn.grouping}")
+        from .. import distributed as rd
+        eps = [tg.batch.ep for tg in es.tags]
+        pen = (eps[0].penalty if len(eps) == 1 else torch.cat([ep.penalty for ep in eps])).to(torch.float32)
+        acc = score_tensor[:, -1].contiguous()
+        dev = acc.device
+        gs = es.group_size
+        if rn.grouping == "state":
+            seg = np.arange(0, es.n_envs + 1, gs, dtype=np.int32)
+            out = torch.ops.ragen_amd.group_normalize(acc, pen.contiguous(), ops.segments(seg, es.n_envs, dev),
+                                                      NORM[rn.method])
+        else:
+            sharded = self.process_group is not None and self.world_size > 1
+            a_all = rd.all_gather_rows(acc, group=self.process_group) if sharded else acc
+            p_all = rd.all_gather_rows(pen.contiguous(), group=self.process_group) if sharded else pen
+            n_all = a_all.numel()
+            if rn.grouping == "batch":
+                seg = np.array([0, n_all], np.int32)
+            else:  # tags: contiguous global env ranges in config order
+                cuts = np.cumsum([0] + [n * gs for n in self.es_cfg.env_configs.n_groups]).astype(np.int32)
+                seg = np.unique(cuts)
+            res = torch.ops.ragen_amd.group_normalize(a_all.contiguous(), p_all.contiguous(),
+                                                      ops.segments(seg, n_all, dev), NORM[rn.method])
+            out = res[es.env_lo:es.env_lo + es.n_envs] if sharded else res
+        score_tensor[:, -1] = out
+        return score_tensor
+
+    def device_metrics(self, es) -> Dict:
+        """The mean / non-zero metrics of get_lm_inputs (ctx_manager.py:308-329) from the device
+        metric rows (es.metric_arrays: one copy per tag), with numpy over whole arrays in env
+        order — the same values and summation order as the reference's lists.  Under sharding
+        every rank's rows are gathered first, so each rank reports the global metrics."""
+        from .. import distributed as rd
+        parts = es.metric_arrays()
+        sharded = self.process_group is not None and self.world_size > 1
+        local = {tag: np.concatenate([m, custom[:, None].astype(np.float64)], 1) for tag, m, custom, _ in parts}
+        per_tag = {}
+        for tag in dict.fromkeys(self.es_cfg.env_configs.tags):  # every rank, same order (collectives)
+            rows = local.get(tag, np.zeros((0, 5), np.float64))
+            if sharded:
+                rows = rd.all_gather_rows(torch.from_numpy(rows).to(self.device), group=self.process_group).cpu().numpy()
+            if len(rows):
+                per_tag[tag] = [rows]
+        metrics, nz = {}, []
+        for tag in dict.fromkeys(self.es_cfg.env_configs.tags):
+            if tag not in per_tag:
+                continue
+            rows = np.concatenate(per_tag[tag])
+            cust = rows[:, 4] != 0
+            cols = [("success", rows[:, 0]), ("num_actions", rows[:, 1].astype(np.int64))]
+            if cust.any():
+                cols += [("action_is_effective", rows[cust, 2]), ("action_is_valid", rows[cust, 3])]
+            for k, v in cols:
+                metrics[f"{tag}/{k}"] = np.sum(v) / self.env_nums[tag]
+                nz.append((f"{tag}/non-zero/{k}", v[v != 0]))
+        for k, v in nz:
+            if len(v):
+                metrics[k] = np.mean(v)
+        return metrics

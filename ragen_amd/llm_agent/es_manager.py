@@ -7,9 +7,18 @@ action strings to ids on the host (es_manager.py:230-240), runs ONE kernel launc
 for the whole turn, then reads back four small per-env vectors to build the dicts.
 
 ``step_tensor`` is the dict-free fast path (used by the benchmark's kernel variant).
+
+Sharding: with ``rank`` / ``world_size`` (or a ``process_group``) the manager
+owns the contiguous, group-aligned shard ``ragen_amd.distributed.shard_groups`` gives this
+rank; env ids, group ids and seeds stay GLOBAL (seed + global env id // group_size,
+es_manager.py:80-82), so a rank's envs are bit-identical to the same envs of a one-process
+run.  The train seed drawn by ``random.randint`` (es_manager.py:88-89) is broadcast from rank
+0 over the process group; without a group a sharded manager needs the seed passed in.
+``rollout_cache`` holds this shard's envs in env order (``env_lo`` = global id of the first).
 """
 import random
 import warnings
+from collections.abc import Sequence
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -17,9 +26,10 @@ import numpy as np
 import torch
 
 from .. import _lib
+from .. import distributed as rd
 from ..env import REGISTERED_ENV_CONFIGS, REGISTERED_ENVS
-from ..torch_ops import ep_args, parse_cfg_bytes
 from ..env.base import BatchEnv
+from ..torch_ops import ep_args, parse_cfg_bytes
 
 
 @dataclass
@@ -47,19 +57,44 @@ class LazyEnvOutputs:
 
     def __getitem__(self, k):
         self._es._materialize()
-        rc = self._es.rollout_cache
+        rc, lo = self._es.rollout_cache, self._es.env_lo
         if isinstance(k, slice):
-            return [rc[int(g)] for g in self.env_ids[k]]
-        return rc[int(self.env_ids[k])]
+            return [rc[int(g) - lo] for g in self.env_ids[k]]
+        return rc[int(self.env_ids[k]) - lo]
 
     def __iter__(self):
-        self._es._materialize()
-        rc = self._es.rollout_cache
-        return iter([rc[int(g)] for g in self.env_ids])
+        rc, lo = self._es.rollout_cache, self._es.env_lo
+        return iter([rc[int(g) - lo] for g in self.env_ids])
+
+
+class LazyRolloutStates(Sequence):
+    """get_rollout_states() on the device path: the rollout cache with its metrics, built on
+    first element access (host parse of the generations, history dicts, per-env metrics).
+    ContextManager.formulate_rollouts reads the device record instead and never builds them."""
+
+    def __init__(self, es):
+        self.es = es
+        self.rollout_id = es.rollout_id
+        self.env_ids = es.env_lo + np.arange(es.n_envs, dtype=np.int64)
+
+    def _full(self):
+        return self.es.rollout_cache
+
+    def __len__(self):
+        return self.es.n_envs
+
+    def __getitem__(self, k):
+        return self._full()[k]
+
+    def __iter__(self):
+        return iter(self._full())
+
+    def __eq__(self, other):
+        return list(self._full()) == list(other)
 
 
 class _Tag:
-    """One env tag = one contiguous env range [lo, hi) = one batch object."""
+    """One env tag of this shard = one contiguous GLOBAL env range [lo, hi) = one batch object."""
 
     def __init__(self, tag, lo, hi, batch, max_actions_per_traj, env_type):
         self.tag, self.lo, self.hi, self.batch = tag, lo, hi, batch
@@ -74,22 +109,47 @@ def _make_env_config(env_type, env_config):
     return cls(**dict(env_config))
 
 
+def shard_plan(n_groups_per_tag, group_size, rank, world_size):
+    """Group-aligned shard of rank r: -> (first global group, n local groups, [(tag index,
+    global env lo, global env hi)] of the tags it intersects).  Pure host logic."""
+    G = sum(n_groups_per_tag)
+    g0, ng = rd.shard_groups(G, world_size, rank)
+    out, cur = [], 0
+    for j, n in enumerate(n_groups_per_tag):
+        lo, hi = max(cur, g0), min(cur + n, g0 + ng)
+        if hi > lo:
+            out.append((j, lo * group_size, hi * group_size))
+        cur += n
+    return g0, ng, out
+
+
 class EnvStateManager:
-    def __init__(self, config, mode: str = "train", device=None):
+    def __init__(self, config, mode: str = "train", device=None, rank: Optional[int] = None,
+                 world_size: Optional[int] = None, process_group=None):
         self.sys_config = config
         self.mode = mode
         self.config = getattr(self.sys_config.es_manager, mode)
         self.env_groups = int(self.config.env_groups)
         self.group_size = int(self.config.group_size)
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.process_group = process_group
+        if process_group is not None:
+            import torch.distributed as dist
+            rank, world_size = dist.get_rank(process_group), dist.get_world_size(process_group)
+        self.rank, self.world_size = int(rank or 0), int(world_size or 1)
         ap = self.sys_config.agent_proxy
         self.max_turn = int(ap.max_turn)
         self.K = int(ap.max_actions_per_turn)
         self.format_penalty = float(self.sys_config.es_manager.format_penalty)
         self._init_envs()
-        self.rollout_cache = None
+        self._rc = None
+        self._states_pending = False  # a LazyRolloutStates was handed out and not built yet
+        self._formulated = False      # the device formulate_rollouts ran: drop the last states when built
+        self._untrimmed = None
+        self.rollout_id = 0
         self._turn = 0
-        self._device_turns = []  # device-path turns whose host bookkeeping is still pending
+        self._turn_records = []  # device-path turns (ContextManager's device prompts read them too)
+        self._mat_upto = 0       # records whose host bookkeeping is done
 
     def _init_envs(self):
         n_groups = list(self.config.env_configs.n_groups)
@@ -98,46 +158,78 @@ class EnvStateManager:
             f"Sum of n_groups must equal env_groups. Got sum({n_groups}) != {self.env_groups}"
         assert len(tags) == len(n_groups), \
             f"Number of tags must equal number of n_groups. Got {len(tags)} != {len(n_groups)}"
+        g0, ng, parts = shard_plan(n_groups, self.group_size, self.rank, self.world_size)
+        self.first_group, self.n_local_groups = g0, ng
+        self.env_lo = g0 * self.group_size
+        self.n_envs = ng * self.group_size
         self.tags: List[_Tag] = []
-        done_groups = 0
-        for tag, ng in zip(tags, n_groups):
+        for j, lo, hi in parts:
+            tag = tags[j]
             cfg_t = self.sys_config.custom_envs[tag]
             env_type = cfg_t.env_type
             env_config = _make_env_config(env_type, cfg_t.get("env_config"))
-            lo, hi = done_groups * self.group_size, (done_groups + ng) * self.group_size
             batch = REGISTERED_ENVS[env_type](env_config, hi - lo, self.max_turn, self.K, self.device)
             self.tags.append(_Tag(tag, lo, hi, batch, cfg_t.max_actions_per_traj, env_type))
-            done_groups += ng
-        self.n_envs = done_groups * self.group_size
         self._tag_of = np.zeros(self.n_envs, np.int32)
         for j, t in enumerate(self.tags):
-            self._tag_of[t.lo:t.hi] = j
+            self._tag_of[t.lo - self.env_lo:t.hi - self.env_lo] = j
         # reference-shaped entries (es_manager.py:69-70); 'env' is the batch, 'local' its row
         self.envs = [{"tag": t.tag, "group_id": i // self.group_size, "env_id": i, "env": t.batch,
                       "local": i - t.lo, "config": t.batch.config, "status": EnvStatus(),
                       "max_actions_per_traj": t.max_actions_per_traj}
                      for t in self.tags for i in range(t.lo, t.hi)]
 
+    @property
+    def rollout_cache(self):
+        """es_manager.py:85's rollout cache (this shard's envs): device-path turns and lazily
+        handed-out rollout states are built into the dicts before it is read."""
+        self._materialize()
+        if self._states_pending:
+            self._rollout_states_host()
+        if self._formulated:  # formulate_rollouts dropped each history's last state (ctx_manager.py:236-237)
+            self._formulated = False
+            self._untrimmed = [c["history"] for c in self._rc]
+            for cache in self._rc:
+                if "state" in cache["history"][-1]:
+                    cache["history"] = cache["history"][:-1]
+        return self._rc
+
     # ---------------------------------------------------------------------- reset
+    def _train_seed(self, seed):
+        if seed is not None:
+            return int(seed)
+        if self.process_group is not None:
+            import torch.distributed as dist
+            box = [random.randint(0, 1000000) if self.rank == 0 else None]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(self.process_group, 0), group=self.process_group)
+            return int(box[0])
+        if self.world_size > 1:
+            raise ValueError("a sharded EnvStateManager without a process group needs reset(seed=...) so that every "
+                             "rank uses the same train seed")
+        return random.randint(0, 1000000)
+
     def reset(self, seed: Optional[int] = None):
         """es_manager.py:75-103."""
-        if self.mode == "train":
-            seed = random.randint(0, 1000000) if seed is None else seed
-        else:
-            seed = 123
-        seeds = seed + np.arange(self.n_envs) // self.group_size  # _expand_seed
+        seed = self._train_seed(seed) if self.mode == "train" else 123
+        gids = self.env_lo + np.arange(self.n_envs)
+        seeds = seed + gids // self.group_size  # _expand_seed, global ids
         for t in self.tags:
-            t.batch.reset(seeds[t.lo:t.hi])
+            t.batch.reset(seeds[t.lo - self.env_lo:t.hi - self.env_lo])
         self._turn = 0
-        self._device_turns = []
+        self._turn_records = []
+        self._mat_upto = 0
+        self.rollout_id += 1
         self._seeds = seeds
-        self.rollout_cache = [{"env_id": e["env_id"], "history": [], "group_id": e["group_id"], "tag": e["tag"],
-                               "penalty": 0} for e in self.envs]
-        for e, cache in zip(self.envs, self.rollout_cache):
-            e["status"] = EnvStatus(seed=int(seeds[e["env_id"]]))
+        self._states_pending = False
+        self._formulated = False
+        self._untrimmed = None
+        self._rc = [{"env_id": e["env_id"], "history": [], "group_id": e["group_id"], "tag": e["tag"],
+                     "penalty": 0} for e in self.envs]
+        for e, cache in zip(self.envs, self._rc):
+            e["status"] = EnvStatus(seed=int(seeds[e["env_id"] - self.env_lo]))
             cache["history"] = self._update_cache_history(cache["history"], e["env"].render(e["local"]),
                                                           e["max_actions_per_traj"], None)
-        return self.rollout_cache
+        return self._rc
 
     # ----------------------------------------------------------------------- step
     def step(self, all_env_inputs: List[Dict]):
@@ -151,6 +243,7 @@ class EnvStateManager:
         if self._turn >= self.max_turn:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
+        lo0 = self.env_lo
         gids_all = [int(inp["env_id"]) for inp in all_env_inputs]
         if len(self.tags) == 1:
             per_tag = {0: (all_env_inputs, gids_all)}
@@ -158,7 +251,7 @@ class EnvStateManager:
             per_tag = {j: ([], []) for j in range(len(self.tags))}
             tag_of = self._tag_of
             for inp, g in zip(all_env_inputs, gids_all):
-                ins, gs = per_tag[int(tag_of[g])]
+                ins, gs = per_tag[int(tag_of[g - lo0])]
                 ins.append(inp)
                 gs.append(g)
         still_active = set()
@@ -188,9 +281,10 @@ class EnvStateManager:
                 ids[np.repeat(r, ln), cols] = [x for m in m_l for x in m]
             is_cd = tg.env_type == "countdown"
             dev = self.device
-            ids_t = torch.from_numpy(ids).to(dev, non_blocking=True)
-            n_t = torch.from_numpy(n).to(dev, non_blocking=True)
-            has_t = torch.from_numpy(has).to(dev, non_blocking=True)
+            # one host -> device copy of the turn's inputs
+            packed = torch.from_numpy(np.concatenate([ids.view(np.uint8).reshape(-1), n, has])).to(dev)
+            ids_t = packed[:B * K].view(torch.int8).view(B, K)
+            n_t, has_t = packed[B * K:B * K + B], packed[B * K + B:]
             kw = {}
             if is_cd:
                 answers = [[] for _ in range(B)]
@@ -201,22 +295,21 @@ class EnvStateManager:
             err = torch.zeros(B, dtype=torch.uint8, device=dev)
             tg.batch.step_turn(t, ids_t, n_t, has_t, tg.max_actions_per_traj, self.format_penalty, err, **kw)
             ep = tg.batch.ep
-            host = torch.stack([ep.flags.to(torch.int64), ep.num_actions.to(torch.int64),
-                                ep.turn_info[t].to(torch.int64), ep.turn_exec[t].to(torch.int64),
-                                err.to(torch.int64)]).cpu().numpy()
+            # one device -> host copy: flags, counters, info, exec count, error bits (as bytes)
+            # and the turn reward / penalty (f64)
+            host = torch.stack([ep.flags, ep.num_actions, ep.turn_info[t], ep.turn_exec[t], err]).cpu().numpy()
+            f64 = torch.stack([ep.turn_reward[t], ep.penalty]).cpu().numpy()
             self._raise_errors(tg, host[4], rows, gids)
-            rw = ep.turn_reward[t].cpu().numpy()
-            pen = ep.penalty.cpu().numpy()
             # one host copy per turn, as Python lists (numpy scalar indexing per env is slower)
             flags, num_actions, info, n_exec = (x.tolist() for x in host[:4])
             # the text observation of every env at once unless the env type renders per env
             obs = tg.batch.render_all() if type(tg.batch).render is BatchEnv.render else None
             still_active |= self._book(tg, t, inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec,
-                                       rw.tolist(), pen.tolist(), obs)
+                                       f64[0].tolist(), f64[1].tolist(), obs)
         self._turn += 1
         # only not-done envs go back for generation, in input order (es_manager.py:168-169)
-        rc = self.rollout_cache
-        return [rc[g] for g in gids_all if g in still_active]
+        rc = self._rc
+        return [rc[g - lo0] for g in gids_all if g in still_active]
 
     def _book(self, tg, t, inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec, rw, pen, obs):
         """The host side of one turn for one tag (es_manager.py:130-169): EnvStatus, penalty and the
@@ -227,10 +320,10 @@ class EnvStateManager:
         is_cd = tg.env_type == "countdown"
         note = getattr(tg.batch, "note_executed", None)
         render = tg.batch.render
-        envs, rcache = self.envs, self.rollout_cache
+        envs, rcache, lo0 = self.envs, self._rc, self.env_lo
         still_active = set()
         for inp, gid, i, acts, m in zip(inputs, gids, rows, acts_l, m_l):
-            entry, cache = envs[gid], rcache[gid]
+            entry, cache = envs[gid - lo0], rcache[gid - lo0]
             ne = n_exec[i]
             executed = (acts if is_cd else [a for a in m if a != 0])[:ne]
             if note is not None:
@@ -239,10 +332,11 @@ class EnvStateManager:
             if is_cd and ne and acc in (0.0, 1.0):
                 acc = int(acc)  # compute_reward returns int 0 / int score (countdown/env.py:73-78)
             inf = info[i]
-            turn_info = {}
             if inf & I_PRES:
                 turn_info = {"action_is_effective": bool(inf & I_EFF), "action_is_valid": bool(inf & I_VAL),
                              "success": bool(inf & I_SUCC)}
+            else:
+                turn_info = {}
             st = entry["status"]
             na = num_actions[i]
             st.num_actions = na
@@ -294,13 +388,12 @@ class EnvStateManager:
         self._turn += 1
         return tg.batch.ep
 
-    # ------------------------------------------------------- get_rollout_states
     def step_text(self, text: torch.Tensor, text_len: torch.Tensor, has_input: Optional[torch.Tensor] = None,
                   enable_think: bool = True, action_sep: str = "||", prepend: bool = True,
                   err: Optional[torch.Tensor] = None):
-        """Device-resident turn from response text (§8(f) rank 2): rows are the envs in env-id
-        order, text u8[n_envs, stride] / text_len i32[n_envs] the decoded generations (e.g.
-        ops.detokenize of the response ids).  Per tag one parse launch
+        """Device-resident turn from response text (§8(f) rank 2): rows are this shard's envs in
+        env-id order, text u8[n_envs, stride] / text_len i32[n_envs] the decoded generations
+        (e.g. ops.detokenize of the response ids).  Per tag one parse launch
         (_parse_response + _extract_map_valid_actions, ctx_manager.py:148-173,
         es_manager.py:230-240) feeds one turn launch; nothing returns to the host.
         -> list of per-tag parse outputs (ops.parse_actions dicts)."""
@@ -309,26 +402,33 @@ class EnvStateManager:
         if text.shape[0] != self.n_envs or text_len.shape[0] != self.n_envs:
             raise ValueError(f"text rows must cover all {self.n_envs} envs")
         outs = []
+        lo0 = self.env_lo
         for tg in self.tags:
+            a, z = tg.lo - lo0, tg.hi - lo0
             cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, prepend)
             acts, n_act, spans, at, al, perr = torch.ops.ragen_amd.parse_actions(
-                parse_cfg_bytes(cfg), text[tg.lo:tg.hi], text_len[tg.lo:tg.hi], sel, True, int(lact))
+                parse_cfg_bytes(cfg), text[a:z], text_len[a:z], sel, True, int(lact))
             p = {"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
                  "action_len": al if lact else None, "err": perr}
-            has = None if has_input is None else has_input[tg.lo:tg.hi]
+            has = None if has_input is None else has_input[a:z]
             kw = {}
             if lact:
                 kw = {"answers": p["action_text"], "answer_len": p["action_len"]}
             tg.batch.step_turn(self._turn, p["actions"], p["n_actions"], has, tg.max_actions_per_traj,
-                               self.format_penalty, None if err is None else err[tg.lo:tg.hi], **kw)
+                               self.format_penalty, None if err is None else err[a:z], **kw)
             outs.append(p)
         self._turn += 1
         return outs
 
+    def _cat(self, xs):
+        return xs[0] if len(xs) == 1 else torch.cat(xs)
+
     def _step_device(self, inp):
         """One turn from the decoded generations on the device: parse + turn per tag (step_text),
         the next observation rendered on the device, the active set read back.  The host
-        bookkeeping (EnvStatus, history dicts, penalties) is deferred to ``_materialize``."""
+        bookkeeping (EnvStatus, history dicts, penalties) is deferred to ``_materialize``; the
+        turn's record (inputs, spans, observation, flags, actions left) is kept for it and for
+        the device prompt path (prompts.DevicePrompts.advance)."""
         if self._turn >= self.max_turn:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
@@ -337,28 +437,31 @@ class EnvStateManager:
         # outside the vocabulary) must not be stepped on: checked before the turn runs
         if bool(inp.err.any()):
             bad = int(torch.nonzero(inp.err)[0, 0])
-            raise ValueError(f"env {bad}: the decoded generation exceeded the device row buffer or held an id "
-                             "outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP)")
+            raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
+                             "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP)")
         has = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
-        has[inp.env_ids_t] = 1
+        has[inp.env_ids_t - self.env_lo] = 1
         err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
         ap = self.sys_config.agent_proxy
         parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
         obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
-        self._device_turns.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs,
-                                   "spans": [p["spans"] for p in parsed], "parsed": parsed})
-        flags = self.tags[0].batch.ep.flags if len(self.tags) == 1 else \
-            torch.cat([tg.batch.ep.flags for tg in self.tags])
+        flags = self._cat([tg.batch.ep.flags for tg in self.tags])
+        left = self._cat([tg.max_actions_per_traj - tg.batch.ep.num_actions.to(torch.int32) for tg in self.tags])
+        self._turn_records.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs,
+                                   "spans": [p["spans"] for p in parsed], "flags": flags.clone(),
+                                   "left": left.to(torch.int32).contiguous()})
         # one device -> host copy: the active set and the turn's per-env error bits, raised in
         # the step where they happen, as the reference raises inside its per-env loop
         n_in = len(inp.env_ids)
-        host = torch.cat([((flags[inp.env_ids_t] & _lib.FLAG_DONE) == 0).to(torch.uint8), err]).cpu().numpy()
+        host = torch.cat([((flags[inp.env_ids_t - self.env_lo] & _lib.FLAG_DONE) == 0).to(torch.uint8),
+                          err]).cpu().numpy()
         still, err_h = host[:n_in].astype(bool), host[n_in:]
         if err_h.any():
             for tg in self.tags:
                 gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]
-                self._raise_errors(tg, err_h[tg.lo:tg.hi], [g - tg.lo for g in gids], gids)
-            self._device_turns[-1]["err_seen"] = True
+                self._raise_errors(tg, err_h[tg.lo - self.env_lo:tg.hi - self.env_lo], [g - tg.lo for g in gids],
+                                   gids)
+            self._turn_records[-1]["err_seen"] = True
         return LazyEnvOutputs(self, inp.env_ids[still])
 
     def _materialize(self):
@@ -367,11 +470,12 @@ class EnvStateManager:
         executed counts, the final flags and penalties, num_actions as the running sum of the
         executed counts — plus the host parse of each decoded generation for the history
         strings (llm_response, llm_raw_response, the executed action names)."""
-        if not self._device_turns:
+        if self._mat_upto >= len(self._turn_records):
             return
         from .. import ops
         from .ctx_manager import parse_response_spans
-        turns, self._device_turns = self._device_turns, []
+        turns = self._turn_records[self._mat_upto:]
+        self._mat_upto = len(self._turn_records)
         ap = self.sys_config.agent_proxy
         prefix = "<think>" if ap.enable_think else "<answer>"
         rec = []
@@ -379,6 +483,7 @@ class EnvStateManager:
             ep = tg.batch.ep
             rec.append((ep.turn_reward.cpu().numpy(), ep.turn_info.cpu().numpy(), ep.turn_exec.cpu().numpy(),
                         ep.flags.cpu().numpy(), ep.penalty.cpu().numpy()))
+        lo0 = self.env_lo
         for d in turns:
             t, inp = d["turn"], d["inp"]
             texts = inp.decoded()
@@ -388,7 +493,7 @@ class EnvStateManager:
                 if not gids:
                     continue
                 rows = [g - tg.lo for g in gids]
-                raws = [prefix + texts[g] for g in gids]
+                raws = [prefix + texts[g - lo0] for g in gids]
                 spans = d["spans"][j].cpu().numpy()  # the device parse's regex match, per tag row
                 parsed = [parse_response_spans(r, spans[i], bool(ap.enable_think), ap.action_sep, self.K)
                           for r, i in zip(raws, rows)]
@@ -396,36 +501,83 @@ class EnvStateManager:
                 acts_l = [a for _, a in parsed]
                 m_l = tg.batch.map_actions_many(rows, acts_l)
                 if not d.get("err_seen"):
-                    self._raise_errors(tg, err[tg.lo:tg.hi], rows, gids)
+                    self._raise_errors(tg, err[tg.lo - lo0:tg.hi - lo0], rows, gids)
                 tr, ti, te, fl, pen = rec[j]
                 num_actions = te[:t + 1].astype(np.int64).sum(0)
                 obs = ops.decode_rows(*d["obs"][j]) if j in d["obs"] else None
                 self._book(tg, t, inputs, gids, rows, acts_l, m_l, fl.tolist(), num_actions.tolist(), ti[t].tolist(),
                            te[t].tolist(), tr[t].tolist(), pen.tolist(), obs)
 
-    def get_rollout_states(self):
-        """es_manager.py:173-207 (per-env metrics reduced on the device)."""
-        self._materialize()
+    # ------------------------------------------------------- get_rollout_states
+    def metric_arrays(self):
+        """Per-env rollout metrics of this shard from the device record, one copy per tag:
+        -> list of (tag, m f64[B_tag, 4] = success, num_actions, action_is_effective mean,
+        action_is_valid mean, custom bool[B_tag] = some turn carried an info dict,
+        info u8[T_seen, B_tag])."""
+        out = []
+        T = min(self._turn, self.max_turn)
         for tg in self.tags:
             ep = tg.batch.ep
-            m = torch.ops.ragen_amd.rollout_metrics(*ep_args(ep)).cpu().numpy()
-            info = ep.turn_info.cpu().numpy()
+            m = torch.ops.ragen_amd.rollout_metrics(*ep_args(ep))
+            info = ep.turn_info[:T]
+            both = torch.cat([m.view(torch.uint8).reshape(-1), info.reshape(-1)]).cpu().numpy()
+            mh = both[:m.numel() * 8].view(np.float64).reshape(m.shape)
+            ih = both[m.numel() * 8:].reshape(T, -1)
+            custom = (ih & _lib.INFO_PRESENT).any(0) if T else np.zeros(mh.shape[0], bool)
+            out.append((tg.tag, mh, custom, ih))
+        return out
+
+    def get_rollout_states(self):
+        """es_manager.py:173-207.  On the device path (turns taken from device token ids) the
+        states are lazy (LazyRolloutStates): ContextManager.formulate_rollouts reads the device
+        record, and the dicts are built only when a caller reads them."""
+        if self._turn_records:
+            self._states_pending = True
+            return LazyRolloutStates(self)
+        return self._rollout_states_host()
+
+    def _rollout_states_host(self):
+        """The per-env metrics dicts (es_manager.py:180-205) from one device -> host copy per
+        tag; the per-env lists are built from whole-array numpy results."""
+        self._materialize()
+        self._states_pending = False
+        eff_k, val_k = "action_is_effective", "action_is_valid"
+        for tag, m, custom, info in self.metric_arrays():
+            tg = next(x for x in self.tags if x.tag == tag)
+            succ = m[:, 0].tolist()
+            na = m[:, 1].astype(np.int64).tolist()
+            eff, val = m[:, 2].tolist(), m[:, 3].tolist()
+            present = (info & _lib.INFO_PRESENT) != 0
+            eff_b = ((info & _lib.INFO_EFFECTIVE) != 0).T.tolist()
+            val_b = ((info & _lib.INFO_VALID) != 0).T.tolist()
+            pres = present.T.tolist()
+            cust = custom.tolist()
+            k_s, k_n, k_e, k_v = f"{tag}/success", f"{tag}/num_actions", f"{tag}/{eff_k}", f"{tag}/{val_k}"
+            base = tg.lo - self.env_lo
             for i in range(tg.hi - tg.lo):
-                gid = tg.lo + i
-                cache = self.rollout_cache[gid]
-                env_metric = {"success": float(m[i, 0]), "num_actions": int(m[i, 1])}
-                custom = {}
-                for tt in range(min(self._turn, info.shape[0])):
-                    if info[tt, i] & _lib.INFO_PRESENT:
-                        custom.setdefault("action_is_effective", []).append(
-                            float(bool(info[tt, i] & _lib.INFO_EFFECTIVE)))
-                        custom.setdefault("action_is_valid", []).append(float(bool(info[tt, i] & _lib.INFO_VALID)))
-                if custom:
-                    env_metric["action_is_effective"] = float(m[i, 2])
-                    env_metric["action_is_valid"] = float(m[i, 3])
-                cache["history"][-1]["metrics"] = custom
-                cache["metrics"] = {f"{tg.tag}/{k}": v for k, v in env_metric.items()}
-        return self.rollout_cache
+                cache = self._rc[base + i]
+                metrics = {k_s: succ[i], k_n: na[i]}
+                if cust[i]:
+                    p = pres[i]
+                    metrics[k_e] = np.float64(eff[i])
+                    metrics[k_v] = np.float64(val[i])
+                    cache["history"][-1]["metrics"] = {
+                        eff_k: [float(x) for x, q in zip(eff_b[i], p) if q],
+                        val_k: [float(x) for x, q in zip(val_b[i], p) if q]}
+                else:
+                    cache["history"][-1]["metrics"] = {}
+                cache["metrics"] = metrics
+        return self._rc
+
+    def _rollout_states_full(self):
+        """Shallow copies of the rollout cache entries with every history entry (as
+        formulate_rollouts found them, before its trim)."""
+        self._materialize()
+        if self._states_pending:
+            self._rollout_states_host()
+        if self._untrimmed is not None:
+            return [dict(c, history=h) for c, h in zip(self._rc, self._untrimmed)]
+        return [dict(c) for c in self._rc]
 
     @staticmethod
     def _update_cache_history(history, next_state, actions_left, num_actions_info=None):

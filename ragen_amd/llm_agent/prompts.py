@@ -1,0 +1,334 @@
+"""Prompt token ids built on the device, turn by turn (§8(f) ranks 1-2).
+
+The reference rebuilds every env's whole conversation each turn — chat messages from the
+history, ``apply_chat_template``, then the tokenizer over all of it (ctx_manager.py:228-278) —
+and once more for the update batch (formulate_rollouts, :354-356 -> :278-306).  Here each env
+keeps its prompt as token ids in a device arena, and a turn APPENDS the ids of the text it
+adds, built and tokenized on the device:
+
+* the chat template is cut once (``ChatTemplate``) into the pieces the reference's messages
+  produce: the system block and the first user opening (``head``), the user / assistant
+  openings and closings, the generation prompt;
+* a reset writes ``head + first user message + user closing`` per env (rmi_prompt_text with
+  the env's instruction prefix, ``Turn 1``, its rendered state, actions left, the format and
+  length lines), then tokenizes it (rmi_bpe_encode);
+* a turn writes ``assistant opening + llm_response + assistant closing`` (llm_response rebuilt
+  from the parse kernel's spans, exactly _parse_response, ctx_manager.py:148-173) and, for an
+  env that goes on, ``user opening + Reward / Turn / State / actions-left block + user
+  closing``, and appends their ids; the position after the assistant block is kept (the
+  update batch ends there: prepare_for_update drops the last state and reward,
+  ctx_manager.py:236-237, :258-262);
+* the generation batch is the arena rows of the active envs plus the ids of the generation
+  prompt (``gen`` + "<think>"), left-padded (rmi_pad_rows); the update batch is the arena rows
+  up to the kept positions with masks and scores (rmi_assemble_rows).
+
+Exactness: tokenizing a concatenation equals concatenating the tokenizations whenever every
+cut falls right before an added token (the tokenizer splits on added tokens first, and the
+pre-tokenizer and BPE never look across that split).  ``ChatTemplate`` checks that each
+appended piece starts with one, and the whole construction against the host tokenizer on a
+probe conversation; otherwise the device path raises NotImplementedError at construction and
+the ContextManager keeps the host path.  A row the kernels flag (text past the row buffer, a
+code point NFC may change, a reward outside the formatter's range) is built and tokenized on
+the host for that env alone (``host_rows``), and counted in ``self.host_rows_used``.
+
+``agent_proxy.max_context_window`` (history truncation with re-numbered turns) is not built
+incrementally: the ContextManager keeps the host path for it.
+"""
+import warnings
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .. import _lib
+from ..tokenizer import DeviceTokenizer
+
+SYSTEM = "You're a helpful assistant. "
+_P = ("@@RMI_S@@", "@@RMI_U1@@", "@@RMI_A1@@", "@@RMI_U2@@", "@@RMI_A2@@")
+
+
+def format_prompt(enable_think: bool) -> str:
+    return ("<think> [Your thoughts] </think> <answer> [your answer] </answer>" if enable_think
+            else "<answer> [your answer] </answer>")
+
+
+class ChatTemplate:
+    """The tokenizer's chat template cut into concatenable pieces (module docstring)."""
+
+    def __init__(self, tokenizer, system: str = SYSTEM):
+        _, U1, A1, U2, A2 = _P
+
+        def ap(msgs, gen):
+            return tokenizer.apply_chat_template(msgs, add_generation_prompt=gen, tokenize=False)
+        sysm = {"role": "system", "content": system}
+        u = lambda c: {"role": "user", "content": c}  # noqa: E731
+        a = lambda c: {"role": "assistant", "content": c}  # noqa: E731
+        r_u, r_ug = ap([sysm, u(U1)], False), ap([sysm, u(U1)], True)
+        r_a = ap([sysm, u(U1), a(A1)], False)
+        r_aug = ap([sysm, u(U1), a(A1), u(U2)], True)
+        r_aua = ap([sysm, u(U1), a(A1), u(U2), a(A2)], False)
+        try:
+            i = r_u.index(U1)
+            self.head, self.u_suf = r_u[:i], r_u[i + len(U1):]
+            assert r_ug.startswith(r_u)
+            self.gen = r_ug[len(r_u):]
+            assert r_a.startswith(r_u)
+            rest = r_a[len(r_u):]
+            j = rest.index(A1)
+            self.a_pre, self.a_suf = rest[:j], rest[j + len(A1):]
+            assert r_aug.startswith(r_a)
+            rest = r_aug[len(r_a):]
+            k = rest.index(U2)
+            self.u_pre = rest[:k]
+            assert rest[k + len(U2):] == self.u_suf + self.gen
+            assert r_aua == r_a + self.u_pre + U2 + self.u_suf + self.a_pre + A2 + self.a_suf
+        except (AssertionError, ValueError):
+            raise NotImplementedError("the chat template is not a concatenation of per-message blocks; the device "
+                                      "prompt path does not apply") from None
+
+
+class DevicePrompts:
+    """Per-env prompt ids on the device for one ContextManager / EnvStateManager pair."""
+
+    def __init__(self, ctx, es, tokenizer, device, capacity: Optional[int] = None):
+        ap = ctx.config.agent_proxy
+        self.ctx, self.es, self.tok = ctx, es, tokenizer
+        self.device = torch.device(device)
+        self.enable_think = bool(ap.enable_think)
+        self.tpl = ChatTemplate(tokenizer)
+        self.dt = DeviceTokenizer.from_hf(tokenizer, self.device)
+        starts = [s for s in self.dt.added]
+        for nm in ("a_pre", "u_pre", "gen"):
+            piece = getattr(self.tpl, nm)
+            if not any(piece.startswith(s) for s in starts):
+                raise NotImplementedError(f"template piece {nm}={piece!r} does not start with an added token")
+        self.pad_id = tokenizer.pad_token_id if getattr(tokenizer, "pad_token_id", None) is not None else 0
+        self.prefix = "<think>" if self.enable_think else "<answer>"
+        self.sep = list(ap.action_sep.encode("utf-8"))
+        self.K = int(ap.max_actions_per_turn)
+        self.max_turn = int(ap.max_turn)
+        cfg_len = getattr(getattr(getattr(ctx.config, "actor_rollout_ref", None), "rollout", None), "max_model_len",
+                          None)
+        self.cap = int(capacity or cfg_len or 8192)
+        n = es.n_envs
+        self.n_envs = n
+        # per-env tag index and per-tag strings (instruction prefix, length line, actions cap)
+        tags = es.tags
+        self.n_tags = len(tags)
+        tag = np.zeros(n, np.uint8)
+        for j, tg in enumerate(tags):
+            tag[tg.lo - es.env_lo:tg.hi - es.env_lo] = j
+        self.tag = torch.from_numpy(tag).to(self.device)
+        self.is_cd = torch.tensor([tg.env_type == "countdown" for tg in tags], device=self.device)[self.tag.long()]
+        prefixes = [ctx.prefix_lookup[tg.lo] for tg in tags]
+        lengths = [f"Max response length: {ctx.env_config_lookup[tg.lo]['max_tokens']} words (tokens)." for tg in tags]
+        self._pool = bytearray()
+        self._tag_tables = []
+        self._tag_table(prefixes)  # table 0: instruction prefix
+        self._tag_table(lengths)   # table 1: length line
+        self.mapt = torch.tensor([tg.max_actions_per_traj for tg in tags], dtype=torch.int32,
+                                 device=self.device)[self.tag.long()]
+        fmt = format_prompt(self.enable_think)
+        self._c_mid = f" actions left. Always output: {fmt} with no extra text. Strictly follow this format. "
+        # device buffers
+        self.arena = torch.zeros(n, self.cap, dtype=torch.int64, device=self.device)
+        self.len = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self.len_upd = torch.zeros(n, dtype=torch.int32, device=self.device)
+        tail = self.dt.encode([self.tpl.gen + self.prefix])[0]
+        if tail is None or tail != list(tokenizer(self.tpl.gen + self.prefix).input_ids):
+            raise NotImplementedError("the generation prompt does not encode like the host tokenizer")
+        self.tail = torch.tensor(tail, dtype=torch.int64, device=self.device)
+        self.host_rows_used = 0
+        self.rollout = None
+        self.turns_done = 0
+        self._verify()
+
+    # ---------------------------------------------------------------- constant pool
+    def _const(self, s: str):
+        b = s.encode("utf-8")
+        off = len(self._pool)
+        self._pool += b
+        return off, len(b)
+
+    def _tag_table(self, strings):
+        tab = []
+        for s in strings:
+            tab += list(self._const(s))
+        self._tag_tables.append(tab)
+
+    def _program(self, pieces):
+        """pieces: (kind, a, b) triples, CONST given as a str -> (program ints, pool, tag_const)."""
+        prog = []
+        for p in pieces:
+            if isinstance(p, str):
+                off, ln = self._const(p)
+                prog.append((_lib.PT_CONST, off, ln))
+            else:
+                prog.append(p)
+        pool = torch.frombuffer(bytearray(self._pool) + b"\0" * 4, dtype=torch.uint8).to(self.device)
+        tc = torch.tensor([x for t in self._tag_tables for x in t], dtype=torch.int32, device=self.device)
+        return prog, pool, tc
+
+    def _run_text(self, pieces, stride, obs, obs_len, ints, reward=None, reward_int=None, resp=None, resp_len=None,
+                  spans=None, cond=None, active=None):
+        prog, pool, tc = self._program(pieces)
+        flat = [len(prog)] + [x for p in prog for x in p] + [self.n_tags, obs.shape[1], 0 if resp is None else
+                                                             resp.shape[1], int(self.enable_think), self.K]
+        return torch.ops.ragen_amd.prompt_text(flat, self.sep, self.n_envs, stride, pool, tc, self.tag, obs, obs_len,
+                                               ints, reward, reward_int, resp, resp_len, spans, cond, active)
+
+    # ------------------------------------------------------------------ rollout steps
+    def _obs(self, rows_by_tag):
+        """Every env's observation text as one [n_envs, stride] buffer: the device render of the
+        tags that have one (``rows_by_tag[j]``), else the env's text at reset."""
+        parts, lens = [], []
+        st = max([r.shape[1] for r in rows_by_tag.values()] + [self._reset_obs[0].shape[1]])
+        for j, tg in enumerate(self.es.tags):
+            if j in rows_by_tag:
+                r, ln = rows_by_tag[j]
+            else:
+                r, ln = self._reset_obs[0][tg.lo - self.es.env_lo:tg.hi - self.es.env_lo], \
+                    self._reset_obs[1][tg.lo - self.es.env_lo:tg.hi - self.es.env_lo]
+            parts.append(torch.nn.functional.pad(r, (0, st - r.shape[1])))
+            lens.append(ln)
+        return torch.cat(parts).contiguous(), torch.cat(lens).contiguous()
+
+    def start(self):
+        """After es.reset(): every env's first prompt (ctx_manager.py:248-263 for history[0])."""
+        es = self.es
+        self.rollout = es.rollout_id
+        self.turns_done = 0
+        texts = []
+        for tg in es.tags:
+            texts += [tg.batch.render(i) for i in range(tg.hi - tg.lo)] if not hasattr(tg.batch, "render_rows") else \
+                [""] * (tg.hi - tg.lo)
+        bs = [t.encode("utf-8") for t in texts]
+        st = max(4, (max(len(x) for x in bs) + 3) // 4 * 4)
+        buf = np.zeros((self.n_envs, st), np.uint8)
+        for i, x in enumerate(bs):
+            buf[i, :len(x)] = np.frombuffer(x, np.uint8)
+        self._reset_obs = (torch.from_numpy(buf).to(self.device),
+                           torch.tensor([len(x) for x in bs], dtype=torch.int32, device=self.device))
+        obs, obs_len = self._obs({j: tg.batch.render_rows() for j, tg in enumerate(es.tags)
+                                  if hasattr(tg.batch, "render_rows")})
+        ints = self.mapt.clone()
+        pieces = [self.tpl.head, (_lib.PT_TAG_CONST, 0, 0), "\nTurn 1:\nState:\n", (_lib.PT_OBS, 0, 0),
+                  "\nYou have ", (_lib.PT_INT, 0, 0), self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
+        stride = self._stride(obs.shape[1] + max(len(p) for p in self.ctx.prefix_lookup.values()) + 1024)
+        text, tlen, _, terr = self._run_text(pieces, stride, obs, obs_len, ints)
+        self.len.zero_()
+        self._encode(text, tlen, terr, None, stride, lambda e: self._host_first(e))
+        self.len_upd.copy_(self.len)
+
+    def advance(self, d):
+        """Append turn d["turn"] (a device-path turn record of EnvStateManager._step_device)."""
+        t = d["turn"]
+        inp = d["inp"]
+        obs, obs_len = self._obs(d["obs"])
+        resp, resp_len = inp.text, inp.text_len
+        spans = torch.cat(d["spans"]) if len(d["spans"]) > 1 else d["spans"][0]
+        eps = [tg.batch.ep for tg in self.es.tags]
+        cat = (lambda xs: torch.cat(xs)) if len(eps) > 1 else (lambda xs: xs[0])  # noqa: E731
+        reward = cat([ep.turn_reward[t] for ep in eps]).contiguous()
+        ne = cat([ep.turn_exec[t] for ep in eps])
+        reward_int = ((ne == 0) | (self.is_cd & ((reward == 0.0) | (reward == 1.0)))).to(torch.uint8)
+        flags = d["flags"]
+        cond = (((flags & _lib.FLAG_DONE) == 0) & (t + 1 < self.max_turn)).to(torch.uint8)
+        ints = d["left"]
+        pieces = [self.tpl.a_pre, (_lib.PT_RESPONSE, 0, 0), self.tpl.a_suf, (_lib.PT_MARK, 0, 0),
+                  (_lib.PT_IF, 0, 0), self.tpl.u_pre + "Reward:\n", (_lib.PT_REWARD, 0, 0),
+                  f"\n\nTurn {t + 2}:\nState:\n", (_lib.PT_OBS, 0, 0), "\nYou have ", (_lib.PT_INT, 0, 0), self._c_mid,
+                  (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
+        stride = self._stride(resp.shape[1] + obs.shape[1] + 1024)
+        text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, reward_int, resp,
+                                                resp_len, spans, cond, d["has"])
+        self._encode(text, tlen, terr, mark, stride, lambda e: self._host_turn(e, t, bool(cond[e])),
+                     active=d["has"])
+        self.turns_done = t + 1
+
+    @staticmethod
+    def _stride(n):
+        return min(3072, (int(n) + 3) // 4 * 4)
+
+    def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None):
+        mx = int(tlen.max()) if tlen.numel() else 0
+        n_tok, mark_tok, err = self.dt.encode_rows(text, tlen, self.arena, self.len, mark, max_len=max(mx, 4))
+        bad = (err != 0) | (terr != 0)
+        if active is not None:
+            bad &= active.bool()
+        if mark is not None:  # the update batch ends after the assistant block
+            upd = torch.where(active.bool(), mark_tok, self.len_upd) if active is not None else mark_tok
+            self.len_upd.copy_(upd)
+        idx = torch.nonzero(bad).flatten().cpu().tolist()
+        if idx:
+            self.host_rows_used += len(idx)
+            warnings.warn(f"{len(idx)} prompt rows built on the host (text past the device row buffer, an NFC-changing "
+                          "code point, or an unsupported reward)", RuntimeWarning)
+            for e in idx:
+                host_fn(e)
+
+    # ---------------------------------------------------------------- host rows
+    def _write_host(self, e, ids_a, ids_b=None):
+        """Append ids for env e (a host-tokenized row); ids_b after the update mark."""
+        cur = int(self.len[e])
+        ids = list(ids_a) + list(ids_b or [])
+        if cur + len(ids) > self.cap:
+            raise RuntimeError(f"env {e}: prompt longer than the device arena ({self.cap} tokens)")
+        self.arena[e, cur:cur + len(ids)] = torch.tensor(ids, dtype=torch.int64, device=self.device)
+        self.len[e] = cur + len(ids)
+        if ids_b is not None:
+            self.len_upd[e] = cur + len(ids_a)
+
+    def _host_first(self, e):
+        g = self.es.env_lo + e
+        cache = self.es.rollout_cache[e]
+        ap = self.ctx.config.agent_proxy
+        h = cache["history"][0]
+        length = f"Max response length: {self.ctx.env_config_lookup[g]['max_tokens']} words (tokens)."
+        text = (self.tpl.head + self.ctx.prefix_lookup[g] + f"\nTurn 1:\nState:\n{h['state']}\nYou have "
+                f"{h['actions_left']}" + self._c_mid + length + "\n" + self.tpl.u_suf)
+        del ap
+        self._write_host(e, self.tok(text).input_ids)
+
+    def _host_turn(self, e, t, cont):
+        self.es._materialize()
+        g = self.es.env_lo + e
+        hist = self.es.rollout_cache[e]["history"]
+        h, nxt = hist[t], hist[t + 1]
+        a = self.tok(self.tpl.a_pre + h["llm_response"] + self.tpl.a_suf).input_ids
+        b = []
+        if cont:
+            length = f"Max response length: {self.ctx.env_config_lookup[g]['max_tokens']} words (tokens)."
+            b = self.tok(self.tpl.u_pre + f"Reward:\n{h['reward']}\n\nTurn {t + 2}:\nState:\n{nxt['state']}\n"
+                         f"You have {nxt['actions_left']}" + self._c_mid + length + "\n" + self.tpl.u_suf).input_ids
+        self._write_host(e, a, b)
+
+    # ------------------------------------------------------------------- batches
+    def gen_batch(self, env_ids: np.ndarray):
+        """get_lm_inputs(prepare_for_update=False)'s tensors for these envs (device)."""
+        rows = torch.from_numpy(np.asarray(env_ids, np.int64) - self.es.env_lo).to(self.device)
+        S = int(self.len[rows].max()) + self.tail.numel() if rows.numel() else 1
+        ids, am, pos, err = torch.ops.ragen_amd.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
+        return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
+
+    def update_rows(self):
+        """(tokens, row_start, row_len) of formulate_rollouts' rows, env order."""
+        start = torch.arange(self.n_envs, dtype=torch.int64, device=self.device) * self.cap
+        return self.arena.view(-1), start, self.len_upd
+
+    # ------------------------------------------------------------------ self-check
+    def _verify(self):
+        """The concatenation rule on a probe conversation, against the host tokenizer."""
+        t = self.tok
+        fmt = self._c_mid
+        first = "instr\nTurn 1:\nState:\n#_P#\nYou have 9" + fmt + "x.\n"
+        resp = "<think>a b</think><answer>Up || Down</answer>"
+        user2 = "Reward:\n-0.1\n\nTurn 2:\nState:\n#P_#\nYou have 7" + fmt + "x.\n"
+        parts = [self.tpl.head + first + self.tpl.u_suf, self.tpl.a_pre + resp + self.tpl.a_suf,
+                 self.tpl.u_pre + user2 + self.tpl.u_suf, self.tpl.gen + self.prefix]
+        whole = t("".join(parts)).input_ids
+        pieces: List[int] = []
+        for p in parts:
+            pieces += t(p).input_ids
+        if list(whole) != pieces:
+            raise NotImplementedError("the tokenizer does not split the chat template at its blocks")

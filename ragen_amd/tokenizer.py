@@ -321,9 +321,11 @@ class DeviceTokenizer:
                 + list(self.added_first))
 
     def encode_rows(self, text: torch.Tensor, text_len: torch.Tensor, out: torch.Tensor,
-                    out_len: Optional[torch.Tensor] = None, mark_byte: Optional[torch.Tensor] = None):
-        """Append the ids of every text row to ``out`` (rmi_bpe_encode).  -> (n_tok, mark_tok, err)."""
-        return torch.ops.ragen_amd.bpe_encode(*self.args(), text, text_len, out, out_len, mark_byte)
+                    out_len: Optional[torch.Tensor] = None, mark_byte: Optional[torch.Tensor] = None,
+                    max_len: int = 0):
+        """Append the ids of every text row to ``out`` (rmi_bpe_encode); max_len (0: the row
+        pitch) bounds the rows' length.  -> (n_tok, mark_tok, err)."""
+        return torch.ops.ragen_amd.bpe_encode(*self.args(), text, text_len, out, out_len, mark_byte, int(max_len))
 
     def encode(self, texts: Sequence[str], stride: int = None) -> List[Optional[List[int]]]:
         """Convenience (tests, tools): ids of each text, or None for a row the device flagged."""

@@ -658,9 +658,10 @@ def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, add
 @_op("bpe_encode", ("out", "out_len"))
 def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tensor, added_bytes: Tensor,
                added_off: Tensor, added_id: Tensor, params: List[int], text: Tensor, text_len: Tensor, out: Tensor,
-               out_len: Optional[Tensor], mark_byte: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor]:
+               out_len: Optional[Tensor], mark_byte: Optional[Tensor], max_len: int = 0) -> Tuple[Tensor, Tensor, Tensor]:
     """The tokenizer call of get_lm_inputs (ctx_manager.py:265-278) for a byte-level BPE:
-    every text row's ids appended to ``out`` (rmi_bpe_encode; tables: ragen_amd.tokenizer)
+    every text row's ids appended to ``out`` (rmi_bpe_encode; tables: ragen_amd.tokenizer).
+    max_len (0: the row pitch) bounds the rows' length and sizes the kernel's LDS.
     -> (n_tok i32[B], mark_tok i32[B], err u8[B])."""
     import ctypes
     tok = _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params)
@@ -677,8 +678,11 @@ def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tens
     n_tok = torch.empty(B, dtype=torch.int32, device=dev)
     mark_tok = torch.zeros(B, dtype=torch.int32, device=dev)
     err = torch.empty(B, dtype=torch.uint8, device=dev)
-    ops.check(ops.lib().rmi_bpe_encode(ctypes.addressof(tok), text.data_ptr(), int(text.shape[1]), text_len.data_ptr(),
-                                       B, out.data_ptr(), int(out.shape[1]), _ptr(out_len), n_tok.data_ptr(),
+    pitch = int(text.shape[1])
+    cap = (int(max_len) + 3) // 4 * 4 if max_len else pitch
+    ops.check(ops.lib().rmi_bpe_encode(ctypes.addressof(tok), text.data_ptr(), pitch, max(min(cap, pitch), 4),
+                                       text_len.data_ptr(), B, out.data_ptr(), int(out.shape[1]), _ptr(out_len),
+                                       n_tok.data_ptr(),
                                        _ptr(mark_byte), mark_tok.data_ptr() if mark_byte is not None else None,
                                        err.data_ptr(), ops._stream(dev)), "rmi_bpe_encode")
     return n_tok, mark_tok, err
@@ -686,7 +690,7 @@ def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tens
 
 @bpe_encode.register_fake
 def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, text, text_len, out, out_len,
-      mark_byte):
+      mark_byte, max_len=0):
     B = text.shape[0]
     return (text.new_empty(B, dtype=torch.int32), text.new_empty(B, dtype=torch.int32),
             text.new_empty(B, dtype=torch.uint8))

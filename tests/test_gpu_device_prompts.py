@@ -1,0 +1,139 @@
+"""The device prompt path (§8(f) ranks 1-2, llm_agent/prompts.py) against the reference's host
+path (ctx_manager.py:228-330: chat template + tokenizer over the whole history each turn) on
+the configs and actions of all five golden traces, with the character tokenizer FakeQwenTok
+and the Qwen2-pipeline byte-level BPE: every turn's generation batch (input_ids,
+attention_mask, position_ids) read by an actor, the formulated batch, its metrics, env ids,
+messages and the rollout cache must be identical.  A second test drives responses through
+every branch of the response rebuild (no match, the special-token cascade, more than K actions,
+whitespace and non-ASCII text, NFC-changing text and overlong rows built on the host)."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from fake_tok import FakeQwenTok
+from ragen_amd import ops, synthetic
+from ragen_amd.llm_agent import LLMAgentProxy, TokenActor
+from ragen_amd.protocol import DataProto
+from test_gpu_facade import TRACES, _config, _hashseed0_reseed
+from trace_util import load, strings
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def qwen_tok():
+    return synthetic.qwen_like_tokenizer()
+
+
+def _responses(name, t, B):
+    d = load(name)
+    S = strings()[name]
+    out = []
+    for i in range(B):
+        if name == "countdown_es":
+            a = S["answers"][t][i]
+            acts = [] if a is None else [a]
+        else:
+            acts = [S["vocab"][c] for c in d["codes"][t, i] if c >= 0]
+        out.append(f"thinking about turn {t}</think> <answer>{' || '.join(acts)}</answer>")
+    return out
+
+
+def _ids(tok, texts, device):
+    rows = [tok._ids(x) if isinstance(tok, FakeQwenTok) else tok(x).input_ids for x in texts]
+    R = max(len(x) for x in rows)
+    pad = tok.pad_token_id
+    a = np.full((len(rows), R), pad, np.int64)
+    for i, x in enumerate(rows):
+        a[i, :len(x)] = x
+    return torch.from_numpy(a).to(device)
+
+
+def _vocab(tok, device):
+    if isinstance(tok, FakeQwenTok):
+        return ops.VocabTable.from_bytes(*tok.byte_table(), device)
+    return ops.VocabTable.from_tokenizer(tok, device)
+
+
+def _rollout(cfg, tok, turn_tokens, device, device_path):
+    actor = TokenActor(turn_tokens, read_prompts=True)
+    proxy = LLMAgentProxy(cfg, actor, tok, device=device)
+    if device_path:
+        proxy.train_ctx_manager.set_device_vocab(_vocab(tok, device))
+    random.seed(7)
+    out = proxy.rollout(DataProto(meta_info={}), val=False)
+    prompts = [tuple(x.cpu() for x in p) for p in actor.prompts]
+    return out, proxy, prompts
+
+
+def _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy):
+    assert len(ref_prompts) == len(dev_prompts)
+    for t, (a, b) in enumerate(zip(ref_prompts, dev_prompts)):
+        for k, x, y in zip(("input_ids", "attention_mask", "position_ids"), a, b):
+            assert torch.equal(x, y), (t, k)
+    assert set(ref.batch.keys()) == set(dev.batch.keys())
+    for k in ref.batch.keys():
+        assert torch.equal(ref.batch[k].cpu(), dev.batch[k].cpu()), k
+    assert ref.meta_info == dev.meta_info
+    for k in ("env_ids", "group_ids", "messages_list"):
+        assert np.asarray(ref.non_tensor_batch[k]).tolist() == np.asarray(dev.non_tensor_batch[k]).tolist(), k
+    assert ref_proxy.train_es_manager.rollout_cache == dev_proxy.train_es_manager.rollout_cache
+
+
+@pytest.mark.parametrize("which", ["fake", "qwen"])
+@pytest.mark.parametrize("name", list(TRACES))
+def test_device_prompts_equal_host_prompts(device, name, which, qwen_tok, monkeypatch):
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok() if which == "fake" else qwen_tok
+    cfg = _config(name)
+    _, ng, gs, T, _ = TRACES[name]
+    B = ng * gs
+    turn_tokens = [_ids(tok, _responses(name, t, B), device) for t in range(T)]
+    ref, ref_proxy, ref_prompts = _rollout(cfg, tok, turn_tokens, device, False)
+    dev, dev_proxy, dev_prompts = _rollout(cfg, tok, turn_tokens, device, True)
+    pr = dev_proxy.train_ctx_manager.prompts()
+    assert pr is not None and pr.host_rows_used == 0
+    assert dev.batch["input_ids"].is_cuda  # the device path's batch stays on the GPU
+    _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)
+
+
+EDGE_RESPONSES = [
+    "no tags at all here",                                               # no match: the raw response
+    "a</think><answer>Up || Down</answer>",                              # plain
+    "  spaced thoughts \t</think>\n  <answer>  Left  ||  Right  </answer>",  # strips
+    "x</think><answer>Up || Down || Left || Right || Up || Down || Left</answer>",  # > K: re-joined
+    "t</think><answer>Up||||Down|| ||Left</answer>",                      # empty pieces
+    "<think>nested</think></think><answer>Up <|im_end|> || Down</answer>",  # special-token cascade
+    "a</think><answer><answer>Right</answer></answer>",                  # cascade in the answer
+    "café — naïve 中文 😀</think><answer>Up</answer>",                    # non-ASCII
+    "u v　</think><answer> Down </answer>",            # Unicode whitespace strips
+    "é combining</think><answer>Up</answer>",                       # NFC-changing: host row
+    "long " * 700 + "</think><answer>Up</answer>",                        # past the row buffer: host row
+    "a</think><answer></answer>",                                         # empty answer
+    "only answer <answer>Left</answer>",                                  # missing </think>
+]
+
+
+@pytest.mark.parametrize("think", [True, False])
+def test_device_prompts_response_branches(device, qwen_tok, think, monkeypatch):
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    cfg = _config("sokoban_es")
+    cfg.agent_proxy.enable_think = think
+    _, ng, gs, T, _ = TRACES["sokoban_es"]
+    B = ng * gs
+    rng = np.random.default_rng(3)
+    turn_tokens = []
+    for t in range(T):
+        texts = [EDGE_RESPONSES[int(rng.integers(len(EDGE_RESPONSES)))] for _ in range(B)]
+        if not think:
+            texts = [x.split("</think>")[-1].replace("<answer>", "", 1) if "<answer>" in x else x for x in texts]
+        turn_tokens.append(_ids(qwen_tok, texts, device))
+    ref, ref_proxy, ref_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, False)
+    with pytest.warns(RuntimeWarning, match="prompt rows built on the host"):
+        dev, dev_proxy, dev_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, True)
+    assert dev_proxy.train_ctx_manager.prompts().host_rows_used > 0
+    _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)    "u v\u3000</think><answer>\u2003Down\xa0</answer>",                   # Unicode whitespace strips    "e\u0301 combining</think><answer>Up</answer>",                     # NFC-changing: host row
