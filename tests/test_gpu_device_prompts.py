@@ -110,7 +110,7 @@ EDGE_RESPONSES = [
     "a</think><answer><answer>Right</answer></answer>",                  # cascade in the answer
     "café — naïve 中文 😀</think><answer>Up</answer>",                    # non-ASCII
     "u v　</think><answer> Down </answer>",            # Unicode whitespace strips
-    "é combining</think><answer>Up</answer>",                       # NFC-changing: host row
+    "e\u0301 combining</think><answer>Up</answer>",               # NFC-changing: host row
     "long " * 700 + "</think><answer>Up</answer>",                        # past the row buffer: host row
     "a</think><answer></answer>",                                         # empty answer
     "only answer <answer>Left</answer>",                                  # missing </think>
@@ -136,4 +136,4 @@ def test_device_prompts_response_branches(device, qwen_tok, think, monkeypatch):
     with pytest.warns(RuntimeWarning, match="prompt rows built on the host"):
         dev, dev_proxy, dev_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, True)
     assert dev_proxy.train_ctx_manager.prompts().host_rows_used > 0
-    _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)    "u v\u3000</think><answer>\u2003Down\xa0</answer>",                   # Unicode whitespace strips    "e\u0301 combining</think><answer>Up</answer>",                     # NFC-changing: host row
+    _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)
