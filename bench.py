@@ -534,12 +534,15 @@ def text_leg(R, device, reps=20):
 def api_leg(device):
     """SURVEY §8(d)'s "API" variant of the headline: the same SK workload (8192 envs, 5 turns, the
     bench's synthetic actions written as LLM responses) driven through the drop-in
-    LLMAgentProxy.rollout (agent_proxy.py:143-159), reset excluded:
-    * ``device`` path — the actor hands back response token ids on the GPU (TokenActor); the
-      ContextManager decodes them on the device, EnvStateManager parses, steps and renders on
-      the device and keeps the history dicts lazy; env-steps/s over the turn loop, with the
-      end-of-rollout costs (get_rollout_states materialising the dicts, formulate_rollouts
-      tokenising the transcripts) reported beside it;
+    LLMAgentProxy.rollout (agent_proxy.py:143-159), reset excluded, with a Qwen2-pipeline
+    byte-level BPE tokenizer (synthetic.qwen_like_tokenizer: the Qwen2.5 tokenizer is a hub
+    download) and an actor that reads the prompt batch every turn, as a vLLM worker group does
+    (input_ids / attention_mask / position_ids, agent_proxy.py:128-141):
+    * ``device`` path — responses arrive as token ids on the GPU; the ContextManager decodes
+      them on the device, EnvStateManager parses, steps and renders on the device, and the
+      prompt ids of the next turn are built and tokenized on the device (llm_agent/prompts.py);
+      ``env_steps_per_s`` = env steps / (turn loop + get_rollout_states + formulate_rollouts),
+      every phase of the rollout after the reset;
     * ``dict`` path — EnvStateManager.step fed the reference's list of dicts with action names
       (per-turn device round trip, host history dicts and text observations each turn)."""
     import random
@@ -550,38 +553,52 @@ def api_leg(device):
     cfg = env_task("SimpleSokoban", B // GROUP, GROUP, max_turn=T, max_actions_per_turn=K)
     ids, n = synthetic.rollout_actions(B, T, K, 1, 4)
     lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
-    table, skip = synthetic.byte_vocab()
-    tokens = [torch.from_numpy(synthetic.tokenize_greedy(synthetic.responses_for_actions(ids[t], n[t], lk,
-                                                                                        seed=100 + t), table)).to(device)
-              for t in range(T)]
-    tok = synthetic.ByteChatTokenizer()
-    actor = TokenActor(tokens)
+    tok = synthetic.qwen_like_tokenizer()
+    tokens = []
+    for t in range(T):
+        enc = tok(synthetic.responses_for_actions(ids[t], n[t], lk, seed=100 + t), padding=False).input_ids
+        R = max(len(x) for x in enc)
+        a = np.full((B, R), tok.pad_token_id, np.int64)
+        for i, x in enumerate(enc):
+            a[i, :len(x)] = x
+        tokens.append(torch.from_numpy(a).to(device))
+    actor = TokenActor(tokens, read_prompts=True)
     proxy = LLMAgentProxy(cfg, actor, tok, device=device)
-    proxy.train_ctx_manager.set_device_vocab(ops.VocabTable.from_bytes(table, skip, device))
+    proxy.train_ctx_manager.set_device_vocab(ops.VocabTable.from_tokenizer(tok, device))
     runs = []
-    for rep in range(3):
+    for rep in range(4):
         random.seed(rep)
         actor.turn = 0
+        actor.prompts, actor.prompt_shapes = [], []
         torch.cuda.synchronize()
         out = proxy.rollout(DataProto(meta_info={}), val=False)
+        torch.cuda.synchronize()
         steps = int(proxy.train_es_manager.tags[0].batch.ep.turn_exec.sum().item())
-        runs.append((steps, dict(proxy.last_timing), len(out)))
-    steps, tm, rows = runs[-1]
-    device_path = {"env_steps": steps, "turn_loop_s": tm["turns_s"], "env_steps_per_s": steps / tm["turns_s"],
-                   "get_rollout_states_s": tm["rollout_states_s"], "formulate_rollouts_s": tm["formulate_s"],
-                   "rows_formulated": rows,
-                   "note": "LLMAgentProxy.rollout, generations as device token ids, lazy history; last of 3 rollouts"}
+        runs.append((steps, dict(proxy.last_timing), len(out), list(actor.prompt_shapes),
+                     tuple(out.batch["input_ids"].shape)))
+    pr = proxy.train_ctx_manager.prompts()
+    steps, tm, rows, shapes, upd = runs[-1]
+    total = tm["turns_s"] + tm["rollout_states_s"] + tm["formulate_s"]
+    device_path = {"env_steps": steps, "turn_loop_s": tm["turns_s"], "get_rollout_states_s": tm["rollout_states_s"],
+                   "formulate_rollouts_s": tm["formulate_s"], "rollout_s": total, "env_steps_per_s": steps / total,
+                   "turn_loop_env_steps_per_s": steps / tm["turns_s"], "rows_formulated": rows,
+                   "prompt_batch_shapes": shapes, "update_batch_shape": upd, "device_prompts": pr is not None,
+                   "host_prompt_rows": pr.host_rows_used if pr is not None else None,
+                   "tokenizer": f"{tok.name_or_path}, vocab {len(tok)}",
+                   "note": "LLMAgentProxy.rollout, response token ids on the GPU, an actor reading input_ids / "
+                           "attention_mask / position_ids every turn, device prompt ids; last of 4 rollouts"}
     # the dict facade: EnvStateManager.step with the reference's list-of-dict inputs
     es = EnvStateManager(cfg, mode="train", device=device)
     es.reset(seed=synthetic.ENV_SEED)
     names = {1: "Up", 2: "Down", 3: "Left", 4: "Right", 0: "Jump"}  # 0 = a name outside the action lookup
+    turn_inputs = [[[names[int(a)] for a in ids[t, i, :int(n[t, i])]] for i in range(B)] for t in range(T)]
     active = list(range(B))
     dsteps = 0
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for t in range(T):
-        inputs = [{"env_id": i, "llm_response": "", "llm_raw_response": "",
-                   "actions": [names[int(a)] for a in ids[t, i, :int(n[t, i])]]} for i in active]
+        inputs = [{"env_id": i, "llm_response": "", "llm_raw_response": "", "actions": turn_inputs[t][i]}
+                  for i in active]
         outs = es.step(inputs)
         active = [o["env_id"] for o in outs]
         dsteps += int(es.tags[0].batch.ep.turn_exec[t].sum().item())
@@ -590,7 +607,8 @@ def api_leg(device):
     dt = time.perf_counter() - t0
     return {"env_steps_per_s": device_path["env_steps_per_s"], "device_path": device_path,
             "dict_path": {"env_steps": dsteps, "seconds": dt, "env_steps_per_s": dsteps / dt,
-                          "note": "EnvStateManager.step facade, host dicts + text obs each turn"}}
+                          "note": "EnvStateManager.step facade, host dicts + text obs each turn (the action-name "
+                                  "lists are built before the timed loop)"}}
 
 
 def cpu_baseline_parallel(R, workers=16, reps=20):

@@ -420,7 +420,7 @@ typedef struct {
  * prefixed text (all -1: no match); action_text [B,K,Lact] / action_len [B,K] = the stripped
  * action strings (Countdown's answers).  err[b] |= RMI_ERR_UNSUP when an action is longer
  * than Lact, RMI_ERR_STATE when text_len[b] is outside [0, stride].
- * stride % 4 == 0, stride <= 12288.                                                        */
+ * stride % 4 == 0, stride <= 8192.                                                         */
 int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, const int32_t* text_len, int64_t B,
                       int32_t stride, const uint8_t* sel, int8_t* actions, uint8_t* n_actions, int32_t* spans,
                       uint8_t* action_text, int32_t* action_len, int32_t Lact, uint8_t* err, rmi_stream_t stream);

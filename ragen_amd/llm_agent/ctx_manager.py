@@ -96,6 +96,7 @@ def _raise_assemble_errors(err, S):
 
 
 SPECIAL_TOKENS = ["<think>", "</think>", "<answer>", "</answer>", "<|im_start|>", "<|im_end|>"]
+PARSE_MAX_ROW = 8192  # rmi_parse_actions' row limit (bytes of a decoded generation)
 
 
 def parse_response(response: str, enable_think: bool, action_sep: str, max_actions_per_turn: int):
@@ -549,8 +550,13 @@ class ContextManager:
         n_ids = torch.zeros(self.n_envs, dtype=torch.int32, device=dev)
         ids[idx - self.env_lo] = resp.to(torch.int64)
         n_ids[idx - self.env_lo] = R
-        per_tok = vocab.max_token_bytes or 16
-        stride = min(12288, (R * per_tok + 3) // 4 * 4)
+        # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
+        # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
+        # the decode and refused by the step (ValueError)
+        n_bytes = (vocab.off[1:] - vocab.off[:-1]).to(torch.int32)
+        raw = torch.where(vocab.skip.bool(), torch.zeros_like(n_bytes), n_bytes)[resp.clamp(0, n_bytes.numel() - 1)]
+        raw_max = int(raw.sum(1).max()) if resp.numel() else 0
+        stride = max(4, min(PARSE_MAX_ROW, (3 * raw_max + 7) // 4 * 4))
         text, tlen, err = torch.ops.ragen_amd.detokenize(ids, n_ids, vocab.off, vocab.data, vocab.skip, stride)
         return DeviceEnvInputs(self, env_ids, idx, text, tlen, err)
 
@@ -582,9 +588,14 @@ class ContextManager:
         tab = (eps[0].turn_reward if len(eps) == 1 else torch.cat([ep.turn_reward for ep in eps], 1)).contiguous()
         n_sc = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
         special_token, reward_token = get_special_tokens(self.tokenizer)
+        # zip_longest's length over the WHOLE batch (ctx_manager.py:52-62): every rank's longest
+        from .. import distributed as rd
+        n_slots = int(n_sc.max()) if n_sc.numel() else 0
+        if self.process_group is not None and self.world_size > 1:
+            n_slots = rd.all_reduce_max_int(n_slots, self.process_group, dev)
         ids, am, pos, score_tensor, loss_mask, response_mask, err = torch.ops.ragen_amd.assemble_rows(
             tokens, start, row_len, max(S, 1), int(pr.pad_id), int(special_token), int(reward_token), tab, n_sc,
-            tab.shape[0], bool(ap.use_turn_scores), bool(self.config.enable_response_mask),
+            n_slots, bool(ap.use_turn_scores), bool(self.config.enable_response_mask),
             "qwen" in self.tokenizer.name_or_path.lower())
         _raise_assemble_errors(err, S)
         normalized = score_tensor

@@ -123,6 +123,8 @@ class DevicePrompts:
         prefixes = [ctx.prefix_lookup[tg.lo] for tg in tags]
         lengths = [f"Max response length: {ctx.env_config_lookup[tg.lo]['max_tokens']} words (tokens)." for tg in tags]
         self._pool = bytearray()
+        self._const_at = {}
+        self._pool_dev = None
         self._tag_tables = []
         self._tag_table(prefixes)  # table 0: instruction prefix
         self._tag_table(lengths)   # table 1: length line
@@ -135,7 +137,7 @@ class DevicePrompts:
         self.len = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.len_upd = torch.zeros(n, dtype=torch.int32, device=self.device)
         tail = self.dt.encode([self.tpl.gen + self.prefix])[0]
-        if tail is None or tail != list(tokenizer(self.tpl.gen + self.prefix).input_ids):
+        if tail is None or tail != self._host_ids(self.tpl.gen + self.prefix):
             raise NotImplementedError("the generation prompt does not encode like the host tokenizer")
         self.tail = torch.tensor(tail, dtype=torch.int64, device=self.device)
         self.host_rows_used = 0
@@ -143,12 +145,17 @@ class DevicePrompts:
         self.turns_done = 0
         self._verify()
 
+    def _host_ids(self, text: str) -> List[int]:
+        """The host tokenizer's ids of one text (the reference's call, ctx_manager.py:265-278)."""
+        return [int(x) for x in self.tok([text], padding=False, truncation=False).input_ids[0]]
+
     # ---------------------------------------------------------------- constant pool
     def _const(self, s: str):
-        b = s.encode("utf-8")
-        off = len(self._pool)
-        self._pool += b
-        return off, len(b)
+        if s not in self._const_at:
+            b = s.encode("utf-8")
+            self._const_at[s] = (len(self._pool), len(b))
+            self._pool += b
+        return self._const_at[s]
 
     def _tag_table(self, strings):
         tab = []
@@ -165,9 +172,11 @@ class DevicePrompts:
                 prog.append((_lib.PT_CONST, off, ln))
             else:
                 prog.append(p)
-        pool = torch.frombuffer(bytearray(self._pool) + b"\0" * 4, dtype=torch.uint8).to(self.device)
-        tc = torch.tensor([x for t in self._tag_tables for x in t], dtype=torch.int32, device=self.device)
-        return prog, pool, tc
+        if self._pool_dev is None or self._pool_dev[0] != len(self._pool):  # upload when it grew
+            pool = torch.frombuffer(bytearray(self._pool) + b"\0" * 4, dtype=torch.uint8).to(self.device)
+            tc = torch.tensor([x for t in self._tag_tables for x in t], dtype=torch.int32, device=self.device)
+            self._pool_dev = (len(self._pool), pool, tc)
+        return prog, self._pool_dev[1], self._pool_dev[2]
 
     def _run_text(self, pieces, stride, obs, obs_len, ints, reward=None, reward_int=None, resp=None, resp_len=None,
                   spans=None, cond=None, active=None):
@@ -182,7 +191,7 @@ class DevicePrompts:
         """Every env's observation text as one [n_envs, stride] buffer: the device render of the
         tags that have one (``rows_by_tag[j]``), else the env's text at reset."""
         parts, lens = [], []
-        st = max([r.shape[1] for r in rows_by_tag.values()] + [self._reset_obs[0].shape[1]])
+        st = max([r[0].shape[1] for r in rows_by_tag.values()] + [self._reset_obs[0].shape[1]])
         for j, tg in enumerate(self.es.tags):
             if j in rows_by_tag:
                 r, ln = rows_by_tag[j]
@@ -288,19 +297,19 @@ class DevicePrompts:
         text = (self.tpl.head + self.ctx.prefix_lookup[g] + f"\nTurn 1:\nState:\n{h['state']}\nYou have "
                 f"{h['actions_left']}" + self._c_mid + length + "\n" + self.tpl.u_suf)
         del ap
-        self._write_host(e, self.tok(text).input_ids)
+        self._write_host(e, self._host_ids(text))
 
     def _host_turn(self, e, t, cont):
         self.es._materialize()
         g = self.es.env_lo + e
         hist = self.es.rollout_cache[e]["history"]
         h, nxt = hist[t], hist[t + 1]
-        a = self.tok(self.tpl.a_pre + h["llm_response"] + self.tpl.a_suf).input_ids
+        a = self._host_ids(self.tpl.a_pre + h["llm_response"] + self.tpl.a_suf)
         b = []
         if cont:
             length = f"Max response length: {self.ctx.env_config_lookup[g]['max_tokens']} words (tokens)."
-            b = self.tok(self.tpl.u_pre + f"Reward:\n{h['reward']}\n\nTurn {t + 2}:\nState:\n{nxt['state']}\n"
-                         f"You have {nxt['actions_left']}" + self._c_mid + length + "\n" + self.tpl.u_suf).input_ids
+            b = self._host_ids(self.tpl.u_pre + f"Reward:\n{h['reward']}\n\nTurn {t + 2}:\nState:\n{nxt['state']}\n"
+                               f"You have {nxt['actions_left']}" + self._c_mid + length + "\n" + self.tpl.u_suf)
         self._write_host(e, a, b)
 
     # ------------------------------------------------------------------- batches
@@ -319,16 +328,15 @@ class DevicePrompts:
     # ------------------------------------------------------------------ self-check
     def _verify(self):
         """The concatenation rule on a probe conversation, against the host tokenizer."""
-        t = self.tok
         fmt = self._c_mid
         first = "instr\nTurn 1:\nState:\n#_P#\nYou have 9" + fmt + "x.\n"
         resp = "<think>a b</think><answer>Up || Down</answer>"
         user2 = "Reward:\n-0.1\n\nTurn 2:\nState:\n#P_#\nYou have 7" + fmt + "x.\n"
         parts = [self.tpl.head + first + self.tpl.u_suf, self.tpl.a_pre + resp + self.tpl.a_suf,
                  self.tpl.u_pre + user2 + self.tpl.u_suf, self.tpl.gen + self.prefix]
-        whole = t("".join(parts)).input_ids
+        whole = self._host_ids("".join(parts))
         pieces: List[int] = []
         for p in parts:
-            pieces += t(p).input_ids
-        if list(whole) != pieces:
+            pieces += self._host_ids(p)
+        if whole != pieces:
             raise NotImplementedError("the tokenizer does not split the chat template at its blocks")

@@ -129,8 +129,9 @@ def test_device_prompts_response_branches(device, qwen_tok, think, monkeypatch):
     turn_tokens = []
     for t in range(T):
         texts = [EDGE_RESPONSES[int(rng.integers(len(EDGE_RESPONSES)))] for _ in range(B)]
-        if not think:
-            texts = [x.split("</think>")[-1].replace("<answer>", "", 1) if "<answer>" in x else x for x in texts]
+        if not think:  # the generation continues after "<answer>": the thoughts become answer text
+            texts = [(x.split("</think>")[0] + " " + x.split("</think>")[1].replace("<answer>", "", 1))
+                     if "</think>" in x else x for x in texts]
         turn_tokens.append(_ids(qwen_tok, texts, device))
     ref, ref_proxy, ref_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, False)
     with pytest.warns(RuntimeWarning, match="prompt rows built on the host"):

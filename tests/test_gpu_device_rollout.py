@@ -62,7 +62,7 @@ def test_device_rollout_equals_dict_rollout(device, name, monkeypatch):
     dev, dev_cache = _rollout(name, device, vocab)
     assert set(ref.batch.keys()) == set(dev.batch.keys())
     for k in ref.batch.keys():
-        assert torch.equal(ref.batch[k], dev.batch[k]), k
+        assert torch.equal(ref.batch[k].cpu(), dev.batch[k].cpu()), k
     assert ref.meta_info == dev.meta_info
     assert list(ref.non_tensor_batch["env_ids"]) == list(dev.non_tensor_batch["env_ids"])
     assert np.asarray(ref.non_tensor_batch["messages_list"]).tolist() == \
