@@ -601,7 +601,11 @@ class ContextManager:
         normalized = score_tensor
         if not ap.use_turn_scores:
             normalized = self._normalize_device(score_tensor, es)
-        response_length = response_mask.sum(dim=-1).float().mean().item()
+        # the mean over the WHOLE batch (ctx_manager.py:305): every rank's row lengths, rank order
+        row_resp = response_mask.sum(dim=-1).float()
+        if self.process_group is not None and self.world_size > 1:
+            row_resp = rd.all_gather_rows(row_resp, group=self.process_group)
+        response_length = row_resp.mean().item()
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
                  "loss_mask": loss_mask, "rm_scores": normalized, "original_rm_scores": normalized}
         env_ids = es.env_lo + np.arange(es.n_envs, dtype=np.int64)
