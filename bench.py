@@ -490,13 +490,33 @@ def text_leg(R, device, reps=20):
     for t in range(T_TURNS):  # the decode reproduces the response texts byte for byte
         assert torch.equal(dec[t][1], bufs[t][1])
     obs = ops.sokoban_render(R.st, B, R.env.config.grid_lookup, device)
+    # the fused decode + parse (rmi_detok_parse) of each turn, writing the parse outputs the
+    # turn structs point at
+    fused = []
+    for t in range(T_TURNS):
+        o, _ = text_turns[t]
+        fo = ops.detok_parse(tok[t], tvocab, stride, cfg, with_spans=False)
+        fused.append(dict(fo, actions=o["actions"], n_actions=o["n_actions"]))
+    torch.cuda.synchronize()
+    for t in range(T_TURNS):
+        ops.detok_parse(tok[t], tvocab, stride, cfg, out=fused[t])
+    torch.cuda.synchronize()
+    for t in range(T_TURNS):  # the same text and actions as the two separate launches
+        assert torch.equal(fused[t]["text_len"], bufs[t][1])
+        assert torch.equal(fused[t]["actions"], R.ids[t]) and torch.equal(fused[t]["n_actions"], R.n[t])
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(reps):
+        ops.detok_parse(tok[0], tvocab, stride, cfg, out=fused[0])
+    e[1].record()
+    torch.cuda.synchronize()
+    fused_us = e[0].elapsed_time(e[1]) * 1e3 / reps
 
     def token_step():
         e = R.env
         for t in range(T_TURNS):
             o, ts = text_turns[t]
-            txt, tl, _ = ops.detokenize(tok[t], tvocab, stride, out=dec[t])
-            ops.parse_actions(cfg, txt, tl, with_spans=False, out=o)
+            ops.detok_parse(tok[t], tvocab, stride, cfg, out=fused[t])
             if t == 0:
                 ops.sokoban_step_turn_first(R.st, e.ep, ts, e.init_state, e.init_player)
             elif t < T_TURNS - 1:
@@ -525,7 +545,10 @@ def text_leg(R, device, reps=20):
             "text_rollout": {"config": "SK rollout from response text: 5 x (parse + turn), restore and finalize fused",
                              "env_steps_per_rollout": steps, "ms_per_rollout": ms,
                              "env_steps_per_s": steps / ms * 1e3},
-            "token_rollout": {"config": "SK rollout from response token ids: 5 x (detokenize + parse + turn + render)",
+            "detok_parse": {"kernel": "rmi_detok_parse", "rows": B, "ids_per_row": int(tok[0].shape[1]),
+                            "vocab": "byte-level (synthetic.byte_vocab)", "us": fused_us,
+                            "note": "the decode fused with the parse: one launch per turn on the token path"},
+            "token_rollout": {"config": "SK rollout from response token ids: 5 x (detok_parse + turn + render)",
                               "env_steps_per_rollout": steps, "ms_per_rollout": ms_tok,
                               "env_steps_per_s": steps / ms_tok * 1e3},
             "render": {"kernel": "rmi_sokoban_render", "envs": B, "us": render_us}}

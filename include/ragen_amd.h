@@ -384,16 +384,25 @@ int rmi_mask_mul(float* x, const uint8_t* mask, int64_t n, rmi_stream_t stream);
  *           EnvStateManager._extract_map_valid_actions (es_manager.py:230-240).
  *
  * rmi_detokenize: byte-level BPE decoding (the tokenizers ByteLevel decoder).  Token id t
- * contributes vocab_bytes[vocab_off[t] .. vocab_off[t+1]) unless skip[t] (special tokens);
- * the concatenation is UTF-8 decoded with U+FFFD replacing each maximal invalid subpart
- * (String::from_utf8_lossy) and written back as UTF-8: out[b, 0 .. out_len[b]) is exactly
- * decoded_str.encode("utf-8").  ids [B,R] (n_ids[b] <= R ids used per row, NULL = R).
- * err[b]: RMI_ERR_INDEX for an id outside [0, V), RMI_ERR_UNSUP when the text exceeds
- * `stride` bytes (truncated).  vocab_bytes holds n_bytes bytes (4-byte aligned); stride % 4
- * == 0, stride <= 16384.                                                                    */
-int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const int64_t* vocab_off,
-                   const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, const uint8_t* skip, uint8_t* out,
-                   int32_t stride, int32_t* out_len, uint8_t* err, rmi_stream_t stream);
+ * contributes its bytes unless it is skipped (special tokens); the concatenation is UTF-8
+ * decoded with U+FFFD replacing each maximal invalid subpart (String::from_utf8_lossy) and
+ * written back as UTF-8: out[b, 0 .. out_len[b]) is exactly decoded_str.encode("utf-8").
+ * ids [B,R] (n_ids[b] <= R ids used per row, NULL = R).  The vocabulary is the packed table
+ * of rmi_vocab_pack (16-B aligned): one 16-byte gather per id.  err[b]: RMI_ERR_INDEX for an
+ * id outside [0, V), RMI_ERR_UNSUP when the text exceeds `stride` bytes (truncated).
+ * stride % 4 == 0, stride <= 16384.                                                         */
+int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const uint32_t* vocab_packed,
+                   const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, uint8_t* out, int32_t stride,
+                   int32_t* out_len, uint8_t* err, rmi_stream_t stream);
+
+/* HOST function (CPU memory): the packed vocabulary of rmi_detokenize from the byte table
+ * vocab_bytes[vocab_off[t] .. vocab_off[t+1]) and skip[t] (NULL = none skipped).
+ * packed u32[V,4]: entry t = (w0, w1, w2, meta); meta bits 0-23 = the token's byte length,
+ * bit 31 = skip; a token of <= 12 bytes holds them in w0..w2 (byte k in bits 8(k%4) of
+ * w[k/4]), a longer one its offset into vocab_bytes in w0.  RMI_EUNSUP for a token longer
+ * than 2^24 - 1 bytes or a blob past 4 GiB.                                                 */
+int rmi_vocab_pack(const int64_t* vocab_off, const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V,
+                   const uint8_t* skip, uint32_t* packed);
 
 /* Parse configuration (agent_proxy.* and the env's action_lookup).  Strings are packed
  * little-endian into two u64 words (byte k of the string = byte k of lo|hi).             */
@@ -424,6 +433,19 @@ typedef struct {
 int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, const int32_t* text_len, int64_t B,
                       int32_t stride, const uint8_t* sel, int8_t* actions, uint8_t* n_actions, int32_t* spans,
                       uint8_t* action_text, int32_t* action_len, int32_t Lact, uint8_t* err, rmi_stream_t stream);
+
+/* rmi_detok_parse: rmi_detokenize then rmi_parse_actions on the decoded rows, fused in one
+ * launch (the per-turn boundary of a device-resident generation: ContextManager.get_env_inputs
+ * ctx_manager.py:332-352 = batch_decode + the "<think>"/"<answer>" prefix + _parse_response,
+ * then es_manager.py:230-240's name map).  The decoded rows are written to text / text_len
+ * exactly as rmi_detokenize writes them (decode_err: its error bits) and parsed exactly as
+ * rmi_parse_actions parses text (parse_err: its error bits); stride <= 8192.                */
+int rmi_detok_parse(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const uint32_t* vocab_packed,
+                    const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, uint8_t* text, int32_t stride,
+                    int32_t* text_len, uint8_t* decode_err, const rmi_parse_cfg_t* cfg, const uint8_t* sel,
+                    int8_t* actions, uint8_t* n_actions, int32_t* spans, uint8_t* action_text, int32_t* action_len,
+                    int32_t Lact, uint8_t* parse_err, rmi_stream_t stream);
+
 
 /* ---------------------------------------------- prompt token ids (§8(f) ranks 1-2)
  * Replaces: the tokenizer call of ContextManager.get_lm_inputs (ctx_manager.py:265-278,

@@ -147,7 +147,11 @@ _SIGS = {
                                    c_void_p]),
     "rmi_mask_mul": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p]),
     "rmi_detokenize": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
-                                 c_void_p, c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+                                 c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
+    "rmi_vocab_pack": (c_int32, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
+    "rmi_detok_parse": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                  c_void_p, c_int32, c_void_p, c_void_p, _P(ParseCfg), c_void_p, c_void_p, c_void_p,
+                                  c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_parse_actions": (c_int32, [_P(ParseCfg), c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),

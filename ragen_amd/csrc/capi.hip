@@ -51,3 +51,27 @@ RMI_API int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream
                        static_cast<uint8_t*>(dst) + done, static_cast<const uint8_t*>(src) + done, rest);
   return launch_status();
 }
+
+// Host-side: the packed vocabulary of rmi_detokenize from the plain byte table (run once per
+// tokenizer; CPU memory in and out).
+RMI_API int rmi_vocab_pack(const int64_t* vocab_off, const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V,
+                           const uint8_t* skip, uint32_t* packed) {
+  if (V < 1 || n_bytes < 0 || !vocab_off || !packed || (n_bytes > 0 && !vocab_bytes)) return RMI_EINVAL;
+  for (int64_t t = 0; t < V; ++t) {
+    const int64_t o = vocab_off[t], len = vocab_off[t + 1] - o;
+    if (o < 0 || len < 0 || o + len > n_bytes) return RMI_EINVAL;
+    if (len > 0xFFFFFF || o > 0xFFFFFFFFll) return RMI_EUNSUP;
+    uint32_t w[3] = {0u, 0u, 0u};
+    if (len <= 12) {
+      for (int64_t k = 0; k < len; ++k) w[k >> 2] |= (uint32_t)vocab_bytes[o + k] << (8 * (k & 3));
+    } else {
+      w[0] = (uint32_t)o;
+    }
+    uint32_t* e = packed + 4 * t;
+    e[0] = w[0];
+    e[1] = w[1];
+    e[2] = w[2];
+    e[3] = (uint32_t)len | ((skip && skip[t]) ? 0x80000000u : 0u);
+  }
+  return RMI_OK;
+}

@@ -33,12 +33,31 @@ namespace {
 // per-wave s_memtime at phase boundaries, kept in SGPRs and written once at the end.
 #ifdef RMI_PARSE_STAMPS
 __device__ unsigned long long* g_parse_stamps;
-#define PSTAMP_DECL unsigned long long pst_[10] = {0}
+__device__ unsigned long long* g_detok_stamps;
+#define PSTAMP_DECL unsigned long long pst_[10] = {0}, prt0_ = __builtin_amdgcn_s_memrealtime()
 #define PSTAMP(i) (pst_[i] = __builtin_amdgcn_s_memtime())
 #define PSTAMP_FLUSH()                                                                 \
   do {                                                                                 \
-    if ((threadIdx.x & 63) == 0)                                                       \
-      for (int s_ = 0; s_ < 10; ++s_) g_parse_stamps[b * 10 + s_] = pst_[s_];          \
+    const unsigned long long rt_ = __builtin_amdgcn_s_memrealtime();                   \
+    if ((threadIdx.x & 63) == 0) {                                                     \
+      for (int s_ = 0; s_ < 10; ++s_) g_parse_stamps[b * 12 + s_] = pst_[s_];          \
+      g_parse_stamps[b * 12 + 10] = prt0_;                                             \
+      g_parse_stamps[b * 12 + 11] = rt_;                                               \
+    }                                                                                  \
+  } while (0)
+// detok: 0 entry | 1 ids landed | 2 offsets landed | 3 bytes placed | 4 validity | 5 stored;
+// 6 / 7 s_memrealtime at entry / end
+#define DSTAMP_DECL unsigned long long dst_[6] = {0}, drt0_ = __builtin_amdgcn_s_memrealtime()
+#define DSTAMP(i) (dst_[i] = __builtin_amdgcn_s_memtime())
+#define DSTAMP_WAIT(i) (__builtin_amdgcn_s_waitcnt(0), dst_[i] = __builtin_amdgcn_s_memtime())
+#define DSTAMP_FLUSH()                                                                 \
+  do {                                                                                 \
+    const unsigned long long rt_ = __builtin_amdgcn_s_memrealtime();                   \
+    if ((threadIdx.x & 63) == 0) {                                                     \
+      for (int s_ = 0; s_ < 6; ++s_) g_detok_stamps[b * 8 + s_] = dst_[s_];            \
+      g_detok_stamps[b * 8 + 6] = drt0_;                                               \
+      g_detok_stamps[b * 8 + 7] = rt_;                                                 \
+    }                                                                                  \
   } while (0)
 #else
 #define PSTAMP_DECL \
@@ -48,6 +67,18 @@ __device__ unsigned long long* g_parse_stamps;
   do {            \
   } while (0)
 #define PSTAMP_FLUSH() \
+  do {                 \
+  } while (0)
+#define DSTAMP_DECL \
+  do {              \
+  } while (0)
+#define DSTAMP(i) \
+  do {            \
+  } while (0)
+#define DSTAMP_WAIT(i) \
+  do {                 \
+  } while (0)
+#define DSTAMP_FLUSH() \
   do {                 \
   } while (0)
 #endif
@@ -301,40 +332,10 @@ __host__ __device__ constexpr size_t parse_lds(int stride) {  // per wave, a mul
   return (2 * (size_t)row_bytes(stride) + 5 * (size_t)list_cap(stride) + 7) & ~(size_t)7;
 }
 
-__global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(8))) void parse_kernel(ParseArgs a) {
-  extern __shared__ uint64_t lds_q[];
-  const int wv = threadIdx.x >> 6;
-  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_q) + wv * parse_lds(a.stride);
-  const int cap = list_cap(a.stride);
-  uint8_t* T = lds + 4;                                                   // the prefixed row
-  uint8_t* Wb = lds + row_bytes(a.stride) + 4;                            // replace-cascade row
-  uint16_t* EL = reinterpret_cast<uint16_t*>(lds + 2 * row_bytes(a.stride));  // '<' positions
-  uint16_t* ES = EL + cap;                                                // separator candidates
-  uint8_t* EI = reinterpret_cast<uint8_t*>(ES + cap);                     // event ids
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-  if (b >= a.B) return;  // the whole wave: no cross-wave barrier follows
-  const rmi_parse_cfg_t& cfg = a.cfg;
-  const int K = cfg.K;
-  PSTAMP_DECL;
-  PSTAMP(0);
-  // ---- 0. stage.  The first 256 bytes are loaded together with the length (one round trip
-  //         for typical responses); the rest, if any, after it.
-  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(a.text + b * a.stride);
-  uint32_t* d4 = reinterpret_cast<uint32_t*>(T + kPre);
-  const int rw = a.stride >> 2;
-  const uint32_t first = lane < rw ? s4[lane] : 0u;
-  int len = a.text_len[b];
-  uint8_t err = 0;
-  if (len < 0 || len > a.stride) {
-    err |= RMI_ERR_STATE;
-    len = 0;
-  }
-  // the name table (kernel arguments) and the lookup column: loaded up front, their latency
-  // hides under the row's
+// The lookup names of one row's id column (kernel arguments, so no memory round trip of its own)
+__device__ __forceinline__ Names load_names(const rmi_parse_cfg_t& cfg, int col) {
   Names nm;
   nm.n = cfg.n_names;
-  const int col = (a.sel && a.sel[b]) ? 1 : 0;
 #pragma unroll
   for (int j = 0; j < RMI_PARSE_MAX_NAMES; ++j) {
     nm.lo[j] = cfg.name_lo[j];
@@ -342,9 +343,26 @@ __global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(
     nm.len[j] = cfg.name_len[j];
     nm.id[j] = cfg.name_id[col][j];
   }
-  const int nw = (len + 3) >> 2;
-  if (lane < nw) d4[lane] = first;
-  for (int i = 64 + lane; i < nw; i += 64) d4[i] = s4[i];
+  return nm;
+}
+
+#ifdef RMI_PARSE_STAMPS
+#define PSTAMP_PARAM , unsigned long long* pst_
+#define PSTAMP_ARG , pst_
+#else
+#define PSTAMP_PARAM
+#define PSTAMP_ARG
+#endif
+
+// One response, staged: its len bytes at T + kPre of the wave's LDS (T, Wb, EL, ES, EI: the
+// regions of parse_lds).  Adds the implicit "<think>" / "<answer>" prefix and the zero tail,
+// then the regex, the special-token cascade, the split and the name lookup, and writes row b's
+// outputs.  err: bits already set for this row (ORed into a.err[b]).
+__device__ __forceinline__ void parse_row(const ParseArgs& a, uint8_t* T, uint8_t* Wb, uint16_t* EL, uint16_t* ES,
+                                          uint8_t* EI, int64_t b, int len, uint8_t err, const Names& nm,
+                                          int lane PSTAMP_PARAM) {
+  const rmi_parse_cfg_t& cfg = a.cfg;
+  const int K = cfg.K;
   const Tag pre = cfg.enable_think ? kThinkOpen : kAnsOpen;
   const int plen = cfg.prepend ? pre.n : 0;
   const int base = kPre - plen, n_end = kPre + len;  // the prefixed response is T[base, n_end)
@@ -515,6 +533,40 @@ __global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(
     if (err_all && a.err) a.err[b] |= err_all;
   }
   PSTAMP(6);
+}
+
+__global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(8))) void parse_kernel(ParseArgs a) {
+  extern __shared__ uint64_t lds_q[];
+  const int wv = threadIdx.x >> 6;
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_q) + wv * parse_lds(a.stride);
+  const int cap = list_cap(a.stride);
+  uint8_t* T = lds + 4;                                                   // the prefixed row
+  uint8_t* Wb = lds + row_bytes(a.stride) + 4;                            // replace-cascade row
+  uint16_t* EL = reinterpret_cast<uint16_t*>(lds + 2 * row_bytes(a.stride));  // '<' positions
+  uint16_t* ES = EL + cap;                                                // separator candidates
+  uint8_t* EI = reinterpret_cast<uint8_t*>(ES + cap);                     // event ids
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (b >= a.B) return;  // the whole wave: no cross-wave barrier follows
+  PSTAMP_DECL;
+  PSTAMP(0);
+  // ---- 0. stage.  The first 256 bytes are loaded together with the length (one round trip
+  //         for typical responses); the rest, if any, after it.
+  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(a.text + b * a.stride);
+  uint32_t* d4 = reinterpret_cast<uint32_t*>(T + kPre);
+  const int rw = a.stride >> 2;
+  const uint32_t first = lane < rw ? s4[lane] : 0u;
+  int len = a.text_len[b];
+  uint8_t err = 0;
+  if (len < 0 || len > a.stride) {
+    err |= RMI_ERR_STATE;
+    len = 0;
+  }
+  const Names nm = load_names(a.cfg, (a.sel && a.sel[b]) ? 1 : 0);
+  const int nw = (len + 3) >> 2;
+  if (lane < nw) d4[lane] = first;
+  for (int i = 64 + lane; i < nw; i += 64) d4[i] = s4[i];
+  parse_row(a, T, Wb, EL, ES, EI, b, len, err, nm, lane PSTAMP_ARG);
   PSTAMP_FLUSH();
 }
 
@@ -587,28 +639,38 @@ __device__ __forceinline__ uint32_t byte_mask_n(int n) {
   return n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << (8 * n)) - 1u);
 }
 __host__ __device__ constexpr size_t detok_lds(int stride) { return 2 * ((size_t)stride + 4) + 16; }  // per wave
-__global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __restrict__ ids, int64_t R,
-                                                   const int32_t* __restrict__ n_ids,
-                                                   const int64_t* __restrict__ voff,
-                                                   const uint8_t* __restrict__ vbytes, int64_t n_bytes, int64_t V,
-                                                   const uint8_t* __restrict__ skip, uint8_t* __restrict__ out,
-                                                   int stride, int32_t* __restrict__ out_len,
-                                                   uint8_t* __restrict__ err_out, int64_t B) {
-  extern __shared__ uint32_t lds_words[];
-  const int wv = threadIdx.x >> 6;
-  uint8_t* buf = reinterpret_cast<uint8_t*>(lds_words) + wv * detok_lds(stride) + 4;  // raw row [stride + 8]
-  uint8_t* fix = buf + stride + 8;                                                      // lossy row [stride + 4]
-  __shared__ int sh_len_a[kRowWaves], sh_over_a[kRowWaves];
-  int& sh_len = sh_len_a[wv];
-  int& sh_over = sh_over_a[wv];
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
-  if (b >= B) return;  // the whole wave
-  int64_t rn = n_ids ? (int64_t)n_ids[b] : R;
-  rn = rn < 0 ? 0 : (rn > R ? R : rn);
-  const int64_t* row = ids + b * R;
-  const uint32_t* v4 = reinterpret_cast<const uint32_t*>(vbytes);
-  const int64_t last4 = n_bytes > 0 ? (n_bytes - 1) >> 2 : 0;  // last dword of the blob
+
+struct DetokArgs {
+  const int64_t* ids;
+  int64_t R;
+  const int32_t* n_ids;
+  const uint4* vpk;
+  const uint8_t* vbytes;
+  int64_t n_bytes, V;
+  uint8_t* out;
+  int stride;
+  int32_t* out_len;
+  uint8_t* err_out;
+  int64_t B;
+};
+
+#ifdef RMI_PARSE_STAMPS
+#define DSTAMP_PARAM , unsigned long long* dst_
+#define DSTAMP_ARG , dst_
+#else
+#define DSTAMP_PARAM
+#define DSTAMP_ARG
+#endif
+
+// Row b decoded into buf (dword aligned; 4 writable bytes before it and stride + 8 after; fix:
+// a second such buffer for the rare lossy rewrite, copied back), then written to out / out_len
+// / err_out.  -> the decoded length (the row stays in buf).
+__device__ __forceinline__ int detok_row(const DetokArgs& d, uint8_t* buf, uint8_t* fix, int64_t b,
+                                         int lane DSTAMP_PARAM) {
+  const int stride = d.stride;
+  int64_t rn = d.n_ids ? (int64_t)d.n_ids[b] : d.R;
+  rn = rn < 0 ? 0 : (rn > d.R ? d.R : rn);
+  const int64_t* row = d.ids + b * d.R;
   int pos = 0;
   bool bad = false, over = false;
   uint32_t high = 0;
@@ -616,57 +678,47 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
   for (int i = lane; i < (stride + 8) / 4; i += 64) reinterpret_cast<uint32_t*>(buf)[i] = 0u;
   wave_sync();
   for (int64_t c0 = 0; c0 < rn; c0 += 64 * kDetokG) {
-    int64_t id[kDetokG], off[kDetokG], end[kDetokG];
-    uint8_t sk[kDetokG];
+    int64_t id[kDetokG];
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {  // (c0 + 64 * g < rn: wave-uniform; empty chunks issue nothing)
       const int64_t i = c0 + 64 * g + lane;
       id[g] = c0 + 64 * g < rn && i < rn ? row[i] : -1;
     }
+    DSTAMP_WAIT(1);
+    // one 16-B gather per id: the token's bytes inline (<= 12) or its blob offset, and its
+    // length / skip bit (rmi_vocab_pack)
+    uint4 ent[kDetokG];
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {
-      off[g] = end[g] = 0;
-      sk[g] = 1;
+      ent[g] = make_uint4(0u, 0u, 0u, 0x80000000u);  // an empty chunk: skipped
       if (c0 + 64 * g >= rn) continue;
       const bool in = c0 + 64 * g + lane < rn;
-      const bool valid = id[g] >= 0 && id[g] < V;
+      const bool valid = id[g] >= 0 && id[g] < d.V;
       bad |= in && !valid;
-      const int64_t k = valid ? id[g] : 0;  // clamped, branch-free gathers
-      off[g] = voff[k];
-      end[g] = voff[k + 1];
-      sk[g] = valid ? skip[k] : (uint8_t)1;
+      ent[g] = d.vpk[valid ? id[g] : 0];  // clamped, branch-free gather
+      if (!valid) ent[g].w = 0x80000000u;
     }
+    DSTAMP_WAIT(2);
     int len[kDetokG], start[kDetokG];
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {
-      len[g] = sk[g] ? 0 : (int)(end[g] - off[g]);
+      len[g] = (ent[g].w >> 31) ? 0 : (int)(ent[g].w & 0xFFFFFFu);
       start[g] = pos;
       if (c0 + 64 * g >= rn) continue;
       const int incl = wave_inclusive_scan(len[g]);
       start[g] = pos + incl - len[g];
       pos += __builtin_amdgcn_readlane(incl, 63);
     }
-    uint32_t w[kDetokG][3];
-#pragma unroll
-    for (int g = 0; g < kDetokG; ++g) {
-      w[g][0] = w[g][1] = w[g][2] = 0u;
-      if (c0 + 64 * g >= rn) continue;
-      const int64_t q = off[g] >> 2;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) w[g][k] = v4[q + k <= last4 ? q + k : last4];
-    }
 #pragma unroll
     for (int g = 0; g < kDetokG; ++g) {
       if (c0 + 64 * g >= rn) continue;
-      const int r = (int)(off[g] & 3);
       const int sl = start[g], ln = len[g];
-      if (ln <= 12 - r && sl + ln <= stride) {
-        // the token's bytes: the 12-byte window at byte r of its dwords, masked to ln bytes,
-        // shifted to the destination's byte offset and OR-ed into <= 4 zeroed dwords (no loop
-        // over the bytes, no divergence)
-        const uint32_t x0 = __builtin_amdgcn_alignbyte(w[g][1], w[g][0], r) & byte_mask_n(ln);
-        const uint32_t x1 = __builtin_amdgcn_alignbyte(w[g][2], w[g][1], r) & byte_mask_n(ln - 4);
-        const uint32_t x2 = (w[g][2] >> (8 * r)) & byte_mask_n(ln - 8);
+      if (ln <= 12 && sl + ln <= stride) {
+        // the token's bytes, masked to ln, shifted to the destination's byte offset and OR-ed
+        // into <= 4 zeroed dwords (no loop over the bytes, no divergence)
+        const uint32_t x0 = ent[g].x & byte_mask_n(ln);
+        const uint32_t x1 = ent[g].y & byte_mask_n(ln - 4);
+        const uint32_t x2 = ent[g].z & byte_mask_n(ln - 8);
         high |= x0 | x1 | x2;
         const int sh = sl & 3;
         const uint32_t y0 = x0 << (8 * sh);
@@ -679,13 +731,15 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
         if (y2) atomicOr(q + 2, y2);
         if (y3) atomicOr(q + 3, y3);
       } else {
-        const uint64_t lo = (uint64_t)w[g][0] | ((uint64_t)w[g][1] << 32);
-        for (int k = 0; k < ln; ++k) {  // tokens longer than the window, or running past the row
+        // tokens longer than 12 bytes (their bytes in the blob at offset .x), or running past
+        // the row: byte by byte
+        for (int k = 0; k < ln; ++k) {
           const int p = sl + k;
-          const int o = k + r;
-          const uint32_t c = o < 8 ? (uint32_t)(lo >> (8 * o)) & 0xFFu
-                           : o < 12 ? (w[g][2] >> (8 * (o - 8))) & 0xFFu
-                                    : vbytes[off[g] + k];
+          uint32_t c;
+          if (ln <= 12)
+            c = ((k < 4 ? ent[g].x : k < 8 ? ent[g].y : ent[g].z) >> (8 * (k & 3))) & 0xFFu;
+          else
+            c = (int64_t)ent[g].x + k < d.n_bytes ? d.vbytes[(int64_t)ent[g].x + k] : 0u;
           if (p < stride) {
             atomicOr(reinterpret_cast<uint32_t*>(buf) + (p >> 2), c << (8 * (p & 3)));
             high |= c;
@@ -696,11 +750,11 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
       }
     }
   }
+  DSTAMP(3);
   int n = pos < stride ? pos : stride;
   if (lane < 8) buf[n + lane] = 0;  // the validity windows read up to 8 bytes past the end
   if (lane < 4) buf[lane - 4] = 0;  // ... and 4 before the start
   wave_sync();
-  const uint8_t* res = buf;
   // Non-ASCII bytes: a wave-parallel validity test first (UTF-8 validity is local: every lead
   // byte needs its continuation bytes with the Table 3-7 ranges, every continuation byte a lead
   // at most 3 bytes back whose sequence covers it).  Only an invalid row takes the serial
@@ -753,53 +807,134 @@ __global__ __launch_bounds__(64 * kRowWaves) void detok_kernel(const int64_t* __
       }
     }
   }
-  if (__ballot(invalid)) {  // some invalid sequence: the lossy rewrite (one lane)
-    if (lane == 0) {
-      bool ov = false;
-      sh_len = utf8_lossy(buf, n, fix, stride, ov);
-      sh_over = ov;
-    }
+  DSTAMP(4);
+  if (__ballot(invalid)) {  // some invalid sequence: the lossy rewrite (one lane), copied back
+    int n0 = 0;
+    bool ov = false;
+    if (lane == 0) n0 = utf8_lossy(buf, n, fix, stride, ov);
+    n = __builtin_amdgcn_readlane(n0, 0);
+    over |= __builtin_amdgcn_readlane((int)ov, 0) != 0;
     wave_sync();
-    n = sh_len;
-    over |= sh_over != 0;
-    res = fix;
+    for (int i = lane; i < (n + 3) >> 2; i += 64)
+      reinterpret_cast<uint32_t*>(buf)[i] = reinterpret_cast<const uint32_t*>(fix)[i];
+    wave_sync();
   }
   const int nw = (n + 3) >> 2;
-  if (lane < 4 && (n & 3)) const_cast<uint8_t*>(res)[n + lane] = 0;  // deterministic tail bytes
+  if (lane < 4 && (n & 3)) buf[n + lane] = 0;  // deterministic tail bytes
   wave_sync();
-  uint32_t* o4 = reinterpret_cast<uint32_t*>(out + b * (int64_t)stride);
-  const uint32_t* r4 = reinterpret_cast<const uint32_t*>(res);
+  uint32_t* o4 = reinterpret_cast<uint32_t*>(d.out + b * (int64_t)stride);
+  const uint32_t* r4 = reinterpret_cast<const uint32_t*>(buf);
   for (int i = lane; i < nw; i += 64) o4[i] = r4[i];
   const uint64_t any_bad = __ballot(bad), any_over = __ballot(over);
   if (lane == 0) {
-    out_len[b] = n;
-    if (err_out) err_out[b] |= (any_bad ? RMI_ERR_INDEX : 0) | (any_over ? RMI_ERR_UNSUP : 0);
+    d.out_len[b] = n;
+    if (d.err_out) d.err_out[b] |= (any_bad ? RMI_ERR_INDEX : 0) | (any_over ? RMI_ERR_UNSUP : 0);
   }
+  DSTAMP(5);
+  return n;
+}
+
+__global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(8))) void detok_kernel(DetokArgs d) {
+  extern __shared__ uint32_t lds_words[];
+  const int wv = threadIdx.x >> 6;
+  uint8_t* buf = reinterpret_cast<uint8_t*>(lds_words) + wv * detok_lds(d.stride) + 4;  // raw row [stride + 8]
+  uint8_t* fix = buf + d.stride + 8;                                                      // lossy row [stride + 4]
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (b >= d.B) return;  // the whole wave
+  DSTAMP_DECL;
+  DSTAMP(0);
+  detok_row(d, buf, fix, b, lane DSTAMP_ARG);
+  DSTAMP_FLUSH();
+}
+
+// The fused per-turn boundary: decode row b straight into the parse's LDS row (T + kPre), write
+// the decoded text out (the prompts and the history read it), then parse it in place: the
+// parse's stage (a global read of the text just written) and one launch disappear, and the
+// decode's memory-bound waves overlap other waves' parse work.
+__global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(8))) void detok_parse_kernel(
+    DetokArgs d, ParseArgs a) {
+  extern __shared__ uint64_t lds_q[];
+  const int wv = threadIdx.x >> 6;
+  uint8_t* lds = reinterpret_cast<uint8_t*>(lds_q) + wv * parse_lds(a.stride);
+  const int cap = list_cap(a.stride);
+  uint8_t* T = lds + 4;
+  uint8_t* Wb = lds + row_bytes(a.stride) + 4;
+  uint16_t* EL = reinterpret_cast<uint16_t*>(lds + 2 * row_bytes(a.stride));
+  uint16_t* ES = EL + cap;
+  uint8_t* EI = reinterpret_cast<uint8_t*>(ES + cap);
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (b >= a.B) return;  // the whole wave: no cross-wave barrier follows
+  PSTAMP_DECL;
+  PSTAMP(0);
+#ifdef RMI_PARSE_STAMPS
+  unsigned long long dst_[6];
+#endif
+  const Names nm = load_names(a.cfg, (a.sel && a.sel[b]) ? 1 : 0);
+  const int n = detok_row(d, T + kPre, Wb + kPre, b, lane DSTAMP_ARG);
+  parse_row(a, T, Wb, EL, ES, EI, b, n, 0, nm, lane PSTAMP_ARG);
+  PSTAMP_FLUSH();
 }
 
 }  // namespace
 }  // namespace rmi
 
-RMI_API int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const int64_t* vocab_off,
-                           const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, const uint8_t* skip, uint8_t* out,
-                           int32_t stride, int32_t* out_len, uint8_t* err, rmi_stream_t stream) {
+RMI_API int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const uint32_t* vocab_packed,
+                           const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, uint8_t* out, int32_t stride,
+                           int32_t* out_len, uint8_t* err, rmi_stream_t stream) {
   using namespace rmi;
-  if (B < 0 || R < 0 || V < 0 || stride <= 0) return RMI_EINVAL;
+  if (B < 0 || R < 0 || V < 1 || stride <= 0) return RMI_EINVAL;
   if (stride % 4 != 0 || stride > kMaxStride || B > 0x7FFFFFFF) return RMI_EUNSUP;
   if (B == 0) return RMI_OK;
-  if (!out || !out_len || !vocab_off || !skip || (R > 0 && !ids) || !vocab_bytes || n_bytes < 0) return RMI_EINVAL;
-  if ((reinterpret_cast<uintptr_t>(out) | reinterpret_cast<uintptr_t>(vocab_bytes)) & 3u) return RMI_EUNSUP;
+  if (!out || !out_len || !vocab_packed || (R > 0 && !ids) || n_bytes < 0 || (n_bytes > 0 && !vocab_bytes))
+    return RMI_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(out) & 3u) || (reinterpret_cast<uintptr_t>(vocab_packed) & 15u)) return RMI_EUNSUP;
   const int nw = row_waves(detok_lds(stride));
   const size_t shm = detok_lds(stride) * nw;
-  hipLaunchKernelGGL(detok_kernel, dim3((unsigned)((B + nw - 1) / nw)), dim3(64 * nw), shm,
-                     as_stream(stream), ids, R, n_ids, vocab_off, vocab_bytes, n_bytes, V, skip, out, (int)stride,
-                     out_len, err, B);
+  DetokArgs d{ids, R, n_ids, reinterpret_cast<const uint4*>(vocab_packed), vocab_bytes, n_bytes, V, out, (int)stride,
+              out_len, err, B};
+  hipLaunchKernelGGL(detok_kernel, dim3((unsigned)((B + nw - 1) / nw)), dim3(64 * nw), shm, as_stream(stream), d);
+  return launch_status();
+}
+
+RMI_API int rmi_detok_parse(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids,
+                            const uint32_t* vocab_packed, const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V,
+                            uint8_t* text, int32_t stride, int32_t* text_len, uint8_t* decode_err,
+                            const rmi_parse_cfg_t* cfg, const uint8_t* sel, int8_t* actions, uint8_t* n_actions,
+                            int32_t* spans, uint8_t* action_text, int32_t* action_len, int32_t Lact,
+                            uint8_t* parse_err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!cfg || B < 0 || R < 0 || V < 1 || stride <= 0) return RMI_EINVAL;
+  if (cfg->K < 1 || cfg->sep_len < 1 || cfg->sep_len > 16 || cfg->n_names < 0) return RMI_EINVAL;
+  if (cfg->K > kMaxK || cfg->n_names > RMI_PARSE_MAX_NAMES || stride % 4 != 0 || stride > kMaxParseStride ||
+      B > 0x7FFFFFFF)
+    return RMI_EUNSUP;
+  for (int j = 0; j < cfg->n_names; ++j)
+    if (cfg->name_len[j] < 1 || cfg->name_len[j] > 16) return RMI_EINVAL;
+  if (B == 0) return RMI_OK;
+  if (!text || !text_len || !vocab_packed || (R > 0 && !ids) || n_bytes < 0 || (n_bytes > 0 && !vocab_bytes) ||
+      !actions || !n_actions)
+    return RMI_EINVAL;
+  if (action_text && (!action_len || Lact < 1)) return RMI_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(text) & 3u) || (reinterpret_cast<uintptr_t>(vocab_packed) & 15u)) return RMI_EUNSUP;
+  DetokArgs d{ids, R, n_ids, reinterpret_cast<const uint4*>(vocab_packed), vocab_bytes, n_bytes, V, text, (int)stride,
+              text_len, decode_err, B};
+  ParseArgs a{*cfg, text, text_len, B, (int)stride, sel, actions, n_actions, spans, action_text, action_len,
+              (int)Lact, parse_err};
+  const int nw = row_waves(parse_lds(stride));
+  const size_t shm = parse_lds(stride) * nw;
+  hipLaunchKernelGGL(detok_parse_kernel, dim3((unsigned)((B + nw - 1) / nw)), dim3(64 * nw), shm,
+                     as_stream(stream), d, a);
   return launch_status();
 }
 
 #ifdef RMI_PARSE_STAMPS
 RMI_API int rmi_parse_set_stamps(unsigned long long* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_parse_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+RMI_API int rmi_detok_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_detok_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
 }
 #endif
 

@@ -172,16 +172,46 @@ def segments_for(grouping: str, env_outputs: List[Dict]):
 
 
 class DeviceEnvInputs:
-    """What ``get_env_inputs`` returns on the device path: the generations of the active envs
-    decoded on the device (rmi_detokenize, = batch_decode(skip_special_tokens=True),
-    ctx_manager.py:334-337) into UTF-8 rows of the FULL env batch (rows of envs without a
-    generation are empty and carry no input), ready for EnvStateManager.step's device turn.
+    """What ``get_env_inputs`` returns on the device path: the generations of the active envs as
+    token ids of the FULL env batch (rows of envs without a generation are empty and carry no
+    input), decoded on the device (rmi_detokenize, = batch_decode(skip_special_tokens=True),
+    ctx_manager.py:334-337) into UTF-8 rows — by EnvStateManager.step's device turn, fused with
+    the parse (rmi_detok_parse), or on first access to ``text`` / ``text_len`` / ``err``.
     Iterating it yields the reference's env-input dicts (host decode + parse), built lazily."""
 
-    def __init__(self, ctx, env_ids, env_ids_t, text, text_len, err):
+    def __init__(self, ctx, env_ids, env_ids_t, ids, n_ids, stride):
         self.ctx, self.env_ids, self.env_ids_t = ctx, env_ids, env_ids_t
-        self.text, self.text_len, self.err = text, text_len, err
+        self.ids, self.n_ids, self.stride = ids, n_ids, stride
+        self.vocab = ctx.device_vocab
+        self._text = self._text_len = self._err = None
         self._decoded = None
+
+    def set_decoded(self, text, text_len, err):
+        self._text, self._text_len, self._err = text, text_len, err
+
+    @property
+    def is_decoded(self):
+        return self._text is not None
+
+    def _ensure(self):
+        if self._text is None:
+            v = self.vocab
+            self.set_decoded(*torch.ops.ragen_amd.detokenize(self.ids, self.n_ids, v.packed, v.data, self.stride))
+
+    @property
+    def text(self):
+        self._ensure()
+        return self._text
+
+    @property
+    def text_len(self):
+        self._ensure()
+        return self._text_len
+
+    @property
+    def err(self):
+        self._ensure()
+        return self._err
 
     def __len__(self):
         return len(self.env_ids)
@@ -553,12 +583,10 @@ class ContextManager:
         # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
         # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
         # the decode and refused by the step (ValueError)
-        n_bytes = (vocab.off[1:] - vocab.off[:-1]).to(torch.int32)
-        raw = torch.where(vocab.skip.bool(), torch.zeros_like(n_bytes), n_bytes)[resp.clamp(0, n_bytes.numel() - 1)]
+        raw = vocab.raw_len[resp.clamp(0, vocab.raw_len.numel() - 1)]
         raw_max = int(raw.sum(1).max()) if resp.numel() else 0
         stride = max(4, min(PARSE_MAX_ROW, (3 * raw_max + 7) // 4 * 4))
-        text, tlen, err = torch.ops.ragen_amd.detokenize(ids, n_ids, vocab.off, vocab.data, vocab.skip, stride)
-        return DeviceEnvInputs(self, env_ids, idx, text, tlen, err)
+        return DeviceEnvInputs(self, env_ids, idx, ids, n_ids, stride)
 
     def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:
         """ctx_manager.py:354-356.  The rollout states of the attached env manager's device path

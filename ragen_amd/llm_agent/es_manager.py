@@ -408,16 +408,42 @@ class EnvStateManager:
             cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, prepend)
             acts, n_act, spans, at, al, perr = torch.ops.ragen_amd.parse_actions(
                 parse_cfg_bytes(cfg), text[a:z], text_len[a:z], sel, True, int(lact))
-            p = {"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
-                 "action_len": al if lact else None, "err": perr}
+            outs.append({"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
+                         "action_len": al if lact else None, "err": perr})
+        self._parsed_turn(outs, has_input, err)
+        return outs
+
+    def _parsed_turn(self, parsed, has_input, err):
+        """One turn launch per tag from the tag's parse outputs (ops.parse_actions dicts)."""
+        lo0 = self.env_lo
+        for tg, p in zip(self.tags, parsed):
+            a, z = tg.lo - lo0, tg.hi - lo0
             has = None if has_input is None else has_input[a:z]
             kw = {}
-            if lact:
+            if p["action_text"] is not None:
                 kw = {"answers": p["action_text"], "answer_len": p["action_len"]}
             tg.batch.step_turn(self._turn, p["actions"], p["n_actions"], has, tg.max_actions_per_traj,
                                self.format_penalty, None if err is None else err[a:z], **kw)
-            outs.append(p)
         self._turn += 1
+
+    def _decode_parse(self, inp, enable_think, action_sep):
+        """The device decode of the turn's generations fused with each tag's parse
+        (rmi_detok_parse, one launch per tag): -> per-tag parse dicts; the decoded rows go into
+        ``inp`` (the prompts and the history read them)."""
+        v = inp.vocab
+        lo0 = self.env_lo
+        outs, texts, lens, derrs = [], [], [], []
+        for tg in self.tags:
+            a, z = tg.lo - lo0, tg.hi - lo0
+            cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, True)
+            text, tlen, derr, acts, n_act, spans, at, al, perr = torch.ops.ragen_amd.detok_parse(
+                inp.ids[a:z], inp.n_ids[a:z], v.packed, v.data, inp.stride, parse_cfg_bytes(cfg), sel, True, int(lact))
+            outs.append({"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
+                         "action_len": al if lact else None, "err": perr})
+            texts.append(text)
+            lens.append(tlen)
+            derrs.append(derr)
+        inp.set_decoded(self._cat(texts), self._cat(lens), self._cat(derrs))
         return outs
 
     def _cat(self, xs):
@@ -433,6 +459,9 @@ class EnvStateManager:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
         dev = self.device
+        ap = self.sys_config.agent_proxy
+        # decode + parse in one launch per tag unless the rows were decoded already
+        parsed = None if inp.is_decoded else self._decode_parse(inp, bool(ap.enable_think), ap.action_sep)
         # a generation the device decode truncated (row stride cap) or could not decode (an id
         # outside the vocabulary) must not be stepped on: checked before the turn runs
         if bool(inp.err.any()):
@@ -442,8 +471,10 @@ class EnvStateManager:
         has = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
         has[inp.env_ids_t - self.env_lo] = 1
         err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
-        ap = self.sys_config.agent_proxy
-        parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
+        if parsed is None:
+            parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
+        else:
+            self._parsed_turn(parsed, has, err)
         obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
         flags = self._cat([tg.batch.ep.flags for tg in self.tags])
         left = self._cat([tg.max_actions_per_traj - tg.batch.ep.num_actions.to(torch.int32) for tg in self.tags])

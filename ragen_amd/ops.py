@@ -491,11 +491,35 @@ def parse_actions(cfg: _lib.ParseCfg, text: torch.Tensor, text_len: torch.Tensor
 @dataclass
 class VocabTable:
     """Device byte table of a byte-level BPE vocabulary: token t decodes to
-    bytes[off[t]:off[t+1]]; skip[t] = special token (dropped by skip_special_tokens=True)."""
+    bytes[off[t]:off[t+1]]; skip[t] = special token (dropped by skip_special_tokens=True).
+    ``packed`` u32[V,4] is rmi_detokenize's form of it (rmi_vocab_pack: the bytes of a token of
+    <= 12 bytes inline, its length and skip bit), built once on the host; ``raw_len`` i32[V]
+    the bytes each id decodes to (0 when skipped), which sizes the decoded rows."""
     off: torch.Tensor    # i64[V+1]
     data: torch.Tensor   # u8[total]
     skip: torch.Tensor   # u8[V]
     max_token_bytes: int = 0  # longest token's bytes (0 = unknown): sizes the decoded rows
+    packed: Optional[torch.Tensor] = None   # u32[V,4] (held as i32)
+    raw_len: Optional[torch.Tensor] = None  # i32[V]
+
+    def __post_init__(self):
+        if self.packed is None:
+            off = np.ascontiguousarray(self.off.cpu().numpy(), np.int64)
+            data = np.ascontiguousarray(self.data.cpu().numpy(), np.uint8)
+            skip = np.ascontiguousarray(self.skip.cpu().numpy(), np.uint8)
+            V = skip.shape[0]
+            if off.shape[0] != V + 1:
+                raise ValueError(f"off must hold V + 1 = {V + 1} offsets, got {off.shape[0]}")
+            pk = np.zeros((V, 4), np.uint32)
+            rc = lib().rmi_vocab_pack(off.ctypes.data, data.ctypes.data if data.size else None, data.size, V,
+                                      skip.ctypes.data, pk.ctypes.data)
+            if rc == _lib.RMI_EUNSUP:
+                raise NotImplementedError("a token longer than 2^24 - 1 bytes, or a vocabulary blob past 4 GiB")
+            check(rc, "rmi_vocab_pack")
+            self.packed = torch.from_numpy(pk.view(np.int32)).to(self.data.device)
+            lens = (off[1:] - off[:-1]).astype(np.int32)
+            lens[skip != 0] = 0
+            self.raw_len = torch.from_numpy(lens).to(self.data.device)
 
     @staticmethod
     def from_bytes(table, skip, device) -> "VocabTable":
@@ -572,11 +596,61 @@ def detokenize(ids: torch.Tensor, vocab: VocabTable, stride: int, n_ids: Optiona
         out = torch.empty(B, stride, dtype=torch.uint8, device=dev)
         n = torch.empty(B, dtype=torch.int32, device=dev)
         err = torch.zeros(B, dtype=torch.uint8, device=dev)
-    V = vocab.skip.numel()
-    check(lib().rmi_detokenize(_ptr(ids), B, R, _ptr(n_ids), _ptr(vocab.off), _ptr(vocab.data), vocab.data.numel(),
-                               V, _ptr(vocab.skip), _ptr(out), stride, _ptr(n), _ptr(err), _stream(ids.device)),
-          "rmi_detokenize")
-    return out, n, err
+    return detokenize_packed(ids, vocab.packed, vocab.data, stride, n_ids, (out, n, err))
+
+
+def detokenize_packed(ids: torch.Tensor, packed: torch.Tensor, data: torch.Tensor, stride: int,
+                      n_ids: Optional[torch.Tensor], out):
+    """rmi_detokenize over a packed vocabulary (VocabTable.packed) into out = (text, len, err)."""
+    _dev(ids, n_ids, packed, data)
+    _dt(packed, torch.int32, "vocab_packed")
+    text, n, err = out
+    B, R = ids.shape
+    if packed.dim() != 2 or packed.shape[1] != 4 or not packed.is_contiguous():
+        raise ValueError("vocab_packed must be a contiguous u32[V, 4]")
+    check(lib().rmi_detokenize(_ptr(ids), B, R, _ptr(n_ids), _ptr(packed), _ptr(data), data.numel(), packed.shape[0],
+                               _ptr(text), text.shape[1], _ptr(n), _ptr(err), _stream(ids.device)), "rmi_detokenize")
+    return text, n, err
+
+
+def detok_parse(ids: torch.Tensor, vocab: "VocabTable", stride: int, cfg: _lib.ParseCfg,
+                n_ids: Optional[torch.Tensor] = None, sel: Optional[torch.Tensor] = None, with_spans: bool = True,
+                action_text_len: int = 0, out: Optional[dict] = None):
+    """detokenize + parse_actions in one launch (rmi_detok_parse): response ids i64[B,R] ->
+    dict(text u8[B,stride], text_len i32[B], decode_err u8[B], and parse_actions' outputs).
+    ``out``: a previous result to write into (graph-capturable)."""
+    _dev(ids, n_ids, sel, vocab.packed, vocab.data)
+    _dt(ids, torch.int64, "ids")
+    _dt(n_ids, torch.int32, "n_ids")
+    _dt(sel, torch.uint8, "sel")
+    B, R = ids.shape
+    stride = (int(stride) + 3) // 4 * 4
+    dev = ids.device
+    K = int(cfg.K)
+    if out is not None:
+        if out["text"].shape != (B, stride) or out["actions"].shape != (B, K):
+            raise ValueError("out= buffers do not match this batch")
+        out["decode_err"].zero_()
+        out["err"].zero_()
+        o = out
+    else:
+        o = {"text": torch.empty(B, stride, dtype=torch.uint8, device=dev),
+             "text_len": torch.empty(B, dtype=torch.int32, device=dev),
+             "decode_err": torch.zeros(B, dtype=torch.uint8, device=dev),
+             "actions": torch.empty(B, K, dtype=torch.int8, device=dev),
+             "n_actions": torch.empty(B, dtype=torch.uint8, device=dev),
+             "spans": torch.empty(B, 4, dtype=torch.int32, device=dev) if with_spans else None,
+             "action_text": None, "action_len": None,
+             "err": torch.zeros(B, dtype=torch.uint8, device=dev)}
+        if action_text_len:
+            o["action_text"] = torch.empty(B, K, int(action_text_len), dtype=torch.uint8, device=dev)
+            o["action_len"] = torch.empty(B, K, dtype=torch.int32, device=dev)
+    check(lib().rmi_detok_parse(_ptr(ids), B, R, _ptr(n_ids), _ptr(vocab.packed), _ptr(vocab.data), vocab.data.numel(),
+                                vocab.packed.shape[0], _ptr(o["text"]), stride, _ptr(o["text_len"]),
+                                _ptr(o["decode_err"]), ctypes.byref(cfg), _ptr(sel), _ptr(o["actions"]),
+                                _ptr(o["n_actions"]), _ptr(o["spans"]), _ptr(o["action_text"]), _ptr(o["action_len"]),
+                                int(action_text_len), _ptr(o["err"]), _stream(dev)), "rmi_detok_parse")
+    return o
 
 
 # ------------------------------------------------------------------- token masks (A11)

@@ -590,15 +590,19 @@ def _(desc, s, nrow, ncol, glyph_bytes, glyph_len):
 
 
 @_op("detokenize")
-def detokenize(ids: Tensor, n_ids: Optional[Tensor], vocab_off: Tensor, vocab_bytes: Tensor, skip: Tensor,
+def detokenize(ids: Tensor, n_ids: Optional[Tensor], vocab_packed: Tensor, vocab_bytes: Tensor,
                stride: int) -> Tuple[Tensor, Tensor, Tensor]:
-    """tokenizer.batch_decode(responses, skip_special_tokens=True) (ctx_manager.py:334-337)
-    -> (UTF-8 rows u8[B, stride], len i32[B], err u8[B])."""
-    return ops.detokenize(ids, ops.VocabTable(vocab_off, vocab_bytes, skip), stride, n_ids)
+    """tokenizer.batch_decode(responses, skip_special_tokens=True) (ctx_manager.py:334-337) over
+    the packed vocabulary (ops.VocabTable.packed) -> (UTF-8 rows u8[B, stride], len i32[B], err u8[B])."""
+    B = ids.shape[0]
+    st = (int(stride) + 3) // 4 * 4
+    out = (torch.empty(B, st, dtype=torch.uint8, device=ids.device), torch.empty(B, dtype=torch.int32, device=ids.device),
+           torch.zeros(B, dtype=torch.uint8, device=ids.device))
+    return ops.detokenize_packed(ids, vocab_packed, vocab_bytes, st, n_ids, out)
 
 
 @detokenize.register_fake
-def _(ids, n_ids, vocab_off, vocab_bytes, skip, stride):
+def _(ids, n_ids, vocab_packed, vocab_bytes, stride):
     B = ids.shape[0]
     st = (int(stride) + 3) // 4 * 4
     return (ids.new_empty(B, st, dtype=torch.uint8), ids.new_empty(B, dtype=torch.int32),
@@ -641,6 +645,37 @@ def _(cfg, text, text_len, sel, with_spans, action_text_len):
             text.new_empty(B if with_spans else 0, 4, dtype=torch.int32),
             text.new_empty(B, K, action_text_len, dtype=torch.uint8), text.new_empty(B, K, dtype=torch.int32),
             text.new_empty(B, dtype=torch.uint8))
+
+
+@_op("detok_parse")
+def detok_parse(ids: Tensor, n_ids: Optional[Tensor], vocab_packed: Tensor, vocab_bytes: Tensor, stride: int,
+                cfg: List[int], sel: Optional[Tensor], with_spans: bool,
+                action_text_len: int) -> Tuple[Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor]:
+    """batch_decode + _parse_response + the name map in one launch (ctx_manager.py:332-352,
+    :148-173, es_manager.py:230-240) -> (text u8[B, stride], text_len i32[B], decode_err u8[B],
+    actions i8[B,K], n_actions u8[B], spans i32[B,4] (0 rows without spans), action_text
+    u8[B,K,Lact], action_len i32[B,K], parse_err u8[B])."""
+    c = _parse_cfg(cfg)
+    vt = ops.VocabTable.__new__(ops.VocabTable)
+    vt.packed, vt.data = vocab_packed, vocab_bytes
+    o = ops.detok_parse(ids, vt, stride, c, n_ids, sel, with_spans, action_text_len)
+    B, K = ids.shape[0], int(c.K)
+    dev = ids.device
+    spans = o["spans"] if o["spans"] is not None else torch.empty(0, 4, dtype=torch.int32, device=dev)
+    at = o["action_text"] if o["action_text"] is not None else torch.empty(B, K, 0, dtype=torch.uint8, device=dev)
+    al = o["action_len"] if o["action_len"] is not None else torch.zeros(B, K, dtype=torch.int32, device=dev)
+    return o["text"], o["text_len"], o["decode_err"], o["actions"], o["n_actions"], spans, at, al, o["err"]
+
+
+@detok_parse.register_fake
+def _(ids, n_ids, vocab_packed, vocab_bytes, stride, cfg, sel, with_spans, action_text_len):
+    B, K = ids.shape[0], int(_parse_cfg(cfg).K)
+    st = (int(stride) + 3) // 4 * 4
+    return (ids.new_empty(B, st, dtype=torch.uint8), ids.new_empty(B, dtype=torch.int32),
+            ids.new_empty(B, dtype=torch.uint8), ids.new_empty(B, K, dtype=torch.int8),
+            ids.new_empty(B, dtype=torch.uint8), ids.new_empty(B if with_spans else 0, 4, dtype=torch.int32),
+            ids.new_empty(B, K, action_text_len, dtype=torch.uint8), ids.new_empty(B, K, dtype=torch.int32),
+            ids.new_empty(B, dtype=torch.uint8))
 
 
 def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params):

@@ -132,7 +132,7 @@ def _random_table(V, seed):
     rng = np.random.default_rng(seed)
     table = []
     for i in range(V):
-        k = int(rng.integers(0, 9))
+        k = int(rng.integers(0, 9)) if i % 11 else int(rng.integers(9, 41))  # some past the 12 inline bytes
         if i % 7 == 0:  # ASCII-only tokens
             table.append(bytes(rng.integers(32, 127, size=k).astype(np.uint8)))
         else:
@@ -303,3 +303,122 @@ def test_detokenize_utf8_validity_edges(device):
         want = b"".join(r).decode("utf-8", "replace").encode("utf-8")
         assert out[i, :n[i]].tobytes() == want, (i, b"".join(r))
     assert not err.any()
+
+
+# ------------------------------------------------------- fused decode + parse (rmi_detok_parse)
+def _byte_word_tokens(texts, words):
+    """Greedy tokenisation over one token per byte + the given words (ids 256..)."""
+    rows = []
+    for t in texts:
+        bts, row, i = t.encode("utf-8"), [], 0
+        while i < len(bts):
+            for w, wb in enumerate(words):
+                if bts.startswith(wb, i):
+                    row.append(256 + w)
+                    i += len(wb)
+                    break
+            else:
+                row.append(bts[i])
+                i += 1
+        rows.append(row)
+    return rows
+
+
+def _fused_vs_separate(device, ids, n_ids, vt, stride, cfg, sel=None, Lact=0):
+    """rmi_detok_parse == rmi_detokenize then rmi_parse_actions, every output."""
+    tid = torch.from_numpy(ids).to(device)
+    tn = None if n_ids is None else torch.from_numpy(n_ids).to(device)
+    ts = None if sel is None else torch.from_numpy(sel).to(device)
+    text, tlen, derr = ops.detokenize(tid, vt, stride, tn)
+    sep = ops.parse_actions(cfg, text, tlen, ts, True, Lact)
+    fu = ops.detok_parse(tid, vt, stride, cfg, tn, ts, True, Lact)
+    torch.cuda.synchronize()
+    tl = tlen.cpu().numpy()
+    ft = fu["text"].cpu().numpy()
+    st = text.cpu().numpy()
+    assert np.array_equal(fu["text_len"].cpu().numpy(), tl)
+    for b in range(len(tl)):  # the row bytes (a row's dwords past its length are not written)
+        assert ft[b, :tl[b]].tobytes() == st[b, :tl[b]].tobytes(), b
+    assert torch.equal(fu["decode_err"], derr)
+    for k in ("actions", "n_actions", "spans", "err", "action_text", "action_len"):
+        if sep[k] is None:
+            assert fu[k] is None
+            continue
+        if k == "action_text":  # the bytes past each action's length are not written
+            al = sep["action_len"].cpu().numpy()
+            a, f = sep[k].cpu().numpy(), fu[k].cpu().numpy()
+            n = sep["n_actions"].cpu().numpy()
+            for b in range(a.shape[0]):
+                for j in range(n[b]):
+                    assert a[b, j, :al[b, j]].tobytes() == f[b, j, :al[b, j]].tobytes(), (b, j)
+            continue
+        assert torch.equal(fu[k], sep[k]), k
+    return fu
+
+
+def test_detok_parse_fused_on_reference_vectors(device):
+    """The 1530 recorded _parse_response vectors, tokenized over bytes + tag / name words,
+    through the fused kernel == the separate kernels (themselves checked against the oracle
+    above), every lookup, with action text for the pass-through lookup."""
+    lookups, cases = _golden()
+    words = [b"<think>", b"</think>", b"<answer>", b"</answer>", b"<|im_end|>", b" || ", b"Up", b"Down", b"Left",
+             b"Right", b"  ", b"\xe2\x80\x83"]
+    table = [bytes([i]) for i in range(256)] + words + [b"<|endoftext|>"]
+    skip = np.zeros(len(table), np.uint8)
+    skip[-1] = 1
+    vt = ops.VocabTable.from_bytes(table, skip, device)
+    groups = {}
+    for c in cases:
+        groups.setdefault((c["enable_think"], c["K"], c["sep"]), []).append(c)
+    for lk_name in ("sokoban", "bandit", "kelvin", "none"):
+        lk = lookups[lk_name]
+        for (think, K, sep), cs in groups.items():
+            rows = _byte_word_tokens([c["text"] for c in cs], words)
+            R = max(len(r) for r in rows) + 2
+            ids = np.full((len(rows), R), len(table) - 1, np.int64)  # right-padded with the skipped pad id
+            for b, r in enumerate(rows):
+                ids[b, :len(r)] = r
+            stride = max(64, (max(len(c["text"].encode()) for c in cs) + 8) // 4 * 4)
+            fu = _fused_vs_separate(device, ids, None, vt, stride, ops.parse_config(think, K, sep, lk),
+                                    Lact=256 if lk is None else 0)
+            # and against the recorded reference outputs
+            n = fu["n_actions"].cpu().numpy()
+            for b, c in enumerate(cs):
+                assert n[b] == len(c["actions"]), c["text"]
+
+
+def test_detok_parse_fused_edges(device):
+    """Random vocabularies (long tokens past the inline 12 bytes, invalid UTF-8, skipped ids),
+    out-of-range ids, ragged n_ids, rows truncated at the stride, Bandit's per-row id column,
+    and rows at the parse row limit."""
+    V = 3000
+    table, skip = _random_table(V, 4)
+    # answer-shaped tokens so that some rows parse to actions
+    table += [b"x</think><answer>", b"Phoenix", b" || ", b"dragon", b"</answer>"]
+    skip = np.concatenate([skip, np.zeros(5, np.uint8)])
+    vt = ops.VocabTable.from_bytes(table, skip, device)
+    rng = np.random.default_rng(8)
+    B, R = 1500, 64
+    ids = rng.integers(0, V, size=(B, R)).astype(np.int64)
+    for b in range(0, B, 3):  # answer rows: head, names, separators, tail
+        k = int(rng.integers(1, 6))
+        body = [V] + [int(rng.choice([V + 1, V + 3, int(rng.integers(0, V))])) if j % 2 == 0 else V + 2
+                      for j in range(2 * k - 1)] + [V + 4]
+        ids[b, :len(body)] = body
+    n_ids = rng.integers(0, R + 1, size=B).astype(np.int32)
+    n_ids[::3] = R
+    ids[7, 2], ids[8, 0] = V + 10, -5  # outside the vocabulary
+    n_ids[7], n_ids[8] = R, R
+    sel = (rng.random(B) < 0.5).astype(np.uint8)
+    lo, hi = {1: "Phoenix", 2: "Dragon"}, {1: "Dragon", 2: "Phoenix"}
+    for stride in (64, 1024, 8192):  # 64: most rows truncated (decode_err UNSUP)
+        for think in (True, False):
+            fu = _fused_vs_separate(device, ids, n_ids, vt, stride, ops.parse_config(think, 3, "||", lo, hi), sel)
+            derr = fu["decode_err"].cpu().numpy()
+            assert derr[7] & _lib.ERR_INDEX and derr[8] & _lib.ERR_INDEX
+            if stride == 64:
+                assert (derr & _lib.ERR_UNSUP).any()
+            if stride == 1024 and think:
+                assert (fu["n_actions"].cpu().numpy() > 0).sum() > B // 10
+    with pytest.raises(NotImplementedError):  # the parse's row limit
+        ops.detok_parse(torch.from_numpy(ids).to(device), vt, 8196, ops.parse_config(True, 3, "||", lo))

@@ -89,6 +89,35 @@ def test_vocab_table_from_hf_tokenizer_matches_oracle():
     assert got == want
 
 
+def test_vocab_pack_layout():
+    """rmi_vocab_pack (host C, the table rmi_detokenize gathers from): every entry decodes back
+    to its token's bytes / skip bit — inline for tokens of <= 12 bytes, by blob offset beyond —
+    on random vocabularies with empty, 12-, 13- and long tokens."""
+    import numpy as np
+    import torch
+    from ragen_amd.ops import VocabTable
+    rng = random.Random(3)
+    for trial in range(20):
+        V = rng.randint(1, 400)
+        table = [bytes(rng.randrange(256) for _ in range(rng.choice([0, 1, 3, 7, 11, 12, 13, 20, 300])))
+                 for _ in range(V)]
+        skip = [rng.random() < 0.1 for _ in range(V)]
+        vt = VocabTable.from_bytes(table, skip, torch.device("cpu"))
+        pk = vt.packed.numpy().view(np.uint32)
+        blob = vt.data.numpy().tobytes()
+        for t, (tb, sk) in enumerate(zip(table, skip)):
+            meta = int(pk[t, 3])
+            assert meta >> 31 == int(sk) and meta & 0xFFFFFF == len(tb)
+            if len(tb) <= 12:
+                got = b"".join(int(pk[t, k]).to_bytes(4, "little") for k in range(3))[:len(tb)]
+                assert got == tb and b"".join(int(pk[t, k]).to_bytes(4, "little") for k in range(3))[len(tb):] == \
+                    bytes(12 - len(tb))
+            else:
+                o = int(pk[t, 0])
+                assert blob[o:o + len(tb)] == tb
+            assert int(vt.raw_len[t]) == (0 if sk else len(tb))
+
+
 def test_synthetic_responses_parse_to_their_actions():
     from ragen_amd import synthetic as S
     lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}

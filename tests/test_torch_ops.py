@@ -24,7 +24,7 @@ def test_every_device_entry_point_is_an_op():
             "frozenlake_reset", "frozenlake_render", "bandit_step_turn", "countdown_step_turn", "countdown_reward",
             "rollout_metrics", "trajectory_scores", "rollout_finalize", "group_normalize", "filter_groups", "row_sum",
             "masks_and_scores", "gae", "bilevel_gae", "masked_whiten_", "masked_whiten_stats_", "whiten_row_stats",
-            "grpo_outcome", "detokenize", "parse_actions", "pcg64_seed", "reinforce_pp_returns", "remax",
+            "grpo_outcome", "detokenize", "detok_parse", "parse_actions", "pcg64_seed", "reinforce_pp_returns", "remax",
             "rloo_outcome", "mask_mul_"}
     assert want <= names, want - names
     for n in MUTATING:  # the schema names what an op writes in place
@@ -76,7 +76,6 @@ def test_fake_kernels_shapes():
                                                device=d), torch.empty(B, dtype=torch.int32, device=d), None, True, 0)
         assert a.shape == (B, 5) and a.dtype == torch.int8 and sp.shape == (B, 4)
         txt, tl, te = R.detokenize(torch.empty(B, 9, dtype=torch.int64, device=d), None,
-                                   torch.empty(11, dtype=torch.int64, device=d), torch.empty(40, dtype=torch.uint8,
-                                                                                          device=d),
-                                   torch.empty(10, dtype=torch.uint8, device=d), 30)
+                                   torch.empty(10, 4, dtype=torch.int32, device=d),
+                                   torch.empty(40, dtype=torch.uint8, device=d), 30)
         assert txt.shape == (B, 32)

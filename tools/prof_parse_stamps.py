@@ -35,7 +35,7 @@ for B, tw, think in ((1024, (8, 60), True), (8192, (8, 60), True), (8192, (0, 2)
     texts = synthetic.responses_for_actions(ids[0], n[0], lk, think_words=tw)
     buf, lens = synthetic.encode_rows(texts)
     text, tl = torch.from_numpy(buf).to(dev), torch.from_numpy(lens).to(dev)
-    st = torch.zeros(B, 10, dtype=torch.int64, device=dev)
+    st = torch.zeros(B, 12, dtype=torch.int64, device=dev)
     L.rmi_parse_set_stamps(ctypes.c_void_p(st.data_ptr()))
     cfg = ops.parse_config(think, 5, "||", lk)
     o = ops.parse_actions(cfg, text, tl)
