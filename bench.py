@@ -148,6 +148,28 @@ def scale_leg(R, device, tile=512, reps=5):
     return dur, B
 
 
+def layout_floor(active, hw=36, all_env_bytes=(1, 2, 1, 1, 1, 1, 8, 1, 5), lines=(64, 128)):
+    """The least HBM read traffic per launch that the turn kernel's access contract allows, for
+    the scale leg's plain turns: the caller-owned SoA keeps done envs
+    interleaved with acting ones, so every env's lane reads its flags and scalars (flags,
+    player, num_env_steps, boxes_on_target, num_actions, n_turns, penalty, n_actions, actions:
+    21 B) and the two grids (room_state, room_fixed) are read wherever an acting env's row
+    touches a line.  active: bool[T, B] per turn.  -> {line: MB per launch (mean over turns)}."""
+    T, B = active.shape
+    out = {}
+    for line in lines:
+        full = sum(-(-B * sz // line) * line for sz in all_env_bytes)
+        tot = 0
+        for t in range(T):
+            idx = np.nonzero(active[t])[0].astype(np.int64)
+            touched = np.zeros(-(-B * hw // line), bool)
+            touched[(idx * hw) // line] = True
+            touched[(idx * hw + hw - 1) // line] = True
+            tot += full + 2 * int(touched.sum()) * line
+        out[line] = tot / T / 1e6
+    return out
+
+
 def hbm_copy_peak(device, nbytes=1 << 30, reps=10):
     """Achievable HBM bandwidth on this box: rmi_device_copy (the library's 16-B-per-lane
     grid-stride streaming copy, MI355X_MICROARCH.md's float4-copy recipe) of 1 GiB, read +
@@ -610,28 +632,58 @@ def api_leg(device):
                    "tokenizer": f"{tok.name_or_path}, vocab {len(tok)}",
                    "note": "LLMAgentProxy.rollout, response token ids on the GPU, an actor reading input_ids / "
                            "attention_mask / position_ids every turn, device prompt ids; last of 4 rollouts"}
-    # the dict facade: EnvStateManager.step with the reference's list-of-dict inputs
-    es = EnvStateManager(cfg, mode="train", device=device)
-    es.reset(seed=synthetic.ENV_SEED)
+    # the dict facade: EnvStateManager.step with the reference's list-of-dict inputs, the turn
+    # reaching the kernel through the torch custom op (the facade's default) and through ctypes
+    from ragen_amd.env import SokobanBatch
     names = {1: "Up", 2: "Down", 3: "Left", 4: "Right", 0: "Jump"}  # 0 = a name outside the action lookup
     turn_inputs = [[[names[int(a)] for a in ids[t, i, :int(n[t, i])]] for i in range(B)] for t in range(T)]
-    active = list(range(B))
-    dsteps = 0
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for t in range(T):
-        inputs = [{"env_id": i, "llm_response": "", "llm_raw_response": "", "actions": turn_inputs[t][i]}
-                  for i in active]
-        outs = es.step(inputs)
-        active = [o["env_id"] for o in outs]
-        dsteps += int(es.tags[0].batch.ep.turn_exec[t].sum().item())
-        if not active:
-            break
-    dt = time.perf_counter() - t0
+
+    def dict_rollout():
+        es = EnvStateManager(cfg, mode="train", device=device)
+        es.reset(seed=synthetic.ENV_SEED)
+        active = list(range(B))
+        dsteps = 0
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for t in range(T):
+            inputs = [{"env_id": i, "llm_response": "", "llm_raw_response": "", "actions": turn_inputs[t][i]}
+                      for i in active]
+            outs = es.step(inputs)
+            active = [o["env_id"] for o in outs]
+            dsteps += int(es.tags[0].batch.ep.turn_exec[t].sum().item())
+            if not active:
+                break
+        return dsteps, time.perf_counter() - t0
+
+    dict_path = {}
+    for mode in ("op", "ctypes"):
+        SokobanBatch.dispatch = mode
+        try:
+            runs = [dict_rollout() for _ in range(3)]
+        finally:
+            SokobanBatch.dispatch = "op"
+        dsteps, dt = min(runs, key=lambda r: r[1])
+        dict_path[mode] = {"env_steps": dsteps, "seconds": dt, "env_steps_per_s": dsteps / dt}
+    # the per-call host cost of the two dispatch routes (one 8192-env turn launch, no env acting)
+    env = SokobanBatch(None, B, T, K, device)
+    z8 = torch.zeros(B, K, dtype=torch.int8, device=device)
+    zu = torch.zeros(B, dtype=torch.uint8, device=device)
+    per_call = {}
+    for mode in ("op", "ctypes"):
+        env.dispatch = mode
+        for _ in range(20):
+            env.step_turn(0, z8, zu, zu, 10, -0.1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(500):
+            env.step_turn(0, z8, zu, zu, 10, -0.1)
+        per_call[mode] = (time.perf_counter() - t0) / 500 * 1e6
+        torch.cuda.synchronize()
     return {"env_steps_per_s": device_path["env_steps_per_s"], "device_path": device_path,
-            "dict_path": {"env_steps": dsteps, "seconds": dt, "env_steps_per_s": dsteps / dt,
-                          "note": "EnvStateManager.step facade, host dicts + text obs each turn (the action-name "
-                                  "lists are built before the timed loop)"}}
+            "dict_path": dict(dict_path["op"], ctypes=dict_path["ctypes"], host_us_per_turn_call=per_call,
+                              note="EnvStateManager.step facade, host dicts + text obs each turn (the action-name "
+                                   "lists are built before the timed loop); best of 3 rollouts; the top level "
+                                   "goes through the torch custom op, `ctypes` through the C ABI directly")}
 
 
 def cpu_baseline_parallel(R, workers=16, reps=20):
@@ -929,11 +981,22 @@ def main():
         s_dur, s_B = scale_leg(R, device)
         s_bytes = bytes_per_rollout * (s_B // R.B)
         s_ach = s_bytes / s_dur / 1e9
+        tile = s_B // R.B
+        act = np.tile(np.stack([n_turns > t for t in range(T_TURNS)]), (1, tile))
+        floor = layout_floor(act)
+        algo_read = float(act.sum()) * 83 / T_TURNS  # 83 of the 141 B per active env-turn are reads
+        pmc_read = _pmc_field(PMC_SCALE_GLOB, "read_bytes_per_launch")
         at_scale = {"envs": s_B, "avg_launch_us": s_dur / T_TURNS * 1e6, "achieved": s_ach,
                     "frac": s_ach / HBM_PEAK_GBS, "frac_of_achievable": (s_ach / copy_peak) if copy_peak else None,
                     "algorithmic_MB_per_launch": s_bytes / T_TURNS / 1e6,
                     "cache": "out of the 256 MiB Infinity Cache (per-launch footprint ~420 MB): HBM-bound",
                     "traffic": _pmc_field(PMC_SCALE_GLOB, "hbm_bytes_per_launch"),
+                    "reads": {"algorithmic_MB_per_launch": algo_read / 1e6,
+                              "layout_floor_MB_per_launch": {f"{k}B_lines": v for k, v in floor.items()},
+                              "pmc_MB_per_launch": pmc_read / 1e6 if pmc_read else None,
+                              "note": "layout floor: every env's 21 B of flags / scalars / actions plus the grid "
+                                      "lines an acting env's 36-B rows touch (done envs interleaved with acting "
+                                      "ones in the caller's SoA), bench.layout_floor"},
                     "note": "same kernel and workload per env, batch tiled 512x"}
 
     if rank == 0:

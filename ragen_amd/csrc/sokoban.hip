@@ -507,7 +507,7 @@ __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMax
 // kFirst: the launch is a fresh episode's first turn fused with the reset (rmi_sokoban_reset):
 // the rows and players come from init_state / init_player, the counters and the episode record
 // start at zero without being read, and every env's state and whole record are written.
-// kLate (large batches, plain turns): the rows are loaded after the activity test and only by
+// kLate (large batches, plain and last turns): the rows are loaded after the activity test and only by
 // the lanes whose env acts this turn, a second memory round trip that a batch this size hides,
 // so the rows of done envs are not fetched (HBM-bound there: done envs were ≈18 % of the bench
 // rollout's env-turns, their rows ≈9 % of its traffic).
@@ -825,7 +825,7 @@ __global__ __launch_bounds__(kBlock) void sokoban_reset_kernel(rmi_sokoban_t env
 }  // namespace rmi
 
 #ifndef RMI_SOK_LATE_MIN
-#define RMI_SOK_LATE_MIN (1 << 17)  // envs from which plain turns take the late row loads (kLate)
+#define RMI_SOK_LATE_MIN (1 << 17)  // envs from which plain and last turns take the late row loads (kLate)
 #endif
 namespace rmi {
 namespace {
@@ -843,7 +843,7 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
   const bool w32 = (H - 1) * W <= 32;  // the board window fits a u32
   // lanes per env: spread a batch too small to fill the chip over 4 lanes per env
   const bool spread = spread_lanes(ep->B);
-  const bool late = !kFin && !kFirst && !spread && ep->B >= RMI_SOK_LATE_MIN;
+  const bool late = !kFirst && !spread && ep->B >= RMI_SOK_LATE_MIN;
 #define RMI_LAUNCH(HW_, M_)                                                                                   \
   do {                                                                                                        \
     if (spread)                                                                                               \
@@ -853,8 +853,8 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
                          dim3(kWave * kSokWpb), 0, s, *env, *ep, *in, hw, border, err, fin, init_state,      \
                          init_player);                                                                        \
     else if (late) {                                                                                          \
-      if constexpr (!kFin && !kFirst)                                                                         \
-        hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, false, false, true>), dim3(grid),           \
+      if constexpr (!kFirst)                                                                                  \
+        hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, false, true>), dim3(grid),            \
                            dim3(kWave * kSokWpb), 0, s, *env, *ep, *in, hw, border, err, fin, init_state,    \
                            init_player);                                                                      \
     } else                                                                                                    \

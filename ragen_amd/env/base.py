@@ -16,6 +16,10 @@ from .. import ops
 
 class BatchEnv:
     env_type = "base"
+    # how a turn reaches the C ABI: "op" = the torch custom operator (torch.ops.ragen_amd.*,
+    # dispatcher + schema checks), "ctypes" = the C entry point straight through ops (the
+    # bench reports the facade both ways)
+    dispatch = "op"
 
     def __init__(self, config, n_envs: int, max_turns: int, max_actions_per_turn: int, device=None):
         self.config = config

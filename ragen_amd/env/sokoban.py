@@ -86,8 +86,14 @@ class SokobanBatch(BatchEnv):
         self._invalidate()
 
     def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
-        torch.ops.ragen_amd.sokoban_step_turn(*self.state_args(), actions, n_actions, has_input, err, int(turn),
-                                              int(max_actions_per_traj), float(format_penalty), *self.dims())
+        if self.dispatch == "ctypes":
+            ops._dev(self.room_state, actions, n_actions, has_input, err)
+            ops.sokoban_step_turn(self.struct(), self.ep, ops.turn_struct(int(turn), actions, n_actions, has_input,
+                                                                          int(max_actions_per_traj),
+                                                                          float(format_penalty)), err)
+        else:
+            torch.ops.ragen_amd.sokoban_step_turn(*self.state_args(), actions, n_actions, has_input, err, int(turn),
+                                                  int(max_actions_per_traj), float(format_penalty), *self.dims())
         self._invalidate()
 
     def render_rows(self):

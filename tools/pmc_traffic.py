@@ -10,6 +10,7 @@ bytes of every 64-B line a store touches.  So hbm_bytes = (2 * FETCH_SIZE + WRIT
 Only launches with Grid_Size >= the given minimum are averaged (separates a tiled batch's
 launches from the small ones of the same process)."""
 import csv
+import gzip
 import glob
 import json
 import os
@@ -18,8 +19,8 @@ import sys
 
 def per_launch(d, kernel, counter, min_grid):
     vals = {}
-    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-        with open(f) as fh:
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True) + glob.glob(os.path.join(d, "**", "*counter_collection.csv.gz"), recursive=True):
+        with (gzip.open(f, "rt") if f.endswith(".gz") else open(f)) as fh:
             for row in csv.DictReader(fh):
                 if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter and \
                         int(row["Grid_Size"]) >= min_grid:

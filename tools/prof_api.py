@@ -76,3 +76,4 @@ pr.enable()
 print("device path (profiled):", dev_rollout())
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(40)
+pstats.Stats(pr).sort_stats("cumulative").print_stats(70)

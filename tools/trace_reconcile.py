@@ -9,6 +9,7 @@ the next - Start).  The sum of the periods over a rollout is the rollout's time 
 kernels' summed durations can exceed it when a launch's end timestamp overlaps the next
 launch's start (AQL completion-signal latency).  Compares both with the line's ms_per_step."""
 import csv
+import gzip
 import glob
 import json
 import os
@@ -21,8 +22,8 @@ import numpy as np
 def main():
     tdir, log, dst = sys.argv[1:4]
     rows = []
-    for f in glob.glob(os.path.join(tdir, "**", "*kernel_trace.csv"), recursive=True):
-        with open(f) as fh:
+    for f in glob.glob(os.path.join(tdir, "**", "*kernel_trace.csv"), recursive=True) + glob.glob(os.path.join(tdir, "**", "*kernel_trace.csv.gz"), recursive=True):
+        with (gzip.open(f, "rt") if f.endswith(".gz") else open(f)) as fh:
             rows += [r for r in csv.DictReader(fh)]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     sk = [r for r in rows if "sokoban_step_turn_kernel" in r["Kernel_Name"] and int(r["Grid_Size_X"]) == 8192]
@@ -30,8 +31,8 @@ def main():
     # runs of back-to-back turn launches: consecutive sokoban launches less than 50 us apart
     start = np.array([int(r["Start_Timestamp"]) for r in sk], np.int64)
     end = np.array([int(r["End_Timestamp"]) for r in sk], np.int64)
-    def kind_of(name):  # sokoban_step_turn_kernel<HW, M, LPE, kFin, kFirst>
-        m = re.search(r"sokoban_step_turn_kernel<[^>]*, (true|false), (true|false)>", name)
+    def kind_of(name):  # sokoban_step_turn_kernel<HW, M, LPE, kFin, kFirst, kLate>
+        m = re.search(r"sokoban_step_turn_kernel<[^>]*, (true|false), (true|false), (true|false)>", name)
         fin, first = (m.group(1) == "true", m.group(2) == "true") if m else (False, False)
         return "first" if first else "finalize" if fin else "plain"
     kind = [kind_of(r["Kernel_Name"]) for r in sk]
