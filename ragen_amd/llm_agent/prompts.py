@@ -207,17 +207,21 @@ class DevicePrompts:
         es = self.es
         self.rollout = es.rollout_id
         self.turns_done = 0
-        texts = []
-        for tg in es.tags:
-            texts += [tg.batch.render(i) for i in range(tg.hi - tg.lo)] if not hasattr(tg.batch, "render_rows") else \
-                [""] * (tg.hi - tg.lo)
-        bs = [t.encode("utf-8") for t in texts]
-        st = max(4, (max(len(x) for x in bs) + 3) // 4 * 4)
+        # the reset text of the tags without a device render, as host rows (the others' rows stay
+        # empty: their observation comes from render_rows)
+        host_tags = [tg for tg in es.tags if not hasattr(tg.batch, "render_rows")]
+        lens = np.zeros(self.n_envs, np.int32)
+        rows = []
+        for tg in host_tags:
+            for i in range(tg.hi - tg.lo):
+                b = tg.batch.render(i).encode("utf-8")
+                rows.append((tg.lo - es.env_lo + i, b))
+                lens[tg.lo - es.env_lo + i] = len(b)
+        st = max(4, (int(lens.max()) + 3) // 4 * 4)
         buf = np.zeros((self.n_envs, st), np.uint8)
-        for i, x in enumerate(bs):
-            buf[i, :len(x)] = np.frombuffer(x, np.uint8)
-        self._reset_obs = (torch.from_numpy(buf).to(self.device),
-                           torch.tensor([len(x) for x in bs], dtype=torch.int32, device=self.device))
+        for e, b in rows:
+            buf[e, :len(b)] = np.frombuffer(b, np.uint8)
+        self._reset_obs = (torch.from_numpy(buf).to(self.device), torch.from_numpy(lens).to(self.device))
         obs, obs_len = self._obs({j: tg.batch.render_rows() for j, tg in enumerate(es.tags)
                                   if hasattr(tg.batch, "render_rows")})
         ints = self.mapt.clone()
