@@ -57,7 +57,7 @@ __device__ void cascade(uint8_t* buf, int& a, int& z) {
   }
 }
 
-__global__ __launch_bounds__(64) void prompt_text_kernel(rmi_prompt_t P, int64_t B, uint8_t* __restrict__ out,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void prompt_text_kernel(rmi_prompt_t P, int64_t B, uint8_t* __restrict__ out,
                                                          int stride, int32_t* __restrict__ out_len,
                                                          int32_t* __restrict__ mark, uint8_t* __restrict__ err) {
   extern __shared__ __align__(16) uint8_t smem[];
@@ -65,7 +65,11 @@ __global__ __launch_bounds__(64) void prompt_text_kernel(rmi_prompt_t P, int64_t
   uint8_t* th = row + stride + 64;             // think content, stride
   uint8_t* an = th + stride;                   // answer content + its re-joined form, 2 * stride + 64
   uint8_t* num = an + 2 * stride + 64;         // formatted number, 64
-  int* sh = reinterpret_cast<int*>(num + 64);  // lane 0 -> wave hand-off, 16 ints
+  int* sh = reinterpret_cast<int*>(num + 64);  // lane 0 -> wave hand-off, 16 ints; the split's
+                                               // piece bounds at sh + 16 / sh + 32 (K + 1 each)
+  char* scr = reinterpret_cast<char*>(sh + 48);  // the number formatter's digit scratch, 64
+  // (lane 0's formatting and split work in LDS, not in per-lane register arrays: the wave
+  // keeps a register budget that lets 8 waves share a SIMD)
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
   if (P.active && !P.active[b]) {
@@ -113,15 +117,14 @@ __global__ __launch_bounds__(64) void prompt_text_kernel(rmi_prompt_t P, int64_t
       case RMI_PT_INT:
       case RMI_PT_REWARD: {
         if (lane == 0) {
-          char tmp[48];
+          char* o = reinterpret_cast<char*>(num);
           int l;
           if (pc.kind == RMI_PT_INT) {
-            l = py_int_repr(P.ints[(int64_t)pc.a * B + b], tmp);
+            l = py_int_repr(P.ints[(int64_t)pc.a * B + b], o);
           } else {
             const double r = P.reward[b];
-            l = (P.reward_int && P.reward_int[b]) ? py_int_repr((int64_t)r, tmp) : py_float_repr(r, tmp);
+            l = (P.reward_int && P.reward_int[b]) ? py_int_repr((int64_t)r, o) : py_float_repr(r, o, scr);
           }
-          for (int i = 0; i < l; ++i) num[i] = (uint8_t)tmp[i];
           sh[0] = l;
         }
         wave_sync();
@@ -189,7 +192,7 @@ __global__ __launch_bounds__(64) void prompt_text_kernel(rmi_prompt_t P, int64_t
           // (a cascade can make new separators: then always counted)
           bool rejoin = false;
           if (any_lt || ncand + 1 > P.K) {
-            int n_act = 0, ps[RMI_PARSE_MAX_NAMES + 1], pe[RMI_PARSE_MAX_NAMES + 1];
+            int n_act = 0, *ps = sh + 16, *pe = sh + 32;
             int seg = a0, i = a0;
             while (n_act <= P.K) {
               bool m = i + P.sep_len <= a1;
@@ -351,8 +354,9 @@ RMI_API int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, i
       (need_obs && (!prog->obs || !prog->obs_len)) || (need_int && !prog->ints) || (need_rew && !prog->reward) ||
       (need_if && !prog->cond) || (need_tag && (!prog->tag_const || !prog->pool || prog->n_tags < 1)))
     return RMI_EINVAL;
-  // row (stride + 64) + think (stride) + answer and its re-joined form (2 * stride + 64) + number + hand-off
-  const size_t lds = (size_t)stride + 64 + (size_t)stride + 2 * (size_t)stride + 64 + 64 + 64;
+  // row (stride + 64) + think (stride) + answer and its re-joined form (2 * stride + 64) + number
+  // (64) + hand-off and piece bounds (48 ints) + digit scratch (64)
+  const size_t lds = (size_t)stride + 64 + (size_t)stride + 2 * (size_t)stride + 64 + 64 + 48 * 4 + 64;
   hipLaunchKernelGGL(prompt_text_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *prog, B, out,
                      (int)stride, out_len, mark, err);
   return launch_status();

@@ -7,6 +7,8 @@
 // the decimal point position is <= -4 or > 16 ("1e-05", "1.5e+16"), else fixed with ".0" added
 // to integral values ("10.0", "0.0001").
 //
+// A double-arithmetic fast path settles every value whose repr has at most 15 significant
+// digits (see py_float_repr); the rest takes the exact integer search.
 // Exact integer arithmetic: the rounding interval of x (the half-way points to its neighbours)
 // is scaled by 10^s and 2^K into 128-bit integers, and for n = 1, 2, ... the first n whose
 // n-digit grid has a point inside the interval gives the digits.  That needs
@@ -41,15 +43,22 @@ RMI_HD u128 shr_ceil(u128 a, int k) {
 }
 
 // Decimal digits of v (v > 0) into out, most significant first; -> count.
-RMI_HD int u128_digits(u128 v, char* out) {
-  char tmp[40];
+RMI_HD void reverse_chars(char* a, int n) {
+  for (int i = 0, j = n - 1; i < j; ++i, --j) {
+    const char t = a[i];
+    a[i] = a[j];
+    a[j] = t;
+  }
+}
+
+RMI_HD int u128_digits(u128 v, char* out) {  // (no local array: out may be LDS on the device)
   int n = 0;
   while (v) {
     const uint64_t lo = (uint64_t)(v % 10u);  // u128 % small constant: lowered without a division call
-    tmp[n++] = (char)('0' + lo);
+    out[n++] = (char)('0' + lo);
     v /= 10u;
   }
-  for (int i = 0; i < n; ++i) out[i] = tmp[n - 1 - i];
+  reverse_chars(out, n);
   return n;
 }
 
@@ -65,14 +74,13 @@ RMI_HD int py_int_repr(int64_t v, char* out) {
     out[n++] = '0';
     return n;
   }
-  char tmp[24];
   int k = 0;
   while (u) {
-    tmp[k++] = (char)('0' + u % 10u);
+    out[n + k++] = (char)('0' + u % 10u);
     u /= 10u;
   }
-  while (k) out[n++] = tmp[--k];
-  return n;
+  reverse_chars(out + n, k);
+  return n + k;
 }
 
 // Lay out digits d[0..nd) with the decimal point at position decpt as PyOS_double_to_string
@@ -112,7 +120,8 @@ RMI_HD int py_layout(bool neg, const char* d, int nd, int decpt, char* out) {
 }
 
 // repr(float(x)); -> length written to out (<= 32), or -1 outside 1e-5 <= |x| < 2^53.
-RMI_HD int py_float_repr(double x, char* out) {
+// scratch: >= 40 bytes for the digits (LDS on the device: no per-lane register array).
+RMI_HD int py_float_repr(double x, char* out, char* scratch) {
   const uint64_t bits = __builtin_bit_cast(uint64_t, x);
   const bool neg = bits >> 63;
   const int bexp = (int)((bits >> 52) & 0x7FF);
@@ -136,12 +145,50 @@ RMI_HD int py_float_repr(double x, char* out) {
   if (!(ax >= 1e-5 && ax < 9007199254740992.0)) return -1;
   const uint64_t f = frac | (1ull << 52);  // normal: |x| >= 1e-5
   const int e = bexp - 1075;               // |x| = f * 2^e
-  char d[40];
+  char* d = scratch;
   if (e >= 0) {  // 2^52 <= |x| < 2^53: an integer, alone in its rounding interval
     const int nd0 = u128_digits((u128)f << e, d);
     int nd = nd0;
     while (nd > 1 && d[nd - 1] == '0') --nd;
     return py_layout(neg, d, nd, nd0, out);
+  }
+  // Fast path, exact, for reprs of at most 15 significant digits (every reward RAGEN's envs
+  // produce): at scale 10^s the rounding interval of |x| is narrower than 10^15 * 2^-52 < 0.23,
+  // so at most one integer c lies in it, and float(c * 10^-s) is the IEEE quotient c / 10^s
+  // (or product c * 10^-s): c < 2^53 and 10^|s| <= 10^22 are exact doubles and the operation
+  // is correctly rounded.  The scales are tried upward from the one where c first reaches 1,
+  // so the first hit has the fewest digits.  Anything else takes the exact search below.
+  {
+    int D0 = 0;  // floor(log10 |x|), possibly off by one: only where the scan starts
+    for (double t = ax; t >= 10.0; t /= 10.0) ++D0;
+    for (double t = ax; t < 1.0; t *= 10.0) --D0;
+    int s = -D0 - 1;  // in [-16, 4] over the supported range
+    double pw = 1.0;  // 10^|s|, exact (every power of ten up to 10^22 is a double)
+    for (int i = 0; i < (s < 0 ? -s : s); ++i) pw *= 10.0;
+    for (; s <= 22; pw = s >= 0 ? pw * 10.0 : pw / 10.0, ++s) {
+      const double y = s >= 0 ? ax * pw : ax / pw;
+      if (y >= 1e15) break;  // more than 15 digits
+      const double m = __builtin_rint(y);
+      int hits = 0;
+      double hit = 0.0;
+      for (int dm = -1; dm <= 1; ++dm) {
+        const double c = m + dm;
+        if (c < 1.0) continue;
+        if ((s >= 0 ? c / pw : c * pw) == ax) {
+          ++hits;
+          hit = c;
+        }
+      }
+      if (hits > 1) break;
+      if (hits == 1) {
+        int k = 0;
+        for (uint64_t u = (uint64_t)hit; u; u /= 10u) d[k++] = (char)('0' + u % 10u);
+        reverse_chars(d, k);
+        const int decpt = k - s;
+        while (k > 1 && d[k - 1] == '0') --k;
+        return py_layout(neg, d, k, decpt, out);
+      }
+    }
   }
   // |x| = V / 2^K with V = 4f; interval [(4f - dl) / 2^K, (4f + 2) / 2^K], closed iff f even
   const int K = 2 - e;

@@ -15,9 +15,9 @@ int main(int argc, char** argv) {
   std::fclose(f);
   std::FILE* o = std::fopen(argv[2], "w");
   if (!o) return 2;
-  char buf[64];
+  char buf[64], scratch[64];
   for (double v : xs) {
-    const int n = rmi::py_float_repr(v, buf);
+    const int n = rmi::py_float_repr(v, buf, scratch);
     if (n < 0) {
       std::fputs("?\n", o);
     } else {
