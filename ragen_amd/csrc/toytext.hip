@@ -80,7 +80,8 @@ struct FrozenLakeDev {
 //    turn is chain state number `exec`;
 //  * categorical_sample's argmax(cumsum(p) > u) with u = (x >> 11) * 2^-53 compares the 53-bit
 //    integer against ceil(cs_i * 2^53) (exact: cs_i * 2^53 is an exact double);
-//  * rows and columns are s >> 2 and s & 3.
+//  * each step is a 16-cell transition table (4 bits per cell) built from its draw and action
+//    alone, so the turn's dependent chain is one table lookup per step (see fl4_turn).
 // Same results bit for bit as the generic turn (FrozenLakeDev::step); taken when every lane
 // of the wave has a 4x4 map, a state in range and action ids in 0..4.
 struct Fl4Out {
@@ -99,8 +100,6 @@ __device__ __forceinline__ uint64_t pcg_out(uint64_t hi, uint64_t lo) {
   const unsigned rot = (unsigned)(hi >> 58);
   return (x >> rot) | (x << ((64u - rot) & 63u));
 }
-
-constexpr uint64_t kFl4Allow = 0x9ddcbffebffe3776ull;
 
 template <int K>
 __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, Pcg64 rng, uint64_t acts, int n_act,
@@ -142,37 +141,55 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
   __builtin_amdgcn_s_waitcnt(0);
   r.t_draws = __builtin_amdgcn_s_memtime();
 #endif
-  uint32_t stop = 0;
-  int ex = 0;
+  // Step k's transition is a map of the 16 cells, fixed once the draw and the action are known:
+  // a terminal cell stays, any other moves by direction b_k (a wall keeps it).  Its table
+  // (4 bits per cell) is built for every k at once — b_k depends on the draw and the action
+  // only, not on the cell — so the dependent chain of the turn is one shift and mask per step:
+  // s_{k+1} = table_k[s_k].  The steps' outputs are then read off the chain (the steps run
+  // while k < n_try and until the first done, exactly the loop's `go`).
+  const uint64_t kMove[4] = {0xedcca98865442100ull, 0xfedcfedcba987654ull,  // LEFT, DOWN
+                             0xffedbba977653321ull, 0xba98765432103210ull}; // RIGHT, UP
+  const uint32_t term16 = hole | goal;
+  uint64_t tm = term16;  // bit j -> nibble j all ones
+  tm = (tm | (tm << 24)) & 0x000000FF000000FFull;
+  tm = (tm | (tm << 12)) & 0x000F000F000F000Full;
+  tm = (tm | (tm << 6)) & 0x0303030303030303ull;
+  tm = (tm | (tm << 3)) & 0x1111111111111111ull;
+  tm *= 0xFull;
+  const uint64_t stay = 0xfedcba9876543210ull & tm;
+  uint64_t chain = (uint64_t)s;  // nibble k = the cell before step k
+  uint32_t done_m = 0, rw_m = 0, eff_m = 0, g_m = 0;
+  int cur = s;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    // 0/1 words and bitwise operators throughout: a short-circuit && / || here compiles to a
-    // divergent branch per step
-    const uint32_t go = (uint32_t)(k < n_try) & (stop ^ 1u);
-    const int ga = (int)((cl >> (8 * k)) & 0xFF) - 1;  // gym action 0..3 (LEFT, DOWN, RIGHT, UP)
+    const int ga = (int)((cl >> (8 * k)) & 0xFF) - 1;  // gym action 0..3 (a step past the list is never used)
     const uint64_t u = draw[k];
-    const uint32_t term = ((hole | goal) >> s) & 1u;
     const int i = (u < t0) ? 0 : (u < t1) ? 1 : (u < t2) ? 2 : 0;
-    const int b = (slippery ? ga + 3 + i : ga) & 3;  // & 3: a step past the exec list (ga = -1) is discarded
-    // branch-free move: bit 4s + b of kFl4Allow = the move stays on the board (LEFT col > 0,
-    // DOWN row < 3, RIGHT col < 3, UP row > 0); the deltas -1 / +4 / +1 / -4 as packed bytes
-    const uint32_t moves = (term ^ 1u) & (uint32_t)((kFl4Allow >> (4 * s + b)) & 1ull);
-    const int ns = s + (moves ? (int)(int8_t)(uint8_t)(0xFC0104FFu >> (8 * b)) : 0);
-    const uint32_t g = (goal >> ns) & 1u, h = (hole >> ns) & 1u;
-    const double rw = ((term ^ 1u) & g) ? 1.0 : 0.0;
-    const uint32_t done = term | g | h;
-    const uint32_t eff = (uint32_t)(ns != s);
-    r.o.acc = go ? r.o.acc + rw : r.o.acc;
-    r.o.info = go ? (uint8_t)(RMI_INFO_PRESENT | RMI_INFO_VALID | (eff << 1) | (g << 3)) : r.o.info;
-    r.succ_last = go ? (bool)g : r.succ_last;
-    r.turn_done = go ? (bool)done : r.turn_done;
-    s = go ? ns : s;
-    ex += (int)go;
-    stop |= go & done;
+    const int b = (slippery ? ga + 3 + i : ga) & 3;
+    const uint64_t table = (kMove[b] & ~tm) | stay;
+    const int ns = (int)((table >> (4 * cur)) & 0xFull);
+    const uint32_t term = (term16 >> cur) & 1u, g = (goal >> ns) & 1u, h = (hole >> ns) & 1u;
+    done_m |= (term | g | h) << k;
+    rw_m |= ((term ^ 1u) & g) << k;
+    eff_m |= (uint32_t)(ns != cur) << k;
+    g_m |= g << k;
+    cur = ns;
+    chain |= (uint64_t)ns << (4 * (k + 1));
   }
+  // executed steps: the first n_try, cut after the first done
+  const int first_done = __builtin_ctz(done_m | (1u << K));
+  const int ex = n_try < first_done + 1 ? n_try : first_done + 1;
+  const uint32_t ran = (1u << ex) - 1u;
+  const int last = ex - 1;
+  // the reward sum: 0.0 / 1.0 terms added in order from +0.0 are exact, so it is their count
+  r.o.acc = (double)__builtin_popcount(rw_m & ran);
+  const uint32_t eff = last >= 0 ? (eff_m >> last) & 1u : 0u, gl = last >= 0 ? (g_m >> last) & 1u : 0u;
+  r.o.info = ex ? (uint8_t)(RMI_INFO_PRESENT | RMI_INFO_VALID | (eff << 1) | (gl << 3)) : (uint8_t)0;
+  r.succ_last = ex && gl;
+  r.turn_done = ex && ((done_m >> last) & 1u);
   r.o.exec = (uint8_t)ex;
   r.o.stepped_any_state = ex > 0;
-  r.s = s;
+  r.s = (int)((chain >> (4 * ex)) & 0xFull);
   r.rng = rng;
 #pragma unroll
   for (int k = 1; k <= K; ++k)
@@ -180,7 +197,6 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
       r.rng.s_hi = shi[k];
       r.rng.s_lo = slo[k];
     }
-  r.o.info = ex ? r.o.info : 0;
   return r;
 }
 

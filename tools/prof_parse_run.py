@@ -1,4 +1,4 @@
-"""Driver for PMC passes over rmi_parse_actions / rmi_detokenize / rmi_sokoban_render
+"""Driver for PMC passes over rmi_parse_actions / rmi_detokenize / rmi_detok_parse
 (8192 SK-shaped rows, 20 launches each)."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -17,8 +17,10 @@ table, skip = synthetic.byte_vocab()
 vt = ops.VocabTable.from_bytes(table, skip, dev)
 tok = torch.from_numpy(synthetic.tokenize_greedy(texts, table)).to(dev)
 dec = ops.detokenize(tok, vt, buf.shape[1])
+fused = ops.detok_parse(tok, vt, buf.shape[1], cfg)
 for _ in range(20):
     ops.parse_actions(cfg, text, tl, out=out)
     ops.detokenize(tok, vt, buf.shape[1], out=dec)
+    ops.detok_parse(tok, vt, buf.shape[1], cfg, out=fused)
 torch.cuda.synchronize()
 print("ok")
