@@ -26,6 +26,8 @@
 #include "common.hpp"
 #include "text.hpp"
 
+#include <stdlib.h>
+
 namespace rmi {
 namespace {
 
@@ -877,6 +879,357 @@ __global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(
   PSTAMP_FLUSH();
 }
 
+// ============================================================ four responses per wave
+// The one-response-per-wave parse is VALU-issue-bound at full occupancy (≈750 VALU + 460 SALU
+// per response; tools/parse_pmc.sh), and most of its steps keep a few lanes busy: a handful of
+// '<' events, four or five action pieces, ballots whose answer one lane reads.  Here a wave
+// parses FOUR responses, one per 16-lane DPP row ("segment"): the byte passes cover 64 bytes
+// per step instead of 256, and every other step serves four responses per instruction.  The
+// control flow of each step is per segment; cross-lane operations (ballots, row scans,
+// bpermute reads) run with every lane active, each segment reading its own 16-bit field.  The
+// rare special-token replace cascade runs the wave-wide code on one row at a time.  Results
+// are those of parse_row, bit for bit (the same steps on the same bytes).
+constexpr int kSegRows = 4;  // responses per wave
+
+__device__ __forceinline__ int seg_scan(int x) {  // inclusive prefix sum inside each 16-lane row
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  return x;
+}
+// the value of lane 15 of this lane's row (ds_swizzle bitmask mode: and 0x10, or 0x0F)
+__device__ __forceinline__ int seg_last(int x) { return __builtin_amdgcn_ds_swizzle(x, 0x1F0); }
+__device__ __forceinline__ uint32_t seg_field(uint64_t m, int r) { return (uint32_t)(m >> (16 * r)) & 0xFFFFu; }
+// lane j of this lane's row (every lane must execute it)
+__device__ __forceinline__ int seg_read(int v, int r, int j) { return __shfl(v, (r << 4) | j, 64); }
+
+// collect() per segment: positions x in [from, to) with B[x] == ch, ascending, into list
+// (16 lanes x 4 bytes per step); -> the row's count (on each of its lanes)
+__device__ int seg_collect(const uint8_t* B, int from, int to, uint32_t ch, uint16_t* list, int l) {
+  int cnt = 0;
+  const uint32_t rep = ch * 0x01010101u;
+  for (int c = from & ~3;; c += 64) {
+    if (!__any(c < to)) break;
+    const int i0 = c + 4 * l;
+    uint32_t m4 = 0;
+    if (c < to && i0 < to) {
+      const uint32_t x = *reinterpret_cast<const uint32_t*>(B + i0) ^ rep;  // zero byte where B == ch
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = i0 + j;
+        const bool hit = ((x >> (8 * j)) & 0xFFu) == 0;
+        if (hit && p >= from && p < to) m4 |= 1u << j;
+      }
+    }
+    const int k = __builtin_popcount(m4);
+    const int incl = seg_scan(k);
+    int o = cnt + incl - k;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (m4 & (1u << j)) list[o++] = (uint16_t)(i0 + j);
+    cnt += seg_last(incl);
+  }
+  return cnt;
+}
+
+// next_event() per segment: the first classified event with id == want (< 0: any tag) at a
+// position in [from, lim) of the rows that ask (act), else -1
+__device__ int seg_next_event(const uint16_t* EL, int n, int want, int from, int lim, bool act, int r, int l) {
+  int res = -1;
+  bool open = act;
+  for (int c = 0;; c += 16) {
+    if (c >= n) open = false;
+    if (!__any(open)) break;
+    const int i = c + l;
+    bool hit = false;
+    int p = 0;
+    if (open && i < n) {  // packed: position | tag id << 12
+      const int ev = EL[i];
+      p = ev & 0xFFF;
+      const int id = ev >> 12;
+      hit = p >= from && p < lim && (want < 0 ? id != E_NONE : id == want);
+    }
+    const uint32_t f = seg_field(__ballot(hit), r);
+    const int q = seg_read(p, r, f ? __builtin_ctz(f) : 0);
+    if (open && f) {
+      res = q;
+      open = false;
+    }
+  }
+  return res;
+}
+
+// piece_id with the lookup column chosen per lane (Bandit's per-env ids): the names are
+// wave-uniform, only the id differs between the columns
+__device__ int piece_id_col(const uint8_t* B, int s, int e, const Names& nm0, const Names& nm1, bool col) {
+  return col ? piece_id(B, s, e, nm1) : piece_id(B, s, e, nm0);
+}
+
+struct SegLds {  // one row's LDS: the prefixed text and its list (events, then separators)
+  uint8_t* T;
+  uint16_t* EL;
+};
+// per row: T row | EL u16[cap]; per wave: 4 rows, then the shared cascade row and the cascade's
+// position list and coverage bytes (the cascade runs on one row at a time)
+__host__ __device__ constexpr size_t seg_row_lds(int stride) {
+  return ((size_t)row_bytes(stride) + 2 * (size_t)list_cap(stride) + 7) & ~(size_t)7;
+}
+__host__ __device__ constexpr size_t seg_wave_lds(int stride) {
+  return (kSegRows * seg_row_lds(stride) + (size_t)row_bytes(stride) + 3 * (size_t)list_cap(stride) + 7) &
+         ~(size_t)7;
+}
+constexpr int kSegMaxStride = 4000;  // event positions packed in 12 bits (kPre + stride < 4096)
+__device__ __forceinline__ SegLds seg_row(uint8_t* wave_lds, int stride, int r) {
+  uint8_t* base = wave_lds + r * seg_row_lds(stride);
+  SegLds L;
+  L.T = base + 4;
+  L.EL = reinterpret_cast<uint16_t*>(base + row_bytes(stride));
+  return L;
+}
+struct SegShared {  // the wave's cascade buffers
+  uint8_t* Wb;
+  uint16_t* lst;
+  uint8_t* cov;
+};
+__device__ __forceinline__ SegShared seg_shared(uint8_t* wave_lds, int stride) {
+  uint8_t* base = wave_lds + kSegRows * seg_row_lds(stride);
+  SegShared S;
+  S.Wb = base + 4;
+  S.lst = reinterpret_cast<uint16_t*>(base + row_bytes(stride));
+  S.cov = reinterpret_cast<uint8_t*>(S.lst + list_cap(stride));
+  return S;
+}
+
+// The four responses of a wave, staged (row r's len bytes at seg_row(r).T + kPre): parse_row's
+// steps per segment.  live: the row exists; err: bits already set for the row.
+__device__ void parse_rows4(const ParseArgs& a, uint8_t* wave_lds, int64_t b, bool live, int len, uint8_t err,
+                            const Names& nm0, const Names& nm1, bool col, int lane) {
+  const rmi_parse_cfg_t& cfg = a.cfg;
+  const int K = cfg.K;
+  const int r = lane >> 4, l = lane & 15;
+  const SegLds L = seg_row(wave_lds, a.stride, r);
+  uint8_t* T = L.T;
+  const SegShared S = seg_shared(wave_lds, a.stride);
+  const Tag pre = cfg.enable_think ? kThinkOpen : kAnsOpen;
+  const int plen = cfg.prepend ? pre.n : 0;
+  const int base = kPre - plen, n_end = kPre + len;
+  wave_sync();
+  for (int i = l; i < kTail; i += 16) T[n_end + i] = 0;
+  if (l < 4 + kPre) T[l - 4] = (l - 4 >= base) ? tag_byte(pre, l - 4 - base) : 0;
+  wave_sync();
+
+  // ---- 1. '<' events, classified
+  const int n_ev = seg_collect(T, base, n_end, '<', L.EL, l);
+  wave_sync();
+  for (int i = l; i < n_ev; i += 16) {
+    const int p = L.EL[i];
+    L.EL[i] = (uint16_t)(p | (classify_tag(T, p) << 12));
+  }
+  wave_sync();
+
+  // ---- 2. the regex (see parse_row)
+  int ts = -1, te = -1, as = -1, ae = -1;
+  if (cfg.enable_think) {
+    const int i = seg_next_event(L.EL, n_ev, E_THINK_O, base, n_end, live, r, l);
+    bool go = live && i >= 0, found = false;
+    int j = i + kThinkOpen.n, k = -1;
+    while (__any(go)) {
+      const int jj = seg_next_event(L.EL, n_ev, E_THINK_C, j, n_end, go, r, l);
+      if (go && jj < 0) go = false;
+      if (go) {
+        j = jj;
+        k = j + kThinkClose.n;
+        for (int w; (w = ws_fwd(T, k, n_end)) != 0;) k += w;  // \s* is greedy and '<' is no space
+      }
+      const bool lt = go && T[k] == '<';
+      const int ao = seg_next_event(L.EL, n_ev, E_ANS_O, k, k + 1, lt, r, l);
+      if (lt && ao == k) {
+        found = true;
+        go = false;
+      } else if (go) {
+        ++j;
+      }
+    }
+    const int e = seg_next_event(L.EL, n_ev, E_ANS_C, k + kAnsOpen.n, n_end, found, r, l);
+    if (found && e >= 0) {
+      ts = i + kThinkOpen.n;
+      te = j;
+      as = k + kAnsOpen.n;
+      ae = e;
+    }
+  } else {
+    const int i = seg_next_event(L.EL, n_ev, E_ANS_O, base, n_end, live, r, l);
+    const int e = seg_next_event(L.EL, n_ev, E_ANS_C, i + kAnsOpen.n, n_end, live && i >= 0, r, l);
+    if (live && i >= 0 && e >= 0) {
+      as = i + kAnsOpen.n;
+      ae = e;
+    }
+  }
+
+  // ---- 3. the replace cascade + strip of the action content
+  int ca = 0, cz = 0;
+  const bool has = as >= 0;
+  if (has) {
+    ca = as;
+    cz = ae;
+  }
+  const bool need = seg_next_event(L.EL, n_ev, -1, ca, cz, has, r, l) >= 0;
+  if (has && !need) strip(T, ca, cz);  // every replace is a no-op, and strip() six times is strip() once
+  const uint64_t needm = __ballot(need && l == 0);
+  for (int rr = 0; rr < kSegRows; ++rr) {
+    if (!((needm >> (16 * rr)) & 1ull)) continue;  // wave-uniform: the whole wave on row rr
+    const SegLds R = seg_row(wave_lds, a.stride, rr);
+    int a0 = __builtin_amdgcn_readlane(ca, 16 * rr), z0 = __builtin_amdgcn_readlane(cz, 16 * rr);
+    uint8_t* C = R.T;
+    for (int q = 0; q < 6; ++q) {  // ctx_manager.py:94 order
+      const Tag tok = q == 0 ? kThinkOpen : q == 1 ? kThinkClose : q == 2 ? kAnsOpen
+                    : q == 3 ? kAnsClose : q == 4 ? kImStart : kImEnd;
+      uint8_t* other = C == R.T ? S.Wb : R.T;
+      C = replace_strip_wave(C, other, S.lst, S.cov, a0, z0, tok, lane);
+      strip(C, a0, z0);
+    }
+    if (C != R.T) {  // back into the row (the shared cascade row serves the next one)
+      wave_sync();
+      for (int x = a0 + lane; x < z0; x += 64) R.T[x] = C[x];
+      if (lane < kTail) R.T[z0 + lane] = 0;
+    }
+    wave_sync();
+    if (r == rr) {
+      ca = a0;
+      cz = z0;
+    }
+  }
+
+  // ---- 4. split(action_sep), strip, drop empties, cap at K; name -> id
+  const Tag sep{cfg.sep_lo, cfg.sep_hi, cfg.sep_len};
+  int count = 0;
+  // candidates -> EL (the events are no longer needed), then the selected ones compacted in
+  // place: a chunk's candidates are read before any of its selections is written, and the
+  // selections so far never outnumber the candidates read
+  const int nc = seg_collect(T, has ? ca : 0, has ? cz : 0, (uint32_t)(sep.lo & 0xFFu), L.EL, l);
+  wave_sync();
+  int ns = 0, last = ca;
+  for (int c = 0;; c += 16) {
+    const bool more = c < nc;
+    if (!__any(more)) break;
+    const int i = c + l;
+    bool m = false;
+    int p = 0;
+    if (more && i < nc) {
+      p = L.EL[i];
+      uint64_t lo, hi;
+      load16(T, p, lo, hi);
+      m = p + sep.n <= cz && tag_eq(lo, hi, sep);
+    }
+    uint32_t bits = seg_field(__ballot(m), r);
+    while (__any(bits != 0)) {  // left to right, non-overlapping (str.split); rows in step
+      const int q = seg_read(p, r, bits ? __builtin_ctz(bits) : 0);
+      if (bits) {
+        bits &= bits - 1;
+        if (q >= last) {
+          if (l == 0) L.EL[ns] = (uint16_t)q;
+          ++ns;
+          last = q + sep.n;
+        }
+      }
+    }
+  }
+  wave_sync();
+  uint8_t perr = 0;
+  for (int c = 0;; c += 16) {
+    const bool more = has && c <= ns && count < K;
+    if (!__any(more)) break;
+    const int i = c + l;
+    int s0 = 0, e0 = 0;
+    if (more && i <= ns) {
+      s0 = i ? L.EL[i - 1] + sep.n : ca;
+      e0 = i < ns ? L.EL[i] : cz;
+      strip(T, s0, e0);
+    }
+    const bool keep = more && e0 > s0;
+    const uint32_t km = seg_field(__ballot(keep), r);
+    const int slot = count + __builtin_popcount(km & ((1u << l) - 1u));
+    if (keep && slot < K) {
+      a.actions[b * K + slot] = (int8_t)(nm0.n > 0 ? piece_id_col(T, s0, e0, nm0, nm1, col) : 1);
+      if (a.action_text) {
+        const int Ln = e0 - s0, Lc = Ln < a.Lact ? Ln : a.Lact;
+        uint8_t* dst = a.action_text + (b * K + slot) * (int64_t)a.Lact;
+        for (int q = 0; q < Lc; ++q) dst[q] = T[s0 + q];
+        a.action_len[b * K + slot] = Lc;
+        if (Ln > a.Lact) perr |= RMI_ERR_UNSUP;
+      }
+    }
+    if (more) count += __builtin_popcount(km);
+  }
+  if (count > K) count = K;
+  if (live && l >= count && l < K) {
+    a.actions[b * K + l] = 0;
+    if (a.action_text) a.action_len[b * K + l] = 0;
+  }
+  const uint8_t err_all = err | (seg_field(__ballot(perr != 0), r) ? (uint8_t)RMI_ERR_UNSUP : (uint8_t)0);
+  if (live && l == 0) {
+    a.n_actions[b] = (uint8_t)count;
+    if (a.spans) {
+      a.spans[4 * b + 0] = ts < 0 ? -1 : ts - base;
+      a.spans[4 * b + 1] = te < 0 ? -1 : te - base;
+      a.spans[4 * b + 2] = as < 0 ? -1 : as - base;
+      a.spans[4 * b + 3] = ae < 0 ? -1 : ae - base;
+    }
+    if (err_all && a.err) a.err[b] |= err_all;
+  }
+}
+
+__device__ __forceinline__ void load_names2(const rmi_parse_cfg_t& cfg, Names& nm0, Names& nm1) {
+  nm0 = load_names(cfg, 0);
+  nm1 = load_names(cfg, 1);
+}
+
+__global__ __launch_bounds__(64 * kRowWaves) __attribute__((amdgpu_waves_per_eu(8))) void parse4_kernel(ParseArgs a) {
+  extern __shared__ uint64_t lds_q[];
+  const int wv = threadIdx.x >> 6;
+  uint8_t* wl = reinterpret_cast<uint8_t*>(lds_q) + wv * seg_wave_lds(a.stride);
+  const int lane = threadIdx.x & 63, r = lane >> 4, l = lane & 15;
+  const int64_t w = (int64_t)blockIdx.x * (blockDim.x >> 6) + wv;
+  if (w * kSegRows >= a.B) return;  // the whole wave
+  const int64_t b = w * kSegRows + r;
+  const bool live = b < a.B;
+  const int64_t bc = live ? b : a.B - 1;
+  const SegLds L = seg_row(wl, a.stride, r);
+  int len = a.text_len[bc];
+  uint8_t err = 0;
+  if (len < 0 || len > a.stride) {
+    err |= RMI_ERR_STATE;
+    len = 0;
+  }
+  if (!live) len = 0;
+  Names nm0, nm1;
+  load_names2(a.cfg, nm0, nm1);
+  const bool col = live && a.sel && a.sel[b];
+  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(a.text + bc * a.stride);
+  uint32_t* d4 = reinterpret_cast<uint32_t*>(L.T + kPre);
+  for (int i = l; i < (len + 3) >> 2; i += 16) d4[i] = s4[i];
+  parse_rows4(a, wl, b, live, len, err, nm0, nm1, col, lane);
+}
+
+}  // namespace
+}  // namespace rmi
+
+namespace rmi {
+namespace {
+// rmi_parse_actions takes the four-responses-per-wave kernel for rows whose LDS (4 rows + the
+// cascade row) fits 48 KB per wave; RAGEN_AMD_PARSE1=1 forces the one-response-per-wave kernel
+// (A/B, tests).  The fused decode + parse keeps one response per wave: four decodes per wave
+// one after another measured 32.7 us against 24.7 us.
+bool use_seg(int stride) {
+  const char* e = getenv("RAGEN_AMD_PARSE1");
+  if (e && e[0] == '1') return false;
+  return stride <= kSegMaxStride && seg_wave_lds(stride) <= 48 * 1024;
+}
+int seg_waves_per_group(int stride) {
+  const size_t n = kWgLds / seg_wave_lds(stride);
+  return n >= (size_t)kRowWaves ? kRowWaves : (n < 1 ? 1 : (int)n);
+}
 }  // namespace
 }  // namespace rmi
 
@@ -956,6 +1309,13 @@ RMI_API int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, c
   if (reinterpret_cast<uintptr_t>(text) & 3u) return RMI_EUNSUP;
   ParseArgs a{*cfg, text, text_len, B, (int)stride, sel, actions, n_actions, spans, action_text, action_len,
               (int)Lact, err};
+  if (use_seg(stride)) {
+    const int nw = seg_waves_per_group(stride);
+    const int64_t rows = (int64_t)nw * kSegRows;
+    hipLaunchKernelGGL(parse4_kernel, dim3((unsigned)((B + rows - 1) / rows)), dim3(64 * nw),
+                       seg_wave_lds(stride) * nw, as_stream(stream), a);
+    return launch_status();
+  }
   const int nw = row_waves(parse_lds(stride));
   const size_t shm = parse_lds(stride) * nw;
   hipLaunchKernelGGL(parse_kernel, dim3((unsigned)((B + nw - 1) / nw)), dim3(64 * nw), shm,

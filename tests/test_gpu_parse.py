@@ -50,8 +50,19 @@ def _check_rows(texts, out, think, K, sep, lookup, prepend=True):
         assert out["err"][b] == 0
 
 
+@pytest.fixture(params=["seg", "wave"])
+def kernel(request, monkeypatch):
+    """The four-responses-per-wave kernels (default for rows that fit) or, with
+    RAGEN_AMD_PARSE1=1, the one-response-per-wave kernels."""
+    if request.param == "wave":
+        monkeypatch.setenv("RAGEN_AMD_PARSE1", "1")
+    else:
+        monkeypatch.delenv("RAGEN_AMD_PARSE1", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("lookup_name", ["sokoban", "frozen_lake", "bandit", "kelvin", "none"])
-def test_parse_matches_reference_vectors(device, lookup_name):
+def test_parse_matches_reference_vectors(device, lookup_name, kernel):
     lookups, cases = _golden()
     lk = lookups[lookup_name]
     groups = {}
@@ -72,7 +83,7 @@ def test_parse_matches_reference_vectors(device, lookup_name):
         _check_rows(texts, out, think, K, sep, lk)
 
 
-def test_parse_bandit_per_env_lookup(device):
+def test_parse_bandit_per_env_lookup(device, kernel):
     """Bandit's action_lookup is per env (bandit/env.py:25-39): sel picks the id column."""
     lo, hi = {1: "Phoenix", 2: "Dragon"}, {1: "Dragon", 2: "Phoenix"}
     texts = ["x</think><answer>Dragon</answer>", "x</think><answer> phoenix </answer>",
@@ -84,7 +95,7 @@ def test_parse_bandit_per_env_lookup(device):
         assert list(out["actions"][b, :out["n_actions"][b]]) == P.action_ids(acts, hi if sel[b] else lo)
 
 
-def test_parse_full_batch_vs_oracle(device):
+def test_parse_full_batch_vs_oracle(device, kernel):
     """8192 SK-shaped responses (synthetic actions of the bench), with no-think prefix too."""
     ids, n = synthetic.rollout_actions(8192, 1, 5, 1, 4)
     for think in (True, False):
@@ -95,16 +106,59 @@ def test_parse_full_batch_vs_oracle(device):
         assert np.array_equal(out["actions"], ids[0])
 
 
-def test_parse_fuzz_and_edges(device):
+def test_parse_fuzz_and_edges(device, kernel):
     rng = random.Random(3)
     frags = ["<think>", "</think>", "<answer>", "</answer>", "<|im_end|>", "<|im_start|>", "|", "||", " ", "\n",
              "　", " ", "\xa0", "K", "Up", "down", "LEFT", "x", "é", "\U0001f600", "<", ">"]
-    texts = ["".join(rng.choice(frags) for _ in range(rng.randint(0, 40))) for _ in range(3000)]
-    texts += ["", "</think><answer>" + "Up || " * 1300 + "</answer>", "a" * 8000]
-    for think in (True, False):
-        for prepend in (True, False):
-            out = _run(texts, device, think, 5, "||", SOKOBAN, prepend=prepend)
-            _check_rows(texts, out, think, 5, "||", SOKOBAN, prepend=prepend)
+    texts = ["".join(rng.choice(frags) for _ in range(rng.randint(0, 40))) for _ in range(3001)]
+    # short rows (both kernels), then rows up to the parse limit (the one-response-per-wave kernel)
+    for batch in (texts + [""], texts + ["", "</think><answer>" + "Up || " * 1300 + "</answer>", "a" * 8000]):
+        for think in (True, False):
+            for prepend in (True, False):
+                out = _run(batch, device, think, 5, "||", SOKOBAN, prepend=prepend)
+                _check_rows(batch, out, think, 5, "||", SOKOBAN, prepend=prepend)
+
+
+def test_parse_seg_equals_wave(device, monkeypatch):
+    """The four-responses-per-wave kernel == the one-response-per-wave kernel on every output
+    (fuzz rows with every tag / separator / whitespace form, batch sizes not a multiple of 4,
+    the pass-through lookup with action text, Bandit's per-row column)."""
+    rng = random.Random(9)
+    frags2 = ["<think>", "</think>", "<answer>", "</answer>", "<|im_end|>", "<|im_start|>", "|", "||", " ", "\n",
+             "　", " ", "\xa0", "K", "Up", "down", "LEFT", "x", "é", "\U0001f600", "<", ">"]
+    frags2 += ["\t", "phoenix", "DRAGON", "|| Up ||"]
+    for B in (1, 3, 6, 1027):
+        texts = ["".join(rng.choice(frags2) for _ in range(rng.randint(0, 60))) for _ in range(B)]
+        buf, lens = synthetic.encode_rows(texts)
+        tb, tl = torch.from_numpy(buf).to(device), torch.from_numpy(lens).to(device)
+        sel = torch.from_numpy(np.array([rng.random() < 0.5 for _ in range(B)], np.uint8)).to(device)
+        for think in (True, False):
+            for cfg, lact, sl in ((ops.parse_config(think, 5, "||", SOKOBAN), 0, None),
+                                  (ops.parse_config(think, 3, "||", None), 24, None),
+                                  (ops.parse_config(think, 2, "||", {1: "Phoenix", 2: "Dragon"},
+                                                    {1: "Dragon", 2: "Phoenix"}), 0, sel)):
+                outs = []
+                for mode in ("seg", "wave"):
+                    if mode == "wave":
+                        monkeypatch.setenv("RAGEN_AMD_PARSE1", "1")
+                    else:
+                        monkeypatch.delenv("RAGEN_AMD_PARSE1", raising=False)
+                    outs.append(ops.parse_actions(cfg, tb, tl, sl, True, lact))
+                torch.cuda.synchronize()
+                a, w = outs
+                n = a["n_actions"].cpu().numpy()
+                assert torch.equal(a["n_actions"], w["n_actions"]) and torch.equal(a["spans"], w["spans"])
+                assert torch.equal(a["err"], w["err"])
+                aa, wa = a["actions"].cpu().numpy(), w["actions"].cpu().numpy()
+                for b in range(B):
+                    assert list(aa[b, :n[b]]) == list(wa[b, :n[b]]), (B, b, texts[b])
+                if lact:
+                    assert torch.equal(a["action_len"], w["action_len"])
+                    at, wt, al = a["action_text"].cpu().numpy(), w["action_text"].cpu().numpy(), \
+                        a["action_len"].cpu().numpy()
+                    for b in range(B):
+                        for k in range(n[b]):
+                            assert at[b, k, :al[b, k]].tobytes() == wt[b, k, :al[b, k]].tobytes()
 
 
 def test_parse_stride_envelope(device):
@@ -356,7 +410,7 @@ def _fused_vs_separate(device, ids, n_ids, vt, stride, cfg, sel=None, Lact=0):
     return fu
 
 
-def test_detok_parse_fused_on_reference_vectors(device):
+def test_detok_parse_fused_on_reference_vectors(device, kernel):
     """The 1530 recorded _parse_response vectors, tokenized over bytes + tag / name words,
     through the fused kernel == the separate kernels (themselves checked against the oracle
     above), every lookup, with action text for the pass-through lookup."""
@@ -387,7 +441,7 @@ def test_detok_parse_fused_on_reference_vectors(device):
                 assert n[b] == len(c["actions"]), c["text"]
 
 
-def test_detok_parse_fused_edges(device):
+def test_detok_parse_fused_edges(device, kernel):
     """Random vocabularies (long tokens past the inline 12 bytes, invalid UTF-8, skipped ids),
     out-of-range ids, ragged n_ids, rows truncated at the stride, Bandit's per-row id column,
     and rows at the parse row limit."""

@@ -12,4 +12,4 @@ for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
   timeout -s KILL 120 rocprofv3 --pmc $set --kernel-trace -d $OUT/pass$i -o pmc --output-format csv -- python3 tools/prof_parse_run.py > $OUT/pass$i.log 2>&1
   rc=$?; echo "pass$i rc=$rc" | tee -a $OUT/status.txt; [ $rc -ne 0 ] && exit $rc
 done
-python3 tools/pmc_per_wave.py $OUT parse_kernel detok_kernel detok_parse_kernel
+python3 tools/pmc_per_wave.py $OUT parse_kernel detok_kernel detok_parse_kernel parse4_kernel detok_parse4_kernel
