@@ -56,31 +56,51 @@ def all_reduce_max(x: torch.Tensor, group=None) -> torch.Tensor:
     return xs.to(x.device)
 
 
-def all_gather_rows(x: torch.Tensor, with_offset: bool = False, group=None):
+def shard_rows(n_groups: int, group_size: int, world_size: int):
+    """Every rank's row count under the group-aligned shard plan (shard_groups), in rank order:
+    known on every host without communication, so a gather given it needs no host sync."""
+    return [shard_groups(n_groups, world_size, r)[1] * group_size for r in range(world_size)]
+
+
+def all_gather_rows(x: torch.Tensor, with_offset: bool = False, group=None, sizes=None):
     """Concatenate every rank's [n_r, ...] rows in rank order (n_r may differ by rank).
     Whenever a process group exists the collective runs (also at world size 1, so the one-GPU
     tests exercise the RCCL path); without one the local rows are returned.
+    sizes: every rank's n_r in rank order when the caller knows them (e.g. ``shard_rows``): the
+    size exchange and its device -> host read are skipped, so the gather is stream-ordered.
+    Without it the sizes are all-gathered and read back (one host synchronisation).
     with_offset: -> (rows, this rank's first row in the result)."""
     if not initialized():
         return (x, 0) if with_offset else x
     W, rank = dist.get_world_size(group), dist.get_rank(group)
     xs = _staged(x.contiguous(), group)
-    n = torch.tensor([xs.shape[0]], dtype=torch.int64, device=xs.device)
-    sizes = [torch.zeros_like(n) for _ in range(W)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s) for s in torch.cat(sizes).cpu().tolist()]
+    if sizes is None:
+        n = torch.tensor([xs.shape[0]], dtype=torch.int64, device=xs.device)
+        gathered = [torch.zeros_like(n) for _ in range(W)]
+        dist.all_gather(gathered, n, group=group)
+        sizes = [int(s) for s in torch.cat(gathered).cpu().tolist()]
+    else:
+        sizes = [int(s) for s in sizes]
+        if len(sizes) != W or sizes[rank] != xs.shape[0]:
+            raise ValueError(f"sizes {sizes} do not match world size {W} / this rank's {xs.shape[0]} rows")
     m = max(sizes)
-    pad = torch.zeros((m,) + tuple(xs.shape[1:]), dtype=xs.dtype, device=xs.device)
-    pad[:xs.shape[0]] = xs
-    bufs = [torch.empty_like(pad) for _ in range(W)]
-    dist.all_gather(bufs, pad, group=group)
-    out = torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0).to(x.device)
+    if all(s == m for s in sizes):  # equal shards: one all-gather straight into the result
+        out = torch.empty((W * m,) + tuple(xs.shape[1:]), dtype=xs.dtype, device=xs.device)
+        dist.all_gather_into_tensor(out, xs, group=group)
+        out = out.to(x.device)
+    else:
+        pad = torch.zeros((m,) + tuple(xs.shape[1:]), dtype=xs.dtype, device=xs.device)
+        pad[:xs.shape[0]] = xs
+        bufs = [torch.empty_like(pad) for _ in range(W)]
+        dist.all_gather(bufs, pad, group=group)
+        out = torch.cat([b[:s] for b, s in zip(bufs, sizes)], dim=0).to(x.device)
     return (out, sum(sizes[:rank])) if with_offset else out
 
 
-def global_whiten_stats(row_stats: torch.Tensor, group=None) -> torch.Tensor:
-    """[n_local, 3] f64 (sum, sum_sq, count) -> [n_global, 3] in global row order."""
-    return all_gather_rows(row_stats, group=group)
+def global_whiten_stats(row_stats: torch.Tensor, group=None, sizes=None) -> torch.Tensor:
+    """[n_local, 3] f64 (sum, sum_sq, count) -> [n_global, 3] in global row order; with
+    ``sizes`` (every rank's row count) free of host synchronisation."""
+    return all_gather_rows(row_stats, group=group, sizes=sizes)
 
 
 def gather_group_scores(scores: torch.Tensor, group_size: int, with_offset: bool = False, group=None):
@@ -159,11 +179,12 @@ def left_pad(x: torch.Tensor, width: int, value) -> torch.Tensor:
     return out
 
 
-def gather_formulated(dp, pad_id: int, group=None):
+def gather_formulated(dp, pad_id: int, group=None, sizes=None):
     """Token-level reassembly of formulate_rollouts' batch over the ranks: the
     reference builds ONE left-padded batch (ctx_manager.py:278-306), so every rank pads its
     shard to the global width S (an all-reduce of max S), then the rows are all-gathered in
-    rank order — the global env order, since shards are contiguous.  Token tensors [B, S],
+    rank order — the global env order, since shards are contiguous (``sizes``: every rank's
+    row count when known, e.g. EnvStateManager.shard_sizes: no size exchange).  Token tensors [B, S],
     masks / scores [B, S-1]; responses = input_ids[:, 1:]; original_rm_scores keeps aliasing
     rm_scores.  env_ids / group_ids are gathered too (messages_list stays with its rank).
     -> a DataProto of the whole batch, identical on every rank."""
@@ -176,7 +197,7 @@ def gather_formulated(dp, pad_id: int, group=None):
     out = {}
     for k, (w, v) in spec.items():
         if k in b.keys():
-            out[k] = all_gather_rows(left_pad(b[k], w, v).contiguous(), group=group)
+            out[k] = all_gather_rows(left_pad(b[k], w, v).contiguous(), group=group, sizes=sizes)
     out["responses"] = out["input_ids"][:, 1:]
     if "original_rm_scores" in b.keys():
         out["original_rm_scores"] = out["rm_scores"]
@@ -184,5 +205,5 @@ def gather_formulated(dp, pad_id: int, group=None):
     for k in ("env_ids", "group_ids"):
         if k in dp.non_tensor_batch:
             loc = torch.tensor(np.asarray(dict.__getitem__(dp.non_tensor_batch, k), np.int64), device=ids.device)
-            nt[k] = np.array(all_gather_rows(loc, group=group).cpu().tolist(), dtype=object)
+            nt[k] = np.array(all_gather_rows(loc, group=group, sizes=sizes).cpu().tolist(), dtype=object)
     return DataProto(out, nt, dict(dp.meta_info))

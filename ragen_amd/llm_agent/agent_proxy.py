@@ -111,7 +111,7 @@ class LLMAgentProxy:
         if self.gather and self.process_group is not None:
             from .. import distributed as rd
             pad = self.tokenizer.pad_token_id if getattr(self.tokenizer, "pad_token_id", None) is not None else 0
-            out = rd.gather_formulated(out, pad, self.process_group)
+            out = rd.gather_formulated(out, pad, self.process_group, sizes=ctx.shard_sizes())
         # phase wall times of the last call (the turn loop is what env-steps/s is measured on)
         self.last_timing = {"reset_s": t1 - t0, "turns_s": t2 - t1, "rollout_states_s": t3 - t2,
                             "formulate_s": time.perf_counter() - t3}

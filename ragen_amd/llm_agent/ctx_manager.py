@@ -334,6 +334,12 @@ class ContextManager:
         self._prompts = None
         self._init_prefix_lookup()
 
+    def shard_sizes(self, tag: Optional[str] = None) -> List[int]:
+        """Every rank's env count (of ``tag``'s if given), rank order (es_manager.shard_sizes)."""
+        from .es_manager import shard_sizes
+        ec = self.es_cfg.env_configs
+        return shard_sizes(ec.n_groups, list(ec.tags), int(self.es_cfg.group_size), self.world_size, tag)
+
     def set_device_vocab(self, vocab: "ops.VocabTable"):
         """Turn on the device path: generations that arrive as token ids on the GPU are decoded by
         rmi_detokenize against this byte table (ops.VocabTable.from_tokenizer for a byte-level
@@ -632,7 +638,7 @@ class ContextManager:
         # the mean over the WHOLE batch (ctx_manager.py:305): every rank's row lengths, rank order
         row_resp = response_mask.sum(dim=-1).float()
         if self.process_group is not None and self.world_size > 1:
-            row_resp = rd.all_gather_rows(row_resp, group=self.process_group)
+            row_resp = rd.all_gather_rows(row_resp, group=self.process_group, sizes=self.shard_sizes())
         response_length = row_resp.mean().item()
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
                  "loss_mask": loss_mask, "rm_scores": normalized, "original_rm_scores": normalized}
@@ -668,8 +674,9 @@ class ContextManager:
                                                       NORM[rn.method])
         else:
             sharded = self.process_group is not None and self.world_size > 1
-            a_all = rd.all_gather_rows(acc, group=self.process_group) if sharded else acc
-            p_all = rd.all_gather_rows(pen.contiguous(), group=self.process_group) if sharded else pen
+            sz = self.shard_sizes() if sharded else None
+            a_all = rd.all_gather_rows(acc, group=self.process_group, sizes=sz) if sharded else acc
+            p_all = rd.all_gather_rows(pen.contiguous(), group=self.process_group, sizes=sz) if sharded else pen
             n_all = a_all.numel()
             if rn.grouping == "batch":
                 seg = np.array([0, n_all], np.int32)
@@ -695,7 +702,8 @@ class ContextManager:
         for tag in dict.fromkeys(self.es_cfg.env_configs.tags):  # every rank, same order (collectives)
             rows = local.get(tag, np.zeros((0, 5), np.float64))
             if sharded:
-                rows = rd.all_gather_rows(torch.from_numpy(rows).to(self.device), group=self.process_group).cpu().numpy()
+                rows = rd.all_gather_rows(torch.from_numpy(rows).to(self.device), group=self.process_group,
+                                          sizes=self.shard_sizes(tag)).cpu().numpy()
             if len(rows):
                 per_tag[tag] = [rows]
         metrics, nz = {}, []

@@ -123,6 +123,16 @@ def shard_plan(n_groups_per_tag, group_size, rank, world_size):
     return g0, ng, out
 
 
+def shard_sizes(n_groups_per_tag, tags, group_size, world_size, tag=None):
+    """Every rank's env count (of ``tag``'s envs if given) under shard_plan, in rank order:
+    host-known, so the collectives over the shards need no size exchange."""
+    out = []
+    for r in range(world_size):
+        _, ng, parts = shard_plan(list(n_groups_per_tag), group_size, r, world_size)
+        out.append(ng * group_size if tag is None else sum(hi - lo for j, lo, hi in parts if tags[j] == tag))
+    return out
+
+
 class EnvStateManager:
     def __init__(self, config, mode: str = "train", device=None, rank: Optional[int] = None,
                  world_size: Optional[int] = None, process_group=None):
@@ -178,6 +188,11 @@ class EnvStateManager:
                       "local": i - t.lo, "config": t.batch.config, "status": EnvStatus(),
                       "max_actions_per_traj": t.max_actions_per_traj}
                      for t in self.tags for i in range(t.lo, t.hi)]
+
+    def shard_sizes(self, tag: Optional[str] = None) -> List[int]:
+        """Every rank's env count (of ``tag``'s envs if given), rank order (shard_sizes)."""
+        return shard_sizes(self.config.env_configs.n_groups, self.config.env_configs.tags, self.group_size,
+                           self.world_size, tag)
 
     @property
     def rollout_cache(self):

@@ -25,12 +25,14 @@ def compute_response_mask(data: DataProto) -> torch.Tensor:
 
 
 def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_repeat=1, multi_turn=False,
-                      norm_adv_by_std_in_grpo=True, bi_level_gae=False, high_level_gamma=1.0, process_group=None):
+                      norm_adv_by_std_in_grpo=True, bi_level_gae=False, high_level_gamma=1.0, process_group=None,
+                      shard_rows=None):
     """agent_trainer.py:60-137: GAE (verl, or RAGEN's bi-level), GRPO, REINFORCE++ (and its
     baseline form), REMAX and RLOO, each on the engine's kernels; an unknown estimator raises
     NotImplementedError as the reference does.  ``process_group``: the batch is this rank's
-    shard and whitening uses the statistics of the whole sharded batch (core_algos)."""
-    pg = {"process_group": process_group}
+    shard and whitening uses the statistics of the whole sharded batch (core_algos); ``shard_rows``
+    (every rank's row count) makes that gather free of host synchronisation."""
+    pg = {"process_group": process_group, "shard_rows": shard_rows}
     if "response_mask" not in data.batch:
         data.batch["response_mask"] = compute_response_mask(data)
     est = getattr(adv_estimator, "value", adv_estimator)

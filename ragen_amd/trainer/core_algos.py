@@ -13,7 +13,9 @@ Batch-global whitening over a sharded batch is opt-in: ``process_group=<group>``
 rank all-gather the per-row fp64 partials and reduce them in global row order, so the shards
 whiten exactly like the whole batch; the error flags are then reduced over the group before
 anything is raised, so every rank raises together.  Without it the statistics are this
-process's rows only, whatever torch.distributed state exists.
+process's rows only, whatever torch.distributed state exists.  ``shard_rows=[n_0, .., n_W-1]``
+(every rank's row count, e.g. ``distributed.shard_rows`` of the shard plan) lets the gather skip
+its size exchange: with ``check=False`` a sharded estimator then never synchronises the host.
 """
 from collections import OrderedDict
 
@@ -36,11 +38,11 @@ def _dev(x, device):
     return x.to(device, non_blocking=True).contiguous()
 
 
-def _whiten(adv, mask, row_stats, group=None):
+def _whiten(adv, mask, row_stats, group=None, sizes=None):
     """In place; -> device status i32[1] (0 ok; 1 / 2 = verl's ValueError cases).  With a
     process group the statistics are the whole sharded batch's (opt-in, module docstring)."""
     if group is not None:
-        return torch.ops.ragen_amd.masked_whiten_stats_(adv, rd.global_whiten_stats(row_stats, group))
+        return torch.ops.ragen_amd.masked_whiten_stats_(adv, rd.global_whiten_stats(row_stats, group, sizes))
     return torch.ops.ragen_amd.masked_whiten_(adv, mask, row_stats)
 
 
@@ -71,7 +73,7 @@ def _back(out_device, tensors, status=None, err=None, check=True, group=None):
 
 
 def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = True, check: bool = True,
-                  process_group=None) -> torch.Tensor:
+                  process_group=None, shard_rows=None) -> torch.Tensor:
     """verl masked_whiten; ValueError for a mask sum of 0 or 1 like verl's masked_var."""
     if not shift_mean:
         raise NotImplementedError("shift_mean=False is not used by RAGEN")
@@ -79,12 +81,12 @@ def masked_whiten(values: torch.Tensor, mask: torch.Tensor, shift_mean: bool = T
     x = _dev(values.float(), dev).clone()
     m = _dev(mask, dev)
     stats = torch.ops.ragen_amd.whiten_row_stats(x, m)
-    status = _whiten(x, m, stats, process_group)
+    status = _whiten(x, m, stats, process_group, shard_rows)
     return _back(values.device, [x], status, check=check, group=process_group)[0]
 
 
 def compute_gae_advantage_return(token_level_rewards, values, response_mask, gamma, lam, variant="legacy",
-                                 check=True, process_group=None):
+                                 check=True, process_group=None, shard_rows=None):
     """verl compute_gae_advantage_return (legacy form by default)."""
     dev = _device(token_level_rewards, values, response_mask)
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(response_mask, dev)
@@ -92,19 +94,19 @@ def compute_gae_advantage_return(token_level_rewards, values, response_mask, gam
     if variant not in VARIANT:
         raise ValueError(f"GAE variant must be 'legacy' or 'masked', got {variant!r}")
     adv, ret = torch.ops.ragen_amd.gae(r, v, m, float(gamma), float(lam), VARIANT[variant], stats)
-    status = _whiten(adv, m, stats, process_group)
+    status = _whiten(adv, m, stats, process_group, shard_rows)
     return tuple(_back(token_level_rewards.device, [adv, ret], status, check=check, group=process_group))
 
 
 def compute_bi_level_gae_advantage_return(token_level_rewards, values, loss_mask, gamma, lam, high_level_gamma,
-                                          check=True, process_group=None):
+                                          check=True, process_group=None, shard_rows=None):
     """core_algos.py:4-92 (IndexError where the reference raises it, core_algos.py:79)."""
     dev = _device(token_level_rewards, values, loss_mask)
     r, v, m = _dev(token_level_rewards.float(), dev), _dev(values.float(), dev), _dev(loss_mask, dev)
     stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
     err = torch.empty(r.shape[0], dtype=torch.uint8, device=dev)
     adv, ret = torch.ops.ragen_amd.bilevel_gae(r, v, m, float(gamma), float(lam), float(high_level_gamma), stats, err)
-    status = _whiten(adv, m, stats, process_group)
+    status = _whiten(adv, m, stats, process_group, shard_rows)
     return tuple(_back(token_level_rewards.device, [adv, ret], status, err, check=check, group=process_group))
 
 
@@ -148,20 +150,21 @@ def compute_grpo_outcome_advantage(token_level_rewards, response_mask, index, ep
 # beyond that restatement (tests/verl_restated.py runs it on CPU torch as the checker).
 
 def compute_reinforce_plus_plus_outcome_advantage(token_level_rewards, response_mask, gamma, check=True,
-                                                  process_group=None):
+                                                  process_group=None, shard_rows=None):
     """verl: returns = right-to-left running = r + gamma * running, reset by the mask;
     advantages = masked_whiten(returns, mask) * mask."""
     dev = _device(token_level_rewards, response_mask)
     r, m = _dev(token_level_rewards.float(), dev), _dev(response_mask, dev)
     stats = torch.empty(r.shape[0], 3, dtype=torch.float64, device=dev)
     adv, ret = torch.ops.ragen_amd.reinforce_pp_returns(r, m, float(gamma), stats)
-    status = _whiten(adv, m, stats, process_group)
+    status = _whiten(adv, m, stats, process_group, shard_rows)
     torch.ops.ragen_amd.mask_mul_(adv, m)
     return tuple(_back(token_level_rewards.device, [adv, ret], status, check=check, group=process_group))
 
 
 def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, response_mask, index,
-                                                           epsilon: float = 1e-6, check=True, process_group=None):
+                                                           epsilon: float = 1e-6, check=True, process_group=None,
+                                                           shard_rows=None):
     """verl: score = sum_t r minus its group's mean (0 for a single-row group), tiled over the
     mask, then masked_whiten(., mask) * mask.  -> (adv, adv)."""
     dev = _device(token_level_rewards, response_mask)
@@ -169,7 +172,7 @@ def compute_reinforce_plus_plus_baseline_outcome_advantage(token_level_rewards, 
     adv = _grouped(r, m, index, dev, lambda rr, mm, seg: torch.ops.ragen_amd.grpo_outcome(
         rr, mm, seg, float(epsilon), False)[0])
     stats = torch.ops.ragen_amd.whiten_row_stats(adv, m)
-    status = _whiten(adv, m, stats, process_group)
+    status = _whiten(adv, m, stats, process_group, shard_rows)
     torch.ops.ragen_amd.mask_mul_(adv, m)
     adv = _back(token_level_rewards.device, [adv], status, check=check, group=process_group)[0]
     return adv, adv

@@ -54,6 +54,15 @@ def _worker(rank, world, port, q):
     out = _rollout(first, ng)
     scores = rd.gather_group_scores(torch.from_numpy(out["score"]), GS).numpy()
     stats = rd.global_whiten_stats(torch.from_numpy(out["stats"])).numpy()
+    # host-known shard sizes: no size exchange (equal shards: one all_gather_into_tensor)
+    sized = rd.global_whiten_stats(torch.from_numpy(out["stats"]), sizes=rd.shard_rows(G_TOTAL, GS, world)).numpy()
+    rag = torch.arange(rank + 3, dtype=torch.float64) + 100 * rank  # ragged: 3 and 4 rows
+    rag_sized, off = rd.all_gather_rows(rag, with_offset=True, sizes=[3 + r for r in range(world)])
+    try:
+        rd.all_gather_rows(rag, sizes=[4, 3])  # wrong on both ranks (a rank whose count matches would
+        bad = False                            # enter the collective and wait for the other)
+    except ValueError:
+        bad = True  # raised on the host before any collective
     traj = rd.gather_rollout({"turn_reward": torch.from_numpy(out["turn_reward"]),
                               "state": torch.from_numpy(out["state"])})
     keep, met, _ = oracle.filter_groups(scores, G_TOTAL, GS, 0.25, "std")
@@ -64,7 +73,9 @@ def _worker(rank, world, port, q):
     views = rd.episode_views(rd.gather_episode(ep), ng * GS, T)
     ep_tr = torch.cat([v.turn_reward for v in views], dim=1).numpy()
     ep_fl = [int(v.flags[0]) for v in views]
-    q.put((rank, scores, stats, traj["turn_reward"].numpy(), traj["state"].numpy(), keep, met, ep_tr, ep_fl))
+    extra = {"sized": sized, "rag": rag_sized.numpy(), "rag_unsized": rd.all_gather_rows(rag).numpy(), "off": off,
+             "bad": bad}
+    q.put((rank, scores, stats, traj["turn_reward"].numpy(), traj["state"].numpy(), keep, met, ep_tr, ep_fl, extra))
     dist.destroy_process_group()
 
 
@@ -95,7 +106,12 @@ def test_two_rank_gloo_matches_single_process():
         assert p.exitcode == 0
     full = _rollout(0, G_TOTAL)
     fkeep, fmet, _ = oracle.filter_groups(full["score"], G_TOTAL, GS, 0.25, "std")
-    for rank, scores, stats, tr, state, keep, met, ep_tr, ep_fl in res:
+    for rank, scores, stats, tr, state, keep, met, ep_tr, ep_fl, extra in res:
+        np.testing.assert_array_equal(extra["sized"], full["stats"])
+        np.testing.assert_array_equal(extra["rag"], [0, 1, 2, 100, 101, 102, 103])
+        np.testing.assert_array_equal(extra["rag_unsized"], extra["rag"])
+        assert extra["off"] == (0, 3)[rank]
+        assert extra["bad"]
         np.testing.assert_array_equal(ep_tr, full["turn_reward"].T)   # gather_episode == full record
         assert ep_fl == [1, 2]
         np.testing.assert_array_equal(scores, full["score"])        # bit-identical global scores
