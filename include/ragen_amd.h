@@ -181,8 +181,8 @@ int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_episode_t* e
  * (es_manager.py:95): desc / s / rng := the generated map, its start state and the seeded PCG64
  * (generate_random_map and the seeding stay on the host), episode record zeroed — one launch.  */
 /* The rollout's last turn fused with its end: rmi_frozenlake_step_turn, then exactly what
- * rmi_rollout_finalize computes, in one launch (as rmi_sokoban_step_turn_finalize; groups of
- * fin->group_size envs must divide 64 and B).                                              */
+ * rmi_rollout_finalize computes, in one launch (as rmi_sokoban_step_turn_finalize; the turn
+ * runs each env on 4 lanes, so fin->group_size must divide 16 and B, else RMI_EUNSUP).      */
 int rmi_frozenlake_step_turn_finalize(const rmi_frozenlake_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                       uint8_t* err, const rmi_finalize_t* fin, rmi_stream_t stream);
 

@@ -19,7 +19,11 @@ constexpr int kToyBlock = 64;
 #ifndef RMI_FL_BLOCK
 #define RMI_FL_BLOCK 64
 #endif
-constexpr int kFlBlock = RMI_FL_BLOCK;  // FrozenLake turn: threads per workgroup (envs, one per lane)
+constexpr int kFlBlock = RMI_FL_BLOCK;  // FrozenLake turn: threads per workgroup
+// FrozenLake turn: lanes per env (see fl4_turn).  8 lanes (one jump per lane) measured 30.7 us
+// per rollout against 29.7 for 4: the wave span shrinks, the dispatch of twice the waves costs
+// more.  The fused finalize needs its group of 16 envs inside one wave (4 lanes at most).
+constexpr int kFlLpe = 4, kFlLpeFin = 4;
 
 struct FrozenLakeDev {
   const uint8_t* desc;  // this env's row
@@ -89,7 +93,8 @@ struct Fl4Out {
   bool turn_done, succ_last;
   int s;
   int nv;  // known-name actions among the first n_act slots
-  Pcg64 rng;
+  Pcg64 rng;       // the state after the turn: valid on the owner lane only
+  bool rng_owner;  // this lane ran the turn's last executed step (stores the PCG64 state)
 #ifdef RMI_STAMPS
   unsigned long long t_draws;  // diagnostic: s_memtime once the turn's draws are computed
 #endif
@@ -101,9 +106,66 @@ __device__ __forceinline__ uint64_t pcg_out(uint64_t hi, uint64_t lo) {
   return (x >> rot) | (x << ((64u - rot) & 63u));
 }
 
-template <int K>
-__device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, Pcg64 rng, uint64_t acts, int n_act,
-                                           int left, bool slippery, uint64_t t0, uint64_t t1, uint64_t t2) {
+// Jump-ahead constants of the PCG64 LCG: the state k steps on is A_k * state + S_k * inc
+// (mod 2^128) with A_k = M^k and S_k = 1 + M + ... + M^(k-1); row k-1 = {A_k hi, lo, S_k hi, lo}.
+typedef unsigned __int128 u128;
+constexpr u128 kPcgMult = ((u128)0x2360ED051FC65DA4ull << 64) | 0x4385DF649FCCF645ull;
+constexpr u128 jump_a(int k) {
+  u128 a = 1;
+  for (int i = 0; i < k; ++i) a *= kPcgMult;
+  return a;
+}
+constexpr u128 jump_s(int k) {
+  u128 s = 0, p = 1;
+  for (int i = 0; i < k; ++i) {
+    s += p;
+    p *= kPcgMult;
+  }
+  return s;
+}
+#define RMI_JROW(k) \
+  {(uint64_t)(jump_a(k) >> 64), (uint64_t)jump_a(k), (uint64_t)(jump_s(k) >> 64), (uint64_t)jump_s(k)}
+__constant__ uint64_t kPcgJump[kMaxK][4] = {RMI_JROW(1), RMI_JROW(2), RMI_JROW(3), RMI_JROW(4),
+                                            RMI_JROW(5), RMI_JROW(6), RMI_JROW(7), RMI_JROW(8)};
+#undef RMI_JROW
+
+// low 128 bits of (a_hi:a_lo) * (b_hi:b_lo)
+__device__ __forceinline__ void mul128lo(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl, uint64_t& h,
+                                         uint64_t& l) {
+  l = al * bl;
+  h = __umul64hi(al, bl) + al * bh + ah * bl;
+}
+
+// The PCG64 state j steps after (s, inc), from row j-1 of kPcgJump (already loaded).
+__device__ __forceinline__ void pcg_jump(const Pcg64& r, const uint64_t* J, uint64_t& h, uint64_t& l) {
+  uint64_t ph, pl, qh, ql;
+  mul128lo(J[0], J[1], r.s_hi, r.s_lo, ph, pl);
+  mul128lo(J[2], J[3], r.i_hi, r.i_lo, qh, ql);
+  l = pl + ql;
+  h = ph + qh + (l < pl ? 1ull : 0ull);
+}
+
+// The cell after step k to the lane of step k + 1: L = 4, lane q of a quad <- lane (q + 3) & 3
+// (DPP quad_perm [3, 0, 1, 2]); L = 8, lane i <- lane i - 1 (row_shr:1; K <= 8 never wraps).
+template <int L>
+__device__ __forceinline__ int chain_pass(int x) {
+  if (L == 4) return __builtin_amdgcn_mov_dpp(x, 0x93, 0xF, 0xF, false);
+  return __builtin_amdgcn_update_dpp(x, x, 0x111, 0xF, 0xF, false);
+}
+
+// The turn of one env on L lanes (lane q = its index in the env's group of L): lane q owns
+// steps q and q + L.  It computes their PCG64 states by jump-ahead from the turn's start state
+// (the K draws no longer form a chain of K 128-bit multiply-adds) and their transition
+// tables; the steps' dependent chain then walks the lanes, one table lookup per step and one
+// DPP move between (chain_pass).  Every lane of the group ends with the same outputs; the
+// PCG64 state after the turn stays on the lane of the last executed step (Fl4Out.rng_owner),
+// which stores it.
+template <int K, int L>
+__device__ __forceinline__ Fl4Out fl4_turn(int q, int grp, uint32_t hole, uint32_t goal, int s, const Pcg64& rng,
+                                           uint64_t acts, int n_act, int left, bool slippery, uint64_t t0,
+                                           uint64_t t1, uint64_t t2, const uint64_t* J0, const uint64_t* J1) {
+  constexpr int P = (K + L - 1) / L;  // steps per lane
+  constexpr uint64_t kGrpMask = (1ull << L) - 1;
   Fl4Out r;
   r.o.acc = 0.0;
   r.o.info = 0;
@@ -123,30 +185,8 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
   }
   r.nv = nv;
   const int n_try = nv < left ? nv : (left > 0 ? left : 0);
-  // the chain's next K states and outputs (draw k of the turn = output of state k + 1)
-  uint64_t shi[K + 1], slo[K + 1], draw[K];
-  shi[0] = rng.s_hi;
-  slo[0] = rng.s_lo;
-  {
-    Pcg64 c = rng;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      c.next64();
-      shi[k + 1] = c.s_hi;
-      slo[k + 1] = c.s_lo;
-      draw[k] = pcg_out(c.s_hi, c.s_lo) >> 11;
-    }
-  }
-#ifdef RMI_STAMPS
-  __builtin_amdgcn_s_waitcnt(0);
-  r.t_draws = __builtin_amdgcn_s_memtime();
-#endif
-  // Step k's transition is a map of the 16 cells, fixed once the draw and the action are known:
-  // a terminal cell stays, any other moves by direction b_k (a wall keeps it).  Its table
-  // (4 bits per cell) is built for every k at once — b_k depends on the draw and the action
-  // only, not on the cell — so the dependent chain of the turn is one shift and mask per step:
-  // s_{k+1} = table_k[s_k].  The steps' outputs are then read off the chain (the steps run
-  // while k < n_try and until the first done, exactly the loop's `go`).
+  // this lane's steps q + L p: the PCG64 state after them (draw k = output of state k + 1)
+  uint64_t sh[P], sl[P], table[P];
   const uint64_t kMove[4] = {0xedcca98865442100ull, 0xfedcfedcba987654ull,  // LEFT, DOWN
                              0xffedbba977653321ull, 0xba98765432103210ull}; // RIGHT, UP
   const uint32_t term16 = hole | goal;
@@ -157,25 +197,46 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
   tm = (tm | (tm << 3)) & 0x1111111111111111ull;
   tm *= 0xFull;
   const uint64_t stay = 0xfedcba9876543210ull & tm;
-  uint64_t chain = (uint64_t)s;  // nibble k = the cell before step k
-  uint32_t done_m = 0, rw_m = 0, eff_m = 0, g_m = 0;
-  int cur = s;
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
+  for (int p = 0; p < P; ++p) {
+    pcg_jump(rng, p ? J1 : J0, sh[p], sl[p]);
+    const uint64_t u = pcg_out(sh[p], sl[p]) >> 11;
+    // Step k's transition is a map of the 16 cells fixed by its draw and action alone: a
+    // terminal cell stays, any other moves by direction b (a wall keeps it); 4 bits per cell.
+    const int k = q + L * p;
     const int ga = (int)((cl >> (8 * k)) & 0xFF) - 1;  // gym action 0..3 (a step past the list is never used)
-    const uint64_t u = draw[k];
     const int i = (u < t0) ? 0 : (u < t1) ? 1 : (u < t2) ? 2 : 0;
     const int b = (slippery ? ga + 3 + i : ga) & 3;
-    const uint64_t table = (kMove[b] & ~tm) | stay;
-    const int ns = (int)((table >> (4 * cur)) & 0xFull);
-    const uint32_t term = (term16 >> cur) & 1u, g = (goal >> ns) & 1u, h = (hole >> ns) & 1u;
-    done_m |= (term | g | h) << k;
-    rw_m |= ((term ^ 1u) & g) << k;
-    eff_m |= (uint32_t)(ns != cur) << k;
-    g_m |= g << k;
-    cur = ns;
-    chain |= (uint64_t)ns << (4 * (k + 1));
+    table[p] = (kMove[b] & ~tm) | stay;
   }
+#ifdef RMI_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  r.t_draws = __builtin_amdgcn_s_memtime();
+#endif
+  // the chain: step k runs on lane k % L from the cell the previous step's lane passed to it
+  int c = s, pre[P], post[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) pre[p] = post[p] = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int p = k / L;
+    const int ns = (int)((table[p] >> (4 * c)) & 0xFull);
+    const bool mine = q == k % L;
+    pre[p] = mine ? c : pre[p];
+    post[p] = mine ? ns : post[p];
+    if (k + 1 < K) c = chain_pass<L>(ns);
+  }
+  // per-step outcomes of this lane's steps, gathered over the group by ballots (bit k = step k)
+  uint32_t done_m = 0, rw_m = 0, eff_m = 0, g_m = 0;
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const uint32_t term = (term16 >> pre[p]) & 1u, g = (goal >> post[p]) & 1u, h = (hole >> post[p]) & 1u;
+    done_m |= (uint32_t)((__ballot((term | g | h) != 0) >> grp) & kGrpMask) << (L * p);
+    rw_m |= (uint32_t)((__ballot(((term ^ 1u) & g) != 0) >> grp) & kGrpMask) << (L * p);
+    eff_m |= (uint32_t)((__ballot(post[p] != pre[p]) >> grp) & kGrpMask) << (L * p);
+    g_m |= (uint32_t)((__ballot(g != 0) >> grp) & kGrpMask) << (L * p);
+  }
+  done_m &= (1u << K) - 1u;  // lanes of steps >= K computed throw-away steps
   // executed steps: the first n_try, cut after the first done
   const int first_done = __builtin_ctz(done_m | (1u << K));
   const int ex = n_try < first_done + 1 ? n_try : first_done + 1;
@@ -189,29 +250,33 @@ __device__ __forceinline__ Fl4Out fl4_turn(uint32_t hole, uint32_t goal, int s, 
   r.turn_done = ex && ((done_m >> last) & 1u);
   r.o.exec = (uint8_t)ex;
   r.o.stepped_any_state = ex > 0;
-  r.s = (int)((chain >> (4 * ex)) & 0xFull);
+  // the cell after the last executed step, from the lane that ran it (same group: all active)
+  const int lp = last >= L ? 1 : 0;
+  const int post_last = P > 1 && lp ? post[P - 1] : post[0];
+  const int from = __shfl(post_last, grp + (last & (L - 1)), 64);
+  r.s = ex ? from : s;
   r.rng = rng;
-#pragma unroll
-  for (int k = 1; k <= K; ++k)
-    if (k == ex) {
-      r.rng.s_hi = shi[k];
-      r.rng.s_lo = slo[k];
-    }
+  r.rng_owner = ex > 0 && q == (last & (L - 1));
+  r.rng.s_hi = P > 1 && lp ? sh[P - 1] : sh[0];
+  r.rng.s_lo = P > 1 && lp ? sl[P - 1] : sl[0];
   return r;
 }
 
-// bit i = (cell i == letter) for a 16-cell map held as two u64 (cell i in byte i): SWAR byte
-// compare, then each dword's 4 byte flags gathered by one multiply (bit 8j -> bit 24 + j).
-__device__ __forceinline__ uint32_t cell_bits(uint64_t lo, uint64_t hi, uint32_t letter) {
-  const uint32_t pat = letter * 0x01010101u;
-  const uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+// The hole / goal bits of a 4x4 map (bit i = cell i is 'H' / 'G') on the lanes of an env's quad:
+// lane q compares dword q of the row (cells 4q..4q+3; SWAR: a zero byte of row ^ letter, then
+// the dword's 4 byte flags gathered by one multiply), two DPP quad swaps OR the parts together.
+__device__ __forceinline__ uint32_t quad_cell_bits(uint64_t lo, uint64_t hi, int q) {
+  const uint64_t w64 = (q & 2) ? hi : lo;
+  const uint32_t w = (uint32_t)(w64 >> (32 * (q & 1)));
   uint32_t bits = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint32_t x = w[j] ^ pat;                                              // zero byte = match
+  for (int j = 0; j < 2; ++j) {  // 'H' -> bits 0..15, 'G' -> bits 16..31
+    const uint32_t x = w ^ ((j ? 'G' : 'H') * 0x01010101u);                      // zero byte = match
     const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // high bit of a zero byte
-    bits |= (((z >> 7) * 0x01020408u) >> 24) << (4 * j);
+    bits |= (((z >> 7) * 0x01020408u) >> 24) << (4 * (q & 3) + 16 * j);
   }
+  bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
+  bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xF, 0xF, false);  // quad_perm [2, 3, 0, 1]
   return bits;
 }
 
@@ -220,19 +285,23 @@ __device__ __forceinline__ uint64_t draw_threshold(double cs) {
   return (uint64_t)ceil(cs * 9007199254740992.0);
 }
 
-__device__ __forceinline__ Fl4Out fl4_dispatch(int K, uint32_t hole, uint32_t goal, int s, const Pcg64& rng,
-                                              uint64_t acts, int n_act, int left, bool slip, uint64_t t0,
-                                              uint64_t t1, uint64_t t2) {
+template <int L>
+__device__ __forceinline__ Fl4Out fl4_dispatch(int K, int q, int grp, uint32_t hole, uint32_t goal, int s,
+                                              const Pcg64& rng, uint64_t acts, int n_act, int left, bool slip,
+                                              uint64_t t0, uint64_t t1, uint64_t t2, const uint64_t* J0,
+                                              const uint64_t* J1) {
+#define RMI_FL4(k) fl4_turn<k, L>(q, grp, hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2, J0, J1)
   switch (K) {  // wave-uniform
-    case 1: return fl4_turn<1>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
-    case 2: return fl4_turn<2>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
-    case 3: return fl4_turn<3>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
-    case 4: return fl4_turn<4>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
-    case 5: return fl4_turn<5>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
-    case 6: return fl4_turn<6>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
-    case 7: return fl4_turn<7>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
-    default: return fl4_turn<8>(hole, goal, s, rng, acts, n_act, left, slip, t0, t1, t2);
+    case 1: return RMI_FL4(1);
+    case 2: return RMI_FL4(2);
+    case 3: return RMI_FL4(3);
+    case 4: return RMI_FL4(4);
+    case 5: return RMI_FL4(5);
+    case 6: return RMI_FL4(6);
+    case 7: return RMI_FL4(7);
+    default: return RMI_FL4(8);
   }
+#undef RMI_FL4
 }
 
 // kFirst: a fresh episode's first turn fused with its reset (rmi_frozenlake_reset): desc, s and
@@ -241,16 +310,18 @@ __device__ __forceinline__ Fl4Out fl4_dispatch(int K, uint32_t hole, uint32_t go
 // kFin: the launch is the rollout's last turn and also runs rmi_rollout_finalize for uniform
 // contiguous groups of fin.group_size envs (each group inside the launch's one wave): every
 // lane, live or not, reaches the group shuffles of finalize_envs.
-template <bool kFirst, bool kFin>
+template <bool kFirst, bool kFin, int L>
 __global__ __launch_bounds__(kFlBlock) void frozenlake_step_turn_kernel(rmi_frozenlake_t env, rmi_episode_t ep,
                                                                          rmi_turn_t in, uint8_t* __restrict__ err_out,
                                                                          const uint8_t* __restrict__ init_desc,
                                                                          const int32_t* __restrict__ init_s,
                                                                          const uint64_t* __restrict__ init_rng,
                                                                          rmi_finalize_t fin) {
-  const int64_t b = (int64_t)blockIdx.x * kFlBlock + threadIdx.x;
+  const int64_t gt = (int64_t)blockIdx.x * kFlBlock + threadIdx.x;
+  const int64_t b = gt / L;  // the env of this lane's group of L
+  const int q = (int)(gt & (L - 1)), grp = (int)(threadIdx.x & 63) & ~(L - 1);
   const int B = ep.B;
-  if (!kFin && b >= B) return;
+  if (!kFin && b >= B) return;  // whole groups (B * L lanes)
   const bool live = b < B;
   const int64_t bc = live ? b : (int64_t)B - 1;  // clamped: every load below is valid
   RMI_STAMP_DECL;
@@ -295,29 +366,42 @@ __global__ __launch_bounds__(kFlBlock) void frozenlake_step_turn_kernel(rmi_froz
   e.cs0 = env.cs0;
   e.cs1 = env.cs1;
   e.cs2 = env.cs2;
+  // jump-ahead rows of this lane's steps q and q + L (loaded with the rest)
+  const uint64_t* J0 = kPcgJump[q];
+  const uint64_t* J1 = kPcgJump[L < kMaxK ? q + L : q];
+  uint64_t j0[4], j1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    j0[i] = J0[i];
+    j1[i] = J1[i];
+  }
   FinRecord rec;
   if (kFin) rec.load(ep, bc);
-  if (kFirst && live) {  // the reset, then the turn (same thread, later stores win)
+  if (kFirst && live) {  // the reset, spread over the env's lanes, then the turn (later stores win)
     uint8_t* desc = const_cast<uint8_t*>(env.desc) + b * n;
     if (n == 16 && ((reinterpret_cast<uintptr_t>(env.desc) & 15u) == 0)) {
-      *reinterpret_cast<uint4*>(desc) = make_uint4((uint32_t)e.d_lo, (uint32_t)(e.d_lo >> 32), (uint32_t)e.d_hi,
-                                                   (uint32_t)(e.d_hi >> 32));
-    } else {
+      const uint64_t w = q < 2 ? e.d_lo : e.d_hi;
+      if (q < 4) reinterpret_cast<uint32_t*>(desc)[q] = (uint32_t)(w >> (32 * (q & 1)));
+    } else if (q == 0) {
       for (int i = 0; i < n; ++i) desc[i] = e.desc[i];
     }
-    env.s[b] = e.s;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) env.rng[k * (int64_t)B + b] = init_rng[k * (int64_t)B + b];
-    ep.num_actions[b] = 0;
-    ep.flags[b] = 0;
-    ep.n_turns[b] = 0;
-    ep.penalty[b] = 0.0;
-    for (int t = 0; t < ep.T; ++t) {
+    if (q < 4) env.rng[q * (int64_t)B + b] = init_rng[q * (int64_t)B + bc];  // lane q: plane q
+    if (q == 0) {
+      env.s[b] = e.s;
+      ep.num_actions[b] = 0;
+      ep.flags[b] = 0;
+      ep.n_turns[b] = 0;
+      ep.penalty[b] = 0.0;
+    }
+    for (int t = q; t < ep.T; t += L) {
       ep.turn_reward[(int64_t)t * B + b] = 0.0;
       ep.turn_info[(int64_t)t * B + b] = 0;
       ep.turn_exec[(int64_t)t * B + b] = 0;
     }
   }
+  // the jump rows are used deep inside the turn: tie them to this point so that their loads go
+  // out with the others (sunk next to their use they cost a second memory round trip)
+  asm volatile("" ::"v"(j0[0]), "v"(j0[1]), "v"(j0[2]), "v"(j0[3]), "v"(j1[0]), "v"(j1[1]), "v"(j1[2]), "v"(j1[3]));
   RMI_STAMP_WAIT(1);
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
   TurnOut o;
@@ -330,14 +414,17 @@ __global__ __launch_bounds__(kFlBlock) void frozenlake_step_turn_kernel(rmi_froz
   const bool ids_ok = ((((acts & 0x7F7F7F7F7F7F7F7Full) + 0x7B7B7B7B7B7B7B7Bull) | acts) &  // every id byte <= 4
                        0x8080808080808080ull) == 0;
   const bool fast = n == 16 && env.ncol == 4 && e.in_regs && in.K >= 1 && ids_ok && e.s >= 0 && e.s < 16;
-  if (__all(fast || !act)) {
+  const bool wave_fast = __all(fast || !act);
+  if (wave_fast) {
     if (act) {
-      const uint32_t hole = cell_bits(e.d_lo, e.d_hi, 'H'), goal = cell_bits(e.d_lo, e.d_hi, 'G');
+      const uint32_t hg = quad_cell_bits(e.d_lo, e.d_hi, q);  // every lane of the quad is active here
+      const uint32_t hole = hg & 0xFFFFu, goal = hg >> 16;
       int n_a = n_act > in.K ? in.K : n_act;
       flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (es_manager.py:168)
       RMI_STAMP(2);
-      const Fl4Out f = fl4_dispatch(in.K, hole, goal, e.s, e.rng, acts, n_a, in.max_actions_per_traj - num_actions,
-                                    e.slippery, draw_threshold(e.cs0), draw_threshold(e.cs1), draw_threshold(e.cs2));
+      const Fl4Out f = fl4_dispatch<L>(in.K, q, grp, hole, goal, e.s, e.rng, acts, n_a,
+                                    in.max_actions_per_traj - num_actions, e.slippery, draw_threshold(e.cs0),
+                                    draw_threshold(e.cs1), draw_threshold(e.cs2), j0, j1);
       RMI_STAMP(3);
 #ifdef RMI_STAMPS
       if ((threadIdx.x & 63) == 0) g_stamps[(blockIdx.x * blockDim.x + threadIdx.x) / 64 * 16 + 11] = f.t_draws;
@@ -354,21 +441,20 @@ __global__ __launch_bounds__(kFlBlock) void frozenlake_step_turn_kernel(rmi_froz
       const uint8_t f_cap = (uint8_t)(flags | fd | RMI_FLAG_TRUNCATED);
       flags = f.turn_done ? f_done : (num_actions >= in.max_actions_per_traj ? f_cap : flags);
       stepped = true;
-      ep.num_actions[b] = num_actions;
-      ep.flags[b] = flags;
-      ep.n_turns[b] = n_turns;
-      ep.penalty[b] = penalty;
-      const int64_t tb = (int64_t)in.turn * B + b;
-      ep.turn_reward[tb] = o.acc;
-      ep.turn_info[tb] = o.info;
-      ep.turn_exec[tb] = o.exec;
-      // s and the PCG64 state: written back whether or not a step ran (unchanged then)
-      e.s = f.s;
-      e.rng = f.rng;
-      env.s[b] = e.s;
-      store_pcg(env.rng, B, b, e.rng);
+      if (q == 0) {
+        ep.num_actions[b] = num_actions;
+        ep.flags[b] = flags;
+        ep.n_turns[b] = n_turns;
+        ep.penalty[b] = penalty;
+        const int64_t tb = (int64_t)in.turn * B + b;
+        ep.turn_reward[tb] = o.acc;
+        ep.turn_info[tb] = o.info;
+        ep.turn_exec[tb] = o.exec;
+        env.s[b] = f.s;  // unchanged when no step ran
+      }
+      if (f.rng_owner) store_pcg(env.rng, B, b, f.rng);  // the lane of the last executed step
     }
-  } else if (act) {
+  } else if (act && q == 0) {  // the generic turn: one lane of the quad
     if (e.s < 0 || e.s >= n) {
       if (err_out) err_out[b] |= RMI_ERR_STATE;
     } else {
@@ -392,9 +478,21 @@ __global__ __launch_bounds__(kFlBlock) void frozenlake_step_turn_kernel(rmi_froz
     }
   }
   if (kFin) {
+    // every lane of a group holds its env's values after the fast turn; after the generic one
+    // (lane 0 only) the group's other lanes take them from it
+    if (!wave_fast) {
+      const int l0 = grp;
+      flags = (uint8_t)__shfl((int)flags, l0, 64);
+      n_turns = __shfl(n_turns, l0, 64);
+      num_actions = __shfl(num_actions, l0, 64);
+      penalty = __shfl(penalty, l0, 64);
+      o.acc = __shfl(o.acc, l0, 64);
+      o.info = (uint8_t)__shfl((int)o.info, l0, 64);
+      stepped = __shfl((int)stepped, l0, 64) != 0;
+    }
     if (stepped) rec.set(in.turn, o.acc, o.info);  // this turn's record is still in registers
-    finalize_envs<1>(ep, fin, rec, b, live, flags, n_turns, num_actions, penalty, stepped ? in.turn : -1, o.acc,
-                     o.info);
+    finalize_envs<L>(ep, fin, rec, b, live && q == 0, flags, n_turns, num_actions, penalty,
+                          stepped ? in.turn : -1, o.acc, o.info);
   }
   RMI_STAMP(4);
 }
@@ -512,8 +610,8 @@ RMI_API int rmi_frozenlake_step_turn(const rmi_frozenlake_t* env, const rmi_epis
   const int rc = check_turn_args(ep, in);
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
-  const unsigned grid = (unsigned)((ep->B + kFlBlock - 1) / kFlBlock);
-  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, false>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
+  const unsigned grid = (unsigned)(((int64_t)ep->B * kFlLpe + kFlBlock - 1) / kFlBlock);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, false, kFlLpe>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
                      *env, *ep, *in, err, nullptr, nullptr, nullptr, rmi_finalize_t{});
   return launch_status();
 }
@@ -527,8 +625,8 @@ RMI_API int rmi_frozenlake_step_turn_first(const rmi_frozenlake_t* env, const rm
   const int rc = check_turn_args(ep, in);
   if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
   if (!env->desc || !env->s || !env->rng || !init_desc || !init_s || !init_rng) return RMI_EINVAL;
-  const unsigned grid = (unsigned)((ep->B + kFlBlock - 1) / kFlBlock);
-  hipLaunchKernelGGL((frozenlake_step_turn_kernel<true, false>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
+  const unsigned grid = (unsigned)(((int64_t)ep->B * kFlLpe + kFlBlock - 1) / kFlBlock);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<true, false, kFlLpe>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
                      *env, *ep, *in, err, init_desc, init_s, init_rng, rmi_finalize_t{});
   return launch_status();
 }
@@ -545,11 +643,11 @@ RMI_API int rmi_frozenlake_step_turn_finalize(const rmi_frozenlake_t* env, const
   if (!env->desc || !env->s || !env->rng) return RMI_EINVAL;
   if (fin->method < 0 || fin->method > 3 || fin->group_size < 1) return RMI_EINVAL;
   // every group inside the one-wave workgroup, and no partial group
-  if (64 % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;  // groups inside one wave
+  if (64 % (fin->group_size * kFlLpeFin) != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;  // groups in one wave
   rmi_finalize_t f = *fin;
   if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member
-  const unsigned grid = (unsigned)((ep->B + kFlBlock - 1) / kFlBlock);
-  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, true>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
+  const unsigned grid = (unsigned)(((int64_t)ep->B * kFlLpeFin + kFlBlock - 1) / kFlBlock);
+  hipLaunchKernelGGL((frozenlake_step_turn_kernel<false, true, kFlLpeFin>), dim3(grid), dim3(kFlBlock), 0, as_stream(stream),
                      *env, *ep, *in, err, nullptr, nullptr, nullptr, f);
   return launch_status();
 }

@@ -32,7 +32,7 @@ ids, n = synthetic.rollout_actions(B, T, K, 1, 4, seed=synthetic.ACTION_SEED + 1
 ids, n = torch.from_numpy(ids).to(dev), torch.from_numpy(n).to(dev)
 turns = [ops.turn_struct(t, ids[t], n[t], None, 10, -0.1) for t in range(T)]
 st = fl.struct()
-waves = (B + 63) // 64
+waves = (4 * B + 63) // 64  # four lanes per env
 stamps = torch.zeros(waves, 16, dtype=torch.int64, device=dev)
 lib = ctypes.CDLL(SO)
 assert lib.rmi_toytext_set_stamps(ctypes.c_void_p(stamps.data_ptr())) == 0
