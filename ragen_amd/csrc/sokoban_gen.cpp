@@ -16,6 +16,7 @@
 // The DFS visits states in the reference's order (actions 0..3, first-visit wins, the
 // explored set keyed on grid contents) so ties in room score resolve identically.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -138,6 +139,145 @@ struct NpLegacy {  // numpy RandomState (legacy MT19937)
 
 const int CH[4][2] = {{-1, 0}, {1, 0}, {0, -1}, {0, 1}};  // CHANGE_COORDINATES
 
+// The reverse-play search for rooms with <= 64 open cells, <= 256 cells and <= 16 boxes (every
+// size RAGEN configures): Gen::dfs's visits in Gen::dfs's order with the same scores and the
+// same explored-set semantics, without its allocations: the state lives in fixed arrays on the
+// stack, the player's cell is carried instead of rescanned, and the explored set is an
+// open-addressing table of 128-bit keys packing the grid (2 bits per open cell: its structure
+// value, box 3, box 4, player 5 — given the fixed structure, the same information as the grid
+// contents the reference keys on).  About 10x the speed of the std::string-keyed search.
+struct FastSearch {
+  static constexpr int kMaxHW = 256, kMaxOpen = 64, kMaxBoxes = 16;
+  static constexpr size_t kCap = 300000;  // depth_first_search's explored-set limit
+  int HW = 0, W = 0, nopen = 0, num_boxes = 0;
+  int8_t slot[kMaxHW];  // open cell -> its 2-bit field in the key (-1: wall)
+  int8_t structure[kMaxHW];
+  int tr[kMaxBoxes], tc[kMaxBoxes];  // box_mapping keys (targets, insertion order)
+  // explored set: 16-B slots, the all-zero key free (a grid always holds the player: code 3)
+  struct Slot {
+    uint64_t a, b;
+  };
+  std::vector<Slot> tab;
+  size_t count = 0, mask = 0;
+  // best
+  long best_score = -1;
+  int8_t best_room[kMaxHW];
+  int best_r[kMaxBoxes], best_c[kMaxBoxes];
+  bool have_best = false;
+
+  static bool usable(const std::vector<int8_t>& state, const std::vector<int8_t>& st_struct, int HW, int nb) {
+    if (HW > kMaxHW || nb > kMaxBoxes) return false;
+    int open = 0, players = 0;
+    for (int i = 0; i < HW; ++i) {
+      open += st_struct[i] != 0;
+      players += state[i] == 5;
+    }
+    return open <= kMaxOpen && players == 1;
+  }
+  static uint64_t mix(uint64_t x) {  // splitmix64 finaliser
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+  }
+  void clear_set() {
+    if (tab.size() != 4096) tab.assign(4096, Slot{0, 0});
+    else std::fill(tab.begin(), tab.end(), Slot{0, 0});
+    mask = 4095;
+    count = 0;
+  }
+  // -> true if the key was absent (and is now present)
+  bool insert(uint64_t a, uint64_t b) {
+    if (2 * (count + 1) > mask + 1) grow();
+    size_t h = mix(a ^ mix(b)) & mask;
+    for (;; h = (h + 1) & mask) {
+      Slot& e = tab[h];
+      if ((e.a | e.b) == 0) {
+        e.a = a;
+        e.b = b;
+        ++count;
+        return true;
+      }
+      if (e.a == a && e.b == b) return false;
+    }
+  }
+  void grow() {
+    std::vector<Slot> old;
+    old.swap(tab);
+    tab.assign(old.size() * 2, Slot{0, 0});
+    mask = tab.size() - 1;
+    count = 0;
+    for (const Slot& e : old)
+      if (e.a | e.b) insert(e.a, e.b);
+  }
+  static uint64_t code(int v) { return v == 5 ? 3u : (v == 4 ? 2u : (v == 3 ? 1u : 0u)); }
+  // cell i changes from value u to v: the key's field follows
+  void rekey(uint64_t& a, uint64_t& b, int i, int u, int v) const {
+    const int j = slot[i];
+    const uint64_t d = code(u) ^ code(v);
+    if (j < 32) a ^= d << (2 * j);
+    else b ^= d << (2 * (j - 32));
+  }
+  long displacement(const int* br, const int* bc) const {
+    long s = 0;
+    for (int k = 0; k < num_boxes; ++k) s += std::abs(br[k] - tr[k]) + std::abs(bc[k] - tc[k]);
+    return s;
+  }
+  // state's key (a, b) and its count of value-2 cells (n2) are carried, updated per move
+  void dfs(const int8_t* state, uint64_t a, uint64_t b, int n2, int pi, const int* br, const int* bc, long box_swaps,
+           int last_pull, int ttl) {
+    ttl -= 1;
+    if (ttl <= 0 || count >= kCap) return;
+    if (!insert(a, b)) return;  // explored (nothing reads the set between the test and the insert)
+    long score = box_swaps * displacement(br, bc);
+    if (n2 != num_boxes) score = 0;
+    if (score > best_score) {
+      memcpy(best_room, state, HW);
+      memcpy(best_r, br, sizeof(int) * num_boxes);
+      memcpy(best_c, bc, sizeof(int) * num_boxes);
+      best_score = score;
+      have_best = true;
+    }
+    const int prow = pi / W, pcol = pi % W;
+    for (int action = 0; action < 4; ++action) {  // reverse_move, then the recursion
+      const int nr = prow + CH[action][0], nc = pcol + CH[action][1];
+      const int ni = nr * W + nc;
+      if (!(state[ni] == 1 || state[ni] == 2)) {  // no move: the same state, explored already
+        dfs(state, a, b, n2, pi, br, bc, box_swaps, last_pull, ttl);
+        continue;
+      }
+      int8_t nxt[kMaxHW];
+      int nr_[kMaxBoxes], nc_[kMaxBoxes];
+      memcpy(nxt, state, HW);
+      memcpy(nr_, br, sizeof(int) * num_boxes);
+      memcpy(nc_, bc, sizeof(int) * num_boxes);
+      uint64_t na = a, nb = b;
+      int nn2 = n2, lp = last_pull;
+      auto set = [&](int i, int v) {
+        rekey(na, nb, i, nxt[i], v);
+        nn2 += (v == 2) - (nxt[i] == 2);
+        nxt[i] = (int8_t)v;
+      };
+      set(pi, structure[pi]);
+      set(ni, 5);
+      const int brow = prow - CH[action][0], bcol = pcol - CH[action][1];
+      const int bi = brow * W + bcol;
+      if (nxt[bi] == 3 || nxt[bi] == 4) {
+        set(pi, 3);
+        set(bi, structure[bi]);
+        for (int k = 0; k < num_boxes; ++k)
+          if (nr_[k] == brow && nc_[k] == bcol) {
+            nr_[k] = prow;
+            nc_[k] = pcol;
+            lp = k;
+          }
+      }
+      dfs(nxt, na, nb, nn2, ni, nr_, nc_, box_swaps + (lp != last_pull ? 1 : 0), lp, ttl);
+    }
+  }
+};
+
 struct Gen {
   int H, W, HW;
   PyRandom pr;
@@ -149,6 +289,8 @@ struct Gen {
   std::vector<int8_t> best_room;
   std::vector<std::pair<int, int>> best_map;  // box_mapping values, keyed by target order
   std::vector<std::pair<int, int>> targets;   // box_mapping keys (insertion order)
+  FastSearch fast;                            // the allocation-free search (most rooms)
+  bool force_string_search = false;           // RMI_SOKOBAN_GEN_STRING_SEARCH=1 (A/B tests)
 
   int at(int r, int c) const { return r * W + c; }
 
@@ -284,13 +426,43 @@ struct Gen {
       for (int i = 0; i < HW; ++i)
         if (room_structure[i] == 2) targets.push_back({i / W, i % W});
       num_boxes = (int)targets.size();
-      explored.clear();
-      best_score = -1;
-      best_room.clear();
-      best_map = targets;
-      dfs(room_state, room_structure, targets, 0, -1, search_depth);
-      if (best_room.empty()) return 1;  // search_depth <= 1: reference would fail later
-      room_state = best_room;
+      if (!force_string_search && FastSearch::usable(room_state, room_structure, HW, num_boxes)) {
+        FastSearch& f = fast;
+        f.HW = HW;
+        f.W = W;
+        f.num_boxes = num_boxes;
+        f.nopen = 0;
+        int pi = 0, n2 = 0;
+        uint64_t ka = 0, kb = 0;
+        for (int i = 0; i < HW; ++i) {
+          f.structure[i] = room_structure[i];
+          f.slot[i] = (int8_t)(room_structure[i] != 0 ? f.nopen++ : -1);
+          if (f.slot[i] >= 0) f.rekey(ka, kb, i, room_structure[i], room_state[i]);
+          if (room_state[i] == 5) pi = i;
+          n2 += room_state[i] == 2;
+        }
+        int br[FastSearch::kMaxBoxes], bc[FastSearch::kMaxBoxes];
+        for (int k = 0; k < num_boxes; ++k) {
+          f.tr[k] = br[k] = targets[k].first;
+          f.tc[k] = bc[k] = targets[k].second;
+        }
+        f.clear_set();
+        f.best_score = -1;
+        f.have_best = false;
+        f.dfs(room_state.data(), ka, kb, n2, pi, br, bc, 0, -1, search_depth);
+        if (!f.have_best) return 1;  // search_depth <= 1: reference would fail later
+        room_state.assign(f.best_room, f.best_room + HW);
+        best_map.clear();
+        for (int k = 0; k < num_boxes; ++k) best_map.push_back({f.best_r[k], f.best_c[k]});
+      } else {
+        explored.clear();
+        best_score = -1;
+        best_room.clear();
+        best_map = targets;
+        dfs(room_state, room_structure, targets, 0, -1, search_depth);
+        if (best_room.empty()) return 1;  // search_depth <= 1: reference would fail later
+        room_state = best_room;
+      }
       for (int i = 0; i < HW; ++i)
         if (room_state[i] == 3) room_state[i] = 4;
       score = displacement(targets, best_map);
@@ -357,9 +529,12 @@ RMI_HOST_API int rmi_sokoban_generate_rooms(const int64_t* seeds, int32_t n, int
     if (seeds[i] < 0 || seeds[i] > 0xffffffffLL) return -1;  // np.random.seed range
   const int num_gen_steps = (int)(1.7 * (H + W));  // gym_sokoban ctor
   const int HW = H * W;
+  const char* ss = getenv("RMI_SOKOBAN_GEN_STRING_SEARCH");  // the std::string-keyed search (tests)
+  const bool string_search = ss && ss[0] == '1';
   auto work = [&](int lo, int hi) {
     for (int i = lo; i < hi; ++i) {
       Gen g;
+      g.force_string_search = string_search;
       g.H = H;
       g.W = W;
       g.HW = HW;

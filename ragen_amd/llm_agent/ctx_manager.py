@@ -347,12 +347,15 @@ class ContextManager:
         (attach_env_manager; LLMAgentProxy does it) — the prompt ids are built on the device
         turn by turn (prompts.DevicePrompts)."""
         self.device_vocab = vocab
+        if self._es is not None:
+            self._es.lazy_outputs = vocab is not None
         return self
 
     def attach_env_manager(self, es):
         """The EnvStateManager whose device record this manager reads on the device path."""
         self._es = es
         self._prompts = None
+        es.lazy_outputs = self.device_vocab is not None  # reset() hands out env ids, dicts on demand
         return self
 
     def prompts(self):

@@ -153,6 +153,11 @@ class EnvStateManager:
         self.format_penalty = float(self.sys_config.es_manager.format_penalty)
         self._init_envs()
         self._rc = None
+        self._reset_pending = False  # reset() ran, its rollout-cache dicts not built yet
+        self._reset_rows = None
+        # set by a ContextManager on the device path (set_device_vocab / attach_env_manager):
+        # reset() then returns LazyEnvOutputs and builds the per-env dicts only when read
+        self.lazy_outputs = False
         self._states_pending = False  # a LazyRolloutStates was handed out and not built yet
         self._formulated = False      # the device formulate_rollouts ran: drop the last states when built
         self._untrimmed = None
@@ -238,13 +243,38 @@ class EnvStateManager:
         self._states_pending = False
         self._formulated = False
         self._untrimmed = None
+        self._rc = None
+        self._reset_pending = True
+        if self.lazy_outputs:  # the device path reads env ids; the dicts wait for a reader
+            # the initial observations rendered now, on the device (decoded when read)
+            self._reset_rows = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags)
+                                if type(tg.batch).render is BatchEnv.render}
+            return LazyEnvOutputs(self, self.env_lo + np.arange(self.n_envs, dtype=np.int64))
+        self._reset_rows = None
+        self._reset_cache()
+        return self._rc
+
+    def _reset_cache(self):
+        """The rollout cache reset() hands out (es_manager.py:92-103): per env its EnvStatus and
+        a history holding the initial observation; built once, when first read."""
+        if not self._reset_pending:
+            return
+        self._reset_pending = False
+        seeds = self._seeds
         self._rc = [{"env_id": e["env_id"], "history": [], "group_id": e["group_id"], "tag": e["tag"],
                      "penalty": 0} for e in self.envs]
+        from .. import ops
+        if self._reset_rows is not None:  # rendered at reset (the envs may have stepped since)
+            obs = {j: ops.decode_rows(*rows) for j, rows in self._reset_rows.items()}
+            self._reset_rows = None
+        else:
+            obs = {j: tg.batch.render_all() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
+        tag_of = self._tag_of
         for e, cache in zip(self.envs, self._rc):
             e["status"] = EnvStatus(seed=int(seeds[e["env_id"] - self.env_lo]))
-            cache["history"] = self._update_cache_history(cache["history"], e["env"].render(e["local"]),
-                                                          e["max_actions_per_traj"], None)
-        return self._rc
+            j = int(tag_of[e["env_id"] - self.env_lo])
+            state = obs[j][e["local"]] if j in obs else e["env"].render(e["local"])
+            cache["history"] = self._update_cache_history(cache["history"], state, e["max_actions_per_traj"], None)
 
     # ----------------------------------------------------------------------- step
     def step(self, all_env_inputs: List[Dict]):
@@ -516,6 +546,7 @@ class EnvStateManager:
         executed counts, the final flags and penalties, num_actions as the running sum of the
         executed counts — plus the host parse of each decoded generation for the history
         strings (llm_response, llm_raw_response, the executed action names)."""
+        self._reset_cache()
         if self._mat_upto >= len(self._turn_records):
             return
         from .. import ops

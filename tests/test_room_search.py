@@ -1,0 +1,36 @@
+"""The allocation-free reverse-play search of sokoban_gen.cpp (FastSearch: fixed arrays, 128-bit
+grid keys in an open-addressing table) against the std::string-keyed search it replaces
+(RMI_SOKOBAN_GEN_STRING_SEARCH=1), on rooms of every size RAGEN configures and a few more: the
+same rooms, players and statuses, bit for bit.  Both follow depth_first_search
+(sokoban/utils.py:440-498); the golden rooms of the reference pin the default path in
+tests/test_oracle.py."""
+import os
+
+import numpy as np
+import pytest
+
+from ragen_amd import ops
+
+CASES = [(6, 6, 1, 300, 400), (6, 6, 2, 300, 300), (8, 8, 2, 100, 200), (5, 7, 1, 50, 400),
+         (10, 10, 3, 100, 40), (12, 12, 2, 60, 40), (3, 3, 1, 10, 50)]
+
+
+def _gen(seeds, H, W, nb, sd, string_search):
+    old = os.environ.get("RMI_SOKOBAN_GEN_STRING_SEARCH")
+    os.environ["RMI_SOKOBAN_GEN_STRING_SEARCH"] = "1" if string_search else "0"
+    try:
+        return ops.generate_sokoban_rooms(seeds, H, W, nb, sd, 4)
+    finally:
+        if old is None:
+            del os.environ["RMI_SOKOBAN_GEN_STRING_SEARCH"]
+        else:
+            os.environ["RMI_SOKOBAN_GEN_STRING_SEARCH"] = old
+
+
+@pytest.mark.parametrize("H,W,nb,sd,n", CASES)
+def test_fast_search_equals_string_search(H, W, nb, sd, n):
+    seeds = np.arange(n, dtype=np.int64) * 7919 + 3 * H + W
+    fast = _gen(seeds, H, W, nb, sd, False)
+    ref = _gen(seeds, H, W, nb, sd, True)
+    for a, b in zip(fast, ref):
+        np.testing.assert_array_equal(a, b)
