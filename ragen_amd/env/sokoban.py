@@ -42,7 +42,7 @@ class SokobanBatch(BatchEnv):
     reseed_fn = staticmethod(lambda s: abs(hash(str(s))) % (2 ** 32))
 
     @classmethod
-    def generate(cls, seeds, H, W, num_boxes, search_depth, n_threads=8):
+    def generate(cls, seeds, H, W, num_boxes, search_depth, n_threads=0):
         seeds = np.asarray(seeds, np.int64)
         uniq, inv = np.unique(seeds, return_inverse=True)
         fixed, state, player, status = ops.generate_sokoban_rooms(uniq, H, W, num_boxes, search_depth, n_threads)

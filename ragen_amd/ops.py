@@ -274,9 +274,25 @@ def countdown_reward(env: _lib.Countdown, answers: torch.Tensor, answer_len: tor
     return reward, flags, err
 
 
-def generate_sokoban_rooms(seeds, H: int, W: int, num_boxes: int, search_depth: int, n_threads: int = 8):
-    """Host-side level generation (sokoban/utils.py:221-278) -> numpy arrays (fixed, state, player, status)."""
+def host_threads() -> int:
+    """Worker threads for host-side work: OMP_NUM_THREADS when set (the GPU boxes set their CPU
+    share there), else the CPUs this process may run on, capped at 16."""
+    import os
+    v = os.environ.get("OMP_NUM_THREADS", "")
+    if v.isdigit() and int(v) > 0:
+        return int(v)
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def generate_sokoban_rooms(seeds, H: int, W: int, num_boxes: int, search_depth: int, n_threads: int = 0):
+    """Host-side level generation (sokoban/utils.py:221-278) -> numpy arrays (fixed, state, player, status).
+    n_threads 0: host_threads(); each thread takes a contiguous range of the seeds."""
     import numpy as np
+    n_threads = n_threads or host_threads()
     seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64))
     n = seeds.shape[0]
     fixed = np.zeros((n, H * W), np.uint8)
