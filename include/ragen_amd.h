@@ -544,6 +544,8 @@ typedef struct {
   uint8_t sep[16];
   const uint8_t* cond;       /* [B]                                                             */
   const uint8_t* active;     /* [B] (NULL: every row)                                           */
+  int32_t pool_len;          /* readable bytes at pool (0: unknown); <= 1024 the wave stages
+                                the pool in LDS with the row's other loads                     */
 } rmi_prompt_t;
 int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, int32_t stride, int32_t* out_len,
                     int32_t* mark, uint8_t* err, rmi_stream_t stream);

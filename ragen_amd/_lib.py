@@ -87,7 +87,8 @@ class Prompt(ctypes.Structure):
                 ("obs_stride", c_int32), ("obs_len", c_void_p), ("ints", c_void_p), ("reward", c_void_p),
                 ("reward_int", c_void_p), ("resp", c_void_p), ("resp_stride", c_int32), ("resp_len", c_void_p),
                 ("spans", c_void_p), ("enable_think", c_int32), ("K", c_int32), ("sep_len", c_int32),
-                ("sep", ctypes.c_uint8 * 16), ("cond", c_void_p), ("active", c_void_p)]
+                ("sep", ctypes.c_uint8 * 16), ("cond", c_void_p), ("active", c_void_p),
+                ("pool_len", c_int32)]
 
 
 _P = ctypes.POINTER

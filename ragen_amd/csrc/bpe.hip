@@ -170,6 +170,8 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     p += S + 16;
     L.C = p;
   }
+  RMI_STAMP_DECL;
+  RMI_STAMP(0);
   const int n = text_len[b];
   const int base_len = out_len ? out_len[b] : 0;
   if (n < 0 || n > S) {
@@ -191,6 +193,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   if (lane < 8) L.AF[lane] = tok.added_first[lane];
   for (int i = lane; i < n + 128; i += 64) L.C[i] = 0;
   wave_sync();
+  RMI_STAMP_WAIT(1);
   // ---- 1. UTF-8 decode and classes
   bool bad = false, unsafe = false;
   for (int p = lane; p < n; p += 64) {
@@ -347,6 +350,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     L.M[p] = (uint16_t)(len > 0 ? len : l0);
   }
   wave_sync();
+  RMI_STAMP(2);
   // ---- 4. the leftmost match chain: pre-token starts (added tokens are pre-tokens too)
   int np = 0;
   for (int p = 0; p < n;) {
@@ -411,6 +415,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     L.K[j] = (uint16_t)cnt;
   }
   wave_sync();
+  RMI_STAMP(3);
   // ---- 6. row offsets (wave scan over pre-tokens), mark, capacity, the ids
   const int mk = mark_byte ? mark_byte[b] : -1;
   int total = 0, before_mark = 0;
@@ -437,10 +442,17 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     if (n_tok) n_tok[b] = total;
     if (mark_tok) mark_tok[b] = base_len + before_mark;
   }
+  RMI_STAMP(4);
 }
 
 }  // namespace
 }  // namespace rmi
+
+#ifdef RMI_STAMPS
+RMI_API int rmi_bpe_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pitch, int32_t stride,
                            const int32_t* text_len, int64_t B, int64_t* out, int64_t out_stride, int32_t* out_len,

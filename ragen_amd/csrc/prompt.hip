@@ -57,9 +57,30 @@ __device__ void cascade(uint8_t* buf, int& a, int& z) {
   }
 }
 
+// The wave's staging of its row's inputs (kernel prologue): the constant pool, the rendered
+// observation and the response, copied into LDS by loads that all go out before the first
+// wait, so the piece loop below runs on LDS alone (it used to issue each piece's global reads
+// when it reached the piece: one memory round trip per piece).
+constexpr int kStagePool = 1024;  // pool bytes staged (4 dwords a lane); a longer pool is read in place
+constexpr int kStageResp = 512;   // response bytes in the first batch (2 dwords a lane); the rest after
+struct StageDims {
+  int pool, obs, resp;  // staged region sizes (bytes, multiples of 4; 0 = not staged)
+};
+__host__ __device__ inline StageDims stage_dims(const rmi_prompt_t& P, int stride, bool need_obs, bool need_resp) {
+  StageDims d;
+  // dword loads: the pool and the response rows staged only when 4-B aligned and whole dwords
+  const bool pool4 = P.pool && P.pool_len > 0 && P.pool_len % 4 == 0 && (reinterpret_cast<uintptr_t>(P.pool) & 3u) == 0;
+  const bool resp4 = P.resp && P.resp_stride > 0 && P.resp_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(P.resp) & 3u) == 0;
+  d.pool = pool4 && P.pool_len <= kStagePool ? P.pool_len : 0;
+  d.obs = need_obs && P.obs_stride > 0 && P.obs_stride <= kMaxStride ? (P.obs_stride + 3) & ~3 : 0;
+  d.resp = need_resp && resp4 ? (P.resp_stride < stride ? P.resp_stride : stride) : 0;
+  return d;
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void prompt_text_kernel(rmi_prompt_t P, int64_t B, uint8_t* __restrict__ out,
                                                          int stride, int32_t* __restrict__ out_len,
-                                                         int32_t* __restrict__ mark, uint8_t* __restrict__ err) {
+                                                         int32_t* __restrict__ mark, uint8_t* __restrict__ err,
+                                                         StageDims sd) {
   extern __shared__ __align__(16) uint8_t smem[];
   uint8_t* row = smem;                         // the assembled row, stride + 64
   uint8_t* th = row + stride + 64;             // think content, stride
@@ -68,6 +89,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
   int* sh = reinterpret_cast<int*>(num + 64);  // lane 0 -> wave hand-off, 16 ints; the split's
                                                // piece bounds at sh + 16 / sh + 32 (K + 1 each)
   char* scr = reinterpret_cast<char*>(sh + 48);  // the number formatter's digit scratch, 64
+  uint8_t* pl = reinterpret_cast<uint8_t*>(scr + 64);  // staged pool, sd.pool
+  uint8_t* ob = pl + sd.pool;                          // staged observation row, sd.obs
+  uint8_t* rs = ob + sd.obs;                           // staged response row, sd.resp (+ 8)
   // (lane 0's formatting and split work in LDS, not in per-lane register arrays: the wave
   // keeps a register budget that lets 8 waves share a SIMD)
   const int lane = threadIdx.x;
@@ -80,6 +104,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
     }
     return;
   }
+  RMI_STAMP_DECL;
+  RMI_STAMP(0);
+  // ---- stage: every load of the row first (pool, observation, response head, length), then
+  //      the LDS stores; a response longer than kStageResp takes a second batch
+  {
+    const uint32_t* pool4 = reinterpret_cast<const uint32_t*>(P.pool);
+    const uint32_t* resp4 = sd.resp ? reinterpret_cast<const uint32_t*>(P.resp + b * (int64_t)P.resp_stride) : nullptr;
+    const uint8_t* obsr = sd.obs ? P.obs + b * (int64_t)P.obs_stride : nullptr;
+    uint32_t pv[4], rv[2];
+    uint8_t ov[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int w = lane + 64 * k;
+      pv[k] = 4 * w < sd.pool ? pool4[w] : 0u;
+      ov[k] = lane + 64 * k < sd.obs && lane + 64 * k < P.obs_stride ? obsr[lane + 64 * k] : (uint8_t)0;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int w = lane + 64 * k;
+      rv[k] = 4 * w < sd.resp && 4 * w < kStageResp ? resp4[w] : 0u;
+    }
+    const int rl = sd.resp ? P.resp_len[b] : 0;
+    uint32_t* pl4 = reinterpret_cast<uint32_t*>(pl);
+    uint32_t* rs4 = reinterpret_cast<uint32_t*>(rs);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int w = lane + 64 * k;
+      if (4 * w < sd.pool) pl4[w] = pv[k];
+      if (lane + 64 * k < sd.obs) ob[lane + 64 * k] = ov[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int w = lane + 64 * k;
+      if (4 * w < sd.resp && 4 * w < kStageResp) rs4[w] = rv[k];
+    }
+    for (int i = 256 + lane; i < sd.obs && i < P.obs_stride; i += 64) ob[i] = obsr[i];  // rows past 256 B
+    const int rw = ((rl < sd.resp ? rl : sd.resp) + 3) >> 2;
+    for (int w = kStageResp / 4 + lane; w < rw; w += 64) rs4[w] = resp4[w];
+  }
+  wave_sync();
+  RMI_STAMP_WAIT(1);
+  const uint8_t* pool = sd.pool ? pl : P.pool;
   const int tg = P.tag ? P.tag[b] : 0;
   int pos = 0, mk = 0;
   bool over = false, unsup = false;
@@ -91,7 +157,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
           over = true;
           break;
         }
-        put(row, pos, P.pool + pc.a, pc.b, lane);
+        put(row, pos, pool + pc.a, pc.b, lane);
         pos += pc.b;
         break;
       case RMI_PT_TAG_CONST: {
@@ -100,7 +166,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
           over = true;
           break;
         }
-        put(row, pos, P.pool + o, l, lane);
+        put(row, pos, pool + o, l, lane);
         pos += l;
         break;
       }
@@ -110,7 +176,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
           over = true;
           break;
         }
-        put(row, pos, P.obs + b * (int64_t)P.obs_stride, l, lane);
+        put(row, pos, sd.obs ? ob : P.obs + b * (int64_t)P.obs_stride, l, lane);
         pos += l;
         break;
       }
@@ -142,8 +208,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
         break;
       }
       case RMI_PT_RESPONSE: {
-        const uint8_t* txt = P.resp + b * (int64_t)P.resp_stride;
         const int tl = P.resp_len[b];
+        const uint8_t* txt = tl <= sd.resp ? rs : P.resp + b * (int64_t)P.resp_stride;  // staged unless too long
         const int plen = P.enable_think ? 7 : 8;
         const uint8_t* pre = reinterpret_cast<const uint8_t*>(P.enable_think ? kThinkO : kAnsO);
         auto raw = [&](int i) -> uint8_t { return i < plen ? pre[i] : txt[i - plen]; };
@@ -249,6 +315,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
         pos += a1 - a0;
         put(row, pos, reinterpret_cast<const uint8_t*>(kAnsC), 9, lane);
         pos += 9;
+        RMI_STAMP(2);
         break;
       }
       case RMI_PT_MARK:
@@ -270,6 +337,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
     }
     return;
   }
+  RMI_STAMP(3);
   uint32_t* o4 = reinterpret_cast<uint32_t*>(out + b * (int64_t)stride);
   const uint32_t* r4 = reinterpret_cast<const uint32_t*>(row);
   for (int w = lane; w < (pos + 3) / 4; w += 64) {
@@ -282,6 +350,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
     if (mark) mark[b] = mk;
     err[b] = 0;
   }
+  RMI_STAMP(4);
 }
 
 // one wave per output row: the row's arena slice and the tail, left-padded (element-wise
@@ -314,6 +383,12 @@ __global__ __launch_bounds__(64) void pad_rows_kernel(const int64_t* __restrict_
 
 }  // namespace
 }  // namespace rmi
+
+#ifdef RMI_STAMPS
+RMI_API int rmi_prompt_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 
 RMI_API int rmi_pad_rows(const int64_t* arena, int64_t arena_stride, const int32_t* arena_len, const int64_t* rows,
                          int64_t n_rows, const int64_t* tail, int32_t n_tail, int64_t S, int64_t pad_id,
@@ -355,9 +430,12 @@ RMI_API int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, i
       (need_if && !prog->cond) || (need_tag && (!prog->tag_const || !prog->pool || prog->n_tags < 1)))
     return RMI_EINVAL;
   // row (stride + 64) + think (stride) + answer and its re-joined form (2 * stride + 64) + number
-  // (64) + hand-off and piece bounds (48 ints) + digit scratch (64)
-  const size_t lds = (size_t)stride + 64 + (size_t)stride + 2 * (size_t)stride + 64 + 64 + 48 * 4 + 64;
+  // (64) + hand-off and piece bounds (48 ints) + digit scratch (64) + the staged pool,
+  // observation and response
+  const StageDims sd = stage_dims(*prog, (int)stride, need_obs, need_resp);
+  const size_t lds = (size_t)stride + 64 + (size_t)stride + 2 * (size_t)stride + 64 + 64 + 48 * 4 + 64 +
+                     (size_t)sd.pool + (size_t)sd.obs + (size_t)sd.resp + 8;
   hipLaunchKernelGGL(prompt_text_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *prog, B, out,
-                     (int)stride, out_len, mark, err);
+                     (int)stride, out_len, mark, err, sd);
   return launch_status();
 }

@@ -173,7 +173,8 @@ class DevicePrompts:
             else:
                 prog.append(p)
         if self._pool_dev is None or self._pool_dev[0] != len(self._pool):  # upload when it grew
-            pool = torch.frombuffer(bytearray(self._pool) + b"\0" * 4, dtype=torch.uint8).to(self.device)
+            pad = 4 + (-len(self._pool)) % 4  # whole dwords: the kernel stages the pool with dword loads
+            pool = torch.frombuffer(bytearray(self._pool) + b"\0" * pad, dtype=torch.uint8).to(self.device)
             tc = torch.tensor([x for t in self._tag_tables for x in t], dtype=torch.int32, device=self.device)
             self._pool_dev = (len(self._pool), pool, tc)
         return prog, self._pool_dev[1], self._pool_dev[2]

@@ -751,6 +751,7 @@ def prompt_struct(program: List[int], sep: List[int], tensors) -> _lib.Prompt:
     for i, x in enumerate(sep):
         P.sep[i] = x
     P.cond, P.active = _ptr(cond), _ptr(active)
+    P.pool_len = pool.numel() if pool is not None else 0
     return P
 
 
