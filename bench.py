@@ -627,6 +627,8 @@ def api_leg(device):
     device_path = {"env_steps": steps, "turn_loop_s": tm["turns_s"], "get_rollout_states_s": tm["rollout_states_s"],
                    "formulate_rollouts_s": tm["formulate_s"], "rollout_s": total, "env_steps_per_s": steps / total,
                    "turn_loop_env_steps_per_s": steps / tm["turns_s"], "rows_formulated": rows,
+                   "reset_s": tm["reset_s"],  # es.reset(): rooms for a fresh train seed (host) + device restore
+                   "env_steps_per_s_with_reset": steps / (total + tm["reset_s"]),
                    "prompt_batch_shapes": shapes, "update_batch_shape": upd, "device_prompts": pr is not None,
                    "host_prompt_rows": pr.host_rows_used if pr is not None else None,
                    "tokenizer": f"{tok.name_or_path}, vocab {len(tok)}",

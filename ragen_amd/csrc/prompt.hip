@@ -92,6 +92,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
   uint8_t* pl = reinterpret_cast<uint8_t*>(scr + 64);  // staged pool, sd.pool
   uint8_t* ob = pl + sd.pool;                          // staged observation row, sd.obs
   uint8_t* rs = ob + sd.obs;                           // staged response row, sd.resp (+ 8)
+  int* pre_iv = reinterpret_cast<int*>(smem + ((rs - smem + sd.resp + 8 + 7) & ~7));  // INT values by piece [64]
+  int2* pre_tc = reinterpret_cast<int2*>(pre_iv + 64);      // TAG_CONST (offset, length) [64]
+  int* pre_s = reinterpret_cast<int*>(pre_tc + 64);         // tag, cond, reward_int
+  double* pre_d = reinterpret_cast<double*>(pre_s + 4);     // reward
   // (lane 0's formatting and split work in LDS, not in per-lane register arrays: the wave
   // keeps a register budget that lets 8 waves share a SIMD)
   const int lane = threadIdx.x;
@@ -126,6 +130,32 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
       rv[k] = 4 * w < sd.resp && 4 * w < kStageResp ? resp4[w] : 0u;
     }
     const int rl = sd.resp ? P.resp_len[b] : 0;
+    // the row's scalars with the same batch: tag, condition, reward, the INT pieces' values
+    // (lane i: piece i), and the TAG_CONST pieces' (offset, length) for every tag (lane
+    // i * n_tags + t, when the pieces and tags fit the wave)
+    const int tg_l = P.tag ? P.tag[b] : 0;
+    const int cond_l = P.cond ? P.cond[b] : 1;
+    const double rew_l = P.reward ? P.reward[b] : 0.0;
+    const int rint_l = P.reward_int ? P.reward_int[b] : 0;
+    int iv = 0;
+    if (lane < P.n_pieces && P.pieces[lane].kind == RMI_PT_INT) iv = P.ints[(int64_t)P.pieces[lane].a * B + b];
+    const bool tc_pre = P.tag_const && P.n_tags > 0 && P.n_pieces * P.n_tags <= 64;
+    int2 tcv = make_int2(0, 0);
+    if (tc_pre && lane < P.n_pieces * P.n_tags) {
+      const int pi = lane / P.n_tags, t = lane - pi * P.n_tags;
+      if (P.pieces[pi].kind == RMI_PT_TAG_CONST) {
+        const int k = 2 * (P.pieces[pi].a * P.n_tags + t);
+        tcv = make_int2(P.tag_const[k], P.tag_const[k + 1]);
+      }
+    }
+    pre_iv[lane] = iv;
+    pre_tc[lane] = tcv;
+    if (lane == 0) {
+      pre_s[0] = tg_l;
+      pre_s[1] = cond_l;
+      pre_s[2] = rint_l;
+      pre_d[0] = rew_l;
+    }
     uint32_t* pl4 = reinterpret_cast<uint32_t*>(pl);
     uint32_t* rs4 = reinterpret_cast<uint32_t*>(rs);
 #pragma unroll
@@ -146,7 +176,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
   wave_sync();
   RMI_STAMP_WAIT(1);
   const uint8_t* pool = sd.pool ? pl : P.pool;
-  const int tg = P.tag ? P.tag[b] : 0;
+  const int tg = pre_s[0];
+  const bool tc_pre = P.tag_const && P.n_tags > 0 && P.n_pieces * P.n_tags <= 64;
   int pos = 0, mk = 0;
   bool over = false, unsup = false;
   for (int pi = 0; pi < P.n_pieces && !over && !unsup; ++pi) {
@@ -161,7 +192,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
         pos += pc.b;
         break;
       case RMI_PT_TAG_CONST: {
-        const int o = P.tag_const[2 * (pc.a * P.n_tags + tg)], l = P.tag_const[2 * (pc.a * P.n_tags + tg) + 1];
+        const int2 ol = tc_pre ? pre_tc[pi * P.n_tags + tg]
+                               : make_int2(P.tag_const[2 * (pc.a * P.n_tags + tg)], P.tag_const[2 * (pc.a * P.n_tags + tg) + 1]);
+        const int o = ol.x, l = ol.y;
         if (pos + l > stride) {
           over = true;
           break;
@@ -182,14 +215,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
       }
       case RMI_PT_INT:
       case RMI_PT_REWARD: {
+        if (pc.kind == RMI_PT_REWARD) RMI_STAMP(2);
         if (lane == 0) {
           char* o = reinterpret_cast<char*>(num);
           int l;
           if (pc.kind == RMI_PT_INT) {
-            l = py_int_repr(P.ints[(int64_t)pc.a * B + b], o);
+            l = py_int_repr(pi < 64 ? pre_iv[pi] : P.ints[(int64_t)pc.a * B + b], o);
           } else {
-            const double r = P.reward[b];
-            l = (P.reward_int && P.reward_int[b]) ? py_int_repr((int64_t)r, o) : py_float_repr(r, o, scr);
+            const double r = pre_d[0];
+            l = pre_s[2] ? py_int_repr((int64_t)r, o) : py_float_repr(r, o, scr);
           }
           sh[0] = l;
         }
@@ -205,6 +239,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
         }
         put(row, pos, num, l, lane);
         pos += l;
+        if (pc.kind == RMI_PT_REWARD) RMI_STAMP_WAIT(3);
         break;
       }
       case RMI_PT_RESPONSE: {
@@ -315,14 +350,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
         pos += a1 - a0;
         put(row, pos, reinterpret_cast<const uint8_t*>(kAnsC), 9, lane);
         pos += 9;
-        RMI_STAMP(2);
         break;
       }
       case RMI_PT_MARK:
         mk = pos;
         break;
       case RMI_PT_IF:
-        if (!P.cond[b]) pi = P.n_pieces;
+        if (!pre_s[1]) pi = P.n_pieces;
         break;
       default:
         unsup = true;
@@ -337,7 +371,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
     }
     return;
   }
-  RMI_STAMP(3);
   uint32_t* o4 = reinterpret_cast<uint32_t*>(out + b * (int64_t)stride);
   const uint32_t* r4 = reinterpret_cast<const uint32_t*>(row);
   for (int w = lane; w < (pos + 3) / 4; w += 64) {
@@ -434,7 +467,7 @@ RMI_API int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, i
   // observation and response
   const StageDims sd = stage_dims(*prog, (int)stride, need_obs, need_resp);
   const size_t lds = (size_t)stride + 64 + (size_t)stride + 2 * (size_t)stride + 64 + 64 + 48 * 4 + 64 +
-                     (size_t)sd.pool + (size_t)sd.obs + (size_t)sd.resp + 8;
+                     (size_t)sd.pool + (size_t)sd.obs + (size_t)sd.resp + 8 + 8 + 64 * 4 + 64 * 8 + 16 + 8;
   hipLaunchKernelGGL(prompt_text_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *prog, B, out,
                      (int)stride, out_len, mark, err, sd);
   return launch_status();

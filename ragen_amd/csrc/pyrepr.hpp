@@ -8,7 +8,9 @@
 // to integral values ("10.0", "0.0001").
 //
 // A double-arithmetic fast path settles every value whose repr has at most 15 significant
-// digits (see py_float_repr); the rest takes the exact integer search.
+// digits (see py_float_repr); the rest takes the exact integer search, starting at the digit
+// count the fast path reached (16 when it ruled out every shorter one: a sum like
+// -0.1 + -0.1 + -0.1 = -0.30000000000000004 costs two rounds of it, not seventeen).
 // Exact integer arithmetic: the rounding interval of x (the half-way points to its neighbours)
 // is scaled by 10^s and 2^K into 128-bit integers, and for n = 1, 2, ... the first n whose
 // n-digit grid has a point inside the interval gives the digits.  That needs
@@ -53,10 +55,18 @@ RMI_HD void reverse_chars(char* a, int n) {
 
 RMI_HD int u128_digits(u128 v, char* out) {  // (no local array: out may be LDS on the device)
   int n = 0;
-  while (v) {
-    const uint64_t lo = (uint64_t)(v % 10u);  // u128 % small constant: lowered without a division call
-    out[n++] = (char)('0' + lo);
+  // every value formatted here is below 10^18 (17 significant digits, or an integer below
+  // 2^53): 64-bit division by 10, which compiles to a multiply-high; a 128-bit division on the
+  // device is a bit-serial loop (it made the reward piece of a prompt row cost ~25 k cycles)
+  uint64_t u = (uint64_t)v;
+  while (v >> 64) {
+    out[n++] = (char)('0' + (uint64_t)(v % 10u));
     v /= 10u;
+    u = (uint64_t)v;
+  }
+  while (u) {
+    out[n++] = (char)('0' + u % 10u);
+    u /= 10u;
   }
   reverse_chars(out, n);
   return n;
@@ -158,6 +168,7 @@ RMI_HD int py_float_repr(double x, char* out, char* scratch) {
   // (or product c * 10^-s): c < 2^53 and 10^|s| <= 10^22 are exact doubles and the operation
   // is correctly rounded.  The scales are tried upward from the one where c first reaches 1,
   // so the first hit has the fewest digits.  Anything else takes the exact search below.
+  int nd_min = 1;  // the exact search's first digit count: fewer were ruled out here
   {
     int D0 = 0;  // floor(log10 |x|), possibly off by one: only where the scan starts
     for (double t = ax; t >= 10.0; t /= 10.0) ++D0;
@@ -167,7 +178,10 @@ RMI_HD int py_float_repr(double x, char* out, char* scratch) {
     for (int i = 0; i < (s < 0 ? -s : s); ++i) pw *= 10.0;
     for (; s <= 22; pw = s >= 0 ? pw * 10.0 : pw / 10.0, ++s) {
       const double y = s >= 0 ? ax * pw : ax / pw;
-      if (y >= 1e15) break;  // more than 15 digits
+      if (y >= 1e15) {  // more than 15 digits: every shorter repr was tried and failed
+        nd_min = 16;
+        break;
+      }
       const double m = __builtin_rint(y);
       int hits = 0;
       double hit = 0.0;
@@ -179,7 +193,12 @@ RMI_HD int py_float_repr(double x, char* out, char* scratch) {
           hit = c;
         }
       }
-      if (hits > 1) break;
+      if (hits > 1) {  // two candidates at this scale: the exact search decides, from about here
+        int dm = 0;
+        for (uint64_t u = (uint64_t)m; u; u /= 10u) ++dm;
+        nd_min = dm > 2 ? dm - 1 : 1;
+        break;
+      }
       if (hits == 1) {
         int k = 0;
         for (uint64_t u = (uint64_t)hit; u; u /= 10u) d[k++] = (char)('0' + u % 10u);
@@ -207,7 +226,7 @@ RMI_HD int py_float_repr(double x, char* out, char* scratch) {
     while (!ge_pow10(D)) --D;
     while (ge_pow10(D + 1)) ++D;
   }
-  for (int nd = 1; nd <= 17; ++nd) {
+  for (int nd = nd_min; nd <= 17; ++nd) {
     const int s = nd - 1 - D;  // candidates: integers c with c / 10^s in the interval
     u128 cmin, cmax, cnear;
     bool tie;

@@ -44,6 +44,9 @@ lib = ctypes.CDLL(SO)
 setter = lib.rmi_prompt_set_stamps if WHICH == "prompt" else lib.rmi_bpe_set_stamps
 stamps = torch.zeros(B * 16, dtype=torch.int64, device=dev)
 dummy = torch.zeros(B * 16, dtype=torch.int64, device=dev)
+# the stamped kernels write through g_stamps unconditionally: point it at a buffer before any
+# launch (the prompt builder's constructor already encodes)
+assert setter(ctypes.c_void_p(dummy.data_ptr())) == 0
 calls = [0]
 name = "_run_text" if WHICH == "prompt" else "_encode"
 orig = getattr(pm.DevicePrompts, name)
@@ -64,8 +67,8 @@ torch.cuda.synchronize()
 s = stamps.view(B, 16).cpu().numpy().astype(np.float64)
 ok = (s[:, 0] > 0) & np.all(np.diff(s[:, 0:10:2], axis=1) > 0, axis=1)
 a = s[ok]
-names = {"prompt": ["stage", "pieces to the response end", "the rest of the pieces", "stores"],
-         "bpe": ["stage", "classes + added + match lengths", "pre-tokens + BPE merges", "offsets + ids out"]}[WHICH]
+names = {"prompt": ["stage", "pieces up to the reward", "the reward piece", "the rest + stores"],
+         "bpe": ["stage", "classes + added + match lengths + chain", "symbols + pair lookups", "merges"]}[WHICH]
 ph = [a[:, 2 * (i + 1)] - a[:, 2 * i] for i in range(4)]
 print(f"{WHICH}: {int(ok.sum())} of {B} waves: mean cycles " + "  ".join(f"{nm} {p.mean():.0f}" for nm, p in zip(names, ph))
       + f"  | span {(a[:, 8] - a[:, 0]).mean():.0f} cycles, {(a[:, 9] - a[:, 1]).mean() / 100:.2f} us realtime; "
