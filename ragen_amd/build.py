@@ -56,6 +56,31 @@ def _compile(src, obj):
     return obj
 
 
+HOSTBOOK_SRC = os.path.join(CSRC, "hostbook.c")
+
+
+def hostbook_path():
+    import sysconfig
+    return os.path.join(OUT, "_hostbook" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_hostbook(force=False, verbose=False):
+    """The CPython extension of the dict facade's host bookkeeping (csrc/hostbook.c), gcc."""
+    import sysconfig
+    so = hostbook_path()
+    if not force and os.path.exists(so) and os.path.getmtime(so) >= os.path.getmtime(HOSTBOOK_SRC):
+        return so
+    tmp = so + ".tmp"
+    cmd = ["gcc", "-O2", "-shared", "-fPIC", "-Wall", "-I", sysconfig.get_paths()["include"], HOSTBOOK_SRC, "-o", tmp]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, so)
+    if verbose:
+        print("built", so)
+    return so
+
+
 def build(force=False, verbose=False):
     os.makedirs(OUT, exist_ok=True)
     srcs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp")))
@@ -82,6 +107,7 @@ def build(force=False, verbose=False):
         os.replace(tmp, LIB)
         if verbose:
             print("linked", LIB)
+    build_hostbook(force, verbose)
     return LIB
 
 

@@ -16,6 +16,9 @@ run.  The train seed drawn by ``random.randint`` (es_manager.py:88-89) is broadc
 0 over the process group; without a group a sharded manager needs the seed passed in.
 ``rollout_cache`` holds this shard's envs in env order (``env_lo`` = global id of the first).
 """
+import functools
+import gc
+import os
 import random
 import warnings
 from collections.abc import Sequence
@@ -131,6 +134,48 @@ def shard_sizes(n_groups_per_tag, tags, group_size, world_size, tag=None):
         _, ng, parts = shard_plan(list(n_groups_per_tag), group_size, r, world_size)
         out.append(ng * group_size if tag is None else sum(hi - lo for j, lo, hi in parts if tags[j] == tag))
     return out
+
+
+def _gc_paused(fn):
+    """Run ``fn`` with Python's cyclic collector paused.  The host bookkeeping allocates tens of
+    thousands of dicts and lists per turn (history entries, rollout-cache entries), none of them
+    cyclic garbage; with a large heap in the process (a trainer's, or the bench's inputs) the
+    collections those allocations trigger scanned the whole heap — ≈35 ms of a 8192-env turn's
+    bookkeeping on the box, whether the loop ran in Python or in C.  The collector's state is
+    restored afterwards; it runs again at its next threshold."""
+    @functools.wraps(fn)
+    def run(*a, **kw):
+        was = gc.isenabled()
+        gc.disable()
+        try:
+            return fn(*a, **kw)
+        finally:
+            if was:
+                gc.enable()
+    return run
+
+
+_BOOK_CONSTS = (_lib.FLAG_TERMINATED, _lib.FLAG_TRUNCATED, _lib.FLAG_DONE, _lib.INFO_PRESENT, _lib.INFO_EFFECTIVE,
+                _lib.INFO_VALID, _lib.INFO_SUCCESS)
+_HOSTBOOK = []
+
+
+def _hostbook():
+    """The dict facade's bookkeeping extension (ragen_amd/_build/_hostbook*.so, built with the
+    library); None when it was not built (the Python definition then runs, with a warning)."""
+    if not _HOSTBOOK:
+        import importlib.util
+        from ..build import hostbook_path
+        path = hostbook_path()
+        mod = None
+        if os.path.exists(path):
+            spec = importlib.util.spec_from_file_location("_hostbook", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+        else:
+            warnings.warn(f"{path} not built: the dict facade's bookkeeping runs in Python", RuntimeWarning)
+        _HOSTBOOK.append(mod)
+    return _HOSTBOOK[0]
 
 
 class EnvStateManager:
@@ -254,6 +299,7 @@ class EnvStateManager:
         self._reset_cache()
         return self._rc
 
+    @_gc_paused
     def _reset_cache(self):
         """The rollout cache reset() hands out (es_manager.py:92-103): per env its EnvStatus and
         a history holding the initial observation; built once, when first read."""
@@ -277,6 +323,7 @@ class EnvStateManager:
             cache["history"] = self._update_cache_history(cache["history"], state, e["max_actions_per_traj"], None)
 
     # ----------------------------------------------------------------------- step
+    @_gc_paused
     def step(self, all_env_inputs: List[Dict]):
         """es_manager.py:105-171: one kernel launch per tag for the whole turn.  Given the device
         form of the inputs (ContextManager.get_env_inputs on the device path) the turn runs
@@ -357,6 +404,17 @@ class EnvStateManager:
         return [rc[g - lo0] for g in gids_all if g in still_active]
 
     def _book(self, tg, t, inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec, rw, pen, obs):
+        """The host side of one turn for one tag (es_manager.py:130-169), in the CPython extension
+        csrc/hostbook.c: exactly _book_py (the definition; tests/test_hostbook.py compares the
+        two).  -> the global ids of the envs still active."""
+        hb = _hostbook()
+        if hb is None:
+            return self._book_py(tg, t, inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec, rw, pen, obs)
+        return hb.book(int(t), inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec, rw, pen, obs,
+                       self.envs, self._rc, int(self.env_lo), tg.env_type == "countdown",
+                       getattr(tg.batch, "note_executed", None), tg.batch.render, _BOOK_CONSTS)
+
+    def _book_py(self, tg, t, inputs, gids, rows, acts_l, m_l, flags, num_actions, info, n_exec, rw, pen, obs):
         """The host side of one turn for one tag (es_manager.py:130-169): EnvStatus, penalty and the
         history entries of the stepped envs, from the turn's device results (lists indexed by the
         tag-local row).  -> the global ids of the envs still active."""
@@ -540,6 +598,7 @@ class EnvStateManager:
             self._turn_records[-1]["err_seen"] = True
         return LazyEnvOutputs(self, inp.env_ids[still])
 
+    @_gc_paused
     def _materialize(self):
         """The host side of the pending device-path turns, in turn order: exactly what ``step``
         records per turn (``_book``), from the device record — the per-turn rewards / info /
@@ -613,6 +672,7 @@ class EnvStateManager:
             return LazyRolloutStates(self)
         return self._rollout_states_host()
 
+    @_gc_paused
     def _rollout_states_host(self):
         """The per-env metrics dicts (es_manager.py:180-205) from one device -> host copy per
         tag; the per-env lists are built from whole-array numpy results."""
