@@ -546,6 +546,16 @@ typedef struct {
   const uint8_t* active;     /* [B] (NULL: every row)                                           */
   int32_t pool_len;          /* readable bytes at pool (0: unknown); <= 1024 the wave stages
                                 the pool in LDS with the row's other loads                     */
+  /* The turn form (turn_exec != NULL; reward_int and cond are then not read): both derived
+   * from the turn record as ContextManager._build_messages prints a turn (ctx_manager.py:
+   * 248-263, es_manager.py:148-160) — the reward is an int when the turn executed no action
+   * (step() recorded the int 0) or, for a tag whose bit is set in int_reward_tags (Countdown's
+   * 0 / 1 integer rewards), when it is 0.0 or 1.0; the next user block follows unless
+   * flags[b] has RMI_FLAG_DONE or last_turn (the rollout's final turn).                     */
+  const uint8_t* turn_exec;  /* [B] actions executed this turn                                  */
+  const uint8_t* flags;      /* [B] episode flags after the turn                                */
+  uint32_t int_reward_tags;  /* bit t: tag t's 0 / 1 rewards print as ints (tags < 32)          */
+  int32_t last_turn;
 } rmi_prompt_t;
 int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, int32_t stride, int32_t* out_len,
                     int32_t* mark, uint8_t* err, rmi_stream_t stream);

@@ -134,9 +134,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
     // (lane i: piece i), and the TAG_CONST pieces' (offset, length) for every tag (lane
     // i * n_tags + t, when the pieces and tags fit the wave)
     const int tg_l = P.tag ? P.tag[b] : 0;
-    const int cond_l = P.cond ? P.cond[b] : 1;
     const double rew_l = P.reward ? P.reward[b] : 0.0;
-    const int rint_l = P.reward_int ? P.reward_int[b] : 0;
+    int cond_l, rint_l;
+    if (P.turn_exec) {  // the turn form: both from the turn record
+      rint_l = P.turn_exec[b] == 0 || (((P.int_reward_tags >> (tg_l & 31)) & 1u) && tg_l < 32 &&
+                                       (rew_l == 0.0 || rew_l == 1.0));
+      cond_l = !(P.flags[b] & RMI_FLAG_DONE) && !P.last_turn;
+    } else {
+      cond_l = P.cond ? P.cond[b] : 1;
+      rint_l = P.reward_int ? P.reward_int[b] : 0;
+    }
     int iv = 0;
     if (lane < P.n_pieces && P.pieces[lane].kind == RMI_PT_INT) iv = P.ints[(int64_t)P.pieces[lane].a * B + b];
     const bool tc_pre = P.tag_const && P.n_tags > 0 && P.n_pieces * P.n_tags <= 64;
@@ -460,7 +467,7 @@ RMI_API int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, i
   }
   if ((need_resp && (!prog->resp || !prog->resp_len || !prog->spans || prog->sep_len < 1 || prog->K < 0)) ||
       (need_obs && (!prog->obs || !prog->obs_len)) || (need_int && !prog->ints) || (need_rew && !prog->reward) ||
-      (need_if && !prog->cond) || (need_tag && (!prog->tag_const || !prog->pool || prog->n_tags < 1)))
+      (need_if && !prog->cond && !prog->turn_exec) || (prog->turn_exec && !prog->flags) || (need_tag && (!prog->tag_const || !prog->pool || prog->n_tags < 1)))
     return RMI_EINVAL;
   // row (stride + 64) + think (stride) + answer and its re-joined form (2 * stride + 64) + number
   // (64) + hand-off and piece bounds (48 ints) + digit scratch (64) + the staged pool,

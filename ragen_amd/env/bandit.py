@@ -65,6 +65,9 @@ class BanditBatch(BatchEnv):
         return ops.parse_config(enable_think, self.K, action_sep, lo_first, hi_first, prepend=prepend), \
             self.hi_is_first, 0
 
+    def parse_sel(self):
+        return self.hi_is_first
+
     def map_actions_many(self, rows, actions):
         c, s0 = self.config, int(self.config.action_space_start)
         hi, lo = c.hi_arm_name.lower(), c.lo_arm_name.lower()

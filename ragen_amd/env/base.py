@@ -79,6 +79,20 @@ class BatchEnv:
         from .. import ops
         return ops.parse_config(enable_think, self.K, action_sep, self.action_lookup(0), prepend=prepend), None, 0
 
+    def glyph_lists(self):
+        """config.grid_lookup as the render ops' glyph lists (ops.glyph_table), built once."""
+        g = self.__dict__.get("_glyph_lists")
+        if g is None:
+            from .. import ops
+            gb, gl = ops.glyph_table(self.config.grid_lookup)
+            g = self._glyph_lists = (gb.tolist(), gl.tolist())
+        return g
+
+    def parse_sel(self):
+        """The per-env lookup column of parse_setup (the part that changes with the episodes);
+        the configuration itself depends on the arguments only."""
+        return None
+
     def close(self):
         self._host = None
         self._text = None

@@ -118,9 +118,7 @@ class FrozenLakeBatch(BatchEnv):
 
     def render_rows(self):
         """FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61) of every env on the device."""
-        gb, gl = ops.glyph_table(self.config.grid_lookup)
-        return torch.ops.ragen_amd.frozenlake_render(self.desc, self.s, self.nrow, self.ncol, gb.tolist(),
-                                                     gl.tolist())
+        return torch.ops.ragen_amd.frozenlake_render(self.desc, self.s, self.nrow, self.ncol, *self.glyph_lists())
 
     def render_all(self):
         if self._text is None:

@@ -99,9 +99,8 @@ class SokobanBatch(BatchEnv):
     def render_rows(self):
         """SokobanEnv.render text mode (sokoban/env.py:53-61) of every env on the device:
         -> (UTF-8 rows u8[B, stride], lengths i32[B])."""
-        gb, gl = ops.glyph_table(self.config.grid_lookup)
-        return torch.ops.ragen_amd.sokoban_render(self.room_fixed, self.room_state, self.H, self.W, gb.tolist(),
-                                                  gl.tolist())
+        return torch.ops.ragen_amd.sokoban_render(self.room_fixed, self.room_state, self.H, self.W,
+                                                  *self.glyph_lists())
 
     def render_all(self):
         if self._text is None:

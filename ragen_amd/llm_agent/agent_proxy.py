@@ -15,6 +15,13 @@ from .ctx_manager import ContextManager
 from .es_manager import EnvStateManager
 
 
+def env_ids_of(dp: DataProto) -> np.ndarray:
+    """The env ids of a batch as int64: a device-path LazyDataProto's own array (no trip through
+    the reference's object array), else non_tensor_batch["env_ids"] converted."""
+    ids = getattr(dp, "env_ids_i64", None)
+    return ids if ids is not None else np.asarray(dp.non_tensor_batch["env_ids"], dtype=np.int64)
+
+
 class ScriptedActor:
     """Stand-in LLM: returns one response text per env from a user callable
     ``policy(env_id, turn) -> str`` (no tokenizer round trip: non_tensor 'response_texts')."""
@@ -49,7 +56,7 @@ class TokenActor:
         self.prompts = []
 
     def generate_sequences(self, lm_inputs: DataProto) -> DataProto:
-        env_ids = np.asarray(lm_inputs.non_tensor_batch["env_ids"], dtype=np.int64)
+        env_ids = env_ids_of(lm_inputs)
         if self.read_prompts:
             b = lm_inputs.batch
             self.prompt_shapes.append(tuple(b["input_ids"].shape))

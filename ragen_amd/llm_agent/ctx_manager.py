@@ -179,8 +179,9 @@ class DeviceEnvInputs:
     the parse (rmi_detok_parse), or on first access to ``text`` / ``text_len`` / ``err``.
     Iterating it yields the reference's env-input dicts (host decode + parse), built lazily."""
 
-    def __init__(self, ctx, env_ids, env_ids_t, ids, n_ids, stride):
-        self.ctx, self.env_ids, self.env_ids_t = ctx, env_ids, env_ids_t
+    def __init__(self, ctx, env_ids, rows_t, ids, n_ids, stride):
+        # rows_t: the generations' rows of the env batch (device), None = every env in order
+        self.ctx, self.env_ids, self.rows_t = ctx, env_ids, rows_t
         self.ids, self.n_ids, self.stride = ids, n_ids, stride
         self.vocab = ctx.device_vocab
         self._text = self._text_len = self._err = None
@@ -235,17 +236,46 @@ class DeviceEnvInputs:
 
 
 class _LazyNonTensor(dict):
-    """non_tensor_batch of a LazyDataProto: 'env_ids' eager, any other access builds the batch."""
+    """non_tensor_batch of a LazyDataProto: 'env_ids' (and, with a device batch, 'group_ids')
+    as the reference's object arrays, converted from the owner's int64 ids on first read; any
+    other access builds the batch."""
 
-    def __init__(self, owner, env_ids):
-        super().__init__(env_ids=env_ids)
+    _IDS = ("env_ids", "group_ids")
+
+    def __init__(self, owner):
+        super().__init__()
         self._owner = owner
 
+    def _ids(self, k):
+        o = self._owner
+        if k == "env_ids":
+            v = o.env_ids_i64.astype(object)
+        elif o._group_size:
+            v = (o.env_ids_i64 // o._group_size).astype(object)
+        else:
+            return None
+        dict.__setitem__(self, k, v)
+        return v
+
     def __missing__(self, k):
+        if k in self._IDS and self._ids(k) is not None:
+            return dict.__getitem__(self, k)
         self._owner._build()
         return dict.__getitem__(self, k)
 
+    def __contains__(self, k):
+        return dict.__contains__(self, k) or k == "env_ids" or (k == "group_ids" and bool(self._owner._group_size))
+
+    def get(self, k, default=None):
+        return self[k] if k in self else default
+
+    def __len__(self):
+        return dict.__len__(self._full())
+
     def _full(self):
+        for k in self._IDS:
+            if not dict.__contains__(self, k):
+                self._ids(k)
         self._owner._build()
         return self
 
@@ -269,11 +299,15 @@ class LazyDataProto(DataProto):
 
     def __init__(self, env_ids, build):
         self._build_fn, self._built, self._batch = build, False, None
-        self.non_tensor_batch = _LazyNonTensor(self, np.asarray(env_ids, dtype=object))
+        # the ids as int64 (what the device path and a device-resident actor read); the
+        # reference's object arrays are made from them on first read of non_tensor_batch
+        self.env_ids_i64 = np.asarray(env_ids, np.int64)
+        self._group_size = 0
+        self.non_tensor_batch = _LazyNonTensor(self)
         self.meta_info = {}
 
     def __len__(self):
-        return len(dict.__getitem__(self.non_tensor_batch, "env_ids"))
+        return len(self.env_ids_i64)
 
     def set_device_batch(self, batch: dict, env_ids, group_size: int):
         """The device prompt path: the tensors are built already (on the GPU), and so are
@@ -282,8 +316,11 @@ class LazyDataProto(DataProto):
         self._batch = TensorBatch(batch)
         self._device_batch = True
         ids = np.asarray(env_ids, np.int64)
-        dict.__setitem__(self.non_tensor_batch, "group_ids", np.array((ids // group_size).tolist(), dtype=object))
-        dict.__setitem__(self.non_tensor_batch, "env_ids", np.array(ids.tolist(), dtype=object))
+        if ids is not self.env_ids_i64 and not np.array_equal(ids, self.env_ids_i64):
+            self.env_ids_i64 = ids
+            dict.pop(self.non_tensor_batch, "env_ids", None)
+        self._group_size = int(group_size)
+        dict.pop(self.non_tensor_batch, "group_ids", None)
 
     @property
     def batch(self):
@@ -583,19 +620,25 @@ class ContextManager:
         dev = self.device
         resp = lm_outputs.batch["responses"].to(dev)
         env_ids = np.asarray(lm_outputs.non_tensor_batch["env_ids"], dtype=np.int64)
-        idx = torch.from_numpy(env_ids).to(dev)
         R = resp.shape[1]
-        ids = torch.zeros(self.n_envs, R, dtype=torch.int64, device=dev)
-        n_ids = torch.zeros(self.n_envs, dtype=torch.int32, device=dev)
-        ids[idx - self.env_lo] = resp.to(torch.int64)
-        n_ids[idx - self.env_lo] = R
+        lo, n = self.env_lo, self.n_envs
+        if len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n)):
+            # every env in order: the generations are the rows (n_ids = None: R ids each)
+            rows_t, n_ids = None, None
+            ids = resp.to(torch.int64).contiguous()
+        else:
+            rows_t = torch.from_numpy(env_ids - lo).to(dev)
+            ids = torch.zeros(n, R, dtype=torch.int64, device=dev)
+            n_ids = torch.zeros(n, dtype=torch.int32, device=dev)
+            ids[rows_t] = resp.to(torch.int64)
+            n_ids[rows_t] = R
         # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
         # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
         # the decode and refused by the step (ValueError)
         raw = vocab.raw_len[resp.clamp(0, vocab.raw_len.numel() - 1)]
         raw_max = int(raw.sum(1).max()) if resp.numel() else 0
         stride = max(4, min(PARSE_MAX_ROW, (3 * raw_max + 7) // 4 * 4))
-        return DeviceEnvInputs(self, env_ids, idx, ids, n_ids, stride)
+        return DeviceEnvInputs(self, env_ids, rows_t, ids, n_ids, stride)
 
     def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:
         """ctx_manager.py:354-356.  The rollout states of the attached env manager's device path

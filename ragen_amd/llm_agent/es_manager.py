@@ -32,7 +32,7 @@ from .. import _lib
 from .. import distributed as rd
 from ..env import REGISTERED_ENV_CONFIGS, REGISTERED_ENVS
 from ..env.base import BatchEnv
-from ..torch_ops import ep_args, parse_cfg_bytes
+from ..torch_ops import ep_args, parse_cfg_words
 
 
 @dataclass
@@ -208,6 +208,8 @@ class EnvStateManager:
         self._untrimmed = None
         self.rollout_id = 0
         self._turn = 0
+        self._all_active = False
+        self.reset_render = None
         self._turn_records = []  # device-path turns (ContextManager's device prompts read them too)
         self._mat_upto = 0       # records whose host bookkeeping is done
 
@@ -290,10 +292,13 @@ class EnvStateManager:
         self._untrimmed = None
         self._rc = None
         self._reset_pending = True
+        self._all_active = True  # every env may step (has_input = None) until a turn says otherwise
         if self.lazy_outputs:  # the device path reads env ids; the dicts wait for a reader
-            # the initial observations rendered now, on the device (decoded when read)
+            # the initial observations rendered now, on the device (decoded when read; the
+            # device prompts' first turn reads them too: reset_render)
             self._reset_rows = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags)
                                 if type(tg.batch).render is BatchEnv.render}
+            self.reset_render = (self.rollout_id, self._reset_rows)
             return LazyEnvOutputs(self, self.env_lo + np.arange(self.n_envs, dtype=np.int64))
         self._reset_rows = None
         self._reset_cache()
@@ -334,6 +339,7 @@ class EnvStateManager:
         self._materialize()
         if self._turn >= self.max_turn:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
+        self._all_active = False
         t = self._turn
         lo0 = self.env_lo
         gids_all = [int(inp["env_id"]) for inp in all_env_inputs]
@@ -508,16 +514,28 @@ class EnvStateManager:
         lo0 = self.env_lo
         for tg in self.tags:
             a, z = tg.lo - lo0, tg.hi - lo0
-            cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, prepend)
+            cfg, sel, lact = self._parse_args(tg, enable_think, action_sep, prepend)
             acts, n_act, spans, at, al, perr = torch.ops.ragen_amd.parse_actions(
-                parse_cfg_bytes(cfg), text[a:z], text_len[a:z], sel, True, int(lact))
+                cfg, text[a:z], text_len[a:z], sel, True, int(lact))
             outs.append({"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
                          "action_len": al if lact else None, "err": perr})
         self._parsed_turn(outs, has_input, err)
         return outs
 
+    def _parse_args(self, tg, enable_think, action_sep, prepend):
+        """tg.batch.parse_setup as the parse ops take it (cfg words, sel, action-text bytes); the
+        configuration is built once per argument set, the per-env column read every turn."""
+        cache = tg.batch.__dict__.setdefault("_parse_cache", {})
+        key = (bool(enable_think), action_sep, bool(prepend))
+        if key not in cache:
+            cfg, _, lact = tg.batch.parse_setup(enable_think, action_sep, prepend)
+            cache[key] = (parse_cfg_words(cfg), int(lact))
+        words, lact = cache[key]
+        return words, tg.batch.parse_sel(), lact
+
     def _parsed_turn(self, parsed, has_input, err):
         """One turn launch per tag from the tag's parse outputs (ops.parse_actions dicts)."""
+        self._all_active = False  # _step_device sets it again from the turn's active set
         lo0 = self.env_lo
         for tg, p in zip(self.tags, parsed):
             a, z = tg.lo - lo0, tg.hi - lo0
@@ -538,9 +556,9 @@ class EnvStateManager:
         outs, texts, lens, derrs = [], [], [], []
         for tg in self.tags:
             a, z = tg.lo - lo0, tg.hi - lo0
-            cfg, sel, lact = tg.batch.parse_setup(enable_think, action_sep, True)
+            cfg, sel, lact = self._parse_args(tg, enable_think, action_sep, True)
             text, tlen, derr, acts, n_act, spans, at, al, perr = torch.ops.ragen_amd.detok_parse(
-                inp.ids[a:z], inp.n_ids[a:z], v.packed, v.data, inp.stride, parse_cfg_bytes(cfg), sel, True, int(lact))
+                inp.ids[a:z], None if inp.n_ids is None else inp.n_ids[a:z], v.packed, v.data, inp.stride, cfg, sel, True, int(lact))
             outs.append({"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
                          "action_len": al if lact else None, "err": perr})
             texts.append(text)
@@ -571,8 +589,15 @@ class EnvStateManager:
             bad = int(torch.nonzero(inp.err)[0, 0])
             raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
                              "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP)")
-        has = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
-        has[inp.env_ids_t - self.env_lo] = 1
+        # the envs with a generation: all of them, every one still running (has_input = None:
+        # the turn kernels then step the envs not done), or the rows given
+        if inp.rows_t is None and self._all_active:
+            has = None
+        elif inp.rows_t is None:
+            has = torch.ones(self.n_envs, dtype=torch.uint8, device=dev)
+        else:
+            has = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
+            has[inp.rows_t] = 1
         err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
         if parsed is None:
             parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
@@ -587,9 +612,10 @@ class EnvStateManager:
         # one device -> host copy: the active set and the turn's per-env error bits, raised in
         # the step where they happen, as the reference raises inside its per-env loop
         n_in = len(inp.env_ids)
-        host = torch.cat([((flags[inp.env_ids_t - self.env_lo] & _lib.FLAG_DONE) == 0).to(torch.uint8),
-                          err]).cpu().numpy()
-        still, err_h = host[:n_in].astype(bool), host[n_in:]
+        host = torch.cat([flags, err]).cpu().numpy()
+        fl_h, err_h = host[:self.n_envs], host[self.n_envs:]
+        still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
+        self._all_active = n_in == self.n_envs and bool(still.all())
         if err_h.any():
             for tg in self.tags:
                 gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]

@@ -119,8 +119,12 @@ class DevicePrompts:
         for j, tg in enumerate(tags):
             tag[tg.lo - es.env_lo:tg.hi - es.env_lo] = j
         self.tag = torch.from_numpy(tag).to(self.device)
-        self.is_cd = torch.tensor([tg.env_type == "countdown" for tg in tags], device=self.device)[self.tag.long()]
+        # tags whose 0 / 1 rewards print as ints (Countdown's integer rewards), as a bit mask
+        if any(tg.env_type == "countdown" for tg in tags[32:]):
+            raise NotImplementedError("a Countdown tag past the 32nd tag of a shard")
+        self.int_reward_tags = sum(1 << j for j, tg in enumerate(tags) if tg.env_type == "countdown")
         prefixes = [ctx.prefix_lookup[tg.lo] for tg in tags]
+        self._max_prefix = max(len(p) for p in ctx.prefix_lookup.values())  # the start row's width bound
         lengths = [f"Max response length: {ctx.env_config_lookup[tg.lo]['max_tokens']} words (tokens)." for tg in tags]
         self._pool = bytearray()
         self._const_at = {}
@@ -180,12 +184,18 @@ class DevicePrompts:
         return prog, self._pool_dev[1], self._pool_dev[2]
 
     def _run_text(self, pieces, stride, obs, obs_len, ints, reward=None, reward_int=None, resp=None, resp_len=None,
-                  spans=None, cond=None, active=None):
+                  spans=None, cond=None, active=None, turn=None):
         prog, pool, tc = self._program(pieces)
         flat = [len(prog)] + [x for p in prog for x in p] + [self.n_tags, obs.shape[1], 0 if resp is None else
                                                              resp.shape[1], int(self.enable_think), self.K]
+        if turn is None:
+            return torch.ops.ragen_amd.prompt_text(flat, self.sep, self.n_envs, stride, pool, tc, self.tag, obs,
+                                                   obs_len, ints, reward, reward_int, resp, resp_len, spans, cond,
+                                                   active)
+        ne, flags, last = turn
         return torch.ops.ragen_amd.prompt_text(flat, self.sep, self.n_envs, stride, pool, tc, self.tag, obs, obs_len,
-                                               ints, reward, reward_int, resp, resp_len, spans, cond, active)
+                                               ints, reward, None, resp, resp_len, spans, None, active, ne, flags,
+                                               self.int_reward_tags, int(last))
 
     # ------------------------------------------------------------------ rollout steps
     def _obs(self, rows_by_tag):
@@ -223,12 +233,14 @@ class DevicePrompts:
         for e, b in rows:
             buf[e, :len(b)] = np.frombuffer(b, np.uint8)
         self._reset_obs = (torch.from_numpy(buf).to(self.device), torch.from_numpy(lens).to(self.device))
-        obs, obs_len = self._obs({j: tg.batch.render_rows() for j, tg in enumerate(es.tags)
-                                  if hasattr(tg.batch, "render_rows")})
+        rr = getattr(es, "reset_render", None)  # the rows es.reset rendered, when it did
+        rows = rr[1] if rr is not None and rr[0] == es.rollout_id else \
+            {j: tg.batch.render_rows() for j, tg in enumerate(es.tags) if hasattr(tg.batch, "render_rows")}
+        obs, obs_len = self._obs(rows)
         ints = self.mapt.clone()
         pieces = [self.tpl.head, (_lib.PT_TAG_CONST, 0, 0), "\nTurn 1:\nState:\n", (_lib.PT_OBS, 0, 0),
                   "\nYou have ", (_lib.PT_INT, 0, 0), self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
-        stride = self._stride(obs.shape[1] + max(len(p) for p in self.ctx.prefix_lookup.values()) + 1024)
+        stride = self._stride(obs.shape[1] + self._max_prefix + 1024)
         text, tlen, _, terr = self._run_text(pieces, stride, obs, obs_len, ints)
         self.len.zero_()
         self._encode(text, tlen, terr, None, stride, lambda e: self._host_first(e))
@@ -244,19 +256,21 @@ class DevicePrompts:
         eps = [tg.batch.ep for tg in self.es.tags]
         cat = (lambda xs: torch.cat(xs)) if len(eps) > 1 else (lambda xs: xs[0])  # noqa: E731
         reward = cat([ep.turn_reward[t] for ep in eps]).contiguous()
-        ne = cat([ep.turn_exec[t] for ep in eps])
-        reward_int = ((ne == 0) | (self.is_cd & ((reward == 0.0) | (reward == 1.0)))).to(torch.uint8)
+        ne = cat([ep.turn_exec[t] for ep in eps]).contiguous()
+        # the reward's int form and the next block's condition come from the turn record on the
+        # device (the prompt op's turn form): turn_exec, flags, the Countdown tags, the last turn
         flags = d["flags"]
-        cond = (((flags & _lib.FLAG_DONE) == 0) & (t + 1 < self.max_turn)).to(torch.uint8)
         ints = d["left"]
         pieces = [self.tpl.a_pre, (_lib.PT_RESPONSE, 0, 0), self.tpl.a_suf, (_lib.PT_MARK, 0, 0),
                   (_lib.PT_IF, 0, 0), self.tpl.u_pre + "Reward:\n", (_lib.PT_REWARD, 0, 0),
                   f"\n\nTurn {t + 2}:\nState:\n", (_lib.PT_OBS, 0, 0), "\nYou have ", (_lib.PT_INT, 0, 0), self._c_mid,
                   (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
         stride = self._stride(resp.shape[1] + obs.shape[1] + 1024)
-        text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, reward_int, resp,
-                                                resp_len, spans, cond, d["has"])
-        self._encode(text, tlen, terr, mark, stride, lambda e: self._host_turn(e, t, bool(cond[e])),
+        last = t + 1 >= self.max_turn
+        text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, None, resp,
+                                                resp_len, spans, None, d["has"], turn=(ne, flags, last))
+        self._encode(text, tlen, terr, mark, stride,
+                     lambda e: self._host_turn(e, t, not last and not int(flags[e]) & _lib.FLAG_DONE),
                      active=d["has"])
         self.turns_done = t + 1
 

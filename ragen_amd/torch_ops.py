@@ -1,7 +1,8 @@
 """The hot path as PyTorch custom operators: ``torch.ops.ragen_amd.*``.
 
 Every entry point of the C ABI (include/ragen_amd.h) is registered with the dispatcher through
-``torch.library.custom_op`` — a schema (argument types, which tensors an op mutates in place),
+``torch.library`` (``Library.define`` + ``impl``, see ``_Op``) — a schema inferred from the
+implementation's annotations (argument types, which tensors an op mutates in place),
 a CUDA (= HIP on ROCm) implementation that enqueues the HIP kernel on the current stream of
 the tensors' device, and a fake (meta) implementation so shape propagation, FakeTensor
 tracing and ``torch.compile`` see the ops as opaque nodes.  The trainer-facing facades
@@ -20,7 +21,6 @@ from typing import List, Optional, Tuple
 
 import torch
 from torch import Tensor
-from torch.library import custom_op
 
 from . import _lib, ops
 
@@ -31,8 +31,36 @@ FILTER = {"std": 0, "std_rev": 1}
 VARIANT = {"legacy": 0, "masked": 1}
 
 
+_LIB = torch.library.Library(NS, "DEF")
+_NAMES = []
+
+
+class _Op:
+    """One operator: the schema inferred from the implementation's annotations (mutated
+    arguments marked ``Tensor(a!)``), the implementation registered for the CUDA dispatch key,
+    a fake kernel added with ``.register_fake``.  Registered through ``torch.library.Library``
+    rather than ``custom_op``: the same dispatcher op, without custom_op's Python autograd and
+    alias-check layers around every call (≈12 µs a call on the host, and the turn loop makes
+    a dozen calls per turn)."""
+
+    def __init__(self, name, fn, mutates):
+        self.name = name
+        _LIB.define(name + torch.library.infer_schema(fn, mutates_args=tuple(mutates)))
+        _LIB.impl(name, fn, "CUDA")
+        _NAMES.append(name)
+        self.__wrapped__ = fn
+        self.__doc__, self.__name__ = fn.__doc__, fn.__name__
+
+    def register_fake(self, fake):
+        torch.library.register_fake(f"{NS}::{self.name}", fake, lib=_LIB)
+        return fake
+
+    def __call__(self, *args, **kwargs):
+        return getattr(torch.ops.ragen_amd, self.name)(*args, **kwargs)
+
+
 def _op(name, mutates=()):
-    return custom_op(f"{NS}::{name}", mutates_args=tuple(mutates), device_types="cuda")
+    return lambda fn: _Op(name, fn, mutates)
 
 
 def _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec) -> ops.EpisodeState:
@@ -609,17 +637,23 @@ def _(ids, n_ids, vocab_packed, vocab_bytes, stride):
             ids.new_empty(B, dtype=torch.uint8))
 
 
-def parse_cfg_bytes(cfg: _lib.ParseCfg) -> List[int]:
-    """An rmi_parse_cfg_t as the list of its bytes (the form the parse op takes)."""
+def parse_cfg_words(cfg: _lib.ParseCfg) -> List[int]:
+    """An rmi_parse_cfg_t as little-endian signed 64-bit words (the form the parse ops take: a
+    192-byte struct is 24 list items, not 192 — each list item costs the dispatcher a conversion)."""
     import ctypes
-    return list(ctypes.string_at(ctypes.addressof(cfg), ctypes.sizeof(cfg)))
+    import struct
+    b = ctypes.string_at(ctypes.addressof(cfg), ctypes.sizeof(cfg))
+    b += b"\0" * (-len(b) % 8)
+    return list(struct.unpack(f"<{len(b) // 8}q", b))
 
 
-def _parse_cfg(cfg_bytes: List[int]) -> _lib.ParseCfg:
+def _parse_cfg(cfg_words: List[int]) -> _lib.ParseCfg:
     import ctypes
-    if len(cfg_bytes) != ctypes.sizeof(_lib.ParseCfg):
-        raise ValueError("cfg must be the bytes of an rmi_parse_cfg_t (torch_ops.parse_cfg_bytes)")
-    return _lib.ParseCfg.from_buffer_copy(bytes(cfg_bytes))
+    import struct
+    n = ctypes.sizeof(_lib.ParseCfg)
+    if len(cfg_words) != (n + 7) // 8:
+        raise ValueError("cfg must be the words of an rmi_parse_cfg_t (torch_ops.parse_cfg_words)")
+    return _lib.ParseCfg.from_buffer_copy(struct.pack(f"<{len(cfg_words)}q", *cfg_words)[:n])
 
 
 @_op("parse_actions")
@@ -731,9 +765,10 @@ def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, par
             text.new_empty(B, dtype=torch.uint8))
 
 
-def prompt_struct(program: List[int], sep: List[int], tensors) -> _lib.Prompt:
+def prompt_struct(program: List[int], sep: List[int], tensors, turn=None) -> _lib.Prompt:
     """program = [n_pieces, (kind, a, b) * n_pieces, n_tags, obs_stride, resp_stride, enable_think, K];
-    tensors = (pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active)."""
+    tensors = (pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active);
+    turn = (turn_exec, flags, int_reward_tags, last_turn): the turn form (rmi_prompt_t)."""
     pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active = tensors
     n = program[0]
     if n > _lib.PROMPT_MAX_PIECES or len(program) != 1 + 3 * n + 5 or len(sep) > 16:
@@ -752,6 +787,9 @@ def prompt_struct(program: List[int], sep: List[int], tensors) -> _lib.Prompt:
         P.sep[i] = x
     P.cond, P.active = _ptr(cond), _ptr(active)
     P.pool_len = pool.numel() if pool is not None else 0
+    if turn is not None and turn[0] is not None:
+        P.turn_exec, P.flags = _ptr(turn[0]), _ptr(turn[1])
+        P.int_reward_tags, P.last_turn = int(turn[2]) & 0xFFFFFFFF, int(turn[3])
     return P
 
 
@@ -760,11 +798,18 @@ def prompt_text(program: List[int], sep: List[int], B: int, stride: int, pool: O
                 tag_const: Optional[Tensor], tag: Optional[Tensor], obs: Optional[Tensor], obs_len: Optional[Tensor],
                 ints: Optional[Tensor], reward: Optional[Tensor], reward_int: Optional[Tensor], resp: Optional[Tensor],
                 resp_len: Optional[Tensor], spans: Optional[Tensor], cond: Optional[Tensor],
-                active: Optional[Tensor]) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
+                active: Optional[Tensor], turn_exec: Optional[Tensor] = None, flags: Optional[Tensor] = None,
+                int_reward_tags: int = 0, last_turn: int = 0) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
     """The prompt text one turn appends (ctx_manager.py:248-263, rmi_prompt_text)
-    -> (text u8[B, stride], text_len i32[B], mark i32[B], err u8[B])."""
+    -> (text u8[B, stride], text_len i32[B], mark i32[B], err u8[B]).  With turn_exec (and
+    flags) the turn form: reward_int / cond derived on the device (rmi_prompt_t)."""
     ts = (pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active)
-    dev = ops._dev(*ts)
+    dev = ops._dev(*ts, turn_exec, flags)
+    if turn_exec is not None:
+        if flags is None:
+            raise ValueError("the turn form needs flags with turn_exec")
+        ops._dt(turn_exec, torch.uint8, "turn_exec")
+        ops._dt(flags, torch.uint8, "flags")
     for t, dt, nm in ((pool, torch.uint8, "pool"), (tag_const, torch.int32, "tag_const"), (tag, torch.uint8, "tag"),
                       (obs, torch.uint8, "obs"), (obs_len, torch.int32, "obs_len"), (ints, torch.int32, "ints"),
                       (reward, torch.float64, "reward"), (reward_int, torch.uint8, "reward_int"),
@@ -772,7 +817,7 @@ def prompt_text(program: List[int], sep: List[int], B: int, stride: int, pool: O
                       (cond, torch.uint8, "cond"), (active, torch.uint8, "active")):
         ops._dt(t, dt, nm)
     import ctypes
-    P = prompt_struct(program, sep, ts)
+    P = prompt_struct(program, sep, ts, (turn_exec, flags, int_reward_tags, last_turn))
     out = torch.empty(B, stride, dtype=torch.uint8, device=dev)
     n = torch.empty(B, dtype=torch.int32, device=dev)
     mark = torch.empty(B, dtype=torch.int32, device=dev)
@@ -784,7 +829,7 @@ def prompt_text(program: List[int], sep: List[int], B: int, stride: int, pool: O
 
 @prompt_text.register_fake
 def _(program, sep, B, stride, pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans,
-      cond, active):
+      cond, active, turn_exec=None, flags=None, int_reward_tags=0, last_turn=0):
     t = next(x for x in (pool, obs, resp, reward) if x is not None)
     return (t.new_empty(B, stride, dtype=torch.uint8), t.new_empty(B, dtype=torch.int32),
             t.new_empty(B, dtype=torch.int32), t.new_empty(B, dtype=torch.uint8))
@@ -794,6 +839,6 @@ def _(program, sep, B, stride, pool, tag_const, tag, obs, obs_len, ints, reward,
 for _name in ("sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_reset",
               "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
               "frozenlake_reset", "bandit_step_turn", "countdown_step_turn", "rollout_finalize"):
-    torch.library.register_fake(f"{NS}::{_name}")(lambda *a, **k: None)
+    torch.library.register_fake(f"{NS}::{_name}", lambda *a, **k: None, lib=_LIB)
 
-OPS = tuple(sorted(n for n in dir(torch.ops.ragen_amd) if not n.startswith("_")))
+OPS = tuple(sorted(_NAMES))

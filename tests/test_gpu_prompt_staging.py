@@ -96,3 +96,51 @@ def test_prompt_text_staged_equals_in_place():
         tail = ("Reward:\n" + rtxt + consts[0] + bytes(obs_np[i, :obs_len_np[i]]).decode() + consts[1] +
                 str(int(ints[0, i])) + consts[2] + ("A:" if int(tag[i]) == 0 else "B:") + "\n")
         assert row.endswith(tail), (i, row[-120:], tail)
+
+
+def test_prompt_text_turn_form_equals_explicit():
+    """The turn form (turn_exec, flags, int_reward_tags, last_turn: reward_int and cond derived
+    on the device) against the same rows with reward_int / cond given: identical bytes, marks and
+    errors, for both tags (tag 1 = Countdown's integer 0 / 1 rewards), done and running envs, the
+    last turn and an earlier one."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11)
+    B, stride = 512, 1024
+    consts = ["Reward:\n", "\nTurn 3:\n", "A:", "B:", "\n"]
+    pool_bytes = b"".join(c.encode() for c in consts)
+    offs = np.cumsum([0] + [len(c.encode()) for c in consts])
+    C = lambda j: (_lib.PT_CONST, int(offs[j]), int(offs[j + 1] - offs[j]))  # noqa: E731
+    tag_const = torch.tensor([int(offs[2]), 2, int(offs[3]), 2], dtype=torch.int32, device=dev)
+    tag_np = rng.integers(0, 2, B).astype(np.uint8)
+    tag = torch.from_numpy(tag_np).to(dev)
+    obs_np = np.zeros((B, 8), np.uint8)
+    obs_np[:, :4] = np.frombuffer(b"#P_#", np.uint8)
+    obs = torch.from_numpy(obs_np).to(dev)
+    obs_len = torch.full((B,), 4, dtype=torch.int32, device=dev)
+    ints = torch.from_numpy(rng.integers(0, 9, (1, B)).astype(np.int32)).to(dev)
+    rw = rng.choice([0.0, 1.0, -0.1, 0.9, 10.0, -1.0], B)
+    reward = torch.from_numpy(rw).to(dev)
+    ne_np = rng.integers(0, 3, B).astype(np.uint8)
+    fl_np = (rng.random(B) < 0.3).astype(np.uint8) * _lib.FLAG_DONE | (rng.random(B) < 0.3).astype(np.uint8)
+    ne, fl = torch.from_numpy(ne_np).to(dev), torch.from_numpy(fl_np).to(dev)
+    pieces = [(_lib.PT_MARK, 0, 0), (_lib.PT_IF, 0, 0), C(0), (_lib.PT_REWARD, 0, 0), C(1), (_lib.PT_OBS, 0, 0),
+              (_lib.PT_INT, 0, 0), (_lib.PT_TAG_CONST, 0, 0), C(4)]
+    prog = _program(pieces, 2, obs.shape[1], 0)
+    pad = (-len(pool_bytes)) % 4 + 4
+    pool = torch.frombuffer(bytearray(pool_bytes) + b"\0" * pad, dtype=torch.uint8).to(dev)
+    R = torch.ops.ragen_amd
+    for last in (0, 1):
+        rint = ((ne_np == 0) | ((tag_np == 1) & ((rw == 0.0) | (rw == 1.0)))).astype(np.uint8)
+        cond = (((fl_np & _lib.FLAG_DONE) == 0) & (not last)).astype(np.uint8)
+        want = R.prompt_text(prog, list(b"||"), B, stride, pool, tag_const, tag, obs, obs_len, ints, reward,
+                             torch.from_numpy(rint).to(dev), None, None, None, torch.from_numpy(cond).to(dev), None)
+        got = R.prompt_text(prog, list(b"||"), B, stride, pool, tag_const, tag, obs, obs_len, ints, reward, None,
+                            None, None, None, None, None, ne, fl, 0b10, last)
+        torch.cuda.synchronize()
+        for w, g in zip(want[1:], got[1:]):  # lengths, marks, errors
+            assert torch.equal(w, g), last
+        lens = got[1].cpu().numpy()
+        tw, tg = want[0].cpu().numpy(), got[0].cpu().numpy()
+        for i in range(B):  # the bytes of each row (the buffer past a row's length is not written)
+            assert bytes(tw[i, :lens[i]]) == bytes(tg[i, :lens[i]]), (last, i)
+        assert (lens[cond == 0] == 0).all() and (lens[cond == 1] > 0).all()

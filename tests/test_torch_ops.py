@@ -72,7 +72,7 @@ def test_fake_kernels_shapes():
                                   torch.empty(B, 36, dtype=torch.uint8, device=d), 6, 6, [0] * 16, [0] * 16)
         assert out.shape == (B, torch_ops.render_stride(36, 6)) and n.dtype == torch.int32
         cfg = ops.parse_config(True, 5, "||", {1: "Up", 2: "Down"})
-        a, na, sp, at, al, e = R.parse_actions(torch_ops.parse_cfg_bytes(cfg), torch.empty(B, 64, dtype=torch.uint8,
+        a, na, sp, at, al, e = R.parse_actions(torch_ops.parse_cfg_words(cfg), torch.empty(B, 64, dtype=torch.uint8,
                                                device=d), torch.empty(B, dtype=torch.int32, device=d), None, True, 0)
         assert a.shape == (B, 5) and a.dtype == torch.int8 and sp.shape == (B, 4)
         txt, tl, te = R.detokenize(torch.empty(B, 9, dtype=torch.int64, device=d), None,
