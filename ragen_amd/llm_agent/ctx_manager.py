@@ -83,11 +83,12 @@ def assemble_batch(rows, tokenizer, all_scores, use_turn_scores: bool, enable_re
     return ids, am, pos, score, lm, rm
 
 
-def _raise_assemble_errors(err, S):
+def _raise_assemble_errors(err, S, bits=None):
     """rmi_assemble_batch's per-row bits: RMI_ERR_UNSUP = a row longer than the batch width S
     (it would have been truncated), RMI_ERR_STATE = a turn with more than one reward-token
     position (the reference's boolean-mask score assignment raises there)."""
-    overlong, multi = torch.stack([(err & _lib.ERR_UNSUP).any(), (err & _lib.ERR_STATE).any()]).cpu().tolist()
+    overlong, multi = bits if bits is not None else \
+        torch.stack([(err & _lib.ERR_UNSUP).any(), (err & _lib.ERR_STATE).any()]).cpu().tolist()
     if overlong:
         raise ValueError(f"a token row is longer than the batch width S={S}")
     if multi:
@@ -663,21 +664,20 @@ class ContextManager:
         ap = self.config.agent_proxy
         dev = self.device
         tokens, start, row_len = pr.update_rows()
-        S = int(row_len.max()) if row_len.numel() else 1
         eps = [tg.batch.ep for tg in es.tags]
         tab = (eps[0].turn_reward if len(eps) == 1 else torch.cat([ep.turn_reward for ep in eps], 1)).contiguous()
         n_sc = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
         special_token, reward_token = get_special_tokens(self.tokenizer)
+        # the longest row and the most turns, in one readback
+        S, n_slots = torch.stack([row_len.max(), n_sc.max()]).cpu().tolist() if row_len.numel() else (1, 0)
         # zip_longest's length over the WHOLE batch (ctx_manager.py:52-62): every rank's longest
         from .. import distributed as rd
-        n_slots = int(n_sc.max()) if n_sc.numel() else 0
         if self.process_group is not None and self.world_size > 1:
             n_slots = rd.all_reduce_max_int(n_slots, self.process_group, dev)
         ids, am, pos, score_tensor, loss_mask, response_mask, err = torch.ops.ragen_amd.assemble_rows(
             tokens, start, row_len, max(S, 1), int(pr.pad_id), int(special_token), int(reward_token), tab, n_sc,
             n_slots, bool(ap.use_turn_scores), bool(self.config.enable_response_mask),
             "qwen" in self.tokenizer.name_or_path.lower())
-        _raise_assemble_errors(err, S)
         normalized = score_tensor
         if not ap.use_turn_scores:
             normalized = self._normalize_device(score_tensor, es)
@@ -685,7 +685,11 @@ class ContextManager:
         row_resp = response_mask.sum(dim=-1).float()
         if self.process_group is not None and self.world_size > 1:
             row_resp = rd.all_gather_rows(row_resp, group=self.process_group, sizes=self.shard_sizes())
-        response_length = row_resp.mean().item()
+        # the assembly's error bits and the mean in one readback (the errors raise first)
+        overlong, multi, response_length = torch.stack([(err & _lib.ERR_UNSUP).any().double(),
+                                                        (err & _lib.ERR_STATE).any().double(),
+                                                        row_resp.mean().double()]).cpu().tolist()
+        _raise_assemble_errors(None, S, (overlong, multi))
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
                  "loss_mask": loss_mask, "rm_scores": normalized, "original_rm_scores": normalized}
         env_ids = es.env_lo + np.arange(es.n_envs, dtype=np.int64)

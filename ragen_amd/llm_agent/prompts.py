@@ -145,6 +145,7 @@ class DevicePrompts:
             raise NotImplementedError("the generation prompt does not encode like the host tokenizer")
         self.tail = torch.tensor(tail, dtype=torch.int64, device=self.device)
         self.host_rows_used = 0
+        self._pending = None  # (bad rows u8/bool[B] on the device, their host builder), not read back yet
         self.rollout = None
         self.turns_done = 0
         self._verify()
@@ -209,8 +210,10 @@ class DevicePrompts:
             else:
                 r, ln = self._reset_obs[0][tg.lo - self.es.env_lo:tg.hi - self.es.env_lo], \
                     self._reset_obs[1][tg.lo - self.es.env_lo:tg.hi - self.es.env_lo]
-            parts.append(torch.nn.functional.pad(r, (0, st - r.shape[1])))
+            parts.append(r if r.shape[1] == st else torch.nn.functional.pad(r, (0, st - r.shape[1])))
             lens.append(ln)
+        if len(parts) == 1:
+            return parts[0].contiguous(), lens[0].contiguous()
         return torch.cat(parts).contiguous(), torch.cat(lens).contiguous()
 
     def start(self):
@@ -279,6 +282,9 @@ class DevicePrompts:
         return min(3072, (int(n) + 3) // 4 * 4)
 
     def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None):
+        """Tokenize the rows onto the arena; the rows the device could not build are left for
+        the host (``_resolve``), read back with the next readback of the arena lengths."""
+        self._resolve()  # an earlier turn's host rows come first in the arena
         mx = int(tlen.max()) if tlen.numel() else 0
         n_tok, mark_tok, err = self.dt.encode_rows(text, tlen, self.arena, self.len, mark, max_len=max(mx, 4))
         bad = (err != 0) | (terr != 0)
@@ -287,6 +293,16 @@ class DevicePrompts:
         if mark is not None:  # the update batch ends after the assistant block
             upd = torch.where(active.bool(), mark_tok, self.len_upd) if active is not None else mark_tok
             self.len_upd.copy_(upd)
+        self._pending = (bad, host_fn)
+
+    def _resolve(self, any_bad=None):
+        """Build the pending host rows (``any_bad``: their any() already read back)."""
+        if self._pending is None:
+            return
+        bad, host_fn = self._pending
+        self._pending = None
+        if any_bad is False:
+            return
         idx = torch.nonzero(bad).flatten().cpu().tolist()
         if idx:
             self.host_rows_used += len(idx)
@@ -335,12 +351,22 @@ class DevicePrompts:
     def gen_batch(self, env_ids: np.ndarray):
         """get_lm_inputs(prepare_for_update=False)'s tensors for these envs (device)."""
         rows = torch.from_numpy(np.asarray(env_ids, np.int64) - self.es.env_lo).to(self.device)
-        S = int(self.len[rows].max()) + self.tail.numel() if rows.numel() else 1
+        if not rows.numel():
+            self._resolve()
+            S = 1
+        elif self._pending is not None:  # one readback: the longest row and whether any row is the host's
+            mx, any_bad = torch.stack([self.len[rows].max().to(torch.int64),
+                                       self._pending[0].any().to(torch.int64)]).cpu().tolist()
+            self._resolve(bool(any_bad))
+            S = (int(self.len[rows].max()) if any_bad else mx) + self.tail.numel()
+        else:
+            S = int(self.len[rows].max()) + self.tail.numel()
         ids, am, pos, err = torch.ops.ragen_amd.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
         return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
 
     def update_rows(self):
         """(tokens, row_start, row_len) of formulate_rollouts' rows, env order."""
+        self._resolve()
         start = torch.arange(self.n_envs, dtype=torch.int64, device=self.device) * self.cap
         return self.arena.view(-1), start, self.len_upd
 
