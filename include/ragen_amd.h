@@ -481,6 +481,13 @@ typedef struct {
   const int32_t* added_off; /* [n_added + 1]                                                 */
   const int32_t* added_id;  /* [n_added]                                                     */
   uint32_t added_first[8];  /* bitmap of the added tokens' first bytes                       */
+  /* Word cache (NULL: off): (word_cache_mask + 1) entries of 16 u32 in HBM, zero-initialised
+   * once and kept across calls for this tokenizer's tables — a pre-token's bytes (2..16) ->
+   * its BPE ids (<= 11).  A pre-token's merges depend on its bytes alone (the tokenizers
+   * crate caches words the same way), so a hit skips its pair lookups and merges.  Entries
+   * are claimed with an atomic compare-and-swap and published with a release store.        */
+  uint32_t* word_cache;
+  uint32_t word_cache_mask; /* entries - 1 (a power of two minus one)                        */
 } rmi_bpe_t;
 
 /* Row b: text[b * pitch .. + text_len[b]) (UTF-8; pitch % 4 == 0); `stride` (% 4 == 0,

@@ -74,6 +74,90 @@ __device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a,
   }
 }
 
+// ---- the word cache (rmi_bpe_t.word_cache): 16 u32 per entry — the word's bytes (4 u32,
+// zero padded), meta = ready | claimed | count << 8 | length, up to 9 ids, and a 64-bit check
+// of all of them.  Linear probing over kWcProbe slots; a slot is claimed by compare-and-swap on
+// meta (0 -> claimed) and written once.  No acquire / release: the 8 XCDs' L2s are not coherent
+// with each other inside a launch, and agent-scope ordering would write back / invalidate L2 on
+// every probe.  A reader may therefore see an older state of a slot — empty, claimed, or a
+// partly written entry — and takes only an entry whose check matches its contents; anything
+// else is a miss (the word is merged as before, and maybe inserted again one slot on).
+// Launch boundaries make every XCD's entries visible to the next call.
+constexpr int kWcWordMax = 16, kWcIdsMax = 9, kWcProbe = 8;
+constexpr uint32_t kWcReady = 1u << 31, kWcClaimed = 1u << 30;
+
+__device__ __forceinline__ void wc_key(const uint8_t* w, int len, uint32_t k[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) k[i] = 0;
+#pragma unroll
+  for (int i = 0; i < kWcWordMax; ++i)  // w has kWcWordMax readable bytes (the row's zero tail)
+    k[i >> 2] |= (i < len ? (uint32_t)w[i] : 0u) << (8 * (i & 3));
+}
+
+__device__ __forceinline__ uint64_t wc_mix(uint64_t h, uint32_t v) {
+  h = (h ^ v) * 0x100000001B3ull;
+  return h ^ (h >> 31);
+}
+
+__device__ __forceinline__ uint32_t wc_slot(const uint32_t k[4], int len, uint32_t mask) {
+  uint64_t x = (((uint64_t)k[1] << 32) | k[0]) * 0x9E3779B97F4A7C15ull;
+  x ^= ((((uint64_t)k[3] << 32) | k[2]) + (uint64_t)len) * 0xC2B2AE3D27D4EB4Full;
+  x ^= x >> 29;
+  return (uint32_t)(x >> 32) & mask;
+}
+
+__device__ __forceinline__ uint64_t wc_check(const uint32_t k[4], uint32_t meta) {
+  uint64_t h = 0xCBF29CE484222325ull;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) h = wc_mix(h, k[i]);
+  return wc_mix(h, meta);
+}
+
+// -> the word's id count (ids written to Y[0..)), or 0 on a miss
+__device__ int wc_find(const rmi_bpe_t& t, const uint32_t k[4], int len, int32_t* Y) {
+  uint32_t h = wc_slot(k, len, t.word_cache_mask);
+  for (int i = 0; i < kWcProbe; ++i, h = (h + 1) & t.word_cache_mask) {
+    const uint32_t* s = t.word_cache + 16 * (size_t)h;
+    const uint4 w0 = reinterpret_cast<const uint4*>(s)[0];
+    const uint4 w1 = reinterpret_cast<const uint4*>(s)[1];
+    const uint32_t m = w1.x;
+    if (m == 0) return 0;
+    if (!(m & kWcReady) || (int)(m & 0xFF) != len || w0.x != k[0] || w0.y != k[1] || w0.z != k[2] || w0.w != k[3])
+      continue;
+    const int cnt = (int)((m >> 8) & 0xFF);
+    if (cnt < 1 || cnt > kWcIdsMax) continue;
+    uint64_t c = wc_check(k, m);
+    for (int q = 0; q < cnt; ++q) {
+      const uint32_t id = s[5 + q];
+      c = wc_mix(c, id);
+      Y[q] = (int32_t)id;
+    }
+    if ((((uint64_t)s[15] << 32) | s[14]) == c) return cnt;
+  }
+  return 0;
+}
+
+// the ids: the symbol chain from a (Y at each symbol start, M the next start)
+__device__ void wc_insert(const rmi_bpe_t& t, const uint32_t k[4], int len, const int32_t* Y, const uint16_t* M,
+                          int a, int cnt) {
+  uint32_t h = wc_slot(k, len, t.word_cache_mask);
+  for (int i = 0; i < kWcProbe; ++i, h = (h + 1) & t.word_cache_mask) {
+    uint32_t* s = t.word_cache + 16 * (size_t)h;
+    if (atomicCAS(s + 4, 0u, kWcClaimed) != 0u) continue;
+    const uint32_t m = kWcReady | ((uint32_t)cnt << 8) | (uint32_t)len;
+    uint64_t c = wc_check(k, m);
+    *reinterpret_cast<uint4*>(s) = make_uint4(k[0], k[1], k[2], k[3]);
+    for (int q = 0, p = a; q < cnt; ++q, p = M[p]) {
+      s[5 + q] = (uint32_t)Y[p];
+      c = wc_mix(c, (uint32_t)Y[p]);
+    }
+    s[14] = (uint32_t)c;
+    s[15] = (uint32_t)(c >> 32);
+    s[4] = m;
+    return;
+  }
+}
+
 __device__ __forceinline__ int utf8_len(uint32_t b) {
   return b < 0x80 ? 1 : (b >= 0xC2 && b <= 0xDF) ? 2 : (b >= 0xE0 && b <= 0xEF) ? 3 : (b >= 0xF0 && b <= 0xF4) ? 4 : 0;
 }
@@ -462,11 +546,28 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   RMI_STAMP(2);
   // ---- 5. BPE: symbols, pair ranks, merges (one lane per pre-token)
   // piece bounds: P[j] .. P[j+1] (or n); the symbol chain in M: next symbol start or kEnd
+  // A word found in the word cache gets its ids as the symbols a .. a+cnt-1 and its bytes
+  // marked B_IN (no pair lookups below); K[j]'s top bit tells the merge loop to skip it.
   for (int j = lane; j < np; j += 64) {
     const int a = L.P[j], e = j + 1 < np ? L.P[j + 1] : n;
+    L.K[j] = 0;
     if (L.C[a] & B_ADD) {  // an added token: one symbol, id set in phase 2
       L.M[a] = kEnd;
       continue;
+    }
+    const int len = e - a;
+    if (tok.word_cache && len >= 2 && len <= kWcWordMax) {
+      uint32_t k[4];
+      wc_key(L.T + a, len, k);
+      const int cnt = wc_find(tok, k, len, L.Y + a);
+      if (cnt > 0) {
+        for (int q = a; q < e; ++q) {
+          L.M[q] = q + 1 < a + cnt ? (uint16_t)(q + 1) : kEnd;
+          L.C[q] |= B_IN;
+        }
+        L.K[j] = (uint16_t)(0x8000 | cnt);
+        continue;
+      }
     }
     for (int q = a; q < e; ++q) {
       L.Y[q] = L.BID[L.T[q]];
@@ -512,6 +613,10 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   // slower: 78-95 k cycles per wave against 75 k.)
   for (int j = lane; j < np; j += 64) {
     const int a = L.P[j];
+    if (L.K[j] & 0x8000) {  // from the word cache
+      L.K[j] &= 0x7FFF;
+      continue;
+    }
     int cnt = 1;
     if (!(L.C[a] & B_ADD)) {
       for (;;) {
@@ -535,6 +640,12 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
       }
       cnt = 0;
       for (int q = a; q != kEnd; q = L.M[q]) ++cnt;
+      const int len = (j + 1 < np ? L.P[j + 1] : n) - a;
+      if (tok.word_cache && len >= 2 && len <= kWcWordMax && cnt <= kWcIdsMax) {
+        uint32_t k[4];
+        wc_key(L.T + a, len, k);
+        wc_insert(tok, k, len, L.Y, L.M, a, cnt);
+      }
     }
     L.K[j] = (uint16_t)cnt;
   }

@@ -164,7 +164,8 @@ class Bpe(ctypes.Structure):
                 ("merges", ctypes.c_void_p), ("merge_mask", ctypes.c_uint32), ("merge_shift", ctypes.c_uint32),
                 ("pretok", ctypes.c_int32), ("nfc", ctypes.c_int32), ("n_added", ctypes.c_int32),
                 ("added_bytes", ctypes.c_void_p), ("added_off", ctypes.c_void_p), ("added_id", ctypes.c_void_p),
-                ("added_first", ctypes.c_uint32 * 8)]
+                ("added_first", ctypes.c_uint32 * 8), ("word_cache", ctypes.c_void_p),
+                ("word_cache_mask", ctypes.c_uint32)]
 
 
 def _backend_json(tokenizer) -> dict:
@@ -249,6 +250,10 @@ class DeviceTokenizer:
     added_id: torch.Tensor
     added_first: List[int]
     added: dict  # content -> id
+    # the word cache (rmi_bpe_t.word_cache): i32[(mask + 1) * 16], zeroed once; None = off
+    word_cache: Optional[torch.Tensor] = None
+
+    WORD_CACHE_ENTRIES = 1 << 15  # 2 MB: the distinct pre-tokens of the prompts with room to spare
 
     @staticmethod
     def from_hf(tokenizer, device) -> "DeviceTokenizer":
@@ -304,7 +309,8 @@ class DeviceTokenizer:
         return DeviceTokenizer(
             t(blk.astype(np.int16).view(np.int16)), t(cls), t(byte_id), t(table.view(np.int64)), mask, shift, pretok,
             int(norm is not None), t(np.frombuffer(data, np.uint8).copy()), t(off),
-            t(np.array(list(added.values()) or [0], np.int32)), first, added)
+            t(np.array(list(added.values()) or [0], np.int32)), first, added,
+            torch.zeros(DeviceTokenizer.WORD_CACHE_ENTRIES * 16, dtype=torch.int32, device=device))
 
     def struct(self) -> Bpe:
         s = Bpe(self.cp_block.data_ptr(), self.cp_class.data_ptr(), self.byte_id.data_ptr(), self.merges.data_ptr(),
@@ -312,6 +318,8 @@ class DeviceTokenizer:
                 self.added_bytes.data_ptr(), self.added_off.data_ptr(), self.added_id.data_ptr())
         for i, w in enumerate(self.added_first):
             s.added_first[i] = w
+        if self.word_cache is not None:
+            s.word_cache, s.word_cache_mask = self.word_cache.data_ptr(), self.word_cache.numel() // 16 - 1
         return s
 
     def args(self):
@@ -325,7 +333,8 @@ class DeviceTokenizer:
                     max_len: int = 0):
         """Append the ids of every text row to ``out`` (rmi_bpe_encode); max_len (0: the row
         pitch) bounds the rows' length.  -> (n_tok, mark_tok, err)."""
-        return torch.ops.ragen_amd.bpe_encode(*self.args(), text, text_len, out, out_len, mark_byte, int(max_len))
+        return torch.ops.ragen_amd.bpe_encode(*self.args(), text, text_len, out, out_len, mark_byte, int(max_len),
+                                              self.word_cache)
 
     def encode(self, texts: Sequence[str], stride: int = None) -> List[Optional[List[int]]]:
         """Convenience (tests, tools): ids of each text, or None for a row the device flagged."""

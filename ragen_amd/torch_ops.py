@@ -712,7 +712,7 @@ def _(ids, n_ids, vocab_packed, vocab_bytes, stride, cfg, sel, with_spans, actio
             ids.new_empty(B, dtype=torch.uint8))
 
 
-def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params):
+def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache=None):
     from .tokenizer import Bpe
     ops._dev(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id)
     if len(params) != 13:
@@ -721,19 +721,27 @@ def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, add
             params[2], params[3], params[4], added_bytes.data_ptr(), added_off.data_ptr(), added_id.data_ptr())
     for i in range(8):
         s.added_first[i] = params[5 + i] & 0xFFFFFFFF
+    if word_cache is not None:
+        ops._dev(word_cache)
+        ops._dt(word_cache, torch.int32, "word_cache")
+        n = word_cache.numel() // 16
+        if n < 1 or n & (n - 1) or word_cache.numel() != 16 * n:
+            raise ValueError("word_cache: 16 int32 per entry, a power-of-two number of entries")
+        s.word_cache, s.word_cache_mask = word_cache.data_ptr(), n - 1
     return s
 
 
-@_op("bpe_encode", ("out", "out_len"))
+@_op("bpe_encode", ("out", "out_len", "word_cache"))
 def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tensor, added_bytes: Tensor,
                added_off: Tensor, added_id: Tensor, params: List[int], text: Tensor, text_len: Tensor, out: Tensor,
-               out_len: Optional[Tensor], mark_byte: Optional[Tensor], max_len: int = 0) -> Tuple[Tensor, Tensor, Tensor]:
+               out_len: Optional[Tensor], mark_byte: Optional[Tensor], max_len: int = 0,
+               word_cache: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """The tokenizer call of get_lm_inputs (ctx_manager.py:265-278) for a byte-level BPE:
     every text row's ids appended to ``out`` (rmi_bpe_encode; tables: ragen_amd.tokenizer).
     max_len (0: the row pitch) bounds the rows' length and sizes the kernel's LDS.
     -> (n_tok i32[B], mark_tok i32[B], err u8[B])."""
     import ctypes
-    tok = _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params)
+    tok = _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache)
     ops._dev(text, text_len, out, out_len, mark_byte)
     ops._dt(text, torch.uint8, "text")
     ops._dt(text_len, torch.int32, "text_len")
@@ -759,7 +767,7 @@ def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tens
 
 @bpe_encode.register_fake
 def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, text, text_len, out, out_len,
-      mark_byte, max_len=0):
+      mark_byte, max_len=0, word_cache=None):
     B = text.shape[0]
     return (text.new_empty(B, dtype=torch.int32), text.new_empty(B, dtype=torch.int32),
             text.new_empty(B, dtype=torch.uint8))

@@ -83,3 +83,31 @@ def test_encode_append_mark_and_overflow(device, qwen_tok):
     assert mark_tok.cpu().tolist()[0] == len(enc(a[0])) + len(enc(b[0][:mark[0].item()]))
     assert e[2] == _lib.ERR_UNSUP and ol[2] == len(enc(a[2]))  # 600 q's do not fit after row 2's first tokens
     assert (o[2, ol[2]:] == -7).all()
+
+
+def test_word_cache_warm_cold_and_torn(device, qwen_tok):
+    """The word cache (rmi_bpe_t.word_cache): the same rows encoded cold (cache empty, words
+    inserted by many waves at once), warm (every word found) and with the cache off give the
+    tokenizers library's ids; entries whose contents no longer match their check (what a reader
+    sees of a half-written entry) are ignored, not used."""
+    back = qwen_tok.backend_tokenizer
+    cases = EDGE + fuzz(1500, seed=9)
+    text = ("<|im_start|>user\nYou are solving the Sokoban puzzle.\nTurn 1:\nState:\n######\n#_P_O#\n#__X_#\n"
+            "######\nYou have 10 actions left. Always output: <think> [Your thoughts] </think> <answer> [your "
+            "answer] </answer> with no extra text.<|im_end|>\n")
+    rows = cases + [text] * 4096  # the same words in thousands of rows of one launch
+    want = [back.encode(s, add_special_tokens=False).ids for s in cases + [text]]
+    want += want[-1:] * 4095
+    dt = DeviceTokenizer.from_hf(qwen_tok, device)
+    assert dt.word_cache is not None
+    for run in ("cold", "warm"):
+        got = dt.encode(rows)
+        assert got == want, run
+    wc = dt.word_cache.view(-1, 16)
+    ready = wc[:, 4] < 0  # the ready bit (bit 31)
+    assert int(ready.sum()) > 100
+    wc[ready, 5] ^= 1  # every entry's first id changed, its check not: each must be refused
+    assert dt.encode(rows) == want
+    off = DeviceTokenizer.from_hf(qwen_tok, device)
+    off.word_cache = None
+    assert off.encode(rows) == want
