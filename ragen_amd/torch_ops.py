@@ -773,26 +773,41 @@ def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, par
             text.new_empty(B, dtype=torch.uint8))
 
 
+_PROMPT_TEMPLATES = {}  # (program, sep) -> the rmi_prompt_t of its pieces and scalars (pointers unset)
+
+
+def _prompt_template(program, sep) -> _lib.Prompt:
+    key = (tuple(program), tuple(sep))
+    P = _PROMPT_TEMPLATES.get(key)
+    if P is None:
+        n = program[0]
+        if n > _lib.PROMPT_MAX_PIECES or len(program) != 1 + 3 * n + 5 or len(sep) > 16:
+            raise ValueError("bad prompt program")
+        P = _lib.Prompt()
+        P.n_pieces = n
+        for i in range(n):
+            P.pieces[i] = _lib.Piece(*program[1 + 3 * i:4 + 3 * i])
+        P.n_tags, P.obs_stride, P.resp_stride, P.enable_think, P.K = program[1 + 3 * n:]
+        P.sep_len = len(sep)
+        for i, x in enumerate(sep):
+            P.sep[i] = x
+        if len(_PROMPT_TEMPLATES) >= 256:  # one program per turn number and stride in practice
+            _PROMPT_TEMPLATES.clear()
+        _PROMPT_TEMPLATES[key] = P
+    return _lib.Prompt.from_buffer_copy(P)
+
+
 def prompt_struct(program: List[int], sep: List[int], tensors, turn=None) -> _lib.Prompt:
     """program = [n_pieces, (kind, a, b) * n_pieces, n_tags, obs_stride, resp_stride, enable_think, K];
     tensors = (pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active);
-    turn = (turn_exec, flags, int_reward_tags, last_turn): the turn form (rmi_prompt_t)."""
+    turn = (turn_exec, flags, int_reward_tags, last_turn): the turn form (rmi_prompt_t).  The pieces
+    and scalars of a program are built once (_prompt_template); each call sets the pointers."""
     pool, tag_const, tag, obs, obs_len, ints, reward, reward_int, resp, resp_len, spans, cond, active = tensors
-    n = program[0]
-    if n > _lib.PROMPT_MAX_PIECES or len(program) != 1 + 3 * n + 5 or len(sep) > 16:
-        raise ValueError("bad prompt program")
-    P = _lib.Prompt()
-    P.n_pieces = n
-    for i in range(n):
-        P.pieces[i] = _lib.Piece(*program[1 + 3 * i:4 + 3 * i])
-    n_tags, obs_stride, resp_stride, enable_think, K = program[1 + 3 * n:]
-    P.pool, P.tag_const, P.n_tags, P.tag = _ptr(pool), _ptr(tag_const), n_tags, _ptr(tag)
-    P.obs, P.obs_stride, P.obs_len, P.ints = _ptr(obs), obs_stride, _ptr(obs_len), _ptr(ints)
-    P.reward, P.reward_int, P.resp, P.resp_stride = _ptr(reward), _ptr(reward_int), _ptr(resp), resp_stride
-    P.resp_len, P.spans, P.enable_think, P.K = _ptr(resp_len), _ptr(spans), enable_think, K
-    P.sep_len = len(sep)
-    for i, x in enumerate(sep):
-        P.sep[i] = x
+    P = _prompt_template(program, sep)
+    P.pool, P.tag_const, P.tag = _ptr(pool), _ptr(tag_const), _ptr(tag)
+    P.obs, P.obs_len, P.ints = _ptr(obs), _ptr(obs_len), _ptr(ints)
+    P.reward, P.reward_int, P.resp = _ptr(reward), _ptr(reward_int), _ptr(resp)
+    P.resp_len, P.spans = _ptr(resp_len), _ptr(spans)
     P.cond, P.active = _ptr(cond), _ptr(active)
     P.pool_len = pool.numel() if pool is not None else 0
     if turn is not None and turn[0] is not None:

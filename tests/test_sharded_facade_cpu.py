@@ -107,7 +107,9 @@ def _worker(rank, world, port, q):
         g0, ng = rd.shard_groups(N_ROWS // 4, world, rank)
         lo, hi = g0 * 4, (g0 + ng) * 4
         out = rd.gather_formulated(_formulated(rows[lo:hi], scores[lo:hi], lo), PAD, dist.group.WORLD)
-        batch = {k: out.batch[k].clone() for k in out.batch.keys()}
+        # numpy copies: a tensor sent through the queue lives in this process's shared memory,
+        # which goes away when the worker exits, before the parent may have read it
+        batch = {k: out.batch[k].numpy().copy() for k in out.batch.keys()}
         nt = {k: list(out.non_tensor_batch[k]) for k in ("env_ids", "group_ids")}
         aliased = out.batch["original_rm_scores"].data_ptr() == out.batch["rm_scores"].data_ptr()
         # the metrics every rank reports
@@ -167,7 +169,7 @@ def test_two_rank_gloo_sharded_facade_host_logic():
         assert seed == want_seed, rank
         assert set(batch) == set(whole.batch.keys())
         for k in whole.batch.keys():
-            assert torch.equal(batch[k], whole.batch[k]), (rank, k)
+            assert torch.equal(torch.from_numpy(batch[k]), whole.batch[k]), (rank, k)
         assert aliased
         assert nt["env_ids"] == list(range(N_ROWS)) and nt["group_ids"] == [e // 4 for e in range(N_ROWS)]
         assert met == want_met, rank
