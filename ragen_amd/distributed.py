@@ -203,7 +203,7 @@ def gather_formulated(dp, pad_id: int, group=None, sizes=None):
         out["original_rm_scores"] = out["rm_scores"]
     nt = {}
     for k in ("env_ids", "group_ids"):
-        if k in dp.non_tensor_batch:
-            loc = torch.tensor(np.asarray(dict.__getitem__(dp.non_tensor_batch, k), np.int64), device=ids.device)
+        if k in dp.non_tensor_batch:  # a LazyDataProto makes these two without building its messages
+            loc = torch.tensor(np.asarray(dp.non_tensor_batch[k], np.int64), device=ids.device)
             nt[k] = np.array(all_gather_rows(loc, group=group, sizes=sizes).cpu().tolist(), dtype=object)
     return DataProto(out, nt, dict(dp.meta_info))

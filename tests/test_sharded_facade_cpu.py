@@ -173,3 +173,24 @@ def test_two_rank_gloo_sharded_facade_host_logic():
         assert aliased
         assert nt["env_ids"] == list(range(N_ROWS)) and nt["group_ids"] == [e // 4 for e in range(N_ROWS)]
         assert met == want_met, rank
+
+
+def test_gather_formulated_lazy_ids():
+    """gather_formulated over the device path's LazyDataProto: env / group ids come from its
+    int64 ids (the object arrays made on read), without building the messages."""
+    from ragen_amd.llm_agent.ctx_manager import LazyDataProto
+    port = _free_port()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        rows, scores = _rows()
+        plain = _formulated(rows, scores, 0)
+        built = []
+        lazy = LazyDataProto(np.arange(N_ROWS), lambda: built.append(1))
+        lazy.set_device_batch({k: plain.batch[k] for k in plain.batch.keys()}, np.arange(N_ROWS), 4)
+        out = rd.gather_formulated(lazy, PAD, dist.group.WORLD)
+        assert list(out.non_tensor_batch["env_ids"]) == list(range(N_ROWS))
+        assert list(out.non_tensor_batch["group_ids"]) == [e // 4 for e in range(N_ROWS)]
+        assert torch.equal(out.batch["input_ids"], plain.batch["input_ids"])
+        assert not built  # messages_list was not built
+    finally:
+        dist.destroy_process_group()
