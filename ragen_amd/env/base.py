@@ -59,7 +59,21 @@ class BatchEnv:
         return [rev.get(a.lower(), 0) for a in actions]
 
     def map_actions_many(self, rows: List[int], actions: List[List[str]]) -> List[List[int]]:
-        """map_actions for many envs of one turn; the reverse table is built once per lookup."""
+        """map_actions for many envs of one turn; the reverse table is built once per lookup.
+        With one lookup for every env (action_lookup not overridden) equal action lists map
+        once: envs with the same actions share one (read-only) id list."""
+        if type(self).action_lookup is BatchEnv.action_lookup:
+            lookup = self.action_lookup(0)
+            rev = {v.lower(): k for k, v in lookup.items()}
+            memo = {}
+            out = []
+            for acts in actions:
+                key = tuple(acts)
+                ids = memo.get(key)
+                if ids is None:
+                    ids = memo[key] = [rev.get(a.lower(), 0) for a in acts]
+                out.append(ids)
+            return out
         revs = {}
         out = []
         for i, acts in zip(rows, actions):

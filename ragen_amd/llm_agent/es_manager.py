@@ -320,10 +320,10 @@ class EnvStateManager:
             self._reset_rows = None
         else:
             obs = {j: tg.batch.render_all() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
-        tag_of = self._tag_of
-        for e, cache in zip(self.envs, self._rc):
-            e["status"] = EnvStatus(seed=int(seeds[e["env_id"] - self.env_lo]))
-            j = int(tag_of[e["env_id"] - self.env_lo])
+        seeds_l, tag_l = seeds.tolist(), self._tag_of.tolist()  # python ints, one conversion
+        for k, (e, cache) in enumerate(zip(self.envs, self._rc)):
+            e["status"] = EnvStatus(seed=seeds_l[k])
+            j = tag_l[k]
             state = obs[j][e["local"]] if j in obs else e["env"].render(e["local"])
             cache["history"] = self._update_cache_history(cache["history"], state, e["max_actions_per_traj"], None)
 

@@ -405,9 +405,9 @@ def _render(fn, env_struct, B: int, cells: int, rows: int, lookup, device, out=N
 
 def decode_rows(out: torch.Tensor, n: torch.Tensor):
     """u8[B, stride] + i32[B] lengths -> list of str (one host copy, one decode per row)."""
-    buf = out.cpu().numpy()
-    lens = n.cpu().numpy()
-    return [buf[i, :lens[i]].tobytes().decode("utf-8") for i in range(len(lens))]
+    st = out.shape[1] if out.dim() == 2 else 0
+    b = out.cpu().numpy().tobytes()  # one bytes object, sliced per row (no numpy view per row)
+    return [b[i * st:i * st + ln].decode("utf-8") for i, ln in enumerate(n.cpu().tolist())]
 
 
 def sokoban_render(env: _lib.Sokoban, B: int, lookup, device, out=None):
