@@ -221,6 +221,7 @@ class DevicePrompts:
         es = self.es
         self.rollout = es.rollout_id
         self.turns_done = 0
+        self._pending = None  # a previous rollout's unread host rows: its arena is rebuilt now
         # the reset text of the tags without a device render, as host rows (the others' rows stay
         # empty: their observation comes from render_rows)
         host_tags = [tg for tg in es.tags if not hasattr(tg.batch, "render_rows")]
