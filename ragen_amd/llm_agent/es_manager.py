@@ -492,6 +492,7 @@ class EnvStateManager:
                     tag_index: int = 0, **kw):
         """Dict-free turn on the device (kernel variant): ids i8[B,K] of one tag batch."""
         tg = self.tags[tag_index]
+        self._all_active = False  # the active set is the caller's from here on
         tg.batch.step_turn(self._turn, actions, n_actions, has_input, tg.max_actions_per_traj, self.format_penalty,
                            **kw)
         self._turn += 1
