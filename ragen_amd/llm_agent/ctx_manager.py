@@ -667,7 +667,9 @@ class ContextManager:
         eps = [tg.batch.ep for tg in es.tags]
         tab = (eps[0].turn_reward if len(eps) == 1 else torch.cat([ep.turn_reward for ep in eps], 1)).contiguous()
         n_sc = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
-        special_token, reward_token = get_special_tokens(self.tokenizer)
+        if getattr(self, "_special", None) is None:  # a tokenizer call: once per manager
+            self._special = get_special_tokens(self.tokenizer)
+        special_token, reward_token = self._special
         # the longest row and the most turns, in one readback
         S, n_slots = torch.stack([row_len.max(), n_sc.max()]).cpu().tolist() if row_len.numel() else (1, 0)
         # zip_longest's length over the WHOLE batch (ctx_manager.py:52-62): every rank's longest
