@@ -1230,6 +1230,35 @@ int seg_waves_per_group(int stride) {
   const size_t n = kWgLds / seg_wave_lds(stride);
   return n >= (size_t)kRowWaves ? kRowWaves : (n < 1 ? 1 : (int)n);
 }
+// ---- the turn's generations onto the env batch (rmi_gen_rows): one wave per env row
+__global__ __launch_bounds__(256) void gen_rows_kernel(const int64_t* __restrict__ resp, int64_t R,
+                                                       const int64_t* __restrict__ src, int64_t n_envs,
+                                                       const uint32_t* __restrict__ packed, int64_t V,
+                                                       int64_t* __restrict__ ids, int32_t* __restrict__ n_ids,
+                                                       int32_t* __restrict__ raw_max) {
+  const int64_t e = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  const int lane = threadIdx.x & 63;
+  if (e >= n_envs) return;
+  const int64_t r = src ? src[e] : e;
+  int64_t* orow = ids ? ids + e * R : nullptr;
+  int raw = 0;
+  if (r >= 0) {
+    const int64_t* row = resp + r * R;
+    for (int64_t k = lane; k < R; k += 64) {
+      const int64_t t = row[k];
+      if (orow) orow[k] = t;
+      const int64_t c = t < 0 ? 0 : (t >= V ? V - 1 : t);  // the clamp of the sizing (ids outside
+      const uint32_t meta = packed[4 * c + 3];              // [0, V) are flagged by the decode)
+      raw += (meta >> 31) ? 0 : (int)(meta & 0xFFFFFFu);
+    }
+  } else if (orow) {
+    for (int64_t k = lane; k < R; k += 64) orow[k] = 0;
+  }
+  if (n_ids && lane == 0) n_ids[e] = r >= 0 ? (int32_t)R : 0;
+  const int tot = __builtin_amdgcn_readlane(wave_inclusive_scan(raw), 63);
+  if (lane == 0 && r >= 0) atomicMax(raw_max, tot);
+}
+
 }  // namespace
 }  // namespace rmi
 
@@ -1320,5 +1349,21 @@ RMI_API int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, c
   const size_t shm = parse_lds(stride) * nw;
   hipLaunchKernelGGL(parse_kernel, dim3((unsigned)((B + nw - 1) / nw)), dim3(64 * nw), shm,
                      as_stream(stream), a);
+  return launch_status();
+}
+
+RMI_API int rmi_gen_rows(const int64_t* resp, int64_t n_resp, int64_t R, const int64_t* src, int64_t n_envs,
+                         const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, int32_t* raw_max,
+                         rmi_stream_t stream) {
+  using namespace rmi;
+  if (n_resp < 0 || R < 0 || n_envs < 0 || V < 1 || !raw_max || !vocab_packed) return RMI_EINVAL;
+  if ((src == nullptr) != (ids == nullptr) || (src == nullptr && n_resp != n_envs)) return RMI_EINVAL;
+  if (!resp && n_resp > 0 && R > 0) return RMI_EINVAL;
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(raw_max, 0, sizeof(int32_t), st) != hipSuccess) return RMI_EDEVICE;
+  if (n_envs == 0) return RMI_OK;
+  const int per_block = 4;  // waves (rows) per 256-thread block
+  hipLaunchKernelGGL(gen_rows_kernel, dim3((unsigned)((n_envs + per_block - 1) / per_block)), dim3(64 * per_block), 0,
+                     st, resp, R, src, n_envs, vocab_packed, V, ids, n_ids, raw_max);
   return launch_status();
 }

@@ -623,21 +623,25 @@ class ContextManager:
         env_ids = np.asarray(lm_outputs.non_tensor_batch["env_ids"], dtype=np.int64)
         R = resp.shape[1]
         lo, n = self.env_lo, self.n_envs
+        resp = resp.to(torch.int64).contiguous()
+        raw = torch.empty(1, dtype=torch.int32, device=dev)
         if len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n)):
             # every env in order: the generations are the rows (n_ids = None: R ids each)
-            rows_t, n_ids = None, None
-            ids = resp.to(torch.int64).contiguous()
-        else:
-            rows_t = torch.from_numpy(env_ids - lo).to(dev)
-            ids = torch.zeros(n, R, dtype=torch.int64, device=dev)
-            n_ids = torch.zeros(n, dtype=torch.int32, device=dev)
-            ids[rows_t] = resp.to(torch.int64)
-            n_ids[rows_t] = R
+            rows_t, n_ids, ids = None, None, resp
+            torch.ops.ragen_amd.gen_rows(resp, None, n, vocab.packed, None, None, raw)
+        else:  # one launch: the rows scattered onto the batch, n_ids, the raw width
+            src = np.full(n + len(env_ids), -1, np.int64)  # src[e] (-1: no row), then the rows
+            src[env_ids - lo] = np.arange(len(env_ids))
+            src[n:] = env_ids - lo
+            both = torch.from_numpy(src).to(dev)
+            rows_t = both[n:]
+            ids = torch.empty(n, R, dtype=torch.int64, device=dev)
+            n_ids = torch.empty(n, dtype=torch.int32, device=dev)
+            torch.ops.ragen_amd.gen_rows(resp, both[:n], n, vocab.packed, ids, n_ids, raw)
         # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
         # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
         # the decode and refused by the step (ValueError)
-        raw = vocab.raw_len[resp.clamp(0, vocab.raw_len.numel() - 1)]
-        raw_max = int(raw.sum(1).max()) if resp.numel() else 0
+        raw_max = int(raw) if resp.numel() else 0
         stride = max(4, min(PARSE_MAX_ROW, (3 * raw_max + 7) // 4 * 4))
         return DeviceEnvInputs(self, env_ids, rows_t, ids, n_ids, stride)
 

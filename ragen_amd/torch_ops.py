@@ -431,6 +431,14 @@ def _(tokens, row_start, row_len, S, pad_id, special_token, reward_token, scores
             tokens.new_empty(B, dtype=torch.uint8))
 
 
+@_op("gen_rows", ("ids", "n_ids", "raw_max"))
+def gen_rows(resp: Tensor, src: Optional[Tensor], n_envs: int, vocab_packed: Tensor, ids: Optional[Tensor],
+             n_ids: Optional[Tensor], raw_max: Tensor) -> None:
+    """The input side of get_env_inputs (ctx_manager.py:332-337): the turn's generations onto
+    the env batch and the longest row's raw bytes (rmi_gen_rows)."""
+    ops.gen_rows(resp, src, n_envs, vocab_packed, ids, n_ids, raw_max)
+
+
 @_op("pad_rows")
 def pad_rows(arena: Tensor, arena_len: Tensor, rows: Tensor, tail: Tensor, S: int,
              pad_id: int) -> Tuple[Tensor, Tensor, Tensor, Tensor]:
@@ -859,8 +867,8 @@ def _(program, sep, B, stride, pool, tag_const, tag, obs, obs_len, ints, reward,
 
 
 # the mutating ops return nothing: their fake kernels only have to exist
-for _name in ("sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_reset",
-              "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
+for _name in ("gen_rows", "sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize",
+              "sokoban_reset", "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
               "frozenlake_reset", "bandit_step_turn", "countdown_step_turn", "rollout_finalize"):
     torch.library.register_fake(f"{NS}::{_name}", lambda *a, **k: None, lib=_LIB)
 

@@ -1,0 +1,67 @@
+"""rmi_gen_rows (csrc/parse.hip): the turn's generations onto the env batch ahead of the fused
+decode + parse — against the torch formulation it replaced in ContextManager._device_env_inputs:
+the rows scattered onto a zeroed [n_envs, R] batch, n_ids = R for the envs given (0 else), and
+the longest given row's raw bytes = the sum of VocabTable.raw_len over its ids clamped to
+[0, V) (skipped tokens 0) — every env, a subset, none, ids outside the vocabulary."""
+import numpy as np
+import pytest
+import torch
+
+from ragen_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _vocab(dev, V=300, seed=3):
+    rng = np.random.default_rng(seed)
+    table = [bytes(rng.integers(32, 127, rng.integers(0, 20)).astype(np.uint8)) for _ in range(V)]
+    skip = (rng.random(V) < 0.1).astype(np.uint8)
+    return ops.VocabTable.from_bytes(table, skip, dev)
+
+
+def _want(resp, env_rows, n, vocab):
+    R = resp.shape[1]
+    V = vocab.raw_len.numel()
+    ids = torch.zeros(n, R, dtype=torch.int64, device=resp.device)
+    n_ids = torch.zeros(n, dtype=torch.int32, device=resp.device)
+    ids[env_rows] = resp
+    n_ids[env_rows] = R
+    raw = vocab.raw_len[resp.clamp(0, V - 1)].sum(1)
+    return ids, n_ids, int(raw.max()) if resp.numel() else 0
+
+
+@pytest.mark.parametrize("R", [1, 63, 64, 200])
+def test_gen_rows_equals_torch(device, R):
+    vocab = _vocab(device)
+    V = vocab.raw_len.numel()
+    rng = np.random.default_rng(R)
+    n = 1000
+    for which in ("all", "subset", "one"):
+        rows = {"all": np.arange(n), "subset": np.sort(rng.choice(n, 437, replace=False)),
+                "one": np.array([n - 1])}[which]
+        resp = torch.from_numpy(rng.integers(-2, V + 3, (len(rows), R))).to(device)
+        rows_t = torch.from_numpy(rows).to(device)
+        ids_w, n_w, raw_w = _want(resp, rows_t, n, vocab)
+        raw = torch.empty(1, dtype=torch.int32, device=device)
+        if which == "all":
+            torch.ops.ragen_amd.gen_rows(resp, None, n, vocab.packed, None, None, raw)
+        else:
+            src = np.full(n, -1, np.int64)
+            src[rows] = np.arange(len(rows))
+            ids = torch.full((n, R), 7, dtype=torch.int64, device=device)  # garbage: every row is written
+            n_ids = torch.full((n,), 7, dtype=torch.int32, device=device)
+            torch.ops.ragen_amd.gen_rows(resp, torch.from_numpy(src).to(device), n, vocab.packed, ids, n_ids, raw)
+            assert torch.equal(ids, ids_w) and torch.equal(n_ids, n_w), which
+        assert int(raw) == raw_w, which
+
+
+def test_gen_rows_no_rows(device):
+    vocab = _vocab(device)
+    n, R = 64, 16
+    resp = torch.empty(0, R, dtype=torch.int64, device=device)
+    ids = torch.full((n, R), 7, dtype=torch.int64, device=device)
+    n_ids = torch.full((n,), 7, dtype=torch.int32, device=device)
+    raw = torch.full((1,), 7, dtype=torch.int32, device=device)
+    torch.ops.ragen_amd.gen_rows(resp, torch.full((n,), -1, dtype=torch.int64, device=device), n, vocab.packed,
+                                 ids, n_ids, raw)
+    assert not ids.any() and not n_ids.any() and int(raw) == 0
