@@ -399,13 +399,13 @@ int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_id
  * input side of ContextManager.get_env_inputs, ctx_manager.py:332-337, for the envs given).
  * resp [n_resp, R] token ids; src[e] = the resp row of env e (-1: none), or src = NULL when
  * resp holds every env's row in order (n_resp == n_envs; ids and n_ids are then not written).
- * With src: ids [n_envs, R] = the rows (zeros for envs without one), n_ids[e] = R or 0 (may be
- * NULL).  raw_max[0] = the most bytes any given row decodes to before U+FFFD replacement (the
+ * With src: ids [n_envs, R] = the rows (zeros for envs without one), n_ids[e] = R or 0 and
+ * has[e] = 1 or 0 (the step kernels' has_input; each may be NULL).  raw_max[0] = the most bytes any given row decodes to before U+FFFD replacement (the
  * sum of its ids' byte lengths, skipped tokens 0, ids clamped to [0, V)); it sizes the decoded
  * rows.  The entry point zeroes raw_max on the stream first.                              */
 int rmi_gen_rows(const int64_t* resp, int64_t n_resp, int64_t R, const int64_t* src, int64_t n_envs,
-                 const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, int32_t* raw_max,
-                 rmi_stream_t stream);
+                 const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, uint8_t* has,
+                 int32_t* raw_max, rmi_stream_t stream);
 
 /* HOST function (CPU memory): the packed vocabulary of rmi_detokenize from the byte table
  * vocab_bytes[vocab_off[t] .. vocab_off[t+1]) and skip[t] (NULL = none skipped).

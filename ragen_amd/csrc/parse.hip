@@ -1235,7 +1235,7 @@ __global__ __launch_bounds__(256) void gen_rows_kernel(const int64_t* __restrict
                                                        const int64_t* __restrict__ src, int64_t n_envs,
                                                        const uint32_t* __restrict__ packed, int64_t V,
                                                        int64_t* __restrict__ ids, int32_t* __restrict__ n_ids,
-                                                       int32_t* __restrict__ raw_max) {
+                                                       uint8_t* __restrict__ has, int32_t* __restrict__ raw_max) {
   const int64_t e = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
   const int lane = threadIdx.x & 63;
   if (e >= n_envs) return;
@@ -1254,7 +1254,10 @@ __global__ __launch_bounds__(256) void gen_rows_kernel(const int64_t* __restrict
   } else if (orow) {
     for (int64_t k = lane; k < R; k += 64) orow[k] = 0;
   }
-  if (n_ids && lane == 0) n_ids[e] = r >= 0 ? (int32_t)R : 0;
+  if (lane == 0) {
+    if (n_ids) n_ids[e] = r >= 0 ? (int32_t)R : 0;
+    if (has) has[e] = r >= 0 ? 1 : 0;
+  }
   const int tot = __builtin_amdgcn_readlane(wave_inclusive_scan(raw), 63);
   if (lane == 0 && r >= 0) atomicMax(raw_max, tot);
 }
@@ -1353,8 +1356,8 @@ RMI_API int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, c
 }
 
 RMI_API int rmi_gen_rows(const int64_t* resp, int64_t n_resp, int64_t R, const int64_t* src, int64_t n_envs,
-                         const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, int32_t* raw_max,
-                         rmi_stream_t stream) {
+                         const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, uint8_t* has,
+                         int32_t* raw_max, rmi_stream_t stream) {
   using namespace rmi;
   if (n_resp < 0 || R < 0 || n_envs < 0 || V < 1 || !raw_max || !vocab_packed) return RMI_EINVAL;
   if ((src == nullptr) != (ids == nullptr) || (src == nullptr && n_resp != n_envs)) return RMI_EINVAL;
@@ -1364,6 +1367,6 @@ RMI_API int rmi_gen_rows(const int64_t* resp, int64_t n_resp, int64_t R, const i
   if (n_envs == 0) return RMI_OK;
   const int per_block = 4;  // waves (rows) per 256-thread block
   hipLaunchKernelGGL(gen_rows_kernel, dim3((unsigned)((n_envs + per_block - 1) / per_block)), dim3(64 * per_block), 0,
-                     st, resp, R, src, n_envs, vocab_packed, V, ids, n_ids, raw_max);
+                     st, resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has, raw_max);
   return launch_status();
 }

@@ -180,9 +180,9 @@ class DeviceEnvInputs:
     the parse (rmi_detok_parse), or on first access to ``text`` / ``text_len`` / ``err``.
     Iterating it yields the reference's env-input dicts (host decode + parse), built lazily."""
 
-    def __init__(self, ctx, env_ids, rows_t, ids, n_ids, stride):
-        # rows_t: the generations' rows of the env batch (device), None = every env in order
-        self.ctx, self.env_ids, self.rows_t = ctx, env_ids, rows_t
+    def __init__(self, ctx, env_ids, has_t, ids, n_ids, stride):
+        # has_t: u8[n_envs] 1 for the envs with a generation (device), None = every env in order
+        self.ctx, self.env_ids, self.has_t = ctx, env_ids, has_t
         self.ids, self.n_ids, self.stride = ids, n_ids, stride
         self.vocab = ctx.device_vocab
         self._text = self._text_len = self._err = None
@@ -627,23 +627,22 @@ class ContextManager:
         raw = torch.empty(1, dtype=torch.int32, device=dev)
         if len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n)):
             # every env in order: the generations are the rows (n_ids = None: R ids each)
-            rows_t, n_ids, ids = None, None, resp
+            has_t, n_ids, ids = None, None, resp
             torch.ops.ragen_amd.gen_rows(resp, None, n, vocab.packed, None, None, raw)
         else:  # one launch: the rows scattered onto the batch, n_ids, the raw width
-            src = np.full(n + len(env_ids), -1, np.int64)  # src[e] (-1: no row), then the rows
+            src = np.full(n, -1, np.int64)  # src[e]: env e's row (-1: none)
             src[env_ids - lo] = np.arange(len(env_ids))
-            src[n:] = env_ids - lo
-            both = torch.from_numpy(src).to(dev)
-            rows_t = both[n:]
             ids = torch.empty(n, R, dtype=torch.int64, device=dev)
             n_ids = torch.empty(n, dtype=torch.int32, device=dev)
-            torch.ops.ragen_amd.gen_rows(resp, both[:n], n, vocab.packed, ids, n_ids, raw)
+            has_t = torch.empty(n, dtype=torch.uint8, device=dev)  # 1: the env has a generation
+            torch.ops.ragen_amd.gen_rows(resp, torch.from_numpy(src).to(dev), n, vocab.packed, ids, n_ids, raw,
+                                         has_t)
         # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
         # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
         # the decode and refused by the step (ValueError)
         raw_max = int(raw) if resp.numel() else 0
         stride = max(4, min(PARSE_MAX_ROW, (3 * raw_max + 7) // 4 * 4))
-        return DeviceEnvInputs(self, env_ids, rows_t, ids, n_ids, stride)
+        return DeviceEnvInputs(self, env_ids, has_t, ids, n_ids, stride)
 
     def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:
         """ctx_manager.py:354-356.  The rollout states of the attached env manager's device path

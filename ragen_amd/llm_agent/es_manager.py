@@ -592,13 +592,12 @@ class EnvStateManager:
                              "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP)")
         # the envs with a generation: all of them, every one still running (has_input = None:
         # the turn kernels then step the envs not done), or the rows given
-        if inp.rows_t is None and self._all_active:
+        if inp.has_t is None and self._all_active:
             has = None
-        elif inp.rows_t is None:
+        elif inp.has_t is None:
             has = torch.ones(self.n_envs, dtype=torch.uint8, device=dev)
         else:
-            has = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
-            has[inp.rows_t] = 1
+            has = inp.has_t  # written by rmi_gen_rows
         err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
         if parsed is None:
             parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)

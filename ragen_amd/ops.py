@@ -766,10 +766,12 @@ def assemble_rows(tokens: torch.Tensor, row_start: torch.Tensor, row_len: torch.
 
 
 def gen_rows(resp: torch.Tensor, src: Optional[torch.Tensor], n_envs: int, vocab_packed: torch.Tensor,
-             ids: Optional[torch.Tensor], n_ids: Optional[torch.Tensor], raw_max: torch.Tensor):
-    """rmi_gen_rows: the turn's generations onto the env batch (ids / n_ids written when src is
-    given) and the longest row's raw bytes into raw_max i32[1]."""
-    _dev(resp, src, vocab_packed, ids, n_ids, raw_max)
+             ids: Optional[torch.Tensor], n_ids: Optional[torch.Tensor], raw_max: torch.Tensor,
+             has: Optional[torch.Tensor] = None):
+    """rmi_gen_rows: the turn's generations onto the env batch (ids / n_ids / has written when
+    src is given) and the longest row's raw bytes into raw_max i32[1]."""
+    _dev(resp, src, vocab_packed, ids, n_ids, raw_max, has)
+    _dt(has, torch.uint8, "has")
     _dt(resp, torch.int64, "resp")
     _dt(src, torch.int64, "src")
     _dt(ids, torch.int64, "ids")
@@ -779,12 +781,14 @@ def gen_rows(resp: torch.Tensor, src: Optional[torch.Tensor], n_envs: int, vocab
         raise ValueError("resp must be [n, R] and raw_max hold one int32")
     R = resp.shape[1]
     if src is not None and (src.numel() != n_envs or ids is None or tuple(ids.shape) != (n_envs, R)
-                            or (n_ids is not None and n_ids.numel() != n_envs)):
+                            or (n_ids is not None and n_ids.numel() != n_envs)
+                            or (has is not None and has.numel() != n_envs)):
         raise ValueError("src, ids and n_ids must have one row per env")
-    if src is None and (resp.shape[0] != n_envs or ids is not None):
+    if src is None and (resp.shape[0] != n_envs or ids is not None or has is not None):
         raise ValueError("without src resp holds every env's row (and ids is not written)")
     check(lib().rmi_gen_rows(_ptr(resp), resp.shape[0], R, _ptr(src), int(n_envs), _ptr(vocab_packed),
-                             vocab_packed.shape[0], _ptr(ids), _ptr(n_ids), _ptr(raw_max), _stream(resp.device)),
+                             vocab_packed.shape[0], _ptr(ids), _ptr(n_ids), _ptr(has), _ptr(raw_max),
+                             _stream(resp.device)),
           "rmi_gen_rows")
 
 

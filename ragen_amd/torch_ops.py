@@ -431,12 +431,12 @@ def _(tokens, row_start, row_len, S, pad_id, special_token, reward_token, scores
             tokens.new_empty(B, dtype=torch.uint8))
 
 
-@_op("gen_rows", ("ids", "n_ids", "raw_max"))
+@_op("gen_rows", ("ids", "n_ids", "raw_max", "has"))
 def gen_rows(resp: Tensor, src: Optional[Tensor], n_envs: int, vocab_packed: Tensor, ids: Optional[Tensor],
-             n_ids: Optional[Tensor], raw_max: Tensor) -> None:
+             n_ids: Optional[Tensor], raw_max: Tensor, has: Optional[Tensor] = None) -> None:
     """The input side of get_env_inputs (ctx_manager.py:332-337): the turn's generations onto
     the env batch and the longest row's raw bytes (rmi_gen_rows)."""
-    ops.gen_rows(resp, src, n_envs, vocab_packed, ids, n_ids, raw_max)
+    ops.gen_rows(resp, src, n_envs, vocab_packed, ids, n_ids, raw_max, has)
 
 
 @_op("pad_rows")

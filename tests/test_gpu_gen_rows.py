@@ -1,7 +1,7 @@
 """rmi_gen_rows (csrc/parse.hip): the turn's generations onto the env batch ahead of the fused
 decode + parse — against the torch formulation it replaced in ContextManager._device_env_inputs:
 the rows scattered onto a zeroed [n_envs, R] batch, n_ids = R for the envs given (0 else), and
-the longest given row's raw bytes = the sum of VocabTable.raw_len over its ids clamped to
+the has-input mask, and the longest given row's raw bytes = the sum of VocabTable.raw_len over its ids clamped to
 [0, V) (skipped tokens 0) — every env, a subset, none, ids outside the vocabulary."""
 import numpy as np
 import pytest
@@ -50,8 +50,11 @@ def test_gen_rows_equals_torch(device, R):
             src[rows] = np.arange(len(rows))
             ids = torch.full((n, R), 7, dtype=torch.int64, device=device)  # garbage: every row is written
             n_ids = torch.full((n,), 7, dtype=torch.int32, device=device)
-            torch.ops.ragen_amd.gen_rows(resp, torch.from_numpy(src).to(device), n, vocab.packed, ids, n_ids, raw)
+            has = torch.full((n,), 7, dtype=torch.uint8, device=device)
+            torch.ops.ragen_amd.gen_rows(resp, torch.from_numpy(src).to(device), n, vocab.packed, ids, n_ids, raw,
+                                         has)
             assert torch.equal(ids, ids_w) and torch.equal(n_ids, n_w), which
+            assert torch.equal(has, (n_w > 0).to(torch.uint8)), which
         assert int(raw) == raw_w, which
 
 
