@@ -693,13 +693,34 @@ def api_leg(device):
                                    "goes through the torch custom op, `ctypes` through the C ABI directly")}
 
 
-def cpu_baseline_parallel(R, workers=16, reps=20):
-    """SURVEY §8(d) CPU baseline (b): one process per host core (the box's 16-core share),
-    env groups partitioned across processes, no shared state.  Worker w runs ``reps`` rollouts
-    of the 2048-env slice (w % 4) of this rank's batch; value = all workers' env steps / wall
-    time of the parallel phase (process start-up excluded)."""
+def host_cpus():
+    """The host cores this process may use: the affinity mask, capped by the box's CPU share
+    (OMP_NUM_THREADS is set to it on the GPU box, where nproc shows the whole machine), plus the
+    machine's nproc and CPU model (SURVEY §8(d) asks for both)."""
+    aff = len(os.sched_getaffinity(0))
+    share = os.environ.get("OMP_NUM_THREADS")
+    cores = min(aff, int(share)) if share and share.isdigit() and int(share) > 0 else aff
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cores": cores, "affinity": aff, "omp_num_threads": share, "nproc": os.cpu_count(), "model": model}
+
+
+def cpu_baseline_parallel(R, workers=None, reps=20):
+    """SURVEY §8(d) CPU baseline (b): one process per host core (host_cpus(): the affinity
+    mask capped by the box's share), env groups partitioned across processes, no shared state.
+    Worker w runs ``reps`` rollouts of the 2048-env slice (w % 4) of this rank's batch; value =
+    all workers' env steps / wall time of the parallel phase (process start-up excluded)."""
     import multiprocessing as mp
     from oracle import port
+    hc = host_cpus()
+    workers = workers or hc["cores"]
     n_envs = 2048
     jobs = []
     for w in range(workers):
@@ -715,7 +736,7 @@ def cpu_baseline_parallel(R, workers=16, reps=20):
         res = pool.starmap(port.timed_rollouts, jobs)
         wall = time.perf_counter() - t0
     steps = sum(r[0] for r in res)
-    return {"value": steps / wall, "unit": "env-steps/s", "cores": workers, "kind": "port",
+    return {"value": steps / wall, "unit": "env-steps/s", "cores": workers, "kind": "port", "host": hc,
             "sample": f"{workers} processes x {reps} rollouts of {n_envs} envs x {T_TURNS} turns, {steps} env.step "
                       f"calls in {wall:.1f}s wall, oracle/port.py"}
 
@@ -732,8 +753,10 @@ def cpu_gae_baseline(R, reps=2):
            "sample": "verl compute_gae_advantage_return (legacy) + masked_whiten on the advantage leg's rows, "
                      f"best of {reps}"}
     old = torch.get_num_threads()
+    many = host_cpus()["cores"]
+    out["threads"] = [1, many]
     try:
-        for threads in (1, 16):
+        for threads in (1, many):
             torch.set_num_threads(threads)
             best = None
             for _ in range(reps):
@@ -770,9 +793,81 @@ def cpu_baseline(R, seconds_budget=20.0):
         reps += 1
         if dt > seconds_budget / 2 or reps >= 40:
             break
-    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+    return {"value": steps / dt, "unit": "env-steps/s", "cores": 1, "kind": "port", "host": host_cpus(),
             "sample": f"{reps} x Sokoban 6x6 rollout of {n_envs} envs x {T_TURNS} turns (reset excluded), "
                       f"{steps} env.step calls in {dt:.1f}s, 1 thread, oracle/port.py"}
+
+
+def launch_plan(gpus, environ, device_count):
+    """How this invocation runs, decided before anything touches the GPU.
+    -> ("run", world)            : this process is one rank of `world` (torchrun set WORLD_SIZE,
+                                   or a plain N=1 run);
+       ("spawn", gpus)           : `python bench.py --gpus N` with no launcher: start N rank
+                                   processes (torch.distributed.run, 127.0.0.1) and exit with
+                                   their status;
+       ("error", message)        : the request cannot be honoured (fewer devices than ranks, or
+                                   a launcher world that disagrees with --gpus) -> exit non-zero,
+                                   never a silently relabelled 1-GPU run."""
+    if gpus < 1:
+        return "error", f"--gpus {gpus}: need at least 1"
+    ws = environ.get("WORLD_SIZE")
+    if ws is None:
+        if gpus == 1:
+            return "run", 1
+        if device_count < gpus:
+            return "error", (f"--gpus {gpus} asks for {gpus} ranks, one per GPU, but this box has {device_count} "
+                             "GPU(s); RCCL does not place two ranks on one device (use --double-buffer to run the "
+                             "N>1 exchange path as a 1-rank group on one GPU)")
+        return "spawn", gpus
+    world = int(ws)
+    if world != gpus:
+        return "error", f"--gpus {gpus} but the launcher started WORLD_SIZE={world} ranks"
+    local = int(environ.get("LOCAL_RANK", "0"))
+    if local >= device_count:
+        return "error", f"LOCAL_RANK {local} has no device (this box has {device_count} GPU(s))"
+    return "run", world
+
+
+def spawn_ranks(gpus, argv):
+    """Start `gpus` rank processes of this script through torch.distributed.run on 127.0.0.1 (a
+    free port), wait, and return their exit status.  The parent never initialises the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
+
+
+def arena_digests(sets):
+    """u8[R, n] (R rows: one rank's arena set per row) -> i64[R] digests: a position-weighted
+    sum of the row's 32-bit words (exact mod 2^64, so independent of reduction order).  A rank
+    broadcasts the digest of its own set; every rank recomputes the digests of the gathered rows
+    and compares, so a garbage or misplaced row of ANY rank fails the check."""
+    R, n = sets.shape
+    pad = (-n) % 4
+    x = sets if pad == 0 else torch.cat([sets, sets.new_zeros(R, pad)], 1)
+    w = x.contiguous().view(torch.int32).to(torch.int64)
+    k = torch.arange(w.shape[1], dtype=torch.int64, device=sets.device)
+    weight = (k * 2654435761 + 40503) % 2147483647 + 1
+    return (w * weight).sum(1)
+
+
+def check_gathered(own, gathered, world, rank, distinct=True):
+    """The N>1 exchange check of one gathered arena set (collective: every rank calls it).
+    own: u8[n] this rank's set; gathered: u8[world * n] the all-gather's result.  Every rank
+    all-gathers the digest of its own set, then checks every row of its gathered copy against
+    those digests, and its own row byte for byte.  distinct: the ranks' sets differ (they seed
+    different groups), so a row copied from another rank also fails.  -> bool (this rank)."""
+    rows = gathered.view(world, -1)
+    every = torch.empty(world, dtype=torch.int64, device=own.device)
+    tdist.all_gather_into_tensor(every, arena_digests(own.reshape(1, -1)))
+    ok = torch.equal(rows[rank], own.reshape(-1)) and torch.equal(arena_digests(rows), every)
+    if distinct and world > 1:
+        ok = ok and int(torch.unique(every).numel()) == world
+    return bool(ok)
 
 
 def main():
@@ -790,7 +885,15 @@ def main():
                     help="run the N>1 exchange path at N=1 (a 1-rank RCCL group, real collectives)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # torch.cuda.device_count() does not initialise the GPU on this image, so the parent of a
+    # self-spawned run stays GPU-free
+    action, what = launch_plan(args.gpus, os.environ, torch.cuda.device_count())
+    if action == "error":
+        print(f"bench.py: {what}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if action == "spawn":
+        sys.exit(spawn_ranks(what, sys.argv[1:]))
+    world = what
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1 or args.double_buffer
@@ -949,13 +1052,24 @@ def main():
         tdist.all_reduce(c)
         total_steps = int(c.item())
     # every replayed rollout wrote a full record (deterministic: all arenas identical), and at
-    # N > 1 this rank's row of each gathered set is its own arenas
+    # N > 1 EVERY rank's row of each gathered set equals the digest that rank broadcast of its
+    # own set (this rank's row also byte for byte)
     exchange_ok = None
+    gathered_info = None
     if graph is not None:
         exchange_ok = all(torch.equal(e.arena, eps[0].arena) for e in eps)
         if dist:
             r = tdist.get_rank()
-            exchange_ok = exchange_ok and all(torch.equal(outs[h].view(W, -1)[r], sets[h]) for h in (0, 1))
+            for h in (0, 1):
+                exchange_ok = check_gathered(sets[h], outs[h], W, r) and exchange_ok
+            gathered_info = {"ranks": W, "bytes_per_rank_per_gather": int(sets.shape[1]),
+                             "bytes_per_gather": int(W * sets.shape[1]), "rollouts_per_gather": G,
+                             "check": "every rank's row of both gathered sets == the i64 digest that rank "
+                                      "all-gathered of its own set; own row byte for byte"}
+        ok_t = torch.tensor([1 if exchange_ok else 0], dtype=torch.int32, device=device)
+        if dist:
+            tdist.all_reduce(ok_t, op=tdist.ReduceOp.MIN)
+        exchange_ok = bool(ok_t.item())
         if not exchange_ok:
             raise RuntimeError("replayed rollouts / gathered arenas do not match")
 
@@ -978,9 +1092,12 @@ def main():
     torch.cuda.synchronize()
     eager_ms = (time.perf_counter() - te) / eager_steps * 1e3
 
-    adv = advantage_leg(R, device) if not args.no_extras else None
-    copy_peak = hbm_copy_peak(device) if not args.no_extras else None
-    toytext = toytext_legs(device) if not args.no_extras else None
+    # the extras (and the CPU baselines below) run on rank 0 only: the other ranks' GPUs hold
+    # identical work, and the headline above is already timed
+    extras = not args.no_extras and rank == 0
+    adv = advantage_leg(R, device) if extras else None
+    copy_peak = hbm_copy_peak(device) if extras else None
+    toytext = toytext_legs(device) if extras else None
     api = api_leg(device) if not args.no_extras and rank == 0 else None
     text = text_leg(R, device) if not args.no_extras and rank == 0 else None
     at_scale = None
@@ -1024,6 +1141,7 @@ def main():
                 except Exception as ex:
                     adv["cpu_baseline"] = {"value": None, "sample": f"failed: {ex}"}
         value = total_steps / elapsed
+        assert world == args.gpus, (world, args.gpus)
         line = {
             "metric": "env-steps/sec (whole node), Sokoban 6x6, 8192 envs x 5 turns",
             "value": value,
@@ -1071,6 +1189,7 @@ def main():
                                else "after them on the same stream") + " (chosen by --exchange " + args.exchange + ")"
                             if graph is not None else "")) if dist else None,
             "records_checked": exchange_ok,
+            "gathered": gathered_info,
             "eager_ms_per_step": eager_ms,
             "speedup_vs_cpu_baseline": (value / cpu["value"]) if cpu and cpu.get("value") else None,
         }

@@ -53,8 +53,17 @@ def test_ops_refuse_cpu_tensors():
 STRUCTS = {  # ctypes mirror in ragen_amd/_lib.py -> C type in include/ragen_amd.h
     "Episode": "rmi_episode_t", "Turn": "rmi_turn_t", "Sokoban": "rmi_sokoban_t", "Finalize": "rmi_finalize_t",
     "FrozenLake": "rmi_frozenlake_t", "Bandit": "rmi_bandit_t", "Countdown": "rmi_countdown_t",
-    "ParseCfg": "rmi_parse_cfg_t",
+    "ParseCfg": "rmi_parse_cfg_t", "Piece": "rmi_piece_t", "Prompt": "rmi_prompt_t", "tokenizer.Bpe": "rmi_bpe_t",
 }
+
+
+def _struct(py):
+    """'Name' -> ragen_amd._lib.Name; 'module.Name' -> ragen_amd.module.Name."""
+    if "." in py:
+        import importlib
+        mod, name = py.rsplit(".", 1)
+        return getattr(importlib.import_module("ragen_amd." + mod), name)
+    return getattr(_lib, py)
 
 
 def test_ctypes_structs_match_the_c_layout(tmp_path):
@@ -63,7 +72,7 @@ def test_ctypes_structs_match_the_c_layout(tmp_path):
     import ctypes
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "ragen_amd.h"', "int main(void) {"]
     for py, c in STRUCTS.items():
-        cls = getattr(_lib, py)
+        cls = _struct(py)
         lines.append(f'  printf("{py} size %zu\\n", sizeof({c}));')
         for name, _ in cls._fields_:
             lines.append(f'  printf("{py} {name} %zu\\n", offsetof({c}, {name}));')
@@ -75,7 +84,7 @@ def test_ctypes_structs_match_the_c_layout(tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
     c_vals = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
     for py in STRUCTS:
-        cls = getattr(_lib, py)
+        cls = _struct(py)
         assert c_vals[(py, "size")] == ctypes.sizeof(cls), py
         for name, _ in cls._fields_:
             assert c_vals[(py, name)] == getattr(cls, name).offset, (py, name)
