@@ -172,6 +172,28 @@ def segments_for(grouping: str, env_outputs: List[Dict]):
     return perm, seg
 
 
+def tag_segments(tags, n_groups, group_size: int):
+    """The "inductive" grouping (ctx_manager.py:184-191: one group per tag NAME, first-seen
+    order) over the env order the config's entries lay down (entry i owns n_groups[i] *
+    group_size contiguous envs).  A tag listed more than once gathers all of its entries' envs.
+    -> (perm i64[B] or None when every tag's envs are already contiguous, seg i32[n_tags+1]);
+    equal to segments_for("inductive", ...) on the per-env tags."""
+    first = {}
+    for t in tags:
+        first.setdefault(t, len(first))
+    sizes = [int(n) * int(group_size) for n in n_groups]
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    order = sorted(range(len(sizes)), key=lambda i: first[tags[i]])  # stable: config order within a tag
+    per_tag = np.zeros(len(first), np.int64)
+    for i, t in enumerate(tags):
+        per_tag[first[t]] += sizes[i]
+    seg = np.concatenate([[0], np.cumsum(per_tag)]).astype(np.int32)
+    if order == list(range(len(sizes))):
+        return None, seg
+    perm = np.concatenate([np.arange(starts[i], starts[i + 1]) for i in order]) if order else np.zeros(0, np.int64)
+    return perm.astype(np.int64), seg
+
+
 class DeviceEnvInputs:
     """What ``get_env_inputs`` returns on the device path: the generations of the active envs as
     token ids of the FULL env batch (rows of envs without a generation are empty and carry no
@@ -468,22 +490,45 @@ class ContextManager:
         rn = self.config.agent_proxy.reward_normalization
         if rn.method not in ("mean_std", "mean", "asym_clip", "identity"):
             raise ValueError(f"Invalid normalization method: {rn.method}")
-        perm, seg = segments_for(rn.grouping, env_outputs)
+        if rn.grouping not in ("state", "inductive", "batch"):
+            raise ValueError(f"Invalid grouping: {rn.grouping}")
         dev = self.device
         acc = score_tensor[:, -1].to(dev, torch.float32)
         pen = torch.tensor([o.get("penalty", 0) for o in env_outputs], dtype=torch.float32).to(dev)
+        off = 0
+        rows = env_outputs
+        if self._sharded() and rn.grouping != "state":
+            # "inductive" / "batch" group over the WHOLE batch: every rank's scores, penalties and
+            # tags gathered in rank order (= global env order), normalised identically on every
+            # rank, own rows kept ("state" groups are group-aligned shards: rank-local)
+            from .. import distributed as rd
+            names = list(dict.fromkeys(self.es_cfg.env_configs.tags))
+            tid = torch.tensor([names.index(o["tag"]) if rn.grouping == "inductive" else 0 for o in env_outputs],
+                               dtype=torch.int64, device=dev)
+            acc, off = rd.all_gather_rows(acc, with_offset=True, group=self.process_group)
+            pen = rd.all_gather_rows(pen, group=self.process_group)
+            rows = [{"tag": names[int(t)]} for t in rd.all_gather_rows(tid, group=self.process_group).cpu().tolist()]
+        perm, seg = segments_for(rn.grouping, rows)
         identity_perm = np.array_equal(perm, np.arange(len(perm)))
         p = None if identity_perm else torch.from_numpy(perm).to(dev)
         a = acc if p is None else acc[p].contiguous()
         b = pen if p is None else pen[p].contiguous()
-        out = torch.ops.ragen_amd.group_normalize(a.contiguous(), b.contiguous(), ops.segments(seg, len(perm), dev),
-                                                  NORM[rn.method])
+        out = self._group_norm(a.contiguous(), b.contiguous(), ops.segments(seg, len(perm), dev), rn.method)
         if p is not None:
             res = torch.empty_like(out)
             res[p] = out
             out = res
+        out = out[off:off + score_tensor.shape[0]]
         score_tensor[:, -1] = out.to(score_tensor.device)
         return score_tensor
+
+    @staticmethod
+    def _group_norm(acc, pen, seg, method):
+        """rmi_group_normalize (group normalisation of ctx_manager.py:193-218) on device tensors."""
+        return torch.ops.ragen_amd.group_normalize(acc, pen, seg, NORM[method])
+
+    def _sharded(self) -> bool:
+        return self.process_group is not None and self.world_size > 1
 
     def get_lm_inputs(self, env_outputs: List[Dict], prepare_for_update: bool) -> DataProto:
         """ctx_manager.py:228-330.  On the device path with device prompts the generation batch
@@ -561,7 +606,11 @@ class ContextManager:
             normalized = score_tensor
             if not ap.use_turn_scores:
                 normalized = self._normalize_score_tensor(score_tensor, env_outputs)
-            response_length = response_mask.sum(dim=-1).float().mean().item()
+            row_resp = response_mask.sum(dim=-1).float()
+            if self._sharded():  # the mean over the WHOLE batch (ctx_manager.py:305)
+                from .. import distributed as rd
+                row_resp = rd.all_gather_rows(row_resp, group=self.process_group)
+            response_length = row_resp.mean().item()
             input_ids = ids.cpu()
             batch = {"input_ids": input_ids, "attention_mask": am.cpu(), "position_ids": pos.cpu(),
                      "responses": input_ids[:, 1:]}
@@ -583,10 +632,7 @@ class ContextManager:
             "messages_list": np.array(messages_list, dtype=object),
         }
         if prepare_for_update:
-            metrics = {}
-            for o in env_outputs:
-                for k, v in o["metrics"].items():
-                    metrics.setdefault(k, []).append(v)
+            metrics = self._gather_metric_lists(env_outputs)
             mean_metrics = {k: np.sum(v) / self.env_nums[k.split("/")[0]] for k, v in metrics.items()}
             for k, values in metrics.items():
                 prefix, suffix = k.split("/", 1)
@@ -596,6 +642,25 @@ class ContextManager:
             mean_metrics["response_length"] = response_length
             out.meta_info = {"metrics": mean_metrics}
         return out
+
+    def _gather_metric_lists(self, env_outputs) -> Dict[str, list]:
+        """The per-env metric values of ctx_manager.py:308-312 as {key: [values in env order]};
+        sharded, every rank's lists are all-gathered (host objects, rank order = global env
+        order) and concatenated, so the means and non-zero means are the whole batch's."""
+        metrics = {}
+        for o in env_outputs:
+            for k, v in o["metrics"].items():
+                metrics.setdefault(k, []).append(v)
+        if not self._sharded():
+            return metrics
+        import torch.distributed as dist
+        parts = [None] * self.world_size
+        dist.all_gather_object(parts, metrics, group=self.process_group)
+        merged = {}
+        for part in parts:
+            for k, v in part.items():
+                merged.setdefault(k, []).extend(v)
+        return merged
 
     def get_env_inputs(self, lm_outputs: DataProto) -> List[Dict]:
         """ctx_manager.py:332-352.  Generations that arrive as token ids on the GPU with the device
@@ -630,8 +695,13 @@ class ContextManager:
             has_t, n_ids, ids = None, None, resp
             torch.ops.ragen_amd.gen_rows(resp, None, n, vocab.packed, None, None, raw)
         else:  # one launch: the rows scattered onto the batch, n_ids, the raw width
+            local = env_ids - lo
+            if local.size and (local.min() < 0 or local.max() >= n):
+                raise ValueError(f"env ids outside this manager's envs [{lo}, {lo + n})")
+            if np.unique(local).size != local.size:
+                raise ValueError("duplicate env ids in the generation batch")
             src = np.full(n, -1, np.int64)  # src[e]: env e's row (-1: none)
-            src[env_ids - lo] = np.arange(len(env_ids))
+            src[local] = np.arange(len(env_ids))
             ids = torch.empty(n, R, dtype=torch.int64, device=dev)
             n_ids = torch.empty(n, dtype=torch.int32, device=dev)
             has_t = torch.empty(n, dtype=torch.uint8, device=dev)  # 1: the env has a generation
@@ -725,21 +795,27 @@ class ContextManager:
         gs = es.group_size
         if rn.grouping == "state":
             seg = np.arange(0, es.n_envs + 1, gs, dtype=np.int32)
-            out = torch.ops.ragen_amd.group_normalize(acc, pen.contiguous(), ops.segments(seg, es.n_envs, dev),
-                                                      NORM[rn.method])
+            out = self._group_norm(acc, pen.contiguous(), ops.segments(seg, es.n_envs, dev), rn.method)
         else:
-            sharded = self.process_group is not None and self.world_size > 1
+            sharded = self._sharded()
             sz = self.shard_sizes() if sharded else None
             a_all = rd.all_gather_rows(acc, group=self.process_group, sizes=sz) if sharded else acc
             p_all = rd.all_gather_rows(pen.contiguous(), group=self.process_group, sizes=sz) if sharded else pen
             n_all = a_all.numel()
+            perm = None
             if rn.grouping == "batch":
                 seg = np.array([0, n_all], np.int32)
-            else:  # tags: contiguous global env ranges in config order
-                cuts = np.cumsum([0] + [n * gs for n in self.es_cfg.env_configs.n_groups]).astype(np.int32)
-                seg = np.unique(cuts)
-            res = torch.ops.ragen_amd.group_normalize(a_all.contiguous(), p_all.contiguous(),
-                                                      ops.segments(seg, n_all, dev), NORM[rn.method])
+            else:  # one group per tag NAME (a tag listed twice in the config is one group)
+                ec = self.es_cfg.env_configs
+                perm, seg = tag_segments(list(ec.tags), list(ec.n_groups), gs)
+            if perm is not None:
+                p = torch.from_numpy(perm).to(dev)
+                a_all, p_all = a_all[p], p_all[p]
+            res = self._group_norm(a_all.contiguous(), p_all.contiguous(), ops.segments(seg, n_all, dev), rn.method)
+            if perm is not None:
+                back = torch.empty_like(res)
+                back[p] = res
+                res = back
             out = res[es.env_lo:es.env_lo + es.n_envs] if sharded else res
         score_tensor[:, -1] = out
         return score_tensor

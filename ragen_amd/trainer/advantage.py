@@ -8,6 +8,21 @@ from ..torch_ops import FILTER
 from . import core_algos
 
 
+_WARNED = set()
+
+
+def _warn_rank_local(what: str, process_group):
+    """Once per call site: torch.distributed is up with more than one rank but no process_group
+    was passed, so `what` runs over this rank's shard only (batch-global is opt-in)."""
+    if process_group is not None or what in _WARNED or not rd.initialized() or rd.world()[0] <= 1:
+        return
+    import warnings
+    _WARNED.add(what)
+    warnings.warn(f"{what}: torch.distributed has {rd.world()[0]} ranks but process_group=None, so it runs over "
+                  "this rank's rows only; pass process_group= for the whole sharded batch", RuntimeWarning,
+                  stacklevel=3)
+
+
 class AdvantageEstimator:
     GAE = "gae"
     GRPO = "grpo"
@@ -33,6 +48,7 @@ def compute_advantage(data: DataProto, adv_estimator, gamma=1.0, lam=1.0, num_re
     shard and whitening uses the statistics of the whole sharded batch (core_algos); ``shard_rows``
     (every rank's row count) makes that gather free of host synchronisation."""
     pg = {"process_group": process_group, "shard_rows": shard_rows}
+    _warn_rank_local("compute_advantage whitening", process_group)
     if "response_mask" not in data.batch:
         data.batch["response_mask"] = compute_response_mask(data)
     est = getattr(adv_estimator, "value", adv_estimator)
@@ -83,6 +99,7 @@ def filter_rollout(batch: DataProto, num_groups: int, group_size: int, ratio: fl
     batch is this rank's shard: the groups are ranked over every rank's scores
     (ragen_amd.distributed.global_filter), so the kept set equals the 1-GPU run's and
     ``num_groups`` is the GLOBAL count (es_manager.train.env_groups), as in the reference."""
+    _warn_rank_local("filter_rollout", process_group)
     rm = batch.batch["original_rm_scores"]
     dev = rm.device if rm.is_cuda else torch.device("cuda", torch.cuda.current_device())
     rows = torch.ops.ragen_amd.row_sum(rm.to(dev, torch.float32).contiguous())
