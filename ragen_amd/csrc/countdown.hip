@@ -13,9 +13,12 @@
 // RMI_ERR_UNSUP in err[] so a caller can see the envelope was left; bare names are modelled
 // (every lookup raises under {"__builtins__": None}: not correct, see name_outcome);
 // every other byte only yields errors in Python too (SyntaxError/TypeError -> False).
-// int results beyond 64 bits (Python big ints) are flagged RMI_ERR_UNSUP as well.
+// Python's ints are unbounded: an int past 64 bits (a literal, or an intermediate such as the
+// a**b of (a**b)//(c**d)) continues in bounded multi-word arithmetic (bigint.hpp, magnitudes
+// below 2^1024, in the row's LDS); only a value past that bound is flagged RMI_ERR_UNSUP.
 #include <math.h>
 
+#include "bigint.hpp"
 #include "common.hpp"
 
 namespace rmi {
@@ -125,11 +128,71 @@ __device__ __forceinline__ bool same_multiset(const uint64_t (&found)[kMaxNums],
 
 // ------------------------------------------------------------------ evaluator
 struct Val {  // no padding: copies stay in registers
-  long long i;
+  long long i;   // an int64, or the pool slot of a big int (is_f == kBig)
   double f;
-  int is_f;
+  int is_f;      // 0 int64, 1 float, kBig big int
   __device__ double as_f() const { return is_f ? f : (double)i; }
 };
+constexpr int kBig = 3;
+
+// The big ints of one evaluation: kBigLive value slots plus the scratch of one operation, in
+// the row's LDS (bigint.hpp's layout).  A value that fits int64 never stays big (demoted after
+// every operation), so the int64 code paths keep every answer that does not need more.
+constexpr int kBigLive = 6;
+constexpr int kBigScratch = (kDivU + 2) + 2 * kBigCap + (kDivU + 2);  // un, vn (+ remainder), xs (= qs)
+constexpr int kBigPoolWords = kBigLive * kBigWords + 2 * 4 + kBigScratch;
+constexpr int kBigPoolBytes = 4 * kBigPoolWords;
+static_assert(2 * kBigWords <= kBigScratch, "big_pow's two temporaries fit the scratch");
+struct BigCtx {
+  uint32_t* slots = nullptr;  // [kBigLive][kBigWords]
+  uint32_t* imm = nullptr;    // [2][4]: int64 operands in big form (two limbs)
+  uint32_t* un = nullptr;     // kDivU + 2
+  uint32_t* vn = nullptr;     // 2 kBigCap
+  uint32_t* xs = nullptr;     // kDivU + 2 (true division's dividend and quotient; big_pow's temporaries)
+  uint32_t free_mask = (1u << kBigLive) - 1;
+  __device__ void init(uint8_t* base) {  // base: 4-B aligned, kBigPoolBytes
+    uint32_t* w = reinterpret_cast<uint32_t*>(base);
+    slots = w;
+    imm = slots + kBigLive * kBigWords;
+    un = imm + 8;
+    vn = un + kDivU + 2;
+    xs = vn + 2 * kBigCap;
+    free_mask = (1u << kBigLive) - 1;
+  }
+  __device__ uint32_t* at(int s) const { return slots + s * kBigWords; }
+  __device__ int alloc() {
+    if (!free_mask) return -1;
+    const int s = __builtin_ctz(free_mask);
+    free_mask &= free_mask - 1;
+    return s;
+  }
+  __device__ void release(const struct Val& v) {
+    if (v.is_f == kBig) free_mask |= 1u << (int)v.i;
+  }
+  // an int operand (int64 or big) as a big value (which: 0 / 1, the imm slot for an int64)
+  __device__ const uint32_t* view(const struct Val& v, int which) {
+    if (v.is_f == kBig) return at((int)v.i);
+    uint32_t* w = imm + 4 * which;
+    big_set_i64(w, v.i);
+    return w;
+  }
+  // slot s holds a result: demote it to an int64 when it is one
+  __device__ void finish(int s, Val& out) {
+    long long x;
+    if (big_to_i64(at(s), x)) {
+      free_mask |= 1u << s;
+      out.is_f = 0;
+      out.i = x;
+    } else {
+      out.is_f = kBig;
+      out.i = s;
+    }
+    out.f = 0.0;
+  }
+};
+__device__ __forceinline__ int big_status(int st) {  // bigint status -> evaluator status
+  return st == BIG_OK ? 0 : (st == BIG_RANGE ? 2 : 1);  // RANGE: outside the model; overflow, /0: raises
+}
 
 enum Op : int8_t {
   OP_LPAREN = 0,
@@ -174,18 +237,34 @@ __device__ double py_floor_div_f(double vx, double wx, double* modp) {  // CPyth
   return floordiv;
 }
 
-__device__ int apply_unary(int op, Val& a) {
+__device__ int apply_unary(int op, Val& a, BigCtx& bc) {
   if (op == OP_POS) return EV_OK;
-  if (op == OP_NEG) {
-    if (a.is_f) a.f = -a.f;
-    else {
-      if (a.i == (-9223372036854775807LL - 1)) return EV_UNSUP;
-      a.i = -a.i;
-    }
+  if (a.is_f == 1) {
+    if (op == OP_INV) return EV_ERR;  // ~float -> TypeError
+    a.f = -a.f;
     return EV_OK;
   }
-  if (a.is_f) return EV_ERR;  // ~float -> TypeError
-  a.i = ~a.i;
+  if (a.is_f == 0 && !(op == OP_NEG && a.i == (-9223372036854775807LL - 1))) {
+    a.i = op == OP_NEG ? -a.i : ~a.i;
+    return EV_OK;
+  }
+  // a big int, or -(-2^63): -a, ~a = -(a + 1)
+  const int s = bc.alloc();
+  if (s < 0) return EV_UNSUP;
+  uint32_t* w = bc.at(s);
+  int st = BIG_OK;
+  if (op == OP_NEG) {
+    big_copy(w, bc.view(a, 0));
+    if (big_n(w)) w[1] ^= 1u;
+  } else {
+    uint32_t* one = bc.imm + 4;
+    big_set_i64(one, 1);
+    st = big_add(bc.view(a, 0), one, false, w);
+    if (big_n(w)) w[1] ^= 1u;
+  }
+  bc.release(a);
+  if (st) return big_status(st);
+  bc.finish(s, a);
   return EV_OK;
 }
 
@@ -244,30 +323,111 @@ __device__ double int_true_div(long long a, long long b) {
   return neg ? -v : v;
 }
 
-__device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
-  const bool fl = a.is_f || b.is_f;
+// float(x) of an int or float operand (PyLong_AsDouble for a big int: OverflowError past DBL_MAX)
+__device__ __forceinline__ int to_f(const Val& v, BigCtx& bc, double& out) {
+  if (v.is_f != kBig) {
+    out = v.as_f();
+    return EV_OK;
+  }
+  return big_status(big_to_double(bc.at((int)v.i), out));
+}
+
+// int (op) int past int64, or with a big operand: bigint.hpp into a fresh slot
+__device__ int big_binary(int op, const Val& a, const Val& b, Val& out, BigCtx& bc) {
+  const int s = bc.alloc();
+  if (s < 0) return EV_UNSUP;
+  uint32_t* w = bc.at(s);
+  const uint32_t* A = bc.view(a, 0);
+  const uint32_t* Bv = bc.view(b, 1);
+  int st = BIG_OK;
+  switch (op) {
+    case OP_ADD: st = big_add(A, Bv, false, w); break;
+    case OP_SUB: st = big_add(A, Bv, true, w); break;
+    case OP_MUL: st = big_mul(A, Bv, w); break;
+    case OP_FDIV: st = big_floordiv(A, Bv, w, nullptr, bc.un, bc.vn); break;
+    case OP_MOD: st = big_floordiv(A, Bv, nullptr, w, bc.un, bc.vn); break;
+    case OP_AND: st = big_bitop(0, A, Bv, w); break;
+    case OP_OR: st = big_bitop(1, A, Bv, w); break;
+    case OP_XOR: st = big_bitop(2, A, Bv, w); break;
+    case OP_POW: {  // b >= 0 here
+      unsigned long long e;
+      if (big_n(Bv) > 2) e = ~0ull;  // past 2^64: only |a| <= 1 stays in range
+      else e = (big_n(Bv) > 0 ? big_d(Bv)[0] : 0u) | (big_n(Bv) > 1 ? (unsigned long long)big_d(Bv)[1] << 32 : 0ull);
+      if (e == ~0ull && big_bits(A) <= 1) e = (big_n(Bv) ? (big_d(Bv)[0] & 1u) : 0u) + 2;  // same parity, >= 2
+      st = big_pow(A, e, w, bc.xs, bc.xs + kBigWords);
+      break;
+    }
+    case OP_SHL:
+    case OP_SHR: {  // b >= 0 here
+      const bool huge = big_n(Bv) > 2 || (big_n(Bv) == 2 && big_d(Bv)[1] >= 0x80000000u);
+      const unsigned long long k = huge ? (1ull << 62)
+                                        : (big_n(Bv) > 0 ? big_d(Bv)[0] : 0u) |
+                                              (big_n(Bv) > 1 ? (unsigned long long)big_d(Bv)[1] << 32 : 0ull);
+      if (op == OP_SHL) st = big_shl(A, k, w);
+      else big_shr_floor(A, k, w);
+      break;
+    }
+    default: st = BIG_RANGE;
+  }
+  bc.release(a);
+  bc.release(b);
+  if (st) {
+    bc.free_mask |= 1u << s;
+    return big_status(st);
+  }
+  bc.finish(s, out);
+  return EV_OK;
+}
+
+__device__ int apply_binary(int op, const Val& a, const Val& b, Val& out, BigCtx& bc) {
+  const bool fl = a.is_f == 1 || b.is_f == 1;
+  const bool big = a.is_f == kBig || b.is_f == kBig;
   out.is_f = false;
   out.i = 0;
   out.f = 0;
+  double x = 0.0, y = 0.0;
+  if (fl) {  // float arithmetic: an int operand converts (OverflowError for a big int past DBL_MAX)
+    int st = to_f(a, bc, x);
+    if (st == EV_OK) st = to_f(b, bc, y);
+    bc.release(a);
+    bc.release(b);
+    if (st != EV_OK) return st;
+  }
   switch (op) {
     case OP_ADD:
     case OP_SUB:
     case OP_MUL:
       if (fl) {
-        const double x = a.as_f(), y = b.as_f();
         out.is_f = true;
         out.f = op == OP_ADD ? x + y : (op == OP_SUB ? x - y : x * y);
         return EV_OK;
       } else {
         long long r;
-        bool ov = op == OP_ADD ? __builtin_add_overflow(a.i, b.i, &r)
-                               : (op == OP_SUB ? __builtin_sub_overflow(a.i, b.i, &r) : __builtin_mul_overflow(a.i, b.i, &r));
-        if (ov) return EV_UNSUP;
-        out.i = r;
-        return EV_OK;
+        if (!big) {
+          bool ov = op == OP_ADD ? __builtin_add_overflow(a.i, b.i, &r)
+                                 : (op == OP_SUB ? __builtin_sub_overflow(a.i, b.i, &r)
+                                                 : __builtin_mul_overflow(a.i, b.i, &r));
+          if (!ov) {
+            out.i = r;
+            return EV_OK;
+          }
+        }
+        return big_binary(op, a, b, out, bc);
       }
     case OP_DIV: {
       if (!fl) {
+        if (big) {  // CPython long_true_divide on the big values (the result is a float: no slot)
+          const uint32_t* A = bc.view(a, 0);
+          const uint32_t* Bv = bc.view(b, 1);
+          double r;
+          const int st = big_true_div(A, Bv, r, bc.un, bc.vn, bc.xs, bc.xs);
+          bc.release(a);
+          bc.release(b);
+          if (st) return big_status(st);
+          out.is_f = true;
+          out.f = r;
+          return EV_OK;
+        }
         if (b.i == 0) return EV_ERR;
         const long long lim = 9007199254740992LL;
         if (a.i > lim || a.i < -lim || b.i > lim || b.i < -lim) {
@@ -275,74 +435,106 @@ __device__ int apply_binary(int op, const Val& a, const Val& b, Val& out) {
           out.f = int_true_div(a.i, b.i);
           return EV_OK;
         }
+        x = (double)a.i;
+        y = (double)b.i;
       }
-      const double y = b.as_f();
       if (y == 0.0) return EV_ERR;
       out.is_f = true;
-      out.f = a.as_f() / y;
+      out.f = x / y;
       return EV_OK;
     }
     case OP_FDIV:
     case OP_MOD:
       if (fl) {
-        const double y = b.as_f();
         if (y == 0.0) return EV_ERR;
         double mod;
-        const double q = py_floor_div_f(a.as_f(), y, &mod);
+        const double q = py_floor_div_f(x, y, &mod);
         out.is_f = true;
         out.f = op == OP_FDIV ? q : mod;
         return EV_OK;
       } else {
-        if (b.i == 0) return EV_ERR;
-        if (a.i == (-9223372036854775807LL - 1) && b.i == -1) return EV_UNSUP;
-        long long q = a.i / b.i, r = a.i % b.i;
-        if (r != 0 && ((r < 0) != (b.i < 0))) {
-          q -= 1;
-          r += b.i;
+        if (!big) {
+          if (b.i == 0) return EV_ERR;
+          if (!(a.i == (-9223372036854775807LL - 1) && b.i == -1)) {
+            long long q = a.i / b.i, r = a.i % b.i;
+            if (r != 0 && ((r < 0) != (b.i < 0))) {
+              q -= 1;
+              r += b.i;
+            }
+            out.i = op == OP_FDIV ? q : r;
+            return EV_OK;
+          }
         }
-        out.i = op == OP_FDIV ? q : r;
-        return EV_OK;
+        return big_binary(op, a, b, out, bc);  // ZeroDivisionError from bigint.hpp for a zero divisor
       }
-    case OP_POW:
-      if (!fl && b.i >= 0) {
-        long long base = a.i, e = b.i, acc = 1;
-        while (e) {
-          if (e & 1) {
-            if (__builtin_mul_overflow(acc, base, &acc)) return EV_UNSUP;
+    case OP_POW: {
+      const bool bneg = b.is_f == kBig ? big_neg(bc.at((int)b.i)) : b.i < 0;
+      if (!fl && !bneg) {
+        if (!big) {
+          long long base = a.i, e = b.i, acc = 1;
+          bool ov = false;
+          while (e) {
+            if ((e & 1) && __builtin_mul_overflow(acc, base, &acc)) {
+              ov = true;
+              break;
+            }
+            e >>= 1;
+            if (e && __builtin_mul_overflow(base, base, &base)) {  // base overflow matters only if a bit remains
+              ov = true;
+              break;
+            }
           }
-          e >>= 1;
-          if (e && __builtin_mul_overflow(base, base, &base)) {
-            // base overflow only matters if another bit remains
-            return EV_UNSUP;
+          if (!ov) {
+            out.i = acc;
+            return EV_OK;
           }
         }
-        out.i = acc;
-        return EV_OK;
+        return big_binary(op, a, b, out, bc);
       } else {
-        if (!fl && a.i == 0) return EV_ERR;  // 0 ** negative int -> ZeroDivisionError
+        if (!fl) {  // int ** negative int: float(a) ** float(b) (CPython long_pow -> float_pow)
+          if (a.is_f == 0 && a.i == 0) {
+            bc.release(b);
+            return EV_ERR;  // 0 ** negative int -> ZeroDivisionError
+          }
+          int st = to_f(a, bc, x);
+          if (st == EV_OK) st = to_f(b, bc, y);
+          bc.release(a);
+          bc.release(b);
+          if (st != EV_OK) return st;
+        }
         out.is_f = true;
-        return float_pow(a.as_f(), b.as_f(), out.f);
+        return float_pow(x, y, out.f);
       }
+    }
     case OP_SHL:
     case OP_SHR:
       if (fl) return EV_ERR;
-      if (b.i < 0) return EV_ERR;  // ValueError: negative shift count
-      if (op == OP_SHR) {
-        out.i = b.i >= 64 ? (a.i < 0 ? -1 : 0) : (a.i >> b.i);
-      } else {
-        if (a.i == 0) { out.i = 0; return EV_OK; }
-        if (b.i >= 63) return EV_UNSUP;
-        const long long r = a.i * (1LL << b.i);
-        if ((r >> b.i) != a.i) return EV_UNSUP;
-        out.i = r;
+      if (b.is_f == kBig ? big_neg(bc.at((int)b.i)) : b.i < 0) return EV_ERR;  // ValueError: negative shift count
+      if (!big) {
+        if (op == OP_SHR) {
+          out.i = b.i >= 64 ? (a.i < 0 ? -1 : 0) : (a.i >> b.i);
+          return EV_OK;
+        }
+        if (a.i == 0) {
+          out.i = 0;
+          return EV_OK;
+        }
+        long long r;  // (a * 2^b without signed-overflow UB: the compiler may not assume it away)
+        if (b.i < 63 && !__builtin_mul_overflow(a.i, 1LL << b.i, &r)) {
+          out.i = r;
+          return EV_OK;
+        }
       }
-      return EV_OK;
+      return big_binary(op, a, b, out, bc);
     case OP_AND:
     case OP_OR:
     case OP_XOR:
       if (fl) return EV_ERR;
-      out.i = op == OP_AND ? (a.i & b.i) : (op == OP_OR ? (a.i | b.i) : (a.i ^ b.i));
-      return EV_OK;
+      if (!big) {
+        out.i = op == OP_AND ? (a.i & b.i) : (op == OP_OR ? (a.i | b.i) : (a.i ^ b.i));
+        return EV_OK;
+      }
+      return big_binary(op, a, b, out, bc);
   }
   return EV_ERR;
 }
@@ -357,16 +549,16 @@ struct SVal {
 };
 __device__ __forceinline__ SVal pack(const Val& v) {
   SVal s;
-  s.bits = v.is_f ? __double_as_longlong(v.f) : v.i;
+  s.bits = v.is_f == 1 ? __double_as_longlong(v.f) : v.i;  // a big int keeps its slot index
   s.is_f = v.is_f;
   s.pad = 0;
   return s;
 }
 __device__ __forceinline__ Val unpack(const SVal& s) {
   Val v;
-  v.is_f = s.is_f != 0;
-  v.i = s.is_f ? 0 : s.bits;
-  v.f = s.is_f ? __longlong_as_double(s.bits) : 0.0;
+  v.is_f = s.is_f;
+  v.i = s.is_f == 1 ? 0 : s.bits;
+  v.f = s.is_f == 1 ? __longlong_as_double(s.bits) : 0.0;
   return v;
 }
 constexpr int kMachineBytes = kStack * (int)sizeof(SVal) + kStack;  // per thread, in LDS
@@ -377,6 +569,7 @@ struct Machine {
   int nv = 0, no = 0;
   int status = EV_OK;
   bool ev = true;  // false: the syntax pass (stack shapes only, no arithmetic)
+  BigCtx big;      // ints past int64
 
   __device__ bool reduce_one() {
     const int op = ops[--no];
@@ -389,14 +582,14 @@ struct Machine {
     if (op == OP_NEG || op == OP_POS || op == OP_INV) {
       if (nv < 1) { status = EV_ERR; return false; }
       Val a = unpack(vals[nv - 1]);
-      const int st = apply_unary(op, a);
+      const int st = apply_unary(op, a, big);
       if (st != EV_OK) { status = st; return false; }
       vals[nv - 1] = pack(a);
       return true;
     }
     if (nv < 2) { status = EV_ERR; return false; }
     Val r;
-    const int st = apply_binary(op, unpack(vals[nv - 2]), unpack(vals[nv - 1]), r);
+    const int st = apply_binary(op, unpack(vals[nv - 2]), unpack(vals[nv - 1]), r, big);
     if (st != EV_OK) { status = st; return false; }
     vals[nv - 2] = pack(r);
     nv -= 1;
@@ -434,9 +627,13 @@ __device__ const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  
                                       1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
 // Lex a number literal at s[i]; returns the index after it.  status EV_ERR = SyntaxError;
-// EV_UNSUP with v.is_f == kValidLit: a valid literal whose value is outside the model.
+// EV_UNSUP with v.is_f == kValidLit: a valid literal whose value is outside the model;
+// EV_UNSUP with v.is_f == kBigLit: an int literal past int64 (v.i = its first byte), which the
+// evaluation builds as a big int.
 constexpr int kValidLit = 2;
+constexpr int kBigLit = 4;
 __device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
+  const int start = i;
   uint64_t mant = 0;
   int ndig = 0, frac = 0, exp10 = 0;
   bool is_float = false, overflow = false, leading_zero = false, nonzero_digit = false;
@@ -510,8 +707,9 @@ __device__ int lex_number(const uint8_t* s, int n, int i, Val& v, int& status) {
       return i;
     }
     if (overflow || mant > 9223372036854775807ull) {
-      status = EV_UNSUP;  // Python big int
-      v.is_f = kValidLit;
+      status = EV_UNSUP;  // a Python big int: built by the evaluation (bigint.hpp)
+      v.is_f = kBigLit;
+      v.i = start;
       return i;
     }
     v.is_f = false;
@@ -616,9 +814,10 @@ __device__ int name_outcome(const uint8_t* s, int n) {
 // evaluate = false: the syntax pass.  Python compiles before it evaluates, so a syntax error
 // anywhere wins over whatever the evaluation would meet first (an int past int64: EV_UNSUP);
 // countdown_reward runs this pass first and evaluates only a well-formed answer.
-__device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work, bool evaluate = true) {
+__device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work, uint8_t* pool, bool evaluate = true) {
   Machine m;
   m.ev = evaluate;
+  if (evaluate) m.big.init(pool);
   m.vals = reinterpret_cast<SVal*>(work);
   m.ops = reinterpret_cast<int8_t*>(work + kStack * sizeof(SVal));
   bool expect_operand = true;
@@ -650,7 +849,18 @@ __device__ int py_eval(const uint8_t* s, int n, Val& out, uint8_t* work, bool ev
       Val v;
       int st = EV_OK;
       i = lex_number(s, n, i, v, st);
-      if (st == EV_UNSUP && !evaluate && v.is_f == kValidLit) st = EV_OK;  // a valid literal, value outside the model
+      if (st == EV_UNSUP && !evaluate && (v.is_f == kValidLit || v.is_f == kBigLit)) {
+        st = EV_OK;  // a valid literal (the syntax pass needs no value)
+        v.is_f = 0;
+      }
+      if (st == EV_UNSUP && v.is_f == kBigLit) {  // an int literal past int64
+        const int slot = m.big.alloc();
+        if (slot < 0) return EV_UNSUP;
+        const int bst = big_from_dec(s + v.i, i - (int)v.i, m.big.at(slot));
+        if (bst) return EV_UNSUP;  // past the bound
+        m.big.finish(slot, v);
+        st = EV_OK;
+      }
       if (st != EV_OK) return st;
       if (!m.push_val(v)) return m.status;
       expect_operand = false;
@@ -935,23 +1145,24 @@ __device__ __forceinline__ bool fast_reward(const uint8_t* row, int n, const int
 // staged: s is the answer in this thread's LDS row (the fast path reads it there)
 __device__ double countdown_reward(const uint8_t* s, int n, bool staged, const int32_t (&nums)[kMaxNums],
                                    int n_nums, int32_t target, double score, double format_score, uint8_t& flags,
-                                   uint8_t& err, uint8_t* work) {
+                                   uint8_t& err, uint8_t* work, uint8_t* pool) {
   flags = 0;
   Val v;
   bool fmt = false;
   int st = EV_ERR;
   if (!staged || !fast_reward(s, n, nums, n_nums, fmt, st, v, work)) {
     fmt = check_format(s, n, nums, n_nums);
-    if (fmt) st = py_eval(s, n, v, work, false);
-    if (fmt && st == EV_OK) st = py_eval(s, n, v, work, true);
+    if (fmt) st = py_eval(s, n, v, work, pool, false);
+    if (fmt && st == EV_OK) st = py_eval(s, n, v, work, pool, true);
   }
   if (!fmt) return 0.0;
   flags |= 1;
   bool correct = false;
   if (st == EV_UNSUP) err |= RMI_ERR_UNSUP;
   if (st == EV_OK) {
-    if (v.is_f) correct = fabs(v.f - (double)target) < 1e-5;  // abs(result - target) < 1e-5
-    else correct = v.i == (long long)target;
+    if (v.is_f == 1) correct = fabs(v.f - (double)target) < 1e-5;  // abs(result - target) < 1e-5
+    else if (v.is_f == 0) correct = v.i == (long long)target;
+    // a big int (past int64) never equals an int32 target; Python compares int and float exactly
   }
   if (!correct) return format_score;
   flags |= 2;
@@ -1004,6 +1215,10 @@ __device__ unsigned long long* g_cd_pstamps;  // [waves][8] inside par_reward (r
 constexpr int kRow = 16;
 constexpr int kParDepth = 3;
 constexpr int kParBytes = 16 * kRow + 2 * kRow + kRow + kRow;  // value slots, children, keys, mask bytes
+// par: the cooperative path's scratch, or (the fallback, after it) the result broadcast in its
+// first kParHead bytes and the big-int pool behind them
+constexpr int kParHead = 16;
+constexpr int kParRegion = kParBytes > kParHead + kBigPoolBytes ? kParBytes : kParHead + kBigPoolBytes;
 enum : int { C_NONE = 0, C_NUM, C_LP, C_RP, C_ADD, C_SUB, C_MUL, C_DIV };
 
 template <int CTRL>
@@ -1257,7 +1472,7 @@ __device__ double row_reward(const uint8_t* stage, const uint8_t* src_global, in
     if (j == 0) {
       uint8_t fl = 0, e = 0;
       const double r = countdown_reward(stage ? stage : src_global, n, stage != nullptr, nums, n_nums, target,
-                                        score, format_score, fl, e, work);
+                                        score, format_score, fl, e, work, par + kParHead);
       *bv = r;
       *bf = (uint32_t)fl | (uint32_t)e << 8;
     }
@@ -1300,7 +1515,7 @@ constexpr int kCdBlock = 64;
 __device__ __attribute__((aligned(16))) const uint32_t kZero16[4] = {0, 0, 0, 0};
 // a staged row is 16-B aligned and readable 80 bytes past its start (the token reads)
 __host__ __device__ constexpr int stage_stride(int Lmax) { return Lmax <= kStageMax ? ((Lmax + 15) & ~15) + 16 : 0; }
-__host__ __device__ constexpr int cd_slice(int Lmax) { return stage_stride(Lmax) + kMachineBytes + kParBytes; }
+__host__ __device__ constexpr int cd_slice(int Lmax) { return stage_stride(Lmax) + kMachineBytes + kParRegion; }
 
 __device__ __forceinline__ void load_nums(const rmi_countdown_t& env, int64_t b, int32_t (&nums)[kMaxNums]) {
 #pragma unroll

@@ -64,11 +64,12 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   const int64_t So = S - 1;  // output columns
   const int64_t* row = kAsm ? nullptr : ids + b * S;
   int64_t a_src = 0, pad = 0;
+  uint8_t e_unsup = 0;  // the row's error byte is written once, at the end (no pre-zeroed buffer)
   if (kAsm) {
     const int64_t o0 = as.off[b], o1 = as.len ? o0 + as.len[b] : as.off[b + 1];
     pad = S - (o1 - o0);
     if (pad < 0) {  // a row longer than S: flagged, assembled from its last S tokens
-      if (lane == 0) err[b] |= RMI_ERR_UNSUP;
+      e_unsup = RMI_ERR_UNSUP;
       a_src = o1 - S;
       pad = 0;
     } else {
@@ -208,6 +209,9 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   // a __threadfence() here would add an L2 write-back per row
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (So <= 0 || !turn_scores) {  // no per-turn positions: only the overlong bit can be set
+    if (lane == 0) err[b] = e_unsup;
+  }
   if (So <= 0) return;  // a one-column batch has no score / mask columns
   if (!turn_scores) {
     if (lane == 0) {  // score_tensor[:, -1] = python sum(all_scores[b]), kept by [:, 1:]
@@ -222,7 +226,9 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   const bool slot = lane < n_slots;
   const float s = slot && lane < nb && lane < T ? (float)scores[(int64_t)lane * B + b] : 0.0f;
   const int n = slot ? cnt[lane] : 0, p = slot ? pos[lane] : -1;
-  if (__any(n > 1) && lane == 0) err[b] |= RMI_ERR_STATE;  // the reference's mask assignment raises
+  // the reference's mask assignment raises on a turn with several reward positions
+  const bool multi = __any(n > 1);  // (a wave-wide vote: every lane takes part)
+  if (lane == 0) err[b] = e_unsup | (multi ? (uint8_t)RMI_ERR_STATE : (uint8_t)0);
   // positions -> output column: roll (+1, Qwen) then drop column 0
   auto out_col = [&](int64_t q) -> int64_t { return (roll ? (q + 1) % S : q) - 1; };
   if (slot && n == 1 && p != S - 1) {

@@ -359,7 +359,7 @@ __device__ __forceinline__ Names load_names(const rmi_parse_cfg_t& cfg, int col)
 // One response, staged: its len bytes at T + kPre of the wave's LDS (T, Wb, EL, ES, EI: the
 // regions of parse_lds).  Adds the implicit "<think>" / "<answer>" prefix and the zero tail,
 // then the regex, the special-token cascade, the split and the name lookup, and writes row b's
-// outputs.  err: bits already set for this row (ORed into a.err[b]).
+// outputs.  err: bits already set for this row (with the parse's own: a.err[b] = them).
 __device__ __forceinline__ void parse_row(const ParseArgs& a, uint8_t* T, uint8_t* Wb, uint16_t* EL, uint16_t* ES,
                                           uint8_t* EI, int64_t b, int len, uint8_t err, const Names& nm,
                                           int lane PSTAMP_PARAM) {
@@ -532,7 +532,7 @@ __device__ __forceinline__ void parse_row(const ParseArgs& a, uint8_t* T, uint8_
       a.spans[4 * b + 2] = as < 0 ? -1 : as - base;
       a.spans[4 * b + 3] = ae < 0 ? -1 : ae - base;
     }
-    if (err_all && a.err) a.err[b] |= err_all;
+    if (a.err) a.err[b] = err_all;  // every row's byte written: no pre-zeroed buffer
   }
   PSTAMP(6);
 }
@@ -830,7 +830,7 @@ __device__ __forceinline__ int detok_row(const DetokArgs& d, uint8_t* buf, uint8
   const uint64_t any_bad = __ballot(bad), any_over = __ballot(over);
   if (lane == 0) {
     d.out_len[b] = n;
-    if (d.err_out) d.err_out[b] |= (any_bad ? RMI_ERR_INDEX : 0) | (any_over ? RMI_ERR_UNSUP : 0);
+    if (d.err_out) d.err_out[b] = (uint8_t)((any_bad ? RMI_ERR_INDEX : 0) | (any_over ? RMI_ERR_UNSUP : 0));
   }
   DSTAMP(5);
   return n;
@@ -1176,7 +1176,7 @@ __device__ void parse_rows4(const ParseArgs& a, uint8_t* wave_lds, int64_t b, bo
       a.spans[4 * b + 2] = as < 0 ? -1 : as - base;
       a.spans[4 * b + 3] = ae < 0 ? -1 : ae - base;
     }
-    if (err_all && a.err) a.err[b] |= err_all;
+    if (a.err) a.err[b] = err_all;
   }
 }
 
@@ -1230,36 +1230,52 @@ int seg_waves_per_group(int stride) {
   const size_t n = kWgLds / seg_wave_lds(stride);
   return n >= (size_t)kRowWaves ? kRowWaves : (n < 1 ? 1 : (int)n);
 }
-// ---- the turn's generations onto the env batch (rmi_gen_rows): one wave per env row
-__global__ __launch_bounds__(256) void gen_rows_kernel(const int64_t* __restrict__ resp, int64_t R,
-                                                       const int64_t* __restrict__ src, int64_t n_envs,
-                                                       const uint32_t* __restrict__ packed, int64_t V,
-                                                       int64_t* __restrict__ ids, int32_t* __restrict__ n_ids,
-                                                       uint8_t* __restrict__ has, int32_t* __restrict__ raw_max) {
-  const int64_t e = (int64_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+// ---- the turn's generations onto the env batch (rmi_gen_rows): one wave per env row.  The
+// rows' longest raw byte count is reduced per wave (scan), then per 16-wave block (LDS), and
+// reaches raw_max with ONE atomic per block: every wave's atomicMax on the same word (8192 at the
+// bench size) serialised at the memory side and made this an 80-us launch.
+constexpr int kGenWaves = 16;
+__global__ __launch_bounds__(64 * kGenWaves) void gen_rows_kernel(const int64_t* __restrict__ resp, int64_t R,
+                                                                  const int64_t* __restrict__ src, int64_t n_envs,
+                                                                  const uint32_t* __restrict__ packed, int64_t V,
+                                                                  int64_t* __restrict__ ids, int32_t* __restrict__ n_ids,
+                                                                  uint8_t* __restrict__ has, int32_t* __restrict__ raw_max) {
+  __shared__ int wave_max[kGenWaves];
+  const int wv = threadIdx.x / 64;
+  const int64_t e = (int64_t)blockIdx.x * kGenWaves + wv;
   const int lane = threadIdx.x & 63;
-  if (e >= n_envs) return;
-  const int64_t r = src ? src[e] : e;
-  int64_t* orow = ids ? ids + e * R : nullptr;
-  int raw = 0;
-  if (r >= 0) {
-    const int64_t* row = resp + r * R;
-    for (int64_t k = lane; k < R; k += 64) {
-      const int64_t t = row[k];
-      if (orow) orow[k] = t;
-      const int64_t c = t < 0 ? 0 : (t >= V ? V - 1 : t);  // the clamp of the sizing (ids outside
-      const uint32_t meta = packed[4 * c + 3];              // [0, V) are flagged by the decode)
-      raw += (meta >> 31) ? 0 : (int)(meta & 0xFFFFFFu);
+  int best = -1;  // this wave's row: its raw bytes, -1 = none
+  if (e < n_envs) {
+    const int64_t r = src ? src[e] : e;
+    int64_t* orow = ids ? ids + e * R : nullptr;
+    int raw = 0;
+    if (r >= 0) {
+      const int64_t* row = resp + r * R;
+      for (int64_t k = lane; k < R; k += 64) {
+        const int64_t t = row[k];
+        if (orow) orow[k] = t;
+        const int64_t c = t < 0 ? 0 : (t >= V ? V - 1 : t);  // the clamp of the sizing (ids outside
+        const uint32_t meta = packed[4 * c + 3];              // [0, V) are flagged by the decode)
+        raw += (meta >> 31) ? 0 : (int)(meta & 0xFFFFFFu);
+      }
+    } else if (orow) {
+      for (int64_t k = lane; k < R; k += 64) orow[k] = 0;
     }
-  } else if (orow) {
-    for (int64_t k = lane; k < R; k += 64) orow[k] = 0;
+    if (lane == 0) {
+      if (n_ids) n_ids[e] = r >= 0 ? (int32_t)R : 0;
+      if (has) has[e] = r >= 0 ? 1 : 0;
+    }
+    const int tot = __builtin_amdgcn_readlane(wave_inclusive_scan(raw), 63);
+    best = r >= 0 ? tot : -1;
   }
-  if (lane == 0) {
-    if (n_ids) n_ids[e] = r >= 0 ? (int32_t)R : 0;
-    if (has) has[e] = r >= 0 ? 1 : 0;
+  if (lane == 0) wave_max[wv] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int m = -1;
+#pragma unroll
+    for (int w = 0; w < kGenWaves; ++w) m = wave_max[w] > m ? wave_max[w] : m;
+    if (m >= 0) atomicMax(raw_max, m);
   }
-  const int tot = __builtin_amdgcn_readlane(wave_inclusive_scan(raw), 63);
-  if (lane == 0 && r >= 0) atomicMax(raw_max, tot);
 }
 
 }  // namespace
@@ -1365,8 +1381,7 @@ RMI_API int rmi_gen_rows(const int64_t* resp, int64_t n_resp, int64_t R, const i
   hipStream_t st = as_stream(stream);
   if (hipMemsetAsync(raw_max, 0, sizeof(int32_t), st) != hipSuccess) return RMI_EDEVICE;
   if (n_envs == 0) return RMI_OK;
-  const int per_block = 4;  // waves (rows) per 256-thread block
-  hipLaunchKernelGGL(gen_rows_kernel, dim3((unsigned)((n_envs + per_block - 1) / per_block)), dim3(64 * per_block), 0,
+  hipLaunchKernelGGL(gen_rows_kernel, dim3((unsigned)((n_envs + kGenWaves - 1) / kGenWaves)), dim3(64 * kGenWaves), 0,
                      st, resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has, raw_max);
   return launch_status();
 }

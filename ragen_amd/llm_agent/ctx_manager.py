@@ -420,18 +420,17 @@ class ContextManager:
 
     def prompts(self):
         """The device prompt builder, or None where it does not apply (no device vocab or env
-        manager, max_context_window set, or a tokenizer / chat template outside
-        prompts.DevicePrompts' envelope: the reason is warned once)."""
+        manager, or a tokenizer / chat template outside prompts.DevicePrompts' envelope: the
+        reason is warned once).  max_context_window > 0 selects its window mode."""
         if self._prompts is not None:
             return self._prompts or None
         if self.device_vocab is None or self._es is None or not self.device_prompts:
             return None
-        if getattr(self.config.agent_proxy, "max_context_window", None) not in (None, 0, -1):
-            self._prompts = False
-            return None
+        max_k = getattr(self.config.agent_proxy, "max_context_window", None)
+        window = max_k if isinstance(max_k, int) and max_k > 0 else None  # ctx_manager.py:244-246
         from .prompts import DevicePrompts
         try:
-            self._prompts = DevicePrompts(self, self._es, self.tokenizer, self.device)
+            self._prompts = DevicePrompts(self, self._es, self.tokenizer, self.device, window=window)
         except NotImplementedError as e:
             warnings.warn(f"device prompt ids off, host tokenizer used: {e}", RuntimeWarning)
             self._prompts = False
@@ -828,7 +827,10 @@ class ContextManager:
         from .. import distributed as rd
         parts = es.metric_arrays()
         sharded = self.process_group is not None and self.world_size > 1
-        local = {tag: np.concatenate([m, custom[:, None].astype(np.float64)], 1) for tag, m, custom, _ in parts}
+        local = {}  # per tag NAME, env order (a tag listed twice in the config: its entries' rows in order)
+        for tag, m, custom, _ in parts:
+            rows = np.concatenate([m, custom[:, None].astype(np.float64)], 1)
+            local[tag] = np.concatenate([local[tag], rows]) if tag in local else rows
         per_tag = {}
         for tag in dict.fromkeys(self.es_cfg.env_configs.tags):  # every rank, same order (collectives)
             rows = local.get(tag, np.zeros((0, 5), np.float64))

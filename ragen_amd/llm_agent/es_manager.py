@@ -705,8 +705,7 @@ class EnvStateManager:
         self._materialize()
         self._states_pending = False
         eff_k, val_k = "action_is_effective", "action_is_valid"
-        for tag, m, custom, info in self.metric_arrays():
-            tg = next(x for x in self.tags if x.tag == tag)
+        for tg, (tag, m, custom, info) in zip(self.tags, self.metric_arrays()):  # one entry per config entry
             succ = m[:, 0].tolist()
             na = m[:, 1].astype(np.int64).tolist()
             eff, val = m[:, 2].tolist(), m[:, 3].tolist()

@@ -31,8 +31,15 @@ the ContextManager keeps the host path.  A row the kernels flag (text past the r
 code point NFC may change, a reward outside the formatter's range) is built and tokenized on
 the host for that env alone (``host_rows``), and counted in ``self.host_rows_used``.
 
-``agent_proxy.max_context_window`` (history truncation with re-numbered turns) is not built
-incrementally: the ContextManager keeps the host path for it.
+``agent_proxy.max_context_window`` = k (history truncation with re-numbered turns,
+ctx_manager.py:244-246) changes every prompt each turn (the window slides and the ``Turn i``
+headers renumber), so it is not an append: the rows are REBUILT on the device from the kept
+turn records (``window`` mode) -- the first kept entry's block (``Turn 1`` and its state, as a
+reset writes it) and, per later entry, the assistant block and the reward / next-state block
+with its renumbered header, each through rmi_prompt_text + rmi_bpe_encode into the env's arena
+row.  The generation batch rebuilds the active envs' windows each turn; the update batch
+rebuilds each env's last k complete entries (envs grouped by their turn count).  A row the
+kernels flag is rebuilt on the host from the env's history (the reference's own message code).
 """
 import warnings
 from typing import List, Optional
@@ -90,8 +97,9 @@ class ChatTemplate:
 class DevicePrompts:
     """Per-env prompt ids on the device for one ContextManager / EnvStateManager pair."""
 
-    def __init__(self, ctx, es, tokenizer, device, capacity: Optional[int] = None):
+    def __init__(self, ctx, es, tokenizer, device, capacity: Optional[int] = None, window: Optional[int] = None):
         ap = ctx.config.agent_proxy
+        self.window = int(window) if window else None  # max_context_window (k > 0), or None
         self.ctx, self.es, self.tok = ctx, es, tokenizer
         self.device = torch.device(device)
         self.enable_think = bool(ap.enable_think)
@@ -242,16 +250,40 @@ class DevicePrompts:
             {j: tg.batch.render_rows() for j, tg in enumerate(es.tags) if hasattr(tg.batch, "render_rows")}
         obs, obs_len = self._obs(rows)
         ints = self.mapt.clone()
-        pieces = [self.tpl.head, (_lib.PT_TAG_CONST, 0, 0), "\nTurn 1:\nState:\n", (_lib.PT_OBS, 0, 0),
-                  "\nYou have ", (_lib.PT_INT, 0, 0), self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
-        stride = self._stride(obs.shape[1] + self._max_prefix + 1024)
-        text, tlen, _, terr = self._run_text(pieces, stride, obs, obs_len, ints)
         self.len.zero_()
+        if self.window:  # rows are rebuilt per batch from the turn records (_build_window)
+            self._obs0 = (obs, obs_len, ints)
+            self.len_upd.zero_()
+            return
+        text, tlen, terr, stride = self._first_text(obs, obs_len, ints)
         self._encode(text, tlen, terr, None, stride, lambda e: self._host_first(e))
         self.len_upd.copy_(self.len)
 
+    def _first_text(self, obs, obs_len, ints, active=None):
+        """The first user block (system + instruction prefix + ``Turn 1`` + the state; at reset,
+        and as the first kept entry of a window) -> (text, len, err, stride)."""
+        pieces = [self.tpl.head, (_lib.PT_TAG_CONST, 0, 0), "\nTurn 1:\nState:\n", (_lib.PT_OBS, 0, 0),
+                  "\nYou have ", (_lib.PT_INT, 0, 0), self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
+        stride = self._stride(obs.shape[1] + self._max_prefix + 1024)
+        text, tlen, _, terr = self._run_text(pieces, stride, obs, obs_len, ints, active=active)
+        return text, tlen, terr, stride
+
     def advance(self, d):
         """Append turn d["turn"] (a device-path turn record of EnvStateManager._step_device)."""
+        t = d["turn"]
+        if self.window:  # window mode: the rows are rebuilt per batch (_build_window)
+            self.turns_done = t + 1
+            return
+        text, tlen, mark, terr, stride, last, flags = self._turn_text(d, t + 2, d["has"])
+        self._encode(text, tlen, terr, mark, stride,
+                     lambda e: self._host_turn(e, t, not last and not int(flags[e]) & _lib.FLAG_DONE),
+                     active=d["has"])
+        self.turns_done = t + 1
+
+    def _turn_text(self, d, number, active):
+        """The text turn d["turn"] appends: the assistant block (its end marked: the update rows
+        stop there) and, for an env that goes on, the user block with the reward and the next
+        state under the header ``Turn {number}``.  -> (text, len, mark, err, stride, last, flags)."""
         t = d["turn"]
         inp = d["inp"]
         obs, obs_len = self._obs(d["obs"])
@@ -267,16 +299,82 @@ class DevicePrompts:
         ints = d["left"]
         pieces = [self.tpl.a_pre, (_lib.PT_RESPONSE, 0, 0), self.tpl.a_suf, (_lib.PT_MARK, 0, 0),
                   (_lib.PT_IF, 0, 0), self.tpl.u_pre + "Reward:\n", (_lib.PT_REWARD, 0, 0),
-                  f"\n\nTurn {t + 2}:\nState:\n", (_lib.PT_OBS, 0, 0), "\nYou have ", (_lib.PT_INT, 0, 0), self._c_mid,
-                  (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
+                  f"\n\nTurn {number}:\nState:\n", (_lib.PT_OBS, 0, 0), "\nYou have ", (_lib.PT_INT, 0, 0),
+                  self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
         stride = self._stride(resp.shape[1] + obs.shape[1] + 1024)
         last = t + 1 >= self.max_turn
         text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, None, resp,
-                                                resp_len, spans, None, d["has"], turn=(ne, flags, last))
-        self._encode(text, tlen, terr, mark, stride,
-                     lambda e: self._host_turn(e, t, not last and not int(flags[e]) & _lib.FLAG_DONE),
-                     active=d["has"])
-        self.turns_done = t + 1
+                                                resp_len, spans, None, active, turn=(ne, flags, last))
+        return text, tlen, mark, terr, stride, last, flags
+
+    # ----------------------------------------------------------- max_context_window
+    def _entry_state(self, j):
+        """(obs, obs_len, actions_left) of history entry j: the reset's, or the turn j-1 record's."""
+        if j == 0:
+            return self._obs0
+        d = self.es._turn_records[j - 1]
+        obs, obs_len = self._obs(d["obs"])
+        return obs, obs_len, d["left"]
+
+    def _build_window(self, sel, n_done, update):
+        """Rebuild the arena rows of the envs in ``sel`` (u8/bool[n_envs] on the device), every one
+        with ``n_done`` completed turns, as their last-k history window (ctx_manager.py:244-246):
+        generation rows keep entries 0..n_done (the last holds the current state only), update
+        rows entries 0..n_done-1 (prepare_for_update drops the last state, :240-241).  The
+        kept entries are renumbered ``Turn 1..``.  Rows a kernel flags are rebuilt on the host."""
+        k = self.window
+        n_entries = n_done if update else n_done + 1
+        j0 = max(0, n_entries - k)
+        sel = sel.to(torch.uint8)
+        keep = sel == 0
+        self.len.copy_(torch.where(keep, self.len, torch.zeros_like(self.len)))
+        self.len_upd_w = self.len_upd.clone()  # the marks this rebuild records
+        obs, obs_len, ints = self._entry_state(j0)
+        text, tlen, terr, stride = self._first_text(obs, obs_len, ints, active=sel)
+        bad = self._encode_window(text, tlen, terr, None, stride, sel)
+        for j in range(j0, n_done):
+            d = self.es._turn_records[j]
+            act = sel & d["has"].to(torch.uint8) if d["has"] is not None else sel
+            text, tlen, mark, terr, stride, _, _ = self._turn_text(d, j - j0 + 2, act)
+            bad |= self._encode_window(text, tlen, terr, mark, stride, act)
+        if update:
+            self.len_upd.copy_(torch.where(keep, self.len_upd, self.len_upd_w))
+        if bool(bad.any()):
+            idx = torch.nonzero(bad).flatten().cpu().tolist()
+            self.host_rows_used += len(idx)
+            warnings.warn(f"{len(idx)} prompt rows built on the host (text past the device row buffer, an NFC-changing "
+                          "code point, or an unsupported reward)", RuntimeWarning)
+            for e in idx:
+                self._host_window(e, update)
+
+    def _encode_window(self, text, tlen, terr, mark, stride, active):
+        """Append one block of a window rebuild; -> the rows the device could not build."""
+        mx = int(tlen.max()) if tlen.numel() else 0
+        n_tok, mark_tok, err = self.dt.encode_rows(text, tlen, self.arena, self.len, mark, max_len=max(mx, 4))
+        if mark is not None:
+            self.len_upd_w = torch.where(active.bool(), mark_tok, self.len_upd_w)
+        return ((err != 0) | (terr != 0)) & active.bool()
+
+    def _host_window(self, e, update):
+        """Env e's window row tokenized on the host: the reference's messages for its history
+        (ContextManager._build_messages applies max_context_window), the generation tail cut off
+        (pad_rows appends it) -- or, for an update row, the whole text."""
+        self.es._materialize()
+        entry = dict(self.es.rollout_cache[e])
+        entry["history"] = list(entry["history"])
+        texts, _ = self.ctx._build_messages([entry], update)
+        ids = self._host_ids(texts[0])
+        if not update:
+            tail = self.tail.tolist()
+            if ids[-len(tail):] != tail:
+                raise RuntimeError("the host prompt does not end with the generation tail")
+            ids = ids[:-len(tail)]
+        if len(ids) > self.cap:
+            raise RuntimeError(f"env {e}: prompt longer than the device arena ({self.cap} tokens)")
+        self.arena[e, :len(ids)] = torch.tensor(ids, dtype=torch.int64, device=self.device)
+        self.len[e] = len(ids)
+        if update:
+            self.len_upd[e] = len(ids)
 
     @staticmethod
     def _stride(n):
@@ -352,6 +450,10 @@ class DevicePrompts:
     def gen_batch(self, env_ids: np.ndarray):
         """get_lm_inputs(prepare_for_update=False)'s tensors for these envs (device)."""
         rows = torch.from_numpy(np.asarray(env_ids, np.int64) - self.es.env_lo).to(self.device)
+        if self.window and rows.numel():  # every active env has the same turn count
+            sel = torch.zeros(self.n_envs, dtype=torch.uint8, device=self.device)
+            sel[rows] = 1
+            self._build_window(sel, self.turns_done, update=False)
         if not rows.numel():
             self._resolve()
             S = 1
@@ -368,6 +470,12 @@ class DevicePrompts:
     def update_rows(self):
         """(tokens, row_start, row_len) of formulate_rollouts' rows, env order."""
         self._resolve()
+        if self.window:  # each env's last k complete entries: envs grouped by their turn count
+            eps = [tg.batch.ep for tg in self.es.tags]
+            n_t = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
+            for n in sorted(set(n_t.cpu().tolist())):
+                if n > 0:
+                    self._build_window(n_t == n, int(n), update=True)
         start = torch.arange(self.n_envs, dtype=torch.int64, device=self.device) * self.cap
         return self.arena.view(-1), start, self.len_upd
 

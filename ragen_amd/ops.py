@@ -487,7 +487,6 @@ def parse_actions(cfg: _lib.ParseCfg, text: torch.Tensor, text_len: torch.Tensor
                                                                    "action_len", "err"))
         if actions.shape != (B, K) or (at is not None and at.shape != (B, K, int(action_text_len))):
             raise ValueError("out= buffers do not match this batch")
-        err.zero_()
     else:
         actions = torch.empty(B, K, dtype=torch.int8, device=dev)
         n_actions = torch.empty(B, dtype=torch.uint8, device=dev)
@@ -496,7 +495,7 @@ def parse_actions(cfg: _lib.ParseCfg, text: torch.Tensor, text_len: torch.Tensor
         if action_text_len:
             at = torch.empty(B, K, int(action_text_len), dtype=torch.uint8, device=dev)
             al = torch.empty(B, K, dtype=torch.int32, device=dev)
-        err = torch.zeros(B, dtype=torch.uint8, device=dev)
+        err = torch.empty(B, dtype=torch.uint8, device=dev)
     check(lib().rmi_parse_actions(ctypes.byref(cfg), _ptr(text), _ptr(text_len), B, stride, _ptr(sel), _ptr(actions),
                                   _ptr(n_actions), _ptr(spans), _ptr(at), _ptr(al), int(action_text_len), _ptr(err),
                                   _stream(text.device)), "rmi_parse_actions")
@@ -607,11 +606,10 @@ def detokenize(ids: torch.Tensor, vocab: VocabTable, stride: int, n_ids: Optiona
         out, n, err = out
         if out.shape != (B, stride):
             raise ValueError("out= buffers do not match this batch")
-        err.zero_()
     else:
         out = torch.empty(B, stride, dtype=torch.uint8, device=dev)
         n = torch.empty(B, dtype=torch.int32, device=dev)
-        err = torch.zeros(B, dtype=torch.uint8, device=dev)
+        err = torch.empty(B, dtype=torch.uint8, device=dev)
     return detokenize_packed(ids, vocab.packed, vocab.data, stride, n_ids, (out, n, err))
 
 
@@ -646,18 +644,16 @@ def detok_parse(ids: torch.Tensor, vocab: "VocabTable", stride: int, cfg: _lib.P
     if out is not None:
         if out["text"].shape != (B, stride) or out["actions"].shape != (B, K):
             raise ValueError("out= buffers do not match this batch")
-        out["decode_err"].zero_()
-        out["err"].zero_()
         o = out
     else:
         o = {"text": torch.empty(B, stride, dtype=torch.uint8, device=dev),
              "text_len": torch.empty(B, dtype=torch.int32, device=dev),
-             "decode_err": torch.zeros(B, dtype=torch.uint8, device=dev),
+             "decode_err": torch.empty(B, dtype=torch.uint8, device=dev),
              "actions": torch.empty(B, K, dtype=torch.int8, device=dev),
              "n_actions": torch.empty(B, dtype=torch.uint8, device=dev),
              "spans": torch.empty(B, 4, dtype=torch.int32, device=dev) if with_spans else None,
              "action_text": None, "action_len": None,
-             "err": torch.zeros(B, dtype=torch.uint8, device=dev)}
+             "err": torch.empty(B, dtype=torch.uint8, device=dev)}
         if action_text_len:
             o["action_text"] = torch.empty(B, K, int(action_text_len), dtype=torch.uint8, device=dev)
             o["action_len"] = torch.empty(B, K, dtype=torch.int32, device=dev)
@@ -690,7 +686,7 @@ def masks_and_scores(ids: torch.Tensor, special_token: int, reward_token: int, s
     score = torch.empty(B, So, dtype=torch.float32, device=dev)
     lm = torch.empty(B, So, dtype=torch.bool, device=dev)
     rm = torch.empty(B, So, dtype=torch.bool, device=dev)
-    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    err = torch.empty(B, dtype=torch.uint8, device=dev)
     flags = ((_lib.MS_TURN_SCORES if use_turn_scores else 0) | (_lib.MS_RESPONSE_MASK if enable_response_mask else 0)
              | (_lib.MS_ROLL if roll else 0))
     check(lib().rmi_masks_and_scores(_ptr(ids), B, S, int(special_token), int(reward_token), _ptr(scores.contiguous()),
@@ -723,7 +719,7 @@ def assemble_batch(tokens: torch.Tensor, row_off: torch.Tensor, S: int, pad_id: 
     score = torch.empty(B, So, dtype=torch.float32, device=dev)
     lm = torch.empty(B, So, dtype=torch.bool, device=dev)
     rm = torch.empty(B, So, dtype=torch.bool, device=dev)
-    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    err = torch.empty(B, dtype=torch.uint8, device=dev)
     flags = ((_lib.MS_TURN_SCORES if use_turn_scores else 0) | (_lib.MS_RESPONSE_MASK if enable_response_mask else 0)
              | (_lib.MS_ROLL if roll else 0))
     check(lib().rmi_assemble_batch(_ptr(tokens), _ptr(row_off), B, int(S), int(pad_id), int(special_token),
@@ -755,7 +751,7 @@ def assemble_rows(tokens: torch.Tensor, row_start: torch.Tensor, row_len: torch.
     score = torch.empty(B, So, dtype=torch.float32, device=dev)
     lm = torch.empty(B, So, dtype=torch.bool, device=dev)
     rm = torch.empty(B, So, dtype=torch.bool, device=dev)
-    err = torch.zeros(B, dtype=torch.uint8, device=dev)
+    err = torch.empty(B, dtype=torch.uint8, device=dev)
     flags = ((_lib.MS_TURN_SCORES if use_turn_scores else 0) | (_lib.MS_RESPONSE_MASK if enable_response_mask else 0)
              | (_lib.MS_ROLL if roll else 0))
     check(lib().rmi_assemble_rows(_ptr(tokens), _ptr(row_start), _ptr(row_len), B, int(S), int(pad_id),
@@ -806,7 +802,7 @@ def pad_rows(arena: torch.Tensor, arena_len: torch.Tensor, rows: torch.Tensor, t
     ids = torch.empty(n, S, dtype=torch.int64, device=dev)
     am = torch.empty_like(ids)
     pos = torch.empty_like(ids)
-    err = torch.zeros(n, dtype=torch.uint8, device=dev)
+    err = torch.empty(n, dtype=torch.uint8, device=dev)
     check(lib().rmi_pad_rows(_ptr(arena), arena.shape[1], _ptr(arena_len), _ptr(rows), n, _ptr(tail), tail.numel(),
                              int(S), int(pad_id), _ptr(ids), _ptr(am), _ptr(pos), _ptr(err), _stream(dev)),
           "rmi_pad_rows")

@@ -633,7 +633,7 @@ def detokenize(ids: Tensor, n_ids: Optional[Tensor], vocab_packed: Tensor, vocab
     B = ids.shape[0]
     st = (int(stride) + 3) // 4 * 4
     out = (torch.empty(B, st, dtype=torch.uint8, device=ids.device), torch.empty(B, dtype=torch.int32, device=ids.device),
-           torch.zeros(B, dtype=torch.uint8, device=ids.device))
+           torch.empty(B, dtype=torch.uint8, device=ids.device))  # every row's error byte is written
     return ops.detokenize_packed(ids, vocab_packed, vocab_bytes, st, n_ids, out)
 
 

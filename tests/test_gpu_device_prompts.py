@@ -138,3 +138,72 @@ def test_device_prompts_response_branches(device, qwen_tok, think, monkeypatch):
         dev, dev_proxy, dev_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, True)
     assert dev_proxy.train_ctx_manager.prompts().host_rows_used > 0
     _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)
+
+
+@pytest.mark.parametrize("grouping", ["inductive", "batch"])
+def test_device_formulate_groupings_repeated_tag(device, grouping, monkeypatch):
+    """formulate_rollouts' reward normalisation on the device path (ContextManager.
+    _normalize_device) == the host path (segments_for over the per-env tags,
+    ctx_manager.py:184-191) with mean_std on a config that lists a tag twice: the reference
+    groups "inductive" by tag NAME, so SimpleSokoban's two entries are one group."""
+    from ragen_amd.config import AttrDict
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    cfg = _config("sokoban_es")
+    ec = cfg.es_manager.train.env_configs
+    ec.tags, ec.n_groups = ["SimpleSokoban", "LargerSokoban", "SimpleSokoban"], [3, 2, 3]
+    cfg.agent_proxy.reward_normalization = AttrDict(grouping=grouping, method="mean_std")
+    tok = FakeQwenTok()
+    _, ng, gs, T, _ = TRACES["sokoban_es"]
+    B = ng * gs
+    turn_tokens = [_ids(tok, _responses("sokoban_es", t, B), device) for t in range(T)]
+    ref, ref_proxy, ref_prompts = _rollout(cfg, tok, turn_tokens, device, False)
+    dev, dev_proxy, dev_prompts = _rollout(cfg, tok, turn_tokens, device, True)
+    assert dev_proxy.train_ctx_manager.prompts() is not None
+    sc = ref.batch["rm_scores"][:, -1].cpu()
+    if grouping == "inductive":  # the two SimpleSokoban entries normalised together: mean 0 over both
+        sok = torch.cat([torch.arange(0, 48), torch.arange(80, 128)])
+        assert abs(float(sc[sok].double().mean())) < 1e-5
+    _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)
+
+
+@pytest.mark.parametrize("k", [1, 2])
+@pytest.mark.parametrize("name", list(TRACES))
+def test_device_prompts_context_window(device, name, k, monkeypatch):
+    """agent_proxy.max_context_window = k (ctx_manager.py:244-246: the last k history entries,
+    renumbered Turn 1..k) on the device path: every turn's generation batch, the formulated
+    batch, its metrics and messages == the host path, on all five golden traces; the device
+    rows are rebuilt on the device (no host rows)."""
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok()
+    cfg = _config(name)
+    cfg.agent_proxy.max_context_window = k
+    _, ng, gs, T, _ = TRACES[name]
+    B = ng * gs
+    turn_tokens = [_ids(tok, _responses(name, t, B), device) for t in range(T)]
+    ref, ref_proxy, ref_prompts = _rollout(cfg, tok, turn_tokens, device, False)
+    dev, dev_proxy, dev_prompts = _rollout(cfg, tok, turn_tokens, device, True)
+    pr = dev_proxy.train_ctx_manager.prompts()
+    assert pr is not None and pr.window == k and pr.host_rows_used == 0
+    _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)
+    # the window holds at most k turns (test_context_window.py:60-84's assertion, per env)
+    for msgs in dev.non_tensor_batch["messages_list"]:
+        text = " ".join(m["content"] for m in msgs)
+        assert text.count("\nTurn ") <= k and f"\nTurn {k + 1}:" not in text
+
+
+def test_device_prompts_context_window_qwen_bpe(device, qwen_tok, monkeypatch):
+    """The window rebuild with the Qwen2-pipeline byte-level BPE (rmi_bpe_encode) on the longest
+    trace, k = 2."""
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    cfg = _config("frozenlake_es")
+    cfg.agent_proxy.max_context_window = 2
+    _, ng, gs, T, _ = TRACES["frozenlake_es"]
+    B = ng * gs
+    turn_tokens = [_ids(qwen_tok, _responses("frozenlake_es", t, B), device) for t in range(T)]
+    ref, ref_proxy, ref_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, False)
+    dev, dev_proxy, dev_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, True)
+    assert dev_proxy.train_ctx_manager.prompts().host_rows_used == 0
+    _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)
