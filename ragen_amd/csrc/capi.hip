@@ -4,22 +4,19 @@
 namespace rmi {
 namespace {
 
-// 16 B per lane, grid-stride (MI355X_MICROARCH.md: the float4 copy that measures the achievable
-// HBM bandwidth, 6.29 TB/s); 256-thread blocks, grid capped at 2048 blocks (HIP guide,
-// guideline 11).  Two 16-B loads in flight per lane before the stores.
+// 16 B per lane, grid-stride, nontemporal (MI355X_MICROARCH.md: the float4 copy that measures
+// the achievable HBM bandwidth).  The grid is what sets the rate: tools/copy_probe.hip swept
+// loads in flight per lane (1, 2, 4, 8), nontemporal vs plain, grid-stride vs one chunk per
+// block and 2 / 4 / 8 / 16 blocks per CU over a 1 GiB copy (profiles/r04_copy_probe.json):
+// 4 blocks per CU with one 16-B load per lane per step reads + writes 6.00 TB/s, 2 per CU with
+// two loads 5.98, while the 8-per-CU grid this used before (2048 blocks) reached 4.86.
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(kBlock) void stream_copy_kernel(v4u* __restrict__ dst, const v4u* __restrict__ src,
                                                              int64_t n16) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
-  int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  for (; i + stride < n16; i += 2 * stride) {
-    const v4u a = __builtin_nontemporal_load(src + i);
-    const v4u b = __builtin_nontemporal_load(src + i + stride);
-    __builtin_nontemporal_store(a, dst + i);
-    __builtin_nontemporal_store(b, dst + i + stride);
-  }
-  if (i < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
 __global__ void tail_copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, int64_t n) {
@@ -40,8 +37,15 @@ RMI_API int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream
   const bool aligned = ((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src)) & 15u) == 0;
   const int64_t n16 = aligned ? (int64_t)(bytes / 16) : 0;
   if (n16) {
+    static int cus = 0;  // the device's CU count, queried once
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1)
+        cus = 256;
+    }
     int64_t blocks = (n16 + kBlock - 1) / kBlock;
-    if (blocks > 2048) blocks = 2048;
+    if (blocks > 4 * (int64_t)cus) blocks = 4 * (int64_t)cus;
     hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, static_cast<v4u*>(dst),
                        static_cast<const v4u*>(src), n16);
   }

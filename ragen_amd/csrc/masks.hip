@@ -257,7 +257,11 @@ RMI_API int rmi_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64
   using namespace rmi;
   if (B < 0 || S < 0 || T < 0 || n_slots < 0) return RMI_EINVAL;
   if (n_slots > kMaxSlots || B > 0x7FFFFFFF) return RMI_EUNSUP;
-  if (B == 0 || S <= 1) return RMI_OK;
+  if (B == 0) return RMI_OK;
+  if (S <= 1) {  // no score / mask columns: only the error bytes (the kernels write every row's)
+    if (!err) return RMI_EINVAL;
+    return hipMemsetAsync(err, 0, (size_t)B, as_stream(stream)) == hipSuccess ? RMI_OK : RMI_EDEVICE;
+  }
   if (!ids || !n_scores || !score_out || !loss_mask || !response_mask || !err || (T > 0 && !scores))
     return RMI_EINVAL;
   hipLaunchKernelGGL(masks_kernel<false>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), ids, B, S, special_token,

@@ -739,6 +739,14 @@ class ContextManager:
         eps = [tg.batch.ep for tg in es.tags]
         tab = (eps[0].turn_reward if len(eps) == 1 else torch.cat([ep.turn_reward for ep in eps], 1)).contiguous()
         n_sc = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
+        if pr.window:  # the kept entries' rewards only: the reference reads the TRIMMED history (:282)
+            k = pr.window
+            j0 = (n_sc - k).clamp(min=0)
+            n_w = n_sc - j0
+            i = torch.arange(k, device=dev, dtype=torch.int32)[:, None]
+            src = (j0[None, :] + i).clamp(max=tab.shape[0] - 1).long()
+            tab = torch.gather(tab, 0, src).masked_fill(i >= n_w[None, :], 0.0).contiguous()
+            n_sc = n_w.to(torch.int32)
         if getattr(self, "_special", None) is None:  # a tokenizer call: once per manager
             self._special = get_special_tokens(self.tokenizer)
         special_token, reward_token = self._special
@@ -773,6 +781,7 @@ class ContextManager:
         metrics["response_length"] = response_length
         out.meta_info = {"metrics": metrics}
         es._formulated = True
+        es._formulated_window = pr.window
         return out
 
     def _normalize_device(self, score_tensor, es):

@@ -256,9 +256,12 @@ class EnvStateManager:
         if self._formulated:  # formulate_rollouts dropped each history's last state (ctx_manager.py:236-237)
             self._formulated = False
             self._untrimmed = [c["history"] for c in self._rc]
+            k = getattr(self, "_formulated_window", None)
             for cache in self._rc:
                 if "state" in cache["history"][-1]:
                     cache["history"] = cache["history"][:-1]
+                if k:  # and kept only the last max_context_window entries (ctx_manager.py:244-246)
+                    cache["history"] = cache["history"][-k:]
         return self._rc
 
     # ---------------------------------------------------------------------- reset
