@@ -311,6 +311,26 @@ def advantage_leg(R, device, reps=20):
     bl_us = e[0].elapsed_time(e[1]) * 1e3 / reps
     grpo_us = e[1].elapsed_time(e[2]) * 1e3 / reps
     tok_b = rb.shape[0] * rb.shape[1]
+    del rb, vb, mb
+    # bi-level GAE past the Infinity Cache: the same turn-score rows left-padded to 4096 tokens
+    # (8192 x 4096: 570 MB of algorithmic traffic per launch), as GAE's out_of_cache
+    rb4, vb4, mb4 = (torch.from_numpy(x).to(device)
+                     for x in synthetic.token_rows(n_turns, score, seed=12, turn_scores=tr, max_len=4096))
+    ops.bilevel_gae(rb4, vb4, mb4, 1.0, 0.95, 0.95, check_errors=False)
+    torch.cuda._sleep(2_000_000)
+    e[0].record()
+    for _ in range(5):
+        ops.bilevel_gae(rb4, vb4, mb4, 1.0, 0.95, 0.95, check_errors=False)
+    e[1].record()
+    torch.cuda.synchronize()
+    bl4_us = e[0].elapsed_time(e[1]) * 1e3 / 5
+    tok_b4 = rb4.numel()
+    bl_out = {"rows": rb4.shape[0], "cols": rb4.shape[1], "tokens_per_launch": tok_b4, "us": bl4_us,
+              "achieved_GBs": tok_b4 * 17 / (bl4_us * 1e-6) / 1e9,
+              "frac": tok_b4 * 17 / (bl4_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+              "cache": "out of the 256 MiB Infinity Cache (570 MB per launch)",
+              "traffic": _pmc_field(os.path.join(ROOT, "profiles", "r*_pmc_bilevel_4096.json"), "hbm_bytes_per_launch")}
+    del rb4, vb4, mb4
     return {"kernel": "rmi_gae (legacy) + row stats", "rows": B, "cols": L, "tokens_per_launch": tokens,
             "cache": "in the Infinity Cache (152 MB per launch, repeated on the same buffers)",
             "out_of_cache": out_of_cache,
@@ -320,7 +340,7 @@ def advantage_leg(R, device, reps=20):
                                  "frac": mgbs / HBM_PEAK_GBS, "bytes_per_token": 14},
             "assemble_batch": assemble,
             "bilevel_gae": {"kernel": "rmi_bilevel_gae", "tokens": tok_b, "us": bl_us,
-                            "achieved_GBs": tok_b * 17 / (bl_us * 1e-6) / 1e9},
+                            "achieved_GBs": tok_b * 17 / (bl_us * 1e-6) / 1e9, "out_of_cache": bl_out},
             "grpo": {"kernel": "rmi_grpo_outcome", "tokens": tok_b, "us": grpo_us,
                      "achieved_GBs": tok_b * 13 / (grpo_us * 1e-6) / 1e9}}
 

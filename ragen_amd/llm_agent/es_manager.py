@@ -588,19 +588,14 @@ class EnvStateManager:
         # decode + parse in one launch per tag unless the rows were decoded already
         parsed = None if inp.is_decoded else self._decode_parse(inp, bool(ap.enable_think), ap.action_sep)
         # a generation the device decode truncated (row stride cap) or could not decode (an id
-        # outside the vocabulary) must not be stepped on: checked before the turn runs
-        if bool(inp.err.any()):
-            bad = int(torch.nonzero(inp.err)[0, 0])
-            raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
-                             "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP)")
-        # the envs with a generation: all of them, every one still running (has_input = None:
-        # the turn kernels then step the envs not done), or the rows given
-        if inp.has_t is None and self._all_active:
-            has = None
-        elif inp.has_t is None:
-            has = torch.ones(self.n_envs, dtype=torch.uint8, device=dev)
+        # outside the vocabulary) is not stepped on: masked out of the turn on the device and
+        # raised after it, from the turn's one readback (no host synchronisation before the turn)
+        dec_ok = inp.err == 0
+        # the envs with a generation (minus undecodable ones): all of them, or the rows given
+        if inp.has_t is None:
+            has = dec_ok.to(torch.uint8)
         else:
-            has = inp.has_t  # written by rmi_gen_rows
+            has = inp.has_t * dec_ok  # has_t written by rmi_gen_rows
         err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
         if parsed is None:
             parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
@@ -615,8 +610,12 @@ class EnvStateManager:
         # one device -> host copy: the active set and the turn's per-env error bits, raised in
         # the step where they happen, as the reference raises inside its per-env loop
         n_in = len(inp.env_ids)
-        host = torch.cat([flags, err]).cpu().numpy()
-        fl_h, err_h = host[:self.n_envs], host[self.n_envs:]
+        host = torch.cat([flags, err, inp.err]).cpu().numpy()
+        fl_h, err_h, dec_h = host[:self.n_envs], host[self.n_envs:2 * self.n_envs], host[2 * self.n_envs:]
+        if dec_h.any():
+            bad = int(np.nonzero(dec_h)[0][0])
+            raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
+                             "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP); its env was not stepped")
         still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
         self._all_active = n_in == self.n_envs and bool(still.all())
         if err_h.any():

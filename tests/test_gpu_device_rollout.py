@@ -68,3 +68,26 @@ def test_device_rollout_equals_dict_rollout(device, name, monkeypatch):
     assert np.asarray(ref.non_tensor_batch["messages_list"]).tolist() == \
         np.asarray(dev.non_tensor_batch["messages_list"]).tolist()
     assert ref_cache == dev_cache
+
+
+def test_device_step_undecodable_generation_raises_unstepped(device, monkeypatch):
+    """A generation the device decode cannot take (an id outside the vocabulary) is masked out
+    of the turn on the device and raised from the turn's one readback: ValueError, and that
+    env's record is untouched while the others stepped (no host sync before the turn)."""
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok()
+    rows = _turn_tokens("sokoban_es", tok, device)
+    rows[0] = rows[0].clone()
+    rows[0][5, 0] = 10 ** 9  # env 5: an id past the vocabulary
+    proxy = LLMAgentProxy(_config("sokoban_es"), TokenActor(rows), tok, device=device)
+    proxy.train_ctx_manager.set_device_vocab(ops.VocabTable.from_bytes(*tok.byte_table(), device))
+    es, ctx = proxy.train_es_manager, proxy.train_ctx_manager
+    random.seed(7)
+    outs = es.reset()
+    lm = ctx.get_lm_inputs(outs, prepare_for_update=False)
+    env_inputs = ctx.get_env_inputs(proxy.generate_sequences(lm))
+    with pytest.raises(ValueError, match="env 5"):
+        es.step(env_inputs)
+    n_turns = es.tags[0].batch.ep.n_turns.cpu().numpy()
+    assert n_turns[5] == 0 and (np.delete(n_turns, 5) == 1).all()

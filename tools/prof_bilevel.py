@@ -18,12 +18,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=8192)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--max-len", type=int, default=None, help="left-pad the rows to this many tokens (4096: out of cache)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0)
     n_turns = rng.integers(1, 6, size=a.rows)
     tr = np.full((a.rows, 5), 0.5, np.float32)
-    r, v, m = synthetic.token_rows(n_turns, np.zeros(a.rows, np.float32), seed=12, turn_scores=tr)
+    r, v, m = synthetic.token_rows(n_turns, np.zeros(a.rows, np.float32), seed=12, turn_scores=tr, max_len=a.max_len)
     tokens = r.size
     r, v, m = (torch.from_numpy(x).to(dev) for x in (r, v, m))
     res = {}
