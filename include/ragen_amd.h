@@ -500,6 +500,14 @@ typedef struct {
    * are claimed with an atomic compare-and-swap and published with a release store.        */
   uint32_t* word_cache;
   uint32_t word_cache_mask; /* entries - 1 (a power of two minus one)                        */
+  /* Expansions (n_exp 0: none): added tokens whose id in added_id is -(e + 1) stand for the
+   * id sequence exp_ids[exp_off[e] .. exp_off[e+1]) instead of one id.  Their bytes are
+   * (0xFF, 0x80 + e): never valid UTF-8, so no text holds them; the prompt programs write them
+   * in place of a constant stretch whose tokenization the host has proven context-free at both
+   * ends (llm_agent/prompts.py), so the kernel skips that stretch's bytes.  n_exp <= 64.       */
+  int32_t n_exp;
+  const int32_t* exp_off;   /* [n_exp + 1]                                                   */
+  const int32_t* exp_ids;
 } rmi_bpe_t;
 
 /* Row b: text[b * pitch .. + text_len[b]) (UTF-8; pitch % 4 == 0); `stride` (% 4 == 0,

@@ -44,7 +44,7 @@ constexpr int kMaxStride = 3072;
 // table is small (Qwen2: 22 added tokens, ~300 bytes): phases 1 and 2 then read no global
 // memory per byte.  (They used to: a class lookup was two dependent global loads per byte, and
 // each added-token comparison a chain of global byte loads — ≈64 k cycles of a wave's 161 k.)
-constexpr int kStageAdded = 32, kStageAddedBytes = 512;
+constexpr int kStageAdded = 64, kStageAddedBytes = 768;
 constexpr int kPairBatch = 8;     // 64-pair chunks whose first hash probes go out together
 struct Lds {  // carved from dynamic LDS, n = stride
   uint8_t* T;    // text, n + 16 (zero tail)
@@ -298,8 +298,8 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   if (lane < 8) L.AF[lane] = tok.added_first[lane];
   const bool stage_added = tok.n_added > 0 && tok.n_added <= kStageAdded;
   if (stage_added) {
-    if (lane <= tok.n_added) L.AO[lane] = tok.added_off[lane];
-    if (lane < tok.n_added) L.AI[lane] = tok.added_id[lane];
+    for (int i = lane; i <= tok.n_added; i += 64) L.AO[i] = tok.added_off[i];
+    for (int i = lane; i < tok.n_added; i += 64) L.AI[i] = tok.added_id[i];
   }
   const uint32_t blk0 = tok.cp_block[0];  // the block of U+0000..U+00FF
   for (int i = lane; i < n + 128; i += 64) L.C[i] = 0;
@@ -315,13 +315,15 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   // the staged tokens as 32-byte words (lane a: token a), compared 8 bytes at a time below
   bool added_words = false;
   if (added_lds) {
-    const int o0 = lane < tok.n_added ? L.AO[lane] : 0, len = lane < tok.n_added ? L.AO[lane + 1] - o0 : 0;
-    added_words = !__any(len > 32);
-    if (added_words && lane < tok.n_added) {
+    bool longer = false;
+    for (int a = lane; a < tok.n_added; a += 64) longer |= L.AO[a + 1] - L.AO[a] > 32;
+    added_words = !__any(longer);
+    for (int a = lane; added_words && a < tok.n_added; a += 64) {
+      const int o0 = L.AO[a], len = L.AO[a + 1] - o0;
       uint64_t w[4] = {0, 0, 0, 0};
       for (int k = 0; k < len; ++k) w[k >> 3] |= (uint64_t)L.AB[o0 + k] << (8 * (k & 7));
 #pragma unroll
-      for (int q = 0; q < 4; ++q) L.AW[4 * lane + q] = w[q];
+      for (int q = 0; q < 4; ++q) L.AW[4 * a + q] = w[q];
     }
     wave_sync();
   }
@@ -331,6 +333,11 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   for (int p = lane; p < n; p += 64) {
     const uint32_t b0 = L.T[p];
     if ((b0 & 0xC0) == 0x80) continue;  // continuation: written by its lead byte's lane
+    if (b0 == 0xFF && tok.n_exp > 0) {  // an expansion placeholder (0xFF, 0x80 + e): an added token
+      if (p + 2 > n || (L.T[p + 1] & 0xC0) != 0x80) bad = true;
+      else L.C[p] = (uint8_t)B_START;  // class "other"; the index byte keeps 0
+      continue;
+    }
     const int l = utf8_len(b0);
     uint32_t cp = 0;
     if (l == 0 || p + l > n) {
@@ -618,7 +625,10 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
       continue;
     }
     int cnt = 1;
-    if (!(L.C[a] & B_ADD)) {
+    if ((L.C[a] & B_ADD) && L.Y[a] < 0) {  // an expansion: its precomputed ids
+      const int e = -L.Y[a] - 1;
+      cnt = tok.exp_off[e + 1] - tok.exp_off[e];
+    } else if (!(L.C[a] & B_ADD)) {
       for (;;) {
         uint32_t best = kNoRank;
         int bq = -1, bprev = -1, prev = -1;
@@ -669,7 +679,13 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   int64_t* orow = out + b * out_stride + base_len;
   for (int j = lane; j < np; j += 64) {
     int o = L.K[j];
-    for (int q = L.P[j]; q != kEnd; q = L.M[q]) orow[o++] = (int64_t)L.Y[q];
+    const int a = L.P[j];
+    if ((L.C[a] & B_ADD) && L.Y[a] < 0) {  // an expansion: its ids from the table
+      const int e = -L.Y[a] - 1;
+      for (int k = tok.exp_off[e]; k < tok.exp_off[e + 1]; ++k) orow[o++] = (int64_t)tok.exp_ids[k];
+      continue;
+    }
+    for (int q = a; q != kEnd; q = L.M[q]) orow[o++] = (int64_t)L.Y[q];
   }
   if (lane == 0) {
     err[b] = 0;
@@ -698,7 +714,8 @@ RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pi
   if (tok->pretok != RMI_PRETOK_QWEN2 && tok->pretok != RMI_PRETOK_CHARS) return RMI_EUNSUP;
   if (B == 0) return RMI_OK;
   if (!text || !text_len || !out || !err || !tok->cp_block || !tok->cp_class || !tok->byte_id || !tok->merges ||
-      (tok->n_added > 0 && (!tok->added_bytes || !tok->added_off || !tok->added_id)))
+      (tok->n_added > 0 && (!tok->added_bytes || !tok->added_off || !tok->added_id)) || tok->n_exp < 0 ||
+      tok->n_exp > 64 || (tok->n_exp > 0 && (!tok->exp_off || !tok->exp_ids)))
     return RMI_EINVAL;
   // R 8 + Y 4 + M, P, K 2 each + T 1 + C 1 bytes per text byte, the byte ids, bitmap and pads,
   // the ASCII classes and the staged added-token tables

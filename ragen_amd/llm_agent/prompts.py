@@ -94,10 +94,108 @@ class ChatTemplate:
                                       "prompt path does not apply") from None
 
 
+# Context probes of the expansion analysis: every text that may stand next to a constant stretch
+# of a prompt (an LLM response, a rendered state, a reward, an int) is arbitrary, so a cut must
+# hold against every class the Qwen2 pre-tokenizer regex tells apart on either side: letters
+# (and the contraction letters after an apostrophe), digits, other numerics, punctuation, the
+# space, other whitespace, newlines, CR, wide and astral characters -- alone, doubled, tripled
+# and in every ordered pair, plus the shapes the prompts actually carry.  (Combining marks and
+# other NFC-unsafe code points never reach the device encoder: their rows go to the host.)
+_PROBE_CHARS = ["a", "Z", "s", "t", "e", "é", "中", "1", "9", "½", "_", ".", ",", "<", ">", "'", '"', "-", "#", "|",
+                " ", "\t", "\n", "\r", "\u00a0", "\u3000", "\U0001F600"]
+_PROBE_EXTRA = ["'s", "'re", "'ll", "x ", "x\n", " \n", "\n ", "\r\n", "1.5", "-0.1", "10.0", "1e-05", "</answer>",
+                "<answer>", "</think>", "Up || Down", "#_P\n##", "  x", "x  ", "abc def", "<|im_end|>", "<|im_start|>"]
+
+
+def _probes():
+    c = _PROBE_CHARS
+    runs = [w * k for w in (" ", "\t", "\n", "\r\n", "-", "=", "#", "a", "1") for k in (4, 5, 6, 8, 12, 16, 24)]
+    return [""] + c + [x * 2 for x in c] + [x * 3 for x in c] + [a + b for a in c for b in c] + runs + _PROBE_EXTRA
+
+
+class ExpansionSplitter:
+    """Finds, in a constant stretch X of prompt text, the longest middle X[q1:q2] whose token ids
+    do not depend on the text around X:  ids(L + X + R) == ids(L + X[:q1]) + I + ids(X[q2:] + R)
+    for every probe L, R (``_probes``) -- exactly what the device encoder computes when the
+    middle is replaced by an added-token placeholder standing for I (the placeholder cuts the
+    regex segments there).  Cuts are tried at X's own token boundaries, outermost first.  The
+    tokenizer's own `tokenizers` backend encodes (batched); results are cached per text."""
+
+    _by_tok = {}
+    MIN_BYTES = 12  # a shorter middle is not worth a placeholder (2 bytes)
+
+    def __init__(self, backend):
+        self.bt = backend
+        self.probes = _probes()
+        self.cache = {}
+
+    @classmethod
+    def for_tokenizer(cls, tokenizer):
+        bt = getattr(tokenizer, "backend_tokenizer", None)
+        if bt is None or not hasattr(bt, "encode_batch"):
+            return None
+        key = id(bt)
+        if key not in cls._by_tok:
+            cls._by_tok[key] = cls(bt)
+        return cls._by_tok[key]
+
+    def _ids(self, texts):
+        return [e.ids for e in self.bt.encode_batch(list(texts), add_special_tokens=False)]
+
+    def split(self, x: str, right_free: bool = False):
+        """-> (q1, ids of X[q1:q2], q2) in characters, or None.  right_free: nothing but an
+        added token or the row end ever follows X."""
+        key = (x, right_free)
+        if key not in self.cache:
+            self.cache[key] = self._split(x, right_free)
+        return self.cache[key]
+
+    def _split(self, x, right_free):
+        if len(x.encode("utf-8")) < self.MIN_BYTES:
+            return None
+        enc = self.bt.encode(x, add_special_tokens=False)
+        ids, starts = list(enc.ids), [o[0] for o in enc.offsets]
+        cuts = sorted(set(starts) | {0, len(x)})
+        P = self.probes
+        whole_l = self._ids([p + x for p in P])
+        q1 = k1 = None
+        for q in cuts:  # the leftmost cut every left context agrees with
+            k = next((i for i, st in enumerate(starts) if st >= q), len(ids))
+            pre = self._ids([p + x[:q] for p in P])
+            if all(w == a + ids[k:] for w, a in zip(whole_l, pre)):
+                q1, k1 = q, k
+                break
+        if q1 is None:
+            return None
+        R = [""] if right_free else P
+        whole_r = self._ids([x + r for r in R])
+        q2 = k2 = None
+        for q in reversed(cuts):  # the rightmost cut every right context agrees with
+            if q < q1:
+                break
+            k = next((i for i, st in enumerate(starts) if st >= q), len(ids))
+            post = self._ids([x[q:] + r for r in R])
+            if all(w == ids[:k] + b for w, b in zip(whole_r, post)):
+                q2, k2 = q, k
+                break
+        if q2 is None or len(x[q1:q2].encode("utf-8")) < self.MIN_BYTES or k2 <= k1:
+            return None
+        mid = ids[k1:k2]
+        # both sides at once, on a spread of pairs
+        pairs = [(P[i], R[(7 * i + 3) % len(R)]) for i in range(0, len(P), 3)]
+        whole = self._ids([l + x + r for l, r in pairs])
+        lefts = self._ids([l + x[:q1] for l, _ in pairs])
+        rights = self._ids([x[q2:] + r for _, r in pairs])
+        if any(w != a + mid + b for w, a, b in zip(whole, lefts, rights)):
+            return None
+        return q1, mid, q2
+
+
 class DevicePrompts:
     """Per-env prompt ids on the device for one ContextManager / EnvStateManager pair."""
 
-    def __init__(self, ctx, es, tokenizer, device, capacity: Optional[int] = None, window: Optional[int] = None):
+    def __init__(self, ctx, es, tokenizer, device, capacity: Optional[int] = None, window: Optional[int] = None,
+                 expansions: bool = True):
         ap = ctx.config.agent_proxy
         self.window = int(window) if window else None  # max_context_window (k > 0), or None
         self.ctx, self.es, self.tok = ctx, es, tokenizer
@@ -105,6 +203,7 @@ class DevicePrompts:
         self.enable_think = bool(ap.enable_think)
         self.tpl = ChatTemplate(tokenizer)
         self.dt = DeviceTokenizer.from_hf(tokenizer, self.device)
+        self.splitter = ExpansionSplitter.for_tokenizer(tokenizer) if expansions else None
         starts = [s for s in self.dt.added]
         for nm in ("a_pre", "u_pre", "gen"):
             piece = getattr(self.tpl, nm)
@@ -138,6 +237,8 @@ class DevicePrompts:
         self._const_at = {}
         self._pool_dev = None
         self._tag_tables = []
+        self._tag_strings = []   # the tables' strings (the expansion analysis reads them)
+        self._exp_cache = {}     # program -> program with expansions (_with_expansions)
         self._tag_table(prefixes)  # table 0: instruction prefix
         self._tag_table(lengths)   # table 1: length line
         self.mapt = torch.tensor([tg.max_actions_per_traj for tg in tags], dtype=torch.int32,
@@ -163,21 +264,28 @@ class DevicePrompts:
         return [int(x) for x in self.tok([text], padding=False, truncation=False).input_ids[0]]
 
     # ---------------------------------------------------------------- constant pool
-    def _const(self, s: str):
+    def _const(self, s):
+        """The pool (offset, length) of a str (UTF-8) or bytes constant (an expansion placeholder
+        is not valid UTF-8)."""
         if s not in self._const_at:
-            b = s.encode("utf-8")
+            b = s.encode("utf-8") if isinstance(s, str) else bytes(s)
             self._const_at[s] = (len(self._pool), len(b))
             self._pool += b
         return self._const_at[s]
 
     def _tag_table(self, strings):
+        """A per-tag constant table (one entry per tag) -> its index (RMI_PT_TAG_CONST's a)."""
         tab = []
         for s in strings:
             tab += list(self._const(s))
         self._tag_tables.append(tab)
+        self._tag_strings.append(list(strings))
+        return len(self._tag_tables) - 1
 
     def _program(self, pieces):
-        """pieces: (kind, a, b) triples, CONST given as a str -> (program ints, pool, tag_const)."""
+        """pieces: (kind, a, b) triples, CONST given as a str -> (program ints, pool, tag_const).
+        Long constant stretches become expansion placeholders (_with_expansions)."""
+        pieces = self._with_expansions(pieces)
         prog = []
         for p in pieces:
             if isinstance(p, str):
@@ -185,12 +293,68 @@ class DevicePrompts:
                 prog.append((_lib.PT_CONST, off, ln))
             else:
                 prog.append(p)
-        if self._pool_dev is None or self._pool_dev[0] != len(self._pool):  # upload when it grew
+        key = (len(self._pool), len(self._tag_tables))
+        if self._pool_dev is None or self._pool_dev[0] != key:  # upload when the pool or the tables grew
             pad = 4 + (-len(self._pool)) % 4  # whole dwords: the kernel stages the pool with dword loads
             pool = torch.frombuffer(bytearray(self._pool) + b"\0" * pad, dtype=torch.uint8).to(self.device)
             tc = torch.tensor([x for t in self._tag_tables for x in t], dtype=torch.int32, device=self.device)
-            self._pool_dev = (len(self._pool), pool, tc)
+            self._pool_dev = (key, pool, tc)
         return prog, self._pool_dev[1], self._pool_dev[2]
+
+    # ------------------------------------------------------------ expansions
+    @staticmethod
+    def _is_const(p):
+        return isinstance(p, (str, bytes)) or p[0] in (_lib.PT_CONST, _lib.PT_TAG_CONST)
+
+    def _const_text(self, p, tag):
+        if isinstance(p, str):
+            return p
+        if p[0] == _lib.PT_TAG_CONST:
+            return self._tag_strings[p[1]][tag]
+        raise ValueError("pool-offset CONST pieces are not analysed")
+
+    def _with_expansions(self, pieces):
+        """Each maximal run of constant pieces (between variable pieces, MARK and IF) whose middle
+        tokenizes the same whatever text surrounds it (ExpansionSplitter: proven against every
+        context probe, per tag) becomes prefix + placeholder + suffix: the placeholder is an
+        added token of the device tokenizer standing for the middle's ids (rmi_bpe_t
+        expansions), so the BPE kernel skips those bytes.  Cached per program."""
+        key = tuple(pieces)
+        hit = self._exp_cache.get(key)
+        if hit is not None:
+            return hit
+        out, i, n = [], 0, len(pieces)
+        split = self.splitter
+        while i < n:
+            if not self._is_const(pieces[i]) or split is None:
+                out.append(pieces[i])
+                i += 1
+                continue
+            j = i
+            while j < n and self._is_const(pieces[j]):
+                j += 1
+            run = pieces[i:j]
+            texts = ["".join(self._const_text(p, tg) for p in run) for tg in range(self.n_tags)]
+            res = [split.split(t, right_free=(j == n)) for t in texts]
+            if any(r is not None for r in res):
+                pre, ph, post = [], [], []
+                for t, r in zip(texts, res):
+                    mark = self.dt.add_expansion(r[1]) if r is not None else None
+                    if mark is None:
+                        pre.append(t)
+                        ph.append("")
+                        post.append("")
+                    else:
+                        q1, _, q2 = r
+                        pre.append(t[:q1])
+                        ph.append(mark)
+                        post.append(t[q2:])
+                out += [(_lib.PT_TAG_CONST, self._tag_table(x), 0) for x in (pre, ph, post) if any(x)]
+            else:
+                out += run
+            i = j
+        self._exp_cache[key] = out
+        return out
 
     def _run_text(self, pieces, stride, obs, obs_len, ints, reward=None, reward_int=None, resp=None, resp_len=None,
                   spans=None, cond=None, active=None, turn=None):

@@ -165,7 +165,8 @@ class Bpe(ctypes.Structure):
                 ("pretok", ctypes.c_int32), ("nfc", ctypes.c_int32), ("n_added", ctypes.c_int32),
                 ("added_bytes", ctypes.c_void_p), ("added_off", ctypes.c_void_p), ("added_id", ctypes.c_void_p),
                 ("added_first", ctypes.c_uint32 * 8), ("word_cache", ctypes.c_void_p),
-                ("word_cache_mask", ctypes.c_uint32)]
+                ("word_cache_mask", ctypes.c_uint32), ("n_exp", ctypes.c_int32), ("exp_off", ctypes.c_void_p),
+                ("exp_ids", ctypes.c_void_p)]
 
 
 def _backend_json(tokenizer) -> dict:
@@ -252,6 +253,13 @@ class DeviceTokenizer:
     added: dict  # content -> id
     # the word cache (rmi_bpe_t.word_cache): i32[(mask + 1) * 16], zeroed once; None = off
     word_cache: Optional[torch.Tensor] = None
+    # expansions (rmi_bpe_t.n_exp / exp_off / exp_ids): placeholder added tokens standing for a
+    # precomputed id sequence (add_expansion); the tables below are rebuilt when one is added
+    exp: Optional[list] = None
+    exp_off: Optional[torch.Tensor] = None
+    exp_ids: Optional[torch.Tensor] = None
+
+    MAX_EXPANSIONS = 64
 
     WORD_CACHE_ENTRIES = 1 << 15  # 2 MB: the distinct pre-tokens of the prompts with room to spare
 
@@ -312,10 +320,51 @@ class DeviceTokenizer:
             t(np.array(list(added.values()) or [0], np.int32)), first, added,
             torch.zeros(DeviceTokenizer.WORD_CACHE_ENTRIES * 16, dtype=torch.int32, device=device))
 
+    def add_expansion(self, ids) -> bytes:
+        """The placeholder bytes (0xFF, 0x80 + e) of the expansion whose tokens are ``ids`` (a
+        constant stretch of prompt text proven context-free by prompts.py); registered once per
+        distinct id sequence.  The added-token tables grow by the placeholder, with id -(e + 1)."""
+        ids = tuple(int(x) for x in ids)
+        if self.exp is None:
+            self.exp = []
+        if ids in self.exp:
+            e = self.exp.index(ids)
+        else:
+            if len(self.exp) >= self.MAX_EXPANSIONS or not ids or len(ids) > 1024:
+                return None
+            self.exp.append(ids)
+            e = len(self.exp) - 1
+            self._rebuild_added()
+        return bytes([0xFF, 0x80 + e])
+
+    def _rebuild_added(self):
+        dev = self.byte_id.device
+        blobs = [c.encode("utf-8") for c in self.added] + [bytes([0xFF, 0x80 + e]) for e in range(len(self.exp))]
+        id_list = list(self.added.values()) + [-(e + 1) for e in range(len(self.exp))]
+        off = np.zeros(len(blobs) + 1, np.int32)
+        np.cumsum([len(x) for x in blobs], out=off[1:])
+        first = [0] * 8
+        for x in blobs:
+            first[x[0] >> 5] |= 1 << (x[0] & 31)
+        self.added_bytes = torch.from_numpy(np.frombuffer(b"".join(blobs) + b"\0" * 4, np.uint8).copy()).to(dev)
+        self.added_off = torch.from_numpy(off).to(dev)
+        self.added_id = torch.from_numpy(np.array(id_list, np.int32)).to(dev)
+        self.added_first = first
+        eo = np.zeros(len(self.exp) + 1, np.int32)
+        np.cumsum([len(x) for x in self.exp], out=eo[1:])
+        self.exp_off = torch.from_numpy(eo).to(dev)
+        self.exp_ids = torch.from_numpy(np.array([i for x in self.exp for i in x], np.int32)).to(dev)
+
+    @property
+    def n_added(self) -> int:
+        return len(self.added) + (len(self.exp) if self.exp else 0)
+
     def struct(self) -> Bpe:
         s = Bpe(self.cp_block.data_ptr(), self.cp_class.data_ptr(), self.byte_id.data_ptr(), self.merges.data_ptr(),
-                self.merge_mask, self.merge_shift, self.pretok, self.nfc, len(self.added),
+                self.merge_mask, self.merge_shift, self.pretok, self.nfc, self.n_added,
                 self.added_bytes.data_ptr(), self.added_off.data_ptr(), self.added_id.data_ptr())
+        if self.exp:
+            s.n_exp, s.exp_off, s.exp_ids = len(self.exp), self.exp_off.data_ptr(), self.exp_ids.data_ptr()
         for i, w in enumerate(self.added_first):
             s.added_first[i] = w
         if self.word_cache is not None:
@@ -325,7 +374,7 @@ class DeviceTokenizer:
     def args(self):
         """The tables in the order torch.ops.ragen_amd.bpe_encode takes them."""
         return (self.cp_block, self.cp_class, self.byte_id, self.merges, self.added_bytes, self.added_off,
-                self.added_id, [self.merge_mask, self.merge_shift, self.pretok, self.nfc, len(self.added)]
+                self.added_id, [self.merge_mask, self.merge_shift, self.pretok, self.nfc, self.n_added]
                 + list(self.added_first))
 
     def encode_rows(self, text: torch.Tensor, text_len: torch.Tensor, out: torch.Tensor,
@@ -334,7 +383,8 @@ class DeviceTokenizer:
         """Append the ids of every text row to ``out`` (rmi_bpe_encode); max_len (0: the row
         pitch) bounds the rows' length.  -> (n_tok, mark_tok, err)."""
         return torch.ops.ragen_amd.bpe_encode(*self.args(), text, text_len, out, out_len, mark_byte, int(max_len),
-                                              self.word_cache)
+                                              self.word_cache, self.exp_off if self.exp else None,
+                                              self.exp_ids if self.exp else None)
 
     def encode(self, texts: Sequence[str], stride: int = None) -> List[Optional[List[int]]]:
         """Convenience (tests, tools): ids of each text, or None for a row the device flagged."""

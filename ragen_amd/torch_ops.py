@@ -720,7 +720,8 @@ def _(ids, n_ids, vocab_packed, vocab_bytes, stride, cfg, sel, with_spans, actio
             ids.new_empty(B, dtype=torch.uint8))
 
 
-def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache=None):
+def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache=None,
+                exp_off=None, exp_ids=None):
     from .tokenizer import Bpe
     ops._dev(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id)
     if len(params) != 13:
@@ -736,6 +737,11 @@ def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, add
         if n < 1 or n & (n - 1) or word_cache.numel() != 16 * n:
             raise ValueError("word_cache: 16 int32 per entry, a power-of-two number of entries")
         s.word_cache, s.word_cache_mask = word_cache.data_ptr(), n - 1
+    if exp_off is not None:  # expansions: placeholder added tokens standing for id sequences
+        ops._dev(exp_off, exp_ids)
+        ops._dt(exp_off, torch.int32, "exp_off")
+        ops._dt(exp_ids, torch.int32, "exp_ids")
+        s.n_exp, s.exp_off, s.exp_ids = exp_off.numel() - 1, exp_off.data_ptr(), exp_ids.data_ptr()
     return s
 
 
@@ -743,13 +749,15 @@ def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, add
 def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tensor, added_bytes: Tensor,
                added_off: Tensor, added_id: Tensor, params: List[int], text: Tensor, text_len: Tensor, out: Tensor,
                out_len: Optional[Tensor], mark_byte: Optional[Tensor], max_len: int = 0,
-               word_cache: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
+               word_cache: Optional[Tensor] = None, exp_off: Optional[Tensor] = None,
+               exp_ids: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """The tokenizer call of get_lm_inputs (ctx_manager.py:265-278) for a byte-level BPE:
     every text row's ids appended to ``out`` (rmi_bpe_encode; tables: ragen_amd.tokenizer).
     max_len (0: the row pitch) bounds the rows' length and sizes the kernel's LDS.
     -> (n_tok i32[B], mark_tok i32[B], err u8[B])."""
     import ctypes
-    tok = _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache)
+    tok = _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache,
+                      exp_off, exp_ids)
     ops._dev(text, text_len, out, out_len, mark_byte)
     ops._dt(text, torch.uint8, "text")
     ops._dt(text_len, torch.int32, "text_len")
@@ -775,7 +783,7 @@ def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tens
 
 @bpe_encode.register_fake
 def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, text, text_len, out, out_len,
-      mark_byte, max_len=0, word_cache=None):
+      mark_byte, max_len=0, word_cache=None, exp_off=None, exp_ids=None):
     B = text.shape[0]
     return (text.new_empty(B, dtype=torch.int32), text.new_empty(B, dtype=torch.int32),
             text.new_empty(B, dtype=torch.uint8))
