@@ -628,6 +628,10 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
 #else
 #define BL_ARG
 #endif
+#ifndef RMI_BL_DEPTH
+#define RMI_BL_DEPTH 4
+#endif
+constexpr int kBlDepth = RMI_BL_DEPTH;  // tiles in the register pipeline (3 before round 4)
 __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                            const uint8_t* __restrict__ mask, int64_t B, int64_t L,
                                                            float g, float gl, float hg, float hgl,
@@ -647,26 +651,26 @@ __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restri
   BilevelWalk wk{0.0f, 0.0f};
   double s1 = 0.0, s2 = 0.0, cnt = 0.0;
   uint32_t bad = 0;
-  GaeTile ta, tb, tc;
 #ifdef RMI_BL_STAMPS
   unsigned long long bl_acc[3] = {0, 0, 0};
   BL_T(tbeg);
 #endif
+  // a kBlDepth-deep register pipeline of tiles (right to left): tile k is walked while tiles
+  // k-1 .. k-kBlDepth+1 are in flight.  Past the Infinity Cache the walks' serial chains leave
+  // the loads alone in the memory system, so the bytes in flight per CU set the rate.
   const int64_t k0 = ntiles - 1;
-  gae_load_tile(ta, r, v, mask, B, L, row0, k0 * kGCols, lane);
-  gae_load_tile(tb, r, v, mask, B, L, row0, (k0 - 1) * kGCols, lane);
-  for (int64_t k = k0; k >= 0; k -= 3) {
-    gae_load_tile(tc, r, v, mask, B, L, row0, (k - 2) * kGCols, lane);
-    bilevel_tile(ta, k * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg, hgl,
-                 adv, ret BL_ARG);
-    if (k - 1 < 0) break;
-    gae_load_tile(ta, r, v, mask, B, L, row0, (k - 3) * kGCols, lane);
-    bilevel_tile(tb, (k - 1) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
-                 hgl, adv, ret BL_ARG);
-    if (k - 2 < 0) break;
-    gae_load_tile(tb, r, v, mask, B, L, row0, (k - 4) * kGCols, lane);
-    bilevel_tile(tc, (k - 2) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
-                 hgl, adv, ret BL_ARG);
+  GaeTile t[kBlDepth];
+#pragma unroll
+  for (int i = 0; i < kBlDepth - 1; ++i) gae_load_tile(t[i], r, v, mask, B, L, row0, (k0 - i) * kGCols, lane);
+  for (int64_t k = k0; k >= 0; k -= kBlDepth) {
+#pragma unroll
+    for (int j = 0; j < kBlDepth; ++j) {
+      if (k - j < 0) break;
+      gae_load_tile(t[(j + kBlDepth - 1) % kBlDepth], r, v, mask, B, L, row0, (k - j - (kBlDepth - 1)) * kGCols,
+                    lane);
+      bilevel_tile(t[j], (k - j) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
+                   hgl, adv, ret BL_ARG);
+    }
   }
 #ifdef RMI_BL_STAMPS
   BL_T(tend);

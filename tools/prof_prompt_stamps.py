@@ -1,7 +1,7 @@
 """Where the time of the device prompt kernels goes (diagnostic, not product): builds
 prompt.hip or bpe.hip with RMI_STAMPS (tools/build_variant.sh prst prompt.hip -DRMI_STAMPS /
 bpst bpe.hip -DRMI_STAMPS), runs bench.api_leg's rollout (8192 envs) on that library and prints,
-over the waves of the second launch (the first turn's advance), the mean cycles of each phase.
+per launch of the rollout, the mean cycles of each phase and the peak number of resident waves.
     python tools/prof_prompt_stamps.py prompt|bpe"""
 import ctypes
 import os
@@ -10,7 +10,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 WHICH = sys.argv[1] if len(sys.argv) > 1 else "prompt"
-SO = os.path.join(ROOT, "tools", "_build", "libragen_amd_%s.so" % ("prst" if WHICH == "prompt" else "bpst"))
+SO = os.environ.get("RAGEN_AMD_STAMP_SO") or os.path.join(
+    os.environ.get("RAGEN_AMD_VARIANT_DIR", os.path.join(ROOT, "tools", "_build")),
+    "libragen_amd_%s.so" % ("prst" if WHICH == "prompt" else "bpst"))
 os.environ["RAGEN_AMD_LIB"] = SO
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
@@ -50,12 +52,17 @@ assert setter(ctypes.c_void_p(dummy.data_ptr())) == 0
 calls = [0]
 name = "_run_text" if WHICH == "prompt" else "_encode"
 orig = getattr(pm.DevicePrompts, name)
+bufs, lens = [], []
 
 
 def hooked(self, *a, **kw):
     calls[0] += 1
     torch.cuda.synchronize()
-    setter(ctypes.c_void_p((stamps if calls[0] == 2 else dummy).data_ptr()))
+    buf = torch.zeros(B * 16, dtype=torch.int64, device=dev)
+    bufs.append(buf)
+    if WHICH == "bpe":
+        lens.append(int(a[1].max()))
+    setter(ctypes.c_void_p(buf.data_ptr()))
     return orig(self, *a, **kw)
 
 
@@ -64,13 +71,26 @@ random.seed(0)
 actor.turn = 0
 proxy.rollout(DataProto(meta_info={}), val=False)
 torch.cuda.synchronize()
-s = stamps.view(B, 16).cpu().numpy().astype(np.float64)
-ok = (s[:, 0] > 0) & np.all(np.diff(s[:, 0:10:2], axis=1) > 0, axis=1)
-a = s[ok]
 names = {"prompt": ["stage", "pieces up to the reward", "the reward piece", "the rest + stores"],
          "bpe": ["stage", "classes + added + match lengths + chain", "symbols + pair lookups", "merges"]}[WHICH]
-ph = [a[:, 2 * (i + 1)] - a[:, 2 * i] for i in range(4)]
-print(f"{WHICH}: {int(ok.sum())} of {B} waves: mean cycles " + "  ".join(f"{nm} {p.mean():.0f}" for nm, p in zip(names, ph))
-      + f"  | span {(a[:, 8] - a[:, 0]).mean():.0f} cycles, {(a[:, 9] - a[:, 1]).mean() / 100:.2f} us realtime; "
-      f"first-to-last wave start {(a[:, 1].max() - a[:, 1].min()) / 100:.1f} us, "
-      f"window {(a[:, 9].max() - a[:, 1].min()) / 100:.1f} us")
+if WHICH == "bpe" and "fine" in os.path.basename(SO):  # bpe.hip built with -DRMI_BPE_FINE
+    names = ["1 classes", "2 added tokens", "3 match lengths", "4 chain"]
+for c, buf in enumerate(bufs):
+    s = buf.view(B, 16).cpu().numpy().astype(np.float64)
+    ok = (s[:, 0] > 0) & np.all(np.diff(s[:, 0:10:2], axis=1) > 0, axis=1)
+    a = s[ok]
+    if not len(a):
+        continue
+    ph = [a[:, 2 * (i + 1)] - a[:, 2 * i] for i in range(4)]
+    # waves resident at once: a sweep over the (start, end) realtime events
+    ev = sorted([(t, 1) for t in a[:, 1]] + [(t, -1) for t in a[:, 9]])
+    cur = peak = 0
+    for _, d in ev:
+        cur += d
+        peak = max(peak, cur)
+    ml = f" max_len {lens[c]}" if lens else ""
+    print(f"{WHICH} call {c}:{ml} {int(ok.sum())} of {B} waves: mean cycles "
+          + "  ".join(f"{nm} {p.mean():.0f}" for nm, p in zip(names, ph))
+          + f"  | span {(a[:, 8] - a[:, 0]).mean():.0f} cycles, {(a[:, 9] - a[:, 1]).mean() / 100:.2f} us realtime; "
+          f"first-to-last wave start {(a[:, 1].max() - a[:, 1].min()) / 100:.1f} us, "
+          f"window {(a[:, 9].max() - a[:, 1].min()) / 100:.1f} us, peak resident waves {peak}")
