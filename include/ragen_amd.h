@@ -596,6 +596,39 @@ int rmi_pad_rows(const int64_t* arena, int64_t arena_stride, const int32_t* aren
                  int64_t n_rows, const int64_t* tail, int32_t n_tail, int64_t S, int64_t pad_id, int64_t* input_ids,
                  int64_t* attention_mask, int64_t* position_ids, uint8_t* err, rmi_stream_t stream);
 
+/* ------------------------------------------------------------ turn-loop glue */
+/* The small per-turn steps of the device turn loop around the kernels above, one launch each
+ * (each replaced several torch elementwise / reduction launches of the Python host side):
+ *
+ * rmi_turn_inputs (EnvStateManager.step's device turn, es_manager.py:105-171, before the step
+ * kernels): has[e] = (has_t ? has_t[e] : 1) && dec_err[e] == 0 — the envs stepped this turn
+ * (a generation, decoded without error) — and err[e] = 0 (the step kernels OR into it).
+ *
+ * rmi_turn_readback (after the turn and the render): flags_copy = flags (the turn record),
+ * left[e] = max_actions[e] - num_actions[e] (the next prompt's "You have N actions left"), and
+ * pack = flags [B] | err [B] | dec_err [B] | zero pad to 4 | int32 max text_len | int32 max
+ * obs_len (NULL lengths: 0) — the one buffer the host reads back per turn (the active set, the
+ * errors es_manager raises, the sizes that bound the next prompt's text).  pack holds
+ * ((3B + 3) & ~3) + 8 bytes, 4-byte aligned.
+ *
+ * rmi_prompt_commit (after rmi_bpe_encode of a turn's prompt text): bad[e] = the row takes
+ * part (active NULL or active[e]) and bpe_err[e] or text_err[e] is set (the host rebuilds it);
+ * with mark_tok, len_upd[e] = mark_tok[e] for the rows that take part (the update batch's row
+ * end, ctx_manager.py:240-241).
+ *
+ * rmi_rows_stats (the generation batch, ctx_manager.py:265-278): stats[0] = max len[rows[i]]
+ * over the n_rows rows (rows NULL: rows 0 .. n_rows-1; 0 when none; rows outside [0, B) are
+ * skipped), stats[1] = 1 if any bad[e] (bad NULL: 0); len and bad hold B entries.           */
+int rmi_turn_inputs(const uint8_t* has_t, const uint8_t* dec_err, int64_t B, uint8_t* has, uint8_t* err,
+                    rmi_stream_t stream);
+int rmi_turn_readback(const uint8_t* flags, const uint8_t* err, const uint8_t* dec_err, const uint8_t* num_actions,
+                      const int32_t* max_actions, const int32_t* text_len, const int32_t* obs_len, int64_t B,
+                      uint8_t* flags_copy, int32_t* left, uint8_t* pack, rmi_stream_t stream);
+int rmi_prompt_commit(const uint8_t* bpe_err, const uint8_t* text_err, const uint8_t* active, const int32_t* mark_tok,
+                      int32_t* len_upd, int64_t B, uint8_t* bad, rmi_stream_t stream);
+int rmi_rows_stats(const int32_t* len, const int64_t* rows, int64_t n_rows, const uint8_t* bad, int64_t B,
+                   int32_t* stats, rmi_stream_t stream);
+
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and
  * FrozenLakeEnv.reset's env RNG (frozen_lake/env.py:28-37), both via gymnasium

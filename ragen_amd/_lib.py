@@ -167,6 +167,11 @@ _SIGS = {
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_bpe_encode": (c_int32, [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_int64, c_void_p, c_int64,
                                  c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_turn_inputs": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rmi_turn_readback": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                    c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_prompt_commit": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rmi_rows_stats": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -37,6 +37,15 @@ enum : uint32_t {
   B_IN = 128                            // any byte of a selected added token
 };
 constexpr uint32_t kNoRank = 0xFFFFFFFFu;
+// Stamp points (diagnostic builds): stage | phases 1-4 | symbols + pair lookups | merges, or with
+// RMI_BPE_FINE phase 1 | 2 | 3 | 4 (tools/prof_prompt_stamps.py prints four spans either way).
+#ifdef RMI_BPE_FINE
+#define BST_N(i) do {} while (0)
+#define BST_F(i) RMI_STAMP(i)
+#else
+#define BST_N(i) RMI_STAMP(i)
+#define BST_F(i) do {} while (0)
+#endif
 constexpr uint16_t kEnd = 0xFFFF;
 constexpr int kMaxStride = 3072;
 
@@ -44,24 +53,33 @@ constexpr int kMaxStride = 3072;
 // table is small (Qwen2: 22 added tokens, ~300 bytes): phases 1 and 2 then read no global
 // memory per byte.  (They used to: a class lookup was two dependent global loads per byte, and
 // each added-token comparison a chain of global byte loads — ≈64 k cycles of a wave's 161 k.)
-constexpr int kStageAdded = 64, kStageAddedBytes = 768;
+constexpr int kStageAdded = 64;
 constexpr int kPairBatch = 8;     // 64-pair chunks whose first hash probes go out together
-struct Lds {  // carved from dynamic LDS, n = stride
-  uint8_t* T;    // text, n + 16 (zero tail)
-  uint8_t* C;    // category bits, n + 128
-  uint16_t* M;   // match length at a position; then the symbol chain (next symbol start)
+// 16 bytes per text byte (T, C 1; M, P, K 2; Y, R 4) and the staged tables (≈1.5 KB for the
+// Qwen2 tokenizer with the prompt expansions): the wave's LDS, which sets how many rows are
+// in flight per CU.  (R held the merged id too, as a u64: 20 bytes per text byte and ≈4.5 KB of
+// tables, with the byte ids, the added tokens' bytes and 64 token slots always staged.)
+struct Lds {  // carved from dynamic LDS, n = stride, na = the staged added tokens (0 or n_added)
+  uint64_t* AW;  // each staged added token's first 32 bytes, zero padded [na][4]
+  uint32_t* R;   // rank of the pair starting at a symbol start (kNoRank: none)
   int32_t* Y;    // symbol id at a symbol start
-  uint64_t* R;   // (rank << 32 | merged id) of the pair starting at a symbol start
+  int32_t* AO;   // added_off [na + 1] (staged tables only)
+  int32_t* AI;   // added_id [na]
+  uint32_t* AF;  // added tokens' first-byte bitmap [8]
+  uint16_t* M;   // match length at a position; then the symbol chain (next symbol start)
   uint16_t* P;   // pre-token starts
   uint16_t* K;   // tokens per pre-token, then the row offsets
-  int32_t* BID;  // byte ids [256]
-  uint32_t* AF;  // added tokens' first-byte bitmap [8]
+  uint8_t* T;    // text, n + 16 (zero tail)
+  uint8_t* C;    // category bits, n + 128
   uint8_t* AC;   // classes of the code points 0..127 [128]
-  int32_t* AO;   // added_off [kStageAdded + 1] (staged tables only)
-  int32_t* AI;   // added_id [kStageAdded]
-  uint8_t* AB;   // added_bytes [kStageAddedBytes]
-  uint64_t* AW;  // each staged added token's first 32 bytes, zero padded [kStageAdded][4]
 };
+__host__ __device__ constexpr int staged_added(int n_added) {
+  return n_added > 0 && n_added <= kStageAdded ? n_added : 0;
+}
+__host__ __device__ constexpr size_t bpe_lds(int stride, int na) {
+  return 32 * (size_t)na + 8 * (size_t)stride + 4 * (size_t)(na + 1) + 4 + 4 * (size_t)na + 32 +
+         6 * (size_t)stride + 128 + (size_t)stride + 16 + (size_t)stride + 128 + 128;
+}
 
 __device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a, uint32_t b) {
   const uint64_t key = ((uint64_t)a << 32) | b;
@@ -143,7 +161,18 @@ __device__ void wc_insert(const rmi_bpe_t& t, const uint32_t k[4], int len, cons
   uint32_t h = wc_slot(k, len, t.word_cache_mask);
   for (int i = 0; i < kWcProbe; ++i, h = (h + 1) & t.word_cache_mask) {
     uint32_t* s = t.word_cache + 16 * (size_t)h;
-    if (atomicCAS(s + 4, 0u, kWcClaimed) != 0u) continue;
+    // a plain read first: on a cold cache thousands of waves insert the same few words, and a
+    // compare-and-swap per wave per probed slot serialises them on a handful of lines (the
+    // reset's encode spent 530 k cycles per wave here).  A slot being written, or a lost race,
+    // is most likely this same word: give up (a missed insert only costs a later merge).
+    const uint32_t m0 = *reinterpret_cast<volatile const uint32_t*>(s + 4);
+    if (m0 != 0u) {
+      if (!(m0 & kWcReady)) return;
+      const uint4 w0 = *reinterpret_cast<const uint4*>(s);
+      if ((int)(m0 & 0xFF) == len && w0.x == k[0] && w0.y == k[1] && w0.z == k[2] && w0.w == k[3]) return;
+      continue;
+    }
+    if (atomicCAS(s + 4, 0u, kWcClaimed) != 0u) return;
     const uint32_t m = kWcReady | ((uint32_t)cnt << 8) | (uint32_t)len;
     uint64_t c = wc_check(k, m);
     *reinterpret_cast<uint4*>(s) = make_uint4(k[0], k[1], k[2], k[3]);
@@ -244,15 +273,20 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int S = stride;
+  const int na = staged_added(tok.n_added);
   Lds L;
-  {
+  {  // (the order of bpe_lds: the 8-byte words first, then 4-, 2- and 1-byte arrays)
     uint8_t* p = smem;
-    L.R = reinterpret_cast<uint64_t*>(p);
-    p += 8 * (size_t)S;
+    L.AW = reinterpret_cast<uint64_t*>(p);
+    p += 32 * (size_t)na;
+    L.R = reinterpret_cast<uint32_t*>(p);
+    p += 4 * (size_t)S;
     L.Y = reinterpret_cast<int32_t*>(p);
     p += 4 * (size_t)S;
-    L.BID = reinterpret_cast<int32_t*>(p);
-    p += 4 * 256;
+    L.AO = reinterpret_cast<int32_t*>(p);
+    p += 4 * (size_t)(na + 1) + 4;
+    L.AI = reinterpret_cast<int32_t*>(p);
+    p += 4 * (size_t)na;
     L.AF = reinterpret_cast<uint32_t*>(p);
     p += 32;
     L.M = reinterpret_cast<uint16_t*>(p);
@@ -266,14 +300,6 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     L.C = p;
     p += S + 128;
     L.AC = p;
-    p += 128;
-    L.AO = reinterpret_cast<int32_t*>(p);
-    p += 4 * (kStageAdded + 1) + 4;
-    L.AI = reinterpret_cast<int32_t*>(p);
-    p += 4 * kStageAdded;
-    L.AB = p;
-    p += kStageAddedBytes;
-    L.AW = reinterpret_cast<uint64_t*>(p);
   }
   RMI_STAMP_DECL;
   RMI_STAMP(0);
@@ -294,9 +320,8 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     if (4 * w + 4 > n && 4 * w < n) v &= 0xFFFFFFFFu >> (8 * (4 * w + 4 - n));
     reinterpret_cast<uint32_t*>(L.T)[w] = v;
   }
-  for (int i = lane; i < 256; i += 64) L.BID[i] = tok.byte_id[i];
   if (lane < 8) L.AF[lane] = tok.added_first[lane];
-  const bool stage_added = tok.n_added > 0 && tok.n_added <= kStageAdded;
+  const bool stage_added = na > 0;
   if (stage_added) {
     for (int i = lane; i <= tok.n_added; i += 64) L.AO[i] = tok.added_off[i];
     for (int i = lane; i < tok.n_added; i += 64) L.AI[i] = tok.added_id[i];
@@ -304,30 +329,28 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   const uint32_t blk0 = tok.cp_block[0];  // the block of U+0000..U+00FF
   for (int i = lane; i < n + 128; i += 64) L.C[i] = 0;
   wave_sync();
-  // second batch: the ASCII classes (from block 0) and the added tokens' bytes
-  const int added_len = stage_added ? L.AO[tok.n_added] : 0;
-  const bool added_lds = stage_added && added_len <= kStageAddedBytes;
+  // second batch: the ASCII classes (from block 0)
   L.AC[lane] = tok.cp_class[blk0 * 256u + (uint32_t)lane];
   L.AC[lane + 64] = tok.cp_class[blk0 * 256u + 64u + (uint32_t)lane];
-  if (added_lds)
-    for (int i = lane; i < added_len; i += 64) L.AB[i] = tok.added_bytes[i];
-  wave_sync();
-  // the staged tokens as 32-byte words (lane a: token a), compared 8 bytes at a time below
+  // the staged tokens as 32-byte words (lane a: token a), compared 8 bytes at a time below; a
+  // token longer than 32 bytes sends the row to the global-table compare
   bool added_words = false;
-  if (added_lds) {
+  if (stage_added) {
     bool longer = false;
-    for (int a = lane; a < tok.n_added; a += 64) longer |= L.AO[a + 1] - L.AO[a] > 32;
+    for (int a = lane; a < na; a += 64) longer |= L.AO[a + 1] - L.AO[a] > 32;
     added_words = !__any(longer);
-    for (int a = lane; added_words && a < tok.n_added; a += 64) {
+    for (int a = lane; added_words && a < na; a += 64) {
       const int o0 = L.AO[a], len = L.AO[a + 1] - o0;
       uint64_t w[4] = {0, 0, 0, 0};
-      for (int k = 0; k < len; ++k) w[k >> 3] |= (uint64_t)L.AB[o0 + k] << (8 * (k & 7));
+      for (int k = 0; k < len; ++k) w[k >> 3] |= (uint64_t)tok.added_bytes[o0 + k] << (8 * (k & 7));
 #pragma unroll
       for (int q = 0; q < 4; ++q) L.AW[4 * a + q] = w[q];
     }
-    wave_sync();
   }
+  wave_sync();
+#ifndef RMI_BPE_FINE
   RMI_STAMP_WAIT(1);
+#endif
   // ---- 1. UTF-8 decode and classes
   bool bad = false, unsafe = false;
   for (int p = lane; p < n; p += 64) {
@@ -375,6 +398,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   if (row_bad) return fail(RMI_ERR_STATE);
   if (row_unsafe) return fail(RMI_ERR_UNSUP);
   wave_sync();
+  BST_F(1);
   // ---- 2. added tokens: the candidate positions (character starts whose first byte starts
   //         some added token) listed first, then one candidate per lane: its longest match;
   //         then the leftmost-longest selection.  (Matching inside the 64-byte chunk loop ran
@@ -422,17 +446,6 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
             best_id = L.AI[a];
           }
         }
-      } else if (added_lds) {  // the staged tables
-        for (int a = 0; a < tok.n_added; ++a) {
-          const int o0 = L.AO[a], len = L.AO[a + 1] - o0;
-          if (len <= best_len || p + len > n) continue;
-          int k = 0;
-          while (k < len && L.AB[o0 + k] == L.T[p + k]) ++k;
-          if (k == len) {
-            best_len = len;
-            best_id = L.AI[a];
-          }
-        }
       } else {
         for (int a = 0; a < tok.n_added; ++a) {
           const int o0 = tok.added_off[a], len = tok.added_off[a + 1] - o0;
@@ -462,6 +475,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     }
     wave_sync();
   }
+  BST_F(2);
   // ---- 3. match length at every character start (outside added tokens)
   for (int w0 = 0; w0 < n; w0 += 64) {
     const int p = w0 + lane;
@@ -535,6 +549,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     L.M[p] = (uint16_t)(len > 0 ? len : l0);
   }
   wave_sync();
+  BST_F(3);
   // ---- 4. the leftmost match chain: pre-token starts (added tokens are pre-tokens too)
   int np = 0;
   for (int p = 0; p < n;) {
@@ -550,7 +565,8 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     np += __builtin_popcountll(starts);
   }
   wave_sync();
-  RMI_STAMP(2);
+  BST_N(2);
+  BST_F(4);
   // ---- 5. BPE: symbols, pair ranks, merges (one lane per pre-token)
   // piece bounds: P[j] .. P[j+1] (or n); the symbol chain in M: next symbol start or kEnd
   // A word found in the word cache gets its ids as the symbols a .. a+cnt-1 and its bytes
@@ -577,7 +593,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
       }
     }
     for (int q = a; q < e; ++q) {
-      L.Y[q] = L.BID[L.T[q]];
+      L.Y[q] = tok.byte_id[L.T[q]];  // 1 KB, cache resident (a word-cache miss only)
       L.M[q] = q + 1 < e ? (uint16_t)(q + 1) : kEnd;
     }
   }
@@ -610,11 +626,11 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
         if (k0[g] == key[g]) r = v0[g];
         else if (k0[g] != ~0ull) r = merge_lookup(tok, (uint32_t)(key[g] >> 32), (uint32_t)key[g]);
       }
-      L.R[q] = r;
+      L.R[q] = (uint32_t)(r >> 32);
     }
   }
   wave_sync();
-  RMI_STAMP(3);
+  BST_N(3);
   // The merges, one lane per pre-token.  (Interleaving several words per lane, with their pair
   // probes in flight together and a bit mask of live symbols instead of the chain walk, measured
   // slower: 78-95 k cycles per wave against 75 k.)
@@ -633,7 +649,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
         uint32_t best = kNoRank;
         int bq = -1, bprev = -1, prev = -1;
         for (int q = a; q != kEnd; prev = q, q = L.M[q]) {
-          const uint32_t r = (uint32_t)(L.R[q] >> 32);
+          const uint32_t r = L.R[q];
           if (r < best) {
             best = r;
             bq = q;
@@ -642,11 +658,13 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
         }
         if (bq < 0) break;
         const int rq = L.M[bq];
-        L.Y[bq] = (int32_t)(uint32_t)L.R[bq];
+        // the merged id: the pair's entry again (R keeps the rank only; a merge is a word-cache
+        // miss, the table line is in cache from the rank lookup)
+        L.Y[bq] = (int32_t)(uint32_t)merge_lookup(tok, (uint32_t)L.Y[bq], (uint32_t)L.Y[rq]);
         const uint16_t nn = L.M[rq];
         L.M[bq] = nn;
-        L.R[bq] = nn != kEnd ? merge_lookup(tok, (uint32_t)L.Y[bq], (uint32_t)L.Y[nn]) : ~0ull;
-        if (bprev >= 0) L.R[bprev] = merge_lookup(tok, (uint32_t)L.Y[bprev], (uint32_t)L.Y[bq]);
+        L.R[bq] = nn != kEnd ? (uint32_t)(merge_lookup(tok, (uint32_t)L.Y[bq], (uint32_t)L.Y[nn]) >> 32) : kNoRank;
+        if (bprev >= 0) L.R[bprev] = (uint32_t)(merge_lookup(tok, (uint32_t)L.Y[bprev], (uint32_t)L.Y[bq]) >> 32);
       }
       cnt = 0;
       for (int q = a; q != kEnd; q = L.M[q]) ++cnt;
@@ -660,7 +678,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     L.K[j] = (uint16_t)cnt;
   }
   wave_sync();
-  RMI_STAMP(4);
+  BST_N(4);
   // ---- 6. row offsets (wave scan over pre-tokens), mark, capacity, the ids
   const int mk = mark_byte ? mark_byte[b] : -1;
   int total = 0, before_mark = 0;
@@ -717,10 +735,7 @@ RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pi
       (tok->n_added > 0 && (!tok->added_bytes || !tok->added_off || !tok->added_id)) || tok->n_exp < 0 ||
       tok->n_exp > 64 || (tok->n_exp > 0 && (!tok->exp_off || !tok->exp_ids)))
     return RMI_EINVAL;
-  // R 8 + Y 4 + M, P, K 2 each + T 1 + C 1 bytes per text byte, the byte ids, bitmap and pads,
-  // the ASCII classes and the staged added-token tables
-  const size_t lds = 20 * (size_t)stride + 4 * 256 + 32 + 128 + 16 + 128 + 128 + 4 * (kStageAdded + 1) + 4 +
-                     4 * kStageAdded + kStageAddedBytes + 32 * kStageAdded + 64;
+  const size_t lds = bpe_lds(stride, staged_added(tok->n_added));
   hipLaunchKernelGGL(bpe_encode_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text, pitch,
                      (int)stride,
                      text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);

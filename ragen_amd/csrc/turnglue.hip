@@ -1,0 +1,159 @@
+// turnglue.hip — the per-turn glue of the device turn loop, one launch each (gfx950).
+//
+//  rmi_turn_inputs    EnvStateManager._step_device before the turn: which envs step (the rows
+//                     with a generation that decoded) and their zeroed error bytes
+//  rmi_turn_readback  _step_device after the turn + render: the turn record's flags copy and
+//                     actions-left column, and ONE packed buffer the host reads back (flags,
+//                     step errors, decode errors, the longest decoded response and observation)
+//  rmi_prompt_commit  DevicePrompts._encode after the BPE launch: the rows the device could not
+//                     build, and the update-batch marks of the rows that took part
+//  rmi_rows_stats     DevicePrompts.gen_batch: the longest arena row among the batch rows and
+//                     whether any row waits for the host, as two ints read back together
+//
+// Each replaced 3-8 torch elementwise / reduction launches; in a kernel trace of the API rollout
+// (profiles/r04_api_timeline.txt) the turn loop's GPU sat idle between small launches for most
+// of each turn.  The reductions (readback, rows_stats) are single 1024-thread workgroups: no
+// atomics, no zero fill, a few microseconds at 8192 rows.
+#include "common.hpp"
+
+namespace rmi {
+namespace {
+
+constexpr int kGlueBlock = 256;
+constexpr int kRedBlock = 1024;
+
+__global__ __launch_bounds__(kGlueBlock) void turn_inputs_kernel(const uint8_t* __restrict__ has_t,
+                                                                 const uint8_t* __restrict__ dec_err, int64_t B,
+                                                                 uint8_t* __restrict__ has, uint8_t* __restrict__ err) {
+  for (int64_t e = (int64_t)blockIdx.x * kGlueBlock + threadIdx.x; e < B; e += (int64_t)gridDim.x * kGlueBlock) {
+    const bool in = has_t ? has_t[e] != 0 : true;
+    has[e] = (in && dec_err[e] == 0) ? 1 : 0;
+    err[e] = 0;
+  }
+}
+
+// block-wide max of one int per thread (kRedBlock threads) -> every thread
+__device__ __forceinline__ int block_max(int v, int* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int m = red[0];
+#pragma unroll
+  for (int w = 1; w < kRedBlock / 64; ++w) m = max(m, red[w]);
+  __syncthreads();
+  return m;
+}
+
+__global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
+    const uint8_t* __restrict__ flags, const uint8_t* __restrict__ err, const uint8_t* __restrict__ dec_err,
+    const uint8_t* __restrict__ num_actions, const int32_t* __restrict__ max_actions,
+    const int32_t* __restrict__ text_len, const int32_t* __restrict__ obs_len, int64_t B,
+    uint8_t* __restrict__ flags_copy, int32_t* __restrict__ left, uint8_t* __restrict__ pack) {
+  __shared__ int red[kRedBlock / 64];
+  int tmax = 0, omax = 0;
+  for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
+    const uint8_t f = flags[e];
+    flags_copy[e] = f;
+    left[e] = max_actions[e] - (int32_t)num_actions[e];
+    pack[e] = f;
+    pack[B + e] = err[e];
+    pack[2 * B + e] = dec_err[e];
+    if (text_len) tmax = max(tmax, text_len[e]);
+    if (obs_len) omax = max(omax, obs_len[e]);
+  }
+  tmax = block_max(tmax, red);
+  omax = block_max(omax, red);
+  if (threadIdx.x == 0) {
+    int32_t* tail = reinterpret_cast<int32_t*>(pack + ((3 * B + 3) & ~(int64_t)3));
+    tail[0] = tmax;
+    tail[1] = omax;
+  }
+}
+
+__global__ __launch_bounds__(kGlueBlock) void prompt_commit_kernel(const uint8_t* __restrict__ bpe_err,
+                                                                   const uint8_t* __restrict__ text_err,
+                                                                   const uint8_t* __restrict__ active,
+                                                                   const int32_t* __restrict__ mark_tok,
+                                                                   int32_t* __restrict__ len_upd, int64_t B,
+                                                                   uint8_t* __restrict__ bad) {
+  for (int64_t e = (int64_t)blockIdx.x * kGlueBlock + threadIdx.x; e < B; e += (int64_t)gridDim.x * kGlueBlock) {
+    const bool on = active ? active[e] != 0 : true;
+    bad[e] = (on && (bpe_err[e] != 0 || text_err[e] != 0)) ? 1 : 0;
+    if (mark_tok && on) len_upd[e] = mark_tok[e];
+  }
+}
+
+__global__ __launch_bounds__(kRedBlock) void rows_stats_kernel(const int32_t* __restrict__ len,
+                                                               const int64_t* __restrict__ rows, int64_t n_rows,
+                                                               const uint8_t* __restrict__ bad, int64_t B,
+                                                               int32_t* __restrict__ stats) {
+  __shared__ int red[kRedBlock / 64];
+  int m = 0, any = 0;
+  for (int64_t i = threadIdx.x; i < n_rows; i += kRedBlock) {
+    const int64_t r = rows ? rows[i] : i;
+    if (r >= 0 && r < B) m = max(m, len[r]);  // (the host validated the rows: a guard, not a rule)
+  }
+  if (bad)
+    for (int64_t e = threadIdx.x; e < B; e += kRedBlock) any |= bad[e];
+  m = block_max(m, red);
+  any = block_max(any != 0 ? 1 : 0, red);
+  if (threadIdx.x == 0) {
+    stats[0] = m;
+    stats[1] = any;
+  }
+}
+
+inline unsigned glue_grid(int64_t B) {
+  const int64_t g = (B + kGlueBlock - 1) / kGlueBlock;
+  return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_turn_inputs(const uint8_t* has_t, const uint8_t* dec_err, int64_t B, uint8_t* has, uint8_t* err,
+                            rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0) return RMI_EINVAL;
+  if (B == 0) return RMI_OK;
+  if (!dec_err || !has || !err) return RMI_EINVAL;
+  hipLaunchKernelGGL(turn_inputs_kernel, dim3(glue_grid(B)), dim3(kGlueBlock), 0, as_stream(stream), has_t, dec_err,
+                     B, has, err);
+  return launch_status();
+}
+
+RMI_API int rmi_turn_readback(const uint8_t* flags, const uint8_t* err, const uint8_t* dec_err,
+                              const uint8_t* num_actions, const int32_t* max_actions, const int32_t* text_len,
+                              const int32_t* obs_len, int64_t B, uint8_t* flags_copy, int32_t* left, uint8_t* pack,
+                              rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0) return RMI_EINVAL;
+  if (!pack || (B > 0 && (!flags || !err || !dec_err || !num_actions || !max_actions || !flags_copy || !left)))
+    return RMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(pack) & 3u) return RMI_EINVAL;
+  hipLaunchKernelGGL(turn_readback_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err, dec_err,
+                     num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack);
+  return launch_status();
+}
+
+RMI_API int rmi_prompt_commit(const uint8_t* bpe_err, const uint8_t* text_err, const uint8_t* active,
+                              const int32_t* mark_tok, int32_t* len_upd, int64_t B, uint8_t* bad, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || (mark_tok && !len_upd)) return RMI_EINVAL;
+  if (B == 0) return RMI_OK;
+  if (!bpe_err || !text_err || !bad) return RMI_EINVAL;
+  hipLaunchKernelGGL(prompt_commit_kernel, dim3(glue_grid(B)), dim3(kGlueBlock), 0, as_stream(stream), bpe_err,
+                     text_err, active, mark_tok, len_upd, B, bad);
+  return launch_status();
+}
+
+RMI_API int rmi_rows_stats(const int32_t* len, const int64_t* rows, int64_t n_rows, const uint8_t* bad, int64_t B,
+                           int32_t* stats, rmi_stream_t stream) {
+  using namespace rmi;
+  if (n_rows < 0 || B < 0 || !stats || (n_rows > 0 && !len)) return RMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(stats) & 3u) return RMI_EINVAL;
+  hipLaunchKernelGGL(rows_stats_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, rows, n_rows, bad, B,
+                     stats);
+  return launch_status();
+}

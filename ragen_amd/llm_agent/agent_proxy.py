@@ -62,7 +62,12 @@ class TokenActor:
             self.prompt_shapes.append(tuple(b["input_ids"].shape))
             self.prompts.append((b["input_ids"], b["attention_mask"], b["position_ids"]))
         tok = self.turn_tokens[self.turn]
-        resp = tok[torch.from_numpy(env_ids - self.env_lo).to(tok.device)]
+        local = env_ids - self.env_lo
+        if len(local) == tok.shape[0] and np.array_equal(local, np.arange(len(local))):
+            resp = tok  # every env, in order
+        else:
+            from .. import ops
+            resp = tok[ops.h2d(local, tok.device)]
         self.turn += 1
         return DataProto({"responses": resp}, {"env_ids": env_ids}, {})
 

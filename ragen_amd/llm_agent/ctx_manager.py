@@ -697,19 +697,18 @@ class ContextManager:
             local = env_ids - lo
             if local.size and (local.min() < 0 or local.max() >= n):
                 raise ValueError(f"env ids outside this manager's envs [{lo}, {lo + n})")
-            if np.unique(local).size != local.size:
-                raise ValueError("duplicate env ids in the generation batch")
             src = np.full(n, -1, np.int64)  # src[e]: env e's row (-1: none)
             src[local] = np.arange(len(env_ids))
+            if np.count_nonzero(src >= 0) != local.size:  # (a sort-free duplicate check)
+                raise ValueError("duplicate env ids in the generation batch")
             ids = torch.empty(n, R, dtype=torch.int64, device=dev)
             n_ids = torch.empty(n, dtype=torch.int32, device=dev)
             has_t = torch.empty(n, dtype=torch.uint8, device=dev)  # 1: the env has a generation
-            torch.ops.ragen_amd.gen_rows(resp, torch.from_numpy(src).to(dev), n, vocab.packed, ids, n_ids, raw,
-                                         has_t)
+            torch.ops.ragen_amd.gen_rows(resp, ops.h2d(src, dev), n, vocab.packed, ids, n_ids, raw, has_t)
         # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
         # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
         # the decode and refused by the step (ValueError)
-        raw_max = int(raw) if resp.numel() else 0
+        raw_max = int(ops.d2h(raw, self)[0]) if resp.numel() else 0
         stride = max(4, min(PARSE_MAX_ROW, (3 * raw_max + 7) // 4 * 4))
         return DeviceEnvInputs(self, env_ids, has_t, ids, n_ids, stride)
 

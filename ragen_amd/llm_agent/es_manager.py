@@ -28,7 +28,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
-from .. import _lib
+from .. import _lib, ops
 from .. import distributed as rd
 from ..env import REGISTERED_ENV_CONFIGS, REGISTERED_ENVS
 from ..env.base import BatchEnv
@@ -211,6 +211,7 @@ class EnvStateManager:
         self._all_active = False
         self.reset_render = None
         self._turn_records = []  # device-path turns (ContextManager's device prompts read them too)
+        self._max_act = None  # i32[n_envs] max_actions_per_traj per env (device turn), built once
         self._mat_upto = 0       # records whose host bookkeeping is done
 
     def _init_envs(self):
@@ -590,28 +591,40 @@ class EnvStateManager:
         # a generation the device decode truncated (row stride cap) or could not decode (an id
         # outside the vocabulary) is not stepped on: masked out of the turn on the device and
         # raised after it, from the turn's one readback (no host synchronisation before the turn)
-        dec_ok = inp.err == 0
-        # the envs with a generation (minus undecodable ones): all of them, or the rows given
-        if inp.has_t is None:
-            has = dec_ok.to(torch.uint8)
-        else:
-            has = inp.has_t * dec_ok  # has_t written by rmi_gen_rows
-        err = torch.zeros(self.n_envs, dtype=torch.uint8, device=dev)
+        # the envs with a generation (all of them, or has_t written by rmi_gen_rows) minus the
+        # undecodable ones, and the zeroed step-error bytes: one launch (rmi_turn_inputs)
+        has = torch.empty(self.n_envs, dtype=torch.uint8, device=dev)
+        err = torch.empty(self.n_envs, dtype=torch.uint8, device=dev)
+        ops.turn_inputs(inp.has_t, inp.err, has, err)
         if parsed is None:
             parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
         else:
             self._parsed_turn(parsed, has, err)
         obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
+        n = self.n_envs
         flags = self._cat([tg.batch.ep.flags for tg in self.tags])
-        left = self._cat([tg.max_actions_per_traj - tg.batch.ep.num_actions.to(torch.int32) for tg in self.tags])
+        num_actions = self._cat([tg.batch.ep.num_actions for tg in self.tags])
+        obs_len = self._cat([obs[j][1] for j in sorted(obs)]) if len(obs) == len(self.tags) else None
+        if self._max_act is None:  # per-env max_actions_per_traj (the "actions left" base)
+            self._max_act = torch.tensor(np.concatenate([np.full(tg.hi - tg.lo, tg.max_actions_per_traj, np.int32)
+                                                         for tg in self.tags]), device=dev)
+        flags_copy = torch.empty(n, dtype=torch.uint8, device=dev)
+        left = torch.empty(n, dtype=torch.int32, device=dev)
+        pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
+        # the record's flags and actions-left columns, and the one packed readback: flags, step
+        # and decode errors, the longest decoded response and observation (rmi_turn_readback)
+        ops.turn_readback(flags, err, inp.err, num_actions, self._max_act, inp.text_len, obs_len, flags_copy, left,
+                          pack)
+        # one device -> host copy (pinned, then the stream waited on): the active set and the
+        # turn's per-env error bits, raised in the step where they happen, as the reference
+        # raises inside its per-env loop
+        host = ops.d2h(pack, self)
+        tmax, omax = (int(x) for x in host[-8:].view(np.int32))
         self._turn_records.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs,
-                                   "spans": [p["spans"] for p in parsed], "flags": flags.clone(),
-                                   "left": left.to(torch.int32).contiguous()})
-        # one device -> host copy: the active set and the turn's per-env error bits, raised in
-        # the step where they happen, as the reference raises inside its per-env loop
+                                   "spans": [p["spans"] for p in parsed], "flags": flags_copy, "left": left,
+                                   "text_max": tmax, "obs_max": omax if obs_len is not None else None})
         n_in = len(inp.env_ids)
-        host = torch.cat([flags, err, inp.err]).cpu().numpy()
-        fl_h, err_h, dec_h = host[:self.n_envs], host[self.n_envs:2 * self.n_envs], host[2 * self.n_envs:]
+        fl_h, err_h, dec_h = host[:n], host[n:2 * n], host[2 * n:3 * n]
         if dec_h.any():
             bad = int(np.nonzero(dec_h)[0][0])
             raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "

@@ -47,7 +47,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
-from .. import _lib
+from .. import _lib, ops
 from ..tokenizer import DeviceTokenizer
 
 SYSTEM = "You're a helpful assistant. "
@@ -249,6 +249,8 @@ class DevicePrompts:
         self.arena = torch.zeros(n, self.cap, dtype=torch.int64, device=self.device)
         self.len = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.len_upd = torch.zeros(n, dtype=torch.int32, device=self.device)
+        self._all_idx = np.arange(n, dtype=np.int64)
+        self._all_rows = torch.arange(n, dtype=torch.int64, device=self.device)
         tail = self.dt.encode([self.tpl.gen + self.prefix])[0]
         if tail is None or tail != self._host_ids(self.tpl.gen + self.prefix):
             raise NotImplementedError("the generation prompt does not encode like the host tokenizer")
@@ -356,9 +358,38 @@ class DevicePrompts:
         self._exp_cache[key] = out
         return out
 
+    def _text_bound(self, prog, obs_max, resp_max):
+        """An upper bound on the longest row a program writes, from the host: the constants'
+        lengths (a tag table's longest entry), the longest observation and decoded response of
+        the turn (rmi_turn_readback), and each number's widest form -> the BPE launch's row size
+        with no device round trip.  None when a length it needs is unknown.  (A row past the
+        bound would be flagged by the encoder and rebuilt on the host, never mis-encoded.)"""
+        n = 0
+        for k, a, b in prog:
+            if k == _lib.PT_CONST:
+                n += b
+            elif k == _lib.PT_TAG_CONST:
+                n += max(self._tag_tables[a][1::2])
+            elif k == _lib.PT_OBS:
+                if obs_max is None:
+                    return None
+                n += obs_max
+            elif k == _lib.PT_INT:
+                n += 11    # str of an int32
+            elif k == _lib.PT_REWARD:
+                n += 32    # repr of a double: at most 24 characters; an int reward fewer
+            elif k == _lib.PT_RESPONSE:
+                if resp_max is None:
+                    return None
+                # the prefix tag, the text, and llm_response's re-join (" sep " around each of at
+                # most K - 1 separators: two spaces each) over the raw answer
+                n += len(self.prefix) + resp_max + 2 * self.K + 8
+        return n
+
     def _run_text(self, pieces, stride, obs, obs_len, ints, reward=None, reward_int=None, resp=None, resp_len=None,
                   spans=None, cond=None, active=None, turn=None):
         prog, pool, tc = self._program(pieces)
+        self._prog_last = prog  # (the caller's _text_bound)
         flat = [len(prog)] + [x for p in prog for x in p] + [self.n_tags, obs.shape[1], 0 if resp is None else
                                                              resp.shape[1], int(self.enable_think), self.K]
         if turn is None:
@@ -438,16 +469,17 @@ class DevicePrompts:
         if self.window:  # window mode: the rows are rebuilt per batch (_build_window)
             self.turns_done = t + 1
             return
-        text, tlen, mark, terr, stride, last, flags = self._turn_text(d, t + 2, d["has"])
+        text, tlen, mark, terr, stride, last, flags, bound = self._turn_text(d, t + 2, d["has"])
         self._encode(text, tlen, terr, mark, stride,
                      lambda e: self._host_turn(e, t, not last and not int(flags[e]) & _lib.FLAG_DONE),
-                     active=d["has"])
+                     active=d["has"], bound=bound)
         self.turns_done = t + 1
 
     def _turn_text(self, d, number, active):
         """The text turn d["turn"] appends: the assistant block (its end marked: the update rows
         stop there) and, for an env that goes on, the user block with the reward and the next
-        state under the header ``Turn {number}``.  -> (text, len, mark, err, stride, last, flags)."""
+        state under the header ``Turn {number}``.  -> (text, len, mark, err, stride, last, flags,
+        the host's bound on the longest row or None)."""
         t = d["turn"]
         inp = d["inp"]
         obs, obs_len = self._obs(d["obs"])
@@ -469,7 +501,8 @@ class DevicePrompts:
         last = t + 1 >= self.max_turn
         text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, None, resp,
                                                 resp_len, spans, None, active, turn=(ne, flags, last))
-        return text, tlen, mark, terr, stride, last, flags
+        bound = self._text_bound(self._prog_last, d.get("obs_max"), d.get("text_max"))
+        return text, tlen, mark, terr, stride, last, flags, bound
 
     # ----------------------------------------------------------- max_context_window
     def _entry_state(self, j):
@@ -499,7 +532,7 @@ class DevicePrompts:
         for j in range(j0, n_done):
             d = self.es._turn_records[j]
             act = sel & d["has"].to(torch.uint8) if d["has"] is not None else sel
-            text, tlen, mark, terr, stride, _, _ = self._turn_text(d, j - j0 + 2, act)
+            text, tlen, mark, terr, stride, _, _, _ = self._turn_text(d, j - j0 + 2, act)
             bad |= self._encode_window(text, tlen, terr, mark, stride, act)
         if update:
             self.len_upd.copy_(torch.where(keep, self.len_upd, self.len_upd_w))
@@ -544,18 +577,23 @@ class DevicePrompts:
     def _stride(n):
         return min(3072, (int(n) + 3) // 4 * 4)
 
-    def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None):
+    def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None, bound=None):
         """Tokenize the rows onto the arena; the rows the device could not build are left for
-        the host (``_resolve``), read back with the next readback of the arena lengths."""
+        the host (``_resolve``), read back with the next readback of the arena lengths.  The
+        launch's row size is ``bound`` (the host's, _text_bound) when given, else the longest
+        row read back."""
         self._resolve()  # an earlier turn's host rows come first in the arena
-        mx = int(tlen.max()) if tlen.numel() else 0
-        n_tok, mark_tok, err = self.dt.encode_rows(text, tlen, self.arena, self.len, mark, max_len=max(mx, 4))
-        bad = (err != 0) | (terr != 0)
-        if active is not None:
-            bad &= active.bool()
-        if mark is not None:  # the update batch ends after the assistant block
-            upd = torch.where(active.bool(), mark_tok, self.len_upd) if active is not None else mark_tok
-            self.len_upd.copy_(upd)
+        if bound is not None:
+            mx = min(int(bound), text.shape[1])
+        else:
+            mx = int(tlen.max()) if tlen.numel() else 0
+        n_tok, mark_tok, err = self.dt.encode_rows(text, tlen, self.arena, self.len, mark,
+                                                   max_len=max((mx + 3) // 4 * 4, 4))
+        # the rows left for the host and the update batch's row ends (after the assistant block):
+        # one launch (rmi_prompt_commit)
+        bad = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
+        act = None if active is None else (active if active.dtype == torch.uint8 else active.to(torch.uint8))
+        ops.prompt_commit(err, terr, act, mark_tok if mark is not None else None, self.len_upd, bad)
         self._pending = (bad, host_fn)
 
     def _resolve(self, any_bad=None):
@@ -613,7 +651,11 @@ class DevicePrompts:
     # ------------------------------------------------------------------- batches
     def gen_batch(self, env_ids: np.ndarray):
         """get_lm_inputs(prepare_for_update=False)'s tensors for these envs (device)."""
-        rows = torch.from_numpy(np.asarray(env_ids, np.int64) - self.es.env_lo).to(self.device)
+        local = np.asarray(env_ids, np.int64) - self.es.env_lo
+        if len(local) == self.n_envs and np.array_equal(local, self._all_idx):
+            rows = self._all_rows  # every env in order (no host -> device copy)
+        else:
+            rows = ops.h2d(local, self.device)
         if self.window and rows.numel():  # every active env has the same turn count
             sel = torch.zeros(self.n_envs, dtype=torch.uint8, device=self.device)
             sel[rows] = 1
@@ -621,13 +663,17 @@ class DevicePrompts:
         if not rows.numel():
             self._resolve()
             S = 1
-        elif self._pending is not None:  # one readback: the longest row and whether any row is the host's
-            mx, any_bad = torch.stack([self.len[rows].max().to(torch.int64),
-                                       self._pending[0].any().to(torch.int64)]).cpu().tolist()
-            self._resolve(bool(any_bad))
-            S = (int(self.len[rows].max()) if any_bad else mx) + self.tail.numel()
-        else:
-            S = int(self.len[rows].max()) + self.tail.numel()
+        else:  # one readback: the longest row and whether any row is the host's (rmi_rows_stats)
+            stats = torch.empty(2, dtype=torch.int32, device=self.device)
+            pend = self._pending[0] if self._pending is not None else None
+            ops.rows_stats(self.len, rows, rows.numel(), pend, stats)
+            mx, any_bad = (int(x) for x in ops.d2h(stats, self))
+            if pend is not None:
+                self._resolve(bool(any_bad))
+            if any_bad:  # host rows were written: the longest row again
+                ops.rows_stats(self.len, rows, rows.numel(), None, stats)
+                mx = int(ops.d2h(stats, self)[0])
+            S = mx + self.tail.numel()
         ids, am, pos, err = torch.ops.ragen_amd.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
         return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
 

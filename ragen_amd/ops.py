@@ -809,6 +809,95 @@ def pad_rows(arena: torch.Tensor, arena_len: torch.Tensor, rows: torch.Tensor, t
     return ids, am, pos, err
 
 
+# ------------------------------------------------------------------- turn-loop glue
+def h2d(a: np.ndarray, device) -> torch.Tensor:
+    """A host array -> the device through pinned memory, without blocking the host (torch's
+    caching host allocator keeps the staging block until the copy has run)."""
+    return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(device, non_blocking=True)
+
+
+def d2h(t: torch.Tensor, owner) -> np.ndarray:
+    """A small device tensor -> a host numpy copy, through a pinned buffer kept on ``owner``
+    (an async copy, then the stream waited on): a pageable ``.cpu()`` stages through the
+    runtime's bounce buffer at several times the cost."""
+    nbytes = t.numel() * t.element_size()
+    buf = getattr(owner, "_pin_buf", None)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1 << 16), dtype=torch.uint8, pin_memory=True)
+        owner._pin_buf = buf
+    dst = buf[:nbytes].view(t.dtype)
+    dst.copy_(t.reshape(-1), non_blocking=True)
+    torch.cuda.current_stream(t.device).synchronize()
+    return dst.numpy().copy()
+
+
+def turn_inputs(has_t: Optional[torch.Tensor], dec_err: torch.Tensor, has: torch.Tensor, err: torch.Tensor):
+    """rmi_turn_inputs: has = (has_t or 1) and not dec_err, err = 0 (u8[B] each)."""
+    dev = _dev(has_t, dec_err, has, err)
+    for t, nm in ((has_t, "has_t"), (dec_err, "dec_err"), (has, "has"), (err, "err")):
+        _dt(t, torch.uint8, nm)
+    B = dec_err.numel()
+    if has.numel() != B or err.numel() != B or (has_t is not None and has_t.numel() != B):
+        raise ValueError("has_t, dec_err, has and err must have one entry per env")
+    check(lib().rmi_turn_inputs(_ptr(has_t), _ptr(dec_err), B, _ptr(has), _ptr(err), _stream(dev)), "rmi_turn_inputs")
+
+
+def readback_bytes(B: int) -> int:
+    """The size of rmi_turn_readback's packed buffer for B envs."""
+    return ((3 * B + 3) & ~3) + 8
+
+
+def turn_readback(flags, err, dec_err, num_actions, max_actions, text_len, obs_len, flags_copy, left, pack):
+    """rmi_turn_readback: flags_copy = flags, left = max_actions - num_actions, and the packed
+    readback (flags | err | dec_err | max text_len, max obs_len) -> pack."""
+    dev = _dev(flags, err, dec_err, num_actions, max_actions, text_len, obs_len, flags_copy, left, pack)
+    for t, dt, nm in ((flags, torch.uint8, "flags"), (err, torch.uint8, "err"), (dec_err, torch.uint8, "dec_err"),
+                      (num_actions, torch.uint8, "num_actions"), (max_actions, torch.int32, "max_actions"),
+                      (text_len, torch.int32, "text_len"), (obs_len, torch.int32, "obs_len"),
+                      (flags_copy, torch.uint8, "flags_copy"), (left, torch.int32, "left"), (pack, torch.uint8, "pack")):
+        _dt(t, dt, nm)
+    B = flags.numel()
+    for t in (err, dec_err, num_actions, max_actions, text_len, obs_len, flags_copy, left):
+        if t is not None and t.numel() != B:
+            raise ValueError("every per-env input must have one entry per env")
+    if pack.numel() < readback_bytes(B):
+        raise ValueError(f"pack needs {readback_bytes(B)} bytes")
+    check(lib().rmi_turn_readback(_ptr(flags), _ptr(err), _ptr(dec_err), _ptr(num_actions), _ptr(max_actions),
+                                  _ptr(text_len), _ptr(obs_len), B, _ptr(flags_copy), _ptr(left), _ptr(pack),
+                                  _stream(dev)), "rmi_turn_readback")
+
+
+def prompt_commit(bpe_err, text_err, active, mark_tok, len_upd, bad):
+    """rmi_prompt_commit: bad = the taking-part rows with an encode or text error; with mark_tok
+    len_upd = mark_tok on those rows."""
+    dev = _dev(bpe_err, text_err, active, mark_tok, len_upd, bad)
+    for t, dt, nm in ((bpe_err, torch.uint8, "bpe_err"), (text_err, torch.uint8, "text_err"),
+                      (active, torch.uint8, "active"), (mark_tok, torch.int32, "mark_tok"),
+                      (len_upd, torch.int32, "len_upd"), (bad, torch.uint8, "bad")):
+        _dt(t, dt, nm)
+    B = bad.numel()
+    for t in (bpe_err, text_err, active, mark_tok, len_upd):
+        if t is not None and t.numel() != B:
+            raise ValueError("every input must have one entry per env")
+    check(lib().rmi_prompt_commit(_ptr(bpe_err), _ptr(text_err), _ptr(active), _ptr(mark_tok), _ptr(len_upd), B,
+                                  _ptr(bad), _stream(dev)), "rmi_prompt_commit")
+
+
+def rows_stats(length, rows, n_rows: int, bad, stats):
+    """rmi_rows_stats: stats i32[2] = (max length[rows], any bad)."""
+    dev = _dev(length, rows, bad, stats)
+    _dt(length, torch.int32, "len")
+    _dt(rows, torch.int64, "rows")
+    _dt(bad, torch.uint8, "bad")
+    _dt(stats, torch.int32, "stats")
+    B = length.numel()
+    if (bad is not None and bad.numel() != B) or stats.numel() < 2 or (rows is not None and rows.numel() != n_rows) \
+            or (rows is None and n_rows > B):
+        raise ValueError("rows_stats: bad holds one entry per env, stats two ints, rows n_rows entries")
+    check(lib().rmi_rows_stats(_ptr(length), _ptr(rows), int(n_rows), _ptr(bad), B, _ptr(stats), _stream(dev)),
+          "rmi_rows_stats")
+
+
 # ------------------------------------------------------------------------ advantages
 def _mask_u8(mask: torch.Tensor) -> torch.Tensor:
     """A boolean mask as u8 bytes.  The kernels read any nonzero byte as 1 (RAGEN passes a bool

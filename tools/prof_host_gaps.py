@@ -1,0 +1,95 @@
+"""Host time of the device turn loop's steps (diagnostic): bench.api_leg's rollout with the
+library ops, the glue helpers and the prompt builder's methods wrapped in a wall clock (no
+synchronisation: the host's own time per call, what leaves the GPU idle between launches),
+printed as mean microseconds per call and per rollout."""
+import os
+import random
+import sys
+import time
+from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from ragen_amd import ops, synthetic  # noqa: E402
+from ragen_amd.config import env_task  # noqa: E402
+from ragen_amd.llm_agent import LLMAgentProxy, TokenActor  # noqa: E402
+from ragen_amd.llm_agent import ctx_manager as cm, es_manager as em, prompts as pm  # noqa: E402
+from ragen_amd.protocol import DataProto  # noqa: E402
+
+dev = torch.device("cuda", 0)
+B, T, K = bench.B_PER_GPU, bench.T_TURNS, bench.K_ACTIONS
+cfg = env_task("SimpleSokoban", B // bench.GROUP, bench.GROUP, max_turn=T, max_actions_per_turn=K)
+ids, n = synthetic.rollout_actions(B, T, K, 1, 4)
+tok = synthetic.qwen_like_tokenizer()
+lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
+tokens = []
+for t in range(T):
+    enc = tok(synthetic.responses_for_actions(ids[t], n[t], lk, seed=100 + t), padding=False).input_ids
+    a = np.full((B, max(len(x) for x in enc)), tok.pad_token_id, np.int64)
+    for i, x in enumerate(enc):
+        a[i, :len(x)] = x
+    tokens.append(torch.from_numpy(a).to(dev))
+actor = TokenActor(tokens, read_prompts=True)
+proxy = LLMAgentProxy(cfg, actor, tok, device=dev)
+proxy.train_ctx_manager.set_device_vocab(ops.VocabTable.from_tokenizer(tok, dev))
+
+acc = defaultdict(float)
+cnt = defaultdict(int)
+on = [False]
+
+
+def wrap(obj, name, label, setter=setattr):
+    f = getattr(obj, name)
+
+    def g(*a, **kw):
+        if not on[0]:
+            return f(*a, **kw)
+        t = time.perf_counter()
+        r = f(*a, **kw)
+        acc[label] += time.perf_counter() - t
+        cnt[label] += 1
+        return r
+    setter(obj, name, g)
+
+
+for nm in ("prompt_text", "bpe_encode", "pad_rows", "detok_parse", "gen_rows", "sokoban_step_turn",
+           "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_render", "assemble_rows",
+           "group_normalize"):
+    try:
+        wrap(torch.ops.ragen_amd, nm, "op " + nm)
+    except Exception as e:  # noqa: BLE001
+        print("cannot wrap", nm, e)
+for nm in ("d2h", "h2d", "turn_inputs", "turn_readback", "prompt_commit", "rows_stats"):
+    wrap(ops, nm, "ops." + nm)
+for nm in ("_turn_text", "_obs", "_program", "_run_text", "_encode", "advance", "gen_batch", "_text_bound"):
+    wrap(pm.DevicePrompts, nm, "prompts." + nm)
+for nm in ("get_lm_inputs", "get_env_inputs", "_device_env_inputs", "formulate_rollouts", "_sync_prompts"):
+    wrap(cm.ContextManager, nm, "ctx." + nm)
+for nm in ("step", "_step_device", "_decode_parse", "_parsed_turn", "_parse_args"):
+    wrap(em.EnvStateManager, nm, "es." + nm)
+wrap(TokenActor, "generate_sequences", "actor")
+
+
+def run():
+    random.seed(0)
+    actor.turn = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    proxy.rollout(DataProto(meta_info={}), val=False)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+for _ in range(3):
+    run()
+print("plain rollout", {k: round(v * 1e3, 3) for k, v in proxy.last_timing.items()}, "ms")
+on[0] = True
+R = 3
+for _ in range(R):
+    run()
+print("wrapped rollout", {k: round(v * 1e3, 3) for k, v in proxy.last_timing.items()}, "ms")
+for k in sorted(acc, key=lambda k: -acc[k]):
+    print(f"  {k:34s} {acc[k] / cnt[k] * 1e6:9.1f} us/call  {cnt[k] / R:5.1f} calls  {acc[k] / R * 1e3:8.3f} ms/rollout")

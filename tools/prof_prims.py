@@ -64,6 +64,12 @@ def pinned1():
 ab = torch.empty(3 * N, dtype=torch.uint8, device=dev)
 t("cat(out=) + 1 pinned copy + event wait", pinned1)
 t("torch.stack([c.max(), c.max()]).cpu().tolist()", lambda: torch.stack([c.max(), c.max()]).cpu().tolist())
+import numpy as np  # noqa: E402
+idx = np.arange(7000, dtype=np.int64)
+t("from_numpy(7000 i64).to(dev) pageable", lambda: torch.from_numpy(idx).to(dev))
+t("from_numpy(7000 i64).pin_memory().to(dev, non_blocking)", lambda: torch.from_numpy(idx).pin_memory().to(dev, non_blocking=True))
+t("torch.cuda.current_stream(dev).cuda_stream", lambda: torch.cuda.current_stream(dev).cuda_stream)
+t("np.unique(7000)", lambda: np.unique(idx))
 x = torch.randn(1 << 20, device=dev)
 t("x.sum() 1M f32 (launch)", lambda: x.sum())
 # a ragen_amd op: the Sokoban render of 8192 envs
