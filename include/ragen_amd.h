@@ -495,9 +495,11 @@ typedef struct {
   uint32_t added_first[8];  /* bitmap of the added tokens' first bytes                       */
   /* Word cache (NULL: off): (word_cache_mask + 1) entries of 16 u32 in HBM, zero-initialised
    * once and kept across calls for this tokenizer's tables — a pre-token's bytes (2..16) ->
-   * its BPE ids (<= 11).  A pre-token's merges depend on its bytes alone (the tokenizers
+   * its BPE ids (<= 9).  A pre-token's merges depend on its bytes alone (the tokenizers
    * crate caches words the same way), so a hit skips its pair lookups and merges.  Entries
-   * are claimed with an atomic compare-and-swap and published with a release store.        */
+   * are claimed with an atomic compare-and-swap after a plain read finds the slot empty, and
+   * carry a 64-bit check of their contents: a reader takes only an entry whose check
+   * matches (no acquire / release across the XCDs' L2s inside a launch).                  */
   uint32_t* word_cache;
   uint32_t word_cache_mask; /* entries - 1 (a power of two minus one)                        */
   /* Expansions (n_exp 0: none): added tokens whose id in added_id is -(e + 1) stand for the
@@ -508,6 +510,13 @@ typedef struct {
   int32_t n_exp;
   const int32_t* exp_off;   /* [n_exp + 1]                                                   */
   const int32_t* exp_ids;
+  /* Staging tables (each NULL: derived in the kernel from the tables above): the added tokens
+   * as zero-padded 32-byte words [n_added][4] (given only when every added token is <= 32
+   * bytes and n_added <= 64), and the classes of the code points 0..127
+   * (= cp_class[cp_block[0] * 256 + cp], [128]).  They take the staging's dependent loads off
+   * every row's critical path.                                                               */
+  const uint64_t* added_words;
+  const uint8_t* ascii_class;
 } rmi_bpe_t;
 
 /* Row b: text[b * pitch .. + text_len[b]) (UTF-8; pitch % 4 == 0); `stride` (% 4 == 0,

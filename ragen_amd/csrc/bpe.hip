@@ -326,16 +326,24 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     for (int i = lane; i <= tok.n_added; i += 64) L.AO[i] = tok.added_off[i];
     for (int i = lane; i < tok.n_added; i += 64) L.AI[i] = tok.added_id[i];
   }
-  const uint32_t blk0 = tok.cp_block[0];  // the block of U+0000..U+00FF
-  for (int i = lane; i < n + 128; i += 64) L.C[i] = 0;
+  // the host's staging tables when given: every load below is independent of the others
+  const bool words_given = stage_added && tok.added_words != nullptr;
+  if (words_given)
+    for (int i = lane; i < 4 * na; i += 64) L.AW[i] = tok.added_words[i];
+  if (tok.ascii_class && lane < 32)
+    reinterpret_cast<uint32_t*>(L.AC)[lane] = reinterpret_cast<const uint32_t*>(tok.ascii_class)[lane];
+  const uint32_t blk0 = tok.ascii_class ? 0u : tok.cp_block[0];  // the block of U+0000..U+00FF
+  for (int w = lane; w < (n + 128 + 3) / 4; w += 64) reinterpret_cast<uint32_t*>(L.C)[w] = 0u;  // (C is 4-aligned)
   wave_sync();
-  // second batch: the ASCII classes (from block 0)
-  L.AC[lane] = tok.cp_class[blk0 * 256u + (uint32_t)lane];
-  L.AC[lane + 64] = tok.cp_class[blk0 * 256u + 64u + (uint32_t)lane];
+  // second batch (without the host's tables): the ASCII classes from block 0, the token words
+  if (!tok.ascii_class) {
+    L.AC[lane] = tok.cp_class[blk0 * 256u + (uint32_t)lane];
+    L.AC[lane + 64] = tok.cp_class[blk0 * 256u + 64u + (uint32_t)lane];
+  }
   // the staged tokens as 32-byte words (lane a: token a), compared 8 bytes at a time below; a
   // token longer than 32 bytes sends the row to the global-table compare
-  bool added_words = false;
-  if (stage_added) {
+  bool added_words = words_given;
+  if (stage_added && !words_given) {
     bool longer = false;
     for (int a = lane; a < na; a += 64) longer |= L.AO[a + 1] - L.AO[a] > 32;
     added_words = !__any(longer);
@@ -413,64 +421,74 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
       n_cand += __builtin_popcountll(m);
     }
     wave_sync();
-    for (int c0 = 0; c0 < n_cand; c0 += 64) {  // the longest match of each -> K (0: none), id -> Y
+    // the longest match of each candidate (one per lane, id -> Y), then the leftmost-longest
+    // selection over the chunk's candidates in ascending order: a scalar walk over the lanes'
+    // (position, length) by readlane, and each selected token's bytes marked by the whole wave.
+    // (A serial walk of lane 0 over the LDS lists, marking byte by byte, took ≈8 k cycles.)
+    int cur = 0;
+    for (int c0 = 0; c0 < n_cand; c0 += 64) {
       const int ci = c0 + lane;
-      if (ci >= n_cand) continue;
-      const int p = L.P[ci];
+      const bool has_c = ci < n_cand;
+      const int p = has_c ? L.P[ci] : 0;
       int best_len = 0, best_id = 0;
-      if (added_words) {  // the text's next 32 bytes against each token, 8 bytes per compare
-        const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.T + (p & ~3));
-        uint32_t d[9];
+      if (has_c) {
+        if (added_words) {  // the text's next 32 bytes against each token, 8 bytes per compare
+          const uint32_t* t4 = reinterpret_cast<const uint32_t*>(L.T + (p & ~3));
+          uint32_t d[9];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) d[q] = t4[q];
-        const int sh = p & 3;
-        uint64_t x[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t lo = sh ? __builtin_amdgcn_alignbyte(d[2 * q + 1], d[2 * q], sh) : d[2 * q];
-          const uint32_t hi = sh ? __builtin_amdgcn_alignbyte(d[2 * q + 2], d[2 * q + 1], sh) : d[2 * q + 1];
-          x[q] = ((uint64_t)hi << 32) | lo;
-        }
-        for (int a = 0; a < tok.n_added; ++a) {
-          const int len = L.AO[a + 1] - L.AO[a];
-          if (len <= best_len || p + len > n) continue;
-          uint64_t diff = 0;
+          for (int q = 0; q < 9; ++q) d[q] = t4[q];
+          const int sh = p & 3;
+          uint64_t x[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const int r = len - 8 * q;  // bytes of this word inside the token
-            const uint64_t m = r >= 8 ? ~0ull : (r <= 0 ? 0ull : (1ull << (8 * r)) - 1);
-            diff |= (x[q] ^ L.AW[4 * a + q]) & m;
+            const uint32_t lo = sh ? __builtin_amdgcn_alignbyte(d[2 * q + 1], d[2 * q], sh) : d[2 * q];
+            const uint32_t hi = sh ? __builtin_amdgcn_alignbyte(d[2 * q + 2], d[2 * q + 1], sh) : d[2 * q + 1];
+            x[q] = ((uint64_t)hi << 32) | lo;
           }
-          if (diff == 0) {
-            best_len = len;
-            best_id = L.AI[a];
+          for (int a = 0; a < tok.n_added; ++a) {
+            const int len = L.AO[a + 1] - L.AO[a];
+            if (len <= best_len || p + len > n) continue;
+            uint64_t diff = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const int r = len - 8 * q;  // bytes of this word inside the token
+              const uint64_t m = r >= 8 ? ~0ull : (r <= 0 ? 0ull : (1ull << (8 * r)) - 1);
+              diff |= (x[q] ^ L.AW[4 * a + q]) & m;
+            }
+            if (diff == 0) {
+              best_len = len;
+              best_id = L.AI[a];
+            }
+          }
+        } else {
+          for (int a = 0; a < tok.n_added; ++a) {
+            const int o0 = tok.added_off[a], len = tok.added_off[a + 1] - o0;
+            if (len <= best_len || p + len > n) continue;
+            int k = 0;
+            while (k < len && tok.added_bytes[o0 + k] == L.T[p + k]) ++k;
+            if (k == len) {
+              best_len = len;
+              best_id = tok.added_id[a];
+            }
           }
         }
-      } else {
-        for (int a = 0; a < tok.n_added; ++a) {
-          const int o0 = tok.added_off[a], len = tok.added_off[a + 1] - o0;
-          if (len <= best_len || p + len > n) continue;
-          int k = 0;
-          while (k < len && tok.added_bytes[o0 + k] == L.T[p + k]) ++k;
-          if (k == len) {
-            best_len = len;
-            best_id = tok.added_id[a];
-          }
+        if (best_len > 0) L.Y[p] = best_id;
+      }
+      const int nc = n_cand - c0 < 64 ? n_cand - c0 : 64;
+      uint64_t sel = 0;
+      for (int i = 0; i < nc; ++i) {
+        const int pi = __builtin_amdgcn_readlane(p, i), li = __builtin_amdgcn_readlane(best_len, i);
+        if (li > 0 && pi >= cur) {
+          sel |= 1ull << i;
+          cur = pi + li;
         }
       }
-      L.K[ci] = (uint16_t)best_len;
-      if (best_len > 0) L.Y[p] = best_id;
-    }
-    wave_sync();
-    if (lane == 0) {
-      int cur = 0;
-      for (int i = 0; i < n_cand; ++i) {
-        const int p = L.P[i], len = L.K[i];
-        if (len == 0 || p < cur) continue;
-        L.C[p] |= B_ADD;
-        for (int q = p; q < p + len; ++q) L.C[q] |= B_IN;
-        L.M[p] = (uint16_t)len;
-        cur = p + len;
+      if ((sel >> lane) & 1) L.M[p] = (uint16_t)best_len;
+      while (sel) {
+        const int i = __builtin_ctzll(sel);
+        sel &= sel - 1;
+        const int pi = __builtin_amdgcn_readlane(p, i), li = __builtin_amdgcn_readlane(best_len, i);
+        for (int q = lane; q < li; q += 64) L.C[pi + q] |= (uint8_t)(q == 0 ? (B_ADD | B_IN) : B_IN);
       }
     }
     wave_sync();

@@ -5,7 +5,7 @@ import numpy as np
 import torch
 
 from .. import _lib, ops
-from ..torch_ops import ep_args
+from ..torch_ops import direct, ep_args
 from .base import BatchEnv
 from .configs import SokobanEnvConfig
 
@@ -92,14 +92,14 @@ class SokobanBatch(BatchEnv):
                                                                           int(max_actions_per_traj),
                                                                           float(format_penalty)), err)
         else:
-            torch.ops.ragen_amd.sokoban_step_turn(*self.state_args(), actions, n_actions, has_input, err, int(turn),
+            direct.sokoban_step_turn(*self.state_args(), actions, n_actions, has_input, err, int(turn),
                                                   int(max_actions_per_traj), float(format_penalty), *self.dims())
         self._invalidate()
 
     def render_rows(self):
         """SokobanEnv.render text mode (sokoban/env.py:53-61) of every env on the device:
         -> (UTF-8 rows u8[B, stride], lengths i32[B])."""
-        return torch.ops.ragen_amd.sokoban_render(self.room_fixed, self.room_state, self.H, self.W,
+        return direct.sokoban_render(self.room_fixed, self.room_state, self.H, self.W,
                                                   *self.glyph_lists())
 
     def render_all(self):

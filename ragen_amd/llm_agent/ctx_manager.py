@@ -17,7 +17,7 @@ import torch
 
 from .. import _lib, ops
 from ..env import REGISTERED_ENV_CONFIGS
-from ..torch_ops import NORM
+from ..torch_ops import NORM, direct
 from ..protocol import DataProto
 
 
@@ -524,7 +524,7 @@ class ContextManager:
     @staticmethod
     def _group_norm(acc, pen, seg, method):
         """rmi_group_normalize (group normalisation of ctx_manager.py:193-218) on device tensors."""
-        return torch.ops.ragen_amd.group_normalize(acc, pen, seg, NORM[method])
+        return direct.group_normalize(acc, pen, seg, NORM[method])
 
     def _sharded(self) -> bool:
         return self.process_group is not None and self.world_size > 1
@@ -692,7 +692,7 @@ class ContextManager:
         if len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n)):
             # every env in order: the generations are the rows (n_ids = None: R ids each)
             has_t, n_ids, ids = None, None, resp
-            torch.ops.ragen_amd.gen_rows(resp, None, n, vocab.packed, None, None, raw)
+            direct.gen_rows(resp, None, n, vocab.packed, None, None, raw)
         else:  # one launch: the rows scattered onto the batch, n_ids, the raw width
             local = env_ids - lo
             if local.size and (local.min() < 0 or local.max() >= n):
@@ -704,7 +704,7 @@ class ContextManager:
             ids = torch.empty(n, R, dtype=torch.int64, device=dev)
             n_ids = torch.empty(n, dtype=torch.int32, device=dev)
             has_t = torch.empty(n, dtype=torch.uint8, device=dev)  # 1: the env has a generation
-            torch.ops.ragen_amd.gen_rows(resp, ops.h2d(src, dev), n, vocab.packed, ids, n_ids, raw, has_t)
+            direct.gen_rows(resp, ops.h2d(src, dev), n, vocab.packed, ids, n_ids, raw, has_t)
         # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
         # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
         # the decode and refused by the step (ValueError)
@@ -755,7 +755,7 @@ class ContextManager:
         from .. import distributed as rd
         if self.process_group is not None and self.world_size > 1:
             n_slots = rd.all_reduce_max_int(n_slots, self.process_group, dev)
-        ids, am, pos, score_tensor, loss_mask, response_mask, err = torch.ops.ragen_amd.assemble_rows(
+        ids, am, pos, score_tensor, loss_mask, response_mask, err = direct.assemble_rows(
             tokens, start, row_len, max(S, 1), int(pr.pad_id), int(special_token), int(reward_token), tab, n_sc,
             n_slots, bool(ap.use_turn_scores), bool(self.config.enable_response_mask),
             "qwen" in self.tokenizer.name_or_path.lower())

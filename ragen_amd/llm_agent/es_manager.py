@@ -32,7 +32,7 @@ from .. import _lib, ops
 from .. import distributed as rd
 from ..env import REGISTERED_ENV_CONFIGS, REGISTERED_ENVS
 from ..env.base import BatchEnv
-from ..torch_ops import ep_args, parse_cfg_words
+from ..torch_ops import direct, ep_args, parse_cfg_words
 
 
 @dataclass
@@ -562,7 +562,7 @@ class EnvStateManager:
         for tg in self.tags:
             a, z = tg.lo - lo0, tg.hi - lo0
             cfg, sel, lact = self._parse_args(tg, enable_think, action_sep, True)
-            text, tlen, derr, acts, n_act, spans, at, al, perr = torch.ops.ragen_amd.detok_parse(
+            text, tlen, derr, acts, n_act, spans, at, al, perr = direct.detok_parse(
                 inp.ids[a:z], None if inp.n_ids is None else inp.n_ids[a:z], v.packed, v.data, inp.stride, cfg, sel, True, int(lact))
             outs.append({"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
                          "action_len": al if lact else None, "err": perr})

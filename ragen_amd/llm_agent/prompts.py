@@ -49,6 +49,7 @@ import torch
 
 from .. import _lib, ops
 from ..tokenizer import DeviceTokenizer
+from ..torch_ops import direct
 
 SYSTEM = "You're a helpful assistant. "
 _P = ("@@RMI_S@@", "@@RMI_U1@@", "@@RMI_A1@@", "@@RMI_U2@@", "@@RMI_A2@@")
@@ -393,11 +394,11 @@ class DevicePrompts:
         flat = [len(prog)] + [x for p in prog for x in p] + [self.n_tags, obs.shape[1], 0 if resp is None else
                                                              resp.shape[1], int(self.enable_think), self.K]
         if turn is None:
-            return torch.ops.ragen_amd.prompt_text(flat, self.sep, self.n_envs, stride, pool, tc, self.tag, obs,
+            return direct.prompt_text(flat, self.sep, self.n_envs, stride, pool, tc, self.tag, obs,
                                                    obs_len, ints, reward, reward_int, resp, resp_len, spans, cond,
                                                    active)
         ne, flags, last = turn
-        return torch.ops.ragen_amd.prompt_text(flat, self.sep, self.n_envs, stride, pool, tc, self.tag, obs, obs_len,
+        return direct.prompt_text(flat, self.sep, self.n_envs, stride, pool, tc, self.tag, obs, obs_len,
                                                ints, reward, None, resp, resp_len, spans, None, active, ne, flags,
                                                self.int_reward_tags, int(last))
 
@@ -604,6 +605,11 @@ class DevicePrompts:
         self._pending = None
         if any_bad is False:
             return
+        if any_bad is None:  # read the any() first (one small kernel): nonzero() is a sort-based pass
+            stats = torch.empty(2, dtype=torch.int32, device=self.device)
+            ops.rows_stats(self.len, None, 0, bad, stats)
+            if not int(ops.d2h(stats, self)[1]):
+                return
         idx = torch.nonzero(bad).flatten().cpu().tolist()
         if idx:
             self.host_rows_used += len(idx)
@@ -674,7 +680,7 @@ class DevicePrompts:
                 ops.rows_stats(self.len, rows, rows.numel(), None, stats)
                 mx = int(ops.d2h(stats, self)[0])
             S = mx + self.tail.numel()
-        ids, am, pos, err = torch.ops.ragen_amd.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
+        ids, am, pos, err = direct.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
         return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
 
     def update_rows(self):

@@ -166,7 +166,7 @@ class Bpe(ctypes.Structure):
                 ("added_bytes", ctypes.c_void_p), ("added_off", ctypes.c_void_p), ("added_id", ctypes.c_void_p),
                 ("added_first", ctypes.c_uint32 * 8), ("word_cache", ctypes.c_void_p),
                 ("word_cache_mask", ctypes.c_uint32), ("n_exp", ctypes.c_int32), ("exp_off", ctypes.c_void_p),
-                ("exp_ids", ctypes.c_void_p)]
+                ("exp_ids", ctypes.c_void_p), ("added_words", ctypes.c_void_p), ("ascii_class", ctypes.c_void_p)]
 
 
 def _backend_json(tokenizer) -> dict:
@@ -258,6 +258,9 @@ class DeviceTokenizer:
     exp: Optional[list] = None
     exp_off: Optional[torch.Tensor] = None
     exp_ids: Optional[torch.Tensor] = None
+    # staging tables (rmi_bpe_t.added_words / ascii_class; _build_staging)
+    added_words: Optional[torch.Tensor] = None
+    ascii_class: Optional[torch.Tensor] = None
 
     MAX_EXPANSIONS = 64
 
@@ -314,11 +317,25 @@ class DeviceTokenizer:
         blk, cls = class_table() if pretok == PRETOK_QWEN2 else _char_class_table()
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
         data = b"".join(blobs) + b"\0" * 4
-        return DeviceTokenizer(
+        dt = DeviceTokenizer(
             t(blk.astype(np.int16).view(np.int16)), t(cls), t(byte_id), t(table.view(np.int64)), mask, shift, pretok,
             int(norm is not None), t(np.frombuffer(data, np.uint8).copy()), t(off),
             t(np.array(list(added.values()) or [0], np.int32)), first, added,
             torch.zeros(DeviceTokenizer.WORD_CACHE_ENTRIES * 16, dtype=torch.int32, device=device))
+        dt.ascii_class = t(np.ascontiguousarray(cls[int(blk[0]) * 256:int(blk[0]) * 256 + 128]).astype(np.uint8))
+        dt._build_staging(blobs)
+        return dt
+
+    def _build_staging(self, blobs):
+        """The added tokens as zero-padded 32-byte words (rmi_bpe_t.added_words), when every
+        one fits (<= 32 bytes, <= 64 tokens); else None (the kernel compares from the tables)."""
+        if not blobs or len(blobs) > 64 or any(len(x) > 32 for x in blobs):
+            self.added_words = None
+            return
+        w = np.zeros((len(blobs), 32), np.uint8)
+        for i, x in enumerate(blobs):
+            w[i, :len(x)] = np.frombuffer(x, np.uint8)
+        self.added_words = torch.from_numpy(w.view(np.int64).reshape(-1).copy()).to(self.byte_id.device)
 
     def add_expansion(self, ids) -> bytes:
         """The placeholder bytes (0xFF, 0x80 + e) of the expansion whose tokens are ``ids`` (a
@@ -354,6 +371,7 @@ class DeviceTokenizer:
         np.cumsum([len(x) for x in self.exp], out=eo[1:])
         self.exp_off = torch.from_numpy(eo).to(dev)
         self.exp_ids = torch.from_numpy(np.array([i for x in self.exp for i in x], np.int32)).to(dev)
+        self._build_staging(blobs)
 
     @property
     def n_added(self) -> int:
@@ -369,6 +387,10 @@ class DeviceTokenizer:
             s.added_first[i] = w
         if self.word_cache is not None:
             s.word_cache, s.word_cache_mask = self.word_cache.data_ptr(), self.word_cache.numel() // 16 - 1
+        if self.added_words is not None:
+            s.added_words = self.added_words.data_ptr()
+        if self.ascii_class is not None:
+            s.ascii_class = self.ascii_class.data_ptr()
         return s
 
     def args(self):
@@ -382,9 +404,10 @@ class DeviceTokenizer:
                     max_len: int = 0):
         """Append the ids of every text row to ``out`` (rmi_bpe_encode); max_len (0: the row
         pitch) bounds the rows' length.  -> (n_tok, mark_tok, err)."""
-        return torch.ops.ragen_amd.bpe_encode(*self.args(), text, text_len, out, out_len, mark_byte, int(max_len),
-                                              self.word_cache, self.exp_off if self.exp else None,
-                                              self.exp_ids if self.exp else None)
+        from .torch_ops import direct
+        return direct.bpe_encode(*self.args(), text, text_len, out, out_len, mark_byte, int(max_len),
+                                 self.word_cache, self.exp_off if self.exp else None,
+                                 self.exp_ids if self.exp else None, self.added_words, self.ascii_class)
 
     def encode(self, texts: Sequence[str], stride: int = None) -> List[Optional[List[int]]]:
         """Convenience (tests, tools): ids of each text, or None for a row the device flagged."""

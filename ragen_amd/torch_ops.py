@@ -63,6 +63,21 @@ def _op(name, mutates=()):
     return lambda fn: _Op(name, fn, mutates)
 
 
+class _Direct:
+    """``direct.<op>``: an op's implementation called straight from Python — the same code the
+    dispatcher runs for the CUDA key, without the dispatcher's argument boxing (≈6-8 µs a call
+    on the host).  The engine's own device turn loop calls its ops this way; callers outside
+    it use ``torch.ops.ragen_amd.<op>``."""
+
+    def __getattr__(self, name):
+        fn = globals()[name].__wrapped__
+        setattr(self, name, fn)
+        return fn
+
+
+direct = _Direct()
+
+
 def _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec) -> ops.EpisodeState:
     return ops.EpisodeState(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec)
 
@@ -676,7 +691,7 @@ def parse_actions(cfg: List[int], text: Tensor, text_len: Tensor, sel: Optional[
     dev = text.device
     spans = o["spans"] if o["spans"] is not None else torch.empty(0, 4, dtype=torch.int32, device=dev)
     at = o["action_text"] if o["action_text"] is not None else torch.empty(B, K, 0, dtype=torch.uint8, device=dev)
-    al = o["action_len"] if o["action_len"] is not None else torch.zeros(B, K, dtype=torch.int32, device=dev)
+    al = o["action_len"] if o["action_len"] is not None else _zeros_i32(B, K, dev)
     return o["actions"], o["n_actions"], spans, at, al, o["err"]
 
 
@@ -687,6 +702,18 @@ def _(cfg, text, text_len, sel, with_spans, action_text_len):
             text.new_empty(B if with_spans else 0, 4, dtype=torch.int32),
             text.new_empty(B, K, action_text_len, dtype=torch.uint8), text.new_empty(B, K, dtype=torch.int32),
             text.new_empty(B, dtype=torch.uint8))
+
+
+_ZEROS = {}  # (B, K, device) -> a zero i32[B, K] (the unused action_len output; read only)
+
+
+def _zeros_i32(B, K, dev):
+    z = _ZEROS.get((B, K, dev))
+    if z is None:
+        if len(_ZEROS) > 64:
+            _ZEROS.clear()
+        z = _ZEROS[(B, K, dev)] = torch.zeros(B, K, dtype=torch.int32, device=dev)
+    return z
 
 
 @_op("detok_parse")
@@ -705,7 +732,7 @@ def detok_parse(ids: Tensor, n_ids: Optional[Tensor], vocab_packed: Tensor, voca
     dev = ids.device
     spans = o["spans"] if o["spans"] is not None else torch.empty(0, 4, dtype=torch.int32, device=dev)
     at = o["action_text"] if o["action_text"] is not None else torch.empty(B, K, 0, dtype=torch.uint8, device=dev)
-    al = o["action_len"] if o["action_len"] is not None else torch.zeros(B, K, dtype=torch.int32, device=dev)
+    al = o["action_len"] if o["action_len"] is not None else _zeros_i32(B, K, dev)
     return o["text"], o["text_len"], o["decode_err"], o["actions"], o["n_actions"], spans, at, al, o["err"]
 
 
@@ -721,7 +748,7 @@ def _(ids, n_ids, vocab_packed, vocab_bytes, stride, cfg, sel, with_spans, actio
 
 
 def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache=None,
-                exp_off=None, exp_ids=None):
+                exp_off=None, exp_ids=None, added_words=None, ascii_class=None):
     from .tokenizer import Bpe
     ops._dev(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id)
     if len(params) != 13:
@@ -742,6 +769,18 @@ def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, add
         ops._dt(exp_off, torch.int32, "exp_off")
         ops._dt(exp_ids, torch.int32, "exp_ids")
         s.n_exp, s.exp_off, s.exp_ids = exp_off.numel() - 1, exp_off.data_ptr(), exp_ids.data_ptr()
+    if added_words is not None:  # staging tables (rmi_bpe_t.added_words / ascii_class)
+        ops._dev(added_words)
+        ops._dt(added_words, torch.int64, "added_words")
+        if added_words.numel() != 4 * params[4] or params[4] > 64:
+            raise ValueError("added_words: 4 words per added token, at most 64 tokens")
+        s.added_words = added_words.data_ptr()
+    if ascii_class is not None:
+        ops._dev(ascii_class)
+        ops._dt(ascii_class, torch.uint8, "ascii_class")
+        if ascii_class.numel() != 128:
+            raise ValueError("ascii_class: 128 classes")
+        s.ascii_class = ascii_class.data_ptr()
     return s
 
 
@@ -750,14 +789,15 @@ def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tens
                added_off: Tensor, added_id: Tensor, params: List[int], text: Tensor, text_len: Tensor, out: Tensor,
                out_len: Optional[Tensor], mark_byte: Optional[Tensor], max_len: int = 0,
                word_cache: Optional[Tensor] = None, exp_off: Optional[Tensor] = None,
-               exp_ids: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
+               exp_ids: Optional[Tensor] = None, added_words: Optional[Tensor] = None,
+               ascii_class: Optional[Tensor] = None) -> Tuple[Tensor, Tensor, Tensor]:
     """The tokenizer call of get_lm_inputs (ctx_manager.py:265-278) for a byte-level BPE:
     every text row's ids appended to ``out`` (rmi_bpe_encode; tables: ragen_amd.tokenizer).
     max_len (0: the row pitch) bounds the rows' length and sizes the kernel's LDS.
     -> (n_tok i32[B], mark_tok i32[B], err u8[B])."""
     import ctypes
     tok = _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache,
-                      exp_off, exp_ids)
+                      exp_off, exp_ids, added_words, ascii_class)
     ops._dev(text, text_len, out, out_len, mark_byte)
     ops._dt(text, torch.uint8, "text")
     ops._dt(text_len, torch.int32, "text_len")
@@ -769,7 +809,9 @@ def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tens
         raise ValueError("text, text_len and out must have one row per text")
     dev = text.device
     n_tok = torch.empty(B, dtype=torch.int32, device=dev)
-    mark_tok = torch.zeros(B, dtype=torch.int32, device=dev)
+    # (the kernel writes every row's mark when given a mark_byte; otherwise the result is zeros)
+    mark_tok = torch.empty(B, dtype=torch.int32, device=dev) if mark_byte is not None else \
+        torch.zeros(B, dtype=torch.int32, device=dev)
     err = torch.empty(B, dtype=torch.uint8, device=dev)
     pitch = int(text.shape[1])
     cap = (int(max_len) + 3) // 4 * 4 if max_len else pitch
@@ -783,7 +825,7 @@ def bpe_encode(cp_block: Tensor, cp_class: Tensor, byte_id: Tensor, merges: Tens
 
 @bpe_encode.register_fake
 def _(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, text, text_len, out, out_len,
-      mark_byte, max_len=0, word_cache=None, exp_off=None, exp_ids=None):
+      mark_byte, max_len=0, word_cache=None, exp_off=None, exp_ids=None, added_words=None, ascii_class=None):
     B = text.shape[0]
     return (text.new_empty(B, dtype=torch.int32), text.new_empty(B, dtype=torch.int32),
             text.new_empty(B, dtype=torch.uint8))

@@ -13,7 +13,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from ragen_amd import ops, synthetic  # noqa: E402
+from ragen_amd import ops, synthetic, torch_ops  # noqa: E402
 from ragen_amd.config import env_task  # noqa: E402
 from ragen_amd.llm_agent import LLMAgentProxy, TokenActor  # noqa: E402
 from ragen_amd.llm_agent import ctx_manager as cm, es_manager as em, prompts as pm  # noqa: E402
@@ -58,10 +58,7 @@ def wrap(obj, name, label, setter=setattr):
 for nm in ("prompt_text", "bpe_encode", "pad_rows", "detok_parse", "gen_rows", "sokoban_step_turn",
            "sokoban_step_turn_first", "sokoban_step_turn_finalize", "sokoban_render", "assemble_rows",
            "group_normalize"):
-    try:
-        wrap(torch.ops.ragen_amd, nm, "op " + nm)
-    except Exception as e:  # noqa: BLE001
-        print("cannot wrap", nm, e)
+    wrap(torch_ops.direct, nm, "op " + nm)  # the device loop calls the implementations directly
 for nm in ("d2h", "h2d", "turn_inputs", "turn_readback", "prompt_commit", "rows_stats"):
     wrap(ops, nm, "ops." + nm)
 for nm in ("_turn_text", "_obs", "_program", "_run_text", "_encode", "advance", "gen_batch", "_text_bound"):
