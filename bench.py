@@ -452,8 +452,9 @@ def text_leg(R, device, reps=20):
     * text rollout: the SK rollout driven from text (5 x (parse + turn), restore and finalize
       fused, in a HIP graph) -> env-steps/s of the device-resident text API;
     * token rollout: the whole per-turn loop between two LLM generations on the device: the
-      response token ids -> rmi_detokenize -> rmi_parse_actions -> the turn -> rmi_sokoban_render
-      (the next observation's text), 5 turns per rollout, in a HIP graph."""
+      response token ids -> rmi_detok_parse (decode + parse) -> the turn with the next observation's
+      text rendered in the same launch (rmi_sokoban_step_turn_render), 5 turns per rollout, in a
+      HIP graph."""
     B = R.B
     lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
     ids_h, n_h = R.ids.cpu().numpy(), R.n.cpu().numpy()
@@ -554,19 +555,25 @@ def text_leg(R, device, reps=20):
     torch.cuda.synchronize()
     fused_us = e[0].elapsed_time(e[1]) * 1e3 / reps
 
-    def token_step():
+    robs = ops.render_struct(R.env.config.grid_lookup, 6, 6, *obs)
+
+    def token_step():  # the turn renders the next observation in the same launch
         e = R.env
         for t in range(T_TURNS):
             o, ts = text_turns[t]
             ops.detok_parse(tok[t], tvocab, stride, cfg, out=fused[t])
             if t == 0:
-                ops.sokoban_step_turn_first(R.st, e.ep, ts, e.init_state, e.init_player)
+                ops.sokoban_step_turn_render(R.st, e.ep, ts, robs, init_state=e.init_state, init_player=e.init_player)
             elif t < T_TURNS - 1:
-                ops.sokoban_step_turn(R.st, e.ep, ts)
+                ops.sokoban_step_turn_render(R.st, e.ep, ts, robs)
             else:
-                ops.sokoban_step_turn_finalize(R.st, e.ep, ts, R.fin)
-            ops.sokoban_render(R.st, B, e.config.grid_lookup, device, out=obs)
+                ops.sokoban_step_turn_render(R.st, e.ep, ts, robs, fin=R.fin)
     token_step()
+    torch.cuda.synchronize()
+    want = ops.sokoban_render(R.st, B, R.env.config.grid_lookup, device)  # the fused rows == a separate render
+    assert torch.equal(want[1], obs[1])
+    assert all(bytes(want[0][i, :int(want[1][i])].cpu().numpy()) == bytes(obs[0][i, :int(obs[1][i])].cpu().numpy())
+               for i in range(0, B, 97))
     torch.cuda.synchronize()
     assert int(R.env.ep.turn_exec.sum().item()) == steps
     ms_tok = _graph_rollout(token_step)
@@ -590,7 +597,8 @@ def text_leg(R, device, reps=20):
             "detok_parse": {"kernel": "rmi_detok_parse", "rows": B, "ids_per_row": int(tok[0].shape[1]),
                             "vocab": "byte-level (synthetic.byte_vocab)", "us": fused_us,
                             "note": "the decode fused with the parse: one launch per turn on the token path"},
-            "token_rollout": {"config": "SK rollout from response token ids: 5 x (detok_parse + turn + render)",
+            "token_rollout": {"config": "SK rollout from response token ids: 5 x (detok_parse + turn with the "
+                                        "next observation rendered in the same launch)",
                               "env_steps_per_rollout": steps, "ms_per_rollout": ms_tok,
                               "env_steps_per_s": steps / ms_tok * 1e3},
             "render": {"kernel": "rmi_sokoban_render", "envs": B, "us": render_us}}
@@ -649,6 +657,8 @@ def api_leg(device):
                    "turn_loop_env_steps_per_s": steps / tm["turns_s"], "rows_formulated": rows,
                    "reset_s": tm["reset_s"],  # es.reset(): rooms for a fresh train seed (host) + device restore
                    "env_steps_per_s_with_reset": steps / (total + tm["reset_s"]),
+                   "readbacks": tm.get("readbacks"), "turns": len(shapes),
+                   "eager_prompt_turns": pr.eager_turns if pr is not None else None,
                    "prompt_batch_shapes": shapes, "update_batch_shape": upd, "device_prompts": pr is not None,
                    "host_prompt_rows": pr.host_rows_used if pr is not None else None,
                    "tokenizer": f"{tok.name_or_path}, vocab {len(tok)}",

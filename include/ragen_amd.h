@@ -162,6 +162,26 @@ int rmi_sokoban_generate_rooms(const int64_t* seeds /*[host][n]*/, int32_t n, in
 int rmi_sokoban_render(const rmi_sokoban_t* env, int32_t B, const uint32_t* glyph_bytes, const uint8_t* glyph_len,
                        uint8_t* out, int32_t stride, int32_t* len, rmi_stream_t stream);
 
+/* The turn and the next observation in ONE launch: EnvStateManager.step (es_manager.py:105-171,
+ * as rmi_sokoban_step_turn) followed by SokobanEnv.render (sokoban/env.py:53-61) of every env's
+ * state after it (es_manager.py:170 `next_state`; the rows rmi_sokoban_render writes, byte for
+ * byte).  fin != NULL: the rollout's last turn fused with its end (rmi_sokoban_step_turn_finalize);
+ * init_state / init_player != NULL: a fresh episode's first turn fused with its reset
+ * (rmi_sokoban_step_turn_first); not both.  The render is done by each env's own lane from the
+ * registers of its turn for 6x6-sized (36-cell) and 64-cell rooms with B > 4096; any other
+ * layout runs the turn launch, then rmi_sokoban_render (same outputs).                         */
+typedef struct {
+  uint32_t glyph_bytes[16]; /* as rmi_sokoban_render's glyph table                          */
+  uint8_t glyph_len[16];    /* 0..4 (0: '?')                                                */
+  uint8_t* out;             /* [B, stride] device, 4-B aligned; stride % 4 == 0 and
+                               >= H*W*4 + H - 1                                              */
+  int32_t stride;
+  int32_t* len;             /* [B] bytes written                                            */
+} rmi_render_t;
+int rmi_sokoban_step_turn_render(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                 uint8_t* err, const rmi_finalize_t* fin, const uint8_t* init_state,
+                                 const int8_t* init_player, const rmi_render_t* obs, rmi_stream_t stream);
+
 /* --------------------------------------------------------------------- FrozenLake
  * Replaces: FrozenLakeEnv.step (frozen_lake/env.py:39-45) -> gymnasium FrozenLakeEnv.step
  *           + categorical_sample (third-party, App. A.2), numpy PCG64 draws (App. A.5). */
@@ -637,6 +657,13 @@ int rmi_prompt_commit(const uint8_t* bpe_err, const uint8_t* text_err, const uin
                       int32_t* len_upd, int64_t B, uint8_t* bad, rmi_stream_t stream);
 int rmi_rows_stats(const int32_t* len, const int64_t* rows, int64_t n_rows, const uint8_t* bad, int64_t B,
                    int32_t* stats, rmi_stream_t stream);
+/* rmi_rows_stats over the envs that go on after a turn -- the next generation batch of
+ * get_lm_inputs (the env outputs es_manager.py:168-171 returns: an input this turn, not done):
+ * e with (has == NULL || has[e]) and !(flags[e] & RMI_FLAG_DONE).  stats i32[3] = (longest
+ * len[e] among them, any bad[e] over all B (0 without bad), their count).  Launched after the
+ * next prompt's encode, into the turn's readback buffer: one readback per turn.              */
+int rmi_next_rows_stats(const int32_t* len, const uint8_t* has, const uint8_t* flags, const uint8_t* bad, int64_t B,
+                        int32_t* stats, rmi_stream_t stream);
 
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and
@@ -654,6 +681,9 @@ const char* rmi_version(void);
 /* Stream-ordered device-to-device copy: a 16-B-per-lane grid-stride streaming kernel (the
  * achievable-HBM-bandwidth probe bench.py reports as roofline.achievable_peak).            */
 int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t stream);
+/* [host] Wait until every launch enqueued on the stream has finished: the turn loop's one
+ * readback (a small async device -> pinned-host copy, then this) with no Stream object.     */
+int rmi_stream_synchronize(rmi_stream_t stream);
 
 #ifdef __cplusplus
 }

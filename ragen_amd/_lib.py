@@ -46,6 +46,12 @@ class Finalize(ctypes.Structure):
                 ("pen", c_void_p), ("norm", c_void_p)]
 
 
+class Render(ctypes.Structure):
+    """rmi_render_t: the observation output of rmi_sokoban_step_turn_render."""
+    _fields_ = [("glyph_bytes", ctypes.c_uint32 * 16), ("glyph_len", ctypes.c_uint8 * 16), ("out", c_void_p),
+                ("stride", c_int32), ("len", c_void_p)]
+
+
 class FrozenLake(ctypes.Structure):
     _fields_ = [("nrow", c_int32), ("ncol", c_int32), ("is_slippery", c_int32), ("cs0", c_double),
                 ("cs1", c_double), ("cs2", c_double), ("desc", c_void_p), ("s", c_void_p), ("rng", c_void_p)]
@@ -112,6 +118,8 @@ _SIGS = {
                                                     c_void_p]),
     "rmi_frozenlake_step_turn_first": (c_int32, [_P(FrozenLake), _P(Episode), _P(Turn), c_void_p, c_void_p,
                                                  c_void_p, c_void_p, c_void_p]),
+    "rmi_sokoban_step_turn_render": (c_int32, [_P(Sokoban), _P(Episode), _P(Turn), c_void_p, _P(Finalize), c_void_p,
+                                               c_void_p, _P(Render), c_void_p]),
     "rmi_sokoban_render": (c_int32, [_P(Sokoban), c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                      c_void_p]),
     "rmi_frozenlake_render": (c_int32, [_P(FrozenLake), c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
@@ -157,6 +165,7 @@ _SIGS = {
     "rmi_parse_actions": (c_int32, [_P(ParseCfg), c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rmi_stream_synchronize": (c_int32, [c_void_p]),
     "rmi_prompt_text": (c_int32, [_P(Prompt), c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_gen_rows": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
@@ -172,6 +181,7 @@ _SIGS = {
                                     c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_prompt_commit": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_rows_stats": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rmi_next_rows_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
 }
 
 _lib = None

@@ -29,6 +29,10 @@ __global__ void tail_copy_kernel(uint8_t* __restrict__ dst, const uint8_t* __res
 
 RMI_API const char* rmi_version(void) { return "ragen_amd 0.2.0 (gfx950)"; }
 
+RMI_API int rmi_stream_synchronize(rmi_stream_t stream) {
+  return hipStreamSynchronize(rmi::as_stream(stream)) == hipSuccess ? RMI_OK : RMI_EDEVICE;
+}
+
 RMI_API int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t stream) {
   using namespace rmi;
   if ((!dst || !src) && bytes) return RMI_EINVAL;

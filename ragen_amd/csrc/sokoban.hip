@@ -495,6 +495,80 @@ constexpr int kSpreadLpe = RMI_SPREAD_LPE;
 constexpr int kSokWpb = RMI_SOK_WPB;
 __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMaxEnvs; }
 
+// ---- the observation a turn launch renders itself (rmi_sokoban_step_turn_render, kObs): the
+// text of SokobanEnv.render (sokoban/env.py:53-61) of every env's state after the turn, byte for
+// byte rmi_sokoban_render's rows (render.hip), built by the env's own lane from what the turn
+// already holds in registers — the final bitboards of a stepped regular room, else the row
+// dwords — so the next observation costs no launch and no reload of the rows.  The glyph table
+// sits one entry per lane (a ds_bpermute per cell: no LDS staging, no barrier); the lane appends
+// each glyph to a 64-bit accumulator and stores every completed dword of its row.
+struct ObsOut {
+  uint32_t gb[16];  // glyph bytes of each code (absent codes: '?'), little-endian
+  uint64_t glen;    // glyph byte count of each code, 4 bits per code (1..4)
+  uint8_t* out;     // [B, stride]
+  int32_t* len;     // [B]
+  int stride;
+};
+
+// The wave renders into a wave-private LDS block laid out like its 64 rows of the output (pitch
+// = the output stride), then copies the block out with coalesced 16-B stores: one lane per row
+// storing to its own row would scatter every store over 64 rows.
+constexpr int obs_pitch_max(int HW) { return HW * 5; }  // >= H*W*4 + H - 1 for any H <= H*W (bytes)
+
+template <int HW, class M, int NWL>
+__device__ __forceinline__ void render_obs(const ObsOut& o, int64_t b0, int lane, int n_live, int W, bool bits,
+                                           M wall, M target, M box, int jp, const uint32_t (&xs)[NWL],
+                                           const uint32_t (&xf)[NWL], uint32_t tabv, uint32_t* blk) {
+  const int pitch_w = o.stride >> 2;
+  uint32_t* row = blk + lane * pitch_w;
+  uint64_t acc = 0;
+  int fill = 0, w = 0, col = 0;
+  auto emit = [&](uint32_t g, int n) {
+    acc |= (uint64_t)g << (8 * fill);
+    fill += n;
+    if (fill >= 4) {
+      row[w++] = (uint32_t)acc;
+      acc >>= 32;
+      fill -= 4;
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < HW; ++i) {
+    // the state byte with the player on a target shown as 6 (sokoban/env.py:55) ...
+    const uint32_t s = (xs[i >> 2] >> (8 * (i & 3))) & 0xFFu, f = (xf[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    int code = (s == 5u && f == 2u) ? 6 : (int)s;
+    // ... or, for a stepped regular room, rebuilt from the bitboards (window bit j = cell W + j;
+    // row 0 is all wall): wall 0, player 5 / 6 on a target, box 4 / 3 on a target, else 1 / 2
+    const int j = i - W;
+    const int jj = j >= 0 ? j : 0;
+    const uint32_t wl = j >= 0 ? (uint32_t)(wall >> jj) & 1u : 1u;
+    const int t = (int)((target >> jj) & 1u), bx = (int)((box >> jj) & 1u);
+    const int bc = wl ? 0 : (j == jp ? 5 + t : (bx ? 4 - t : 1 + t));
+    code = bits ? bc : code;
+    const uint32_t g = (uint32_t)__shfl((int)tabv, code & 15, 64);
+    const int n = code < 16 ? (int)((o.glen >> (4 * (code & 15))) & 15u) : 1;
+    emit(code < 16 ? g : (uint32_t)'?', n);
+    if (++col == W) {  // wave-uniform
+      col = 0;
+      if (i < HW - 1) emit((uint32_t)'\n', 1);
+    }
+  }
+  if (fill > 0) row[w] = (uint32_t)acc;  // the last dword's unused bytes are zero
+  if (lane < n_live) o.len[b0 + lane] = 4 * w + fill;
+  wave_sync();
+  // the block out: rows b0 .. b0 + n_live - 1 are one contiguous run of n_live * stride bytes
+  const int nb = n_live * o.stride;
+  uint8_t* dst = o.out + b0 * (int64_t)o.stride;
+  if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
+    const int n16 = nb >> 4;
+    for (int k = lane; k < n16; k += 64)
+      reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(blk)[k];
+    for (int k = (n16 << 2) + lane; k < (nb >> 2); k += 64) reinterpret_cast<uint32_t*>(dst)[k] = blk[k];
+  } else {
+    for (int k = lane; k < (nb >> 2); k += 64) reinterpret_cast<uint32_t*>(dst)[k] = blk[k];
+  }
+}
+
 // One launch = one turn of every env.  LPE consecutive lanes own one env (LPE = 1 for big
 // batches; 4 when the batch is too small to fill the chip, so the per-wave instruction
 // chain — decode, row rebuild, loads, stores — is split LPE ways; the steps themselves run
@@ -511,12 +585,15 @@ __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMax
 // the lanes whose env acts this turn, a second memory round trip that a batch this size hides,
 // so the rows of done envs are not fetched (HBM-bound there: done envs were ≈18 % of the bench
 // rollout's env-turns, their rows ≈9 % of its traffic).
-template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
+// kObs (HW != 0, LPE == 1): the launch also renders every env's observation after the turn (render_obs).
+template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false, bool kObs = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
                                                                   uint8_t* __restrict__ err_out, rmi_finalize_t fin,
                                                                   const uint8_t* __restrict__ init_state = nullptr,
-                                                                  const int8_t* __restrict__ init_player = nullptr) {
+                                                                  const int8_t* __restrict__ init_player = nullptr,
+                                                                  ObsOut obs = ObsOut{}) {
+  static_assert(!kObs || (HW != 0 && LPE == 1 && !kLate), "the fused render needs a fixed room size, one lane per env");
   constexpr int NW = HW ? HW / 4 : kMaxWords;
   constexpr int NWL = (NW + LPE - 1) / LPE;      // row dwords per lane
   constexpr int kEnvs = kWave / LPE;             // envs per wave
@@ -524,6 +601,7 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   __shared__ uint32_t lds_fixed[kSokWpb * kEnvs * NW];
   const int hw = HW ? HW : hw_rt;
   const int row_words = hw >> 2;
+  __shared__ uint32_t lds_obs[kObs ? kSokWpb * kWave * (obs_pitch_max(HW) / 4) : 1];  // kObs: the wave's rows
   const int B = ep.B;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int sub = lane % LPE, slot = lane / LPE;
@@ -563,6 +641,7 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   }
   int n_act = in.n_actions[bc];
   const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K, ep.flags + bc);
+  const uint32_t tabv = kObs ? obs.gb[lane & 15] : 0u;  // the glyph table, one entry per lane
   FinRecord rec;
   if (kFin) rec.load(ep, bc);
   if (!live) flags = RMI_FLAG_DONE;
@@ -616,7 +695,8 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   // kFirst: the reset row's store (above) has completed before any lane of the env writes
   // cells of it (with several lanes per env they are other lanes' dwords)
   if (kFirst) __builtin_amdgcn_s_waitcnt(0);
-  if (__all(regular)) {
+  const bool fast = __all(regular);
+  if (fast) {
     if (act) {
       const M box0 = box;
       const int jp0 = jp;
@@ -788,6 +868,12 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
     if (row_changed) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
   }
   RMI_STAMP(4);
+  if constexpr (kObs) {
+    const int64_t b0 = ((int64_t)blockIdx.x * kSokWpb + wave) * kWave;
+    const int n_live = B - b0 < kWave ? (int)(B - b0) : kWave;  // <= 0 for a wave past B: nothing stored
+    render_obs<HW, M, NWL>(obs, b0, lane, n_live, W, fast && act, wall, target, box, jp, xs, xf, tabv,
+                           lds_obs + wave * kWave * (obs_pitch_max(HW) / 4));
+  }
   if (kFin) {
     if (act) rec.set(in.turn, o.acc, o.info);  // this turn's record is still in registers
     finalize_envs<LPE>(ep, fin, rec, b, live && sub == 0, flags, n_turns, num_actions, penalty, act ? in.turn : -1,
@@ -876,6 +962,33 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
   return launch_status();
 }
 
+// The turn with the render fused (kObs): fixed room sizes (36 / 64 cells), one lane per env.
+// -> RMI_EUNSUP for any other layout (the caller launches the turn and the render separately).
+template <bool kFin, bool kFirst>
+int sokoban_step_turn_obs_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in, uint8_t* err,
+                                 const rmi_finalize_t& fin, hipStream_t s, const uint8_t* init_state,
+                                 const int8_t* init_player, const ObsOut& obs) {
+  const int hw = env->H * env->W;
+  const int H = env->H, W = env->W;
+  if (spread_lanes(ep->B) || (hw != 36 && hw != 64) || obs.stride > obs_pitch_max(hw)) return RMI_EUNSUP;
+  uint64_t border = 0;
+  for (int r = 0; r < H; ++r)
+    for (int c = 0; c < W; ++c)
+      if (r == 0 || c == 0 || r == H - 1 || c == W - 1) border |= 1ull << (r * W + c);
+  const bool w32 = (H - 1) * W <= 32;
+  const dim3 grid((unsigned)((ep->B + kWave * kSokWpb - 1) / (kWave * kSokWpb))), block(kWave * kSokWpb);
+  if (hw == 36 && w32)
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint32_t, 1, kFin, kFirst, false, true>), grid, block, 0, s, *env,
+                       *ep, *in, hw, border, err, fin, init_state, init_player, obs);
+  else if (hw == 36)
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint64_t, 1, kFin, kFirst, false, true>), grid, block, 0, s, *env,
+                       *ep, *in, hw, border, err, fin, init_state, init_player, obs);
+  else
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<64, uint64_t, 1, kFin, kFirst, false, true>), grid, block, 0, s, *env,
+                       *ep, *in, hw, border, err, fin, init_state, init_player, obs);
+  return launch_status();
+}
+
 int sokoban_check(const rmi_sokoban_t* env) {
   if (!env) return RMI_EINVAL;
   const int hw = env->H * env->W;
@@ -897,36 +1010,54 @@ RMI_API int rmi_sokoban_set_stamps(unsigned long long* buf) {
 }
 #endif
 
+namespace rmi {
+namespace {
+constexpr int kSkip = 1;  // (validate_turn: an empty batch, nothing to launch)
+// The argument checks of the three turn forms (plain; fin: the last turn fused with the
+// finalize; init_state: the first turn fused with the reset).  -> RMI_OK (f = the finalize
+// arguments to launch with), kSkip, or the error.
+int validate_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in, const rmi_finalize_t* fin,
+                  const uint8_t* init_state, const int8_t* init_player, rmi_finalize_t& f) {
+  if (!env || (init_state && !ep)) return RMI_EINVAL;
+  if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
+  const int rc = check_turn_args(ep, in);
+  if (rc != RMI_OK) return rc > 0 ? kSkip : rc;
+  const int ec = sokoban_check(env);
+  if (ec != RMI_OK) return ec;
+  f = rmi_finalize_t{};
+  if (fin) {
+    if (fin->method < 0 || fin->method > 3 || fin->group_size < 1) return RMI_EINVAL;
+    // every group inside one wave (64 envs, or 16 when 4 lanes share an env), and no partial group
+    const int per_wave = spread_lanes(ep->B) ? kWave / kSpreadLpe : kWave;
+    if (per_wave % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;
+    f = *fin;
+    if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member
+  }
+  if (init_state) {
+    if (!init_player) return RMI_EINVAL;
+    if (reinterpret_cast<uintptr_t>(init_state) & 3u) return RMI_EUNSUP;
+  }
+  return RMI_OK;
+}
+}  // namespace
+}  // namespace rmi
+
 RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                   uint8_t* err, rmi_stream_t stream) {
   using namespace rmi;
-  if (!env) return RMI_EINVAL;
-  if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
-  const int rc = check_turn_args(ep, in);
-  if (rc != RMI_OK) return rc > 0 ? RMI_OK : rc;
-  const int ec = sokoban_check(env);
-  if (ec != RMI_OK) return ec;
-  return sokoban_step_turn_launch<false>(env, ep, in, err, rmi_finalize_t{}, as_stream(stream));
+  rmi_finalize_t f;
+  const int rc = validate_turn(env, ep, in, nullptr, nullptr, nullptr, f);
+  if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
+  return sokoban_step_turn_launch<false>(env, ep, in, err, f, as_stream(stream));
 }
 
 RMI_API int rmi_sokoban_step_turn_finalize(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                                            uint8_t* err, const rmi_finalize_t* fin, rmi_stream_t stream) {
   using namespace rmi;
-  if (!env || !fin) return RMI_EINVAL;
-  if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
-  const int rc = check_turn_args(ep, in);
-  if (rc < 0) return rc;
-  if (ep->B == 0) return RMI_OK;
-  const int ec = sokoban_check(env);
-  if (ec != RMI_OK) return ec;
-  if (fin->method < 0 || fin->method > 3 || fin->group_size < 1) return RMI_EINVAL;
-  if (!ep->turn_reward || !ep->turn_info || !ep->penalty || !ep->flags || !ep->n_turns || !ep->num_actions)
-    return RMI_EINVAL;
-  // every group inside one wave (64 envs, or 16 when 4 lanes share an env), and no partial group
-  const int per_wave = spread_lanes(ep->B) ? kWave / kSpreadLpe : kWave;
-  if (per_wave % fin->group_size != 0 || ep->B % fin->group_size != 0) return RMI_EUNSUP;
-  rmi_finalize_t f = *fin;
-  if (f.group_size == 1) f.method = RMI_NORM_IDENTITY;  // ctx_manager.py:220: no group with > 1 member
+  if (!fin) return RMI_EINVAL;
+  rmi_finalize_t f;
+  const int rc = validate_turn(env, ep, in, fin, nullptr, nullptr, f);
+  if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
   return sokoban_step_turn_launch<true>(env, ep, in, err, f, as_stream(stream));
 }
 
@@ -934,20 +1065,46 @@ RMI_API int rmi_sokoban_step_turn_first(const rmi_sokoban_t* env, const rmi_epis
                                         const uint8_t* init_state, const int8_t* init_player, uint8_t* err,
                                         rmi_stream_t stream) {
   using namespace rmi;
-  if (!env || !ep) return RMI_EINVAL;
-  if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
-  const int rc = check_turn_args(ep, in);
-  if (rc < 0) return rc;
-  if (ep->B == 0) return RMI_OK;
-  const int ec = sokoban_check(env);
-  if (ec != RMI_OK) return ec;
-  if (!init_state || !init_player || !ep->num_actions || !ep->flags || !ep->n_turns || !ep->penalty ||
-      !ep->turn_reward || !ep->turn_info || !ep->turn_exec || ep->T <= 0)
-    return RMI_EINVAL;
-  if (in->turn < 0 || in->turn >= ep->T) return RMI_EINVAL;
-  if (reinterpret_cast<uintptr_t>(init_state) & 3u) return RMI_EUNSUP;
-  return sokoban_step_turn_launch<false, true>(env, ep, in, err, rmi_finalize_t{}, as_stream(stream), init_state,
-                                               init_player);
+  if (!init_state || !init_player) return RMI_EINVAL;
+  rmi_finalize_t f;
+  const int rc = validate_turn(env, ep, in, nullptr, init_state, init_player, f);
+  if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
+  return sokoban_step_turn_launch<false, true>(env, ep, in, err, f, as_stream(stream), init_state, init_player);
+}
+
+RMI_API int rmi_sokoban_step_turn_render(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                         uint8_t* err, const rmi_finalize_t* fin, const uint8_t* init_state,
+                                         const int8_t* init_player, const rmi_render_t* obs, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!obs || (fin && init_state) || (!init_state) != (!init_player)) return RMI_EINVAL;
+  if (!env || env->H <= 0 || env->W <= 0) return RMI_EINVAL;
+  for (int k = 0; k < 16; ++k)
+    if (obs->glyph_len[k] > 4) return RMI_EINVAL;
+  if (obs->stride < env->H * env->W * 4 + env->H - 1 || obs->stride % 4) return RMI_EINVAL;
+  rmi_finalize_t f;
+  const int rc = validate_turn(env, ep, in, fin, init_state, init_player, f);
+  if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
+  if (!obs->out || !obs->len || (reinterpret_cast<uintptr_t>(obs->out) & 3u)) return RMI_EINVAL;
+  ObsOut o;
+  o.glen = 0;
+  for (int k = 0; k < 16; ++k) {  // absent glyphs render '?' (as rmi_sokoban_render)
+    o.gb[k] = obs->glyph_len[k] ? obs->glyph_bytes[k] : (uint32_t)'?';
+    o.glen |= (uint64_t)(obs->glyph_len[k] ? obs->glyph_len[k] : 1) << (4 * k);
+  }
+  o.out = obs->out;
+  o.len = obs->len;
+  o.stride = obs->stride;
+  hipStream_t s = as_stream(stream);
+  int lc = fin ? sokoban_step_turn_obs_launch<true, false>(env, ep, in, err, f, s, nullptr, nullptr, o)
+           : init_state ? sokoban_step_turn_obs_launch<false, true>(env, ep, in, err, f, s, init_state, init_player, o)
+                        : sokoban_step_turn_obs_launch<false, false>(env, ep, in, err, f, s, nullptr, nullptr, o);
+  if (lc != RMI_EUNSUP) return lc;
+  // another layout: the turn, then the render
+  lc = fin ? sokoban_step_turn_launch<true>(env, ep, in, err, f, s)
+       : init_state ? sokoban_step_turn_launch<false, true>(env, ep, in, err, f, s, init_state, init_player)
+                    : sokoban_step_turn_launch<false>(env, ep, in, err, f, s);
+  if (lc != RMI_OK) return lc;
+  return rmi_sokoban_render(env, ep->B, obs->glyph_bytes, obs->glyph_len, obs->out, obs->stride, obs->len, stream);
 }
 
 RMI_API int rmi_sokoban_reset(const rmi_sokoban_t* env, const rmi_episode_t* ep, const uint8_t* init_state,

@@ -9,6 +9,9 @@
 //                     build, and the update-batch marks of the rows that took part
 //  rmi_rows_stats     DevicePrompts.gen_batch: the longest arena row among the batch rows and
 //                     whether any row waits for the host, as two ints read back together
+//  rmi_next_rows_stats  the same over the envs that go on after a turn (a generation this turn,
+//                     not done), launched by the turn itself after the next prompt's encode, so
+//                     the turn's one readback carries them (no readback of its own)
 //
 // Each replaced 3-8 torch elementwise / reduction launches; in a kernel trace of the API rollout
 // (profiles/r04_api_timeline.txt) the turn loop's GPU sat idle between small launches for most
@@ -104,6 +107,37 @@ __global__ __launch_bounds__(kRedBlock) void rows_stats_kernel(const int32_t* __
   }
 }
 
+__global__ __launch_bounds__(kRedBlock) void next_rows_stats_kernel(const int32_t* __restrict__ len,
+                                                                    const uint8_t* __restrict__ has,
+                                                                    const uint8_t* __restrict__ flags,
+                                                                    const uint8_t* __restrict__ bad, int64_t B,
+                                                                    int32_t* __restrict__ stats) {
+  __shared__ int red[kRedBlock / 64];
+  int m = 0, any = 0, cnt = 0;
+  for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
+    const bool next = (has ? has[e] != 0 : true) && !(flags[e] & RMI_FLAG_DONE);
+    if (next) {
+      m = max(m, len[e]);
+      ++cnt;
+    }
+    if (bad) any |= bad[e];
+  }
+  m = block_max(m, red);
+  any = block_max(any != 0 ? 1 : 0, red);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int c = 0;
+#pragma unroll
+    for (int w = 0; w < kRedBlock / 64; ++w) c += red[w];
+    stats[0] = m;
+    stats[1] = any;
+    stats[2] = c;
+  }
+}
+
 inline unsigned glue_grid(int64_t B) {
   const int64_t g = (B + kGlueBlock - 1) / kGlueBlock;
   return (unsigned)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
@@ -154,6 +188,16 @@ RMI_API int rmi_rows_stats(const int32_t* len, const int64_t* rows, int64_t n_ro
   if (n_rows < 0 || B < 0 || !stats || (n_rows > 0 && !len)) return RMI_EINVAL;
   if (reinterpret_cast<uintptr_t>(stats) & 3u) return RMI_EINVAL;
   hipLaunchKernelGGL(rows_stats_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, rows, n_rows, bad, B,
+                     stats);
+  return launch_status();
+}
+
+RMI_API int rmi_next_rows_stats(const int32_t* len, const uint8_t* has, const uint8_t* flags, const uint8_t* bad,
+                                int64_t B, int32_t* stats, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || !stats || (B > 0 && (!len || !flags))) return RMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(stats) & 3u) return RMI_EINVAL;
+  hipLaunchKernelGGL(next_rows_stats_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, has, flags, bad, B,
                      stats);
   return launch_status();
 }

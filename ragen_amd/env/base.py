@@ -31,6 +31,7 @@ class BatchEnv:
         self.seeds = np.zeros(self.B, np.int64)
         self._host = None  # lazily synced host mirror (env-specific use)
         self._text = None  # this turn's observations, rendered on the device for every env at once
+        self._rows = None
 
     # --- API ----------------------------------------------------------------------
     def reset(self, seeds) -> None:
@@ -110,11 +111,13 @@ class BatchEnv:
     def close(self):
         self._host = None
         self._text = None
+        self._rows = None
 
     # --- helpers ------------------------------------------------------------------
     def _invalidate(self):
         self._host = None
         self._text = None
+        self._rows = None  # device rows of a fused turn + render (SokobanBatch)
 
     def expand_seeds(self, base_seed: int, group_size: int, first_group: int = 0) -> np.ndarray:
         """es_manager.py:80-82: env i of the batch gets base + (global group index)."""

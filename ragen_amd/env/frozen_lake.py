@@ -120,6 +120,13 @@ class FrozenLakeBatch(BatchEnv):
         """FrozenLakeEnv.render text mode (frozen_lake/env.py:47-61) of every env on the device."""
         return torch.ops.ragen_amd.frozenlake_render(self.desc, self.s, self.nrow, self.ncol, *self.glyph_lists())
 
+    def obs_bound(self) -> int:
+        """The longest render row (bytes): one player cell (codes 0 / 4 / 5), the other cells
+        floor / hole / goal (1 / 2 / 3), plus the newlines."""
+        g = self.config.grid_lookup or {}
+        L = [len(str(g.get(c, "?")).encode("utf-8")) for c in range(6)]
+        return (self.nrow * self.ncol - 1) * max(L[1], L[2], L[3]) + max(L) + self.nrow - 1
+
     def render_all(self):
         if self._text is None:
             self._text = ops.decode_rows(*self.render_rows())

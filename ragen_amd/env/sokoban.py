@@ -85,7 +85,21 @@ class SokobanBatch(BatchEnv):
         torch.ops.ragen_amd.sokoban_reset(*self.state_args(), self.init_state, self.init_player, *self.dims())
         self._invalidate()
 
-    def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None, **kw):
+    # step_turn(render=True) renders every env's next observation in the same launch
+    # (rmi_sokoban_step_turn_render); render_rows() then returns those rows without a launch
+    fused_render = True
+
+    def step_turn(self, turn, actions, n_actions, has_input, max_actions_per_traj, format_penalty, err=None,
+                  render=False, **kw):
+        if render and self.dispatch != "ctypes":
+            H, W = self.H, self.W
+            rows = ops.render_buffers(self.B, H, W, self.device)  # fresh: turn records keep each turn's rows
+            direct.sokoban_step_turn_render(*self.state_args(), actions, n_actions, has_input, err, *rows,
+                                            *self.glyph_lists(), int(turn), int(max_actions_per_traj),
+                                            float(format_penalty), *self.dims())
+            self._invalidate()
+            self._rows = rows
+            return
         if self.dispatch == "ctypes":
             ops._dev(self.room_state, actions, n_actions, has_input, err)
             ops.sokoban_step_turn(self.struct(), self.ep, ops.turn_struct(int(turn), actions, n_actions, has_input,
@@ -98,9 +112,23 @@ class SokobanBatch(BatchEnv):
 
     def render_rows(self):
         """SokobanEnv.render text mode (sokoban/env.py:53-61) of every env on the device:
-        -> (UTF-8 rows u8[B, stride], lengths i32[B])."""
+        -> (UTF-8 rows u8[B, stride], lengths i32[B]) -- the rows the last step_turn(render=True)
+        wrote, while the state has not changed since."""
+        rows = self.__dict__.get("_rows")
+        if rows is not None:
+            return rows
         return direct.sokoban_render(self.room_fixed, self.room_state, self.H, self.W,
                                                   *self.glyph_lists())
+
+    def obs_bound(self) -> int:
+        """The longest render row (bytes) of a room with this config's box count: every cell a
+        wall / floor / target glyph but the boxes' and the player's, plus the newlines (a
+        hand-made room past it is built on the host by the device prompt path)."""
+        g = self.config.grid_lookup or {}
+        L = [len(str(g.get(c, "?")).encode("utf-8")) for c in range(7)]
+        nb = max(0, min(int(self.config.num_boxes), self.H * self.W - 1))
+        base = max(L[0], L[1], L[2])
+        return (self.H * self.W - nb - 1) * base + nb * max(base, L[3], L[4]) + max(base, L[5], L[6]) + self.H - 1
 
     def render_all(self):
         if self._text is None:

@@ -105,9 +105,12 @@ class LLMAgentProxy:
         ctx = self.val_ctx_manager if val else self.train_ctx_manager
         if hasattr(self.actor_wg, "turn"):
             self.actor_wg.turn = 0
+        from ..ops import D2H_COUNT  # device -> host readbacks of the device path, per phase
+        c0 = D2H_COUNT[0]
         t0 = time.perf_counter()
         env_outputs: List[Dict] = es.reset()
         t1 = time.perf_counter()
+        c1 = D2H_COUNT[0]
         for _ in range(self.config.agent_proxy.max_turn):
             lm_inputs = ctx.get_lm_inputs(env_outputs, prepare_for_update=False)
             lm_inputs.meta_info = dataproto.meta_info
@@ -117,6 +120,7 @@ class LLMAgentProxy:
             if len(env_outputs) == 0:
                 break
         t2 = time.perf_counter()
+        c2 = D2H_COUNT[0]
         rollout_states = es.get_rollout_states()
         t3 = time.perf_counter()
         out = ctx.formulate_rollouts(rollout_states)
@@ -126,5 +130,6 @@ class LLMAgentProxy:
             out = rd.gather_formulated(out, pad, self.process_group, sizes=ctx.shard_sizes())
         # phase wall times of the last call (the turn loop is what env-steps/s is measured on)
         self.last_timing = {"reset_s": t1 - t0, "turns_s": t2 - t1, "rollout_states_s": t3 - t2,
-                            "formulate_s": time.perf_counter() - t3}
+                            "formulate_s": time.perf_counter() - t3,
+                            "readbacks": {"reset": c1 - c0, "turns": c2 - c1, "after": D2H_COUNT[0] - c2}}
         return out

@@ -100,6 +100,11 @@ SPECIAL_TOKENS = ["<think>", "</think>", "<answer>", "</answer>", "<|im_start|>"
 PARSE_MAX_ROW = 8192  # rmi_parse_actions' row limit (bytes of a decoded generation)
 
 
+def decode_stride(raw: int, factor: int) -> int:
+    """The decode's row (bytes): factor x raw, whole dwords, within the parse's row limit."""
+    return max(4, min(PARSE_MAX_ROW, (factor * int(raw) + 7) // 4 * 4))
+
+
 def parse_response(response: str, enable_think: bool, action_sep: str, max_actions_per_turn: int):
     """ContextManager._parse_response (ctx_manager.py:148-173) as a function of the agent_proxy
     settings: -> (llm_response, actions).  The device path (rmi_parse_actions) computes the
@@ -206,6 +211,8 @@ class DeviceEnvInputs:
         # has_t: u8[n_envs] 1 for the envs with a generation (device), None = every env in order
         self.ctx, self.env_ids, self.has_t = ctx, env_ids, has_t
         self.ids, self.n_ids, self.stride = ids, n_ids, stride
+        self.raw_max = None  # host int: the longest generation's raw bytes, when known
+        self.raw_dev = None  # the same on the device (i32[1], rmi_gen_rows)
         self.vocab = ctx.device_vocab
         self._text = self._text_len = self._err = None
         self._decoded = None
@@ -389,6 +396,8 @@ class ContextManager:
         self.env_lo = g0 * int(self.es_cfg.group_size)
         self.n_envs = ng * int(self.es_cfg.group_size)  # this shard's envs (all of them unsharded)
         self.device_vocab = None
+        self._raw_hint = None      # decode row hint (raw bytes), note_raw
+        self._raw_hint_pin = None  # (tests) a fixed hint for every turn
         self.device_prompts = True  # build prompt ids on the device when the device path is on
         self._es = None
         self._prompts = None
@@ -438,8 +447,10 @@ class ContextManager:
         return self._prompts
 
     def _sync_prompts(self, pr):
-        """Bring the prompt arena up to the env manager's turns."""
+        """Bring the prompt arena up to the env manager's turns (and let the env manager's device
+        turns append the next prompt themselves, DevicePrompts.advance_eager)."""
         es = self._es
+        es._prompt_hook = pr if not pr.window else None
         if pr.rollout != es.rollout_id:
             pr.start()
         for d in es._turn_records[pr.turns_done:]:
@@ -705,12 +716,32 @@ class ContextManager:
             n_ids = torch.empty(n, dtype=torch.int32, device=dev)
             has_t = torch.empty(n, dtype=torch.uint8, device=dev)  # 1: the env has a generation
             direct.gen_rows(resp, ops.h2d(src, dev), n, vocab.packed, ids, n_ids, raw, has_t)
-        # the decoded rows' width: the longest row's raw bytes (x3 for U+FFFD replacements of
-        # invalid UTF-8), within the parse kernel's row limit; a longer generation is flagged by
-        # the decode and refused by the step (ValueError)
-        raw_max = int(ops.d2h(raw, self)[0]) if resp.numel() else 0
-        stride = max(4, min(PARSE_MAX_ROW, (3 * raw_max + 7) // 4 * 4))
-        return DeviceEnvInputs(self, env_ids, has_t, ids, n_ids, stride)
+        # the decoded rows' width.  With a hint from the turns before (the longest generation
+        # seen, with a margin) no readback: a longer generation overflows the decode's row, is
+        # masked out of the turn's first pass and stepped by a second pass sized from the
+        # lengths the turn reads back (EnvStateManager._step_device).  Without one (a manager's
+        # first turn): the longest row's raw bytes read back now (x3 for U+FFFD replacements of
+        # invalid UTF-8).  Either way within the parse kernel's row limit; a generation past it
+        # is flagged by the decode and refused by the step (ValueError).
+        hint = self._raw_hint_pin if self._raw_hint_pin is not None else self._raw_hint
+        if hint is None or not resp.numel():
+            raw_max = int(ops.d2h(raw, self)[0]) if resp.numel() else 0
+            stride = decode_stride(raw_max, 3)
+            self.note_raw(raw_max)
+        else:
+            raw_max = None
+            stride = decode_stride(hint, 1)
+        inp = DeviceEnvInputs(self, env_ids, has_t, ids, n_ids, stride)
+        inp.raw_max = raw_max  # the decoded rows' length bound (longer only with U+FFFD replacements)
+        inp.raw_dev = raw      # i32[1] on the device: the longest row's raw bytes (read back with the turn)
+        return inp
+
+    RAW_HINT_MARGIN = 1.25  # the decode's row over the longest generation seen
+
+    def note_raw(self, raw_max: int):
+        """A turn's longest generation (raw bytes, read back) -> the next turns' decode hint."""
+        h = int(raw_max * self.RAW_HINT_MARGIN) + 64
+        self._raw_hint = h if self._raw_hint is None else max(self._raw_hint, h)
 
     def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:
         """ctx_manager.py:354-356.  The rollout states of the attached env manager's device path

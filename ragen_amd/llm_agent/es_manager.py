@@ -210,6 +210,9 @@ class EnvStateManager:
         self._turn = 0
         self._all_active = False
         self.reset_render = None
+        # the device prompt builder whose next prompt a device turn appends before its readback
+        # (prompts.DevicePrompts.advance_eager; set by the ContextManager), or None
+        self._prompt_hook = None
         self._turn_records = []  # device-path turns (ContextManager's device prompts read them too)
         self._max_act = None  # i32[n_envs] max_actions_per_traj per env (device turn), built once
         self._mat_upto = 0       # records whose host bookkeeping is done
@@ -504,7 +507,7 @@ class EnvStateManager:
 
     def step_text(self, text: torch.Tensor, text_len: torch.Tensor, has_input: Optional[torch.Tensor] = None,
                   enable_think: bool = True, action_sep: str = "||", prepend: bool = True,
-                  err: Optional[torch.Tensor] = None):
+                  err: Optional[torch.Tensor] = None, render: bool = False):
         """Device-resident turn from response text (§8(f) rank 2): rows are this shard's envs in
         env-id order, text u8[n_envs, stride] / text_len i32[n_envs] the decoded generations
         (e.g. ops.detokenize of the response ids).  Per tag one parse launch
@@ -524,7 +527,7 @@ class EnvStateManager:
                 cfg, text[a:z], text_len[a:z], sel, True, int(lact))
             outs.append({"actions": acts, "n_actions": n_act, "spans": spans, "action_text": at if lact else None,
                          "action_len": al if lact else None, "err": perr})
-        self._parsed_turn(outs, has_input, err)
+        self._parsed_turn(outs, has_input, err, render)
         return outs
 
     def _parse_args(self, tg, enable_think, action_sep, prepend):
@@ -538,8 +541,10 @@ class EnvStateManager:
         words, lact = cache[key]
         return words, tg.batch.parse_sel(), lact
 
-    def _parsed_turn(self, parsed, has_input, err):
-        """One turn launch per tag from the tag's parse outputs (ops.parse_actions dicts)."""
+    def _parsed_turn(self, parsed, has_input, err, render=False):
+        """One turn launch per tag from the tag's parse outputs (ops.parse_actions dicts); with
+        ``render`` a batch that can renders its next observations in the same launch
+        (SokobanBatch.fused_render: render_rows() then reads them)."""
         self._all_active = False  # _step_device sets it again from the turn's active set
         lo0 = self.env_lo
         for tg, p in zip(self.tags, parsed):
@@ -548,6 +553,8 @@ class EnvStateManager:
             kw = {}
             if p["action_text"] is not None:
                 kw = {"answers": p["action_text"], "answer_len": p["action_len"]}
+            if render and getattr(tg.batch, "fused_render", False):
+                kw["render"] = True
             tg.batch.step_turn(self._turn, p["actions"], p["n_actions"], has, tg.max_actions_per_traj,
                                self.format_penalty, None if err is None else err[a:z], **kw)
         self._turn += 1
@@ -580,51 +587,49 @@ class EnvStateManager:
         the next observation rendered on the device, the active set read back.  The host
         bookkeeping (EnvStatus, history dicts, penalties) is deferred to ``_materialize``; the
         turn's record (inputs, spans, observation, flags, actions left) is kept for it and for
-        the device prompt path (prompts.DevicePrompts.advance)."""
+        the device prompt path (prompts.DevicePrompts.advance).  ONE readback per turn: the
+        decode's row size comes from a hint (ContextManager._device_env_inputs), and a
+        generation longer than it is masked out of this pass and stepped by a second pass over
+        those envs, sized from the lengths the first pass read back (rare: the hint keeps a
+        margin over every length seen)."""
         if self._turn >= self.max_turn:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
-        dev = self.device
-        ap = self.sys_config.agent_proxy
-        # decode + parse in one launch per tag unless the rows were decoded already
-        parsed = None if inp.is_decoded else self._decode_parse(inp, bool(ap.enable_think), ap.action_sep)
-        # a generation the device decode truncated (row stride cap) or could not decode (an id
-        # outside the vocabulary) is not stepped on: masked out of the turn on the device and
-        # raised after it, from the turn's one readback (no host synchronisation before the turn)
-        # the envs with a generation (all of them, or has_t written by rmi_gen_rows) minus the
-        # undecodable ones, and the zeroed step-error bytes: one launch (rmi_turn_inputs)
-        has = torch.empty(self.n_envs, dtype=torch.uint8, device=dev)
-        err = torch.empty(self.n_envs, dtype=torch.uint8, device=dev)
-        ops.turn_inputs(inp.has_t, inp.err, has, err)
-        if parsed is None:
-            parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err)
-        else:
-            self._parsed_turn(parsed, has, err)
-        obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
         n = self.n_envs
-        flags = self._cat([tg.batch.ep.flags for tg in self.tags])
-        num_actions = self._cat([tg.batch.ep.num_actions for tg in self.tags])
-        obs_len = self._cat([obs[j][1] for j in sorted(obs)]) if len(obs) == len(self.tags) else None
-        if self._max_act is None:  # per-env max_actions_per_traj (the "actions left" base)
-            self._max_act = torch.tensor(np.concatenate([np.full(tg.hi - tg.lo, tg.max_actions_per_traj, np.int32)
-                                                         for tg in self.tags]), device=dev)
-        flags_copy = torch.empty(n, dtype=torch.uint8, device=dev)
-        left = torch.empty(n, dtype=torch.int32, device=dev)
-        pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
-        # the record's flags and actions-left columns, and the one packed readback: flags, step
-        # and decode errors, the longest decoded response and observation (rmi_turn_readback)
-        ops.turn_readback(flags, err, inp.err, num_actions, self._max_act, inp.text_len, obs_len, flags_copy, left,
-                          pack)
+        rec, pack, hook, eager = self._device_pass(inp, t, None)
         # one device -> host copy (pinned, then the stream waited on): the active set and the
         # turn's per-env error bits, raised in the step where they happen, as the reference
         # raises inside its per-env loop
         host = ops.d2h(pack, self)
-        tmax, omax = (int(x) for x in host[-8:].view(np.int32))
-        self._turn_records.append({"turn": t, "inp": inp, "has": has, "err": err, "obs": obs,
-                                   "spans": [p["spans"] for p in parsed], "flags": flags_copy, "left": left,
-                                   "text_max": tmax, "obs_max": omax if obs_len is not None else None})
+        o = (3 * n + 3) & ~3
+        tail = host[o:o + 24].view(np.int32)  # max text / obs, the next batch's stats, raw max
+        if inp.raw_max is None:
+            inp.ctx.note_raw(int(tail[5]))
+        err_h = host[n:2 * n].copy()
+        dec_h = host[2 * n:3 * n]
+        over = ((dec_h & _lib.ERR_UNSUP) != 0) & ((dec_h & _lib.ERR_INDEX) == 0)
+        if over.any() and inp.raw_max is None and not (dec_h & _lib.ERR_INDEX).any():
+            # the second pass: every row decoded again at the size the lengths ask for (the
+            # rows of the first pass decode and parse the same), only the overflowed envs step
+            from .ctx_manager import decode_stride
+            raw = int(tail[5])
+            over_t = ops.h2d(over.astype(np.uint8), self.device)
+            inp2 = type(inp)(inp.ctx, inp.env_ids, over_t, inp.ids, inp.n_ids, decode_stride(raw, 3))
+            inp2.raw_max, inp2.raw_dev = raw, inp.raw_dev
+            self._turn = t
+            rec2, pack2, hook, eager2 = self._device_pass(inp2, t, rec)
+            host = ops.d2h(pack2, self)
+            tail = host[o:o + 24].view(np.int32)
+            err_h |= host[n:2 * n]
+            dec_h = host[2 * n:3 * n]
+            eager = eager and eager2
+            rec = rec2
+        rec["text_max"], rec["obs_max"] = int(tail[0]), (int(tail[1]) if rec.pop("_obs_known") else None)
+        if eager:
+            hook.set_next_stats(t, tail[2:5])
+        self._turn_records.append(rec)
         n_in = len(inp.env_ids)
-        fl_h, err_h, dec_h = host[:n], host[n:2 * n], host[2 * n:3 * n]
+        fl_h = host[:n]
         if dec_h.any():
             bad = int(np.nonzero(dec_h)[0][0])
             raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
@@ -638,6 +643,63 @@ class EnvStateManager:
                                    gids)
             self._turn_records[-1]["err_seen"] = True
         return LazyEnvOutputs(self, inp.env_ids[still])
+
+    def _device_pass(self, inp, t, first):
+        """The device launches of one pass of turn t over the envs with a generation in ``inp``
+        (all of them, or inp.has_t) that decode: decode + parse, the turn with its render, the
+        record's columns and the packed readback buffer (rmi_turn_readback, then the next
+        prompt's append and the next batch's stats, DevicePrompts.advance_eager).  ``first``:
+        the record of the turn's first pass when this is its second (the overflowed envs):
+        the record returned then covers both.  -> (record, readback buffer, prompt hook,
+        whether the hook appended)."""
+        dev = self.device
+        n = self.n_envs
+        ap = self.sys_config.agent_proxy
+        # decode + parse in one launch per tag unless the rows were decoded already
+        parsed = None if inp.is_decoded else self._decode_parse(inp, bool(ap.enable_think), ap.action_sep)
+        # a generation the device decode truncated (row stride) or could not decode (an id
+        # outside the vocabulary) is not stepped on: masked out of the turn on the device and
+        # handled after it, from the turn's readback (no host synchronisation before the turn)
+        # the envs with a generation (all of them, or has_t written by rmi_gen_rows) minus the
+        # undecodable ones, and the zeroed step-error bytes: one launch (rmi_turn_inputs)
+        has = torch.empty(n, dtype=torch.uint8, device=dev)
+        err = torch.empty(n, dtype=torch.uint8, device=dev)
+        ops.turn_inputs(inp.has_t, inp.err, has, err)
+        if parsed is None:
+            parsed = self.step_text(inp.text, inp.text_len, has, bool(ap.enable_think), ap.action_sep, True, err=err,
+                                    render=True)
+        else:
+            self._parsed_turn(parsed, has, err, render=True)
+        obs = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags) if type(tg.batch).render is BatchEnv.render}
+        flags = self._cat([tg.batch.ep.flags for tg in self.tags])
+        num_actions = self._cat([tg.batch.ep.num_actions for tg in self.tags])
+        obs_len = self._cat([obs[j][1] for j in sorted(obs)]) if len(obs) == len(self.tags) else None
+        if self._max_act is None:  # per-env max_actions_per_traj (the "actions left" base)
+            self._max_act = torch.tensor(np.concatenate([np.full(tg.hi - tg.lo, tg.max_actions_per_traj, np.int32)
+                                                         for tg in self.tags]), device=dev)
+        flags_copy = torch.empty(n, dtype=torch.uint8, device=dev)
+        left = torch.empty(n, dtype=torch.int32, device=dev)
+        pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
+        # the record's flags and actions-left columns, and the one packed readback: flags, step
+        # and decode errors, the longest decoded response and observation (rmi_turn_readback)
+        ops.turn_readback(flags, err, inp.err, num_actions, self._max_act, inp.text_len, obs_len, flags_copy, left,
+                          pack)
+        if inp.raw_max is None:  # the longest generation's raw bytes ride along (the next hint)
+            ops.readback_raw(pack, n).copy_(inp.raw_dev)
+        rec = {"turn": t, "inp": inp, "has": has, "err": err, "obs": obs, "spans": [p["spans"] for p in parsed],
+               "flags": flags_copy, "left": left, "_obs_known": obs_len is not None}
+        has_next = has
+        if first is not None:  # the second pass: this pass's envs and the first's
+            has_next = has | first["has"]
+        # with device prompts the next prompt's text and ids are appended by this turn's own
+        # launches, and the next generation batch's row stats land in the readback buffer
+        # (DevicePrompts.advance_eager): the turn's one readback serves the prompt batch too
+        hook = self._prompt_hook
+        eager = hook is not None and hook.advance_eager(rec, ops.readback_stats(pack, n), has_next=has_next,
+                                                        again=first is not None)
+        if first is not None:
+            rec["has"], rec["err"] = has_next, err | first["err"]
+        return rec, pack, hook, eager
 
     @_gc_paused
     def _materialize(self):

@@ -258,6 +258,9 @@ class DevicePrompts:
         self.tail = torch.tensor(tail, dtype=torch.int64, device=self.device)
         self.host_rows_used = 0
         self._pending = None  # (bad rows u8/bool[B] on the device, their host builder), not read back yet
+        self._next_stats = None  # (turns done, longest row, any host row, rows) of advance_eager
+        self.eager_turns = 0     # turns appended by advance_eager (the rest at get_lm_inputs)
+        self._reset_obs_max = 0
         self.rollout = None
         self.turns_done = 0
         self._verify()
@@ -426,6 +429,7 @@ class DevicePrompts:
         self.rollout = es.rollout_id
         self.turns_done = 0
         self._pending = None  # a previous rollout's unread host rows: its arena is rebuilt now
+        self._next_stats = None
         # the reset text of the tags without a device render, as host rows (the others' rows stay
         # empty: their observation comes from render_rows)
         host_tags = [tg for tg in es.tags if not hasattr(tg.batch, "render_rows")]
@@ -437,6 +441,7 @@ class DevicePrompts:
                 rows.append((tg.lo - es.env_lo + i, b))
                 lens[tg.lo - es.env_lo + i] = len(b)
         st = max(4, (int(lens.max()) + 3) // 4 * 4)
+        self._reset_obs_max = int(lens.max()) if lens.size else 0
         buf = np.zeros((self.n_envs, st), np.uint8)
         for e, b in rows:
             buf[e, :len(b)] = np.frombuffer(b, np.uint8)
@@ -464,19 +469,69 @@ class DevicePrompts:
         text, tlen, _, terr = self._run_text(pieces, stride, obs, obs_len, ints, active=active)
         return text, tlen, terr, stride
 
-    def advance(self, d):
-        """Append turn d["turn"] (a device-path turn record of EnvStateManager._step_device)."""
+    def advance(self, d, bounds=None, merge=False):
+        """Append turn d["turn"] (a device-path turn record of EnvStateManager._step_device).
+        bounds: (longest observation, longest response) in bytes when the record does not carry
+        them yet (advance_eager); merge: the rows of a turn's second pass (their host rows join
+        the first pass's, unresolved)."""
         t = d["turn"]
         if self.window:  # window mode: the rows are rebuilt per batch (_build_window)
             self.turns_done = t + 1
             return
-        text, tlen, mark, terr, stride, last, flags, bound = self._turn_text(d, t + 2, d["has"])
+        text, tlen, mark, terr, stride, last, flags, bound = self._turn_text(d, t + 2, d["has"], bounds)
         self._encode(text, tlen, terr, mark, stride,
                      lambda e: self._host_turn(e, t, not last and not int(flags[e]) & _lib.FLAG_DONE),
-                     active=d["has"], bound=bound)
+                     active=d["has"], bound=bound, merge=merge)
         self.turns_done = t + 1
 
-    def _turn_text(self, d, number, active):
+    def advance_eager(self, d, stats, has_next=None, again=False) -> bool:
+        """Turn d's append launched from inside the turn (EnvStateManager._step_device), BEFORE the
+        turn's readback: the row sizes come from host bounds (the longest generation's raw bytes,
+        rmi_gen_rows; each env type's widest render row) instead of the readback's exact maxima
+        (a row past them is flagged by the encoder and built on the host, never mis-encoded),
+        and rmi_next_rows_stats writes the next generation batch's longest row, whether a row
+        waits for the host and the row count into ``stats`` (inside the readback buffer) -- so
+        gen_batch needs no readback of its own.  has_next: the envs that had a generation this
+        turn (default d["has"]); again: d is the turn's second pass (the envs whose generation
+        overflowed the first pass's decode), appended after the first.  -> False when it does
+        not apply (window mode, a stale rollout, unknown bounds): the prompt is then appended at
+        the next get_lm_inputs."""
+        es = self.es
+        t = d["turn"]
+        if self.window or self.rollout != es.rollout_id or self.turns_done != (t + 1 if again else t):
+            return False
+        inp = d["inp"]
+        # a generation's decoded length: at most the decode's row (rows past it were not stepped)
+        resp_max = inp.raw_max if inp.raw_max is not None else inp.stride
+        obs_max = self._obs_bound(d["obs"])
+        if obs_max is None and not again:
+            return False
+        self.advance(d, bounds=(obs_max, resp_max), merge=again)
+        self.eager_turns += 0 if again else 1
+        pend = self._pending[0] if self._pending is not None else None
+        ops.next_rows_stats(self.len, d["has"] if has_next is None else has_next, d["flags"], pend, stats)
+        self._next_stats = None
+        return True
+
+    def set_next_stats(self, turn, vals):
+        """advance_eager's stats as read back with the turn: (turns done, longest row, any host
+        row, row count)."""
+        self._next_stats = (turn + 1, int(vals[0]), int(vals[1]), int(vals[2]))
+
+    def _obs_bound(self, rows_by_tag):
+        """The widest observation row (bytes) this turn's rows can hold, from the host: each
+        rendering tag's bound (its batch's obs_bound), the reset text of the others."""
+        b = self._reset_obs_max
+        for j, tg in enumerate(self.es.tags):
+            if j in rows_by_tag:
+                f = getattr(tg.batch, "obs_bound", None)
+                x = f() if f is not None else None
+                if x is None:
+                    return None
+                b = max(b, int(x))
+        return b
+
+    def _turn_text(self, d, number, active, bounds=None):
         """The text turn d["turn"] appends: the assistant block (its end marked: the update rows
         stop there) and, for an env that goes on, the user block with the reward and the next
         state under the header ``Turn {number}``.  -> (text, len, mark, err, stride, last, flags,
@@ -502,7 +557,8 @@ class DevicePrompts:
         last = t + 1 >= self.max_turn
         text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, None, resp,
                                                 resp_len, spans, None, active, turn=(ne, flags, last))
-        bound = self._text_bound(self._prog_last, d.get("obs_max"), d.get("text_max"))
+        obs_max, resp_max = bounds if bounds is not None else (d.get("obs_max"), d.get("text_max"))
+        bound = self._text_bound(self._prog_last, obs_max, resp_max)
         return text, tlen, mark, terr, stride, last, flags, bound
 
     # ----------------------------------------------------------- max_context_window
@@ -578,12 +634,15 @@ class DevicePrompts:
     def _stride(n):
         return min(3072, (int(n) + 3) // 4 * 4)
 
-    def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None, bound=None):
+    def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None, bound=None, merge=False):
         """Tokenize the rows onto the arena; the rows the device could not build are left for
         the host (``_resolve``), read back with the next readback of the arena lengths.  The
         launch's row size is ``bound`` (the host's, _text_bound) when given, else the longest
-        row read back."""
-        self._resolve()  # an earlier turn's host rows come first in the arena
+        row read back.  merge: other rows of the same turn (its second pass): the pending host
+        rows stay pending and are joined by these."""
+        prev = self._pending if merge else None
+        if not merge:
+            self._resolve()  # an earlier turn's host rows come first in the arena
         if bound is not None:
             mx = min(int(bound), text.shape[1])
         else:
@@ -595,6 +654,8 @@ class DevicePrompts:
         bad = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
         act = None if active is None else (active if active.dtype == torch.uint8 else active.to(torch.uint8))
         ops.prompt_commit(err, terr, act, mark_tok if mark is not None else None, self.len_upd, bad)
+        if prev is not None:
+            bad = bad | prev[0]
         self._pending = (bad, host_fn)
 
     def _resolve(self, any_bad=None):
@@ -669,14 +730,22 @@ class DevicePrompts:
         if not rows.numel():
             self._resolve()
             S = 1
-        else:  # one readback: the longest row and whether any row is the host's (rmi_rows_stats)
-            stats = torch.empty(2, dtype=torch.int32, device=self.device)
-            pend = self._pending[0] if self._pending is not None else None
-            ops.rows_stats(self.len, rows, rows.numel(), pend, stats)
-            mx, any_bad = (int(x) for x in ops.d2h(stats, self))
-            if pend is not None:
+        else:
+            ns, self._next_stats = self._next_stats, None
+            if ns is not None and ns[0] == self.turns_done and ns[3] == rows.numel():
+                # the stats came with the turn's readback (advance_eager): these rows are the
+                # envs that went on, the ones it counted
+                mx, any_bad = ns[1], ns[2]
                 self._resolve(bool(any_bad))
+            else:  # one readback: the longest row and whether any row is the host's (rmi_rows_stats)
+                stats = torch.empty(2, dtype=torch.int32, device=self.device)
+                pend = self._pending[0] if self._pending is not None else None
+                ops.rows_stats(self.len, rows, rows.numel(), pend, stats)
+                mx, any_bad = (int(x) for x in ops.d2h(stats, self))
+                if pend is not None:
+                    self._resolve(bool(any_bad))
             if any_bad:  # host rows were written: the longest row again
+                stats = torch.empty(2, dtype=torch.int32, device=self.device)
                 ops.rows_stats(self.len, rows, rows.numel(), None, stats)
                 mx = int(ops.d2h(stats, self)[0])
             S = mx + self.tail.numel()

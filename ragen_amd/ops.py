@@ -20,25 +20,40 @@ def _ptr(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = torch._C._cuda_getCurrentRawStream  # (device index) -> hipStream_t, no Stream object
+
+
 def _stream(device):
-    """torch's current stream ON THE TENSORS' DEVICE (not on the process's current device)."""
-    return torch.cuda.current_stream(device).cuda_stream
+    """torch's current stream ON THE TENSORS' DEVICE (not on the process's current device), as
+    the raw hipStream_t (torch.cuda.current_stream builds a Stream object: several us a call,
+    and the turn loop passes a stream to a dozen launches per turn)."""
+    idx = device if isinstance(device, int) else device.index
+    return _raw_stream(torch.cuda.current_device() if idx is None else idx)
+
+
+_DEVICES = {}  # device index -> torch.device
 
 
 def _dev(*ts):
     """Validate GPU tensors (contiguous, one device) -> that device (None if all are None)."""
-    dev = None
+    idx = None
     for t in ts:
         if t is not None:
             if not t.is_cuda:
                 raise ValueError("ragen_amd ops take GPU tensors (the engine has no CPU path)")
             if not t.is_contiguous():
                 raise ValueError("ragen_amd ops take contiguous tensors")
-            if dev is None:
-                dev = t.device
-            elif t.device != dev:
-                raise ValueError(f"ragen_amd ops take tensors on one device, got {dev} and {t.device}")
-    return dev
+            i = t.get_device()
+            if idx is None:
+                idx = i
+            elif i != idx:
+                raise ValueError(f"ragen_amd ops take tensors on one device, got cuda:{idx} and cuda:{i}")
+    if idx is None:
+        return None
+    d = _DEVICES.get(idx)
+    if d is None:
+        d = _DEVICES[idx] = torch.device("cuda", idx)
+    return d
 
 
 def _dt(t, dtype, name):
@@ -413,6 +428,46 @@ def decode_rows(out: torch.Tensor, n: torch.Tensor):
 def sokoban_render(env: _lib.Sokoban, B: int, lookup, device, out=None):
     """SokobanEnv.render text of every env (sokoban/env.py:53-61) -> (u8[B,stride], i32[B])."""
     return _render(lib().rmi_sokoban_render, env, B, env.H * env.W, env.H, lookup, device, out)
+
+
+def render_struct(lookup, H: int, W: int, out: torch.Tensor, n: torch.Tensor) -> _lib.Render:
+    """rmi_render_t of a grid_lookup and the (rows u8[B, stride], lengths i32[B]) it fills; the
+    tensors must outlive every launch (or graph replay) that uses the struct."""
+    _dev(out, n)
+    _dt(out, torch.uint8, "out")
+    _dt(n, torch.int32, "len")
+    gb, gl = glyph_table(lookup)
+    r = _lib.Render()
+    for k in range(16):
+        r.glyph_bytes[k], r.glyph_len[k] = int(gb[k]), int(gl[k])
+    r.out, r.stride, r.len = _ptr(out), int(out.shape[1]), _ptr(n)
+    return r
+
+
+def render_buffers(B: int, H: int, W: int, device):
+    """(rows u8[B, stride], lengths i32[B]) for a Sokoban render of H x W rooms."""
+    stride = (H * W * 4 + H - 1 + 3) // 4 * 4
+    return (torch.empty(B, stride, dtype=torch.uint8, device=device),
+            torch.empty(B, dtype=torch.int32, device=device))
+
+
+def sokoban_step_turn_render(env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn, obs: _lib.Render,
+                             err: Optional[torch.Tensor] = None, fin: Optional[_lib.Finalize] = None,
+                             init_state: Optional[torch.Tensor] = None, init_player: Optional[torch.Tensor] = None):
+    """A turn (plain; with fin the rollout's last, fused with its end; with init_state /
+    init_player a fresh episode's first, fused with its reset) and every env's observation after
+    it, rendered by the same launch into obs (rmi_sokoban_step_turn_render)."""
+    _dev(init_state, init_player, err)
+    rc = lib().rmi_sokoban_step_turn_render(env, ep.struct(), turn, _ptr(err), fin, _ptr(init_state),
+                                            _ptr(init_player), obs, _stream(ep.device))
+    if rc == _lib.RMI_EUNSUP and fin is not None and fin.group_size >= 1 and ep.B % fin.group_size == 0:
+        # groups that would straddle a wave: the turn with its render, then the finalize
+        sokoban_step_turn_render(env, ep, turn, obs, err)
+        seg = torch.arange(0, ep.B + 1, fin.group_size, dtype=torch.int32, device=ep.flags.device)
+        check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, fin.method, fin.metrics,
+                                         fin.score, fin.pen, fin.norm, _stream(ep.device)), "rmi_rollout_finalize")
+        return
+    check(rc, "rmi_sokoban_step_turn_render")
 
 
 def frozenlake_render(env: _lib.FrozenLake, B: int, lookup, device, out=None):
@@ -816,6 +871,9 @@ def h2d(a: np.ndarray, device) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a)).pin_memory().to(device, non_blocking=True)
 
 
+D2H_COUNT = [0]  # readbacks through d2h so far (the bench reports them per rollout)
+
+
 def d2h(t: torch.Tensor, owner) -> np.ndarray:
     """A small device tensor -> a host numpy copy, through a pinned buffer kept on ``owner``
     (an async copy, then the stream waited on): a pageable ``.cpu()`` stages through the
@@ -827,7 +885,8 @@ def d2h(t: torch.Tensor, owner) -> np.ndarray:
         owner._pin_buf = buf
     dst = buf[:nbytes].view(t.dtype)
     dst.copy_(t.reshape(-1), non_blocking=True)
-    torch.cuda.current_stream(t.device).synchronize()
+    D2H_COUNT[0] += 1
+    check(lib().rmi_stream_synchronize(_stream(t.device)), "rmi_stream_synchronize")
     return dst.numpy().copy()
 
 
@@ -843,8 +902,22 @@ def turn_inputs(has_t: Optional[torch.Tensor], dec_err: torch.Tensor, has: torch
 
 
 def readback_bytes(B: int) -> int:
-    """The size of rmi_turn_readback's packed buffer for B envs."""
-    return ((3 * B + 3) & ~3) + 8
+    """The size of the turn's packed readback buffer for B envs: rmi_turn_readback's (flags |
+    err | dec_err | max text_len, max obs_len), then room for rmi_next_rows_stats' three ints
+    (readback_stats) and the longest generation's raw bytes (readback_raw)."""
+    return ((3 * B + 3) & ~3) + 8 + 16
+
+
+def readback_stats(pack: torch.Tensor, B: int) -> torch.Tensor:
+    """The i32[3] of the packed readback buffer that rmi_next_rows_stats writes."""
+    o = ((3 * B + 3) & ~3) + 8
+    return pack[o:o + 12].view(torch.int32)
+
+
+def readback_raw(pack: torch.Tensor, B: int) -> torch.Tensor:
+    """The i32[1] of the packed readback buffer that carries the turn's longest generation."""
+    o = ((3 * B + 3) & ~3) + 20
+    return pack[o:o + 4].view(torch.int32)
 
 
 def turn_readback(flags, err, dec_err, num_actions, max_actions, text_len, obs_len, flags_copy, left, pack):
@@ -881,6 +954,23 @@ def prompt_commit(bpe_err, text_err, active, mark_tok, len_upd, bad):
             raise ValueError("every input must have one entry per env")
     check(lib().rmi_prompt_commit(_ptr(bpe_err), _ptr(text_err), _ptr(active), _ptr(mark_tok), _ptr(len_upd), B,
                                   _ptr(bad), _stream(dev)), "rmi_prompt_commit")
+
+
+def next_rows_stats(length, has, flags, bad, stats):
+    """rmi_next_rows_stats: stats i32[3] = (max length over the envs with has (None: every env)
+    and flags without FLAG_DONE, any bad, their count)."""
+    dev = _dev(length, has, flags, bad, stats)
+    _dt(length, torch.int32, "len")
+    _dt(has, torch.uint8, "has")
+    _dt(flags, torch.uint8, "flags")
+    _dt(bad, torch.uint8, "bad")
+    _dt(stats, torch.int32, "stats")
+    B = length.numel()
+    if flags.numel() != B or (has is not None and has.numel() != B) or (bad is not None and bad.numel() != B) \
+            or stats.numel() < 3:
+        raise ValueError("next_rows_stats: len, has, flags and bad hold one entry per env, stats three ints")
+    check(lib().rmi_next_rows_stats(_ptr(length), _ptr(has), _ptr(flags), _ptr(bad), B, _ptr(stats), _stream(dev)),
+          "rmi_next_rows_stats")
 
 
 def rows_stats(length, rows, n_rows: int, bad, stats):

@@ -612,6 +612,49 @@ def sokoban_render(room_fixed: Tensor, room_state: Tensor, H: int, W: int, glyph
     return out, n
 
 
+_RENDER_TEMPLATES = {}  # glyph table -> its rmi_render_t (pointers unset)
+
+
+def _render_struct(glyph_bytes: List[int], glyph_len: List[int], obs: Tensor, obs_len: Tensor) -> _lib.Render:
+    key = (tuple(glyph_bytes), tuple(glyph_len))
+    R = _RENDER_TEMPLATES.get(key)
+    if R is None:
+        gb, gl = _glyphs(glyph_bytes, glyph_len)
+        if (gl > 4).any():
+            raise ValueError("glyphs are at most 4 UTF-8 bytes")
+        R = _lib.Render()
+        for k in range(16):
+            R.glyph_bytes[k], R.glyph_len[k] = int(gb[k]), int(gl[k])
+        if len(_RENDER_TEMPLATES) > 64:
+            _RENDER_TEMPLATES.clear()
+        _RENDER_TEMPLATES[key] = R
+    r = _lib.Render.from_buffer_copy(R)
+    r.out, r.stride, r.len = obs.data_ptr(), int(obs.shape[1]), obs_len.data_ptr()
+    return r
+
+
+@_op("sokoban_step_turn_render", _SOK_MUT + ("err", "obs", "obs_len"))
+def sokoban_step_turn_render(room_fixed: Tensor, room_state: Tensor, player: Tensor, num_env_steps: Tensor,
+                             boxes_on_target: Tensor, num_actions: Tensor, flags: Tensor, n_turns: Tensor,
+                             penalty: Tensor, turn_reward: Tensor, turn_info: Tensor, turn_exec: Tensor,
+                             actions: Tensor, n_actions: Tensor, has_input: Optional[Tensor], err: Optional[Tensor],
+                             obs: Tensor, obs_len: Tensor, glyph_bytes: List[int], glyph_len: List[int], turn: int,
+                             max_actions_per_traj: int, format_penalty: float, H: int, W: int, num_boxes: int,
+                             max_steps: int) -> None:
+    """EnvStateManager.step (es_manager.py:105-171) and SokobanEnv.render of the next state
+    (sokoban/env.py:53-61) in one launch: obs u8[B, stride] / obs_len i32[B] as sokoban_render's."""
+    env = _sokoban(room_fixed, room_state, player, num_env_steps, boxes_on_target, H, W, num_boxes, max_steps)
+    ep = _ep(num_actions, flags, n_turns, penalty, turn_reward, turn_info, turn_exec)
+    ops._dev(room_state, flags, actions, n_actions, has_input, err, obs, obs_len)
+    ops._dt(obs, torch.uint8, "obs")
+    ops._dt(obs_len, torch.int32, "obs_len")
+    if obs.dim() != 2 or obs.shape[0] != room_state.shape[0] or obs_len.numel() != room_state.shape[0]:
+        raise ValueError("obs / obs_len must have one row per env")
+    ops.sokoban_step_turn_render(env, ep, ops.turn_struct(turn, actions, n_actions, has_input, max_actions_per_traj,
+                                                          format_penalty),
+                                 _render_struct(glyph_bytes, glyph_len, obs, obs_len), err)
+
+
 @sokoban_render.register_fake
 def _(room_fixed, room_state, H, W, glyph_bytes, glyph_len):
     B = room_state.shape[0]
@@ -918,6 +961,7 @@ def _(program, sep, B, stride, pool, tag_const, tag, obs, obs_len, ints, reward,
 
 # the mutating ops return nothing: their fake kernels only have to exist
 for _name in ("gen_rows", "sokoban_step_turn", "sokoban_step_turn_first", "sokoban_step_turn_finalize",
+              "sokoban_step_turn_render",
               "sokoban_reset", "frozenlake_step_turn", "frozenlake_step_turn_first", "frozenlake_step_turn_finalize",
               "frozenlake_reset", "bandit_step_turn", "countdown_step_turn", "rollout_finalize"):
     torch.library.register_fake(f"{NS}::{_name}", lambda *a, **k: None, lib=_LIB)

@@ -207,3 +207,42 @@ def test_device_prompts_context_window_qwen_bpe(device, qwen_tok, monkeypatch):
     dev, dev_proxy, dev_prompts = _rollout(cfg, qwen_tok, turn_tokens, device, True)
     assert dev_proxy.train_ctx_manager.prompts().host_rows_used == 0
     _compare(ref, dev, ref_prompts, dev_prompts, ref_proxy, dev_proxy)
+
+
+@pytest.mark.parametrize("which", ["fake", "qwen"])
+def test_device_turn_decode_overflow_second_pass(device, which, qwen_tok, monkeypatch):
+    """The device turn's one readback: the decode's row comes from a hint (the longest generation
+    seen), and generations longer than it overflow the first pass, are masked out of it and are
+    stepped by a second pass over those envs (EnvStateManager._step_device).  With the hint
+    pinned far below every generation each turn takes both passes; the rollout must still equal
+    the host path exactly.  Without the pin, the readbacks are one per turn (+ the first turn's
+    decode size and the first generation batch's row stats)."""
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok() if which == "fake" else qwen_tok
+    name = "sokoban_es"
+    cfg = _config(name)
+    _, ng, gs, T, _ = TRACES[name]
+    B = ng * gs
+    rng = np.random.default_rng(11)
+    texts = [[r + " pad" * int(rng.integers(0, 40)) for r in _responses(name, t, B)] for t in range(T)]
+    turn_tokens = [_ids(tok, texts[t], device) for t in range(T)]
+    ref, ref_proxy, ref_prompts = _rollout(cfg, tok, turn_tokens, device, False)
+    # pinned hint: every turn overflows
+    actor = TokenActor(turn_tokens, read_prompts=True)
+    proxy = LLMAgentProxy(cfg, actor, tok, device=device)
+    proxy.train_ctx_manager.set_device_vocab(_vocab(tok, device))
+    proxy.train_ctx_manager._raw_hint_pin = 24
+    random.seed(7)
+    dev = proxy.rollout(DataProto(meta_info={}), val=False)
+    _compare(ref, dev, ref_prompts, [tuple(x.cpu() for x in p) for p in actor.prompts], ref_proxy, proxy)
+    assert proxy.last_timing["readbacks"]["turns"] >= 2 * len(actor.prompts)
+    # free hint: one readback per turn from the second rollout on
+    proxy.train_ctx_manager._raw_hint_pin = None
+    for _ in range(2):
+        actor.turn, actor.prompts, actor.prompt_shapes = 0, [], []
+        random.seed(7)
+        dev = proxy.rollout(DataProto(meta_info={}), val=False)
+    _compare(ref, dev, ref_prompts, [tuple(x.cpu() for x in p) for p in actor.prompts], ref_proxy, proxy)
+    n_turns = len(actor.prompts)
+    assert proxy.last_timing["readbacks"]["turns"] == n_turns + 1, proxy.last_timing

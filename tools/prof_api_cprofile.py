@@ -47,12 +47,13 @@ def run():
 
 for _ in range(3):
     tm = run()
-print("plain:", {k: round(v * 1e3, 2) for k, v in tm.items()}, "ms")
-pr = cProfile.Profile()
-pr.enable()
-tm = run()
-pr.disable()
-print("profiled:", {k: round(v * 1e3, 2) for k, v in tm.items()}, "ms")
-st = pstats.Stats(pr)
-st.sort_stats("cumulative").print_stats(50)
-st.sort_stats("tottime").print_stats(35)
+if __name__ == "__main__":  # (imported by prof_api_host.py for the setup and warm-up)
+    print("plain:", {k: (round(v * 1e3, 2) if isinstance(v, float) else v) for k, v in tm.items()}, "ms")
+    pr = cProfile.Profile()
+    pr.enable()
+    tm = run()
+    pr.disable()
+    print("profiled:", {k: (round(v * 1e3, 2) if isinstance(v, float) else v) for k, v in tm.items()}, "ms")
+    st = pstats.Stats(pr)
+    st.sort_stats("cumulative").print_stats(50)
+    st.sort_stats("tottime").print_stats(35)

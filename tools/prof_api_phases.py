@@ -50,7 +50,7 @@ def run():
 
 for _ in range(3):
     wall, tm = run()
-print("plain:", {k: round(v * 1e3, 2) for k, v in tm.items()}, "ms")
+print("plain:", {k: (round(v * 1e3, 2) if isinstance(v, float) else v) for k, v in tm.items()}, "ms")
 
 acc = defaultdict(float)
 cnt = defaultdict(int)
@@ -86,6 +86,6 @@ wall, tm = run()
 acc.clear()
 cnt.clear()
 wall, tm = run()
-print("phased:", {k: round(v * 1e3, 2) for k, v in tm.items()}, "ms")
+print("phased:", {k: (round(v * 1e3, 2) if isinstance(v, float) else v) for k, v in tm.items()}, "ms")
 for k in acc:
     print(f"  {k:28s} {acc[k] * 1e3:8.2f} ms  ({cnt[k]} calls)")

@@ -82,11 +82,11 @@ def run():
 
 for _ in range(3):
     run()
-print("plain rollout", {k: round(v * 1e3, 3) for k, v in proxy.last_timing.items()}, "ms")
+print("plain rollout", {k: (round(v * 1e3, 3) if isinstance(v, float) else v) for k, v in proxy.last_timing.items()}, "ms")
 on[0] = True
 R = 3
 for _ in range(R):
     run()
-print("wrapped rollout", {k: round(v * 1e3, 3) for k, v in proxy.last_timing.items()}, "ms")
+print("wrapped rollout", {k: (round(v * 1e3, 3) if isinstance(v, float) else v) for k, v in proxy.last_timing.items()}, "ms")
 for k in sorted(acc, key=lambda k: -acc[k]):
     print(f"  {k:34s} {acc[k] / cnt[k] * 1e6:9.1f} us/call  {cnt[k] / R:5.1f} calls  {acc[k] / R * 1e3:8.3f} ms/rollout")
