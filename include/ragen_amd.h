@@ -684,6 +684,12 @@ int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t strea
 /* [host] Wait until every launch enqueued on the stream has finished: the turn loop's one
  * readback (a small async device -> pinned-host copy, then this) with no Stream object.     */
 int rmi_stream_synchronize(rmi_stream_t stream);
+/* [host] The turn loop's readback: bytes from device src to host dst (pinned), enqueued on the
+ * stream after its launches, then the stream waited on.                                      */
+int rmi_readback(void* dst /*[host]*/, const void* src, size_t bytes, rmi_stream_t stream);
+/* [host] Enqueue a host (pinned) -> device copy on the stream, no wait (the turn loop's small
+ * index uploads).                                                                            */
+int rmi_upload(void* dst, const void* src /*[host]*/, size_t bytes, rmi_stream_t stream);
 
 #ifdef __cplusplus
 }

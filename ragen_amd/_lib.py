@@ -166,6 +166,8 @@ _SIGS = {
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int32, c_void_p, c_void_p]),
     "rmi_device_copy": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "rmi_stream_synchronize": (c_int32, [c_void_p]),
+    "rmi_readback": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rmi_upload": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "rmi_prompt_text": (c_int32, [_P(Prompt), c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_gen_rows": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),

@@ -33,6 +33,21 @@ RMI_API int rmi_stream_synchronize(rmi_stream_t stream) {
   return hipStreamSynchronize(rmi::as_stream(stream)) == hipSuccess ? RMI_OK : RMI_EDEVICE;
 }
 
+RMI_API int rmi_upload(void* dst, const void* src, size_t bytes, rmi_stream_t stream) {
+  if (!bytes) return RMI_OK;
+  if (!dst || !src) return RMI_EINVAL;
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, rmi::as_stream(stream)) == hipSuccess ? RMI_OK
+                                                                                                   : RMI_EDEVICE;
+}
+
+RMI_API int rmi_readback(void* dst, const void* src, size_t bytes, rmi_stream_t stream) {
+  if (!bytes) return RMI_OK;
+  if (!dst || !src) return RMI_EINVAL;
+  hipStream_t s = rmi::as_stream(stream);
+  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return RMI_EDEVICE;
+  return hipStreamSynchronize(s) == hipSuccess ? RMI_OK : RMI_EDEVICE;
+}
+
 RMI_API int rmi_device_copy(void* dst, const void* src, size_t bytes, rmi_stream_t stream) {
   using namespace rmi;
   if ((!dst || !src) && bytes) return RMI_EINVAL;

@@ -17,6 +17,8 @@
 //      numpy's negative-index wrap, gym_sokoban's IndexError points).
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace rmi {
 namespace {
 
@@ -497,11 +499,13 @@ __host__ __device__ inline bool spread_lanes(int64_t B) { return B <= kSpreadMax
 
 // ---- the observation a turn launch renders itself (rmi_sokoban_step_turn_render, kObs): the
 // text of SokobanEnv.render (sokoban/env.py:53-61) of every env's state after the turn, byte for
-// byte rmi_sokoban_render's rows (render.hip), built by the env's own lane from what the turn
-// already holds in registers — the final bitboards of a stepped regular room, else the row
-// dwords — so the next observation costs no launch and no reload of the rows.  The glyph table
-// sits one entry per lane (a ds_bpermute per cell: no LDS staging, no barrier); the lane appends
-// each glyph to a 64-bit accumulator and stores every completed dword of its row.
+// byte rmi_sokoban_render's rows (render.hip), with no launch and no reload of the rows of its
+// own.  A turn lane leaves its env's final state in LDS (the row dwords, or for a stepped
+// regular room the bitboards, which hold it); the workgroup then renders its envs with
+// kObsLpe lanes each — the turn's waves plus kObsFan - 1 helper waves per turn wave, which skip
+// the turn (one lane per env would make the render a ~40-step serial chain per lane: measured
+// 11.4 us per launch against 4.5 for the turn alone) — into an LDS block laid out like the
+// output rows, and copies the block out with coalesced 16-B stores.
 struct ObsOut {
   uint32_t gb[16];  // glyph bytes of each code (absent codes: '?'), little-endian
   uint64_t glen;    // glyph byte count of each code, 4 bits per code (1..4)
@@ -509,63 +513,114 @@ struct ObsOut {
   int32_t* len;     // [B]
   int stride;
 };
-
-// The wave renders into a wave-private LDS block laid out like its 64 rows of the output (pitch
-// = the output stride), then copies the block out with coalesced 16-B stores: one lane per row
-// storing to its own row would scatter every store over 64 rows.
+constexpr int kObsFan = 4;  // waves per turn wave in a kObs workgroup (the render's lanes)
+constexpr int kObsLpe = 4;  // render lanes per env
 constexpr int obs_pitch_max(int HW) { return HW * 5; }  // >= H*W*4 + H - 1 for any H <= H*W (bytes)
 
-template <int HW, class M, int NWL>
-__device__ __forceinline__ void render_obs(const ObsOut& o, int64_t b0, int lane, int n_live, int W, bool bits,
-                                           M wall, M target, M box, int jp, const uint32_t (&xs)[NWL],
-                                           const uint32_t (&xf)[NWL], uint32_t tabv, uint32_t* blk) {
-  const int pitch_w = o.stride >> 2;
-  uint32_t* row = blk + lane * pitch_w;
-  uint64_t acc = 0;
-  int fill = 0, w = 0, col = 0;
-  auto emit = [&](uint32_t g, int n) {
-    acc |= (uint64_t)g << (8 * fill);
-    fill += n;
-    if (fill >= 4) {
-      row[w++] = (uint32_t)acc;
-      acc >>= 32;
-      fill -= 4;
-    }
-  };
+template <int HW, class M>
+struct ObsLds {  // the workgroup's envs after the turn, and its output block
+  static constexpr int kEnvs = kWave * kSokWpb;
+  uint32_t xs[kEnvs][HW / 4], xf[kEnvs][HW / 4];
+  M wall[kEnvs], target[kEnvs], box[kEnvs];
+  int jp[kEnvs];  // the player's window bit for a stepped regular room, else INT32_MIN (use the rows)
+  uint32_t gb[18];  // the glyph bytes of codes 0..15, then '?' and '\n'
+  uint32_t blk[kEnvs * (obs_pitch_max(HW) / 4)];
+};
+
+// The workgroup's render (every thread): env e = threadIdx.x / kObsLpe of the group, its tokens
+// (H*W cells and H - 1 newlines, in order) split into kObsLpe contiguous runs; each lane sizes
+// its run's glyphs, a 4-lane scan places them, the bytes go into the block, the block goes out.
+template <int HW, class M>
+__device__ __forceinline__ void render_group(const ObsOut& o, ObsLds<HW, M>& L, int64_t B, int H, int W) {
+  constexpr int kTokMax = (2 * HW + kObsLpe - 1) / kObsLpe;  // T = H*(W+1) - 1 < 2*H*W
+  const int e = threadIdx.x / kObsLpe, j = threadIdx.x % kObsLpe;
+  const int64_t g0 = (int64_t)blockIdx.x * ObsLds<HW, M>::kEnvs;
+  const int T = H * (W + 1) - 1;
+  const int per = (T + kObsLpe - 1) / kObsLpe;
+  const int t0 = j * per;
+  const int r0 = t0 / (W + 1), c0 = t0 - r0 * (W + 1);
+  // the env's record (its row bytes are read per cell below: LDS byte reads, issued together)
+  const int jp = L.jp[e];
+  const M wall = L.wall[e], target = L.target[e], box = L.box[e];
+  const uint8_t* rs = reinterpret_cast<const uint8_t*>(L.xs[e]);
+  const uint8_t* rf = reinterpret_cast<const uint8_t*>(L.xf[e]);
+  const bool bits = jp != INT32_MIN;
+  uint32_t code[kTokMax];
+  int r = r0, c = c0;
 #pragma unroll
-  for (int i = 0; i < HW; ++i) {
-    // the state byte with the player on a target shown as 6 (sokoban/env.py:55) ...
-    const uint32_t s = (xs[i >> 2] >> (8 * (i & 3))) & 0xFFu, f = (xf[i >> 2] >> (8 * (i & 3))) & 0xFFu;
-    int code = (s == 5u && f == 2u) ? 6 : (int)s;
-    // ... or, for a stepped regular room, rebuilt from the bitboards (window bit j = cell W + j;
-    // row 0 is all wall): wall 0, player 5 / 6 on a target, box 4 / 3 on a target, else 1 / 2
-    const int j = i - W;
-    const int jj = j >= 0 ? j : 0;
-    const uint32_t wl = j >= 0 ? (uint32_t)(wall >> jj) & 1u : 1u;
-    const int t = (int)((target >> jj) & 1u), bx = (int)((box >> jj) & 1u);
-    const int bc = wl ? 0 : (j == jp ? 5 + t : (bx ? 4 - t : 1 + t));
-    code = bits ? bc : code;
-    const uint32_t g = (uint32_t)__shfl((int)tabv, code & 15, 64);
-    const int n = code < 16 ? (int)((o.glen >> (4 * (code & 15))) & 15u) : 1;
-    emit(code < 16 ? g : (uint32_t)'?', n);
-    if (++col == W) {  // wave-uniform
-      col = 0;
-      if (i < HW - 1) emit((uint32_t)'\n', 1);
+  for (int k = 0; k < kTokMax; ++k) {
+    const bool tok = k < per && t0 + k < T;
+    const bool newline = c == W;
+    const int i = r * W + c;
+    int cd = 0xFF;  // 0xFF: newline / no token
+    if (tok && !newline) {
+      const int ic = i < HW ? i : HW - 1;
+      const uint32_t s = rs[ic], f = rf[ic];
+      cd = (s == 5u && f == 2u) ? 6 : (int)s;  // the player on a target shown as 6 (sokoban/env.py:55)
+      // a stepped regular room: from the bitboards (window bit q = cell W + q; row 0 all wall)
+      const int qb = i - W;
+      const int qq = qb >= 0 ? qb : 0;
+      const uint32_t wl = qb >= 0 ? (uint32_t)(wall >> qq) & 1u : 1u;
+      const int tg = (int)((target >> qq) & 1u), bx = (int)((box >> qq) & 1u);
+      const int bc = wl ? 0 : (qb == jp ? 5 + tg : (bx ? 4 - tg : 1 + tg));
+      cd = bits ? bc : cd;
+      cd = cd > 0xFE ? 0xFE : cd;
+    }
+    code[k] = tok ? (uint32_t)cd : 0x100u;  // 0x100: no token
+    if (++c > W) {
+      c = 0;
+      ++r;
     }
   }
-  if (fill > 0) row[w] = (uint32_t)acc;  // the last dword's unused bytes are zero
-  if (lane < n_live) o.len[b0 + lane] = 4 * w + fill;
-  wave_sync();
-  // the block out: rows b0 .. b0 + n_live - 1 are one contiguous run of n_live * stride bytes
+  // the glyphs: LDS table reads ([16] = '?', [17] = '\n'), all issued before any is used
+  uint32_t gl[kTokMax];
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < kTokMax; ++k) {
+    const uint32_t cd = code[k];
+    gl[k] = L.gb[cd < 16 ? cd : (cd == 0xFF ? 17 : 16)];
+  }
+  int nl[kTokMax];
+#pragma unroll
+  for (int k = 0; k < kTokMax; ++k) {
+    const uint32_t cd = code[k];
+    nl[k] = cd == 0x100u ? 0 : cd == 0xFF ? 1 : (cd < 16 ? (int)((o.glen >> (4 * (cd & 15))) & 15u) : 1);
+    n += nl[k];
+  }
+  // exclusive scan of the byte counts over the env's kObsLpe lanes
+  int incl = n;
+#pragma unroll
+  for (int d = 1; d < kObsLpe; d <<= 1) {
+    const int v = __shfl_up(incl, d, kObsLpe);
+    if (j >= d) incl += v;
+  }
+  const int off = incl - n;
+  const int total = __shfl(incl, kObsLpe - 1, kObsLpe);
+  uint8_t* row = reinterpret_cast<uint8_t*>(L.blk) + e * o.stride;
+  int p = off;
+#pragma unroll
+  for (int k = 0; k < kTokMax; ++k) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (q < nl[k]) row[p + q] = (uint8_t)(gl[k] >> (8 * q));
+    p += nl[k];
+  }
+  if (j == kObsLpe - 1)
+    for (int q = total; q < ((total + 3) & ~3); ++q) row[q] = 0;  // the last dword's unused bytes
+  if (j == 0 && g0 + e < B) o.len[g0 + e] = total;
+  __syncthreads();
+  // the block out: the group's rows are one contiguous run of n_live * stride bytes
+  const int64_t left = B - g0;
+  const int n_live = left < ObsLds<HW, M>::kEnvs ? (int)left : ObsLds<HW, M>::kEnvs;
   const int nb = n_live * o.stride;
-  uint8_t* dst = o.out + b0 * (int64_t)o.stride;
+  uint8_t* dst = o.out + g0 * (int64_t)o.stride;
+  const int nt = blockDim.x;
   if ((reinterpret_cast<uintptr_t>(dst) & 15u) == 0) {
     const int n16 = nb >> 4;
-    for (int k = lane; k < n16; k += 64)
-      reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(blk)[k];
-    for (int k = (n16 << 2) + lane; k < (nb >> 2); k += 64) reinterpret_cast<uint32_t*>(dst)[k] = blk[k];
+    for (int k = threadIdx.x; k < n16; k += nt) reinterpret_cast<uint4*>(dst)[k] = reinterpret_cast<const uint4*>(L.blk)[k];
+    for (int k = (n16 << 2) + threadIdx.x; k < (nb >> 2); k += nt) reinterpret_cast<uint32_t*>(dst)[k] = L.blk[k];
   } else {
-    for (int k = lane; k < (nb >> 2); k += 64) reinterpret_cast<uint32_t*>(dst)[k] = blk[k];
+    for (int k = threadIdx.x; k < (nb >> 2); k += nt) reinterpret_cast<uint32_t*>(dst)[k] = L.blk[k];
   }
 }
 
@@ -585,15 +640,16 @@ __device__ __forceinline__ void render_obs(const ObsOut& o, int64_t b0, int lane
 // the lanes whose env acts this turn, a second memory round trip that a batch this size hides,
 // so the rows of done envs are not fetched (HBM-bound there: done envs were ≈18 % of the bench
 // rollout's env-turns, their rows ≈9 % of its traffic).
-// kObs (HW != 0, LPE == 1): the launch also renders every env's observation after the turn (render_obs).
+// kObs (HW == 36, LPE == 1): the launch also renders every env's observation after the turn
+// (render_group; kObsFan times the waves per workgroup, the extra ones only render).
 template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false, bool kObs = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
-__global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
+__global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
                                                                   uint8_t* __restrict__ err_out, rmi_finalize_t fin,
                                                                   const uint8_t* __restrict__ init_state = nullptr,
                                                                   const int8_t* __restrict__ init_player = nullptr,
                                                                   ObsOut obs = ObsOut{}) {
-  static_assert(!kObs || (HW != 0 && LPE == 1 && !kLate), "the fused render needs a fixed room size, one lane per env");
+  static_assert(!kObs || (HW == 36 && LPE == 1 && !kLate), "the fused render: 36-cell rooms, one lane per env");
   constexpr int NW = HW ? HW / 4 : kMaxWords;
   constexpr int NWL = (NW + LPE - 1) / LPE;      // row dwords per lane
   constexpr int kEnvs = kWave / LPE;             // envs per wave
@@ -601,11 +657,13 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   __shared__ uint32_t lds_fixed[kSokWpb * kEnvs * NW];
   const int hw = HW ? HW : hw_rt;
   const int row_words = hw >> 2;
-  __shared__ uint32_t lds_obs[kObs ? kSokWpb * kWave * (obs_pitch_max(HW) / 4) : 1];  // kObs: the wave's rows
+  using ObsL = ObsLds<kObs ? HW : 36, M>;
+  __shared__ typename std::conditional<kObs, ObsL, char>::type lds_obs;  // kObs: the group's envs and rows
   const int B = ep.B;
   const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
   const int sub = lane % LPE, slot = lane / LPE;
-  const int64_t b = ((int64_t)blockIdx.x * kSokWpb + wave) * kEnvs + slot;
+  const bool turn_wave = !kObs || wave < kSokWpb;  // kObs helper waves only render
+  const int64_t b = turn_wave ? ((int64_t)blockIdx.x * kSokWpb + wave) * kEnvs + slot : (int64_t)B;
   const bool live = b < B;
   const int H = env.H, W = env.W;
   const uint32_t w_magic = (65536u + (uint32_t)W - 1u) / (uint32_t)W;  // off the critical path
@@ -641,7 +699,6 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   }
   int n_act = in.n_actions[bc];
   const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K, ep.flags + bc);
-  const uint32_t tabv = kObs ? obs.gb[lane & 15] : 0u;  // the glyph table, one entry per lane
   FinRecord rec;
   if (kFin) rec.load(ep, bc);
   if (!live) flags = RMI_FLAG_DONE;
@@ -869,10 +926,23 @@ __global__ __launch_bounds__(kWave * kSokWpb) void sokoban_step_turn_kernel(rmi_
   }
   RMI_STAMP(4);
   if constexpr (kObs) {
-    const int64_t b0 = ((int64_t)blockIdx.x * kSokWpb + wave) * kWave;
-    const int n_live = B - b0 < kWave ? (int)(B - b0) : kWave;  // <= 0 for a wave past B: nothing stored
-    render_obs<HW, M, NWL>(obs, b0, lane, n_live, W, fast && act, wall, target, box, jp, xs, xf, tabv,
-                           lds_obs + wave * kWave * (obs_pitch_max(HW) / 4));
+    if (turn_wave) {  // this env's state after the turn, for the group's render
+      const int e = wave * kWave + lane;
+#pragma unroll
+      for (int i = 0; i < NW; ++i) {
+        lds_obs.xs[e][i] = xs[i];
+        lds_obs.xf[e][i] = xf[i];
+      }
+      lds_obs.wall[e] = wall;
+      lds_obs.target[e] = target;
+      lds_obs.box[e] = box;
+      lds_obs.jp[e] = (fast && act) ? jp : INT32_MIN;
+    }
+    if (threadIdx.x < 18) lds_obs.gb[threadIdx.x] = threadIdx.x < 16 ? obs.gb[threadIdx.x] : (threadIdx.x == 16 ? '?' : '\n');
+    __syncthreads();
+#ifndef RMI_OBS_SKIP_RENDER  // (diagnostic variant: the record and the barrier only)
+    render_group<HW, M>(obs, lds_obs, B, H, W);
+#endif
   }
   if (kFin) {
     if (act) rec.set(in.turn, o.acc, o.info);  // this turn's record is still in registers
@@ -962,7 +1032,7 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
   return launch_status();
 }
 
-// The turn with the render fused (kObs): fixed room sizes (36 / 64 cells), one lane per env.
+// The turn with the render fused (kObs): 36-cell rooms, one lane per env.
 // -> RMI_EUNSUP for any other layout (the caller launches the turn and the render separately).
 template <bool kFin, bool kFirst>
 int sokoban_step_turn_obs_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in, uint8_t* err,
@@ -970,21 +1040,18 @@ int sokoban_step_turn_obs_launch(const rmi_sokoban_t* env, const rmi_episode_t* 
                                  const int8_t* init_player, const ObsOut& obs) {
   const int hw = env->H * env->W;
   const int H = env->H, W = env->W;
-  if (spread_lanes(ep->B) || (hw != 36 && hw != 64) || obs.stride > obs_pitch_max(hw)) return RMI_EUNSUP;
+  if (spread_lanes(ep->B) || hw != 36 || obs.stride > obs_pitch_max(hw)) return RMI_EUNSUP;
   uint64_t border = 0;
   for (int r = 0; r < H; ++r)
     for (int c = 0; c < W; ++c)
       if (r == 0 || c == 0 || r == H - 1 || c == W - 1) border |= 1ull << (r * W + c);
   const bool w32 = (H - 1) * W <= 32;
-  const dim3 grid((unsigned)((ep->B + kWave * kSokWpb - 1) / (kWave * kSokWpb))), block(kWave * kSokWpb);
-  if (hw == 36 && w32)
+  const dim3 grid((unsigned)((ep->B + kWave * kSokWpb - 1) / (kWave * kSokWpb))), block(kWave * kSokWpb * kObsFan);
+  if (w32)
     hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint32_t, 1, kFin, kFirst, false, true>), grid, block, 0, s, *env,
                        *ep, *in, hw, border, err, fin, init_state, init_player, obs);
-  else if (hw == 36)
-    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint64_t, 1, kFin, kFirst, false, true>), grid, block, 0, s, *env,
-                       *ep, *in, hw, border, err, fin, init_state, init_player, obs);
   else
-    hipLaunchKernelGGL((sokoban_step_turn_kernel<64, uint64_t, 1, kFin, kFirst, false, true>), grid, block, 0, s, *env,
+    hipLaunchKernelGGL((sokoban_step_turn_kernel<36, uint64_t, 1, kFin, kFirst, false, true>), grid, block, 0, s, *env,
                        *ep, *in, hw, border, err, fin, init_state, init_player, obs);
   return launch_status();
 }

@@ -213,6 +213,7 @@ class DeviceEnvInputs:
         self.ids, self.n_ids, self.stride = ids, n_ids, stride
         self.raw_max = None  # host int: the longest generation's raw bytes, when known
         self.raw_dev = None  # the same on the device (i32[1], rmi_gen_rows)
+        self.pack = None     # the turn's readback buffer raw_dev lives in
         self.vocab = ctx.device_vocab
         self._text = self._text_len = self._err = None
         self._decoded = None
@@ -699,7 +700,10 @@ class ContextManager:
         R = resp.shape[1]
         lo, n = self.env_lo, self.n_envs
         resp = resp.to(torch.int64).contiguous()
-        raw = torch.empty(1, dtype=torch.int32, device=dev)
+        # the turn's readback buffer, allocated here so rmi_gen_rows writes the longest
+        # generation's raw bytes straight into it (EnvStateManager._device_pass reads it back)
+        pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
+        raw = ops.readback_raw(pack, n)
         if len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n)):
             # every env in order: the generations are the rows (n_ids = None: R ids each)
             has_t, n_ids, ids = None, None, resp
@@ -734,13 +738,14 @@ class ContextManager:
         inp = DeviceEnvInputs(self, env_ids, has_t, ids, n_ids, stride)
         inp.raw_max = raw_max  # the decoded rows' length bound (longer only with U+FFFD replacements)
         inp.raw_dev = raw      # i32[1] on the device: the longest row's raw bytes (read back with the turn)
+        inp.pack = pack
         return inp
 
-    RAW_HINT_MARGIN = 1.25  # the decode's row over the longest generation seen
+    RAW_HINT_MARGIN = 1.1  # the decode's row over the longest generation seen (+ 32 bytes)
 
     def note_raw(self, raw_max: int):
         """A turn's longest generation (raw bytes, read back) -> the next turns' decode hint."""
-        h = int(raw_max * self.RAW_HINT_MARGIN) + 64
+        h = int(raw_max * self.RAW_HINT_MARGIN) + 32
         self._raw_hint = h if self._raw_hint is None else max(self._raw_hint, h)
 
     def formulate_rollouts(self, env_outputs: List[Dict]) -> DataProto:

@@ -679,13 +679,16 @@ class EnvStateManager:
                                                          for tg in self.tags]), device=dev)
         flags_copy = torch.empty(n, dtype=torch.uint8, device=dev)
         left = torch.empty(n, dtype=torch.int32, device=dev)
-        pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
+        pack = getattr(inp, "pack", None) if first is None else None  # (rmi_gen_rows wrote the raw max there)
+        if pack is None:
+            pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
         # the record's flags and actions-left columns, and the one packed readback: flags, step
         # and decode errors, the longest decoded response and observation (rmi_turn_readback)
         ops.turn_readback(flags, err, inp.err, num_actions, self._max_act, inp.text_len, obs_len, flags_copy, left,
                           pack)
-        if inp.raw_max is None:  # the longest generation's raw bytes ride along (the next hint)
-            ops.readback_raw(pack, n).copy_(inp.raw_dev)
+        raw_v = ops.readback_raw(pack, n)
+        if inp.raw_max is None and inp.raw_dev.data_ptr() != raw_v.data_ptr():
+            raw_v.copy_(inp.raw_dev)  # the longest generation's raw bytes ride along (the next hint)
         rec = {"turn": t, "inp": inp, "has": has, "err": err, "obs": obs, "spans": [p["spans"] for p in parsed],
                "flags": flags_copy, "left": left, "_obs_known": obs_len is not None}
         has_next = has

@@ -5,11 +5,12 @@
 set -eu
 cd "$(dirname "$0")/.."
 NAME=$1; SRC=$2; shift 2
-mkdir -p tools/_build
+OUTD=${VARIANT_DIR:-tools/_build}  # (tools/_build stays here; VARIANT_DIR=variants ships to the GPU box)
+mkdir -p tools/_build "$OUTD"
 B=$(basename "$SRC")
 /opt/rocm/bin/hipcc -c -x hip --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden \
   -Iinclude -Iragen_amd/csrc "$@" "ragen_amd/csrc/$B" -o "tools/_build/${B}_$NAME.o"
 OBJS=$(ls ragen_amd/_build/*.o | grep -v "/$B.o")
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "tools/_build/libragen_amd_$NAME.so" $OBJS \
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$OUTD/libragen_amd_$NAME.so" $OBJS \
   "tools/_build/${B}_$NAME.o" -lpthread
-echo "tools/_build/libragen_amd_$NAME.so"
+echo "$OUTD/libragen_amd_$NAME.so"
