@@ -770,7 +770,10 @@ class ContextManager:
         self._sync_prompts(pr)
         ap = self.config.agent_proxy
         dev = self.device
-        tokens, start, row_len = pr.update_rows()
+        # the rows the device could not build are resolved after the readback below, which
+        # carries their any() (one readback fewer)
+        pend = pr._pending[0] if pr._pending is not None and not pr.window else None
+        tokens, start, row_len = pr.update_rows(resolve=pend is None)
         eps = [tg.batch.ep for tg in es.tags]
         tab = (eps[0].turn_reward if len(eps) == 1 else torch.cat([ep.turn_reward for ep in eps], 1)).contiguous()
         n_sc = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
@@ -785,8 +788,19 @@ class ContextManager:
         if getattr(self, "_special", None) is None:  # a tokenizer call: once per manager
             self._special = get_special_tokens(self.tokenizer)
         special_token, reward_token = self._special
-        # the longest row and the most turns, in one readback
-        S, n_slots = torch.stack([row_len.max(), n_sc.max()]).cpu().tolist() if row_len.numel() else (1, 0)
+        # the longest row, the most turns and whether a row waits for the host, in one readback
+        if row_len.numel():
+            st = torch.empty(3, dtype=torch.int32, device=dev)
+            ops.rows_stats(row_len, None, row_len.numel(), pend, st)  # (max row, any pending)
+            st[2:].copy_(n_sc.max().view(1))
+            S, any_bad, n_slots = (int(x) for x in ops.d2h(st, es))
+            if pend is not None:
+                pr._resolve(bool(any_bad))
+                if any_bad:  # host rows were written: the longest row again
+                    S = int(row_len.max())
+        else:
+            pr._resolve()
+            S, n_slots = 1, 0
         # zip_longest's length over the WHOLE batch (ctx_manager.py:52-62): every rank's longest
         from .. import distributed as rd
         if self.process_group is not None and self.world_size > 1:
@@ -799,20 +813,22 @@ class ContextManager:
         if not ap.use_turn_scores:
             normalized = self._normalize_device(score_tensor, es)
         # the mean over the WHOLE batch (ctx_manager.py:305): every rank's row lengths, rank order
-        row_resp = response_mask.sum(dim=-1).float()
+        # (the counts summed as bytes into int32: the values of response_mask.sum(-1))
+        row_resp = response_mask.view(torch.uint8).sum(dim=-1, dtype=torch.int32).float()
         if self.process_group is not None and self.world_size > 1:
             row_resp = rd.all_gather_rows(row_resp, group=self.process_group, sizes=self.shard_sizes())
-        # the assembly's error bits and the mean in one readback (the errors raise first)
-        overlong, multi, response_length = torch.stack([(err & _lib.ERR_UNSUP).any().double(),
-                                                        (err & _lib.ERR_STATE).any().double(),
-                                                        row_resp.mean().double()]).cpu().tolist()
+        # the assembly's error bits, the mean and the metric rows in one readback (errors first)
+        extra = torch.stack([(err & _lib.ERR_UNSUP).any().double(), (err & _lib.ERR_STATE).any().double(),
+                             row_resp.mean().double()]).view(torch.uint8)
+        parts, ext = es.metric_arrays(extra)
+        overlong, multi, response_length = (float(x) for x in ext.view(np.float64))
         _raise_assemble_errors(None, S, (overlong, multi))
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
                  "loss_mask": loss_mask, "rm_scores": normalized, "original_rm_scores": normalized}
         env_ids = es.env_lo + np.arange(es.n_envs, dtype=np.int64)
         out = LazyDataProto(env_ids, lambda: self._messages_only(es._rollout_states_full(), True))
         out.set_device_batch(batch, env_ids, es.group_size)
-        metrics = self.device_metrics(es)
+        metrics = self.device_metrics(es, parts)
         metrics["response_length"] = response_length
         out.meta_info = {"metrics": metrics}
         es._formulated = True
@@ -863,13 +879,15 @@ class ContextManager:
         score_tensor[:, -1] = out
         return score_tensor
 
-    def device_metrics(self, es) -> Dict:
+    def device_metrics(self, es, parts=None) -> Dict:
         """The mean / non-zero metrics of get_lm_inputs (ctx_manager.py:308-329) from the device
-        metric rows (es.metric_arrays: one copy per tag), with numpy over whole arrays in env
-        order — the same values and summation order as the reference's lists.  Under sharding
-        every rank's rows are gathered first, so each rank reports the global metrics."""
+        metric rows (es.metric_arrays: one copy; ``parts`` when read already), with numpy over
+        whole arrays in env order — the same values and summation order as the reference's
+        lists.  Under sharding every rank's rows are gathered first, so each rank reports the
+        global metrics."""
         from .. import distributed as rd
-        parts = es.metric_arrays()
+        if parts is None:
+            parts = es.metric_arrays()
         sharded = self.process_group is not None and self.world_size > 1
         local = {}  # per tag NAME, env order (a tag listed twice in the config: its entries' rows in order)
         for tag, m, custom, _ in parts:

@@ -751,23 +751,31 @@ class EnvStateManager:
                            te[t].tolist(), tr[t].tolist(), pen.tolist(), obs)
 
     # ------------------------------------------------------- get_rollout_states
-    def metric_arrays(self):
-        """Per-env rollout metrics of this shard from the device record, one copy per tag:
+    def metric_arrays(self, extra: Optional[torch.Tensor] = None):
+        """Per-env rollout metrics of this shard from the device record, one copy for every tag:
         -> list of (tag, m f64[B_tag, 4] = success, num_actions, action_is_effective mean,
         action_is_valid mean, custom bool[B_tag] = some turn carried an info dict,
-        info u8[T_seen, B_tag])."""
-        out = []
+        info u8[T_seen, B_tag]).  extra (u8 on the device, optional): read back in the same
+        copy -> (list, extra's host bytes)."""
         T = min(self._turn, self.max_turn)
+        parts, shapes = [] if extra is None else [extra.reshape(-1)], []
         for tg in self.tags:
             ep = tg.batch.ep
-            m = torch.ops.ragen_amd.rollout_metrics(*ep_args(ep))
+            m = direct.rollout_metrics(*ep_args(ep))
             info = ep.turn_info[:T]
-            both = torch.cat([m.view(torch.uint8).reshape(-1), info.reshape(-1)]).cpu().numpy()
-            mh = both[:m.numel() * 8].view(np.float64).reshape(m.shape)
-            ih = both[m.numel() * 8:].reshape(T, -1)
+            parts += [m.view(torch.uint8).reshape(-1), info.reshape(-1)]
+            shapes.append((tg, m.shape, m.numel() * 8, info.numel()))
+        flat = parts[0] if len(parts) == 1 else torch.cat(parts)
+        host = ops.d2h(flat, self)
+        o = 0 if extra is None else extra.numel()
+        out = []
+        for tg, mshape, nm, ni in shapes:
+            mh = host[o:o + nm].view(np.float64).reshape(mshape)
+            ih = host[o + nm:o + nm + ni].reshape(T, -1)
+            o += nm + ni
             custom = (ih & _lib.INFO_PRESENT).any(0) if T else np.zeros(mh.shape[0], bool)
             out.append((tg.tag, mh, custom, ih))
-        return out
+        return out if extra is None else (out, host[:extra.numel()])
 
     def get_rollout_states(self):
         """es_manager.py:173-207.  On the device path (turns taken from device token ids) the

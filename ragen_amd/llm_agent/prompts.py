@@ -752,17 +752,21 @@ class DevicePrompts:
         ids, am, pos, err = direct.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
         return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
 
-    def update_rows(self):
-        """(tokens, row_start, row_len) of formulate_rollouts' rows, env order."""
-        self._resolve()
+    def update_rows(self, resolve=True):
+        """(tokens, row_start, row_len) of formulate_rollouts' rows, env order.  resolve=False:
+        pending host rows stay pending (the caller reads their any() with its own readback and
+        calls _resolve)."""
+        if resolve or self.window:
+            self._resolve()
         if self.window:  # each env's last k complete entries: envs grouped by their turn count
             eps = [tg.batch.ep for tg in self.es.tags]
             n_t = (eps[0].n_turns if len(eps) == 1 else torch.cat([ep.n_turns for ep in eps])).to(torch.int32)
             for n in sorted(set(n_t.cpu().tolist())):
                 if n > 0:
                     self._build_window(n_t == n, int(n), update=True)
-        start = torch.arange(self.n_envs, dtype=torch.int64, device=self.device) * self.cap
-        return self.arena.view(-1), start, self.len_upd
+        if getattr(self, "_row_start", None) is None:
+            self._row_start = torch.arange(self.n_envs, dtype=torch.int64, device=self.device) * self.cap
+        return self.arena.view(-1), self._row_start, self.len_upd
 
     # ------------------------------------------------------------------ self-check
     def _verify(self):
