@@ -62,6 +62,17 @@ def _pmc_field(pattern, key):
         return json.load(f).get(key)
 
 
+def _pmc_source(pattern):
+    """Where the line's PMC traffic figures come from (a counter pass cannot run inside the timed
+    process): the newest committed summary and the counter runs it was computed from."""
+    files = sorted(glob.glob(pattern))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return {"file": os.path.relpath(files[-1], ROOT), "from": d.get("source"), "workload": d.get("workload")}
+
+
 class Rollout:
     def __init__(self, device, rank, B=B_PER_GPU):
         self.device = device
@@ -1200,6 +1211,7 @@ def main():
                        "graph": graph is not None, "rollouts_per_replay": G, "parallelism": f"env-sharded x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": _pmc_source(PMC_GLOB),
                          "achievable_peak": copy_peak,
                          "frac_of_achievable": (achieved / copy_peak) if copy_peak else None,
                          "kernel": "rmi_sokoban_step_turn", "avg_launch_us": avg_launch_us,

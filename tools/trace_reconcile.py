@@ -31,8 +31,8 @@ def main():
     # runs of back-to-back turn launches: consecutive sokoban launches less than 50 us apart
     start = np.array([int(r["Start_Timestamp"]) for r in sk], np.int64)
     end = np.array([int(r["End_Timestamp"]) for r in sk], np.int64)
-    def kind_of(name):  # sokoban_step_turn_kernel<HW, M, LPE, kFin, kFirst, kLate>
-        m = re.search(r"sokoban_step_turn_kernel<[^>]*, (true|false), (true|false), (true|false)>", name)
+    def kind_of(name):  # sokoban_step_turn_kernel<HW, M, LPE, kFin, kFirst, kLate[, kObs]>
+        m = re.search(r"sokoban_step_turn_kernel<[^,>]*, [^,>]*, [^,>]*, (true|false), (true|false)", name)
         fin, first = (m.group(1) == "true", m.group(2) == "true") if m else (False, False)
         return "first" if first else "finalize" if fin else "plain"
     kind = [kind_of(r["Kernel_Name"]) for r in sk]
