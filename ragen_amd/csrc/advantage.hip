@@ -53,6 +53,35 @@ struct __attribute__((packed, aligned(1))) U8x4 {
   uint32_t x;
 };
 
+// Streamed tile loads and output stores.  NT (a launch whose rows are far past the 256 MiB
+// Infinity Cache): nontemporal, the copy probe's faster form there (profiles/r04_copy_probe.json);
+// in-cache launches keep the cached form (nontemporal loads measured 31 -> 55 us at 8192 x 1093).
+typedef float rmi_f4u __attribute__((ext_vector_type(4), aligned(4)));
+template <bool NT>
+__device__ __forceinline__ F4 ld_f4(const float* p) {
+  if constexpr (NT) {
+    const rmi_f4u x = __builtin_nontemporal_load(reinterpret_cast<const rmi_f4u*>(p));
+    return F4{x.x, x.y, x.z, x.w};
+  } else {
+    return *reinterpret_cast<const F4*>(p);
+  }
+}
+template <bool NT>
+__device__ __forceinline__ void st_f4(float* p, const F4& v) {
+#ifdef RMI_NT_LOADS_ONLY  // (A/B build: streamed loads, cached stores)
+  if constexpr (false) {
+#else
+  if constexpr (NT) {
+#endif
+    const rmi_f4u x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<rmi_f4u*>(p));
+  } else {
+    *reinterpret_cast<F4*>(p) = v;
+  }
+}
+constexpr double kStreamBytes = 256.0 * 1024 * 1024;  // a launch's traffic from which NT is used
+
+
 // Mask bytes -> 0x01 per nonzero byte: a mask is a boolean (RAGEN passes a bool loss_mask,
 // ctx_manager.py:46-49), so any nonzero byte counts as 1 in the recurrence, the whitening
 // count and the sums alike.
@@ -78,6 +107,7 @@ struct GaeTile {
   __device__ __forceinline__ uint32_t mask(int j) const { return nz8(m[j] | mor); }
 };
 
+template <bool NT = false>
 __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restrict__ r, const float* __restrict__ v,
                                               const uint8_t* __restrict__ mask, int64_t B, int64_t L, int64_t row0,
                                               int64_t c0, int lane) {
@@ -92,8 +122,8 @@ __device__ __forceinline__ void gae_load_tile(GaeTile& t, const float* __restric
   for (int j = 0; j < kGLoads; ++j) {
     const int64_t row = min<int64_t>(row0 + 4 * j + (lane >> 4), B - 1);
     const int64_t o = dummy ? min<int64_t>(row0, B - 1) * L : (full_col ? row * L + col : row * L);
-    t.r[j] = *reinterpret_cast<const F4*>(r + o);
-    t.v[j] = *reinterpret_cast<const F4*>(v + o);
+    t.r[j] = ld_f4<NT>(r + o);
+    t.v[j] = ld_f4<NT>(v + o);
     t.m[j] = reinterpret_cast<const U8x4*>((mask ? mask : reinterpret_cast<const uint8_t*>(r)) + o)->x;
   }
   // 2. the ragged group at a row end (L % 4 != 0: one group per row, in one tile) and rows
@@ -161,7 +191,7 @@ __device__ __forceinline__ void gae_col(float rt, float vt, float mt, float g, f
   ret_out = last + vt;
 }
 
-template <int VARIANT>
+template <int VARIANT, bool NT = false>
 __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                  const uint8_t* __restrict__ mask, int64_t B, int64_t L, float g,
                                                  float gl, float* __restrict__ adv, float* __restrict__ ret,
@@ -180,7 +210,7 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, co
   double s1a = 0.0, s1b = 0.0, s2a = 0.0, s2b = 0.0, cnt = 0.0;  // row stats, two chains each
 
   GaeTile t;
-  gae_load_tile(t, r, v, mask, B, L, row0, (ntiles - 1) * kGCols, lane);
+  gae_load_tile<NT>(t, r, v, mask, B, L, row0, (ntiles - 1) * kGCols, lane);
   for (int64_t k = ntiles - 1; k >= 0; --k) {
     const int64_t c0 = k * kGCols;
     // registers -> LDS (the tile's 4-column groups), then prefetch the next tile to the left
@@ -192,7 +222,7 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, co
       *reinterpret_cast<uint32_t*>(sm + row * kGMStr + 4 * grp) = t.mask(j);
     }
     __syncthreads();
-    if (k > 0) gae_load_tile(t, r, v, mask, B, L, row0, c0 - kGCols, lane);
+    if (k > 0) gae_load_tile<NT>(t, r, v, mask, B, L, row0, c0 - kGCols, lane);
     // the walk: lane = row, columns right to left, 4 at a time
     if (walker) {
       float* pr = sr + lane * kGStr;
@@ -233,8 +263,8 @@ __global__ __launch_bounds__(64) void gae_kernel(const float* __restrict__ r, co
         const F4 t4 = *reinterpret_cast<const F4*>(sv + row * kGStr + 4 * grp);
         const int64_t o = grow * L + col;
         if (col + 4 <= L) {
-          *reinterpret_cast<F4*>(adv + o) = a4;
-          *reinterpret_cast<F4*>(ret + o) = t4;
+          st_f4<NT>(adv + o, a4);
+          st_f4<NT>(ret + o, t4);
         } else {
           const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
           for (int e = 0; e < 4; ++e)
@@ -282,6 +312,7 @@ struct GaeLegacyState {
 
 // One 32 x 64 tile (columns [c0, c0+64)); c0 < 0 is a pipeline dummy (zero data: the walk
 // continues past column 0 harmlessly, nothing is stored).
+template <bool NT>
 __device__ __forceinline__ void gae_legacy_tile(const GaeTile& cur, int64_t c0, GaeLegacyState& st, float* sd,
                                                 int lane, bool walker, int64_t row0, int64_t B, int64_t L, float g,
                                                 float gl, float* __restrict__ adv, float* __restrict__ ret) {
@@ -340,8 +371,8 @@ __device__ __forceinline__ void gae_legacy_tile(const GaeTile& cur, int64_t c0, 
     if (grow < B && col >= 0 && col < L) {
       const int64_t o = grow * L + col;
       if (col + 4 <= L) {
-        *reinterpret_cast<F4*>(adv + o) = a4;
-        *reinterpret_cast<F4*>(ret + o) = t4;
+        st_f4<NT>(adv + o, a4);
+        st_f4<NT>(ret + o, t4);
       } else {
         const float aa[4] = {a4.x, a4.y, a4.z, a4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
         for (int e = 0; e < 4; ++e)
@@ -355,6 +386,7 @@ __device__ __forceinline__ void gae_legacy_tile(const GaeTile& cur, int64_t c0, 
   __syncthreads();
 }
 
+template <bool NT = false>
 __global__ __launch_bounds__(64) void gae_legacy_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                         const uint8_t* __restrict__ mask, int64_t B, int64_t L,
                                                         float g, float gl, float* __restrict__ adv,
@@ -378,15 +410,15 @@ __global__ __launch_bounds__(64) void gae_legacy_kernel(const float* __restrict_
   // accounting lets the prefetches overlap the walk
   GaeTile ta, tb, tc;
   const int64_t k0 = ntiles - 1;
-  gae_load_tile(ta, r, v, mask, B, L, row0, k0 * kGCols, lane);
-  gae_load_tile(tb, r, v, mask, B, L, row0, (k0 - 1) * kGCols, lane);
+  gae_load_tile<NT>(ta, r, v, mask, B, L, row0, k0 * kGCols, lane);
+  gae_load_tile<NT>(tb, r, v, mask, B, L, row0, (k0 - 1) * kGCols, lane);
   for (int64_t k = k0; k >= 0; k -= 3) {
-    gae_load_tile(tc, r, v, mask, B, L, row0, (k - 2) * kGCols, lane);
-    gae_legacy_tile(ta, k * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
-    gae_load_tile(ta, r, v, mask, B, L, row0, (k - 3) * kGCols, lane);
-    gae_legacy_tile(tb, (k - 1) * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
-    gae_load_tile(tb, r, v, mask, B, L, row0, (k - 4) * kGCols, lane);
-    gae_legacy_tile(tc, (k - 2) * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
+    gae_load_tile<NT>(tc, r, v, mask, B, L, row0, (k - 2) * kGCols, lane);
+    gae_legacy_tile<NT>(ta, k * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
+    gae_load_tile<NT>(ta, r, v, mask, B, L, row0, (k - 3) * kGCols, lane);
+    gae_legacy_tile<NT>(tb, (k - 1) * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
+    gae_load_tile<NT>(tb, r, v, mask, B, L, row0, (k - 4) * kGCols, lane);
+    gae_legacy_tile<NT>(tc, (k - 2) * kGCols, st, sd, lane, walker, row0, B, L, g, gl, adv, ret);
   }
   // per-row partials: the 16 lanes of a DPP row hold one row's groups
   if (row_stats) {
@@ -468,6 +500,7 @@ struct BilevelWalk {  // the row walker's (group-0 lane's) chain state
   float hl, ll;
 };
 
+template <bool NT>
 __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, BilevelCarry& cy, BilevelWalk& wk,
                                              double& s1, double& s2, double& cnt, uint32_t& bad, float* sv, float* sd,
                                              float* sh, float* su, uint32_t* sf, int lane, int64_t row0, int64_t B,
@@ -608,8 +641,8 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
   if (grow < B && col >= 0 && col < L) {
     const int64_t go = grow * L + col;
     if (col + 4 <= L) {
-      *reinterpret_cast<F4*>(adv + go) = F4{oa[0], oa[1], oa[2], oa[3]};
-      *reinterpret_cast<F4*>(ret + go) = F4{oq[0], oq[1], oq[2], oq[3]};
+      st_f4<NT>(adv + go, F4{oa[0], oa[1], oa[2], oa[3]});
+      st_f4<NT>(ret + go, F4{oq[0], oq[1], oq[2], oq[3]});
     } else {
       for (int e = 0; e < 4; ++e)
         if (col + e < L) {
@@ -632,6 +665,7 @@ __device__ __forceinline__ void bilevel_tile(const GaeTile& cur, int64_t c0, Bil
 #define RMI_BL_DEPTH 4
 #endif
 constexpr int kBlDepth = RMI_BL_DEPTH;  // tiles in the register pipeline (3 before round 4)
+template <bool NT = false>
 __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                            const uint8_t* __restrict__ mask, int64_t B, int64_t L,
                                                            float g, float gl, float hg, float hgl,
@@ -661,14 +695,14 @@ __global__ __launch_bounds__(64) void bilevel_tiled_kernel(const float* __restri
   const int64_t k0 = ntiles - 1;
   GaeTile t[kBlDepth];
 #pragma unroll
-  for (int i = 0; i < kBlDepth - 1; ++i) gae_load_tile(t[i], r, v, mask, B, L, row0, (k0 - i) * kGCols, lane);
+  for (int i = 0; i < kBlDepth - 1; ++i) gae_load_tile<NT>(t[i], r, v, mask, B, L, row0, (k0 - i) * kGCols, lane);
   for (int64_t k = k0; k >= 0; k -= kBlDepth) {
 #pragma unroll
     for (int j = 0; j < kBlDepth; ++j) {
       if (k - j < 0) break;
-      gae_load_tile(t[(j + kBlDepth - 1) % kBlDepth], r, v, mask, B, L, row0, (k - j - (kBlDepth - 1)) * kGCols,
+      gae_load_tile<NT>(t[(j + kBlDepth - 1) % kBlDepth], r, v, mask, B, L, row0, (k - j - (kBlDepth - 1)) * kGCols,
                     lane);
-      bilevel_tile(t[j], (k - j) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
+      bilevel_tile<NT>(t[j], (k - j) * kGCols, cy, wk, s1, s2, cnt, bad, sv, sd, sh, su, sf, lane, row0, B, L, g, gl, hg,
                    hgl, adv, ret BL_ARG);
     }
   }
@@ -900,13 +934,14 @@ __device__ __forceinline__ void bs_walk(float* __restrict__ Dr, const uint8_t* _
 }
 
 // v groups c0, c0 + 64, ..., c0 + 7 * 64 of one row (zeros past L; the ragged group at L % 4)
+template <bool NT>
 __device__ __forceinline__ void bs_load_v(F4 (&vq)[8], const float* __restrict__ vrow, int64_t c0, int64_t L) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
     const int64_t c = c0 + (int64_t)u * kGCols;
     vq[u] = F4{0.f, 0.f, 0.f, 0.f};
     if (c + 4 <= L) {
-      vq[u] = *reinterpret_cast<const F4*>(vrow + c);
+      vq[u] = ld_f4<NT>(vrow + c);
     } else if (c < L) {
       float t[4] = {0.f, 0.f, 0.f, 0.f};
       for (int e = 0; e < 4; ++e)
@@ -916,6 +951,7 @@ __device__ __forceinline__ void bs_load_v(F4 (&vq)[8], const float* __restrict__
   }
 }
 
+template <bool NT = false>
 __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict__ r, const float* __restrict__ v,
                                                          const uint8_t* __restrict__ mask, int64_t B, int64_t L,
                                                          float g, float gl, float hg, float hgl,
@@ -942,12 +978,12 @@ __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict
   GaeTile tq[kBsPipe];
   const int64_t k0 = ntiles - 1;
 #pragma unroll
-  for (int u = 0; u < kBsPipe - 1; ++u) gae_load_tile(tq[u], r, v, mask, B, L, row0, (k0 - u) * kGCols, lane);
+  for (int u = 0; u < kBsPipe - 1; ++u) gae_load_tile<NT>(tq[u], r, v, mask, B, L, row0, (k0 - u) * kGCols, lane);
   for (int64_t k = k0; k >= 0; k -= kBsPipe) {
 #pragma unroll
     for (int u = 0; u < kBsPipe; ++u) {
       if (k - u < 0) break;
-      gae_load_tile(tq[(u + kBsPipe - 1) % kBsPipe], r, v, mask, B, L, row0, (k - u - (kBsPipe - 1)) * kGCols, lane);
+      gae_load_tile<NT>(tq[(u + kBsPipe - 1) % kBsPipe], r, v, mask, B, L, row0, (k - u - (kBsPipe - 1)) * kGCols, lane);
       bs_tile(tq[u], (k - u) * kGCols, cy, hl, nseg, bad, D, F, S, sv, VG, Lr, lane, g, hg, hgl);
     }
   }
@@ -983,7 +1019,7 @@ __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict
   int icnt = 0;  // the valid-column count (a sum of 1.0s is exact: counted as an integer)
   for (int64_t cb = 4 * grp; cb < L; cb += 8 * kGCols) {
     F4 cur[8];
-    bs_load_v(cur, vrow, cb, L);
+    bs_load_v<NT>(cur, vrow, cb, L);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int64_t c = cb + (int64_t)u * kGCols;
@@ -1008,8 +1044,8 @@ __global__ __launch_bounds__(64) void bilevel_seg_kernel(const float* __restrict
       if (live) {
         const int64_t go = grow * L + c;
         if (c + 4 <= L) {
-          *reinterpret_cast<F4*>(adv + go) = F4{oa[0], oa[1], oa[2], oa[3]};
-          *reinterpret_cast<F4*>(ret + go) = F4{oq[0], oq[1], oq[2], oq[3]};
+          st_f4<NT>(adv + go, F4{oa[0], oa[1], oa[2], oa[3]});
+          st_f4<NT>(ret + go, F4{oq[0], oq[1], oq[2], oq[3]});
         } else {
           for (int e = 0; e < 4; ++e)
             if (c + e < L) {
@@ -1245,11 +1281,18 @@ RMI_API int rmi_gae(const float* r, const float* v, const uint8_t* mask, int64_t
   const float g = (float)gamma;
   const float gl = (float)(gamma * lam);  // python: gamma * lam * lastgaelam
   const unsigned grid = (unsigned)((B + kGRows - 1) / kGRows);
-  if (variant == 0)
-    hipLaunchKernelGGL(gae_legacy_kernel, dim3(grid), dim3(64), 0, as_stream(stream), r, v, mask, B, L, g, gl, adv,
-                       ret, row_stats);
+  const bool nt = (double)B * (double)L * 17.0 > kStreamBytes;  // r, V, mask in; adv, ret out
+  hipStream_t s = as_stream(stream);
+  if (variant == 0 && nt)
+    hipLaunchKernelGGL(gae_legacy_kernel<true>, dim3(grid), dim3(64), 0, s, r, v, mask, B, L, g, gl, adv, ret,
+                       row_stats);
+  else if (variant == 0)
+    hipLaunchKernelGGL(gae_legacy_kernel<false>, dim3(grid), dim3(64), 0, s, r, v, mask, B, L, g, gl, adv, ret,
+                       row_stats);
+  else if (nt)
+    hipLaunchKernelGGL((gae_kernel<1, true>), dim3(grid), dim3(64), 0, s, r, v, mask, B, L, g, gl, adv, ret, row_stats);
   else
-    hipLaunchKernelGGL(gae_kernel<1>, dim3(grid), dim3(64), 0, as_stream(stream), r, v, mask, B, L, g, gl, adv, ret,
+    hipLaunchKernelGGL((gae_kernel<1, false>), dim3(grid), dim3(64), 0, s, r, v, mask, B, L, g, gl, adv, ret,
                        row_stats);
   return launch_status();
 }
@@ -1270,12 +1313,22 @@ RMI_API int rmi_bilevel_gae(const float* r, const float* v, const uint8_t* mask,
   const float g = (float)gamma, gl = (float)(gamma * lam), hg = (float)high_level_gamma,
               hgl = (float)(high_level_gamma * lam);
   const int64_t lds = bs_lds_bytes(L);
-  if (lds <= kBsMaxLds && !bilevel_force_tiled())
-    hipLaunchKernelGGL(bilevel_seg_kernel, grid, dim3(64), (unsigned)lds, as_stream(stream), r, v, mask, B, L, g, gl,
-                       hg, hgl, adv, ret, row_stats, err);
-  else
-    hipLaunchKernelGGL(bilevel_tiled_kernel, grid, dim3(64), 0, as_stream(stream), r, v, mask, B, L, g, gl, hg, hgl,
-                       adv, ret, row_stats, err);
+  const bool nt = (double)B * (double)L * 17.0 > kStreamBytes;
+  hipStream_t s = as_stream(stream);
+  if (lds <= kBsMaxLds && !bilevel_force_tiled()) {
+    if (nt)
+      hipLaunchKernelGGL(bilevel_seg_kernel<true>, grid, dim3(64), (unsigned)lds, s, r, v, mask, B, L, g, gl, hg, hgl,
+                         adv, ret, row_stats, err);
+    else
+      hipLaunchKernelGGL(bilevel_seg_kernel<false>, grid, dim3(64), (unsigned)lds, s, r, v, mask, B, L, g, gl, hg,
+                         hgl, adv, ret, row_stats, err);
+  } else if (nt) {
+    hipLaunchKernelGGL(bilevel_tiled_kernel<true>, grid, dim3(64), 0, s, r, v, mask, B, L, g, gl, hg, hgl, adv, ret,
+                       row_stats, err);
+  } else {
+    hipLaunchKernelGGL(bilevel_tiled_kernel<false>, grid, dim3(64), 0, s, r, v, mask, B, L, g, gl, hg, hgl, adv, ret,
+                       row_stats, err);
+  }
   return launch_status();
 }
 
@@ -1352,7 +1405,7 @@ RMI_API int rmi_reinforce_pp_returns(const float* r, const uint8_t* mask, int64_
   if (B == 0 || L == 0) return RMI_OK;
   const unsigned grid = (unsigned)((B + kGRows - 1) / kGRows);
   // v is not part of this recurrence: r stands in for it (read, never used)
-  hipLaunchKernelGGL(gae_kernel<2>, dim3(grid), dim3(64), 0, as_stream(stream), r, r, mask, B, L, (float)gamma, 0.0f,
+  hipLaunchKernelGGL((gae_kernel<2, false>), dim3(grid), dim3(64), 0, as_stream(stream), r, r, mask, B, L, (float)gamma, 0.0f,
                      adv, ret, row_stats, nullptr);
   return launch_status();
 }
@@ -1363,7 +1416,7 @@ RMI_API int rmi_remax(const float* r, const uint8_t* mask, const float* baseline
   if (!r || !mask || !baseline || !adv || !ret || B < 0 || L < 0) return RMI_EINVAL;
   if (B == 0 || L == 0) return RMI_OK;
   const unsigned grid = (unsigned)((B + kGRows - 1) / kGRows);
-  hipLaunchKernelGGL(gae_kernel<3>, dim3(grid), dim3(64), 0, as_stream(stream), r, r, mask, B, L, 0.0f, 0.0f, adv,
+  hipLaunchKernelGGL((gae_kernel<3, false>), dim3(grid), dim3(64), 0, as_stream(stream), r, r, mask, B, L, 0.0f, 0.0f, adv,
                      ret, nullptr, baseline);
   return launch_status();
 }

@@ -1077,3 +1077,32 @@ def test_frozenlake_fast_and_generic_paths_vs_oracle(device, slippery, bad_waves
                 np.testing.assert_array_equal(h[k][ok], getattr(oep, k)[ok], err_msg=f"K={K} t={t} {k}")
             for k in ("turn_reward", "turn_info", "turn_exec"):
                 np.testing.assert_array_equal(h[k][:, ok], getattr(oep, k)[:, ok], err_msg=f"K={K} t={t} {k}")
+
+
+@pytest.mark.parametrize("kind", ["gae", "bilevel_seg", "bilevel_tiled"])
+def test_streamed_launches_vs_oracle(device, monkeypatch, kind):
+    """Launches whose traffic passes 256 MiB (8192 x 2112 tokens, 294 MB) take the nontemporal
+    load / store forms of the GAE and bi-level kernels (advantage.hip, kStreamBytes): the same
+    results as the oracle, bit for bit."""
+    B, L = 8192, 2112
+    rng = np.random.default_rng(77)
+    n_turns = rng.integers(1, 6, B).astype(np.int32)
+    tr = rng.choice([0.5, -1.1, 10.9], size=(B, 5)).astype(np.float32)
+    r, v, m = synthetic.token_rows(n_turns, rng.standard_normal(B).astype(np.float32), seed=5, turn_scores=tr,
+                                   max_len=L)
+    assert r.shape[1] * B * 17 > 256 * 1024 * 1024
+    rd, vd, md = _t(r, device), _t(v, device), _t(m, device)
+    if kind == "gae":
+        for variant, (g, lam) in (("legacy", (1.0, 1.0)), ("masked", (0.99, 0.95))):
+            adv, ret = ops.gae(rd, vd, md, g, lam, variant)
+            oadv, oret = oracle.gae(r, v, m, g, lam, variant)
+            np.testing.assert_array_equal(ret.cpu().numpy(), oret)
+            np.testing.assert_array_equal(adv.cpu().numpy(), oadv)
+        return
+    if kind == "bilevel_tiled":
+        monkeypatch.setenv("RAGEN_AMD_BILEVEL_TILED", "1")
+    oa, oret, oerr = oracle.bilevel_gae(r, v, m, 0.99, 0.95, 0.9)
+    adv, ret = ops.bilevel_gae(rd, vd, md, 0.99, 0.95, 0.9, check_errors=False)
+    ok = oerr == 0
+    np.testing.assert_array_equal(ret.cpu().numpy()[ok], oret[ok])
+    np.testing.assert_array_equal(adv.cpu().numpy()[ok], oa[ok])
