@@ -37,6 +37,10 @@ class BatchEnv:
     def reset(self, seeds) -> None:
         raise NotImplementedError
 
+    def prefetch(self, seeds) -> None:
+        """Hint: a later reset(seeds) will follow.  Envs whose reset does host work may start it
+        in the background; the state reset() produces must not depend on whether it did."""
+
     def step_turn(self, turn: int, actions: torch.Tensor, n_actions: torch.Tensor, has_input: Optional[torch.Tensor],
                   max_actions_per_traj: int, format_penalty: float, err: Optional[torch.Tensor] = None,
                   **kw) -> None:

@@ -1,4 +1,5 @@
 """Batched Sokoban (replaces ragen/env/sokoban/env.py + gym_sokoban step, App. A.1)."""
+import threading
 from typing import Optional
 
 import numpy as np
@@ -58,16 +59,54 @@ class SokobanBatch(BatchEnv):
                 raise RuntimeError(f"Sokoban generation failed repeatedly for seed {uniq[i]}")
         return fixed[inv], state[inv], player[inv]
 
+    def prefetch(self, seeds):
+        """Generate the rooms of a later reset(seeds) on host threads in the background (the
+        generator releases the GIL; one core stays with the caller).  reset() with the same
+        seeds takes them; other seeds generate afresh.  Rooms are a pure function of the seed,
+        so the state after reset() is the same either way."""
+        seeds = np.asarray(seeds, np.int64).copy()
+        c = self.config
+        box = {}
+        n = max(1, ops.host_threads() - 1)
+
+        def run():
+            try:
+                box["rooms"] = self.generate(seeds, self.H, self.W, int(c.num_boxes), int(c.search_depth), n)
+            except BaseException as e:  # re-raised by the reset() that takes these rooms
+                box["error"] = e
+
+        th = threading.Thread(target=run, name="sokoban-prefetch", daemon=True)
+        th.start()
+        self._prefetched = (seeds, th, box)
+
+    def _rooms(self, seeds):
+        c = self.config
+        pf, self._prefetched = getattr(self, "_prefetched", None), None
+        if pf is not None:
+            pseeds, th, box = pf
+            th.join()
+            if pseeds.shape == seeds.shape and np.array_equal(pseeds, seeds):
+                if "error" in box:
+                    raise box["error"]
+                return box["rooms"]
+        return self.generate(seeds, self.H, self.W, int(c.num_boxes), int(c.search_depth))
+
     def reset(self, seeds):
         self.seeds = np.asarray(seeds, np.int64).copy()
-        c = self.config
-        fixed, state, player = self.generate(self.seeds, self.H, self.W, int(c.num_boxes), int(c.search_depth))
+        fixed, state, player = self._rooms(self.seeds)
         self.load_state(fixed, state, player)
 
     def load_state(self, fixed, state, player):
-        self.room_fixed.copy_(torch.from_numpy(np.ascontiguousarray(fixed)))
-        self.init_state.copy_(torch.from_numpy(np.ascontiguousarray(state)))
-        self.init_player.copy_(torch.from_numpy(np.ascontiguousarray(player)))
+        # one pinned upload of [fixed | state | player] rows, then three device copies
+        B, HW = self.B, self.H * self.W
+        buf = np.empty((B, 2 * HW + 2), np.uint8)
+        buf[:, :HW] = np.asarray(fixed).reshape(B, HW)
+        buf[:, HW:2 * HW] = np.asarray(state).reshape(B, HW)
+        buf[:, 2 * HW:] = np.asarray(player, np.int8).reshape(B, 2).view(np.uint8)
+        d = ops.h2d(buf, self.device)
+        self.room_fixed.copy_(d[:, :HW])
+        self.init_state.copy_(d[:, HW:2 * HW])
+        self.init_player.copy_(d[:, 2 * HW:].view(torch.int8))
         self.restore()
 
     # ---- the custom ops (torch.ops.ragen_amd.*) over this batch's tensors

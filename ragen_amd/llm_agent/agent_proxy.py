@@ -62,12 +62,15 @@ class TokenActor:
             self.prompt_shapes.append(tuple(b["input_ids"].shape))
             self.prompts.append((b["input_ids"], b["attention_mask"], b["position_ids"]))
         tok = self.turn_tokens[self.turn]
-        local = env_ids - self.env_lo
-        if len(local) == tok.shape[0] and np.array_equal(local, np.arange(len(local))):
+        if env_ids is not getattr(self, "_ids_seen", None) or tok.shape[0] != self._ids_n:
+            local = env_ids - self.env_lo  # (the manager hands the same array each turn)
+            self._ids_seen, self._ids_n = env_ids, tok.shape[0]
+            self._ids_all = len(local) == tok.shape[0] and np.array_equal(local, np.arange(len(local)))
+        if self._ids_all:
             resp = tok  # every env, in order
         else:
             from .. import ops
-            resp = tok[ops.h2d(local, tok.device)]
+            resp = tok[ops.h2d(env_ids - self.env_lo, tok.device)]
         self.turn += 1
         return DataProto({"responses": resp}, {"env_ids": env_ids}, {})
 

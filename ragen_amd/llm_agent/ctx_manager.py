@@ -695,16 +695,19 @@ class ContextManager:
     def _device_env_inputs(self, lm_outputs: DataProto) -> DeviceEnvInputs:
         vocab = self.device_vocab
         dev = self.device
-        resp = lm_outputs.batch["responses"].to(dev)
+        resp = lm_outputs.batch["responses"]
+        if resp.device != dev or resp.dtype != torch.int64 or not resp.is_contiguous():
+            resp = resp.to(dev, torch.int64).contiguous()
         env_ids = np.asarray(lm_outputs.non_tensor_batch["env_ids"], dtype=np.int64)
         R = resp.shape[1]
         lo, n = self.env_lo, self.n_envs
-        resp = resp.to(torch.int64).contiguous()
+        es = getattr(self, "_es", None)
+        in_order = es is not None and env_ids is es._ids_in_order  # reset()'s own array: every env, in order
         # the turn's readback buffer, allocated here so rmi_gen_rows writes the longest
         # generation's raw bytes straight into it (EnvStateManager._device_pass reads it back)
         pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
         raw = ops.readback_raw(pack, n)
-        if len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n)):
+        if in_order or (len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n))):
             # every env in order: the generations are the rows (n_ids = None: R ids each)
             has_t, n_ids, ids = None, None, resp
             direct.gen_rows(resp, None, n, vocab.packed, None, None, raw)

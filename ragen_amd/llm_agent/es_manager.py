@@ -179,6 +179,10 @@ def _hostbook():
 
 
 class EnvStateManager:
+    # reset() with a drawn train seed starts the next reset's host work (Sokoban room
+    # generation) in the background, for the seed random will draw next
+    prefetch_resets = True
+
     def __init__(self, config, mode: str = "train", device=None, rank: Optional[int] = None,
                  world_size: Optional[int] = None, process_group=None):
         self.sys_config = config
@@ -207,6 +211,7 @@ class EnvStateManager:
         self._formulated = False      # the device formulate_rollouts ran: drop the last states when built
         self._untrimmed = None
         self.rollout_id = 0
+        self._ids_in_order = None  # the env-id array reset() handed out (all envs, in order)
         self._turn = 0
         self._all_active = False
         self.reset_render = None
@@ -284,11 +289,21 @@ class EnvStateManager:
 
     def reset(self, seed: Optional[int] = None):
         """es_manager.py:75-103."""
+        drawn = self.mode == "train" and seed is None and self.process_group is None
         seed = self._train_seed(seed) if self.mode == "train" else 123
         gids = self.env_lo + np.arange(self.n_envs)
         seeds = seed + gids // self.group_size  # _expand_seed, global ids
         for t in self.tags:
             t.batch.reset(seeds[t.lo - self.env_lo:t.hi - self.env_lo])
+        if self.prefetch_resets and drawn:
+            # the next reset()'s train seed, peeked without drawing it (random's state is put
+            # back): the envs start that reset's host work now, behind this rollout's turns.  A
+            # different seed then (random drawn from in between) only costs the prefetch.
+            st = random.getstate()
+            nxt = seeds - seed + random.randint(0, 1000000)
+            random.setstate(st)
+            for t in self.tags:
+                t.batch.prefetch(nxt[t.lo - self.env_lo:t.hi - self.env_lo])
         self._turn = 0
         self._turn_records = []
         self._mat_upto = 0
@@ -306,7 +321,8 @@ class EnvStateManager:
             self._reset_rows = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags)
                                 if type(tg.batch).render is BatchEnv.render}
             self.reset_render = (self.rollout_id, self._reset_rows)
-            return LazyEnvOutputs(self, self.env_lo + np.arange(self.n_envs, dtype=np.int64))
+            self._ids_in_order = self.env_lo + np.arange(self.n_envs, dtype=np.int64)
+            return LazyEnvOutputs(self, self._ids_in_order)
         self._reset_rows = None
         self._reset_cache()
         return self._rc
@@ -634,15 +650,19 @@ class EnvStateManager:
             bad = int(np.nonzero(dec_h)[0][0])
             raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
                              "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP); its env was not stepped")
-        still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
-        self._all_active = n_in == self.n_envs and bool(still.all())
+        if inp.env_ids is self._ids_in_order:  # every env, in order (no gather)
+            still = (fl_h & _lib.FLAG_DONE) == 0
+        else:
+            still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
+        all_still = bool(still.all())
+        self._all_active = n_in == self.n_envs and all_still
         if err_h.any():
             for tg in self.tags:
                 gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]
                 self._raise_errors(tg, err_h[tg.lo - self.env_lo:tg.hi - self.env_lo], [g - tg.lo for g in gids],
                                    gids)
             self._turn_records[-1]["err_seen"] = True
-        return LazyEnvOutputs(self, inp.env_ids[still])
+        return LazyEnvOutputs(self, inp.env_ids if all_still else inp.env_ids[still])
 
     def _device_pass(self, inp, t, first):
         """The device launches of one pass of turn t over the envs with a generation in ``inp``

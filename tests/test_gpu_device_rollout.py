@@ -91,3 +91,34 @@ def test_device_step_undecodable_generation_raises_unstepped(device, monkeypatch
         es.step(env_inputs)
     n_turns = es.tags[0].batch.ep.n_turns.cpu().numpy()
     assert n_turns[5] == 0 and (np.delete(n_turns, 5) == 1).all()
+
+
+@pytest.mark.parametrize("draw_between", [False, True])
+def test_reset_prefetch_gives_the_same_rooms(device, monkeypatch, draw_between):
+    """EnvStateManager.reset with a drawn train seed starts the next reset's room generation in
+    the background (for the seed random will draw next, peeked without drawing it).  Two resets
+    give the same rooms with and without the prefetch, also when random is drawn from in between
+    (then the prefetch is for another seed and not taken)."""
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok()
+    got = {}
+    for pf in (False, True):
+        proxy = LLMAgentProxy(_config("sokoban_es"), TokenActor(_turn_tokens("sokoban_es", tok, device)), tok,
+                              device=device)
+        es = proxy.train_es_manager
+        es.prefetch_resets = pf
+        random.seed(11)
+        rooms = []
+        for _ in range(3):
+            es.reset()
+            b = es.tags[0].batch
+            assert (getattr(b, "_prefetched", None) is not None) == pf
+            rooms.append([x.cpu().numpy().copy() for x in (b.room_fixed, b.init_state, b.init_player)])
+            if draw_between:
+                random.random()
+        got[pf] = (rooms, random.random())
+    for a, b in zip(got[False][0], got[True][0]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    assert got[False][1] == got[True][1]  # the peek leaves random's sequence alone

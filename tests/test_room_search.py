@@ -34,3 +34,39 @@ def test_fast_search_equals_string_search(H, W, nb, sd, n):
     ref = _gen(seeds, H, W, nb, sd, True)
     for a, b in zip(fast, ref):
         np.testing.assert_array_equal(a, b)
+
+
+def _batch(H=6, W=6, nb=1, sd=100):
+    from ragen_amd.env.configs import SokobanEnvConfig
+    from ragen_amd.env.sokoban import SokobanBatch
+    b = object.__new__(SokobanBatch)  # the host side of reset() only (no device tensors)
+    b.config = SokobanEnvConfig(dim_x=W, dim_y=H, num_boxes=nb, search_depth=sd)
+    b.H, b.W = H, W
+    return b
+
+
+def test_prefetched_rooms_equal_generated():
+    """SokobanBatch.prefetch: the rooms a prefetch made are the ones reset() would generate; a
+    reset with other seeds ignores them and generates its own."""
+    from ragen_amd.env.sokoban import SokobanBatch
+    b = _batch()
+    seeds = np.repeat(np.arange(40, dtype=np.int64) + 5000, 4)
+    want = SokobanBatch.generate(seeds, 6, 6, 1, 100)
+    b.prefetch(seeds)
+    for x, y in zip(b._rooms(seeds.copy()), want):
+        np.testing.assert_array_equal(x, y)
+    assert b._prefetched is None
+    other = seeds + 1
+    b.prefetch(seeds)
+    for x, y in zip(b._rooms(other), SokobanBatch.generate(other, 6, 6, 1, 100)):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_prefetch_error_raised_by_the_reset_that_takes_it():
+    b = _batch()
+    bad = np.array([2 ** 33], np.int64)
+    b.prefetch(bad)
+    with pytest.raises(ValueError):
+        b._rooms(bad)
+    b.prefetch(bad)  # not taken: the other seeds generate, the prefetch's error is dropped
+    assert b._rooms(np.array([7], np.int64))[0].shape == (1, 36)
