@@ -655,8 +655,8 @@ def api_leg(device):
     proxy = LLMAgentProxy(cfg, actor, tok, device=device)
     proxy.train_ctx_manager.set_device_vocab(ops.VocabTable.from_tokenizer(tok, device))
     runs = []
+    random.seed(0)  # one train-seed sequence, as a training loop draws it (reset() prefetches the next rooms)
     for rep in range(4):
-        random.seed(rep)
         actor.turn = 0
         actor.prompts, actor.prompt_shapes = [], []
         torch.cuda.synchronize()
@@ -664,14 +664,16 @@ def api_leg(device):
         torch.cuda.synchronize()
         steps = int(proxy.train_es_manager.tags[0].batch.ep.turn_exec.sum().item())
         runs.append((steps, dict(proxy.last_timing), len(out), list(actor.prompt_shapes),
-                     tuple(out.batch["input_ids"].shape)))
+                     tuple(out.batch["input_ids"].shape),
+                     bool(getattr(proxy.train_es_manager.tags[0].batch, "reset_prefetched", False))))
     pr = proxy.train_ctx_manager.prompts()
-    steps, tm, rows, shapes, upd = runs[-1]
+    steps, tm, rows, shapes, upd, prefetched = runs[-1]
     total = tm["turns_s"] + tm["rollout_states_s"] + tm["formulate_s"]
     device_path = {"env_steps": steps, "turn_loop_s": tm["turns_s"], "get_rollout_states_s": tm["rollout_states_s"],
                    "formulate_rollouts_s": tm["formulate_s"], "rollout_s": total, "env_steps_per_s": steps / total,
                    "turn_loop_env_steps_per_s": steps / tm["turns_s"], "rows_formulated": rows,
                    "reset_s": tm["reset_s"],  # es.reset(): rooms for a fresh train seed (host) + device restore
+                   "reset_rooms_prefetched": prefetched,  # generated behind the previous rollout (SokobanBatch.prefetch)
                    "env_steps_per_s_with_reset": steps / (total + tm["reset_s"]),
                    "readbacks": tm.get("readbacks"), "turns": len(shapes),
                    "eager_prompt_turns": pr.eager_turns if pr is not None else None,

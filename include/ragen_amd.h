@@ -154,6 +154,17 @@ int rmi_sokoban_generate_rooms(const int64_t* seeds /*[host][n]*/, int32_t n, in
                                int8_t* player /*[host][n,2]*/, uint8_t* status /*[host][n]*/,
                                int32_t n_threads);
 
+/* rmi_sokoban_generate_rooms on a host thread of its own (the generation of a later reset, behind
+ * the current rollout): returns a job handle (NULL: could not start) at once; every buffer must
+ * stay valid until rmi_sokoban_generate_rooms_wait(job), which joins it, frees the handle and
+ * returns rmi_sokoban_generate_rooms' result.  Every started job is waited on exactly once. */
+typedef struct rmi_rooms_job rmi_rooms_job;
+rmi_rooms_job* rmi_sokoban_generate_rooms_start(const int64_t* seeds /*[host][n]*/, int32_t n, int32_t H,
+                                                int32_t W, int32_t num_boxes, int32_t search_depth,
+                                                uint8_t* room_fixed, uint8_t* room_state, int8_t* player,
+                                                uint8_t* status, int32_t n_threads);
+int rmi_sokoban_generate_rooms_wait(rmi_rooms_job* job);
+
 /* Replaces: SokobanEnv.render text mode (sokoban/env.py:53-61): room_state, the player on a
  * target shown as code 6, each code through the config's grid_lookup, rows joined by '\n'.
  * glyph_bytes[16] / glyph_len[16] (HOST memory): UTF-8 bytes of each code packed little-endian,

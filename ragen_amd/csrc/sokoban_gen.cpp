@@ -20,6 +20,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
 #include <thread>
 #include <unordered_set>
 #include <vector>
@@ -552,4 +553,35 @@ RMI_HOST_API int rmi_sokoban_generate_rooms(const int64_t* seeds, int32_t n, int
     for (auto& x : th) x.join();
   }
   return 0;
+}
+
+struct rmi_rooms_job {
+  std::thread th;
+  int rc = 0;
+};
+
+RMI_HOST_API rmi_rooms_job* rmi_sokoban_generate_rooms_start(const int64_t* seeds, int32_t n, int32_t H, int32_t W,
+                                                             int32_t num_boxes, int32_t search_depth,
+                                                             uint8_t* room_fixed, uint8_t* room_state, int8_t* player,
+                                                             uint8_t* status, int32_t n_threads) {
+  rmi_rooms_job* j = new (std::nothrow) rmi_rooms_job;
+  if (!j) return nullptr;
+  try {
+    j->th = std::thread([=] {
+      j->rc = rmi_sokoban_generate_rooms(seeds, n, H, W, num_boxes, search_depth, room_fixed, room_state, player,
+                                         status, n_threads);
+    });
+  } catch (...) {
+    delete j;
+    return nullptr;
+  }
+  return j;
+}
+
+RMI_HOST_API int rmi_sokoban_generate_rooms_wait(rmi_rooms_job* job) {
+  if (!job) return -1;
+  job->th.join();
+  const int rc = job->rc;
+  delete job;
+  return rc;
 }

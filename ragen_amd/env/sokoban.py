@@ -1,5 +1,4 @@
 """Batched Sokoban (replaces ragen/env/sokoban/env.py + gym_sokoban step, App. A.1)."""
-import threading
 from typing import Optional
 
 import numpy as np
@@ -42,11 +41,22 @@ class SokobanBatch(BatchEnv):
     # (hash() of a str depends on PYTHONHASHSEED — exactly as in the reference process.)
     reseed_fn = staticmethod(lambda s: abs(hash(str(s))) % (2 ** 32))
 
-    @classmethod
-    def generate(cls, seeds, H, W, num_boxes, search_depth, n_threads=0):
+    @staticmethod
+    def _distinct(seeds):
+        """-> (distinct seeds, inv).  reset()'s seeds come sorted (seed + group id): no sort."""
         seeds = np.asarray(seeds, np.int64)
-        uniq, inv = np.unique(seeds, return_inverse=True)
-        fixed, state, player, status = ops.generate_sokoban_rooms(uniq, H, W, num_boxes, search_depth, n_threads)
+        if seeds.size and (seeds[1:] >= seeds[:-1]).all():
+            first = np.empty(seeds.size, bool)
+            first[0] = True
+            np.not_equal(seeds[1:], seeds[:-1], out=first[1:])
+            return seeds[first], np.cumsum(first) - 1
+        return np.unique(seeds, return_inverse=True)
+
+    @classmethod
+    def _finish(cls, uniq, rooms, H, W, num_boxes, search_depth):
+        """The generator's output for the distinct seeds -> rows u8[U, 2HW+2] (fixed | state |
+        player bytes); a seed the reference would reject is reseeded (sokoban/env.py:41)."""
+        fixed, state, player, status = rooms
         for i in np.nonzero(status)[0]:
             s = int(uniq[i])
             for _ in range(64):
@@ -57,53 +67,78 @@ class SokobanBatch(BatchEnv):
                     break
             else:
                 raise RuntimeError(f"Sokoban generation failed repeatedly for seed {uniq[i]}")
-        return fixed[inv], state[inv], player[inv]
+        HW = H * W
+        rows = np.empty((len(uniq), 2 * HW + 2), np.uint8)
+        rows[:, :HW], rows[:, HW:2 * HW], rows[:, 2 * HW:] = fixed, state, player.view(np.uint8)
+        return rows
+
+    @classmethod
+    def generate_unique(cls, seeds, H, W, num_boxes, search_depth, n_threads=0):
+        """Each distinct seed's room once -> (rows u8[U, 2HW+2] = fixed | state | player bytes,
+        inv i64[B]: every env's row)."""
+        uniq, inv = cls._distinct(seeds)
+        rooms = ops.generate_sokoban_rooms(uniq, H, W, num_boxes, search_depth, n_threads)
+        return cls._finish(uniq, rooms, H, W, num_boxes, search_depth), inv
+
+    @classmethod
+    def generate(cls, seeds, H, W, num_boxes, search_depth, n_threads=0):
+        """-> (fixed u8[B, HW], state u8[B, HW], player i8[B, 2]) for every seed."""
+        rows, inv = cls.generate_unique(seeds, H, W, num_boxes, search_depth, n_threads)
+        r = np.take(rows, inv, axis=0)
+        HW = H * W
+        return (np.ascontiguousarray(r[:, :HW]), np.ascontiguousarray(r[:, HW:2 * HW]),
+                np.ascontiguousarray(r[:, 2 * HW:]).view(np.int8))
 
     def prefetch(self, seeds):
-        """Generate the rooms of a later reset(seeds) on host threads in the background (the
-        generator releases the GIL; one core stays with the caller).  reset() with the same
-        seeds takes them; other seeds generate afresh.  Rooms are a pure function of the seed,
-        so the state after reset() is the same either way."""
+        """Start generating the rooms of a later reset(seeds) on a native host thread
+        (ops.RoomsJob; one core stays with the caller).  reset() with the same seeds takes them;
+        other seeds generate afresh.  Rooms are a pure function of the seed, so the state after
+        reset() is the same either way."""
         seeds = np.asarray(seeds, np.int64).copy()
         c = self.config
-        box = {}
-        n = max(1, ops.host_threads() - 1)
-
-        def run():
-            try:
-                box["rooms"] = self.generate(seeds, self.H, self.W, int(c.num_boxes), int(c.search_depth), n)
-            except BaseException as e:  # re-raised by the reset() that takes these rooms
-                box["error"] = e
-
-        th = threading.Thread(target=run, name="sokoban-prefetch", daemon=True)
-        th.start()
-        self._prefetched = (seeds, th, box)
+        uniq, inv = self._distinct(seeds)
+        job = ops.RoomsJob(uniq, self.H, self.W, int(c.num_boxes), int(c.search_depth),
+                           max(1, ops.host_threads() - 1))
+        self._prefetched = (seeds, uniq, inv, job)
 
     def _rooms(self, seeds):
+        """-> generate_unique(seeds): from the prefetch for these seeds if there is one."""
         c = self.config
+        dims = (self.H, self.W, int(c.num_boxes), int(c.search_depth))
         pf, self._prefetched = getattr(self, "_prefetched", None), None
+        self.reset_prefetched = False  # (whether the last reset took prefetched rooms)
         if pf is not None:
-            pseeds, th, box = pf
-            th.join()
+            pseeds, uniq, inv, job = pf
             if pseeds.shape == seeds.shape and np.array_equal(pseeds, seeds):
-                if "error" in box:
-                    raise box["error"]
-                return box["rooms"]
-        return self.generate(seeds, self.H, self.W, int(c.num_boxes), int(c.search_depth))
+                rows = self._finish(uniq, job.wait(), *dims)
+                self.reset_prefetched = True
+                return rows, inv
+            try:
+                job.wait()  # not taken (its error, if any, with it)
+            except ValueError:
+                pass
+        return self.generate_unique(seeds, *dims)
 
     def reset(self, seeds):
         self.seeds = np.asarray(seeds, np.int64).copy()
-        fixed, state, player = self._rooms(self.seeds)
-        self.load_state(fixed, state, player)
+        rows, inv = self._rooms(self.seeds)
+        # the distinct rooms and every env's row in them uploaded (pinned), expanded on the device
+        d = ops.h2d(rows, self.device)
+        if len(rows) != self.B or not np.array_equal(inv, np.arange(self.B)):
+            d = d.index_select(0, ops.h2d(inv, self.device))
+        self._load_rows(d)
 
     def load_state(self, fixed, state, player):
-        # one pinned upload of [fixed | state | player] rows, then three device copies
         B, HW = self.B, self.H * self.W
         buf = np.empty((B, 2 * HW + 2), np.uint8)
         buf[:, :HW] = np.asarray(fixed).reshape(B, HW)
         buf[:, HW:2 * HW] = np.asarray(state).reshape(B, HW)
         buf[:, 2 * HW:] = np.asarray(player, np.int8).reshape(B, 2).view(np.uint8)
-        d = ops.h2d(buf, self.device)
+        self._load_rows(ops.h2d(buf, self.device))
+
+    def _load_rows(self, d):
+        """d u8[B, 2HW+2] on the device: [fixed | state | player] per env."""
+        HW = self.H * self.W
         self.room_fixed.copy_(d[:, :HW])
         self.init_state.copy_(d[:, HW:2 * HW])
         self.init_player.copy_(d[:, 2 * HW:].view(torch.int8))

@@ -321,6 +321,37 @@ def generate_sokoban_rooms(seeds, H: int, W: int, num_boxes: int, search_depth: 
     return fixed, state, player, status
 
 
+class RoomsJob:
+    """generate_sokoban_rooms on a native host thread (rmi_sokoban_generate_rooms_start): no
+    Python thread and no GIL held while it runs.  wait() -> (fixed, state, player, status)."""
+
+    def __init__(self, seeds, H: int, W: int, num_boxes: int, search_depth: int, n_threads: int = 0):
+        import numpy as np
+        self.seeds = np.ascontiguousarray(np.asarray(seeds, dtype=np.int64))
+        n = self.seeds.shape[0]
+        self.out = (np.zeros((n, H * W), np.uint8), np.zeros((n, H * W), np.uint8), np.zeros((n, 2), np.int8),
+                    np.zeros(n, np.uint8))
+        f, st, p, ok = self.out
+        self._job = lib().rmi_sokoban_generate_rooms_start(self.seeds.ctypes.data, n, H, W, num_boxes, search_depth,
+                                                           f.ctypes.data, st.ctypes.data, p.ctypes.data,
+                                                           ok.ctypes.data, n_threads or host_threads())
+        if not self._job:
+            raise RuntimeError("rmi_sokoban_generate_rooms_start: could not start a host thread")
+
+    def wait(self):
+        job, self._job = self._job, None
+        if job is None:
+            raise RuntimeError("RoomsJob.wait: already waited on")
+        if lib().rmi_sokoban_generate_rooms_wait(job) != 0:
+            raise ValueError("rmi_sokoban_generate_rooms: invalid arguments (seeds must be in [0, 2**32))")
+        return self.out
+
+    def __del__(self):  # a job nobody took: joined before its buffers go
+        if getattr(self, "_job", None):
+            lib().rmi_sokoban_generate_rooms_wait(self._job)
+            self._job = None
+
+
 # ------------------------------------------------------------------- episode reductions
 def rollout_metrics(ep: EpisodeState) -> torch.Tensor:
     out = torch.empty(ep.B, 4, dtype=torch.float64, device=ep.flags.device)

@@ -51,15 +51,33 @@ def test_prefetched_rooms_equal_generated():
     from ragen_amd.env.sokoban import SokobanBatch
     b = _batch()
     seeds = np.repeat(np.arange(40, dtype=np.int64) + 5000, 4)
-    want = SokobanBatch.generate(seeds, 6, 6, 1, 100)
+    want = SokobanBatch.generate_unique(seeds, 6, 6, 1, 100)
     b.prefetch(seeds)
     for x, y in zip(b._rooms(seeds.copy()), want):
         np.testing.assert_array_equal(x, y)
-    assert b._prefetched is None
+    assert b._prefetched is None and b.reset_prefetched
     other = seeds + 1
     b.prefetch(seeds)
-    for x, y in zip(b._rooms(other), SokobanBatch.generate(other, 6, 6, 1, 100)):
+    for x, y in zip(b._rooms(other), SokobanBatch.generate_unique(other, 6, 6, 1, 100)):
         np.testing.assert_array_equal(x, y)
+    assert not b.reset_prefetched
+
+
+@pytest.mark.parametrize("order", ["sorted", "shuffled"])
+def test_generate_unique_expands_to_per_seed_rooms(order):
+    """generate_unique (each distinct seed once; sorted seeds without a sort) expanded by its
+    inverse = the generator run on every seed."""
+    from ragen_amd.env.sokoban import SokobanBatch
+    seeds = np.repeat(np.arange(30, dtype=np.int64) * 13 + 7, 3)
+    if order == "shuffled":
+        seeds = np.random.default_rng(0).permutation(seeds)
+    f, s_, p, st = ops.generate_sokoban_rooms(seeds, 6, 6, 1, 100, 2)
+    assert not st.any()
+    rows, inv = SokobanBatch.generate_unique(seeds, 6, 6, 1, 100)
+    assert len(rows) == 30
+    for x, y in zip(SokobanBatch.generate(seeds, 6, 6, 1, 100), (f, s_, p)):
+        np.testing.assert_array_equal(x, y)
+    np.testing.assert_array_equal(rows[inv, :36], f)
 
 
 def test_prefetch_error_raised_by_the_reset_that_takes_it():
@@ -69,4 +87,19 @@ def test_prefetch_error_raised_by_the_reset_that_takes_it():
     with pytest.raises(ValueError):
         b._rooms(bad)
     b.prefetch(bad)  # not taken: the other seeds generate, the prefetch's error is dropped
-    assert b._rooms(np.array([7], np.int64))[0].shape == (1, 36)
+    assert b._rooms(np.array([7], np.int64))[0].shape == (1, 74)  # fixed | state | player
+
+
+def test_rooms_job_equals_the_synchronous_generator():
+    """ops.RoomsJob (rmi_sokoban_generate_rooms_start / _wait: the generator on a native host
+    thread) writes the rooms the synchronous call writes; a job never waited on is joined when
+    it is dropped."""
+    seeds = np.arange(64, dtype=np.int64) * 31 + 11
+    job = ops.RoomsJob(seeds, 6, 6, 1, 100, 3)
+    for x, y in zip(job.wait(), ops.generate_sokoban_rooms(seeds, 6, 6, 1, 100, 2)):
+        np.testing.assert_array_equal(x, y)
+    with pytest.raises(RuntimeError):
+        job.wait()
+    ops.RoomsJob(seeds, 6, 6, 1, 100, 2)  # dropped at once: __del__ joins it
+    with pytest.raises(ValueError):
+        ops.RoomsJob(np.array([-1], np.int64), 6, 6, 1, 100).wait()
