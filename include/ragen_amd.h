@@ -143,6 +143,16 @@ int rmi_sokoban_step_turn_first(const rmi_sokoban_t* env, const rmi_episode_t* e
 int rmi_sokoban_reset(const rmi_sokoban_t* env, const rmi_episode_t* ep, const uint8_t* init_state,
                       const int8_t* init_player, rmi_stream_t stream);
 
+/* rmi_sokoban_reset from the distinct generated rooms, in one launch: env i takes row
+ * room_of[i] (NULL: row i) of rooms u8[n_rooms, 2*H*W+2] (device; per row room_fixed |
+ * room_state | player as int8 bytes) into env->room_fixed, init_state u8[B, H*W] and init_player
+ * i8[B, 2] (kept for a later rmi_sokoban_reset), then room_state / player := those, counters and
+ * the whole episode record zeroed.  A row index outside [0, n_rooms) loads an empty room and
+ * sets RMI_ERR_INDEX in err u8[B] (optional; else 0 per env).                                */
+int rmi_sokoban_load_rooms(const rmi_sokoban_t* env, const rmi_episode_t* ep, const uint8_t* rooms,
+                           int32_t n_rooms, const int32_t* room_of, uint8_t* init_state, int8_t* init_player,
+                           uint8_t* err, rmi_stream_t stream);
+
 /* Replaces: SokobanEnv.reset (sokoban/env.py:28-42) -> generate_room (sokoban/utils.py:221-278)
  * under all_seed (ragen/utils.py:7-18).  [host] CPU function: exact CPython-random /
  * numpy-legacy MT19937 semantics.  Writes one room per seed.  Returns per seed

@@ -110,6 +110,8 @@ _SIGS = {
                                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int32]),
     "rmi_sokoban_generate_rooms_wait": (c_int32, [c_void_p]),
     "rmi_sokoban_reset": (c_int32, [_P(Sokoban), _P(Episode), c_void_p, c_void_p, c_void_p]),
+    "rmi_sokoban_load_rooms": (c_int32, [_P(Sokoban), _P(Episode), c_void_p, c_int32, c_void_p, c_void_p, c_void_p,
+                                         c_void_p, c_void_p]),
     "rmi_sokoban_step_turn_first": (c_int32, [_P(Sokoban), _P(Episode), _P(Turn), c_void_p, c_void_p, c_void_p,
                                               c_void_p]),
     "rmi_rollout_finalize": (c_int32, [_P(Episode), c_void_p, c_int32, c_int32, c_void_p, c_void_p, c_void_p,

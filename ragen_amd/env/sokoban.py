@@ -122,11 +122,13 @@ class SokobanBatch(BatchEnv):
     def reset(self, seeds):
         self.seeds = np.asarray(seeds, np.int64).copy()
         rows, inv = self._rooms(self.seeds)
-        # the distinct rooms and every env's row in them uploaded (pinned), expanded on the device
-        d = ops.h2d(rows, self.device)
-        if len(rows) != self.B or not np.array_equal(inv, np.arange(self.B)):
-            d = d.index_select(0, ops.h2d(inv, self.device))
-        self._load_rows(d)
+        # the distinct rooms and every env's row in them uploaded (pinned); one launch expands
+        # them and resets (rmi_sokoban_load_rooms)
+        room_of = None if len(rows) == self.B and np.array_equal(inv, np.arange(self.B)) else \
+            ops.h2d(inv.astype(np.int32), self.device)
+        ops.sokoban_load_rooms(self.struct(), self.ep, ops.h2d(rows, self.device), room_of, self.init_state,
+                               self.init_player)
+        self._invalidate()
 
     def load_state(self, fixed, state, player):
         B, HW = self.B, self.H * self.W

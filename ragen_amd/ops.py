@@ -206,6 +206,27 @@ def sokoban_reset(env: _lib.Sokoban, ep: EpisodeState, init_state: torch.Tensor,
           "rmi_sokoban_reset")
 
 
+def sokoban_load_rooms(env: _lib.Sokoban, ep: EpisodeState, rooms: torch.Tensor, room_of: Optional[torch.Tensor],
+                       init_state: torch.Tensor, init_player: torch.Tensor, err: Optional[torch.Tensor] = None):
+    """Fused device reset from the distinct generated rooms u8[U, 2HW+2] (env i takes row
+    room_of[i], or row i): room_fixed, init_state / init_player, then the reset (rmi_sokoban_load_rooms)."""
+    _dev(rooms, room_of, init_state, init_player, err)
+    _dt(rooms, torch.uint8, "rooms")
+    _dt(room_of, torch.int32, "room_of")
+    _dt(init_state, torch.uint8, "init_state")
+    _dt(init_player, torch.int8, "init_player")
+    _dt(err, torch.uint8, "err")
+    HW = env.H * env.W
+    if rooms.dim() != 2 or rooms.shape[1] != 2 * HW + 2:
+        raise ValueError(f"rooms: u8[U, {2 * HW + 2}] rows (fixed | state | player)")
+    B = ep.B
+    if init_state.numel() != B * HW or init_player.numel() != 2 * B or (room_of is not None and room_of.numel() != B) \
+            or (err is not None and err.numel() != B) or (room_of is None and rooms.shape[0] < B):
+        raise ValueError("init_state / init_player / room_of / err: one row per env")
+    check(lib().rmi_sokoban_load_rooms(env, ep.struct(), _ptr(rooms), rooms.shape[0], _ptr(room_of), _ptr(init_state),
+                                       _ptr(init_player), _ptr(err), _stream(ep.device)), "rmi_sokoban_load_rooms")
+
+
 def frozenlake_reset(env: _lib.FrozenLake, ep: EpisodeState, init_desc: torch.Tensor, init_s: torch.Tensor,
                      init_rng: torch.Tensor):
     """Fused device reset from the generated maps (desc, start state, seeded PCG64, record)."""

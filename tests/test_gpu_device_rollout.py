@@ -122,3 +122,37 @@ def test_reset_prefetch_gives_the_same_rooms(device, monkeypatch, draw_between):
         for x, y in zip(a, b):
             np.testing.assert_array_equal(x, y)
     assert got[False][1] == got[True][1]  # the peek leaves random's sequence alone
+
+
+def test_load_rooms_equals_load_state(device):
+    """rmi_sokoban_load_rooms (the distinct rooms expanded on the device, fused with the reset)
+    leaves every env as load_state with the expanded host rooms does; an out-of-range row index
+    loads an empty room and flags RMI_ERR_INDEX."""
+    from ragen_amd import _lib
+    from ragen_amd.env import SokobanBatch
+    from ragen_amd.env.configs import SokobanEnvConfig
+    B = 1000
+    seeds = np.repeat(np.arange(125, dtype=np.int64) + 900, 8)
+    cfg = SokobanEnvConfig(num_boxes=1, search_depth=100)
+    a = SokobanBatch(cfg, B, 4, 3, device)
+    b = SokobanBatch(cfg, B, 4, 3, device)
+    for x in (a, b):  # dirty state the reset must overwrite
+        x.room_state.fill_(7)
+        x.ep.turn_exec.fill_(1)
+        x.ep.penalty.fill_(-1)
+    a.reset(seeds)
+    assert len(SokobanBatch.generate_unique(seeds, 6, 6, 1, 100)[0]) == 125
+    b.load_state(*SokobanBatch.generate(seeds, 6, 6, 1, 100))
+    for k in ("room_fixed", "room_state", "player", "num_env_steps", "boxes_on_target", "init_state", "init_player"):
+        assert torch.equal(getattr(a, k), getattr(b, k)), k
+    for k in ("num_actions", "flags", "n_turns", "penalty", "turn_reward", "turn_info", "turn_exec"):
+        assert torch.equal(getattr(a.ep, k), getattr(b.ep, k)), k
+    rows, inv = SokobanBatch.generate_unique(seeds, 6, 6, 1, 100)
+    room_of = torch.from_numpy(inv.astype(np.int32)).to(device)
+    room_of[3] = 125
+    err = torch.empty(B, dtype=torch.uint8, device=device)
+    ops.sokoban_load_rooms(a.struct(), a.ep, torch.from_numpy(rows).to(device), room_of, a.init_state,
+                           a.init_player, err)
+    e = err.cpu().numpy()
+    assert e[3] == _lib.ERR_INDEX and not np.delete(e, 3).any()
+    assert not a.room_state[3].any() and torch.equal(a.room_state[4], b.room_state[4])
