@@ -790,8 +790,27 @@ def _(ids, n_ids, vocab_packed, vocab_bytes, stride, cfg, sel, with_spans, actio
             ids.new_empty(B, dtype=torch.uint8))
 
 
-def _bpe_struct(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache=None,
-                exp_off=None, exp_ids=None, added_words=None, ascii_class=None):
+_BPE_STRUCTS = {}  # the tables' tensors (held) + params -> their validated rmi_bpe_t
+
+
+def _bpe_struct(*args):
+    """rmi_bpe_t of a tokenizer's device tables, validated and built once per set of tables (the
+    tables are constant across calls; the cache holds the tensors, so a key's objects stay the
+    same objects, and their data pointers are part of the key)."""
+    key = tuple((id(a), a.data_ptr()) if isinstance(a, Tensor) else
+                (tuple(a) if isinstance(a, (list, tuple)) else a) for a in args)
+    hit = _BPE_STRUCTS.get(key)
+    if hit is not None:
+        return hit[0]
+    s = _bpe_struct_build(*args)
+    if len(_BPE_STRUCTS) >= 16:
+        _BPE_STRUCTS.clear()
+    _BPE_STRUCTS[key] = (s, args)
+    return s
+
+
+def _bpe_struct_build(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache=None,
+                      exp_off=None, exp_ids=None, added_words=None, ascii_class=None):
     from .tokenizer import Bpe
     ops._dev(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id)
     if len(params) != 13:
