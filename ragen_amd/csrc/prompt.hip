@@ -393,16 +393,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
   RMI_STAMP(4);
 }
 
-// one wave per output row: the row's arena slice and the tail, left-padded (element-wise
-// 8-B loads and stores; consecutive lanes take consecutive columns)
-__global__ __launch_bounds__(64) void pad_rows_kernel(const int64_t* __restrict__ arena, int64_t arena_stride,
-                                                      const int32_t* __restrict__ arena_len,
-                                                      const int64_t* __restrict__ rows, const int64_t* __restrict__ tail,
-                                                      int n_tail, int64_t S, int64_t pad_id, int64_t* __restrict__ ids,
-                                                      int64_t* __restrict__ am, int64_t* __restrict__ pos,
-                                                      uint8_t* __restrict__ err) {
-  const int lane = threadIdx.x;
-  const int64_t i = blockIdx.x;
+// one wave per output row, kPadRows rows per workgroup: the row's arena slice and the tail,
+// left-padded (element-wise 8-B loads and stores; consecutive lanes take consecutive columns;
+// the loop unrolled so a wave has several loads in flight).  NT: nontemporal stores (a batch
+// far past the caches, read by a later kernel).
+#ifndef RMI_PAD_ROWS_PER_BLOCK
+#define RMI_PAD_ROWS_PER_BLOCK 4
+#endif
+constexpr int kPadRows = RMI_PAD_ROWS_PER_BLOCK;
+
+template <bool NT>
+__device__ __forceinline__ void st_i64(int64_t* p, int64_t v) {
+  if (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(64 * kPadRows) void pad_rows_kernel(const int64_t* __restrict__ arena,
+                                                                 int64_t arena_stride,
+                                                                 const int32_t* __restrict__ arena_len,
+                                                                 const int64_t* __restrict__ rows,
+                                                                 const int64_t* __restrict__ tail, int n_tail,
+                                                                 int64_t n_rows, int64_t S, int64_t pad_id,
+                                                                 int64_t* __restrict__ ids, int64_t* __restrict__ am,
+                                                                 int64_t* __restrict__ pos, uint8_t* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * kPadRows + (threadIdx.x >> 6);
+  if (i >= n_rows) return;
   const int64_t r = rows[i];
   const int64_t na = arena_len[r], n = na + n_tail;
   const int64_t cut = n > S ? n - S : 0;  // an overlong row keeps its last S tokens
@@ -411,12 +430,13 @@ __global__ __launch_bounds__(64) void pad_rows_kernel(const int64_t* __restrict_
   int64_t* io = ids + i * S;
   int64_t* ao = am + i * S;
   int64_t* po = pos + i * S;
+#pragma unroll 4
   for (int64_t c = lane; c < S; c += 64) {
     const int64_t k = c - pad + cut;  // index into the row's n tokens
     const bool on = c >= pad;
-    io[c] = !on ? pad_id : (k < na ? src[k] : tail[k - na]);
-    ao[c] = on ? 1 : 0;
-    po[c] = on ? c - pad + 1 : 0;
+    st_i64<NT>(io + c, !on ? pad_id : (k < na ? src[k] : tail[k - na]));
+    st_i64<NT>(ao + c, on ? 1 : 0);
+    st_i64<NT>(po + c, on ? c - pad + 1 : 0);
   }
   if (lane == 0) err[i] = n > S ? RMI_ERR_UNSUP : 0;
 }
@@ -440,8 +460,16 @@ RMI_API int rmi_pad_rows(const int64_t* arena, int64_t arena_stride, const int32
   if (n_rows == 0) return RMI_OK;
   if (!arena || !arena_len || !rows || (n_tail && !tail) || !input_ids || !attention_mask || !position_ids || !err)
     return RMI_EINVAL;
-  hipLaunchKernelGGL(pad_rows_kernel, dim3((unsigned)n_rows), dim3(64), 0, as_stream(stream), arena, arena_stride,
-                     arena_len, rows, tail, (int)n_tail, S, pad_id, input_ids, attention_mask, position_ids, err);
+#ifndef RMI_PAD_NT_BYTES
+#define RMI_PAD_NT_BYTES (256ll << 20)  // outputs past the Infinity Cache: streamed stores
+#endif
+  const dim3 grid((unsigned)((n_rows + kPadRows - 1) / kPadRows)), block(64 * kPadRows);
+  if (n_rows * S * 24 > RMI_PAD_NT_BYTES)
+    hipLaunchKernelGGL(pad_rows_kernel<true>, grid, block, 0, as_stream(stream), arena, arena_stride, arena_len, rows,
+                       tail, (int)n_tail, n_rows, S, pad_id, input_ids, attention_mask, position_ids, err);
+  else
+    hipLaunchKernelGGL(pad_rows_kernel<false>, grid, block, 0, as_stream(stream), arena, arena_stride, arena_len, rows,
+                       tail, (int)n_tail, n_rows, S, pad_id, input_ids, attention_mask, position_ids, err);
   return launch_status();
 }
 

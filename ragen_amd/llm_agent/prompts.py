@@ -553,12 +553,15 @@ class DevicePrompts:
                   (_lib.PT_IF, 0, 0), self.tpl.u_pre + "Reward:\n", (_lib.PT_REWARD, 0, 0),
                   f"\n\nTurn {number}:\nState:\n", (_lib.PT_OBS, 0, 0), "\nYou have ", (_lib.PT_INT, 0, 0),
                   self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
-        stride = self._stride(resp.shape[1] + obs.shape[1] + 1024)
         last = t + 1 >= self.max_turn
+        obs_max, resp_max = bounds if bounds is not None else (d.get("obs_max"), d.get("text_max"))
+        # the text rows sized from the host's bound on the longest row when it has one (the
+        # kernel's LDS grows with the row: a tight row keeps more waves resident); a row past it
+        # is flagged by the kernel and built on the host
+        bound = self._text_bound(self._program(pieces)[0], obs_max, resp_max)
+        stride = self._stride(bound + 4) if bound is not None else self._stride(resp.shape[1] + obs.shape[1] + 1024)
         text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, None, resp,
                                                 resp_len, spans, None, active, turn=(ne, flags, last))
-        obs_max, resp_max = bounds if bounds is not None else (d.get("obs_max"), d.get("text_max"))
-        bound = self._text_bound(self._prog_last, obs_max, resp_max)
         return text, tlen, mark, terr, stride, last, flags, bound
 
     # ----------------------------------------------------------- max_context_window
