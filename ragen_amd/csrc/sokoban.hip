@@ -979,44 +979,49 @@ __global__ __launch_bounds__(kBlock) void sokoban_reset_kernel(rmi_sokoban_t env
 
 // Reset from the distinct generated rooms (rmi_sokoban_load_rooms): env i takes row room_of[i]
 // of rooms [n_rooms, 2HW+2] (fixed | state | player bytes) into room_fixed / init_state /
-// init_player, then the reset above (room_state, player, counters, record).  A thread per env.
+// init_player, then the reset above (room_state, player, counters, record).  A thread per
+// (env, cell) for the rooms, a thread per env for the rest.
 __global__ __launch_bounds__(kBlock) void sokoban_load_rooms_kernel(rmi_sokoban_t env, rmi_episode_t ep, int hw,
                                                                     const uint8_t* __restrict__ rooms, int n_rooms,
                                                                     const int32_t* __restrict__ room_of,
                                                                     uint8_t* __restrict__ init_state,
                                                                     int8_t* __restrict__ init_player,
                                                                     uint8_t* __restrict__ err) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t B = ep.B;
-  if (i >= B) return;
-  int r = room_of ? room_of[i] : (int)i;
-  const bool bad = r < 0 || r >= n_rooms;
-  if (err) err[i] = bad ? RMI_ERR_INDEX : 0;
-  const uint8_t* src = rooms + (int64_t)(bad ? 0 : r) * (2 * hw + 2);
-  uint8_t* fx = const_cast<uint8_t*>(env.room_fixed) + i * hw;  // (read-only to the turn; the reset writes it)
-  uint8_t* st = env.room_state + i * hw;
-  uint8_t* is = init_state + i * hw;
-  for (int k = 0; k < hw; ++k) {
-    const uint8_t f = bad ? 0 : src[k], v = bad ? 0 : src[hw + k];
-    fx[k] = f;
-    st[k] = v;
-    is[k] = v;
+  const int64_t pitch = 2 * hw + 2;
+  if (t < B * hw) {  // cell k of env i
+    const int64_t i = t / hw;
+    const int k = (int)(t - i * hw);
+    const int r = room_of ? room_of[i] : (int)i;
+    const bool bad = r < 0 || r >= n_rooms;
+    const uint8_t f = bad ? 0 : rooms[(int64_t)r * pitch + k], v = bad ? 0 : rooms[(int64_t)r * pitch + hw + k];
+    const_cast<uint8_t*>(env.room_fixed)[t] = f;  // (read-only to the turn; the reset writes it)
+    env.room_state[t] = v;
+    init_state[t] = v;
   }
-  const int8_t p0 = bad ? 0 : (int8_t)src[2 * hw], p1 = bad ? 0 : (int8_t)src[2 * hw + 1];
-  init_player[2 * i] = p0;
-  init_player[2 * i + 1] = p1;
-  env.player[2 * i] = p0;
-  env.player[2 * i + 1] = p1;
-  env.num_env_steps[i] = 0;
-  env.boxes_on_target[i] = 0;
-  ep.num_actions[i] = 0;
-  ep.flags[i] = 0;
-  ep.n_turns[i] = 0;
-  ep.penalty[i] = 0.0;
-  for (int t = 0; t < ep.T; ++t) {
-    ep.turn_reward[t * B + i] = 0.0;
-    ep.turn_info[t * B + i] = 0;
-    ep.turn_exec[t * B + i] = 0;
+  if (t < B) {
+    const int64_t i = t;
+    const int r = room_of ? room_of[i] : (int)i;
+    const bool bad = r < 0 || r >= n_rooms;
+    if (err) err[i] = bad ? RMI_ERR_INDEX : 0;
+    const uint8_t* src = rooms + (int64_t)(bad ? 0 : r) * pitch + 2 * hw;
+    const int8_t p0 = bad ? 0 : (int8_t)src[0], p1 = bad ? 0 : (int8_t)src[1];
+    init_player[2 * i] = p0;
+    init_player[2 * i + 1] = p1;
+    env.player[2 * i] = p0;
+    env.player[2 * i + 1] = p1;
+    env.num_env_steps[i] = 0;
+    env.boxes_on_target[i] = 0;
+    ep.num_actions[i] = 0;
+    ep.flags[i] = 0;
+    ep.n_turns[i] = 0;
+    ep.penalty[i] = 0.0;
+    for (int u = 0; u < ep.T; ++u) {
+      ep.turn_reward[u * B + i] = 0.0;
+      ep.turn_info[u * B + i] = 0;
+      ep.turn_exec[u * B + i] = 0;
+    }
   }
 }
 
@@ -1229,7 +1234,8 @@ RMI_API int rmi_sokoban_load_rooms(const rmi_sokoban_t* env, const rmi_episode_t
       !env->room_state || !env->player || !env->num_env_steps || !env->boxes_on_target || !ep->num_actions ||
       !ep->flags || !ep->n_turns || !ep->penalty || !ep->turn_reward || !ep->turn_info || !ep->turn_exec)
     return RMI_EINVAL;
-  hipLaunchKernelGGL(sokoban_load_rooms_kernel, dim3((unsigned)((ep->B + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+  const int64_t nt = (int64_t)ep->B * hw;  // >= B (hw >= 1)
+  hipLaunchKernelGGL(sokoban_load_rooms_kernel, dim3((unsigned)((nt + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      as_stream(stream), *env, *ep, hw, rooms, (int)n_rooms, room_of, init_state, init_player, err);
   return launch_status();
 }

@@ -6,7 +6,7 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-resets = [i for i, r in enumerate(rows) if "sokoban_reset_kernel" in r["Kernel_Name"]]
+resets = [i for i, r in enumerate(rows) if "sokoban_reset_kernel" in r["Kernel_Name"] or "sokoban_load_rooms_kernel" in r["Kernel_Name"]]
 # api_leg: 4 device-path rollouts (one reset each), then the dict-path rollouts
 a, b = resets[3], resets[4] if len(resets) > 4 else len(rows)
 seg = rows[a:b]
