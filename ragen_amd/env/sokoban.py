@@ -91,16 +91,14 @@ class SokobanBatch(BatchEnv):
 
     def prefetch(self, seeds):
         """Start generating the rooms of a later reset(seeds) on a native host thread
-        (ops.RoomsJob, on half the host threads).  reset() with the same seeds takes them;
+        (ops.RoomsJob; one core stays with the caller).  reset() with the same seeds takes them;
         other seeds generate afresh.  Rooms are a pure function of the seed, so the state after
         reset() is the same either way."""
         seeds = np.asarray(seeds, np.int64).copy()
         c = self.config
         uniq, inv = self._distinct(seeds)
-        # half the host threads: the caller's turn loop keeps its cores (with all but one, the
-        # turn loop measured up to 15 % slower while the generation ran)
         job = ops.RoomsJob(uniq, self.H, self.W, int(c.num_boxes), int(c.search_depth),
-                           max(1, ops.host_threads() // 2))
+                           max(1, ops.host_threads() - 1))
         self._prefetched = (seeds, uniq, inv, job)
 
     def _rooms(self, seeds):

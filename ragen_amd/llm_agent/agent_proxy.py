@@ -135,4 +135,6 @@ class LLMAgentProxy:
         self.last_timing = {"reset_s": t1 - t0, "turns_s": t2 - t1, "rollout_states_s": t3 - t2,
                             "formulate_s": time.perf_counter() - t3,
                             "readbacks": {"reset": c1 - c0, "turns": c2 - c1, "after": D2H_COUNT[0] - c2}}
+        # the next reset's room generation, behind the caller's use of this batch (the update)
+        es.prefetch_next()
         return out

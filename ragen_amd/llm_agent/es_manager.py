@@ -179,8 +179,8 @@ def _hostbook():
 
 
 class EnvStateManager:
-    # reset() with a drawn train seed starts the next reset's host work (Sokoban room
-    # generation) in the background, for the seed random will draw next
+    # after a rollout from a drawn train seed, prefetch_next() starts the next reset's host
+    # work (Sokoban room generation) in the background, for the seed random will draw next
     prefetch_resets = True
 
     def __init__(self, config, mode: str = "train", device=None, rank: Optional[int] = None,
@@ -287,6 +287,21 @@ class EnvStateManager:
                              "rank uses the same train seed")
         return random.randint(0, 1000000)
 
+    def prefetch_next(self):
+        """Start the next reset()'s host work (Sokoban room generation, on native host threads)
+        for the train seed ``random`` will draw next, peeked without drawing it (its state is
+        put back).  LLMAgentProxy.rollout calls it when the rollout is done, so the generation
+        runs while the trainer updates the policy; the next reset() takes the rooms when its
+        seeds match, and generates afresh when ``random`` was drawn from in between."""
+        if not (self.prefetch_resets and getattr(self, "_seed_drawn", False)):
+            return
+        st = random.getstate()
+        seed = random.randint(0, 1000000)
+        random.setstate(st)
+        nxt = seed + (self.env_lo + np.arange(self.n_envs)) // self.group_size
+        for t in self.tags:
+            t.batch.prefetch(nxt[t.lo - self.env_lo:t.hi - self.env_lo])
+
     def reset(self, seed: Optional[int] = None):
         """es_manager.py:75-103."""
         drawn = self.mode == "train" and seed is None and self.process_group is None
@@ -295,15 +310,7 @@ class EnvStateManager:
         seeds = seed + gids // self.group_size  # _expand_seed, global ids
         for t in self.tags:
             t.batch.reset(seeds[t.lo - self.env_lo:t.hi - self.env_lo])
-        if self.prefetch_resets and drawn:
-            # the next reset()'s train seed, peeked without drawing it (random's state is put
-            # back): the envs start that reset's host work now, behind this rollout's turns.  A
-            # different seed then (random drawn from in between) only costs the prefetch.
-            st = random.getstate()
-            nxt = seeds - seed + random.randint(0, 1000000)
-            random.setstate(st)
-            for t in self.tags:
-                t.batch.prefetch(nxt[t.lo - self.env_lo:t.hi - self.env_lo])
+        self._seed_drawn = drawn  # (prefetch_next: the next reset draws its seed too)
         self._turn = 0
         self._turn_records = []
         self._mat_upto = 0

@@ -95,8 +95,8 @@ def test_device_step_undecodable_generation_raises_unstepped(device, monkeypatch
 
 @pytest.mark.parametrize("draw_between", [False, True])
 def test_reset_prefetch_gives_the_same_rooms(device, monkeypatch, draw_between):
-    """EnvStateManager.reset with a drawn train seed starts the next reset's room generation in
-    the background (for the seed random will draw next, peeked without drawing it).  Two resets
+    """EnvStateManager.prefetch_next after a reset with a drawn train seed starts the next reset's
+    room generation in the background (for the seed random will draw next, peeked without drawing it).  Two resets
     give the same rooms with and without the prefetch, also when random is drawn from in between
     (then the prefetch is for another seed and not taken)."""
     from ragen_amd.env import SokobanBatch
@@ -110,11 +110,13 @@ def test_reset_prefetch_gives_the_same_rooms(device, monkeypatch, draw_between):
         es.prefetch_resets = pf
         random.seed(11)
         rooms = []
-        for _ in range(3):
+        for k in range(3):
             es.reset()
             b = es.tags[0].batch
-            assert (getattr(b, "_prefetched", None) is not None) == pf
+            assert b.reset_prefetched == (pf and k > 0 and not draw_between)
             rooms.append([x.cpu().numpy().copy() for x in (b.room_fixed, b.init_state, b.init_player)])
+            es.prefetch_next()  # (LLMAgentProxy.rollout calls it when a rollout is done)
+            assert (getattr(b, "_prefetched", None) is not None) == pf
             if draw_between:
                 random.random()
         got[pf] = (rooms, random.random())
