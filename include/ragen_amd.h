@@ -448,6 +448,13 @@ int rmi_gen_rows(const int64_t* resp, int64_t n_resp, int64_t R, const int64_t* 
                  const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, uint8_t* has,
                  int32_t* raw_max, rmi_stream_t stream);
 
+/* rmi_gen_rows without the zeroing launch, for a caller that alternates two raw_max slots
+ * across turns: raw_max must be 0 on entry (zeroed by the previous call's raw_next, or by the
+ * caller), and the launch sets raw_next[0] = 0 (NULL: not written; must not alias raw_max). */
+int rmi_gen_rows_chained(const int64_t* resp, int64_t n_resp, int64_t R, const int64_t* src, int64_t n_envs,
+                         const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, uint8_t* has,
+                         int32_t* raw_max, int32_t* raw_next, rmi_stream_t stream);
+
 /* HOST function (CPU memory): the packed vocabulary of rmi_detokenize from the byte table
  * vocab_bytes[vocab_off[t] .. vocab_off[t+1]) and skip[t] (NULL = none skipped).
  * packed u32[V,4]: entry t = (w0, w1, w2, meta); meta bits 0-23 = the token's byte length,

@@ -1239,8 +1239,10 @@ __global__ __launch_bounds__(64 * kGenWaves) void gen_rows_kernel(const int64_t*
                                                                   const int64_t* __restrict__ src, int64_t n_envs,
                                                                   const uint32_t* __restrict__ packed, int64_t V,
                                                                   int64_t* __restrict__ ids, int32_t* __restrict__ n_ids,
-                                                                  uint8_t* __restrict__ has, int32_t* __restrict__ raw_max) {
+                                                                  uint8_t* __restrict__ has, int32_t* __restrict__ raw_max,
+                                                                  int32_t* __restrict__ raw_next) {
   __shared__ int wave_max[kGenWaves];
+  if (raw_next && blockIdx.x == 0 && threadIdx.x == 0) *raw_next = 0;  // the next call's raw_max
   const int wv = threadIdx.x / 64;
   const int64_t e = (int64_t)blockIdx.x * kGenWaves + wv;
   const int lane = threadIdx.x & 63;
@@ -1382,6 +1384,22 @@ RMI_API int rmi_gen_rows(const int64_t* resp, int64_t n_resp, int64_t R, const i
   if (hipMemsetAsync(raw_max, 0, sizeof(int32_t), st) != hipSuccess) return RMI_EDEVICE;
   if (n_envs == 0) return RMI_OK;
   hipLaunchKernelGGL(gen_rows_kernel, dim3((unsigned)((n_envs + kGenWaves - 1) / kGenWaves)), dim3(64 * kGenWaves), 0,
-                     st, resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has, raw_max);
+                     st, resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has, raw_max, nullptr);
+  return launch_status();
+}
+
+RMI_API int rmi_gen_rows_chained(const int64_t* resp, int64_t n_resp, int64_t R, const int64_t* src, int64_t n_envs,
+                                 const uint32_t* vocab_packed, int64_t V, int64_t* ids, int32_t* n_ids, uint8_t* has,
+                                 int32_t* raw_max, int32_t* raw_next, rmi_stream_t stream) {
+  using namespace rmi;
+  if (n_resp < 0 || R < 0 || n_envs < 0 || V < 1 || !raw_max || !vocab_packed || raw_next == raw_max) return RMI_EINVAL;
+  if ((src == nullptr) != (ids == nullptr) || (src == nullptr && n_resp != n_envs)) return RMI_EINVAL;
+  if (!resp && n_resp > 0 && R > 0) return RMI_EINVAL;
+  if (n_envs == 0) {  // nothing to reduce: raw_max stays 0; raw_next still zeroed
+    return raw_next && hipMemsetAsync(raw_next, 0, sizeof(int32_t), as_stream(stream)) != hipSuccess ? RMI_EDEVICE
+                                                                                                   : RMI_OK;
+  }
+  hipLaunchKernelGGL(gen_rows_kernel, dim3((unsigned)((n_envs + kGenWaves - 1) / kGenWaves)), dim3(64 * kGenWaves), 0,
+                     as_stream(stream), resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has, raw_max, raw_next);
   return launch_status();
 }

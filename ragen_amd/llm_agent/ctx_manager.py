@@ -703,14 +703,22 @@ class ContextManager:
         lo, n = self.env_lo, self.n_envs
         es = getattr(self, "_es", None)
         in_order = es is not None and env_ids is es._ids_in_order  # reset()'s own array: every env, in order
-        # the turn's readback buffer, allocated here so rmi_gen_rows writes the longest
-        # generation's raw bytes straight into it (EnvStateManager._device_pass reads it back)
-        pack = torch.empty(ops.readback_bytes(n), dtype=torch.uint8, device=dev)
-        raw = ops.readback_raw(pack, n)
+        # the turn's readback buffer, here so rmi_gen_rows writes the longest generation's raw
+        # bytes straight into it (EnvStateManager._device_pass reads it back).  Two buffers,
+        # alternating by turn: each turn's gen_rows zeroes the other's raw slot for the next turn
+        # (rmi_gen_rows_chained: no zeroing launch); a turn's buffer is read back (and done with)
+        # before the turn after next reuses it.
+        nb = ops.readback_bytes(n)
+        packs = getattr(self, "_packs", None)
+        if packs is None or packs[0].numel() != nb or packs[0].device != resp.device:
+            packs = self._packs = [torch.zeros(nb, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self._pack_i = 0
+        pack, nxt = packs[self._pack_i], packs[1 - self._pack_i]
+        raw, raw_next = ops.readback_raw(pack, n), ops.readback_raw(nxt, n)
         if in_order or (len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n))):
             # every env in order: the generations are the rows (n_ids = None: R ids each)
             has_t, n_ids, ids = None, None, resp
-            direct.gen_rows(resp, None, n, vocab.packed, None, None, raw)
+            direct.gen_rows(resp, None, n, vocab.packed, None, None, raw, None, raw_next)
         else:  # one launch: the rows scattered onto the batch, n_ids, the raw width
             local = env_ids - lo
             if local.size and (local.min() < 0 or local.max() >= n):
@@ -722,7 +730,8 @@ class ContextManager:
             ids = torch.empty(n, R, dtype=torch.int64, device=dev)
             n_ids = torch.empty(n, dtype=torch.int32, device=dev)
             has_t = torch.empty(n, dtype=torch.uint8, device=dev)  # 1: the env has a generation
-            direct.gen_rows(resp, ops.h2d(src, dev), n, vocab.packed, ids, n_ids, raw, has_t)
+            direct.gen_rows(resp, ops.h2d(src, dev), n, vocab.packed, ids, n_ids, raw, has_t, raw_next)
+        self._pack_i ^= 1  # (after the launch that zeroed the other buffer's slot)
         # the decoded rows' width.  With a hint from the turns before (the longest generation
         # seen, with a margin) no readback: a longer generation overflows the decode's row, is
         # masked out of the turn's first pass and stepped by a second pass sized from the

@@ -870,10 +870,12 @@ def assemble_rows(tokens: torch.Tensor, row_start: torch.Tensor, row_len: torch.
 
 def gen_rows(resp: torch.Tensor, src: Optional[torch.Tensor], n_envs: int, vocab_packed: torch.Tensor,
              ids: Optional[torch.Tensor], n_ids: Optional[torch.Tensor], raw_max: torch.Tensor,
-             has: Optional[torch.Tensor] = None):
+             has: Optional[torch.Tensor] = None, raw_next: Optional[torch.Tensor] = None):
     """rmi_gen_rows: the turn's generations onto the env batch (ids / n_ids / has written when
-    src is given) and the longest row's raw bytes into raw_max i32[1]."""
-    _dev(resp, src, vocab_packed, ids, n_ids, raw_max, has)
+    src is given) and the longest row's raw bytes into raw_max i32[1].  With raw_next
+    (rmi_gen_rows_chained): raw_max is 0 already and raw_next is zeroed for the next call."""
+    _dev(resp, src, vocab_packed, ids, n_ids, raw_max, has, raw_next)
+    _dt(raw_next, torch.int32, "raw_next")
     _dt(has, torch.uint8, "has")
     _dt(resp, torch.int64, "resp")
     _dt(src, torch.int64, "src")
@@ -889,6 +891,14 @@ def gen_rows(resp: torch.Tensor, src: Optional[torch.Tensor], n_envs: int, vocab
         raise ValueError("src, ids and n_ids must have one row per env")
     if src is None and (resp.shape[0] != n_envs or ids is not None or has is not None):
         raise ValueError("without src resp holds every env's row (and ids is not written)")
+    if raw_next is not None:
+        if raw_next.numel() < 1 or raw_next.data_ptr() == raw_max.data_ptr():
+            raise ValueError("raw_next: one int32 apart from raw_max")
+        check(lib().rmi_gen_rows_chained(_ptr(resp), resp.shape[0], R, _ptr(src), int(n_envs), _ptr(vocab_packed),
+                                         vocab_packed.shape[0], _ptr(ids), _ptr(n_ids), _ptr(has), _ptr(raw_max),
+                                         _ptr(raw_next), _stream(resp.device)),
+              "rmi_gen_rows_chained")
+        return
     check(lib().rmi_gen_rows(_ptr(resp), resp.shape[0], R, _ptr(src), int(n_envs), _ptr(vocab_packed),
                              vocab_packed.shape[0], _ptr(ids), _ptr(n_ids), _ptr(has), _ptr(raw_max),
                              _stream(resp.device)),

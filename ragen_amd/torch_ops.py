@@ -446,12 +446,14 @@ def _(tokens, row_start, row_len, S, pad_id, special_token, reward_token, scores
             tokens.new_empty(B, dtype=torch.uint8))
 
 
-@_op("gen_rows", ("ids", "n_ids", "raw_max", "has"))
+@_op("gen_rows", ("ids", "n_ids", "raw_max", "has", "raw_next"))
 def gen_rows(resp: Tensor, src: Optional[Tensor], n_envs: int, vocab_packed: Tensor, ids: Optional[Tensor],
-             n_ids: Optional[Tensor], raw_max: Tensor, has: Optional[Tensor] = None) -> None:
+             n_ids: Optional[Tensor], raw_max: Tensor, has: Optional[Tensor] = None,
+             raw_next: Optional[Tensor] = None) -> None:
     """The input side of get_env_inputs (ctx_manager.py:332-337): the turn's generations onto
-    the env batch and the longest row's raw bytes (rmi_gen_rows)."""
-    ops.gen_rows(resp, src, n_envs, vocab_packed, ids, n_ids, raw_max, has)
+    the env batch and the longest row's raw bytes (rmi_gen_rows; with raw_next the chained form,
+    raw_max zero on entry and raw_next zeroed for the next turn)."""
+    ops.gen_rows(resp, src, n_envs, vocab_packed, ids, n_ids, raw_max, has, raw_next)
 
 
 @_op("pad_rows")

@@ -68,3 +68,35 @@ def test_gen_rows_no_rows(device):
     torch.ops.ragen_amd.gen_rows(resp, torch.full((n,), -1, dtype=torch.int64, device=device), n, vocab.packed,
                                  ids, n_ids, raw)
     assert not ids.any() and not n_ids.any() and int(raw) == 0
+
+
+def test_gen_rows_chained(device):
+    """rmi_gen_rows_chained (the device turn loop's form, two alternating raw slots): the same
+    rows and raw max as rmi_gen_rows when raw_max starts at 0, no zeroing of raw_max, and
+    raw_next zeroed; alternating two slots over several turns reads each turn's own max."""
+    vocab = _vocab(device)
+    rng = np.random.default_rng(5)
+    n, V = 1000, vocab.raw_len.numel()
+    slots = torch.zeros(2, dtype=torch.int32, device=device)
+    for turn in range(5):
+        R = int(rng.integers(1, 120))
+        resp = torch.from_numpy(rng.integers(-3, V + 3, (n, R))).to(device)
+        _, _, want = _want(resp, torch.arange(n, device=device), n, vocab)
+        cur, nxt = slots[turn % 2:turn % 2 + 1], slots[1 - turn % 2:2 - turn % 2]
+        nxt.fill_(12345)  # stale: the call zeroes it
+        ops.gen_rows(resp, None, n, vocab.packed, None, None, cur, raw_next=nxt)
+        assert int(cur.item()) == want and int(nxt.item()) == 0
+    src = torch.full((n,), -1, dtype=torch.int64, device=device)
+    src[::3] = torch.arange(len(range(0, n, 3)), device=device)
+    resp = torch.from_numpy(rng.integers(0, V, (len(range(0, n, 3)), 40))).to(device)
+    ids = torch.empty(n, 40, dtype=torch.int64, device=device)
+    n_ids = torch.empty(n, dtype=torch.int32, device=device)
+    has = torch.empty(n, dtype=torch.uint8, device=device)
+    cur = torch.full((1,), 7, dtype=torch.int32, device=device)  # not zeroed by the chained form
+    nxt = torch.ones(1, dtype=torch.int32, device=device)
+    ops.gen_rows(resp, src, n, vocab.packed, ids, n_ids, cur, has, raw_next=nxt)
+    w_ids, w_n, want = _want(resp, torch.arange(0, n, 3, device=device), n, vocab)
+    assert torch.equal(ids, w_ids) and torch.equal(n_ids, w_n) and int(nxt.item()) == 0
+    assert int(cur.item()) == max(7, want)
+    with pytest.raises(ValueError):
+        ops.gen_rows(resp, src, n, vocab.packed, ids, n_ids, cur, has, raw_next=cur)
