@@ -829,12 +829,13 @@ class ContextManager:
         row_resp = response_mask.view(torch.uint8).sum(dim=-1, dtype=torch.int32).float()
         if self.process_group is not None and self.world_size > 1:
             row_resp = rd.all_gather_rows(row_resp, group=self.process_group, sizes=self.shard_sizes())
-        # the assembly's error bits, the mean and the metric rows in one readback (errors first)
-        extra = torch.stack([(err & _lib.ERR_UNSUP).any().double(), (err & _lib.ERR_STATE).any().double(),
-                             row_resp.mean().double()]).view(torch.uint8)
-        parts, ext = es.metric_arrays(extra)
-        overlong, multi, response_length = (float(x) for x in ext.view(np.float64))
-        _raise_assemble_errors(None, S, (overlong, multi))
+        # the mean, the assembly's per-row error bytes and the metric rows in one readback (the
+        # error bits reduced on the host: no launches for them)
+        mean = row_resp.mean().double().reshape(1).view(torch.uint8)
+        parts, ext = es.metric_arrays([mean, err])
+        response_length = float(ext[:8].view(np.float64)[0])
+        err_h = ext[8:]
+        _raise_assemble_errors(None, S, (bool((err_h & _lib.ERR_UNSUP).any()), bool((err_h & _lib.ERR_STATE).any())))
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
                  "loss_mask": loss_mask, "rm_scores": normalized, "original_rm_scores": normalized}
         env_ids = es.env_lo + np.arange(es.n_envs, dtype=np.int64)

@@ -782,10 +782,12 @@ class EnvStateManager:
         """Per-env rollout metrics of this shard from the device record, one copy for every tag:
         -> list of (tag, m f64[B_tag, 4] = success, num_actions, action_is_effective mean,
         action_is_valid mean, custom bool[B_tag] = some turn carried an info dict,
-        info u8[T_seen, B_tag]).  extra (u8 on the device, optional): read back in the same
-        copy -> (list, extra's host bytes)."""
+        info u8[T_seen, B_tag]).  extra (u8 on the device, or a list of them; optional): read back
+        in the same copy -> (list, extra's host bytes, concatenated)."""
         T = min(self._turn, self.max_turn)
-        parts, shapes = [] if extra is None else [extra.reshape(-1)], []
+        extras = [] if extra is None else [x.reshape(-1) for x in (extra if isinstance(extra, (list, tuple)) else [extra])]
+        n_extra = sum(x.numel() for x in extras)
+        parts, shapes = list(extras), []
         for tg in self.tags:
             ep = tg.batch.ep
             m = direct.rollout_metrics(*ep_args(ep))
@@ -794,7 +796,7 @@ class EnvStateManager:
             shapes.append((tg, m.shape, m.numel() * 8, info.numel()))
         flat = parts[0] if len(parts) == 1 else torch.cat(parts)
         host = ops.d2h(flat, self)
-        o = 0 if extra is None else extra.numel()
+        o = n_extra
         out = []
         for tg, mshape, nm, ni in shapes:
             mh = host[o:o + nm].view(np.float64).reshape(mshape)
@@ -802,7 +804,7 @@ class EnvStateManager:
             o += nm + ni
             custom = (ih & _lib.INFO_PRESENT).any(0) if T else np.zeros(mh.shape[0], bool)
             out.append((tg.tag, mh, custom, ih))
-        return out if extra is None else (out, host[:extra.numel()])
+        return out if extra is None else (out, host[:n_extra])
 
     def get_rollout_states(self):
         """es_manager.py:173-207.  On the device path (turns taken from device token ids) the
