@@ -356,6 +356,10 @@ int rmi_assemble_rows(const int64_t* tokens, const int64_t* row_start, const int
                       int64_t* attention_mask, int64_t* position_ids, float* score_out, uint8_t* loss_mask,
                       uint8_t* response_mask, uint8_t* err, rmi_stream_t stream);
 
+/* response_length's row sums (ctx_manager.py:305, response_mask.sum(-1)): out[i] = the number
+ * of nonzero bytes of row i of mask u8[B, S] (a bool mask); one launch, no widening copy.   */
+int rmi_row_counts(const uint8_t* mask, int64_t B, int64_t S, int32_t* out, rmi_stream_t stream);
+
 /* ------------------------------------------------------------------- A13 advantages
  * Replaces: verl compute_gae_advantage_return (called agent_trainer.py:77-83; App. A.4).
  * variant 0 = legacy (RAGEN's snapshot), 1 = masked (newer verl).  Sequential f32

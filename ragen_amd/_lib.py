@@ -176,6 +176,7 @@ _SIGS = {
     "rmi_prompt_text": (c_int32, [_P(Prompt), c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_gen_rows": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
+    "rmi_row_counts": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "rmi_gen_rows_chained": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_pad_rows": (c_int32, [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_void_p, c_int32, c_int64, c_int64,

@@ -247,8 +247,42 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   }
 }
 
+// per-row count of the nonzero bytes of a u8 [B, S] mask (response_mask.sum(-1)): a wave per
+// row, dword loads where the row is 4-B aligned, a wave reduction
+__global__ __launch_bounds__(256) void row_counts_kernel(const uint8_t* __restrict__ m, int64_t B, int64_t S,
+                                                         int32_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= B) return;
+  const uint8_t* row = m + i * S;
+  int c = 0;
+  int64_t k0 = 0;
+  if ((S & 3) == 0) {  // every row 4-B aligned (the base is): whole dwords
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(row);
+    for (int64_t k = lane; k < (S >> 2); k += 64) {
+      const uint32_t x = w[k];
+      c += ((x & 0xFFu) != 0) + ((x & 0xFF00u) != 0) + ((x & 0xFF0000u) != 0) + ((x >> 24) != 0);
+    }
+    k0 = S;
+  }
+  for (int64_t k = k0 + lane; k < S; k += 64) c += row[k] != 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if (lane == 0) out[i] = c;
+}
+
 }  // namespace
 }  // namespace rmi
+
+RMI_API int rmi_row_counts(const uint8_t* mask, int64_t B, int64_t S, int32_t* out, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || S < 0 || (B > 0 && (!out || (S > 0 && !mask)))) return RMI_EINVAL;
+  if (B > 0x7FFFFFFFll * 4) return RMI_EUNSUP;
+  if (B == 0) return RMI_OK;
+  if ((S & 3) == 0 && (reinterpret_cast<uintptr_t>(mask) & 3u)) return RMI_EUNSUP;
+  hipLaunchKernelGGL(row_counts_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, as_stream(stream), mask, B, S,
+                     out);
+  return launch_status();
+}
 
 RMI_API int rmi_masks_and_scores(const int64_t* ids, int64_t B, int64_t S, int64_t special_token,
                                  int64_t reward_token, const double* scores, const int32_t* n_scores, int32_t T,

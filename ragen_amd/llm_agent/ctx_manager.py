@@ -825,8 +825,8 @@ class ContextManager:
         if not ap.use_turn_scores:
             normalized = self._normalize_device(score_tensor, es)
         # the mean over the WHOLE batch (ctx_manager.py:305): every rank's row lengths, rank order
-        # (the counts summed as bytes into int32: the values of response_mask.sum(-1))
-        row_resp = response_mask.view(torch.uint8).sum(dim=-1, dtype=torch.int32).float()
+        # (rmi_row_counts: the values of response_mask.sum(-1), without torch's widening copy)
+        row_resp = ops.row_counts(response_mask).float()
         if self.process_group is not None and self.world_size > 1:
             row_resp = rd.all_gather_rows(row_resp, group=self.process_group, sizes=self.shard_sizes())
         # the mean, the assembly's per-row error bytes and the metric rows in one readback (the

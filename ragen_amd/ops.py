@@ -868,6 +868,17 @@ def assemble_rows(tokens: torch.Tensor, row_start: torch.Tensor, row_len: torch.
     return ids, am, pos, score, lm, rm, err
 
 
+def row_counts(mask: torch.Tensor) -> torch.Tensor:
+    """i32[B]: the nonzero bytes of each row of a bool / u8 [B, S] mask (rmi_row_counts)."""
+    _dev(mask)
+    if mask.dtype not in (torch.bool, torch.uint8) or mask.dim() != 2:
+        raise ValueError("mask: bool or u8 [B, S]")
+    out = torch.empty(mask.shape[0], dtype=torch.int32, device=mask.device)
+    check(lib().rmi_row_counts(_ptr(mask), mask.shape[0], mask.shape[1], _ptr(out), _stream(mask.device)),
+          "rmi_row_counts")
+    return out
+
+
 def gen_rows(resp: torch.Tensor, src: Optional[torch.Tensor], n_envs: int, vocab_packed: torch.Tensor,
              ids: Optional[torch.Tensor], n_ids: Optional[torch.Tensor], raw_max: torch.Tensor,
              has: Optional[torch.Tensor] = None, raw_next: Optional[torch.Tensor] = None):

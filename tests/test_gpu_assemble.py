@@ -142,3 +142,15 @@ def test_assemble_ragged_shapes_vs_host(device, S):
             np.testing.assert_array_equal(rm.cpu().numpy().astype(np.uint8), orm)
             exp_err |= np.where(np.asarray(oerr) != 0, 4, 0)  # RMI_ERR_STATE: the reference raises
         np.testing.assert_array_equal(err.cpu().numpy(), exp_err.astype(np.uint8))
+
+
+@pytest.mark.parametrize("S", [1, 3, 4, 64, 257, 1100])
+def test_row_counts_equal_torch(device, S):
+    """rmi_row_counts (formulate_rollouts' response_length row sums) == response_mask.sum(-1)."""
+    g = torch.Generator(device="cpu").manual_seed(S)
+    for B, dt in ((1003, torch.bool), (8, torch.uint8), (0, torch.bool)):
+        m = (torch.rand(B, S, generator=g) < 0.3)
+        m = (m if dt == torch.bool else (m.to(torch.uint8) * torch.randint(1, 256, (B, S), generator=g,
+                                                                           dtype=torch.int32).to(torch.uint8))).to(device)
+        got = ops.row_counts(m)
+        assert torch.equal(got.cpu(), (m != 0).sum(-1).to(torch.int32).cpu())
