@@ -48,6 +48,15 @@ __device__ __forceinline__ int block_max(int v, int* red) {
   return m;
 }
 
+// V8: eight envs per thread with 8-B / 16-B loads and stores (B % 8 == 0, aligned arrays): at
+// 8192 envs one pass of independent loads instead of eight dependent loop trips
+// (NULL counts as aligned: an absent optional array)
+inline bool aligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) == 0; }
+__device__ __forceinline__ int4 ld_i4(const int32_t* p) { return *reinterpret_cast<const int4*>(p); }
+__device__ __forceinline__ uint64_t ld_u8x8(const uint8_t* p) { return *reinterpret_cast<const uint64_t*>(p); }
+__device__ __forceinline__ int max4(int4 v) { return max(max(v.x, v.y), max(v.z, v.w)); }
+
+template <bool V8>
 __global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
     const uint8_t* __restrict__ flags, const uint8_t* __restrict__ err, const uint8_t* __restrict__ dec_err,
     const uint8_t* __restrict__ num_actions, const int32_t* __restrict__ max_actions,
@@ -55,15 +64,33 @@ __global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
     uint8_t* __restrict__ flags_copy, int32_t* __restrict__ left, uint8_t* __restrict__ pack) {
   __shared__ int red[kRedBlock / 64];
   int tmax = 0, omax = 0;
-  for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
-    const uint8_t f = flags[e];
-    flags_copy[e] = f;
-    left[e] = max_actions[e] - (int32_t)num_actions[e];
-    pack[e] = f;
-    pack[B + e] = err[e];
-    pack[2 * B + e] = dec_err[e];
-    if (text_len) tmax = max(tmax, text_len[e]);
-    if (obs_len) omax = max(omax, obs_len[e]);
+  if (V8) {
+    for (int64_t g = threadIdx.x; g < (B >> 3); g += kRedBlock) {
+      const int64_t e = g << 3;
+      const uint64_t f = ld_u8x8(flags + e), er = ld_u8x8(err + e), de = ld_u8x8(dec_err + e);
+      const uint64_t na = ld_u8x8(num_actions + e);
+      const int4 m0 = ld_i4(max_actions + e), m1 = ld_i4(max_actions + e + 4);
+      if (text_len) tmax = max(tmax, max(max4(ld_i4(text_len + e)), max4(ld_i4(text_len + e + 4))));
+      if (obs_len) omax = max(omax, max(max4(ld_i4(obs_len + e)), max4(ld_i4(obs_len + e + 4))));
+      *reinterpret_cast<uint64_t*>(flags_copy + e) = f;
+      const auto nb = [na](int j) { return (int32_t)((na >> (8 * j)) & 0xFFu); };
+      *reinterpret_cast<int4*>(left + e) = make_int4(m0.x - nb(0), m0.y - nb(1), m0.z - nb(2), m0.w - nb(3));
+      *reinterpret_cast<int4*>(left + e + 4) = make_int4(m1.x - nb(4), m1.y - nb(5), m1.z - nb(6), m1.w - nb(7));
+      *reinterpret_cast<uint64_t*>(pack + e) = f;
+      *reinterpret_cast<uint64_t*>(pack + B + e) = er;
+      *reinterpret_cast<uint64_t*>(pack + 2 * B + e) = de;
+    }
+  } else {
+    for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
+      const uint8_t f = flags[e];
+      flags_copy[e] = f;
+      left[e] = max_actions[e] - (int32_t)num_actions[e];
+      pack[e] = f;
+      pack[B + e] = err[e];
+      pack[2 * B + e] = dec_err[e];
+      if (text_len) tmax = max(tmax, text_len[e]);
+      if (obs_len) omax = max(omax, obs_len[e]);
+    }
   }
   tmax = block_max(tmax, red);
   omax = block_max(omax, red);
@@ -107,6 +134,7 @@ __global__ __launch_bounds__(kRedBlock) void rows_stats_kernel(const int32_t* __
   }
 }
 
+template <bool V8>
 __global__ __launch_bounds__(kRedBlock) void next_rows_stats_kernel(const int32_t* __restrict__ len,
                                                                     const uint8_t* __restrict__ has,
                                                                     const uint8_t* __restrict__ flags,
@@ -114,13 +142,31 @@ __global__ __launch_bounds__(kRedBlock) void next_rows_stats_kernel(const int32_
                                                                     int32_t* __restrict__ stats) {
   __shared__ int red[kRedBlock / 64];
   int m = 0, any = 0, cnt = 0;
-  for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
-    const bool next = (has ? has[e] != 0 : true) && !(flags[e] & RMI_FLAG_DONE);
-    if (next) {
-      m = max(m, len[e]);
-      ++cnt;
+  if (V8) {
+    for (int64_t g = threadIdx.x; g < (B >> 3); g += kRedBlock) {
+      const int64_t e = g << 3;
+      const uint64_t f = ld_u8x8(flags + e), h = has ? ld_u8x8(has + e) : ~0ull;
+      const int4 l0 = ld_i4(len + e), l1 = ld_i4(len + e + 4);
+      if (bad) any |= ld_u8x8(bad + e) != 0;
+      const int lv[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool next = ((h >> (8 * j)) & 0xFFu) != 0 && !((f >> (8 * j)) & RMI_FLAG_DONE);
+        if (next) {
+          m = max(m, lv[j]);
+          ++cnt;
+        }
+      }
     }
-    if (bad) any |= bad[e];
+  } else {
+    for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
+      const bool next = (has ? has[e] != 0 : true) && !(flags[e] & RMI_FLAG_DONE);
+      if (next) {
+        m = max(m, len[e]);
+        ++cnt;
+      }
+      if (bad) any |= bad[e];
+    }
   }
   m = block_max(m, red);
   any = block_max(any != 0 ? 1 : 0, red);
@@ -166,8 +212,15 @@ RMI_API int rmi_turn_readback(const uint8_t* flags, const uint8_t* err, const ui
   if (!pack || (B > 0 && (!flags || !err || !dec_err || !num_actions || !max_actions || !flags_copy || !left)))
     return RMI_EINVAL;
   if (reinterpret_cast<uintptr_t>(pack) & 3u) return RMI_EINVAL;
-  hipLaunchKernelGGL(turn_readback_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err, dec_err,
-                     num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack);
+  const bool v8 = B % 8 == 0 && aligned(flags, 8) && aligned(err, 8) && aligned(dec_err, 8) &&
+                  aligned(num_actions, 8) && aligned(flags_copy, 8) && aligned(pack, 8) && aligned(max_actions, 16) &&
+                  aligned(left, 16) && aligned(text_len, 16) && aligned(obs_len, 16);
+  if (v8)
+    hipLaunchKernelGGL(turn_readback_kernel<true>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err, dec_err,
+                       num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack);
+  else
+    hipLaunchKernelGGL(turn_readback_kernel<false>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err,
+                       dec_err, num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack);
   return launch_status();
 }
 
@@ -197,7 +250,12 @@ RMI_API int rmi_next_rows_stats(const int32_t* len, const uint8_t* has, const ui
   using namespace rmi;
   if (B < 0 || !stats || (B > 0 && (!len || !flags))) return RMI_EINVAL;
   if (reinterpret_cast<uintptr_t>(stats) & 3u) return RMI_EINVAL;
-  hipLaunchKernelGGL(next_rows_stats_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, has, flags, bad, B,
-                     stats);
+  const bool v8 = B % 8 == 0 && aligned(len, 16) && aligned(has, 8) && aligned(flags, 8) && aligned(bad, 8);
+  if (v8)
+    hipLaunchKernelGGL(next_rows_stats_kernel<true>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, has, flags,
+                       bad, B, stats);
+  else
+    hipLaunchKernelGGL(next_rows_stats_kernel<false>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, has, flags,
+                       bad, B, stats);
   return launch_status();
 }

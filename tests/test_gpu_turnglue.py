@@ -1,0 +1,49 @@
+"""The turn loop's reductions (csrc/turnglue.hip) against torch: rmi_turn_readback (flags copy,
+actions left, the packed readback with the longest text / observation) and rmi_next_rows_stats
+(longest next row, any pending host row, count) — the eight-envs-per-thread form (B % 8 == 0,
+aligned arrays) and the scalar form (ragged B, or arrays at odd offsets), optional inputs absent."""
+import numpy as np
+import pytest
+import torch
+
+from ragen_amd import _lib, ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _arrays(B, device, off, g):
+    def u8(hi):
+        return torch.randint(0, hi, (B + off,), generator=g, dtype=torch.int32).to(torch.uint8).to(device)[off:]
+
+    def i32(hi):
+        return torch.randint(0, hi, (B + off,), generator=g, dtype=torch.int32).to(device)[off:]
+    return u8, i32
+
+
+@pytest.mark.parametrize("B,off", [(8192, 0), (1000, 0), (8, 0), (4096, 1), (24, 3)])
+def test_turn_readback_and_next_rows_stats(device, B, off):
+    g = torch.Generator(device="cpu").manual_seed(B + off)
+    u8, i32 = _arrays(B, device, off, g)
+    flags, err, dec_err, num_actions = u8(8), u8(3), u8(2), u8(20)
+    max_actions, text_len, obs_len = i32(40) + 10, i32(5000), i32(90)
+    for tl, ol in ((text_len, obs_len), (None, None)):
+        flags_copy = torch.empty(B, dtype=torch.uint8, device=device)
+        left = torch.empty(B, dtype=torch.int32, device=device)
+        pack = torch.full((ops.readback_bytes(B),), 0xAB, dtype=torch.uint8, device=device)
+        ops.turn_readback(flags, err, dec_err, num_actions, max_actions, tl, ol, flags_copy, left, pack)
+        assert torch.equal(flags_copy, flags)
+        assert torch.equal(left, max_actions - num_actions.to(torch.int32))
+        h = pack.cpu().numpy()
+        assert (h[:B] == flags.cpu().numpy()).all() and (h[B:2 * B] == err.cpu().numpy()).all()
+        assert (h[2 * B:3 * B] == dec_err.cpu().numpy()).all()
+        o = (3 * B + 3) & ~3
+        tail = h[o:o + 8].view(np.int32)
+        assert tail[0] == (int(tl.max()) if tl is not None else 0) and tail[1] == (int(ol.max()) if ol is not None else 0)
+    length, has, bad = i32(3000), u8(2), u8(2)
+    for hs, bd in ((has, bad), (None, None)):
+        stats = torch.empty(3, dtype=torch.int32, device=device)
+        ops.next_rows_stats(length, hs, flags, bd, stats)
+        nxt = ((flags & _lib.FLAG_DONE) == 0) & ((hs != 0) if hs is not None else True)
+        want = [int(length[nxt].max()) if bool(nxt.any()) else 0, int(bool((bd != 0).any())) if bd is not None else 0,
+                int(nxt.sum())]
+        assert stats.cpu().tolist() == want
