@@ -697,6 +697,13 @@ int rmi_rows_stats(const int32_t* len, const int64_t* rows, int64_t n_rows, cons
 int rmi_next_rows_stats(const int32_t* len, const uint8_t* has, const uint8_t* flags, const uint8_t* bad, int64_t B,
                         int32_t* stats, rmi_stream_t stream);
 
+/* rmi_prompt_commit then rmi_next_rows_stats with bad = the rows the commit flags, in one
+ * launch: bad / len_upd exactly as rmi_prompt_commit; stats = (the longest len over the envs
+ * with has (NULL: every env) and flags without FLAG_DONE, any bad row, their count).       */
+int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_err, const uint8_t* active,
+                            const int32_t* mark_tok, int32_t* len_upd, int64_t B, uint8_t* bad, const int32_t* len,
+                            const uint8_t* has, const uint8_t* flags, int32_t* stats, rmi_stream_t stream);
+
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and
  * FrozenLakeEnv.reset's env RNG (frozen_lake/env.py:28-37), both via gymnasium

@@ -176,6 +176,8 @@ _SIGS = {
     "rmi_prompt_text": (c_int32, [_P(Prompt), c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_gen_rows": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),
+    "rmi_prompt_commit_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_row_counts": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_void_p]),
     "rmi_gen_rows_chained": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),

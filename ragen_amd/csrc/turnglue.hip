@@ -114,6 +114,43 @@ __global__ __launch_bounds__(kGlueBlock) void prompt_commit_kernel(const uint8_t
   }
 }
 
+// rmi_prompt_commit followed by rmi_next_rows_stats over the bad rows it writes, in one
+// workgroup (both on the turn's critical path after the encode): bad / len_upd per env as
+// prompt_commit_kernel, then (longest next row, any bad, count) as next_rows_stats_kernel
+__global__ __launch_bounds__(kRedBlock) void prompt_commit_stats_kernel(
+    const uint8_t* __restrict__ bpe_err, const uint8_t* __restrict__ text_err, const uint8_t* __restrict__ active,
+    const int32_t* __restrict__ mark_tok, int32_t* __restrict__ len_upd, int64_t B, uint8_t* __restrict__ bad,
+    const int32_t* __restrict__ len, const uint8_t* __restrict__ has, const uint8_t* __restrict__ flags,
+    int32_t* __restrict__ stats) {
+  __shared__ int red[kRedBlock / 64];
+  int m = 0, any = 0, cnt = 0;
+  for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
+    const bool on = active ? active[e] != 0 : true;
+    const bool b = on && (bpe_err[e] != 0 || text_err[e] != 0);
+    bad[e] = b ? 1 : 0;
+    if (mark_tok && on) len_upd[e] = mark_tok[e];
+    any |= b;
+    if ((has ? has[e] != 0 : true) && !(flags[e] & RMI_FLAG_DONE)) {
+      m = max(m, len[e]);
+      ++cnt;
+    }
+  }
+  m = block_max(m, red);
+  any = block_max(any, red);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = cnt;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int c = 0;
+#pragma unroll
+    for (int w = 0; w < kRedBlock / 64; ++w) c += red[w];
+    stats[0] = m;
+    stats[1] = any;
+    stats[2] = c;
+  }
+}
+
 __global__ __launch_bounds__(kRedBlock) void rows_stats_kernel(const int32_t* __restrict__ len,
                                                                const int64_t* __restrict__ rows, int64_t n_rows,
                                                                const uint8_t* __restrict__ bad, int64_t B,
@@ -232,6 +269,19 @@ RMI_API int rmi_prompt_commit(const uint8_t* bpe_err, const uint8_t* text_err, c
   if (!bpe_err || !text_err || !bad) return RMI_EINVAL;
   hipLaunchKernelGGL(prompt_commit_kernel, dim3(glue_grid(B)), dim3(kGlueBlock), 0, as_stream(stream), bpe_err,
                      text_err, active, mark_tok, len_upd, B, bad);
+  return launch_status();
+}
+
+RMI_API int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_err, const uint8_t* active,
+                                    const int32_t* mark_tok, int32_t* len_upd, int64_t B, uint8_t* bad,
+                                    const int32_t* len, const uint8_t* has, const uint8_t* flags, int32_t* stats,
+                                    rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || (mark_tok && !len_upd) || !stats) return RMI_EINVAL;
+  if (B > 0 && (!bpe_err || !text_err || !bad || !len || !flags)) return RMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(stats) & 3u) return RMI_EINVAL;
+  hipLaunchKernelGGL(prompt_commit_stats_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), bpe_err, text_err,
+                     active, mark_tok, len_upd, B, bad, len, has, flags, stats);
   return launch_status();
 }
 

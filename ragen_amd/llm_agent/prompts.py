@@ -469,7 +469,7 @@ class DevicePrompts:
         text, tlen, _, terr = self._run_text(pieces, stride, obs, obs_len, ints, active=active)
         return text, tlen, terr, stride
 
-    def advance(self, d, bounds=None, merge=False):
+    def advance(self, d, bounds=None, merge=False, stats=None):
         """Append turn d["turn"] (a device-path turn record of EnvStateManager._step_device).
         bounds: (longest observation, longest response) in bytes when the record does not carry
         them yet (advance_eager); merge: the rows of a turn's second pass (their host rows join
@@ -481,7 +481,7 @@ class DevicePrompts:
         text, tlen, mark, terr, stride, last, flags, bound = self._turn_text(d, t + 2, d["has"], bounds)
         self._encode(text, tlen, terr, mark, stride,
                      lambda e: self._host_turn(e, t, not last and not int(flags[e]) & _lib.FLAG_DONE),
-                     active=d["has"], bound=bound, merge=merge)
+                     active=d["has"], bound=bound, merge=merge, stats=stats)
         self.turns_done = t + 1
 
     def advance_eager(self, d, stats, has_next=None, again=False) -> bool:
@@ -506,10 +506,14 @@ class DevicePrompts:
         obs_max = self._obs_bound(d["obs"])
         if obs_max is None and not again:
             return False
-        self.advance(d, bounds=(obs_max, resp_max), merge=again)
+        has_n = d["has"] if has_next is None else has_next
+        # the first pass: the commit and the next batch's stats in one launch (the rows the
+        # commit flags are the only pending ones: an earlier turn's were resolved first)
+        self.advance(d, bounds=(obs_max, resp_max), merge=again, stats=None if again else (has_n, d["flags"], stats))
         self.eager_turns += 0 if again else 1
-        pend = self._pending[0] if self._pending is not None else None
-        ops.next_rows_stats(self.len, d["has"] if has_next is None else has_next, d["flags"], pend, stats)
+        if again:
+            pend = self._pending[0] if self._pending is not None else None
+            ops.next_rows_stats(self.len, has_n, d["flags"], pend, stats)
         self._next_stats = None
         return True
 
@@ -637,7 +641,7 @@ class DevicePrompts:
     def _stride(n):
         return min(3072, (int(n) + 3) // 4 * 4)
 
-    def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None, bound=None, merge=False):
+    def _encode(self, text, tlen, terr, mark, stride, host_fn, active=None, bound=None, merge=False, stats=None):
         """Tokenize the rows onto the arena; the rows the device could not build are left for
         the host (``_resolve``), read back with the next readback of the arena lengths.  The
         launch's row size is ``bound`` (the host's, _text_bound) when given, else the longest
@@ -656,7 +660,11 @@ class DevicePrompts:
         # one launch (rmi_prompt_commit)
         bad = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
         act = None if active is None else (active if active.dtype == torch.uint8 else active.to(torch.uint8))
-        ops.prompt_commit(err, terr, act, mark_tok if mark is not None else None, self.len_upd, bad)
+        if stats is not None and prev is None:  # (has, flags, out): rmi_next_rows_stats fused in
+            ops.prompt_commit_stats(err, terr, act, mark_tok if mark is not None else None, self.len_upd, bad,
+                                    self.len, stats[0], stats[1], stats[2])
+        else:
+            ops.prompt_commit(err, terr, act, mark_tok if mark is not None else None, self.len_upd, bad)
         if prev is not None:
             bad = bad | prev[0]
         self._pending = (bad, host_fn)

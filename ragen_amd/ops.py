@@ -1073,6 +1073,26 @@ def prompt_commit(bpe_err, text_err, active, mark_tok, len_upd, bad):
                                   _ptr(bad), _stream(dev)), "rmi_prompt_commit")
 
 
+def prompt_commit_stats(bpe_err, text_err, active, mark_tok, len_upd, bad, length, has, flags, stats):
+    """rmi_prompt_commit_stats: prompt_commit, then next_rows_stats over the bad rows it wrote,
+    in one launch."""
+    dev = _dev(bpe_err, text_err, active, mark_tok, len_upd, bad, length, has, flags, stats)
+    for t, dt, nm in ((bpe_err, torch.uint8, "bpe_err"), (text_err, torch.uint8, "text_err"),
+                      (active, torch.uint8, "active"), (mark_tok, torch.int32, "mark_tok"),
+                      (len_upd, torch.int32, "len_upd"), (bad, torch.uint8, "bad"), (length, torch.int32, "len"),
+                      (has, torch.uint8, "has"), (flags, torch.uint8, "flags"), (stats, torch.int32, "stats")):
+        _dt(t, dt, nm)
+    B = bad.numel()
+    for t in (bpe_err, text_err, active, mark_tok, len_upd, length, has, flags):
+        if t is not None and t.numel() != B:
+            raise ValueError("every input must have one entry per env")
+    if stats.numel() < 3:
+        raise ValueError("stats: three ints")
+    check(lib().rmi_prompt_commit_stats(_ptr(bpe_err), _ptr(text_err), _ptr(active), _ptr(mark_tok), _ptr(len_upd), B,
+                                        _ptr(bad), _ptr(length), _ptr(has), _ptr(flags), _ptr(stats), _stream(dev)),
+          "rmi_prompt_commit_stats")
+
+
 def next_rows_stats(length, has, flags, bad, stats):
     """rmi_next_rows_stats: stats i32[3] = (max length over the envs with has (None: every env)
     and flags without FLAG_DONE, any bad, their count)."""

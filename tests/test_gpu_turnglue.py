@@ -47,3 +47,22 @@ def test_turn_readback_and_next_rows_stats(device, B, off):
         want = [int(length[nxt].max()) if bool(nxt.any()) else 0, int(bool((bd != 0).any())) if bd is not None else 0,
                 int(nxt.sum())]
         assert stats.cpu().tolist() == want
+
+
+@pytest.mark.parametrize("B", [8192, 1000, 1])
+def test_prompt_commit_stats_equals_the_two_launches(device, B):
+    """rmi_prompt_commit_stats == rmi_prompt_commit then rmi_next_rows_stats over its bad rows."""
+    g = torch.Generator(device="cpu").manual_seed(B)
+    u8, i32 = _arrays(B, device, 0, g)
+    bpe_err, text_err, active, flags, has = u8(2), u8(2), u8(2), u8(8), u8(2)
+    mark, length = i32(900), i32(3000)
+    for act, mk, hs in ((active, mark, has), (None, None, None)):
+        want_upd, got_upd = (i32(50) for _ in range(2))
+        got_upd.copy_(want_upd)
+        want_bad, got_bad = (torch.empty(B, dtype=torch.uint8, device=device) for _ in range(2))
+        want_st, got_st = (torch.empty(3, dtype=torch.int32, device=device) for _ in range(2))
+        ops.prompt_commit(bpe_err, text_err, act, mk, want_upd, want_bad)
+        ops.next_rows_stats(length, hs, flags, want_bad, want_st)
+        ops.prompt_commit_stats(bpe_err, text_err, act, mk, got_upd, got_bad, length, hs, flags, got_st)
+        assert torch.equal(got_bad, want_bad) and torch.equal(got_upd, want_upd)
+        assert got_st.cpu().tolist() == want_st.cpu().tolist()
