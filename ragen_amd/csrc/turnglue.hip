@@ -117,6 +117,7 @@ __global__ __launch_bounds__(kGlueBlock) void prompt_commit_kernel(const uint8_t
 // rmi_prompt_commit followed by rmi_next_rows_stats over the bad rows it writes, in one
 // workgroup (both on the turn's critical path after the encode): bad / len_upd per env as
 // prompt_commit_kernel, then (longest next row, any bad, count) as next_rows_stats_kernel
+template <bool V8>
 __global__ __launch_bounds__(kRedBlock) void prompt_commit_stats_kernel(
     const uint8_t* __restrict__ bpe_err, const uint8_t* __restrict__ text_err, const uint8_t* __restrict__ active,
     const int32_t* __restrict__ mark_tok, int32_t* __restrict__ len_upd, int64_t B, uint8_t* __restrict__ bad,
@@ -124,6 +125,43 @@ __global__ __launch_bounds__(kRedBlock) void prompt_commit_stats_kernel(
     int32_t* __restrict__ stats) {
   __shared__ int red[kRedBlock / 64];
   int m = 0, any = 0, cnt = 0;
+  if (V8) {  // eight envs per thread, 8- and 16-B accesses (B % 8 == 0, aligned arrays)
+    for (int64_t g = threadIdx.x; g < (B >> 3); g += kRedBlock) {
+      const int64_t e = g << 3;
+      const uint64_t be = ld_u8x8(bpe_err + e), te = ld_u8x8(text_err + e), f = ld_u8x8(flags + e);
+      const uint64_t ac = active ? ld_u8x8(active + e) : ~0ull, h = has ? ld_u8x8(has + e) : ~0ull;
+      const int4 l0 = ld_i4(len + e), l1 = ld_i4(len + e + 4);
+      int4 k0 = make_int4(0, 0, 0, 0), k1 = k0, u0 = k0, u1 = k0;
+      if (mark_tok) {
+        k0 = ld_i4(mark_tok + e);
+        k1 = ld_i4(mark_tok + e + 4);
+        u0 = ld_i4(len_upd + e);
+        u1 = ld_i4(len_upd + e + 4);
+      }
+      const int lv[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+      const int kv[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+      int uv[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      uint64_t bw = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int sh = 8 * j;
+        const bool on = ((ac >> sh) & 0xFFu) != 0;
+        const bool b = on && (((be >> sh) & 0xFFu) != 0 || ((te >> sh) & 0xFFu) != 0);
+        bw |= (uint64_t)(b ? 1 : 0) << sh;
+        any |= b;
+        if (on) uv[j] = kv[j];
+        if (((h >> sh) & 0xFFu) != 0 && !((f >> sh) & RMI_FLAG_DONE)) {
+          m = max(m, lv[j]);
+          ++cnt;
+        }
+      }
+      *reinterpret_cast<uint64_t*>(bad + e) = bw;
+      if (mark_tok) {
+        *reinterpret_cast<int4*>(len_upd + e) = make_int4(uv[0], uv[1], uv[2], uv[3]);
+        *reinterpret_cast<int4*>(len_upd + e + 4) = make_int4(uv[4], uv[5], uv[6], uv[7]);
+      }
+    }
+  } else
   for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
     const bool on = active ? active[e] != 0 : true;
     const bool b = on && (bpe_err[e] != 0 || text_err[e] != 0);
@@ -280,8 +318,15 @@ RMI_API int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_
   if (B < 0 || (mark_tok && !len_upd) || !stats) return RMI_EINVAL;
   if (B > 0 && (!bpe_err || !text_err || !bad || !len || !flags)) return RMI_EINVAL;
   if (reinterpret_cast<uintptr_t>(stats) & 3u) return RMI_EINVAL;
-  hipLaunchKernelGGL(prompt_commit_stats_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), bpe_err, text_err,
-                     active, mark_tok, len_upd, B, bad, len, has, flags, stats);
+  const bool v8 = B % 8 == 0 && aligned(bpe_err, 8) && aligned(text_err, 8) && aligned(active, 8) &&
+                  aligned(mark_tok, 16) && aligned(len_upd, 16) && aligned(bad, 8) && aligned(len, 16) &&
+                  aligned(has, 8) && aligned(flags, 8);
+  if (v8)
+    hipLaunchKernelGGL(prompt_commit_stats_kernel<true>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), bpe_err,
+                       text_err, active, mark_tok, len_upd, B, bad, len, has, flags, stats);
+  else
+    hipLaunchKernelGGL(prompt_commit_stats_kernel<false>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), bpe_err,
+                       text_err, active, mark_tok, len_upd, B, bad, len, has, flags, stats);
   return launch_status();
 }
 
