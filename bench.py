@@ -181,6 +181,9 @@ def layout_floor(active, hw=36, all_env_bytes=(1, 2, 1, 1, 1, 1, 8, 1, 5), lines
     return out
 
 
+GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: HBM3E 6.29 TB/s measured (float4 copy)
+
+
 def hbm_copy_peak(device, nbytes=1 << 30, reps=10):
     """Achievable HBM bandwidth on this box: rmi_device_copy (the library's 16-B-per-lane
     grid-stride streaming copy, MI355X_MICROARCH.md's float4-copy recipe) of 1 GiB, read +
@@ -737,7 +740,7 @@ def api_leg(device):
     return {"env_steps_per_s": device_path["env_steps_per_s"], "device_path": device_path,
             "dict_path": dict(dict_path["op"], ctypes=dict_path["ctypes"], host_us_per_turn_call=per_call,
                               note="EnvStateManager.step facade, host dicts + text obs each turn (the action-name "
-                                   "lists are built before the timed loop); best of 3 rollouts; the top level "
+                                   "lists are built before the timed loop); best of 4 rollouts; the top level "
                                    "goes through the torch custom op, `ctypes` through the C ABI directly")}
 
 
@@ -876,6 +879,46 @@ def launch_plan(gpus, environ, device_count):
     return "run", world
 
 
+def exchange_plan(mode, per_gather, G):
+    """The N>1 exchange placement: -> (mode, rollouts per gather).  The default is StarPO's own
+    order (agent_trainer.py:514-655): every rollout's record all-gathered right after it, serial
+    on the critical path, because the gathered batch feeds compute_advantage and the update
+    before the next rollout starts.  A gather per several rollouts (per_gather > 1) or the
+    overlapped placement (a gather behind the NEXT rollouts, which training cannot do) are
+    extras; overlap always gathers a whole replay's G rollouts."""
+    per_gather = int(per_gather)
+    if per_gather < 1:
+        raise ValueError("--rollouts-per-gather must be >= 1")
+    if mode == "serial":
+        if G % per_gather:
+            raise ValueError(f"--rollouts-per-gather {per_gather} must divide the {G} rollouts of a graph replay")
+        return "serial", per_gather
+    return mode, G  # overlap / auto: the amortised placements (auto picks between them)
+
+
+def serial_exchange(step, chunk, outs, G, p, gather=None):
+    """G rollouts on one stream, each run of p followed by its all-gather (step(j) runs rollout
+    j; chunk(p, k) is the k-th run of p arenas; outs[k] its gathered bytes): with p = 1 every
+    rollout's record is reassembled before the next rollout starts, the StarPO order."""
+    gather = gather or rd.gather_bytes
+    for j in range(G):
+        step(j)
+        if (j + 1) % p == 0:
+            k = j // p
+            gather(chunk(p, k), outs[k])
+
+
+def exchange_label(mode, P, G, asked, graph):
+    if not graph:
+        return "all-gather of the episode arena after every rollout, serial (eager)"
+    if mode == "overlap":
+        return (f"one all-gather per {G} rollouts, overlapped with the next {G} on a comm stream "
+                f"(amortised extra; --exchange {asked})")
+    if P == 1:
+        return "all-gather of the episode arena after every rollout, serial on the same stream (StarPO order)"
+    return f"one all-gather per {P} rollouts, serial on the same stream (amortised extra; --exchange {asked})"
+
+
 def spawn_ranks(gpus, argv):
     """Start `gpus` rank processes of this script through torch.distributed.run on 127.0.0.1 (a
     free port), wait, and return their exit status.  The parent never initialises the GPU."""
@@ -918,7 +961,7 @@ def check_gathered(own, gathered, world, rank, distinct=True):
     return bool(ok)
 
 
-def main():
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -927,11 +970,20 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the advantage leg and the copy-peak probe")
     ap.add_argument("--group", type=int, default=8, help="rollouts per graph replay (reduced to divide --steps)")
-    ap.add_argument("--exchange", choices=("auto", "overlap", "serial"), default="auto",
-                    help="N>1: gather overlapped with the next rollouts on a comm stream, or serial after them")
+    ap.add_argument("--exchange", choices=("serial", "overlap", "auto"), default="serial",
+                    help="N>1: the all-gather serial after its rollouts on the same stream (StarPO: the gathered "
+                         "batch feeds compute_advantage and the update before the next rollout), or overlapped "
+                         "with the next rollouts on a comm stream (an extra: training cannot do that)")
+    ap.add_argument("--rollouts-per-gather", type=int, default=1,
+                    help="N>1: rollouts whose arenas one all-gather reassembles (1 = every rollout's batch "
+                         "gathered before its update, as agent_trainer.fit does; >1 amortises it: an extra)")
     ap.add_argument("--double-buffer", action="store_true",
                     help="run the N>1 exchange path at N=1 (a 1-rank RCCL group, real collectives)")
-    args = ap.parse_args()
+    return ap
+
+
+def main():
+    args = make_parser().parse_args()
 
     # torch.cuda.device_count() does not initialise the GPU on this image, so the parent of a
     # self-spawned run stays GPU-free
@@ -975,6 +1027,7 @@ def main():
         if 1 <= g <= args.group and args.steps % g == 0:
             G = g
             break
+    exchange_mode, P = exchange_plan(args.exchange, args.rollouts_per_gather, G) if dist else (None, 1)
 
     def capture(fn, stream=None):
         g = torch.cuda.CUDAGraph()
@@ -983,7 +1036,7 @@ def main():
         return g
 
     graph = None
-    exchange_mode = None
+    variants = None
     if not args.no_graph:
         s = torch.cuda.Stream(device)
         s.wait_stream(torch.cuda.current_stream(device))
@@ -1010,20 +1063,37 @@ def main():
                 count[0] += G
         else:
             W = tdist.get_world_size()
-            outs = [torch.empty(W * sets.shape[1], dtype=torch.uint8, device=device) for _ in (0, 1)]
+            arena_bytes = sets.shape[1] // G
+            # outs[p][h][k]: the gathered bytes of set h's k-th chunk of p rollouts (p = 1: every
+            # rollout's arena on its own, the StarPO headline; p = G: one gather per replay)
+            outs = {p: [[torch.empty(W * p * arena_bytes, dtype=torch.uint8, device=device) for _ in range(G // p)]
+                        for _ in (0, 1)] for p in sorted({1, G})}
+
+            def chunk(h, p, k):  # set h's k-th run of p contiguous arenas
+                return sets[h][k * p * arena_bytes:(k + 1) * p * arena_bytes]
+
             comm, cap_s = torch.cuda.Stream(device), torch.cuda.Stream(device)
             comm.wait_stream(main_s)
             with torch.cuda.stream(comm):  # communicator setup must not happen under capture
-                for h in (0, 1):
-                    rd.gather_bytes(sets[h], outs[h])
+                for p in outs:
+                    for h in (0, 1):
+                        for k in range(G // p):
+                            rd.gather_bytes(chunk(h, p, k), outs[p][h][k])
             torch.cuda.synchronize()
-            gather_g = [capture(lambda h=h: rd.gather_bytes(sets[h], outs[h]), stream=cap_s) for h in (0, 1)]
-            serial_g = [capture(lambda h=h: (rollouts(h), rd.gather_bytes(sets[h], outs[h]))) for h in (0, 1)]
+
+            def serial_body(h, p):
+                def step(j):
+                    R.env.ep = eps[h * G + j]
+                    R.step()
+                serial_exchange(step, lambda q, k: chunk(h, q, k), outs[p][h], G, p)
+
+            serial_g = {p: [capture(lambda h=h, p=p: serial_body(h, p)) for h in (0, 1)] for p in outs}
+            gather_g = [capture(lambda h=h: rd.gather_bytes(sets[h], outs[G][h][0]), stream=cap_s) for h in (0, 1)]
             R.env.ep = eps[0]
             rolled = [torch.cuda.Event(), torch.cuda.Event()]
             gathered = [torch.cuda.Event(), torch.cuda.Event()]
 
-            def run_overlap():
+            def run_overlap():  # amortised: one gather per G rollouts, behind the next G (an extra)
                 h = (count[0] // G) & 1
                 if count[0] >= 2 * G:
                     main_s.wait_event(gathered[h])  # set h's previous gather has read it
@@ -1036,9 +1106,11 @@ def main():
                 torch.cuda.set_stream(main_s)
                 count[0] += G
 
-            def run_serial():  # G rollouts, then their gather, one single-stream graph
-                serial_g[(count[0] // G) & 1].replay()
-                count[0] += G
+            def run_serial_p(p):
+                def run_s():
+                    serial_g[p][(count[0] // G) & 1].replay()
+                    count[0] += G
+                return run_s
 
             def trial(fn, n=4):
                 tdist.barrier()
@@ -1051,12 +1123,20 @@ def main():
                 tdist.all_reduce(dt, op=tdist.ReduceOp.MAX)  # every rank picks the same mode
                 return float(dt.item())
 
-            exchange_mode = args.exchange
-            if exchange_mode == "auto":  # which wins depends on the gather's cost at this W
+            if exchange_mode == "auto":  # amortised placements only (P = G): which wins depends on W
                 t_ov = min(trial(run_overlap) for _ in range(3))
-                t_se = min(trial(run_serial) for _ in range(3))
+                t_se = min(trial(run_serial_p(G)) for _ in range(3))
                 exchange_mode = "overlap" if t_ov <= t_se else "serial"
-            run = run_overlap if exchange_mode == "overlap" else run_serial
+            run = run_overlap if exchange_mode == "overlap" else run_serial_p(P)
+
+            def variants_fn():
+                """ms per rollout of every placement, max over ranks, best of 3 trials of 4 replays
+                each: the StarPO form (a gather per rollout, serial) beside the amortised ones."""
+                forms = {"serial_gather_per_rollout": run_serial_p(1)}
+                if G > 1:
+                    forms[f"serial_gather_per_{G}_rollouts"] = run_serial_p(G)
+                    forms[f"overlap_gather_per_{G}_rollouts"] = run_overlap
+                return {k: min(trial(f) for _ in range(3)) / (4 * G) * 1e3 for k, f in forms.items()}
     else:
         G = 1
 
@@ -1108,18 +1188,23 @@ def main():
         exchange_ok = all(torch.equal(e.arena, eps[0].arena) for e in eps)
         if dist:
             r = tdist.get_rank()
+            p_run = G if exchange_mode == "overlap" else P
             for h in (0, 1):
-                exchange_ok = check_gathered(sets[h], outs[h], W, r) and exchange_ok
-            gathered_info = {"ranks": W, "bytes_per_rank_per_gather": int(sets.shape[1]),
-                             "bytes_per_gather": int(W * sets.shape[1]), "rollouts_per_gather": G,
-                             "check": "every rank's row of both gathered sets == the i64 digest that rank "
-                                      "all-gathered of its own set; own row byte for byte"}
+                for k in range(G // p_run):
+                    exchange_ok = check_gathered(chunk(h, p_run, k), outs[p_run][h][k], W, r,
+                                                 distinct=True) and exchange_ok
+            gathered_info = {"ranks": W, "bytes_per_rank_per_gather": int(p_run * arena_bytes),
+                             "bytes_per_gather": int(W * p_run * arena_bytes), "rollouts_per_gather": p_run,
+                             "check": "every rank's row of every gathered chunk == the i64 digest that rank "
+                                      "all-gathered of its own chunk; own row byte for byte"}
         ok_t = torch.tensor([1 if exchange_ok else 0], dtype=torch.int32, device=device)
         if dist:
             tdist.all_reduce(ok_t, op=tdist.ReduceOp.MIN)
         exchange_ok = bool(ok_t.item())
         if not exchange_ok:
             raise RuntimeError("replayed rollouts / gathered arenas do not match")
+        if dist:  # every placement timed beside the headline (collective: every rank)
+            variants = variants_fn()
 
     # ---- dominant-kernel roofline: HIP events around the turn launches (eager, same stream)
     n_prof = min(args.steps, 50)
@@ -1144,7 +1229,10 @@ def main():
     # identical work, and the headline above is already timed
     extras = not args.no_extras and rank == 0
     adv = advantage_leg(R, device) if extras else None
-    copy_peak = hbm_copy_peak(device) if extras else None
+    copy_probe = hbm_copy_peak(device) if extras else None
+    # frac_of_achievable's denominator: the larger of this box's probe and the guide's measured
+    # float4 copy (MI355X_MICROARCH.md: 6.29 TB/s), so a slow probe never inflates the fraction
+    copy_peak = max(copy_probe, GUIDE_COPY_GBS) if copy_probe else None
     toytext = toytext_legs(device) if extras else None
     api = api_leg(device) if not args.no_extras and rank == 0 else None
     text = text_leg(R, device) if not args.no_extras and rank == 0 else None
@@ -1210,11 +1298,15 @@ def main():
             "config": {"workload": f"Sokoban 6x6 1-box, {B_PER_GPU} envs/GPU x {T_TURNS} turns, K={K_ACTIONS}, "
                                    f"cap {MAX_ACTIONS}, groups of {GROUP}; rollout phase (reset excluded)",
                        "envs_per_gpu": B_PER_GPU, "env_steps_per_rollout_rank0": steps_per_rollout,
-                       "graph": graph is not None, "rollouts_per_replay": G, "parallelism": f"env-sharded x{world}"},
+                       "graph": graph is not None, "rollouts_per_replay": G, "parallelism": f"env-sharded x{world}",
+                       "exchange_mode": exchange_mode if dist else None,
+                       "rollouts_per_gather": (G if exchange_mode == "overlap" else P) if dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": _pmc_source(PMC_GLOB),
                          "achievable_peak": copy_peak,
+                         "achievable_peak_probe": copy_probe, "achievable_peak_guide": GUIDE_COPY_GBS,
+                         "achievable_peak_rule": "max(probe on this box, guide's float4 copy)",
                          "frac_of_achievable": (achieved / copy_peak) if copy_peak else None,
                          "kernel": "rmi_sokoban_step_turn", "avg_launch_us": avg_launch_us,
                          "bytes_per_env_turn": BYTES_PER_ENV_TURN, "active_envs_per_turn": active_per_turn,
@@ -1232,11 +1324,8 @@ def main():
             "toytext": toytext,
             "api_variant": api,
             "text_api": text,
-            "exchange": ("all-gather of the episode arena per rollout"
-                         + (f", one captured all-gather per {G} rollouts, "
-                            + (f"overlapped with the next {G} on a comm stream" if exchange_mode == "overlap"
-                               else "after them on the same stream") + " (chosen by --exchange " + args.exchange + ")"
-                            if graph is not None else "")) if dist else None,
+            "exchange": exchange_label(exchange_mode, P, G, args.exchange, graph is not None) if dist else None,
+            "exchange_variants_ms_per_rollout": variants,
             "records_checked": exchange_ok,
             "gathered": gathered_info,
             "eager_ms_per_step": eager_ms,

@@ -648,8 +648,6 @@ class EnvStateManager:
             eager = eager and eager2
             rec = rec2
         rec["text_max"], rec["obs_max"] = int(tail[0]), (int(tail[1]) if rec.pop("_obs_known") else None)
-        if eager:
-            hook.set_next_stats(t, tail[2:5])
         self._turn_records.append(rec)
         n_in = len(inp.env_ids)
         fl_h = host[:n]
@@ -663,13 +661,16 @@ class EnvStateManager:
             still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
         all_still = bool(still.all())
         self._all_active = n_in == self.n_envs and all_still
+        out_ids = inp.env_ids if all_still else inp.env_ids[still]
+        if eager:  # the next batch's stats, valid for exactly the env-id array handed out below
+            hook.set_next_stats(t, tail[2:5], out_ids)
         if err_h.any():
             for tg in self.tags:
                 gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]
                 self._raise_errors(tg, err_h[tg.lo - self.env_lo:tg.hi - self.env_lo], [g - tg.lo for g in gids],
                                    gids)
             self._turn_records[-1]["err_seen"] = True
-        return LazyEnvOutputs(self, inp.env_ids if all_still else inp.env_ids[still])
+        return LazyEnvOutputs(self, out_ids)
 
     def _device_pass(self, inp, t, first):
         """The device launches of one pass of turn t over the envs with a generation in ``inp``

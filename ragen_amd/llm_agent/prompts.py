@@ -517,10 +517,11 @@ class DevicePrompts:
         self._next_stats = None
         return True
 
-    def set_next_stats(self, turn, vals):
+    def set_next_stats(self, turn, vals, env_ids):
         """advance_eager's stats as read back with the turn: (turns done, longest row, any host
-        row, row count)."""
-        self._next_stats = (turn + 1, int(vals[0]), int(vals[1]), int(vals[2]))
+        row, row count, the env-id array they were counted over -- EnvStateManager hands that
+        very array out; gen_batch takes the stats only for it)."""
+        self._next_stats = (turn + 1, int(vals[0]), int(vals[1]), int(vals[2]), env_ids)
 
     def _obs_bound(self, rows_by_tag):
         """The widest observation row (bytes) this turn's rows can hold, from the host: each
@@ -743,9 +744,9 @@ class DevicePrompts:
             S = 1
         else:
             ns, self._next_stats = self._next_stats, None
-            if ns is not None and ns[0] == self.turns_done and ns[3] == rows.numel():
-                # the stats came with the turn's readback (advance_eager): these rows are the
-                # envs that went on, the ones it counted
+            if ns is not None and ns[0] == self.turns_done and ns[4] is env_ids and ns[3] == rows.numel():
+                # the stats came with the turn's readback (advance_eager) for exactly these env
+                # ids (the array the turn handed out: the envs that went on, the ones it counted)
                 mx, any_bad = ns[1], ns[2]
                 self._resolve(bool(any_bad))
             else:  # one readback: the longest row and whether any row is the host's (rmi_rows_stats)

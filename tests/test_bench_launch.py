@@ -108,3 +108,70 @@ def test_check_gathered_gloo_world2():
         assert not corrupt
         assert not duplicated
         assert not same   # identical sets on every rank: not distinct
+
+
+def test_exchange_default_is_a_serial_gather_per_rollout():
+    """The N>1 headline runs StarPO's order by default (agent_trainer.py:514-655): each rollout's
+    record all-gathered right after it, on the critical path; amortised / overlapped placements
+    only on request."""
+    args = bench.make_parser().parse_args([])
+    assert args.exchange == "serial" and args.rollouts_per_gather == 1
+    assert bench.exchange_plan(args.exchange, args.rollouts_per_gather, 4) == ("serial", 1)
+    assert bench.exchange_plan("serial", 4, 4) == ("serial", 4)
+    assert bench.exchange_plan("overlap", 1, 4) == ("overlap", 4)   # overlap gathers a whole replay
+    assert "every rollout" in bench.exchange_label("serial", 1, 4, "serial", True)
+    assert "extra" in bench.exchange_label("overlap", 4, 4, "overlap", True)
+    assert "extra" in bench.exchange_label("serial", 4, 4, "serial", True)
+    for bad in ((0, 4), (3, 4)):
+        try:
+            bench.exchange_plan("serial", *bad)
+        except ValueError:
+            continue
+        raise AssertionError(f"exchange_plan accepted --rollouts-per-gather {bad[0]} for G={bad[1]}")
+
+
+def _serial_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    G, n = 4, 37
+    arenas = torch.zeros(G * n, dtype=torch.uint8)
+    order = []
+
+    def step(j):  # rollout j writes its arena (rank- and rollout-specific bytes)
+        order.append(("roll", j))
+        arenas[j * n:(j + 1) * n] = torch.arange(n, dtype=torch.uint8) * (rank + 1) + 17 * j
+
+    def gather(buf, out):
+        order.append(("gather", len([o for o in order if o[0] == "gather"])))
+        rd.gather_bytes(buf, out)
+
+    res = {}
+    for p in (1, G):
+        order.clear()
+        arenas.zero_()
+        outs = [torch.empty(world * p * n, dtype=torch.uint8) for _ in range(G // p)]
+        bench.serial_exchange(step, lambda q_, k: arenas[k * q_ * n:(k + 1) * q_ * n], outs, G, p, gather=gather)
+        ok = all(bench.check_gathered(arenas[k * p * n:(k + 1) * p * n], outs[k], world, rank) for k in range(G // p))
+        res[p] = (list(order), ok)
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_serial_exchange_gathers_each_rollout_before_the_next_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = [ctx.Process(target=_serial_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, r in res:
+        order1, ok1 = r[1]
+        assert ok1 and order1 == [x for j in range(4) for x in (("roll", j), ("gather", j))]
+        order4, ok4 = r[4]
+        assert ok4 and order4 == [("roll", j) for j in range(4)] + [("gather", 0)]
