@@ -704,6 +704,96 @@ int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_err, con
                             const int32_t* mark_tok, int32_t* len_upd, int64_t B, uint8_t* bad, const int32_t* len,
                             const uint8_t* has, const uint8_t* flags, int32_t* stats, rmi_stream_t stream);
 
+/* ------------------------------------------------------------ the turn chain
+ * Replaces: one turn of LLMAgentProxy.rollout's loop (agent_proxy.py:150-155) from the actor's
+ *           output to the next generation batch's shape -- ContextManager.get_env_inputs
+ *           (ctx_manager.py:332-352), EnvStateManager.step (es_manager.py:105-171) with the
+ *           env's render (sokoban/env.py:53-61, frozen_lake/env.py:47-61), and the part of the
+ *           next get_lm_inputs (ctx_manager.py:228-278) that one turn adds to each prompt --
+ *           as ONE host call that enqueues every launch of the turn on `stream`, copies the
+ *           turn's packed readback to host memory and waits for it.  [host] struct; every
+ *           pointer in it is a device pointer unless marked [host].
+ *
+ * In order (each step exactly the entry point named; see there):
+ *   1. rmi_gen_rows_chained(resp, n_resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has_t,
+ *      raw_max, raw_next) with ids / n_ids / has_t passed only when src != NULL -- skipped when
+ *      resp == NULL (the rows are on the device already)
+ *   2. rmi_detok_parse(ids, n_envs, R, n_ids, vocab, text, stride, text_len, dec_err, parse, sel,
+ *      actions, n_actions, spans, -, -, 0, parse_err): ids [n_envs, R] are every env's row (= resp
+ *      when src == NULL), n_ids NULL = R ids each
+ *   3. rmi_turn_inputs(has_t, dec_err, n_envs, has, err): has_t NULL = every env has a generation
+ *   4. the env's turn on {turn, K, actions, n_actions, has, max_actions_per_traj,
+ *      format_penalty} with its render into obs: rmi_sokoban_step_turn_render (env_kind 0), or
+ *      rmi_frozenlake_step_turn then rmi_frozenlake_render (env_kind 1)
+ *   5. rmi_turn_readback(ep->flags, err, dec_err, ep->num_actions, max_actions, text_len,
+ *      obs->len, n_envs, flags_copy, left, pack)
+ *   6. (prompt != NULL) rmi_prompt_text(prompt, n_envs, ptext, pstride, ptext_len, pmark, pterr),
+ *      rmi_bpe_encode(bpe, ptext, pstride, bpe_stride, ptext_len, n_envs, arena, arena_stride,
+ *      arena_len, NULL, pmark, mark_tok, bpe_err) and rmi_prompt_commit_stats(bpe_err, pterr,
+ *      has, mark_tok, len_upd, n_envs, bad, arena_len, has, flags_copy, stats)
+ *   7. rmi_readback(host, pack, pack_bytes): the copy, then the stream waited on.
+ * One env tag (one env batch) per chain.  A step that fails returns its code at once (the
+ * steps before it are enqueued; nothing after it is).                                       */
+enum { RMI_CHAIN_SOKOBAN = 0, RMI_CHAIN_FROZENLAKE = 1 };
+typedef struct {
+  int64_t n_envs;
+  /* 1. the generations */
+  const int64_t* resp;
+  int64_t n_resp, R;
+  const int64_t* src;               /* [n_envs] row of each env (-1: none); NULL: every env in order */
+  const uint32_t* vocab_packed;
+  const uint8_t* vocab_bytes;
+  int64_t vocab_n_bytes, V;
+  int64_t* ids;                     /* [n_envs, R] every env's row (written by step 1 when src)    */
+  int32_t* n_ids;                   /* [n_envs] or NULL (R each)                                   */
+  uint8_t* has_t;                   /* [n_envs] or NULL (every env)                                */
+  int32_t* raw_max, *raw_next;
+  /* 2. decode + parse */
+  const rmi_parse_cfg_t* parse;
+  const uint8_t* sel;
+  uint8_t* text;
+  int32_t stride;
+  int32_t* text_len;
+  uint8_t* dec_err;
+  int8_t* actions;                  /* [n_envs, K]                                                  */
+  uint8_t* n_actions;
+  int32_t* spans;                   /* [n_envs, 4]                                                  */
+  uint8_t* parse_err;
+  /* 3-4. the turn and its render */
+  uint8_t* has, *err;
+  int32_t env_kind;                 /* RMI_CHAIN_*                                                  */
+  const rmi_sokoban_t* sokoban;
+  const rmi_frozenlake_t* frozenlake;
+  const rmi_episode_t* ep;
+  int32_t turn, K, max_actions_per_traj;
+  double format_penalty;
+  const rmi_render_t* obs;
+  /* 5. the record's columns and the packed readback */
+  const int32_t* max_actions;
+  uint8_t* flags_copy;
+  int32_t* left;
+  uint8_t* pack;
+  /* 6. the next prompt's append (prompt NULL: none) */
+  const rmi_prompt_t* prompt;
+  uint8_t* ptext;
+  int32_t pstride;
+  int32_t* ptext_len, *pmark;
+  uint8_t* pterr;
+  const rmi_bpe_t* bpe;
+  int32_t bpe_stride;
+  int64_t* arena;
+  int64_t arena_stride;
+  int32_t* arena_len, *mark_tok;
+  uint8_t* bpe_err;
+  int32_t* len_upd;
+  uint8_t* bad;
+  int32_t* stats;                   /* i32[3], inside pack                                          */
+  /* 7. the readback */
+  void* host;                       /* [host] pinned, >= pack_bytes                                 */
+  int64_t pack_bytes;
+} rmi_turn_chain_t;
+int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t stream);
+
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and
  * FrozenLakeEnv.reset's env RNG (frozen_lake/env.py:28-37), both via gymnasium

@@ -98,6 +98,29 @@ class Prompt(ctypes.Structure):
                 ("int_reward_tags", ctypes.c_uint32), ("last_turn", c_int32)]
 
 
+class TurnChain(ctypes.Structure):
+    """rmi_turn_chain_t: one device turn of the rollout loop as one call (rmi_turn_chain)."""
+    _fields_ = [("n_envs", c_int64),
+                ("resp", c_void_p), ("n_resp", c_int64), ("R", c_int64), ("src", c_void_p),
+                ("vocab_packed", c_void_p), ("vocab_bytes", c_void_p), ("vocab_n_bytes", c_int64), ("V", c_int64),
+                ("ids", c_void_p), ("n_ids", c_void_p), ("has_t", c_void_p), ("raw_max", c_void_p),
+                ("raw_next", c_void_p),
+                ("parse", c_void_p), ("sel", c_void_p), ("text", c_void_p), ("stride", c_int32),
+                ("text_len", c_void_p), ("dec_err", c_void_p), ("actions", c_void_p), ("n_actions", c_void_p),
+                ("spans", c_void_p), ("parse_err", c_void_p),
+                ("has", c_void_p), ("err", c_void_p), ("env_kind", c_int32), ("sokoban", c_void_p),
+                ("frozenlake", c_void_p), ("ep", c_void_p), ("turn", c_int32), ("K", c_int32),
+                ("max_actions_per_traj", c_int32), ("format_penalty", c_double), ("obs", c_void_p),
+                ("max_actions", c_void_p), ("flags_copy", c_void_p), ("left", c_void_p), ("pack", c_void_p),
+                ("prompt", c_void_p), ("ptext", c_void_p), ("pstride", c_int32), ("ptext_len", c_void_p),
+                ("pmark", c_void_p), ("pterr", c_void_p), ("bpe", c_void_p), ("bpe_stride", c_int32),
+                ("arena", c_void_p), ("arena_stride", c_int64), ("arena_len", c_void_p), ("mark_tok", c_void_p),
+                ("bpe_err", c_void_p), ("len_upd", c_void_p), ("bad", c_void_p), ("stats", c_void_p),
+                ("host", c_void_p), ("pack_bytes", c_int64)]
+
+
+CHAIN_SOKOBAN, CHAIN_FROZENLAKE = 0, 1
+
 _P = ctypes.POINTER
 _SIGS = {
     "rmi_version": (ctypes.c_char_p, []),
@@ -194,6 +217,7 @@ _SIGS = {
     "rmi_prompt_commit": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_rows_stats": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_next_rows_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rmi_turn_chain": (c_int32, [_P(TurnChain), c_void_p]),
 }
 
 _lib = None

@@ -1,0 +1,72 @@
+// chain.cpp — rmi_turn_chain: one device turn of the rollout loop as one host call (host code:
+// it only sequences the library's own entry points on the caller's stream; include/ragen_amd.h).
+//
+// The Python turn loop paid ~20-60 us of interpreter and dispatcher work per launch between the
+// turn's ~10 launches (profiles/r04_api_host_stamps.txt: ~400 us of host time per 8192-env turn
+// against ~290 us of kernels), so the GPU idled between them.  Enqueued from here the launches
+// go back to back and the host's share of a turn is this call plus the Python that reads its
+// readback.
+#include <stdint.h>
+
+#include "ragen_amd.h"
+
+#define RMI_HOST_API extern "C" __attribute__((visibility("default")))
+
+RMI_HOST_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
+  if (!chain) return RMI_EINVAL;
+  const rmi_turn_chain_t& c = *chain;
+  const int64_t B = c.n_envs;
+  if (B < 1 || !c.ep || c.ep->B != B || !c.obs || !c.pack || !c.host || c.pack_bytes < 1 || !c.parse ||
+      (c.env_kind == RMI_CHAIN_SOKOBAN ? !c.sokoban : c.env_kind == RMI_CHAIN_FROZENLAKE ? !c.frozenlake : true))
+    return RMI_EINVAL;
+  int rc;
+  // 1. the generations onto the env rows (the longest one's raw bytes into the readback)
+  if (c.resp) {
+    rc = rmi_gen_rows_chained(c.resp, c.n_resp, c.R, c.src, B, c.vocab_packed, c.V, c.src ? c.ids : nullptr,
+                              c.src ? c.n_ids : nullptr, c.src ? c.has_t : nullptr, c.raw_max, c.raw_next, s);
+    if (rc) return rc;
+  }
+  // 2. decode + parse
+  rc = rmi_detok_parse(c.ids, B, c.R, c.n_ids, c.vocab_packed, c.vocab_bytes, c.vocab_n_bytes, c.V,
+                       c.text, c.stride, c.text_len, c.dec_err, c.parse, c.sel, c.actions, c.n_actions, c.spans,
+                       nullptr, nullptr, 0, c.parse_err, s);
+  if (rc) return rc;
+  // 3. the envs that step: a generation, decoded without error; the step errors zeroed
+  rc = rmi_turn_inputs(c.has_t, c.dec_err, B, c.has, c.err, s);
+  if (rc) return rc;
+  // 4. the turn and the next observation
+  rmi_turn_t in;
+  in.turn = c.turn;
+  in.K = c.K;
+  in.actions = c.actions;
+  in.n_actions = c.n_actions;
+  in.has_input = c.has;
+  in.max_actions_per_traj = c.max_actions_per_traj;
+  in.format_penalty = c.format_penalty;
+  if (c.env_kind == RMI_CHAIN_SOKOBAN) {
+    rc = rmi_sokoban_step_turn_render(c.sokoban, c.ep, &in, c.err, nullptr, nullptr, nullptr, c.obs, s);
+  } else {
+    rc = rmi_frozenlake_step_turn(c.frozenlake, c.ep, &in, c.err, s);
+    if (!rc)
+      rc = rmi_frozenlake_render(c.frozenlake, (int32_t)B, c.obs->glyph_bytes, c.obs->glyph_len, c.obs->out,
+                                 c.obs->stride, c.obs->len, s);
+  }
+  if (rc) return rc;
+  // 5. the record's flags / actions-left columns and the packed readback
+  rc = rmi_turn_readback(c.ep->flags, c.err, c.dec_err, c.ep->num_actions, c.max_actions, c.text_len, c.obs->len, B,
+                         c.flags_copy, c.left, c.pack, s);
+  if (rc) return rc;
+  // 6. the next prompt's text, its ids appended to the arena, the commit and the next batch's stats
+  if (c.prompt) {
+    rc = rmi_prompt_text(c.prompt, B, c.ptext, c.pstride, c.ptext_len, c.pmark, c.pterr, s);
+    if (rc) return rc;
+    rc = rmi_bpe_encode(c.bpe, c.ptext, c.pstride, c.bpe_stride, c.ptext_len, B, c.arena, c.arena_stride,
+                        c.arena_len, nullptr, c.pmark, c.mark_tok, c.bpe_err, s);
+    if (rc) return rc;
+    rc = rmi_prompt_commit_stats(c.bpe_err, c.pterr, c.has, c.mark_tok, c.len_upd, B, c.bad, c.arena_len, c.has,
+                                 c.flags_copy, c.stats, s);
+    if (rc) return rc;
+  }
+  // 7. the one readback of the turn
+  return rmi_readback(c.host, c.pack, (size_t)c.pack_bytes, s);
+}

@@ -209,14 +209,63 @@ class DeviceEnvInputs:
 
     def __init__(self, ctx, env_ids, has_t, ids, n_ids, stride):
         # has_t: u8[n_envs] 1 for the envs with a generation (device), None = every env in order
-        self.ctx, self.env_ids, self.has_t = ctx, env_ids, has_t
-        self.ids, self.n_ids, self.stride = ids, n_ids, stride
+        self.ctx, self.env_ids, self._has_t = ctx, env_ids, has_t
+        self._ids, self._n_ids, self.stride = ids, n_ids, stride
         self.raw_max = None  # host int: the longest generation's raw bytes, when known
         self.raw_dev = None  # the same on the device (i32[1], rmi_gen_rows)
+        self.raw_next = None  # the other readback buffer's raw slot (rmi_gen_rows_chained zeroes it)
         self.pack = None     # the turn's readback buffer raw_dev lives in
+        # (resp, src host array or None): the generations not yet scattered onto the envs --
+        # the turn's first launch does it (llm_agent/turn_chain.py), or flush() on first use
+        self.pending_gen = None
         self.vocab = ctx.device_vocab
         self._text = self._text_len = self._err = None
         self._decoded = None
+
+    def flush(self):
+        """Launch the deferred rmi_gen_rows (the step-by-step path, or a reader before the turn)."""
+        if self.pending_gen is None:
+            return
+        resp, src = self.pending_gen
+        self.pending_gen = None
+        n, dev, v = self.ctx.n_envs, resp.device, self.vocab
+        if src is None:
+            direct.gen_rows(resp, None, n, v.packed, None, None, self.raw_dev, None, self.raw_next)
+            self._ids, self._n_ids, self._has_t = resp, None, None
+            return
+        R = resp.shape[1]
+        self._ids = torch.empty(n, R, dtype=torch.int64, device=dev)
+        self._n_ids = torch.empty(n, dtype=torch.int32, device=dev)
+        self._has_t = torch.empty(n, dtype=torch.uint8, device=dev)
+        direct.gen_rows(resp, ops.h2d(src, dev), n, v.packed, self._ids, self._n_ids, self.raw_dev, self._has_t,
+                        self.raw_next)
+
+    @property
+    def ids(self):
+        self.flush()
+        return self._ids
+
+    @ids.setter
+    def ids(self, v):
+        self._ids = v
+
+    @property
+    def n_ids(self):
+        self.flush()
+        return self._n_ids
+
+    @n_ids.setter
+    def n_ids(self, v):
+        self._n_ids = v
+
+    @property
+    def has_t(self):
+        self.flush()
+        return self._has_t
+
+    @has_t.setter
+    def has_t(self, v):
+        self._has_t = v
 
     def set_decoded(self, text, text_len, err):
         self._text, self._text_len, self._err = text, text_len, err
@@ -708,18 +757,11 @@ class ContextManager:
         # alternating by turn: each turn's gen_rows zeroes the other's raw slot for the next turn
         # (rmi_gen_rows_chained: no zeroing launch); a turn's buffer is read back (and done with)
         # before the turn after next reuses it.
-        nb = ops.readback_bytes(n)
-        packs = getattr(self, "_packs", None)
-        if packs is None or packs[0].numel() != nb or packs[0].device != resp.device:
-            packs = self._packs = [torch.zeros(nb, dtype=torch.uint8, device=dev) for _ in range(2)]
-            self._pack_i = 0
-        pack, nxt = packs[self._pack_i], packs[1 - self._pack_i]
+        pack, nxt = self.turn_packs()
         raw, raw_next = ops.readback_raw(pack, n), ops.readback_raw(nxt, n)
         if in_order or (len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n))):
-            # every env in order: the generations are the rows (n_ids = None: R ids each)
-            has_t, n_ids, ids = None, None, resp
-            direct.gen_rows(resp, None, n, vocab.packed, None, None, raw, None, raw_next)
-        else:  # one launch: the rows scattered onto the batch, n_ids, the raw width
+            src = None  # every env in order: the generations are the rows (n_ids = None: R ids each)
+        else:  # one launch: the rows scattered onto the batch, n_ids, has_t, the raw width
             local = env_ids - lo
             if local.size and (local.min() < 0 or local.max() >= n):
                 raise ValueError(f"env ids outside this manager's envs [{lo}, {lo + n})")
@@ -727,11 +769,7 @@ class ContextManager:
             src[local] = np.arange(len(env_ids))
             if np.count_nonzero(src >= 0) != local.size:  # (a sort-free duplicate check)
                 raise ValueError("duplicate env ids in the generation batch")
-            ids = torch.empty(n, R, dtype=torch.int64, device=dev)
-            n_ids = torch.empty(n, dtype=torch.int32, device=dev)
-            has_t = torch.empty(n, dtype=torch.uint8, device=dev)  # 1: the env has a generation
-            direct.gen_rows(resp, ops.h2d(src, dev), n, vocab.packed, ids, n_ids, raw, has_t, raw_next)
-        self._pack_i ^= 1  # (after the launch that zeroed the other buffer's slot)
+        self._pack_i ^= 1  # (the launch below zeroes the other buffer's slot before it is used again)
         # the decoded rows' width.  With a hint from the turns before (the longest generation
         # seen, with a margin) no readback: a longer generation overflows the decode's row, is
         # masked out of the turn's first pass and stepped by a second pass sized from the
@@ -740,18 +778,38 @@ class ContextManager:
         # invalid UTF-8).  Either way within the parse kernel's row limit; a generation past it
         # is flagged by the decode and refused by the step (ValueError).
         hint = self._raw_hint_pin if self._raw_hint_pin is not None else self._raw_hint
-        if hint is None or not resp.numel():
+        inp = DeviceEnvInputs(self, env_ids, None, None, None, 0)
+        inp.raw_dev = raw      # i32[1] on the device: the longest row's raw bytes (read back with the turn)
+        inp.raw_next = raw_next
+        inp.pack = pack
+        # the generation batch's pad_rows counted its flagged rows into this pack (DevicePrompts.gen_batch)
+        inp.pad_counted = self._pad_counted is pack
+        self._pad_counted = None
+        inp.pending_gen = (resp, src)
+        if hint is None or not resp.numel():  # the rows now: the decode is sized from their read-back width
+            inp.flush()
             raw_max = int(ops.d2h(raw, self)[0]) if resp.numel() else 0
             stride = decode_stride(raw_max, 3)
             self.note_raw(raw_max)
-        else:
+        else:  # the scatter waits for the turn's own launches (turn_chain), or its first reader
             raw_max = None
             stride = decode_stride(hint, 1)
-        inp = DeviceEnvInputs(self, env_ids, has_t, ids, n_ids, stride)
+        inp.stride = stride
         inp.raw_max = raw_max  # the decoded rows' length bound (longer only with U+FFFD replacements)
-        inp.raw_dev = raw      # i32[1] on the device: the longest row's raw bytes (read back with the turn)
-        inp.pack = pack
         return inp
+
+    _pad_counted = None  # the readback pack the last generation batch counted its flagged rows into
+
+    def turn_packs(self):
+        """(this turn's readback buffer, the other one): two, alternating by turn (allocated on
+        first use)."""
+        n, dev = self.n_envs, self.device
+        nb = ops.readback_bytes(n)
+        packs = getattr(self, "_packs", None)
+        if packs is None or packs[0].numel() != nb:
+            packs = self._packs = [torch.zeros(nb, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self._pack_i = 0
+        return packs[self._pack_i], packs[1 - self._pack_i]
 
     RAW_HINT_MARGIN = 1.1  # the decode's row over the longest generation seen (+ 32 bytes)
 

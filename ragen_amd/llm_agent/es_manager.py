@@ -619,13 +619,23 @@ class EnvStateManager:
             raise RuntimeError(f"more than agent_proxy.max_turn={self.max_turn} turns in one rollout")
         t = self._turn
         n = self.n_envs
-        rec, pack, hook, eager = self._device_pass(inp, t, None)
-        # one device -> host copy (pinned, then the stream waited on): the active set and the
-        # turn's per-env error bits, raised in the step where they happen, as the reference
-        # raises inside its per-env loop
-        host = ops.d2h(pack, self)
+        # the whole turn in one call into the library where it applies (turn_chain.py), else
+        # launch by launch; either way one device -> host copy (pinned, then the stream waited
+        # on): the active set and the turn's per-env error bits, raised in the step where they
+        # happen, as the reference raises inside its per-env loop
+        chain = self._turn_chain()
+        res = chain.run(inp, t) if chain is not None else None
+        if res is not None:
+            rec, host = res
+            hook, eager = self._prompt_hook, True
+        else:
+            rec, pack, hook, eager = self._device_pass(inp, t, None)
+            host = ops.d2h(pack, self)
         o = (3 * n + 3) & ~3
-        tail = host[o:o + 24].view(np.int32)  # max text / obs, the next batch's stats, raw max
+        tail = host[o:o + 28].view(np.int32)  # max text / obs, the next batch's stats, raw max, pad count
+        if getattr(inp, "pad_counted", False) and tail[6]:
+            raise RuntimeError(f"{int(tail[6])} rows of this turn's generation batch were longer than its width "
+                               "(rmi_pad_rows RMI_ERR_UNSUP): the actor was given left-cut prompts")
         if inp.raw_max is None:
             inp.ctx.note_raw(int(tail[5]))
         err_h = host[n:2 * n].copy()
@@ -642,7 +652,7 @@ class EnvStateManager:
             self._turn = t
             rec2, pack2, hook, eager2 = self._device_pass(inp2, t, rec)
             host = ops.d2h(pack2, self)
-            tail = host[o:o + 24].view(np.int32)
+            tail = host[o:o + 28].view(np.int32)
             err_h |= host[n:2 * n]
             dec_h = host[2 * n:3 * n]
             eager = eager and eager2
@@ -671,6 +681,20 @@ class EnvStateManager:
                                    gids)
             self._turn_records[-1]["err_seen"] = True
         return LazyEnvOutputs(self, out_ids)
+
+    use_turn_chain = True  # (tests compare the chained turn with the step-by-step one)
+
+    def _turn_chain(self):
+        """The turn chain of this manager and its device prompts (turn_chain.TurnChain), built
+        on first use; None where it does not apply."""
+        hook = self._prompt_hook
+        if not self.use_turn_chain or hook is None:
+            return None
+        ch = self.__dict__.get("_chain")
+        if ch is None or ch.pr is not hook:
+            from .turn_chain import TurnChain
+            ch = self._chain = TurnChain(self, hook.ctx, hook) if TurnChain.applies(self, hook) else None
+        return ch
 
     def _device_pass(self, inp, t, first):
         """The device launches of one pass of turn t over the envs with a generation in ``inp``

@@ -554,11 +554,7 @@ class DevicePrompts:
         # device (the prompt op's turn form): turn_exec, flags, the Countdown tags, the last turn
         flags = d["flags"]
         ints = d["left"]
-        pieces = [self.tpl.a_pre, (_lib.PT_RESPONSE, 0, 0), self.tpl.a_suf, (_lib.PT_MARK, 0, 0),
-                  (_lib.PT_IF, 0, 0), self.tpl.u_pre + "Reward:\n", (_lib.PT_REWARD, 0, 0),
-                  f"\n\nTurn {number}:\nState:\n", (_lib.PT_OBS, 0, 0), "\nYou have ", (_lib.PT_INT, 0, 0),
-                  self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
-        last = t + 1 >= self.max_turn
+        pieces, last = self.turn_pieces(t, number)
         obs_max, resp_max = bounds if bounds is not None else (d.get("obs_max"), d.get("text_max"))
         # the text rows sized from the host's bound on the longest row when it has one (the
         # kernel's LDS grows with the row: a tight row keeps more waves resident); a row past it
@@ -568,6 +564,16 @@ class DevicePrompts:
         text, tlen, mark, terr = self._run_text(pieces, stride, obs, obs_len, ints, reward, None, resp,
                                                 resp_len, spans, None, active, turn=(ne, flags, last))
         return text, tlen, mark, terr, stride, last, flags, bound
+
+    def turn_pieces(self, t, number):
+        """The program of the text turn t appends (the assistant block, its end marked, then --
+        unless the env is done or t is the rollout's last turn -- the user block with the reward
+        and the state under ``Turn {number}``): -> (pieces, last turn)."""
+        pieces = [self.tpl.a_pre, (_lib.PT_RESPONSE, 0, 0), self.tpl.a_suf, (_lib.PT_MARK, 0, 0),
+                  (_lib.PT_IF, 0, 0), self.tpl.u_pre + "Reward:\n", (_lib.PT_REWARD, 0, 0),
+                  f"\n\nTurn {number}:\nState:\n", (_lib.PT_OBS, 0, 0), "\nYou have ", (_lib.PT_INT, 0, 0),
+                  self._c_mid, (_lib.PT_TAG_CONST, 1, 0), "\n" + self.tpl.u_suf]
+        return pieces, t + 1 >= self.max_turn
 
     # ----------------------------------------------------------- max_context_window
     def _entry_state(self, j):
@@ -762,6 +768,10 @@ class DevicePrompts:
                 mx = int(ops.d2h(stats, self)[0])
             S = mx + self.tail.numel()
         ids, am, pos, err = direct.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
+        if rows.numel():  # rows longer than S would be left-cut: counted into the next turn's readback
+            pack, _ = self.ctx.turn_packs()
+            ops.count_nonzero_into(err, ops.readback_pad(pack, self.n_envs))
+            self.ctx._pad_counted = pack
         return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
 
     def update_rows(self, resolve=True):

@@ -1021,8 +1021,9 @@ def turn_inputs(has_t: Optional[torch.Tensor], dec_err: torch.Tensor, has: torch
 def readback_bytes(B: int) -> int:
     """The size of the turn's packed readback buffer for B envs: rmi_turn_readback's (flags |
     err | dec_err | max text_len, max obs_len), then room for rmi_next_rows_stats' three ints
-    (readback_stats) and the longest generation's raw bytes (readback_raw)."""
-    return ((3 * B + 3) & ~3) + 8 + 16
+    (readback_stats), the longest generation's raw bytes (readback_raw) and the count of the
+    generation batch's rows rmi_pad_rows flagged (readback_pad)."""
+    return ((3 * B + 3) & ~3) + 8 + 20
 
 
 def readback_stats(pack: torch.Tensor, B: int) -> torch.Tensor:
@@ -1035,6 +1036,21 @@ def readback_raw(pack: torch.Tensor, B: int) -> torch.Tensor:
     """The i32[1] of the packed readback buffer that carries the turn's longest generation."""
     o = ((3 * B + 3) & ~3) + 20
     return pack[o:o + 4].view(torch.int32)
+
+
+def readback_pad(pack: torch.Tensor, B: int) -> torch.Tensor:
+    """The i32[1] of the packed readback buffer that counts the generation batch's flagged rows."""
+    o = ((3 * B + 3) & ~3) + 24
+    return pack[o:o + 4].view(torch.int32)
+
+
+def count_nonzero_into(x: torch.Tensor, out: torch.Tensor):
+    """out i32[1] = the nonzero bytes of the u8 vector x (rmi_row_counts over one row): no
+    allocation, no readback of its own."""
+    _dev(x, out)
+    _dt(x, torch.uint8, "x")
+    _dt(out, torch.int32, "out")
+    check(lib().rmi_row_counts(_ptr(x), 1, x.numel(), _ptr(out), _stream(out.device)), "rmi_row_counts")
 
 
 def turn_readback(flags, err, dec_err, num_actions, max_actions, text_len, obs_len, flags_copy, left, pack):

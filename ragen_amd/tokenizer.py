@@ -399,6 +399,13 @@ class DeviceTokenizer:
                 self.added_id, [self.merge_mask, self.merge_shift, self.pretok, self.nfc, self.n_added]
                 + list(self.added_first))
 
+    def bpe_struct(self):
+        """The validated rmi_bpe_t of the current tables (expansions included), built once per
+        set of tables (torch_ops._bpe_struct): what rmi_bpe_encode / rmi_turn_chain take."""
+        from .torch_ops import _bpe_struct
+        return _bpe_struct(*self.args(), self.word_cache, self.exp_off if self.exp else None,
+                           self.exp_ids if self.exp else None, self.added_words, self.ascii_class)
+
     def encode_rows(self, text: torch.Tensor, text_len: torch.Tensor, out: torch.Tensor,
                     out_len: Optional[torch.Tensor] = None, mark_byte: Optional[torch.Tensor] = None,
                     max_len: int = 0):

@@ -246,3 +246,35 @@ def test_device_turn_decode_overflow_second_pass(device, which, qwen_tok, monkey
     _compare(ref, dev, ref_prompts, [tuple(x.cpu() for x in p) for p in actor.prompts], ref_proxy, proxy)
     n_turns = len(actor.prompts)
     assert proxy.last_timing["readbacks"]["turns"] == n_turns + 1, proxy.last_timing
+
+
+def test_gen_batch_takes_eager_stats_only_for_the_counted_ids(device, qwen_tok, monkeypatch):
+    """The next batch's row stats come back with the turn (advance_eager) for exactly the env-id
+    array the turn handed out; gen_batch given any other array (even an equal copy) reads the
+    stats back itself -- and builds the same batch."""
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    name = "sokoban_es"
+    cfg = _config(name)
+    _, ng, gs, T, _ = TRACES[name]
+    B = ng * gs
+    turn_tokens = [_ids(qwen_tok, _responses(name, t, B), device) for t in range(T)]
+    batches, counts = [], []
+    for copy_ids in (False, True):
+        proxy = LLMAgentProxy(cfg, TokenActor(turn_tokens), qwen_tok, device=device)
+        ctx, es = proxy.train_ctx_manager, proxy.train_es_manager
+        ctx.set_device_vocab(_vocab(qwen_tok, device))
+        env_outputs = es.reset(seed=11)
+        out = []
+        for t in range(2):
+            lm = ctx.get_lm_inputs(env_outputs, prepare_for_update=False)
+            out.append(lm.batch["input_ids"].cpu())
+            env_outputs = es.step(ctx.get_env_inputs(proxy.generate_sequences(lm)))
+        ids = env_outputs.env_ids.copy() if copy_ids else env_outputs.env_ids
+        c0 = ops.D2H_COUNT[0]
+        out.append(ctx.prompts().gen_batch(ids)["input_ids"].cpu())
+        counts.append(ops.D2H_COUNT[0] - c0)
+        batches.append(out)
+    assert counts == [0, 1]
+    for a, b in zip(*batches):
+        assert torch.equal(a, b)

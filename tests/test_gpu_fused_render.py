@@ -157,6 +157,31 @@ def test_first_and_last_turn_forms(device, B):
         torch.testing.assert_close(x, y, rtol=0, atol=0, equal_nan=True)
 
 
+@pytest.mark.parametrize("B", [8192, 65536])
+def test_first_form_helper_waves_leave_other_envs_alone(device, B):
+    """Pins round 4's room_state divergence of the fused first form: the render
+    helper waves of a workgroup (kObsFan - 1 per turn wave) must map to no env.  When they took
+    an env index from their wave number they indexed envs of the NEXT workgroups, skipped the
+    turn (not a turn wave) but still ran the reset-row store of the first form, rewriting those
+    envs' rows with their init rows after their own workgroup had stepped them: only room_state,
+    only the first form, and only where several workgroups run -- timing-dependent, so the launch
+    is repeated at two grid sizes."""
+    (a, b), _ = _pair(device, B, 6, 6, 1, seed=11)
+    ids, n = synthetic.rollout_actions(B, 1, 5, 1, 4, seed=5)
+    act, na = torch.from_numpy(ids[0]).to(device), torch.from_numpy(n[0]).to(device)
+    ts = ops.turn_struct(0, act, na, None, 10, -0.1)
+    ops.sokoban_step_turn_first(b.struct(), b.ep, ts, b.init_state, b.init_player)
+    torch.cuda.synchronize()
+    assert not torch.equal(b.room_state, b.init_state)  # envs moved: a reset store would show
+    lk = a.config.grid_lookup
+    for rep in range(6):
+        obs = ops.render_buffers(B, 6, 6, device)
+        r = ops.render_struct(lk, 6, 6, *obs)
+        ops.sokoban_step_turn_render(a.struct(), a.ep, ts, r, init_state=a.init_state, init_player=a.init_player)
+        torch.cuda.synchronize()
+        _state_equal(a, b, rep)
+
+
 def test_render_entry_validation(device):
     """Argument errors as the separate entry points report them."""
     B = 8192

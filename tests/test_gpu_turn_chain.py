@@ -1,0 +1,103 @@
+"""The turn chain (rmi_turn_chain, llm_agent/turn_chain.py: one call per device turn) against
+the step-by-step device turn (EnvStateManager._device_pass: the same kernels launched one by one
+from Python): LLMAgentProxy.rollout both ways on the golden traces' configs (Sokoban 6x6,
+Sokoban 8x8 with 2 boxes, FrozenLake), with the character tokenizer and the Qwen2-pipeline BPE,
+and on the bench's 8192-env workload -- every turn's generation batch, the formulated batch,
+its metrics and the rollout cache identical, the chain taken on every turn, its per-turn buffers
+reused by a second rollout."""
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from fake_tok import FakeQwenTok
+from ragen_amd import ops, synthetic
+from ragen_amd.llm_agent import EnvStateManager, LLMAgentProxy, TokenActor
+from ragen_amd.protocol import DataProto
+from test_gpu_device_prompts import _ids, _responses, _vocab
+from test_gpu_facade import TRACES, _config, _hashseed0_reseed
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def qwen_tok():
+    return synthetic.qwen_like_tokenizer()
+
+
+def _run(cfg, tok, turn_tokens, device, chain, reps=1, seed=7):
+    EnvStateManager.use_turn_chain = chain
+    try:
+        actor = TokenActor(turn_tokens, read_prompts=True)
+        proxy = LLMAgentProxy(cfg, actor, tok, device=device)
+        proxy.train_ctx_manager.set_device_vocab(_vocab(tok, device))
+        random.seed(seed)
+        outs = []
+        for _ in range(reps):
+            actor.prompts = []
+            out = proxy.rollout(DataProto(meta_info={}), val=False)
+            prompts = [tuple(x.cpu() for x in p) for p in actor.prompts]
+            outs.append((out, prompts, proxy.train_es_manager.rollout_cache, dict(out.meta_info)))
+        ch = proxy.train_es_manager.__dict__.get("_chain")
+        return outs, (ch.runs if ch is not None else 0), proxy
+    finally:
+        EnvStateManager.use_turn_chain = True
+
+
+def _same(a, b):
+    out_a, pr_a, rc_a, meta_a = a
+    out_b, pr_b, rc_b, meta_b = b
+    assert len(pr_a) == len(pr_b)
+    for t, (x, y) in enumerate(zip(pr_a, pr_b)):
+        for k, u, v in zip(("input_ids", "attention_mask", "position_ids"), x, y):
+            assert torch.equal(u, v), (t, k)
+    assert set(out_a.batch.keys()) == set(out_b.batch.keys())
+    for k in out_a.batch.keys():
+        assert torch.equal(out_a.batch[k].cpu(), out_b.batch[k].cpu()), k
+    assert meta_a == meta_b
+    assert rc_a == rc_b
+
+
+@pytest.mark.parametrize("which", ["fake", "qwen"])
+@pytest.mark.parametrize("name", ["sokoban_es", "sokoban8_es", "frozenlake_es"])
+def test_turn_chain_equals_step_by_step(device, name, which, qwen_tok, monkeypatch):
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok() if which == "fake" else qwen_tok
+    cfg = _config(name)
+    _, ng, gs, T, _ = TRACES[name]
+    B = ng * gs
+    turn_tokens = [_ids(tok, _responses(name, t, B), device) for t in range(T)]
+    chained, runs, proxy = _run(cfg, tok, turn_tokens, device, True, reps=2)
+    plain, runs0, _ = _run(cfg, tok, turn_tokens, device, False, reps=2)
+    assert runs0 == 0
+    n_turns = sum(len(o[1]) for o in chained)
+    assert runs == n_turns, (runs, n_turns)  # every turn of both rollouts went through the chain
+    for a, b in zip(chained, plain):
+        _same(a, b)
+    assert proxy.train_ctx_manager.prompts().host_rows_used == 0
+
+
+def test_turn_chain_bench_workload(device):
+    """The API leg's workload (8192 Sokoban envs x 5 turns, 10 % unknown action names, the
+    Qwen2-pipeline BPE): two rollouts chained == step by step."""
+    from ragen_amd.config import env_task
+    B, T, K = 8192, 5, 5
+    cfg = env_task("SimpleSokoban", B // 16, 16, max_turn=T, max_actions_per_turn=K)
+    ids, n = synthetic.rollout_actions(B, T, K, 1, 4)
+    lk = {1: "Up", 2: "Down", 3: "Left", 4: "Right"}
+    tok = synthetic.qwen_like_tokenizer()
+    tokens = []
+    for t in range(T):
+        enc = tok(synthetic.responses_for_actions(ids[t], n[t], lk, seed=100 + t), padding=False).input_ids
+        R = max(len(x) for x in enc)
+        a = np.full((B, R), tok.pad_token_id, np.int64)
+        for i, x in enumerate(enc):
+            a[i, :len(x)] = x
+        tokens.append(torch.from_numpy(a).to(device))
+    chained, runs, _ = _run(cfg, tok, tokens, device, True, reps=2, seed=0)
+    plain, _, _ = _run(cfg, tok, tokens, device, False, reps=2, seed=0)
+    assert runs == sum(len(o[1]) for o in chained)
+    for a, b in zip(chained, plain):
+        _same(a, b)

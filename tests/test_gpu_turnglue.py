@@ -66,3 +66,16 @@ def test_prompt_commit_stats_equals_the_two_launches(device, B):
         ops.prompt_commit_stats(bpe_err, text_err, act, mk, got_upd, got_bad, length, hs, flags, got_st)
         assert torch.equal(got_bad, want_bad) and torch.equal(got_upd, want_upd)
         assert got_st.cpu().tolist() == want_st.cpu().tolist()
+
+
+@pytest.mark.parametrize("n", [8192, 1000, 3, 1])
+def test_count_nonzero_into_the_readback(device, n):
+    """The generation batch's flagged-row count (ops.count_nonzero_into -> readback_pad slot)."""
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x = (torch.rand(n, generator=g) < 0.01).to(torch.uint8) * torch.randint(1, 256, (n,), generator=g).to(torch.uint8)
+    x = x.to(device)
+    pack = torch.full((ops.readback_bytes(64),), 0xAB, dtype=torch.uint8, device=device)
+    slot = ops.readback_pad(pack, 64)
+    ops.count_nonzero_into(x, slot)
+    assert int(slot.item()) == int((x != 0).sum())
+    assert (pack[:-4].cpu().numpy() == 0xAB).all()  # nothing else of the pack written
