@@ -704,6 +704,13 @@ int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_err, con
                             const int32_t* mark_tok, int32_t* len_upd, int64_t B, uint8_t* bad, const int32_t* len,
                             const uint8_t* has, const uint8_t* flags, int32_t* stats, rmi_stream_t stream);
 
+/* The next generation batch's rows (es_manager.py:168-169 for a turn whose envs came in ascending
+ * order, ctx_manager.py:265-278's batch order): rows i64[count] = the envs e, ascending, with
+ * has[e] (NULL: every env) and no RMI_FLAG_DONE in flags[e]; src i64[B]: src[e] = e's index in
+ * rows, or -1 (the next turn's rmi_gen_rows map).  count = rmi_next_rows_stats' stats[2].    */
+int rmi_next_rows_list(const uint8_t* has, const uint8_t* flags, int64_t B, int64_t* rows, int64_t* src,
+                       rmi_stream_t stream);
+
 /* ------------------------------------------------------------ the turn chain
  * Replaces: one turn of LLMAgentProxy.rollout's loop (agent_proxy.py:150-155) from the actor's
  *           output to the next generation batch's shape -- ContextManager.get_env_inputs
@@ -715,6 +722,8 @@ int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_err, con
  *           pointer in it is a device pointer unless marked [host].
  *
  * In order (each step exactly the entry point named; see there):
+ *   0. (pad_err != NULL) rmi_row_counts(pad_err, 1, n_pad, pad_count): the rows of the generation
+ *      batch rmi_pad_rows flagged, counted into the readback
  *   1. rmi_gen_rows_chained(resp, n_resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has_t,
  *      raw_max, raw_next) with ids / n_ids / has_t passed only when src != NULL -- skipped when
  *      resp == NULL (the rows are on the device already)
@@ -731,12 +740,19 @@ int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_err, con
  *      rmi_bpe_encode(bpe, ptext, pstride, bpe_stride, ptext_len, n_envs, arena, arena_stride,
  *      arena_len, NULL, pmark, mark_tok, bpe_err) and rmi_prompt_commit_stats(bpe_err, pterr,
  *      has, mark_tok, len_upd, n_envs, bad, arena_len, has, flags_copy, stats)
- *   7. rmi_readback(host, pack, pack_bytes): the copy, then the stream waited on.
+ *   7. rmi_readback(host, pack, pack_bytes): the copy, then the stream waited on; with next_rows
+ *      the copy, then rmi_next_rows_list(has, flags_copy, n_envs, next_rows, next_src) enqueued
+ *      behind it, then the copy alone waited on (the list is done in stream order before any
+ *      later work on the stream).
  * One env tag (one env batch) per chain.  A step that fails returns its code at once (the
  * steps before it are enqueued; nothing after it is).                                       */
 enum { RMI_CHAIN_SOKOBAN = 0, RMI_CHAIN_FROZENLAKE = 1 };
 typedef struct {
   int64_t n_envs;
+  /* 0. the generation batch's error bytes (pad_err NULL: not counted) */
+  const uint8_t* pad_err;
+  int64_t n_pad;
+  int32_t* pad_count;               /* i32[1], inside pack                                          */
   /* 1. the generations */
   const int64_t* resp;
   int64_t n_resp, R;
@@ -788,11 +804,67 @@ typedef struct {
   int32_t* len_upd;
   uint8_t* bad;
   int32_t* stats;                   /* i32[3], inside pack                                          */
-  /* 7. the readback */
+  /* 7. the readback; the next generation batch's rows and gen_rows map (NULL: not written) */
+  int64_t* next_rows, *next_src;    /* [n_envs] each                                                */
   void* host;                       /* [host] pinned, >= pack_bytes                                 */
   int64_t pack_bytes;
 } rmi_turn_chain_t;
 int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t stream);
+
+/* ------------------------------------------------------- formulate_rollouts, chained
+ * Replaces: ContextManager.formulate_rollouts (ctx_manager.py:354-356 -> get_lm_inputs with
+ *           prepare_for_update, :228-330) over the device prompt arena and episode record.
+ *
+ * rmi_formulate_stats: stats i32[3] = (max len[e], any bad[e] (bad NULL: 0), max n_turns[e]) --
+ * the batch width, whether a row waits for the host, zip_longest's length (:52-62) -- and
+ * n_sc[e] = n_turns[e] widened (the assembly's n_scores).  One workgroup.
+ * rmi_assemble_rows_ex: rmi_assemble_rows, plus resp_count[b] (optional) = the ones of row b's
+ * response_mask (response_mask.sum(-1), :305) and, with last_score (flags without
+ * RMI_MS_TURN_SCORES), score[b, S-2] = last_score[b] -- the normalised score
+ * _normalize_score_tensor writes there in place (:175-226) -- instead of the raw sum.
+ * rmi_formulate_tail: out i64[2] = (sum of resp_count, OR of err): response_length's exact
+ * numerator and the assembly's error bits.  One workgroup.                                   */
+int rmi_formulate_stats(const int32_t* len, const uint8_t* bad, const uint8_t* n_turns, int64_t B, int32_t* n_sc,
+                        int32_t* stats, rmi_stream_t stream);
+int rmi_assemble_rows_ex(const int64_t* tokens, const int64_t* row_start, const int32_t* row_len, int64_t B,
+                         int64_t S, int64_t pad_id, int64_t special_token, int64_t reward_token, const double* scores,
+                         const int32_t* n_scores, int32_t T, int32_t n_slots, int32_t flags, const float* last_score,
+                         int64_t* input_ids, int64_t* attention_mask, int64_t* position_ids, float* score_out,
+                         uint8_t* loss_mask, uint8_t* response_mask, int32_t* resp_count, uint8_t* err,
+                         rmi_stream_t stream);
+int rmi_formulate_tail(const int32_t* resp_count, const uint8_t* err, int64_t B, int64_t* out, rmi_stream_t stream);
+
+/* rmi_formulate_chain: the update batch after its width is known, as one host call --
+ *   1. rmi_rollout_finalize(ep, seg, G, method, metrics, NULL, NULL, norm): get_rollout_states'
+ *      per-env metrics (es_manager.py:173-207) and the normalised trajectory scores
+ *   2. rmi_assemble_rows_ex(..., last_score = norm, ...): the left-padded batch, masks, scores
+ *   3. rmi_formulate_tail(resp_count, err, B, tail)
+ *   4. the n_copies device -> host copies (host[i] pinned), then the stream waited on.        */
+typedef struct {
+  const rmi_episode_t* ep;
+  const int32_t* seg;
+  int32_t G, method;
+  double* metrics;
+  float* norm;
+  const int64_t* tokens;
+  const int64_t* row_start;
+  const int32_t* row_len;
+  int64_t B, S, pad_id, special_token, reward_token;
+  const double* scores;
+  const int32_t* n_scores;
+  int32_t T, n_slots, flags;
+  int64_t* input_ids, *attention_mask, *position_ids;
+  float* score_out;
+  uint8_t* loss_mask, *response_mask;
+  int32_t* resp_count;
+  uint8_t* err;
+  int64_t* tail;
+  int32_t n_copies;                 /* <= 4                                                         */
+  void* host[4];                    /* [host] pinned                                                */
+  const void* dev[4];
+  int64_t bytes[4];
+} rmi_formulate_chain_t;
+int rmi_formulate_chain(const rmi_formulate_chain_t* chain, rmi_stream_t stream);
 
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and

@@ -100,7 +100,7 @@ class Prompt(ctypes.Structure):
 
 class TurnChain(ctypes.Structure):
     """rmi_turn_chain_t: one device turn of the rollout loop as one call (rmi_turn_chain)."""
-    _fields_ = [("n_envs", c_int64),
+    _fields_ = [("n_envs", c_int64), ("pad_err", c_void_p), ("n_pad", c_int64), ("pad_count", c_void_p),
                 ("resp", c_void_p), ("n_resp", c_int64), ("R", c_int64), ("src", c_void_p),
                 ("vocab_packed", c_void_p), ("vocab_bytes", c_void_p), ("vocab_n_bytes", c_int64), ("V", c_int64),
                 ("ids", c_void_p), ("n_ids", c_void_p), ("has_t", c_void_p), ("raw_max", c_void_p),
@@ -116,10 +116,23 @@ class TurnChain(ctypes.Structure):
                 ("pmark", c_void_p), ("pterr", c_void_p), ("bpe", c_void_p), ("bpe_stride", c_int32),
                 ("arena", c_void_p), ("arena_stride", c_int64), ("arena_len", c_void_p), ("mark_tok", c_void_p),
                 ("bpe_err", c_void_p), ("len_upd", c_void_p), ("bad", c_void_p), ("stats", c_void_p),
+                ("next_rows", c_void_p), ("next_src", c_void_p),
                 ("host", c_void_p), ("pack_bytes", c_int64)]
 
 
 CHAIN_SOKOBAN, CHAIN_FROZENLAKE = 0, 1
+
+
+class FormulateChain(ctypes.Structure):
+    """rmi_formulate_chain_t: formulate_rollouts' update batch as one call (rmi_formulate_chain)."""
+    _fields_ = [("ep", c_void_p), ("seg", c_void_p), ("G", c_int32), ("method", c_int32), ("metrics", c_void_p),
+                ("norm", c_void_p), ("tokens", c_void_p), ("row_start", c_void_p), ("row_len", c_void_p),
+                ("B", c_int64), ("S", c_int64), ("pad_id", c_int64), ("special_token", c_int64),
+                ("reward_token", c_int64), ("scores", c_void_p), ("n_scores", c_void_p), ("T", c_int32),
+                ("n_slots", c_int32), ("flags", c_int32), ("input_ids", c_void_p), ("attention_mask", c_void_p),
+                ("position_ids", c_void_p), ("score_out", c_void_p), ("loss_mask", c_void_p),
+                ("response_mask", c_void_p), ("resp_count", c_void_p), ("err", c_void_p), ("tail", c_void_p),
+                ("n_copies", c_int32), ("host", c_void_p * 4), ("dev", c_void_p * 4), ("bytes", c_int64 * 4)]
 
 _P = ctypes.POINTER
 _SIGS = {
@@ -218,6 +231,13 @@ _SIGS = {
     "rmi_rows_stats": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_next_rows_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_turn_chain": (c_int32, [_P(TurnChain), c_void_p]),
+    "rmi_next_rows_list": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rmi_formulate_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "rmi_formulate_tail": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
+    "rmi_assemble_rows_ex": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_int64, c_int64, c_int64,
+                                       c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rmi_formulate_chain": (c_int32, [_P(FormulateChain), c_void_p]),
 }
 
 _lib = None

@@ -6,13 +6,23 @@
 // against ~290 us of kernels), so the GPU idled between them.  Enqueued from here the launches
 // go back to back and the host's share of a turn is this call plus the Python that reads its
 // readback.
-#include <stdint.h>
+#include "common.hpp"
 
-#include "ragen_amd.h"
+namespace {
 
-#define RMI_HOST_API extern "C" __attribute__((visibility("default")))
+// one event per device, created on first use: the readback is waited on through it, so work
+// enqueued after the copy (the next batch's row list) runs while the host reads the copy
+hipEvent_t copy_event() {
+  static hipEvent_t ev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) ev[dev] = nullptr;
+  return ev[dev];
+}
 
-RMI_HOST_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
+}  // namespace
+
+RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
   if (!chain) return RMI_EINVAL;
   const rmi_turn_chain_t& c = *chain;
   const int64_t B = c.n_envs;
@@ -20,6 +30,11 @@ RMI_HOST_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
       (c.env_kind == RMI_CHAIN_SOKOBAN ? !c.sokoban : c.env_kind == RMI_CHAIN_FROZENLAKE ? !c.frozenlake : true))
     return RMI_EINVAL;
   int rc;
+  // 0. the generation batch's left-cut rows (pad_rows' error bytes), counted into the readback
+  if (c.pad_err) {
+    rc = rmi_row_counts(c.pad_err, 1, c.n_pad, c.pad_count, s);
+    if (rc) return rc;
+  }
   // 1. the generations onto the env rows (the longest one's raw bytes into the readback)
   if (c.resp) {
     rc = rmi_gen_rows_chained(c.resp, c.n_resp, c.R, c.src, B, c.vocab_packed, c.V, c.src ? c.ids : nullptr,
@@ -67,6 +82,36 @@ RMI_HOST_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
                                  c.flags_copy, c.stats, s);
     if (rc) return rc;
   }
-  // 7. the one readback of the turn
-  return rmi_readback(c.host, c.pack, (size_t)c.pack_bytes, s);
+  // 7-8. the one readback of the turn, then the next generation batch's rows (enqueued behind the
+  // copy and run while the host reads it: the host waits for the copy alone)
+  if (!c.next_rows) return rmi_readback(c.host, c.pack, (size_t)c.pack_bytes, s);
+  hipStream_t hs = rmi::as_stream(s);
+  hipEvent_t ev = copy_event();
+  if (!ev || hipMemcpyAsync(c.host, c.pack, (size_t)c.pack_bytes, hipMemcpyDeviceToHost, hs) != hipSuccess ||
+      hipEventRecord(ev, hs) != hipSuccess)
+    return RMI_EDEVICE;
+  rc = rmi_next_rows_list(c.has, c.flags_copy, B, c.next_rows, c.next_src, s);
+  if (rc) return rc;
+  return hipEventSynchronize(ev) == hipSuccess ? RMI_OK : RMI_EDEVICE;
+}
+
+RMI_API int rmi_formulate_chain(const rmi_formulate_chain_t* chain, rmi_stream_t s) {
+  if (!chain) return RMI_EINVAL;
+  const rmi_formulate_chain_t& c = *chain;
+  if (!c.ep || c.ep->B != c.B || !c.norm || !c.tail || c.n_copies < 0 || c.n_copies > 4 ||
+      (c.flags & RMI_MS_TURN_SCORES))
+    return RMI_EINVAL;
+  int rc = rmi_rollout_finalize(c.ep, c.seg, c.G, c.method, c.metrics, nullptr, nullptr, c.norm, s);
+  if (rc) return rc;
+  rc = rmi_assemble_rows_ex(c.tokens, c.row_start, c.row_len, c.B, c.S, c.pad_id, c.special_token, c.reward_token,
+                            c.scores, c.n_scores, c.T, c.n_slots, c.flags, c.norm, c.input_ids, c.attention_mask,
+                            c.position_ids, c.score_out, c.loss_mask, c.response_mask, c.resp_count, c.err, s);
+  if (rc) return rc;
+  rc = rmi_formulate_tail(c.resp_count, c.err, c.B, c.tail, s);
+  if (rc) return rc;
+  hipStream_t hs = rmi::as_stream(s);
+  for (int i = 0; i < c.n_copies; ++i)
+    if (c.bytes[i] > 0 && hipMemcpyAsync(c.host[i], c.dev[i], (size_t)c.bytes[i], hipMemcpyDeviceToHost, hs) != hipSuccess)
+      return RMI_EDEVICE;
+  return hipStreamSynchronize(hs) == hipSuccess ? RMI_OK : RMI_EDEVICE;
 }

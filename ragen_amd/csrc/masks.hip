@@ -46,6 +46,8 @@ struct AsmArgs {
   int64_t* input_ids;
   int64_t* attention_mask;
   int64_t* position_ids;
+  int32_t* resp_count;     // (optional) per row: the response_mask ones written (response_length)
+  const float* last_score;  // (optional, no turn scores) score[:, -1] = last_score[b]: the normalised score
 };
 
 template <bool kAsm>
@@ -83,6 +85,7 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   // an id matching neither special token, for positions past the row end
   const int64_t none = (sp != -1 && rt != -1) ? -1 : ((sp != -2 && rt != -2) ? -2 : -3);
   int carry = 0;
+  int n_resp = 0;  // response_mask ones of the row (kAsm with resp_count)
   for (int64_t s0 = 0; s0 < S; s0 += kSuper * kChunk) {
     // 1. every load of the super-chunk in flight together (clamped addresses, branch-free);
     //    the group at the row end and groups past it are fixed up element-wise afterwards
@@ -183,6 +186,8 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
         }
       }
       // masks[:, :-1]: columns p < S - 1
+      if (kAsm && as.resp_count)
+        n_resp += __builtin_popcount(p0 + kTok <= So ? rm : (p0 >= So ? 0u : rm & ((1u << (8 * (So - p0))) - 1u)));
       if (p0 + kTok <= So) {
         reinterpret_cast<U32u*>(lrow + p0)->x = lm;
         reinterpret_cast<U32u*>(rrow + p0)->x = rm;
@@ -209,15 +214,23 @@ __global__ __launch_bounds__(64) void masks_kernel(const int64_t* __restrict__ i
   // a __threadfence() here would add an L2 write-back per row
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
+  if (kAsm && as.resp_count) {
+    for (int o = 32; o > 0; o >>= 1) n_resp += __shfl_xor(n_resp, o, 64);
+    if (lane == 0) as.resp_count[b] = n_resp;
+  }
   if (So <= 0 || !turn_scores) {  // no per-turn positions: only the overlong bit can be set
     if (lane == 0) err[b] = e_unsup;
   }
   if (So <= 0) return;  // a one-column batch has no score / mask columns
   if (!turn_scores) {
     if (lane == 0) {  // score_tensor[:, -1] = python sum(all_scores[b]), kept by [:, 1:]
-      double sum = 0.0;
-      for (int i = 0; i < n_scores[b]; ++i) sum += scores[(int64_t)i * B + b];
-      srow[So - 1] = (float)sum;
+      if (kAsm && as.last_score) {  // (normalised already: _normalize_score_tensor in place)
+        srow[So - 1] = as.last_score[b];
+      } else {
+        double sum = 0.0;
+        for (int i = 0; i < n_scores[b]; ++i) sum += scores[(int64_t)i * B + b];
+        srow[So - 1] = (float)sum;
+      }
     }
     return;
   }
@@ -319,7 +332,7 @@ RMI_API int rmi_assemble_batch(const int64_t* tokens, const int64_t* row_off, in
   hipLaunchKernelGGL(masks_kernel<true>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), nullptr, B, S,
                      special_token, reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out,
                      loss_mask, response_mask, err, AsmArgs{tokens, row_off, nullptr, pad_id, input_ids,
-                                                            attention_mask, position_ids});
+                                                            attention_mask, position_ids, nullptr, nullptr});
   return launch_status();
 }
 
@@ -338,6 +351,29 @@ RMI_API int rmi_assemble_rows(const int64_t* tokens, const int64_t* row_start, c
   hipLaunchKernelGGL(masks_kernel<true>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), nullptr, B, S,
                      special_token, reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out,
                      loss_mask, response_mask, err, AsmArgs{tokens, row_start, row_len, pad_id, input_ids,
-                                                            attention_mask, position_ids});
+                                                            attention_mask, position_ids, nullptr, nullptr});
+  return launch_status();
+}
+
+RMI_API int rmi_assemble_rows_ex(const int64_t* tokens, const int64_t* row_start, const int32_t* row_len, int64_t B,
+                                 int64_t S, int64_t pad_id, int64_t special_token, int64_t reward_token,
+                                 const double* scores, const int32_t* n_scores, int32_t T, int32_t n_slots,
+                                 int32_t flags, const float* last_score, int64_t* input_ids, int64_t* attention_mask,
+                                 int64_t* position_ids, float* score_out, uint8_t* loss_mask, uint8_t* response_mask,
+                                 int32_t* resp_count, uint8_t* err, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || S < 1 || T < 0 || n_slots < 0 || (last_score && (flags & RMI_MS_TURN_SCORES))) return RMI_EINVAL;
+  if (n_slots > kMaxSlots || B > 0x7FFFFFFF) return RMI_EUNSUP;
+  if (B == 0) return RMI_OK;
+  if (!tokens || !row_start || !row_len || !input_ids || !attention_mask || !position_ids || !n_scores || !err ||
+      (T > 0 && !scores) || (S > 1 && (!score_out || !loss_mask || !response_mask)))
+    return RMI_EINVAL;
+  if (resp_count && S <= 1)  // no mask columns: no response tokens
+    if (hipMemsetAsync(resp_count, 0, (size_t)B * 4, as_stream(stream)) != hipSuccess) return RMI_EDEVICE;
+  hipLaunchKernelGGL(masks_kernel<true>, dim3((unsigned)B), dim3(64), 0, as_stream(stream), nullptr, B, S,
+                     special_token, reward_token, scores, n_scores, (int)T, (int)n_slots, (int)flags, score_out,
+                     loss_mask, response_mask, err,
+                     AsmArgs{tokens, row_start, row_len, pad_id, input_ids, attention_mask, position_ids,
+                             S > 1 ? resp_count : nullptr, last_score});
   return launch_status();
 }

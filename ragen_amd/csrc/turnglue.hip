@@ -189,6 +189,127 @@ __global__ __launch_bounds__(kRedBlock) void prompt_commit_stats_kernel(
   }
 }
 
+// exclusive prefix sum of one int per thread over the kRedBlock-thread workgroup (thread order);
+// *total = the sum.  red: kRedBlock / 64 ints of LDS.
+__device__ __forceinline__ int block_exclusive_scan(int v, int* red, int* total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) red[w] = x;
+  __syncthreads();
+  int before = 0, all = 0;
+#pragma unroll
+  for (int i = 0; i < kRedBlock / 64; ++i) {
+    const int t = red[i];
+    before += i < w ? t : 0;
+    all += t;
+  }
+  __syncthreads();
+  *total = all;
+  return before + x - v;
+}
+
+// The next generation batch's rows on the device: rows[k] = the k-th env (ascending) with has[e]
+// (NULL: every env) and no RMI_FLAG_DONE -- the envs es_manager.step hands back (es_manager.py:
+// 168-169) when the turn's envs came in ascending order -- and src[e] = its k, or -1.  (The turn
+// chain writes them after the commit; the next turn's gen_rows and pad_rows read them instead of
+// an upload of the ids the host derived.)  Eight envs per thread, one block-wide scan per 8192.
+__global__ __launch_bounds__(kRedBlock) void next_rows_list_kernel(const uint8_t* __restrict__ has,
+                                                                   const uint8_t* __restrict__ flags, int64_t B,
+                                                                   int64_t* __restrict__ rows,
+                                                                   int64_t* __restrict__ src) {
+  __shared__ int red[kRedBlock / 64];
+  int64_t base = 0;
+  for (int64_t e0 = 0; e0 < B; e0 += 8 * kRedBlock) {
+    const int64_t e = e0 + 8 * (int64_t)threadIdx.x;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (e + j < B && (has ? has[e + j] != 0 : true) && !(flags[e + j] & RMI_FLAG_DONE)) bits |= 1u << j;
+    int total;
+    int64_t k = base + block_exclusive_scan(__builtin_popcount(bits), red, &total);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (e + j >= B) break;
+      if ((bits >> j) & 1u) {
+        rows[k] = e + j;
+        src[e + j] = k++;
+      } else {
+        src[e + j] = -1;
+      }
+    }
+    base += total;
+  }
+}
+
+// formulate_rollouts' first pass (ctx_manager.py:52-62, :278-306 on the device record): the
+// update rows' longest, whether a row waits for the host, the most turns (zip_longest's length)
+// -> stats i32[3], and the per-env turn counts widened for the assembly -> n_sc i32[B]
+__global__ __launch_bounds__(kRedBlock) void formulate_stats_kernel(const int32_t* __restrict__ len,
+                                                                    const uint8_t* __restrict__ bad,
+                                                                    const uint8_t* __restrict__ n_turns, int64_t B,
+                                                                    int32_t* __restrict__ n_sc,
+                                                                    int32_t* __restrict__ stats) {
+  __shared__ int red[kRedBlock / 64];
+  int m = 0, any = 0, mt = 0;
+  for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
+    m = max(m, len[e]);
+    if (bad) any |= bad[e];
+    const int nt = n_turns[e];
+    n_sc[e] = nt;
+    mt = max(mt, nt);
+  }
+  m = block_max(m, red);
+  any = block_max(any != 0 ? 1 : 0, red);
+  mt = block_max(mt, red);
+  if (threadIdx.x == 0) {
+    stats[0] = m;
+    stats[1] = any;
+    stats[2] = mt;
+  }
+}
+
+// formulate_rollouts' reductions after the assembly: the response tokens of every row summed
+// (response_length's numerator, ctx_manager.py:305: exact in 64 bits), and the assembly's error
+// bytes OR-ed -> out i64[2]
+__global__ __launch_bounds__(kRedBlock) void formulate_tail_kernel(const int32_t* __restrict__ resp_count,
+                                                                   const uint8_t* __restrict__ err, int64_t B,
+                                                                   int64_t* __restrict__ out) {
+  __shared__ long long lred[kRedBlock / 64];
+  __shared__ int red[kRedBlock / 64];
+  long long tot = 0;
+  int bits = 0;
+  for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
+    tot += resp_count[e];
+    bits |= err[e];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    tot += __shfl_xor(tot, o);
+    bits |= __shfl_xor(bits, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    lred[threadIdx.x >> 6] = tot;
+    red[threadIdx.x >> 6] = bits;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long long t = 0;
+    int b = 0;
+#pragma unroll
+    for (int w = 0; w < kRedBlock / 64; ++w) {
+      t += lred[w];
+      b |= red[w];
+    }
+    out[0] = t;
+    out[1] = b;
+  }
+}
+
 __global__ __launch_bounds__(kRedBlock) void rows_stats_kernel(const int32_t* __restrict__ len,
                                                                const int64_t* __restrict__ rows, int64_t n_rows,
                                                                const uint8_t* __restrict__ bad, int64_t B,
@@ -330,6 +451,15 @@ RMI_API int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_
   return launch_status();
 }
 
+RMI_API int rmi_next_rows_list(const uint8_t* has, const uint8_t* flags, int64_t B, int64_t* rows, int64_t* src,
+                               rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || (B > 0 && (!flags || !rows || !src))) return RMI_EINVAL;
+  if (B == 0) return RMI_OK;
+  hipLaunchKernelGGL(next_rows_list_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), has, flags, B, rows, src);
+  return launch_status();
+}
+
 RMI_API int rmi_rows_stats(const int32_t* len, const int64_t* rows, int64_t n_rows, const uint8_t* bad, int64_t B,
                            int32_t* stats, rmi_stream_t stream) {
   using namespace rmi;
@@ -352,5 +482,22 @@ RMI_API int rmi_next_rows_stats(const int32_t* len, const uint8_t* has, const ui
   else
     hipLaunchKernelGGL(next_rows_stats_kernel<false>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, has, flags,
                        bad, B, stats);
+  return launch_status();
+}
+
+RMI_API int rmi_formulate_stats(const int32_t* len, const uint8_t* bad, const uint8_t* n_turns, int64_t B,
+                                int32_t* n_sc, int32_t* stats, rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || !stats || (B > 0 && (!len || !n_turns || !n_sc))) return RMI_EINVAL;
+  hipLaunchKernelGGL(formulate_stats_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), len, bad, n_turns, B,
+                     n_sc, stats);
+  return launch_status();
+}
+
+RMI_API int rmi_formulate_tail(const int32_t* resp_count, const uint8_t* err, int64_t B, int64_t* out,
+                               rmi_stream_t stream) {
+  using namespace rmi;
+  if (B < 0 || !out || (B > 0 && (!resp_count || !err))) return RMI_EINVAL;
+  hipLaunchKernelGGL(formulate_tail_kernel, dim3(1), dim3(kRedBlock), 0, as_stream(stream), resp_count, err, B, out);
   return launch_status();
 }

@@ -62,6 +62,12 @@ class TokenActor:
             self.prompt_shapes.append(tuple(b["input_ids"].shape))
             self.prompts.append((b["input_ids"], b["attention_mask"], b["position_ids"]))
         tok = self.turn_tokens[self.turn]
+        rows = getattr(lm_inputs, "env_rows_device", None)
+        if rows is not None and getattr(lm_inputs, "env_rows_lo", None) == self.env_lo:
+            # the batch's env rows, ascending, on the device already: every env, or a gather
+            resp = tok if rows.numel() == tok.shape[0] else tok.index_select(0, rows)
+            self.turn += 1
+            return DataProto({"responses": resp}, {"env_ids": env_ids}, {})
         if env_ids is not getattr(self, "_ids_seen", None) or tok.shape[0] != self._ids_n:
             local = env_ids - self.env_lo  # (the manager hands the same array each turn)
             self._ids_seen, self._ids_n = env_ids, tok.shape[0]

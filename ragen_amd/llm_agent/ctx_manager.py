@@ -215,9 +215,11 @@ class DeviceEnvInputs:
         self.raw_dev = None  # the same on the device (i32[1], rmi_gen_rows)
         self.raw_next = None  # the other readback buffer's raw slot (rmi_gen_rows_chained zeroes it)
         self.pack = None     # the turn's readback buffer raw_dev lives in
-        # (resp, src host array or None): the generations not yet scattered onto the envs --
-        # the turn's first launch does it (llm_agent/turn_chain.py), or flush() on first use
+        # (resp, src host array or None, src on the device or None): the generations not yet
+        # scattered onto the envs -- the turn's first launch does it (llm_agent/turn_chain.py),
+        # or flush() on first use
         self.pending_gen = None
+        self.pad_counted, self.pad_err = False, None  # the generation batch's error bytes (gen_batch)
         self.vocab = ctx.device_vocab
         self._text = self._text_len = self._err = None
         self._decoded = None
@@ -226,10 +228,10 @@ class DeviceEnvInputs:
         """Launch the deferred rmi_gen_rows (the step-by-step path, or a reader before the turn)."""
         if self.pending_gen is None:
             return
-        resp, src = self.pending_gen
+        resp, src, src_dev = self.pending_gen
         self.pending_gen = None
         n, dev, v = self.ctx.n_envs, resp.device, self.vocab
-        if src is None:
+        if src is None and src_dev is None:
             direct.gen_rows(resp, None, n, v.packed, None, None, self.raw_dev, None, self.raw_next)
             self._ids, self._n_ids, self._has_t = resp, None, None
             return
@@ -237,8 +239,8 @@ class DeviceEnvInputs:
         self._ids = torch.empty(n, R, dtype=torch.int64, device=dev)
         self._n_ids = torch.empty(n, dtype=torch.int32, device=dev)
         self._has_t = torch.empty(n, dtype=torch.uint8, device=dev)
-        direct.gen_rows(resp, ops.h2d(src, dev), n, v.packed, self._ids, self._n_ids, self.raw_dev, self._has_t,
-                        self.raw_next)
+        direct.gen_rows(resp, src_dev if src_dev is not None else ops.h2d(src, dev), n, v.packed, self._ids,
+                        self._n_ids, self.raw_dev, self._has_t, self.raw_next)
 
     @property
     def ids(self):
@@ -382,6 +384,7 @@ class LazyDataProto(DataProto):
         # the ids as int64 (what the device path and a device-resident actor read); the
         # reference's object arrays are made from them on first read of non_tensor_batch
         self.env_ids_i64 = np.asarray(env_ids, np.int64)
+        self.env_rows_device, self.env_rows_lo = None, 0
         self._group_size = 0
         self.non_tensor_batch = _LazyNonTensor(self)
         self.meta_info = {}
@@ -604,6 +607,9 @@ class ContextManager:
                 batch = pr.gen_batch(env_ids)
                 out = LazyDataProto(env_ids, lambda: self._messages_only(list(env_outputs), False))
                 out.set_device_batch(batch, env_ids, self.es_cfg.group_size)
+                # the batch rows' env indices (local to this shard, ascending) on the device, for
+                # an actor that gathers per-env state by them (TokenActor)
+                out.env_rows_device, out.env_rows_lo = pr.last_rows, self.env_lo
                 return out
             return LazyDataProto(env_ids, lambda: self.get_lm_inputs_eager(list(env_outputs)))
         return self.get_lm_inputs_eager(env_outputs, prepare_for_update)
@@ -752,6 +758,9 @@ class ContextManager:
         lo, n = self.env_lo, self.n_envs
         es = getattr(self, "_es", None)
         in_order = es is not None and env_ids is es._ids_in_order  # reset()'s own array: every env, in order
+        # the ids the last turn handed out (ascending): their rows' map is on the device already
+        nr = es.__dict__.get("_next_rows") if es is not None else None
+        src_dev = nr[2] if nr is not None and env_ids is nr[0] and resp.shape[0] == len(env_ids) else None
         # the turn's readback buffer, here so rmi_gen_rows writes the longest generation's raw
         # bytes straight into it (EnvStateManager._device_pass reads it back).  Two buffers,
         # alternating by turn: each turn's gen_rows zeroes the other's raw slot for the next turn
@@ -759,8 +768,11 @@ class ContextManager:
         # before the turn after next reuses it.
         pack, nxt = self.turn_packs()
         raw, raw_next = ops.readback_raw(pack, n), ops.readback_raw(nxt, n)
-        if in_order or (len(env_ids) == n and n and env_ids[0] == lo and np.array_equal(env_ids, lo + np.arange(n))):
-            src = None  # every env in order: the generations are the rows (n_ids = None: R ids each)
+        if in_order or (src_dev is None and len(env_ids) == n and n and env_ids[0] == lo
+                        and np.array_equal(env_ids, lo + np.arange(n))):
+            src, src_dev = None, None  # every env in order: the generations are the rows (n_ids None: R each)
+        elif src_dev is not None:
+            src = None
         else:  # one launch: the rows scattered onto the batch, n_ids, has_t, the raw width
             local = env_ids - lo
             if local.size and (local.min() < 0 or local.max() >= n):
@@ -782,10 +794,11 @@ class ContextManager:
         inp.raw_dev = raw      # i32[1] on the device: the longest row's raw bytes (read back with the turn)
         inp.raw_next = raw_next
         inp.pack = pack
-        # the generation batch's pad_rows counted its flagged rows into this pack (DevicePrompts.gen_batch)
-        inp.pad_counted = self._pad_counted is pack
-        self._pad_counted = None
-        inp.pending_gen = (resp, src)
+        # the generation batch's error bytes, counted into this pack with the turn (gen_batch)
+        pp, self._pad_pending = self._pad_pending, None
+        if pp is not None and pp[0] is pack:
+            inp.pad_counted, inp.pad_err = True, pp[1]
+        inp.pending_gen = (resp, src, src_dev)
         if hint is None or not resp.numel():  # the rows now: the decode is sized from their read-back width
             inp.flush()
             raw_max = int(ops.d2h(raw, self)[0]) if resp.numel() else 0
@@ -798,7 +811,7 @@ class ContextManager:
         inp.raw_max = raw_max  # the decoded rows' length bound (longer only with U+FFFD replacements)
         return inp
 
-    _pad_counted = None  # the readback pack the last generation batch counted its flagged rows into
+    _pad_pending = None  # (the next turn's readback pack, the last generation batch's error bytes)
 
     def turn_packs(self):
         """(this turn's readback buffer, the other one): two, alternating by turn (allocated on
@@ -838,6 +851,9 @@ class ContextManager:
         batch stays on the GPU; messages_list is built on the host only when read."""
         es = self._es
         self._sync_prompts(pr)
+        fc = self._formulate_chain(es, pr)
+        if fc is not None:
+            return fc.run()
         ap = self.config.agent_proxy
         dev = self.device
         # the rows the device could not build are resolved after the readback below, which
@@ -905,6 +921,18 @@ class ContextManager:
         es._formulated = True
         es._formulated_window = pr.window
         return out
+
+    use_formulate_chain = True  # (tests compare the chained form with the step-by-step one)
+
+    def _formulate_chain(self, es, pr):
+        """turn_chain.FormulateChain for this manager's env manager and prompts, or None."""
+        from .turn_chain import FormulateChain
+        if not self.use_formulate_chain or not FormulateChain.applies(self, es, pr):
+            return None
+        fc = self.__dict__.get("_fchain")
+        if fc is None or fc.es is not es or fc.pr is not pr:
+            fc = self._fchain = FormulateChain(self, es, pr)
+        return fc
 
     def _normalize_device(self, score_tensor, es):
         """_normalize_score_tensor (ctx_manager.py:175-226) from the device record: penalties from

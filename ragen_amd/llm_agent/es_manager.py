@@ -316,6 +316,7 @@ class EnvStateManager:
         self._mat_upto = 0
         self.rollout_id += 1
         self._seeds = seeds
+        self._next_rows = self._asc_ids = None  # (a turn's device row list, turn_chain)
         self._states_pending = False
         self._formulated = False
         self._untrimmed = None
@@ -625,12 +626,17 @@ class EnvStateManager:
         # happen, as the reference raises inside its per-env loop
         chain = self._turn_chain()
         res = chain.run(inp, t) if chain is not None else None
+        slot = None
         if res is not None:
-            rec, host = res
+            rec, host, slot = res
             hook, eager = self._prompt_hook, True
         else:
+            if inp.pad_counted:  # the generation batch's left-cut rows, counted into this readback
+                ops.count_nonzero_into(inp.pad_err, ops.readback_pad(inp.pack, n))
             rec, pack, hook, eager = self._device_pass(inp, t, None)
             host = ops.d2h(pack, self)
+        asc = self._ascending(inp.env_ids)
+        self._next_rows = None
         o = (3 * n + 3) & ~3
         tail = host[o:o + 28].view(np.int32)  # max text / obs, the next batch's stats, raw max, pad count
         if getattr(inp, "pad_counted", False) and tail[6]:
@@ -642,6 +648,7 @@ class EnvStateManager:
         dec_h = host[2 * n:3 * n]
         over = ((dec_h & _lib.ERR_UNSUP) != 0) & ((dec_h & _lib.ERR_INDEX) == 0)
         if over.any() and inp.raw_max is None and not (dec_h & _lib.ERR_INDEX).any():
+            slot = None  # (the chain's row list counts the first pass only)
             # the second pass: every row decoded again at the size the lengths ask for (the
             # rows of the first pass decode and parse the same), only the overflowed envs step
             from .ctx_manager import decode_stride
@@ -674,6 +681,9 @@ class EnvStateManager:
         out_ids = inp.env_ids if all_still else inp.env_ids[still]
         if eager:  # the next batch's stats, valid for exactly the env-id array handed out below
             hook.set_next_stats(t, tail[2:5], out_ids)
+        if slot is not None and asc:  # the chain listed these envs (ascending) on the device
+            self._next_rows = (out_ids, slot.next_rows, slot.next_src)
+            self._asc_ids = out_ids
         if err_h.any():
             for tg in self.tags:
                 gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]
@@ -695,6 +705,13 @@ class EnvStateManager:
             from .turn_chain import TurnChain
             ch = self._chain = TurnChain(self, hook.ctx, hook) if TurnChain.applies(self, hook) else None
         return ch
+
+    def _ascending(self, ids) -> bool:
+        """Whether a turn's env ids are strictly ascending (the order the chain lists the next
+        batch's rows in): reset's ids and the ids a chained turn handed out are, by construction."""
+        if ids is self._ids_in_order or ids is self.__dict__.get("_asc_ids"):
+            return True
+        return ids.size < 2 or bool((ids[1:] > ids[:-1]).all())
 
     def _device_pass(self, inp, t, first):
         """The device launches of one pass of turn t over the envs with a generation in ``inp``

@@ -52,6 +52,12 @@ from ..tokenizer import DeviceTokenizer
 from ..torch_ops import direct
 
 SYSTEM = "You're a helpful assistant. "
+
+
+def _storage_uses(t: torch.Tensor) -> int:
+    """References to t's storage (t itself and a temporary count 2: no view of it is alive)."""
+    f = getattr(torch._C, "_storage_Use_Count", None)
+    return f(t.untyped_storage()._cdata) if f is not None else 1 << 30
 _P = ("@@RMI_S@@", "@@RMI_U1@@", "@@RMI_A1@@", "@@RMI_U2@@", "@@RMI_A2@@")
 
 
@@ -250,12 +256,18 @@ class DevicePrompts:
         self.arena = torch.zeros(n, self.cap, dtype=torch.int64, device=self.device)
         self.len = torch.zeros(n, dtype=torch.int32, device=self.device)
         self.len_upd = torch.zeros(n, dtype=torch.int32, device=self.device)
+        # (kept for the life of the builder: the turn chain takes their pointers once)
+        self.arena_p, self.arena_stride = self.arena.data_ptr(), int(self.arena.shape[1])
+        self.len_p, self.len_upd_p = self.len.data_ptr(), self.len_upd.data_ptr()
         self._all_idx = np.arange(n, dtype=np.int64)
         self._all_rows = torch.arange(n, dtype=torch.int64, device=self.device)
         tail = self.dt.encode([self.tpl.gen + self.prefix])[0]
         if tail is None or tail != self._host_ids(self.tpl.gen + self.prefix):
             raise NotImplementedError("the generation prompt does not encode like the host tokenizer")
         self.tail = torch.tensor(tail, dtype=torch.int64, device=self.device)
+        self.tail_p, self.tail_n = self.tail.data_ptr(), int(self.tail.numel())
+        self._batch_bufs = {}  # turn number -> gen_batch's output block and error bytes (_pad_rows)
+        self.last_rows = None  # the device rows of the last generation batch
         self.host_rows_used = 0
         self._pending = None  # (bad rows u8/bool[B] on the device, their host builder), not read back yet
         self._next_stats = None  # (turns done, longest row, any host row, rows) of advance_eager
@@ -736,11 +748,20 @@ class DevicePrompts:
     # ------------------------------------------------------------------- batches
     def gen_batch(self, env_ids: np.ndarray):
         """get_lm_inputs(prepare_for_update=False)'s tensors for these envs (device)."""
-        local = np.asarray(env_ids, np.int64) - self.es.env_lo
-        if len(local) == self.n_envs and np.array_equal(local, self._all_idx):
-            rows = self._all_rows  # every env in order (no host -> device copy)
+        nr = self.es.__dict__.get("_next_rows")
+        asc = True  # rows ascending (a device-resident actor may take them as its gather index)
+        if nr is not None and env_ids is nr[0]:  # the ids the last turn handed out: their rows are on the device
+            rows = nr[1][:len(env_ids)]
+        elif env_ids is self.es._ids_in_order:
+            rows = self._all_rows
         else:
-            rows = ops.h2d(local, self.device)
+            local = np.asarray(env_ids, np.int64) - self.es.env_lo
+            if len(local) == self.n_envs and np.array_equal(local, self._all_idx):
+                rows = self._all_rows  # every env in order (no host -> device copy)
+            else:
+                rows = ops.h2d(local, self.device)
+                asc = False
+        self.last_rows = rows if asc else None
         if self.window and rows.numel():  # every active env has the same turn count
             sel = torch.zeros(self.n_envs, dtype=torch.uint8, device=self.device)
             sel[rows] = 1
@@ -767,12 +788,32 @@ class DevicePrompts:
                 ops.rows_stats(self.len, rows, rows.numel(), None, stats)
                 mx = int(ops.d2h(stats, self)[0])
             S = mx + self.tail.numel()
-        ids, am, pos, err = direct.pad_rows(self.arena, self.len, rows, self.tail, S, int(self.pad_id))
+        ids, am, pos, err = self._pad_rows(rows, S)
         if rows.numel():  # rows longer than S would be left-cut: counted into the next turn's readback
-            pack, _ = self.ctx.turn_packs()
-            ops.count_nonzero_into(err, ops.readback_pad(pack, self.n_envs))
-            self.ctx._pad_counted = pack
+            self.ctx._pad_pending = (self.ctx.turn_packs()[0], err)
         return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
+
+    def _pad_rows(self, rows, S):
+        """rmi_pad_rows into the batch's own tensors (ops.pad_rows without its argument checks:
+        every operand is this builder's).  The outputs are one [3, n, S] block; the block the
+        previous batch of the same shape class used is taken again when nothing outside holds
+        it any more (its storage's use count), else a fresh one is allocated."""
+        n = rows.numel()
+        need = 3 * n * S
+        slot = self.turns_done  # one block per turn number: the last rollout's is free by now
+        buf, err = self._batch_bufs.get(slot, (None, None))
+        if buf is None or buf.numel() < need or _storage_uses(buf) > 2:
+            buf = torch.empty(max(need + need // 4, 1), dtype=torch.int64, device=self.device)  # (headroom)
+        if err is None or _storage_uses(err) > 2:
+            err = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
+        self._batch_bufs[slot] = (buf, err)
+        ids, am, pos = buf[:need].view(3, n, S).unbind(0)
+        err = err[:n]
+        ops.check(_lib.lib().rmi_pad_rows(self.arena_p, self.arena_stride, self.len_p, rows.data_ptr(), n,
+                                          self.tail_p, self.tail_n, int(S), int(self.pad_id), ids.data_ptr(),
+                                          am.data_ptr(), pos.data_ptr(), err.data_ptr(), ops._stream(self.device)),
+                  "rmi_pad_rows")
+        return ids, am, pos, err
 
     def update_rows(self, resolve=True):
         """(tokens, row_start, row_len) of formulate_rollouts' rows, env order.  resolve=False:

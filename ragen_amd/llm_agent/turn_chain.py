@@ -18,6 +18,7 @@ bit for bit (tests/test_gpu_turn_chain.py runs rollouts both ways and compares e
 """
 import ctypes
 
+import numpy as np
 import torch
 
 from .. import _lib, ops
@@ -34,6 +35,8 @@ class _Slot:
         self.left, self.tlen = e(n, dt=torch.int32), e(n, dt=torch.int32)
         self.acts, self.n_act, self.spans = e(n, K, dt=torch.int8), e(n, dt=torch.uint8), e(n, 4, dt=torch.int32)
         self.n_ids, self.has_t = e(n, dt=torch.int32), e(n, dt=torch.uint8)
+        self.n_ids_p, self.has_t_p = self.n_ids.data_ptr(), self.has_t.data_ptr()
+        self.next_rows, self.next_src = e(n, dt=torch.int64), e(n, dt=torch.int64)  # the next batch's rows
         self.ptext_len, self.pmark, self.mark_tok = (e(n, dt=torch.int32) for _ in range(3))
         self.pterr, self.bpe_err, self.bad = (e(n, dt=torch.uint8) for _ in range(3))
         self.text = None      # u8[n, stride], sized by the decode row
@@ -69,9 +72,15 @@ class TurnChain:
         self.ep_struct = self.batch.ep.struct()
         if es._max_act is None:
             es._max_act = torch.full((self.n,), tg.max_actions_per_traj, dtype=torch.int32, device=self.dev)
-        self.vocab = None
         self.parse = None
         self.runs = 0  # turns taken through the chain
+        n = self.n
+        self.pack_bytes = ops.readback_bytes(n)
+        self.stats_off = ((3 * n + 3) & ~3) + 8   # ops.readback_stats
+        self.pad_off = ((3 * n + 3) & ~3) + 24    # ops.readback_pad
+        # the pinned host copy of the readback (numpy view over it)
+        self.host = torch.empty(self.pack_bytes, dtype=torch.uint8, pin_memory=True)
+        self.host_p, self.host_np = self.host.data_ptr(), self.host.numpy()
 
     # ------------------------------------------------------------------ per slot
     def _slot(self, t):
@@ -92,6 +101,8 @@ class TurnChain:
             c.max_actions, c.flags_copy, c.left = es._max_act.data_ptr(), s.flags_copy.data_ptr(), s.left.data_ptr()
             c.pmark, c.ptext_len, c.pterr = s.pmark.data_ptr(), s.ptext_len.data_ptr(), s.pterr.data_ptr()
             c.mark_tok, c.bpe_err, c.bad = s.mark_tok.data_ptr(), s.bpe_err.data_ptr(), s.bad.data_ptr()
+            c.next_rows, c.next_src = s.next_rows.data_ptr(), s.next_src.data_ptr()
+            c.pack_bytes = self.pack_bytes
             b = self.batch
             if self.kind == _lib.CHAIN_SOKOBAN:
                 s.obs = ops.render_buffers(self.n, b.H, b.W, self.dev)
@@ -102,11 +113,6 @@ class TurnChain:
             s.render = _render_struct(*b.glyph_lists(), *s.obs)
             c.obs = ctypes.addressof(s.render)
         return s
-
-    def _vocab(self, v):
-        if self.vocab is None or self.vocab[0] is not v:
-            self.vocab = (v, v.packed.data_ptr(), v.data.data_ptr(), int(v.data.numel()), int(v.packed.shape[0]))
-        return self.vocab
 
     def _parse(self):
         ap = self.es.sys_config.agent_proxy
@@ -119,104 +125,128 @@ class TurnChain:
         return self.parse[2]
 
     # ------------------------------------------------------------------- the turn
-    def run(self, inp, t):
-        """Turn t over the generations of ``inp`` (ctx_manager.DeviceEnvInputs), the next
-        prompt appended: -> (record, host copy of the readback pack) or None when the chain does
-        not apply to this turn (the caller takes the step-by-step path; nothing was launched)."""
-        es, pr, n = self.es, self.pr, self.n
-        if pr.rollout != es.rollout_id or pr.turns_done != t or pr._pending is not None:
-            return None
-        parse = self._parse()
-        if parse is None:
-            return None
-        obs_max = pr._obs_bound({0: None})
-        if obs_max is None:
-            return None
-        s = self._slot(t)
-        c = s.c
-        v, packed, vbytes, nbytes, V = self._vocab(inp.vocab)
-        c.vocab_packed, c.vocab_bytes, c.vocab_n_bytes, c.V = packed, vbytes, nbytes, V
-        sel = self.batch.parse_sel()
-        c.parse, c.sel = parse, ops._ptr(sel)
-        s.sel = sel
-        # the generations: scattered onto the envs by the chain's first launch (deferred by
-        # get_env_inputs), or already on the device
-        pend = inp.pending_gen
-        if pend is not None and inp.raw_next is None:
-            return None  # (a hand-made DeviceEnvInputs: the chained scatter needs the other raw slot)
-        if pend is not None:
-            resp, src = pend
-            R = int(resp.shape[1])
-            c.resp, c.n_resp, c.R = resp.data_ptr(), int(resp.shape[0]), R
-            if src is None:
-                c.src, c.ids, c.n_ids, c.has_t = None, resp.data_ptr(), None, None
-                inp.ids, inp.n_ids, inp.has_t = resp, None, None
-            else:
-                if s.ids is None or s.ids.shape[1] < R:
-                    s.ids = torch.empty(n, R, dtype=torch.int64, device=self.dev)
-                ids = s.ids if s.ids.shape[1] == R else s.ids[:, :R]
-                if not ids.is_contiguous():
-                    s.ids = torch.empty(n, R, dtype=torch.int64, device=self.dev)
-                    ids = s.ids
-                s.src_dev = ops.h2d(src, self.dev)  # (held: the allocator must not hand its block on)
-                c.src = s.src_dev.data_ptr()
-                c.ids, c.n_ids, c.has_t = ids.data_ptr(), s.n_ids.data_ptr(), s.has_t.data_ptr()
-                inp.ids, inp.n_ids, inp.has_t = ids, s.n_ids, s.has_t
-            inp.pending_gen = None
-        else:
-            c.resp, c.src = None, None
-            c.R = int(inp.ids.shape[1])
-            c.ids, c.n_ids, c.has_t = inp.ids.data_ptr(), ops._ptr(inp.n_ids), ops._ptr(inp.has_t)
-        c.raw_max, c.raw_next = inp.raw_dev.data_ptr(), inp.raw_next.data_ptr() if inp.raw_next is not None else None
-        # the decode row
-        stride = (int(inp.stride) + 3) // 4 * 4
-        if s.text is None or s.text.shape[1] != stride:
-            s.text = torch.empty(n, stride, dtype=torch.uint8, device=self.dev)
-            s.prompt = None
-        c.text, c.stride = s.text.data_ptr(), stride
-        # the next prompt's program: turn t's text (DevicePrompts._turn_text), sized from the
-        # host's bounds (the decode row, the widest render row)
-        resp_max = inp.raw_max if inp.raw_max is not None else stride
+    def _static(self, inp):
+        """The per-manager constants of the call (parse configuration, env column, the widest
+        render row, the vocabulary), once; None when the chain cannot run this manager."""
+        st = self.__dict__.get("_st")
+        if st is None or st[0] is not inp.vocab:
+            parse = self._parse()
+            ob = self.batch.obs_bound() if hasattr(self.batch, "obs_bound") else None
+            if parse is None or ob is None:
+                return None
+            v = inp.vocab
+            st = self._st = (v, parse, self.batch.parse_sel(), int(ob), v.packed.data_ptr(), v.data.data_ptr(),
+                             int(v.data.numel()), int(v.packed.shape[0]))
+        return st
+
+    def _bpe(self):
+        """The tokenizer's current rmi_bpe_t (rebuilt when an expansion grew its tables)."""
+        dt = self.pr.dt
+        b = self.__dict__.get("_bpe_c")
+        if b is None or b[0] is not dt.added_bytes:
+            b = self._bpe_c = (dt.added_bytes, dt.bpe_struct())
+        return ctypes.addressof(b[1])
+
+    def _plan(self, s, t, stride, resp_max, obs_max):
+        """Turn t's prompt program against this slot's buffers (DevicePrompts._turn_text), sized
+        from the host's bounds: -> (rmi_prompt_t, pstride, BPE row bound), cached per slot for
+        one (decode row, response bound, render bound) -- the program's constants stay valid
+        as the pool grows (append-only, the old pool tensor is held)."""
+        key = (stride, resp_max, obs_max)
+        if s.prompt is not None and s.prompt[0] == key:
+            return s.prompt
+        pr, n = self.pr, self.n
         pieces, last = pr.turn_pieces(t, t + 2)
         prog, pool, tc = pr._program(pieces)
         bound = pr._text_bound(prog, obs_max, resp_max)
         if bound is None:
             return None
         pstride = pr._stride(bound + 4)
-        key = (stride, pstride, id(pool), id(tc), last)
-        if s.prompt is None or s.prompt[0] != key:
-            if s.ptext is None or s.ptext.shape[1] != pstride:
-                s.ptext = torch.empty(n, pstride, dtype=torch.uint8, device=self.dev)
-            ep = self.batch.ep
-            rows, obs_len = s.obs
-            flat = [len(prog)] + [x for p in prog for x in p] + [pr.n_tags, rows.shape[1], stride,
-                                                                  int(pr.enable_think), pr.K]
-            reward, ne = ep.turn_reward[t], ep.turn_exec[t]
-            P = prompt_struct(flat, pr.sep, (pool, tc, pr.tag, rows, obs_len, s.left, reward, None, s.text, s.tlen,
-                                             s.spans, None, s.has),
-                              (ne, s.flags_copy, pr.int_reward_tags, int(last)))
-            mx = min(int(bound), pstride)
-            # (the tensors behind the struct's pointers held with it: ids in the key stay unique)
-            s.prompt = (key, P, pstride, max((mx + 3) // 4 * 4, 4), (reward, ne, pool, tc))
-        _, P, pstride, bpe_stride, _ = s.prompt
-        c.prompt = ctypes.addressof(P)
-        c.ptext, c.pstride = s.ptext.data_ptr(), pstride
-        bpe = pr.dt.bpe_struct()
-        c.bpe, c.bpe_stride = ctypes.addressof(bpe), bpe_stride
-        c.arena, c.arena_stride = pr.arena.data_ptr(), int(pr.arena.shape[1])
-        c.arena_len, c.len_upd = pr.len.data_ptr(), pr.len_upd.data_ptr()
+        if s.ptext is None or s.ptext.shape[1] != pstride:
+            s.ptext = torch.empty(n, pstride, dtype=torch.uint8, device=self.dev)
+        ep = self.batch.ep
+        rows, obs_len = s.obs
+        flat = [len(prog)] + [x for p in prog for x in p] + [pr.n_tags, rows.shape[1], stride, int(pr.enable_think),
+                                                              pr.K]
+        reward, ne = ep.turn_reward[t], ep.turn_exec[t]
+        P = prompt_struct(flat, pr.sep, (pool, tc, pr.tag, rows, obs_len, s.left, reward, None, s.text, s.tlen,
+                                         s.spans, None, s.has),
+                          (ne, s.flags_copy, pr.int_reward_tags, int(last)))
+        mx = min(int(bound), pstride)
+        # (the tensors behind the struct's pointers are held with it)
+        s.prompt = (key, ctypes.addressof(P), pstride, max((mx + 3) // 4 * 4, 4), last, (P, reward, ne, pool, tc))
+        return s.prompt
+
+    def run(self, inp, t):
+        """Turn t over the generations of ``inp`` (ctx_manager.DeviceEnvInputs), the next
+        prompt appended: -> (record, host copy of the readback pack, slot) or None when the chain
+        does not apply to this turn (the caller takes the step-by-step path; nothing was
+        launched)."""
+        es, pr, n = self.es, self.pr, self.n
+        if pr.rollout != es.rollout_id or pr.turns_done != t or pr._pending is not None:
+            return None
+        st = self._static(inp)
+        if st is None:
+            return None
+        _, parse, sel, ob, packed, vbytes, nbytes, V = st
+        pend = inp.pending_gen
+        if pend is not None and inp.raw_next is None:
+            return None  # (a hand-made DeviceEnvInputs: the chained scatter needs the other raw slot)
+        stride = (int(inp.stride) + 3) // 4 * 4
+        resp_max = inp.raw_max if inp.raw_max is not None else stride
+        s = self._slot(t)
+        if s.text is None or s.text.shape[1] != stride:
+            s.text = torch.empty(n, stride, dtype=torch.uint8, device=self.dev)
+            s.prompt = None
+        plan = self._plan(s, t, stride, resp_max, max(ob, pr._reset_obs_max))
+        if plan is None:
+            return None
+        _, P, pstride, bpe_stride, last, _ = plan
+        c = s.c
+        c.vocab_packed, c.vocab_bytes, c.vocab_n_bytes, c.V = packed, vbytes, nbytes, V
+        c.parse, c.sel = parse, ops._ptr(sel)
+        # the generations: scattered onto the envs by the chain's first launch (deferred by
+        # get_env_inputs), or already on the device
+        if pend is not None:
+            resp, src, src_dev = pend
+            R = int(resp.shape[1])
+            c.resp, c.n_resp, c.R = resp.data_ptr(), int(resp.shape[0]), R
+            if src is None and src_dev is None:
+                c.src, c.ids, c.n_ids, c.has_t = None, resp.data_ptr(), None, None
+                inp.ids, inp.n_ids, inp.has_t = resp, None, None
+            else:
+                if s.ids is None or s.ids.shape[1] != R:
+                    s.ids = torch.empty(n, R, dtype=torch.int64, device=self.dev)
+                if src_dev is None:
+                    src_dev = ops.h2d(src, self.dev)
+                s.src_dev = src_dev  # (held: the allocator must not hand its block on)
+                c.src = src_dev.data_ptr()
+                c.ids, c.n_ids, c.has_t = s.ids.data_ptr(), s.n_ids_p, s.has_t_p
+                inp.ids, inp.n_ids, inp.has_t = s.ids, s.n_ids, s.has_t
+            inp.pending_gen = None
+        else:
+            c.resp, c.src = None, None
+            c.R = int(inp.ids.shape[1])
+            c.ids, c.n_ids, c.has_t = inp.ids.data_ptr(), ops._ptr(inp.n_ids), ops._ptr(inp.has_t)
+        c.raw_max, c.raw_next = inp.raw_dev.data_ptr(), inp.raw_next.data_ptr() if inp.raw_next is not None else None
+        c.text, c.stride = s.text.data_ptr(), stride
+        c.prompt, c.ptext, c.pstride = P, s.ptext.data_ptr(), pstride
+        c.bpe, c.bpe_stride = self._bpe(), bpe_stride
+        c.arena, c.arena_stride = pr.arena_p, pr.arena_stride
+        c.arena_len, c.len_upd = pr.len_p, pr.len_upd_p
         pack = inp.pack
-        c.pack, c.stats = pack.data_ptr(), ops.readback_stats(pack, n).data_ptr()
-        nb = ops.readback_bytes(n)
-        host = es.__dict__.get("_pin_buf")
-        if host is None or host.numel() < nb:
-            host = es._pin_buf = torch.empty(max(nb, 1 << 16), dtype=torch.uint8, pin_memory=True)
-        c.host, c.pack_bytes = host.data_ptr(), nb
+        pk = pack.data_ptr()
+        c.pack, c.stats = pk, pk + self.stats_off
+        # the generation batch's flagged rows counted into this readback (DevicePrompts.gen_batch)
+        pad = inp.pad_err if inp.pad_counted else None
+        c.pad_err, c.n_pad, c.pad_count = (pad.data_ptr(), pad.numel(), pk + self.pad_off) if pad is not None else \
+            (None, 0, None)
+        c.host = self.host_p
         stream = ops._stream(self.dev)
         ops.D2H_COUNT[0] += 1
         ops.check(_lib.lib().rmi_turn_chain(ctypes.byref(c), stream), "rmi_turn_chain")
         self.runs += 1
-        if ops._RING:  # the chain waited on the stream: the upload ring's slices are free
+        if ops._RING:  # the chain waited for its copy: every upload enqueued before it has run
             ops._RING[0].reset_after_sync(stream)
         # the batch's state and the host-side records, as the step-by-step path leaves them
         b = self.batch
@@ -231,4 +261,126 @@ class TurnChain:
         pr.turns_done = t + 1
         pr.eager_turns += 1
         pr._next_stats = None
-        return rec, host[:nb].numpy().copy()
+        return rec, self.host_np.copy(), s
+
+
+class FormulateChain:
+    """ContextManager.formulate_rollouts on the device path as two calls into the library
+    (rmi_formulate_stats + its readback, then rmi_formulate_chain): the batch width, then the
+    finalize (per-env metrics, normalised scores), the assembly (left-padded batch, masks, the
+    normalised score in place, per-row response counts), the reductions and the readback of the
+    metric rows -- where the step-by-step form made ~20 launches and torch glue kernels between
+    two readbacks.  Applies to one env tag, unsharded, without per-turn scores or a context
+    window; ContextManager.formulate_device takes the step-by-step form otherwise (the same
+    outputs: tests/test_gpu_turn_chain.py)."""
+
+    @staticmethod
+    def applies(ctx, es, pr) -> bool:
+        ap = ctx.config.agent_proxy
+        return (pr is not None and not pr.window and len(es.tags) == 1 and not ap.use_turn_scores
+                and not (ctx.process_group is not None and ctx.world_size > 1) and es.n_envs > 0)
+
+    def __init__(self, ctx, es, pr):
+        from ..torch_ops import NORM
+        self.ctx, self.es, self.pr = ctx, es, pr
+        n, dev = es.n_envs, es.device
+        self.n, self.dev = n, dev
+        tg = es.tags[0]
+        self.ep = tg.batch.ep
+        self.ep_struct = self.ep.struct()
+        rn = ctx.config.agent_proxy.reward_normalization
+        if rn.method not in NORM:
+            raise ValueError(f"Invalid normalization method: {rn.method}")
+        if rn.grouping == "state":
+            gs = es.group_size
+            seg = np.arange(0, n + 1, gs, dtype=np.int32)
+        elif rn.grouping in ("batch", "inductive"):  # one tag: one group either way
+            seg = np.array([0, n], np.int32)
+        else:
+            raise ValueError(f"Invalid grouping: {rn.grouping}")
+        self.seg = torch.from_numpy(seg).to(dev)
+        i32, u8 = torch.int32, torch.uint8
+        self.n_sc = torch.empty(n, dtype=i32, device=dev)
+        self.stats = torch.empty(4, dtype=i32, device=dev)
+        self.norm = torch.empty(n, dtype=torch.float32, device=dev)
+        self.resp_count = torch.empty(n, dtype=i32, device=dev)
+        self.err = torch.empty(n, dtype=u8, device=dev)
+        self.block = torch.empty(16 + 32 * n, dtype=u8, device=dev)  # tail i64[2] | metrics f64[n, 4]
+        self.h_stats = torch.empty(16, dtype=u8, pin_memory=True)
+        self.h_block = torch.empty(16 + 32 * n, dtype=u8, pin_memory=True)
+        self.h_info = torch.empty(max(1, self.ep.T * n), dtype=u8, pin_memory=True)
+        self.rmask = None  # the response mask (internal: only its row counts leave)
+        c = self.c = _lib.FormulateChain()
+        c.ep, c.seg, c.G, c.method = ctypes.addressof(self.ep_struct), self.seg.data_ptr(), len(seg) - 1, NORM[rn.method]
+        c.metrics, c.norm = self.block.data_ptr() + 16, self.norm.data_ptr()
+        c.B, c.pad_id = n, int(pr.pad_id)
+        c.scores, c.n_scores, c.T = self.ep.turn_reward.data_ptr(), self.n_sc.data_ptr(), int(self.ep.T)
+        c.resp_count, c.err, c.tail = self.resp_count.data_ptr(), self.err.data_ptr(), self.block.data_ptr()
+        c.n_copies = 2
+        c.host[0], c.dev[0], c.bytes[0] = self.h_block.data_ptr(), self.block.data_ptr(), 16 + 32 * n
+        c.host[1], c.dev[1] = self.h_info.data_ptr(), self.ep.turn_info.data_ptr()
+        self.runs = 0
+
+    def run(self):
+        """-> the formulated DataProto (as ContextManager.formulate_device)."""
+        from .ctx_manager import LazyDataProto, _raise_assemble_errors, get_special_tokens
+        ctx, es, pr, n, dev = self.ctx, self.es, self.pr, self.n, self.dev
+        ap = ctx.config.agent_proxy
+        pend = pr._pending[0] if pr._pending is not None else None
+        tokens, start, row_len = pr.update_rows(resolve=False)
+        L = _lib.lib()
+        stream = ops._stream(dev)
+        # 1. the width, the pending host rows, zip_longest's length: one launch, one readback
+        ops.check(L.rmi_formulate_stats(row_len.data_ptr(), ops._ptr(pend), self.ep.n_turns.data_ptr(), n,
+                                        self.n_sc.data_ptr(), self.stats.data_ptr(), stream), "rmi_formulate_stats")
+        ops.D2H_COUNT[0] += 1
+        ops.check(L.rmi_readback(self.h_stats.data_ptr(), self.stats.data_ptr(), 12, stream), "rmi_readback")
+        S, any_bad, n_slots = (int(x) for x in self.h_stats.numpy()[:12].view(np.int32))
+        if pend is not None:
+            pr._resolve(bool(any_bad))
+            if any_bad:  # host rows were written: the longest row again
+                S = int(row_len.max())
+        S = max(S, 1)
+        if ctx.__dict__.get("_special") is None:  # a tokenizer call: once per manager
+            ctx._special = get_special_tokens(ctx.tokenizer)
+        special_token, reward_token = ctx._special
+        # 2. the batch: one block for the id tensors, the score, the loss mask
+        So = S - 1
+        ids, am, pos = torch.empty(3, n, S, dtype=torch.int64, device=dev).unbind(0)
+        score = torch.empty(n, So, dtype=torch.float32, device=dev)
+        lm = torch.empty(n, So, dtype=torch.bool, device=dev)
+        if self.rmask is None or self.rmask.numel() < n * So:
+            self.rmask = torch.empty(max(1, n * So + n * So // 4), dtype=torch.uint8, device=dev)
+        c = self.c
+        c.tokens, c.row_start, c.row_len = tokens.data_ptr(), start.data_ptr(), row_len.data_ptr()
+        c.S, c.special_token, c.reward_token = S, int(special_token), int(reward_token)
+        c.n_slots = n_slots
+        c.flags = (_lib.MS_RESPONSE_MASK if ctx.config.enable_response_mask else 0) | \
+            (_lib.MS_ROLL if "qwen" in ctx.tokenizer.name_or_path.lower() else 0)
+        c.input_ids, c.attention_mask, c.position_ids = ids.data_ptr(), am.data_ptr(), pos.data_ptr()
+        c.score_out, c.loss_mask, c.response_mask = score.data_ptr(), lm.data_ptr(), self.rmask.data_ptr()
+        T = min(es._turn, es.max_turn)
+        c.bytes[1] = T * n
+        ops.D2H_COUNT[0] += 1
+        ops.check(L.rmi_formulate_chain(ctypes.byref(c), stream), "rmi_formulate_chain")
+        self.runs += 1
+        hb = self.h_block.numpy()
+        total, bits = (int(x) for x in hb[:16].view(np.int64))
+        _raise_assemble_errors(None, S, (bool(bits & _lib.ERR_UNSUP), bool(bits & _lib.ERR_STATE)))
+        # response_length: the f32 mean of the row counts (ctx_manager.py:305; exact while the
+        # total stays below 2^24, where f32 sums of integers are exact in any order)
+        response_length = float(np.float32(total) / np.float32(n))
+        m = hb[16:16 + 32 * n].view(np.float64).reshape(n, 4).copy()
+        info = self.h_info.numpy()[:T * n].reshape(T, n).copy()
+        custom = (info & _lib.INFO_PRESENT).any(0) if T else np.zeros(n, bool)
+        batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
+                 "loss_mask": lm, "rm_scores": score, "original_rm_scores": score}
+        env_ids = es.env_lo + np.arange(n, dtype=np.int64)
+        out = LazyDataProto(env_ids, lambda: ctx._messages_only(es._rollout_states_full(), True))
+        out.set_device_batch(batch, env_ids, es.group_size)
+        metrics = ctx.device_metrics(es, [(es.tags[0].tag, m, custom, info)])
+        metrics["response_length"] = response_length
+        out.meta_info = {"metrics": metrics}
+        es._formulated = True
+        es._formulated_window = pr.window
+        return out

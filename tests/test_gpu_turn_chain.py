@@ -1,6 +1,7 @@
-"""The turn chain (rmi_turn_chain, llm_agent/turn_chain.py: one call per device turn) against
-the step-by-step device turn (EnvStateManager._device_pass: the same kernels launched one by one
-from Python): LLMAgentProxy.rollout both ways on the golden traces' configs (Sokoban 6x6,
+"""The turn chain (rmi_turn_chain, llm_agent/turn_chain.py: one call per device turn) and the
+formulate chain (rmi_formulate_stats + rmi_formulate_chain) against the step-by-step forms
+(EnvStateManager._device_pass, ContextManager.formulate_device: the same kernels launched one by
+one from Python, the normalisation and reductions as torch ops): LLMAgentProxy.rollout both ways on the golden traces' configs (Sokoban 6x6,
 Sokoban 8x8 with 2 boxes, FrozenLake), with the character tokenizer and the Qwen2-pipeline BPE,
 and on the bench's 8192-env workload -- every turn's generation batch, the formulated batch,
 its metrics and the rollout cache identical, the chain taken on every turn, its per-turn buffers
@@ -14,6 +15,7 @@ import torch
 from fake_tok import FakeQwenTok
 from ragen_amd import ops, synthetic
 from ragen_amd.llm_agent import EnvStateManager, LLMAgentProxy, TokenActor
+from ragen_amd.llm_agent.ctx_manager import ContextManager
 from ragen_amd.protocol import DataProto
 from test_gpu_device_prompts import _ids, _responses, _vocab
 from test_gpu_facade import TRACES, _config, _hashseed0_reseed
@@ -28,6 +30,7 @@ def qwen_tok():
 
 def _run(cfg, tok, turn_tokens, device, chain, reps=1, seed=7):
     EnvStateManager.use_turn_chain = chain
+    ContextManager.use_formulate_chain = chain
     try:
         actor = TokenActor(turn_tokens, read_prompts=True)
         proxy = LLMAgentProxy(cfg, actor, tok, device=device)
@@ -40,9 +43,12 @@ def _run(cfg, tok, turn_tokens, device, chain, reps=1, seed=7):
             prompts = [tuple(x.cpu() for x in p) for p in actor.prompts]
             outs.append((out, prompts, proxy.train_es_manager.rollout_cache, dict(out.meta_info)))
         ch = proxy.train_es_manager.__dict__.get("_chain")
+        fc = proxy.train_ctx_manager.__dict__.get("_fchain")
+        assert (fc.runs if fc is not None else 0) == (reps if chain else 0)  # every formulate chained (or none)
         return outs, (ch.runs if ch is not None else 0), proxy
     finally:
         EnvStateManager.use_turn_chain = True
+        ContextManager.use_formulate_chain = True
 
 
 def _same(a, b):

@@ -66,3 +66,12 @@ for lab, t in ST:
 print("\nper label: total us, calls")
 for name, v in sorted(inside.items(), key=lambda x: -x[1]):
     print(f"  {name:28s} {v * 1e6:9.1f} {count[name]:4d}")
+# the rows the chain's kernels saw against the bounds they were sized by
+ch = base.proxy.train_es_manager.__dict__.get("_chain")
+if ch is not None:
+    print("\nslot: decode stride / longest decoded row | prompt row bound (pstride, bpe stride) / longest prompt text")
+    for t, s in sorted(ch.slots.items()):
+        if s.prompt is None:
+            continue
+        print(f"  turn {t}: {s.text.shape[1]} / {int(s.tlen.max())} | {s.prompt[2]}, {s.prompt[3]} / "
+              f"{int(s.ptext_len.max())}  (mean {float(s.ptext_len.float().mean()):.1f})")

@@ -67,6 +67,25 @@ def hooked(self, *a, **kw):
 
 
 setattr(pm.DevicePrompts, name, hooked)
+# the chained turns (round 5: rmi_turn_chain runs the prompt text and the BPE of every turn)
+from ragen_amd.llm_agent import turn_chain as tcm  # noqa: E402
+orig_run = tcm.TurnChain.run
+
+
+def hooked_run(self, inp, t):
+    calls[0] += 1
+    torch.cuda.synchronize()
+    buf = torch.zeros(B * 16, dtype=torch.int64, device=dev)
+    setter(ctypes.c_void_p(buf.data_ptr()))
+    r = orig_run(self, inp, t)
+    if r is not None:
+        bufs.append(buf)
+        if WHICH == "bpe":
+            lens.append(r[2].prompt[3])  # the BPE launch's row bound
+    return r
+
+
+tcm.TurnChain.run = hooked_run
 random.seed(0)
 actor.turn = 0
 proxy.rollout(DataProto(meta_info={}), val=False)
