@@ -188,9 +188,11 @@ int rmi_sokoban_render(const rmi_sokoban_t* env, int32_t B, const uint32_t* glyp
  * state after it (es_manager.py:170 `next_state`; the rows rmi_sokoban_render writes, byte for
  * byte).  fin != NULL: the rollout's last turn fused with its end (rmi_sokoban_step_turn_finalize);
  * init_state / init_player != NULL: a fresh episode's first turn fused with its reset
- * (rmi_sokoban_step_turn_first); not both.  The render is done by each env's own lane from the
- * registers of its turn for 6x6-sized (36-cell) and 64-cell rooms with B > 4096; any other
- * layout runs the turn launch, then rmi_sokoban_render (same outputs).                         */
+ * (rmi_sokoban_step_turn_first); not both.  The render is fused into the turn's launch for
+ * 36-cell rooms (6x6 and other 36-cell shapes) with B > 4096 (one lane per env: the turn waves
+ * leave their envs' state in LDS and the workgroup's helper waves render it); any other layout
+ * (other room sizes, 64-cell rooms included, or B <= 4096) runs the turn launch, then
+ * rmi_sokoban_render (same outputs).                                                          */
 typedef struct {
   uint32_t glyph_bytes[16]; /* as rmi_sokoban_render's glyph table                          */
   uint8_t glyph_len[16];    /* 0..4 (0: '?')                                                */
@@ -433,8 +435,9 @@ int rmi_mask_mul(float* x, const uint8_t* mask, int64_t n, rmi_stream_t stream);
  * decoded with U+FFFD replacing each maximal invalid subpart (String::from_utf8_lossy) and
  * written back as UTF-8: out[b, 0 .. out_len[b]) is exactly decoded_str.encode("utf-8").
  * ids [B,R] (n_ids[b] <= R ids used per row, NULL = R).  The vocabulary is the packed table
- * of rmi_vocab_pack (16-B aligned): one 16-byte gather per id.  err[b]: RMI_ERR_INDEX for an
- * id outside [0, V), RMI_ERR_UNSUP when the text exceeds `stride` bytes (truncated).
+ * of rmi_vocab_pack (16-B aligned): one 16-byte gather per id.  err[b] is written for every
+ * row (not OR-ed into): RMI_ERR_INDEX for an id outside [0, V), RMI_ERR_UNSUP when the text
+ * exceeds `stride` bytes (truncated), else 0.
  * stride % 4 == 0, stride <= 16384.                                                         */
 int rmi_detokenize(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_ids, const uint32_t* vocab_packed,
                    const uint8_t* vocab_bytes, int64_t n_bytes, int64_t V, uint8_t* out, int32_t stride,
@@ -491,8 +494,9 @@ typedef struct {
  * exactly the rmi_turn_t inputs.  Optional: sel[b] picks the id column (Bandit's per-env
  * lookup, bandit/env.py:25-39); spans[b,4] = think [start, end), answer [start, end) in the
  * prefixed text (all -1: no match); action_text [B,K,Lact] / action_len [B,K] = the stripped
- * action strings (Countdown's answers).  err[b] |= RMI_ERR_UNSUP when an action is longer
- * than Lact, RMI_ERR_STATE when text_len[b] is outside [0, stride].
+ * action strings (Countdown's answers).  err[b] (optional) is WRITTEN for every row (not
+ * OR-ed into: a caller's bits already there are overwritten): RMI_ERR_UNSUP when an action is
+ * longer than Lact, RMI_ERR_STATE when text_len[b] is outside [0, stride], else 0.
  * stride % 4 == 0, stride <= 8192.                                                         */
 int rmi_parse_actions(const rmi_parse_cfg_t* cfg, const uint8_t* text, const int32_t* text_len, int64_t B,
                       int32_t stride, const uint8_t* sel, int8_t* actions, uint8_t* n_actions, int32_t* spans,
@@ -557,7 +561,7 @@ typedef struct {
   /* Expansions (n_exp 0: none): added tokens whose id in added_id is -(e + 1) stand for the
    * id sequence exp_ids[exp_off[e] .. exp_off[e+1]) instead of one id.  Their bytes are
    * (0xFF, 0x80 + e): never valid UTF-8, so no text holds them; the prompt programs write them
-   * in place of a constant stretch whose tokenization the host has proven context-free at both
+   * in place of a constant stretch whose tokenization the host has checked context-free at both
    * ends (llm_agent/prompts.py), so the kernel skips that stretch's bytes.  n_exp <= 64.       */
   int32_t n_exp;
   const int32_t* exp_off;   /* [n_exp + 1]                                                   */
@@ -685,6 +689,13 @@ int rmi_turn_inputs(const uint8_t* has_t, const uint8_t* dec_err, int64_t B, uin
 int rmi_turn_readback(const uint8_t* flags, const uint8_t* err, const uint8_t* dec_err, const uint8_t* num_actions,
                       const int32_t* max_actions, const int32_t* text_len, const int32_t* obs_len, int64_t B,
                       uint8_t* flags_copy, int32_t* left, uint8_t* pack, rmi_stream_t stream);
+/* rmi_turn_readback that also counts the generation batch's rows rmi_pad_rows flagged (left-cut:
+ * pad_err u8[n_pad] nonzero) into the pack's int32 at byte ((3B + 3) & ~3) + 24 (pad_err NULL:
+ * exactly rmi_turn_readback).                                                                */
+int rmi_turn_readback_pad(const uint8_t* flags, const uint8_t* err, const uint8_t* dec_err, const uint8_t* num_actions,
+                          const int32_t* max_actions, const int32_t* text_len, const int32_t* obs_len, int64_t B,
+                          uint8_t* flags_copy, int32_t* left, uint8_t* pack, const uint8_t* pad_err, int64_t n_pad,
+                          rmi_stream_t stream);
 int rmi_prompt_commit(const uint8_t* bpe_err, const uint8_t* text_err, const uint8_t* active, const int32_t* mark_tok,
                       int32_t* len_upd, int64_t B, uint8_t* bad, rmi_stream_t stream);
 int rmi_rows_stats(const int32_t* len, const int64_t* rows, int64_t n_rows, const uint8_t* bad, int64_t B,
@@ -722,8 +733,6 @@ int rmi_next_rows_list(const uint8_t* has, const uint8_t* flags, int64_t B, int6
  *           pointer in it is a device pointer unless marked [host].
  *
  * In order (each step exactly the entry point named; see there):
- *   0. (pad_err != NULL) rmi_row_counts(pad_err, 1, n_pad, pad_count): the rows of the generation
- *      batch rmi_pad_rows flagged, counted into the readback
  *   1. rmi_gen_rows_chained(resp, n_resp, R, src, n_envs, vocab_packed, V, ids, n_ids, has_t,
  *      raw_max, raw_next) with ids / n_ids / has_t passed only when src != NULL -- skipped when
  *      resp == NULL (the rows are on the device already)
@@ -734,8 +743,9 @@ int rmi_next_rows_list(const uint8_t* has, const uint8_t* flags, int64_t B, int6
  *   4. the env's turn on {turn, K, actions, n_actions, has, max_actions_per_traj,
  *      format_penalty} with its render into obs: rmi_sokoban_step_turn_render (env_kind 0), or
  *      rmi_frozenlake_step_turn then rmi_frozenlake_render (env_kind 1)
- *   5. rmi_turn_readback(ep->flags, err, dec_err, ep->num_actions, max_actions, text_len,
- *      obs->len, n_envs, flags_copy, left, pack)
+ *   5. rmi_turn_readback_pad(ep->flags, err, dec_err, ep->num_actions, max_actions, text_len,
+ *      obs->len, n_envs, flags_copy, left, pack, pad_err, n_pad): pad_err (NULL: not counted) =
+ *      the generation batch's error bytes
  *   6. (prompt != NULL) rmi_prompt_text(prompt, n_envs, ptext, pstride, ptext_len, pmark, pterr),
  *      rmi_bpe_encode(bpe, ptext, pstride, bpe_stride, ptext_len, n_envs, arena, arena_stride,
  *      arena_len, NULL, pmark, mark_tok, bpe_err) and rmi_prompt_commit_stats(bpe_err, pterr,
@@ -749,10 +759,9 @@ int rmi_next_rows_list(const uint8_t* has, const uint8_t* flags, int64_t B, int6
 enum { RMI_CHAIN_SOKOBAN = 0, RMI_CHAIN_FROZENLAKE = 1 };
 typedef struct {
   int64_t n_envs;
-  /* 0. the generation batch's error bytes (pad_err NULL: not counted) */
+  /* 5. the generation batch's error bytes (pad_err NULL: not counted) */
   const uint8_t* pad_err;
   int64_t n_pad;
-  int32_t* pad_count;               /* i32[1], inside pack                                          */
   /* 1. the generations */
   const int64_t* resp;
   int64_t n_resp, R;

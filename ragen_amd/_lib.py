@@ -100,7 +100,7 @@ class Prompt(ctypes.Structure):
 
 class TurnChain(ctypes.Structure):
     """rmi_turn_chain_t: one device turn of the rollout loop as one call (rmi_turn_chain)."""
-    _fields_ = [("n_envs", c_int64), ("pad_err", c_void_p), ("n_pad", c_int64), ("pad_count", c_void_p),
+    _fields_ = [("n_envs", c_int64), ("pad_err", c_void_p), ("n_pad", c_int64),
                 ("resp", c_void_p), ("n_resp", c_int64), ("R", c_int64), ("src", c_void_p),
                 ("vocab_packed", c_void_p), ("vocab_bytes", c_void_p), ("vocab_n_bytes", c_int64), ("V", c_int64),
                 ("ids", c_void_p), ("n_ids", c_void_p), ("has_t", c_void_p), ("raw_max", c_void_p),
@@ -231,6 +231,8 @@ _SIGS = {
     "rmi_rows_stats": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_next_rows_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_turn_chain": (c_int32, [_P(TurnChain), c_void_p]),
+    "rmi_turn_readback_pad": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                        c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rmi_next_rows_list": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rmi_formulate_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "rmi_formulate_tail": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),

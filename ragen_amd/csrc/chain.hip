@@ -30,11 +30,6 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
       (c.env_kind == RMI_CHAIN_SOKOBAN ? !c.sokoban : c.env_kind == RMI_CHAIN_FROZENLAKE ? !c.frozenlake : true))
     return RMI_EINVAL;
   int rc;
-  // 0. the generation batch's left-cut rows (pad_rows' error bytes), counted into the readback
-  if (c.pad_err) {
-    rc = rmi_row_counts(c.pad_err, 1, c.n_pad, c.pad_count, s);
-    if (rc) return rc;
-  }
   // 1. the generations onto the env rows (the longest one's raw bytes into the readback)
   if (c.resp) {
     rc = rmi_gen_rows_chained(c.resp, c.n_resp, c.R, c.src, B, c.vocab_packed, c.V, c.src ? c.ids : nullptr,
@@ -67,9 +62,9 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
                                  c.obs->stride, c.obs->len, s);
   }
   if (rc) return rc;
-  // 5. the record's flags / actions-left columns and the packed readback
-  rc = rmi_turn_readback(c.ep->flags, c.err, c.dec_err, c.ep->num_actions, c.max_actions, c.text_len, c.obs->len, B,
-                         c.flags_copy, c.left, c.pack, s);
+  // 5. the record's flags / actions-left columns and the packed readback (the batch's left-cut rows counted)
+  rc = rmi_turn_readback_pad(c.ep->flags, c.err, c.dec_err, c.ep->num_actions, c.max_actions, c.text_len,
+                             c.obs->len, B, c.flags_copy, c.left, c.pack, c.pad_err, c.n_pad, s);
   if (rc) return rc;
   // 6. the next prompt's text, its ids appended to the arena, the commit and the next batch's stats
   if (c.prompt) {

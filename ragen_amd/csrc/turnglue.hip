@@ -48,6 +48,19 @@ __device__ __forceinline__ int block_max(int v, int* red) {
   return m;
 }
 
+// block-wide sum of one int per thread -> every thread
+__device__ __forceinline__ int block_sum(int v, int* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int m = 0;
+#pragma unroll
+  for (int w = 0; w < kRedBlock / 64; ++w) m += red[w];
+  __syncthreads();
+  return m;
+}
+
 // V8: eight envs per thread with 8-B / 16-B loads and stores (B % 8 == 0, aligned arrays): at
 // 8192 envs one pass of independent loads instead of eight dependent loop trips
 // (NULL counts as aligned: an absent optional array)
@@ -61,9 +74,12 @@ __global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
     const uint8_t* __restrict__ flags, const uint8_t* __restrict__ err, const uint8_t* __restrict__ dec_err,
     const uint8_t* __restrict__ num_actions, const int32_t* __restrict__ max_actions,
     const int32_t* __restrict__ text_len, const int32_t* __restrict__ obs_len, int64_t B,
-    uint8_t* __restrict__ flags_copy, int32_t* __restrict__ left, uint8_t* __restrict__ pack) {
+    uint8_t* __restrict__ flags_copy, int32_t* __restrict__ left, uint8_t* __restrict__ pack,
+    const uint8_t* __restrict__ pad_err = nullptr, int64_t n_pad = 0) {
   __shared__ int red[kRedBlock / 64];
-  int tmax = 0, omax = 0;
+  int tmax = 0, omax = 0, npad = 0;
+  if (pad_err)  // the generation batch's rows rmi_pad_rows flagged (left-cut): counted
+    for (int64_t i = threadIdx.x; i < n_pad; i += kRedBlock) npad += pad_err[i] != 0;
   if (V8) {
     for (int64_t g = threadIdx.x; g < (B >> 3); g += kRedBlock) {
       const int64_t e = g << 3;
@@ -94,10 +110,12 @@ __global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
   }
   tmax = block_max(tmax, red);
   omax = block_max(omax, red);
+  if (pad_err) npad = block_sum(npad, red);
   if (threadIdx.x == 0) {
     int32_t* tail = reinterpret_cast<int32_t*>(pack + ((3 * B + 3) & ~(int64_t)3));
     tail[0] = tmax;
     tail[1] = omax;
+    if (pad_err) tail[6] = npad;
   }
 }
 
@@ -417,6 +435,30 @@ RMI_API int rmi_turn_readback(const uint8_t* flags, const uint8_t* err, const ui
   else
     hipLaunchKernelGGL(turn_readback_kernel<false>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err,
                        dec_err, num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack);
+  return launch_status();
+}
+
+RMI_API int rmi_turn_readback_pad(const uint8_t* flags, const uint8_t* err, const uint8_t* dec_err,
+                                  const uint8_t* num_actions, const int32_t* max_actions, const int32_t* text_len,
+                                  const int32_t* obs_len, int64_t B, uint8_t* flags_copy, int32_t* left, uint8_t* pack,
+                                  const uint8_t* pad_err, int64_t n_pad, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!pad_err || n_pad < 0)
+    return rmi_turn_readback(flags, err, dec_err, num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack,
+                             stream);
+  if (B < 0) return RMI_EINVAL;
+  if (!pack || (B > 0 && (!flags || !err || !dec_err || !num_actions || !max_actions || !flags_copy || !left)))
+    return RMI_EINVAL;
+  if (reinterpret_cast<uintptr_t>(pack) & 3u) return RMI_EINVAL;
+  const bool v8 = B % 8 == 0 && aligned(flags, 8) && aligned(err, 8) && aligned(dec_err, 8) &&
+                  aligned(num_actions, 8) && aligned(flags_copy, 8) && aligned(pack, 8) && aligned(max_actions, 16) &&
+                  aligned(left, 16) && aligned(text_len, 16) && aligned(obs_len, 16);
+  if (v8)
+    hipLaunchKernelGGL(turn_readback_kernel<true>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err, dec_err,
+                       num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack, pad_err, n_pad);
+  else
+    hipLaunchKernelGGL(turn_readback_kernel<false>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err,
+                       dec_err, num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack, pad_err, n_pad);
   return launch_status();
 }
 

@@ -122,29 +122,37 @@ def _probes():
 
 class ExpansionSplitter:
     """Finds, in a constant stretch X of prompt text, the longest middle X[q1:q2] whose token ids
-    do not depend on the text around X:  ids(L + X + R) == ids(L + X[:q1]) + I + ids(X[q2:] + R)
-    for every probe L, R (``_probes``) -- exactly what the device encoder computes when the
-    middle is replaced by an added-token placeholder standing for I (the placeholder cuts the
-    regex segments there).  Cuts are tried at X's own token boundaries, outermost first.  The
-    tokenizer's own `tokenizers` backend encodes (batched); results are cached per text."""
+    did not depend on the text around X in any of the probe contexts:  ids(L + X + R) ==
+    ids(L + X[:q1]) + I + ids(X[q2:] + R) for every probe L, R -- exactly what the device
+    encoder computes when the middle is replaced by an added-token placeholder standing for I
+    (the placeholder cuts the regex segments there).  This is CHECKED against a finite probe
+    set, not proven for every context: the generic probes (``_probes``: every pre-tokenizer
+    class alone, doubled, tripled and in pairs, runs, and prompt shapes) plus the texts that can
+    actually stand next to a stretch in this run's prompts (``extra``: the env tags' render
+    glyphs and rendered rows, the reward and integer forms, the chat template's added tokens).
+    Cuts are tried at X's own token boundaries, outermost first.  The tokenizer's own
+    `tokenizers` backend encodes (batched); results are cached per text."""
 
     _by_tok = {}
     MIN_BYTES = 12  # a shorter middle is not worth a placeholder (2 bytes)
 
-    def __init__(self, backend):
+    def __init__(self, backend, extra=()):
         self.bt = backend
-        self.probes = _probes()
+        base = _probes()
+        seen = set(base)
+        self.probes = base + [x for x in dict.fromkeys(extra) if x not in seen]
         self.cache = {}
 
     @classmethod
-    def for_tokenizer(cls, tokenizer):
+    def for_tokenizer(cls, tokenizer, extra=()):
         bt = getattr(tokenizer, "backend_tokenizer", None)
         if bt is None or not hasattr(bt, "encode_batch"):
             return None
-        key = id(bt)
+        key = (id(bt), tuple(dict.fromkeys(extra)))
         if key not in cls._by_tok:
-            cls._by_tok[key] = cls(bt)
+            cls._by_tok[key] = cls(bt, extra)
         return cls._by_tok[key]
+
 
     def _ids(self, texts):
         return [e.ids for e in self.bt.encode_batch(list(texts), add_special_tokens=False)]
@@ -198,6 +206,27 @@ class ExpansionSplitter:
         return q1, mid, q2
 
 
+def context_probes(es, tpl, added) -> list:
+    """The texts that can stand next to a constant stretch of this run's prompts, beyond the
+    generic probes: each tag's render glyphs (alone, doubled, as a row), a rendered state of each
+    env batch, the reward forms a turn prints (ints, step sums, successes), integers, and the
+    chat template's pieces and added tokens."""
+    out = []
+    for tg in es.tags:
+        g = getattr(tg.batch.config, "grid_lookup", None) or {}
+        glyphs = [str(v) for v in g.values()]
+        out += glyphs + [x * 2 for x in glyphs] + ["".join(glyphs), "\n".join(glyphs)]
+        if hasattr(tg.batch, "render"):
+            try:
+                out.append(tg.batch.render(0))
+            except Exception:  # (a batch not reset yet renders nothing useful)
+                pass
+    out += ["0", "1", "-1", "0.0", "1.0", "-0.1", "-0.2", "-0.30000000000000004", "0.9", "10.9", "-1.1", "9.9",
+            "0.7999999999999999", "10", "100", "255", "4294967295"]
+    out += [tpl.head, tpl.u_suf, tpl.a_pre, tpl.a_suf, tpl.u_pre, tpl.gen] + list(added)
+    return [x for x in out if x]
+
+
 class DevicePrompts:
     """Per-env prompt ids on the device for one ContextManager / EnvStateManager pair."""
 
@@ -210,7 +239,8 @@ class DevicePrompts:
         self.enable_think = bool(ap.enable_think)
         self.tpl = ChatTemplate(tokenizer)
         self.dt = DeviceTokenizer.from_hf(tokenizer, self.device)
-        self.splitter = ExpansionSplitter.for_tokenizer(tokenizer) if expansions else None
+        self.splitter = ExpansionSplitter.for_tokenizer(
+            tokenizer, context_probes(es, self.tpl, list(self.dt.added))) if expansions else None
         starts = [s for s in self.dt.added]
         for nm in ("a_pre", "u_pre", "gen"):
             piece = getattr(self.tpl, nm)
@@ -333,8 +363,8 @@ class DevicePrompts:
 
     def _with_expansions(self, pieces):
         """Each maximal run of constant pieces (between variable pieces, MARK and IF) whose middle
-        tokenizes the same whatever text surrounds it (ExpansionSplitter: proven against every
-        context probe, per tag) becomes prefix + placeholder + suffix: the placeholder is an
+        tokenized the same in every context it was checked against (ExpansionSplitter: the
+        generic and this run's probes, per tag) becomes prefix + placeholder + suffix: the placeholder is an
         added token of the device tokenizer standing for the middle's ids (rmi_bpe_t
         expansions), so the BPE kernel skips those bytes.  Cached per program."""
         key = tuple(pieces)

@@ -77,7 +77,6 @@ class TurnChain:
         n = self.n
         self.pack_bytes = ops.readback_bytes(n)
         self.stats_off = ((3 * n + 3) & ~3) + 8   # ops.readback_stats
-        self.pad_off = ((3 * n + 3) & ~3) + 24    # ops.readback_pad
         # the pinned host copy of the readback (numpy view over it)
         self.host = torch.empty(self.pack_bytes, dtype=torch.uint8, pin_memory=True)
         self.host_p, self.host_np = self.host.data_ptr(), self.host.numpy()
@@ -239,8 +238,7 @@ class TurnChain:
         c.pack, c.stats = pk, pk + self.stats_off
         # the generation batch's flagged rows counted into this readback (DevicePrompts.gen_batch)
         pad = inp.pad_err if inp.pad_counted else None
-        c.pad_err, c.n_pad, c.pad_count = (pad.data_ptr(), pad.numel(), pk + self.pad_off) if pad is not None else \
-            (None, 0, None)
+        c.pad_err, c.n_pad = (pad.data_ptr(), pad.numel()) if pad is not None else (None, 0)
         c.host = self.host_p
         stream = ops._stream(self.dev)
         ops.D2H_COUNT[0] += 1

@@ -79,3 +79,95 @@ def test_count_nonzero_into_the_readback(device, n):
     ops.count_nonzero_into(x, slot)
     assert int(slot.item()) == int((x != 0).sum())
     assert (pack[:-4].cpu().numpy() == 0xAB).all()  # nothing else of the pack written
+
+
+def _call(name, *args):
+    from ragen_amd import _lib
+    ops.check(getattr(_lib.lib(), name)(*args), name)
+
+
+@pytest.mark.parametrize("B", [8192, 20000, 1000, 1])
+def test_next_rows_list(device, B):
+    """rmi_next_rows_list: the envs with has and not done, ascending, and every env's index in
+    that list (-1: not in it) == numpy."""
+    g = torch.Generator(device="cpu").manual_seed(B)
+    u8, _ = _arrays(B, device, 0, g)
+    has, flags = u8(2), u8(8)
+    for hs in (has, None):
+        rows = torch.full((B,), -7, dtype=torch.int64, device=device)
+        src = torch.full((B,), -7, dtype=torch.int64, device=device)
+        _call("rmi_next_rows_list", ops._ptr(hs), flags.data_ptr(), B, rows.data_ptr(), src.data_ptr(),
+              ops._stream(device))
+        h = np.ones(B, bool) if hs is None else hs.cpu().numpy() != 0
+        nxt = h & ((flags.cpu().numpy() & _lib.FLAG_DONE) == 0)
+        want = np.nonzero(nxt)[0]
+        r = rows.cpu().numpy()
+        assert np.array_equal(r[:len(want)], want) and (r[len(want):] == -7).all()
+        w_src = np.full(B, -1, np.int64)
+        w_src[want] = np.arange(len(want))
+        assert np.array_equal(src.cpu().numpy(), w_src)
+
+
+@pytest.mark.parametrize("B", [8192, 1000, 3])
+def test_formulate_stats_and_tail(device, B):
+    g = torch.Generator(device="cpu").manual_seed(B)
+    u8, i32 = _arrays(B, device, 0, g)
+    length, bad, n_turns = i32(3000), u8(2), u8(6)
+    n_sc = torch.empty(B, dtype=torch.int32, device=device)
+    stats = torch.empty(3, dtype=torch.int32, device=device)
+    for bd in (bad, None):
+        _call("rmi_formulate_stats", length.data_ptr(), ops._ptr(bd), n_turns.data_ptr(), B, n_sc.data_ptr(),
+              stats.data_ptr(), ops._stream(device))
+        want = [int(length.max()), int(bool((bd != 0).any())) if bd is not None else 0, int(n_turns.max())]
+        assert stats.cpu().tolist() == want
+        assert torch.equal(n_sc, n_turns.to(torch.int32))
+    counts, err = i32(1500), u8(5) * (u8(2) != 0).to(torch.uint8)
+    out = torch.empty(2, dtype=torch.int64, device=device)
+    _call("rmi_formulate_tail", counts.data_ptr(), err.data_ptr(), B, out.data_ptr(), ops._stream(device))
+    bits = 0
+    for x in err.cpu().tolist():
+        bits |= x
+    assert out.cpu().tolist() == [int(counts.to(torch.int64).sum()), bits]
+
+
+def test_assemble_rows_ex_counts_and_normalised_score(device):
+    """rmi_assemble_rows_ex == rmi_assemble_rows, plus the response_mask row counts and the
+    last score column replaced by the given scores."""
+    g = torch.Generator(device="cpu").manual_seed(0)
+    B, cap = 700, 900
+    im_start = 151644
+    tokens = torch.randint(100, 1000, (B, cap), generator=g)
+    tokens[torch.rand(B, cap, generator=g) < 0.05] = im_start
+    tokens = tokens.to(device)
+    row_len = torch.randint(1, cap, (B,), generator=g, dtype=torch.int32).to(device)
+    start = (torch.arange(B, dtype=torch.int64) * cap).to(device)
+    S = int(row_len.max())
+    T = 4
+    scores = torch.randn(T, B, generator=g, dtype=torch.float64).to(device)
+    n_sc = torch.randint(0, T + 1, (B,), generator=g, dtype=torch.int32).to(device)
+    last = torch.randn(B, generator=g).to(device)
+    flags = _lib.MS_RESPONSE_MASK | _lib.MS_ROLL
+    outs = []
+    for ex in (False, True):
+        ids, am, pos = (torch.empty(B, S, dtype=torch.int64, device=device) for _ in range(3))
+        sc = torch.empty(B, S - 1, dtype=torch.float32, device=device)
+        lm, rm = (torch.empty(B, S - 1, dtype=torch.uint8, device=device) for _ in range(2))
+        err = torch.empty(B, dtype=torch.uint8, device=device)
+        cnt = torch.empty(B, dtype=torch.int32, device=device)
+        common = (tokens.data_ptr(), start.data_ptr(), row_len.data_ptr(), B, S, 151643, im_start, 151645,
+                  scores.data_ptr(), n_sc.data_ptr(), T, T, flags)
+        tail = (ids.data_ptr(), am.data_ptr(), pos.data_ptr(), sc.data_ptr(), lm.data_ptr(), rm.data_ptr())
+        if ex:
+            _call("rmi_assemble_rows_ex", *common, last.data_ptr(), *tail, cnt.data_ptr(), err.data_ptr(),
+                  ops._stream(device))
+        else:
+            _call("rmi_assemble_rows", *common, *tail, err.data_ptr(), ops._stream(device))
+        outs.append((ids, am, pos, sc, lm, rm, err, cnt))
+    a, b = outs
+    for x, y in zip(a[:7], b[:7]):
+        if x.dtype == torch.float32:
+            assert torch.equal(x[:, :-1], y[:, :-1])
+        else:
+            assert torch.equal(x, y)
+    assert torch.equal(b[3][:, -1], last)
+    assert torch.equal(b[7], a[5].to(torch.int32).sum(1).to(torch.int32))

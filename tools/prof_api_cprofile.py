@@ -41,6 +41,7 @@ random.seed(0)  # one train-seed sequence: each reset takes the rooms the one be
 
 def run():
     actor.turn = 0
+    actor.prompts, actor.prompt_shapes = [], []  # (as bench.api_leg: the last rollout's batches let go)
     torch.cuda.synchronize()
     proxy.rollout(DataProto(meta_info={}), val=False)
     torch.cuda.synchronize()

@@ -34,12 +34,21 @@ for cls, names in ((em.EnvStateManager, ("step", "_step_device", "_turn_chain", 
                    (cm.ContextManager, ("get_lm_inputs", "get_env_inputs", "_device_env_inputs", "_sync_prompts",
                                         "prompts", "formulate_rollouts")),
                    (cm.LazyDataProto, ("__init__", "set_device_batch")),
-                   (pm.DevicePrompts, ("gen_batch", "turn_pieces", "_program", "_text_bound", "_obs_bound")),
+                   (pm.DevicePrompts, ("gen_batch", "_pad_rows", "_resolve", "turn_pieces", "_program", "_text_bound",
+                                       "_obs_bound")),
+                   (cm.ContextManager, ("turn_packs",)),
                    (tc.TurnChain, ("run", "_slot", "_parse")),
                    (tk.DeviceTokenizer, ("bpe_struct",)),
                    (ap.LLMAgentProxy, ("generate_sequences",))):
     for nm in names:
         setattr(cls, nm, stamp(nm, getattr(cls, nm)))
+pm._storage_uses = stamp("_storage_uses", pm._storage_uses)
+import torch  # noqa: E402
+_empty = torch.empty
+torch.empty = stamp("torch.empty", _empty)
+em.LazyEnvOutputs = em.LazyEnvOutputs
+es_cls = em.EnvStateManager
+es_cls._ascending = stamp("_ascending", es_cls._ascending)
 L = _lib.lib()
 L.rmi_turn_chain = stamp("rmi_turn_chain", L.rmi_turn_chain)
 to.direct.pad_rows = stamp("pad_rows", to.direct.pad_rows)
