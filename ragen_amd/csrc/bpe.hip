@@ -356,12 +356,41 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     }
   }
   wave_sync();
+  // the expansion placeholders are the last n_exp added tokens, e at n_plain + e with bytes
+  // (0xFF, 0x80 + e) and id -(e + 1) (tokenizer.py builds them so): phase 2 then matches a 0xFF
+  // candidate by its index byte and compares the others with the plain tokens only
+  const int n_plain = tok.n_added - tok.n_exp;
+  bool exp_tail = added_words && tok.n_exp > 0 && n_plain >= 0;
+  if (exp_tail) {
+    bool ok = true;
+    for (int e = lane; e < tok.n_exp; e += 64) {
+      const int a = n_plain + e;
+      ok &= L.AI[a] == -(e + 1) && L.AO[a + 1] - L.AO[a] == 2 &&
+            (uint32_t)(L.AW[4 * a] & 0xFFFFu) == (0xFFu | ((0x80u + (uint32_t)e) << 8));
+    }
+    exp_tail = !__any(!ok);
+  }
 #ifndef RMI_BPE_FINE
   RMI_STAMP_WAIT(1);
 #endif
-  // ---- 1. UTF-8 decode and classes
+  // ---- 1. UTF-8 decode and classes: a dword (4 text bytes) per lane; an all-ASCII dword (the
+  //         bulk of a prompt) takes four class lookups and one dword store, any other goes
+  //         byte by byte (a lead byte writes its continuation bytes, which their own lanes skip)
   bool bad = false, unsafe = false;
-  for (int p = lane; p < n; p += 64) {
+  for (int w = lane; 4 * w < n; w += 64) {
+    const uint32_t v = reinterpret_cast<const uint32_t*>(L.T)[w];
+    if ((v & 0x80808080u) == 0 && 4 * w + 4 <= n) {
+      uint32_t cw = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t bk = (v >> (8 * k)) & 0xFFu;
+        const uint32_t cat = (uint32_t)L.AC[bk] & (B_L | B_N | B_W | B_NL);
+        cw |= (cat | B_START | (bk == 0x20 ? B_SP : 0u)) << (8 * k);
+      }
+      reinterpret_cast<uint32_t*>(L.C)[w] = cw;
+      continue;
+    }
+    for (int p = 4 * w; p < 4 * w + 4 && p < n; ++p) {
     const uint32_t b0 = L.T[p];
     if ((b0 & 0xC0) == 0x80) continue;  // continuation: written by its lead byte's lane
     if (b0 == 0xFF && tok.n_exp > 0) {  // an expansion placeholder (0xFF, 0x80 + e): an added token
@@ -394,6 +423,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     const uint32_t cat = cls & (B_L | B_N | B_W | B_NL);
     L.C[p] = (uint8_t)(cat | B_START | (b0 == 0x20 ? B_SP : 0u));
     for (int k = 1; k < l; ++k) L.C[p + k] = (uint8_t)cat;
+    }
   }
   const bool row_bad = __any(bad), row_unsafe = __any(unsafe);
   auto fail = [&](uint8_t code) {
@@ -445,19 +475,30 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
             const uint32_t hi = sh ? __builtin_amdgcn_alignbyte(d[2 * q + 2], d[2 * q + 1], sh) : d[2 * q + 1];
             x[q] = ((uint64_t)hi << 32) | lo;
           }
-          for (int a = 0; a < tok.n_added; ++a) {
-            const int len = L.AO[a + 1] - L.AO[a];
-            if (len <= best_len || p + len > n) continue;
-            uint64_t diff = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-              const int r = len - 8 * q;  // bytes of this word inside the token
-              const uint64_t m = r >= 8 ? ~0ull : (r <= 0 ? 0ull : (1ull << (8 * r)) - 1);
-              diff |= (x[q] ^ L.AW[4 * a + q]) & m;
+          if (exp_tail && L.T[p] == 0xFFu) {  // an expansion placeholder: its index byte names it
+            const int e = (int)L.T[p + 1] - 0x80;
+            if (p + 2 <= n && e >= 0 && e < tok.n_exp) {
+              best_len = 2;
+              best_id = L.AI[n_plain + e];
             }
-            if (diff == 0) {
-              best_len = len;
-              best_id = L.AI[a];
+          } else {
+            const int n_cmp = exp_tail ? n_plain : tok.n_added;
+            for (int a = 0; a < n_cmp; ++a) {
+              const int len = L.AO[a + 1] - L.AO[a];
+              // the first word first: most tokens differ there (the rest only for a match)
+              const uint64_t m0 = len >= 8 ? ~0ull : (1ull << (8 * len)) - 1;
+              if (((x[0] ^ L.AW[4 * a]) & m0) != 0 || len <= best_len || p + len > n) continue;
+              uint64_t diff = 0;
+#pragma unroll
+              for (int q = 1; q < 4; ++q) {
+                const int r = len - 8 * q;  // bytes of this word inside the token
+                const uint64_t m = r >= 8 ? ~0ull : (r <= 0 ? 0ull : (1ull << (8 * r)) - 1);
+                diff |= (x[q] ^ L.AW[4 * a + q]) & m;
+              }
+              if (diff == 0) {
+                best_len = len;
+                best_id = L.AI[a];
+              }
             }
           }
         } else {

@@ -92,7 +92,7 @@ proxy.rollout(DataProto(meta_info={}), val=False)
 torch.cuda.synchronize()
 names = {"prompt": ["stage", "pieces up to the reward", "the reward piece", "the rest + stores"],
          "bpe": ["stage", "classes + added + match lengths + chain", "symbols + pair lookups", "merges"]}[WHICH]
-if WHICH == "bpe" and "fine" in os.path.basename(SO):  # bpe.hip built with -DRMI_BPE_FINE
+if WHICH == "bpe" and ("fine" in os.path.basename(SO) or "bpstf" in os.path.basename(SO)):  # -DRMI_BPE_FINE
     names = ["1 classes", "2 added tokens", "3 match lengths", "4 chain"]
 for c, buf in enumerate(bufs):
     s = buf.view(B, 16).cpu().numpy().astype(np.float64)
