@@ -680,6 +680,7 @@ def api_leg(device):
                    "env_steps_per_s_with_reset": steps / (total + tm["reset_s"]),
                    "readbacks": tm.get("readbacks"), "turns": len(shapes),
                    "eager_prompt_turns": pr.eager_turns if pr is not None else None,
+                   "chain_padded_batches": pr.chain_padded if pr is not None else None,  # (4 rollouts)
                    "prompt_batch_shapes": shapes, "update_batch_shape": upd, "device_prompts": pr is not None,
                    "host_prompt_rows": pr.host_rows_used if pr is not None else None,
                    "tokenizer": f"{tok.name_or_path}, vocab {len(tok)}",

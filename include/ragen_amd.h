@@ -573,6 +573,9 @@ typedef struct {
    * every row's critical path.                                                               */
   const uint64_t* added_words;
   const uint8_t* ascii_class;
+  /* exp_off[n_exp] when the caller knows it (0: unknown); <= 512 -> the kernel stages the
+   * expansion tables in LDS with each row (one dependent HBM load per copied id otherwise).   */
+  int32_t n_exp_ids;
 } rmi_bpe_t;
 
 /* Row b: text[b * pitch .. + text_len[b]) (UTF-8; pitch % 4 == 0); `stride` (% 4 == 0,
@@ -689,9 +692,11 @@ int rmi_turn_inputs(const uint8_t* has_t, const uint8_t* dec_err, int64_t B, uin
 int rmi_turn_readback(const uint8_t* flags, const uint8_t* err, const uint8_t* dec_err, const uint8_t* num_actions,
                       const int32_t* max_actions, const int32_t* text_len, const int32_t* obs_len, int64_t B,
                       uint8_t* flags_copy, int32_t* left, uint8_t* pack, rmi_stream_t stream);
-/* rmi_turn_readback that also counts the generation batch's rows rmi_pad_rows flagged (left-cut:
- * pad_err u8[n_pad] nonzero) into the pack's int32 at byte ((3B + 3) & ~3) + 24 (pad_err NULL:
- * exactly rmi_turn_readback).                                                                */
+/* rmi_turn_readback with a longer tail: the pack's int32s after byte ((3B + 3) & ~3) get
+ * [6] = the generation batch's rows rmi_pad_rows flagged (left-cut: pad_err u8[n_pad] nonzero;
+ * pad_err NULL: 0), [7] = the OR of the err bytes | the OR of the dec_err bytes << 8, [8] = the
+ * envs whose flags have RMI_FLAG_DONE ([2..5] are left to other writers): pack holds
+ * ((3B + 3) & ~3) + 36 bytes.                                                                  */
 int rmi_turn_readback_pad(const uint8_t* flags, const uint8_t* err, const uint8_t* dec_err, const uint8_t* num_actions,
                           const int32_t* max_actions, const int32_t* text_len, const int32_t* obs_len, int64_t B,
                           uint8_t* flags_copy, int32_t* left, uint8_t* pack, const uint8_t* pad_err, int64_t n_pad,
@@ -754,6 +759,13 @@ int rmi_next_rows_list(const uint8_t* has, const uint8_t* flags, int64_t B, int6
  *      the copy, then rmi_next_rows_list(has, flags_copy, n_envs, next_rows, next_src) enqueued
  *      behind it, then the copy alone waited on (the list is done in stream order before any
  *      later work on the stream).
+ *   8. (pad_block and next_rows != NULL) with the readback's stats (longest, any_bad, count) =
+ *      pack's int32 [2..4] after the tail offset: when any_bad == 0, count > 0 and
+ *      3 * count * S <= pad_cap for S = longest + pad_tail_n, rmi_pad_rows(arena, arena_stride,
+ *      arena_len, next_rows, count, pad_tail, pad_tail_n, S, pad_id, pad_block,
+ *      pad_block + count * S, pad_block + 2 * count * S, pad_err_next) is enqueued (the
+ *      next get_lm_inputs' batch, ctx_manager.py:265-278, built while the host reads the
+ *      readback) and *pad_S_out = S; else *pad_S_out = 0 and nothing is launched.
  * One env tag (one env batch) per chain.  A step that fails returns its code at once (the
  * steps before it are enqueued; nothing after it is).                                       */
 enum { RMI_CHAIN_SOKOBAN = 0, RMI_CHAIN_FROZENLAKE = 1 };
@@ -817,6 +829,14 @@ typedef struct {
   int64_t* next_rows, *next_src;    /* [n_envs] each                                                */
   void* host;                       /* [host] pinned, >= pack_bytes                                 */
   int64_t pack_bytes;
+  /* 8. the next generation batch padded in the same call (pad_block NULL or next_rows NULL: not) */
+  int64_t* pad_block;               /* i64[pad_cap]: input_ids | attention_mask | position_ids      */
+  int64_t pad_cap;
+  const int64_t* pad_tail;          /* [pad_tail_n] the generation prompt's ids                     */
+  int32_t pad_tail_n;
+  int64_t pad_id;
+  uint8_t* pad_err_next;            /* [n_envs] rmi_pad_rows' err                                   */
+  int64_t* pad_S_out;               /* [host] the batch width padded to, 0: not padded              */
 } rmi_turn_chain_t;
 int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t stream);
 

@@ -117,7 +117,9 @@ class TurnChain(ctypes.Structure):
                 ("arena", c_void_p), ("arena_stride", c_int64), ("arena_len", c_void_p), ("mark_tok", c_void_p),
                 ("bpe_err", c_void_p), ("len_upd", c_void_p), ("bad", c_void_p), ("stats", c_void_p),
                 ("next_rows", c_void_p), ("next_src", c_void_p),
-                ("host", c_void_p), ("pack_bytes", c_int64)]
+                ("host", c_void_p), ("pack_bytes", c_int64),
+                ("pad_block", c_void_p), ("pad_cap", c_int64), ("pad_tail", c_void_p), ("pad_tail_n", c_int32),
+                ("pad_id", c_int64), ("pad_err_next", c_void_p), ("pad_S_out", c_void_p)]
 
 
 CHAIN_SOKOBAN, CHAIN_FROZENLAKE = 0, 1

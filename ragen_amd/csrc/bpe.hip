@@ -47,6 +47,7 @@ constexpr uint32_t kNoRank = 0xFFFFFFFFu;
 #define BST_F(i) do {} while (0)
 #endif
 constexpr uint16_t kEnd = 0xFFFF;
+constexpr int kKHit = 0x8000, kKMerge = 0x4000;  // K[j] flags of phase 5 (counts stay < 0x4000)
 constexpr int kMaxStride = 3072;
 
 // The added tokens and the ASCII code points' classes are staged in the wave's LDS when the
@@ -72,13 +73,22 @@ struct Lds {  // carved from dynamic LDS, n = stride, na = the staged added toke
   uint8_t* T;    // text, n + 16 (zero tail)
   uint8_t* C;    // category bits, n + 128
   uint8_t* AC;   // classes of the code points 0..127 [128]
+  int32_t* EO;   // exp_off [ne + 1] (staged expansions only)
+  int32_t* EI;   // exp_ids [nei]
 };
 __host__ __device__ constexpr int staged_added(int n_added) {
   return n_added > 0 && n_added <= kStageAdded ? n_added : 0;
 }
-__host__ __device__ constexpr size_t bpe_lds(int stride, int na) {
+// the expansion tables are staged with the row when small (their ids are copied to every row
+// that holds one; from HBM that was one dependent load per id)
+constexpr int kStageExpIds = 512;
+__host__ __device__ constexpr bool staged_exp(int n_exp, int n_exp_ids) {
+  return n_exp > 0 && n_exp_ids > 0 && n_exp_ids <= kStageExpIds;
+}
+__host__ __device__ constexpr size_t bpe_lds(int stride, int na, int ne, int nei) {
   return 32 * (size_t)na + 8 * (size_t)stride + 4 * (size_t)(na + 1) + 4 + 4 * (size_t)na + 32 +
-         6 * (size_t)stride + 128 + (size_t)stride + 16 + (size_t)stride + 128 + 128;
+         6 * (size_t)stride + 128 + (size_t)stride + 16 + (size_t)stride + 128 + 128 +
+         (staged_exp(ne, nei) ? 4 * (size_t)(ne + 1) + 4 * (size_t)nei : 0);
 }
 
 __device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a, uint32_t b) {
@@ -104,12 +114,21 @@ __device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a,
 constexpr int kWcWordMax = 16, kWcIdsMax = 9, kWcProbe = 8;
 constexpr uint32_t kWcReady = 1u << 31, kWcClaimed = 1u << 30;
 
-__device__ __forceinline__ void wc_key(const uint8_t* w, int len, uint32_t k[4]) {
+// the word T[a, a + len) as the key's four little-endian words, zero padded: five aligned dword
+// reads of the row and a byte shift (T is 4-aligned with a zero tail; the fifth dword may reach
+// into the next LDS array, whose bytes are masked off)
+__device__ __forceinline__ void wc_key(const uint8_t* T, int a, int len, uint32_t k[4]) {
+  const uint32_t* t4 = reinterpret_cast<const uint32_t*>(T + (a & ~3));
+  uint32_t d[5];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) k[i] = 0;
+  for (int i = 0; i < 5; ++i) d[i] = t4[i];
+  const int sh = a & 3;
 #pragma unroll
-  for (int i = 0; i < kWcWordMax; ++i)  // w has kWcWordMax readable bytes (the row's zero tail)
-    k[i >> 2] |= (i < len ? (uint32_t)w[i] : 0u) << (8 * (i & 3));
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t v = sh ? __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh) : d[i];
+    const int r = len - 4 * i;  // bytes of the word in this key word
+    k[i] = v & (r >= 4 ? ~0u : (r <= 0 ? 0u : (1u << (8 * r)) - 1u));
+  }
 }
 
 __device__ __forceinline__ uint64_t wc_mix(uint64_t h, uint32_t v) {
@@ -131,26 +150,43 @@ __device__ __forceinline__ uint64_t wc_check(const uint32_t k[4], uint32_t meta)
   return wc_mix(h, meta);
 }
 
-// -> the word's id count (ids written to Y[0..)), or 0 on a miss
-__device__ int wc_find(const rmi_bpe_t& t, const uint32_t k[4], int len, int32_t* Y) {
-  uint32_t h = wc_slot(k, len, t.word_cache_mask);
-  for (int i = 0; i < kWcProbe; ++i, h = (h + 1) & t.word_cache_mask) {
-    const uint32_t* s = t.word_cache + 16 * (size_t)h;
-    const uint4 w0 = reinterpret_cast<const uint4*>(s)[0];
-    const uint4 w1 = reinterpret_cast<const uint4*>(s)[1];
-    const uint32_t m = w1.x;
-    if (m == 0) return 0;
-    if (!(m & kWcReady) || (int)(m & 0xFF) != len || w0.x != k[0] || w0.y != k[1] || w0.z != k[2] || w0.w != k[3])
-      continue;
-    const int cnt = (int)((m >> 8) & 0xFF);
-    if (cnt < 1 || cnt > kWcIdsMax) continue;
-    uint64_t c = wc_check(k, m);
-    for (int q = 0; q < cnt; ++q) {
-      const uint32_t id = s[5 + q];
-      c = wc_mix(c, id);
-      Y[q] = (int32_t)id;
-    }
-    if ((((uint64_t)s[15] << 32) | s[14]) == c) return cnt;
+// One probed entry, loaded whole (the ids and the check come with the key: no second round
+// trip for a hit): -> the word's id count (ids written to Y[0..)) if it holds the word, else 0;
+// empty: the slot is empty (the probe sequence ends there).
+__device__ __forceinline__ int wc_take(const uint4 (&w)[4], const uint32_t k[4], int len, int32_t* Y, bool& empty) {
+  const uint32_t m = w[1].x;
+  empty = m == 0;
+  if (!(m & kWcReady) || (int)(m & 0xFF) != len || w[0].x != k[0] || w[0].y != k[1] || w[0].z != k[2] ||
+      w[0].w != k[3])
+    return 0;
+  const int cnt = (int)((m >> 8) & 0xFF);
+  if (cnt < 1 || cnt > kWcIdsMax) return 0;
+  const uint32_t ids[kWcIdsMax] = {w[1].y, w[1].z, w[1].w, w[2].x, w[2].y, w[2].z, w[2].w, w[3].x, w[3].y};
+  uint64_t c = wc_check(k, m);
+#pragma unroll
+  for (int q = 0; q < kWcIdsMax; ++q)
+    if (q < cnt) c = wc_mix(c, ids[q]);
+  if ((((uint64_t)w[3].w << 32) | w[3].z) != c) return 0;
+#pragma unroll
+  for (int q = 0; q < kWcIdsMax; ++q)
+    if (q < cnt) Y[q] = (int32_t)ids[q];
+  return cnt;
+}
+
+__device__ __forceinline__ void wc_load(const rmi_bpe_t& t, uint32_t h, uint4 (&w)[4]) {
+  const uint4* s = reinterpret_cast<const uint4*>(t.word_cache + 16 * (size_t)h);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = s[i];
+}
+
+// the probe sequence from its (i0)th slot h on: -> the word's id count, or 0 on a miss
+__device__ int wc_find_from(const rmi_bpe_t& t, const uint32_t k[4], int len, int32_t* Y, uint32_t h, int i0) {
+  for (int i = i0; i < kWcProbe; ++i, h = (h + 1) & t.word_cache_mask) {
+    uint4 w[4];
+    wc_load(t, h, w);
+    bool empty;
+    const int cnt = wc_take(w, k, len, Y, empty);
+    if (cnt || empty) return cnt;
   }
   return 0;
 }
@@ -300,9 +336,23 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     L.C = p;
     p += S + 128;
     L.AC = p;
+    p += 128;
+    L.EO = reinterpret_cast<int32_t*>(p);  // (4-aligned: every array above is a multiple of 4 bytes)
+    L.EI = L.EO + (tok.n_exp + 1);
   }
+  const bool exp_lds = staged_exp(tok.n_exp, tok.n_exp_ids);
+  const int32_t* EO = exp_lds ? L.EO : tok.exp_off;
+  const int32_t* EI = exp_lds ? L.EI : tok.exp_ids;
   RMI_STAMP_DECL;
   RMI_STAMP(0);
+  // the row's first 1 KB is loaded with its length (one round trip, not two: every row has
+  // min(stride, pitch) readable bytes)
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(text + b * pitch);
+  const int readable = (S < pitch ? S : (int)pitch) / 4;
+  constexpr int kPre = 4;
+  uint32_t pre[kPre];
+#pragma unroll
+  for (int i = 0; i < kPre; ++i) pre[i] = lane + 64 * i < readable ? src[lane + 64 * i] : 0u;
   const int n = text_len[b];
   const int base_len = out_len ? out_len[b] : 0;
   if (n < 0 || n > S) {
@@ -314,12 +364,17 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     return;
   }
   // ---- stage the row (dwords, the bytes past n zeroed), the byte ids, the first-byte bitmap
-  const uint32_t* src = reinterpret_cast<const uint32_t*>(text + b * pitch);
-  for (int w = lane; w < (n + 3) / 4 + 4; w += 64) {
-    uint32_t v = 4 * w < n ? src[w] : 0u;
-    if (4 * w + 4 > n && 4 * w < n) v &= 0xFFFFFFFFu >> (8 * (4 * w + 4 - n));
-    reinterpret_cast<uint32_t*>(L.T)[w] = v;
+  const auto tail_mask = [n](int w, uint32_t v) {
+    if (4 * w >= n) return 0u;
+    return 4 * w + 4 > n ? v & (0xFFFFFFFFu >> (8 * (4 * w + 4 - n))) : v;
+  };
+#pragma unroll
+  for (int i = 0; i < kPre; ++i) {
+    const int w = lane + 64 * i;
+    if (w < (n + 3) / 4 + 4) reinterpret_cast<uint32_t*>(L.T)[w] = tail_mask(w, pre[i]);
   }
+  for (int w = lane + 64 * kPre; w < (n + 3) / 4 + 4; w += 64)
+    reinterpret_cast<uint32_t*>(L.T)[w] = tail_mask(w, 4 * w < n ? src[w] : 0u);
   if (lane < 8) L.AF[lane] = tok.added_first[lane];
   const bool stage_added = na > 0;
   if (stage_added) {
@@ -332,6 +387,10 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     for (int i = lane; i < 4 * na; i += 64) L.AW[i] = tok.added_words[i];
   if (tok.ascii_class && lane < 32)
     reinterpret_cast<uint32_t*>(L.AC)[lane] = reinterpret_cast<const uint32_t*>(tok.ascii_class)[lane];
+  if (exp_lds) {
+    for (int i = lane; i <= tok.n_exp; i += 64) L.EO[i] = tok.exp_off[i];
+    for (int i = lane; i < tok.n_exp_ids; i += 64) L.EI[i] = tok.exp_ids[i];
+  }
   const uint32_t blk0 = tok.ascii_class ? 0u : tok.cp_block[0];  // the block of U+0000..U+00FF
   for (int w = lane; w < (n + 128 + 3) / 4; w += 64) reinterpret_cast<uint32_t*>(L.C)[w] = 0u;  // (C is 4-aligned)
   wave_sync();
@@ -627,36 +686,85 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   BST_N(2);
   BST_F(4);
   // ---- 5. BPE: symbols, pair ranks, merges (one lane per pre-token)
-  // piece bounds: P[j] .. P[j+1] (or n); the symbol chain in M: next symbol start or kEnd
-  // A word found in the word cache gets its ids as the symbols a .. a+cnt-1 and its bytes
-  // marked B_IN (no pair lookups below); K[j]'s top bit tells the merge loop to skip it.
-  for (int j = lane; j < np; j += 64) {
-    const int a = L.P[j], e = j + 1 < np ? L.P[j + 1] : n;
-    L.K[j] = 0;
-    if (L.C[a] & B_ADD) {  // an added token: one symbol, id set in phase 2
-      L.M[a] = kEnd;
-      continue;
+  // piece bounds: P[j] .. P[j+1] (or n); the symbol chain in M: next symbol start or kEnd.
+  // K[j] after this loop: an added token's or a word-cache hit's id count (a hit flagged
+  // kKHit: its ids sit at Y[a ..)), or kKMerge for a word the merge loop below takes.  A row
+  // without such a word (a warm cache) skips the symbol set-up, the pair lookups and the merges.
+  // Two pre-tokens per lane per trip, every global load of both (the word-cache entry at the
+  // first probe, a single byte's id) issued before any is waited on.
+  struct Probe {
+    int j, a, len, kind;  // kind: 0 none, 1 added token, 2 one byte, 3 word cache, 4 merge
+    uint32_t k[4];
+    uint32_t h;
+    uint4 w[4];
+    int32_t bid;
+  };
+  const auto issue = [&](int j, Probe& q) {
+    q.j = j;
+    q.kind = 0;
+    q.a = 0;
+    q.len = 0;
+    if (j < np) {
+      q.a = L.P[j];
+      q.len = (j + 1 < np ? L.P[j + 1] : n) - q.a;
+      q.kind = (L.C[q.a] & B_ADD) ? 1 : q.len == 1 ? 2 : (tok.word_cache && q.len <= kWcWordMax) ? 3 : 4;
     }
-    const int len = e - a;
-    if (tok.word_cache && len >= 2 && len <= kWcWordMax) {
-      uint32_t k[4];
-      wc_key(L.T + a, len, k);
-      const int cnt = wc_find(tok, k, len, L.Y + a);
+    q.bid = tok.byte_id[q.kind == 2 ? L.T[q.a] : 0];
+    if (tok.word_cache) {
+      if (q.kind == 3) wc_key(L.T, q.a, q.len, q.k);
+      q.h = q.kind == 3 ? wc_slot(q.k, q.len, tok.word_cache_mask) : 0u;
+      wc_load(tok, q.h, q.w);
+    }
+  };
+  bool miss = false;
+  const auto finish = [&](Probe& q) {
+    const int j = q.j, a = q.a;
+    if (q.kind == 0) return;
+    if (q.kind == 1) {  // an added token: one symbol (id set in phase 2), or an expansion's ids
+      L.M[a] = kEnd;
+      const int32_t y = L.Y[a];
+      L.K[j] = (uint16_t)(y < 0 ? EO[-y] - EO[-y - 1] : 1);
+      return;
+    }
+    if (q.kind == 2) {  // one byte: its byte id (no pair)
+      L.Y[a] = q.bid;
+      L.K[j] = (uint16_t)(kKHit | 1);
+      return;
+    }
+    if (q.kind == 3) {
+      bool empty;
+      int cnt = wc_take(q.w, q.k, q.len, L.Y + a, empty);
+      if (!cnt && !empty) cnt = wc_find_from(tok, q.k, q.len, L.Y + a, (q.h + 1) & tok.word_cache_mask, 1);
       if (cnt > 0) {
-        for (int q = a; q < e; ++q) {
-          L.M[q] = q + 1 < a + cnt ? (uint16_t)(q + 1) : kEnd;
-          L.C[q] |= B_IN;
-        }
-        L.K[j] = (uint16_t)(0x8000 | cnt);
-        continue;
+        L.K[j] = (uint16_t)(kKHit | cnt);
+        return;
       }
     }
-    for (int q = a; q < e; ++q) {
-      L.Y[q] = tok.byte_id[L.T[q]];  // 1 KB, cache resident (a word-cache miss only)
-      L.M[q] = q + 1 < e ? (uint16_t)(q + 1) : kEnd;
+    miss = true;
+    L.K[j] = kKMerge;
+    for (int p = a; p < a + q.len; ++p) {
+      L.Y[p] = tok.byte_id[L.T[p]];  // 1 KB, cache resident (a word-cache miss only)
+      L.M[p] = p + 1 < a + q.len ? (uint16_t)(p + 1) : kEnd;
     }
+  };
+  for (int j0 = 0; j0 < np; j0 += 128) {
+    Probe q0, q1;
+    issue(j0 + lane, q0);
+    issue(j0 + 64 + lane, q1);
+    finish(q0);
+    finish(q1);
+  }
+  const bool row_merges = __any(miss);
+  if (row_merges) {
+    // the hits' bytes take no pair lookup
+    for (int j = lane; j < np; j += 64)
+      if (L.K[j] & kKHit) {
+        const int a = L.P[j], e = j + 1 < np ? L.P[j + 1] : n;
+        for (int q = a; q < e; ++q) L.C[q] |= B_IN;
+      }
   }
   wave_sync();
+  if (row_merges) {
   // every adjacent pair of the row: the first probe of 8 chunks' pairs in flight together, the
   // rare second probe (a collision) after
   for (int q0 = 0; q0 < n; q0 += 64 * kPairBatch) {
@@ -695,15 +803,9 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   // slower: 78-95 k cycles per wave against 75 k.)
   for (int j = lane; j < np; j += 64) {
     const int a = L.P[j];
-    if (L.K[j] & 0x8000) {  // from the word cache
-      L.K[j] &= 0x7FFF;
-      continue;
-    }
+    if (L.K[j] != kKMerge) continue;  // an added token or a word-cache hit
     int cnt = 1;
-    if ((L.C[a] & B_ADD) && L.Y[a] < 0) {  // an expansion: its precomputed ids
-      const int e = -L.Y[a] - 1;
-      cnt = tok.exp_off[e + 1] - tok.exp_off[e];
-    } else if (!(L.C[a] & B_ADD)) {
+    {
       for (;;) {
         uint32_t best = kNoRank;
         int bq = -1, bprev = -1, prev = -1;
@@ -730,36 +832,45 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
       const int len = (j + 1 < np ? L.P[j + 1] : n) - a;
       if (tok.word_cache && len >= 2 && len <= kWcWordMax && cnt <= kWcIdsMax) {
         uint32_t k[4];
-        wc_key(L.T + a, len, k);
+        wc_key(L.T, a, len, k);
         wc_insert(tok, k, len, L.Y, L.M, a, cnt);
       }
     }
     L.K[j] = (uint16_t)cnt;
   }
   wave_sync();
+  }  // row_merges
   BST_N(4);
   // ---- 6. row offsets (wave scan over pre-tokens), mark, capacity, the ids
   const int mk = mark_byte ? mark_byte[b] : -1;
   int total = 0, before_mark = 0;
   for (int j0 = 0; j0 < np; j0 += 64) {
     const int j = j0 + lane;
-    const int c = j < np ? L.K[j] : 0;
+    const int kj = j < np ? L.K[j] : 0;
+    const int c = kj & ~kKHit;
     const int incl = wave_inclusive_scan(c);
     const bool pre = j < np && (int)L.P[j] < mk;
     const int pre_sum = wave_inclusive_scan(pre ? c : 0);
     before_mark += __builtin_amdgcn_readlane(pre_sum, 63);
-    if (j < np) L.K[j] = (uint16_t)(total + incl - c);  // exclusive offset (< 65536: n <= 3072)
+    // the exclusive offset (< 4096: n <= 3072), the hit flag kept
+    if (j < np) L.K[j] = (uint16_t)((total + incl - c) | (kj & kKHit));
     total += __builtin_amdgcn_readlane(incl, 63);
   }
   if (base_len + total > out_stride) return fail(RMI_ERR_UNSUP);
   wave_sync();
   int64_t* orow = out + b * out_stride + base_len;
   for (int j = lane; j < np; j += 64) {
-    int o = L.K[j];
+    const int kj = L.K[j];
+    int o = kj & ~kKHit;
     const int a = L.P[j];
+    if (kj & kKHit) {  // a word-cache hit: its ids at Y[a ..), the count up to the next offset
+      const int o1 = j + 1 < np ? (L.K[j + 1] & ~kKHit) : total;
+      for (int q = a; o < o1; ++q) orow[o++] = (int64_t)L.Y[q];
+      continue;
+    }
     if ((L.C[a] & B_ADD) && L.Y[a] < 0) {  // an expansion: its ids from the table
       const int e = -L.Y[a] - 1;
-      for (int k = tok.exp_off[e]; k < tok.exp_off[e + 1]; ++k) orow[o++] = (int64_t)tok.exp_ids[k];
+      for (int k = EO[e]; k < EO[e + 1]; ++k) orow[o++] = (int64_t)EI[k];
       continue;
     }
     for (int q = a; q != kEnd; q = L.M[q]) orow[o++] = (int64_t)L.Y[q];
@@ -794,7 +905,8 @@ RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pi
       (tok->n_added > 0 && (!tok->added_bytes || !tok->added_off || !tok->added_id)) || tok->n_exp < 0 ||
       tok->n_exp > 64 || (tok->n_exp > 0 && (!tok->exp_off || !tok->exp_ids)))
     return RMI_EINVAL;
-  const size_t lds = bpe_lds(stride, staged_added(tok->n_added));
+  if (tok->n_exp_ids < 0) return RMI_EINVAL;
+  const size_t lds = bpe_lds(stride, staged_added(tok->n_added), tok->n_exp, tok->n_exp_ids);
   hipLaunchKernelGGL(bpe_encode_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text, pitch,
                      (int)stride,
                      text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);

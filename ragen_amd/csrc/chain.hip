@@ -87,7 +87,23 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
     return RMI_EDEVICE;
   rc = rmi_next_rows_list(c.has, c.flags_copy, B, c.next_rows, c.next_src, s);
   if (rc) return rc;
-  return hipEventSynchronize(ev) == hipSuccess ? RMI_OK : RMI_EDEVICE;
+  if (hipEventSynchronize(ev) != hipSuccess) return RMI_EDEVICE;
+  // 8. the next generation batch, padded while the host reads the readback (its width is in it)
+  if (!c.pad_block) return RMI_OK;
+  if (!c.pad_S_out) return RMI_EINVAL;
+  *c.pad_S_out = 0;
+  const int64_t off = (3 * B + 3) & ~(int64_t)3;
+  if (c.pack_bytes < off + 20) return RMI_EINVAL;
+  const int32_t* tail = reinterpret_cast<const int32_t*>(static_cast<const uint8_t*>(c.host) + off);
+  const int64_t longest = tail[2], any_bad = tail[3], count = tail[4];
+  if (any_bad || count < 1 || count > B || longest < 0) return RMI_OK;
+  const int64_t S = longest + c.pad_tail_n;
+  if (S < 1 || 3 * count * S > c.pad_cap) return RMI_OK;
+  rc = rmi_pad_rows(c.arena, c.arena_stride, c.arena_len, c.next_rows, count, c.pad_tail, c.pad_tail_n, S, c.pad_id,
+                    c.pad_block, c.pad_block + count * S, c.pad_block + 2 * count * S, c.pad_err_next, s);
+  if (rc) return rc;
+  *c.pad_S_out = S;
+  return RMI_OK;
 }
 
 RMI_API int rmi_formulate_chain(const rmi_formulate_chain_t* chain, rmi_stream_t s) {

@@ -61,6 +61,27 @@ __device__ __forceinline__ int block_sum(int v, int* red) {
   return m;
 }
 
+// block-wide OR of one int per thread -> every thread
+__device__ __forceinline__ int block_or(int v, int* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int m = 0;
+#pragma unroll
+  for (int w = 0; w < kRedBlock / 64; ++w) m |= red[w];
+  __syncthreads();
+  return m;
+}
+
+// the OR of the eight bytes of x
+__device__ __forceinline__ uint32_t fold_or(uint64_t x) {
+  x |= x >> 32;
+  x |= x >> 16;
+  x |= x >> 8;
+  return (uint32_t)(x & 0xFFu);
+}
+
 // V8: eight envs per thread with 8-B / 16-B loads and stores (B % 8 == 0, aligned arrays): at
 // 8192 envs one pass of independent loads instead of eight dependent loop trips
 // (NULL counts as aligned: an absent optional array)
@@ -75,9 +96,10 @@ __global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
     const uint8_t* __restrict__ num_actions, const int32_t* __restrict__ max_actions,
     const int32_t* __restrict__ text_len, const int32_t* __restrict__ obs_len, int64_t B,
     uint8_t* __restrict__ flags_copy, int32_t* __restrict__ left, uint8_t* __restrict__ pack,
-    const uint8_t* __restrict__ pad_err = nullptr, int64_t n_pad = 0) {
+    const uint8_t* __restrict__ pad_err = nullptr, int64_t n_pad = 0, bool summary = false) {
   __shared__ int red[kRedBlock / 64];
-  int tmax = 0, omax = 0, npad = 0;
+  int tmax = 0, omax = 0, npad = 0, ndone = 0;
+  uint32_t eor = 0, dor = 0;  // (summary) OR of the step / decode error bytes
   if (pad_err)  // the generation batch's rows rmi_pad_rows flagged (left-cut): counted
     for (int64_t i = threadIdx.x; i < n_pad; i += kRedBlock) npad += pad_err[i] != 0;
   if (V8) {
@@ -95,6 +117,9 @@ __global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
       *reinterpret_cast<uint64_t*>(pack + e) = f;
       *reinterpret_cast<uint64_t*>(pack + B + e) = er;
       *reinterpret_cast<uint64_t*>(pack + 2 * B + e) = de;
+      eor |= fold_or(er);
+      dor |= fold_or(de);
+      ndone += __popcll(f & (0x0101010101010101ull * RMI_FLAG_DONE));
     }
   } else {
     for (int64_t e = threadIdx.x; e < B; e += kRedBlock) {
@@ -104,18 +129,29 @@ __global__ __launch_bounds__(kRedBlock) void turn_readback_kernel(
       pack[e] = f;
       pack[B + e] = err[e];
       pack[2 * B + e] = dec_err[e];
+      eor |= err[e];
+      dor |= dec_err[e];
+      ndone += (f & RMI_FLAG_DONE) != 0;
       if (text_len) tmax = max(tmax, text_len[e]);
       if (obs_len) omax = max(omax, obs_len[e]);
     }
   }
   tmax = block_max(tmax, red);
   omax = block_max(omax, red);
-  if (pad_err) npad = block_sum(npad, red);
+  if (summary) {
+    npad = block_sum(npad, red);
+    ndone = block_sum(ndone, red);
+    eor = (uint32_t)block_or((int)(eor | (dor << 8)), red);
+  }
   if (threadIdx.x == 0) {
     int32_t* tail = reinterpret_cast<int32_t*>(pack + ((3 * B + 3) & ~(int64_t)3));
     tail[0] = tmax;
     tail[1] = omax;
-    if (pad_err) tail[6] = npad;
+    if (summary) {
+      tail[6] = npad;
+      tail[7] = (int32_t)eor;
+      tail[8] = ndone;
+    }
   }
 }
 
@@ -443,10 +479,8 @@ RMI_API int rmi_turn_readback_pad(const uint8_t* flags, const uint8_t* err, cons
                                   const int32_t* obs_len, int64_t B, uint8_t* flags_copy, int32_t* left, uint8_t* pack,
                                   const uint8_t* pad_err, int64_t n_pad, rmi_stream_t stream) {
   using namespace rmi;
-  if (!pad_err || n_pad < 0)
-    return rmi_turn_readback(flags, err, dec_err, num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack,
-                             stream);
-  if (B < 0) return RMI_EINVAL;
+  if (B < 0 || n_pad < 0 || (n_pad > 0 && !pad_err)) return RMI_EINVAL;
+  if (!pad_err) n_pad = 0;
   if (!pack || (B > 0 && (!flags || !err || !dec_err || !num_actions || !max_actions || !flags_copy || !left)))
     return RMI_EINVAL;
   if (reinterpret_cast<uintptr_t>(pack) & 3u) return RMI_EINVAL;
@@ -455,10 +489,10 @@ RMI_API int rmi_turn_readback_pad(const uint8_t* flags, const uint8_t* err, cons
                   aligned(left, 16) && aligned(text_len, 16) && aligned(obs_len, 16);
   if (v8)
     hipLaunchKernelGGL(turn_readback_kernel<true>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err, dec_err,
-                       num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack, pad_err, n_pad);
+                       num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack, pad_err, n_pad, true);
   else
     hipLaunchKernelGGL(turn_readback_kernel<false>, dim3(1), dim3(kRedBlock), 0, as_stream(stream), flags, err,
-                       dec_err, num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack, pad_err, n_pad);
+                       dec_err, num_actions, max_actions, text_len, obs_len, B, flags_copy, left, pack, pad_err, n_pad, true);
   return launch_status();
 }
 

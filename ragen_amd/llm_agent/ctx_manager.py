@@ -317,6 +317,31 @@ class DeviceEnvInputs:
             yield {"env_id": int(e), "llm_raw_response": raw, "llm_response": llm_response, "actions": actions}
 
 
+class _LazyState:
+    """What a LazyDataProto and its non_tensor_batch share: the ids, the group size, the build
+    function and its result.  Neither of the two is referenced from here, so the pair holds no
+    reference cycle: a batch is freed when its last user lets go (a cycle kept the generation
+    batch's tensors alive until the cyclic GC ran, and its block could not be taken again by
+    the next rollout, DevicePrompts.batch_block)."""
+    __slots__ = ("env_ids_i64", "group_size", "build_fn", "built", "batch", "device_batch")
+
+    def __init__(self, env_ids_i64, build_fn):
+        self.env_ids_i64, self.build_fn = env_ids_i64, build_fn
+        self.group_size, self.built, self.batch, self.device_batch = 0, False, None, False
+
+    def build(self, nt: dict):
+        """Run the build once; its non-tensor entries go into ``nt``."""
+        if self.built:
+            return
+        self.built = True
+        real = self.build_fn()
+        if self.device_batch:  # only the host strings are missing
+            dict.__setitem__(nt, "messages_list", real.non_tensor_batch["messages_list"])
+            return
+        self.batch = real.batch
+        dict.update(nt, real.non_tensor_batch)
+
+
 class _LazyNonTensor(dict):
     """non_tensor_batch of a LazyDataProto: 'env_ids' (and, with a device batch, 'group_ids')
     as the reference's object arrays, converted from the owner's int64 ids on first read; any
@@ -324,16 +349,16 @@ class _LazyNonTensor(dict):
 
     _IDS = ("env_ids", "group_ids")
 
-    def __init__(self, owner):
+    def __init__(self, st: _LazyState):
         super().__init__()
-        self._owner = owner
+        self._st = st
 
     def _ids(self, k):
-        o = self._owner
+        st = self._st
         if k == "env_ids":
-            v = o.env_ids_i64.astype(object)
-        elif o._group_size:
-            v = (o.env_ids_i64 // o._group_size).astype(object)
+            v = st.env_ids_i64.astype(object)
+        elif st.group_size:
+            v = (st.env_ids_i64 // st.group_size).astype(object)
         else:
             return None
         dict.__setitem__(self, k, v)
@@ -342,11 +367,11 @@ class _LazyNonTensor(dict):
     def __missing__(self, k):
         if k in self._IDS and self._ids(k) is not None:
             return dict.__getitem__(self, k)
-        self._owner._build()
+        self._st.build(self)
         return dict.__getitem__(self, k)
 
     def __contains__(self, k):
-        return dict.__contains__(self, k) or k == "env_ids" or (k == "group_ids" and bool(self._owner._group_size))
+        return dict.__contains__(self, k) or k == "env_ids" or (k == "group_ids" and bool(self._st.group_size))
 
     def get(self, k, default=None):
         return self[k] if k in self else default
@@ -358,7 +383,7 @@ class _LazyNonTensor(dict):
         for k in self._IDS:
             if not dict.__contains__(self, k):
                 self._ids(k)
-        self._owner._build()
+        self._st.build(self)
         return self
 
     def keys(self):
@@ -380,51 +405,47 @@ class LazyDataProto(DataProto):
     actor that reads only the env ids (a device-resident policy) never pays for them."""
 
     def __init__(self, env_ids, build):
-        self._build_fn, self._built, self._batch = build, False, None
         # the ids as int64 (what the device path and a device-resident actor read); the
         # reference's object arrays are made from them on first read of non_tensor_batch
-        self.env_ids_i64 = np.asarray(env_ids, np.int64)
+        self._st = _LazyState(np.asarray(env_ids, np.int64), build)
         self.env_rows_device, self.env_rows_lo = None, 0
-        self._group_size = 0
-        self.non_tensor_batch = _LazyNonTensor(self)
+        self.non_tensor_batch = _LazyNonTensor(self._st)
         self.meta_info = {}
 
+    @property
+    def env_ids_i64(self):
+        return self._st.env_ids_i64
+
     def __len__(self):
-        return len(self.env_ids_i64)
+        return len(self._st.env_ids_i64)
 
     def set_device_batch(self, batch: dict, env_ids, group_size: int):
         """The device prompt path: the tensors are built already (on the GPU), and so are
         env_ids / group_ids; only messages_list (host strings) is left to the lazy build."""
         from ..protocol import TensorBatch
-        self._batch = TensorBatch(batch)
-        self._device_batch = True
+        st = self._st
+        st.batch = TensorBatch(batch)
+        st.device_batch = True
         ids = np.asarray(env_ids, np.int64)
-        if ids is not self.env_ids_i64 and not np.array_equal(ids, self.env_ids_i64):
-            self.env_ids_i64 = ids
+        if ids is not st.env_ids_i64 and not np.array_equal(ids, st.env_ids_i64):
+            st.env_ids_i64 = ids
             dict.pop(self.non_tensor_batch, "env_ids", None)
-        self._group_size = int(group_size)
+        st.group_size = int(group_size)
         dict.pop(self.non_tensor_batch, "group_ids", None)
 
     @property
     def batch(self):
-        if not getattr(self, "_device_batch", False):
+        if not self._st.device_batch:
             self._build()
-        return self._batch
+        return self._st.batch
 
     @batch.setter
     def batch(self, v):
-        self._batch = v
+        self._st.batch = v
 
     def _build(self):
-        if self._built:
-            return
-        self._built = True
-        real = self._build_fn()
-        if getattr(self, "_device_batch", False):  # only the host strings are missing
-            dict.__setitem__(self.non_tensor_batch, "messages_list", real.non_tensor_batch["messages_list"])
-            return
-        self._batch = real.batch
-        dict.update(self.non_tensor_batch, real.non_tensor_batch)
+        nt = self.non_tensor_batch
+        self._st.build(nt if isinstance(nt, dict) else {})
 
 
 class ContextManager:

@@ -212,6 +212,7 @@ class EnvStateManager:
         self._untrimmed = None
         self.rollout_id = 0
         self._ids_in_order = None  # the env-id array reset() handed out (all envs, in order)
+        self._live_ids = None      # the env-id array the last turn handed out (its envs not done)
         self._turn = 0
         self._all_active = False
         self.reset_render = None
@@ -317,6 +318,7 @@ class EnvStateManager:
         self.rollout_id += 1
         self._seeds = seeds
         self._next_rows = self._asc_ids = None  # (a turn's device row list, turn_chain)
+        self._live_ids = None  # the env ids the last turn handed out (its envs not done)
         self._states_pending = False
         self._formulated = False
         self._untrimmed = None
@@ -329,7 +331,7 @@ class EnvStateManager:
             self._reset_rows = {j: tg.batch.render_rows() for j, tg in enumerate(self.tags)
                                 if type(tg.batch).render is BatchEnv.render}
             self.reset_render = (self.rollout_id, self._reset_rows)
-            self._ids_in_order = self.env_lo + np.arange(self.n_envs, dtype=np.int64)
+            self._ids_in_order = self._live_ids = self.env_lo + np.arange(self.n_envs, dtype=np.int64)
             return LazyEnvOutputs(self, self._ids_in_order)
         self._reset_rows = None
         self._reset_cache()
@@ -638,17 +640,26 @@ class EnvStateManager:
         asc = self._ascending(inp.env_ids)
         self._next_rows = None
         o = (3 * n + 3) & ~3
-        tail = host[o:o + 28].view(np.int32)  # max text / obs, the next batch's stats, raw max, pad count
+        # max text / obs, the next batch's stats, raw max, pad count (and from the chain: the
+        # OR of the error bytes, the done count -- the numpy passes below skipped when clean)
+        tail = host[o:o + 36].view(np.int32)
         if getattr(inp, "pad_counted", False) and tail[6]:
             raise RuntimeError(f"{int(tail[6])} rows of this turn's generation batch were longer than its width "
                                "(rmi_pad_rows RMI_ERR_UNSUP): the actor was given left-cut prompts")
         if inp.raw_max is None:
             inp.ctx.note_raw(int(tail[5]))
-        err_h = host[n:2 * n].copy()
+        summ = ops.readback_summary(tail) if slot is not None else None
+        err_h = host[n:2 * n]
         dec_h = host[2 * n:3 * n]
-        over = ((dec_h & _lib.ERR_UNSUP) != 0) & ((dec_h & _lib.ERR_INDEX) == 0)
-        if over.any() and inp.raw_max is None and not (dec_h & _lib.ERR_INDEX).any():
-            slot = None  # (the chain's row list counts the first pass only)
+        if summ is None or summ[1]:
+            over = ((dec_h & _lib.ERR_UNSUP) != 0) & ((dec_h & _lib.ERR_INDEX) == 0)
+        else:
+            over = None
+        if over is not None and over.any() and inp.raw_max is None and not (dec_h & _lib.ERR_INDEX).any():
+            slot = summ = None  # (the chain's row list and summary count the first pass only)
+            err_h = err_h.copy()
+            if self._prompt_hook is not None:  # (this pass appends more rows: the batch is built later)
+                self._prompt_hook._eager_pad = None
             # the second pass: every row decoded again at the size the lengths ask for (the
             # rows of the first pass decode and parse the same), only the overflowed envs step
             from .ctx_manager import decode_stride
@@ -659,7 +670,7 @@ class EnvStateManager:
             self._turn = t
             rec2, pack2, hook, eager2 = self._device_pass(inp2, t, rec)
             host = ops.d2h(pack2, self)
-            tail = host[o:o + 28].view(np.int32)
+            tail = host[o:o + 36].view(np.int32)
             err_h |= host[n:2 * n]
             dec_h = host[2 * n:3 * n]
             eager = eager and eager2
@@ -668,23 +679,30 @@ class EnvStateManager:
         self._turn_records.append(rec)
         n_in = len(inp.env_ids)
         fl_h = host[:n]
-        if dec_h.any():
+        if (summ[1] if summ is not None else dec_h.any()):
             bad = int(np.nonzero(dec_h)[0][0])
             raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
                              "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP); its env was not stepped")
-        if inp.env_ids is self._ids_in_order:  # every env, in order (no gather)
-            still = (fl_h & _lib.FLAG_DONE) == 0
+        if summ is not None and inp.env_ids is self._live_ids and summ[2] == n - n_in:
+            # the envs outside this turn's ids were all done before it (the ids are the last
+            # turn's survivors): no input became done
+            all_still = True
         else:
-            still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
-        all_still = bool(still.all())
+            if inp.env_ids is self._ids_in_order:  # every env, in order (no gather)
+                still = (fl_h & _lib.FLAG_DONE) == 0
+            else:
+                still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
+            all_still = bool(still.all())
         self._all_active = n_in == self.n_envs and all_still
         out_ids = inp.env_ids if all_still else inp.env_ids[still]
+        self._live_ids = out_ids
         if eager:  # the next batch's stats, valid for exactly the env-id array handed out below
             hook.set_next_stats(t, tail[2:5], out_ids)
         if slot is not None and asc:  # the chain listed these envs (ascending) on the device
             self._next_rows = (out_ids, slot.next_rows, slot.next_src)
             self._asc_ids = out_ids
-        if err_h.any():
+        if (summ[0] if summ is not None else err_h.any()):
+            err_h = err_h.copy()
             for tg in self.tags:
                 gids = [int(g) for g in inp.env_ids if tg.lo <= g < tg.hi]
                 self._raise_errors(tg, err_h[tg.lo - self.env_lo:tg.hi - self.env_lo], [g - tg.lo for g in gids],

@@ -301,6 +301,8 @@ class DevicePrompts:
         self.host_rows_used = 0
         self._pending = None  # (bad rows u8/bool[B] on the device, their host builder), not read back yet
         self._next_stats = None  # (turns done, longest row, any host row, rows) of advance_eager
+        self._eager_pad = None   # ((rollout, turns done), S, rows, block, err) the turn chain padded
+        self.chain_padded = 0    # generation batches taken from the turn chain's pad
         self.eager_turns = 0     # turns appended by advance_eager (the rest at get_lm_inputs)
         self._reset_obs_max = 0
         self.rollout = None
@@ -471,7 +473,7 @@ class DevicePrompts:
         self.rollout = es.rollout_id
         self.turns_done = 0
         self._pending = None  # a previous rollout's unread host rows: its arena is rebuilt now
-        self._next_stats = None
+        self._next_stats = self._eager_pad = None
         # the reset text of the tags without a device render, as host rows (the others' rows stay
         # empty: their observation comes from render_rows)
         host_tags = [tg for tg in es.tags if not hasattr(tg.batch, "render_rows")]
@@ -818,10 +820,39 @@ class DevicePrompts:
                 ops.rows_stats(self.len, rows, rows.numel(), None, stats)
                 mx = int(ops.d2h(stats, self)[0])
             S = mx + self.tail.numel()
-        ids, am, pos, err = self._pad_rows(rows, S)
+        ep, self._eager_pad = self._eager_pad, None
+        if (ep is not None and nr is not None and env_ids is nr[0] and rows.numel() and not any_bad
+                and ep[0] == (self.rollout, self.turns_done) and ep[1] == S and ep[2] == rows.numel()):
+            # padded by the turn chain right after its readback (the same rmi_pad_rows launch
+            # over the same rows, width and block: TurnChain.run)
+            n = rows.numel()
+            ids, am, pos = ep[3][:3 * n * S].view(3, n, S).unbind(0)
+            err = ep[4][:n]
+            self.chain_padded += 1
+        else:
+            ids, am, pos, err = self._pad_rows(rows, S)
         if rows.numel():  # rows longer than S would be left-cut: counted into the next turn's readback
             self.ctx._pad_pending = (self.ctx.turn_packs()[0], err)
         return {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:]}
+
+    def batch_block(self, slot, n=None, S=None):
+        """The output block (i64, >= 3 n S) and error bytes of turn number ``slot``'s generation
+        batch: the block the previous batch of that turn number used when nothing outside holds
+        it any more (its storage's use count), else a fresh one with room for every env's row at
+        1.25 S (the turn chain pads the next rollout's batch of this turn number into it: its row
+        count varies with the envs done, its width a little with the rooms).  n=None: the free
+        block as it is, or None when there is none (TurnChain.run)."""
+        buf, err = self._batch_bufs.get(slot, (None, None))
+        if n is None:
+            if buf is None or _storage_uses(buf) > 2 or _storage_uses(err) > 2:
+                return None
+            return buf, err
+        if buf is None or buf.numel() < 3 * n * S or _storage_uses(buf) > 2:
+            buf = torch.empty(max(3 * max(n, self.n_envs) * (S + S // 4), 1), dtype=torch.int64, device=self.device)
+        if err is None or _storage_uses(err) > 2:
+            err = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
+        self._batch_bufs[slot] = (buf, err)
+        return buf, err
 
     def _pad_rows(self, rows, S):
         """rmi_pad_rows into the batch's own tensors (ops.pad_rows without its argument checks:
@@ -830,13 +861,7 @@ class DevicePrompts:
         it any more (its storage's use count), else a fresh one is allocated."""
         n = rows.numel()
         need = 3 * n * S
-        slot = self.turns_done  # one block per turn number: the last rollout's is free by now
-        buf, err = self._batch_bufs.get(slot, (None, None))
-        if buf is None or buf.numel() < need or _storage_uses(buf) > 2:
-            buf = torch.empty(max(need + need // 4, 1), dtype=torch.int64, device=self.device)  # (headroom)
-        if err is None or _storage_uses(err) > 2:
-            err = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
-        self._batch_bufs[slot] = (buf, err)
+        buf, err = self.batch_block(self.turns_done, n, S)
         ids, am, pos = buf[:need].view(3, n, S).unbind(0)
         err = err[:n]
         ops.check(_lib.lib().rmi_pad_rows(self.arena_p, self.arena_stride, self.len_p, rows.data_ptr(), n,

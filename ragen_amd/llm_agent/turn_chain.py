@@ -80,6 +80,8 @@ class TurnChain:
         # the pinned host copy of the readback (numpy view over it)
         self.host = torch.empty(self.pack_bytes, dtype=torch.uint8, pin_memory=True)
         self.host_p, self.host_np = self.host.data_ptr(), self.host.numpy()
+        self.pad_S = ctypes.c_int64(0)  # the width the chain padded the next batch to (0: not)
+        self.padded = 0  # next batches the chain padded
 
     # ------------------------------------------------------------------ per slot
     def _slot(self, t):
@@ -240,6 +242,15 @@ class TurnChain:
         pad = inp.pad_err if inp.pad_counted else None
         c.pad_err, c.n_pad = (pad.data_ptr(), pad.numel()) if pad is not None else (None, 0)
         c.host = self.host_p
+        # the next generation batch padded by the chain itself, into the block of that turn
+        # number's batch when nothing outside holds it (DevicePrompts.gen_batch takes it)
+        blk = None if last else pr.batch_block(t + 1)
+        if blk is not None:
+            c.pad_block, c.pad_cap, c.pad_err_next = blk[0].data_ptr(), blk[0].numel(), blk[1].data_ptr()
+            c.pad_tail, c.pad_tail_n, c.pad_id = pr.tail_p, pr.tail_n, int(pr.pad_id)
+            c.pad_S_out = ctypes.addressof(self.pad_S)
+        else:
+            c.pad_block = None
         stream = ops._stream(self.dev)
         ops.D2H_COUNT[0] += 1
         ops.check(_lib.lib().rmi_turn_chain(ctypes.byref(c), stream), "rmi_turn_chain")
@@ -259,7 +270,16 @@ class TurnChain:
         pr.turns_done = t + 1
         pr.eager_turns += 1
         pr._next_stats = None
-        return rec, self.host_np.copy(), s
+        host = self.host_np.copy()
+        S = self.pad_S.value if blk is not None else 0
+        if S:
+            o = (3 * n + 3) & ~3
+            count = int(host[o + 16:o + 20].view(np.int32)[0])
+            pr._eager_pad = ((pr.rollout, t + 1), S, count, blk[0], blk[1])
+            self.padded += 1
+        else:
+            pr._eager_pad = None
+        return rec, host, s
 
 
 class FormulateChain:

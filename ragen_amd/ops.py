@@ -1022,8 +1022,9 @@ def readback_bytes(B: int) -> int:
     """The size of the turn's packed readback buffer for B envs: rmi_turn_readback's (flags |
     err | dec_err | max text_len, max obs_len), then room for rmi_next_rows_stats' three ints
     (readback_stats), the longest generation's raw bytes (readback_raw) and the count of the
-    generation batch's rows rmi_pad_rows flagged (readback_pad)."""
-    return ((3 * B + 3) & ~3) + 8 + 20
+    generation batch's rows rmi_pad_rows flagged (readback_pad), and rmi_turn_readback_pad's
+    summary: the OR of the err / dec_err bytes and the count of done envs (readback_summary)."""
+    return ((3 * B + 3) & ~3) + 8 + 28
 
 
 def readback_stats(pack: torch.Tensor, B: int) -> torch.Tensor:
@@ -1042,6 +1043,14 @@ def readback_pad(pack: torch.Tensor, B: int) -> torch.Tensor:
     """The i32[1] of the packed readback buffer that counts the generation batch's flagged rows."""
     o = ((3 * B + 3) & ~3) + 24
     return pack[o:o + 4].view(torch.int32)
+
+
+def readback_summary(tail) -> tuple:
+    """(OR of the step error bytes, OR of the decode error bytes, count of envs with
+    FLAG_DONE) from the host copy of the readback tail (i32 view from its offset on)
+    rmi_turn_readback_pad wrote."""
+    w = int(tail[7])
+    return w & 0xFF, (w >> 8) & 0xFF, int(tail[8])
 
 
 def count_nonzero_into(x: torch.Tensor, out: torch.Tensor):

@@ -166,7 +166,8 @@ class Bpe(ctypes.Structure):
                 ("added_bytes", ctypes.c_void_p), ("added_off", ctypes.c_void_p), ("added_id", ctypes.c_void_p),
                 ("added_first", ctypes.c_uint32 * 8), ("word_cache", ctypes.c_void_p),
                 ("word_cache_mask", ctypes.c_uint32), ("n_exp", ctypes.c_int32), ("exp_off", ctypes.c_void_p),
-                ("exp_ids", ctypes.c_void_p), ("added_words", ctypes.c_void_p), ("ascii_class", ctypes.c_void_p)]
+                ("exp_ids", ctypes.c_void_p), ("added_words", ctypes.c_void_p), ("ascii_class", ctypes.c_void_p),
+                ("n_exp_ids", ctypes.c_int32)]
 
 
 def _backend_json(tokenizer) -> dict:
@@ -383,6 +384,7 @@ class DeviceTokenizer:
                 self.added_bytes.data_ptr(), self.added_off.data_ptr(), self.added_id.data_ptr())
         if self.exp:
             s.n_exp, s.exp_off, s.exp_ids = len(self.exp), self.exp_off.data_ptr(), self.exp_ids.data_ptr()
+            s.n_exp_ids = int(self.exp_ids.numel())
         for i, w in enumerate(self.added_first):
             s.added_first[i] = w
         if self.word_cache is not None:

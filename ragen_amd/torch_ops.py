@@ -833,6 +833,7 @@ def _bpe_struct_build(cp_block, cp_class, byte_id, merges, added_bytes, added_of
         ops._dt(exp_off, torch.int32, "exp_off")
         ops._dt(exp_ids, torch.int32, "exp_ids")
         s.n_exp, s.exp_off, s.exp_ids = exp_off.numel() - 1, exp_off.data_ptr(), exp_ids.data_ptr()
+        s.n_exp_ids = int(exp_ids.numel())
     if added_words is not None:  # staging tables (rmi_bpe_t.added_words / ascii_class)
         ops._dev(added_words)
         ops._dt(added_words, torch.int64, "added_words")

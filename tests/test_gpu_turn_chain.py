@@ -82,6 +82,8 @@ def test_turn_chain_equals_step_by_step(device, name, which, qwen_tok, monkeypat
     assert runs == n_turns, (runs, n_turns)  # every turn of both rollouts went through the chain
     for a, b in zip(chained, plain):
         _same(a, b)
+    # generation batches of the second rollout were padded by the chain (the first's blocks free)
+    assert proxy.train_es_manager._chain.padded > 0
     assert proxy.train_ctx_manager.prompts().host_rows_used == 0
 
 
@@ -102,8 +104,11 @@ def test_turn_chain_bench_workload(device):
         for i, x in enumerate(enc):
             a[i, :len(x)] = x
         tokens.append(torch.from_numpy(a).to(device))
-    chained, runs, _ = _run(cfg, tok, tokens, device, True, reps=2, seed=0)
+    chained, runs, proxy = _run(cfg, tok, tokens, device, True, reps=2, seed=0)
     plain, _, _ = _run(cfg, tok, tokens, device, False, reps=2, seed=0)
     assert runs == sum(len(o[1]) for o in chained)
+    # the second rollout's batches after the first turn were padded by the chain and taken
+    assert proxy.train_es_manager._chain.padded == len(chained[1][1]) - 1
+    assert proxy.train_ctx_manager.prompts().chain_padded == len(chained[1][1]) - 1
     for a, b in zip(chained, plain):
         _same(a, b)

@@ -78,7 +78,39 @@ def test_count_nonzero_into_the_readback(device, n):
     slot = ops.readback_pad(pack, 64)
     ops.count_nonzero_into(x, slot)
     assert int(slot.item()) == int((x != 0).sum())
-    assert (pack[:-4].cpu().numpy() == 0xAB).all()  # nothing else of the pack written
+    h = pack.cpu().numpy()
+    o = ((3 * 64 + 3) & ~3) + 24
+    assert (np.delete(h, np.arange(o, o + 4)) == 0xAB).all()  # nothing else of the pack written
+
+
+@pytest.mark.parametrize("B,off", [(8192, 0), (1000, 0), (4096, 1), (24, 3)])
+def test_turn_readback_pad_summary(device, B, off):
+    """rmi_turn_readback_pad: rmi_turn_readback's pack plus the tail's pad count, the OR of the
+    step / decode error bytes and the done count (the chain's host reads these instead of
+    scanning the arrays)."""
+    g = torch.Generator(device="cpu").manual_seed(7 * B + off)
+    u8, i32 = _arrays(B, device, off, g)
+    flags, num_actions = u8(8), u8(20)
+    max_actions, text_len, obs_len = i32(40) + 10, i32(5000), i32(90)
+    zero = torch.zeros(B, dtype=torch.uint8, device=device)
+    for err, dec_err, pad in ((u8(3), u8(2), u8(2)), (zero, zero, None), (zero, u8(9), zero[:5])):
+        flags_copy = torch.empty(B, dtype=torch.uint8, device=device)
+        left = torch.empty(B, dtype=torch.int32, device=device)
+        pack = torch.full((ops.readback_bytes(B),), 0xAB, dtype=torch.uint8, device=device)
+        p = ops._ptr
+        _call("rmi_turn_readback_pad", p(flags), p(err), p(dec_err), p(num_actions), p(max_actions), p(text_len),
+              p(obs_len), B, p(flags_copy), p(left), p(pack), p(pad), 0 if pad is None else pad.numel(),
+              ops._stream(device))
+        h = pack.cpu().numpy()
+        o = (3 * B + 3) & ~3
+        tail = h[o:o + 36].view(np.int32)
+        assert (h[:B] == flags.cpu().numpy()).all() and (h[2 * B:3 * B] == dec_err.cpu().numpy()).all()
+        assert tail[0] == int(text_len.max()) and tail[1] == int(obs_len.max())
+        assert tail[6] == (0 if pad is None else int((pad != 0).sum()))
+        e_or = int(np.bitwise_or.reduce(err.cpu().numpy()))
+        d_or = int(np.bitwise_or.reduce(dec_err.cpu().numpy()))
+        assert ops.readback_summary(tail) == (e_or, d_or, int(((flags & _lib.FLAG_DONE) != 0).sum()))
+        assert (h[o + 8:o + 24] == 0xAB).all()  # the stats and raw slots are other writers'
 
 
 def _call(name, *args):

@@ -49,3 +49,20 @@ def test_env_ids_of_plain_dataproto():
     d = DataProto(None, {"env_ids": np.array([3, 1, 2], dtype=object)})
     ids = env_ids_of(d)
     assert ids.dtype == np.int64 and list(ids) == [3, 1, 2]
+
+
+def test_freed_without_the_cyclic_gc():
+    """A LazyDataProto and its non_tensor_batch hold no reference cycle: the batch is freed as
+    soon as the caller drops it (its tensors' block is then free for the next rollout's batch)."""
+    import gc
+    import weakref
+    gc.disable()
+    try:
+        d = LazyDataProto(np.arange(4), lambda: None)
+        d.set_device_batch({"input_ids": torch.zeros(4, 3, dtype=torch.int64)}, np.arange(4), 2)
+        assert list(d.non_tensor_batch["group_ids"]) == [0, 0, 1, 1] and "env_ids" in d.non_tensor_batch
+        w = weakref.ref(d)
+        del d
+        assert w() is None
+    finally:
+        gc.enable()

@@ -15,6 +15,7 @@ import torch  # noqa: E402
 from ragen_amd import _lib, ops  # noqa: E402
 
 TURN = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+PMC = len(sys.argv) > 2 and sys.argv[2] == "pmc"  # (rocprofv3 --pmc: 10 launches at the bound only)
 base.run()
 es = base.proxy.train_es_manager
 ch = es._chain
@@ -55,6 +56,13 @@ def timed(stride, reps=20):
     return e0.elapsed_time(e1) * 1e3 / reps
 
 
+if PMC:
+    torch.cuda.synchronize()
+    for _ in range(10):
+        launch(bound)
+    torch.cuda.synchronize()
+    print(json.dumps({"turn": TURN, "rows": n, "bound": bound, "text_bytes": int(tlen.sum()), "launches": 10}))
+    sys.exit(0)
 ref_ids = None
 res = {"turn": TURN, "rows": n, "bound": bound, "longest_row": longest, "mean_row": float(tlen.float().mean()),
        "text_bytes": int(tlen.sum())}
