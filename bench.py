@@ -23,6 +23,7 @@ rocprofv3 pass (profiles/), and the CPU baseline (the oracle's per-env Python po
 reference path, timed on this host).
 """
 import argparse
+import ctypes
 import glob
 import json
 import os
@@ -37,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from ragen_amd import distributed as rd  # noqa: E402
-from ragen_amd import ops, synthetic  # noqa: E402
+from ragen_amd import _lib, ops, synthetic  # noqa: E402
 from ragen_amd.env import SokobanBatch  # noqa: E402
 from ragen_amd.env.configs import SokobanEnvConfig  # noqa: E402
 
@@ -623,6 +624,136 @@ def text_leg(R, device, reps=20):
             "render": {"kernel": "rmi_sokoban_render", "envs": B, "us": render_us}}
 
 
+def prompt_kernels(proxy, tok, device, turn=2, reps=10):
+    """the caller path's text kernels on the API rollout's own rows (the last
+    rollout's turn-``turn`` slot of the turn chain, 8192 envs), relaunched alone with HIP events:
+    * prompt_text (rmi_prompt_text): the assistant + user block text of every row; bytes = the
+      decoded responses and observation rows read + the text written;
+    * bpe_encode (rmi_bpe_encode): that text -> ids at the chain's row bound; bytes = text in + 8 B
+      per id out (word cache warm; also one launch with it cleared);
+    * pad_rows (rmi_pad_rows): the generation batch of the final turn (every env's arena row,
+      left-padded to the widest + the generation prompt); bytes = 8 B per arena id read + 3 x 8 B
+      per output cell;
+    * bpe_merge_table: the same turn's text built on the host (no expansion placeholders: every
+      template byte is encoded) through the 5 k-merge tokenizer and through a Qwen2-sized one
+      (synthetic.qwen_scale_tokenizer, 151 000 merges), ids checked against the HF tokenizers."""
+    from ragen_amd.tokenizer import DeviceTokenizer
+    es = proxy.train_es_manager
+    ch = es.__dict__.get("_chain")
+    if ch is None or turn not in ch.slots or ch.slots[turn].prompt is None:
+        return None
+    s, pr, n = ch.slots[turn], ch.pr, es.n_envs
+    L = _lib.lib()
+    stream = ops._stream(device)
+    _, _, pstride, bound, _, held = s.prompt
+    P = ctypes.byref(held[0])  # the turn's rmi_prompt_t
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+
+    def timed(fn, r=reps):
+        fn()
+        torch.cuda.synchronize()
+        torch.cuda._sleep(1_000_000)
+        ev[0].record()
+        for _ in range(r):
+            fn()
+        ev[1].record()
+        torch.cuda.synchronize()
+        return ev[0].elapsed_time(ev[1]) * 1e3 / r
+
+    def blk(us, nbytes, **kw):
+        gbs = nbytes / (us * 1e-6) / 1e9
+        return dict(kw, us=us, bytes=int(nbytes), achieved_GBs=gbs, frac=gbs / HBM_PEAK_GBS)
+
+    out = {"rows": n, "turn": turn}
+    # prompt_text
+    pt_us = timed(lambda: ops.check(L.rmi_prompt_text(P, n, s.ptext.data_ptr(), pstride, s.ptext_len.data_ptr(),
+                                                      s.pmark.data_ptr(), s.pterr.data_ptr(), stream),
+                                    "rmi_prompt_text"))
+    act = s.has.bool()
+    resp_b = int(s.tlen[act].to(torch.int64).sum())
+    obs_b = int(s.obs[1][act].to(torch.int64).sum())
+    text_b = int(s.ptext_len.to(torch.int64).sum())
+    out["prompt_text"] = blk(pt_us, resp_b + obs_b + text_b, kernel="rmi_prompt_text", text_bytes_out=text_b)
+    # bpe_encode
+    dt = pr.dt
+    bs = dt.bpe_struct()
+    ids = torch.zeros(n, 2048, dtype=torch.int64, device=device)
+    olen = torch.zeros(n, dtype=torch.int32, device=device)
+    ntok = torch.empty(n, dtype=torch.int32, device=device)
+    mtok = torch.empty(n, dtype=torch.int32, device=device)
+    err = torch.empty(n, dtype=torch.uint8, device=device)
+
+    def bpe():
+        ops.check(L.rmi_bpe_encode(ctypes.addressof(bs), s.ptext.data_ptr(), pstride, bound, s.ptext_len.data_ptr(),
+                                   n, ids.data_ptr(), 2048, None, ntok.data_ptr(), s.pmark.data_ptr(),
+                                   mtok.data_ptr(), err.data_ptr(), stream), "rmi_bpe_encode")
+    bpe_us = timed(bpe)
+    n_ids = int(ntok.to(torch.int64).sum())
+    assert int((err != 0).sum()) == 0
+    cold = None
+    if dt.word_cache is not None:
+        saved = dt.word_cache.clone()
+        dt.word_cache.zero_()
+        cold = timed(bpe, 1)
+        dt.word_cache.copy_(saved)
+    out["bpe_encode"] = blk(bpe_us, text_b + 8 * n_ids, kernel="rmi_bpe_encode", row_bound=bound, ids_out=n_ids,
+                            text_GBs=text_b / (bpe_us * 1e-6) / 1e9, us_word_cache_cleared=cold,
+                            note="the chain's text: template stretches as expansion placeholders (their ids "
+                                 "copied, their bytes not encoded)")
+    # pad_rows: the final turn's generation batch shape over every env
+    S = int(pr.len.max()) + pr.tail_n
+    rows = torch.arange(n, dtype=torch.int64, device=device)
+    pad = torch.empty(3, n, S, dtype=torch.int64, device=device)
+    perr = torch.empty(n, dtype=torch.uint8, device=device)
+    pad_us = timed(lambda: ops.check(L.rmi_pad_rows(pr.arena_p, pr.arena_stride, pr.len_p, rows.data_ptr(), n,
+                                                    pr.tail_p, pr.tail_n, S, int(pr.pad_id), pad[0].data_ptr(),
+                                                    pad[1].data_ptr(), pad[2].data_ptr(), perr.data_ptr(), stream),
+                                    "rmi_pad_rows"))
+    arena_ids = int(pr.len.to(torch.int64).sum()) + n * pr.tail_n
+    out["pad_rows"] = blk(pad_us, 8 * arena_ids + 24 * n * S, kernel="rmi_pad_rows", width=S)
+    del pad
+    # the merge-table size: the same turn's text from the host, both tokenizers
+    texts = []
+    has_h, fl_h = s.has.cpu().numpy(), s.flags_copy.cpu().numpy()
+    for e in np.flatnonzero(has_h):
+        a, b = pr.host_turn_text(int(e), turn, not (int(fl_h[e]) & _lib.FLAG_DONE))
+        texts.append(a + b)
+    buf, lens = synthetic.encode_rows(texts)
+    tb = torch.from_numpy(buf).to(device)
+    tl = torch.from_numpy(lens).to(device)
+    stride = min(3072, (int(lens.max()) + 3) // 4 * 4)
+    big = synthetic.qwen_scale_tokenizer(base=tok)
+    res = {"rows": len(texts), "text_bytes": int(lens.sum()), "row_bound": stride}
+    for name, t in (("merges_5k", tok), ("merges_151k", big)):
+        d = DeviceTokenizer.from_hf(t, device)
+        o = torch.zeros(len(texts), 2048, dtype=torch.int64, device=device)
+        oln = torch.zeros(len(texts), dtype=torch.int32, device=device)
+
+        def enc():
+            oln.zero_()
+            return d.encode_rows(tb, tl, o, oln, max_len=stride)
+        n_tok, _, e8 = enc()
+        torch.cuda.synchronize()
+        assert int((e8 != 0).sum()) == 0
+        for i in range(0, len(texts), max(1, len(texts) // 64)):  # ids == the HF tokenizer's, 64 rows
+            want = t(texts[i], add_special_tokens=False).input_ids
+            assert o[i, :int(n_tok[i])].tolist() == want, (name, i)
+        us = timed(lambda: enc())
+        cold_us = None
+        if d.word_cache is not None:
+            d.word_cache.zero_()
+            cold_us = timed(lambda: enc(), 1)
+        merges = int(len(json.loads(t.backend_tokenizer.to_str())["model"]["merges"]))
+        res[name] = {"merges": merges, "us": us, "us_word_cache_cleared": cold_us,
+                     "ids_out": int(n_tok.to(torch.int64).sum()),
+                     "text_GBs": int(lens.sum()) / (us * 1e-6) / 1e9}
+    res["ratio_151k_to_5k"] = res["merges_151k"]["us"] / res["merges_5k"]["us"]
+    res["ratio_151k_to_5k_cold"] = (res["merges_151k"]["us_word_cache_cleared"] /
+                                    res["merges_5k"]["us_word_cache_cleared"])
+    out["bpe_merge_table"] = res
+    return out
+
+
 def api_leg(device):
     """SURVEY §8(d)'s "API" variant of the headline: the same SK workload (8192 envs, 5 turns, the
     bench's synthetic actions written as LLM responses) driven through the drop-in
@@ -738,7 +869,8 @@ def api_leg(device):
             env.step_turn(0, z8, zu, zu, 10, -0.1)
         per_call[mode] = (time.perf_counter() - t0) / 500 * 1e6
         torch.cuda.synchronize()
-    return {"env_steps_per_s": device_path["env_steps_per_s"], "device_path": device_path,
+    prompt = prompt_kernels(proxy, tok, device)
+    return {"env_steps_per_s": device_path["env_steps_per_s"], "device_path": device_path, "prompt_kernels": prompt,
             "dict_path": dict(dict_path["op"], ctypes=dict_path["ctypes"], host_us_per_turn_call=per_call,
                               note="EnvStateManager.step facade, host dicts + text obs each turn (the action-name "
                                    "lists are built before the timed loop); best of 4 rollouts; the top level "
@@ -1237,6 +1369,8 @@ def main():
     toytext = toytext_legs(device) if extras else None
     api = api_leg(device) if not args.no_extras and rank == 0 else None
     text = text_leg(R, device) if not args.no_extras and rank == 0 else None
+    if text is not None and api is not None:  # the caller path's text kernels (measured in api_leg)
+        text["prompt"] = api.pop("prompt_kernels", None)
     at_scale = None
     if not args.no_extras and rank == 0:
         s_dur, s_B = scale_leg(R, device)

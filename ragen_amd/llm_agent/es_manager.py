@@ -683,10 +683,13 @@ class EnvStateManager:
             bad = int(np.nonzero(dec_h)[0][0])
             raise ValueError(f"env {self.env_lo + bad}: the decoded generation exceeded the device row buffer or held "
                              "an id outside the vocabulary (rmi_detokenize RMI_ERR_UNSUP); its env was not stepped")
-        if summ is not None and inp.env_ids is self._live_ids and summ[2] == n - n_in:
+        if summ is not None and asc and inp.env_ids is self._live_ids:
             # the envs outside this turn's ids were all done before it (the ids are the last
-            # turn's survivors): no input became done
-            all_still = True
+            # turn's survivors, ascending): the inputs that go on are the envs not done
+            all_still = summ[2] == n - n_in
+            if not all_still:
+                still = None
+                out_local = np.flatnonzero((fl_h & _lib.FLAG_DONE) == 0)
         else:
             if inp.env_ids is self._ids_in_order:  # every env, in order (no gather)
                 still = (fl_h & _lib.FLAG_DONE) == 0
@@ -694,7 +697,12 @@ class EnvStateManager:
                 still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
             all_still = bool(still.all())
         self._all_active = n_in == self.n_envs and all_still
-        out_ids = inp.env_ids if all_still else inp.env_ids[still]
+        if all_still:
+            out_ids = inp.env_ids
+        elif still is None:
+            out_ids = out_local + self.env_lo if self.env_lo else out_local
+        else:
+            out_ids = inp.env_ids[still]
         self._live_ids = out_ids
         if eager:  # the next batch's stats, valid for exactly the env-id array handed out below
             hook.set_next_stats(t, tail[2:5], out_ids)

@@ -764,18 +764,25 @@ class DevicePrompts:
         del ap
         self._write_host(e, self._host_ids(text))
 
-    def _host_turn(self, e, t, cont):
+    def host_turn_text(self, e, t, cont):
+        """The text turn t appends to env e's prompt, built on the host from its history
+        (ctx_manager.py:248-263 under the chat template): (assistant block, user block or "")."""
         self.es._materialize()
         g = self.es.env_lo + e
         hist = self.es.rollout_cache[e]["history"]
-        h, nxt = hist[t], hist[t + 1]
-        a = self._host_ids(self.tpl.a_pre + h["llm_response"] + self.tpl.a_suf)
-        b = []
+        h = hist[t]
+        a = self.tpl.a_pre + h["llm_response"] + self.tpl.a_suf
+        b = ""
         if cont:
+            nxt = hist[t + 1]
             length = f"Max response length: {self.ctx.env_config_lookup[g]['max_tokens']} words (tokens)."
-            b = self._host_ids(self.tpl.u_pre + f"Reward:\n{h['reward']}\n\nTurn {t + 2}:\nState:\n{nxt['state']}\n"
-                               f"You have {nxt['actions_left']}" + self._c_mid + length + "\n" + self.tpl.u_suf)
-        self._write_host(e, a, b)
+            b = (self.tpl.u_pre + f"Reward:\n{h['reward']}\n\nTurn {t + 2}:\nState:\n{nxt['state']}\n"
+                 f"You have {nxt['actions_left']}" + self._c_mid + length + "\n" + self.tpl.u_suf)
+        return a, b
+
+    def _host_turn(self, e, t, cont):
+        a, b = self.host_turn_text(e, t, cont)
+        self._write_host(e, self._host_ids(a), self._host_ids(b) if cont else [])
 
     # ------------------------------------------------------------------- batches
     def gen_batch(self, env_ids: np.ndarray):

@@ -346,3 +346,60 @@ def qwen_like_tokenizer(vocab_size: int = 6000, n_docs: int = 1500, seed: int = 
     return PreTrainedTokenizerFast(tokenizer_object=tok, name_or_path="Qwen/Qwen2.5-0.5B-Instruct (synthetic BPE)",
                                    eos_token="<|im_end|>", pad_token="<|endoftext|>", chat_template=QWEN_CHAT_TEMPLATE,
                                    clean_up_tokenization_spaces=False)
+
+
+def qwen_scale_tokenizer(n_merges: int = 151000, seed: int = 11, base=None):
+    """qwen_like_tokenizer's pipeline with a merge table of Qwen2's size (~151 k merges; the real
+    table is a hub download): the trained tokenizer's merges, then random merges of two tokens
+    already in the vocabulary (ranked after every trained one, words up to 16 bytes) until the
+    table holds ``n_merges``.  A stand-in for the merge-table SIZE (hash-table footprint and
+    lookups); which pairs merge is arbitrary.  Deterministic in ``seed``."""
+    import json
+    from tokenizers import Tokenizer
+    from transformers import PreTrainedTokenizerFast
+    base = base if base is not None else qwen_like_tokenizer()
+    j = json.loads(base.backend_tokenizer.to_str())
+    m = j["model"]
+    vocab, merges = m["vocab"], [list(x) for x in m["merges"]]
+    special = {t["id"] for t in j.get("added_tokens", [])}
+    toks = [t for t, i in sorted(vocab.items(), key=lambda x: x[1]) if i not in special]
+    nxt = max(vocab.values()) + 1
+    rng = np.random.default_rng(seed)
+    seen = {(a, b) for a, b in merges}
+    by_len = [[] for _ in range(17)]  # tokens by their byte length (a new word stays <= 16 bytes)
+    for t in toks:
+        n = len(t.encode())
+        if n <= 16:
+            by_len[n].append(t)
+    draws = rng.random((2 * n_merges, 2))
+    k = 0
+    while len(merges) < n_merges:
+        if k == len(draws):
+            draws, k = rng.random((2 * n_merges, 2)), 0
+        la = 1 + int(draws[k, 0] * 8)  # a: 1..8 bytes, b: what is left of 16
+        lb = 1 + int(draws[k, 1] * (16 - la))
+        k += 1
+        if not by_len[la] or not by_len[lb]:
+            continue
+        a = by_len[la][int(rng.integers(len(by_len[la])))]
+        b = by_len[lb][int(rng.integers(len(by_len[lb])))]
+        w = a + b
+        if (a, b) in seen or w in vocab:
+            continue
+        seen.add((a, b))
+        merges.append([a, b])
+        vocab[w] = nxt
+        by_len[la + lb].append(w)
+        nxt += 1
+    # the added tokens keep their ids: move them past the new ones
+    for t in j.get("added_tokens", []):
+        t["id"] = nxt
+        vocab.pop(t["content"], None)
+        nxt += 1
+    m["merges"] = merges
+    tk = Tokenizer.from_str(json.dumps(j))
+    # (no name at construction: above 100 k tokens transformers looks the name up on the hub)
+    out = PreTrainedTokenizerFast(tokenizer_object=tk, eos_token="<|im_end|>", pad_token="<|endoftext|>",
+                                  chat_template=base.chat_template, clean_up_tokenization_spaces=False)
+    out.name_or_path = base.name_or_path + f", {n_merges} merges"
+    return out
