@@ -37,7 +37,7 @@ enum : uint32_t {
   B_IN = 128                            // any byte of a selected added token
 };
 constexpr uint32_t kNoRank = 0xFFFFFFFFu;
-// Stamp points (diagnostic builds): stage | phases 1-4 | symbols + pair lookups | merges, or with
+// Stamp points (diagnostic builds): stage | phases 1-4 | word cache + symbols | merges, or with
 // RMI_BPE_FINE phase 1 | 2 | 3 | 4 (tools/prof_prompt_stamps.py prints four spans either way).
 #ifdef RMI_BPE_FINE
 #define BST_N(i) do {} while (0)
@@ -55,14 +55,13 @@ constexpr int kMaxStride = 3072;
 // memory per byte.  (They used to: a class lookup was two dependent global loads per byte, and
 // each added-token comparison a chain of global byte loads — ≈64 k cycles of a wave's 161 k.)
 constexpr int kStageAdded = 64;
-constexpr int kPairBatch = 8;     // 64-pair chunks whose first hash probes go out together
+constexpr int kPairBatch = 4;     // a merge step's pair lookups in flight together
 // 16 bytes per text byte (T, C 1; M, P, K 2; Y, R 4) and the staged tables (≈1.5 KB for the
 // Qwen2 tokenizer with the prompt expansions): the wave's LDS, which sets how many rows are
 // in flight per CU.  (R held the merged id too, as a u64: 20 bytes per text byte and ≈4.5 KB of
 // tables, with the byte ids, the added tokens' bytes and 64 token slots always staged.)
 struct Lds {  // carved from dynamic LDS, n = stride, na = the staged added tokens (0 or n_added)
   uint64_t* AW;  // each staged added token's first 32 bytes, zero padded [na][4]
-  uint32_t* R;   // rank of the pair starting at a symbol start (kNoRank: none)
   int32_t* Y;    // symbol id at a symbol start
   int32_t* AO;   // added_off [na + 1] (staged tables only)
   int32_t* AI;   // added_id [na]
@@ -79,14 +78,23 @@ struct Lds {  // carved from dynamic LDS, n = stride, na = the staged added toke
 __host__ __device__ constexpr int staged_added(int n_added) {
   return n_added > 0 && n_added <= kStageAdded ? n_added : 0;
 }
+// the staged tokens' 32-byte words: the plain tokens only when expansions follow them (an
+// expansion is matched by its index byte, never by a word compare)
+__host__ __device__ constexpr int staged_words(int n_added, int n_exp) {
+  return staged_added(n_added) > 0 && n_exp > 0 && n_exp <= n_added ? n_added - n_exp : staged_added(n_added);
+}
 // the expansion tables are staged with the row when small (their ids are copied to every row
 // that holds one; from HBM that was one dependent load per id)
 constexpr int kStageExpIds = 512;
 __host__ __device__ constexpr bool staged_exp(int n_exp, int n_exp_ids) {
+#ifdef RMI_BPE_NO_EXP_LDS  // (A/B variant)
+  return false;
+#else
   return n_exp > 0 && n_exp_ids > 0 && n_exp_ids <= kStageExpIds;
+#endif
 }
-__host__ __device__ constexpr size_t bpe_lds(int stride, int na, int ne, int nei) {
-  return 32 * (size_t)na + 8 * (size_t)stride + 4 * (size_t)(na + 1) + 4 + 4 * (size_t)na + 32 +
+__host__ __device__ constexpr size_t bpe_lds(int stride, int na, int nw, int ne, int nei) {
+  return 32 * (size_t)nw + 4 * (size_t)stride + 4 * (size_t)(na + 1) + 4 + 4 * (size_t)na + 32 +
          6 * (size_t)stride + 128 + (size_t)stride + 16 + (size_t)stride + 128 + 128 +
          (staged_exp(ne, nei) ? 4 * (size_t)(ne + 1) + 4 * (size_t)nei : 0);
 }
@@ -309,14 +317,12 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int S = stride;
-  const int na = staged_added(tok.n_added);
+  const int na = staged_added(tok.n_added), nw = staged_words(tok.n_added, tok.n_exp);
   Lds L;
   {  // (the order of bpe_lds: the 8-byte words first, then 4-, 2- and 1-byte arrays)
     uint8_t* p = smem;
     L.AW = reinterpret_cast<uint64_t*>(p);
-    p += 32 * (size_t)na;
-    L.R = reinterpret_cast<uint32_t*>(p);
-    p += 4 * (size_t)S;
+    p += 32 * (size_t)nw;
     L.Y = reinterpret_cast<int32_t*>(p);
     p += 4 * (size_t)S;
     L.AO = reinterpret_cast<int32_t*>(p);
@@ -384,7 +390,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   // the host's staging tables when given: every load below is independent of the others
   const bool words_given = stage_added && tok.added_words != nullptr;
   if (words_given)
-    for (int i = lane; i < 4 * na; i += 64) L.AW[i] = tok.added_words[i];
+    for (int i = lane; i < 4 * nw; i += 64) L.AW[i] = tok.added_words[i];
   if (tok.ascii_class && lane < 32)
     reinterpret_cast<uint32_t*>(L.AC)[lane] = reinterpret_cast<const uint32_t*>(tok.ascii_class)[lane];
   if (exp_lds) {
@@ -404,9 +410,9 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   bool added_words = words_given;
   if (stage_added && !words_given) {
     bool longer = false;
-    for (int a = lane; a < na; a += 64) longer |= L.AO[a + 1] - L.AO[a] > 32;
+    for (int a = lane; a < nw; a += 64) longer |= L.AO[a + 1] - L.AO[a] > 32;
     added_words = !__any(longer);
-    for (int a = lane; added_words && a < na; a += 64) {
+    for (int a = lane; added_words && a < nw; a += 64) {
       const int o0 = L.AO[a], len = L.AO[a + 1] - o0;
       uint64_t w[4] = {0, 0, 0, 0};
       for (int k = 0; k < len; ++k) w[k >> 3] |= (uint64_t)tok.added_bytes[o0 + k] << (8 * (k & 7));
@@ -420,15 +426,17 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   // candidate by its index byte and compares the others with the plain tokens only
   const int n_plain = tok.n_added - tok.n_exp;
   bool exp_tail = added_words && tok.n_exp > 0 && n_plain >= 0;
-  if (exp_tail) {
+  if (exp_tail) {  // (the expansions' bytes from the table: their words are not staged)
     bool ok = true;
     for (int e = lane; e < tok.n_exp; e += 64) {
       const int a = n_plain + e;
-      ok &= L.AI[a] == -(e + 1) && L.AO[a + 1] - L.AO[a] == 2 &&
-            (uint32_t)(L.AW[4 * a] & 0xFFFFu) == (0xFFu | ((0x80u + (uint32_t)e) << 8));
+      ok &= L.AI[a] == -(e + 1) && L.AO[a + 1] - L.AO[a] == 2 && tok.added_bytes[L.AO[a]] == 0xFFu &&
+            tok.added_bytes[L.AO[a] + 1] == (uint8_t)(0x80u + (uint32_t)e);
     }
     exp_tail = !__any(!ok);
   }
+  // without that layout every token is compared, and only nw of them are staged as words
+  if (!exp_tail && nw < tok.n_added) added_words = false;
 #ifndef RMI_BPE_FINE
   RMI_STAMP_WAIT(1);
 #endif
@@ -747,6 +755,13 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
       L.M[p] = p + 1 < a + q.len ? (uint16_t)(p + 1) : kEnd;
     }
   };
+#ifdef RMI_BPE_ONE_PROBE  // (A/B variant: one pre-token per lane per trip)
+  for (int j0 = 0; j0 < np; j0 += 64) {
+    Probe q0;
+    issue(j0 + lane, q0);
+    finish(q0);
+  }
+#else
   for (int j0 = 0; j0 < np; j0 += 128) {
     Probe q0, q1;
     issue(j0 + lane, q0);
@@ -754,78 +769,58 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     finish(q0);
     finish(q1);
   }
+#endif
   const bool row_merges = __any(miss);
-  if (row_merges) {
-    // the hits' bytes take no pair lookup
-    for (int j = lane; j < np; j += 64)
-      if (L.K[j] & kKHit) {
-        const int a = L.P[j], e = j + 1 < np ? L.P[j + 1] : n;
-        for (int q = a; q < e; ++q) L.C[q] |= B_IN;
-      }
-  }
-  wave_sync();
-  if (row_merges) {
-  // every adjacent pair of the row: the first probe of 8 chunks' pairs in flight together, the
-  // rare second probe (a collision) after
-  for (int q0 = 0; q0 < n; q0 += 64 * kPairBatch) {
-    uint64_t key[kPairBatch], h[kPairBatch], k0[kPairBatch], v0[kPairBatch];
-#pragma unroll
-    for (int g = 0; g < kPairBatch; ++g) {
-      const int q = q0 + 64 * g + lane;
-      key[g] = ~0ull;
-      if (q < n) {
-        const uint16_t nx = (L.C[q] & B_IN) ? kEnd : L.M[q];
-        if (nx != kEnd) key[g] = ((uint64_t)(uint32_t)L.Y[q] << 32) | (uint32_t)L.Y[nx];
-      }
-      h[g] = (key[g] * 0x9E3779B97F4A7C15ull) >> tok.merge_shift;
-    }
-#pragma unroll
-    for (int g = 0; g < kPairBatch; ++g) {
-      k0[g] = key[g] != ~0ull ? tok.merges[2 * h[g]] : ~0ull;
-      v0[g] = key[g] != ~0ull ? tok.merges[2 * h[g] + 1] : ~0ull;
-    }
-#pragma unroll
-    for (int g = 0; g < kPairBatch; ++g) {
-      const int q = q0 + 64 * g + lane;
-      if (q >= n) continue;
-      uint64_t r = ~0ull;
-      if (key[g] != ~0ull) {
-        if (k0[g] == key[g]) r = v0[g];
-        else if (k0[g] != ~0ull) r = merge_lookup(tok, (uint32_t)(key[g] >> 32), (uint32_t)key[g]);
-      }
-      L.R[q] = (uint32_t)(r >> 32);
-    }
-  }
   wave_sync();
   BST_N(3);
-  // The merges, one lane per pre-token.  (Interleaving several words per lane, with their pair
-  // probes in flight together and a bit mask of live symbols instead of the chain walk, measured
-  // slower: 78-95 k cycles per wave against 75 k.)
+  // The merges, one lane per word-cache miss.  (Interleaving several words per lane, with their
+  // pair probes in flight together and a bit mask of live symbols instead of the chain walk,
+  // measured slower in round 3: 78-95 k cycles per wave against 75 k.)  A row without a miss
+  // skips this block.
+  if (row_merges) {
   for (int j = lane; j < np; j += 64) {
     const int a = L.P[j];
     if (L.K[j] != kKMerge) continue;  // an added token or a word-cache hit
     int cnt = 1;
     {
+      // each step: the ranks of the word's current pairs (kPairBatch first probes in flight
+      // together; the entry carries the merged id with the rank), then the lowest rank merged
+      // (leftmost on ties: the scan keeps the first of equal ranks)
       for (;;) {
-        uint32_t best = kNoRank;
-        int bq = -1, bprev = -1, prev = -1;
-        for (int q = a; q != kEnd; prev = q, q = L.M[q]) {
-          const uint32_t r = L.R[q];
-          if (r < best) {
-            best = r;
-            bq = q;
-            bprev = prev;
+        uint64_t best = ~0ull;
+        int bq = -1;
+        for (int q = a; q != kEnd;) {
+          int qs[kPairBatch];
+          uint64_t key[kPairBatch];
+          uint4 ent[kPairBatch];
+#pragma unroll
+          for (int g = 0; g < kPairBatch; ++g) {
+            qs[g] = q;
+            const int nq = q != kEnd ? L.M[q] : kEnd;
+            key[g] = (q != kEnd && nq != kEnd) ? ((uint64_t)(uint32_t)L.Y[q] << 32) | (uint32_t)L.Y[nq] : ~0ull;
+            q = q != kEnd ? nq : kEnd;
+          }
+#pragma unroll
+          for (int g = 0; g < kPairBatch; ++g) {
+            const uint64_t h = (key[g] * 0x9E3779B97F4A7C15ull) >> tok.merge_shift;
+            ent[g] = key[g] != ~0ull ? *reinterpret_cast<const uint4*>(tok.merges + 2 * h) : make_uint4(~0u, ~0u, ~0u, ~0u);
+          }
+#pragma unroll
+          for (int g = 0; g < kPairBatch; ++g) {
+            if (key[g] == ~0ull) continue;
+            const uint64_t k0 = ((uint64_t)ent[g].y << 32) | ent[g].x, v0 = ((uint64_t)ent[g].w << 32) | ent[g].z;
+            const uint64_t v = k0 == key[g] ? v0 : (k0 == ~0ull ? ~0ull : merge_lookup(tok, (uint32_t)(key[g] >> 32),
+                                                                                         (uint32_t)key[g]));
+            if ((v >> 32) < (best >> 32)) {
+              best = v;
+              bq = qs[g];
+            }
           }
         }
         if (bq < 0) break;
         const int rq = L.M[bq];
-        // the merged id: the pair's entry again (R keeps the rank only; a merge is a word-cache
-        // miss, the table line is in cache from the rank lookup)
-        L.Y[bq] = (int32_t)(uint32_t)merge_lookup(tok, (uint32_t)L.Y[bq], (uint32_t)L.Y[rq]);
-        const uint16_t nn = L.M[rq];
-        L.M[bq] = nn;
-        L.R[bq] = nn != kEnd ? (uint32_t)(merge_lookup(tok, (uint32_t)L.Y[bq], (uint32_t)L.Y[nn]) >> 32) : kNoRank;
-        if (bprev >= 0) L.R[bprev] = (uint32_t)(merge_lookup(tok, (uint32_t)L.Y[bprev], (uint32_t)L.Y[bq]) >> 32);
+        L.Y[bq] = (int32_t)(uint32_t)best;
+        L.M[bq] = L.M[rq];
       }
       cnt = 0;
       for (int q = a; q != kEnd; q = L.M[q]) ++cnt;
@@ -906,7 +901,8 @@ RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pi
       tok->n_exp > 64 || (tok->n_exp > 0 && (!tok->exp_off || !tok->exp_ids)))
     return RMI_EINVAL;
   if (tok->n_exp_ids < 0) return RMI_EINVAL;
-  const size_t lds = bpe_lds(stride, staged_added(tok->n_added), tok->n_exp, tok->n_exp_ids);
+  const size_t lds = bpe_lds(stride, staged_added(tok->n_added), staged_words(tok->n_added, tok->n_exp), tok->n_exp,
+                             tok->n_exp_ids);
   hipLaunchKernelGGL(bpe_encode_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text, pitch,
                      (int)stride,
                      text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);

@@ -65,7 +65,8 @@ if PMC:
     sys.exit(0)
 ref_ids = None
 res = {"turn": TURN, "rows": n, "bound": bound, "longest_row": longest, "mean_row": float(tlen.float().mean()),
-       "text_bytes": int(tlen.sum())}
+       "text_bytes": int(tlen.sum()), "n_added": int(tok.n_added), "n_exp": int(tok.n_exp),
+       "n_exp_ids": int(tok.n_exp_ids)}
 launch(bound)
 torch.cuda.synchronize()
 ref = (out.clone(), out_len.clone(), err.clone())

@@ -91,7 +91,7 @@ actor.turn = 0
 proxy.rollout(DataProto(meta_info={}), val=False)
 torch.cuda.synchronize()
 names = {"prompt": ["stage", "pieces up to the reward", "the reward piece", "the rest + stores"],
-         "bpe": ["stage", "classes + added + match lengths + chain", "symbols + pair lookups", "merges"]}[WHICH]
+         "bpe": ["stage", "classes + added + match lengths + chain", "word cache + symbols", "merges"]}[WHICH]
 if WHICH == "bpe" and ("fine" in os.path.basename(SO) or "bpstf" in os.path.basename(SO)):  # -DRMI_BPE_FINE
     names = ["1 classes", "2 added tokens", "3 match lengths", "4 chain"]
 for c, buf in enumerate(bufs):
