@@ -576,6 +576,20 @@ typedef struct {
   /* exp_off[n_exp] when the caller knows it (0: unknown); <= 512 -> the kernel stages the
    * expansion tables in LDS with each row (one dependent HBM load per copied id otherwise).   */
   int32_t n_exp_ids;
+  /* Two-pass scratch (all NULL, or pre_cap < rows * stride: one kernel per call).  With it the
+   * call is three launches: the pre-tokenizer pass (its LDS is 6 B per text byte, so more rows
+   * are in flight) writes each row's pre-token list (pre[row * stride + j] = start | length << 12
+   * | added << 24, pre_np[row] entries; pre_gid[row * stride + start] = an added token's id);
+   * the word pass looks each pre-token up in the word cache and merges the misses in a small
+   * per-wave scratch; a row whose misses outgrow that scratch is flagged in pre_retry and
+   * encoded again by the one-kernel algorithm.  Same outputs either way, except that a row
+   * flagged for passing out_stride may have had ids written past out_len[b] (out_len[b], n_tok
+   * and mark_tok are as for any flagged row).                                                 */
+  uint32_t* pre;            /* [pre_cap]                                                     */
+  int32_t* pre_gid;         /* [pre_cap]                                                     */
+  int32_t* pre_np;          /* [pre_cap / 4]                                                 */
+  uint8_t* pre_retry;       /* [pre_cap / 4]                                                 */
+  int64_t pre_cap;          /* taken when rows * stride <= pre_cap (then rows <= pre_cap / 4) */
 } rmi_bpe_t;
 
 /* Row b: text[b * pitch .. + text_len[b]) (UTF-8; pitch % 4 == 0); `stride` (% 4 == 0,

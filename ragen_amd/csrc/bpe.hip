@@ -93,10 +93,15 @@ __host__ __device__ constexpr bool staged_exp(int n_exp, int n_exp_ids) {
   return n_exp > 0 && n_exp_ids > 0 && n_exp_ids <= kStageExpIds;
 #endif
 }
-__host__ __device__ constexpr size_t bpe_lds(int stride, int na, int nw, int ne, int nei) {
-  return 32 * (size_t)nw + 4 * (size_t)stride + 4 * (size_t)(na + 1) + 4 + 4 * (size_t)na + 32 +
-         6 * (size_t)stride + 128 + (size_t)stride + 16 + (size_t)stride + 128 + 128 +
-         (staged_exp(ne, nei) ? 4 * (size_t)(ne + 1) + 4 * (size_t)nei : 0);
+// kernel modes: the one-kernel algorithm, its pre-tokenizer pass alone (two-pass form: no
+// symbol ids, no counts, no expansion tables in LDS), the one-kernel algorithm over the rows the
+// word pass flagged
+enum { kModeFull = 0, kModePretok = 1, kModeRetry = 2 };
+__host__ __device__ constexpr size_t bpe_lds(int stride, int na, int nw, int ne, int nei, int mode = kModeFull) {
+  return 32 * (size_t)nw + (mode == kModePretok ? 0 : 4 * (size_t)stride) + 4 * (size_t)(na + 1) + 4 +
+         4 * (size_t)na + 32 + 4 * (size_t)stride + (mode == kModePretok ? 0 : 2 * (size_t)stride + 128) +
+         (size_t)stride + 16 + (size_t)stride + 128 + 128 +
+         (mode != kModePretok && staged_exp(ne, nei) ? 4 * (size_t)(ne + 1) + 4 * (size_t)nei : 0);
 }
 
 __device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a, uint32_t b) {
@@ -188,7 +193,8 @@ __device__ __forceinline__ void wc_load(const rmi_bpe_t& t, uint32_t h, uint4 (&
 }
 
 // the probe sequence from its (i0)th slot h on: -> the word's id count, or 0 on a miss
-__device__ int wc_find_from(const rmi_bpe_t& t, const uint32_t k[4], int len, int32_t* Y, uint32_t h, int i0) {
+__device__ __forceinline__ int wc_find_from(const rmi_bpe_t& t, const uint32_t k[4], int len, int32_t* Y, uint32_t h,
+                                            int i0) {
   for (int i = i0; i < kWcProbe; ++i, h = (h + 1) & t.word_cache_mask) {
     uint4 w[4];
     wc_load(t, h, w);
@@ -306,6 +312,54 @@ __device__ int match_serial(const uint8_t* T, const uint8_t* C, int p, int s1) {
   return e - p;
 }
 
+// The merges of one word whose symbols are the chain Y / M from a (the tokenizers crate's
+// word.rs merge_all order: lowest rank first, leftmost on ties) -> its symbol count.
+__device__ int merge_word(const rmi_bpe_t& tok, int32_t* Y, uint16_t* M, int a) {
+  // each step: the ranks of the word's current pairs (kPairBatch first probes in flight
+  // together; the entry carries the merged id with the rank), then the lowest rank merged
+  // (leftmost on ties: the scan keeps the first of equal ranks)
+  for (;;) {
+    uint64_t best = ~0ull;
+    int bq = -1;
+    for (int q = a; q != kEnd;) {
+      int qs[kPairBatch];
+      uint64_t key[kPairBatch];
+      uint4 ent[kPairBatch];
+#pragma unroll
+      for (int g = 0; g < kPairBatch; ++g) {
+        qs[g] = q;
+        const int nq = q != kEnd ? M[q] : kEnd;
+        key[g] = (q != kEnd && nq != kEnd) ? ((uint64_t)(uint32_t)Y[q] << 32) | (uint32_t)Y[nq] : ~0ull;
+        q = q != kEnd ? nq : kEnd;
+      }
+#pragma unroll
+      for (int g = 0; g < kPairBatch; ++g) {
+        const uint64_t h = (key[g] * 0x9E3779B97F4A7C15ull) >> tok.merge_shift;
+        ent[g] = key[g] != ~0ull ? *reinterpret_cast<const uint4*>(tok.merges + 2 * h) : make_uint4(~0u, ~0u, ~0u, ~0u);
+      }
+#pragma unroll
+      for (int g = 0; g < kPairBatch; ++g) {
+        if (key[g] == ~0ull) continue;
+        const uint64_t k0 = ((uint64_t)ent[g].y << 32) | ent[g].x, v0 = ((uint64_t)ent[g].w << 32) | ent[g].z;
+        const uint64_t v = k0 == key[g] ? v0 : (k0 == ~0ull ? ~0ull : merge_lookup(tok, (uint32_t)(key[g] >> 32),
+                                                                                     (uint32_t)key[g]));
+        if ((v >> 32) < (best >> 32)) {
+          best = v;
+          bq = qs[g];
+        }
+      }
+    }
+    if (bq < 0) break;
+    const int rq = M[bq];
+    Y[bq] = (int32_t)(uint32_t)best;
+    M[bq] = M[rq];
+  }
+  int cnt = 0;
+  for (int q = a; q != kEnd; q = M[q]) ++cnt;
+  return cnt;
+}
+
+template <int kMode>
 __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uint8_t* __restrict__ text, int64_t pitch,
                                                         int stride,
                                                         const int32_t* __restrict__ text_len, int64_t* __restrict__ out,
@@ -317,14 +371,19 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   const int lane = threadIdx.x;
   const int64_t b = blockIdx.x;
   const int S = stride;
+  if (kMode == kModeRetry && !tok.pre_retry[b]) return;  // finished by the word pass
+  if (kMode == kModePretok && threadIdx.x == 0) tok.pre_retry[b] = 0;
   const int na = staged_added(tok.n_added), nw = staged_words(tok.n_added, tok.n_exp);
   Lds L;
   {  // (the order of bpe_lds: the 8-byte words first, then 4-, 2- and 1-byte arrays)
     uint8_t* p = smem;
     L.AW = reinterpret_cast<uint64_t*>(p);
     p += 32 * (size_t)nw;
-    L.Y = reinterpret_cast<int32_t*>(p);
-    p += 4 * (size_t)S;
+    L.Y = nullptr;
+    if (kMode != kModePretok) {
+      L.Y = reinterpret_cast<int32_t*>(p);
+      p += 4 * (size_t)S;
+    }
     L.AO = reinterpret_cast<int32_t*>(p);
     p += 4 * (size_t)(na + 1) + 4;
     L.AI = reinterpret_cast<int32_t*>(p);
@@ -335,8 +394,11 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     p += 2 * (size_t)S;
     L.P = reinterpret_cast<uint16_t*>(p);
     p += 2 * (size_t)S;
-    L.K = reinterpret_cast<uint16_t*>(p);
-    p += 2 * (size_t)S + 128;
+    L.K = nullptr;
+    if (kMode != kModePretok) {
+      L.K = reinterpret_cast<uint16_t*>(p);
+      p += 2 * (size_t)S + 128;
+    }
     L.T = p;
     p += S + 16;
     L.C = p;
@@ -346,7 +408,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     L.EO = reinterpret_cast<int32_t*>(p);  // (4-aligned: every array above is a multiple of 4 bytes)
     L.EI = L.EO + (tok.n_exp + 1);
   }
-  const bool exp_lds = staged_exp(tok.n_exp, tok.n_exp_ids);
+  const bool exp_lds = kMode != kModePretok && staged_exp(tok.n_exp, tok.n_exp_ids);
   const int32_t* EO = exp_lds ? L.EO : tok.exp_off;
   const int32_t* EI = exp_lds ? L.EI : tok.exp_ids;
   RMI_STAMP_DECL;
@@ -580,7 +642,10 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
             }
           }
         }
-        if (best_len > 0) L.Y[p] = best_id;
+        if (best_len > 0) {
+          if (kMode == kModePretok) tok.pre_gid[b * (int64_t)S + p] = best_id;  // (read by the word pass)
+          else L.Y[p] = best_id;
+        }
       }
       const int nc = n_cand - c0 < 64 ? n_cand - c0 : 64;
       uint64_t sel = 0;
@@ -693,6 +758,18 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   wave_sync();
   BST_N(2);
   BST_F(4);
+  if constexpr (kMode == kModePretok) {  // the row's pre-token list, then the word pass
+    uint32_t* pe = tok.pre + b * (int64_t)S;
+    for (int j = lane; j < np; j += 64) {
+      const int a = L.P[j], e = j + 1 < np ? L.P[j + 1] : n;
+      pe[j] = (uint32_t)a | ((uint32_t)(e - a) << 12) | ((L.C[a] & B_ADD) ? (1u << 24) : 0u);
+    }
+    if (lane == 0) {
+      tok.pre_np[b] = np;
+      err[b] = 0;
+    }
+    return;
+  }
   // ---- 5. BPE: symbols, pair ranks, merges (one lane per pre-token)
   // piece bounds: P[j] .. P[j+1] (or n); the symbol chain in M: next symbol start or kEnd.
   // K[j] after this loop: an added token's or a word-cache hit's id count (a hit flagged
@@ -783,47 +860,7 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     if (L.K[j] != kKMerge) continue;  // an added token or a word-cache hit
     int cnt = 1;
     {
-      // each step: the ranks of the word's current pairs (kPairBatch first probes in flight
-      // together; the entry carries the merged id with the rank), then the lowest rank merged
-      // (leftmost on ties: the scan keeps the first of equal ranks)
-      for (;;) {
-        uint64_t best = ~0ull;
-        int bq = -1;
-        for (int q = a; q != kEnd;) {
-          int qs[kPairBatch];
-          uint64_t key[kPairBatch];
-          uint4 ent[kPairBatch];
-#pragma unroll
-          for (int g = 0; g < kPairBatch; ++g) {
-            qs[g] = q;
-            const int nq = q != kEnd ? L.M[q] : kEnd;
-            key[g] = (q != kEnd && nq != kEnd) ? ((uint64_t)(uint32_t)L.Y[q] << 32) | (uint32_t)L.Y[nq] : ~0ull;
-            q = q != kEnd ? nq : kEnd;
-          }
-#pragma unroll
-          for (int g = 0; g < kPairBatch; ++g) {
-            const uint64_t h = (key[g] * 0x9E3779B97F4A7C15ull) >> tok.merge_shift;
-            ent[g] = key[g] != ~0ull ? *reinterpret_cast<const uint4*>(tok.merges + 2 * h) : make_uint4(~0u, ~0u, ~0u, ~0u);
-          }
-#pragma unroll
-          for (int g = 0; g < kPairBatch; ++g) {
-            if (key[g] == ~0ull) continue;
-            const uint64_t k0 = ((uint64_t)ent[g].y << 32) | ent[g].x, v0 = ((uint64_t)ent[g].w << 32) | ent[g].z;
-            const uint64_t v = k0 == key[g] ? v0 : (k0 == ~0ull ? ~0ull : merge_lookup(tok, (uint32_t)(key[g] >> 32),
-                                                                                         (uint32_t)key[g]));
-            if ((v >> 32) < (best >> 32)) {
-              best = v;
-              bq = qs[g];
-            }
-          }
-        }
-        if (bq < 0) break;
-        const int rq = L.M[bq];
-        L.Y[bq] = (int32_t)(uint32_t)best;
-        L.M[bq] = L.M[rq];
-      }
-      cnt = 0;
-      for (int q = a; q != kEnd; q = L.M[q]) ++cnt;
+      cnt = merge_word(tok, L.Y, L.M, a);
       const int len = (j + 1 < np ? L.P[j + 1] : n) - a;
       if (tok.word_cache && len >= 2 && len <= kWcWordMax && cnt <= kWcIdsMax) {
         uint32_t k[4];
@@ -854,18 +891,24 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   if (base_len + total > out_stride) return fail(RMI_ERR_UNSUP);
   wave_sync();
   int64_t* orow = out + b * out_stride + base_len;
-  for (int j = lane; j < np; j += 64) {
-    const int kj = L.K[j];
+  for (int j0 = 0; j0 < np; j0 += 64) {
+    const int j = j0 + lane;
+    const int kj = j < np ? L.K[j] : 0;
     int o = kj & ~kKHit;
-    const int a = L.P[j];
+    const int a = j < np ? L.P[j] : 0;
+    const bool is_exp = j < np && !(kj & kKHit) && (L.C[a] & B_ADD) && L.Y[a] < 0;
+    // expansions: the wave copies each one's ids together (a lane's own copy loop waited on a
+    // table read per id, tens of ids per expansion)
+    for (uint64_t em = __ballot(is_exp); em; em &= em - 1) {
+      const int src_l = __builtin_ctzll(em);
+      const int e = -L.Y[__builtin_amdgcn_readlane(a, src_l)] - 1, eo = __builtin_amdgcn_readlane(o, src_l);
+      const int e0 = EO[e], ec = EO[e + 1] - e0;
+      for (int i = lane; i < ec; i += 64) orow[eo + i] = (int64_t)EI[e0 + i];
+    }
+    if (j >= np || is_exp) continue;
     if (kj & kKHit) {  // a word-cache hit: its ids at Y[a ..), the count up to the next offset
       const int o1 = j + 1 < np ? (L.K[j + 1] & ~kKHit) : total;
       for (int q = a; o < o1; ++q) orow[o++] = (int64_t)L.Y[q];
-      continue;
-    }
-    if ((L.C[a] & B_ADD) && L.Y[a] < 0) {  // an expansion: its ids from the table
-      const int e = -L.Y[a] - 1;
-      for (int k = EO[e]; k < EO[e + 1]; ++k) orow[o++] = (int64_t)EI[k];
       continue;
     }
     for (int q = a; q != kEnd; q = L.M[q]) orow[o++] = (int64_t)L.Y[q];
@@ -875,6 +918,192 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
     if (out_len) out_len[b] = base_len + total;
     if (n_tok) n_tok[b] = total;
     if (mark_tok) mark_tok[b] = base_len + before_mark;
+  }
+}
+
+// ---- the word pass of the two-pass form: one wave per row over the pre-token list the
+// pre-tokenizer pass wrote, 64 pre-tokens per trip, one per lane: an added token's id (or an
+// expansion's ids), a byte's id, or the word cache's ids, all loads of a trip issued together;
+// the misses merged lane by lane in a per-wave scratch (kScr symbols for the trip's misses
+// together), the trip's counts scanned into the row's offsets and its ids stored.  LDS: the row's
+// text (keys, merges), the scratch and the expansion tables -- a few KB, so the pass runs at full
+// occupancy.  A row whose trip needs more scratch is flagged for the one-kernel pass.
+constexpr int kScr = 256;
+__host__ __device__ constexpr size_t words_lds(int stride, int ne, int nei) {
+  return (size_t)stride + 16 + 4 * (size_t)kScr + 2 * (size_t)kScr +
+         (staged_exp(ne, nei) ? 4 * (size_t)(ne + 1) + 4 * (size_t)nei : 0);
+}
+
+__global__ __launch_bounds__(64) void bpe_words_kernel(rmi_bpe_t tok, const uint8_t* __restrict__ text, int64_t pitch,
+                                                       int stride, const int32_t* __restrict__ text_len,
+                                                       int64_t* __restrict__ out, int64_t out_stride,
+                                                       int32_t* __restrict__ out_len, int32_t* __restrict__ n_tok,
+                                                       const int32_t* __restrict__ mark_byte,
+                                                       int32_t* __restrict__ mark_tok, uint8_t* __restrict__ err) {
+  extern __shared__ __align__(16) uint8_t smem[];
+  const int lane = threadIdx.x;
+  const int64_t b = blockIdx.x;
+  const int S = stride;
+  uint8_t* T = smem;                                                  // S + 16 (4-aligned: S % 4 == 0)
+  int32_t* Ys = reinterpret_cast<int32_t*>(smem + S + 16);            // [kScr] symbol ids of the trip's misses
+  int32_t* EOl = Ys + kScr;                                            // [n_exp + 1], [n_exp_ids] (staged)
+  int32_t* EIl = EOl + (tok.n_exp + 1);
+  const bool exp_lds = staged_exp(tok.n_exp, tok.n_exp_ids);
+  uint16_t* Ms = reinterpret_cast<uint16_t*>(exp_lds ? EIl + tok.n_exp_ids : EOl);  // [kScr] their chain
+  const int32_t* EO = exp_lds ? EOl : tok.exp_off;
+  const int32_t* EI = exp_lds ? EIl : tok.exp_ids;
+  // one batch of loads: the row's state, its first 128 pre-token entries and first 1 KB of text
+  // (none depends on another: entries past the row's count and bytes past its length are masked)
+  const uint32_t* pe = tok.pre + b * (int64_t)S;
+  const int32_t* gid = tok.pre_gid + b * (int64_t)S;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(text + b * pitch);
+  const int readable = (S < pitch ? S : (int)pitch) / 4;
+  constexpr int kPre = 4;
+  uint32_t tpre[kPre];
+#pragma unroll
+  for (int i = 0; i < kPre; ++i) tpre[i] = lane + 64 * i < readable ? src[lane + 64 * i] : 0u;
+  uint32_t ent0 = lane < S ? pe[lane] : 0u, ent1 = lane + 64 < S ? pe[lane + 64] : 0u;
+  const uint8_t row_err = err[b];
+  const int n = text_len[b], np = tok.pre_np[b];
+  const int base_len = out_len ? out_len[b] : 0;
+  const int mk = mark_byte ? mark_byte[b] : -1;
+  if (row_err != 0) return;  // the pre-tokenizer pass failed the row (its outputs are written)
+  const auto tail_mask = [n](int w, uint32_t v) {
+    if (4 * w >= n) return 0u;
+    return 4 * w + 4 > n ? v & (0xFFFFFFFFu >> (8 * (4 * w + 4 - n))) : v;
+  };
+#pragma unroll
+  for (int i = 0; i < kPre; ++i) {
+    const int w = lane + 64 * i;
+    if (w < (n + 3) / 4 + 4) reinterpret_cast<uint32_t*>(T)[w] = tail_mask(w, tpre[i]);
+  }
+  for (int w = lane + 64 * kPre; w < (n + 3) / 4 + 4; w += 64)
+    reinterpret_cast<uint32_t*>(T)[w] = tail_mask(w, 4 * w < n ? src[w] : 0u);
+  if (exp_lds) {
+    for (int i = lane; i <= tok.n_exp; i += 64) EOl[i] = tok.exp_off[i];
+    for (int i = lane; i < tok.n_exp_ids; i += 64) EIl[i] = tok.exp_ids[i];
+  }
+  wave_sync();
+  int64_t* orow = out + b * out_stride + base_len;
+  int total = 0, before_mark = 0;
+  bool retry = false, over = false;
+  struct Q {
+    int j, a, len, kind;  // kind: 0 none, 1 added token, 2 one byte, 3 word cache, 4 merge
+    uint32_t k[4];
+    uint32_t h;
+    uint4 w[4];
+    int32_t bid, aid;
+  };
+  // every load of a pre-token (the byte id, the added id, the word-cache entry), issued for two
+  // pre-tokens per lane before either is waited on
+  const auto issue = [&](int j, uint32_t ent, Q& q) {
+    const bool act = j < np;
+    q.j = j;
+    q.a = (int)(ent & 0xFFFu);
+    q.len = (int)((ent >> 12) & 0xFFFu);
+    q.kind = !act ? 0 : ((ent >> 24) & 1u) ? 1 : q.len == 1 ? 2 : (tok.word_cache && q.len <= kWcWordMax) ? 3 : 4;
+    q.bid = tok.byte_id[q.kind == 2 ? T[q.a] : 0];
+    q.aid = gid[q.kind == 1 ? q.a : 0];
+    q.k[0] = q.k[1] = q.k[2] = q.k[3] = 0u;
+    q.h = 0;
+    if (tok.word_cache) {
+      if (q.kind == 3) {
+        wc_key(T, q.a, q.len, q.k);
+        q.h = wc_slot(q.k, q.len, tok.word_cache_mask);
+      }
+      wc_load(tok, q.h, q.w);
+    }
+  };
+  // one trip of 64 pre-tokens (every lane together): ids, the misses merged in the scratch, the
+  // counts scanned into the row's offsets, the ids stored; false: the row goes to the retry pass
+  const auto finish = [&](Q& q) -> bool {
+    const bool act = q.kind != 0;
+    const int a = q.a, len = q.len;
+    int cnt = 0;
+    int32_t ids[kWcIdsMax];
+    bool miss = q.kind == 4;
+    if (q.kind == 1) {
+      cnt = q.aid < 0 ? EO[-q.aid] - EO[-q.aid - 1] : 1;
+    } else if (q.kind == 2) {
+      cnt = 1;
+    } else if (q.kind == 3) {
+      bool empty;
+      cnt = wc_take(q.w, q.k, len, ids, empty);
+      if (!cnt && !empty) cnt = wc_find_from(tok, q.k, len, ids, (q.h + 1) & tok.word_cache_mask, 1);
+      miss = cnt == 0;
+    }
+    const int need = miss ? len : 0;
+    const int need_incl = wave_inclusive_scan(need);
+    if (__builtin_amdgcn_readlane(need_incl, 63) > kScr) return false;
+    const int off = need_incl - need;
+    if (miss) {
+      for (int i = 0; i < len; ++i) {
+        Ys[off + i] = tok.byte_id[T[a + i]];  // 1 KB, cache resident (a word-cache miss only)
+        Ms[off + i] = i + 1 < len ? (uint16_t)(off + i + 1) : kEnd;
+      }
+      cnt = merge_word(tok, Ys, Ms, off);
+      if (q.kind == 3 && cnt <= kWcIdsMax) wc_insert(tok, q.k, len, Ys, Ms, off, cnt);
+    }
+    const int incl = wave_inclusive_scan(cnt);
+    const int trip = __builtin_amdgcn_readlane(incl, 63);
+    const int pre_sum = wave_inclusive_scan(act && a < mk ? cnt : 0);
+    before_mark += __builtin_amdgcn_readlane(pre_sum, 63);
+    if (base_len + total + trip > out_stride) {
+      over = true;
+      return true;
+    }
+    int o = total + incl - cnt;
+    // expansions: the wave copies each one's ids together (a lane's own copy loop waited on an
+    // LDS read per id, tens of ids per expansion)
+    const bool is_exp = q.kind == 1 && q.aid < 0;
+    for (uint64_t em = __ballot(is_exp); em; em &= em - 1) {
+      const int src_l = __builtin_ctzll(em);
+      const int e = -__builtin_amdgcn_readlane(q.aid, src_l) - 1, eo = __builtin_amdgcn_readlane(o, src_l);
+      const int e0 = EO[e], ec = EO[e + 1] - e0;
+      for (int i = lane; i < ec; i += 64) orow[eo + i] = (int64_t)EI[e0 + i];
+    }
+    if (q.kind == 1) {
+      if (q.aid >= 0) orow[o] = (int64_t)q.aid;
+    } else if (q.kind == 2) {
+      orow[o] = (int64_t)q.bid;
+    } else if (miss) {
+      for (int i = off; i != kEnd; i = Ms[i]) orow[o++] = (int64_t)Ys[i];
+    } else if (q.kind == 3) {
+#pragma unroll
+      for (int i = 0; i < kWcIdsMax; ++i)
+        if (i < cnt) orow[o + i] = (int64_t)ids[i];
+    }
+    total += trip;
+    wave_sync();  // (the scratch is the next trip's)
+    return true;
+  };
+  for (int j0 = 0; j0 < np && !retry && !over; j0 += 128) {
+    if (j0) {  // entries past the first 128
+      ent0 = j0 + lane < np ? pe[j0 + lane] : 0u;
+      ent1 = j0 + 64 + lane < np ? pe[j0 + 64 + lane] : 0u;
+    }
+    if (j0 + lane >= np) ent0 = 0u;
+    if (j0 + 64 + lane >= np) ent1 = 0u;
+    Q q0, q1;
+    issue(j0 + lane, ent0, q0);
+    issue(j0 + 64 + lane, ent1, q1);
+    retry = !finish(q0);
+    if (!retry && !over && j0 + 64 < np) retry = !finish(q1);
+  }
+  if (retry) {  // the one-kernel pass takes the row (its outputs from out_len[b] on, as here)
+    if (lane == 0) tok.pre_retry[b] = 1;
+    return;
+  }
+  if (lane == 0) {
+    if (over) {
+      err[b] = RMI_ERR_UNSUP;
+      if (n_tok) n_tok[b] = 0;
+      if (mark_tok) mark_tok[b] = base_len;
+    } else {
+      if (out_len) out_len[b] = base_len + total;
+      if (n_tok) n_tok[b] = total;
+      if (mark_tok) mark_tok[b] = base_len + before_mark;
+    }
   }
 }
 
@@ -901,10 +1130,23 @@ RMI_API int rmi_bpe_encode(const rmi_bpe_t* tok, const uint8_t* text, int64_t pi
       tok->n_exp > 64 || (tok->n_exp > 0 && (!tok->exp_off || !tok->exp_ids)))
     return RMI_EINVAL;
   if (tok->n_exp_ids < 0) return RMI_EINVAL;
-  const size_t lds = bpe_lds(stride, staged_added(tok->n_added), staged_words(tok->n_added, tok->n_exp), tok->n_exp,
-                             tok->n_exp_ids);
-  hipLaunchKernelGGL(bpe_encode_kernel, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text, pitch,
-                     (int)stride,
-                     text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);
+  const int na = staged_added(tok->n_added), nw = staged_words(tok->n_added, tok->n_exp);
+  const size_t lds = bpe_lds(stride, na, nw, tok->n_exp, tok->n_exp_ids);
+  const bool two_pass = tok->pre && tok->pre_gid && tok->pre_np && tok->pre_retry && tok->pre_cap >= B * (int64_t)stride &&
+                        tok->pretok == RMI_PRETOK_QWEN2;
+  if (!two_pass) {
+    hipLaunchKernelGGL(bpe_encode_kernel<kModeFull>, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text,
+                       pitch, (int)stride, text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);
+    return launch_status();
+  }
+  // the pre-tokenizer pass, the word pass, the one-kernel pass over the rows the word pass flagged
+  hipLaunchKernelGGL(bpe_encode_kernel<kModePretok>, dim3((unsigned)B), dim3(64),
+                     bpe_lds(stride, na, nw, tok->n_exp, tok->n_exp_ids, kModePretok), as_stream(stream), *tok, text,
+                     pitch, (int)stride, text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);
+  hipLaunchKernelGGL(bpe_words_kernel, dim3((unsigned)B), dim3(64), words_lds(stride, tok->n_exp, tok->n_exp_ids),
+                     as_stream(stream), *tok, text, pitch, (int)stride, text_len, out, out_stride, out_len, n_tok,
+                     mark_byte, mark_tok, err);
+  hipLaunchKernelGGL(bpe_encode_kernel<kModeRetry>, dim3((unsigned)B), dim3(64), lds, as_stream(stream), *tok, text,
+                     pitch, (int)stride, text_len, out, out_stride, out_len, n_tok, mark_byte, mark_tok, err);
   return launch_status();
 }

@@ -58,6 +58,15 @@ def _storage_uses(t: torch.Tensor) -> int:
     """References to t's storage (t itself and a temporary count 2: no view of it is alive)."""
     f = getattr(torch._C, "_storage_Use_Count", None)
     return f(t.untyped_storage()._cdata) if f is not None else 1 << 30
+
+
+_USE_COUNT = getattr(torch._C, "_storage_Use_Count", None)
+
+
+def _uses(st) -> int:
+    """References to a held storage object's storage (its tensor and the object itself count
+    2: no view of it is alive)."""
+    return _USE_COUNT(st._cdata) if _USE_COUNT is not None else 1 << 30
 _P = ("@@RMI_S@@", "@@RMI_U1@@", "@@RMI_A1@@", "@@RMI_U2@@", "@@RMI_A2@@")
 
 
@@ -849,16 +858,20 @@ class DevicePrompts:
         1.25 S (the turn chain pads the next rollout's batch of this turn number into it: its row
         count varies with the envs done, its width a little with the rooms).  n=None: the free
         block as it is, or None when there is none (TurnChain.run)."""
-        buf, err = self._batch_bufs.get(slot, (None, None))
+        # (each block kept with its storage object: the use count of a held storage is the
+        # block, that object and any view; untyped_storage() per check cost ~2 us)
+        buf, err, bst, est = self._batch_bufs.get(slot, (None, None, None, None))
         if n is None:
-            if buf is None or _storage_uses(buf) > 2 or _storage_uses(err) > 2:
+            if buf is None or _uses(bst) > 2 or _uses(est) > 2:
                 return None
             return buf, err
-        if buf is None or buf.numel() < 3 * n * S or _storage_uses(buf) > 2:
+        if buf is None or buf.numel() < 3 * n * S or _uses(bst) > 2:
             buf = torch.empty(max(3 * max(n, self.n_envs) * (S + S // 4), 1), dtype=torch.int64, device=self.device)
-        if err is None or _storage_uses(err) > 2:
+            bst = buf.untyped_storage()
+        if err is None or _uses(est) > 2:
             err = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
-        self._batch_bufs[slot] = (buf, err)
+            est = err.untyped_storage()
+        self._batch_bufs[slot] = (buf, err, bst, est)
         return buf, err
 
     def _pad_rows(self, rows, S):

@@ -140,12 +140,16 @@ class TurnChain:
                              int(v.data.numel()), int(v.packed.shape[0]))
         return st
 
-    def _bpe(self):
-        """The tokenizer's current rmi_bpe_t (rebuilt when an expansion grew its tables)."""
+    two_pass_bpe = True  # (tests compare the two-pass BPE with the one-kernel form)
+
+    def _bpe(self, stride):
+        """The tokenizer's current rmi_bpe_t (rebuilt when an expansion grew its tables or the
+        two-pass scratch grew: rows x the BPE row bound)."""
         dt = self.pr.dt
+        grew = self.two_pass_bpe and dt.ensure_two_pass(self.n, stride)
         b = self.__dict__.get("_bpe_c")
-        if b is None or b[0] is not dt.added_bytes:
-            b = self._bpe_c = (dt.added_bytes, dt.bpe_struct())
+        if b is None or b[0] is not dt.added_bytes or grew or b[2] is not dt.pre or b[3] != self.two_pass_bpe:
+            b = self._bpe_c = (dt.added_bytes, dt.bpe_struct(self.two_pass_bpe), dt.pre, self.two_pass_bpe)
         return ctypes.addressof(b[1])
 
     def _plan(self, s, t, stride, resp_max, obs_max):
@@ -232,7 +236,7 @@ class TurnChain:
         c.raw_max, c.raw_next = inp.raw_dev.data_ptr(), inp.raw_next.data_ptr() if inp.raw_next is not None else None
         c.text, c.stride = s.text.data_ptr(), stride
         c.prompt, c.ptext, c.pstride = P, s.ptext.data_ptr(), pstride
-        c.bpe, c.bpe_stride = self._bpe(), bpe_stride
+        c.bpe, c.bpe_stride = self._bpe(bpe_stride), bpe_stride
         c.arena, c.arena_stride = pr.arena_p, pr.arena_stride
         c.arena_len, c.len_upd = pr.len_p, pr.len_upd_p
         pack = inp.pack

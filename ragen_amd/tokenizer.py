@@ -167,7 +167,8 @@ class Bpe(ctypes.Structure):
                 ("added_first", ctypes.c_uint32 * 8), ("word_cache", ctypes.c_void_p),
                 ("word_cache_mask", ctypes.c_uint32), ("n_exp", ctypes.c_int32), ("exp_off", ctypes.c_void_p),
                 ("exp_ids", ctypes.c_void_p), ("added_words", ctypes.c_void_p), ("ascii_class", ctypes.c_void_p),
-                ("n_exp_ids", ctypes.c_int32)]
+                ("n_exp_ids", ctypes.c_int32), ("pre", ctypes.c_void_p), ("pre_gid", ctypes.c_void_p),
+                ("pre_np", ctypes.c_void_p), ("pre_retry", ctypes.c_void_p), ("pre_cap", ctypes.c_int64)]
 
 
 def _backend_json(tokenizer) -> dict:
@@ -262,6 +263,8 @@ class DeviceTokenizer:
     # staging tables (rmi_bpe_t.added_words / ascii_class; _build_staging)
     added_words: Optional[torch.Tensor] = None
     ascii_class: Optional[torch.Tensor] = None
+    # the two-pass form's scratch (rmi_bpe_t.pre*; ensure_two_pass): None = one kernel per call
+    pre: Optional[tuple] = None
 
     MAX_EXPANSIONS = 64
 
@@ -401,12 +404,45 @@ class DeviceTokenizer:
                 self.added_id, [self.merge_mask, self.merge_shift, self.pretok, self.nfc, self.n_added]
                 + list(self.added_first))
 
-    def bpe_struct(self):
+    def bpe_struct(self, two_pass: bool = True):
         """The validated rmi_bpe_t of the current tables (expansions included), built once per
-        set of tables (torch_ops._bpe_struct): what rmi_bpe_encode / rmi_turn_chain take."""
+        set of tables (torch_ops._bpe_struct): what rmi_bpe_encode / rmi_turn_chain take; with
+        the two-pass scratch when it is allocated (ensure_two_pass) and ``two_pass``."""
         from .torch_ops import _bpe_struct
         return _bpe_struct(*self.args(), self.word_cache, self.exp_off if self.exp else None,
-                           self.exp_ids if self.exp else None, self.added_words, self.ascii_class)
+                           self.exp_ids if self.exp else None, self.added_words, self.ascii_class,
+                           self.pre if two_pass else None)
+
+    def ensure_two_pass(self, rows: int, stride: int) -> bool:
+        """Scratch for the two-pass form of rmi_bpe_encode over ``rows`` rows of at most
+        ``stride`` bytes (pre-token lists and added ids: 8 B per row byte), grown when too small.
+        -> whether it was (re)allocated (a cached rmi_bpe_t must be rebuilt)."""
+        need = int(rows) * int(stride)
+        if self.pre is not None and self.pre[0].numel() >= need:
+            return False
+        cap = max(need, 1)
+        dev = self.byte_id.device
+        # (the per-row arrays hold cap / 4 entries: every call the C side accepts has rows <= cap / 4)
+        self.pre = (torch.empty(cap, dtype=torch.int32, device=dev), torch.empty(cap, dtype=torch.int32, device=dev),
+                    torch.empty(max(cap // 4, 1), dtype=torch.int32, device=dev),
+                    torch.empty(max(cap // 4, 1), dtype=torch.uint8, device=dev))
+        return True
+
+    def encode_two_pass(self, text: torch.Tensor, text_len: torch.Tensor, out: torch.Tensor, stride: int):
+        """rmi_bpe_encode in its two-pass form (ensure_two_pass's scratch) over every row of
+        ``text`` (u8 [rows, pitch], rows of at most ``stride`` bytes): -> (n_tok, err)."""
+        import ctypes
+        from . import _lib, ops
+        B = int(text.shape[0])
+        self.ensure_two_pass(B, stride)
+        st = self.bpe_struct(True)
+        n_tok = torch.empty(B, dtype=torch.int32, device=text.device)
+        err = torch.empty(B, dtype=torch.uint8, device=text.device)
+        ops.check(_lib.lib().rmi_bpe_encode(ctypes.addressof(st), text.data_ptr(), int(text.shape[1]), int(stride),
+                                            text_len.data_ptr(), B, out.data_ptr(), int(out.shape[1]), None,
+                                            n_tok.data_ptr(), None, None, err.data_ptr(), ops._stream(text.device)),
+                  "rmi_bpe_encode")
+        return n_tok, err
 
     def encode_rows(self, text: torch.Tensor, text_len: torch.Tensor, out: torch.Tensor,
                     out_len: Optional[torch.Tensor] = None, mark_byte: Optional[torch.Tensor] = None,
@@ -418,8 +454,9 @@ class DeviceTokenizer:
                                  self.word_cache, self.exp_off if self.exp else None,
                                  self.exp_ids if self.exp else None, self.added_words, self.ascii_class)
 
-    def encode(self, texts: Sequence[str], stride: int = None) -> List[Optional[List[int]]]:
-        """Convenience (tests, tools): ids of each text, or None for a row the device flagged."""
+    def encode(self, texts: Sequence[str], stride: int = None, two_pass: bool = False) -> List[Optional[List[int]]]:
+        """Convenience (tests, tools): ids of each text, or None for a row the device flagged.
+        two_pass: through the two-pass form of rmi_bpe_encode (the turn chain's)."""
         dev = self.byte_id.device
         rows = [t.encode("utf-8") for t in texts]
         stride = stride or max(4, (max((len(r) for r in rows), default=0) + 3) // 4 * 4)
@@ -428,7 +465,10 @@ class DeviceTokenizer:
             buf[i, :len(r)] = np.frombuffer(r, np.uint8)
         lens = torch.tensor([len(r) for r in rows], dtype=torch.int32, device=dev)
         out = torch.zeros(len(rows), max(stride, 1), dtype=torch.int64, device=dev)
-        n_tok, _, err = self.encode_rows(torch.from_numpy(buf).to(dev), lens, out)
+        if two_pass:
+            n_tok, err = self.encode_two_pass(torch.from_numpy(buf).to(dev), lens, out, stride)
+        else:
+            n_tok, _, err = self.encode_rows(torch.from_numpy(buf).to(dev), lens, out)
         n_tok, err, out = n_tok.cpu().tolist(), err.cpu().tolist(), out.cpu().numpy()
         return [None if e else out[i, :n].tolist() for i, (n, e) in enumerate(zip(n_tok, err))]
 

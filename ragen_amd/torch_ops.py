@@ -812,7 +812,7 @@ def _bpe_struct(*args):
 
 
 def _bpe_struct_build(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id, params, word_cache=None,
-                      exp_off=None, exp_ids=None, added_words=None, ascii_class=None):
+                      exp_off=None, exp_ids=None, added_words=None, ascii_class=None, pre=None):
     from .tokenizer import Bpe
     ops._dev(cp_block, cp_class, byte_id, merges, added_bytes, added_off, added_id)
     if len(params) != 13:
@@ -846,6 +846,13 @@ def _bpe_struct_build(cp_block, cp_class, byte_id, merges, added_bytes, added_of
         if ascii_class.numel() != 128:
             raise ValueError("ascii_class: 128 classes")
         s.ascii_class = ascii_class.data_ptr()
+    if pre is not None:  # the two-pass scratch: (pre, pre_gid, pre_np, pre_retry)
+        p_, g_, n_, r_ = pre
+        ops._dev(p_, g_, n_, r_)
+        if p_.numel() != g_.numel() or n_.numel() != r_.numel() or n_.numel() < p_.numel() // 4:
+            raise ValueError("pre / pre_gid: pre_cap entries each, pre_np / pre_retry: pre_cap / 4")
+        s.pre, s.pre_gid, s.pre_np, s.pre_retry = p_.data_ptr(), g_.data_ptr(), n_.data_ptr(), r_.data_ptr()
+        s.pre_cap = p_.numel() if n_.numel() else 0
     return s
 
 

@@ -66,3 +66,18 @@ def test_freed_without_the_cyclic_gc():
         assert w() is None
     finally:
         gc.enable()
+
+
+def test_block_use_count_with_a_held_storage():
+    """DevicePrompts.batch_block's reuse check: a block and its held storage object count 2;
+    any live view of it (the batch's unbound rows, a slice of them) raises the count."""
+    from ragen_amd.llm_agent.prompts import _uses
+    t = torch.empty(12, dtype=torch.int64)
+    st = t.untyped_storage()
+    assert _uses(st) == 2
+    a, b, c = t[:9].view(3, 3).unbind(0)
+    r = a[1:]
+    del a, b, c
+    assert _uses(st) > 2  # the slice still holds the block
+    del r
+    assert _uses(st) == 2

@@ -35,21 +35,21 @@ L = _lib.lib()
 stream = ops._stream(dev)
 
 
-def launch(stride):
+def launch(stride, st=None):
     out_len.zero_()
-    ops.check(L.rmi_bpe_encode(ctypes.addressof(tok), text.data_ptr(), int(text.shape[1]), int(stride),
+    ops.check(L.rmi_bpe_encode(ctypes.addressof(st or tok), text.data_ptr(), int(text.shape[1]), int(stride),
                                tlen.data_ptr(), n, out.data_ptr(), 2048, out_len.data_ptr(), None,
                                s.pmark.data_ptr(), mark_tok.data_ptr(), err.data_ptr(), stream), "rmi_bpe_encode")
 
 
-def timed(stride, reps=20):
-    launch(stride)
+def timed(stride, reps=20, st=None):
+    launch(stride, st)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda._sleep(1_000_000)
     e0.record()
     for _ in range(reps):
-        launch(stride)
+        launch(stride, st)
     e1.record()
     torch.cuda.synchronize()
     # (each launch also zeroes out_len: a 32 KB fill, ~2 us)
@@ -79,6 +79,14 @@ for st in strides:
     ok = int((err == 0).sum())
     same = bool(torch.equal(out_len[err == 0], ref[1][err == 0]))
     res["us_at_stride"][st] = {"us": us, "rows_encoded": ok, "same_lengths": same}
+# the one-kernel form at the bound (the struct without the two-pass scratch), same outputs
+one = pr.dt.bpe_struct(False)
+res["two_pass"] = tok.pre is not None and tok.pre_cap > 0
+res["us_one_kernel_at_bound"] = timed(bound, st=one)
+launch(bound, one)
+torch.cuda.synchronize()
+res["one_kernel_same_ids"] = bool(torch.equal(out_len, ref[1]) and torch.equal(err, ref[2]) and all(
+    torch.equal(out[i, :int(ref[1][i])], ref[0][i, :int(ref[1][i])]) for i in range(0, n, 97)))
 # the word cache cold (cleared) for one launch at the bound
 if pr.dt.word_cache is not None:
     wc = pr.dt.word_cache

@@ -1,0 +1,5 @@
+set -u
+cd "${GRAFT_REPO_ROOT}"
+bash tools/r05_check.sh r05t "tests/test_gpu_bpe_two_pass.py tests/test_gpu_turn_chain.py tests/test_gpu_tokenizer.py tests/test_gpu_device_prompts.py" || exit $?
+grep -n "bpe" gpurun_out/r05t/api_timeline.txt | head -12
+timeout -k 10 300 python tools/bench_bpe.py > gpurun_out/r05t/bench_bpe.txt 2>&1 || exit $?; tail -1 gpurun_out/r05t/bench_bpe.txt
