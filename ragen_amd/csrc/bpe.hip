@@ -906,9 +906,14 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
       for (int i = lane; i < ec; i += 64) orow[eo + i] = (int64_t)EI[e0 + i];
     }
     if (j >= np || is_exp) continue;
-    if (kj & kKHit) {  // a word-cache hit: its ids at Y[a ..), the count up to the next offset
-      const int o1 = j + 1 < np ? (L.K[j + 1] & ~kKHit) : total;
-      for (int q = a; o < o1; ++q) orow[o++] = (int64_t)L.Y[q];
+    if (kj & kKHit) {  // a word-cache hit (<= kWcIdsMax ids at Y[a ..)): every read, then every store
+      const int c = (j + 1 < np ? (L.K[j + 1] & ~kKHit) : total) - o;
+      int32_t v[kWcIdsMax];
+#pragma unroll
+      for (int i = 0; i < kWcIdsMax; ++i) v[i] = i < c ? L.Y[a + i] : 0;
+#pragma unroll
+      for (int i = 0; i < kWcIdsMax; ++i)
+        if (i < c) orow[o + i] = (int64_t)v[i];
       continue;
     }
     for (int q = a; q != kEnd; q = L.M[q]) orow[o++] = (int64_t)L.Y[q];

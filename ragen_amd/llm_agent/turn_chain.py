@@ -140,7 +140,9 @@ class TurnChain:
                              int(v.data.numel()), int(v.packed.shape[0]))
         return st
 
-    two_pass_bpe = True  # (tests compare the two-pass BPE with the one-kernel form)
+    # the two-pass form of rmi_bpe_encode measured no faster than the one-kernel form on the
+    # API turn's text (78 vs 75 us): off by default, kept as a tested option
+    two_pass_bpe = False
 
     def _bpe(self, stride):
         """The tokenizer's current rmi_bpe_t (rebuilt when an expansion grew its tables or the

@@ -54,3 +54,25 @@ def test_two_pass_flags_like_one_kernel(device, qwen_tok):
     dt = DeviceTokenizer.from_hf(qwen_tok, device)
     rows = nfc_unsafe() + ["plain text", "x" * 50]
     assert dt.encode(rows, two_pass=True) == dt.encode(rows)
+
+
+def test_turn_chain_with_the_two_pass_bpe(device, qwen_tok, monkeypatch):
+    """The turn chain with its BPE launch in the two-pass form == the step-by-step rollout (the
+    one-kernel form) on a golden-trace config: every generation batch and the formulated batch."""
+    from ragen_amd.env import SokobanBatch
+    from ragen_amd.llm_agent.turn_chain import TurnChain
+    from test_gpu_device_prompts import _ids, _responses
+    from test_gpu_facade import TRACES, _config, _hashseed0_reseed
+    from test_gpu_turn_chain import _run, _same
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    monkeypatch.setattr(TurnChain, "two_pass_bpe", True)
+    name = "sokoban_es"
+    cfg = _config(name)
+    _, ng, gs, T, _ = TRACES[name]
+    turn_tokens = [_ids(qwen_tok, _responses(name, t, ng * gs), device) for t in range(T)]
+    chained, runs, proxy = _run(cfg, qwen_tok, turn_tokens, device, True, reps=2)
+    plain, _, _ = _run(cfg, qwen_tok, turn_tokens, device, False, reps=2)
+    assert runs == sum(len(o[1]) for o in chained)
+    assert proxy.train_ctx_manager.prompts().dt.pre is not None  # the chain took the two-pass form
+    for a, b in zip(chained, plain):
+        _same(a, b)

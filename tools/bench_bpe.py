@@ -25,7 +25,8 @@ n = es.n_envs
 text, tlen = s.ptext, s.ptext_len
 bound = s.prompt[3]
 longest = int(tlen.max())
-tok = pr.dt.bpe_struct()
+pr.dt.ensure_two_pass(es.n_envs, 3072)  # (both forms timed below)
+tok = pr.dt.bpe_struct(True)
 dev = text.device
 out = torch.zeros(n, 2048, dtype=torch.int64, device=dev)
 out_len = torch.zeros(n, dtype=torch.int32, device=dev)
