@@ -8,8 +8,10 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r05check}; mkdir -p $OUT
 TESTS=${2:-tests}
 step() { echo "[$1] rc=$2" | tee -a $OUT/status.txt; if [ "$2" -ne 0 ]; then exit "$2"; fi; }
-timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; step pytest $?
-tail -3 $OUT/pytest_gpu.log
+if [ "${SKIP_PYTEST:-0}" = "0" ]; then
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1; step pytest $?
+  tail -3 $OUT/pytest_gpu.log
+fi
 if [ "${SKIP_API:-0}" = "0" ]; then
   timeout -k 10 300 python tools/api_leg.py > $OUT/api.json 2> $OUT/api.err; step api $?
   python -c "import json;d=json.load(open('$OUT/api.json'))['device_path'];print({k:d[k] for k in ('env_steps_per_s','turn_loop_s','formulate_rollouts_s','reset_s','readbacks')})"
