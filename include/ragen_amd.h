@@ -665,6 +665,12 @@ typedef struct {
   const uint8_t* flags;      /* [B] episode flags after the turn                                */
   uint32_t int_reward_tags;  /* bit t: tag t's 0 / 1 rewards print as ints (tags < 32)          */
   int32_t last_turn;
+  /* Reward text cache (NULL: off): (num_cache_mask + 1) entries of 16 u32, zero-initialised and
+   * kept across calls — a reward's float bits -> its CPython repr (<= 24 bytes), with a 64-bit
+   * check of the entry (a torn or foreign entry is a miss).  A turn's rewards take a handful of
+   * values; a hit replaces the row's shortest-repr search on one lane.                       */
+  uint32_t* num_cache;
+  uint32_t num_cache_mask;  /* entries - 1 (a power of two minus one)                          */
 } rmi_prompt_t;
 int rmi_prompt_text(const rmi_prompt_t* prog, int64_t B, uint8_t* out, int32_t stride, int32_t* out_len,
                     int32_t* mark, uint8_t* err, rmi_stream_t stream);

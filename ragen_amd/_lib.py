@@ -95,7 +95,8 @@ class Prompt(ctypes.Structure):
                 ("spans", c_void_p), ("enable_think", c_int32), ("K", c_int32), ("sep_len", c_int32),
                 ("sep", ctypes.c_uint8 * 16), ("cond", c_void_p), ("active", c_void_p),
                 ("pool_len", c_int32), ("turn_exec", c_void_p), ("flags", c_void_p),
-                ("int_reward_tags", ctypes.c_uint32), ("last_turn", c_int32)]
+                ("int_reward_tags", ctypes.c_uint32), ("last_turn", c_int32), ("num_cache", c_void_p),
+                ("num_cache_mask", ctypes.c_uint32)]
 
 
 class TurnChain(ctypes.Structure):

@@ -300,6 +300,8 @@ class DevicePrompts:
         self.len_p, self.len_upd_p = self.len.data_ptr(), self.len_upd.data_ptr()
         self._all_idx = np.arange(n, dtype=np.int64)
         self._all_rows = torch.arange(n, dtype=torch.int64, device=self.device)
+        # the reward text cache of the chained prompt launches (rmi_prompt_t.num_cache): 64 KB
+        self.num_cache = torch.zeros(1024 * 16, dtype=torch.int32, device=self.device)
         tail = self.dt.encode([self.tpl.gen + self.prefix])[0]
         if tail is None or tail != self._host_ids(self.tpl.gen + self.prefix):
             raise NotImplementedError("the generation prompt does not encode like the host tokenizer")

@@ -179,6 +179,7 @@ class TurnChain:
         P = prompt_struct(flat, pr.sep, (pool, tc, pr.tag, rows, obs_len, s.left, reward, None, s.text, s.tlen,
                                          s.spans, None, s.has),
                           (ne, s.flags_copy, pr.int_reward_tags, int(last)))
+        P.num_cache, P.num_cache_mask = pr.num_cache.data_ptr(), pr.num_cache.numel() // 16 - 1  # (held by pr)
         mx = min(int(bound), pstride)
         # (the tensors behind the struct's pointers are held with it)
         s.prompt = (key, ctypes.addressof(P), pstride, max((mx + 3) // 4 * 4, 4), last, (P, reward, ne, pool, tc))

@@ -112,3 +112,33 @@ def test_turn_chain_bench_workload(device):
     assert proxy.train_ctx_manager.prompts().chain_padded == len(chained[1][1]) - 1
     for a, b in zip(chained, plain):
         _same(a, b)
+
+
+def test_reward_text_cache_refuses_torn_entries(device, qwen_tok, monkeypatch):
+    """The chained prompt launches' reward text cache (rmi_prompt_t.num_cache): a second rollout
+    after every cached entry's text was altered (its check not) prints the same prompts as the
+    step-by-step path: an entry whose contents do not match its check is recomputed, not used."""
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    name = "sokoban_es"
+    cfg = _config(name)
+    _, ng, gs, T, _ = TRACES[name]
+    turn_tokens = [_ids(qwen_tok, _responses(name, t, ng * gs), device) for t in range(T)]
+    plain, _, _ = _run(cfg, qwen_tok, turn_tokens, device, False, reps=2)
+    actor = TokenActor(turn_tokens, read_prompts=True)
+    proxy = LLMAgentProxy(cfg, actor, qwen_tok, device=device)
+    proxy.train_ctx_manager.set_device_vocab(_vocab(qwen_tok, device))
+    random.seed(7)
+    outs = []
+    for rep in range(2):
+        if rep == 1:
+            nc = proxy.train_ctx_manager.prompts().num_cache.view(-1, 16)
+            ready = nc[:, 2] < 0  # the ready bit
+            assert int(ready.sum()) > 0  # the first rollout cached its rewards' text
+            nc[ready, 3] ^= 0x01010101  # every entry's text changed, its check not
+        actor.prompts = []
+        out = proxy.rollout(DataProto(meta_info={}), val=False)
+        outs.append((out, [tuple(x.cpu() for x in p) for p in actor.prompts], proxy.train_es_manager.rollout_cache,
+                     dict(out.meta_info)))
+    for a, b in zip(outs, plain):
+        _same(a, b)
