@@ -104,6 +104,20 @@ __host__ __device__ constexpr size_t bpe_lds(int stride, int na, int nw, int ne,
          (mode != kModePretok && staged_exp(ne, nei) ? 4 * (size_t)(ne + 1) + 4 * (size_t)nei : 0);
 }
 
+// dst[0, n) = src[0, n) by one wave, 8 loads a lane in flight before the stores (a plain
+// load-store loop waited on each load: one memory round trip per 64 entries)
+__device__ __forceinline__ void stage_i32(int32_t* dst, const int32_t* __restrict__ src, int n, int lane) {
+  constexpr int kU = 8;
+  for (int i0 = 0; i0 < n; i0 += 64 * kU) {
+    int32_t v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) v[u] = i0 + 64 * u + lane < n ? src[i0 + 64 * u + lane] : 0;
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (i0 + 64 * u + lane < n) dst[i0 + 64 * u + lane] = v[u];
+  }
+}
+
 __device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a, uint32_t b) {
   const uint64_t key = ((uint64_t)a << 32) | b;
   uint64_t h = (key * 0x9E3779B97F4A7C15ull) >> t.merge_shift;
@@ -456,9 +470,13 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   if (tok.ascii_class && lane < 32)
     reinterpret_cast<uint32_t*>(L.AC)[lane] = reinterpret_cast<const uint32_t*>(tok.ascii_class)[lane];
   if (exp_lds) {
-    for (int i = lane; i <= tok.n_exp; i += 64) L.EO[i] = tok.exp_off[i];
-    for (int i = lane; i < tok.n_exp_ids; i += 64) L.EI[i] = tok.exp_ids[i];
+    stage_i32(L.EO, tok.exp_off, tok.n_exp + 1, lane);
+    stage_i32(L.EI, tok.exp_ids, tok.n_exp_ids, lane);
   }
+  // an expansion's first two bytes (lane e: expansion e), for the layout check below
+  const int n_plain0 = tok.n_added - tok.n_exp;
+  const uint64_t xw = (words_given && tok.n_exp > 0 && n_plain0 >= 0 && lane < tok.n_exp)
+                          ? tok.added_words[4 * (n_plain0 + lane)] : 0ull;
   const uint32_t blk0 = tok.ascii_class ? 0u : tok.cp_block[0];  // the block of U+0000..U+00FF
   for (int w = lane; w < (n + 128 + 3) / 4; w += 64) reinterpret_cast<uint32_t*>(L.C)[w] = 0u;  // (C is 4-aligned)
   wave_sync();
@@ -487,13 +505,13 @@ __global__ __launch_bounds__(64) void bpe_encode_kernel(rmi_bpe_t tok, const uin
   // (0xFF, 0x80 + e) and id -(e + 1) (tokenizer.py builds them so): phase 2 then matches a 0xFF
   // candidate by its index byte and compares the others with the plain tokens only
   const int n_plain = tok.n_added - tok.n_exp;
-  bool exp_tail = added_words && tok.n_exp > 0 && n_plain >= 0;
-  if (exp_tail) {  // (the expansions' bytes from the table: their words are not staged)
+  bool exp_tail = words_given && added_words && tok.n_exp > 0 && tok.n_exp <= 64 && n_plain >= 0;
+  if (exp_tail) {  // (the expansions' first bytes came with the staging batch: xw, lane e)
     bool ok = true;
-    for (int e = lane; e < tok.n_exp; e += 64) {
-      const int a = n_plain + e;
-      ok &= L.AI[a] == -(e + 1) && L.AO[a + 1] - L.AO[a] == 2 && tok.added_bytes[L.AO[a]] == 0xFFu &&
-            tok.added_bytes[L.AO[a] + 1] == (uint8_t)(0x80u + (uint32_t)e);
+    if (lane < tok.n_exp) {
+      const int e = lane, a = n_plain + e;
+      ok = L.AI[a] == -(e + 1) && L.AO[a + 1] - L.AO[a] == 2 &&
+           (uint32_t)(xw & 0xFFFFu) == (0xFFu | ((0x80u + (uint32_t)e) << 8));
     }
     exp_tail = !__any(!ok);
   }
@@ -985,8 +1003,8 @@ __global__ __launch_bounds__(64) void bpe_words_kernel(rmi_bpe_t tok, const uint
   for (int w = lane + 64 * kPre; w < (n + 3) / 4 + 4; w += 64)
     reinterpret_cast<uint32_t*>(T)[w] = tail_mask(w, 4 * w < n ? src[w] : 0u);
   if (exp_lds) {
-    for (int i = lane; i <= tok.n_exp; i += 64) EOl[i] = tok.exp_off[i];
-    for (int i = lane; i < tok.n_exp_ids; i += 64) EIl[i] = tok.exp_ids[i];
+    stage_i32(EOl, tok.exp_off, tok.n_exp + 1, lane);
+    stage_i32(EIl, tok.exp_ids, tok.n_exp_ids, lane);
   }
   wave_sync();
   int64_t* orow = out + b * out_stride + base_len;
