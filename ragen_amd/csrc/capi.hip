@@ -40,11 +40,65 @@ RMI_API int rmi_upload(void* dst, const void* src, size_t bytes, rmi_stream_t st
                                                                                                    : RMI_EDEVICE;
 }
 
+namespace rmi {
+namespace {
+constexpr int kCopyBlock = 256;
+// 16-B stores (fewer PCIe writes) while both ends are 16-B aligned, then the dword tail
+__global__ __launch_bounds__(kCopyBlock) void readback_kernel(const uint32_t* __restrict__ src, uint32_t* dst,
+                                                              int64_t n32) {
+  const bool v4 = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
+  const int64_t n4 = v4 ? n32 / 4 : 0;
+  const int64_t t = (int64_t)blockIdx.x * kCopyBlock + threadIdx.x, step = (int64_t)gridDim.x * kCopyBlock;
+  for (int64_t i = t; i < n4; i += step)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  for (int64_t i = 4 * n4 + t; i < n32; i += step) dst[i] = src[i];
+}
+
+// the device address of a pinned host buffer, or nullptr: a few recent lookups cached per
+// thread (the turn loop alternates a handful of pinned buffers)
+void* host_mapping(void* host) {
+  constexpr int kSlots = 8;
+  thread_local void* keys[kSlots] = {};
+  thread_local void* vals[kSlots] = {};
+  thread_local int next = 0;
+  for (int i = 0; i < kSlots; ++i)
+    if (keys[i] == host) return vals[i];
+  hipPointerAttribute_t attr;
+  void* dev = nullptr;
+  // (only where the runtime's host address is the one asked about: its device address is then
+  // that byte's, whether or not the runtime offsets interior pointers)
+  if (hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer &&
+      attr.hostPointer == host)
+    dev = attr.devicePointer;
+  else
+    (void)hipGetLastError();  // (clear the lookup's error: pageable memory)
+  keys[next] = host;
+  vals[next] = dev;
+  next = (next + 1) % kSlots;
+  return dev;
+}
+}  // namespace
+
+int readback_async(void* host, const void* dev, size_t bytes, hipStream_t s) {
+  const bool a4 = bytes % 4 == 0 && ((reinterpret_cast<uintptr_t>(host) | reinterpret_cast<uintptr_t>(dev)) & 3u) == 0;
+  void* hdev = a4 ? host_mapping(host) : nullptr;
+  if (!hdev)
+    return hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s) == hipSuccess ? RMI_OK : RMI_EDEVICE;
+  const int64_t n32 = (int64_t)(bytes / 4);
+  int64_t grid = (n32 / 4 + kCopyBlock - 1) / kCopyBlock;  // (one 16-B store a thread)
+  grid = grid < 1 ? 1 : (grid > 1024 ? 1024 : grid);
+  hipLaunchKernelGGL(readback_kernel, dim3((unsigned)grid), dim3(kCopyBlock), 0, s, static_cast<const uint32_t*>(dev),
+                     static_cast<uint32_t*>(hdev), n32);
+  return hipGetLastError() == hipSuccess ? RMI_OK : RMI_EDEVICE;
+}
+}  // namespace rmi
+
 RMI_API int rmi_readback(void* dst, const void* src, size_t bytes, rmi_stream_t stream) {
   if (!bytes) return RMI_OK;
   if (!dst || !src) return RMI_EINVAL;
   hipStream_t s = rmi::as_stream(stream);
-  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, s) != hipSuccess) return RMI_EDEVICE;
+  const int rc = rmi::readback_async(dst, src, bytes, s);
+  if (rc) return rc;
   return hipStreamSynchronize(s) == hipSuccess ? RMI_OK : RMI_EDEVICE;
 }
 

@@ -20,53 +20,6 @@ hipEvent_t copy_event() {
   return ev[dev];
 }
 
-// The readback as a kernel that stores straight into the pinned host buffer (its device
-// mapping), instead of hipMemcpyAsync: on this runtime the async copy started ~11 us after the
-// last kernel of the turn (a blit kernel behind a barrier), every turn on the critical path.
-// Taken only when the runtime reports a device address for the host buffer; otherwise the copy.
-constexpr int kCopyBlock = 256;
-// 16-B stores (fewer PCIe writes) while both ends are 16-B aligned, then the dword tail
-__global__ __launch_bounds__(kCopyBlock) void readback_kernel(const uint32_t* __restrict__ src, uint32_t* dst,
-                                                              int64_t n32) {
-  const bool v4 = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15u) == 0;
-  const int64_t n4 = v4 ? n32 / 4 : 0;
-  const int64_t t = (int64_t)blockIdx.x * kCopyBlock + threadIdx.x, step = (int64_t)gridDim.x * kCopyBlock;
-  for (int64_t i = t; i < n4; i += step)
-    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
-  for (int64_t i = 4 * n4 + t; i < n32; i += step) dst[i] = src[i];
-}
-
-// the device address of a pinned host buffer, or nullptr (the last lookup is cached)
-void* host_mapping(void* host) {
-  static void* last_host = nullptr;
-  static void* last_dev = nullptr;
-  if (host == last_host) return last_dev;
-  hipPointerAttribute_t attr;
-  void* dev = nullptr;
-  if (hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer)
-    dev = attr.devicePointer;
-  else
-    (void)hipGetLastError();  // (clear the lookup's error)
-  last_host = host;
-  last_dev = dev;
-  return dev;
-}
-
-// the pack into host memory, then the event recorded behind it
-int readback_to_host(void* host, const void* pack, int64_t bytes, hipStream_t hs, hipEvent_t ev) {
-  void* hdev = (bytes % 4 == 0) ? host_mapping(host) : nullptr;
-  if (hdev) {
-    const int64_t n32 = bytes / 4;
-    const int grid = (int)((n32 / 4 + kCopyBlock - 1) / kCopyBlock);  // (one 16-B store a thread)
-    hipLaunchKernelGGL(readback_kernel, dim3(grid < 1 ? 1 : grid), dim3(kCopyBlock), 0, hs,
-                       static_cast<const uint32_t*>(pack), static_cast<uint32_t*>(hdev), n32);
-    if (hipGetLastError() != hipSuccess) return RMI_EDEVICE;
-  } else if (hipMemcpyAsync(host, pack, (size_t)bytes, hipMemcpyDeviceToHost, hs) != hipSuccess) {
-    return RMI_EDEVICE;
-  }
-  return hipEventRecord(ev, hs) == hipSuccess ? RMI_OK : RMI_EDEVICE;
-}
-
 }  // namespace
 
 RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
@@ -130,8 +83,9 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
   hipStream_t hs = rmi::as_stream(s);
   hipEvent_t ev = copy_event();
   if (!ev) return RMI_EDEVICE;
-  rc = readback_to_host(c.host, c.pack, c.pack_bytes, hs, ev);
+  rc = rmi::readback_async(c.host, c.pack, (size_t)c.pack_bytes, hs);
   if (rc) return rc;
+  if (hipEventRecord(ev, hs) != hipSuccess) return RMI_EDEVICE;
   rc = rmi_next_rows_list(c.has, c.flags_copy, B, c.next_rows, c.next_src, s);
   if (rc) return rc;
   if (hipEventSynchronize(ev) != hipSuccess) return RMI_EDEVICE;
@@ -169,7 +123,6 @@ RMI_API int rmi_formulate_chain(const rmi_formulate_chain_t* chain, rmi_stream_t
   if (rc) return rc;
   hipStream_t hs = rmi::as_stream(s);
   for (int i = 0; i < c.n_copies; ++i)
-    if (c.bytes[i] > 0 && hipMemcpyAsync(c.host[i], c.dev[i], (size_t)c.bytes[i], hipMemcpyDeviceToHost, hs) != hipSuccess)
-      return RMI_EDEVICE;
+    if (c.bytes[i] > 0 && (rc = rmi::readback_async(c.host[i], c.dev[i], (size_t)c.bytes[i], hs)) != RMI_OK) return rc;
   return hipStreamSynchronize(hs) == hipSuccess ? RMI_OK : RMI_EDEVICE;
 }

@@ -54,6 +54,10 @@ inline int launch_status() {
 }
 
 inline hipStream_t as_stream(rmi_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+// A device -> pinned-host copy enqueued on s (capi.hip): a kernel storing into the host buffer's
+// device mapping when the runtime reports one (and both ends are 4-B aligned, bytes % 4 == 0),
+// else hipMemcpyAsync (whose blit started ~11 us after the stream's last kernel here).
+int readback_async(void* host, const void* dev, size_t bytes, hipStream_t s);
 
 // 64-lane inclusive prefix sum on DPP (no LDS): row_shr 1/2/4/8 inside each 16-lane row,
 // then row_bcast:15 / row_bcast:31 carry the row totals across rows (gfx9 DPP).
