@@ -14,6 +14,15 @@ for i in range(1, len(seg)):  # the rollout ends at the first idle stretch over 
     if int(seg[i]["Start_Timestamp"]) - int(seg[i - 1]["End_Timestamp"]) > 5_000_000:
         seg = seg[:i]
         break
+# ... and at the formulated batch: formulate_tail_kernel and the readbacks right behind it (what
+# follows is the bench's own step count after rollout() returned)
+tails = [i for i, r in enumerate(seg) if "formulate_tail_kernel" in r["Kernel_Name"]]
+if tails:
+    j = tails[-1] + 1
+    while (j < len(seg) and ("readback_kernel" in seg[j]["Kernel_Name"] or "copyBuffer" in seg[j]["Kernel_Name"])
+           and int(seg[j]["Start_Timestamp"]) - int(seg[j - 1]["End_Timestamp"]) < 50_000):
+        j += 1
+    seg = seg[:j]
 t0 = int(seg[0]["Start_Timestamp"])
 busy, prev = 0, t0
 for r in seg:
