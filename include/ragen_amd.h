@@ -747,6 +747,13 @@ int rmi_prompt_commit_stats(const uint8_t* bpe_err, const uint8_t* text_err, con
 int rmi_next_rows_list(const uint8_t* has, const uint8_t* flags, int64_t B, int64_t* rows, int64_t* src,
                        rmi_stream_t stream);
 
+/* [host] The env ids that go on, from a turn's read-back flags (es_manager.py:168-169 over a
+ * turn whose inputs were the previous turn's survivors): out[k] = lo + i for every i < n with
+ * no bit of done_bits in flags[i], ascending -> their count, or -1 when more than cap (or a NULL
+ * argument).  Host memory only: the turn loop's survivor list without a numpy pass.          */
+int64_t rmi_host_live_ids(const uint8_t* flags, int64_t n, uint32_t done_bits, int64_t lo, int64_t* out,
+                          int64_t cap);
+
 /* ------------------------------------------------------------ the turn chain
  * Replaces: one turn of LLMAgentProxy.rollout's loop (agent_proxy.py:150-155) from the actor's
  *           output to the next generation batch's shape -- ContextManager.get_env_inputs

@@ -234,6 +234,7 @@ _SIGS = {
     "rmi_rows_stats": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_next_rows_stats": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p]),
     "rmi_turn_chain": (c_int32, [_P(TurnChain), c_void_p]),
+    "rmi_host_live_ids": (ctypes.c_int64, [c_void_p, c_int64, ctypes.c_uint32, c_int64, c_void_p, c_int64]),
     "rmi_turn_readback_pad": (c_int32, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "rmi_next_rows_list": (c_int32, [c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),

@@ -93,6 +93,18 @@ int readback_async(void* host, const void* dev, size_t bytes, hipStream_t s) {
 }
 }  // namespace rmi
 
+RMI_API int64_t rmi_host_live_ids(const uint8_t* flags, int64_t n, uint32_t done_bits, int64_t lo, int64_t* out,
+                                  int64_t cap) {
+  if (!flags || n < 0 || (!out && cap > 0)) return -1;
+  // branch-free in the flags (their pattern is random: a branch per env mispredicted often)
+  int64_t k = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    if (k < cap) out[k] = lo + i;
+    k += (flags[i] & done_bits) == 0;
+  }
+  return k <= cap ? k : -1;
+}
+
 RMI_API int rmi_readback(void* dst, const void* src, size_t bytes, rmi_stream_t stream) {
   if (!bytes) return RMI_OK;
   if (!dst || !src) return RMI_EINVAL;

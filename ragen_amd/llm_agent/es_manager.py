@@ -20,6 +20,7 @@ import functools
 import gc
 import os
 import random
+import time
 import warnings
 from collections.abc import Sequence
 from dataclasses import dataclass, field
@@ -43,6 +44,9 @@ class EnvStatus:
     num_actions: int = 0
     rewards: List[float] = field(default_factory=list)
     seed: Optional[int] = None
+
+
+STEP_STAMPS = None  # a list: _step_device appends (label, perf_counter) checkpoints (tools/prof_chain_stamps.py)
 
 
 class LazyEnvOutputs:
@@ -638,6 +642,7 @@ class EnvStateManager:
             rec, pack, hook, eager = self._device_pass(inp, t, None)
             host = ops.d2h(pack, self)
         asc = self._ascending(inp.env_ids)
+        _cp = STEP_STAMPS.append if STEP_STAMPS is not None else None  # (diagnostic checkpoints)
         self._next_rows = None
         o = (3 * n + 3) & ~3
         # max text / obs, the next batch's stats, raw max, pad count (and from the chain: the
@@ -648,6 +653,8 @@ class EnvStateManager:
                                "(rmi_pad_rows RMI_ERR_UNSUP): the actor was given left-cut prompts")
         if inp.raw_max is None:
             inp.ctx.note_raw(int(tail[5]))
+        if _cp:
+            _cp(("t1", time.perf_counter()))
         summ = ops.readback_summary(tail) if slot is not None else None
         err_h = host[n:2 * n]
         dec_h = host[2 * n:3 * n]
@@ -675,6 +682,8 @@ class EnvStateManager:
             dec_h = host[2 * n:3 * n]
             eager = eager and eager2
             rec = rec2
+        if _cp:
+            _cp(("t2", time.perf_counter()))
         rec["text_max"], rec["obs_max"] = int(tail[0]), (int(tail[1]) if rec.pop("_obs_known") else None)
         self._turn_records.append(rec)
         n_in = len(inp.env_ids)
@@ -687,23 +696,32 @@ class EnvStateManager:
             # the envs outside this turn's ids were all done before it (the ids are the last
             # turn's survivors, ascending): the inputs that go on are the envs not done
             all_still = summ[2] == n - n_in
-            if not all_still:
+            if not all_still:  # the survivors' ids from the flags in one C pass (rmi_host_live_ids)
                 still = None
-                out_local = np.flatnonzero((fl_h & _lib.FLAG_DONE) == 0)
+                out_local = np.empty(n - summ[2], np.int64)
+                # (the flags from the chain's pinned buffer: the same bytes as fl_h, pointer at hand)
+                k = _lib.lib().rmi_host_live_ids(self._chain.host_p, n, _lib.FLAG_DONE, self.env_lo,
+                                                 out_local.ctypes.data, out_local.size)
+                if k != out_local.size:
+                    raise RuntimeError(f"the turn's done count ({summ[2]}) disagrees with its flags")
         else:
             if inp.env_ids is self._ids_in_order:  # every env, in order (no gather)
                 still = (fl_h & _lib.FLAG_DONE) == 0
             else:
                 still = (fl_h[inp.env_ids - self.env_lo] & _lib.FLAG_DONE) == 0
             all_still = bool(still.all())
+        if _cp:
+            _cp(("t3", time.perf_counter()))
         self._all_active = n_in == self.n_envs and all_still
         if all_still:
             out_ids = inp.env_ids
         elif still is None:
-            out_ids = out_local + self.env_lo if self.env_lo else out_local
+            out_ids = out_local  # (env_lo added by rmi_host_live_ids)
         else:
             out_ids = inp.env_ids[still]
         self._live_ids = out_ids
+        if _cp:
+            _cp(("t4", time.perf_counter()))
         if eager:  # the next batch's stats, valid for exactly the env-id array handed out below
             hook.set_next_stats(t, tail[2:5], out_ids)
         if slot is not None and asc:  # the chain listed these envs (ascending) on the device
@@ -716,6 +734,8 @@ class EnvStateManager:
                 self._raise_errors(tg, err_h[tg.lo - self.env_lo:tg.hi - self.env_lo], [g - tg.lo for g in gids],
                                    gids)
             self._turn_records[-1]["err_seen"] = True
+        if _cp:
+            _cp(("t5", time.perf_counter()))
         return LazyEnvOutputs(self, out_ids)
 
     use_turn_chain = True  # (tests compare the chained turn with the step-by-step one)

@@ -844,7 +844,8 @@ class DevicePrompts:
             # padded by the turn chain right after its readback (the same rmi_pad_rows launch
             # over the same rows, width and block: TurnChain.run)
             n = rows.numel()
-            ids, am, pos = ep[3][:3 * n * S].view(3, n, S).unbind(0)
+            blk = ep[3]
+            ids, am, pos = (blk.as_strided((n, S), (S, 1), blk.storage_offset() + k * n * S) for k in range(3))
             err = ep[4][:n]
             self.chain_padded += 1
         else:

@@ -211,8 +211,22 @@ class TurnChain:
             return None
         _, P, pstride, bpe_stride, last, _ = plan
         c = s.c
-        c.vocab_packed, c.vocab_bytes, c.vocab_n_bytes, c.V = packed, vbytes, nbytes, V
-        c.parse, c.sel = parse, ops._ptr(sel)
+        bpe = self._bpe(bpe_stride)
+        # the fields that stay the same from rollout to rollout (vocabulary, parse, the slot's
+        # rows, the prompt program, the tokenizer, the arena): set when they change only
+        skey = (id(st), s.text.data_ptr(), stride, P, bpe)
+        if s.__dict__.get("static_key") != skey:
+            c.vocab_packed, c.vocab_bytes, c.vocab_n_bytes, c.V = packed, vbytes, nbytes, V
+            c.parse, c.sel = parse, ops._ptr(sel)
+            c.text, c.stride = s.text.data_ptr(), stride
+            c.prompt, c.ptext, c.pstride = P, s.ptext.data_ptr(), pstride
+            c.bpe, c.bpe_stride = bpe, bpe_stride
+            c.arena, c.arena_stride = pr.arena_p, pr.arena_stride
+            c.arena_len, c.len_upd = pr.len_p, pr.len_upd_p
+            c.host = self.host_p
+            c.pad_tail, c.pad_tail_n, c.pad_id = pr.tail_p, pr.tail_n, int(pr.pad_id)
+            c.pad_S_out = ctypes.addressof(self.pad_S)
+            s.static_key = skey
         # the generations: scattered onto the envs by the chain's first launch (deferred by
         # get_env_inputs), or already on the device
         if pend is not None:
@@ -237,25 +251,17 @@ class TurnChain:
             c.R = int(inp.ids.shape[1])
             c.ids, c.n_ids, c.has_t = inp.ids.data_ptr(), ops._ptr(inp.n_ids), ops._ptr(inp.has_t)
         c.raw_max, c.raw_next = inp.raw_dev.data_ptr(), inp.raw_next.data_ptr() if inp.raw_next is not None else None
-        c.text, c.stride = s.text.data_ptr(), stride
-        c.prompt, c.ptext, c.pstride = P, s.ptext.data_ptr(), pstride
-        c.bpe, c.bpe_stride = self._bpe(bpe_stride), bpe_stride
-        c.arena, c.arena_stride = pr.arena_p, pr.arena_stride
-        c.arena_len, c.len_upd = pr.len_p, pr.len_upd_p
         pack = inp.pack
         pk = pack.data_ptr()
         c.pack, c.stats = pk, pk + self.stats_off
         # the generation batch's flagged rows counted into this readback (DevicePrompts.gen_batch)
         pad = inp.pad_err if inp.pad_counted else None
         c.pad_err, c.n_pad = (pad.data_ptr(), pad.numel()) if pad is not None else (None, 0)
-        c.host = self.host_p
         # the next generation batch padded by the chain itself, into the block of that turn
         # number's batch when nothing outside holds it (DevicePrompts.gen_batch takes it)
         blk = None if last else pr.batch_block(t + 1)
         if blk is not None:
             c.pad_block, c.pad_cap, c.pad_err_next = blk[0].data_ptr(), blk[0].numel(), blk[1].data_ptr()
-            c.pad_tail, c.pad_tail_n, c.pad_id = pr.tail_p, pr.tail_n, int(pr.pad_id)
-            c.pad_S_out = ctypes.addressof(self.pad_S)
         else:
             c.pad_block = None
         stream = ops._stream(self.dev)

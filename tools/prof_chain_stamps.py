@@ -46,7 +46,7 @@ pm._storage_uses = stamp("_storage_uses", pm._storage_uses)
 import torch  # noqa: E402
 _empty = torch.empty
 torch.empty = stamp("torch.empty", _empty)
-em.LazyEnvOutputs = em.LazyEnvOutputs
+em.STEP_STAMPS = ST  # _step_device's own checkpoints (t1..t5) into the same trace
 es_cls = em.EnvStateManager
 es_cls._ascending = stamp("_ascending", es_cls._ascending)
 L = _lib.lib()
@@ -67,6 +67,8 @@ count = collections.Counter()
 open_ = {}
 for lab, t in ST:
     name, kind = lab[:-1], lab[-1]
+    if kind not in "<>":  # (a checkpoint, no span)
+        continue
     if kind == ">":
         open_.setdefault(name, []).append(t)
     else:
