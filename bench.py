@@ -595,6 +595,20 @@ def text_leg(R, device, reps=20):
     assert int(R.env.ep.turn_exec.sum().item()) == steps
     ms_tok = _graph_rollout(token_step)
     ms_tok_fused = _graph_rollout(lambda: token_step(True))
+    # one launch per turn: rmi_sokoban_token_turn (decode + parse, the turn and the render)
+    tok_rows = [ops.token_rows_struct(tok[t], tvocab, cfg, fused[t]) for t in range(T_TURNS)]
+
+    def token_turn_step():
+        e = R.env
+        for t in range(T_TURNS):
+            _, ts = text_turns[t]
+            kw = {"init_state": e.init_state, "init_player": e.init_player} if t == 0 else \
+                ({"fin": R.fin} if t == T_TURNS - 1 else {})
+            ops.sokoban_token_turn(tok_rows[t], R.st, e.ep, ts, robs, **kw)
+    token_turn_step()
+    torch.cuda.synchronize()
+    assert int(R.env.ep.turn_exec.sum().item()) == steps
+    ms_tok_one = _graph_rollout(token_turn_step)
     # render alone
     torch.cuda._sleep(2_000_000)
     e[0].record()
@@ -615,12 +629,14 @@ def text_leg(R, device, reps=20):
             "detok_parse": {"kernel": "rmi_detok_parse", "rows": B, "ids_per_row": int(tok[0].shape[1]),
                             "vocab": "byte-level (synthetic.byte_vocab)", "us": fused_us,
                             "note": "the decode fused with the parse: one launch per turn on the token path"},
-            "token_rollout": {"config": "SK rollout from response token ids: 5 x (detok_parse + turn + render)",
-                              "env_steps_per_rollout": steps, "ms_per_rollout": ms_tok,
-                              "env_steps_per_s": steps / ms_tok * 1e3,
+            "token_rollout": {"config": "SK rollout from response token ids: 5 x rmi_sokoban_token_turn (decode + "
+                                        "parse, turn and render in one launch per turn)",
+                              "env_steps_per_rollout": steps, "ms_per_rollout": ms_tok_one,
+                              "env_steps_per_s": steps / ms_tok_one * 1e3,
+                              "ms_per_rollout_three_launches": ms_tok,
                               "ms_per_rollout_turn_render_fused": ms_tok_fused,
-                              "note": "fused: rmi_sokoban_step_turn_render (the render in the turn's launch; "
-                                      "slower on the GPU at this size, DESIGN 3.10)"},
+                              "note": "three launches: detok_parse, the turn, the render per turn; "
+                                      "turn_render_fused: detok_parse, then rmi_sokoban_step_turn_render (DESIGN 3.10)"},
             "render": {"kernel": "rmi_sokoban_render", "envs": B, "us": render_us}}
 
 

@@ -514,6 +514,37 @@ int rmi_detok_parse(const int64_t* ids, int64_t B, int64_t R, const int32_t* n_i
                     int8_t* actions, uint8_t* n_actions, int32_t* spans, uint8_t* action_text, int32_t* action_len,
                     int32_t Lact, uint8_t* parse_err, rmi_stream_t stream);
 
+/* rmi_sokoban_token_turn: one Sokoban turn from the generations' token ids in ONE launch — the
+ * decode + parse of rmi_detok_parse (ContextManager.get_env_inputs, ctx_manager.py:332-352, and
+ * es_manager.py:230-240), then the turn and the next observation of rmi_sokoban_step_turn_render
+ * (EnvStateManager.step es_manager.py:105-171, SokobanEnv.render sokoban/env.py:53-61).  Outputs:
+ * exactly those of rmi_detok_parse(tok..., B = ep->B, actions = in->actions, n_actions =
+ * in->n_actions, action_text = NULL) followed by rmi_sokoban_step_turn_render(env, ep, in, err,
+ * fin, init_state, init_player, obs); tok->cfg->K == in->K.  A workgroup holds 16 envs: each wave
+ * decodes and parses one env's generation, the group's turn then runs on one wave (a lane per env),
+ * and each wave renders its env.  Fused for 36-cell rooms whose board window fits 32 bits and
+ * H*(W+1)-1 <= 64, fin == NULL or fin->group_size dividing 16, and rows whose LDS fits (16 rows of
+ * the parse's per-wave LDS within 56 KB); anything else runs the two calls (same outputs).        */
+typedef struct {
+  const int64_t* ids;           /* [B, R] generated ids                                        */
+  int64_t R;
+  const int32_t* n_ids;         /* [B] ids per row, or NULL (R each)                            */
+  const uint32_t* vocab_packed; /* rmi_vocab_pack's 16-B entries (16-B aligned)                 */
+  const uint8_t* vocab_bytes;   /* the blob of tokens longer than 12 bytes                     */
+  int64_t n_bytes, V;
+  uint8_t* text;                /* [B, stride] decoded rows (4-B aligned)                      */
+  int32_t stride;
+  int32_t* text_len;
+  uint8_t* decode_err;          /* [B] or NULL                                                  */
+  const rmi_parse_cfg_t* cfg;
+  const uint8_t* sel;           /* [B] name-id column, or NULL                                  */
+  int32_t* spans;               /* [B, 4] or NULL                                               */
+  uint8_t* parse_err;           /* [B] or NULL                                                  */
+} rmi_token_rows_t;
+int rmi_sokoban_token_turn(const rmi_token_rows_t* tok, const rmi_sokoban_t* env, const rmi_episode_t* ep,
+                           const rmi_turn_t* in, uint8_t* err, const rmi_finalize_t* fin, const uint8_t* init_state,
+                           const int8_t* init_player, const rmi_render_t* obs, rmi_stream_t stream);
+
 
 /* ---------------------------------------------- prompt token ids (§8(f) ranks 1-2)
  * Replaces: the tokenizer call of ContextManager.get_lm_inputs (ctx_manager.py:265-278,

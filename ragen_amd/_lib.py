@@ -78,6 +78,14 @@ class ParseCfg(ctypes.Structure):
                 ("name_hi", ctypes.c_uint64 * PARSE_MAX_NAMES), ("name_id", (ctypes.c_int8 * PARSE_MAX_NAMES) * 2)]
 
 
+class TokenRows(ctypes.Structure):
+    """rmi_token_rows_t: the decode + parse inputs and outputs of rmi_sokoban_token_turn."""
+    _fields_ = [("ids", c_void_p), ("R", c_int64), ("n_ids", c_void_p), ("vocab_packed", c_void_p),
+                ("vocab_bytes", c_void_p), ("n_bytes", c_int64), ("V", c_int64), ("text", c_void_p),
+                ("stride", c_int32), ("text_len", c_void_p), ("decode_err", c_void_p), ("cfg", ctypes.POINTER(ParseCfg)),
+                ("sel", c_void_p), ("spans", c_void_p), ("parse_err", c_void_p)]
+
+
 PROMPT_MAX_PIECES = 32
 PT_CONST, PT_TAG_CONST, PT_OBS, PT_INT, PT_REWARD, PT_RESPONSE, PT_MARK, PT_IF = range(8)
 
@@ -164,6 +172,8 @@ _SIGS = {
                                                  c_void_p, c_void_p, c_void_p]),
     "rmi_sokoban_step_turn_render": (c_int32, [_P(Sokoban), _P(Episode), _P(Turn), c_void_p, _P(Finalize), c_void_p,
                                                c_void_p, _P(Render), c_void_p]),
+    "rmi_sokoban_token_turn": (c_int32, [_P(TokenRows), _P(Sokoban), _P(Episode), _P(Turn), c_void_p, _P(Finalize),
+                                         c_void_p, c_void_p, _P(Render), c_void_p]),
     "rmi_sokoban_render": (c_int32, [_P(Sokoban), c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,
                                      c_void_p]),
     "rmi_frozenlake_render": (c_int32, [_P(FrozenLake), c_int32, c_void_p, c_void_p, c_void_p, c_int32, c_void_p,

@@ -16,6 +16,7 @@
 //   4. any irregular room sends its whole wave to the exact path (env-private LDS rows,
 //      numpy's negative-index wrap, gym_sokoban's IndexError points).
 #include "common.hpp"
+#include "parse_core.hpp"
 
 #include <type_traits>
 
@@ -183,6 +184,8 @@ __device__ __forceinline__ uint32_t env_or(uint32_t x) {
   if (LPE >= 2) x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
   if (LPE >= 4) x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
   if (LPE >= 8) x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if (LPE >= 16) x |= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+  static_assert(LPE <= 16, "an env's lanes lie in one DPP row");
   return x;
 }
 template <int LPE>
@@ -642,28 +645,22 @@ __device__ __forceinline__ void render_group(const ObsOut& o, ObsLds<HW, M>& L, 
 // rollout's env-turns, their rows ≈9 % of its traffic).
 // kObs (HW == 36, LPE == 1): the launch also renders every env's observation after the turn
 // (render_group; kObsFan times the waves per workgroup, the extra ones only render).
-template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false, bool kObs = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
-__global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
-                                                                  int hw_rt, uint64_t border,
-                                                                  uint8_t* __restrict__ err_out, rmi_finalize_t fin,
-                                                                  const uint8_t* __restrict__ init_state = nullptr,
-                                                                  const int8_t* __restrict__ init_player = nullptr,
-                                                                  ObsOut obs = ObsOut{}) {
-  static_assert(!kObs || (HW == 36 && LPE == 1 && !kLate), "the fused render: 36-cell rooms, one lane per env");
+// The turn of env b (this lane is its sub-th of LPE): the body of sokoban_step_turn_kernel and of the
+// token turn (sokoban_token_turn_kernel).  ls / lf: the env's exact-path LDS rows (row_words dwords
+// each).  at_end(xs, xf, wall, target, box, jp): the env's state after the turn, for a fused render
+// (jp = the player's window bit of a stepped regular room — read the bitboards — else INT32_MIN:
+// read the rows); called by every lane after the turn's stores, before the fused finalize.
+template <int HW, class M, int LPE, bool kFin, bool kFirst, bool kLate, class AtEnd>
+__device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_episode_t& ep, const rmi_turn_t& in,
+                                         int hw_rt, uint64_t border, uint8_t* __restrict__ err_out,
+                                         const rmi_finalize_t& fin, const uint8_t* __restrict__ init_state,
+                                         const int8_t* __restrict__ init_player, int64_t b, int sub, uint32_t* ls,
+                                         uint32_t* lf, AtEnd&& at_end) {
   constexpr int NW = HW ? HW / 4 : kMaxWords;
   constexpr int NWL = (NW + LPE - 1) / LPE;      // row dwords per lane
-  constexpr int kEnvs = kWave / LPE;             // envs per wave
-  __shared__ uint32_t lds_state[kSokWpb * kEnvs * NW];  // exact path only: env-private rows
-  __shared__ uint32_t lds_fixed[kSokWpb * kEnvs * NW];
   const int hw = HW ? HW : hw_rt;
   const int row_words = hw >> 2;
-  using ObsL = ObsLds<kObs ? HW : 36, M>;
-  __shared__ typename std::conditional<kObs, ObsL, char>::type lds_obs;  // kObs: the group's envs and rows
   const int B = ep.B;
-  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
-  const int sub = lane % LPE, slot = lane / LPE;
-  const bool turn_wave = !kObs || wave < kSokWpb;  // kObs helper waves only render
-  const int64_t b = turn_wave ? ((int64_t)blockIdx.x * kSokWpb + wave) * kEnvs + slot : (int64_t)B;
   const bool live = b < B;
   const int H = env.H, W = env.W;
   const uint32_t w_magic = (65536u + (uint32_t)W - 1u) / (uint32_t)W;  // off the critical path
@@ -834,8 +831,6 @@ __global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoba
   } else {
     // rare: some room of the wave is irregular -> the exact path on an env-private LDS row,
     // assembled from the env's lanes and stepped by its first lane
-    uint32_t* ls = lds_state + (wave * kEnvs + slot) * row_words;
-    uint32_t* lf = lds_fixed + (wave * kEnvs + slot) * row_words;
     if (act) {
 #pragma unroll
       for (int i = 0; i < NWL; ++i) {
@@ -925,30 +920,59 @@ __global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoba
     if (row_changed) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
   }
   RMI_STAMP(4);
-  if constexpr (kObs) {
-    if (turn_wave) {  // this env's state after the turn, for the group's render
-      const int e = wave * kWave + lane;
-#pragma unroll
-      for (int i = 0; i < NW; ++i) {
-        lds_obs.xs[e][i] = xs[i];
-        lds_obs.xf[e][i] = xf[i];
-      }
-      lds_obs.wall[e] = wall;
-      lds_obs.target[e] = target;
-      lds_obs.box[e] = box;
-      lds_obs.jp[e] = (fast && act) ? jp : INT32_MIN;
-    }
-    if (threadIdx.x < 18) lds_obs.gb[threadIdx.x] = threadIdx.x < 16 ? obs.gb[threadIdx.x] : (threadIdx.x == 16 ? '?' : '\n');
-    __syncthreads();
-#ifndef RMI_OBS_SKIP_RENDER  // (diagnostic variant: the record and the barrier only)
-    render_group<HW, M>(obs, lds_obs, B, H, W);
-#endif
-  }
+  at_end(xs, xf, wall, target, box, (fast && act) ? jp : INT32_MIN);
   if (kFin) {
     if (act) rec.set(in.turn, o.acc, o.info);  // this turn's record is still in registers
     finalize_envs<LPE>(ep, fin, rec, b, live && sub == 0, flags, n_turns, num_actions, penalty, act ? in.turn : -1,
                        o.acc, o.info);
   }
+}
+
+template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false, bool kObs = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
+__global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
+                                                                  int hw_rt, uint64_t border,
+                                                                  uint8_t* __restrict__ err_out, rmi_finalize_t fin,
+                                                                  const uint8_t* __restrict__ init_state = nullptr,
+                                                                  const int8_t* __restrict__ init_player = nullptr,
+                                                                  ObsOut obs = ObsOut{}) {
+  static_assert(!kObs || (HW == 36 && LPE == 1 && !kLate), "the fused render: 36-cell rooms, one lane per env");
+  constexpr int NW = HW ? HW / 4 : kMaxWords;
+  constexpr int kEnvs = kWave / LPE;             // envs per wave
+  __shared__ uint32_t lds_state[kSokWpb * kEnvs * NW];  // exact path only: env-private rows
+  __shared__ uint32_t lds_fixed[kSokWpb * kEnvs * NW];
+  using ObsL = ObsLds<kObs ? HW : 36, M>;
+  __shared__ typename std::conditional<kObs, ObsL, char>::type lds_obs;  // kObs: the group's envs and rows
+  const int B = ep.B;
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int sub = lane % LPE, slot = lane / LPE;
+  const bool turn_wave = !kObs || wave < kSokWpb;  // kObs helper waves only render
+  const int64_t b = turn_wave ? ((int64_t)blockIdx.x * kSokWpb + wave) * kEnvs + slot : (int64_t)B;
+  const int row_words = (HW ? HW : hw_rt) >> 2;
+  turn_env<HW, M, LPE, kFin, kFirst, kLate>(
+      env, ep, in, hw_rt, border, err_out, fin, init_state, init_player, b, sub,
+      lds_state + (wave * kEnvs + slot) * row_words, lds_fixed + (wave * kEnvs + slot) * row_words,
+      [&](const auto& xs, const auto& xf, M wall, M target, M box, int jp) {
+        if constexpr (kObs) {
+          const int H = env.H, W = env.W;
+          if (turn_wave) {  // this env's state after the turn, for the group's render
+            const int e = wave * kWave + lane;
+#pragma unroll
+            for (int i = 0; i < NW; ++i) {
+              lds_obs.xs[e][i] = xs[i];
+              lds_obs.xf[e][i] = xf[i];
+            }
+            lds_obs.wall[e] = wall;
+            lds_obs.target[e] = target;
+            lds_obs.box[e] = box;
+            lds_obs.jp[e] = jp;
+          }
+          if (threadIdx.x < 18) lds_obs.gb[threadIdx.x] = threadIdx.x < 16 ? obs.gb[threadIdx.x] : (threadIdx.x == 16 ? '?' : '\n');
+          __syncthreads();
+#ifndef RMI_OBS_SKIP_RENDER  // (diagnostic variant: the record and the barrier only)
+          render_group<HW, M>(obs, lds_obs, B, H, W);
+#endif
+        }
+      });
 }
 
 // Fused reset: room_state/player from the generated rooms, counters and the whole episode
@@ -1023,6 +1047,161 @@ __global__ __launch_bounds__(kBlock) void sokoban_load_rooms_kernel(rmi_sokoban_
       ep.turn_exec[u * B + i] = 0;
     }
   }
+}
+
+
+// ---- the token turn (rmi_sokoban_token_turn): the decode + parse, the turn and the render of a
+// Sokoban turn in one launch.  A workgroup holds kTokEnvs envs = kTokEnvs waves: wave w decodes and
+// parses env b0 + w's generation (detok_parse_kernel's body, its rows in the wave's LDS); after
+// the barrier wave 0 steps the group's envs, one lane each (turn_env: the turn kernel's code, and
+// its fused finalize for groups inside the 16 envs), leaving each env's state after the turn in
+// LDS; after the second barrier wave w renders env b0 + w, one lane per token (cell or newline),
+// into an LDS row copied out as dwords — the bytes rmi_sokoban_render writes.  The per-turn launch
+// count of the token path drops from three (decode + parse, turn, render) to one, and the turn's
+// and the render's launches (their ramps and tails) go with it.
+constexpr int kTokEnvs = 16;
+constexpr int kTokRowWords = 48;  // >= (36 * 4 + 35 + 3) / 4: the longest 36-cell observation, in dwords
+struct TokRec {                  // an env's state after the turn (36-cell room, u32 board window)
+  uint32_t xs[9], xf[9];
+  uint32_t wall, target, box;
+  int jp;                        // a stepped regular room's player bit (the bitboards hold it), else INT32_MIN
+};
+__host__ __device__ constexpr size_t tok_static_lds() {
+  return 2 * kTokEnvs * 9 * 4 + kTokEnvs * sizeof(TokRec) + kTokEnvs * kTokRowWords * 4 + 18 * 4;
+}
+
+template <bool kFin, bool kFirst>
+__global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu(8))) void sokoban_token_turn_kernel(
+    DetokArgs d, ParseArgs a, rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in, uint64_t border,
+    uint8_t* __restrict__ err_out, rmi_finalize_t fin, const uint8_t* __restrict__ init_state,
+    const int8_t* __restrict__ init_player, ObsOut obs) {
+  extern __shared__ uint64_t lds_q[];  // kTokEnvs parse regions (parse_lds(stride) each)
+  __shared__ uint32_t lds_state[kTokEnvs * 9], lds_fixed[kTokEnvs * 9];
+  __shared__ TokRec rec[kTokEnvs];
+  __shared__ uint32_t blk[kTokEnvs][kTokRowWords];
+  __shared__ uint32_t gb[18];  // glyph bytes of codes 0..15, then '?' and '\n'
+  // the render's scalars, staged here so that none of them stays live in registers across the
+  // decode, the parse and the turn (the kernel runs at the parse's 64-VGPR budget)
+  __shared__ struct {
+    uint8_t* out;
+    int32_t* len;
+    uint64_t glen;
+    int stride, H, W, B;
+  } rp;
+  // wave-uniform in SGPRs (a VGPR copy of the wave index was spilled and reloaded from scratch)
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t b0 = (int64_t)blockIdx.x * kTokEnvs, b = b0 + wv;
+  if (threadIdx.x < 18) gb[threadIdx.x] = threadIdx.x < 16 ? obs.gb[threadIdx.x] : (threadIdx.x == 16 ? '?' : '\n');
+  if (threadIdx.x == 64) {
+    rp.out = obs.out;
+    rp.len = obs.len;
+    rp.glen = obs.glen;
+    rp.stride = obs.stride;
+    rp.H = env.H;
+    rp.W = env.W;
+    rp.B = ep.B;
+  }
+
+  // ---- 1. env b's generation: decoded into the parse's LDS row (and written out), parsed in place
+  if (b < a.B) {
+    uint8_t* lds = reinterpret_cast<uint8_t*>(lds_q) + wv * parse_lds(a.stride);
+    const int cap = list_cap(a.stride);
+    uint8_t* T = lds + 4;
+    uint8_t* Wb = lds + row_bytes(a.stride) + 4;
+    uint16_t* EL = reinterpret_cast<uint16_t*>(lds + 2 * row_bytes(a.stride));
+    uint16_t* ES = EL + cap;
+    uint8_t* EI = reinterpret_cast<uint8_t*>(ES + cap);
+    const Names nm = load_names(a.cfg, (a.sel && a.sel[b]) ? 1 : 0);
+#ifdef RMI_PARSE_STAMPS
+    unsigned long long pst_[10], dst_[6];
+#endif
+    const int n = detok_row(d, T + kPre, Wb + kPre, b, lane DSTAMP_ARG);
+    parse_row(a, T, Wb, EL, ES, EI, b, n, 0, nm, lane PSTAMP_ARG);
+  }
+  __syncthreads();  // the group's actions (global stores of its parse waves) visible to wave 0
+
+  // ---- 2. the turn of the group's envs: kLpeT = 16 lanes per env on the first 4 waves (env
+  //         b0 + t / 16 for thread t): one row dword per lane keeps the turn inside the parse's
+  //         64-VGPR budget.  The last turn's finalize runs after it (section 3)
+  constexpr int kLpeT = 16;
+  constexpr int kTurnWaves = kTokEnvs * kLpeT / kWave;
+#ifndef RMI_TOK_NO_TURN  // (diagnostic variants: tools/bench_token_turn.py)
+  if (wv < kTurnWaves) {
+    const int t = wv * kWave + lane, e = t / kLpeT, sub = t % kLpeT;
+    const int64_t be = b0 + e;
+    turn_env<36, uint32_t, kLpeT, false, kFirst, false>(
+        env, ep, in, 36, border, err_out, fin, init_state, init_player, be, sub, lds_state + e * 9, lds_fixed + e * 9,
+        [&](const auto& xs, const auto& xf, uint32_t wall, uint32_t target, uint32_t box, int jp) {
+#pragma unroll
+          for (int i = 0; i < (9 + kLpeT - 1) / kLpeT; ++i) {
+            const int w = sub + kLpeT * i;
+            if (w < 9) {
+              rec[e].xs[w] = xs[i];
+              rec[e].xf[w] = xf[i];
+            }
+          }
+          if (sub == 0) {
+            rec[e].wall = wall;
+            rec[e].target = target;
+            rec[e].box = box;
+            rec[e].jp = jp;
+          }
+        });
+  }
+#endif
+  __syncthreads();
+  // ---- 3. the last turn: rmi_rollout_finalize's work for the group's envs on wave 0, one lane per
+  //         env (finalize_envs, as the fused turn form runs it), from the record the turn just wrote
+  if constexpr (kFin) {
+    if (wv == 0) {
+      const int64_t be = b0 + (lane & (kTokEnvs - 1)), bc = be < ep.B ? be : (int64_t)ep.B - 1;
+      FinRecord fr;
+      fr.load(ep, bc);
+      finalize_envs<1>(ep, fin, fr, be, lane < kTokEnvs && be < ep.B, ep.flags[bc], ep.n_turns[bc],
+                       ep.num_actions[bc], ep.penalty[bc], -1, 0.0, 0);
+    }
+  }
+#ifdef RMI_TOK_NO_RENDER
+  return;
+#endif
+
+  // ---- 4. env b's observation (rmi_sokoban_render's row): token t = lane, t = r * (W + 1) + c is
+  //         cell (r, c) for c < W, a newline for c == W
+  if (b >= rp.B) return;
+  const int H = rp.H, W = rp.W, T = H * (W + 1) - 1;
+  const TokRec& R = rec[wv];
+  const int r = lane / (W + 1), c = lane - r * (W + 1);
+  uint32_t cd = 0x100u;  // no token
+  if (lane < T) {
+    if (c == W) {
+      cd = 0xFFu;  // newline
+    } else {
+      const int i = r * W + c;
+      const uint32_t s_ = (R.xs[i >> 2] >> (8 * (i & 3))) & 0xFFu, f_ = (R.xf[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+      int v = (s_ == 5u && f_ == 2u) ? 6 : (int)s_;  // the player on a target shown as 6 (sokoban/env.py:55)
+      if (R.jp != INT32_MIN) {  // a stepped regular room: from the bitboards (window bit q = cell W + q)
+        const int qb = i - W, qq = qb >= 0 ? qb : 0;
+        const uint32_t wl = qb >= 0 ? (R.wall >> qq) & 1u : 1u;
+        const int tg = (int)((R.target >> qq) & 1u), bx = (int)((R.box >> qq) & 1u);
+        v = wl ? 0 : (qb == R.jp ? 5 + tg : (bx ? 4 - tg : 1 + tg));
+      }
+      cd = (uint32_t)(v > 0xFE ? 0xFE : v);
+    }
+  }
+  const uint32_t g = gb[cd < 16u ? cd : (cd == 0xFFu ? 17u : 16u)];
+  const int len = cd == 0x100u ? 0 : (cd < 16u ? (int)((rp.glen >> (4 * cd)) & 15u) : 1);
+  const int incl = wave_inclusive_scan(len);
+  const int off = incl - len, total = __builtin_amdgcn_readlane(incl, 63), nw = (total + 3) >> 2;
+  uint32_t* row = blk[wv];
+  if (lane < nw) row[lane] = 0u;  // the last dword's unused bytes stay 0
+  wave_sync();
+  uint8_t* rb = reinterpret_cast<uint8_t*>(row);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (q < len) rb[off + q] = (uint8_t)(g >> (8 * q));
+  wave_sync();
+  if (lane < nw) reinterpret_cast<uint32_t*>(rp.out + b * (int64_t)rp.stride)[lane] = row[lane];
+  if (lane == 0) rp.len[b] = total;
 }
 
 }  // namespace
@@ -1187,20 +1366,14 @@ RMI_API int rmi_sokoban_step_turn_first(const rmi_sokoban_t* env, const rmi_epis
   return sokoban_step_turn_launch<false, true>(env, ep, in, err, f, as_stream(stream), init_state, init_player);
 }
 
-RMI_API int rmi_sokoban_step_turn_render(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
-                                         uint8_t* err, const rmi_finalize_t* fin, const uint8_t* init_state,
-                                         const int8_t* init_player, const rmi_render_t* obs, rmi_stream_t stream) {
-  using namespace rmi;
-  if (!obs || (fin && init_state) || (!init_state) != (!init_player)) return RMI_EINVAL;
-  if (!env || env->H <= 0 || env->W <= 0) return RMI_EINVAL;
+namespace rmi {
+namespace {
+// rmi_sokoban_step_turn_render's glyph table and output checks -> the kernel's ObsOut.
+int obs_out(const rmi_sokoban_t* env, const rmi_render_t* obs, ObsOut& o) {
+  if (!obs || !env || env->H <= 0 || env->W <= 0) return RMI_EINVAL;
   for (int k = 0; k < 16; ++k)
     if (obs->glyph_len[k] > 4) return RMI_EINVAL;
   if (obs->stride < env->H * env->W * 4 + env->H - 1 || obs->stride % 4) return RMI_EINVAL;
-  rmi_finalize_t f;
-  const int rc = validate_turn(env, ep, in, fin, init_state, init_player, f);
-  if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
-  if (!obs->out || !obs->len || (reinterpret_cast<uintptr_t>(obs->out) & 3u)) return RMI_EINVAL;
-  ObsOut o;
   o.glen = 0;
   for (int k = 0; k < 16; ++k) {  // absent glyphs render '?' (as rmi_sokoban_render)
     o.gb[k] = obs->glyph_len[k] ? obs->glyph_bytes[k] : (uint32_t)'?';
@@ -1209,6 +1382,23 @@ RMI_API int rmi_sokoban_step_turn_render(const rmi_sokoban_t* env, const rmi_epi
   o.out = obs->out;
   o.len = obs->len;
   o.stride = obs->stride;
+  return RMI_OK;
+}
+}  // namespace
+}  // namespace rmi
+
+RMI_API int rmi_sokoban_step_turn_render(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
+                                         uint8_t* err, const rmi_finalize_t* fin, const uint8_t* init_state,
+                                         const int8_t* init_player, const rmi_render_t* obs, rmi_stream_t stream) {
+  using namespace rmi;
+  if (!obs || (fin && init_state) || (!init_state) != (!init_player)) return RMI_EINVAL;
+  ObsOut o;
+  const int oc = obs_out(env, obs, o);
+  if (oc != RMI_OK) return oc;
+  rmi_finalize_t f;
+  const int rc = validate_turn(env, ep, in, fin, init_state, init_player, f);
+  if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
+  if (!obs->out || !obs->len || (reinterpret_cast<uintptr_t>(obs->out) & 3u)) return RMI_EINVAL;
   hipStream_t s = as_stream(stream);
   int lc = fin ? sokoban_step_turn_obs_launch<true, false>(env, ep, in, err, f, s, nullptr, nullptr, o)
            : init_state ? sokoban_step_turn_obs_launch<false, true>(env, ep, in, err, f, s, init_state, init_player, o)
@@ -1257,5 +1447,57 @@ RMI_API int rmi_sokoban_reset(const rmi_sokoban_t* env, const rmi_episode_t* ep,
   const int64_t n = nw > ep->B ? nw : ep->B;
   hipLaunchKernelGGL(sokoban_reset_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                      as_stream(stream), *env, *ep, hw, init_state, init_player);
+  return launch_status();
+}
+
+
+RMI_API int rmi_sokoban_token_turn(const rmi_token_rows_t* tok, const rmi_sokoban_t* env, const rmi_episode_t* ep,
+                                   const rmi_turn_t* in, uint8_t* err, const rmi_finalize_t* fin,
+                                   const uint8_t* init_state, const int8_t* init_player, const rmi_render_t* obs,
+                                   rmi_stream_t stream) {
+  using namespace rmi;
+  if (!tok || !ep || !in || !obs || !tok->cfg || (fin && init_state) || (!init_state) != (!init_player))
+    return RMI_EINVAL;
+  if (tok->cfg->K != in->K) return RMI_EINVAL;
+  const int64_t B = ep->B;
+  DetokArgs d;
+  ParseArgs a;
+  int rc = detok_parse_args(tok->ids, B, tok->R, tok->n_ids, tok->vocab_packed, tok->vocab_bytes, tok->n_bytes, tok->V,
+                            tok->text, tok->stride, tok->text_len, tok->decode_err, tok->cfg, tok->sel, const_cast<int8_t*>(in->actions),
+                            const_cast<uint8_t*>(in->n_actions), tok->spans, nullptr, nullptr, 0, tok->parse_err, d, a);
+  if (rc < 0) return rc;
+  ObsOut o;
+  rc = obs_out(env, obs, o);
+  if (rc != RMI_OK) return rc;
+  rmi_finalize_t f;
+  rc = validate_turn(env, ep, in, fin, init_state, init_player, f);
+  if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
+  if (!obs->out || !obs->len || (reinterpret_cast<uintptr_t>(obs->out) & 3u)) return RMI_EINVAL;
+  const int H = env->H, W = env->W;
+  const size_t shm = (size_t)kTokEnvs * parse_lds(tok->stride);
+  const bool fused = H * W == 36 && (H - 1) * W <= 32 && H * (W + 1) - 1 <= kWave && (!fin || kTokEnvs % fin->group_size == 0) &&
+                     shm + tok_static_lds() <= 56 * 1024 && o.stride <= obs_pitch_max(36);
+  if (!fused) {  // the two calls
+    rc = rmi_detok_parse(tok->ids, B, tok->R, tok->n_ids, tok->vocab_packed, tok->vocab_bytes, tok->n_bytes, tok->V,
+                         tok->text, tok->stride, tok->text_len, tok->decode_err, tok->cfg, tok->sel, const_cast<int8_t*>(in->actions),
+                         const_cast<uint8_t*>(in->n_actions), tok->spans, nullptr, nullptr, 0, tok->parse_err, stream);
+    if (rc != RMI_OK) return rc;
+    return rmi_sokoban_step_turn_render(env, ep, in, err, fin, init_state, init_player, obs, stream);
+  }
+  uint64_t border = 0;
+  for (int r = 0; r < H; ++r)
+    for (int c = 0; c < W; ++c)
+      if (r == 0 || c == 0 || r == H - 1 || c == W - 1) border |= 1ull << (r * W + c);
+  const dim3 grid((unsigned)((B + kTokEnvs - 1) / kTokEnvs)), block(kWave * kTokEnvs);
+  hipStream_t s = as_stream(stream);
+  if (fin)
+    hipLaunchKernelGGL((sokoban_token_turn_kernel<true, false>), grid, block, shm, s, d, a, *env, *ep, *in, border, err, f,
+                       nullptr, nullptr, o);
+  else if (init_state)
+    hipLaunchKernelGGL((sokoban_token_turn_kernel<false, true>), grid, block, shm, s, d, a, *env, *ep, *in, border, err, f,
+                       init_state, init_player, o);
+  else
+    hipLaunchKernelGGL((sokoban_token_turn_kernel<false, false>), grid, block, shm, s, d, a, *env, *ep, *in, border, err,
+                       f, nullptr, nullptr, o);
   return launch_status();
 }

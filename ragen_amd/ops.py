@@ -772,6 +772,46 @@ def detok_parse(ids: torch.Tensor, vocab: "VocabTable", stride: int, cfg: _lib.P
     return o
 
 
+
+def token_rows_struct(ids: torch.Tensor, vocab: "VocabTable", cfg: _lib.ParseCfg, out: dict,
+                      n_ids: Optional[torch.Tensor] = None, sel: Optional[torch.Tensor] = None) -> _lib.TokenRows:
+    """rmi_token_rows_t of a token batch and a detok_parse result dict ``out`` (its text, lengths,
+    spans and error bytes are written; its actions / n_actions are the turn's, see
+    sokoban_token_turn).  The tensors (and cfg) must outlive every launch that uses the struct."""
+    _dev(ids, n_ids, sel, vocab.packed, vocab.data)
+    _dt(ids, torch.int64, "ids")
+    _dt(n_ids, torch.int32, "n_ids")
+    _dt(sel, torch.uint8, "sel")
+    t = _lib.TokenRows()
+    t.ids, t.R, t.n_ids = _ptr(ids), int(ids.shape[1]), _ptr(n_ids)
+    t.vocab_packed, t.vocab_bytes = _ptr(vocab.packed), _ptr(vocab.data)
+    t.n_bytes, t.V = vocab.data.numel(), vocab.packed.shape[0]
+    t.text, t.stride, t.text_len = _ptr(out["text"]), int(out["text"].shape[1]), _ptr(out["text_len"])
+    t.decode_err, t.cfg, t.sel = _ptr(out["decode_err"]), ctypes.pointer(cfg), _ptr(sel)
+    t.spans, t.parse_err = _ptr(out["spans"]), _ptr(out["err"])
+    t._keep = (cfg,)
+    return t
+
+
+def sokoban_token_turn(tok: _lib.TokenRows, env: _lib.Sokoban, ep: EpisodeState, turn: _lib.Turn, obs: _lib.Render,
+                       err: Optional[torch.Tensor] = None, fin: Optional[_lib.Finalize] = None,
+                       init_state: Optional[torch.Tensor] = None, init_player: Optional[torch.Tensor] = None):
+    """One Sokoban turn from the generations' token ids in ONE launch (rmi_sokoban_token_turn):
+    detok_parse into tok's buffers with the actions into turn.actions / turn.n_actions, then the
+    turn (plain; fin: the rollout's last; init_state / init_player: the first) and the render
+    into obs — the outputs of detok_parse followed by sokoban_step_turn_render."""
+    _dev(init_state, init_player, err)
+    rc = lib().rmi_sokoban_token_turn(ctypes.byref(tok), env, ep.struct(), turn, _ptr(err), fin, _ptr(init_state),
+                                      _ptr(init_player), obs, _stream(ep.device))
+    if rc == _lib.RMI_EUNSUP and fin is not None:
+        # finalize groups that straddle a wave: the token turn, then the finalize
+        sokoban_token_turn(tok, env, ep, turn, obs, err)
+        seg = torch.arange(0, ep.B + 1, fin.group_size, dtype=torch.int32, device=ep.flags.device)
+        check(lib().rmi_rollout_finalize(ep.struct(), _ptr(seg), seg.numel() - 1, fin.method, fin.metrics,
+                                         fin.score, fin.pen, fin.norm, _stream(ep.device)), "rmi_rollout_finalize")
+        return
+    check(rc, "rmi_sokoban_token_turn")
+
 # ------------------------------------------------------------------- token masks (A11)
 def masks_and_scores(ids: torch.Tensor, special_token: int, reward_token: int, scores: torch.Tensor,
                      n_scores: torch.Tensor, n_slots: int, use_turn_scores: bool, enable_response_mask: bool,
