@@ -584,6 +584,34 @@ constexpr int kDetokG = 4;  // 64-id chunks per step
 __device__ __forceinline__ uint32_t byte_mask_n(int n) {
   return n >= 4 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << (8 * n)) - 1u);
 }
+// UTF-8 well-formedness (Unicode Table 3-7, what CPython's strict decode accepts) of the 4 bytes
+// of dword w, with the 4 bytes before them in wp; -> bit 7 of each bad byte.  SWAR, no branches:
+// a byte is a continuation byte (10xxxxxx) exactly when a lead 1-3 bytes back expects one (the
+// byte before >= C0, two before >= E0, three before >= F0); C0, C1 and F5..FF never occur; and
+// the second byte after E0 / ED / F0 / F4 is limited to A0-BF / 80-9F / 90-BF / 80-8F.  Bytewise
+// compares use only bit 7 of each byte (shifted-in bits from the byte below never reach it).
+__device__ __forceinline__ uint32_t swar_zero_bytes(uint32_t z) {  // bit 7 of each zero byte
+  return ~((((z & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | z) & 0x80808080u) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t utf8_dword_bad(uint32_t w, uint32_t wp) {
+  constexpr uint32_t H = 0x80808080u, L = 0x01010101u;
+  const uint32_t c = w;
+  const uint32_t p1 = __builtin_amdgcn_alignbyte(w, wp, 3);  // the byte before each byte of w
+  const uint32_t p2 = __builtin_amdgcn_alignbyte(w, wp, 2);
+  const uint32_t p3 = __builtin_amdgcn_alignbyte(w, wp, 1);
+  const uint32_t cont = c & ~(c << 1) & H;
+  const uint32_t expect = (p1 & (p1 << 1)) | (p2 & (p2 << 1) & (p2 << 2)) | (p3 & (p3 << 1) & (p3 << 2) & (p3 << 3));
+  uint32_t err = (cont ^ expect) & H;
+  err |= swar_zero_bytes((c & 0xFEFEFEFEu) ^ 0xC0C0C0C0u);                                   // C0, C1
+  err |= c & (c << 1) & (c << 2) & (c << 3) & (c << 4);                                       // F8..FF
+  err |= swar_zero_bytes((c & 0xF8F8F8F8u) ^ 0xF0F0F0F0u) & (c << 5) & ((c << 6) | (c << 7));  // F5..F7
+  const uint32_t b5 = c << 2, b4 = c << 3;  // bits 5 and 4 of each byte, at bit 7
+  err |= swar_zero_bytes(p1 ^ (0xE0u * L)) & ~b5;
+  err |= swar_zero_bytes(p1 ^ (0xEDu * L)) & b5;
+  err |= swar_zero_bytes(p1 ^ (0xF0u * L)) & ~(b5 | b4);
+  err |= swar_zero_bytes(p1 ^ (0xF4u * L)) & (b5 | b4);
+  return err & H;
+}
 __host__ __device__ constexpr size_t detok_lds(int stride) { return 2 * ((size_t)stride + 4) + 16; }  // per wave
 
 struct DetokArgs {
@@ -701,56 +729,17 @@ __device__ __forceinline__ int detok_row(const DetokArgs& d, uint8_t* buf, uint8
   if (lane < 8) buf[n + lane] = 0;  // the validity windows read up to 8 bytes past the end
   if (lane < 4) buf[lane - 4] = 0;  // ... and 4 before the start
   wave_sync();
-  // Non-ASCII bytes: a wave-parallel validity test first (UTF-8 validity is local: every lead
-  // byte needs its continuation bytes with the Table 3-7 ranges, every continuation byte a lead
-  // at most 3 bytes back whose sequence covers it).  Only an invalid row takes the serial
-  // replacement pass.
+  // Non-ASCII bytes: a wave-parallel validity test first, branch-free over 4 bytes per lane
+  // (utf8_dword_bad).  Positions n .. n + 2 are tested too: the zero bytes after the row are no
+  // continuation bytes, so a sequence cut off by the row's end is an error there.  Only an invalid
+  // row takes the serial replacement pass.
   bool invalid = false;
   if (__ballot((high & 0x80808080u) != 0)) {  // high: the OR of the row's bytes, 4 per dword
-    for (int c0 = 0; c0 < n; c0 += 256) {
+    for (int c0 = 0; c0 < n + 3; c0 += 256) {
       const int i0 = c0 + 4 * lane;
-      if (i0 >= n) continue;
-      const uint32_t* b4 = reinterpret_cast<const uint32_t*>(buf + i0 - 4);
-      const uint64_t lo = (uint64_t)b4[0] | ((uint64_t)b4[1] << 32);  // bytes [i0 - 4, i0 + 4)
-      const uint32_t hi = b4[2];                                       // bytes [i0 + 4, i0 + 8)
-      auto at = [&](int k) -> uint32_t {  // byte i0 + k, k in [-4, 8)
-        return k < 4 ? (uint32_t)(lo >> (8 * (k + 4))) & 0xFFu : (hi >> (8 * (k - 4))) & 0xFFu;
-      };
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int p = i0 + j;
-        if (p >= n) break;
-        const uint32_t c = at(j);
-        if (c < 0x80) continue;
-        if (c >= 0xC2 && c <= 0xF4) {  // lead: its continuation bytes, inside the row
-          const int need = c >= 0xF0 ? 3 : (c >= 0xE0 ? 2 : 1);
-          const uint32_t lo1 = c == 0xE0 ? 0xA0u : (c == 0xF0 ? 0x90u : 0x80u);
-          const uint32_t hi1 = c == 0xED ? 0x9Fu : (c == 0xF4 ? 0x8Fu : 0xBFu);
-          bool ok = p + need < n;
-#pragma unroll
-          for (int k = 1; k <= 3; ++k)
-            if (k <= need) {
-              const uint32_t d = at(j + k);
-              ok = ok && d >= (k == 1 ? lo1 : 0x80u) && d <= (k == 1 ? hi1 : 0xBFu);
-            }
-          invalid |= !ok;
-        } else if (c >= 0x80 && c <= 0xBF) {  // continuation: the nearest non-continuation byte back
-          int back = 0;
-          uint32_t lead = 0;
-#pragma unroll
-          for (int k = 1; k <= 3; ++k) {
-            const uint32_t d = p - k >= 0 ? at(j - k) : 0u;
-            if (back == 0 && (d < 0x80 || d > 0xBF)) {
-              back = k;
-              lead = d;
-            }
-          }
-          const int need = lead >= 0xF0 ? 3 : (lead >= 0xE0 ? 2 : (lead >= 0xC2 ? 1 : 0));
-          invalid |= back == 0 || lead < 0xC2 || lead > 0xF4 || back > need;
-        } else {
-          invalid = true;  // C0, C1, F5..FF never appear in UTF-8
-        }
-      }
+      if (i0 >= n + 3) continue;
+      const uint32_t* b4 = reinterpret_cast<const uint32_t*>(buf + i0);  // buf[-4, 0), buf[n, n + 8): zero
+      invalid |= utf8_dword_bad(b4[0], b4[-1]) != 0u;
     }
   }
   DSTAMP(4);
