@@ -437,59 +437,109 @@ __device__ __forceinline__ void parse_row(const ParseArgs& a, uint8_t* T, uint8_
   // ---- 4. split(action_sep), strip, drop empties, cap at K (:165-169); name -> id (es :230-240)
   const Tag sep{cfg.sep_lo, cfg.sep_hi, cfg.sep_len};
   int count = 0;
-  if (as >= 0) {
-    // separator candidates: positions of its first byte, full compare, greedy selection
-    const int nc = collect(C, ca, cz, (uint32_t)(sep.lo & 0xFFu), ES, lane);
-    wave_sync();
-    PSTAMP(7);
-    int ns = 0, last = ca;  // selected separators -> EL (the '<' list is no longer needed)
-    for (int c = 0; c < nc; c += 64) {
-      const int i = c + lane;
-      bool m = false;
-      int p = 0;
-      if (i < nc) {
-        p = ES[i];
-        uint64_t lo, hi;
-        load16(C, p, lo, hi);
-        m = p + sep.n <= cz && tag_eq(lo, hi, sep);
-      }
-      uint64_t bits = __ballot(m);
-      while (bits) {  // left to right, non-overlapping (str.split)
-        const int L = __builtin_ctzll(bits);
-        bits &= bits - 1;
-        const int q = __builtin_amdgcn_readlane(p, L);
-        if (q >= last) {
-          if (lane == 0) EL[ns] = (uint16_t)q;
-          ++ns;
-          last = q + sep.n;
-        }
+  // one step of up to 64 pieces, lane i's stripped [s, e) (in: lane i holds a piece): the
+  // non-empty ones take the next slots in order, up to K
+  auto put_pieces = [&](bool in, int s, int e) {
+    const bool keep = in && e > s;
+    const uint64_t km = __ballot(keep);
+    const int slot = count + __builtin_popcountll(km & ((1ull << lane) - 1ull));
+    if (keep && slot < K) {
+      a.actions[b * K + slot] = (int8_t)(nm.n > 0 ? piece_id(C, s, e, nm) : 1);
+      if (a.action_text) {
+        const int L = e - s, Lc = L < a.Lact ? L : a.Lact;
+        uint8_t* dst = a.action_text + (b * K + slot) * (int64_t)a.Lact;
+        for (int q = 0; q < Lc; ++q) dst[q] = C[s + q];
+        a.action_len[b * K + slot] = Lc;
+        if (L > a.Lact) err |= RMI_ERR_UNSUP;
       }
     }
-    wave_sync();
-    PSTAMP(8);
-    // pieces: piece i = [i ? sel[i-1] + sep.n : ca, i < ns ? sel[i] : cz); one per lane
-    for (int c = 0; c <= ns && count < K; c += 64) {
-      const int i = c + lane;
-      int s = 0, e = 0;
-      if (i <= ns) {
-        s = i ? EL[i - 1] + sep.n : ca;
-        e = i < ns ? EL[i] : cz;
-        strip(C, s, e);
-      }
-      const bool keep = e > s;
-      const uint64_t km = __ballot(keep);
-      const int slot = count + __builtin_popcountll(km & ((1ull << lane) - 1ull));
-      if (keep && slot < K) {
-        a.actions[b * K + slot] = (int8_t)(nm.n > 0 ? piece_id(C, s, e, nm) : 1);
-        if (a.action_text) {
-          const int L = e - s, Lc = L < a.Lact ? L : a.Lact;
-          uint8_t* dst = a.action_text + (b * K + slot) * (int64_t)a.Lact;
-          for (int q = 0; q < Lc; ++q) dst[q] = C[s + q];
-          a.action_len[b * K + slot] = Lc;
-          if (L > a.Lact) err |= RMI_ERR_UNSUP;
+    count += __builtin_popcountll(km);
+  };
+  if (as >= 0) {
+    // An all-ASCII answer shorter than 64 bytes (the usual one) is split on bit masks, one byte
+    // per lane: the separator's occurrences are the AND of one ballot per separator byte, the
+    // greedy left-to-right selection (str.split) walks their bits, the pieces' bounds go to
+    // their lanes by a select per piece, and each strip is the first / last non-whitespace bit of the
+    // piece's span — no LDS lists and no per-byte loops.  Anything else takes the lists below.
+    const int La = cz - ca;
+    const uint32_t ch = lane < La ? (uint32_t)C[ca + lane] : 0u;
+    if (La < 64 && __ballot(ch >= 0x80u) == 0) {
+      const uint64_t live = (1ull << La) - 1ull;
+      uint64_t m = La >= sep.n ? live >> (sep.n - 1) : 0ull;  // occurrence starts i, i + sep.n <= La
+      for (int k = 0; k < sep.n; ++k) m &= (__ballot(ch == tag_byte(sep, k)) & live) >> k;
+      PSTAMP(7);
+      uint64_t sel = 0;
+      for (int last = 0; m;) {  // left to right, non-overlapping
+        const int i = __builtin_ctzll(m);
+        m &= m - 1;
+        if (i >= last) {
+          sel |= 1ull << i;
+          last = i + sep.n;
         }
       }
-      count += __builtin_popcountll(km);
+      int ps = 0, pe = 0, np = 0;  // piece np = [ps, pe) on lane np (answer offsets)
+      for (int start = 0;; ++np) {
+        const int end = sel ? __builtin_ctzll(sel) : La;
+        ps = lane == np ? start : ps;
+        pe = lane == np ? end : pe;
+        if (!sel) break;
+        start = end + sep.n;
+        sel &= sel - 1;
+      }
+      ++np;
+      const bool sp = (ch >= 9u && ch <= 13u) || (ch >= 0x1Cu && ch <= 0x20u);  // str.isspace, ASCII
+      const uint64_t text = live & ~__ballot(sp);
+      PSTAMP(8);
+      int s = 0, e = 0;
+      if (lane < np) {
+        const uint64_t in = text & ((1ull << pe) - 1ull) & ~((1ull << ps) - 1ull);  // ps <= pe <= La < 64
+        if (in) {
+          s = ca + __builtin_ctzll(in);
+          e = ca + 64 - __builtin_clzll(in);
+        }
+      }
+      put_pieces(lane < np, s, e);
+    } else {
+      // separator candidates: positions of its first byte, full compare, greedy selection
+      const int nc = collect(C, ca, cz, (uint32_t)(sep.lo & 0xFFu), ES, lane);
+      wave_sync();
+      PSTAMP(7);
+      int ns = 0, last = ca;  // selected separators -> EL (the '<' list is no longer needed)
+      for (int c = 0; c < nc; c += 64) {
+        const int i = c + lane;
+        bool m = false;
+        int p = 0;
+        if (i < nc) {
+          p = ES[i];
+          uint64_t lo, hi;
+          load16(C, p, lo, hi);
+          m = p + sep.n <= cz && tag_eq(lo, hi, sep);
+        }
+        uint64_t bits = __ballot(m);
+        while (bits) {  // left to right, non-overlapping (str.split)
+          const int L = __builtin_ctzll(bits);
+          bits &= bits - 1;
+          const int q = __builtin_amdgcn_readlane(p, L);
+          if (q >= last) {
+            if (lane == 0) EL[ns] = (uint16_t)q;
+            ++ns;
+            last = q + sep.n;
+          }
+        }
+      }
+      wave_sync();
+      PSTAMP(8);
+      // pieces: piece i = [i ? sel[i-1] + sep.n : ca, i < ns ? sel[i] : cz); one per lane
+      for (int c = 0; c <= ns && count < K; c += 64) {
+        const int i = c + lane;
+        int s = 0, e = 0;
+        if (i <= ns) {
+          s = i ? EL[i - 1] + sep.n : ca;
+          e = i < ns ? EL[i] : cz;
+          strip(C, s, e);
+        }
+        put_pieces(i <= ns, s, e);
+      }
     }
     if (count > K) count = K;
   }
