@@ -417,7 +417,21 @@ __device__ __forceinline__ void parse_row(const ParseArgs& a, uint8_t* T, uint8_
     ca = as;
     cz = ae;
     if (next_event(E, -1, ca, cz, lane) < 0) {
-      strip(T, ca, cz);  // every replace is a no-op, and strip() six times is strip() once
+      // every replace is a no-op, and strip() six times is strip() once.  An all-ASCII content of
+      // <= 64 bytes strips on a mask (one byte per lane), anything else byte by byte
+      const int Lr = cz - ca;
+      const uint32_t cr = lane < Lr ? (uint32_t)T[ca + lane] : 0u;
+      if (Lr <= 64 && __ballot(cr >= 0x80u) == 0) {
+        const uint64_t text = __ballot(lane < Lr && !ascii_space(cr));
+        if (text) {
+          cz = ca + 64 - __builtin_clzll(text);
+          ca += __builtin_ctzll(text);
+        } else {
+          ca = cz;
+        }
+      } else {
+        strip(T, ca, cz);
+      }
     } else {
       for (int q = 0; q < 6; ++q) {  // ctx_manager.py:94 order
         const Tag tok = q == 0 ? kThinkOpen
@@ -487,8 +501,7 @@ __device__ __forceinline__ void parse_row(const ParseArgs& a, uint8_t* T, uint8_
         sel &= sel - 1;
       }
       ++np;
-      const bool sp = (ch >= 9u && ch <= 13u) || (ch >= 0x1Cu && ch <= 0x20u);  // str.isspace, ASCII
-      const uint64_t text = live & ~__ballot(sp);
+      const uint64_t text = live & ~__ballot(ascii_space(ch));
       PSTAMP(8);
       int s = 0, e = 0;
       if (lane < np) {

@@ -17,6 +17,8 @@ __device__ __forceinline__ int ws_len3(uint32_t c, uint32_t c1, uint32_t c2) {
   if (c == 0xE3) return (c1 == 0x80 && c2 == 0x80) ? 3 : 0;
   return 0;
 }
+// str.isspace of an ASCII byte (ws_len3's first line)
+__device__ __forceinline__ bool ascii_space(uint32_t c) { return (c >= 9u && c <= 13u) || (c >= 0x1Cu && c <= 0x20u); }
 // ... starting at p inside [.., lim), or 0
 __device__ __forceinline__ int ws_fwd(const uint8_t* V, int p, int lim) {
   if (p >= lim) return 0;
