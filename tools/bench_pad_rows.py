@@ -17,7 +17,7 @@ arena = torch.randint(0, 150000, (n, cap), generator=g, dtype=torch.int64).to(de
 tail = torch.tensor([151644, 77091, 198], dtype=torch.int64, device=dev)
 rows = torch.arange(n, dtype=torch.int64, device=dev)
 out = {}
-for S in (160, 300, 500, 700):
+for S in (160, 500, 700, 1001, 1100):
     alen = (S - 3 - torch.randint(0, 40, (n,), generator=g)).clamp(min=1).to(torch.int32).to(dev)
     for _ in range(3):
         ops.pad_rows(arena, alen, rows, tail, S, 151643)
