@@ -540,6 +540,11 @@ typedef struct {
   const uint8_t* sel;           /* [B] name-id column, or NULL                                  */
   int32_t* spans;               /* [B, 4] or NULL                                               */
   uint8_t* parse_err;           /* [B] or NULL                                                  */
+  /* has != NULL: rmi_turn_inputs between the decode and the turn (the turn chain's step 3): has[b]
+   * = (has_t == NULL || has_t[b]) && decode_err[b] == 0, err[b] zeroed; in->has_input must be
+   * has and decode_err non-NULL.                                                                */
+  const uint8_t* has_t;
+  uint8_t* has;
 } rmi_token_rows_t;
 int rmi_sokoban_token_turn(const rmi_token_rows_t* tok, const rmi_sokoban_t* env, const rmi_episode_t* ep,
                            const rmi_turn_t* in, uint8_t* err, const rmi_finalize_t* fin, const uint8_t* init_state,

@@ -83,7 +83,8 @@ class TokenRows(ctypes.Structure):
     _fields_ = [("ids", c_void_p), ("R", c_int64), ("n_ids", c_void_p), ("vocab_packed", c_void_p),
                 ("vocab_bytes", c_void_p), ("n_bytes", c_int64), ("V", c_int64), ("text", c_void_p),
                 ("stride", c_int32), ("text_len", c_void_p), ("decode_err", c_void_p), ("cfg", ctypes.POINTER(ParseCfg)),
-                ("sel", c_void_p), ("spans", c_void_p), ("parse_err", c_void_p)]
+                ("sel", c_void_p), ("spans", c_void_p), ("parse_err", c_void_p), ("has_t", c_void_p),
+                ("has", c_void_p)]
 
 
 PROMPT_MAX_PIECES = 32

@@ -36,15 +36,9 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
                               c.src ? c.n_ids : nullptr, c.src ? c.has_t : nullptr, c.raw_max, c.raw_next, s);
     if (rc) return rc;
   }
-  // 2. decode + parse
-  rc = rmi_detok_parse(c.ids, B, c.R, c.n_ids, c.vocab_packed, c.vocab_bytes, c.vocab_n_bytes, c.V,
-                       c.text, c.stride, c.text_len, c.dec_err, c.parse, c.sel, c.actions, c.n_actions, c.spans,
-                       nullptr, nullptr, 0, c.parse_err, s);
-  if (rc) return rc;
-  // 3. the envs that step: a generation, decoded without error; the step errors zeroed
-  rc = rmi_turn_inputs(c.has_t, c.dec_err, B, c.has, c.err, s);
-  if (rc) return rc;
-  // 4. the turn and the next observation
+  // 2-4. decode + parse; the envs that step (a generation, decoded without error; the step errors
+  //      zeroed); the turn and the next observation.  Sokoban: one launch (rmi_sokoban_token_turn,
+  //      which runs the three steps' launches itself for layouts it does not fuse)
   rmi_turn_t in;
   in.turn = c.turn;
   in.K = c.K;
@@ -54,9 +48,31 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
   in.max_actions_per_traj = c.max_actions_per_traj;
   in.format_penalty = c.format_penalty;
   if (c.env_kind == RMI_CHAIN_SOKOBAN) {
-    rc = rmi_sokoban_step_turn_render(c.sokoban, c.ep, &in, c.err, nullptr, nullptr, nullptr, c.obs, s);
+    rmi_token_rows_t tok;
+    tok.ids = c.ids;
+    tok.R = c.R;
+    tok.n_ids = c.n_ids;
+    tok.vocab_packed = c.vocab_packed;
+    tok.vocab_bytes = c.vocab_bytes;
+    tok.n_bytes = c.vocab_n_bytes;
+    tok.V = c.V;
+    tok.text = c.text;
+    tok.stride = c.stride;
+    tok.text_len = c.text_len;
+    tok.decode_err = c.dec_err;
+    tok.cfg = c.parse;
+    tok.sel = c.sel;
+    tok.spans = c.spans;
+    tok.parse_err = c.parse_err;
+    tok.has_t = c.has_t;
+    tok.has = c.has;
+    rc = rmi_sokoban_token_turn(&tok, c.sokoban, c.ep, &in, c.err, nullptr, nullptr, nullptr, c.obs, s);
   } else {
-    rc = rmi_frozenlake_step_turn(c.frozenlake, c.ep, &in, c.err, s);
+    rc = rmi_detok_parse(c.ids, B, c.R, c.n_ids, c.vocab_packed, c.vocab_bytes, c.vocab_n_bytes, c.V, c.text,
+                         c.stride, c.text_len, c.dec_err, c.parse, c.sel, c.actions, c.n_actions, c.spans, nullptr,
+                         nullptr, 0, c.parse_err, s);
+    if (!rc) rc = rmi_turn_inputs(c.has_t, c.dec_err, B, c.has, c.err, s);
+    if (!rc) rc = rmi_frozenlake_step_turn(c.frozenlake, c.ep, &in, c.err, s);
     if (!rc)
       rc = rmi_frozenlake_render(c.frozenlake, (int32_t)B, c.obs->glyph_bytes, c.obs->glyph_len, c.obs->out,
                                  c.obs->stride, c.obs->len, s);
@@ -99,9 +115,10 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
   const int64_t longest = tail[2], any_bad = tail[3], count = tail[4];
   if (any_bad || count < 1 || count > B || longest < 0) return RMI_OK;
   const int64_t S = longest + c.pad_tail_n;
-  if (S < 1 || 3 * count * S > c.pad_cap) return RMI_OK;
+  const int64_t P = (count * S + 1) & ~(int64_t)1;  // the outputs at k * P: 16-B aligned alike (column pairs)
+  if (S < 1 || 3 * P > c.pad_cap) return RMI_OK;
   rc = rmi_pad_rows(c.arena, c.arena_stride, c.arena_len, c.next_rows, count, c.pad_tail, c.pad_tail_n, S, c.pad_id,
-                    c.pad_block, c.pad_block + count * S, c.pad_block + 2 * count * S, c.pad_err_next, s);
+                    c.pad_block, c.pad_block + P, c.pad_block + 2 * P, c.pad_err_next, s);
   if (rc) return rc;
   *c.pad_S_out = S;
   return RMI_OK;

@@ -701,9 +701,9 @@ struct DetokArgs {
 
 // Row b decoded into buf (dword aligned; 4 writable bytes before it and stride + 8 after; fix:
 // a second such buffer for the rare lossy rewrite, copied back), then written to out / out_len
-// / err_out.  -> the decoded length (the row stays in buf).
+// / err_out (and *derr, wave-uniform, when given).  -> the decoded length (the row stays in buf).
 __device__ __forceinline__ int detok_row(const DetokArgs& d, uint8_t* buf, uint8_t* fix, int64_t b,
-                                         int lane DSTAMP_PARAM) {
+                                         int lane DSTAMP_PARAM, uint8_t* derr = nullptr) {
   const int stride = d.stride;
   int64_t rn = d.n_ids ? (int64_t)d.n_ids[b] : d.R;
   rn = rn < 0 ? 0 : (rn > d.R ? d.R : rn);
@@ -824,9 +824,11 @@ __device__ __forceinline__ int detok_row(const DetokArgs& d, uint8_t* buf, uint8
   const uint32_t* r4 = reinterpret_cast<const uint32_t*>(buf);
   for (int i = lane; i < nw; i += 64) o4[i] = r4[i];
   const uint64_t any_bad = __ballot(bad), any_over = __ballot(over);
+  const uint8_t de = (uint8_t)((any_bad ? RMI_ERR_INDEX : 0) | (any_over ? RMI_ERR_UNSUP : 0));
+  if (derr) *derr = de;
   if (lane == 0) {
     d.out_len[b] = n;
-    if (d.err_out) d.err_out[b] = (uint8_t)((any_bad ? RMI_ERR_INDEX : 0) | (any_over ? RMI_ERR_UNSUP : 0));
+    if (d.err_out) d.err_out[b] = de;
   }
   DSTAMP(5);
   return n;

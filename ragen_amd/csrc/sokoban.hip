@@ -1074,7 +1074,7 @@ template <bool kFin, bool kFirst>
 __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu(8))) void sokoban_token_turn_kernel(
     DetokArgs d, ParseArgs a, rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in, uint64_t border,
     uint8_t* __restrict__ err_out, rmi_finalize_t fin, const uint8_t* __restrict__ init_state,
-    const int8_t* __restrict__ init_player, ObsOut obs) {
+    const int8_t* __restrict__ init_player, ObsOut obs, const uint8_t* __restrict__ has_t, uint8_t* __restrict__ has) {
   extern __shared__ uint64_t lds_q[];  // kTokEnvs parse regions (parse_lds(stride) each)
   __shared__ uint32_t lds_state[kTokEnvs * 9], lds_fixed[kTokEnvs * 9];
   __shared__ TokRec rec[kTokEnvs];
@@ -1115,7 +1115,12 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
 #ifdef RMI_PARSE_STAMPS
     unsigned long long pst_[10], dst_[6];
 #endif
-    const int n = detok_row(d, T + kPre, Wb + kPre, b, lane DSTAMP_ARG);
+    uint8_t derr;
+    const int n = detok_row(d, T + kPre, Wb + kPre, b, lane DSTAMP_ARG, &derr);
+    if (has && lane == 0) {  // rmi_turn_inputs: the env steps when it has a generation decoded without error
+      has[b] = ((!has_t || has_t[b]) && derr == 0) ? 1 : 0;
+      err_out[b] = 0;
+    }
     parse_row(a, T, Wb, EL, ES, EI, b, n, 0, nm, lane PSTAMP_ARG);
   }
   __syncthreads();  // the group's actions (global stores of its parse waves) visible to wave 0
@@ -1459,6 +1464,7 @@ RMI_API int rmi_sokoban_token_turn(const rmi_token_rows_t* tok, const rmi_sokoba
   if (!tok || !ep || !in || !obs || !tok->cfg || (fin && init_state) || (!init_state) != (!init_player))
     return RMI_EINVAL;
   if (tok->cfg->K != in->K) return RMI_EINVAL;
+  if (tok->has && (in->has_input != tok->has || !tok->decode_err || !err)) return RMI_EINVAL;
   const int64_t B = ep->B;
   DetokArgs d;
   ParseArgs a;
@@ -1476,12 +1482,16 @@ RMI_API int rmi_sokoban_token_turn(const rmi_token_rows_t* tok, const rmi_sokoba
   const int H = env->H, W = env->W;
   const size_t shm = (size_t)kTokEnvs * parse_lds(tok->stride);
   const bool fused = H * W == 36 && (H - 1) * W <= 32 && H * (W + 1) - 1 <= kWave && (!fin || kTokEnvs % fin->group_size == 0) &&
-                     shm + tok_static_lds() <= 56 * 1024 && o.stride <= obs_pitch_max(36);
+                     shm + tok_static_lds() <= 64 * 1024 && o.stride <= obs_pitch_max(36);
   if (!fused) {  // the two calls
     rc = rmi_detok_parse(tok->ids, B, tok->R, tok->n_ids, tok->vocab_packed, tok->vocab_bytes, tok->n_bytes, tok->V,
                          tok->text, tok->stride, tok->text_len, tok->decode_err, tok->cfg, tok->sel, const_cast<int8_t*>(in->actions),
                          const_cast<uint8_t*>(in->n_actions), tok->spans, nullptr, nullptr, 0, tok->parse_err, stream);
     if (rc != RMI_OK) return rc;
+    if (tok->has) {
+      rc = rmi_turn_inputs(tok->has_t, tok->decode_err, B, tok->has, err, stream);
+      if (rc != RMI_OK) return rc;
+    }
     return rmi_sokoban_step_turn_render(env, ep, in, err, fin, init_state, init_player, obs, stream);
   }
   uint64_t border = 0;
@@ -1492,12 +1502,12 @@ RMI_API int rmi_sokoban_token_turn(const rmi_token_rows_t* tok, const rmi_sokoba
   hipStream_t s = as_stream(stream);
   if (fin)
     hipLaunchKernelGGL((sokoban_token_turn_kernel<true, false>), grid, block, shm, s, d, a, *env, *ep, *in, border, err, f,
-                       nullptr, nullptr, o);
+                       nullptr, nullptr, o, tok->has_t, tok->has);
   else if (init_state)
     hipLaunchKernelGGL((sokoban_token_turn_kernel<false, true>), grid, block, shm, s, d, a, *env, *ep, *in, border, err, f,
-                       init_state, init_player, o);
+                       init_state, init_player, o, tok->has_t, tok->has);
   else
     hipLaunchKernelGGL((sokoban_token_turn_kernel<false, false>), grid, block, shm, s, d, a, *env, *ep, *in, border, err,
-                       f, nullptr, nullptr, o);
+                       f, nullptr, nullptr, o, tok->has_t, tok->has);
   return launch_status();
 }

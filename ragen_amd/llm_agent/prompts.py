@@ -845,7 +845,8 @@ class DevicePrompts:
             # over the same rows, width and block: TurnChain.run)
             n = rows.numel()
             blk = ep[3]
-            ids, am, pos = (blk.as_strided((n, S), (S, 1), blk.storage_offset() + k * n * S) for k in range(3))
+            P = (n * S + 1) & ~1  # the outputs at k * P (rmi_turn_chain's step 8)
+            ids, am, pos = (blk.as_strided((n, S), (S, 1), blk.storage_offset() + k * P) for k in range(3))
             err = ep[4][:n]
             self.chain_padded += 1
         else:
@@ -868,8 +869,8 @@ class DevicePrompts:
             if buf is None or _uses(bst) > 2 or _uses(est) > 2:
                 return None
             return buf, err
-        if buf is None or buf.numel() < 3 * n * S or _uses(bst) > 2:
-            buf = torch.empty(max(3 * max(n, self.n_envs) * (S + S // 4), 1), dtype=torch.int64, device=self.device)
+        if buf is None or buf.numel() < 3 * (n * S + 1) or _uses(bst) > 2:
+            buf = torch.empty(3 * (max(n, self.n_envs) * (S + S // 4) + 1), dtype=torch.int64, device=self.device)
             bst = buf.untyped_storage()
         if err is None or _uses(est) > 2:
             err = torch.empty(self.n_envs, dtype=torch.uint8, device=self.device)
@@ -879,13 +880,14 @@ class DevicePrompts:
 
     def _pad_rows(self, rows, S):
         """rmi_pad_rows into the batch's own tensors (ops.pad_rows without its argument checks:
-        every operand is this builder's).  The outputs are one [3, n, S] block; the block the
+        every operand is this builder's).  The outputs are views of one block at k * P (P = n S
+        rounded up to even); the block the
         previous batch of the same shape class used is taken again when nothing outside holds
         it any more (its storage's use count), else a fresh one is allocated."""
         n = rows.numel()
-        need = 3 * n * S
+        P = (n * S + 1) & ~1  # the three outputs at k * P: 16-B aligned alike (rmi_pad_rows' column pairs)
         buf, err = self.batch_block(self.turns_done, n, S)
-        ids, am, pos = buf[:need].view(3, n, S).unbind(0)
+        ids, am, pos = (buf[k * P:k * P + n * S].view(n, S) for k in range(3))
         err = err[:n]
         ops.check(_lib.lib().rmi_pad_rows(self.arena_p, self.arena_stride, self.len_p, rows.data_ptr(), n,
                                           self.tail_p, self.tail_n, int(S), int(self.pad_id), ids.data_ptr(),

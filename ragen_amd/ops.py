@@ -967,7 +967,9 @@ def pad_rows(arena: torch.Tensor, arena_len: torch.Tensor, rows: torch.Tensor, t
     _dt(tail, torch.int64, "tail")
     n = rows.numel()
     dev = arena.device
-    ids, am, pos = torch.empty(3, n, S, dtype=torch.int64, device=dev).unbind(0)  # one allocation
+    P = (n * S + 1) & ~1  # one allocation, the outputs at k * P: 16-B aligned alike (column pairs)
+    flat = torch.empty(3 * P, dtype=torch.int64, device=dev)
+    ids, am, pos = (flat[k * P:k * P + n * S].view(n, S) for k in range(3))
     err = torch.empty(n, dtype=torch.uint8, device=dev)
     check(lib().rmi_pad_rows(_ptr(arena), arena.shape[1], _ptr(arena_len), _ptr(rows), n, _ptr(tail), tail.numel(),
                              int(S), int(pad_id), _ptr(ids), _ptr(am), _ptr(pos), _ptr(err), _stream(dev)),
