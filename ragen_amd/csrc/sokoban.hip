@@ -1060,6 +1060,23 @@ __global__ __launch_bounds__(kBlock) void sokoban_load_rooms_kernel(rmi_sokoban_
 // count of the token path drops from three (decode + parse, turn, render) to one, and the turn's
 // and the render's launches (their ramps and tails) go with it.
 constexpr int kTokEnvs = 16;
+// Diagnostic build only (tools/prof_token_turn.py compiles this file with RMI_TOK_STAMPS): per wave
+// s_memtime at the phase boundaries and s_memrealtime at entry / exit, written once at the end.
+#ifdef RMI_TOK_STAMPS
+__device__ unsigned long long* g_tok_stamps;
+#define TST_DECL unsigned long long tst_[8] = {0}; tst_[0] = __builtin_amdgcn_s_memrealtime(); tst_[1] = __builtin_amdgcn_s_memtime()
+#define TST(i) (tst_[i] = __builtin_amdgcn_s_memtime())
+#define TST_FLUSH(w)                                                                              \
+  do {                                                                                            \
+    tst_[7] = __builtin_amdgcn_s_memrealtime();                                                   \
+    if ((threadIdx.x & 63) == 0 && g_tok_stamps)                                                  \
+      for (int s_ = 0; s_ < 8; ++s_) g_tok_stamps[((int64_t)blockIdx.x * kTokEnvs + (w)) * 8 + s_] = tst_[s_]; \
+  } while (0)
+#else
+#define TST_DECL do {} while (0)
+#define TST(i) do {} while (0)
+#define TST_FLUSH(w) do {} while (0)
+#endif
 constexpr int kTokRowWords = 48;  // >= (36 * 4 + 35 + 3) / 4: the longest 36-cell observation, in dwords
 struct TokRec {                  // an env's state after the turn (36-cell room, u32 board window)
   uint32_t xs[9], xf[9];
@@ -1091,6 +1108,7 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
   // wave-uniform in SGPRs (a VGPR copy of the wave index was spilled and reloaded from scratch)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t b0 = (int64_t)blockIdx.x * kTokEnvs, b = b0 + wv;
+  TST_DECL;
   if (threadIdx.x < 18) gb[threadIdx.x] = threadIdx.x < 16 ? obs.gb[threadIdx.x] : (threadIdx.x == 16 ? '?' : '\n');
   if (threadIdx.x == 64) {
     rp.out = obs.out;
@@ -1123,7 +1141,9 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
     }
     parse_row(a, T, Wb, EL, ES, EI, b, n, 0, nm, lane PSTAMP_ARG);
   }
+  TST(2);
   __syncthreads();  // the group's actions (global stores of its parse waves) visible to wave 0
+  TST(3);
 
   // ---- 2. the turn of the group's envs: kLpeT = 16 lanes per env on the first 4 waves (env
   //         b0 + t / 16 for thread t): one row dword per lane keeps the turn inside the parse's
@@ -1154,7 +1174,9 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
         });
   }
 #endif
+  TST(4);
   __syncthreads();
+  TST(5);
   // ---- 3. the last turn: rmi_rollout_finalize's work for the group's envs on wave 0, one lane per
   //         env (finalize_envs, as the fused turn form runs it), from the record the turn just wrote
   if constexpr (kFin) {
@@ -1172,7 +1194,10 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
 
   // ---- 4. env b's observation (rmi_sokoban_render's row): token t = lane, t = r * (W + 1) + c is
   //         cell (r, c) for c < W, a newline for c == W
-  if (b >= rp.B) return;
+  if (b >= rp.B) {
+    TST_FLUSH(wv);
+    return;
+  }
   const int H = rp.H, W = rp.W, T = H * (W + 1) - 1;
   const TokRec& R = rec[wv];
   const int r = lane / (W + 1), c = lane - r * (W + 1);
@@ -1207,6 +1232,8 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
   wave_sync();
   if (lane < nw) reinterpret_cast<uint32_t*>(rp.out + b * (int64_t)rp.stride)[lane] = row[lane];
   if (lane == 0) rp.len[b] = total;
+  TST(6);
+  TST_FLUSH(wv);
 }
 
 }  // namespace
@@ -1303,6 +1330,11 @@ int sokoban_check(const rmi_sokoban_t* env) {
 }  // namespace
 }  // namespace rmi
 
+#ifdef RMI_TOK_STAMPS
+RMI_API int rmi_tok_set_stamps(unsigned long long* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_tok_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
+}
+#endif
 #ifdef RMI_STAMPS
 RMI_API int rmi_sokoban_set_stamps(unsigned long long* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(rmi::g_stamps), &buf, sizeof(buf)) == hipSuccess ? 0 : -2;
