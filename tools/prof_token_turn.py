@@ -50,6 +50,11 @@ def main():
           f"wait A {wait_a.mean():.0f} | turn (turn waves) {turn[tw].mean():.0f} / {np.percentile(turn[tw], 90):.0f} | "
           f"wait B (other waves) {wait_b[~tw].mean():.0f} (turn waves {wait_b[tw].mean():.0f}) | render {render.mean():.0f} / "
           f"{np.percentile(render, 90):.0f}")
+    tl = oa["text_len"].cpu().numpy()
+    for lo, hi in ((0, 128), (128, 192), (192, 256), (256, 320), (320, 4096)):
+        m = (tl >= lo) & (tl < hi)
+        if m.any():
+            print(f"  text {lo}-{hi} B: {m.sum()} rows, parse mean {parse[m].mean():.0f} p90 {np.percentile(parse[m], 90):.0f}")
     g = s.reshape(-1, 16, 8)
     t_parse_max = (g[:, :, 2] - g[:, :, 1].min(1, keepdims=True)).max(1)
     t_end = (g[:, :, 6] - g[:, :, 1].min(1, keepdims=True)).max(1)
