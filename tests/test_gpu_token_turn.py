@@ -6,7 +6,9 @@ state and the whole episode record, the turn's error bytes, every observation ro
 and the finalize's outputs.  Covered: the three turn forms over a 5-turn rollout, partial
 has_input masks, batches that end inside a workgroup, waves on the exact path with absent and
 4-byte glyphs, finalize groups of 4 and 16 (fused) and 32 (the two-call form), and room layouts
-the fused launch does not take (a u64 board window, 8x8 rooms), which run the two calls."""
+the fused launch does not take (a u64 board window, 8x8 rooms), which run the two calls; and the
+turn-inputs form the turn chain takes (has set: rmi_turn_inputs between the decode and the turn,
+decode errors, a partial has_t), fused and through the separate launches."""
 import numpy as np
 import pytest
 import torch
@@ -138,3 +140,46 @@ def test_token_turn_validation(device):
     with pytest.raises(ValueError):  # first and last form together
         ops.sokoban_token_turn(tok, a.struct(), a.ep, ts, r, fin=fin, init_state=a.init_state,
                                init_player=a.init_player)
+
+
+@pytest.mark.parametrize("pad", [0, 600])
+def test_token_turn_with_turn_inputs(device, pad):
+    """has set (the turn chain's steps 2-4 in one call): == rmi_detok_parse, rmi_turn_inputs, then
+    the turn with the render; rows with out-of-range ids (decode errors: those envs do not step)
+    and a partial has_t.  pad widens the rows past the fused launch's LDS, so the call runs the
+    separate launches itself."""
+    B = 4096
+    (a, b), rng = _pair(device, B, 6, 6, 1, seed=21 + pad)
+    cfg, vt, toks, stride = _tokens(device, B, 2, 5, 21)
+    stride += pad
+    glk = a.config.grid_lookup
+    for t in range(2):
+        tk = toks[t].clone()
+        tk[::37, 3] = 10 ** 9  # an id outside the vocabulary: RMI_ERR_INDEX in the decode
+        has_t = torch.from_numpy((rng.random(B) < 0.8).astype(np.uint8)).to(device)
+        kw_a = {"init_state": a.init_state, "init_player": a.init_player} if t == 0 else {}
+        kw_b = {"init_state": b.init_state, "init_player": b.init_player} if t == 0 else {}
+        oa = ops.detok_parse(tk, vt, stride, cfg)
+        torch.cuda.synchronize()
+        _dirty(oa)
+        tok = ops.token_rows_struct(tk, vt, cfg, oa)
+        has_a = torch.full((B,), 7, dtype=torch.uint8, device=device)
+        tok.has_t, tok.has = has_t.data_ptr(), has_a.data_ptr()
+        ea = torch.full((B,), 0x55, dtype=torch.uint8, device=device)  # zeroed by the turn inputs
+        tsa = ops.turn_struct(t, oa["actions"], oa["n_actions"], has_a, 10, -0.1)
+        obs_a = ops.render_buffers(B, 6, 6, device)
+        ops.sokoban_token_turn(tok, a.struct(), a.ep, tsa, ops.render_struct(glk, 6, 6, *obs_a), err=ea, **kw_a)
+        ob = ops.detok_parse(tk, vt, stride, cfg)
+        has_b = torch.empty(B, dtype=torch.uint8, device=device)
+        eb = torch.full((B,), 0x55, dtype=torch.uint8, device=device)
+        ops.turn_inputs(has_t, ob["decode_err"], has_b, eb)
+        tsb = ops.turn_struct(t, ob["actions"], ob["n_actions"], has_b, 10, -0.1)
+        obs_b = ops.render_buffers(B, 6, 6, device)
+        ops.sokoban_step_turn_render(b.struct(), b.ep, tsb, ops.render_struct(glk, 6, 6, *obs_b), err=eb, **kw_b)
+        torch.cuda.synchronize()
+        assert int(ob["decode_err"].ne(0).sum()) > 0 and int(has_b.eq(0).sum()) > 0
+        for k in ("text_len", "decode_err", "actions", "n_actions", "spans", "err"):
+            assert torch.equal(oa[k], ob[k]), (t, k)
+        assert torch.equal(has_a, has_b) and torch.equal(ea, eb), t
+        _state_equal(a, b, t)
+        _rows_equal(obs_a, obs_b)
