@@ -1057,7 +1057,43 @@ def serial_exchange(step, chunk, outs, G, p, gather=None):
             gather(chunk(p, k), outs[k])
 
 
-def exchange_label(mode, P, G, asked, graph):
+def setup_ipc_exchange(nbytes, device, src, probes=4):
+    """The one-shot exchange (ragen_amd.exchange) for this rank's arena of nbytes, checked before
+    use: `probes` eager exchanges of src, each gathered slot checked with check_gathered (every
+    rank's row against the digest its owner all-gathered).  Collective.  -> (ArenaExchange or
+    None, reason): None on every rank when any rank failed the setup or a probe (the caller
+    then gathers with RCCL)."""
+    from ragen_amd import exchange as xgm
+    try:
+        xg = xgm.ArenaExchange(nbytes, device)
+    except Exception as ex:  # raised on every rank alike (the setup agrees after each step)
+        return None, f"setup failed: {ex}"
+    ok, why = True, ""
+    try:
+        g = torch.Generator(device="cpu").manual_seed(7919 + xg.rank)
+        for _ in range(probes):  # rank-distinct bytes: a row landing in the wrong place fails
+            src.copy_(torch.randint(0, 256, (nbytes,), dtype=torch.uint8, generator=g))
+            xg.run(src)
+            ok = check_gathered(src.reshape(-1), xg.slot().contiguous().view(-1), xg.world, xg.rank,
+                                distinct=True) and ok
+        torch.cuda.synchronize()
+        err = xg.error()
+        ok = ok and err == 0
+        why = f"probe: rows {'ok' if ok else 'WRONG'}, err bits {err}"
+    except Exception as ex:
+        ok, why = False, f"probe raised: {ex}"
+    if not xgm.agree(ok):
+        tdist.barrier()
+        xg.close()
+        return None, why or "probe failed on another rank"
+    xg.sync_epoch()
+    return xg, why
+
+
+def exchange_label(mode, P, G, asked, graph, transport="rccl"):
+    if transport == "ipc" and graph and mode == "serial" and P == 1:
+        return ("one-shot exchange of the episode arena after every rollout, serial on the same stream (StarPO "
+                "order): every rank stores its arena into every rank's IPC-mapped region, one launch")
     if not graph:
         return "all-gather of the episode arena after every rollout, serial (eager)"
     if mode == "overlap":
@@ -1128,6 +1164,10 @@ def make_parser():
                          "gathered before its update, as agent_trainer.fit does; >1 amortises it: an extra)")
     ap.add_argument("--double-buffer", action="store_true",
                     help="run the N>1 exchange path at N=1 (a 1-rank RCCL group, real collectives)")
+    ap.add_argument("--transport", choices=("auto", "ipc", "rccl"), default="auto",
+                    help="N>1: how the per-rollout arena gather moves bytes: 'ipc' = the one-shot exchange "
+                         "(every rank stores its arena into every peer's IPC-mapped region, rmi_xgather), 'rccl' = "
+                         "RCCL's all-gather; 'auto' = ipc when its setup and probe pass on every rank, else rccl")
     return ap
 
 
@@ -1186,6 +1226,7 @@ def main():
 
     graph = None
     variants = None
+    transport, xg, xg_note = ("rccl" if dist else None), None, None
     if not args.no_graph:
         s = torch.cuda.Stream(device)
         s.wait_stream(torch.cuda.current_stream(device))
@@ -1237,6 +1278,30 @@ def main():
                 serial_exchange(step, lambda q, k: chunk(h, q, k), outs[p][h], G, p)
 
             serial_g = {p: [capture(lambda h=h, p=p: serial_body(h, p)) for h in (0, 1)] for p in outs}
+            # the one-shot exchange (ipc): every rollout's arena stored into every rank's region
+            # by one launch right after the rollout, on the same stream (the StarPO order)
+            xg, xg_note = None, "--transport rccl"
+            if args.transport != "rccl":
+                xg, xg_note = setup_ipc_exchange(arena_bytes, device,
+                                                 torch.empty(arena_bytes, dtype=torch.uint8, device=device))
+                if xg is None and args.transport == "ipc":
+                    raise RuntimeError(f"--transport ipc: {xg_note}")
+            transport = "ipc" if xg is not None else "rccl"
+            if xg is not None:
+                def ipc_body(h):
+                    def step(j):
+                        R.env.ep = eps[h * G + j]
+                        R.step()
+                    serial_exchange(step, lambda q, k: chunk(h, q, k), [None] * G, G, 1,
+                                    gather=lambda src, out: xg.run(src))
+
+                ipc_g = [capture(lambda h=h: ipc_body(h)) for h in (0, 1)]
+                xg.sync_epoch()  # (capture recorded the launches without running them)
+
+                def run_ipc():
+                    ipc_g[(count[0] // G) & 1].replay()
+                    count[0] += G
+                    xg.advance(G)
             gather_g = [capture(lambda h=h: rd.gather_bytes(sets[h], outs[G][h][0]), stream=cap_s) for h in (0, 1)]
             R.env.ep = eps[0]
             rolled = [torch.cuda.Event(), torch.cuda.Event()]
@@ -1277,11 +1342,18 @@ def main():
                 t_se = min(trial(run_serial_p(G)) for _ in range(3))
                 exchange_mode = "overlap" if t_ov <= t_se else "serial"
             run = run_overlap if exchange_mode == "overlap" else run_serial_p(P)
+            if transport == "ipc" and exchange_mode == "serial" and P == 1:
+                run = run_ipc
+            else:
+                transport = "rccl"  # (the amortised placements gather with RCCL)
 
             def variants_fn():
                 """ms per rollout of every placement, max over ranks, best of 3 trials of 4 replays
-                each: the StarPO form (a gather per rollout, serial) beside the amortised ones."""
+                each: the StarPO form (a gather per rollout, serial) over RCCL and over the
+                one-shot exchange, beside the amortised ones."""
                 forms = {"serial_gather_per_rollout": run_serial_p(1)}
+                if xg is not None:
+                    forms["ipc_one_shot_per_rollout"] = run_ipc
                 if G > 1:
                     forms[f"serial_gather_per_{G}_rollouts"] = run_serial_p(G)
                     forms[f"overlap_gather_per_{G}_rollouts"] = run_overlap
@@ -1335,7 +1407,20 @@ def main():
     gathered_info = None
     if graph is not None:
         exchange_ok = all(torch.equal(e.arena, eps[0].arena) for e in eps)
-        if dist:
+        if dist and transport == "ipc":
+            r = tdist.get_rank()
+            torch.cuda.synchronize()
+            for e in (xg.epoch - 1, xg.epoch):  # the two slots: the last two rollouts' gathers
+                exchange_ok = check_gathered(eps[0].arena, xg.slot(e).contiguous().view(-1), W, r,
+                                             distinct=True) and exchange_ok
+            xg_err = xg.error()
+            exchange_ok = exchange_ok and xg_err == 0
+            gathered_info = {"ranks": W, "bytes_per_rank_per_gather": int(arena_bytes),
+                             "bytes_per_gather": int(W * arena_bytes), "rollouts_per_gather": 1,
+                             "transport": "ipc", "exchanges": xg.epoch, "err_bits": xg_err,
+                             "check": "every rank's row of the last two gathered slots == the i64 digest that "
+                                      "rank all-gathered of its own arena; own row byte for byte"}
+        elif dist:
             r = tdist.get_rank()
             p_run = G if exchange_mode == "overlap" else P
             for h in (0, 1):
@@ -1344,6 +1429,7 @@ def main():
                                                  distinct=True) and exchange_ok
             gathered_info = {"ranks": W, "bytes_per_rank_per_gather": int(p_run * arena_bytes),
                              "bytes_per_gather": int(W * p_run * arena_bytes), "rollouts_per_gather": p_run,
+                             "transport": "rccl",
                              "check": "every rank's row of every gathered chunk == the i64 digest that rank "
                                       "all-gathered of its own chunk; own row byte for byte"}
         ok_t = torch.tensor([1 if exchange_ok else 0], dtype=torch.int32, device=device)
@@ -1451,6 +1537,7 @@ def main():
                        "envs_per_gpu": B_PER_GPU, "env_steps_per_rollout_rank0": steps_per_rollout,
                        "graph": graph is not None, "rollouts_per_replay": G, "parallelism": f"env-sharded x{world}",
                        "exchange_mode": exchange_mode if dist else None,
+                       "exchange_transport": transport, "exchange_transport_note": xg_note,
                        "rollouts_per_gather": (G if exchange_mode == "overlap" else P) if dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -1475,7 +1562,7 @@ def main():
             "toytext": toytext,
             "api_variant": api,
             "text_api": text,
-            "exchange": exchange_label(exchange_mode, P, G, args.exchange, graph is not None) if dist else None,
+            "exchange": exchange_label(exchange_mode, P, G, args.exchange, graph is not None, transport) if dist else None,
             "exchange_variants_ms_per_rollout": variants,
             "records_checked": exchange_ok,
             "gathered": gathered_info,
@@ -1484,6 +1571,10 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if dist:
+        if xg is not None:
+            torch.cuda.synchronize()
+            tdist.barrier()  # no rank unmaps a region a peer may still store into
+            xg.close()
         tdist.destroy_process_group()
 
 

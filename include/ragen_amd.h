@@ -830,7 +830,10 @@ int64_t rmi_host_live_ids(const uint8_t* flags, int64_t n, uint32_t done_bits, i
  *      next get_lm_inputs' batch, ctx_manager.py:265-278, built while the host reads the
  *      readback) and *pad_S_out = S; else *pad_S_out = 0 and nothing is launched.
  * One env tag (one env batch) per chain.  A step that fails returns its code at once (the
- * steps before it are enqueued; nothing after it is).                                       */
+ * steps before it are enqueued; nothing after it is).  next_rows or pad_block set without
+ * prompt and stats is RMI_EINVAL before anything is enqueued: steps 7-8 read the stats that
+ * only step 6 writes.  The readback's host buffer is looked up (pinned or pageable) on every
+ * call; nothing about it is remembered between calls.                                      */
 enum { RMI_CHAIN_SOKOBAN = 0, RMI_CHAIN_FROZENLAKE = 1 };
 typedef struct {
   int64_t n_envs;
@@ -983,6 +986,69 @@ int rmi_readback(void* dst /*[host]*/, const void* src, size_t bytes, rmi_stream
 /* [host] Enqueue a host (pinned) -> device copy on the stream, no wait (the turn loop's small
  * index uploads).                                                                            */
 int rmi_upload(void* dst, const void* src /*[host]*/, size_t bytes, rmi_stream_t stream);
+
+/* ------------------------------------------------------------ the one-shot arena exchange
+ * Replaces: the reassembly of every rank's rollout record before compute_advantage and the
+ *           update (agent_trainer.py:514-515 rollout + filter, :623-655 advantage + update
+ *           consume the WHOLE batch) -- in the build's N>1 path an RCCL ring
+ *           all-gather (torch.distributed.all_gather_into_tensor) of the per-rank episode
+ *           arena, W-1 serial hops over one xGMI link per hop.  Here every rank STORES its
+ *           nbytes into all W ranks' receive regions at once (one direct hop, the W-1 peers'
+ *           links in parallel), then publishes a per-(sender) arrival count with a
+ *           system-scope release; a rank's gather is complete when all W senders' counts
+ *           reached the epoch's.  Receive regions are allocated here (uncached or fine-grained
+ *           device memory, so stores arriving over xGMI are never shadowed by a stale L2 line)
+ *           and mapped into the peers' processes once, through HIP IPC handles the caller
+ *           exchanges over its process group.
+ *
+ * Region layout (one per rank, rmi_xgather_region_bytes): a 4096-B header -- u64 consumed at
+ * byte 0 (the last epoch whose slot this rank has finished reading), u64 arrivals[W] at byte
+ * 64 (sender q's arrivals at 64 + 8q) -- then two slots of W rows of nbp =
+ * round_up(nbytes, 4096) bytes; epoch e (1, 2, ...) lands in slot e & 1, sender q's bytes at
+ * row q (rmi_xgather_slot_offset + q * nbp).  Two slots let epoch e+1's stores land while the
+ * consumer still reads epoch e; a sender stores epoch e into peer p's slot only after p's
+ * consumed >= e - 2 (p is done with the slot's previous epoch).
+ *
+ * rmi_xgather(x, src, flags) enqueues ONE kernel on `stream`:
+ *   RMI_XG_PUBLISH: e = state[0] + 1; marks this rank's consumed = e - 1 (everything enqueued
+ *     before on the stream has finished with the slot of e - 1); for each rank p, waits for
+ *     p's consumed >= e - 2, stores src[0, nbytes) into p's slot e & 1, row `rank`, then adds
+ *     the storing blocks' arrivals to p's arrivals[rank] (release, system scope).
+ *   RMI_XG_WAIT: waits until every sender's arrivals in this rank's region reached e *
+ *     blocks_per_peer and this rank's own storing blocks all finished, then sets state[0] = e.
+ *   Both (the default use): one launch that returns when the whole gather has landed.
+ * PUBLISH alone followed later by WAIT alone splits the exchange (each rank's halves in stream
+ * order; several ranks may share one stream, every rank's PUBLISH before any WAIT).  Every
+ * wait is bounded by timeout_us (0: 2 s) of the GPU's constant 100-MHz clock: on expiry the
+ * kernel sets RMI_XG_ERR_* in *err (sticky) and returns, so a missing peer never hangs the
+ * device.  nbytes % 16 == 0, src 16-B aligned, 1 <= world <= RMI_XG_MAX_RANKS.             */
+#define RMI_XG_MAX_RANKS 16
+enum { RMI_XG_PUBLISH = 1, RMI_XG_WAIT = 2 };
+enum { RMI_XG_ERR_PEER_BUSY = 1, RMI_XG_ERR_ARRIVALS = 2 };
+enum { RMI_XG_MEM_UNCACHED = 0, RMI_XG_MEM_FINEGRAINED = 1 };
+typedef struct {
+  int32_t world, rank;
+  int64_t nbytes;                      /* each rank's contribution                              */
+  void* region[RMI_XG_MAX_RANKS];      /* every rank's region as mapped here (own at [rank])    */
+  uint64_t* state;                     /* u64[2] this rank's, zeroed: epoch, own blocks finished */
+  uint32_t* err;                       /* u32[1]: RMI_XG_ERR_* bits, OR-ed in                    */
+  uint64_t timeout_us;                 /* bound on every wait (0: 2 000 000)                     */
+  int32_t blocks_per_peer;             /* 0: by size (rmi_xgather_blocks_per_peer)               */
+} rmi_xgather_t;
+/* [host] bytes of one rank's region; -1 for a bad world / nbytes                              */
+int64_t rmi_xgather_region_bytes(int32_t world, int64_t nbytes);
+/* [host] byte offset, in a region, of the slot epoch e (>= 1) lands in; -1 if invalid         */
+int64_t rmi_xgather_slot_offset(int32_t world, int64_t nbytes, int64_t epoch);
+/* [host] the storing blocks per peer rmi_xgather launches for nbytes (0 asked)                */
+int32_t rmi_xgather_blocks_per_peer(int64_t nbytes);
+/* [host] allocate + zero a region of `bytes` on the current device (mode RMI_XG_MEM_*) and
+ * write its IPC handle (64 B) to handle [host]; free with rmi_xgather_free                     */
+int rmi_xgather_alloc(int64_t bytes, int32_t mode, void** region /*[host]*/, uint8_t* handle /*[host] 64 B*/);
+/* [host] map a peer's region from its handle into this process / unmap it                     */
+int rmi_xgather_open(const uint8_t* handle /*[host] 64 B*/, void** region /*[host]*/);
+int rmi_xgather_close(void* region);
+int rmi_xgather_free(void* region);
+int rmi_xgather(const rmi_xgather_t* x /*[host]*/, const void* src, int32_t flags, rmi_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -146,6 +146,19 @@ class FormulateChain(ctypes.Structure):
                 ("response_mask", c_void_p), ("resp_count", c_void_p), ("err", c_void_p), ("tail", c_void_p),
                 ("n_copies", c_int32), ("host", c_void_p * 4), ("dev", c_void_p * 4), ("bytes", c_int64 * 4)]
 
+XG_MAX_RANKS = 16
+XG_PUBLISH, XG_WAIT = 1, 2
+XG_ERR_PEER_BUSY, XG_ERR_ARRIVALS = 1, 2
+XG_MEM_UNCACHED, XG_MEM_FINEGRAINED = 0, 1
+
+
+class XGather(ctypes.Structure):
+    """rmi_xgather_t: the one-shot arena exchange of one rank (include/ragen_amd.h)."""
+    _fields_ = [("world", c_int32), ("rank", c_int32), ("nbytes", c_int64), ("region", c_void_p * XG_MAX_RANKS),
+                ("state", c_void_p), ("err", c_void_p), ("timeout_us", ctypes.c_uint64),
+                ("blocks_per_peer", c_int32)]
+
+
 _P = ctypes.POINTER
 _SIGS = {
     "rmi_version": (ctypes.c_char_p, []),
@@ -223,6 +236,14 @@ _SIGS = {
     "rmi_stream_synchronize": (c_int32, [c_void_p]),
     "rmi_readback": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "rmi_upload": (c_int32, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rmi_xgather_region_bytes": (c_int64, [c_int32, c_int64]),
+    "rmi_xgather_slot_offset": (c_int64, [c_int32, c_int64, c_int64]),
+    "rmi_xgather_blocks_per_peer": (c_int32, [c_int64]),
+    "rmi_xgather_alloc": (c_int32, [c_int64, c_int32, _P(c_void_p), c_void_p]),
+    "rmi_xgather_open": (c_int32, [c_void_p, _P(c_void_p)]),
+    "rmi_xgather_close": (c_int32, [c_void_p]),
+    "rmi_xgather_free": (c_int32, [c_void_p]),
+    "rmi_xgather": (c_int32, [_P(XGather), c_void_p, c_int32, c_void_p]),
     "rmi_prompt_text": (c_int32, [_P(Prompt), c_int64, c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_gen_rows": (c_int32, [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                c_void_p, c_void_p, c_void_p]),

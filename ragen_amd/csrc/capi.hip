@@ -54,28 +54,20 @@ __global__ __launch_bounds__(kCopyBlock) void readback_kernel(const uint32_t* __
   for (int64_t i = 4 * n4 + t; i < n32; i += step) dst[i] = src[i];
 }
 
-// the device address of a pinned host buffer, or nullptr: a few recent lookups cached per
-// thread (the turn loop alternates a handful of pinned buffers)
+// the device address of a pinned host buffer, or nullptr (pageable memory).  Looked up on every
+// call, never cached: a pinned buffer may be released (hipHostFree, hipHostUnregister, torch's
+// host-cache flush) and its address reused by pageable memory or another registration, and a
+// remembered mapping would then send the readback kernel's stores to a stale device address.
+// The lookup is a runtime map search (well under a microsecond against a launch).
 void* host_mapping(void* host) {
-  constexpr int kSlots = 8;
-  thread_local void* keys[kSlots] = {};
-  thread_local void* vals[kSlots] = {};
-  thread_local int next = 0;
-  for (int i = 0; i < kSlots; ++i)
-    if (keys[i] == host) return vals[i];
   hipPointerAttribute_t attr;
-  void* dev = nullptr;
   // (only where the runtime's host address is the one asked about: its device address is then
   // that byte's, whether or not the runtime offsets interior pointers)
   if (hipPointerGetAttributes(&attr, host) == hipSuccess && attr.type == hipMemoryTypeHost && attr.devicePointer &&
       attr.hostPointer == host)
-    dev = attr.devicePointer;
-  else
-    (void)hipGetLastError();  // (clear the lookup's error: pageable memory)
-  keys[next] = host;
-  vals[next] = dev;
-  next = (next + 1) % kSlots;
-  return dev;
+    return attr.devicePointer;
+  (void)hipGetLastError();  // (clear the lookup's error: pageable memory)
+  return nullptr;
 }
 }  // namespace
 

@@ -10,10 +10,12 @@
 
 namespace {
 
-// one event per device, created on first use: the readback is waited on through it, so work
-// enqueued after the copy (the next batch's row list) runs while the host reads the copy
+// one event per (host thread, device), created on first use: the readback is waited on through
+// it, so work enqueued after the copy (the next batch's row list) runs while the host reads the
+// copy.  Per thread: two threads running chains on one device must not wait on each other's
+// record (each would read its readback tail before its own copy had landed).
 hipEvent_t copy_event() {
-  static hipEvent_t ev[64] = {};
+  thread_local hipEvent_t ev[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
   if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) ev[dev] = nullptr;
@@ -29,6 +31,9 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
   if (B < 1 || !c.ep || c.ep->B != B || !c.obs || !c.pack || !c.host || c.pack_bytes < 1 || !c.parse ||
       (c.env_kind == RMI_CHAIN_SOKOBAN ? !c.sokoban : c.env_kind == RMI_CHAIN_FROZENLAKE ? !c.frozenlake : true))
     return RMI_EINVAL;
+  // the next batch's row list and its pad read the readback tail's stats (longest, any_bad,
+  // count), which only step 6's rmi_prompt_commit_stats writes: without a prompt they are stale
+  if ((c.next_rows || c.pad_block) && (!c.prompt || !c.stats)) return RMI_EINVAL;
   int rc;
   // 1. the generations onto the env rows (the longest one's raw bytes into the readback)
   if (c.resp) {

@@ -929,6 +929,10 @@ class ContextManager:
         mean = row_resp.mean().double().reshape(1).view(torch.uint8)
         parts, ext = es.metric_arrays([mean, err])
         response_length = float(ext[:8].view(np.float64)[0])
+        if row_resp.numel() * max(S, 1) >= (1 << 24):
+            # partial f32 sums of the counts may round here, and the device's reduction order is
+            # not torch CPU's: the reference's own op on the counts (exact below 2^24 either way)
+            response_length = float(row_resp.cpu().mean().item())
         err_h = ext[8:]
         _raise_assemble_errors(None, S, (bool((err_h & _lib.ERR_UNSUP).any()), bool((err_h & _lib.ERR_STATE).any())))
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],

@@ -25,6 +25,19 @@ from .. import _lib, ops
 from ..torch_ops import _parse_cfg, _render_struct, prompt_struct
 
 
+def ref_f32_mean(total: int, n: int, counts) -> float:
+    """``response_mask.sum(-1).float().mean()`` (ctx_manager.py:305) from the integer total of the
+    n row counts.  Below 2^24 every f32 partial sum of integers is exact, whatever the order, so the
+    mean is f32(total) / f32(n), one rounding, as torch's.  From 2^24 up the partial sums round and
+    the result depends on the reduction order: ``counts()`` (the per-row counts, any device) then
+    goes through the reference's own op, torch's CPU f32 mean."""
+    if n < 1:
+        return float("nan")
+    if total < (1 << 24):
+        return float(np.float32(total) / np.float32(n))
+    return float(counts().to("cpu", torch.int64).float().mean().item())
+
+
 class _Slot:
     """The buffers of one turn number, reused by every rollout (the turn record of that turn
     points at them until the next reset)."""
@@ -398,9 +411,10 @@ class FormulateChain:
         hb = self.h_block.numpy()
         total, bits = (int(x) for x in hb[:16].view(np.int64))
         _raise_assemble_errors(None, S, (bool(bits & _lib.ERR_UNSUP), bool(bits & _lib.ERR_STATE)))
-        # response_length: the f32 mean of the row counts (ctx_manager.py:305; exact while the
-        # total stays below 2^24, where f32 sums of integers are exact in any order)
-        response_length = float(np.float32(total) / np.float32(n))
+        # response_length: the f32 mean of the row counts (ctx_manager.py:305); exact while the
+        # total stays below 2^24, where f32 sums of integers are exact in any order.  Above it the
+        # partial sums round, so the counts go through the reference's own op: torch's CPU f32 mean
+        response_length = ref_f32_mean(total, n, lambda: self.resp_count[:n])
         m = hb[16:16 + 32 * n].view(np.float64).reshape(n, 4).copy()
         info = self.h_info.numpy()[:T * n].reshape(T, n).copy()
         custom = (info & _lib.INFO_PRESENT).any(0) if T else np.zeros(n, bool)

@@ -7,6 +7,7 @@ class FakeQwenTok:
     name_or_path = "Qwen/Qwen2.5-0.5B-Instruct"
     IM_START, IM_END, PAD = 151644, 151645, 151643
     pad_token_id = 151643
+    ADDED = {"<|im_start|>": IM_START, "<|im_end|>": IM_END}
 
     def encode(self, text):
         return {"<|im_start|>": [self.IM_START], "<|im_end|>": [self.IM_END]}[text]
@@ -18,12 +19,10 @@ class FakeQwenTok:
     def _ids(self, text):
         out, i = [], 0
         while i < len(text):
-            if text.startswith("<|im_start|>", i):
-                out.append(self.IM_START)
-                i += 12
-            elif text.startswith("<|im_end|>", i):
-                out.append(self.IM_END)
-                i += 10
+            hit = next((t for t in self.ADDED if text.startswith(t, i)), None)
+            if hit is not None:
+                out.append(self.ADDED[hit])
+                i += len(hit)
             else:
                 out.append(ord(text[i]) % 150000)
                 i += 1
@@ -49,7 +48,7 @@ class FakeQwenTok:
         return o
 
     def decode(self, ids, skip_special_tokens=True):
-        drop = {self.IM_START, self.IM_END, self.PAD} if skip_special_tokens else set()
+        drop = set(self.ADDED.values()) | {self.PAD} if skip_special_tokens else set()
         return "".join(chr(int(i)) for i in ids if int(i) not in drop)
 
     def batch_decode(self, rows, skip_special_tokens=True):
@@ -63,7 +62,8 @@ class FakeQwenTok:
                 table.append(chr(i).encode("utf-8"))
             except UnicodeEncodeError:  # surrogates
                 table.append(b"")
-        skip = [1 if i in (self.IM_START, self.IM_END, self.PAD) else 0 for i in range(V)]
+        special = set(self.ADDED.values()) | {self.PAD}
+        skip = [1 if i in special else 0 for i in range(V)]
         return table, skip
 
     _backend = None
@@ -75,12 +75,13 @@ class FakeQwenTok:
         rebuild every Basic-Multilingual-Plane character from its UTF-8 bytes into the id
         ord(c) % 150000, and <|im_start|> / <|im_end|> as added tokens.  Checked against _ids by
         tests/test_tokenizer.py."""
-        if FakeQwenTok._backend is None:
-            FakeQwenTok._backend = _char_bpe(self.IM_START, self.IM_END)
-        return FakeQwenTok._backend
+        if type(self)._backend is None:
+            type(self)._backend = _char_bpe(self.ADDED)
+        return type(self)._backend
 
 
-def _char_bpe(im_start, im_end):
+def _char_bpe(added):
+    """added: {token text: id} of the added (special) tokens."""
     import json
 
     from tokenizers import Tokenizer
@@ -106,7 +107,7 @@ def _char_bpe(im_start, im_end):
             cur = tok
     # the added tokens hold their Qwen ids in the model vocabulary too (else tokenizers renumbers
     # them past the vocabulary); unused ids get placeholder tokens (no holes in the id space)
-    vocab["<|im_start|>"], vocab["<|im_end|>"] = im_start, im_end
+    vocab.update(added)
     used = set(vocab.values())
     for i in range(max(used) + 1):
         if i not in used:
@@ -114,7 +115,7 @@ def _char_bpe(im_start, im_end):
     j = {"version": "1.0", "truncation": None, "padding": None,
          "added_tokens": [{"id": i, "content": t, "single_word": False, "lstrip": False, "rstrip": False,
                            "normalized": False, "special": True}
-                          for i, t in ((im_start, "<|im_start|>"), (im_end, "<|im_end|>"))],
+                          for t, i in added.items()],
          "normalizer": None,
          "pre_tokenizer": {"type": "Sequence", "pretokenizers": [
              {"type": "Split", "pattern": {"Regex": "."}, "behavior": "Isolated", "invert": False},
@@ -125,3 +126,25 @@ def _char_bpe(im_start, im_end):
                    "end_of_word_suffix": None, "fuse_unk": False, "byte_fallback": False, "ignore_merges": False,
                    "vocab": vocab, "merges": merges}}
     return Tokenizer.from_str(json.dumps(j))
+
+
+class FakeLlama3Tok(FakeQwenTok):
+    """The same byte-level stand-in under a Llama-3 name: get_special_tokens' second branch
+    (ctx_manager.py:27-29, ids 128006 / 128009, no Qwen roll), the Llama-3 chat layout
+    (<|begin_of_text|>, <|start_header_id|> role <|end_header_id|> \\n\\n content <|eot_id|>) and its
+    special ids; other characters keep the id ord(c) % 150000 (below 128000 for the BMP text of
+    these tests)."""
+    name_or_path = "meta-llama/Meta-Llama-3-8B-Instruct"
+    BOT, IM_START, EH, IM_END, PAD = 128000, 128006, 128007, 128009, 128001
+    pad_token_id = 128001
+    ADDED = {"<|begin_of_text|>": BOT, "<|start_header_id|>": IM_START, "<|end_header_id|>": EH,
+             "<|eot_id|>": IM_END}
+    _backend = None
+
+    def encode(self, text):
+        raise AssertionError("the Llama-3 branch of get_special_tokens calls no encode")
+
+    def apply_chat_template(self, messages, add_generation_prompt, tokenize):
+        s = "<|begin_of_text|>" + "".join(
+            f"<|start_header_id|>{m['role']}<|end_header_id|>\n\n{m['content']}<|eot_id|>" for m in messages)
+        return s + ("<|start_header_id|>assistant<|end_header_id|>\n\n" if add_generation_prompt else "")

@@ -55,7 +55,7 @@ STRUCTS = {  # ctypes mirror in ragen_amd/_lib.py -> C type in include/ragen_amd
     "FrozenLake": "rmi_frozenlake_t", "Bandit": "rmi_bandit_t", "Countdown": "rmi_countdown_t",
     "ParseCfg": "rmi_parse_cfg_t", "Piece": "rmi_piece_t", "Prompt": "rmi_prompt_t", "tokenizer.Bpe": "rmi_bpe_t",
     "Render": "rmi_render_t", "TurnChain": "rmi_turn_chain_t",
-    "FormulateChain": "rmi_formulate_chain_t", "TokenRows": "rmi_token_rows_t",
+    "FormulateChain": "rmi_formulate_chain_t", "TokenRows": "rmi_token_rows_t", "XGather": "rmi_xgather_t",
 }
 
 

@@ -50,6 +50,29 @@ def test_assemble_golden(device):
             np.testing.assert_array_equal(rm.cpu().numpy().astype(np.uint8), d[key + "_response_mask"])
 
 
+def test_assemble_llama3_golden(device):
+    """assemble_batch with a Llama-3 tokenizer (ids 128006 / 128009, no roll) on the rows of the
+    reference-run Llama fixture: the same ids and the reference's masks / scores."""
+    from fake_tok import FakeLlama3Tok
+    d = load("masks_scores_llama")
+    ids = d["input_ids"]
+    rows = [r[np.argmax(r != 128001):] if (r != 128001).any() else r[:0] for r in ids]
+    lens, flat = d["scores_len"], d["scores_flat"]
+    scores, o = [], 0
+    for n in lens:
+        scores.append(list(flat[o:o + n]))
+        o += n
+    tok = FakeLlama3Tok()
+    for uts in (False, True):
+        for erm in (False, True):
+            i, am, pos, sc, lm, rm = assemble_batch(rows, tok, scores, uts, erm, device, S=ids.shape[1])
+            key = f"uts{int(uts)}_erm{int(erm)}"
+            np.testing.assert_array_equal(i.cpu().numpy(), ids)
+            np.testing.assert_array_equal(sc.cpu().numpy(), d[key + "_score"])
+            np.testing.assert_array_equal(lm.cpu().numpy().astype(np.uint8), d[key + "_loss_mask"])
+            np.testing.assert_array_equal(rm.cpu().numpy().astype(np.uint8), d[key + "_response_mask"])
+
+
 def test_assemble_full_size(device):
     """8192 rows up to 1024 tokens of chat-shaped ids: == torch left padding + cumsum and the
     oracle's get_masks_and_scores on the padded ids, both score placements."""

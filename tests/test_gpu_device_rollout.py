@@ -158,3 +158,54 @@ def test_load_rooms_equals_load_state(device):
     e = err.cpu().numpy()
     assert e[3] == _lib.ERR_INDEX and not np.delete(e, 3).any()
     assert not a.room_state[3].any() and torch.equal(a.room_state[4], b.room_state[4])
+
+
+@pytest.mark.parametrize("uts", [False, True])
+def test_device_formulate_llama3_against_oracle(device, uts, monkeypatch):
+    """formulate_rollouts on the device path with a Llama-3 tokenizer (get_special_tokens'
+    second branch, ctx_manager.py:27-29: ids 128006 / 128009 and no Qwen roll at :60-62), both
+    score placements: the batch's masks and scores == the oracle's get_masks_and_scores (roll
+    off) on the batch's own ids with the history scores (ctx_manager.py:282), and without turn
+    scores the last column == the oracle's group normalisation of sum + penalty
+    (ctx_manager.py:213-223); the device rollout == the dict rollout as for Qwen."""
+    import oracle
+    from fake_tok import FakeLlama3Tok
+    from ragen_amd.env import SokobanBatch
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    name = "sokoban_es"
+    tok = FakeLlama3Tok()
+    vocab = ops.VocabTable.from_bytes(*tok.byte_table(), device)
+    outs = []
+    for v in (None, vocab):
+        cfg = _config(name)
+        cfg.agent_proxy.use_turn_scores = uts
+        proxy = LLMAgentProxy(cfg, TokenActor(_turn_tokens(name, tok, device)), tok, device=device)
+        if v is not None:
+            proxy.train_ctx_manager.set_device_vocab(v)
+        random.seed(7)
+        outs.append((proxy.rollout(DataProto(meta_info={}), val=False), proxy.train_es_manager.rollout_cache))
+    (ref, ref_cache), (out, cache) = outs
+    for k in ref.batch.keys():
+        assert torch.equal(ref.batch[k].cpu(), out.batch[k].cpu()), k
+    assert ref.meta_info == out.meta_info and ref_cache == cache
+    ids = out.batch["input_ids"].cpu().numpy()
+    assert (ids == 128006).any() and (ids == 128009).any() and not (ids == 151644).any()
+    scores = [[h.get("reward", 0.0) for h in e["history"]] for e in cache]
+    B, T = len(scores), max(len(x) for x in scores)
+    tab = np.zeros((T, B))
+    for b, x in enumerate(scores):
+        tab[:len(x), b] = x
+    n = np.array([len(x) for x in scores], np.int32)
+    sc, lm, rm, err = oracle.masks_and_scores(ids, 128006, 128009, tab, n, T, uts, True, False)
+    assert not err.any()
+    np.testing.assert_array_equal(out.batch["loss_mask"].cpu().numpy().astype(np.uint8), lm)
+    got = out.batch["rm_scores"].cpu().numpy()
+    if uts:
+        np.testing.assert_array_equal(got, sc)
+        assert (got != 0).any()
+    else:
+        np.testing.assert_array_equal(got[:, :-1], sc[:, :-1])
+        pen = np.array([e.get("penalty", 0) for e in cache], np.float32)
+        gid = np.array([e["group_id"] for e in cache])
+        seg = np.concatenate([[0], np.nonzero(np.diff(gid))[0] + 1, [B]]).astype(np.int32)
+        np.testing.assert_array_equal(got[:, -1], oracle.group_normalize(sc[:, -1], pen, seg, "identity"))

@@ -123,6 +123,27 @@ def test_get_masks_and_scores_golden(device):
             np.testing.assert_array_equal(rm.cpu().numpy().astype(np.uint8), d[key + "_response_mask"])
 
 
+def test_get_masks_and_scores_llama3_golden(device):
+    """The Llama-3 branch (ctx_manager.py:27-29, no roll at :60-62) on the device kernel == the
+    reference-run fixture (tests/golden/make_golden_llama.py), all four mode pairs."""
+    from fake_tok import FakeLlama3Tok
+    d = load("masks_scores_llama")
+    tok = FakeLlama3Tok()
+    ids = torch.from_numpy(d["input_ids"]).to(device)
+    lens, flat = d["scores_len"], d["scores_flat"]
+    scores, o = [], 0
+    for n in lens:
+        scores.append(list(flat[o:o + n]))
+        o += n
+    for uts in (False, True):
+        for erm in (False, True):
+            st, lm, rm = get_masks_and_scores(ids, tok, scores, use_turn_scores=uts, enable_response_mask=erm)
+            key = f"uts{int(uts)}_erm{int(erm)}"
+            np.testing.assert_array_equal(st.cpu().numpy(), d[key + "_score"])
+            np.testing.assert_array_equal(lm.cpu().numpy().astype(np.uint8), d[key + "_loss_mask"])
+            np.testing.assert_array_equal(rm.cpu().numpy().astype(np.uint8), d[key + "_response_mask"])
+
+
 def test_parse_response_golden(device):
     for case in strings()["parse_response"]:
         cfg = default_config(agent_proxy={"enable_think": case["enable_think"]})

@@ -273,3 +273,36 @@ def test_masks_and_scores_golden():
             np.testing.assert_array_equal(lm, d[key + "_loss_mask"])
             np.testing.assert_array_equal(rm, d[key + "_response_mask"])
             assert not err.any()
+
+
+def test_masks_and_scores_llama3_golden():
+    """The Llama-3 branch (ctx_manager.py:27-29: ids 128006 / 128009, and no roll at :60-62):
+    oracle.masks_and_scores with roll off == get_masks_and_scores run by the reference on
+    Llama-3 chat rows (tests/golden/make_golden_llama.py), both score placements and both mask
+    modes; rows with fewer turns than the batch keep zip_longest's fill 0 on their own last
+    column, which the roll would have carried off.  The facade's get_special_tokens takes the
+    same branch."""
+    from fake_tok import FakeLlama3Tok
+    from ragen_amd.llm_agent.ctx_manager import get_special_tokens
+    d = load("masks_scores_llama")
+    sp, rt = (int(x) for x in d["special"])
+    assert get_special_tokens(FakeLlama3Tok()) == (sp, rt) == (128006, 128009)
+    lens, flat = d["scores_len"], d["scores_flat"]
+    B, T = len(lens), int(lens.max())
+    tab = np.zeros((T, B), np.float64)
+    o = 0
+    for b, n in enumerate(lens):
+        tab[:n, b] = flat[o:o + n]
+        o += n
+    for uts in (False, True):
+        for erm in (False, True):
+            sc, lm, rm, err = oracle.masks_and_scores(d["input_ids"], sp, rt, tab, lens, T, uts, erm, False)
+            key = f"uts{int(uts)}_erm{int(erm)}"
+            np.testing.assert_array_equal(sc, d[key + "_score"])
+            np.testing.assert_array_equal(lm, d[key + "_loss_mask"])
+            np.testing.assert_array_equal(rm, d[key + "_response_mask"])
+            assert not err.any()
+    # the fixture holds the case the roll hides: a shorter row whose last turn's score was overwritten
+    last = d["uts1_erm0_score"][:, -1]
+    ends_on_eot = d["input_ids"][:, -1] == rt
+    assert ((lens < T) & ends_on_eot & (last == 0)).any()
