@@ -75,7 +75,12 @@ def _pmc_source(pattern):
 
 
 class Rollout:
-    def __init__(self, device, rank, B=B_PER_GPU):
+    """The SK rollout on one rank.  boards: the turn launches keep the board cache
+    (SokobanBatch.enable_boards): the first turn of a rollout builds it (a fresh episode always
+    does), the later turns read one 16-B entry per env instead of the two grid rows and skip
+    their decode."""
+
+    def __init__(self, device, rank, B=B_PER_GPU, boards=True):
         self.device = device
         self.B = B
         cfg = SokobanEnvConfig(dim_x=6, dim_y=6, num_boxes=1, max_steps=100)
@@ -91,6 +96,10 @@ class Rollout:
         self.metrics = torch.empty(B, 4, dtype=torch.float64, device=device)
         self.turns = [ops.turn_struct(t, self.ids[t], self.n[t], None, MAX_ACTIONS, -0.1) for t in range(T_TURNS)]
         self.st = e.struct()
+        self.boards = bool(boards) and e.enable_boards()
+        # turn 0 (after a restore or fused with it) builds the cache, turns 1.. use it
+        self.st_first = e.board_struct(_lib.BOARDS_BUILD) if self.boards else self.st
+        self.st_next = e.board_struct(_lib.BOARDS_USE) if self.boards else self.st
         self.fin = ops.finalize_struct(GROUP, "identity", self.norm, self.metrics)
 
     def step(self):
@@ -99,17 +108,17 @@ class Rollout:
         for bit), the last with the rollout's finalize (metrics + scores + normalisation ==
         rmi_rollout_finalize, tested bit for bit)."""
         e = self.env
-        ops.sokoban_step_turn_first(self.st, e.ep, self.turns[0], e.init_state, e.init_player)
+        ops.sokoban_step_turn_first(self.st_first, e.ep, self.turns[0], e.init_state, e.init_player)
         for t in range(1, T_TURNS - 1):
-            ops.sokoban_step_turn(self.st, e.ep, self.turns[t])
-        ops.sokoban_step_turn_finalize(self.st, e.ep, self.turns[-1], self.fin)
+            ops.sokoban_step_turn(self.st_next, e.ep, self.turns[t])
+        ops.sokoban_step_turn_finalize(self.st_next, e.ep, self.turns[-1], self.fin)
 
     def step_unfused(self):
         """The same rollout with T plain turn launches and the separate finalize launch (the
         dominant kernel alone, for the roofline and PMC passes)."""
         self.env.restore()
         for t in range(T_TURNS):
-            ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
+            ops.sokoban_step_turn(self.st_next if t else self.st_first, self.env.ep, self.turns[t])
         ops.rollout_finalize(self.env.ep, self.seg, "identity", self.norm, metrics=self.metrics)
 
     def timed_turns(self):
@@ -121,7 +130,7 @@ class Rollout:
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         for t in range(T_TURNS):
-            ops.sokoban_step_turn(self.st, self.env.ep, self.turns[t])
+            ops.sokoban_step_turn(self.st_next if t else self.st_first, self.env.ep, self.turns[t])
         b.record()
         ops.rollout_finalize(self.env.ep, self.seg, "identity", self.norm, metrics=self.metrics)
         return a, b

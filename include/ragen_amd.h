@@ -105,7 +105,22 @@ typedef struct {
   int8_t* player;             /* [B,2]    player_position (row, col)                       */
   uint8_t* num_env_steps;     /* [B]  (<= num_actions <= 255: one env step per action)     */
   int8_t* boxes_on_target;    /* [B]  num_boxes - open targets: -64..64 for H*W <= 64      */
+  /* Optional board cache (NULL: none), caller-owned like every other field: 16 B per env
+   * holding the room's bitboards after the last turn (window wall | target | box u32, then
+   * the player's cell index and a tag byte: 1 = the room is regular and the entry is its
+   * state).  boards_mode RMI_BOARDS_BUILD: the turn decodes every env's rows as without a
+   * cache and writes every live env's entry; RMI_BOARDS_USE: the turn trusts the tagged
+   * entries of the acting envs (no row loads, no decode) and keeps them current -- valid only
+   * while nothing but rmi_sokoban_step_turn{,_first,_finalize} launches with this cache have
+   * written room_state / room_fixed / player since a BUILD launch (the caller tracks that).
+   * A wave with an acting env whose entry is untagged (or whose actions leave the regular
+   * path) loads and decodes its rows as without a cache.  Only 6x6 rooms (the window in a
+   * u32) at one lane per env (4097 <= B < 131072) maintain it: any other launch given a
+   * non-NULL boards returns RMI_EUNSUP.                                                    */
+  uint8_t* boards;            /* [B,16] or NULL                                            */
+  int32_t boards_mode;        /* RMI_BOARDS_*                                              */
 } rmi_sokoban_t;
+enum { RMI_BOARDS_NONE = 0, RMI_BOARDS_BUILD = 1, RMI_BOARDS_USE = 2 };
 
 int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in,
                           uint8_t* err, rmi_stream_t stream);
@@ -702,9 +717,14 @@ typedef struct {
   uint32_t int_reward_tags;  /* bit t: tag t's 0 / 1 rewards print as ints (tags < 32)          */
   int32_t last_turn;
   /* Reward text cache (NULL: off): (num_cache_mask + 1) entries of 16 u32, zero-initialised and
-   * kept across calls — a reward's float bits -> its CPython repr (<= 24 bytes), with a 64-bit
-   * check of the entry (a torn or foreign entry is a miss).  A turn's rewards take a handful of
-   * values; a hit replaces the row's shortest-repr search on one lane.                       */
+   * kept across calls — a reward's float bits -> its CPython repr (<= 24 bytes).  An entry is
+   * written once: its writer claims the empty slot by a 64-bit compare-and-swap of the key word,
+   * then stores the text and the ready | length word, and no one writes the slot again.  Every
+   * word of an entry therefore goes from zero to its final value exactly once, and a reader
+   * takes an entry only when its key matches, it is ready and every text byte below the length
+   * is nonzero (a repr has no zero byte): a word not yet visible reads as zero and is a miss.
+   * A turn's rewards take a handful of values; a hit replaces the row's shortest-repr search
+   * on one lane.                                                                             */
   uint32_t* num_cache;
   uint32_t num_cache_mask;  /* entries - 1 (a power of two minus one)                          */
 } rmi_prompt_t;
@@ -996,8 +1016,9 @@ int rmi_upload(void* dst, const void* src /*[host]*/, size_t bytes, rmi_stream_t
  *           nbytes into all W ranks' receive regions at once (one direct hop, the W-1 peers'
  *           links in parallel), then publishes a per-(sender) arrival count with a
  *           system-scope release; a rank's gather is complete when all W senders' counts
- *           reached the epoch's.  Receive regions are allocated here (uncached or fine-grained
- *           device memory, so stores arriving over xGMI are never shadowed by a stale L2 line)
+ *           reached the epoch's.  Receive regions are allocated here (fine-grained device
+ *           memory: its L2 lines are invalidated at every kernel boundary and by a system-scope
+ *           acquire, so stores arriving over xGMI are never shadowed by a stale L2 line)
  *           and mapped into the peers' processes once, through HIP IPC handles the caller
  *           exchanges over its process group.
  *
@@ -1025,6 +1046,9 @@ int rmi_upload(void* dst, const void* src /*[host]*/, size_t bytes, rmi_stream_t
 #define RMI_XG_MAX_RANKS 16
 enum { RMI_XG_PUBLISH = 1, RMI_XG_WAIT = 2 };
 enum { RMI_XG_ERR_PEER_BUSY = 1, RMI_XG_ERR_ARRIVALS = 2 };
+/* RMI_XG_MEM_FINEGRAINED is the one to use.  RMI_XG_MEM_UNCACHED (hipDeviceMallocUncached) is
+ * kept for measurement only: in one process, after earlier exchanges' uncached regions were
+ * freed, it read stale slot rows in 2 of 5 runs on MI355X.                     */
 enum { RMI_XG_MEM_UNCACHED = 0, RMI_XG_MEM_FINEGRAINED = 1 };
 typedef struct {
   int32_t world, rank;

@@ -21,6 +21,7 @@ FLAG_TERMINATED, FLAG_TRUNCATED, FLAG_DONE = 1, 2, 4
 INFO_PRESENT, INFO_EFFECTIVE, INFO_VALID, INFO_SUCCESS = 1, 2, 4, 8
 ERR_ACTION, ERR_INDEX, ERR_STATE, ERR_UNSUP = 1, 2, 4, 8
 MS_TURN_SCORES, MS_RESPONSE_MASK, MS_ROLL = 1, 2, 4
+BOARDS_NONE, BOARDS_BUILD, BOARDS_USE = 0, 1, 2
 NORM_METHODS = {"identity": 0, "mean": 1, "mean_std": 2, "asym_clip": 3}
 
 
@@ -38,7 +39,8 @@ class Turn(ctypes.Structure):
 class Sokoban(ctypes.Structure):
     _fields_ = [("H", c_int32), ("W", c_int32), ("num_boxes", c_int32), ("max_steps", c_int32),
                 ("room_fixed", c_void_p), ("room_state", c_void_p), ("player", c_void_p),
-                ("num_env_steps", c_void_p), ("boxes_on_target", c_void_p)]
+                ("num_env_steps", c_void_p), ("boxes_on_target", c_void_p),
+                ("boards", c_void_p), ("boards_mode", c_int32)]
 
 
 class Finalize(ctypes.Structure):

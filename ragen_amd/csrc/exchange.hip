@@ -12,8 +12,9 @@
 // because the readers are other devices): every storing thread releases at system scope, the
 // block barrier joins them, then ONE lane adds the block's arrival with a system-scope release;
 // the waiting lanes poll relaxed at system scope (these loads bypass the caches) and fence once
-// with a system-scope acquire.  The receive regions are uncached (or fine-grained) device
-// memory, so no L2 on the receiving GPU holds a stale copy of a slot a peer rewrote.
+// with a system-scope acquire.  The receive regions are fine-grained device memory, whose L2
+// lines (MTYPE NC) are invalidated by that acquire and at every kernel boundary, so no L2 on the
+// receiving GPU serves a stale copy of a slot a peer rewrote.
 // Every wait is bounded by the constant 100-MHz clock: a missing peer sets an error bit and the
 // grid drains.
 #include <string.h>

@@ -23,49 +23,44 @@ namespace {
 
 constexpr int kMaxStride = 3072;
 
-// ---- the reward text cache (rmi_prompt_t.num_cache): 16 u32 per entry — the float's bits (2),
-// meta = ready | length, the text (6 u32, zero padded), a 64-bit check of all of them (14, 15).
-// Written by plain stores (no fence: agent-scope release would write the L2 back); a reader
-// takes an entry only when its check matches (racing writers of one key write the same words;
-// a torn or foreign entry fails the check and the row computes its text).
+// ---- the reward text cache (rmi_prompt_t.num_cache): 16 u32 per entry — the claimed key
+// (the float's bits xor kNumKeyMix, 2 u32; 0 = empty), meta = ready | length, the text (6 u32,
+// zero padded).  Written once per slot (include/ragen_amd.h): the writer that wins the key's
+// compare-and-swap stores the text, then the meta word; nothing rewrites a claimed slot.  So
+// every dword goes 0 -> final value once (dword stores and loads are single-copy atomic), and
+// a reader that sees the key, the ready bit and a nonzero byte at every text position below the
+// length holds exactly the writer's text — whatever order the words became visible in, and
+// with no fence on either side (a word still invisible reads 0: a miss, the row computes).
 constexpr uint32_t kNumReady = 1u << 31;
-__device__ __forceinline__ uint64_t num_mix(uint64_t h, uint32_t v) {
-  h = (h ^ v) * 0x100000001B3ull;
-  return h ^ (h >> 31);
-}
-__device__ __forceinline__ uint64_t num_check(uint64_t key, uint32_t meta, const uint32_t (&t)[6]) {
-  uint64_t h = num_mix(num_mix(0xCBF29CE484222325ull, (uint32_t)key), (uint32_t)(key >> 32));
-  h = num_mix(h, meta);
-#pragma unroll
-  for (int i = 0; i < 6; ++i) h = num_mix(h, t[i]);
-  return h;
-}
+constexpr uint64_t kNumKeyMix = 0x7FF4C0FFEE15BAD1ull;  // a NaN payload: no finite reward maps to 0
 __device__ __forceinline__ uint32_t num_slot(uint64_t key, uint32_t mask) {
   return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 40) & mask;
 }
 // the cached text of key into out -> its length, or -1
 __device__ __forceinline__ int num_take(const uint4 (&e)[4], uint64_t key, char* out) {
+  const uint64_t kk = key ^ kNumKeyMix;
   const uint32_t meta = e[0].z;
-  if (!(meta & kNumReady) || (((uint64_t)e[0].y << 32) | e[0].x) != key) return -1;
+  if (kk == 0 || !(meta & kNumReady) || (((uint64_t)e[0].y << 32) | e[0].x) != kk) return -1;
   const int len = (int)(meta & 0xFFu);
   if (len < 1 || len > 24) return -1;
   const uint32_t t[6] = {e[0].w, e[1].x, e[1].y, e[1].z, e[1].w, e[2].x};
-  if (num_check(key, meta, t) != (((uint64_t)e[3].w << 32) | e[3].z)) return -1;
-  for (int i = 0; i < len; ++i) out[i] = (char)((t[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+  for (int i = 0; i < len; ++i) {
+    const uint32_t ch = (t[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    if (ch == 0) return -1;  // that word is not visible here yet
+    out[i] = (char)ch;
+  }
   return len;
 }
 __device__ __forceinline__ void num_put(uint32_t* s, uint64_t key, const char* txt, int len) {
+  const uint64_t kk = key ^ kNumKeyMix;
+  if (kk == 0) return;
+  // claim the empty slot; a slot another key (or another writer of this key) holds is left alone
+  if (atomicCAS(reinterpret_cast<unsigned long long*>(s), 0ull, (unsigned long long)kk) != 0ull) return;
   uint32_t t[6] = {0, 0, 0, 0, 0, 0};
   for (int i = 0; i < len; ++i) t[i >> 2] |= (uint32_t)(uint8_t)txt[i] << (8 * (i & 3));
-  const uint32_t meta = kNumReady | (uint32_t)len;
-  const uint64_t c = num_check(key, meta, t);
-  s[0] = (uint32_t)key;
-  s[1] = (uint32_t)(key >> 32);
 #pragma unroll
   for (int i = 0; i < 6; ++i) s[3 + i] = t[i];
-  s[14] = (uint32_t)c;
-  s[15] = (uint32_t)(c >> 32);
-  s[2] = meta;  // (no fence: a reader that sees a part of the entry fails its check)
+  s[2] = kNumReady | (uint32_t)len;
 }
 
 struct Tok6 {

@@ -650,7 +650,12 @@ __device__ __forceinline__ void render_group(const ObsOut& o, ObsLds<HW, M>& L, 
 // each).  at_end(xs, xf, wall, target, box, jp): the env's state after the turn, for a fused render
 // (jp = the player's window bit of a stepped regular room — read the bitboards — else INT32_MIN:
 // read the rows); called by every lane after the turn's stores, before the fused finalize.
-template <int HW, class M, int LPE, bool kFin, bool kFirst, bool kLate, class AtEnd>
+// kBoards (HW == 36, M = u32, one lane per env, not kLate): env.boards / boards_mode are honoured
+// (include/ragen_amd.h: the board cache).  BUILD decodes every live env's rows (acting or not)
+// and stores its entry; USE loads the 16-B entry instead of the two rows and skips the decode,
+// unless some acting env of the wave has an untagged entry or actions off the regular path:
+// that wave then loads its rows (a second round trip) and decodes them as without a cache.
+template <int HW, class M, int LPE, bool kFin, bool kFirst, bool kLate, bool kBoards, class AtEnd>
 __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_episode_t& ep, const rmi_turn_t& in,
                                          int hw_rt, uint64_t border, uint8_t* __restrict__ err_out,
                                          const rmi_finalize_t& fin, const uint8_t* __restrict__ init_state,
@@ -664,6 +669,10 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   const bool live = b < B;
   const int H = env.H, W = env.W;
   const uint32_t w_magic = (65536u + (uint32_t)W - 1u) / (uint32_t)W;  // off the critical path
+  static_assert(!kBoards || (HW == 36 && LPE == 1 && !kLate && sizeof(M) == 4), "the board cache: 6x6, u32 window");
+  // the cache mode of this launch (wave-uniform): a fresh episode's first turn always builds
+  const int bmode = kBoards && env.boards ? (kFirst ? RMI_BOARDS_BUILD : env.boards_mode) : RMI_BOARDS_NONE;
+  const bool use = bmode == RMI_BOARDS_USE;
   RMI_STAMP_DECL;
   RMI_STAMP(0);
 
@@ -674,7 +683,10 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   uint32_t xs[NWL], xf[NWL];
 #pragma unroll
   for (int i = 0; i < NWL; ++i) xs[i] = xf[i] = 0;
-  if (!kLate) {
+  Dw4 ent = {0u, 0u, 0u, 0u};  // the env's board-cache entry (USE)
+  if (use) {
+    ent = reinterpret_cast<const Dw4*>(env.boards)[bc];
+  } else if (!kLate) {
     load_row<NWL, LPE, HW != 0>((kFirst ? init_state : env.room_state) + bc * hw, xs, sub, row_words);
     load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
   }
@@ -710,24 +722,40 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   // ---- 2. format penalty and the regular-room test
   if (n_act > in.K) n_act = in.K;
   const int left = in.max_actions_per_traj - num_actions;
-  bool regular = true;
+  // valid = action slots < n_act holding a known name (id != 0)  (es_manager.py:156, :239)
+  const uint64_t slots = n_act >= 8 ? ~0ull : (1ull << (8 * n_act)) - 1;
+  const uint32_t sl = (uint32_t)slots, sh = (uint32_t)(slots >> 32);
+  const uint32_t al = (uint32_t)acts, ah = (uint32_t)(acts >> 32);
+  const uint32_t vl = nonzero_bytes(al) & sl, vh = nonzero_bytes(ah) & sh;
+  const bool acts_ok = ((gt8_bytes(al) & vl) | (gt8_bytes(ah) & vh)) == 0;
+  // USE: the entry stands in for the rows while it is tagged and the actions stay on the
+  // regular path; else this wave loads its rows now and decodes them
+  bool from_cache = use && (ent.w >> 8 & 0xFFu) == 1u && acts_ok;
+  if (use && !__all(from_cache || !act)) {
+    from_cache = false;
+    load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+  }
+  bool regular = true, room_ok = false;
   M wall = 0, target = 0, box = 0;
   int jp = 0;
   if (act) {
     flags &= (uint8_t)~RMI_FLAG_DONE;  // done-ness is decided per stepped turn (:168)
-    // valid = action slots < n_act holding a known name (id != 0)  (es_manager.py:156, :239)
-    const uint64_t slots = n_act >= 8 ? ~0ull : (1ull << (8 * n_act)) - 1;
-    const uint32_t sl = (uint32_t)slots, sh = (uint32_t)(slots >> 32);
-    const uint32_t al = (uint32_t)acts, ah = (uint32_t)(acts >> 32);
-    const uint32_t vl = nonzero_bytes(al) & sl, vh = nonzero_bytes(ah) & sh;
     const int nv = __popc(vl) + __popc(vh);
     if (nv != n_act || nv == 0) penalty += in.format_penalty;  // :158-159
-    const bool acts_ok = ((gt8_bytes(al) & vl) | (gt8_bytes(ah) & vh)) == 0;
+  }
+  if (from_cache && act) {  // the tagged entry: a regular room's window boards and player cell
+    wall = (M)ent.x;
+    target = (M)ent.y;
+    box = (M)ent.z;
+    jp = (int)(ent.w & 0xFFu) - W;
+  } else if (act || (bmode == RMI_BOARDS_BUILD && live)) {  // BUILD: every live env's entry
     const bool interior = r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2;
     const int p = interior ? r * W + c : 0;
     uint64_t wall64, target64, box64;
     const bool consistent = decode_rows<NWL, LPE>(xs, xf, sub, row_words, p, wall64, target64, box64);
-    regular = consistent && acts_ok && interior && (border & ~wall64) == 0 && ((wall64 >> p) & 1) == 0;
+    room_ok = consistent && interior && (border & ~wall64) == 0 && ((wall64 >> p) & 1) == 0;
+    regular = !act || (room_ok && acts_ok);
     // window: bit j = cell W + j; the cells past row H-1 are padding walls
     const int used = (H - 1) * W;
     const M pad = used >= WordBits<M>::kBits ? (M)0 : ~(((M)1 << used) - 1);
@@ -919,6 +947,18 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     }
     if (row_changed) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
   }
+  if (bmode != RMI_BOARDS_NONE && live) {
+    // the entry after the turn: an acting env of a fast wave (its boards were stepped), every
+    // decoded env under BUILD; an env of the exact path is untagged (its room may not be
+    // regular any more); a USE env that did not act keeps its entry
+    const bool stepped_fast = fast && act;
+    const bool write = bmode == RMI_BOARDS_BUILD || act;
+    const uint32_t tag = (stepped_fast || !act) ? (from_cache || room_ok ? 1u : 0u) : 0u;
+    if (write) {
+      const uint32_t cell = (uint32_t)(jp + W) & 0xFFu;
+      reinterpret_cast<Dw4*>(env.boards)[b] = Dw4{(uint32_t)wall, (uint32_t)target, (uint32_t)box, cell | (tag << 8)};
+    }
+  }
   RMI_STAMP(4);
   at_end(xs, xf, wall, target, box, (fast && act) ? jp : INT32_MIN);
   if (kFin) {
@@ -948,7 +988,7 @@ __global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoba
   const bool turn_wave = !kObs || wave < kSokWpb;  // kObs helper waves only render
   const int64_t b = turn_wave ? ((int64_t)blockIdx.x * kSokWpb + wave) * kEnvs + slot : (int64_t)B;
   const int row_words = (HW ? HW : hw_rt) >> 2;
-  turn_env<HW, M, LPE, kFin, kFirst, kLate>(
+  turn_env<HW, M, LPE, kFin, kFirst, kLate, (HW == 36 && LPE == 1 && !kLate && !kObs && sizeof(M) == 4)>(
       env, ep, in, hw_rt, border, err_out, fin, init_state, init_player, b, sub,
       lds_state + (wave * kEnvs + slot) * row_words, lds_fixed + (wave * kEnvs + slot) * row_words,
       [&](const auto& xs, const auto& xf, M wall, M target, M box, int jp) {
@@ -1154,7 +1194,7 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
   if (wv < kTurnWaves) {
     const int t = wv * kWave + lane, e = t / kLpeT, sub = t % kLpeT;
     const int64_t be = b0 + e;
-    turn_env<36, uint32_t, kLpeT, false, kFirst, false>(
+    turn_env<36, uint32_t, kLpeT, false, kFirst, false, false>(
         env, ep, in, 36, border, err_out, fin, init_state, init_player, be, sub, lds_state + e * 9, lds_fixed + e * 9,
         [&](const auto& xs, const auto& xf, uint32_t wall, uint32_t target, uint32_t box, int jp) {
 #pragma unroll
@@ -1259,6 +1299,11 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
   // lanes per env: spread a batch too small to fill the chip over 4 lanes per env
   const bool spread = spread_lanes(ep->B);
   const bool late = !kFirst && !spread && ep->B >= RMI_SOK_LATE_MIN;
+  // the board cache is kept only by the 6x6 one-lane-per-env launch (include/ragen_amd.h)
+  if (env->boards && (hw != 36 || !w32 || spread || ep->B >= RMI_SOK_LATE_MIN ||
+                      (env->boards_mode != RMI_BOARDS_BUILD && env->boards_mode != RMI_BOARDS_USE) ||
+                      (reinterpret_cast<uintptr_t>(env->boards) & 15u)))
+    return RMI_EUNSUP;
 #define RMI_LAUNCH(HW_, M_)                                                                                   \
   do {                                                                                                        \
     if (spread)                                                                                               \
@@ -1348,8 +1393,9 @@ constexpr int kSkip = 1;  // (validate_turn: an empty batch, nothing to launch)
 // finalize; init_state: the first turn fused with the reset).  -> RMI_OK (f = the finalize
 // arguments to launch with), kSkip, or the error.
 int validate_turn(const rmi_sokoban_t* env, const rmi_episode_t* ep, const rmi_turn_t* in, const rmi_finalize_t* fin,
-                  const uint8_t* init_state, const int8_t* init_player, rmi_finalize_t& f) {
+                  const uint8_t* init_state, const int8_t* init_player, rmi_finalize_t& f, bool boards_ok = false) {
   if (!env || (init_state && !ep)) return RMI_EINVAL;
+  if (env->boards && !boards_ok) return RMI_EUNSUP;  // only the plain turn forms keep the board cache
   if (env->H <= 0 || env->W <= 0 || env->H * env->W > kMaxCells) return RMI_EUNSUP;
   const int rc = check_turn_args(ep, in);
   if (rc != RMI_OK) return rc > 0 ? kSkip : rc;
@@ -1377,7 +1423,7 @@ RMI_API int rmi_sokoban_step_turn(const rmi_sokoban_t* env, const rmi_episode_t*
                                   uint8_t* err, rmi_stream_t stream) {
   using namespace rmi;
   rmi_finalize_t f;
-  const int rc = validate_turn(env, ep, in, nullptr, nullptr, nullptr, f);
+  const int rc = validate_turn(env, ep, in, nullptr, nullptr, nullptr, f, true);
   if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
   return sokoban_step_turn_launch<false>(env, ep, in, err, f, as_stream(stream));
 }
@@ -1387,7 +1433,7 @@ RMI_API int rmi_sokoban_step_turn_finalize(const rmi_sokoban_t* env, const rmi_e
   using namespace rmi;
   if (!fin) return RMI_EINVAL;
   rmi_finalize_t f;
-  const int rc = validate_turn(env, ep, in, fin, nullptr, nullptr, f);
+  const int rc = validate_turn(env, ep, in, fin, nullptr, nullptr, f, true);
   if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
   return sokoban_step_turn_launch<true>(env, ep, in, err, f, as_stream(stream));
 }
@@ -1398,7 +1444,7 @@ RMI_API int rmi_sokoban_step_turn_first(const rmi_sokoban_t* env, const rmi_epis
   using namespace rmi;
   if (!init_state || !init_player) return RMI_EINVAL;
   rmi_finalize_t f;
-  const int rc = validate_turn(env, ep, in, nullptr, init_state, init_player, f);
+  const int rc = validate_turn(env, ep, in, nullptr, init_state, init_player, f, true);
   if (rc != RMI_OK) return rc == kSkip ? RMI_OK : rc;
   return sokoban_step_turn_launch<false, true>(env, ep, in, err, f, as_stream(stream), init_state, init_player);
 }
@@ -1454,6 +1500,7 @@ RMI_API int rmi_sokoban_load_rooms(const rmi_sokoban_t* env, const rmi_episode_t
                                    int8_t* init_player, uint8_t* err, rmi_stream_t stream) {
   using namespace rmi;
   if (!env || !ep || ep->B < 0 || ep->T <= 0 || n_rooms < 0) return RMI_EINVAL;
+  if (env->boards) return RMI_EUNSUP;  // a writer of the state: the caller's cache is invalid after it
   const int hw = env->H * env->W;
   if (hw <= 0 || hw > kMaxCells) return RMI_EUNSUP;
   if (ep->B == 0) return RMI_OK;
@@ -1471,6 +1518,7 @@ RMI_API int rmi_sokoban_reset(const rmi_sokoban_t* env, const rmi_episode_t* ep,
                               const int8_t* init_player, rmi_stream_t stream) {
   using namespace rmi;
   if (!env || !ep || ep->B < 0 || ep->T <= 0) return RMI_EINVAL;
+  if (env->boards) return RMI_EUNSUP;  // a writer of the state: the caller's cache is invalid after it
   const int hw = env->H * env->W;
   if (hw <= 0 || hw > kMaxCells) return RMI_EUNSUP;
   if (ep->B == 0) return RMI_OK;

@@ -29,6 +29,49 @@ class SokobanBatch(BatchEnv):
         # the generated rooms: reset() uploads here once, restore() re-initialises from them
         self.init_state = torch.zeros(B, HW, dtype=torch.uint8, device=d)
         self.init_player = torch.zeros(B, 2, dtype=torch.int8, device=d)
+        # the turn kernel's optional board cache (enable_boards; include/ragen_amd.h)
+        self.boards = None
+        self._boards_valid = False
+
+    # 6x6 rooms at one lane per env (the plain turn launch's layout: 4097 <= B < 2^17)
+    BOARDS_MIN_B, BOARDS_MAX_B = 4097, 1 << 17
+
+    def enable_boards(self) -> bool:
+        """Give the turn launches a board cache: 16 B per env holding each room's bitboards after
+        its last turn, so a turn reads one entry instead of the two grid rows and skips their
+        decode.  The cache is this batch's: every state write through its methods keeps it
+        current or marks it stale (the next turn rebuilds it); a caller that writes room_state /
+        room_fixed / player directly must call invalidate_boards().  -> whether the layout
+        supports it (6x6 rooms, BOARDS_MIN_B <= B < BOARDS_MAX_B)."""
+        if self.H * self.W != 36 or (self.H - 1) * self.W > 32 or not (self.BOARDS_MIN_B <= self.B < self.BOARDS_MAX_B):
+            return False
+        if self.boards is None:
+            self.boards = torch.zeros(self.B, 16, dtype=torch.uint8, device=self.device)
+        self._boards_valid = False
+        return True
+
+    def invalidate_boards(self):
+        """The state was written outside the cached turn launches: the next turn rebuilds."""
+        self._boards_valid = False
+
+    def board_struct(self, mode: int) -> _lib.Sokoban:
+        """struct() carrying the board cache in `mode` (_lib.BOARDS_BUILD / BOARDS_USE), for
+        callers that sequence the turn launches themselves (a captured rollout: BUILD for a turn
+        after any other state write, USE after a cached turn)."""
+        if self.boards is None:
+            raise RuntimeError("enable_boards() first")
+        st = self.struct()
+        st.boards, st.boards_mode = self.boards.data_ptr(), int(mode)
+        return st
+
+    def _turn_struct(self):
+        """The state struct of a step_turn launch: with the cache when it is enabled (BUILD when
+        stale, USE when current); the cache is current after the launch."""
+        if self.boards is None:
+            return self.struct()
+        st = self.board_struct(_lib.BOARDS_USE if self._boards_valid else _lib.BOARDS_BUILD)
+        self._boards_valid = True
+        return st
 
     def struct(self) -> _lib.Sokoban:
         c = self.config
@@ -128,6 +171,7 @@ class SokobanBatch(BatchEnv):
             ops.h2d(inv.astype(np.int32), self.device)
         ops.sokoban_load_rooms(self.struct(), self.ep, ops.h2d(rows, self.device), room_of, self.init_state,
                                self.init_player)
+        self._boards_valid = False
         self._invalidate()
 
     def load_state(self, fixed, state, player):
@@ -159,6 +203,7 @@ class SokobanBatch(BatchEnv):
     def restore(self):
         """Back to the post-reset state of the last reset() (one fused launch)."""
         torch.ops.ragen_amd.sokoban_reset(*self.state_args(), self.init_state, self.init_player, *self.dims())
+        self._boards_valid = False
         self._invalidate()
 
     # step_turn(render=True) renders every env's next observation in the same launch
@@ -173,12 +218,13 @@ class SokobanBatch(BatchEnv):
             direct.sokoban_step_turn_render(*self.state_args(), actions, n_actions, has_input, err, *rows,
                                             *self.glyph_lists(), int(turn), int(max_actions_per_traj),
                                             float(format_penalty), *self.dims())
+            self._boards_valid = False  # (the render-fused turn keeps no cache)
             self._invalidate()
             self._rows = rows
             return
-        if self.dispatch == "ctypes":
+        if self.dispatch == "ctypes" or self.boards is not None:
             ops._dev(self.room_state, actions, n_actions, has_input, err)
-            ops.sokoban_step_turn(self.struct(), self.ep, ops.turn_struct(int(turn), actions, n_actions, has_input,
+            ops.sokoban_step_turn(self._turn_struct(), self.ep, ops.turn_struct(int(turn), actions, n_actions, has_input,
                                                                           int(max_actions_per_traj),
                                                                           float(format_penalty)), err)
         else:

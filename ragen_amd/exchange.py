@@ -143,10 +143,11 @@ class ArenaExchange:
     """One rank's side of the one-shot exchange of `nbytes` per rank.
 
     group: the process group whose ranks exchange (None: the default group if initialised, else a
-    1-rank exchange).  mode: "uncached" (default) or "finegrained" receive memory.  Every rank
+    1-rank exchange).  mode: "finegrained" (default) or "uncached" receive memory (measurement
+    only: it served stale rows in one process after earlier regions were freed).  Every rank
     must construct it (collective: the handle exchange)."""
 
-    def __init__(self, nbytes: int, device, group=None, mode: str = "uncached", timeout_us: int = 2_000_000,
+    def __init__(self, nbytes: int, device, group=None, mode: str = "finegrained", timeout_us: int = 2_000_000,
                  blocks_per_peer: int = 0, _regions=None, _rank=None, _world=None):
         self.device = torch.device(device)
         self.nbytes = int(nbytes)
@@ -209,7 +210,7 @@ class ArenaExchange:
         self._view = device_bytes(regions[self.rank], region_bytes(self.world, self.nbytes), self.device, self._keep)
 
     @classmethod
-    def in_process(cls, world: int, nbytes: int, device, mode: str = "uncached", **kw) -> List["ArenaExchange"]:
+    def in_process(cls, world: int, nbytes: int, device, mode: str = "finegrained", **kw) -> List["ArenaExchange"]:
         """W ranks' exchanges in ONE process on one device (no IPC): regions allocated here, each
         rank's pointer table holding all W.  Launch every rank's PUBLISH before any WAIT when they
         share a stream (a rank's WAIT needs every sender's PUBLISH)."""

@@ -279,6 +279,8 @@ class TurnChain:
             c.pad_block = None
         stream = ops._stream(self.dev)
         ops.D2H_COUNT[0] += 1
+        if getattr(self.batch, "boards", None) is not None:
+            self.batch.invalidate_boards()  # (the chain's token turn keeps no board cache)
         ops.check(_lib.lib().rmi_turn_chain(ctypes.byref(c), stream), "rmi_turn_chain")
         self.runs += 1
         if ops._RING:  # the chain waited for its copy: every upload enqueued before it has run

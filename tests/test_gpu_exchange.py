@@ -46,7 +46,16 @@ def test_in_process_split_exchange(device, W, nbytes):
             want = torch.stack(srcs)
             for r in range(W):
                 assert exs[r].epoch == e
-                assert torch.equal(exs[r].slot(), want), (W, e, r)
+                got = exs[r].slot()
+                if not torch.equal(got, want):
+                    d = (got != want).nonzero()
+                    exp = torch.stack([_arena(q, e, base) for q in range(W)])
+                    raise AssertionError(
+                        f"W={W} e={e} rank {r}: {d.shape[0]} bytes differ, first {d[:3].tolist()} last {d[-3:].tolist()}; "
+                        f"slot==regenerated {torch.equal(got, exp)} sources==regenerated {torch.equal(want, exp)}; "
+                        f"srcs {[hex(x.data_ptr()) for x in srcs]} regions {[hex(q) for q in exs[0].regions]} "
+                        f"state {[hex(x.state.data_ptr()) for x in exs]} err {[hex(x.err.data_ptr()) for x in exs]} "
+                        f"base {[hex(x.data_ptr()) for x in base]}")
             if e >= 2:  # the previous epoch's slot is intact until epoch e + 1 rewrites it
                 prev = torch.stack([_arena(q, e - 1, base) for q in range(W)])
                 assert torch.equal(exs[0].slot(e - 1), prev)

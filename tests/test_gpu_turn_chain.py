@@ -115,9 +115,12 @@ def test_turn_chain_bench_workload(device):
 
 
 def test_reward_text_cache_refuses_torn_entries(device, qwen_tok, monkeypatch):
-    """The chained prompt launches' reward text cache (rmi_prompt_t.num_cache): a second rollout
-    after every cached entry's text was altered (its check not) prints the same prompts as the
-    step-by-step path: an entry whose contents do not match its check is recomputed, not used."""
+    """The chained prompt launches' reward text cache (rmi_prompt_t.num_cache) is write-once and
+    exact: after the first rollout, half of the cached entries lose a text word (as a reader would
+    see an entry whose text is not yet visible: a zero byte below the length) and the other half
+    their key (another value's slot); the second rollout prints the same prompts as the
+    step-by-step path (every such entry is a miss and the row computes its text), and no claimed
+    slot is written again (the altered entries are still as altered)."""
     from ragen_amd.env import SokobanBatch
     monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
     name = "sokoban_es"
@@ -130,15 +133,21 @@ def test_reward_text_cache_refuses_torn_entries(device, qwen_tok, monkeypatch):
     proxy.train_ctx_manager.set_device_vocab(_vocab(qwen_tok, device))
     random.seed(7)
     outs = []
+    altered = None
     for rep in range(2):
         if rep == 1:
             nc = proxy.train_ctx_manager.prompts().num_cache.view(-1, 16)
-            ready = nc[:, 2] < 0  # the ready bit
-            assert int(ready.sum()) > 0  # the first rollout cached its rewards' text
-            nc[ready, 3] ^= 0x01010101  # every entry's text changed, its check not
+            ready = torch.nonzero(nc[:, 2] < 0).flatten()  # the ready bit
+            assert ready.numel() > 1  # the first rollout cached its rewards' text
+            torn, foreign = ready[0::2], ready[1::2]
+            nc[torn, 3] = 0                  # the text's first word not visible
+            nc[foreign, 0] ^= 0x00010000     # another value's key
+            altered = nc.clone()
         actor.prompts = []
         out = proxy.rollout(DataProto(meta_info={}), val=False)
         outs.append((out, [tuple(x.cpu() for x in p) for p in actor.prompts], proxy.train_es_manager.rollout_cache,
                      dict(out.meta_info)))
+    nc = proxy.train_ctx_manager.prompts().num_cache.view(-1, 16)
+    assert torch.equal(nc[ready], altered[ready]), "a claimed slot was written again"
     for a, b in zip(outs, plain):
         _same(a, b)
