@@ -1173,6 +1173,8 @@ def make_parser():
                          "gathered before its update, as agent_trainer.fit does; >1 amortises it: an extra)")
     ap.add_argument("--double-buffer", action="store_true",
                     help="run the N>1 exchange path at N=1 (a 1-rank RCCL group, real collectives)")
+    ap.add_argument("--no-boards", action="store_true",
+                    help="turn launches without the board cache (every turn decodes the grid rows; A/B)")
     ap.add_argument("--transport", choices=("auto", "ipc", "rccl"), default="auto",
                     help="N>1: how the per-rollout arena gather moves bytes: 'ipc' = the one-shot exchange "
                          "(every rank stores its arena into every peer's IPC-mapped region, rmi_xgather), 'rccl' = "
@@ -1203,7 +1205,7 @@ def main():
                 os.environ.setdefault(k, v)
         tdist.init_process_group("nccl", device_id=device)
 
-    R = Rollout(device, rank)
+    R = Rollout(device, rank, boards=not args.no_boards)
     # env steps per rollout (deterministic: every replay executes the same actions)
     R.step()
     torch.cuda.synchronize()
@@ -1545,6 +1547,7 @@ def main():
                                    f"cap {MAX_ACTIONS}, groups of {GROUP}; rollout phase (reset excluded)",
                        "envs_per_gpu": B_PER_GPU, "env_steps_per_rollout_rank0": steps_per_rollout,
                        "graph": graph is not None, "rollouts_per_replay": G, "parallelism": f"env-sharded x{world}",
+                       "board_cache": R.boards,
                        "exchange_mode": exchange_mode if dist else None,
                        "exchange_transport": transport, "exchange_transport_note": xg_note,
                        "rollouts_per_gather": (G if exchange_mode == "overlap" else P) if dist else None},

@@ -106,9 +106,9 @@ typedef struct {
   uint8_t* num_env_steps;     /* [B]  (<= num_actions <= 255: one env step per action)     */
   int8_t* boxes_on_target;    /* [B]  num_boxes - open targets: -64..64 for H*W <= 64      */
   /* Optional board cache (NULL: none), caller-owned like every other field: 16 B per env
-   * holding the room's bitboards after the last turn (window wall | target | box u32, then
-   * the player's cell index and a tag byte: 1 = the room is regular and the entry is its
-   * state).  boards_mode RMI_BOARDS_BUILD: the turn decodes every env's rows as without a
+   * holding the room's state after the last turn (window wall | target | box u32, then the
+   * player's cell index, a tag byte -- 1 = the room is regular and the entry is its state --,
+   * num_env_steps and boxes_on_target; the SoA fields are written as without a cache).  boards_mode RMI_BOARDS_BUILD: the turn decodes every env's rows as without a
    * cache and writes every live env's entry; RMI_BOARDS_USE: the turn trusts the tagged
    * entries of the acting envs (no row loads, no decode) and keeps them current -- valid only
    * while nothing but rmi_sokoban_step_turn{,_first,_finalize} launches with this cache have

@@ -8,11 +8,14 @@
 // hop: each rank stores its arena into every peer's receive region, all 7 links at once, and
 // the gather is complete when all W senders' arrival counts reached the epoch's.
 //
-// Memory model (MI355X_MICROARCH.md / cdna_hip_programming.md §6 G16, carried to system scope
-// because the readers are other devices): every storing thread releases at system scope, the
-// block barrier joins them, then ONE lane adds the block's arrival with a system-scope release;
-// the waiting lanes poll relaxed at system scope (these loads bypass the caches) and fence once
-// with a system-scope acquire.  The receive regions are fine-grained device memory, whose L2
+// Memory model (MI355X_MICROARCH.md / cdna_hip_programming.md §6 G16, in its no-release form,
+// carried to system scope because the readers are other devices): every store of the handed-off
+// bytes is a system-scope (sc0 sc1) store, written through to the receiving memory, and drained
+// (vmcnt 0) before the block barrier; then ONE lane adds the block's arrival.  No release fence:
+// a system-scope release writes back the whole L2 of the XCD (buffer_wbl2), which the rollout
+// just filled with dirty lines — measured +4 us per exchange at W = 1.  The waiting lanes poll
+// relaxed at system scope (these loads bypass the caches) and fence once with a system-scope
+// acquire.  The receive regions are fine-grained device memory, whose L2
 // lines (MTYPE NC) are invalidated by that acquire and at every kernel boundary, so no L2 on the
 // receiving GPU serves a stale copy of a slot a peer rewrote.
 // Every wait is bounded by the constant 100-MHz clock: a missing peer sets an error bit and the
@@ -31,6 +34,8 @@ constexpr int kXgBlock = 256;
 constexpr int64_t kXgHdr = 4096;   // header bytes: consumed at 0, arrivals[q] at 64 + 8q
 constexpr int64_t kXgAlign = 4096;  // row alignment inside a slot
 constexpr int kArrivals = 8;        // u64 index of arrivals[0]
+constexpr int kSysStore = 1 | 16;   // buffer cache policy: sc0 | sc1 = system scope (write-through)
+constexpr int kRsrcWord3 = 0x00020000;  // gfx9 raw buffer descriptor word 3 (32-bit data format)
 
 struct XgArgs {
   const v4u* src;
@@ -67,8 +72,9 @@ __global__ __launch_bounds__(kXgBlock) void xgather_kernel(XgArgs a) {
     const int p = b / a.nb, c = b - p * a.nb;
     u64* hdr = reinterpret_cast<u64*>(a.region[p]);
     // everything enqueued before this launch has finished reading slot (e - 1) & 1 of our region
+    // (a kernel boundary: reads need no release)
     if (b == 0 && tid == 0)
-      __hip_atomic_store(reinterpret_cast<u64*>(a.region[a.rank]), e - 1, __ATOMIC_RELEASE,
+      __hip_atomic_store(reinterpret_cast<u64*>(a.region[a.rank]), e - 1, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid == 0) {
       // slot e & 1 of peer p last held epoch e - 2: p must be done with it
@@ -80,14 +86,23 @@ __global__ __launch_bounds__(kXgBlock) void xgather_kernel(XgArgs a) {
     if (!s_ok) return;
     const int64_t per = (a.n16 + a.nb - 1) / a.nb;
     const int64_t lo = (int64_t)c * per, hi = lo + per < a.n16 ? lo + per : a.n16;
-    v4u* dst = reinterpret_cast<v4u*>(a.region[p] + kXgHdr + (int64_t)(e & 1) * a.slot_bytes +
-                                      (int64_t)a.rank * a.nbp);
-    for (int64_t i = lo + tid; i < hi; i += kXgBlock) dst[i] = __builtin_nontemporal_load(a.src + i);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // this thread's stores, system scope
+    // this block's chunk of the row, as system-scope (sc0 sc1: write-through) 16-B buffer stores
+    uint8_t* dst = a.region[p] + kXgHdr + (int64_t)(e & 1) * a.slot_bytes + (int64_t)a.rank * a.nbp + lo * 16;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7FFFFFF0, kRsrcWord3);
+    // two 16-B pieces per lane per step, both loads issued before either store (a block holds
+    // ~8 KB: one step for most lanes)
+    for (int64_t i0 = lo + tid; i0 < hi; i0 += 2 * kXgBlock) {
+      const int64_t i1 = i0 + kXgBlock;
+      const v4u v0 = __builtin_nontemporal_load(a.src + i0);
+      const v4u v1 = __builtin_nontemporal_load(a.src + (i1 < hi ? i1 : i0));
+      __builtin_amdgcn_raw_buffer_store_b128(v0, rs, (int)((i0 - lo) * 16), 0, kSysStore);
+      if (i1 < hi) __builtin_amdgcn_raw_buffer_store_b128(v1, rs, (int)((i1 - lo) * 16), 0, kSysStore);
+    }
+    __builtin_amdgcn_s_waitcnt(0);  // every store acknowledged by the memory it was written to
     __syncthreads();
     if (tid == 0) {
-      __hip_atomic_fetch_add(hdr + kArrivals + a.rank, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_fetch_add(a.state + 1, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(hdr + kArrivals + a.rank, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_fetch_add(a.state + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -100,7 +115,7 @@ __global__ __launch_bounds__(kXgBlock) void xgather_kernel(XgArgs a) {
     ok = wait_ge(a.state + 1, e * (u64)a.W * (u64)a.nb, deadline);
   if (!ok) atomicOr(a.err, (uint32_t)RMI_XG_ERR_ARRIVALS);
   __syncthreads();
-  if (tid == 0) __hip_atomic_store(a.state, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(a.state, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // read after the kernel boundary
 }
 
 int64_t row_bytes(int64_t nbytes) { return (nbytes + kXgAlign - 1) / kXgAlign * kXgAlign; }
@@ -119,10 +134,11 @@ RMI_API int64_t rmi_xgather_slot_offset(int32_t world, int64_t nbytes, int64_t e
 }
 
 RMI_API int32_t rmi_xgather_blocks_per_peer(int64_t nbytes) {
-  // ~32 KB per storing block: 8 16-B stores in flight per lane, and enough blocks per peer
-  // (16 for the 0.5-MB SK arena) to keep the link to that peer busy
-  int64_t nb = (nbytes + 32767) / 32768;
-  return (int32_t)(nb < 1 ? 1 : (nb > 64 ? 64 : nb));
+  // ~8 KB per storing block: two 16-B pieces per lane, one step, so a block's latency is one
+  // load and one write-through store; 61 blocks per peer for the 0.5-MB SK arena (the first
+  // form, 32 KB per block in 8 dependent steps, measured 6.3 us per exchange at W = 1)
+  int64_t nb = (nbytes + 8191) / 8192;
+  return (int32_t)(nb < 1 ? 1 : (nb > 256 ? 256 : nb));
 }
 
 RMI_API int rmi_xgather_alloc(int64_t bytes, int32_t mode, void** region, uint8_t* handle) {

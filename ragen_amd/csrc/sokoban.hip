@@ -691,7 +691,11 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
   }
   const int8_t* pl = kFirst ? init_player : env.player;
-  int r = pl[2 * bc], c = pl[2 * bc + 1];
+  int r = 0, c = 0;
+  if (!use) {  // (USE: the entry holds the player cell and the two counters)
+    r = pl[2 * bc];
+    c = pl[2 * bc + 1];
+  }
   // branch-free: a conditional load here would make the compiler wait for the rows first
   const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
   uint8_t flags = 0;
@@ -700,8 +704,10 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   double penalty = 0.0;
   if (!kFirst) {  // a fresh episode's record is all zero (EnvStatus(), es_manager.py:95)
     flags = ep.flags[bc];
-    nes = env.num_env_steps[bc];
-    bot = env.boxes_on_target[bc];
+    if (!use) {
+      nes = env.num_env_steps[bc];
+      bot = env.boxes_on_target[bc];
+    }
     num_actions = ep.num_actions[bc];
     n_turns = ep.n_turns[bc];
     penalty = ep.penalty[bc];
@@ -731,10 +737,23 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   // USE: the entry stands in for the rows while it is tagged and the actions stay on the
   // regular path; else this wave loads its rows now and decodes them
   bool from_cache = use && (ent.w >> 8 & 0xFFu) == 1u && acts_ok;
+  if (use) {
+    // the tagged entry's player cell and counters (entry word 3: cell | tag << 8 | nes << 16 |
+    // bot << 24); an untagged entry's are reloaded below with the rows
+    const int p = (int)(ent.w & 0xFFu);
+    r = (int)(((uint32_t)p * w_magic) >> 16);
+    c = p - r * W;
+    nes = (int)(ent.w >> 16 & 0xFFu);
+    bot = (int)(int8_t)(ent.w >> 24);
+  }
   if (use && !__all(from_cache || !act)) {
     from_cache = false;
     load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
     load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+    r = env.player[2 * bc];
+    c = env.player[2 * bc + 1];
+    nes = env.num_env_steps[bc];
+    bot = env.boxes_on_target[bc];
   }
   bool regular = true, room_ok = false;
   M wall = 0, target = 0, box = 0;
@@ -956,7 +975,9 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     const uint32_t tag = (stepped_fast || !act) ? (from_cache || room_ok ? 1u : 0u) : 0u;
     if (write) {
       const uint32_t cell = (uint32_t)(jp + W) & 0xFFu;
-      reinterpret_cast<Dw4*>(env.boards)[b] = Dw4{(uint32_t)wall, (uint32_t)target, (uint32_t)box, cell | (tag << 8)};
+      reinterpret_cast<Dw4*>(env.boards)[b] = Dw4{(uint32_t)wall, (uint32_t)target, (uint32_t)box,
+                                                   cell | (tag << 8) | ((uint32_t)nes & 0xFFu) << 16 |
+                                                       ((uint32_t)bot & 0xFFu) << 24};
     }
   }
   RMI_STAMP(4);

@@ -14,13 +14,13 @@ from ragen_amd import exchange
 
 def test_plan_layout():
     p = exchange.plan(8, 499712)
-    assert p["row_bytes"] == 499712 and p["blocks_per_peer"] == 16 and p["grid"] == 8 * 16 + 1
+    assert p["row_bytes"] == 499712 and p["blocks_per_peer"] == 61 and p["grid"] == 8 * 61 + 1
     assert p["region_bytes"] == 4096 + 2 * 8 * 499712
     assert p["slot_offsets"] == [4096 + 8 * 499712, 4096]  # epoch 1 -> slot 1, epoch 2 -> slot 0
     assert exchange.slot_offset(8, 499712, 3) == exchange.slot_offset(8, 499712, 1)
     q = exchange.plan(3, 4096 + 48)
     assert q["row_bytes"] == 8192 and q["region_bytes"] == 4096 + 2 * 3 * 8192 and q["blocks_per_peer"] == 1
-    assert exchange.plan(16, 1 << 30)["blocks_per_peer"] == 64
+    assert exchange.plan(16, 1 << 30)["blocks_per_peer"] == 256
     for bad in ((0, 16), (17, 16), (2, 0)):
         with pytest.raises(ValueError):
             exchange.region_bytes(*bad)

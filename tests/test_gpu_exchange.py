@@ -71,7 +71,7 @@ def test_fused_single_rank_and_plan(device):
     (ex,) = ArenaExchange.in_process(1, ARENA, device)
     try:
         p = plan(1, ARENA)
-        assert p["blocks_per_peer"] == 16 and p["grid"] == 17 and p["row_bytes"] == 499712
+        assert p["blocks_per_peer"] == 61 and p["grid"] == 62 and p["row_bytes"] == 499712
         src = torch.randint(0, 256, (ARENA,), dtype=torch.uint8, device=device)
         for e in range(1, 6):
             src.add_(1)
