@@ -604,9 +604,11 @@ typedef struct {
    * once and kept across calls for this tokenizer's tables — a pre-token's bytes (2..16) ->
    * its BPE ids (<= 9).  A pre-token's merges depend on its bytes alone (the tokenizers
    * crate caches words the same way), so a hit skips its pair lookups and merges.  Entries
-   * are claimed with an atomic compare-and-swap after a plain read finds the slot empty, and
-   * carry a 64-bit check of their contents: a reader takes only an entry whose check
-   * matches (no acquire / release across the XCDs' L2s inside a launch).                  */
+   * are claimed with an atomic compare-and-swap after a plain read finds the slot empty and
+   * written once; every dword goes from zero to its final value once, ids are stored plus
+   * one, and only words with no all-zero key dword are cached, so a reader (no acquire /
+   * release across the XCDs' L2s inside a launch) that sees the key, the ready meta and
+   * nonzero ids holds exactly the writer's entry; any other state is a miss.              */
   uint32_t* word_cache;
   uint32_t word_cache_mask; /* entries - 1 (a power of two minus one)                        */
   /* Expansions (n_exp 0: none): added tokens whose id in added_id is -(e + 1) stand for the

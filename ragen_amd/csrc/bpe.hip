@@ -130,14 +130,18 @@ __device__ __forceinline__ uint64_t merge_lookup(const rmi_bpe_t& t, uint32_t a,
 }
 
 // ---- the word cache (rmi_bpe_t.word_cache): 16 u32 per entry — the word's bytes (4 u32,
-// zero padded), meta = ready | claimed | count << 8 | length, up to 9 ids, and a 64-bit check
-// of all of them.  Linear probing over kWcProbe slots; a slot is claimed by compare-and-swap on
-// meta (0 -> claimed) and written once.  No acquire / release: the 8 XCDs' L2s are not coherent
-// with each other inside a launch, and agent-scope ordering would write back / invalidate L2 on
-// every probe.  A reader may therefore see an older state of a slot — empty, claimed, or a
-// partly written entry — and takes only an entry whose check matches its contents; anything
-// else is a miss (the word is merged as before, and maybe inserted again one slot on).
-// Launch boundaries make every XCD's entries visible to the next call.
+// zero padded), meta = ready | claimed | count << 8 | length, up to 9 ids stored as id + 1.
+// Linear probing over kWcProbe slots; a slot is claimed by compare-and-swap on meta
+// (0 -> claimed) and written once.  No acquire / release: the 8 XCDs' L2s are not coherent with
+// each other inside a launch, and agent-scope ordering would write back / invalidate L2 on every
+// probe.  A reader may therefore see an older state of a slot — empty, claimed, or a partly
+// written entry — and the entry is laid out so that any such state is a miss, exactly: every
+// dword of a slot goes 0 -> its final value once (dword stores and loads are single-copy
+// atomic); meta is ready only in its final value; only words whose every key dword below the
+// length is nonzero are inserted, and ids are stored plus one, so a dword still invisible (0)
+// never equals the reader's key dword and never passes as an id.  Such a miss merges the word
+// as before (and maybe inserts it again one slot on).  Launch boundaries make every XCD's
+// entries visible to the next call.
 constexpr int kWcWordMax = 16, kWcIdsMax = 9, kWcProbe = 8;
 constexpr uint32_t kWcReady = 1u << 31, kWcClaimed = 1u << 30;
 
@@ -158,11 +162,6 @@ __device__ __forceinline__ void wc_key(const uint8_t* T, int a, int len, uint32_
   }
 }
 
-__device__ __forceinline__ uint64_t wc_mix(uint64_t h, uint32_t v) {
-  h = (h ^ v) * 0x100000001B3ull;
-  return h ^ (h >> 31);
-}
-
 __device__ __forceinline__ uint32_t wc_slot(const uint32_t k[4], int len, uint32_t mask) {
   uint64_t x = (((uint64_t)k[1] << 32) | k[0]) * 0x9E3779B97F4A7C15ull;
   x ^= ((((uint64_t)k[3] << 32) | k[2]) + (uint64_t)len) * 0xC2B2AE3D27D4EB4Full;
@@ -170,16 +169,9 @@ __device__ __forceinline__ uint32_t wc_slot(const uint32_t k[4], int len, uint32
   return (uint32_t)(x >> 32) & mask;
 }
 
-__device__ __forceinline__ uint64_t wc_check(const uint32_t k[4], uint32_t meta) {
-  uint64_t h = 0xCBF29CE484222325ull;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) h = wc_mix(h, k[i]);
-  return wc_mix(h, meta);
-}
-
-// One probed entry, loaded whole (the ids and the check come with the key: no second round
-// trip for a hit): -> the word's id count (ids written to Y[0..)) if it holds the word, else 0;
-// empty: the slot is empty (the probe sequence ends there).
+// One probed entry, loaded whole (the ids come with the key: no second round trip for a hit):
+// -> the word's id count (ids written to Y[0..)) if it holds the word, else 0; empty: the slot
+// is empty (the probe sequence ends there).
 __device__ __forceinline__ int wc_take(const uint4 (&w)[4], const uint32_t k[4], int len, int32_t* Y, bool& empty) {
   const uint32_t m = w[1].x;
   empty = m == 0;
@@ -189,14 +181,14 @@ __device__ __forceinline__ int wc_take(const uint4 (&w)[4], const uint32_t k[4],
   const int cnt = (int)((m >> 8) & 0xFF);
   if (cnt < 1 || cnt > kWcIdsMax) return 0;
   const uint32_t ids[kWcIdsMax] = {w[1].y, w[1].z, w[1].w, w[2].x, w[2].y, w[2].z, w[2].w, w[3].x, w[3].y};
-  uint64_t c = wc_check(k, m);
+  bool vis = true;  // every id written (stored + 1: 0 = not visible here yet)
 #pragma unroll
   for (int q = 0; q < kWcIdsMax; ++q)
-    if (q < cnt) c = wc_mix(c, ids[q]);
-  if ((((uint64_t)w[3].w << 32) | w[3].z) != c) return 0;
+    if (q < cnt) vis &= ids[q] != 0u;
+  if (!vis) return 0;
 #pragma unroll
   for (int q = 0; q < kWcIdsMax; ++q)
-    if (q < cnt) Y[q] = (int32_t)ids[q];
+    if (q < cnt) Y[q] = (int32_t)(ids[q] - 1u);
   return cnt;
 }
 
@@ -222,6 +214,11 @@ __device__ __forceinline__ int wc_find_from(const rmi_bpe_t& t, const uint32_t k
 // the ids: the symbol chain from a (Y at each symbol start, M the next start)
 __device__ void wc_insert(const rmi_bpe_t& t, const uint32_t k[4], int len, const int32_t* Y, const uint16_t* M,
                           int a, int cnt) {
+  // a key dword below the length that is zero could not tell "not visible yet" from the word
+  // (four NUL bytes): such words are not cached
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * i < len && k[i] == 0u) return;
   uint32_t h = wc_slot(k, len, t.word_cache_mask);
   for (int i = 0; i < kWcProbe; ++i, h = (h + 1) & t.word_cache_mask) {
     uint32_t* s = t.word_cache + 16 * (size_t)h;
@@ -238,14 +235,8 @@ __device__ void wc_insert(const rmi_bpe_t& t, const uint32_t k[4], int len, cons
     }
     if (atomicCAS(s + 4, 0u, kWcClaimed) != 0u) return;
     const uint32_t m = kWcReady | ((uint32_t)cnt << 8) | (uint32_t)len;
-    uint64_t c = wc_check(k, m);
     *reinterpret_cast<uint4*>(s) = make_uint4(k[0], k[1], k[2], k[3]);
-    for (int q = 0, p = a; q < cnt; ++q, p = M[p]) {
-      s[5 + q] = (uint32_t)Y[p];
-      c = wc_mix(c, (uint32_t)Y[p]);
-    }
-    s[14] = (uint32_t)c;
-    s[15] = (uint32_t)(c >> 32);
+    for (int q = 0, p = a; q < cnt; ++q, p = M[p]) s[5 + q] = (uint32_t)Y[p] + 1u;
     s[4] = m;
     return;
   }
