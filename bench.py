@@ -74,6 +74,36 @@ def _pmc_source(pattern):
     return {"file": os.path.relpath(files[-1], ROOT), "from": d.get("source"), "workload": d.get("workload")}
 
 
+ISSUE_GLOB = os.path.join(ROOT, "profiles", "r*_issue_frac.json")  # the text kernels' issue-rate pass
+
+
+def attach_issue_fracs(text):
+    """The text kernels are bound by instruction issue, not HBM (their `frac` of 8 TB/s is near
+    zero): each text_api block gets the issue-rate figures of the newest committed PMC pass
+    (tools/r06_issue_pmc.sh, tools/issue_frac.py) -- instructions per launch and durations from
+    the same profiled launches (a counter pass cannot run inside the timed process)."""
+    files = sorted(glob.glob(ISSUE_GLOB))
+    if not files:
+        return
+    with open(files[-1]) as f:
+        d = json.load(f)
+    where = {"parse": ("parse",), "detok": ("detokenize",), "detok_parse": ("detok_parse",),
+             "token_turn": ("token_rollout",), "bpe_encode": ("prompt", "bpe_encode"),
+             "prompt_text": ("prompt", "prompt_text")}
+    for k, path in where.items():
+        v = d["kernels"].get(k)
+        blk = text
+        for p in path:
+            blk = blk.get(p) if isinstance(blk, dict) else None
+        if v is None or not isinstance(blk, dict):
+            continue
+        blk["issue_frac"] = v["issue_frac"]
+        blk["valu_frac"] = v["valu_frac"]
+        blk["salu_frac"] = v["salu_frac"]
+        blk["issue_source"] = {"file": os.path.relpath(files[-1], ROOT), "profiled_avg_us": v["avg_us"],
+                               "insts_per_wave": v["per_wave"], "definition": d["definition"]}
+
+
 class Rollout:
     """The SK rollout on one rank.  boards: the turn launches keep the board cache
     (SokobanBatch.enable_boards): the first turn of a rollout builds it (a fresh episode always
@@ -1484,6 +1514,8 @@ def main():
     text = text_leg(R, device) if not args.no_extras and rank == 0 else None
     if text is not None and api is not None:  # the caller path's text kernels (measured in api_leg)
         text["prompt"] = api.pop("prompt_kernels", None)
+    if text is not None:
+        attach_issue_fracs(text)
     at_scale = None
     if not args.no_extras and rank == 0:
         s_dur, s_B = scale_leg(R, device)
