@@ -294,7 +294,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6))) void pr
               l = nc ? num_take(ne, nkey, o) : -1;
               if (l < 0) {
                 l = py_float_repr(r, o, scr);
-                if (nc && l > 0 && l <= 24) num_put(P.num_cache + 16 * (size_t)num_slot(nkey, P.num_cache_mask), nkey, o, l);
+                // inserted from the rows whose early-loaded entry was empty, and from one row in 16:
+                // thousands of rows of one launch miss on the same new value, and a compare-and-swap
+                // from each would serialise them on one line (ragen_amd/csrc/bpe.hip wc_insert)
+                if (nc && l > 0 && l <= 24 && (ne[0].x | ne[0].y) == 0u && (b & 15) == 0)
+                  num_put(P.num_cache + 16 * (size_t)num_slot(nkey, P.num_cache_mask), nkey, o, l);
               }
             }
 #endif

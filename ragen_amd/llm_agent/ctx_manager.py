@@ -1015,7 +1015,13 @@ class ContextManager:
         sharded = self.process_group is not None and self.world_size > 1
         local = {}  # per tag NAME, env order (a tag listed twice in the config: its entries' rows in order)
         for tag, m, custom, _ in parts:
+            if tag not in local and not sharded:
+                local[tag] = (m, custom)  # (one entry: the metric rows and the custom mask as they are)
+                continue
             rows = np.concatenate([m, custom[:, None].astype(np.float64)], 1)
+            if tag in local and isinstance(local[tag], tuple):
+                m0, c0 = local[tag]
+                local[tag] = np.concatenate([m0, c0[:, None].astype(np.float64)], 1)
             local[tag] = np.concatenate([local[tag], rows]) if tag in local else rows
         per_tag = {}
         for tag in dict.fromkeys(self.es_cfg.env_configs.tags):  # every rank, same order (collectives)
@@ -1023,17 +1029,23 @@ class ContextManager:
             if sharded:
                 rows = rd.all_gather_rows(torch.from_numpy(rows).to(self.device), group=self.process_group,
                                           sizes=self.shard_sizes(tag)).cpu().numpy()
-            if len(rows):
-                per_tag[tag] = [rows]
+            if len(rows[0] if isinstance(rows, tuple) else rows):
+                per_tag[tag] = rows
         metrics, nz = {}, []
         for tag in dict.fromkeys(self.es_cfg.env_configs.tags):
             if tag not in per_tag:
                 continue
-            rows = np.concatenate(per_tag[tag])
-            cust = rows[:, 4] != 0
-            cols = [("success", rows[:, 0]), ("num_actions", rows[:, 1].astype(np.int64))]
+            rows = per_tag[tag]
+            if isinstance(rows, tuple):  # the metric rows [n, 4] and the custom mask, unconcatenated
+                m, cust = rows
+                m = np.ascontiguousarray(m.T)  # one pass: each column contiguous for its reductions
+            else:
+                m, cust = np.ascontiguousarray(rows[:, :4].T), rows[:, 4] != 0
+            cols = [("success", m[0]), ("num_actions", m[1].astype(np.int64))]
             if cust.any():
-                cols += [("action_is_effective", rows[cust, 2]), ("action_is_valid", rows[cust, 3])]
+                all_c = bool(cust.all())
+                cols += [("action_is_effective", m[2] if all_c else m[2][cust]),
+                         ("action_is_valid", m[3] if all_c else m[3][cust])]
             for k, v in cols:
                 metrics[f"{tag}/{k}"] = np.sum(v) / self.env_nums[tag]
                 nz.append((f"{tag}/non-zero/{k}", v[v != 0]))
