@@ -151,3 +151,40 @@ def test_reward_text_cache_refuses_torn_entries(device, qwen_tok, monkeypatch):
     assert torch.equal(nc[ready], altered[ready]), "a claimed slot was written again"
     for a, b in zip(outs, plain):
         _same(a, b)
+
+
+def test_turn_chain_decode_overflow_second_pass(device, monkeypatch):
+    """A later turn's generations longer than the decode's row hint (the longest generation seen
+    so far, with a margin): after the chained turn has run its whole chain for every env, the
+    overflowed envs are masked out of that pass and stepped by a second pass
+    (EnvStateManager._step_device).  Chained == step by step -- every generation batch, the
+    formulated batch, its metrics and the rollout cache -- and the second pass ran in both."""
+    from ragen_amd.env import SokobanBatch
+    from ragen_amd.llm_agent import es_manager as esm
+    monkeypatch.setattr(SokobanBatch, "reseed_fn", staticmethod(_hashseed0_reseed))
+    tok = FakeQwenTok()
+    name = "sokoban_es"
+    cfg = _config(name)
+    _, ng, gs, T, _ = TRACES[name]
+    B = ng * gs
+    turn_tokens = []
+    for t in range(T):
+        texts = _responses(name, t, B)
+        if t == 2:  # every third env thinks at length: ~5x the longest generation of turns 0-1
+            texts = [("let me think " * 30 + x) if i % 3 == 0 else x for i, x in enumerate(texts)]
+        turn_tokens.append(_ids(tok, texts, device))
+    seconds = []
+    real = esm.EnvStateManager._device_pass
+
+    def counting(self, inp, t, first, *a, **kw):
+        if first is not None:
+            seconds.append(t)
+        return real(self, inp, t, first, *a, **kw)
+
+    monkeypatch.setattr(esm.EnvStateManager, "_device_pass", counting)
+    chained, runs, _ = _run(cfg, tok, turn_tokens, device, True, reps=1)
+    n_chain = len(seconds)
+    plain, runs0, _ = _run(cfg, tok, turn_tokens, device, False, reps=1)
+    assert runs == len(chained[0][1]) and runs0 == 0
+    assert n_chain == 1 and seconds == [2, 2], seconds  # turn 2 took the second pass, both ways
+    _same(chained[0], plain[0])
