@@ -1385,6 +1385,13 @@ def main():
             run = run_overlap if exchange_mode == "overlap" else run_serial_p(P)
             if transport == "ipc" and exchange_mode == "serial" and P == 1:
                 run = run_ipc
+                if args.transport == "auto":  # the faster of the two transports on this node
+                    t_ipc = min(trial(run_ipc) for _ in range(3))
+                    t_rccl = min(trial(run_serial_p(1)) for _ in range(3))
+                    xg_note = (f"{xg_note}; auto: one-shot {t_ipc / (4 * G) * 1e3:.4f} ms vs RCCL "
+                               f"{t_rccl / (4 * G) * 1e3:.4f} ms per rollout (best of 3 trials, max over ranks)")
+                    if t_rccl < t_ipc:
+                        run, transport = run_serial_p(1), "rccl"
             else:
                 transport = "rccl"  # (the amortised placements gather with RCCL)
 

@@ -31,10 +31,12 @@ waves = (B + 63) // 64
 stamps = torch.zeros(waves, 16, dtype=torch.int64, device=dev)
 assert ctypes.CDLL(SO).rmi_sokoban_set_stamps(ctypes.c_void_p(stamps.data_ptr())) == 0
 e = R.env
+# "noboards": every turn decodes its rows (the form before the board cache)
+st0, stn = (R.st, R.st) if "noboards" in sys.argv else (R.st_first, R.st_next)
 for rep in range(5):
-    ops.sokoban_step_turn_first(R.st, e.ep, R.turns[0], e.init_state, e.init_player)
+    ops.sokoban_step_turn_first(st0, e.ep, R.turns[0], e.init_state, e.init_player)
     for t in range(1, 3):
-        ops.sokoban_step_turn(R.st, e.ep, R.turns[t])
+        ops.sokoban_step_turn(stn, e.ep, R.turns[t])
     torch.cuda.synchronize()
 a = stamps.cpu().numpy().astype(np.float64)
 ph = [a[:, 2 * (i + 1)] - a[:, 2 * i] for i in range(4)]
