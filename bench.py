@@ -127,8 +127,10 @@ class Rollout:
         self.turns = [ops.turn_struct(t, self.ids[t], self.n[t], None, MAX_ACTIONS, -0.1) for t in range(T_TURNS)]
         self.st = e.struct()
         self.boards = bool(boards) and e.enable_boards()
-        # turn 0 (after a restore or fused with it) builds the cache, turns 1.. use it
+        # turn 0 (after a restore or fused with it) builds the cache, turns 1.. use it; the fused
+        # first turn builds the reset state's entries once, and later rollouts' first turns read them
         self.st_first = e.board_struct(_lib.BOARDS_BUILD) if self.boards else self.st
+        self.st_first_use = e.board_struct(_lib.BOARDS_USE) if self.boards else self.st
         self.st_next = e.board_struct(_lib.BOARDS_USE) if self.boards else self.st
         self.fin = ops.finalize_struct(GROUP, "identity", self.norm, self.metrics)
 
@@ -138,7 +140,9 @@ class Rollout:
         for bit), the last with the rollout's finalize (metrics + scores + normalisation ==
         rmi_rollout_finalize, tested bit for bit)."""
         e = self.env
-        ops.sokoban_step_turn_first(self.st_first, e.ep, self.turns[0], e.init_state, e.init_player)
+        first = self.st_first_use if e.init_boards_valid else self.st_first
+        ops.sokoban_step_turn_first(first, e.ep, self.turns[0], e.init_state, e.init_player)
+        e.init_boards_valid = self.boards
         for t in range(1, T_TURNS - 1):
             ops.sokoban_step_turn(self.st_next, e.ep, self.turns[t])
         ops.sokoban_step_turn_finalize(self.st_next, e.ep, self.turns[-1], self.fin)

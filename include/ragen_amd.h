@@ -119,6 +119,12 @@ typedef struct {
    * non-NULL boards returns RMI_EUNSUP.                                                    */
   uint8_t* boards;            /* [B,16] or NULL                                            */
   int32_t boards_mode;        /* RMI_BOARDS_*                                              */
+  /* The reset state's entries (NULL: none), for rmi_sokoban_step_turn_first: under BUILD that
+   * launch decodes the reset rows and writes them here as well; under USE it reads them
+   * instead of decoding the reset rows again (the rows are still loaded: they are the reset's
+   * store).  Valid while init_state / init_player / room_fixed are unchanged since that BUILD
+   * launch (a reset or load_rooms changes them; a restore does not).                       */
+  uint8_t* init_boards;       /* [B,16] or NULL                                            */
 } rmi_sokoban_t;
 enum { RMI_BOARDS_NONE = 0, RMI_BOARDS_BUILD = 1, RMI_BOARDS_USE = 2 };
 

@@ -40,7 +40,7 @@ class Sokoban(ctypes.Structure):
     _fields_ = [("H", c_int32), ("W", c_int32), ("num_boxes", c_int32), ("max_steps", c_int32),
                 ("room_fixed", c_void_p), ("room_state", c_void_p), ("player", c_void_p),
                 ("num_env_steps", c_void_p), ("boxes_on_target", c_void_p),
-                ("boards", c_void_p), ("boards_mode", c_int32)]
+                ("boards", c_void_p), ("boards_mode", c_int32), ("init_boards", c_void_p)]
 
 
 class Finalize(ctypes.Structure):

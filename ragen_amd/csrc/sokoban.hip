@@ -670,8 +670,11 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   const int H = env.H, W = env.W;
   const uint32_t w_magic = (65536u + (uint32_t)W - 1u) / (uint32_t)W;  // off the critical path
   static_assert(!kBoards || (HW == 36 && LPE == 1 && !kLate && sizeof(M) == 4), "the board cache: 6x6, u32 window");
-  // the cache mode of this launch (wave-uniform): a fresh episode's first turn always builds
-  const int bmode = kBoards && env.boards ? (kFirst ? RMI_BOARDS_BUILD : env.boards_mode) : RMI_BOARDS_NONE;
+  // the cache mode of this launch (wave-uniform).  A fresh episode's first turn (kFirst) reads
+  // the RESET state: under USE from env.init_boards (the reset rows' entries, written by a
+  // first turn under BUILD), its rows still loaded -- they are the reset's store
+  const int bmode = kBoards && env.boards ? (kFirst && !env.init_boards ? RMI_BOARDS_BUILD : env.boards_mode)
+                                          : RMI_BOARDS_NONE;
   const bool use = bmode == RMI_BOARDS_USE;
   RMI_STAMP_DECL;
   RMI_STAMP(0);
@@ -684,17 +687,17 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
 #pragma unroll
   for (int i = 0; i < NWL; ++i) xs[i] = xf[i] = 0;
   Dw4 ent = {0u, 0u, 0u, 0u};  // the env's board-cache entry (USE)
-  if (use) {
-    ent = reinterpret_cast<const Dw4*>(env.boards)[bc];
-  } else if (!kLate) {
+  if (use) ent = reinterpret_cast<const Dw4*>(kFirst ? env.init_boards : env.boards)[bc];
+  if ((!use || kFirst) && !kLate) {
     load_row<NWL, LPE, HW != 0>((kFirst ? init_state : env.room_state) + bc * hw, xs, sub, row_words);
     load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
   }
   const int8_t* pl = kFirst ? init_player : env.player;
   int r = 0, c = 0;
-  if (!use) {  // (USE: the entry holds the player cell and the two counters)
-    r = pl[2 * bc];
-    c = pl[2 * bc + 1];
+  if (!use || kFirst) {  // (plain USE turns: the entry holds the player cell and the two counters)
+    const uint16_t rc = *reinterpret_cast<const uint16_t*>(pl + 2 * bc);  // (row, col): one load
+    r = (int)(int8_t)(rc & 0xFFu);
+    c = (int)(int8_t)(rc >> 8);
   }
   // branch-free: a conditional load here would make the compiler wait for the rows first
   const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
@@ -736,7 +739,8 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   const bool acts_ok = ((gt8_bytes(al) & vl) | (gt8_bytes(ah) & vh)) == 0;
   // USE: the entry stands in for the rows while it is tagged and the actions stay on the
   // regular path; else this wave loads its rows now and decodes them
-  bool from_cache = use && (ent.w >> 8 & 0xFFu) == 1u && acts_ok;
+  // (an env that does not act needs no actions check: a first turn writes its reset entry)
+  bool from_cache = use && (ent.w >> 8 & 0xFFu) == 1u && (acts_ok || !act);
   if (use) {
     // the tagged entry's player cell and counters (entry word 3: cell | tag << 8 | nes << 16 |
     // bot << 24); an untagged entry's are reloaded below with the rows
@@ -746,14 +750,20 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     nes = (int)(ent.w >> 16 & 0xFFu);
     bot = (int)(int8_t)(ent.w >> 24);
   }
-  if (use && !__all(from_cache || !act)) {
+  if (use && !__all(from_cache || !live || (!act && !kFirst))) {
     from_cache = false;
-    load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
-    load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
-    r = env.player[2 * bc];
-    c = env.player[2 * bc + 1];
-    nes = env.num_env_steps[bc];
-    bot = env.boxes_on_target[bc];
+    if (kFirst) {  // the reset rows and player are loaded already; the counters start at 0
+      r = pl[2 * bc];
+      c = pl[2 * bc + 1];
+      nes = bot = 0;
+    } else {
+      load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
+      load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+      r = env.player[2 * bc];
+      c = env.player[2 * bc + 1];
+      nes = env.num_env_steps[bc];
+      bot = env.boxes_on_target[bc];
+    }
   }
   bool regular = true, room_ok = false;
   M wall = 0, target = 0, box = 0;
@@ -763,12 +773,13 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     const int nv = __popc(vl) + __popc(vh);
     if (nv != n_act || nv == 0) penalty += in.format_penalty;  // :158-159
   }
-  if (from_cache && act) {  // the tagged entry: a regular room's window boards and player cell
+  if (from_cache && (act || kFirst)) {  // the tagged entry: a regular room's window boards and player cell
     wall = (M)ent.x;
     target = (M)ent.y;
     box = (M)ent.z;
     jp = (int)(ent.w & 0xFFu) - W;
-  } else if (act || (bmode == RMI_BOARDS_BUILD && live)) {  // BUILD: every live env's entry
+  } else if (act || ((bmode == RMI_BOARDS_BUILD || kFirst) && bmode != RMI_BOARDS_NONE && live)) {
+    // (BUILD, and a first turn that fell back: every live env's entry)
     const bool interior = r >= 1 && r <= H - 2 && c >= 1 && c <= W - 2;
     const int p = interior ? r * W + c : 0;
     uint64_t wall64, target64, box64;
@@ -782,6 +793,11 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     target = (M)(target64 >> W);
     box = (M)(box64 >> W);
     jp = p - W;
+    // a first turn under BUILD also keeps the reset state's entry for the next rollouts' first
+    // turns (USE reads it instead of decoding the reset rows again)
+    if (kFirst && bmode == RMI_BOARDS_BUILD && env.init_boards && live)
+      reinterpret_cast<Dw4*>(env.init_boards)[b] =
+          Dw4{(uint32_t)wall, (uint32_t)target, (uint32_t)box, ((uint32_t)p & 0xFFu) | (room_ok ? 1u : 0u) << 8};
   }
   RMI_STAMP(2);
 
@@ -971,7 +987,7 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     // decoded env under BUILD; an env of the exact path is untagged (its room may not be
     // regular any more); a USE env that did not act keeps its entry
     const bool stepped_fast = fast && act;
-    const bool write = bmode == RMI_BOARDS_BUILD || act;
+    const bool write = bmode == RMI_BOARDS_BUILD || act || kFirst;
     const uint32_t tag = (stepped_fast || !act) ? (from_cache || room_ok ? 1u : 0u) : 0u;
     if (write) {
       const uint32_t cell = (uint32_t)(jp + W) & 0xFFu;
@@ -1323,7 +1339,7 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
   // the board cache is kept only by the 6x6 one-lane-per-env launch (include/ragen_amd.h)
   if (env->boards && (hw != 36 || !w32 || spread || ep->B >= RMI_SOK_LATE_MIN ||
                       (env->boards_mode != RMI_BOARDS_BUILD && env->boards_mode != RMI_BOARDS_USE) ||
-                      (reinterpret_cast<uintptr_t>(env->boards) & 15u)))
+                      ((reinterpret_cast<uintptr_t>(env->boards) | reinterpret_cast<uintptr_t>(env->init_boards)) & 15u)))
     return RMI_EUNSUP;
 #define RMI_LAUNCH(HW_, M_)                                                                                   \
   do {                                                                                                        \

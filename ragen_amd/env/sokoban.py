@@ -31,7 +31,9 @@ class SokobanBatch(BatchEnv):
         self.init_player = torch.zeros(B, 2, dtype=torch.int8, device=d)
         # the turn kernel's optional board cache (enable_boards; include/ragen_amd.h)
         self.boards = None
+        self.init_boards = None  # the reset state's entries (rmi_sokoban_step_turn_first)
         self._boards_valid = False
+        self.init_boards_valid = False  # a first turn under BUILD wrote them since the last reset / load
 
     # 6x6 rooms at one lane per env (the plain turn launch's layout: 4097 <= B < 2^17)
     BOARDS_MIN_B, BOARDS_MAX_B = 4097, 1 << 17
@@ -47,12 +49,15 @@ class SokobanBatch(BatchEnv):
             return False
         if self.boards is None:
             self.boards = torch.zeros(self.B, 16, dtype=torch.uint8, device=self.device)
+            self.init_boards = torch.zeros(self.B, 16, dtype=torch.uint8, device=self.device)
         self._boards_valid = False
+        self.init_boards_valid = False
         return True
 
     def invalidate_boards(self):
-        """The state was written outside the cached turn launches: the next turn rebuilds."""
-        self._boards_valid = False
+        """The state was written outside the cached turn launches: the next turn rebuilds (and,
+        for a write to the reset rows or room_fixed, the next first turn)."""
+        self._boards_valid = self.init_boards_valid = False
 
     def board_struct(self, mode: int) -> _lib.Sokoban:
         """struct() carrying the board cache in `mode` (_lib.BOARDS_BUILD / BOARDS_USE), for
@@ -61,7 +66,7 @@ class SokobanBatch(BatchEnv):
         if self.boards is None:
             raise RuntimeError("enable_boards() first")
         st = self.struct()
-        st.boards, st.boards_mode = self.boards.data_ptr(), int(mode)
+        st.boards, st.boards_mode, st.init_boards = self.boards.data_ptr(), int(mode), self.init_boards.data_ptr()
         return st
 
     def _turn_struct(self):
@@ -171,7 +176,7 @@ class SokobanBatch(BatchEnv):
             ops.h2d(inv.astype(np.int32), self.device)
         ops.sokoban_load_rooms(self.struct(), self.ep, ops.h2d(rows, self.device), room_of, self.init_state,
                                self.init_player)
-        self._boards_valid = False
+        self._boards_valid = self.init_boards_valid = False
         self._invalidate()
 
     def load_state(self, fixed, state, player):
@@ -185,6 +190,7 @@ class SokobanBatch(BatchEnv):
     def _load_rows(self, d):
         """d u8[B, 2HW+2] on the device: [fixed | state | player] per env."""
         HW = self.H * self.W
+        self.init_boards_valid = False
         self.room_fixed.copy_(d[:, :HW])
         self.init_state.copy_(d[:, HW:2 * HW])
         self.init_player.copy_(d[:, 2 * HW:].view(torch.int8))

@@ -186,3 +186,57 @@ def test_boards_invalidate_after_direct_write(device):
         oracle.sokoban_turn(6, 6, 1, 100, fixed, state, player, nes, bot, oep, t, ids[t], n[t], None, 10, -0.1)
         torch.cuda.synchronize()
         _match(env, oep, fixed, state, player, nes, bot)
+
+
+@pytest.mark.parametrize("frac_irregular", [0.0, 0.02])
+def test_boards_first_turn_reads_reset_entries_vs_oracle(device, frac_irregular):
+    """The fused first turn (rmi_sokoban_step_turn_first): the first rollout's under BUILD writes
+    the reset state's entries (init_boards), the later rollouts' under USE read them instead of
+    decoding the reset rows -- with envs left out of turn 0 (their entries are the reset's),
+    irregular reset rooms (untagged: their waves decode) and off-path action ids -- == the oracle
+    every turn of 3 rollouts."""
+    rng = np.random.default_rng(int(frac_irregular * 100) + 3)
+    B, T, K, H, W = 8192, 3, 5, 6, 6
+    env = SokobanBatch(SokobanEnvConfig(dim_x=H, dim_y=W, num_boxes=1, max_steps=100), B, T, K, device)
+    assert env.enable_boards()
+    env.reset(synthetic.env_seeds(B))
+    fixed0 = env.room_fixed.cpu().numpy().copy()
+    state0 = env.room_state.cpu().numpy().copy()
+    player0 = env.player.cpu().numpy().copy()
+    idx = np.nonzero(rng.random(B) < frac_irregular)[0]
+    if len(idx):
+        f2, s2, p2 = fixed0[idx].copy(), state0[idx].copy(), player0[idx].copy()
+        _irregular_rooms(rng, len(idx), H, W, f2, s2, p2)
+        fixed0[idx], state0[idx], player0[idx] = f2, s2, p2
+        env.load_state(fixed0, state0, player0)
+    assert not env.init_boards_valid
+    for rollout in range(3):
+        fixed, state, player = fixed0.copy(), state0.copy(), player0.copy()
+        nes, bot = np.zeros(B, np.int32), np.zeros(B, np.int32)
+        oep = oracle.Episode(B, T)
+        bad = np.zeros(B, bool)
+        for t in range(T):
+            ids = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9], size=(B, K),
+                             p=[0.05] + [0.115] * 8 + [0.03]).astype(np.int8)
+            if frac_irregular == 0.0:
+                ids = np.clip(ids, 1, 4).astype(np.int8)
+            n = rng.integers(0, K + 1, size=B).astype(np.uint8)
+            h_in = (rng.random(B) < 0.7).astype(np.uint8) if t == 0 else None
+            err = torch.zeros(B, dtype=torch.uint8, device=device)
+            if t == 0:
+                mode = _lib.BOARDS_USE if env.init_boards_valid else _lib.BOARDS_BUILD
+                keep = (_t(ids, device), _t(n, device), _t(h_in, device))  # alive through the launch
+                turn = ops.turn_struct(0, *keep, 10, -0.1)
+                ops.sokoban_step_turn_first(env.board_struct(mode), env.ep, turn, env.init_state, env.init_player, err)
+                env.init_boards_valid = True
+                env._boards_valid = True  # the first turn wrote every live env's entry
+            else:
+                env.step_turn(t, _t(ids, device), _t(n, device), None, 10, -0.1, err)
+            oerr = oracle.sokoban_turn(H, W, 1, 100, fixed, state, player, nes, bot, oep, t, ids, n, h_in, 10, -0.1)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(err.cpu().numpy() != 0, oerr != 0)
+            bad |= oerr != 0
+            _match(env, oep, fixed, state, player, nes, bot, ~bad)
+        if rollout == 0:
+            ent = env.init_boards.cpu().numpy()
+            assert (ent[:, 13] == 1).sum() >= B - len(idx)  # every regular reset room tagged
