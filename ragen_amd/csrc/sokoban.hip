@@ -16,6 +16,7 @@
 //   4. any irregular room sends its whole wave to the exact path (env-private LDS rows,
 //      numpy's negative-index wrap, gym_sokoban's IndexError points).
 #include "common.hpp"
+#include "board_step.hpp"
 #include "parse_core.hpp"
 
 #include <type_traits>
@@ -267,62 +268,10 @@ struct WordBits<uint64_t> {
   __device__ __forceinline__ static int ctz(uint64_t x) { return __builtin_ctzll(x); }
 };
 
-// One EnvStateManager turn (es_manager.py:149-169) of one regular room on window bitboards,
-// straight-line and predicated: action slot k runs iff it is a known name (id != 0), the
-// turn has not hit done and fewer than `left` actions ran (valid[:left]).  K (slots per
-// turn) is a template parameter so the K steps unroll into one branch-free block the
-// compiler can interleave (a lone wave is latency-bound: ILP is what shortens it).
-// Bit-identical to the LDS path.
-struct BoardTurn {
-  double acc;
-  uint32_t info, taken, stop, succ, moved;
-  int nes, bot;
-};
-template <class M, int K>
-__device__ __forceinline__ BoardTurn board_turn_k(M wall, M target, M& box, int& jp, int W, uint64_t acts, int n_act,
-                                                  int left, int nes, int bot, int num_boxes, int max_steps) {
-  constexpr int kMask = WordBits<M>::kBits - 1;
-  BoardTurn t;
-  t.acc = 0.0;
-  t.info = t.taken = t.stop = t.succ = t.moved = 0;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int a = (int)(acts >> (8 * k)) & 0xFF;  // 1..8 when valid (checked by the caller)
-    const uint32_t go = (t.stop == 0) & (k < n_act) & ((int)t.taken < left) & (a != 0);
-    const int dir = (a - 1) & 3;  // CHANGE_COORDINATES[(a-1) % 4]: up down left right
-    const int mag = (dir & 2) ? 1 : W;
-    const int s = (dir & 1) ? mag : -mag;
-    const int jn = jp + s, jb = jn + s;
-    const M nb = (M)1 << (jn & kMask), bb = (M)1 << (jb & kMask);
-    const M occ = wall | box;
-    const uint32_t n_box = (box & nb) != 0;
-    const uint32_t n_free = (occ & nb) == 0;                             // state[new] in {1, 2}
-    const uint32_t is_push = go & (a <= 4) & n_box & ((occ & bb) == 0);  // _push; state[new_box] in {1, 2}
-    const uint32_t moved = go & (is_push | n_free);                      // _push falls back to _move
-    box ^= is_push ? (nb | bb) : (M)0;
-    jp = moved ? jn : jp;
-    // _calc_reward: open targets = (state == 2) | ((fixed == 2) & (state == 5)) = targets without a box
-    const int n_open = WordBits<M>::popc(target & ~box);
-    const int cur = num_boxes - n_open;
-    const double d_box = cur > bot ? 1.0 : (cur < bot ? -1.0 : 0.0);
-    const uint32_t all_on = n_open == 0;
-    const double rw = (-0.1 + d_box) + (all_on ? 10.0 : 0.0);  // penalty_for_step, box on/off, finished
-    const int nes1 = nes + 1;
-    const uint32_t done = all_on | (max_steps == nes1);
-    const uint32_t succ = cur == num_boxes;  // sokoban/env.py:49
-    nes = go ? nes1 : nes;
-    bot = go ? cur : bot;
-    t.acc += go ? rw : 0.0;  // acc is never -0.0, so + 0.0 is an exact identity
-    t.info = go ? (RMI_INFO_PRESENT | RMI_INFO_VALID | (moved << 1) | (succ << 3)) : t.info;
-    t.succ = go ? succ : t.succ;
-    t.moved |= moved;
-    t.taken += go;
-    t.stop |= go & done;
-  }
-  t.nes = nes;
-  t.bot = bot;
-  return t;
-}
+// One EnvStateManager turn (es_manager.py:149-169) of one regular room on window bitboards:
+// board_step.hpp (the K slots as one unrolled, branch-free block; K is a template parameter).
+using bs::board_turn_k;
+using bs::BoardTurn;
 
 template <class M>
 __device__ __forceinline__ TurnOut board_turn(M wall, M target, M& box, int& jp, int W, uint64_t acts, int K, int n_act,
