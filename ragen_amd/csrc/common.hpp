@@ -133,6 +133,28 @@ struct TurnOut {
   bool stepped_any_state;  // the env's state may have changed
 };
 
+// Per-env element addressing: a wave-uniform base pointer plus this env's element index.  With
+// Ix = uint32_t the byte offset is formed in 32 bits, so the access compiles to
+// global_load/store v_offset, s[base] (no 64-bit address arithmetic per access, which on a
+// latency-bound wave sits ahead of its loads); the caller guarantees the offset fits
+// (kOff32MaxB envs of at most kOff32MaxRow bytes each).  Ix = int64_t is plain pointer
+// arithmetic.
+#ifndef RMI_OFF32_MAX_B  // (a diagnostic variant sets 0: every launch takes the 64-bit form)
+#define RMI_OFF32_MAX_B ((int64_t)1 << 26)
+#endif
+constexpr int64_t kOff32MaxB = RMI_OFF32_MAX_B;
+constexpr int kOff32MaxRow = 64;
+template <class Ix, class T>
+__device__ __forceinline__ T* elem(T* base, int64_t i) {
+  if constexpr (sizeof(Ix) == 4) {
+    uint32_t off = (uint32_t)i * (uint32_t)sizeof(T);
+    // (a byte array's offset would otherwise fold back into 64-bit "i & 0xffffffff")
+    if constexpr (sizeof(T) == 1) asm("" : "+v"(off));
+    return (T*)((const char*)base + off);
+  } else
+    return base + i;
+}
+
 // Actions of one env packed into a u64 (K <= 8 bytes), loaded once per turn: the at most three
 // aligned dwords that hold the row's K bytes, issued back to back with clamped addresses (never
 // a dword past the one holding the row's last byte, so never outside the row's page) and
@@ -154,6 +176,29 @@ __device__ __forceinline__ uint64_t load_actions(const int8_t* acts, int K, cons
   // bytes sh .. sh + 7 of d0 | d1 | d2
   const uint64_t v = sh ? (lo >> (8 * sh)) | ((uint64_t)d2 << (64 - 8 * sh)) : lo;
   return K >= 8 ? v : (K <= 0 ? 0ull : v & ((1ull << (8 * K)) - 1ull));
+}
+
+// The same for env b of a [B, K] action array at `acts` (K > 0) or, with K == 0, the byte `alt`
+// [b]: the clamped dword loads address base + 32-bit offsets under Ix = uint32_t.
+template <class Ix>
+__device__ __forceinline__ uint64_t load_actions_at(const int8_t* acts, int64_t b, int K, const uint8_t* alt) {
+  if constexpr (sizeof(Ix) != 4) {
+    return load_actions(acts + b * (int64_t)K, K, alt + b);
+  } else {
+    const char* base = K > 0 ? (const char*)acts : (const char*)alt;  // uniform
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(base) & 3u);
+    const char* abase = base - mis;                                   // 4-aligned, uniform
+    const int Kc = K > 0 ? K : 1;
+    const uint32_t o = (uint32_t)b * (uint32_t)(K > 0 ? K : 1) + mis;  // the row's first byte from abase
+    const uint32_t o4 = o & ~3u;
+    const int sh = (int)(o & 3u);
+    const int last = (sh + Kc - 1) >> 2;
+    const uint32_t d0 = *(const uint32_t*)(abase + o4), d1 = *(const uint32_t*)(abase + (o4 + (last >= 1 ? 4u : 0u)));
+    const uint32_t d2 = *(const uint32_t*)(abase + (o4 + 4u * (uint32_t)(last >= 2 ? 2 : last)));
+    const uint64_t lo = ((uint64_t)d1 << 32) | d0;
+    const uint64_t v = sh ? (lo >> (8 * sh)) | ((uint64_t)d2 << (64 - 8 * sh)) : lo;
+    return K >= 8 ? v : (K <= 0 ? 0ull : v & ((1ull << (8 * K)) - 1ull));
+  }
 }
 
 template <class Env>
@@ -221,13 +266,14 @@ constexpr int kFinT = 8;  // turns of the record loaded up front
 struct FinRecord {
   double r[kFinT];
   uint8_t info[kFinT];
+  template <class Ix = int64_t>
   __device__ __forceinline__ void load(const rmi_episode_t& ep, int64_t bc) {
     const int64_t B = ep.B;
 #pragma unroll
     for (int k = 0; k < kFinT; ++k) {
       const int64_t t = k < ep.T ? k : ep.T - 1;  // clamped, always valid
-      r[k] = ep.turn_reward[t * B + bc];
-      info[k] = ep.turn_info[t * B + bc];
+      r[k] = *elem<Ix>(ep.turn_reward + t * B, bc);
+      info[k] = *elem<Ix>(ep.turn_info + t * B, bc);
     }
   }
   __device__ __forceinline__ void set(int turn, double acc, uint8_t inf) {
@@ -246,7 +292,7 @@ __device__ __forceinline__ double group_sum(double x, int gs) {  // xor butterfl
   return x;
 }
 
-template <int LPE>
+template <int LPE, class Ix = int64_t>
 __device__ __forceinline__ void finalize_envs(const rmi_episode_t& ep, const rmi_finalize_t& fin, const FinRecord& rec,
                                               int64_t b, bool writer, uint8_t flags, int32_t n_turns,
                                               int32_t num_actions, double penalty, int acted_turn, double acc,
@@ -265,19 +311,19 @@ __device__ __forceinline__ void finalize_envs(const rmi_episode_t& ep, const rmi
   for (int t = kFinT; t < ep.T; ++t) {  // long episodes only
     const int64_t bc = b < B ? b : B - 1;
     const bool mine = t == acted_turn;  // written by this launch: use the registers
-    const uint8_t inf = mine ? acc_info : ep.turn_info[t * B + bc];
-    score += mine ? acc : ep.turn_reward[t * B + bc];
+    const uint8_t inf = mine ? acc_info : *elem<Ix>(ep.turn_info + (int64_t)t * B, bc);
+    score += mine ? acc : *elem<Ix>(ep.turn_reward + (int64_t)t * B, bc);
     present |= inf & RMI_INFO_PRESENT;
     eff += (inf >> 1) & 1;
     val += (inf >> 2) & 1;
   }
   const float scf = (float)score, pf = (float)penalty, x = scf + pf;
   if (writer) {
-    if (fin.score) fin.score[b] = scf;
-    if (fin.pen) fin.pen[b] = pf;
+    if (fin.score) *elem<Ix>(fin.score, b) = scf;
+    if (fin.pen) *elem<Ix>(fin.pen, b) = pf;
     if (fin.metrics) {
       const double nt = (double)n_turns;
-      double* m = fin.metrics + 4 * b;
+      double* m = elem<Ix>(fin.metrics, 4 * b);
       m[0] = ((flags & RMI_FLAG_TERMINATED) && !(flags & RMI_FLAG_TRUNCATED)) ? 1.0 : 0.0;
       m[1] = (double)num_actions;
       m[2] = present ? (double)eff / nt : __builtin_nan("");
@@ -302,7 +348,7 @@ __device__ __forceinline__ void finalize_envs(const rmi_episode_t& ep, const rmi
     y = use ? (x - mean) / (sd + 1e-6f) : 0.0f;
     if (method == RMI_NORM_ASYM_CLIP) y = fminf(fmaxf(y, -1.0f), 3.0f);
   }
-  if (writer) fin.norm[b] = y;
+  if (writer) *elem<Ix>(fin.norm, b) = y;
 }
 
 inline int check_turn_args(const rmi_episode_t* ep, const rmi_turn_t* in) {

@@ -604,7 +604,7 @@ __device__ __forceinline__ void render_group(const ObsOut& o, ObsLds<HW, M>& L, 
 // and stores its entry; USE loads the 16-B entry instead of the two rows and skips the decode,
 // unless some acting env of the wave has an untagged entry or actions off the regular path:
 // that wave then loads its rows (a second round trip) and decodes them as without a cache.
-template <int HW, class M, int LPE, bool kFin, bool kFirst, bool kLate, bool kBoards, class AtEnd>
+template <int HW, class M, int LPE, bool kFin, bool kFirst, bool kLate, bool kBoards, class Ix, class AtEnd>
 __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_episode_t& ep, const rmi_turn_t& in,
                                          int hw_rt, uint64_t border, uint8_t* __restrict__ err_out,
                                          const rmi_finalize_t& fin, const uint8_t* __restrict__ init_state,
@@ -636,46 +636,46 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
 #pragma unroll
   for (int i = 0; i < NWL; ++i) xs[i] = xf[i] = 0;
   Dw4 ent = {0u, 0u, 0u, 0u};  // the env's board-cache entry (USE)
-  if (use) ent = reinterpret_cast<const Dw4*>(kFirst ? env.init_boards : env.boards)[bc];
+  if (use) ent = *elem<Ix>(reinterpret_cast<const Dw4*>(kFirst ? env.init_boards : env.boards), bc);
   if ((!use || kFirst) && !kLate) {
-    load_row<NWL, LPE, HW != 0>((kFirst ? init_state : env.room_state) + bc * hw, xs, sub, row_words);
-    load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(elem<Ix>(kFirst ? init_state : env.room_state, bc * hw), xs, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(elem<Ix>(env.room_fixed, bc * hw), xf, sub, row_words);
   }
   const int8_t* pl = kFirst ? init_player : env.player;
   int r = 0, c = 0;
   if (!use || kFirst) {  // (plain USE turns: the entry holds the player cell and the two counters)
-    const uint16_t rc = *reinterpret_cast<const uint16_t*>(pl + 2 * bc);  // (row, col): one load
+    const uint16_t rc = *elem<Ix>(reinterpret_cast<const uint16_t*>(pl), bc);  // (row, col): one load
     r = (int)(int8_t)(rc & 0xFFu);
     c = (int)(int8_t)(rc >> 8);
   }
   // branch-free: a conditional load here would make the compiler wait for the rows first
-  const uint8_t has_in = *(in.has_input ? in.has_input + bc : ep.flags + bc);
+  const uint8_t has_in = *elem<Ix>(in.has_input ? in.has_input : ep.flags, bc);
   uint8_t flags = 0;
   int nes = 0, bot = 0;
   int32_t num_actions = 0, n_turns = 0;
   double penalty = 0.0;
   if (!kFirst) {  // a fresh episode's record is all zero (EnvStatus(), es_manager.py:95)
-    flags = ep.flags[bc];
+    flags = *elem<Ix>(ep.flags, bc);
     if (!use) {
-      nes = env.num_env_steps[bc];
-      bot = env.boxes_on_target[bc];
+      nes = *elem<Ix>(env.num_env_steps, bc);
+      bot = *elem<Ix>(env.boxes_on_target, bc);
     }
-    num_actions = ep.num_actions[bc];
-    n_turns = ep.n_turns[bc];
-    penalty = ep.penalty[bc];
+    num_actions = *elem<Ix>(ep.num_actions, bc);
+    n_turns = *elem<Ix>(ep.n_turns, bc);
+    penalty = *elem<Ix>(ep.penalty, bc);
   }
-  int n_act = in.n_actions[bc];
-  const uint64_t acts = load_actions(in.actions + bc * (int64_t)in.K, in.K, ep.flags + bc);
+  int n_act = *elem<Ix>(in.n_actions, bc);
+  const uint64_t acts = load_actions_at<Ix>(in.actions, bc, in.K, ep.flags);
   FinRecord rec;
-  if (kFin) rec.load(ep, bc);
+  if (kFin) rec.load<Ix>(ep, bc);
   if (!live) flags = RMI_FLAG_DONE;
   const bool act = live && (in.has_input ? has_in != 0 : !(flags & RMI_FLAG_DONE));
   if (kLate && act) {
-    load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
-    load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(elem<Ix>(env.room_state, bc * hw), xs, sub, row_words);
+    load_row<NWL, LPE, HW != 0>(elem<Ix>(env.room_fixed, bc * hw), xf, sub, row_words);
   }
   RMI_STAMP_WAIT(1);
-  if (kFirst && live) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);  // the reset
+  if (kFirst && live) store_row<NWL, LPE, HW != 0>(elem<Ix>(env.room_state, b * hw), xs, sub, row_words);  // the reset
 
   // ---- 2. format penalty and the regular-room test
   if (n_act > in.K) n_act = in.K;
@@ -702,16 +702,16 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   if (use && !__all(from_cache || !live || (!act && !kFirst))) {
     from_cache = false;
     if (kFirst) {  // the reset rows and player are loaded already; the counters start at 0
-      r = pl[2 * bc];
-      c = pl[2 * bc + 1];
+      r = elem<Ix>(pl, 2 * bc)[0];
+      c = elem<Ix>(pl, 2 * bc)[1];
       nes = bot = 0;
     } else {
-      load_row<NWL, LPE, HW != 0>(env.room_state + bc * hw, xs, sub, row_words);
-      load_row<NWL, LPE, HW != 0>(env.room_fixed + bc * hw, xf, sub, row_words);
-      r = env.player[2 * bc];
-      c = env.player[2 * bc + 1];
-      nes = env.num_env_steps[bc];
-      bot = env.boxes_on_target[bc];
+      load_row<NWL, LPE, HW != 0>(elem<Ix>(env.room_state, bc * hw), xs, sub, row_words);
+      load_row<NWL, LPE, HW != 0>(elem<Ix>(env.room_fixed, bc * hw), xf, sub, row_words);
+      r = elem<Ix>(env.player, 2 * bc)[0];
+      c = elem<Ix>(env.player, 2 * bc)[1];
+      nes = *elem<Ix>(env.num_env_steps, bc);
+      bot = *elem<Ix>(env.boxes_on_target, bc);
     }
   }
   bool regular = true, room_ok = false;
@@ -745,7 +745,7 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     // a first turn under BUILD also keeps the reset state's entry for the next rollouts' first
     // turns (USE reads it instead of decoding the reset rows again)
     if (kFirst && bmode == RMI_BOARDS_BUILD && env.init_boards && live)
-      reinterpret_cast<Dw4*>(env.init_boards)[b] =
+      *elem<Ix>(reinterpret_cast<Dw4*>(env.init_boards), b) =
           Dw4{(uint32_t)wall, (uint32_t)target, (uint32_t)box, ((uint32_t)p & 0xFFu) | (room_ok ? 1u : 0u) << 8};
   }
   RMI_STAMP(2);
@@ -790,7 +790,7 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
             m &= m - 1;
             dirty |= 1u << ((j + W) >> 2);
           }
-          uint32_t* r1 = reinterpret_cast<uint32_t*>(env.room_state + b * hw);
+          uint32_t* r1 = reinterpret_cast<uint32_t*>(elem<Ix>(env.room_state, b * hw));
           while (dirty) {
             const int dw = __builtin_ctz(dirty);
             dirty &= dirty - 1;
@@ -815,7 +815,7 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
           // flipped — 2 to 4 for one box pushed any number of times.  The first 4 are stored
           // straight-line (a missing one repeats the first: the same byte, the same value); only
           // a turn that moved several boxes loops over the rest.
-          uint8_t* win = env.room_state + b * hw + W;  // window bit j = cell W + j
+          const int64_t win = b * hw + W;  // window bit j = cell W + j
           int jj[4];
           jj[0] = WordBits<M>::ctz(m);
           m &= m - 1;
@@ -828,13 +828,13 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
           for (int k = 0; k < 4; ++k) {
             const int j = jj[k];
             const uint32_t t = (uint32_t)(target >> j) & 1u, bx = (uint32_t)(box >> j) & 1u;
-            win[j] = (uint8_t)(j == jp ? 5u : (bx ? 4u - t : 1u + t));
+            *elem<Ix>(env.room_state, win + j) = (uint8_t)(j == jp ? 5u : (bx ? 4u - t : 1u + t));
           }
           while (m) {
             const int j = WordBits<M>::ctz(m);
             m &= m - 1;
             const uint32_t t = (uint32_t)(target >> j) & 1u, bx = (uint32_t)(box >> j) & 1u;
-            win[j] = (uint8_t)(j == jp ? 5u : (bx ? 4u - t : 1u + t));
+            *elem<Ix>(env.room_state, win + j) = (uint8_t)(j == jp ? 5u : (bx ? 4u - t : 1u + t));
           }
         }
         row_changed = false;  // stored
@@ -894,42 +894,42 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
 
   // ---- 4. outputs: scalars from the env's first lane, row dwords from every lane
   if (kFirst && live && !act && sub == 0) {  // no input this turn: the env keeps its reset state
-    env.player[2 * b] = (int8_t)r;
-    env.player[2 * b + 1] = (int8_t)c;
-    env.num_env_steps[b] = 0;
-    env.boxes_on_target[b] = 0;
-    ep.num_actions[b] = 0;
-    ep.flags[b] = 0;
-    ep.n_turns[b] = 0;
-    ep.penalty[b] = 0.0;
+    elem<Ix>(env.player, 2 * b)[0] = (int8_t)r;
+    elem<Ix>(env.player, 2 * b)[1] = (int8_t)c;
+    *elem<Ix>(env.num_env_steps, b) = 0;
+    *elem<Ix>(env.boxes_on_target, b) = 0;
+    *elem<Ix>(ep.num_actions, b) = 0;
+    *elem<Ix>(ep.flags, b) = 0;
+    *elem<Ix>(ep.n_turns, b) = 0;
+    *elem<Ix>(ep.penalty, b) = 0.0;
   }
   if (kFirst && live && sub == 0)
     for (int t = 0; t < ep.T; ++t)
       if (t != in.turn || !act) {
-        ep.turn_reward[(int64_t)t * B + b] = 0.0;
-        ep.turn_info[(int64_t)t * B + b] = 0;
-        ep.turn_exec[(int64_t)t * B + b] = 0;
+        *elem<Ix>(ep.turn_reward + (int64_t)t * B, b) = 0.0;
+        *elem<Ix>(ep.turn_info + (int64_t)t * B, b) = 0;
+        *elem<Ix>(ep.turn_exec + (int64_t)t * B, b) = 0;
       }
   if (act) {
     if (sub == 0) {
       finish_turn(o, turn_done, succ_last, num_actions, flags, n_turns, in.max_actions_per_traj);
-      ep.num_actions[b] = num_actions;
-      ep.flags[b] = flags;
-      ep.n_turns[b] = n_turns;
-      ep.penalty[b] = penalty;
-      const int64_t tb = (int64_t)in.turn * B + b;
-      ep.turn_reward[tb] = o.acc;
-      ep.turn_info[tb] = o.info;
-      ep.turn_exec[tb] = o.exec;
+      *elem<Ix>(ep.num_actions, b) = num_actions;
+      *elem<Ix>(ep.flags, b) = flags;
+      *elem<Ix>(ep.n_turns, b) = n_turns;
+      *elem<Ix>(ep.penalty, b) = penalty;
+      const int64_t tb = (int64_t)in.turn * B;  // this turn's row of the record
+      *elem<Ix>(ep.turn_reward + tb, b) = o.acc;
+      *elem<Ix>(ep.turn_info + tb, b) = o.info;
+      *elem<Ix>(ep.turn_exec + tb, b) = o.exec;
       if (kFirst || o.stepped_any_state) {
-        env.player[2 * b] = (int8_t)r;
-        env.player[2 * b + 1] = (int8_t)c;
-        env.num_env_steps[b] = nes;
-        env.boxes_on_target[b] = bot;
+        elem<Ix>(env.player, 2 * b)[0] = (int8_t)r;
+        elem<Ix>(env.player, 2 * b)[1] = (int8_t)c;
+        *elem<Ix>(env.num_env_steps, b) = nes;
+        *elem<Ix>(env.boxes_on_target, b) = bot;
       }
-      if (err_out && err) err_out[b] |= err;
+      if (err_out && err) *elem<Ix>(err_out, b) |= err;
     }
-    if (row_changed) store_row<NWL, LPE, HW != 0>(env.room_state + b * hw, xs, sub, row_words);
+    if (row_changed) store_row<NWL, LPE, HW != 0>(elem<Ix>(env.room_state, b * hw), xs, sub, row_words);
   }
   if (bmode != RMI_BOARDS_NONE && live) {
     // the entry after the turn: an acting env of a fast wave (its boards were stepped), every
@@ -940,7 +940,7 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
     const uint32_t tag = (stepped_fast || !act) ? (from_cache || room_ok ? 1u : 0u) : 0u;
     if (write) {
       const uint32_t cell = (uint32_t)(jp + W) & 0xFFu;
-      reinterpret_cast<Dw4*>(env.boards)[b] = Dw4{(uint32_t)wall, (uint32_t)target, (uint32_t)box,
+      *elem<Ix>(reinterpret_cast<Dw4*>(env.boards), b) = Dw4{(uint32_t)wall, (uint32_t)target, (uint32_t)box,
                                                    cell | (tag << 8) | ((uint32_t)nes & 0xFFu) << 16 |
                                                        ((uint32_t)bot & 0xFFu) << 24};
     }
@@ -949,12 +949,13 @@ __device__ __forceinline__ void turn_env(const rmi_sokoban_t& env, const rmi_epi
   at_end(xs, xf, wall, target, box, (fast && act) ? jp : INT32_MIN);
   if (kFin) {
     if (act) rec.set(in.turn, o.acc, o.info);  // this turn's record is still in registers
-    finalize_envs<LPE>(ep, fin, rec, b, live && sub == 0, flags, n_turns, num_actions, penalty, act ? in.turn : -1,
+    finalize_envs<LPE, Ix>(ep, fin, rec, b, live && sub == 0, flags, n_turns, num_actions, penalty, act ? in.turn : -1,
                        o.acc, o.info);
   }
 }
 
-template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false, bool kObs = false>  // HW = H*W (0 = runtime); H*W % 4 == 0
+template <int HW, class M, int LPE, bool kFin, bool kFirst = false, bool kLate = false, bool kObs = false,
+          class Ix = int64_t>  // HW = H*W (0 = runtime); H*W % 4 == 0
 __global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoban_step_turn_kernel(rmi_sokoban_t env, rmi_episode_t ep, rmi_turn_t in,
                                                                   int hw_rt, uint64_t border,
                                                                   uint8_t* __restrict__ err_out, rmi_finalize_t fin,
@@ -974,10 +975,7 @@ __global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoba
   const bool turn_wave = !kObs || wave < kSokWpb;  // kObs helper waves only render
   const int64_t b = turn_wave ? ((int64_t)blockIdx.x * kSokWpb + wave) * kEnvs + slot : (int64_t)B;
   const int row_words = (HW ? HW : hw_rt) >> 2;
-  turn_env<HW, M, LPE, kFin, kFirst, kLate, (HW == 36 && LPE == 1 && !kLate && !kObs && sizeof(M) == 4)>(
-      env, ep, in, hw_rt, border, err_out, fin, init_state, init_player, b, sub,
-      lds_state + (wave * kEnvs + slot) * row_words, lds_fixed + (wave * kEnvs + slot) * row_words,
-      [&](const auto& xs, const auto& xf, M wall, M target, M box, int jp) {
+  auto at_end = [&](const auto& xs, const auto& xf, M wall, M target, M box, int jp) {
         if constexpr (kObs) {
           const int H = env.H, W = env.W;
           if (turn_wave) {  // this env's state after the turn, for the group's render
@@ -998,7 +996,12 @@ __global__ __launch_bounds__(kWave * kSokWpb * (kObs ? kObsFan : 1)) void sokoba
           render_group<HW, M>(obs, lds_obs, B, H, W);
 #endif
         }
-      });
+      };
+  constexpr bool kBoards = HW == 36 && LPE == 1 && !kLate && !kObs && sizeof(M) == 4;
+  static_assert(sizeof(Ix) == 8 || kBoards, "32-bit env offsets: the SK layout only (launched below kOff32MaxB envs)");
+  turn_env<HW, M, LPE, kFin, kFirst, kLate, kBoards, Ix>(env, ep, in, hw_rt, border, err_out, fin, init_state,
+                                                         init_player, b, sub, lds_state + (wave * kEnvs + slot) * row_words,
+                                                         lds_fixed + (wave * kEnvs + slot) * row_words, at_end);
 }
 
 // Fused reset: room_state/player from the generated rooms, counters and the whole episode
@@ -1180,7 +1183,7 @@ __global__ __launch_bounds__(kWave* kTokEnvs) __attribute__((amdgpu_waves_per_eu
   if (wv < kTurnWaves) {
     const int t = wv * kWave + lane, e = t / kLpeT, sub = t % kLpeT;
     const int64_t be = b0 + e;
-    turn_env<36, uint32_t, kLpeT, false, kFirst, false, false>(
+    turn_env<36, uint32_t, kLpeT, false, kFirst, false, false, int64_t>(
         env, ep, in, 36, border, err_out, fin, init_state, init_player, be, sub, lds_state + e * 9, lds_fixed + e * 9,
         [&](const auto& xs, const auto& xf, uint32_t wall, uint32_t target, uint32_t box, int jp) {
 #pragma unroll
@@ -1303,11 +1306,22 @@ int sokoban_step_turn_launch(const rmi_sokoban_t* env, const rmi_episode_t* ep, 
         hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, false, true>), dim3(grid),            \
                            dim3(kWave * kSokWpb), 0, s, *env, *ep, *in, hw, border, err, fin, init_state,    \
                            init_player);                                                                      \
-    } else                                                                                                    \
+    } else {                                                                                                  \
+      if constexpr (HW_ == 36 && sizeof(M_) == 4) {                                                           \
+        if (ep->B < kOff32MaxB) {                                                                             \
+          hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, kFirst, false, false, uint32_t>),    \
+                             dim3(grid), dim3(kWave * kSokWpb), 0, s, *env, *ep, *in, hw, border, err, fin,   \
+                             init_state, init_player);                                                        \
+          break;                                                                                              \
+        }                                                                                                     \
+      }                                                                                                       \
       hipLaunchKernelGGL((sokoban_step_turn_kernel<HW_, M_, 1, kFin, kFirst>), dim3(grid), dim3(kWave * kSokWpb), \
-                         0, s,                                                                                \
-                         *env, *ep, *in, hw, border, err, fin, init_state, init_player);                      \
+                         0, s, *env, *ep, *in, hw, border, err, fin, init_state, init_player);                \
+    }                                                                                                         \
   } while (0)
+  // (the SK layout -- 6x6 u32 window, one lane per env, early row loads -- addresses the env
+  // arrays with 32-bit offsets below kOff32MaxB envs, elem<uint32_t>; every other form with
+  // 64-bit ones)
   if (hw == 36 && w32)
     RMI_LAUNCH(36, uint32_t);
   else if (hw == 36)
