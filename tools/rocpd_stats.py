@@ -1,8 +1,9 @@
-"""Turn a rocprofv3 rocpd database (`--kernel-trace` without `--output-format csv`) into the same
-kernel_stats.csv layout `--stats` writes: Name, Calls, TotalDurationNs, AverageNs, Percentage,
-MinNs, MaxNs, StdDev, one row per kernel name, ordered by total time.
+"""Turn a rocprofv3 rocpd database (`--kernel-trace` without `--output-format csv`), or a
+`*_kernel_trace.csv`, into the kernel_stats.csv layout `--stats` writes: Name, Calls,
+TotalDurationNs, AverageNs, Percentage, MinNs, MaxNs, StdDev, one row per kernel name, ordered
+by total time.
 
-usage: python tools/rocpd_stats.py RUN_results.db OUT.csv
+usage: python tools/rocpd_stats.py RUN_results.db|RUN_kernel_trace.csv OUT.csv
 """
 import csv
 import math
@@ -11,11 +12,14 @@ import sys
 from collections import defaultdict
 
 
-def stats(db):
-    c = sqlite3.connect(db)
+def stats(src):
     dur = defaultdict(list)
-    for name, d in c.execute("select name, duration from kernels"):
-        dur[name].append(int(d))
+    if src.endswith(".csv"):
+        for r in csv.DictReader(open(src)):
+            dur[r["Kernel_Name"]].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    else:
+        for name, d in sqlite3.connect(src).execute("select name, duration from kernels"):
+            dur[name].append(int(d))
     total = sum(sum(v) for v in dur.values()) or 1
     rows = []
     for name, v in dur.items():
