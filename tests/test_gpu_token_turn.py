@@ -8,13 +8,19 @@ has_input masks, batches that end inside a workgroup, waves on the exact path wi
 4-byte glyphs, finalize groups of 4 and 16 (fused) and 32 (the two-call form), and room layouts
 the fused launch does not take (a u64 board window, 8x8 rooms), which run the two calls; and the
 turn-inputs form the turn chain takes (has set: rmi_turn_inputs between the decode and the turn,
-decode errors, a partial has_t), fused and through the separate launches."""
+decode errors, a partial has_t), fused and through the separate launches.  And the token turn
+straight against the oracle: the host decode + `_parse_response` + action mapping
+(oracle/parse.py), oracle.sokoban_turn, oracle.sokoban_render and the finalize's metrics and
+normalised scores (test_token_turn_against_oracle)."""
 import numpy as np
 import pytest
 import torch
 
+import oracle
+from oracle import parse as oparse
 from ragen_amd import ops, synthetic
 from test_gpu_fused_render import LK_WIDE, _pair, _rows_equal, _state_equal
+from test_gpu_parity import _host_ep
 
 pytestmark = pytest.mark.gpu
 
@@ -183,3 +189,72 @@ def test_token_turn_with_turn_inputs(device, pad):
         assert torch.equal(has_a, has_b) and torch.equal(ea, eb), t
         _state_equal(a, b, t)
         _rows_equal(obs_a, obs_b)
+
+
+@pytest.mark.parametrize("has_every", [0, 2])
+def test_token_turn_against_oracle(device, has_every):
+    """The fused token turn against the oracle, not against the separate launches: every turn's
+    token rows are decoded on the host (oracle.parse.detokenize over the byte vocabulary), given
+    back their '<think>' prefix and parsed by the reference's `_parse_response` restatement with
+    its action mapping (unknown names -> id 0); oracle.sokoban_turn steps the same rooms with
+    those actions (first turn fused with the reset, plain turns, the last fused with the
+    finalize), and each turn's observation rows equal oracle.sokoban_render of the oracle's state;
+    the finalize's metrics and normalised scores equal oracle.rollout_metrics and
+    oracle.group_normalize of the oracle's trajectory scores."""
+    B, T, K, gs = 2048, 4, 5, 16
+    (a, _), rng = _pair(device, B, 6, 6, 1, seed=77 + has_every)
+    cfg, vt, toks, stride = _tokens(device, B, T, K, 77 + has_every)
+    table, skip = synthetic.byte_vocab()
+    glk = a.config.grid_lookup
+    fixed = a.room_fixed.cpu().numpy().copy()
+    state = a.init_state.cpu().numpy().copy()
+    player = a.init_player.cpu().numpy().copy()
+    nes, bot = np.zeros(B, np.int32), np.zeros(B, np.int32)
+    oep = oracle.Episode(B, a.ep.T)  # (the record holds 6 turns; T of them run)
+    norm = torch.empty(B, dtype=torch.float32, device=device)
+    met = torch.empty(B, 4, dtype=torch.float64, device=device)
+    fin = ops.finalize_struct(gs, "mean_std", norm, met)
+    stepped = 0
+    for t in range(T):
+        has = None
+        if has_every and t % has_every == 1:
+            has = (rng.random(B) < 0.7).astype(np.uint8)
+        # the oracle's actions: host decode, the reference's parse and action mapping
+        rows = toks[t].cpu().numpy()
+        ids = np.zeros((B, K), np.int8)
+        n = np.zeros(B, np.uint8)
+        for i in range(B):
+            text = oparse.prefixed(oparse.detokenize(rows[i].tolist(), table, skip), True)
+            _, acts = oparse.parse_response(text, True, K, "||")
+            aid = oparse.action_ids(acts, NAMES)
+            ids[i, :len(aid)] = aid
+            n[i] = len(aid)
+        # the token turn
+        o = ops.detok_parse(toks[t], vt, stride, cfg)
+        tok = ops.token_rows_struct(toks[t], vt, cfg, o)
+        ts = ops.turn_struct(t, o["actions"], o["n_actions"], None if has is None else torch.from_numpy(has).to(device),
+                             10, -0.1)
+        obs = ops.render_buffers(B, 6, 6, device)
+        kw = {}
+        if t == 0:
+            kw = {"init_state": a.init_state, "init_player": a.init_player}
+        elif t == T - 1:
+            kw = {"fin": fin}
+        ops.sokoban_token_turn(tok, a.struct(), a.ep, ts, ops.render_struct(glk, 6, 6, *obs), **kw)
+        oracle.sokoban_turn(6, 6, 1, 100, fixed, state, player, nes, bot, oep, t, ids, n, has, 10, -0.1)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(o["n_actions"].cpu().numpy(), n)
+        np.testing.assert_array_equal(o["actions"].cpu().numpy(), ids)
+        np.testing.assert_array_equal(a.room_state.cpu().numpy(), state)
+        np.testing.assert_array_equal(a.player.cpu().numpy(), player)
+        h = _host_ep(a.ep)
+        for k in ("num_actions", "flags", "n_turns", "penalty", "turn_reward", "turn_info", "turn_exec"):
+            np.testing.assert_array_equal(h[k], getattr(oep, k), err_msg=f"turn {t}: {k}")
+        want = [oracle.sokoban_render(state[i], fixed[i], 6, 6, glk) for i in range(B)]
+        assert ops.decode_rows(*obs) == want, t
+        stepped += int(oep.turn_exec[t].sum())
+    assert stepped > B and (n == 0).any()
+    np.testing.assert_array_equal(met.cpu().numpy(), oracle.rollout_metrics(oep))
+    sc, pen = oracle.trajectory_scores(oep)
+    want_norm = oracle.group_normalize(sc, pen, np.arange(0, B + 1, gs, dtype=np.int32), "mean_std")
+    np.testing.assert_allclose(norm.cpu().numpy(), want_norm, rtol=0, atol=1e-5)
