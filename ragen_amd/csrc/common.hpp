@@ -145,7 +145,18 @@ struct TurnOut {
 constexpr int64_t kOff32MaxB = RMI_OFF32_MAX_B;
 constexpr int kOff32MaxRow = 64;
 template <class Ix, class T>
-__device__ __forceinline__ T* elem(T* base, int64_t i) {
+__device__ __forceinline__ T* elem(T* base, int64_t i
+#ifdef RMI_ELEM_CHECK  // (diagnostic variant: an index outside the offset form's range is reported and clamped)
+                                   , int line = __builtin_LINE()
+#endif
+) {
+#ifdef RMI_ELEM_CHECK
+  if (i < 0 || (sizeof(Ix) == 4 && (uint64_t)i * sizeof(T) > 0xFFFFFFFFull)) {
+    printf("RMI_ELEM_CHECK line %d index %lld block %d thread %d\n", line, (long long)i, (int)blockIdx.x,
+           (int)threadIdx.x);
+    i = 0;
+  }
+#endif
   if constexpr (sizeof(Ix) == 4) {
     uint32_t off = (uint32_t)i * (uint32_t)sizeof(T);
     // (a byte array's offset would otherwise fold back into 64-bit "i & 0xffffffff")
