@@ -753,7 +753,10 @@ constexpr int kBsSeg = 48;
 #define RMI_BS_PIPE 6
 #endif
 constexpr int kBsPipe = RMI_BS_PIPE;
-constexpr int64_t kBsMaxLds = 65536;
+#ifndef RMI_BS_MAX_LDS  // the segment kernel's LDS ceiling per wave (rows past it take the tiled kernel)
+#define RMI_BS_MAX_LDS 65536
+#endif
+constexpr int64_t kBsMaxLds = RMI_BS_MAX_LDS;
 
 __host__ __device__ inline int64_t bs_lr(int64_t L) { return (L + 3) & ~(int64_t)3; }
 __host__ __device__ inline int64_t bs_foff(int64_t Lr) { return (int64_t)kGRows * Lr * 4; }
@@ -1316,6 +1319,14 @@ RMI_API int rmi_bilevel_gae(const float* r, const float* v, const uint8_t* mask,
   const bool nt = (double)B * (double)L * 17.0 > kStreamBytes;
   hipStream_t s = as_stream(stream);
   if (lds <= kBsMaxLds && !bilevel_force_tiled()) {
+    if (lds > 65536) {  // (past 64 KB a launch declares the larger dynamic LDS first; gfx950 has 160 KB a CU)
+      static const bool raised =
+          hipFuncSetAttribute(reinterpret_cast<const void*>(bilevel_seg_kernel<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBsMaxLds) == hipSuccess &&
+          hipFuncSetAttribute(reinterpret_cast<const void*>(bilevel_seg_kernel<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBsMaxLds) == hipSuccess;
+      if (!raised) return RMI_EDEVICE;
+    }
     if (nt)
       hipLaunchKernelGGL(bilevel_seg_kernel<true>, grid, dim3(64), (unsigned)lds, s, r, v, mask, B, L, g, gl, hg, hgl,
                          adv, ret, row_stats, err);
