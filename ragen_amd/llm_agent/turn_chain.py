@@ -353,7 +353,8 @@ class FormulateChain:
         self.err = torch.empty(n, dtype=u8, device=dev)
         self.block = torch.empty(16 + 32 * n, dtype=u8, device=dev)  # tail i64[2] | metrics f64[n, 4]
         self.h_stats = torch.empty(16, dtype=u8, pin_memory=True)
-        self.h_block = torch.empty(16 + 32 * n, dtype=u8, pin_memory=True)
+        self.h_tail = torch.empty(16, dtype=u8, pin_memory=True)
+        self.h_met = torch.empty(32 * n, dtype=u8, pin_memory=True)
         self.h_info = torch.empty(max(1, self.ep.T * n), dtype=u8, pin_memory=True)
         self.rmask = None  # the response mask (internal: only its row counts leave)
         c = self.c = _lib.FormulateChain()
@@ -362,9 +363,12 @@ class FormulateChain:
         c.B, c.pad_id = n, int(pr.pad_id)
         c.scores, c.n_scores, c.T = self.ep.turn_reward.data_ptr(), self.n_sc.data_ptr(), int(self.ep.T)
         c.resp_count, c.err, c.tail = self.resp_count.data_ptr(), self.err.data_ptr(), self.block.data_ptr()
-        c.n_copies = 2
-        c.host[0], c.dev[0], c.bytes[0] = self.h_block.data_ptr(), self.block.data_ptr(), 16 + 32 * n
+        # copies 0-1 (the metric rows, turn_info: the finalize's outputs and older) land while the
+        # assembly runs (rmi_formulate_chain_split, n_early = 2); copy 2, the tail, at the end
+        c.n_copies = 3
+        c.host[0], c.dev[0], c.bytes[0] = self.h_met.data_ptr(), self.block.data_ptr() + 16, 32 * n
         c.host[1], c.dev[1] = self.h_info.data_ptr(), self.ep.turn_info.data_ptr()
+        c.host[2], c.dev[2], c.bytes[2] = self.h_tail.data_ptr(), self.block.data_ptr(), 16
         self.runs = 0
 
     def run(self):
@@ -407,17 +411,13 @@ class FormulateChain:
         c.score_out, c.loss_mask, c.response_mask = score.data_ptr(), lm.data_ptr(), self.rmask.data_ptr()
         T = min(es._turn, es.max_turn)
         c.bytes[1] = T * n
-        ops.D2H_COUNT[0] += 1
-        ops.check(L.rmi_formulate_chain(ctypes.byref(c), stream), "rmi_formulate_chain")
+        # the finalize, the metric copies, then the assembly and the tail: the host reduces the
+        # metric rows while the assembly runs, then waits for the tail (two waits)
+        ops.D2H_COUNT[0] += 2
+        ops.check(L.rmi_formulate_chain_split(ctypes.byref(c), 2, stream), "rmi_formulate_chain_split")
         self.runs += 1
-        hb = self.h_block.numpy()
-        total, bits = (int(x) for x in hb[:16].view(np.int64))
-        _raise_assemble_errors(None, S, (bool(bits & _lib.ERR_UNSUP), bool(bits & _lib.ERR_STATE)))
-        # response_length: the f32 mean of the row counts (ctx_manager.py:305); exact while the
-        # total stays below 2^24, where f32 sums of integers are exact in any order.  Above it the
-        # partial sums round, so the counts go through the reference's own op: torch's CPU f32 mean
-        response_length = ref_f32_mean(total, n, lambda: self.resp_count[:n])
-        m = hb[16:16 + 32 * n].view(np.float64).reshape(n, 4).copy()
+        ops.check(L.rmi_formulate_chain_wait(0, stream), "rmi_formulate_chain_wait")
+        m = self.h_met.numpy().view(np.float64).reshape(n, 4).copy()
         info = self.h_info.numpy()[:T * n].reshape(T, n).copy()
         custom = (info & _lib.INFO_PRESENT).any(0) if T else np.zeros(n, bool)
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
@@ -426,6 +426,13 @@ class FormulateChain:
         out = LazyDataProto(env_ids, lambda: ctx._messages_only(es._rollout_states_full(), True))
         out.set_device_batch(batch, env_ids, es.group_size)
         metrics = ctx.device_metrics(es, [(es.tags[0].tag, m, custom, info)])
+        ops.check(L.rmi_formulate_chain_wait(1, stream), "rmi_formulate_chain_wait")
+        total, bits = (int(x) for x in self.h_tail.numpy().view(np.int64))
+        _raise_assemble_errors(None, S, (bool(bits & _lib.ERR_UNSUP), bool(bits & _lib.ERR_STATE)))
+        # response_length: the f32 mean of the row counts (ctx_manager.py:305); exact while the
+        # total stays below 2^24, where f32 sums of integers are exact in any order.  Above it the
+        # partial sums round, so the counts go through the reference's own op: torch's CPU f32 mean
+        response_length = ref_f32_mean(total, n, lambda: self.resp_count[:n])
         metrics["response_length"] = response_length
         out.meta_info = {"metrics": metrics}
         es._formulated = True
