@@ -988,14 +988,14 @@ typedef struct {
   int64_t bytes[4];
 } rmi_formulate_chain_t;
 int rmi_formulate_chain(const rmi_formulate_chain_t* chain, rmi_stream_t stream);
-/* rmi_formulate_chain_split: the same launches and copies, the first n_early copies (those that
- * read only the finalize's outputs or older data: the metric rows, turn_info) enqueued right after
- * step 1 and followed by an event, the rest after step 3; returns without waiting.  The caller
- * then computes on the early copies while the assembly runs:
- * rmi_formulate_chain_wait(0, s): the early copies have landed (this host thread's last split);
- * rmi_formulate_chain_wait(1, s): the stream is done (every copy, the batch). */
-int rmi_formulate_chain_split(const rmi_formulate_chain_t* chain, int32_t n_early, rmi_stream_t stream);
-int rmi_formulate_chain_wait(int32_t which, rmi_stream_t stream);
+/* rmi_formulate_chain_part: the same launches and copies in two calls that do not wait -- part 1:
+ * step 1 (the finalize) and copies [0, n_early), which may read only what the finalize or earlier
+ * work wrote (the metric rows, turn_info, rmi_formulate_stats' stats launched just before);
+ * part 2: steps 2-3 (the assembly, the tail) and copies [n_early, n_copies).  A caller waits after
+ * part 1 for the batch width (rmi_formulate_chain_wait), launches part 2 with it, and reduces the
+ * metric rows on the host while the assembly runs.  rmi_formulate_chain_wait: the stream waited on. */
+int rmi_formulate_chain_part(const rmi_formulate_chain_t* chain, int32_t part, int32_t n_early, rmi_stream_t stream);
+int rmi_formulate_chain_wait(rmi_stream_t stream);
 
 /* --------------------------------------------------------------- reset seeding */
 /* Replaces the per-env numpy seeding of BanditEnv.reset (bandit/env.py:25-39) and

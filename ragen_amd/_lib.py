@@ -278,8 +278,8 @@ _SIGS = {
                                        c_void_p, c_void_p, c_int32, c_int32, c_int32, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rmi_formulate_chain": (c_int32, [_P(FormulateChain), c_void_p]),
-    "rmi_formulate_chain_split": (c_int32, [_P(FormulateChain), c_int32, c_void_p]),
-    "rmi_formulate_chain_wait": (c_int32, [c_int32, c_void_p]),
+    "rmi_formulate_chain_part": (c_int32, [_P(FormulateChain), c_int32, c_int32, c_void_p]),
+    "rmi_formulate_chain_wait": (c_int32, [c_void_p]),
 }
 
 _lib = None

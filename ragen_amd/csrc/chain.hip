@@ -131,30 +131,25 @@ RMI_API int rmi_turn_chain(const rmi_turn_chain_t* chain, rmi_stream_t s) {
 
 namespace {
 
-// the split formulate chain's event (per host thread and device, as copy_event): recorded after
-// the early copies, waited on by rmi_formulate_chain_wait(0)
-hipEvent_t formulate_event() {
-  thread_local hipEvent_t ev[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!ev[dev] && hipEventCreateWithFlags(&ev[dev], hipEventDisableTiming) != hipSuccess) ev[dev] = nullptr;
-  return ev[dev];
-}
-
-// steps 1-3 of the chain with the first n_early copies enqueued (and, with `ev`, the event
-// recorded) between the finalize and the assembly, the other copies after the tail
-int formulate_enqueue(const rmi_formulate_chain_t* chain, int n_early, hipEvent_t ev, rmi_stream_t s) {
+// the chain's launches and copies, whole (part 0) or in two parts: part 1 = step 1 (the finalize)
+// and copies [0, n_early), part 2 = steps 2-3 (the assembly, the tail) and copies [n_early,
+// n_copies).  Nothing is waited on here.
+int formulate_enqueue(const rmi_formulate_chain_t* chain, int part, int n_early, rmi_stream_t s) {
   if (!chain) return RMI_EINVAL;
   const rmi_formulate_chain_t& c = *chain;
   if (!c.ep || c.ep->B != c.B || !c.norm || !c.tail || c.n_copies < 0 || c.n_copies > 4 ||
-      (c.flags & RMI_MS_TURN_SCORES) || n_early < 0 || n_early > c.n_copies)
+      (c.flags & RMI_MS_TURN_SCORES) || part < 0 || part > 2 || n_early < 0 || n_early > c.n_copies)
     return RMI_EINVAL;
   hipStream_t hs = rmi::as_stream(s);
-  int rc = rmi_rollout_finalize(c.ep, c.seg, c.G, c.method, c.metrics, nullptr, nullptr, c.norm, s);
-  if (rc) return rc;
-  for (int i = 0; i < n_early; ++i)
-    if (c.bytes[i] > 0 && (rc = rmi::readback_async(c.host[i], c.dev[i], (size_t)c.bytes[i], hs)) != RMI_OK) return rc;
-  if (ev && hipEventRecord(ev, hs) != hipSuccess) return RMI_EDEVICE;
+  int rc;
+  if (part != 2) {
+    rc = rmi_rollout_finalize(c.ep, c.seg, c.G, c.method, c.metrics, nullptr, nullptr, c.norm, s);
+    if (rc) return rc;
+    for (int i = 0; i < n_early; ++i)
+      if (c.bytes[i] > 0 && (rc = rmi::readback_async(c.host[i], c.dev[i], (size_t)c.bytes[i], hs)) != RMI_OK)
+        return rc;
+    if (part == 1) return RMI_OK;
+  }
   rc = rmi_assemble_rows_ex(c.tokens, c.row_start, c.row_len, c.B, c.S, c.pad_id, c.special_token, c.reward_token,
                             c.scores, c.n_scores, c.T, c.n_slots, c.flags, c.norm, c.input_ids, c.attention_mask,
                             c.position_ids, c.score_out, c.loss_mask, c.response_mask, c.resp_count, c.err, s);
@@ -169,22 +164,17 @@ int formulate_enqueue(const rmi_formulate_chain_t* chain, int n_early, hipEvent_
 }  // namespace
 
 RMI_API int rmi_formulate_chain(const rmi_formulate_chain_t* chain, rmi_stream_t s) {
-  const int rc = formulate_enqueue(chain, 0, nullptr, s);
+  const int rc = formulate_enqueue(chain, 0, 0, s);
   if (rc) return rc;
   return hipStreamSynchronize(rmi::as_stream(s)) == hipSuccess ? RMI_OK : RMI_EDEVICE;
 }
 
-RMI_API int rmi_formulate_chain_split(const rmi_formulate_chain_t* chain, int32_t n_early, rmi_stream_t s) {
-  hipEvent_t ev = formulate_event();
-  if (!ev) return RMI_EDEVICE;
-  return formulate_enqueue(chain, n_early, ev, s);
+RMI_API int rmi_formulate_chain_part(const rmi_formulate_chain_t* chain, int32_t part, int32_t n_early,
+                                     rmi_stream_t s) {
+  if (part != 1 && part != 2) return RMI_EINVAL;
+  return formulate_enqueue(chain, part, n_early, s);
 }
 
-RMI_API int rmi_formulate_chain_wait(int32_t which, rmi_stream_t s) {
-  if (which == 0) {
-    hipEvent_t ev = formulate_event();
-    return ev && hipEventSynchronize(ev) == hipSuccess ? RMI_OK : RMI_EDEVICE;
-  }
-  if (which != 1) return RMI_EINVAL;
+RMI_API int rmi_formulate_chain_wait(rmi_stream_t s) {
   return hipStreamSynchronize(rmi::as_stream(s)) == hipSuccess ? RMI_OK : RMI_EDEVICE;
 }

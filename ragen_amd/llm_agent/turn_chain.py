@@ -311,14 +311,16 @@ class TurnChain:
 
 
 class FormulateChain:
-    """ContextManager.formulate_rollouts on the device path as two calls into the library
-    (rmi_formulate_stats + its readback, then rmi_formulate_chain): the batch width, then the
-    finalize (per-env metrics, normalised scores), the assembly (left-padded batch, masks, the
-    normalised score in place, per-row response counts), the reductions and the readback of the
-    metric rows -- where the step-by-step form made ~20 launches and torch glue kernels between
-    two readbacks.  Applies to one env tag, unsharded, without per-turn scores or a context
+    """ContextManager.formulate_rollouts on the device path as two waits on the library
+    (rmi_formulate_chain_part): the batch width (rmi_formulate_stats) with the finalize (per-env
+    metrics, normalised scores) and the copies of both, then the assembly (left-padded batch,
+    masks, the normalised score in place, per-row response counts) and the reductions, during
+    which the host reduces the metric rows -- where the step-by-step form made ~20 launches and
+    torch glue kernels between two readbacks.  Applies to one env tag, unsharded, without per-turn scores or a context
     window; ContextManager.formulate_device takes the step-by-step form otherwise (the same
     outputs: tests/test_gpu_turn_chain.py)."""
+
+    overlap = True  # the metric rows reduced on the host while the assembly runs
 
     @staticmethod
     def applies(ctx, es, pr) -> bool:
@@ -363,12 +365,13 @@ class FormulateChain:
         c.B, c.pad_id = n, int(pr.pad_id)
         c.scores, c.n_scores, c.T = self.ep.turn_reward.data_ptr(), self.n_sc.data_ptr(), int(self.ep.T)
         c.resp_count, c.err, c.tail = self.resp_count.data_ptr(), self.err.data_ptr(), self.block.data_ptr()
-        # copies 0-1 (the metric rows, turn_info: the finalize's outputs and older) land while the
-        # assembly runs (rmi_formulate_chain_split, n_early = 2); copy 2, the tail, at the end
-        c.n_copies = 3
+        # copies 0-2 (the metric rows, turn_info, the width stats) after part 1 (the finalize, with
+        # rmi_formulate_stats before it), copy 3 (the tail) after part 2 (rmi_formulate_chain_part)
+        c.n_copies = 4
         c.host[0], c.dev[0], c.bytes[0] = self.h_met.data_ptr(), self.block.data_ptr() + 16, 32 * n
         c.host[1], c.dev[1] = self.h_info.data_ptr(), self.ep.turn_info.data_ptr()
-        c.host[2], c.dev[2], c.bytes[2] = self.h_tail.data_ptr(), self.block.data_ptr(), 16
+        c.host[2], c.dev[2], c.bytes[2] = self.h_stats.data_ptr(), self.stats.data_ptr(), 12
+        c.host[3], c.dev[3], c.bytes[3] = self.h_tail.data_ptr(), self.block.data_ptr(), 16
         self.runs = 0
 
     def run(self):
@@ -380,11 +383,16 @@ class FormulateChain:
         tokens, start, row_len = pr.update_rows(resolve=False)
         L = _lib.lib()
         stream = ops._stream(dev)
-        # 1. the width, the pending host rows, zip_longest's length: one launch, one readback
+        T = min(es._turn, es.max_turn)
+        c = self.c
+        c.bytes[1] = T * n
+        # 1. the width, the pending host rows, zip_longest's length (rmi_formulate_stats) and the
+        #    finalize (per-env metrics, normalised scores; part 1), their copies, one wait
         ops.check(L.rmi_formulate_stats(row_len.data_ptr(), ops._ptr(pend), self.ep.n_turns.data_ptr(), n,
                                         self.n_sc.data_ptr(), self.stats.data_ptr(), stream), "rmi_formulate_stats")
         ops.D2H_COUNT[0] += 1
-        ops.check(L.rmi_readback(self.h_stats.data_ptr(), self.stats.data_ptr(), 12, stream), "rmi_readback")
+        ops.check(L.rmi_formulate_chain_part(ctypes.byref(c), 1, 3, stream), "rmi_formulate_chain_part")
+        ops.check(L.rmi_formulate_chain_wait(stream), "rmi_formulate_chain_wait")
         S, any_bad, n_slots = (int(x) for x in self.h_stats.numpy()[:12].view(np.int32))
         if pend is not None:
             pr._resolve(bool(any_bad))
@@ -401,7 +409,6 @@ class FormulateChain:
         lm = torch.empty(n, So, dtype=torch.bool, device=dev)
         if self.rmask is None or self.rmask.numel() < n * So:
             self.rmask = torch.empty(max(1, n * So + n * So // 4), dtype=torch.uint8, device=dev)
-        c = self.c
         c.tokens, c.row_start, c.row_len = tokens.data_ptr(), start.data_ptr(), row_len.data_ptr()
         c.S, c.special_token, c.reward_token = S, int(special_token), int(reward_token)
         c.n_slots = n_slots
@@ -409,14 +416,13 @@ class FormulateChain:
             (_lib.MS_ROLL if "qwen" in ctx.tokenizer.name_or_path.lower() else 0)
         c.input_ids, c.attention_mask, c.position_ids = ids.data_ptr(), am.data_ptr(), pos.data_ptr()
         c.score_out, c.loss_mask, c.response_mask = score.data_ptr(), lm.data_ptr(), self.rmask.data_ptr()
-        T = min(es._turn, es.max_turn)
-        c.bytes[1] = T * n
-        # the finalize, the metric copies, then the assembly and the tail: the host reduces the
-        # metric rows while the assembly runs, then waits for the tail (two waits)
-        ops.D2H_COUNT[0] += 2
-        ops.check(L.rmi_formulate_chain_split(ctypes.byref(c), 2, stream), "rmi_formulate_chain_split")
+        # the assembly and the tail (part 2), not waited on: the host reduces the metric rows
+        # meanwhile, then waits for the tail
+        ops.D2H_COUNT[0] += 1
+        ops.check(L.rmi_formulate_chain_part(ctypes.byref(c), 2, 3, stream), "rmi_formulate_chain_part")
         self.runs += 1
-        ops.check(L.rmi_formulate_chain_wait(0, stream), "rmi_formulate_chain_wait")
+        if not self.overlap:  # (A/B: the host's reductions after the assembly, not beside it)
+            ops.check(L.rmi_formulate_chain_wait(stream), "rmi_formulate_chain_wait")
         m = self.h_met.numpy().view(np.float64).reshape(n, 4).copy()
         info = self.h_info.numpy()[:T * n].reshape(T, n).copy()
         custom = (info & _lib.INFO_PRESENT).any(0) if T else np.zeros(n, bool)
@@ -426,7 +432,7 @@ class FormulateChain:
         out = LazyDataProto(env_ids, lambda: ctx._messages_only(es._rollout_states_full(), True))
         out.set_device_batch(batch, env_ids, es.group_size)
         metrics = ctx.device_metrics(es, [(es.tags[0].tag, m, custom, info)])
-        ops.check(L.rmi_formulate_chain_wait(1, stream), "rmi_formulate_chain_wait")
+        ops.check(L.rmi_formulate_chain_wait(stream), "rmi_formulate_chain_wait")
         total, bits = (int(x) for x in self.h_tail.numpy().view(np.int64))
         _raise_assemble_errors(None, S, (bool(bits & _lib.ERR_UNSUP), bool(bits & _lib.ERR_STATE)))
         # response_length: the f32 mean of the row counts (ctx_manager.py:305); exact while the

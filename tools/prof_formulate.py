@@ -1,7 +1,7 @@
 """Host anatomy of formulate_rollouts on the device path (diagnostic): bench.api_leg's rollout
-(tools/prof_api_cprofile.py's setup and warm-up), then 8 rollouts with perf_counter wrappers
-around the pieces of FormulateChain.run; prints per piece the median microseconds per rollout
-and what the pieces leave of the phase's wall time."""
+(tools/prof_api_cprofile.py's setup and warm-up), then 16 rollouts, FormulateChain.overlap on
+and off alternating, with perf_counter wrappers around the pieces of FormulateChain.run; prints
+per piece the median microseconds per rollout, and the phase's wall time per form."""
 import os
 import sys
 import time
@@ -45,13 +45,16 @@ wrap(pr, "_resolve", "_resolve")
 wrap(turn_chain.FormulateChain, "run", "FormulateChain.run")
 wrap(ctx, "formulate_rollouts", "formulate_rollouts")
 
-for _ in range(8):
+for i in range(16):  # alternating: the host's reductions beside the assembly / after it
+    turn_chain.FormulateChain.overlap = i % 2 == 0
     cur.clear()
     tm = base.run()
     for k, v in cur.items():
         T[k].append(v)
-    T["(proxy formulate_s)"].append(tm["formulate_s"])
+    tag = "overlap" if i % 2 == 0 else "serial"
+    T[f"(proxy formulate_s, {tag})"].append(tm["formulate_s"])
     T["(proxy turns_s)"].append(tm["turns_s"])
-print("median us per rollout over 8 rollouts")
+turn_chain.FormulateChain.overlap = True
+print("median us per rollout over 16 rollouts (8 per formulate form)")
 for k, v in sorted(T.items(), key=lambda kv: -np.median(kv[1])):
     print(f"{np.median(v) * 1e6:10.1f}  {k}")
