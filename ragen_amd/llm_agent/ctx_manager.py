@@ -1041,15 +1041,21 @@ class ContextManager:
                 m = np.ascontiguousarray(m.T)  # one pass: each column contiguous for its reductions
             else:
                 m, cust = np.ascontiguousarray(rows[:, :4].T), rows[:, 4] != 0
-            cols = [("success", m[0]), ("num_actions", m[1].astype(np.int64))]
+            # success and num_actions hold integers (the finalize's 0 / 1 and action counts): their
+            # sums are exact in any order, so their non-zero means are sum / count -- the values
+            # np.mean over the non-zero entries gives -- with two reductions for both columns
+            tot, cnt = m[:2].sum(axis=1), np.count_nonzero(m[:2], axis=1)
+            metrics[f"{tag}/success"] = tot[0] / self.env_nums[tag]
+            metrics[f"{tag}/num_actions"] = np.int64(tot[1]) / self.env_nums[tag]
+            nz += [(f"{tag}/non-zero/success", tot[0], cnt[0]), (f"{tag}/non-zero/num_actions", tot[1], cnt[1])]
             if cust.any():
                 all_c = bool(cust.all())
-                cols += [("action_is_effective", m[2] if all_c else m[2][cust]),
-                         ("action_is_valid", m[3] if all_c else m[3][cust])]
-            for k, v in cols:
-                metrics[f"{tag}/{k}"] = np.sum(v) / self.env_nums[tag]
-                nz.append((f"{tag}/non-zero/{k}", v[v != 0]))
-        for k, v in nz:
-            if len(v):
-                metrics[k] = np.mean(v)
+                for k, v in (("action_is_effective", m[2] if all_c else m[2][cust]),
+                             ("action_is_valid", m[3] if all_c else m[3][cust])):
+                    metrics[f"{tag}/{k}"] = np.sum(v) / self.env_nums[tag]
+                    v = v[v != 0]  # (fractions: the reference's order of summation over the non-zero ones)
+                    nz.append((f"{tag}/non-zero/{k}", np.sum(v), len(v)))
+        for k, t, c in nz:
+            if c:
+                metrics[k] = np.float64(t) / c
         return metrics

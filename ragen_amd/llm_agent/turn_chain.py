@@ -423,15 +423,16 @@ class FormulateChain:
         self.runs += 1
         if not self.overlap:  # (A/B: the host's reductions after the assembly, not beside it)
             ops.check(L.rmi_formulate_chain_wait(stream), "rmi_formulate_chain_wait")
-        m = self.h_met.numpy().view(np.float64).reshape(n, 4).copy()
-        info = self.h_info.numpy()[:T * n].reshape(T, n).copy()
+        # the metric rows as columns (one copy; device_metrics reduces each column contiguously)
+        m = np.ascontiguousarray(self.h_met.numpy().view(np.float64).reshape(n, 4).T).T
+        info = self.h_info.numpy()[:T * n].reshape(T, n)
         custom = (info & _lib.INFO_PRESENT).any(0) if T else np.zeros(n, bool)
         batch = {"input_ids": ids, "attention_mask": am, "position_ids": pos, "responses": ids[:, 1:],
                  "loss_mask": lm, "rm_scores": score, "original_rm_scores": score}
         env_ids = es.env_lo + np.arange(n, dtype=np.int64)
         out = LazyDataProto(env_ids, lambda: ctx._messages_only(es._rollout_states_full(), True))
         out.set_device_batch(batch, env_ids, es.group_size)
-        metrics = ctx.device_metrics(es, [(es.tags[0].tag, m, custom, info)])
+        metrics = ctx.device_metrics(es, [(es.tags[0].tag, m, custom, None)])
         ops.check(L.rmi_formulate_chain_wait(stream), "rmi_formulate_chain_wait")
         total, bits = (int(x) for x in self.h_tail.numpy().view(np.int64))
         _raise_assemble_errors(None, S, (bool(bits & _lib.ERR_UNSUP), bool(bits & _lib.ERR_STATE)))
