@@ -239,6 +239,8 @@ def context_probes(es, tpl, added) -> list:
 class DevicePrompts:
     """Per-env prompt ids on the device for one ContextManager / EnvStateManager pair."""
 
+    first_bound = True  # the first prompt's BPE row size from the host's bound (A/B: read back)
+
     def __init__(self, ctx, es, tokenizer, device, capacity: Optional[int] = None, window: Optional[int] = None,
                  expansions: bool = True):
         ap = ctx.config.agent_proxy
@@ -522,7 +524,10 @@ class DevicePrompts:
             self.len_upd.zero_()
             return
         text, tlen, terr, stride = self._first_text(obs, obs_len, ints)
-        self._encode(text, tlen, terr, None, stride, lambda e: self._host_first(e))
+        # the BPE launch's row size from the host's bound (no device round trip for the longest
+        # row; None when a length it needs is unknown: then the longest row is read back)
+        bound = self._text_bound(self._prog_last, self._obs_bound(rows), None) if self.first_bound else None
+        self._encode(text, tlen, terr, None, stride, lambda e: self._host_first(e), bound=bound)
         self.len_upd.copy_(self.len)
 
     def _first_text(self, obs, obs_len, ints, active=None):
